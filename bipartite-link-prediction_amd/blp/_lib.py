@@ -1,0 +1,133 @@
+"""ctypes binding of libblp.so (include/blp.h). No torch, no fallback.
+
+The library is built in-tree (``csrc/Makefile`` -> ``blp/libblp.so``, see
+``__graft_entry__.build``). If it is missing or fails to load, every entry point of the
+engine raises :class:`BLPUnavailable` -- there is deliberately no CPU path behind it.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("BLP_LIB", os.path.join(_HERE, "libblp.so"))
+
+CN, JACCARD, ADAMIC = 1, 2, 4
+E_ZERODIV = -5
+
+K_SCORE, K_GROUP, K_SVD_PAIRS, K_SVD_TOPK, K_WALK, K_HOP3 = range(6)
+
+
+class BLPUnavailable(RuntimeError):
+    """libblp.so (the HIP engine) is not built or cannot be loaded."""
+
+
+class BLPError(RuntimeError):
+    """A libblp call returned an error code."""
+
+    def __init__(self, code, msg):
+        super().__init__("%s (code %d)" % (msg, code))
+        self.code = code
+
+
+_P = ctypes.c_void_p
+_I64 = ctypes.c_int64
+_I32 = ctypes.c_int
+_U32 = ctypes.c_uint32
+_DP = ctypes.POINTER(ctypes.c_double)
+_PP = ctypes.POINTER(ctypes.c_void_p)
+
+# name -> argtypes (all return int unless listed in _RESTYPE)
+SIGNATURES = {
+    "blp_last_error": [],
+    "blp_version": [],
+    "blp_device_count": [ctypes.POINTER(ctypes.c_int)],
+    "blp_device_sync": [_I32],
+    "blp_edges_parse": [ctypes.c_char_p, _I32, _I32, _P, _P, ctypes.POINTER(ctypes.c_int64)],
+    "blp_csr_from_edges": [_I64, _I64, _P, _P, _P, _P, _P, ctypes.POINTER(ctypes.c_int64)],
+    "blp_graph_create": [_P, _P, _I64, _P, _I32, _PP],
+    "blp_graph_destroy": [_P],
+    "blp_graph_info": [_P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
+                       ctypes.POINTER(ctypes.c_int)],
+    "blp_graph_sync": [_P],
+    "blp_score_pairs": [_P, _I32, _U32, _P, _P, _I64, _P, _P, _P],
+    "blp_batch_create": [_P, _P, _P, _I64, _PP],
+    "blp_batch_score": [_P, _P, _U32],
+    "blp_batch_fetch": [_P, _P, _P, _P, _P],
+    "blp_batch_destroy": [_P],
+    "blp_batch_plan": [_P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
+                       ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
+                       ctypes.POINTER(ctypes.c_int)],
+    "blp_stats_reset": [_P],
+    "blp_stats_get": [_P, _I32, _DP, ctypes.POINTER(ctypes.c_int64)],
+}
+_RESTYPE = {"blp_last_error": ctypes.c_char_p, "blp_version": ctypes.c_char_p}
+
+_lib = None
+
+
+def lib():
+    """Load libblp.so once; raise BLPUnavailable (loudly) if it cannot be loaded."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise BLPUnavailable(
+            "libblp.so not found at %s: build the HIP engine first "
+            "(python -c 'import __graft_entry__ as g; g.build()')" % LIB_PATH)
+    try:
+        L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    except OSError as e:  # pragma: no cover - depends on the box
+        raise BLPUnavailable("cannot load %s: %s" % (LIB_PATH, e))
+    for name, args in SIGNATURES.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = _RESTYPE.get(name, ctypes.c_int)
+    _lib = L
+    return L
+
+
+def register(name, argtypes, restype=ctypes.c_int):
+    """Add a signature for entry points defined by later translation units."""
+    SIGNATURES[name] = argtypes
+    if restype is not ctypes.c_int:
+        _RESTYPE[name] = restype
+    if _lib is not None:
+        fn = getattr(_lib, name)
+        fn.argtypes = argtypes
+        fn.restype = restype
+
+
+def check(rc):
+    if rc != 0:
+        msg = lib().blp_last_error().decode(errors="replace")
+        if rc == E_ZERODIV:
+            raise ZeroDivisionError("float division by zero")
+        raise BLPError(rc, msg)
+    return rc
+
+
+def ptr(a):
+    """Raw data pointer of a C-contiguous numpy array (None passes NULL)."""
+    if a is None:
+        return None
+    assert a.flags["C_CONTIGUOUS"], "array must be C-contiguous"
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def device_count():
+    n = ctypes.c_int(0)
+    check(lib().blp_device_count(ctypes.byref(n)))
+    return n.value
+
+
+def device_sync(device=0):
+    check(lib().blp_device_sync(device))
+
+
+def version():
+    return lib().blp_version().decode()
+
+
+def as_i32(a):
+    return np.ascontiguousarray(a, dtype=np.int32)

@@ -1,0 +1,228 @@
+"""Device-resident graph handle: the engine's replacement for SNAP's PUNGraph.
+
+``load_edge_list(path)`` replaces ``snap.LoadEdgeList(snap.PUNGraph, path, 0, 1)``
+(similarity.py:16). The graph is the undirected simple graph of the edge list:
+
+* node ids are the integers of graph.txt (SNAP TInt); they are remapped to dense ids
+  ``0..n-1`` -- nodes seen in column 0 first (ascending), then the column-1-only nodes --
+  so a reference bipartite file puts users in one contiguous range and businesses in
+  another (``dataset_maker.py:197`` writes "user business");
+* duplicate / reversed edges are merged; a self-loop is not stored in the CSR (it never
+  changes a BFS hop set) but adds 1 to the node's SNAP degree (TUNGraph stores it once);
+* the CSR (both directions, sorted rows) and the per-node Adamic-Adar weight
+  ``(log deg)^-1`` (0 for deg <= 1, similarity.py:121-125) live in HBM. The weights are
+  computed here with Python's ``math.log`` -- the reference's own arithmetic -- once per
+  distinct degree.
+"""
+import ctypes
+import math
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, lib, ptr
+
+
+def parse_edge_list(path, c0=0, c1=1):
+    """graph.txt -> (a, b) int64 arrays (SNAP LoadEdgeList text semantics)."""
+    L = lib()
+    m = ctypes.c_int64(0)
+    bpath = path.encode() if isinstance(path, str) else path
+    check(L.blp_edges_parse(bpath, c0, c1, None, None, ctypes.byref(m)))
+    a = np.empty(m.value, np.int64)
+    b = np.empty(m.value, np.int64)
+    check(L.blp_edges_parse(bpath, c0, c1, ptr(a), ptr(b), ctypes.byref(m)))
+    return a[: m.value], b[: m.value]
+
+
+def aa_weights_from_degree(deg):
+    """Per-node Adamic-Adar term with the reference's arithmetic (similarity.py:121-125)."""
+    deg = np.asarray(deg)
+    out = np.zeros(len(deg), np.float64)
+    if len(deg) == 0:
+        return out
+    uniq, inv = np.unique(deg, return_inverse=True)
+    table = np.array([(math.log(int(d)) ** -1) if d > 1 else 0.0 for d in uniq], np.float64)
+    return table[inv]
+
+
+class HostGraph:
+    """Host half of the graph: id map, CSR, SNAP degrees, Adamic-Adar weights.
+
+    Needs libblp.so's host helpers only (no GPU), so the id/CSR logic is testable on a
+    CPU-only machine. :class:`DeviceGraph` adds the HBM copy and the kernels.
+    """
+
+    def __init__(self, a_ids, b_ids, aa=True):
+        a_ids = np.asarray(a_ids, dtype=np.int64)
+        b_ids = np.asarray(b_ids, dtype=np.int64)
+        if len(a_ids) != len(b_ids):
+            raise ValueError("edge endpoint arrays differ in length")
+        u0 = np.unique(a_ids)
+        u1 = np.setdiff1d(np.unique(b_ids), u0, assume_unique=True)
+        self.node_ids = np.concatenate([u0, u1])  # dense id -> original id
+        self.n = len(self.node_ids)
+        if self.n >= 2**31 - 1:
+            raise ValueError("too many nodes for int32 dense ids")
+        self._sort = np.argsort(self.node_ids, kind="stable")
+        self._sorted_ids = self.node_ids[self._sort]
+        da = self.dense(a_ids)
+        db = self.dense(b_ids)
+        self.n_edges_in = len(a_ids)
+        rp = np.zeros(self.n + 1, np.int64)
+        ci = np.empty(max(2 * len(da), 1), np.int32)
+        sl = np.zeros(max(self.n, 1), np.uint8)
+        nnz = ctypes.c_int64(0)
+        check(lib().blp_csr_from_edges(self.n, len(da), ptr(da), ptr(db), ptr(rp), ptr(ci), ptr(sl),
+                                       ctypes.byref(nnz)))
+        self.row_ptr = rp
+        self.col_idx = ci[: nnz.value].copy()
+        self.self_loop = sl[: self.n]
+        self.hop1_size = np.diff(rp)  # |GetNodesAtHop(v, 1)|
+        self.degree = self.hop1_size + self.self_loop  # SNAP GetDeg
+        self.aa_weight = aa_weights_from_degree(self.degree) if aa else None
+
+    @property
+    def nnz(self):
+        return len(self.col_idx)
+
+    # ------------------------------------------------------------------ ids
+    def lookup(self, ids):
+        """original ids -> (dense ids, present mask); absent ids map to -1."""
+        ids = np.asarray(ids, dtype=np.int64)
+        if self.n == 0:
+            return np.full(len(ids), -1, np.int32), np.zeros(len(ids), bool)
+        pos = np.searchsorted(self._sorted_ids, ids)
+        pos = np.minimum(pos, self.n - 1)
+        present = self._sorted_ids[pos] == ids
+        dense = np.where(present, self._sort[pos], -1).astype(np.int32)
+        return dense, present
+
+    def dense(self, ids):
+        d, ok = self.lookup(ids)
+        if not ok.all():
+            raise KeyError("node id not in graph")
+        return d
+
+    def __contains__(self, node_id):
+        return bool(self.lookup([int(node_id)])[1][0])
+
+    def GetNodes(self):  # SNAP-style accessors used by the reference's drivers
+        return self.n
+
+    def GetEdges(self):
+        return int(self.nnz // 2 + self.self_loop.sum())
+
+    def GetDeg(self, node_id):
+        return int(self.degree[self.dense([int(node_id)])[0]])
+
+
+class DeviceGraph(HostGraph):
+    """Undirected simple graph in HBM (CSR over dense ids) + the id map on the host.
+
+    Mirrors the pieces of SNAP's PUNGraph the reference uses: node membership
+    (``int(u) in nodes``, similarity.py:22,26,38,52), degree (``GetNI(i).GetDeg()``,
+    :121) and the hop sets (:29,:41,:74,:85), which the kernels compute on the device.
+    """
+
+    def __init__(self, a_ids, b_ids, device=0, aa=True):
+        HostGraph.__init__(self, a_ids, b_ids, aa=aa)
+        self.device = device
+        h = ctypes.c_void_p()
+        check(lib().blp_graph_create(ptr(self.row_ptr), ptr(self.col_idx), self.n,
+                                     ptr(self.aa_weight) if aa else None, device, ctypes.byref(h)))
+        self.handle = h
+
+    # ------------------------------------------------------------------ lifecycle
+    def close(self):
+        if getattr(self, "handle", None):
+            lib().blp_graph_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ scoring
+    def score_pairs(self, x, y, mask=7):
+        """Pairs (x, y) of dense ids -> dict(cn, jaccard, adamic) arrays (caller order).
+
+        x is the node whose exact 2-hop set is built (user side: user; business side:
+        business), y the node whose 1-hop set is intersected with it."""
+        x = _lib.as_i32(x)
+        y = _lib.as_i32(y)
+        n = len(x)
+        cn = np.zeros(n, np.uint32)
+        jac = np.zeros(n, np.float64) if mask & _lib.JACCARD else None
+        aa = np.zeros(n, np.float64) if mask & _lib.ADAMIC else None
+        if n:
+            check(lib().blp_score_pairs(self.handle, 0, mask | _lib.CN, ptr(x), ptr(y), n, ptr(cn), ptr(jac),
+                                        ptr(aa)))
+        return {"cn": cn, "jaccard": jac, "adamic": aa}
+
+    def batch(self, x, y):
+        return PairBatch(self, x, y)
+
+    def stats(self, kernel):
+        ms = ctypes.c_double(0)
+        n = ctypes.c_int64(0)
+        check(lib().blp_stats_get(self.handle, kernel, ctypes.byref(ms), ctypes.byref(n)))
+        return ms.value, n.value
+
+    def stats_reset(self):
+        check(lib().blp_stats_reset(self.handle))
+
+    def sync(self):
+        check(lib().blp_graph_sync(self.handle))
+
+
+class PairBatch:
+    """Pairs resident in HBM for repeated scoring (bench); see blp_batch_* in blp.h."""
+
+    def __init__(self, graph, x, y):
+        self.graph = graph
+        self.x = _lib.as_i32(x)
+        self.y = _lib.as_i32(y)
+        self.n = len(self.x)
+        h = ctypes.c_void_p()
+        check(lib().blp_batch_create(graph.handle, ptr(self.x), ptr(self.y), self.n, ctypes.byref(h)))
+        self.handle = h
+
+    def plan(self):
+        lo, hi = ctypes.c_int64(), ctypes.c_int64()
+        ch, blk, grp = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        check(lib().blp_batch_plan(self.handle, ctypes.byref(lo), ctypes.byref(hi), ctypes.byref(ch),
+                                   ctypes.byref(blk), ctypes.byref(grp)))
+        return {"lo": lo.value, "hi": hi.value, "chunks": ch.value, "block": blk.value, "group": grp.value}
+
+    def score(self, mask=7):
+        check(lib().blp_batch_score(self.graph.handle, self.handle, mask))
+
+    def fetch(self, mask=7):
+        cn = np.zeros(self.n, np.uint32)
+        jac = np.zeros(self.n, np.float64) if mask & _lib.JACCARD else None
+        aa = np.zeros(self.n, np.float64) if mask & _lib.ADAMIC else None
+        check(lib().blp_batch_fetch(self.graph.handle, self.handle, ptr(cn), ptr(jac), ptr(aa)))
+        return {"cn": cn, "jaccard": jac, "adamic": aa}
+
+    def close(self):
+        if getattr(self, "handle", None):
+            lib().blp_batch_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def load_edge_list(path, c0=0, c1=1, device=0):
+    """snap.LoadEdgeList(snap.PUNGraph, path, c0, c1) -> DeviceGraph (similarity.py:16)."""
+    a, b = parse_edge_list(path, c0, c1)
+    return DeviceGraph(a, b, device=device)
+
+
+LoadEdgeList = load_edge_list

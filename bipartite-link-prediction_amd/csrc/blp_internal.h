@@ -1,0 +1,73 @@
+// Internal definitions shared by the libblp.so translation units (gfx950 / CDNA4 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "blp.h"
+
+namespace blp {
+
+void set_error(const std::string& msg);
+int fail(int code, const std::string& msg);
+int hip_fail(hipError_t e, const char* what, const char* file, int line);
+
+#define BLP_HIP(call)                                                         \
+  do {                                                                        \
+    hipError_t _e = (call);                                                   \
+    if (_e != hipSuccess) return ::blp::hip_fail(_e, #call, __FILE__, __LINE__); \
+  } while (0)
+
+#define BLP_CHECK(cond, code, msg)       \
+  do {                                   \
+    if (!(cond)) return ::blp::fail((code), (msg)); \
+  } while (0)
+
+// Device scratch buffer that grows on demand (never shrinks while the handle lives).
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  int reserve(size_t want);
+  void release();
+  template <class T> T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+enum KernelId { K_SCORE = 0, K_GROUP = 1, K_SVD_PAIRS = 2, K_SVD_TOPK = 3, K_WALK = 4, K_HOP3 = 5, K_COUNT = 6 };
+
+// Event-pair timer on the graph stream; accumulated lazily when the stats are read.
+struct KernelTimer {
+  std::vector<hipEvent_t> pending_start, pending_stop;
+  std::vector<hipEvent_t> free_events;
+  double total_ms = 0.0;
+  int64_t launches = 0;
+};
+
+}  // namespace blp
+
+struct blp_graph {
+  int device = 0;
+  int n_cu = 256;
+  hipStream_t stream = nullptr;
+  int64_t n = 0;    // nodes
+  int64_t nnz = 0;  // stored CSR entries (both directions, no self-loops)
+  int64_t* d_rp = nullptr;   // [n+1]
+  int32_t* d_ci = nullptr;   // [nnz]
+  double* d_aaw = nullptr;   // [n] Adamic-Adar weight per node (or null)
+  // host mirrors used only for launch planning (bitmap universe bounds)
+  std::vector<int64_t> h_rp;
+  std::vector<int32_t> h_ci;
+  // grouping scratch (per handle, reused by every batch)
+  blp::DevBuf cnt, off, cursor, active, scratch;
+  blp::KernelTimer timers[blp::K_COUNT];
+};
+
+namespace blp {
+int timer_begin(blp_graph* g, int k, hipEvent_t* start);
+int timer_end(blp_graph* g, int k, hipEvent_t start);
+int timers_collect(blp_graph* g);
+int set_device(const blp_graph* g);
+}  // namespace blp

@@ -1,0 +1,267 @@
+// Graph handle, host CSR builder, errors, timers (libblp.so).
+//
+// Replaces snap.LoadEdgeList(snap.PUNGraph, ...) (similarity.py:16) and SNAP's degree
+// lookups (similarity.py:121): the undirected simple graph lives in HBM as one CSR over
+// dense node ids, both directions stored, rows sorted ascending, int64 row offsets and
+// int32 column ids.
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+
+#include "blp_internal.h"
+
+namespace blp {
+
+static thread_local std::string g_last_error;
+
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+int fail(int code, const std::string& msg) {
+  set_error(msg);
+  return code;
+}
+
+int hip_fail(hipError_t e, const char* what, const char* file, int line) {
+  char buf[512];
+  snprintf(buf, sizeof(buf), "%s failed: %s (%d) at %s:%d", what, hipGetErrorString(e), (int)e, file, line);
+  set_error(buf);
+  return BLP_E_HIP_BASE - (int)e;
+}
+
+int DevBuf::reserve(size_t want) {
+  if (want <= bytes && p) return BLP_OK;
+  if (p) {
+    BLP_HIP(hipFree(p));
+    p = nullptr;
+    bytes = 0;
+  }
+  size_t sz = std::max<size_t>(want, 256);
+  BLP_HIP(hipMalloc(&p, sz));
+  bytes = sz;
+  return BLP_OK;
+}
+
+void DevBuf::release() {
+  if (p) (void)hipFree(p);
+  p = nullptr;
+  bytes = 0;
+}
+
+int set_device(const blp_graph* g) {
+  BLP_HIP(hipSetDevice(g->device));
+  return BLP_OK;
+}
+
+int timer_begin(blp_graph* g, int k, hipEvent_t* start) {
+  KernelTimer& t = g->timers[k];
+  if (t.free_events.empty()) {
+    hipEvent_t e;
+    BLP_HIP(hipEventCreate(&e));
+    t.free_events.push_back(e);
+  }
+  *start = t.free_events.back();
+  t.free_events.pop_back();
+  BLP_HIP(hipEventRecord(*start, g->stream));
+  return BLP_OK;
+}
+
+int timer_end(blp_graph* g, int k, hipEvent_t start) {
+  KernelTimer& t = g->timers[k];
+  hipEvent_t stop;
+  if (t.free_events.empty()) {
+    BLP_HIP(hipEventCreate(&stop));
+  } else {
+    stop = t.free_events.back();
+    t.free_events.pop_back();
+  }
+  BLP_HIP(hipEventRecord(stop, g->stream));
+  t.pending_start.push_back(start);
+  t.pending_stop.push_back(stop);
+  t.launches++;
+  // keep the pending list bounded: fold finished pairs in as we go
+  if (t.pending_stop.size() > 4096) return timers_collect(g);
+  return BLP_OK;
+}
+
+int timers_collect(blp_graph* g) {
+  for (int k = 0; k < K_COUNT; ++k) {
+    KernelTimer& t = g->timers[k];
+    for (size_t i = 0; i < t.pending_stop.size(); ++i) {
+      BLP_HIP(hipEventSynchronize(t.pending_stop[i]));
+      float ms = 0.f;
+      BLP_HIP(hipEventElapsedTime(&ms, t.pending_start[i], t.pending_stop[i]));
+      t.total_ms += ms;
+      t.free_events.push_back(t.pending_start[i]);
+      t.free_events.push_back(t.pending_stop[i]);
+    }
+    t.pending_start.clear();
+    t.pending_stop.clear();
+  }
+  return BLP_OK;
+}
+
+}  // namespace blp
+
+using namespace blp;
+
+extern "C" {
+
+const char* blp_last_error(void) { return g_last_error.c_str(); }
+
+const char* blp_version(void) { return "libblp 0.1 (gfx950)"; }
+
+int blp_device_count(int* n) {
+  BLP_CHECK(n, BLP_E_ARG, "blp_device_count: null out");
+  BLP_HIP(hipGetDeviceCount(n));
+  return BLP_OK;
+}
+
+int blp_device_sync(int device) {
+  BLP_HIP(hipSetDevice(device));
+  BLP_HIP(hipDeviceSynchronize());
+  return BLP_OK;
+}
+
+int blp_csr_from_edges(int64_t n, int64_t m, const int32_t* a, const int32_t* b, int64_t* row_ptr,
+                       int32_t* col_idx, uint8_t* self_loop, int64_t* nnz_out) {
+  BLP_CHECK(n >= 0 && m >= 0 && row_ptr && nnz_out && (m == 0 || (a && b && col_idx)), BLP_E_ARG,
+            "blp_csr_from_edges: bad arguments");
+  BLP_CHECK(n < (int64_t(1) << 31), BLP_E_ARG, "blp_csr_from_edges: n_nodes must fit int32");
+  std::vector<int64_t> cnt(n + 1, 0);
+  if (self_loop) std::memset(self_loop, 0, (size_t)n);
+  for (int64_t i = 0; i < m; ++i) {
+    int32_t u = a[i], v = b[i];
+    if (u < 0 || v < 0 || u >= n || v >= n) return fail(BLP_E_ARG, "blp_csr_from_edges: node id out of range");
+    if (u == v) {
+      if (self_loop) self_loop[u] = 1;
+      continue;
+    }
+    cnt[u + 1]++;
+    cnt[v + 1]++;
+  }
+  for (int64_t i = 0; i < n; ++i) cnt[i + 1] += cnt[i];
+  std::vector<int64_t> cur(cnt.begin(), cnt.end() - 1);
+  for (int64_t i = 0; i < m; ++i) {
+    int32_t u = a[i], v = b[i];
+    if (u == v) continue;
+    col_idx[cur[u]++] = v;
+    col_idx[cur[v]++] = u;
+  }
+  // sort each row and drop duplicate edges (SNAP keeps one copy of a multi-edge)
+  int64_t w = 0;
+  row_ptr[0] = 0;
+  for (int64_t r = 0; r < n; ++r) {
+    int64_t s = cnt[r], e = cnt[r + 1];
+    std::sort(col_idx + s, col_idx + e);
+    int64_t start = w;
+    for (int64_t i = s; i < e; ++i)
+      if (i == s || col_idx[i] != col_idx[i - 1]) col_idx[w++] = col_idx[i];
+    (void)start;
+    row_ptr[r + 1] = w;
+  }
+  *nnz_out = w;
+  return BLP_OK;
+}
+
+int blp_graph_create(const int64_t* row_ptr, const int32_t* col_idx, int64_t n, const double* aaw,
+                     int device, blp_graph** out) {
+  BLP_CHECK(out && row_ptr && n >= 0, BLP_E_ARG, "blp_graph_create: bad arguments");
+  BLP_CHECK(n < (int64_t(1) << 31), BLP_E_ARG, "blp_graph_create: n_nodes must fit int32");
+  int64_t nnz = row_ptr[n];
+  BLP_CHECK(nnz >= 0 && (nnz == 0 || col_idx), BLP_E_ARG, "blp_graph_create: bad row_ptr/col_idx");
+  for (int64_t i = 0; i < n; ++i)
+    BLP_CHECK(row_ptr[i] <= row_ptr[i + 1], BLP_E_ARG, "blp_graph_create: row_ptr not monotone");
+  for (int64_t i = 0; i < nnz; ++i)
+    BLP_CHECK(col_idx[i] >= 0 && col_idx[i] < n, BLP_E_ARG, "blp_graph_create: col_idx out of range");
+  int ndev = 0;
+  BLP_HIP(hipGetDeviceCount(&ndev));
+  BLP_CHECK(device >= 0 && device < ndev, BLP_E_ARG, "blp_graph_create: no such device");
+  BLP_HIP(hipSetDevice(device));
+  blp_graph* g = new blp_graph();
+  g->device = device;
+  g->n = n;
+  g->nnz = nnz;
+  int rc = BLP_OK;
+  auto cleanup = [&](int code) {
+    blp_graph_destroy(g);
+    return code;
+  };
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess) g->n_cu = prop.multiProcessorCount;
+  if ((rc = [&]() -> int {
+         BLP_HIP(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
+         BLP_HIP(hipMalloc(&g->d_rp, sizeof(int64_t) * (n + 1)));
+         BLP_HIP(hipMalloc(&g->d_ci, sizeof(int32_t) * std::max<int64_t>(nnz, 1)));
+         BLP_HIP(hipMemcpy(g->d_rp, row_ptr, sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice));
+         if (nnz) BLP_HIP(hipMemcpy(g->d_ci, col_idx, sizeof(int32_t) * nnz, hipMemcpyHostToDevice));
+         if (aaw) {
+           BLP_HIP(hipMalloc(&g->d_aaw, sizeof(double) * std::max<int64_t>(n, 1)));
+           if (n) BLP_HIP(hipMemcpy(g->d_aaw, aaw, sizeof(double) * n, hipMemcpyHostToDevice));
+         }
+         return BLP_OK;
+       }()) != BLP_OK)
+    return cleanup(rc);
+  g->h_rp.assign(row_ptr, row_ptr + n + 1);
+  g->h_ci.assign(col_idx, col_idx + nnz);
+  *out = g;
+  return BLP_OK;
+}
+
+int blp_graph_destroy(blp_graph* g) {
+  if (!g) return BLP_OK;
+  (void)hipSetDevice(g->device);
+  if (g->stream) (void)hipStreamSynchronize(g->stream);
+  for (auto& t : g->timers) {
+    for (auto e : t.pending_start) (void)hipEventDestroy(e);
+    for (auto e : t.pending_stop) (void)hipEventDestroy(e);
+    for (auto e : t.free_events) (void)hipEventDestroy(e);
+  }
+  g->cnt.release();
+  g->off.release();
+  g->cursor.release();
+  g->active.release();
+  g->scratch.release();
+  if (g->d_rp) (void)hipFree(g->d_rp);
+  if (g->d_ci) (void)hipFree(g->d_ci);
+  if (g->d_aaw) (void)hipFree(g->d_aaw);
+  if (g->stream) (void)hipStreamDestroy(g->stream);
+  delete g;
+  return BLP_OK;
+}
+
+int blp_graph_info(const blp_graph* g, int64_t* n, int64_t* nnz, int* device) {
+  BLP_CHECK(g, BLP_E_ARG, "blp_graph_info: null graph");
+  if (n) *n = g->n;
+  if (nnz) *nnz = g->nnz;
+  if (device) *device = g->device;
+  return BLP_OK;
+}
+
+int blp_graph_sync(blp_graph* g) {
+  BLP_CHECK(g, BLP_E_ARG, "blp_graph_sync: null graph");
+  BLP_HIP(hipSetDevice(g->device));
+  BLP_HIP(hipStreamSynchronize(g->stream));
+  return BLP_OK;
+}
+
+int blp_stats_reset(blp_graph* g) {
+  BLP_CHECK(g, BLP_E_ARG, "blp_stats_reset: null graph");
+  int rc = timers_collect(g);
+  if (rc) return rc;
+  for (auto& t : g->timers) {
+    t.total_ms = 0.0;
+    t.launches = 0;
+  }
+  return BLP_OK;
+}
+
+int blp_stats_get(blp_graph* g, int kernel, double* total_ms, int64_t* launches) {
+  BLP_CHECK(g && kernel >= 0 && kernel < K_COUNT, BLP_E_ARG, "blp_stats_get: bad arguments");
+  int rc = timers_collect(g);
+  if (rc) return rc;
+  if (total_ms) *total_ms = g->timers[kernel].total_ms;
+  if (launches) *launches = g->timers[kernel].launches;
+  return BLP_OK;
+}
+
+}  // extern "C"

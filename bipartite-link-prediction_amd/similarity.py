@@ -1,0 +1,183 @@
+"""Drop-in for the reference's similarity.py, computed by the HIP engine (libblp.so).
+
+Same call surface (similarity.py:11-126) and the same score files, bit-for-bit in value:
+
+* ``main(example_file, graph_file, u_methods, u_outfiles, b_methods, b_outfiles)``
+* ``users(examples, G, methods, outfiles)`` / ``business(examples, G, methods, outfiles)``
+* ``common_neighbors(s1, s2)``, ``jaccard(s1, s2)``, ``adamic_adar(s1, s2, G)``
+
+``G`` is a :class:`blp.DeviceGraph` (from ``load_edge_list``), the engine's stand-in for
+SNAP's PUNGraph. ``users``/``business`` score every (user, business) pair of
+``examples`` in ONE fused device pass for all requested methods (the reference loops
+once per method, similarity.py:48,91) and then write one JSON file per method in the
+reference's dict order.
+
+Reference behaviour kept on purpose:
+* a pair with a node absent from the graph scores ``0`` (similarity.py:59-60,104-105);
+* common_neighbors is a JSON int; jaccard a float; adamic_adar a float, or the int ``0``
+  when nothing was added (similarity.py:118);
+* an unknown method name assigns nothing for present pairs (no branch matches);
+* business side: the Adamic-Adar branch only fires for the string at similarity.py:102,
+  so ``'adamic_adar'`` yields a file holding only the missing-node zeros. Pass
+  ``fix_adamic=True`` to score it instead (useful downstream, supervised_models.py:124);
+* the per-pair ``print`` calls of business() (similarity.py:97,100) are not reproduced.
+"""
+import datetime
+
+import numpy as np
+
+import blp
+import util
+
+BUGGY_B_ADAMIC = "Beginning adamic adar coefficient computation"  # similarity.py:102
+_U_BITS = {"common_neighbors": blp.CN, "jaccard": blp.JACCARD, "adamic_adar": blp.ADAMIC}
+_B_BITS = {"common_neighbors": blp.CN, "jaccard": blp.JACCARD, BUGGY_B_ADAMIC: blp.ADAMIC}
+
+
+# ----------------------------------------------------------------------------- host helpers
+def flatten_examples(examples):
+    """examples {u: {v: label}} -> (u_keys, v_keys, u_ids, v_ids) in dict order."""
+    u_keys, v_keys = [], []
+    for u, inner in examples.items():
+        for v in inner:
+            u_keys.append(u)
+            v_keys.append(v)
+    u_ids = np.array([int(k) for k in u_keys], dtype=np.int64)
+    v_ids = np.array([int(k) for k in v_keys], dtype=np.int64)
+    return u_keys, v_keys, u_ids, v_ids
+
+
+def method_mask(methods, table):
+    m = 0
+    for name in methods:
+        m |= table.get(name, 0)
+    return m
+
+
+def _values(method_bit, present, scores):
+    """Per-pair Python values for one method, None where the reference assigns nothing."""
+    n = len(present)
+    if not method_bit:  # unknown method string: only the missing-node zeros are written
+        vals = [None] * n
+        for i in np.flatnonzero(~present).tolist():
+            vals[i] = 0
+        return vals
+    if method_bit == blp.CN:
+        got = scores["cn"].astype(np.int64).tolist()
+    elif method_bit == blp.JACCARD:
+        got = scores["jaccard"].tolist()
+    else:
+        a = scores["adamic"]
+        got = a.tolist()
+        for i in np.flatnonzero(a == 0.0).tolist():
+            got[i] = 0  # similarity.py:118: the untouched int 0
+    if present.all():
+        return got
+    vals = [0] * n  # similarity.py:59-60 / 104-105: missing node -> 0
+    for k, i in enumerate(np.flatnonzero(present).tolist()):
+        vals[i] = got[k]
+    return vals
+
+
+def assemble(examples, vals):
+    """Nest per-pair values back into {u: {v: value}} (defaultdict(dict) semantics)."""
+    out = {}
+    i = 0
+    for u, inner in examples.items():
+        d = None
+        for v in inner:
+            val = vals[i]
+            i += 1
+            if val is not None:
+                if d is None:
+                    d = out[u] = {}
+                d[v] = val
+    return out
+
+
+def score_examples(examples, G, side, mask):
+    """Score every pair of `examples` on the device.
+
+    Returns (present mask over the flattened pairs, scores dict over present pairs)."""
+    _, _, u_ids, v_ids = flatten_examples(examples)
+    du, pu = G.lookup(u_ids)
+    dv, pv = G.lookup(v_ids)
+    present = pu & pv
+    if side == 0:
+        scores = G.score_pairs(du[present], dv[present], mask)
+    else:
+        scores = G.score_pairs(dv[present], du[present], mask)
+    return present, scores
+
+
+def _run_side(examples, G, methods, outfiles, table, side):
+    mask = method_mask(methods, table)
+    present, scores = score_examples(examples, G, side, mask | blp.CN)
+    results = []
+    for m, f in zip(methods, outfiles):
+        sim = assemble(examples, _values(table.get(m, 0), present, scores))
+        if f is not None:
+            util.write_json(sim, f)
+        results.append(sim)
+    return results
+
+
+# ----------------------------------------------------------------------------- reference API
+def main(example_file, graph_file, u_methods, u_outfiles, b_methods, b_outfiles):
+    """similarity.main (similarity.py:11-18)."""
+    datetime.datetime.now()
+    print("Loading examples...")
+    examples = util.load_json(example_file)
+    print("Loading graph...")
+    G = blp.load_edge_list(graph_file)
+    users(examples, G, u_methods, u_outfiles)
+    business(examples, G, b_methods, b_outfiles)
+
+
+def users(examples, G, methods, outfiles):
+    """similarity.users (similarity.py:20-61): x = user (exact 2-hop set), y = business."""
+    print("Scoring user side on the device...")
+    return _run_side(examples, G, methods, outfiles, _U_BITS, side=0)
+
+
+def business(examples, G, methods, outfiles, *, fix_adamic=False):
+    """similarity.business (similarity.py:63-106): x = business (exact 2-hop set), y = user."""
+    print("Scoring business side on the device...")
+    table = dict(_B_BITS)
+    if fix_adamic:
+        table["adamic_adar"] = blp.ADAMIC
+    return _run_side(examples, G, methods, outfiles, table, side=1)
+
+
+# Scalar set-level definitions (similarity.py:108-126), kept for API compatibility with
+# callers that hold their own Python sets. The batch path above never calls them.
+def jaccard(setone, settwo):
+    intersection = len(setone.intersection(settwo))
+    union = len(setone.union(settwo))
+    return float(intersection) / float(union)
+
+
+def common_neighbors(setone, settwo):
+    return len(setone.intersection(settwo))
+
+
+def adamic_adar(setone, settwo, G):
+    import math
+
+    total = 0
+    for i in setone.intersection(settwo):
+        deg = G.GetDeg(i)
+        if deg > 1:
+            total += math.log(deg) ** -1
+        else:
+            total += 0
+    return total
+
+
+if __name__ == "__main__":
+    names = ["common_neighbors", "jaccard", "adamic_adar"]
+    for split in ("train", "test"):
+        d = "./data/%s/" % split
+        main(d + "examples.json", d + "graph.txt", names,
+             [d + "u_cn.json", d + "u_jaccard.json", d + "u_adamic.json"], names,
+             [d + "b_cn.json", d + "b_jaccard.json", d + "b_adamic.json"])

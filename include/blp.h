@@ -1,0 +1,123 @@
+/*
+ * blp.h — C-ABI of libblp.so, the MI355X-native bipartite link-scoring engine.
+ *
+ * Drop-in boundary for the reference's hot path. The reference has no
+ * FFI of its own: its boundary is the Python module surface of similarity.py / svd.py /
+ * random_walks.py plus the JSON score-file contract. The Python host modules in
+ * bipartite-link-prediction_amd/ keep that surface and bind these entry points with ctypes
+ * (see INTEGRATION.md). Every function below names the reference computation it replaces.
+ *
+ * Conventions
+ *   - Plain pointers and sizes only; no torch / HIP types cross the ABI.
+ *   - Return 0 on success, a negative code on failure (BLP_E_*; HIP errors are
+ *     -1000 - hipError_t). blp_last_error() returns a thread-local message.
+ *   - Host buffers passed in are read during the call only; the caller keeps ownership.
+ *   - A graph handle owns its device memory and one HIP stream; calls on one handle are
+ *     serialised by the caller (not re-entrant). One host thread per GPU may drive
+ *     several handles concurrently.
+ *   - Node ids are dense int32 in [0, n_nodes). The Python host maps the reference's
+ *     integer node ids (SNAP TInt) to dense ids.
+ *   - Methods are a bit mask: BLP_CN=1 (common_neighbors), BLP_JACCARD=2, BLP_ADAMIC=4.
+ */
+#ifndef BLP_H_
+#define BLP_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BLP_OK 0
+#define BLP_E_ARG (-1)      /* bad argument (null pointer, id out of range, size overflow) */
+#define BLP_E_STATE (-2)    /* handle used in the wrong state */
+#define BLP_E_NOMEM (-3)    /* host allocation failed */
+#define BLP_E_UNSUP (-4)    /* configuration not supported by this build */
+#define BLP_E_ZERODIV (-5)  /* Jaccard union of size 0 (reference raises ZeroDivisionError) */
+#define BLP_E_HIP_BASE (-1000)
+
+#define BLP_CN 1u
+#define BLP_JACCARD 2u
+#define BLP_ADAMIC 4u
+
+typedef struct blp_graph blp_graph;
+typedef struct blp_batch blp_batch;
+
+/* ---------------------------------------------------------------- runtime */
+const char* blp_last_error(void);
+const char* blp_version(void);
+int blp_device_count(int* n);
+int blp_device_sync(int device); /* hipDeviceSynchronize on `device` */
+
+/* ---------------------------------------------------------------- graph
+ * Replaces snap.LoadEdgeList(snap.PUNGraph, graph_file, 0, 1) (similarity.py:16) and the
+ * per-node degree lookups G.GetNI(i).GetDeg() (similarity.py:121).
+ *
+ * blp_csr_from_edges: host helper. Builds the undirected simple-graph CSR of an edge list
+ * over dense ids: both directions, duplicates removed, rows sorted ascending, self-loops
+ * NOT stored in the CSR (they never change a BFS hop set) but flagged in self_loop[] because
+ * SNAP's GetDeg counts a self-loop once. row_ptr has n_nodes+1 entries; col_idx must hold
+ * 2*n_edges entries; *nnz_out receives the stored entry count.                           */
+int blp_csr_from_edges(int64_t n_nodes, int64_t n_edges, const int32_t* a, const int32_t* b,
+                       int64_t* row_ptr, int32_t* col_idx, uint8_t* self_loop, int64_t* nnz_out);
+
+/* blp_edges_parse: SNAP LoadEdgeList's text format (similarity.py:16): one edge per line,
+ * whitespace-separated integer columns c0 and c1, lines starting with '#' skipped, lines
+ * with too few columns skipped. Two calls: with a == b == NULL it only counts (*m_out);
+ * then call again with arrays of *m_out entries. Multi-threaded, reads the file once per
+ * call (the OS page cache serves the second read).                                       */
+int blp_edges_parse(const char* path, int c0, int c1, int64_t* a, int64_t* b, int64_t* m_out);
+
+/* Upload a CSR (from blp_csr_from_edges or equivalent) to device `device`.
+ * aa_weight[n_nodes]: per-node Adamic-Adar term, (log deg)^-1 for SNAP degree > 1 else 0,
+ * computed by the caller with the reference's own arithmetic (similarity.py:121-125);
+ * may be NULL when BLP_ADAMIC is never requested.                                        */
+int blp_graph_create(const int64_t* row_ptr, const int32_t* col_idx, int64_t n_nodes,
+                     const double* aa_weight, int device, blp_graph** out);
+int blp_graph_destroy(blp_graph* g);
+int blp_graph_info(const blp_graph* g, int64_t* n_nodes, int64_t* nnz, int* device);
+int blp_graph_sync(blp_graph* g); /* wait for all work queued on the handle's stream */
+
+/* ---------------------------------------------------------------- pair scoring
+ * Replaces the hot loops of similarity.users (similarity.py:20-61) and similarity.business
+ * (similarity.py:63-106): for each pair (x, y), with H2(x) = GetNodesAtHop(x, 2) (nodes at
+ * exact BFS distance 2) and N(y) = GetNodesAtHop(y, 1):
+ *   cn  = |H2(x) ∩ N(y)|                                    common_neighbors  (:113-114)
+ *   jac = cn / |H2(x) ∪ N(y)|  (fp64, correctly rounded)    jaccard           (:108-111)
+ *   aa  = Σ_{w ∈ H2(x) ∩ N(y)} aa_weight[w]                  adamic_adar       (:116-126)
+ * User side (users()):  x = user, y = business.  Business side (business()): x = business,
+ * y = user. Pairs whose node is absent from the graph never reach the engine (the host
+ * writes the reference's 0, similarity.py:59-60,104-105).
+ *
+ * blp_score_pairs: one-shot (host in, host out; synchronous).
+ *   side 0: x = pair_user, y = pair_business;  side 1: x = pair_business, y = pair_user.
+ *   Output arrays may be NULL for methods not in `mask`.                                   */
+int blp_score_pairs(blp_graph* g, int side, uint32_t mask, const int32_t* pair_user,
+                    const int32_t* pair_business, int64_t n_pairs, uint32_t* cn, double* jac,
+                    double* aa);
+
+/* Device-resident batch (bench / repeated scoring). blp_batch_create copies the pairs to
+ * HBM and plans the launch (bitmap universe, variant). blp_batch_score enqueues one full
+ * pass on the graph's stream: group pairs by source on the device, score, write results in
+ * the caller's pair order into device buffers. blp_batch_fetch copies results to the host. */
+int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n_pairs,
+                     blp_batch** out);
+int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask);
+int blp_batch_fetch(blp_graph* g, blp_batch* b, uint32_t* cn, double* jac, double* aa);
+int blp_batch_destroy(blp_batch* b);
+/* Launch plan actually used: universe lo/hi (bitmap range), bitmap chunks, threads per
+ * block, lanes per pair group. For tests and DESIGN.md bookkeeping.                       */
+int blp_batch_plan(const blp_batch* b, int64_t* lo, int64_t* hi, int* chunks, int* block,
+                   int* group);
+
+/* ---------------------------------------------------------------- stats
+ * Per-kernel device time (ms, HIP events on the handle's stream) accumulated since the
+ * last reset, for bench.py's roofline figure. kernel: 0 = pair scorer, 1 = grouping
+ * (count+scan+scatter), 2 = svd pairs, 3 = svd dense top-k, 4 = random walk, 5 = hop-3. */
+int blp_stats_reset(blp_graph* g);
+int blp_stats_get(blp_graph* g, int kernel, double* total_ms, int64_t* launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BLP_H_ */

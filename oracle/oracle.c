@@ -1,0 +1,204 @@
+/*
+ * CPU ORACLE (C restatement) — TEST INFRASTRUCTURE ONLY.
+ *
+ * Checker for the HIP engine on cases too large for the pure-Python oracle, and the
+ * `cpu_baseline` leg of bench.py. Never linked or loaded by the product.
+ *
+ * It restates the reference algorithm with the same structure:
+ *   - og_create:       snap.LoadEdgeList(PUNGraph, ...) adjacency (similarity.py:16):
+ *                      undirected, deduplicated, a self-loop stored once (GetDeg counts it once).
+ *   - og_score_pairs:  similarity.users/business (similarity.py:20-106): per distinct source x
+ *                      the exact-distance-2 set H2(x) (GetNodesAtHop(x,2), :29/:74) as a BFS
+ *                      marker set; per pair |H2(x) ∩ N(y)| (:113-114), the Jaccard quotient
+ *                      float(|∩|)/float(|∪|) (:108-111) and the Adamic-Adar sum of
+ *                      (log deg)^-1 over deg > 1 (:116-126), N(y) = GetNodesAtHop(y,1) (:41/:85).
+ *   - og_hop3:         dataset_maker.py:139 GetNodesAtHop(G,u,3) candidate sets.
+ * Pinned against tests/golden (reference outputs) by tests/test_oracle.py.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+typedef struct {
+    int64_t n;
+    int64_t* rp;   /* n+1 */
+    int32_t* ci;   /* rp[n]; sorted, unique; includes a self-loop once if present */
+    int32_t* deg;  /* SNAP GetDeg = row length */
+    uint8_t* self; /* 1 if the node has a self-loop */
+} og_graph;
+
+static int cmp_u64(const void* a, const void* b) {
+    uint64_t x = *(const uint64_t*)a, y = *(const uint64_t*)b;
+    return x < y ? -1 : (x > y);
+}
+
+static int cmp_i32(const void* a, const void* b) {
+    int32_t x = *(const int32_t*)a, y = *(const int32_t*)b;
+    return x < y ? -1 : (x > y);
+}
+
+og_graph* og_create(int64_t n, int64_t m, const int32_t* a, const int32_t* b) {
+    og_graph* g = (og_graph*)calloc(1, sizeof(og_graph));
+    uint64_t* keys = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)(2 * m + 1));
+    int64_t k = 0;
+    for (int64_t i = 0; i < m; ++i) {
+        keys[k++] = ((uint64_t)(uint32_t)a[i] << 32) | (uint32_t)b[i];
+        if (a[i] != b[i]) keys[k++] = ((uint64_t)(uint32_t)b[i] << 32) | (uint32_t)a[i];
+    }
+    qsort(keys, (size_t)k, sizeof(uint64_t), cmp_u64);
+    int64_t u = 0;
+    for (int64_t i = 0; i < k; ++i)
+        if (i == 0 || keys[i] != keys[i - 1]) keys[u++] = keys[i];
+    g->n = n;
+    g->rp = (int64_t*)calloc((size_t)n + 1, sizeof(int64_t));
+    g->ci = (int32_t*)malloc(sizeof(int32_t) * (size_t)(u + 1));
+    g->deg = (int32_t*)calloc((size_t)n + 1, sizeof(int32_t));
+    g->self = (uint8_t*)calloc((size_t)n + 1, 1);
+    for (int64_t i = 0; i < u; ++i) {
+        int32_t r = (int32_t)(keys[i] >> 32), c = (int32_t)(keys[i] & 0xffffffffu);
+        g->rp[r + 1]++;
+        g->ci[i] = c;
+        if (r == c) g->self[r] = 1;
+    }
+    for (int64_t i = 0; i < n; ++i) {
+        g->rp[i + 1] += g->rp[i];
+        g->deg[i] = (int32_t)(g->rp[i + 1] - g->rp[i]);
+    }
+    free(keys);
+    return g;
+}
+
+void og_destroy(og_graph* g) {
+    if (!g) return;
+    free(g->rp);
+    free(g->ci);
+    free(g->deg);
+    free(g->self);
+    free(g);
+}
+
+int64_t og_n(const og_graph* g) { return g->n; }
+int64_t og_nnz(const og_graph* g) { return g->rp[g->n]; }
+int32_t og_degree(const og_graph* g, int32_t v) { return g->deg[v]; }
+
+/* Exact BFS distances from x up to `depth` into dist[] (-1 = farther). Returns the
+ * number of nodes at exactly `depth`. visited[] lists touched nodes for cleanup. */
+static int64_t bfs_exact(const og_graph* g, int32_t x, int depth, int8_t* dist, int32_t* visited,
+                         int64_t* nvisited) {
+    int64_t nv = 0, lo = 0, at = 0;
+    dist[x] = 0;
+    visited[nv++] = x;
+    for (int d = 0; d < depth; ++d) {
+        int64_t hi = nv;
+        for (int64_t i = lo; i < hi; ++i) {
+            int32_t z = visited[i];
+            for (int64_t e = g->rp[z]; e < g->rp[z + 1]; ++e) {
+                int32_t w = g->ci[e];
+                if (dist[w] < 0) {
+                    dist[w] = (int8_t)(d + 1);
+                    visited[nv++] = w;
+                }
+            }
+        }
+        lo = hi;
+    }
+    at = nv - lo;
+    *nvisited = nv;
+    return at;
+}
+
+/* One pair batch; pairs need not be grouped (we group by x internally, in x order). */
+int og_score_pairs(const og_graph* g, int64_t np, const int32_t* xs, const int32_t* ys, uint32_t mask,
+                   uint32_t* cn, double* jac, double* aa, uint32_t* h2out, int nthreads) {
+    int64_t n = g->n;
+    int64_t* cnt = (int64_t*)calloc((size_t)n + 1, sizeof(int64_t));
+    int64_t* perm = (int64_t*)malloc(sizeof(int64_t) * (size_t)(np + 1));
+    for (int64_t i = 0; i < np; ++i) cnt[xs[i] + 1]++;
+    for (int64_t i = 0; i < n; ++i) cnt[i + 1] += cnt[i];
+    int64_t* cur = (int64_t*)malloc(sizeof(int64_t) * (size_t)(n + 1));
+    memcpy(cur, cnt, sizeof(int64_t) * (size_t)(n + 1));
+    for (int64_t i = 0; i < np; ++i) perm[cur[xs[i]]++] = i;
+    free(cur);
+    int bad = 0;
+#ifdef _OPENMP
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel num_threads(nthreads) reduction(| : bad)
+#endif
+    {
+        int8_t* dist = (int8_t*)malloc((size_t)n + 1);
+        int32_t* visited = (int32_t*)malloc(sizeof(int32_t) * ((size_t)n + 1));
+        memset(dist, -1, (size_t)n + 1);
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 1)
+#endif
+        for (int64_t x = 0; x < n; ++x) {
+            if (cnt[x + 1] == cnt[x]) continue;
+            int64_t nv = 0;
+            int64_t h2 = bfs_exact(g, (int32_t)x, 2, dist, visited, &nv);
+            for (int64_t k = cnt[x]; k < cnt[x + 1]; ++k) {
+                int64_t p = perm[k];
+                int32_t y = ys[p];
+                uint32_t c = 0;
+                double s = 0.0;
+                int64_t hop1 = g->deg[y] - g->self[y];
+                for (int64_t e = g->rp[y]; e < g->rp[y + 1]; ++e) {
+                    int32_t w = g->ci[e];
+                    if (w == y) continue;
+                    if (dist[w] == 2) {
+                        ++c;
+                        if (g->deg[w] > 1) s += pow(log((double)g->deg[w]), -1.0);
+                    }
+                }
+                if (mask & 1u) cn[p] = c;
+                if (mask & 2u) {
+                    int64_t uni = h2 + hop1 - (int64_t)c;
+                    if (uni == 0) {
+                        jac[p] = NAN;
+                        bad = 1;
+                    } else
+                        jac[p] = (double)c / (double)uni;
+                }
+                if (mask & 4u) aa[p] = s;
+                if (h2out) h2out[p] = (uint32_t)h2;
+            }
+            for (int64_t i = 0; i < nv; ++i) dist[visited[i]] = -1;
+        }
+        free(dist);
+        free(visited);
+    }
+    free(cnt);
+    free(perm);
+    return bad ? 1 : 0;
+}
+
+/* Exact distance-3 sets for `nu` sources: counts[i] = |H3(users[i])|; when out != NULL
+ * the members are written (ascending) at out[sum(counts[:i])] up to cap entries. */
+int64_t og_hop3(const og_graph* g, int64_t nu, const int32_t* users, int64_t* counts, int32_t* out,
+                int64_t cap) {
+    int64_t n = g->n, total = 0;
+    int8_t* dist = (int8_t*)malloc((size_t)n + 1);
+    int32_t* visited = (int32_t*)malloc(sizeof(int32_t) * ((size_t)n + 1));
+    int32_t* tmp = (int32_t*)malloc(sizeof(int32_t) * ((size_t)n + 1));
+    memset(dist, -1, (size_t)n + 1);
+    for (int64_t i = 0; i < nu; ++i) {
+        int64_t nv = 0;
+        int64_t c = bfs_exact(g, users[i], 3, dist, visited, &nv);
+        counts[i] = c;
+        if (out) {
+            int64_t t = 0;
+            for (int64_t j = nv - c; j < nv; ++j) tmp[t++] = visited[j];
+            qsort(tmp, (size_t)t, sizeof(int32_t), cmp_i32); /* canonical ascending listing */
+            for (int64_t j = 0; j < t && total + j < cap; ++j) out[total + j] = tmp[j];
+        }
+        total += c;
+        for (int64_t j = 0; j < nv; ++j) dist[visited[j]] = -1;
+    }
+    free(dist);
+    free(visited);
+    free(tmp);
+    return total;
+}

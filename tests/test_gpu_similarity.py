@@ -1,0 +1,139 @@
+"""GPU parity: the HIP pair scorer (via the drop-in similarity module and the C-ABI)
+against the reference's golden outputs and the C oracle. Marked `gpu`."""
+import math
+import os
+
+import numpy as np
+import pytest
+
+import blp
+import coracle
+import similarity
+from helpers import (B_FILES, GOLDEN, METHODS, SIM_CASES, U_FILES, assert_same_scores, bipartite_edges, dense_edges,
+                     golden, load)
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("case", SIM_CASES)
+def test_main_writes_reference_files(gpu, case, tmp_path):
+    d = os.path.join(GOLDEN, case)
+    uf = [str(tmp_path / f) for f in U_FILES]
+    bf = [str(tmp_path / f) for f in B_FILES]
+    similarity.main(os.path.join(d, "examples.json"), os.path.join(d, "graph.txt"), METHODS, uf, METHODS, bf)
+    for m, f in zip(METHODS, U_FILES):
+        assert_same_scores(load(str(tmp_path / f)), golden(case, f), m)
+    for m, f in zip(METHODS, B_FILES):
+        assert_same_scores(load(str(tmp_path / f)), golden(case, f), m)
+
+
+def _check_against_oracle(ga, gb, x, y, mask=7):
+    """Device scores of dense-id pairs vs the C oracle on the same edge list."""
+    G = blp.DeviceGraph(ga, gb)
+    ids, da, db = dense_edges(ga, gb)
+    og = coracle.OracleGraph(len(ids), da, db)
+    # both sides use original ids; map to each engine's own dense ids
+    xo, yo = G.node_ids[x], G.node_ids[y]
+    got = G.score_pairs(x, y, mask)
+    cn, jac, aa, _ = og.score_pairs(np.searchsorted(ids, xo), np.searchsorted(ids, yo), mask)
+    np.testing.assert_array_equal(got["cn"], cn)
+    if mask & blp.JACCARD:
+        np.testing.assert_array_equal(got["jaccard"], jac)  # bit-exact
+    if mask & blp.ADAMIC:
+        np.testing.assert_allclose(got["adamic"], aa, rtol=1e-12, atol=0)
+        assert np.array_equal(got["adamic"] == 0, aa == 0)
+    return G
+
+
+@pytest.mark.parametrize("n_users,n_bus,n_draws,seed", [
+    (2000, 300, 20000, 0),     # small universe: SMALL variant, user side
+    (30000, 2000, 150000, 1),  # MED variant
+    (300000, 5000, 600000, 2), # LARGE variant, long rows (popular businesses)
+])
+def test_user_and_business_side_vs_oracle(gpu, n_users, n_bus, n_draws, seed):
+    rng = np.random.default_rng(seed)
+    a, b = bipartite_edges(rng, n_users, n_bus, n_draws)
+    G = blp.DeviceGraph(a, b)
+    nu = G.n - len(np.unique(b))
+    users = rng.choice(nu, size=min(200, nu), replace=False)
+    x = np.repeat(users, 40).astype(np.int32)
+    y = rng.integers(nu, G.n, len(x)).astype(np.int32)
+    _check_against_oracle(a, b, x, y)          # user side
+    _check_against_oracle(a, b, y, x)          # business side
+
+
+def test_general_graph_exact_distance(gpu):
+    rng = np.random.default_rng(5)
+    a = rng.integers(0, 3000, 20000)
+    b = rng.integers(0, 3000, 20000)
+    a[:50] = b[:50]  # self-loops: SNAP degree +1, hop sets unchanged
+    G = blp.DeviceGraph(a, b)
+    x = rng.integers(0, G.n, 5000).astype(np.int32)
+    y = rng.integers(0, G.n, 5000).astype(np.int32)
+    _check_against_oracle(a, b, x, y)
+
+
+@pytest.mark.parametrize("knobs", [
+    {"BLP_CHUNK_BITS": "1024"},                       # multi-chunk bitmap universe
+    {"BLP_LONG_ROW": "3"},                            # deferred long-row loops (+ list overflow)
+    {"BLP_GROUP": "8"}, {"BLP_GROUP": "16"}, {"BLP_GROUP": "32"}, {"BLP_GROUP": "64"},
+    {"BLP_CHUNK_BITS": "2048", "BLP_LONG_ROW": "7", "BLP_GROUP": "16"},
+])
+def test_kernel_paths_vs_oracle(gpu, knobs, monkeypatch):
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    rng = np.random.default_rng(11)
+    a, b = bipartite_edges(rng, 6000, 400, 40000)
+    G = blp.DeviceGraph(a, b)
+    nu = G.n - len(np.unique(b))
+    x = np.repeat(rng.choice(nu, 60, replace=False), 30).astype(np.int32)
+    y = rng.integers(nu, G.n, len(x)).astype(np.int32)
+    _check_against_oracle(a, b, x, y)
+    _check_against_oracle(a, b, y, x)
+
+
+def test_batch_repeat_is_deterministic(gpu):
+    rng = np.random.default_rng(3)
+    a, b = bipartite_edges(rng, 20000, 1000, 100000)
+    G = blp.DeviceGraph(a, b)
+    nu = G.n - len(np.unique(b))
+    x = np.repeat(rng.choice(nu, 100, replace=False), 50).astype(np.int32)
+    y = rng.integers(nu, G.n, len(x)).astype(np.int32)
+    bt = G.batch(x, y)
+    bt.score(7)
+    r1 = bt.fetch(7)
+    for _ in range(3):
+        bt.score(7)
+    r2 = bt.fetch(7)
+    for k in r1:
+        np.testing.assert_array_equal(r1[k], r2[k])
+    ms, launches = G.stats(blp._lib.K_SCORE)
+    assert launches == 4 and ms > 0
+
+
+def test_empty_and_zero_division(gpu):
+    G = blp.DeviceGraph(np.array([0, 2]), np.array([1, 3]))
+    r = G.score_pairs(np.zeros(0, np.int32), np.zeros(0, np.int32))
+    assert len(r["cn"]) == 0
+    # x = 0 has H2 = {} (its only neighbour 1 has no other neighbour); y = 3 has N = {2};
+    # union non-empty -> 0.0
+    d0, d3 = G.dense([0, 3])
+    r = G.score_pairs(np.array([d0], np.int32), np.array([d3], np.int32))
+    assert r["cn"][0] == 0 and r["jaccard"][0] == 0.0 and r["adamic"][0] == 0.0
+    # a node whose only edge is a self-loop has an empty hop-1 set: union of two empty sets
+    G2 = blp.DeviceGraph(np.array([5, 6]), np.array([5, 7]))
+    d5 = G2.dense([5])[0]
+    with pytest.raises(ZeroDivisionError):
+        G2.score_pairs(np.array([d5], np.int32), np.array([d5], np.int32))
+
+
+def test_business_fix_adamic_matches_oracle(gpu):
+    import blp_oracle as O
+
+    d = os.path.join(GOLDEN, "bip", "train")
+    ex = golden("bip/train", "examples.json")
+    G = blp.load_edge_list(os.path.join(d, "graph.txt"))
+    got = similarity.business(ex, G, ["adamic_adar"], [None], fix_adamic=True)[0]
+    adj = O.load_edge_list(os.path.join(d, "graph.txt"))
+    exp = O.business(ex, adj, [O.BUGGY_B_ADAMIC])[0]
+    assert_same_scores(got, exp, "adamic_adar")
