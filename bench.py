@@ -1,0 +1,278 @@
+"""Benchmark: candidate (user, business) pairs scored per second on MI355X.
+
+Workload (BASELINE.json configs[1], "config 2"): synthetic review graph of 1M users x
+100K businesses from 10M draws (9,947,457 unique edges), 10K example
+users per GPU, their exact distance-3 candidates sampled at 1% (dataset_maker.py:137-144)
+-> ~7M (user, business) pairs per GPU. One step = the device work of similarity.main on
+that batch (similarity.py:17-18): the user side (u_cn, u_jaccard, u_adamic fused) and the
+business side (b_cn, b_jaccard; b_adamic is the reference's empty bug file), each pass
+grouping the raw pair list by source on the device and scoring every pair. Inputs are in
+HBM before the timed region; results stay in HBM.
+
+Multi-GPU: one process per GPU (torchrun); every rank holds a replica of the graph and
+scores its own 10K users (weak scaling, no data-path collective, SURVEY.md §8(e) "small
+configs may use replicas"). Timing: barrier + device sync on both sides, max over ranks.
+
+Prints ONE JSON line (rank 0). Extras: roofline of the dominant kernel (user-side scorer,
+HIP events on its stream), the CPU baseline (C oracle, 1 thread, bounded sample) and a
+parity spot-check plus AUCs of the scores.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "bipartite-link-prediction_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+import numpy as np  # noqa: E402
+
+import blp  # noqa: E402
+from blp import synth  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+METRIC = "candidate (user,business) pairs scored/sec at 1/2/4/8 GPUs; AUC parity vs ref"
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+class Dist:
+    """torch.distributed (gloo, CPU tensors) only for the barrier and max-over-ranks."""
+
+    def __init__(self):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.pg = None
+        if self.world > 1:
+            import torch.distributed as td
+
+            td.init_process_group("gloo")
+            self.td = td
+
+    def barrier(self):
+        if self.world > 1:
+            self.td.barrier()
+
+    def max(self, v):
+        if self.world == 1:
+            return v
+        import torch
+
+        t = torch.tensor([float(v)], dtype=torch.float64)
+        self.td.all_reduce(t, op=self.td.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum(self, v):
+        if self.world == 1:
+            return v
+        import torch
+
+        t = torch.tensor([float(v)], dtype=torch.float64)
+        self.td.all_reduce(t, op=self.td.ReduceOp.SUM)
+        return float(t.item())
+
+
+def alg_bytes(G, x, y, mask, cn=None):
+    """SURVEY.md §8(d) algorithmic bytes of one scorer pass over pairs (x -> y).
+
+    per source x:  16 + 4 d_x + sum_{z in N(x)} (16 + 4 d_z)     (build H2(x))
+    per pair:      8 (pair ids) + 16 + 4 d_y (scan N(y)) + 8 CN (AA weights, if AA)
+                   + 4 (cn) + 8 (jaccard, if J) + 8 (adamic, if AA)"""
+    d = G.hop1_size.astype(np.int64)
+    src = np.unique(x)
+    rp, ci = G.row_ptr, G.col_idx
+    dz = d[ci]  # degree of each neighbour entry
+    csum = np.concatenate([[0], np.cumsum(dz)])
+    nbr_deg_sum = csum[rp[src + 1]] - csum[rp[src]]
+    per_src = (16 + 4 * d[src] + 16 * d[src] + 4 * nbr_deg_sum).sum()
+    per_pair = len(x) * (8 + 16 + 4) + 4 * d[y].sum()
+    if mask & blp.JACCARD:
+        per_pair += 8 * len(x)
+    if mask & blp.ADAMIC:
+        per_pair += 8 * len(x) + 8 * int(cn.astype(np.int64).sum())
+    return int(per_src + per_pair)
+
+
+def cpu_baseline(G, ex_x, ex_y, target_s=15.0):
+    """C oracle (oracle/oracle.c), 1 thread, on a bounded sample of the same workload:
+    all pairs of a subset of the example users (user side) and all pairs of a subset of
+    the candidate businesses (business side); rate = 1 / (1/r_user + 1/r_business)."""
+    import coracle
+
+    og = coracle.OracleGraph(G.n, *_dense_edges(G))
+    rng = np.random.default_rng(123)
+
+    def side_rate(src_arr, dst_arr, mask, budget):
+        srcs = np.unique(src_arr)
+        rng.shuffle(srcs)
+        k = max(1, min(len(srcs), 8))
+        done_pairs, spent, used = 0, 0.0, 0
+        while spent < budget and used < len(srcs):
+            pick = srcs[used:used + k]
+            used += len(pick)
+            sel = np.isin(src_arr, pick)
+            t = time.perf_counter()
+            og.score_pairs(src_arr[sel], dst_arr[sel], mask, nthreads=1)
+            spent += time.perf_counter() - t
+            done_pairs += int(sel.sum())
+            k = min(k * 2, 4096)
+        return done_pairs / spent, done_pairs, used, spent
+
+    ru, pu, su, tu = side_rate(ex_x, ex_y, 7, target_s / 2)
+    rb, pb, sb, tb = side_rate(ex_y, ex_x, 3, target_s / 2)
+    rate = 1.0 / (1.0 / ru + 1.0 / rb)
+    return {"value": rate, "unit": "pairs/s", "cores": 1, "kind": "port",
+            "sample": "C oracle (oracle/oracle.c, reference algorithm: per-source exact BFS 2-hop set, per-pair "
+                      "N(y) scan), 1 thread: user side %d pairs of %d users in %.1fs (%.0f pairs/s), business "
+                      "side %d pairs of %d businesses in %.1fs (%.0f pairs/s); combined = harmonic" %
+                      (pu, su, tu, ru, pb, sb, tb, rb)}
+
+
+def _dense_edges(G):
+    """Edge list (dense ids, each undirected edge once, self-loops restored) from the CSR."""
+    rows = np.repeat(np.arange(G.n, dtype=np.int32), np.diff(G.row_ptr))
+    keep = rows < G.col_idx
+    a = rows[keep]
+    b = G.col_idx[keep]
+    loops = np.flatnonzero(G.self_loop).astype(np.int32)
+    return np.concatenate([a, loops]), np.concatenate([b, loops])
+
+
+def parity_check(G, ex_x, ex_y, ures, bres, n_users=40):
+    """Spot-check a sample of example users (both sides) against the C oracle (not timed)."""
+    import coracle
+
+    og = coracle.OracleGraph(G.n, *_dense_edges(G))
+    rng = np.random.default_rng(7)
+    pick = rng.choice(np.unique(ex_x), size=min(n_users, len(np.unique(ex_x))), replace=False)
+    sel = np.isin(ex_x, pick)
+    cn, jac, aa, _ = og.score_pairs(ex_x[sel], ex_y[sel], 7, nthreads=8)
+    ok_u = (np.array_equal(ures["cn"][sel], cn) and np.array_equal(ures["jaccard"][sel], jac)
+            and np.allclose(ures["adamic"][sel], aa, rtol=1e-12, atol=0))
+    bcn, bjac, _, _ = og.score_pairs(ex_y[sel], ex_x[sel], 3, nthreads=8)
+    ok_b = np.array_equal(bres["cn"][sel], bcn) and np.array_equal(bres["jaccard"][sel], bjac)
+    return {"checked_pairs": int(sel.sum()), "users": int(len(pick)), "user_side_exact": bool(ok_u),
+            "business_side_exact": bool(ok_b)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2", choices=sorted(synth.CONFIGS))
+    ap.add_argument("--users", type=int, default=10_000)
+    ap.add_argument("--rate", type=float, default=0.01)
+    ap.add_argument("--sides", default="both", choices=["both", "user", "business"])
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true")
+    args = ap.parse_args()
+
+    dist = Dist()
+    dev = dist.local
+    blp.lib()
+    U, B, D = synth.CONFIGS[args.config]
+    t0 = time.time()
+    a, b = synth.review_edges(U, B, D, seed=0)
+    G = blp.DeviceGraph(a, b, device=dev)
+    del a, b
+    log("graph: %d nodes, %d unique edges, built in %.1fs" % (G.n, G.nnz // 2, time.time() - t0))
+    t0 = time.time()
+    ex_x, ex_y, ex_l = synth.make_examples(G, U, B, D, n_users=args.users, rate=args.rate, seed=dist.rank)
+    log("examples: %d pairs for %d users (%d positives) in %.1fs" %
+        (len(ex_x), len(np.unique(ex_x)), int(ex_l.sum()), time.time() - t0))
+
+    passes = []
+    if args.sides in ("both", "user"):
+        passes.append(("user", G.batch(ex_x, ex_y), blp.CN | blp.JACCARD | blp.ADAMIC))
+    if args.sides in ("both", "business"):
+        passes.append(("business", G.batch(ex_y, ex_x), blp.CN | blp.JACCARD))
+    for name, bt, _ in passes:
+        log("plan %s: %s" % (name, bt.plan()))
+
+    for _ in range(args.warmup):
+        for _, bt, mask in passes:
+            bt.score(mask)
+    blp.device_sync(dev)
+    for _, bt, _ in passes:
+        bt.stats_reset()
+
+    dist.barrier()
+    blp.device_sync(dev)
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        for _, bt, mask in passes:
+            bt.score(mask)
+    blp.device_sync(dev)
+    t_local = time.perf_counter() - t_start
+    dist.barrier()
+    t_max = dist.max(t_local)
+    pairs_total = dist.sum(len(ex_x))
+
+    # per-kernel device times (HIP events on the graph stream, same launches as timed)
+    ktimes = {}
+    for name, bt, _ in passes:
+        ms, n = bt.stats(0)
+        gms, gn = bt.stats(1)
+        ktimes[name] = {"score_ms": ms / max(n, 1), "group_ms": gms / max(gn, 1)}
+    res = {name: bt.fetch(mask) for name, bt, mask in passes}
+
+    out = {
+        "metric": METRIC,
+        "value": pairs_total * args.steps / t_max,
+        "unit": "pairs/s",
+        "n_gpus": dist.world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1e3 * t_max / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": "synthetic",
+        "config": {
+            "workload": "config2: synthetic %dK users x %dK businesses, %dM draws (%d unique edges); %d example "
+                        "users/GPU, exact hop-3 candidates kept at %g (+held-out positives); step = similarity.main "
+                        "device work: %s" % (U // 1000, B // 1000, D // 10**6, G.nnz // 2, len(np.unique(ex_x)),
+                                             args.rate, "user side CN+Jaccard+AA fused + business side CN+Jaccard"
+                                             if args.sides == "both" else args.sides + " side"),
+            "pairs_per_gpu": int(len(ex_x)),
+            "global_batch": int(pairs_total),
+            "parallelism": "replicas x%d (graph replicated, users split, no collective)" % dist.world,
+        },
+        "kernels_ms": ktimes,
+    }
+    # roofline of the dominant kernel: the user-side scorer (falls back to the first pass)
+    name0, bt0, mask0 = passes[0]
+    cn0 = res[name0]["cn"]
+    xs, ys = (ex_x, ex_y) if name0 == "user" else (ex_y, ex_x)
+    byts = alg_bytes(G, xs, ys, mask0, cn0)
+    sec = ktimes[name0]["score_ms"] / 1e3
+    out["roofline"] = {"bound": "hbm", "achieved": byts / sec / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                       "frac": byts / sec / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                       "kernel": "k_score<1024,36864> (%s side)" % name0, "alg_bytes_per_launch": byts}
+    if dist.rank == 0 and not args.no_parity and args.sides == "both":
+        out["parity"] = parity_check(G, ex_x, ex_y, res["user"], res["business"])
+        import importlib
+
+        sys.path.insert(0, os.path.join(ROOT, "bipartite-link-prediction_amd"))
+        ev = importlib.import_module("eval")
+        out["auc"] = {"u_cn": ev.roc_auc(ex_l, res["user"]["cn"]), "u_jaccard": ev.roc_auc(ex_l, res["user"]["jaccard"]),
+                      "u_adamic": ev.roc_auc(ex_l, res["user"]["adamic"]),
+                      "b_cn": ev.roc_auc(ex_l, res["business"]["cn"]),
+                      "b_jaccard": ev.roc_auc(ex_l, res["business"]["jaccard"])}
+    if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline and args.sides == "both":
+        out["cpu_baseline"] = cpu_baseline(G, ex_x, ex_y, args.cpu_seconds)
+    if dist.rank == 0:
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

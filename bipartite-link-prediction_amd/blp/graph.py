@@ -165,6 +165,39 @@ class DeviceGraph(HostGraph):
     def batch(self, x, y):
         return PairBatch(self, x, y)
 
+    def hop3_sample(self, src, pos_off=None, pos_y=None, rate=0.01, seed=0):
+        """Exact-distance-3 candidates of each source, sampled (dataset_maker.py:137-144).
+
+        src: dense source ids; pos_off/pos_y: CSR of each source's held-out positives
+        (dense ids). Returns (x, y, label) arrays, grouped by source in `src` order;
+        within a source: positives first, then kept negatives by ascending dense id."""
+        src = _lib.as_i32(src)
+        ns = len(src)
+        if pos_off is None:
+            pos_off = np.zeros(ns + 1, np.int32)
+            pos_y = np.zeros(1, np.int32)
+        pos_off = _lib.as_i32(pos_off)
+        pos_y = _lib.as_i32(pos_y if len(pos_y) else np.zeros(1, np.int32))
+        cap = max(1024, int(ns * 64))
+        while True:
+            ox = np.empty(cap, np.int32)
+            oy = np.empty(cap, np.int32)
+            ol = np.empty(cap, np.uint8)
+            n_out = ctypes.c_int64(0)
+            check(lib().blp_hop3_sample(self.handle, ptr(src), ns, ptr(pos_off), ptr(pos_y), float(rate),
+                                        int(seed) & (2**64 - 1), ptr(ox), ptr(oy), ptr(ol), cap,
+                                        ctypes.byref(n_out)))
+            if n_out.value <= cap:
+                break
+            cap = int(n_out.value)
+        n = n_out.value
+        ox, oy, ol = ox[:n], oy[:n], ol[:n]
+        # deterministic order: by source position, keeping each source's emission order
+        rank = np.empty(self.n, np.int64)
+        rank[src] = np.arange(ns)
+        order = np.argsort(rank[ox], kind="stable")
+        return ox[order], oy[order], ol[order]
+
     def stats(self, kernel):
         ms = ctypes.c_double(0)
         n = ctypes.c_int64(0)
@@ -199,6 +232,16 @@ class PairBatch:
 
     def score(self, mask=7):
         check(lib().blp_batch_score(self.graph.handle, self.handle, mask))
+
+    def stats(self, which=0):
+        """(total ms, launches) of this batch's scorer (0) or grouping (1) kernels."""
+        ms = ctypes.c_double(0)
+        n = ctypes.c_int64(0)
+        check(lib().blp_batch_stats(self.handle, which, ctypes.byref(ms), ctypes.byref(n)))
+        return ms.value, n.value
+
+    def stats_reset(self):
+        check(lib().blp_batch_stats_reset(self.handle))
 
     def fetch(self, mask=7):
         cn = np.zeros(self.n, np.uint32)

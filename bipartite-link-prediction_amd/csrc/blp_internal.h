@@ -69,5 +69,9 @@ namespace blp {
 int timer_begin(blp_graph* g, int k, hipEvent_t* start);
 int timer_end(blp_graph* g, int k, hipEvent_t start);
 int timers_collect(blp_graph* g);
+int timer_begin(KernelTimer& t, hipStream_t s, hipEvent_t* start);
+int timer_end(KernelTimer& t, hipStream_t s, hipEvent_t start);
+int timer_collect(KernelTimer& t);
+void timer_release(KernelTimer& t);
 int set_device(const blp_graph* g);
 }  // namespace blp

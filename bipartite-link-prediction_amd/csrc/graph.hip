@@ -52,8 +52,7 @@ int set_device(const blp_graph* g) {
   return BLP_OK;
 }
 
-int timer_begin(blp_graph* g, int k, hipEvent_t* start) {
-  KernelTimer& t = g->timers[k];
+int timer_begin(KernelTimer& t, hipStream_t s, hipEvent_t* start) {
   if (t.free_events.empty()) {
     hipEvent_t e;
     BLP_HIP(hipEventCreate(&e));
@@ -61,12 +60,11 @@ int timer_begin(blp_graph* g, int k, hipEvent_t* start) {
   }
   *start = t.free_events.back();
   t.free_events.pop_back();
-  BLP_HIP(hipEventRecord(*start, g->stream));
+  BLP_HIP(hipEventRecord(*start, s));
   return BLP_OK;
 }
 
-int timer_end(blp_graph* g, int k, hipEvent_t start) {
-  KernelTimer& t = g->timers[k];
+int timer_end(KernelTimer& t, hipStream_t s, hipEvent_t start) {
   hipEvent_t stop;
   if (t.free_events.empty()) {
     BLP_HIP(hipEventCreate(&stop));
@@ -74,28 +72,46 @@ int timer_end(blp_graph* g, int k, hipEvent_t start) {
     stop = t.free_events.back();
     t.free_events.pop_back();
   }
-  BLP_HIP(hipEventRecord(stop, g->stream));
+  BLP_HIP(hipEventRecord(stop, s));
   t.pending_start.push_back(start);
   t.pending_stop.push_back(stop);
   t.launches++;
   // keep the pending list bounded: fold finished pairs in as we go
-  if (t.pending_stop.size() > 4096) return timers_collect(g);
+  if (t.pending_stop.size() > 4096) return timer_collect(t);
   return BLP_OK;
 }
 
+int timer_collect(KernelTimer& t) {
+  for (size_t i = 0; i < t.pending_stop.size(); ++i) {
+    BLP_HIP(hipEventSynchronize(t.pending_stop[i]));
+    float ms = 0.f;
+    BLP_HIP(hipEventElapsedTime(&ms, t.pending_start[i], t.pending_stop[i]));
+    t.total_ms += ms;
+    t.free_events.push_back(t.pending_start[i]);
+    t.free_events.push_back(t.pending_stop[i]);
+  }
+  t.pending_start.clear();
+  t.pending_stop.clear();
+  return BLP_OK;
+}
+
+void timer_release(KernelTimer& t) {
+  for (auto e : t.pending_start) (void)hipEventDestroy(e);
+  for (auto e : t.pending_stop) (void)hipEventDestroy(e);
+  for (auto e : t.free_events) (void)hipEventDestroy(e);
+  t.pending_start.clear();
+  t.pending_stop.clear();
+  t.free_events.clear();
+}
+
+int timer_begin(blp_graph* g, int k, hipEvent_t* start) { return timer_begin(g->timers[k], g->stream, start); }
+
+int timer_end(blp_graph* g, int k, hipEvent_t start) { return timer_end(g->timers[k], g->stream, start); }
+
 int timers_collect(blp_graph* g) {
   for (int k = 0; k < K_COUNT; ++k) {
-    KernelTimer& t = g->timers[k];
-    for (size_t i = 0; i < t.pending_stop.size(); ++i) {
-      BLP_HIP(hipEventSynchronize(t.pending_stop[i]));
-      float ms = 0.f;
-      BLP_HIP(hipEventElapsedTime(&ms, t.pending_start[i], t.pending_stop[i]));
-      t.total_ms += ms;
-      t.free_events.push_back(t.pending_start[i]);
-      t.free_events.push_back(t.pending_stop[i]);
-    }
-    t.pending_start.clear();
-    t.pending_stop.clear();
+    int rc = timer_collect(g->timers[k]);
+    if (rc) return rc;
   }
   return BLP_OK;
 }
@@ -211,11 +227,7 @@ int blp_graph_destroy(blp_graph* g) {
   if (!g) return BLP_OK;
   (void)hipSetDevice(g->device);
   if (g->stream) (void)hipStreamSynchronize(g->stream);
-  for (auto& t : g->timers) {
-    for (auto e : t.pending_start) (void)hipEventDestroy(e);
-    for (auto e : t.pending_stop) (void)hipEventDestroy(e);
-    for (auto e : t.free_events) (void)hipEventDestroy(e);
-  }
+  for (auto& t : g->timers) timer_release(t);
   g->cnt.release();
   g->off.release();
   g->cursor.release();

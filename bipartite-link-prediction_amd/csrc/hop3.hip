@@ -1,0 +1,290 @@
+// Hop-3 candidate generation (dataset_maker.make_examples, dataset_maker.py:137-144).
+//
+// For each sampled source u:  H3(u) = GetNodesAtHop(G, u, 3) (nodes at EXACT distance 3,
+// :139). A candidate b is labelled 1 if (u, b) is a held-out new edge (:141-142), else kept
+// as a negative with probability `rate` (:143-144). The reference draws Python's
+// random.random() in SNAP's BFS order; here the draw is a counter-based hash of
+// (seed, u, b), so the kept set is reproducible and order-independent (the sample itself is
+// statistical parity only; the candidate SET is exact -- tested with rate = 1).
+//
+// One workgroup per source (dequeued), two LDS bitmaps: H2(u) over [lo2, hi2) and the
+// distance-3 marks over [lo3, hi3). Positives are emitted first (in the caller's order),
+// then the sampled negatives in ascending dense id.
+#include <algorithm>
+
+#include "blp_internal.h"
+
+namespace {
+
+constexpr int H_BLOCK = 1024;
+constexpr int H_WORDS = 39936;  // 156 KiB of LDS shared by the two bitmaps
+
+struct Hop3Args {
+  const int64_t* rp;
+  const int32_t* ci;
+  const int32_t* src;      // sources (dense ids)
+  const int32_t* pos_off;  // [n_src+1] positives per source
+  const int32_t* pos_y;    // positive targets
+  int n_src;
+  int64_t lo2, hi2, lo3, hi3;
+  int w2;  // words of the H2 bitmap (the H3 bitmap follows)
+  double rate;
+  uint64_t seed;
+  int32_t* out_x;
+  int32_t* out_y;
+  uint8_t* out_label;
+  int64_t cap;
+  unsigned long long* counters;  // [0] queue, [1] emitted
+};
+
+__device__ inline uint64_t mix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__device__ inline bool keep_negative(uint64_t seed, int u, int b, double rate) {
+  const uint64_t h = mix64(seed ^ mix64(((uint64_t)(uint32_t)u << 32) | (uint32_t)b));
+  return (double)(h >> 11) * 0x1.0p-53 < rate;
+}
+
+__device__ inline bool bit_test(const uint32_t* bm, int64_t r) { return (bm[r >> 5] >> (r & 31)) & 1u; }
+
+__global__ __launch_bounds__(H_BLOCK) void k_hop3(Hop3Args a) {
+  __shared__ uint32_t lds[H_WORDS];
+  __shared__ int s_item;
+  __shared__ unsigned s_warp[H_BLOCK / 64];
+  __shared__ unsigned long long s_base;
+  uint32_t* bm2 = lds;
+  uint32_t* bm3 = lds + a.w2;
+  const int64_t span2 = a.hi2 - a.lo2, span3 = a.hi3 - a.lo3;
+  const int w3 = (int)((span3 + 31) >> 5);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (;;) {
+    if (threadIdx.x == 0) s_item = (int)atomicAdd(&a.counters[0], 1ull);
+    __syncthreads();
+    const int it = s_item;
+    if (it >= a.n_src) break;
+    const int x = a.src[it];
+    for (int i = threadIdx.x; i < a.w2 + w3; i += H_BLOCK) lds[i] = 0;
+    __syncthreads();
+    const int64_t xb = a.rp[x], xe = a.rp[x + 1];
+    // H2 marks: N(N(x)); one wave per z, lanes stride the row
+    for (int64_t k = xb + wid; k < xe; k += H_BLOCK / 64) {
+      const int z = a.ci[k];
+      for (int64_t e = a.rp[z] + lane; e < a.rp[z + 1]; e += 64) {
+        const int64_t r = (int64_t)a.ci[e] - a.lo2;
+        if (r >= 0 && r < span2) atomicOr(&bm2[r >> 5], 1u << (r & 31));
+      }
+    }
+    __syncthreads();
+    for (int64_t k = xb + threadIdx.x; k <= xe; k += H_BLOCK) {
+      const int64_t r = (k == xe ? (int64_t)x : (int64_t)a.ci[k]) - a.lo2;
+      if (r >= 0 && r < span2) atomicAnd(&bm2[r >> 5], ~(1u << (r & 31)));
+    }
+    __syncthreads();
+    // distance-3 marks: N(H2(x)); each thread walks the set bits of its H2 words
+    for (int wi = threadIdx.x; wi < a.w2; wi += H_BLOCK) {
+      uint32_t bits = bm2[wi];
+      while (bits) {
+        const int t = __ffs(bits) - 1;
+        bits &= bits - 1;
+        const int w = (int)(a.lo2 + (int64_t)wi * 32 + t);
+        for (int64_t e = a.rp[w]; e < a.rp[w + 1]; ++e) {
+          const int64_t r = (int64_t)a.ci[e] - a.lo3;
+          if (r >= 0 && r < span3) atomicOr(&bm3[r >> 5], 1u << (r & 31));
+        }
+      }
+    }
+    __syncthreads();
+    // exact distance: drop x, N(x) and H2(x) from the distance-3 marks
+    for (int64_t k = xb + threadIdx.x; k <= xe; k += H_BLOCK) {
+      const int64_t r = (k == xe ? (int64_t)x : (int64_t)a.ci[k]) - a.lo3;
+      if (r >= 0 && r < span3) atomicAnd(&bm3[r >> 5], ~(1u << (r & 31)));
+    }
+    // H2 ∩ [lo3, hi3) (general graphs only: the ranges are disjoint for bipartite files)
+    {
+      const int64_t olo = max(a.lo2, a.lo3), ohi = min(a.hi2, a.hi3);
+      for (int64_t v = olo + threadIdx.x; v < ohi; v += H_BLOCK)
+        if (bit_test(bm2, v - a.lo2)) atomicAnd(&bm3[(v - a.lo3) >> 5], ~(1u << ((v - a.lo3) & 31)));
+    }
+    __syncthreads();
+    // positives first (caller order), cleared from the candidate marks
+    const int pb = a.pos_off[it], pe = a.pos_off[it + 1];
+    if (threadIdx.x == 0) {
+      for (int k = pb; k < pe; ++k) {
+        const int64_t r = (int64_t)a.pos_y[k] - a.lo3;
+        if (r >= 0 && r < span3 && bit_test(bm3, r)) {
+          bm3[r >> 5] &= ~(1u << (r & 31));
+          const unsigned long long o = atomicAdd(&a.counters[1], 1ull);
+          if ((int64_t)o < a.cap) {
+            a.out_x[o] = x;
+            a.out_y[o] = a.pos_y[k];
+            a.out_label[o] = 1;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    // sampled negatives: per-thread contiguous word ranges keep ascending id order
+    const int per = (w3 + H_BLOCK - 1) / H_BLOCK;
+    const int w_beg = min(w3, (int)threadIdx.x * per), w_end = min(w3, w_beg + per);
+    unsigned mine = 0;
+    for (int wi = w_beg; wi < w_end; ++wi) {
+      uint32_t bits = bm3[wi];
+      while (bits) {
+        const int t = __ffs(bits) - 1;
+        bits &= bits - 1;
+        if (keep_negative(a.seed, x, (int)(a.lo3 + (int64_t)wi * 32 + t), a.rate)) ++mine;
+      }
+    }
+    // block exclusive scan of the per-thread counts
+    unsigned inc = mine;
+    for (int d = 1; d < 64; d <<= 1) {
+      const unsigned t = __shfl_up(inc, d, 64);
+      if (lane >= d) inc += t;
+    }
+    if (lane == 63) s_warp[wid] = inc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned run = 0;
+      for (int w = 0; w < H_BLOCK / 64; ++w) {
+        const unsigned t = s_warp[w];
+        s_warp[w] = run;
+        run += t;
+      }
+      s_base = atomicAdd(&a.counters[1], (unsigned long long)run);
+    }
+    __syncthreads();
+    unsigned long long o = s_base + s_warp[wid] + inc - mine;
+    for (int wi = w_beg; wi < w_end; ++wi) {
+      uint32_t bits = bm3[wi];
+      while (bits) {
+        const int t = __ffs(bits) - 1;
+        bits &= bits - 1;
+        const int b = (int)(a.lo3 + (int64_t)wi * 32 + t);
+        if (keep_negative(a.seed, x, b, a.rate)) {
+          if ((int64_t)o < a.cap) {
+            a.out_x[o] = x;
+            a.out_y[o] = b;
+            a.out_label[o] = 0;
+          }
+          ++o;
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace
+
+using namespace blp;
+
+extern "C" int blp_hop3_sample(blp_graph* g, const int32_t* src, int64_t n_src, const int32_t* pos_off,
+                               const int32_t* pos_y, double rate, uint64_t seed, int32_t* out_x, int32_t* out_y,
+                               uint8_t* out_label, int64_t cap, int64_t* n_out) {
+  BLP_CHECK(g && n_out && n_src >= 0 && (n_src == 0 || (src && pos_off)), BLP_E_ARG, "blp_hop3_sample: bad arguments");
+  BLP_CHECK(n_src < (int64_t(1) << 31), BLP_E_ARG, "blp_hop3_sample: too many sources");
+  BLP_CHECK(cap == 0 || (out_x && out_y && out_label), BLP_E_ARG, "blp_hop3_sample: null outputs");
+  const int64_t* rp = g->h_rp.data();
+  const int32_t* ci = g->h_ci.data();
+  const int64_t n = g->n;
+  // plan the two universes: H2 ⊂ N(N(x)), distance-3 marks ⊂ N(H2) ⊂ the rows' neighbour ranges
+  int64_t lo2 = INT64_MAX, hi2 = INT64_MIN;
+  for (int64_t i = 0; i < n_src; ++i) {
+    const int32_t x = src[i];
+    if (x < 0 || x >= n) return fail(BLP_E_ARG, "blp_hop3_sample: source id out of range");
+    for (int64_t k = rp[x]; k < rp[x + 1]; ++k) {
+      const int32_t z = ci[k];
+      if (rp[z + 1] > rp[z]) {
+        lo2 = std::min<int64_t>(lo2, ci[rp[z]]);
+        hi2 = std::max<int64_t>(hi2, (int64_t)ci[rp[z + 1] - 1] + 1);
+      }
+    }
+  }
+  if (lo2 > hi2) lo2 = hi2 = 0;
+  int64_t lo3 = INT64_MAX, hi3 = INT64_MIN;
+  for (int64_t v = lo2; v < hi2; ++v)
+    if (rp[v + 1] > rp[v]) {
+      lo3 = std::min<int64_t>(lo3, ci[rp[v]]);
+      hi3 = std::max<int64_t>(hi3, (int64_t)ci[rp[v + 1] - 1] + 1);
+    }
+  if (lo3 > hi3) lo3 = hi3 = 0;
+  const int64_t w2 = (((hi2 - lo2) + 31) / 32 + 3) / 4 * 4, w3 = ((hi3 - lo3) + 31) / 32;
+  if (w2 + w3 > H_WORDS)
+    return fail(BLP_E_UNSUP, "blp_hop3_sample: 2-hop + 3-hop universes exceed one workgroup's LDS (" +
+                                 std::to_string(hi2 - lo2) + " + " + std::to_string(hi3 - lo3) + " nodes)");
+  for (int64_t i = 0; i < (n_src ? pos_off[n_src] : 0); ++i)
+    BLP_CHECK(pos_y[i] >= 0 && pos_y[i] < n, BLP_E_ARG, "blp_hop3_sample: positive id out of range");
+  int rc = set_device(g);
+  if (rc) return rc;
+  Hop3Args a{};
+  void *d_src = nullptr, *d_off = nullptr, *d_pos = nullptr, *d_cnt = nullptr, *d_x = nullptr, *d_y = nullptr,
+       *d_l = nullptr;
+  const int64_t npos = n_src ? pos_off[n_src] : 0;
+  auto cleanup = [&]() {
+    for (void* p : {d_src, d_off, d_pos, d_cnt, d_x, d_y, d_l})
+      if (p) (void)hipFree(p);
+  };
+  auto hip = [&](hipError_t e, const char* what) {
+    if (e != hipSuccess) {
+      cleanup();
+      return hip_fail(e, what, __FILE__, __LINE__);
+    }
+    return 0;
+  };
+  if ((rc = hip(hipMalloc(&d_src, 4 * std::max<int64_t>(n_src, 1)), "hipMalloc"))) return rc;
+  if ((rc = hip(hipMalloc(&d_off, 4 * (n_src + 1)), "hipMalloc"))) return rc;
+  if ((rc = hip(hipMalloc(&d_pos, 4 * std::max<int64_t>(npos, 1)), "hipMalloc"))) return rc;
+  if ((rc = hip(hipMalloc(&d_cnt, 16), "hipMalloc"))) return rc;
+  const int64_t dcap = std::max<int64_t>(cap, 1);
+  if ((rc = hip(hipMalloc(&d_x, 4 * dcap), "hipMalloc"))) return rc;
+  if ((rc = hip(hipMalloc(&d_y, 4 * dcap), "hipMalloc"))) return rc;
+  if ((rc = hip(hipMalloc(&d_l, dcap), "hipMalloc"))) return rc;
+  if (n_src) {
+    if ((rc = hip(hipMemcpy(d_src, src, 4 * n_src, hipMemcpyHostToDevice), "hipMemcpy"))) return rc;
+    if ((rc = hip(hipMemcpy(d_off, pos_off, 4 * (n_src + 1), hipMemcpyHostToDevice), "hipMemcpy"))) return rc;
+  }
+  if (npos && (rc = hip(hipMemcpy(d_pos, pos_y, 4 * npos, hipMemcpyHostToDevice), "hipMemcpy"))) return rc;
+  if ((rc = hip(hipMemsetAsync(d_cnt, 0, 16, g->stream), "hipMemsetAsync"))) return rc;
+  a.rp = g->d_rp;
+  a.ci = g->d_ci;
+  a.src = (const int32_t*)d_src;
+  a.pos_off = (const int32_t*)d_off;
+  a.pos_y = (const int32_t*)d_pos;
+  a.n_src = (int)n_src;
+  a.lo2 = lo2;
+  a.hi2 = hi2;
+  a.lo3 = lo3;
+  a.hi3 = hi3;
+  a.w2 = (int)w2;
+  a.rate = rate;
+  a.seed = seed;
+  a.out_x = (int32_t*)d_x;
+  a.out_y = (int32_t*)d_y;
+  a.out_label = (uint8_t*)d_l;
+  a.cap = cap;
+  a.counters = (unsigned long long*)d_cnt;
+  hipEvent_t t0;
+  if ((rc = timer_begin(g, K_HOP3, &t0))) return cleanup(), rc;
+  if (n_src) {
+    hipLaunchKernelGGL(k_hop3, dim3(g->n_cu), dim3(H_BLOCK), 0, g->stream, a);
+    if ((rc = hip(hipGetLastError(), "k_hop3 launch"))) return rc;
+  }
+  if ((rc = timer_end(g, K_HOP3, t0))) return cleanup(), rc;
+  if ((rc = hip(hipStreamSynchronize(g->stream), "hipStreamSynchronize"))) return rc;
+  unsigned long long cnt[2];
+  if ((rc = hip(hipMemcpy(cnt, d_cnt, 16, hipMemcpyDeviceToHost), "hipMemcpy"))) return rc;
+  const int64_t got = (int64_t)cnt[1];
+  const int64_t ncopy = std::min(got, cap);
+  if (ncopy > 0) {
+    if ((rc = hip(hipMemcpy(out_x, d_x, 4 * ncopy, hipMemcpyDeviceToHost), "hipMemcpy"))) return rc;
+    if ((rc = hip(hipMemcpy(out_y, d_y, 4 * ncopy, hipMemcpyDeviceToHost), "hipMemcpy"))) return rc;
+    if ((rc = hip(hipMemcpy(out_label, d_l, ncopy, hipMemcpyDeviceToHost), "hipMemcpy"))) return rc;
+  }
+  cleanup();
+  *n_out = got;
+  return BLP_OK;
+}

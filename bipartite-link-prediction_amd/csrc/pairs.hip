@@ -416,6 +416,7 @@ struct blp_batch {
   int group = 64;
   int chunks = 1;
   int64_t n_sources = 0;
+  blp::KernelTimer t_score, t_group;
 };
 
 using namespace blp;
@@ -515,6 +516,9 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
 int blp_batch_destroy(blp_batch* b) {
   if (!b) return BLP_OK;
   if (b->g) (void)hipSetDevice(b->g->device);
+  if (b->g && b->g->stream) (void)hipStreamSynchronize(b->g->stream);
+  timer_release(b->t_score);
+  timer_release(b->t_group);
   void* ps[] = {b->d_x, b->d_y, b->d_cn, b->d_jac, b->d_aa, b->d_perm, b->d_misc};
   for (void* p : ps)
     if (p) (void)hipFree(p);
@@ -546,8 +550,9 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   if ((rc = g->cursor.reserve(4 * (n + 1)))) return rc;
   if ((rc = g->active.reserve(4 * (n + 1)))) return rc;
   if ((rc = g->scratch.reserve(sizeof(int2) * (ntiles + 1)))) return rc;
-  hipEvent_t t0;
+  hipEvent_t t0, bt0;
   if ((rc = timer_begin(g, K_GROUP, &t0))) return rc;
+  if ((rc = timer_begin(b->t_group, g->stream, &bt0))) return rc;
   BLP_HIP(hipMemsetAsync(g->cnt.p, 0, 4 * (n + 1), g->stream));
   BLP_HIP(hipMemsetAsync(b->d_misc, 0, sizeof(Misc), g->stream));
   const int ew_grid = (int)std::min<int64_t>(std::max<int64_t>((np + 255) / 256, 1), (int64_t)g->n_cu * 16);
@@ -562,6 +567,7 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   }
   if (np) hipLaunchKernelGGL(k_scatter, dim3(ew_grid), dim3(256), 0, g->stream, b->d_x, np, g->cursor.as<int32_t>(), b->d_perm);
   BLP_HIP(hipGetLastError());
+  if ((rc = timer_end(b->t_group, g->stream, bt0))) return rc;
   if ((rc = timer_end(g, K_GROUP, t0))) return rc;
 
   ScoreArgs a;
@@ -592,8 +598,9 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
     int64_t v = atoll(e);
     if (v >= 1) a.long_row = v;
   }
-  hipEvent_t t1;
+  hipEvent_t t1, bt1;
   if ((rc = timer_begin(g, K_SCORE, &t1))) return rc;
+  if ((rc = timer_begin(b->t_score, g->stream, &bt1))) return rc;
   if (np) {
     if (b->variant == V_SMALL)
       rc = launch_score<BLOCK_SMALL, CAP_SMALL>(g, a);
@@ -603,7 +610,31 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
       rc = launch_score<BLOCK_LARGE, CAP_LARGE>(g, a);
     if (rc) return rc;
   }
+  if ((rc = timer_end(b->t_score, g->stream, bt1))) return rc;
   return timer_end(g, K_SCORE, t1);
+}
+
+int blp_batch_stats(blp_batch* b, int which, double* total_ms, int64_t* launches) {
+  BLP_CHECK(b && (which == 0 || which == 1), BLP_E_ARG, "blp_batch_stats: bad arguments");
+  KernelTimer& t = which == 0 ? b->t_score : b->t_group;
+  int rc = set_device(b->g);
+  if (rc) return rc;
+  if ((rc = timer_collect(t))) return rc;
+  if (total_ms) *total_ms = t.total_ms;
+  if (launches) *launches = t.launches;
+  return BLP_OK;
+}
+
+int blp_batch_stats_reset(blp_batch* b) {
+  BLP_CHECK(b, BLP_E_ARG, "blp_batch_stats_reset: null batch");
+  int rc = set_device(b->g);
+  if (rc) return rc;
+  for (KernelTimer* t : {&b->t_score, &b->t_group}) {
+    if ((rc = timer_collect(*t))) return rc;
+    t->total_ms = 0;
+    t->launches = 0;
+  }
+  return BLP_OK;
 }
 
 int blp_batch_fetch(blp_graph* g, blp_batch* b, uint32_t* cn, double* jac, double* aa) {

@@ -110,6 +110,24 @@ int blp_batch_destroy(blp_batch* b);
 int blp_batch_plan(const blp_batch* b, int64_t* lo, int64_t* hi, int* chunks, int* block,
                    int* group);
 
+/* Per-batch device time of the last/accumulated blp_batch_score calls (HIP events on the
+ * graph stream): which 0 = scorer kernel, 1 = grouping kernels. Reset with blp_batch_stats_reset. */
+int blp_batch_stats(blp_batch* b, int which, double* total_ms, int64_t* launches);
+int blp_batch_stats_reset(blp_batch* b);
+
+/* ---------------------------------------------------------------- candidate generation
+ * Replaces dataset_maker.make_examples' candidate loop (dataset_maker.py:137-144): for each
+ * source u in src[], every node at EXACT distance 3 (GetNodesAtHop(G,u,3), :139) is a
+ * candidate; candidates listed in u's positives (pos_y[pos_off[i]:pos_off[i+1]], the held-out
+ * new edges, :141-142) are emitted with label 1, the others are kept with probability `rate`
+ * (:143-144) by a counter-based hash of (seed, u, b) and emitted with label 0.
+ * Up to `cap` (x, y, label) triples are written; *n_out receives the total produced (call
+ * again with a larger cap if *n_out > cap). Output order across sources is unspecified;
+ * within a source: positives first, then negatives by ascending dense id.                   */
+int blp_hop3_sample(blp_graph* g, const int32_t* src, int64_t n_src, const int32_t* pos_off,
+                    const int32_t* pos_y, double rate, uint64_t seed, int32_t* out_x,
+                    int32_t* out_y, uint8_t* out_label, int64_t cap, int64_t* n_out);
+
 /* ---------------------------------------------------------------- stats
  * Per-kernel device time (ms, HIP events on the handle's stream) accumulated since the
  * last reset, for bench.py's roofline figure. kernel: 0 = pair scorer, 1 = grouping
