@@ -154,7 +154,7 @@ def parity_check(G, ex_x, ex_y, ures, bres, n_users=40):
     sel = np.isin(ex_x, pick)
     cn, jac, aa, _ = og.score_pairs(ex_x[sel], ex_y[sel], 7, nthreads=8)
     ok_u = (np.array_equal(ures["cn"][sel], cn) and np.array_equal(ures["jaccard"][sel], jac)
-            and np.allclose(ures["adamic"][sel], aa, rtol=1e-12, atol=0))
+            and np.allclose(ures["adamic"][sel], aa, rtol=1e-9, atol=0))
     bcn, bjac, _, _ = og.score_pairs(ex_y[sel], ex_x[sel], 3, nthreads=8)
     ok_b = np.array_equal(bres["cn"][sel], bcn) and np.array_equal(bres["jaccard"][sel], bjac)
     return {"checked_pairs": int(sel.sum()), "users": int(len(pick)), "user_side_exact": bool(ok_u),

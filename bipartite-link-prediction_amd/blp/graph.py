@@ -225,10 +225,10 @@ class PairBatch:
 
     def plan(self):
         lo, hi = ctypes.c_int64(), ctypes.c_int64()
-        ch, blk, grp = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        ch, blk, hv = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         check(lib().blp_batch_plan(self.handle, ctypes.byref(lo), ctypes.byref(hi), ctypes.byref(ch),
-                                   ctypes.byref(blk), ctypes.byref(grp)))
-        return {"lo": lo.value, "hi": hi.value, "chunks": ch.value, "block": blk.value, "group": grp.value}
+                                   ctypes.byref(blk), ctypes.byref(hv)))
+        return {"lo": lo.value, "hi": hi.value, "chunks": ch.value, "block": blk.value, "heavy": hv.value}
 
     def score(self, mask=7):
         check(lib().blp_batch_score(self.graph.handle, self.handle, mask))

@@ -36,6 +36,10 @@ struct DevBuf {
   template <class T> T* as() const { return reinterpret_cast<T*>(p); }
 };
 
+// Adamic-Adar terms are summed in 2^-40 fixed point: exact, order-independent integer sums
+// (the reference's own order is Python set order); |term| <= 1/ln 2 < 2^1.
+constexpr double AA_SCALE = 1099511627776.0;  // 2^40
+
 enum KernelId { K_SCORE = 0, K_GROUP = 1, K_SVD_PAIRS = 2, K_SVD_TOPK = 3, K_WALK = 4, K_HOP3 = 5, K_COUNT = 6 };
 
 // Event-pair timer on the graph stream; accumulated lazily when the stats are read.
@@ -56,7 +60,7 @@ struct blp_graph {
   int64_t nnz = 0;  // stored CSR entries (both directions, no self-loops)
   int64_t* d_rp = nullptr;   // [n+1]
   int32_t* d_ci = nullptr;   // [nnz]
-  double* d_aaw = nullptr;   // [n] Adamic-Adar weight per node (or null)
+  long long* d_aaw_fx = nullptr;  // [n] Adamic-Adar weight per node, fixed point 2^-40 (or null)
   // host mirrors used only for launch planning (bitmap universe bounds)
   std::vector<int64_t> h_rp;
   std::vector<int32_t> h_ci;

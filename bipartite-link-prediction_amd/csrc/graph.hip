@@ -5,6 +5,7 @@
 // dense node ids, both directions stored, rows sorted ascending, int64 row offsets and
 // int32 column ids.
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <mutex>
 
@@ -211,8 +212,10 @@ int blp_graph_create(const int64_t* row_ptr, const int32_t* col_idx, int64_t n, 
          BLP_HIP(hipMemcpy(g->d_rp, row_ptr, sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice));
          if (nnz) BLP_HIP(hipMemcpy(g->d_ci, col_idx, sizeof(int32_t) * nnz, hipMemcpyHostToDevice));
          if (aaw) {
-           BLP_HIP(hipMalloc(&g->d_aaw, sizeof(double) * std::max<int64_t>(n, 1)));
-           if (n) BLP_HIP(hipMemcpy(g->d_aaw, aaw, sizeof(double) * n, hipMemcpyHostToDevice));
+           std::vector<long long> fx((size_t)n);
+           for (int64_t i = 0; i < n; ++i) fx[i] = llrint(aaw[i] * AA_SCALE);
+           BLP_HIP(hipMalloc(&g->d_aaw_fx, sizeof(long long) * std::max<int64_t>(n, 1)));
+           if (n) BLP_HIP(hipMemcpy(g->d_aaw_fx, fx.data(), sizeof(long long) * n, hipMemcpyHostToDevice));
          }
          return BLP_OK;
        }()) != BLP_OK)
@@ -235,7 +238,7 @@ int blp_graph_destroy(blp_graph* g) {
   g->scratch.release();
   if (g->d_rp) (void)hipFree(g->d_rp);
   if (g->d_ci) (void)hipFree(g->d_ci);
-  if (g->d_aaw) (void)hipFree(g->d_aaw);
+  if (g->d_aaw_fx) (void)hipFree(g->d_aaw_fx);
   if (g->stream) (void)hipStreamDestroy(g->stream);
   delete g;
   return BLP_OK;

@@ -6,19 +6,25 @@
 //   N(y)  = GetNodesAtHop(G, y, 1)  (similarity.py:41 / :85)
 //   cn  = |H2(x) ∩ N(y)|                                       (:113-114)
 //   jac = float(cn) / float(|H2(x)| + |N(y)| - cn)              (:108-111)
-//   aa  = Σ_{w ∈ H2(x) ∩ N(y)} aaw[w],  aaw = (log deg)^-1 | 0  (:116-126)
+//   aa  = Σ_{w ∈ H2(x) ∩ N(y)} (log deg w)^-1 [deg > 1]        (:116-126)
 //
 // One step (blp_batch_score), all on the graph's stream:
-//   1. group:  counting sort of the pairs by source x on the device (count -> scan ->
-//              scatter) + compaction of the active sources.
-//   2. score:  persistent workgroups dequeue one source at a time. The workgroup builds
-//              H2(x) as a bitmap in LDS over the batch's node universe [lo, hi) (chunked
-//              when it exceeds LDS), removes distance 0/1 (x and N(x)), popcounts |H2(x)|,
-//              then scans N(y) of every pair of x, testing bits. Lanes are split into
-//              groups of G (8..64) so short rows do not idle a whole wave.
-// The graph, the pairs and the outputs stay in HBM; the host only plans the launch.
+//   1. group   counting sort of the raw pair list by source x on the device: run-aggregated
+//              counts -> scan -> scatter. The scatter also gathers each pair's N(y) row
+//              (start, length) so the scorer never walks the pair -> y -> row_ptr chain.
+//   2. heavy   (planned sources only) sources whose H2 build is far above the per-workgroup
+//              average are pre-built by several workgroups into HBM bitmaps.
+//   3. score   persistent workgroups dequeue sources. Per source: H2(x) as a bitmap in LDS over
+//              the batch's node universe [lo, hi) (chunked when larger than LDS), built from
+//              the rows of N(x); distance 0/1 removed; |H2| popcounted; then every pair's N(y)
+//              is scanned against the bitmap. Both the build and the scan run as merge-path
+//              segment loops: the rows of a chunk are concatenated, every thread takes K
+//              consecutive elements (K independent loads in flight), one LDS binary search per
+//              K elements maps an element to its row. Short and very long rows cost the same.
+// Adamic-Adar terms are summed in 2^-40 fixed point (exact integer adds in any order).
 #include <algorithm>
 #include <cmath>
+#include <numeric>
 
 #include "blp_internal.h"
 
@@ -27,6 +33,8 @@ namespace {
 constexpr int SCAN_BLOCK = 256;
 constexpr int SCAN_ITEMS = 16;
 constexpr int SCAN_TILE = SCAN_BLOCK * SCAN_ITEMS;
+constexpr int RUN_CHUNK = 16;  // pairs per thread in the run-aggregated count / scatter
+constexpr int KPT = 8;         // merge-path elements per thread per step
 
 struct Misc {
   int n_active;
@@ -36,9 +44,25 @@ struct Misc {
 };
 
 // ------------------------------------------------------------------ grouping kernels
+// Counts per source. Each thread owns RUN_CHUNK consecutive pairs and issues one atomic per
+// run of equal x (device-scope atomics execute at the memory side on a multi-XCD part).
 __global__ void k_count(const int32_t* __restrict__ x, int64_t n_pairs, int32_t* __restrict__ cnt) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n_pairs; i += (int64_t)gridDim.x * blockDim.x)
-    atomicAdd(&cnt[x[i]], 1);
+  const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c * RUN_CHUNK < n_pairs; c += nthr) {
+    const int64_t b = c * RUN_CHUNK, e = min(n_pairs, b + RUN_CHUNK);
+    int cur = x[b], run = 1;
+    for (int64_t i = b + 1; i < e; ++i) {
+      const int xi = x[i];
+      if (xi == cur) {
+        ++run;
+      } else {
+        atomicAdd(&cnt[cur], run);
+        cur = xi;
+        run = 1;
+      }
+    }
+    atomicAdd(&cnt[cur], run);
+  }
 }
 
 // block-wide exclusive scan of (count, flag) pairs; returns the block total in *tot
@@ -141,11 +165,223 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan_apply(const int32_t* __rest
   }
 }
 
-__global__ void k_scatter(const int32_t* __restrict__ x, int64_t n_pairs, int32_t* __restrict__ cursor,
-                          int32_t* __restrict__ perm) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n_pairs; i += (int64_t)gridDim.x * blockDim.x) {
-    int pos = atomicAdd(&cursor[x[i]], 1);
-    perm[pos] = (int32_t)i;
+// Scatter into source order; one atomic per run of equal x. Also gathers N(y)'s row.
+__global__ void k_scatter(const int32_t* __restrict__ x, const int32_t* __restrict__ y, int64_t n_pairs,
+                          const int64_t* __restrict__ rp, int32_t* __restrict__ cursor, int32_t* __restrict__ g_out,
+                          int64_t* __restrict__ g_yb, int32_t* __restrict__ g_yl) {
+  const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c * RUN_CHUNK < n_pairs; c += nthr) {
+    const int64_t b = c * RUN_CHUNK, e = min(n_pairs, b + RUN_CHUNK);
+    int64_t i = b;
+    while (i < e) {
+      const int cur = x[i];
+      int64_t j = i + 1;
+      while (j < e && x[j] == cur) ++j;
+      int pos = atomicAdd(&cursor[cur], (int)(j - i));
+      for (int64_t k = i; k < j; ++k, ++pos) {
+        const int yk = y[k];
+        const int64_t s = rp[yk];
+        g_out[pos] = (int32_t)k;
+        g_yb[pos] = s;
+        g_yl[pos] = (int32_t)(rp[yk + 1] - s);
+      }
+      i = j;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ segment machinery
+// Exclusive scan of one int per thread over the block (values of threads >= n are 0).
+template <int BLOCK>
+__device__ inline int block_exscan(int v, int* red, int* total) {
+  constexpr int NW = BLOCK / 64;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int inc = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int t = __shfl_up(inc, d, 64);
+    if (lane >= d) inc += t;
+  }
+  if (lane == 63) red[wid] = inc;
+  __syncthreads();
+  int base = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    const int t = red[w];
+    base += w < wid ? t : 0;
+    tot += t;
+  }
+  __syncthreads();
+  *total = tot;
+  return base + inc - v;
+}
+
+// last s in [0, ns) with off[s] <= f (requires off[0] <= f < off[ns])
+__device__ inline int seg_search(const int32_t* off, int ns, int f) {
+  int lo = 0, hi = ns;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (off[mid] <= f)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  return lo;
+}
+
+// Set the bits of every element of the ns segments (rows of ci) inside [c0, c0 + width).
+template <int BLOCK>
+__device__ inline void mp_build(const int32_t* __restrict__ ci, const int64_t* s_start, const int32_t* s_off, int ns,
+                                int64_t c0, int64_t width, uint32_t* bm) {
+  const int T = s_off[ns];
+  for (int base = 0; base < T; base += BLOCK * KPT) {
+    const int f0 = base + (int)threadIdx.x * KPT;
+    if (f0 >= T) continue;
+    int s = seg_search(s_off, ns, f0);
+    int next = s_off[s + 1];
+    int64_t pos = s_start[s] + (f0 - s_off[s]);
+    int w[KPT];
+#pragma unroll
+    for (int k = 0; k < KPT; ++k) {
+      const int f = f0 + k;
+      w[k] = -1;
+      if (f < T) {
+        while (f >= next) {
+          ++s;
+          next = s_off[s + 1];
+          pos = s_start[s];
+        }
+        w[k] = ci[pos++];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < KPT; ++k) {
+      const int64_t r = (int64_t)w[k] - c0;
+      if (w[k] >= 0 && r >= 0 && r < width) atomicOr(&bm[r >> 5], 1u << (r & 31));
+    }
+  }
+}
+
+// Test every element of the ns segments against the bitmap; per-segment hit counts and
+// fixed-point Adamic-Adar sums accumulate into s_cn / s_aa (LDS).
+template <int BLOCK, bool AA>
+__device__ inline void mp_scan(const int32_t* __restrict__ ci, const long long* __restrict__ aaw, const int64_t* s_start,
+                               const int32_t* s_off, int ns, int64_t c0, int64_t width, const uint32_t* bm,
+                               uint32_t* s_cn, unsigned long long* s_aa) {
+  const int T = s_off[ns];
+  for (int base = 0; base < T; base += BLOCK * KPT) {
+    const int f0 = base + (int)threadIdx.x * KPT;
+    if (f0 >= T) continue;
+    int s = seg_search(s_off, ns, f0);
+    int next = s_off[s + 1];
+    int64_t pos = s_start[s] + (f0 - s_off[s]);
+    int w[KPT], sk[KPT];
+#pragma unroll
+    for (int k = 0; k < KPT; ++k) {
+      const int f = f0 + k;
+      w[k] = -1;
+      sk[k] = -1;
+      if (f < T) {
+        while (f >= next) {
+          ++s;
+          next = s_off[s + 1];
+          pos = s_start[s];
+        }
+        w[k] = ci[pos++];
+        sk[k] = s;
+      }
+    }
+    bool hit[KPT];
+#pragma unroll
+    for (int k = 0; k < KPT; ++k) {
+      const int64_t r = (int64_t)w[k] - c0;
+      hit[k] = w[k] >= 0 && r >= 0 && r < width && ((bm[r >> 5] >> (r & 31)) & 1u);
+    }
+    long long wt[KPT];
+    if (AA) {
+#pragma unroll
+      for (int k = 0; k < KPT; ++k) wt[k] = hit[k] ? aaw[w[k]] : 0ll;
+    }
+    int cur = sk[0];
+    unsigned c = 0;
+    unsigned long long acc = 0;
+#pragma unroll
+    for (int k = 0; k < KPT; ++k) {
+      if (sk[k] != cur) {
+        if (c) {
+          atomicAdd(&s_cn[cur], c);
+          if (AA) atomicAdd(&s_aa[cur], acc);
+        }
+        cur = sk[k];
+        c = 0;
+        acc = 0;
+      }
+      if (hit[k]) {
+        ++c;
+        if (AA) acc += (unsigned long long)wt[k];
+      }
+    }
+    if (c && cur >= 0) {
+      atomicAdd(&s_cn[cur], c);
+      if (AA) atomicAdd(&s_aa[cur], acc);
+    }
+  }
+}
+
+// Load the rows of N(x)[k0, k0 + ns) as segments: start / exclusive offsets (s_off[ns] = total).
+template <int BLOCK>
+__device__ inline void load_row_segments(const int64_t* __restrict__ rp, const int32_t* __restrict__ ci, int64_t k0,
+                                         int ns, int64_t* s_start, int32_t* s_off, int* red) {
+  int len = 0;
+  if ((int)threadIdx.x < ns) {
+    const int z = ci[k0 + threadIdx.x];
+    const int64_t st = rp[z];
+    s_start[threadIdx.x] = st;
+    len = (int)(rp[z + 1] - st);
+  }
+  int tot;
+  const int ex = block_exscan<BLOCK>(len, red, &tot);
+  if ((int)threadIdx.x < ns) s_off[threadIdx.x] = ex;
+  if (threadIdx.x == 0) s_off[ns] = tot;
+  __syncthreads();
+}
+
+// ------------------------------------------------------------------ heavy-source pre-build
+struct HeavyItem {
+  int32_t slot;
+  int32_t pad;
+  int64_t kb, ke;  // rows N(x) = ci[kb, ke) handled by this item
+};
+
+struct HeavyArgs {
+  const int64_t* rp;
+  const int32_t* ci;
+  const HeavyItem* items;
+  uint32_t* heavy_bm;  // [slots][hb_words]
+  int64_t hb_words;
+  int64_t lo, width;
+};
+
+template <int BLOCK, int CAP_WORDS, int SEG>
+__global__ __launch_bounds__(BLOCK) void k_heavy(HeavyArgs h) {
+  __shared__ uint32_t bm[CAP_WORDS];
+  __shared__ int64_t s_start[SEG];
+  __shared__ int32_t s_off[SEG + 1];
+  __shared__ int red[BLOCK / 64];
+  const HeavyItem it = h.items[blockIdx.x];
+  const int nw = (int)((h.width + 31) >> 5);
+  for (int i = threadIdx.x; i < nw; i += BLOCK) bm[i] = 0;
+  __syncthreads();
+  for (int64_t k0 = it.kb; k0 < it.ke; k0 += SEG) {
+    const int ns = (int)min<int64_t>(SEG, it.ke - k0);
+    load_row_segments<BLOCK>(h.rp, h.ci, k0, ns, s_start, s_off, red);
+    mp_build<BLOCK>(h.ci, s_start, s_off, ns, h.lo, h.width, bm);
+    __syncthreads();
+  }
+  uint32_t* dst = h.heavy_bm + (int64_t)it.slot * h.hb_words;
+  for (int i = threadIdx.x; i < nw; i += BLOCK) {
+    const uint32_t v = bm[i];
+    if (v) atomicOr(&dst[i], v);
   }
 }
 
@@ -153,28 +389,25 @@ __global__ void k_scatter(const int32_t* __restrict__ x, int64_t n_pairs, int32_
 struct ScoreArgs {
   const int64_t* rp;
   const int32_t* ci;
-  const double* aaw;
-  const int32_t* y;       // pair targets, caller order
-  const int32_t* perm;    // grouped position -> caller index
-  const int32_t* off;     // per node: first grouped position of its pairs
-  const int32_t* cnt;     // per node: number of pairs with that source
-  const int32_t* active;  // active sources
+  const long long* aaw;    // fixed-point Adamic-Adar weights
+  const int32_t* off;      // per node: first grouped position of its pairs
+  const int32_t* cnt;      // per node: number of pairs with that source
+  const int32_t* active;   // active sources
+  const int32_t* g_out;    // grouped position -> caller index
+  const int64_t* g_yb;     // grouped position -> start of N(y) in ci
+  const int32_t* g_yl;     // grouped position -> |N(y)|
+  const int32_t* heavy_slot;  // per node: pre-built bitmap slot or -1 (null: none)
+  const uint32_t* heavy_bm;
+  int64_t hb_words;
   Misc* misc;
   uint32_t* cn;
   double* jac;
   double* aa;
-  int64_t lo, hi;  // bitmap universe
-  uint32_t mask;
-  int group;         // lanes per pair group
+  int64_t lo, hi;    // bitmap universe
   int64_t cap_bits;  // bitmap bits per chunk (<= template capacity; lowered only by tests)
-  int64_t long_row;  // rows longer than this go to the block-cooperative loops
+  uint32_t mask;
+  int dq;            // sources per dequeue
 };
-
-template <typename T>
-__device__ inline T group_sum(T v, int G) {
-  for (int o = G >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
 
 template <int BLOCK>
 __device__ inline unsigned long long block_sum_u64(unsigned long long v, unsigned long long* red) {
@@ -190,214 +423,138 @@ __device__ inline unsigned long long block_sum_u64(unsigned long long v, unsigne
   return t;
 }
 
-// Rows longer than LONG_ROW(BLOCK) entries are deferred from the lane-group loops to a
-// block-cooperative loop, so one very popular node (d up to ~2e5 at config 2) cannot
-// leave one wave working while the rest of the workgroup waits at the next barrier.
-constexpr int LONG_LIST = 256;
-
-template <int BLOCK, int CAP_WORDS>
+template <int BLOCK, int CAP_WORDS, int SEG>
 __global__ __launch_bounds__(BLOCK) void k_score(ScoreArgs a) {
   constexpr int NW = BLOCK / 64;
-  const int64_t CAP_BITS = a.cap_bits;
-  const int64_t LONG_ROW = a.long_row;
   __shared__ uint32_t bm[CAP_WORDS];
-  __shared__ unsigned long long red[NW];
-  __shared__ double redd[NW];
+  __shared__ int64_t s_start[SEG];
+  __shared__ int32_t s_off[SEG + 1];
+  __shared__ uint32_t s_cn[SEG];
+  __shared__ unsigned long long s_aa[SEG];
+  __shared__ unsigned long long red64[NW];
+  __shared__ int red[NW];
   __shared__ int s_src;
-  __shared__ int s_nlong;
-  __shared__ int s_long[LONG_LIST];
 
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int G = a.group;
-  const int gpw = 64 / G;
-  const int gid = lane / G, gl = lane - gid * G;
-  const int n_groups = NW * gpw;
-  const int my_group = wid * gpw + gid;
+  const int64_t CAP_BITS = a.cap_bits;
   const int64_t span = a.hi - a.lo;
   const int nchunks = span <= CAP_BITS ? 1 : (int)((span + CAP_BITS - 1) / CAP_BITS);
   const bool want_j = (a.mask & BLP_JACCARD) != 0;
   const bool want_a = (a.mask & BLP_ADAMIC) != 0;
   uint4* bm4 = reinterpret_cast<uint4*>(bm);
+  const int n_active = a.misc->n_active;
 
   for (;;) {
-    if (threadIdx.x == 0) {
-      s_src = atomicAdd(&a.misc->queue, 1);
-      s_nlong = 0;
-    }
+    if (threadIdx.x == 0) s_src = atomicAdd(&a.misc->queue, a.dq);
     __syncthreads();
-    const int s = s_src;
-    if (s >= a.misc->n_active) break;
-    const int x = a.active[s];
-    const int pbeg = a.off[x], pcnt = a.cnt[x];
-    const int64_t xb = a.rp[x], xe = a.rp[x + 1];
-    unsigned long long h2 = 0;
+    const int s_first = s_src;
+    __syncthreads();
+    if (s_first >= n_active) break;
+    const int s_last = min(n_active, s_first + a.dq);
+    for (int s = s_first; s < s_last; ++s) {
+      const int x = a.active[s];
+      const int pbeg = a.off[x], pcnt = a.cnt[x];
+      const int64_t xb = a.rp[x], xe = a.rp[x + 1];
+      const int hslot = a.heavy_slot ? a.heavy_slot[x] : -1;
+      // value range of N(x) (rows are sorted): distance-1 removal is skipped when disjoint
+      const int64_t nx_lo = xe > xb ? a.ci[xb] : 0, nx_hi = xe > xb ? a.ci[xe - 1] : -1;
+      unsigned long long h2 = 0;
 
-    for (int ch = 0; ch < nchunks; ++ch) {
-      const int64_t c0 = a.lo + (int64_t)ch * CAP_BITS;
-      const int64_t c1 = min(a.hi, c0 + CAP_BITS);
-      const int64_t width = max<int64_t>(c1 - c0, 0);
-      const int nw4 = (int)((((width + 31) >> 5) + 3) >> 2);
-      const bool last = ch == nchunks - 1;
-      // 1. clear the chunk's words
-      for (int i = threadIdx.x; i < nw4; i += BLOCK) bm4[i] = make_uint4(0, 0, 0, 0);
-      __syncthreads();
-      // 2. mark N(N(x)) within [c0, c1): short rows by lane groups, long rows deferred
-      for (int64_t k = xb + my_group; k < xe; k += n_groups) {
-        const int z = a.ci[k];
-        const int64_t zb = a.rp[z], ze = a.rp[z + 1];
-        if (ze - zb > LONG_ROW && gl == 0) {
-          const int slot = atomicAdd(&s_nlong, 1);
-          if (slot < LONG_LIST) s_long[slot] = z;
-        }
-        if (ze - zb > LONG_ROW) continue;  // deferred: block loop below (list or rescan)
-        for (int64_t e = zb + gl; e < ze; e += G) {
-          const int64_t r = (int64_t)a.ci[e] - c0;
-          if (r >= 0 && r < width) atomicOr(&bm[r >> 5], 1u << (r & 31));
-        }
-      }
-      __syncthreads();
-      {
-        const int nl = s_nlong;
-        // overflowed long rows (more than LONG_LIST of them) are found again by a block scan
-        if (nl > LONG_LIST) {
-          for (int64_t k = xb; k < xe; ++k) {
-            const int z = a.ci[k];
-            const int64_t zb = a.rp[z], ze = a.rp[z + 1];
-            if (ze - zb <= LONG_ROW) continue;
-            for (int64_t e = zb + threadIdx.x; e < ze; e += BLOCK) {
-              const int64_t r = (int64_t)a.ci[e] - c0;
-              if (r >= 0 && r < width) atomicOr(&bm[r >> 5], 1u << (r & 31));
-            }
-          }
+      for (int ch = 0; ch < nchunks; ++ch) {
+        const int64_t c0 = a.lo + (int64_t)ch * CAP_BITS;
+        const int64_t c1 = min(a.hi, c0 + CAP_BITS);
+        const int64_t width = max<int64_t>(c1 - c0, 0);
+        const int nw4 = (int)((((width + 31) >> 5) + 3) >> 2);
+        const bool last = ch == nchunks - 1;
+        if (hslot >= 0) {
+          // 1'. pre-built by k_heavy (single-chunk universes only)
+          const uint4* src4 = reinterpret_cast<const uint4*>(a.heavy_bm + (int64_t)hslot * a.hb_words);
+          for (int i = threadIdx.x; i < nw4; i += BLOCK) bm4[i] = src4[i];
+          __syncthreads();
         } else {
-          for (int l = 0; l < nl; ++l) {
-            const int z = s_long[l];
-            const int64_t zb = a.rp[z], ze = a.rp[z + 1];
-            for (int64_t e = zb + threadIdx.x; e < ze; e += BLOCK) {
-              const int64_t r = (int64_t)a.ci[e] - c0;
-              if (r >= 0 && r < width) atomicOr(&bm[r >> 5], 1u << (r & 31));
-            }
-          }
-        }
-      }
-      __syncthreads();
-      if (threadIdx.x == 0) s_nlong = 0;
-      // 3. exact distance 2: drop x (distance 0) and N(x) (distance 1)
-      for (int64_t k = xb + threadIdx.x; k <= xe; k += BLOCK) {
-        const int64_t r = (k == xe ? (int64_t)x : (int64_t)a.ci[k]) - c0;
-        if (r >= 0 && r < width) atomicAnd(&bm[r >> 5], ~(1u << (r & 31)));
-      }
-      __syncthreads();
-      // 4. |H2(x) ∩ chunk|
-      if (want_j) {
-        unsigned long long pc = 0;
-        for (int i = threadIdx.x; i < nw4; i += BLOCK) {
-          uint4 q = bm4[i];
-          pc += __popc(q.x) + __popc(q.y) + __popc(q.z) + __popc(q.w);
-        }
-        h2 += block_sum_u64<BLOCK>(pc, red);
-      }
-      // 5. scan N(y) for every pair of x (long rows deferred to the block loop below)
-      for (int j = my_group; j < pcnt; j += n_groups) {
-        const int p = a.perm[pbeg + j];
-        const int y = a.y[p];
-        const int64_t yb = a.rp[y], ye = a.rp[y + 1];
-        if (ye - yb > LONG_ROW) {
-          if (gl == 0) {
-            const int slot = atomicAdd(&s_nlong, 1);
-            if (slot < LONG_LIST) s_long[slot] = j;
-          }
-          continue;
-        }
-        unsigned c = 0;
-        double sw = 0.0;
-        for (int64_t e = yb + gl; e < ye; e += G) {
-          const int w = a.ci[e];
-          const int64_t r = (int64_t)w - c0;
-          if (r >= 0 && r < width && ((bm[r >> 5] >> (r & 31)) & 1u)) {
-            ++c;
-            if (want_a) sw += a.aaw[w];
-          }
-        }
-        c = group_sum(c, G);
-        if (want_a) sw = group_sum(sw, G);
-        if (gl == 0) {
-          if (ch > 0) {
-            c += a.cn[p];
-            if (want_a) sw += a.aa[p];
-          }
-          a.cn[p] = c;
-          if (want_a) a.aa[p] = sw;
-          if (want_j && last) {
-            const long long uni = (long long)h2 + (ye - yb) - (long long)c;
-            if (uni <= 0) {
-              a.jac[p] = __builtin_nan("");
-              atomicOr(&a.misc->zero_div, 1);
-            } else {
-              a.jac[p] = (double)c / (double)uni;
-            }
-          }
-        }
-      }
-      __syncthreads();
-      {
-        const int nl = s_nlong;
-        const int count = nl > LONG_LIST ? pcnt : nl;
-        for (int l = 0; l < count; ++l) {
-          const int j = nl > LONG_LIST ? l : s_long[l];
-          const int p = a.perm[pbeg + j];
-          const int y = a.y[p];
-          const int64_t yb = a.rp[y], ye = a.rp[y + 1];
-          if (ye - yb <= LONG_ROW) continue;  // only in the overflow rescan
-          unsigned long long c = 0;
-          double sw = 0.0;
-          for (int64_t e = yb + threadIdx.x; e < ye; e += BLOCK) {
-            const int w = a.ci[e];
-            const int64_t r = (int64_t)w - c0;
-            if (r >= 0 && r < width && ((bm[r >> 5] >> (r & 31)) & 1u)) {
-              ++c;
-              if (want_a) sw += a.aaw[w];
-            }
-          }
-          c = block_sum_u64<BLOCK>(c, red);
-          if (want_a) {
-            for (int o = 32; o > 0; o >>= 1) sw += __shfl_xor(sw, o, 64);
-            if (lane == 0) redd[wid] = sw;
-            __syncthreads();
-            sw = 0.0;
-            for (int w2 = 0; w2 < NW; ++w2) sw += redd[w2];
+          // 1. clear, 2. mark N(N(x)) ∩ [c0, c1) through merge-path row segments
+          for (int i = threadIdx.x; i < nw4; i += BLOCK) bm4[i] = make_uint4(0, 0, 0, 0);
+          __syncthreads();
+          for (int64_t k0 = xb; k0 < xe; k0 += SEG) {
+            const int ns = (int)min<int64_t>(SEG, xe - k0);
+            load_row_segments<BLOCK>(a.rp, a.ci, k0, ns, s_start, s_off, red);
+            mp_build<BLOCK>(a.ci, s_start, s_off, ns, c0, width, bm);
             __syncthreads();
           }
-          if (threadIdx.x == 0) {
-            unsigned cc = (unsigned)c;
+        }
+        // 3. exact distance 2: drop x (distance 0) and N(x) (distance 1)
+        if (nx_hi >= c0 && nx_lo < c1) {
+          for (int64_t k = xb + threadIdx.x; k < xe; k += BLOCK) {
+            const int64_t r = (int64_t)a.ci[k] - c0;
+            if (r >= 0 && r < width) atomicAnd(&bm[r >> 5], ~(1u << (r & 31)));
+          }
+        }
+        if (threadIdx.x == 0 && x >= c0 && x < c1) atomicAnd(&bm[(x - c0) >> 5], ~(1u << ((x - c0) & 31)));
+        __syncthreads();
+        // 4. |H2(x) ∩ chunk|
+        if (want_j) {
+          unsigned long long pc = 0;
+          for (int i = threadIdx.x; i < nw4; i += BLOCK) {
+            const uint4 q = bm4[i];
+            pc += __popc(q.x) + __popc(q.y) + __popc(q.z) + __popc(q.w);
+          }
+          h2 += block_sum_u64<BLOCK>(pc, red64);
+        }
+        // 5. scan N(y) of every pair of x, SEG pairs at a time
+        for (int sb = 0; sb < pcnt; sb += SEG) {
+          const int ns = min(SEG, pcnt - sb);
+          int len = 0;
+          if ((int)threadIdx.x < ns) {
+            const int gp = pbeg + sb + threadIdx.x;
+            s_start[threadIdx.x] = a.g_yb[gp];
+            len = a.g_yl[gp];
+            s_cn[threadIdx.x] = 0;
+            s_aa[threadIdx.x] = 0;
+          }
+          int tot;
+          const int ex = block_exscan<BLOCK>(len, red, &tot);
+          if ((int)threadIdx.x < ns) s_off[threadIdx.x] = ex;
+          if (threadIdx.x == 0) s_off[ns] = tot;
+          __syncthreads();
+          if (want_a)
+            mp_scan<BLOCK, true>(a.ci, a.aaw, s_start, s_off, ns, c0, width, bm, s_cn, s_aa);
+          else
+            mp_scan<BLOCK, false>(a.ci, a.aaw, s_start, s_off, ns, c0, width, bm, s_cn, s_aa);
+          __syncthreads();
+          for (int t = threadIdx.x; t < ns; t += BLOCK) {
+            const int p = a.g_out[pbeg + sb + t];
+            unsigned c = s_cn[t];
+            double av = (double)s_aa[t] * (1.0 / blp::AA_SCALE);
             if (ch > 0) {
-              cc += a.cn[p];
-              if (want_a) sw += a.aa[p];
+              c += a.cn[p];
+              if (want_a) av += a.aa[p];
             }
-            a.cn[p] = cc;
-            if (want_a) a.aa[p] = sw;
+            a.cn[p] = c;
+            if (want_a) a.aa[p] = av;
             if (want_j && last) {
-              const long long uni = (long long)h2 + (ye - yb) - (long long)cc;
+              const long long uni = (long long)h2 + (s_off[t + 1] - s_off[t]) - (long long)c;
               if (uni <= 0) {
                 a.jac[p] = __builtin_nan("");
                 atomicOr(&a.misc->zero_div, 1);
               } else {
-                a.jac[p] = (double)cc / (double)uni;
+                a.jac[p] = (double)c / (double)uni;  // correctly rounded, as Python's float division
               }
             }
           }
+          __syncthreads();
         }
       }
-      __syncthreads();
-      if (threadIdx.x == 0) s_nlong = 0;
-      __syncthreads();
     }
   }
 }
 
 enum Variant { V_SMALL = 0, V_MED = 1, V_LARGE = 2 };
-constexpr int CAP_SMALL = 4096, CAP_MED = 16384, CAP_LARGE = 36864;  // words: 16 / 64 / 144 KiB
+// LDS bitmap words (16 / 64 / 136 KiB), threads per block, pair/row segments per chunk
+constexpr int CAP_SMALL = 4096, CAP_MED = 16384, CAP_LARGE = 34816;
 constexpr int BLOCK_SMALL = 256, BLOCK_MED = 512, BLOCK_LARGE = 1024;
+constexpr int SEG_SMALL = 256, SEG_MED = 512, SEG_LARGE = 512;
+
+inline int variant_block(int v) { return v == V_SMALL ? BLOCK_SMALL : v == V_MED ? BLOCK_MED : BLOCK_LARGE; }
+inline int64_t variant_cap_bits(int v) { return 32ll * (v == V_SMALL ? CAP_SMALL : v == V_MED ? CAP_MED : CAP_LARGE); }
 
 }  // namespace
 
@@ -409,25 +566,49 @@ struct blp_batch {
   uint32_t* d_cn = nullptr;
   double* d_jac = nullptr;
   double* d_aa = nullptr;
-  int32_t* d_perm = nullptr;
+  int32_t* d_gout = nullptr;
+  int64_t* d_gyb = nullptr;
+  int32_t* d_gyl = nullptr;
   Misc* d_misc = nullptr;
+  // heavy sources (planned at create)
+  int32_t* d_heavy_slot = nullptr;
+  uint32_t* d_heavy_bm = nullptr;
+  HeavyItem* d_heavy_items = nullptr;
+  int64_t n_heavy = 0, n_heavy_items = 0, hb_words = 0;
   int64_t lo = 0, hi = 0;
   int variant = V_SMALL;
-  int group = 64;
   int chunks = 1;
+  int dq = 1;
+  int64_t cap_bits = 0;
   int64_t n_sources = 0;
   blp::KernelTimer t_score, t_group;
 };
 
 using namespace blp;
 
-template <int BLOCK, int CAP>
-static int launch_score(blp_graph* g, const ScoreArgs& a) {
-  int per_cu = 0;
-  BLP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_score<BLOCK, CAP>, BLOCK, 0));
-  per_cu = std::max(per_cu, 1);
-  const int grid = g->n_cu * per_cu;
-  hipLaunchKernelGGL((k_score<BLOCK, CAP>), dim3(grid), dim3(BLOCK), 0, g->stream, a);
+template <int BLOCK, int CAP, int SEG>
+static int score_occupancy(int* per_cu) {
+  BLP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, k_score<BLOCK, CAP, SEG>, BLOCK, 0));
+  *per_cu = std::max(*per_cu, 1);
+  return BLP_OK;
+}
+
+static int variant_occupancy(int v, int* per_cu) {
+  if (v == V_SMALL) return score_occupancy<BLOCK_SMALL, CAP_SMALL, SEG_SMALL>(per_cu);
+  if (v == V_MED) return score_occupancy<BLOCK_MED, CAP_MED, SEG_MED>(per_cu);
+  return score_occupancy<BLOCK_LARGE, CAP_LARGE, SEG_LARGE>(per_cu);
+}
+
+template <int BLOCK, int CAP, int SEG>
+static int launch_score(blp_graph* g, const ScoreArgs& a, int per_cu) {
+  hipLaunchKernelGGL((k_score<BLOCK, CAP, SEG>), dim3(g->n_cu * per_cu), dim3(BLOCK), 0, g->stream, a);
+  BLP_HIP(hipGetLastError());
+  return BLP_OK;
+}
+
+template <int BLOCK, int CAP, int SEG>
+static int launch_heavy(blp_graph* g, const HeavyArgs& h, int64_t n_items) {
+  hipLaunchKernelGGL((k_heavy<BLOCK, CAP, SEG>), dim3((unsigned)n_items), dim3(BLOCK), 0, g->stream, h);
   BLP_HIP(hipGetLastError());
   return BLP_OK;
 }
@@ -440,11 +621,12 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   const int64_t n = g->n;
   const int64_t* rp = g->h_rp.data();
   const int32_t* ci = g->h_ci.data();
-  // ---- plan: node universe touched by H2(x) and N(y), lane group size
+  // ---- plan: node universe touched by H2(x) and N(y); per-source build work
   int64_t lo = INT64_MAX, hi = INT64_MIN;
   std::vector<uint8_t> seen((size_t)n, 0);
-  double ysum = 0.0;
-  int64_t n_src = 0;
+  std::vector<int32_t> srcs;
+  std::vector<int64_t> work;
+  int64_t scan_work = 0;
   for (int64_t i = 0; i < n_pairs; ++i) {
     const int32_t xi = x[i], yi = y[i];
     if (xi < 0 || xi >= n || yi < 0 || yi >= n) return fail(BLP_E_ARG, "blp_batch_create: node id out of range");
@@ -452,17 +634,20 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
       lo = std::min<int64_t>(lo, ci[rp[yi]]);
       hi = std::max<int64_t>(hi, (int64_t)ci[rp[yi + 1] - 1] + 1);
     }
-    ysum += (double)(rp[yi + 1] - rp[yi]);
+    scan_work += rp[yi + 1] - rp[yi];
     if (!seen[xi]) {
       seen[xi] = 1;
-      ++n_src;
+      srcs.push_back(xi);
+      int64_t wsum = 0;
       for (int64_t k = rp[xi]; k < rp[xi + 1]; ++k) {
         const int32_t z = ci[k];
+        wsum += rp[z + 1] - rp[z];
         if (rp[z + 1] > rp[z]) {
           lo = std::min<int64_t>(lo, ci[rp[z]]);
           hi = std::max<int64_t>(hi, (int64_t)ci[rp[z + 1] - 1] + 1);
         }
       }
+      work.push_back(wsum);
     }
   }
   if (lo > hi) lo = hi = 0;
@@ -471,42 +656,77 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   b->n_pairs = n_pairs;
   b->lo = lo;
   b->hi = hi;
-  b->n_sources = n_src;
+  b->n_sources = (int64_t)srcs.size();
   const int64_t span = hi - lo;
-  if (span <= (int64_t)CAP_SMALL * 32)
+  if (span <= variant_cap_bits(V_SMALL))
     b->variant = V_SMALL;
-  else if (span <= (int64_t)CAP_MED * 32)
+  else if (span <= variant_cap_bits(V_MED))
     b->variant = V_MED;
   else
     b->variant = V_LARGE;
-  int64_t cap_bits = 32ll * (b->variant == V_SMALL ? CAP_SMALL : b->variant == V_MED ? CAP_MED : CAP_LARGE);
-  if (const char* e = getenv("BLP_CHUNK_BITS")) {
+  b->cap_bits = variant_cap_bits(b->variant);
+  if (const char* e = getenv("BLP_CHUNK_BITS")) {  // test knob: force multi-chunk on small graphs
     int64_t v = atoll(e);
-    if (v >= 128 && v % 128 == 0 && v < cap_bits) cap_bits = v;
+    if (v >= 128 && v % 128 == 0 && v < b->cap_bits) b->cap_bits = v;
   }
-  b->chunks = span <= cap_bits ? 1 : (int)((span + cap_bits - 1) / cap_bits);
-  const double ymean = n_pairs ? ysum / (double)n_pairs : 64.0;
-  b->group = ymean >= 48 ? 64 : ymean >= 24 ? 32 : ymean >= 12 ? 16 : 8;
-  if (const char* e = getenv("BLP_GROUP")) {
-    int gsz = atoi(e);
-    if (gsz == 8 || gsz == 16 || gsz == 32 || gsz == 64) b->group = gsz;
-  }
-  // ---- device buffers
+  b->chunks = span <= b->cap_bits ? 1 : (int)((span + b->cap_bits - 1) / b->cap_bits);
   auto bail = [&](int rc) {
     blp_batch_destroy(b);
     return rc;
   };
   int rc = set_device(g);
   if (rc) return bail(rc);
+  int per_cu = 1;
+  if ((rc = variant_occupancy(b->variant, &per_cu))) return bail(rc);
+  const int64_t n_wg = (int64_t)g->n_cu * per_cu;
+  b->dq = (int)std::max<int64_t>(1, std::min<int64_t>(8, b->n_sources / (n_wg * 16)));
+  // ---- heavy sources: build work far above the per-workgroup share goes to k_heavy
+  const int64_t total_work = std::accumulate(work.begin(), work.end(), (int64_t)0) + scan_work;
+  int64_t item_work = std::max<int64_t>(16384, total_work / std::max<int64_t>(n_wg, 1));
+  if (const char* e = getenv("BLP_HEAVY_WORK")) item_work = std::max<int64_t>(1, atoll(e));  // test knob
+  std::vector<int32_t> heavy_slot;
+  std::vector<HeavyItem> items;
+  if (b->chunks == 1 && span > 0) {
+    for (size_t i = 0; i < srcs.size(); ++i) {
+      if (work[i] <= 2 * item_work) continue;
+      if (heavy_slot.empty()) heavy_slot.assign((size_t)n, -1);
+      const int32_t xs = srcs[i];
+      const int32_t slot = (int32_t)b->n_heavy++;
+      heavy_slot[xs] = slot;
+      int64_t acc = 0, kb = rp[xs];
+      for (int64_t k = rp[xs]; k < rp[xs + 1]; ++k) {
+        acc += rp[ci[k] + 1] - rp[ci[k]];
+        if (acc >= item_work || k + 1 == rp[xs + 1]) {
+          items.push_back(HeavyItem{slot, 0, kb, k + 1});
+          kb = k + 1;
+          acc = 0;
+        }
+      }
+    }
+  }
+  b->n_heavy_items = (int64_t)items.size();
+  b->hb_words = ((span + 31) / 32 + 3) / 4 * 4;
+  // ---- device buffers
   const size_t np = (size_t)std::max<int64_t>(n_pairs, 1);
   if (hipMalloc(&b->d_x, 4 * np) != hipSuccess || hipMalloc(&b->d_y, 4 * np) != hipSuccess ||
       hipMalloc(&b->d_cn, 4 * np) != hipSuccess || hipMalloc(&b->d_jac, 8 * np) != hipSuccess ||
-      hipMalloc(&b->d_aa, 8 * np) != hipSuccess || hipMalloc(&b->d_perm, 4 * np) != hipSuccess ||
+      hipMalloc(&b->d_aa, 8 * np) != hipSuccess || hipMalloc(&b->d_gout, 4 * np) != hipSuccess ||
+      hipMalloc(&b->d_gyb, 8 * np) != hipSuccess || hipMalloc(&b->d_gyl, 4 * np) != hipSuccess ||
       hipMalloc(&b->d_misc, sizeof(Misc)) != hipSuccess)
     return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: hipMalloc failed"));
   if (n_pairs) {
     if (hipMemcpy(b->d_x, x, 4 * n_pairs, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(b->d_y, y, 4 * n_pairs, hipMemcpyHostToDevice) != hipSuccess)
+      return bail(fail(BLP_E_HIP_BASE, "blp_batch_create: upload failed"));
+  }
+  if (b->n_heavy) {
+    if (hipMalloc(&b->d_heavy_slot, 4 * n) != hipSuccess ||
+        hipMalloc(&b->d_heavy_bm, 4 * b->hb_words * b->n_heavy) != hipSuccess ||
+        hipMalloc(&b->d_heavy_items, sizeof(HeavyItem) * items.size()) != hipSuccess)
+      return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: hipMalloc failed"));
+    if (hipMemcpy(b->d_heavy_slot, heavy_slot.data(), 4 * n, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(b->d_heavy_items, items.data(), sizeof(HeavyItem) * items.size(), hipMemcpyHostToDevice) !=
+            hipSuccess)
       return bail(fail(BLP_E_HIP_BASE, "blp_batch_create: upload failed"));
   }
   *out = b;
@@ -519,27 +739,28 @@ int blp_batch_destroy(blp_batch* b) {
   if (b->g && b->g->stream) (void)hipStreamSynchronize(b->g->stream);
   timer_release(b->t_score);
   timer_release(b->t_group);
-  void* ps[] = {b->d_x, b->d_y, b->d_cn, b->d_jac, b->d_aa, b->d_perm, b->d_misc};
+  void* ps[] = {b->d_x,    b->d_y,    b->d_cn,   b->d_jac,  b->d_aa,          b->d_gout,        b->d_gyb,
+                b->d_gyl,  b->d_misc, b->d_heavy_slot, b->d_heavy_bm, b->d_heavy_items};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   delete b;
   return BLP_OK;
 }
 
-int blp_batch_plan(const blp_batch* b, int64_t* lo, int64_t* hi, int* chunks, int* block, int* group) {
+int blp_batch_plan(const blp_batch* b, int64_t* lo, int64_t* hi, int* chunks, int* block, int* heavy) {
   BLP_CHECK(b, BLP_E_ARG, "blp_batch_plan: null batch");
   if (lo) *lo = b->lo;
   if (hi) *hi = b->hi;
   if (chunks) *chunks = b->chunks;
-  if (block) *block = b->variant == V_SMALL ? BLOCK_SMALL : b->variant == V_MED ? BLOCK_MED : BLOCK_LARGE;
-  if (group) *group = b->group;
+  if (block) *block = variant_block(b->variant);
+  if (heavy) *heavy = (int)b->n_heavy;
   return BLP_OK;
 }
 
 int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   BLP_CHECK(g && b && b->g == g, BLP_E_ARG, "blp_batch_score: graph/batch mismatch");
   BLP_CHECK((mask & ~7u) == 0, BLP_E_ARG, "blp_batch_score: unknown method bits");
-  BLP_CHECK(!(mask & BLP_ADAMIC) || g->d_aaw, BLP_E_STATE,
+  BLP_CHECK(!(mask & BLP_ADAMIC) || g->d_aaw_fx, BLP_E_STATE,
             "blp_batch_score: adamic_adar requested but the graph has no aa_weight table");
   int rc = set_device(g);
   if (rc) return rc;
@@ -555,7 +776,8 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   if ((rc = timer_begin(b->t_group, g->stream, &bt0))) return rc;
   BLP_HIP(hipMemsetAsync(g->cnt.p, 0, 4 * (n + 1), g->stream));
   BLP_HIP(hipMemsetAsync(b->d_misc, 0, sizeof(Misc), g->stream));
-  const int ew_grid = (int)std::min<int64_t>(std::max<int64_t>((np + 255) / 256, 1), (int64_t)g->n_cu * 16);
+  const int64_t nchunk = (np + RUN_CHUNK - 1) / RUN_CHUNK;
+  const int ew_grid = (int)std::min<int64_t>(std::max<int64_t>((nchunk + 255) / 256, 1), (int64_t)g->n_cu * 16);
   if (np) hipLaunchKernelGGL(k_count, dim3(ew_grid), dim3(256), 0, g->stream, b->d_x, np, g->cnt.as<int32_t>());
   if (ntiles) {
     hipLaunchKernelGGL(k_scan_tiles, dim3((unsigned)ntiles), dim3(SCAN_BLOCK), 0, g->stream, g->cnt.as<int32_t>(), n,
@@ -565,49 +787,58 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
     hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)ntiles), dim3(SCAN_BLOCK), 0, g->stream, g->cnt.as<int32_t>(), n,
                        g->scratch.as<int2>(), g->off.as<int32_t>(), g->cursor.as<int32_t>(), g->active.as<int32_t>());
   }
-  if (np) hipLaunchKernelGGL(k_scatter, dim3(ew_grid), dim3(256), 0, g->stream, b->d_x, np, g->cursor.as<int32_t>(), b->d_perm);
+  if (np)
+    hipLaunchKernelGGL(k_scatter, dim3(ew_grid), dim3(256), 0, g->stream, b->d_x, b->d_y, np, g->d_rp,
+                       g->cursor.as<int32_t>(), b->d_gout, b->d_gyb, b->d_gyl);
   BLP_HIP(hipGetLastError());
   if ((rc = timer_end(b->t_group, g->stream, bt0))) return rc;
   if ((rc = timer_end(g, K_GROUP, t0))) return rc;
 
+  hipEvent_t t1, bt1;
+  if ((rc = timer_begin(g, K_SCORE, &t1))) return rc;
+  if ((rc = timer_begin(b->t_score, g->stream, &bt1))) return rc;
+  if (b->n_heavy) {
+    BLP_HIP(hipMemsetAsync(b->d_heavy_bm, 0, 4 * b->hb_words * b->n_heavy, g->stream));
+    HeavyArgs h{g->d_rp, g->d_ci, b->d_heavy_items, b->d_heavy_bm, b->hb_words, b->lo, b->hi - b->lo};
+    if (b->variant == V_SMALL)
+      rc = launch_heavy<BLOCK_SMALL, CAP_SMALL, SEG_SMALL>(g, h, b->n_heavy_items);
+    else if (b->variant == V_MED)
+      rc = launch_heavy<BLOCK_MED, CAP_MED, SEG_MED>(g, h, b->n_heavy_items);
+    else
+      rc = launch_heavy<BLOCK_LARGE, CAP_LARGE, SEG_LARGE>(g, h, b->n_heavy_items);
+    if (rc) return rc;
+  }
   ScoreArgs a;
   a.rp = g->d_rp;
   a.ci = g->d_ci;
-  a.aaw = g->d_aaw;
-  a.y = b->d_y;
-  a.perm = b->d_perm;
+  a.aaw = g->d_aaw_fx;
   a.off = g->off.as<int32_t>();
   a.cnt = g->cnt.as<int32_t>();
   a.active = g->active.as<int32_t>();
+  a.g_out = b->d_gout;
+  a.g_yb = b->d_gyb;
+  a.g_yl = b->d_gyl;
+  a.heavy_slot = b->d_heavy_slot;
+  a.heavy_bm = b->d_heavy_bm;
+  a.hb_words = b->hb_words;
   a.misc = b->d_misc;
   a.cn = b->d_cn;
   a.jac = b->d_jac;
   a.aa = b->d_aa;
   a.lo = b->lo;
   a.hi = b->hi;
+  a.cap_bits = b->cap_bits;
   a.mask = mask | BLP_CN;  // counts are always produced (Jaccard needs them)
-  a.group = b->group;
-  const int block = b->variant == V_SMALL ? BLOCK_SMALL : b->variant == V_MED ? BLOCK_MED : BLOCK_LARGE;
-  a.cap_bits = 32ll * (b->variant == V_SMALL ? CAP_SMALL : b->variant == V_MED ? CAP_MED : CAP_LARGE);
-  a.long_row = block;
-  if (const char* e = getenv("BLP_CHUNK_BITS")) {  // test knob: force multi-chunk on small graphs
-    int64_t v = atoll(e);
-    if (v >= 128 && v % 128 == 0 && v < a.cap_bits) a.cap_bits = v;
-  }
-  if (const char* e = getenv("BLP_LONG_ROW")) {  // test knob: exercise the deferred-row loops
-    int64_t v = atoll(e);
-    if (v >= 1) a.long_row = v;
-  }
-  hipEvent_t t1, bt1;
-  if ((rc = timer_begin(g, K_SCORE, &t1))) return rc;
-  if ((rc = timer_begin(b->t_score, g->stream, &bt1))) return rc;
+  a.dq = b->dq;
   if (np) {
+    int per_cu = 1;
+    if ((rc = variant_occupancy(b->variant, &per_cu))) return rc;
     if (b->variant == V_SMALL)
-      rc = launch_score<BLOCK_SMALL, CAP_SMALL>(g, a);
+      rc = launch_score<BLOCK_SMALL, CAP_SMALL, SEG_SMALL>(g, a, per_cu);
     else if (b->variant == V_MED)
-      rc = launch_score<BLOCK_MED, CAP_MED>(g, a);
+      rc = launch_score<BLOCK_MED, CAP_MED, SEG_MED>(g, a, per_cu);
     else
-      rc = launch_score<BLOCK_LARGE, CAP_LARGE>(g, a);
+      rc = launch_score<BLOCK_LARGE, CAP_LARGE, SEG_LARGE>(g, a, per_cu);
     if (rc) return rc;
   }
   if ((rc = timer_end(b->t_score, g->stream, bt1))) return rc;

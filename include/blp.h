@@ -106,9 +106,9 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask);
 int blp_batch_fetch(blp_graph* g, blp_batch* b, uint32_t* cn, double* jac, double* aa);
 int blp_batch_destroy(blp_batch* b);
 /* Launch plan actually used: universe lo/hi (bitmap range), bitmap chunks, threads per
- * block, lanes per pair group. For tests and DESIGN.md bookkeeping.                       */
+ * block, number of heavy sources pre-built across workgroups. For tests and DESIGN.md.     */
 int blp_batch_plan(const blp_batch* b, int64_t* lo, int64_t* hi, int* chunks, int* block,
-                   int* group);
+                   int* heavy);
 
 /* Per-batch device time of the last/accumulated blp_batch_score calls (HIP events on the
  * graph stream): which 0 = scorer kernel, 1 = grouping kernels. Reset with blp_batch_stats_reset. */

@@ -40,7 +40,7 @@ def _check_against_oracle(ga, gb, x, y, mask=7):
     if mask & blp.JACCARD:
         np.testing.assert_array_equal(got["jaccard"], jac)  # bit-exact
     if mask & blp.ADAMIC:
-        np.testing.assert_allclose(got["adamic"], aa, rtol=1e-12, atol=0)
+        np.testing.assert_allclose(got["adamic"], aa, rtol=1e-9, atol=0)
         assert np.array_equal(got["adamic"] == 0, aa == 0)
     return G
 
@@ -74,10 +74,11 @@ def test_general_graph_exact_distance(gpu):
 
 
 @pytest.mark.parametrize("knobs", [
-    {"BLP_CHUNK_BITS": "1024"},                       # multi-chunk bitmap universe
-    {"BLP_LONG_ROW": "3"},                            # deferred long-row loops (+ list overflow)
-    {"BLP_GROUP": "8"}, {"BLP_GROUP": "16"}, {"BLP_GROUP": "32"}, {"BLP_GROUP": "64"},
-    {"BLP_CHUNK_BITS": "2048", "BLP_LONG_ROW": "7", "BLP_GROUP": "16"},
+    {},
+    {"BLP_CHUNK_BITS": "1024"},                         # multi-chunk bitmap universe
+    {"BLP_HEAVY_WORK": "50"},                           # heavy sources pre-built by k_heavy
+    {"BLP_HEAVY_WORK": "1"},                            # one row per heavy item
+    {"BLP_CHUNK_BITS": "2048", "BLP_HEAVY_WORK": "50"}, # multi-chunk disables the heavy path
 ])
 def test_kernel_paths_vs_oracle(gpu, knobs, monkeypatch):
     for k, v in knobs.items():
@@ -90,6 +91,33 @@ def test_kernel_paths_vs_oracle(gpu, knobs, monkeypatch):
     y = rng.integers(nu, G.n, len(x)).astype(np.int32)
     _check_against_oracle(a, b, x, y)
     _check_against_oracle(a, b, y, x)
+    if "BLP_HEAVY_WORK" in knobs and "BLP_CHUNK_BITS" not in knobs:
+        assert G.batch(y, x).plan()["heavy"] > 0
+
+
+def test_many_pairs_per_source_vs_oracle(gpu):
+    # > SEG pairs per source and > SEG rows in N(x): the segment-chunk loops
+    rng = np.random.default_rng(12)
+    a, b = bipartite_edges(rng, 20000, 1500, 200000)
+    G = blp.DeviceGraph(a, b)
+    nu = G.n - len(np.unique(b))
+    users = rng.choice(nu, 6, replace=False)
+    x = np.repeat(users, 1400).astype(np.int32)
+    y = rng.integers(nu, G.n, len(x)).astype(np.int32)
+    _check_against_oracle(a, b, x, y)
+    _check_against_oracle(a, b, y, x)   # popular businesses: N(x) has thousands of rows
+
+
+def test_unsorted_pair_order_vs_oracle(gpu):
+    # grouping must not assume any input order (runs of x broken up)
+    rng = np.random.default_rng(13)
+    a, b = bipartite_edges(rng, 20000, 1500, 200000)
+    G = blp.DeviceGraph(a, b)
+    nu = G.n - len(np.unique(b))
+    x = np.repeat(rng.choice(nu, 100, replace=False), 50).astype(np.int32)
+    y = rng.integers(nu, G.n, len(x)).astype(np.int32)
+    perm = rng.permutation(len(x))
+    _check_against_oracle(a, b, x[perm], y[perm])
 
 
 def test_batch_repeat_is_deterministic(gpu):
