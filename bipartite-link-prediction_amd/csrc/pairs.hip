@@ -33,8 +33,6 @@ namespace {
 constexpr int SCAN_BLOCK = 256;
 constexpr int SCAN_ITEMS = 16;
 constexpr int SCAN_TILE = SCAN_BLOCK * SCAN_ITEMS;
-constexpr int RUN_CHUNK = 16;  // pairs per thread in the run-aggregated count / scatter
-constexpr int KPT = 8;         // merge-path elements per thread per step
 
 struct Misc {
   int n_active;
@@ -44,149 +42,188 @@ struct Misc {
 };
 
 // ------------------------------------------------------------------ grouping kernels
-// Counts per source. Each thread owns RUN_CHUNK consecutive pairs and issues one atomic per
-// run of equal x (device-scope atomics execute at the memory side on a multi-XCD part).
-__global__ void k_count(const int32_t* __restrict__ x, int64_t n_pairs, int32_t* __restrict__ cnt) {
-  const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c * RUN_CHUNK < n_pairs; c += nthr) {
-    const int64_t b = c * RUN_CHUNK, e = min(n_pairs, b + RUN_CHUNK);
-    int cur = x[b], run = 1;
-    for (int64_t i = b + 1; i < e; ++i) {
-      const int xi = x[i];
-      if (xi == cur) {
-        ++run;
-      } else {
-        atomicAdd(&cnt[cur], run);
-        cur = xi;
-        run = 1;
-      }
-    }
-    atomicAdd(&cnt[cur], run);
-  }
-}
+// Two-pass MSD bucket sort of the pairs by source x, with every atomic in LDS (a device-
+// scope atomic executes at the memory side on a multi-XCD part and costs ~50x more):
+//   1. k_bucket_hist    per-block histogram of buckets b = x >> shift  (bucket-major table)
+//   2. scan_ex          exclusive scan of that table -> bucket/block write offsets
+//   3. k_bucket_scatter pair indices into bucket order
+//   4. k_bucket_group   one block per bucket: counting sort of its keys in LDS, per-node
+//                       off/cnt, grouped pair metadata (caller index, N(y) start and length)
+//   5. scan_ex          of the per-bucket active-source counts
+//   6. k_active_write   the active-source list in ascending id order
+constexpr int GP_BLOCK = 1024;  // passes 1 and 3
+constexpr int GB_BLOCK = 256;   // passes 4 and 6
+constexpr int NB_MAX = 4096;    // buckets
 
-// block-wide exclusive scan of (count, flag) pairs; returns the block total in *tot
-__device__ inline int2 block_exscan2(int2 v, int2* lds, int2* tot) {
+// block-wide exclusive scan of one int per thread; *tot receives the block total
+template <int BLOCK>
+__device__ inline int block_exscan_i(int v, int* red, int* tot) {
+  constexpr int NW = BLOCK / 64;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  constexpr int NW = SCAN_BLOCK / 64;
-  int2 inc = v;
+  int inc = v;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
-    int tx = __shfl_up(inc.x, d, 64);
-    int ty = __shfl_up(inc.y, d, 64);
-    if (lane >= d) {
-      inc.x += tx;
-      inc.y += ty;
-    }
+    const int t = __shfl_up(inc, d, 64);
+    if (lane >= d) inc += t;
   }
-  if (lane == 63) lds[wid] = inc;
+  if (lane == 63) red[wid] = inc;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    int2 run = make_int2(0, 0);
-    for (int w = 0; w < NW; ++w) {
-      int2 t = lds[w];
-      lds[w] = run;
-      run.x += t.x;
-      run.y += t.y;
-    }
-    lds[NW] = run;
+  int base = 0, all = 0;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    const int t = red[w];
+    base += w < wid ? t : 0;
+    all += t;
   }
   __syncthreads();
-  int2 base = lds[wid];
-  *tot = lds[NW];
-  __syncthreads();
-  return make_int2(base.x + inc.x - v.x, base.y + inc.y - v.y);
+  *tot = all;
+  return base + inc - v;
 }
 
-// pass 1: per-tile totals of (cnt, cnt > 0)
-__global__ __launch_bounds__(SCAN_BLOCK) void k_scan_tiles(const int32_t* __restrict__ cnt, int64_t n,
-                                                           int2* __restrict__ tile_sum) {
-  __shared__ int2 lds[SCAN_BLOCK / 64 + 1];
-  int64_t base = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)threadIdx.x * SCAN_ITEMS;
-  int2 v = make_int2(0, 0);
+// --- generic exclusive scan of an int32 array (3 kernels), total -> *total_out
+__global__ __launch_bounds__(SCAN_BLOCK) void k_scan_sum(const int32_t* __restrict__ in, int64_t n,
+                                                         int32_t* __restrict__ tile_sum) {
+  __shared__ int red[SCAN_BLOCK / 64];
+  const int64_t base = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)threadIdx.x * SCAN_ITEMS;
+  int v = 0;
 #pragma unroll
-  for (int k = 0; k < SCAN_ITEMS; ++k) {
-    int64_t i = base + k;
-    int c = i < n ? cnt[i] : 0;
-    v.x += c;
-    v.y += c > 0;
-  }
-  int2 tot;
-  block_exscan2(v, lds, &tot);
+  for (int k = 0; k < SCAN_ITEMS; ++k) v += base + k < n ? in[base + k] : 0;
+  int tot;
+  block_exscan_i<SCAN_BLOCK>(v, red, &tot);
   if (threadIdx.x == 0) tile_sum[blockIdx.x] = tot;
 }
 
-// pass 2: exclusive scan of the tile totals (one block); writes n_active
-__global__ __launch_bounds__(SCAN_BLOCK) void k_scan_tilesums(int2* __restrict__ tile_sum, int64_t ntiles,
-                                                              Misc* __restrict__ misc) {
-  __shared__ int2 lds[SCAN_BLOCK / 64 + 1];
-  int2 carry = make_int2(0, 0);
+__global__ __launch_bounds__(SCAN_BLOCK) void k_scan_mid(int32_t* __restrict__ tile_sum, int64_t ntiles,
+                                                         int32_t* __restrict__ total_out) {
+  __shared__ int red[SCAN_BLOCK / 64];
+  int carry = 0;
   for (int64_t b = 0; b < ntiles; b += SCAN_BLOCK) {
-    int64_t i = b + threadIdx.x;
-    int2 v = i < ntiles ? tile_sum[i] : make_int2(0, 0);
-    int2 tot;
-    int2 e = block_exscan2(v, lds, &tot);
-    if (i < ntiles) tile_sum[i] = make_int2(e.x + carry.x, e.y + carry.y);
-    carry.x += tot.x;
-    carry.y += tot.y;
+    const int64_t i = b + threadIdx.x;
+    const int v = i < ntiles ? tile_sum[i] : 0;
+    int tot;
+    const int e = block_exscan_i<SCAN_BLOCK>(v, red, &tot);
+    if (i < ntiles) tile_sum[i] = e + carry;
+    carry += tot;
   }
-  if (threadIdx.x == 0) misc->n_active = carry.y;
+  if (threadIdx.x == 0 && total_out) *total_out = carry;
 }
 
-// pass 3: offsets, scatter cursors, active-source list
-__global__ __launch_bounds__(SCAN_BLOCK) void k_scan_apply(const int32_t* __restrict__ cnt, int64_t n,
-                                                           const int2* __restrict__ tile_sum,
-                                                           int32_t* __restrict__ off, int32_t* __restrict__ cursor,
-                                                           int32_t* __restrict__ active) {
-  __shared__ int2 lds[SCAN_BLOCK / 64 + 1];
-  int64_t base = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)threadIdx.x * SCAN_ITEMS;
+__global__ __launch_bounds__(SCAN_BLOCK) void k_scan_out(const int32_t* __restrict__ in, int64_t n,
+                                                         const int32_t* __restrict__ tile_sum, int32_t* __restrict__ out) {
+  __shared__ int red[SCAN_BLOCK / 64];
+  const int64_t base = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)threadIdx.x * SCAN_ITEMS;
   int c[SCAN_ITEMS];
-  int2 v = make_int2(0, 0);
+  int v = 0;
 #pragma unroll
   for (int k = 0; k < SCAN_ITEMS; ++k) {
-    int64_t i = base + k;
-    c[k] = i < n ? cnt[i] : 0;
-    v.x += c[k];
-    v.y += c[k] > 0;
+    c[k] = base + k < n ? in[base + k] : 0;
+    v += c[k];
   }
-  int2 tot;
-  int2 e = block_exscan2(v, lds, &tot);
-  int2 t = tile_sum[blockIdx.x];
-  int o = e.x + t.x, a = e.y + t.y;
+  int tot;
+  int o = block_exscan_i<SCAN_BLOCK>(v, red, &tot) + tile_sum[blockIdx.x];
 #pragma unroll
-  for (int k = 0; k < SCAN_ITEMS; ++k) {
-    int64_t i = base + k;
-    if (i < n) {
-      off[i] = o;
-      cursor[i] = o;
-      if (c[k] > 0) active[a++] = (int32_t)i;
+  for (int k = 0; k < SCAN_ITEMS; ++k)
+    if (base + k < n) {
+      out[base + k] = o;
       o += c[k];
     }
+}
+
+__global__ __launch_bounds__(GP_BLOCK) void k_bucket_hist(const int32_t* __restrict__ x, int64_t np, int32_t xlo,
+                                                          int shift, int nb, int nblk, int64_t per_blk,
+                                                          int32_t* __restrict__ hist) {
+  __shared__ int h[NB_MAX];
+  for (int i = threadIdx.x; i < nb; i += GP_BLOCK) h[i] = 0;
+  __syncthreads();
+  const int64_t b0 = (int64_t)blockIdx.x * per_blk, b1 = min(np, b0 + per_blk);
+  for (int64_t i = b0 + threadIdx.x; i < b1; i += GP_BLOCK) atomicAdd(&h[(x[i] - xlo) >> shift], 1);
+  __syncthreads();
+  for (int i = threadIdx.x; i < nb; i += GP_BLOCK) hist[(int64_t)i * nblk + blockIdx.x] = h[i];
+}
+
+__global__ __launch_bounds__(GP_BLOCK) void k_bucket_scatter(const int32_t* __restrict__ x, int64_t np, int32_t xlo,
+                                                             int shift, int nb, int nblk, int64_t per_blk,
+                                                             const int32_t* __restrict__ hoff, int32_t* __restrict__ tmp) {
+  __shared__ int cur[NB_MAX];
+  for (int i = threadIdx.x; i < nb; i += GP_BLOCK) cur[i] = hoff[(int64_t)i * nblk + blockIdx.x];
+  __syncthreads();
+  const int64_t b0 = (int64_t)blockIdx.x * per_blk, b1 = min(np, b0 + per_blk);
+  for (int64_t i = b0 + threadIdx.x; i < b1; i += GP_BLOCK) tmp[atomicAdd(&cur[(x[i] - xlo) >> shift], 1)] = (int32_t)i;
+}
+
+// One block per bucket of KEYS consecutive node ids.
+template <int KEYS>
+__global__ __launch_bounds__(GB_BLOCK) void k_bucket_group(const int32_t* __restrict__ x, const int32_t* __restrict__ y,
+                                                           const int64_t* __restrict__ rp, const int32_t* __restrict__ tmp,
+                                                           const int32_t* __restrict__ hoff, int nblk, int nb, int shift,
+                                                           int32_t xlo, int64_t xspan, int64_t np, int32_t* __restrict__ off,
+                                                           int32_t* __restrict__ cnt, int32_t* __restrict__ bucket_active,
+                                                           int32_t* __restrict__ g_out, int64_t* __restrict__ g_yb,
+                                                           int32_t* __restrict__ g_yl) {
+  constexpr int PER = KEYS / GB_BLOCK;
+  __shared__ int h[KEYS];
+  __shared__ int red[GB_BLOCK / 64];
+  const int b = blockIdx.x;
+  const int64_t k0 = (int64_t)xlo + ((int64_t)b << shift);
+  const int nk = (int)min<int64_t>((int64_t)1 << shift, xspan - ((int64_t)b << shift));
+  const int bs = hoff[(int64_t)b * nblk];
+  const int be = b + 1 < nb ? hoff[(int64_t)(b + 1) * nblk] : (int)np;
+  for (int i = threadIdx.x; i < KEYS; i += GB_BLOCK) h[i] = 0;
+  __syncthreads();
+  for (int k = bs + threadIdx.x; k < be; k += GB_BLOCK) atomicAdd(&h[x[tmp[k]] - k0], 1);
+  __syncthreads();
+  int v = 0, act = 0;
+  for (int q = 0; q < PER; ++q) {
+    const int c = h[threadIdx.x * PER + q];
+    v += c;
+    act += c > 0;
+  }
+  int tot;
+  int o = block_exscan_i<GB_BLOCK>(v, red, &tot);
+  int acts;
+  block_exscan_i<GB_BLOCK>(act, red, &acts);
+  for (int q = 0; q < PER; ++q) {
+    const int j = threadIdx.x * PER + q;
+    const int c = h[j];
+    if (j < nk) {
+      off[k0 + j] = bs + o;
+      cnt[k0 + j] = c;
+    }
+    h[j] = o;  // cursor
+    o += c;
+  }
+  if (threadIdx.x == 0) bucket_active[b] = acts;
+  __syncthreads();
+  for (int k = bs + threadIdx.x; k < be; k += GB_BLOCK) {
+    const int i = tmp[k];
+    const int pos = bs + atomicAdd(&h[x[i] - k0], 1);
+    const int yi = y[i];
+    const int64_t st = rp[yi];
+    g_out[pos] = i;
+    g_yb[pos] = st;
+    g_yl[pos] = (int32_t)(rp[yi + 1] - st);
   }
 }
 
-// Scatter into source order; one atomic per run of equal x. Also gathers N(y)'s row.
-__global__ void k_scatter(const int32_t* __restrict__ x, const int32_t* __restrict__ y, int64_t n_pairs,
-                          const int64_t* __restrict__ rp, int32_t* __restrict__ cursor, int32_t* __restrict__ g_out,
-                          int64_t* __restrict__ g_yb, int32_t* __restrict__ g_yl) {
-  const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c * RUN_CHUNK < n_pairs; c += nthr) {
-    const int64_t b = c * RUN_CHUNK, e = min(n_pairs, b + RUN_CHUNK);
-    int64_t i = b;
-    while (i < e) {
-      const int cur = x[i];
-      int64_t j = i + 1;
-      while (j < e && x[j] == cur) ++j;
-      int pos = atomicAdd(&cursor[cur], (int)(j - i));
-      for (int64_t k = i; k < j; ++k, ++pos) {
-        const int yk = y[k];
-        const int64_t s = rp[yk];
-        g_out[pos] = (int32_t)k;
-        g_yb[pos] = s;
-        g_yl[pos] = (int32_t)(rp[yk + 1] - s);
-      }
-      i = j;
-    }
+template <int KEYS>
+__global__ __launch_bounds__(GB_BLOCK) void k_active_write(const int32_t* __restrict__ cnt,
+                                                           const int32_t* __restrict__ abase, int shift, int32_t xlo,
+                                                           int64_t xspan, int32_t* __restrict__ active) {
+  constexpr int PER = KEYS / GB_BLOCK;
+  __shared__ int red[GB_BLOCK / 64];
+  const int b = blockIdx.x;
+  const int64_t k0 = (int64_t)xlo + ((int64_t)b << shift);
+  const int nk = (int)min<int64_t>((int64_t)1 << shift, xspan - ((int64_t)b << shift));
+  int v = 0;
+  for (int q = 0; q < PER; ++q) {
+    const int j = threadIdx.x * PER + q;
+    v += j < nk && cnt[k0 + j] > 0;
+  }
+  int tot;
+  int o = block_exscan_i<GB_BLOCK>(v, red, &tot) + abase[b];
+  for (int q = 0; q < PER; ++q) {
+    const int j = threadIdx.x * PER + q;
+    if (j < nk && cnt[k0 + j] > 0) active[o++] = (int32_t)(k0 + j);
   }
 }
 
@@ -229,84 +266,88 @@ __device__ inline int seg_search(const int32_t* off, int ns, int f) {
   return lo;
 }
 
-// Set the bits of every element of the ns segments (rows of ci) inside [c0, c0 + width).
-template <int BLOCK>
-__device__ inline void mp_build(const int32_t* __restrict__ ci, const int64_t* s_start, const int32_t* s_off, int ns,
-                                int64_t c0, int64_t width, uint32_t* bm) {
-  const int T = s_off[ns];
-  for (int base = 0; base < T; base += BLOCK * KPT) {
-    const int f0 = base + (int)threadIdx.x * KPT;
-    if (f0 >= T) continue;
-    int s = seg_search(s_off, ns, f0);
-    int next = s_off[s + 1];
-    int64_t pos = s_start[s] + (f0 - s_off[s]);
-    int w[KPT];
+// Fetch one merge-path step: the K consecutive elements [f0, f0 + K) of the concatenated
+// segments (w = node id or -1, sk = segment or -1). One LDS binary search per K elements.
+template <int K>
+__device__ inline void mp_fetch(const int32_t* __restrict__ ci, const int64_t* s_start, const int32_t* s_off, int ns,
+                                int T, int f0, int* w, int* sk) {
+  if (f0 >= T) {
 #pragma unroll
-    for (int k = 0; k < KPT; ++k) {
-      const int f = f0 + k;
-      w[k] = -1;
-      if (f < T) {
-        while (f >= next) {
-          ++s;
-          next = s_off[s + 1];
-          pos = s_start[s];
-        }
-        w[k] = ci[pos++];
+    for (int k = 0; k < K; ++k) w[k] = sk[k] = -1;
+    return;
+  }
+  int s = seg_search(s_off, ns, f0);
+  int next = s_off[s + 1];
+  int64_t pos = s_start[s] + (f0 - s_off[s]);
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int f = f0 + k;
+    w[k] = -1;
+    sk[k] = -1;
+    if (f < T) {
+      while (f >= next) {
+        ++s;
+        next = s_off[s + 1];
+        pos = s_start[s];
       }
-    }
-#pragma unroll
-    for (int k = 0; k < KPT; ++k) {
-      const int64_t r = (int64_t)w[k] - c0;
-      if (w[k] >= 0 && r >= 0 && r < width) atomicOr(&bm[r >> 5], 1u << (r & 31));
+      w[k] = ci[pos];
+      ++pos;
+      sk[k] = s;
     }
   }
 }
 
+// Set the bits of every element of the ns segments (rows of ci) inside [c0, c0 + width).
+// Software-pipelined: the loads of step i+1 are in flight while step i's atomics issue.
+template <int BLOCK, int K>
+__device__ inline void mp_build(const int32_t* __restrict__ ci, const int64_t* s_start, const int32_t* s_off, int ns,
+                                int64_t c0, int64_t width, uint32_t* bm) {
+  const int T = s_off[ns];
+  constexpr int STEP = BLOCK * K;
+  int w[K], sk[K];
+  mp_fetch<K>(ci, s_start, s_off, ns, T, (int)threadIdx.x * K, w, sk);
+  for (int base = 0; base < T; base += STEP) {
+    int wn[K], skn[K];
+    mp_fetch<K>(ci, s_start, s_off, ns, T, base + STEP + (int)threadIdx.x * K, wn, skn);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int64_t r = (int64_t)w[k] - c0;
+      if (w[k] >= 0 && r >= 0 && r < width) atomicOr(&bm[r >> 5], 1u << (r & 31));
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) w[k] = wn[k];
+  }
+}
+
 // Test every element of the ns segments against the bitmap; per-segment hit counts and
-// fixed-point Adamic-Adar sums accumulate into s_cn / s_aa (LDS).
-template <int BLOCK, bool AA>
+// fixed-point Adamic-Adar sums accumulate into s_cn / s_aa (LDS). Pipelined like mp_build.
+template <int BLOCK, int K, bool AA>
 __device__ inline void mp_scan(const int32_t* __restrict__ ci, const long long* __restrict__ aaw, const int64_t* s_start,
                                const int32_t* s_off, int ns, int64_t c0, int64_t width, const uint32_t* bm,
                                uint32_t* s_cn, unsigned long long* s_aa) {
   const int T = s_off[ns];
-  for (int base = 0; base < T; base += BLOCK * KPT) {
-    const int f0 = base + (int)threadIdx.x * KPT;
-    if (f0 >= T) continue;
-    int s = seg_search(s_off, ns, f0);
-    int next = s_off[s + 1];
-    int64_t pos = s_start[s] + (f0 - s_off[s]);
-    int w[KPT], sk[KPT];
+  constexpr int STEP = BLOCK * K;
+  int w[K], sk[K];
+  mp_fetch<K>(ci, s_start, s_off, ns, T, (int)threadIdx.x * K, w, sk);
+  for (int base = 0; base < T; base += STEP) {
+    int wn[K], skn[K];
+    mp_fetch<K>(ci, s_start, s_off, ns, T, base + STEP + (int)threadIdx.x * K, wn, skn);
+    bool hit[K];
 #pragma unroll
-    for (int k = 0; k < KPT; ++k) {
-      const int f = f0 + k;
-      w[k] = -1;
-      sk[k] = -1;
-      if (f < T) {
-        while (f >= next) {
-          ++s;
-          next = s_off[s + 1];
-          pos = s_start[s];
-        }
-        w[k] = ci[pos++];
-        sk[k] = s;
-      }
-    }
-    bool hit[KPT];
-#pragma unroll
-    for (int k = 0; k < KPT; ++k) {
+    for (int k = 0; k < K; ++k) {
       const int64_t r = (int64_t)w[k] - c0;
       hit[k] = w[k] >= 0 && r >= 0 && r < width && ((bm[r >> 5] >> (r & 31)) & 1u);
     }
-    long long wt[KPT];
+    long long wt[K];
     if (AA) {
 #pragma unroll
-      for (int k = 0; k < KPT; ++k) wt[k] = hit[k] ? aaw[w[k]] : 0ll;
+      for (int k = 0; k < K; ++k) wt[k] = hit[k] ? aaw[w[k]] : 0ll;
     }
     int cur = sk[0];
     unsigned c = 0;
     unsigned long long acc = 0;
 #pragma unroll
-    for (int k = 0; k < KPT; ++k) {
+    for (int k = 0; k < K; ++k) {
       if (sk[k] != cur) {
         if (c) {
           atomicAdd(&s_cn[cur], c);
@@ -324,6 +365,11 @@ __device__ inline void mp_scan(const int32_t* __restrict__ ci, const long long* 
     if (c && cur >= 0) {
       atomicAdd(&s_cn[cur], c);
       if (AA) atomicAdd(&s_aa[cur], acc);
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      w[k] = wn[k];
+      sk[k] = skn[k];
     }
   }
 }
@@ -364,6 +410,7 @@ struct HeavyArgs {
 
 template <int BLOCK, int CAP_WORDS, int SEG>
 __global__ __launch_bounds__(BLOCK) void k_heavy(HeavyArgs h) {
+  constexpr int K = 8;
   __shared__ uint32_t bm[CAP_WORDS];
   __shared__ int64_t s_start[SEG];
   __shared__ int32_t s_off[SEG + 1];
@@ -375,7 +422,7 @@ __global__ __launch_bounds__(BLOCK) void k_heavy(HeavyArgs h) {
   for (int64_t k0 = it.kb; k0 < it.ke; k0 += SEG) {
     const int ns = (int)min<int64_t>(SEG, it.ke - k0);
     load_row_segments<BLOCK>(h.rp, h.ci, k0, ns, s_start, s_off, red);
-    mp_build<BLOCK>(h.ci, s_start, s_off, ns, h.lo, h.width, bm);
+    mp_build<BLOCK, K>(h.ci, s_start, s_off, ns, h.lo, h.width, bm);
     __syncthreads();
   }
   uint32_t* dst = h.heavy_bm + (int64_t)it.slot * h.hb_words;
@@ -423,7 +470,7 @@ __device__ inline unsigned long long block_sum_u64(unsigned long long v, unsigne
   return t;
 }
 
-template <int BLOCK, int CAP_WORDS, int SEG>
+template <int BLOCK, int CAP_WORDS, int SEG, int K>
 __global__ __launch_bounds__(BLOCK) void k_score(ScoreArgs a) {
   constexpr int NW = BLOCK / 64;
   __shared__ uint32_t bm[CAP_WORDS];
@@ -477,7 +524,7 @@ __global__ __launch_bounds__(BLOCK) void k_score(ScoreArgs a) {
           for (int64_t k0 = xb; k0 < xe; k0 += SEG) {
             const int ns = (int)min<int64_t>(SEG, xe - k0);
             load_row_segments<BLOCK>(a.rp, a.ci, k0, ns, s_start, s_off, red);
-            mp_build<BLOCK>(a.ci, s_start, s_off, ns, c0, width, bm);
+            mp_build<BLOCK, K>(a.ci, s_start, s_off, ns, c0, width, bm);
             __syncthreads();
           }
         }
@@ -516,9 +563,9 @@ __global__ __launch_bounds__(BLOCK) void k_score(ScoreArgs a) {
           if (threadIdx.x == 0) s_off[ns] = tot;
           __syncthreads();
           if (want_a)
-            mp_scan<BLOCK, true>(a.ci, a.aaw, s_start, s_off, ns, c0, width, bm, s_cn, s_aa);
+            mp_scan<BLOCK, K, true>(a.ci, a.aaw, s_start, s_off, ns, c0, width, bm, s_cn, s_aa);
           else
-            mp_scan<BLOCK, false>(a.ci, a.aaw, s_start, s_off, ns, c0, width, bm, s_cn, s_aa);
+            mp_scan<BLOCK, K, false>(a.ci, a.aaw, s_start, s_off, ns, c0, width, bm, s_cn, s_aa);
           __syncthreads();
           for (int t = threadIdx.x; t < ns; t += BLOCK) {
             const int p = a.g_out[pbeg + sb + t];
@@ -579,6 +626,10 @@ struct blp_batch {
   int variant = V_SMALL;
   int chunks = 1;
   int dq = 1;
+  int shift = 10, nb = 1, nblk = 1;
+  int32_t xlo = 0;
+  int64_t xspan = 0;
+  int64_t per_blk = 1;
   int64_t cap_bits = 0;
   int64_t n_sources = 0;
   blp::KernelTimer t_score, t_group;
@@ -586,11 +637,28 @@ struct blp_batch {
 
 using namespace blp;
 
-template <int BLOCK, int CAP, int SEG>
-static int score_occupancy(int* per_cu) {
-  BLP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, k_score<BLOCK, CAP, SEG>, BLOCK, 0));
+// elements per thread per merge-path step (template; BLP_KPT=4|8|16 selects another build)
+static int kpt_choice() {
+  static int k = [] {
+    const char* e = getenv("BLP_KPT");
+    const int v = e ? atoi(e) : 8;
+    return (v == 4 || v == 16) ? v : 8;
+  }();
+  return k;
+}
+
+template <int BLOCK, int CAP, int SEG, int K>
+static int score_occ(int* per_cu) {
+  BLP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, k_score<BLOCK, CAP, SEG, K>, BLOCK, 0));
   *per_cu = std::max(*per_cu, 1);
   return BLP_OK;
+}
+
+template <int BLOCK, int CAP, int SEG>
+static int score_occupancy(int* per_cu) {
+  const int k = kpt_choice();
+  return k == 4 ? score_occ<BLOCK, CAP, SEG, 4>(per_cu) : k == 16 ? score_occ<BLOCK, CAP, SEG, 16>(per_cu)
+                                                                  : score_occ<BLOCK, CAP, SEG, 8>(per_cu);
 }
 
 static int variant_occupancy(int v, int* per_cu) {
@@ -601,7 +669,14 @@ static int variant_occupancy(int v, int* per_cu) {
 
 template <int BLOCK, int CAP, int SEG>
 static int launch_score(blp_graph* g, const ScoreArgs& a, int per_cu) {
-  hipLaunchKernelGGL((k_score<BLOCK, CAP, SEG>), dim3(g->n_cu * per_cu), dim3(BLOCK), 0, g->stream, a);
+  const dim3 grid(g->n_cu * per_cu), block(BLOCK);
+  const int k = kpt_choice();
+  if (k == 4)
+    hipLaunchKernelGGL((k_score<BLOCK, CAP, SEG, 4>), grid, block, 0, g->stream, a);
+  else if (k == 16)
+    hipLaunchKernelGGL((k_score<BLOCK, CAP, SEG, 16>), grid, block, 0, g->stream, a);
+  else
+    hipLaunchKernelGGL((k_score<BLOCK, CAP, SEG, 8>), grid, block, 0, g->stream, a);
   BLP_HIP(hipGetLastError());
   return BLP_OK;
 }
@@ -706,6 +781,24 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   }
   b->n_heavy_items = (int64_t)items.size();
   b->hb_words = ((span + 31) / 32 + 3) / 4 * 4;
+  // ---- grouping geometry: buckets of 2^shift node ids, at most NB_MAX buckets
+  {
+    // buckets cover the sources' id range [xlo, xhi): ~2K buckets of 2^shift ids each
+    int32_t xlo = INT32_MAX, xhi = 0;
+    for (int32_t v : srcs) {
+      xlo = std::min(xlo, v);
+      xhi = std::max(xhi, v + 1);
+    }
+    if (srcs.empty()) xlo = xhi = 0;
+    b->xlo = xlo;
+    b->xspan = (int64_t)xhi - xlo;
+    b->shift = 0;
+    while ((b->xspan >> b->shift) > 2048) ++b->shift;
+    b->nb = (int)std::max<int64_t>(1, (b->xspan + (int64_t(1) << b->shift) - 1) >> b->shift);
+    if (b->shift > 15 || b->nb > NB_MAX) return bail(fail(BLP_E_UNSUP, "blp_batch_create: source id range too wide"));
+    b->nblk = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)g->n_cu * 2, (n_pairs + 4095) / 4096));
+    b->per_blk = (n_pairs + b->nblk - 1) / b->nblk;
+  }
   // ---- device buffers
   const size_t np = (size_t)std::max<int64_t>(n_pairs, 1);
   if (hipMalloc(&b->d_x, 4 * np) != hipSuccess || hipMalloc(&b->d_y, 4 * np) != hipSuccess ||
@@ -765,31 +858,64 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   int rc = set_device(g);
   if (rc) return rc;
   const int64_t n = g->n, np = b->n_pairs;
-  const int64_t ntiles = (n + SCAN_TILE - 1) / SCAN_TILE;
+  const int64_t nh = (int64_t)b->nb * b->nblk;
+  const int64_t tiles_h = (nh + SCAN_TILE - 1) / SCAN_TILE, tiles_b = (b->nb + SCAN_TILE - 1) / SCAN_TILE;
   if ((rc = g->cnt.reserve(4 * (n + 1)))) return rc;
   if ((rc = g->off.reserve(4 * (n + 1)))) return rc;
-  if ((rc = g->cursor.reserve(4 * (n + 1)))) return rc;
   if ((rc = g->active.reserve(4 * (n + 1)))) return rc;
-  if ((rc = g->scratch.reserve(sizeof(int2) * (ntiles + 1)))) return rc;
+  // scratch: hist | hoff | tiles | bucket_active | abase | tmp
+  const int64_t sc_ints = 2 * nh + std::max(tiles_h, tiles_b) + 1 + 2 * (int64_t)b->nb + np;
+  if ((rc = g->scratch.reserve(4 * (sc_ints + 16)))) return rc;
+  int32_t* hist = g->scratch.as<int32_t>();
+  int32_t* hoff = hist + nh;
+  int32_t* tiles = hoff + nh;
+  int32_t* bact = tiles + std::max(tiles_h, tiles_b) + 1;
+  int32_t* abase = bact + b->nb;
+  int32_t* tmp = abase + b->nb;
   hipEvent_t t0, bt0;
   if ((rc = timer_begin(g, K_GROUP, &t0))) return rc;
   if ((rc = timer_begin(b->t_group, g->stream, &bt0))) return rc;
-  BLP_HIP(hipMemsetAsync(g->cnt.p, 0, 4 * (n + 1), g->stream));
   BLP_HIP(hipMemsetAsync(b->d_misc, 0, sizeof(Misc), g->stream));
-  const int64_t nchunk = (np + RUN_CHUNK - 1) / RUN_CHUNK;
-  const int ew_grid = (int)std::min<int64_t>(std::max<int64_t>((nchunk + 255) / 256, 1), (int64_t)g->n_cu * 16);
-  if (np) hipLaunchKernelGGL(k_count, dim3(ew_grid), dim3(256), 0, g->stream, b->d_x, np, g->cnt.as<int32_t>());
-  if (ntiles) {
-    hipLaunchKernelGGL(k_scan_tiles, dim3((unsigned)ntiles), dim3(SCAN_BLOCK), 0, g->stream, g->cnt.as<int32_t>(), n,
-                       g->scratch.as<int2>());
-    hipLaunchKernelGGL(k_scan_tilesums, dim3(1), dim3(SCAN_BLOCK), 0, g->stream, g->scratch.as<int2>(), ntiles,
-                       b->d_misc);
-    hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)ntiles), dim3(SCAN_BLOCK), 0, g->stream, g->cnt.as<int32_t>(), n,
-                       g->scratch.as<int2>(), g->off.as<int32_t>(), g->cursor.as<int32_t>(), g->active.as<int32_t>());
+  if (np) {
+    hipLaunchKernelGGL(k_bucket_hist, dim3(b->nblk), dim3(GP_BLOCK), 0, g->stream, b->d_x, np, b->xlo, b->shift, b->nb,
+                       b->nblk, b->per_blk, hist);
+    hipLaunchKernelGGL(k_scan_sum, dim3((unsigned)tiles_h), dim3(SCAN_BLOCK), 0, g->stream, hist, nh, tiles);
+    hipLaunchKernelGGL(k_scan_mid, dim3(1), dim3(SCAN_BLOCK), 0, g->stream, tiles, tiles_h, (int32_t*)nullptr);
+    hipLaunchKernelGGL(k_scan_out, dim3((unsigned)tiles_h), dim3(SCAN_BLOCK), 0, g->stream, hist, nh, tiles, hoff);
+    hipLaunchKernelGGL(k_bucket_scatter, dim3(b->nblk), dim3(GP_BLOCK), 0, g->stream, b->d_x, np, b->xlo, b->shift,
+                       b->nb, b->nblk, b->per_blk, hoff, tmp);
+    const int keys = 1 << b->shift;
+#define BLP_GROUP_LAUNCH(K)                                                                                         \
+  hipLaunchKernelGGL(k_bucket_group<K>, dim3(b->nb), dim3(GB_BLOCK), 0, g->stream, b->d_x, b->d_y, g->d_rp, tmp, hoff, \
+                     b->nblk, b->nb, b->shift, b->xlo, b->xspan, np, g->off.as<int32_t>(), g->cnt.as<int32_t>(), bact,  \
+                     b->d_gout,                                                                                       \
+                     b->d_gyb, b->d_gyl)
+    if (keys <= 256)
+      BLP_GROUP_LAUNCH(256);
+    else if (keys <= 1024)
+      BLP_GROUP_LAUNCH(1024);
+    else if (keys <= 4096)
+      BLP_GROUP_LAUNCH(4096);
+    else
+      BLP_GROUP_LAUNCH(32768);
+#undef BLP_GROUP_LAUNCH
+    hipLaunchKernelGGL(k_scan_sum, dim3((unsigned)tiles_b), dim3(SCAN_BLOCK), 0, g->stream, bact, (int64_t)b->nb, tiles);
+    hipLaunchKernelGGL(k_scan_mid, dim3(1), dim3(SCAN_BLOCK), 0, g->stream, tiles, tiles_b, &b->d_misc->n_active);
+    hipLaunchKernelGGL(k_scan_out, dim3((unsigned)tiles_b), dim3(SCAN_BLOCK), 0, g->stream, bact, (int64_t)b->nb, tiles,
+                       abase);
+#define BLP_ACTIVE_LAUNCH(K)                                                                                   \
+  hipLaunchKernelGGL(k_active_write<K>, dim3(b->nb), dim3(GB_BLOCK), 0, g->stream, g->cnt.as<int32_t>(), abase, b->shift, \
+                     b->xlo, b->xspan, g->active.as<int32_t>())
+    if (keys <= 256)
+      BLP_ACTIVE_LAUNCH(256);
+    else if (keys <= 1024)
+      BLP_ACTIVE_LAUNCH(1024);
+    else if (keys <= 4096)
+      BLP_ACTIVE_LAUNCH(4096);
+    else
+      BLP_ACTIVE_LAUNCH(32768);
+#undef BLP_ACTIVE_LAUNCH
   }
-  if (np)
-    hipLaunchKernelGGL(k_scatter, dim3(ew_grid), dim3(256), 0, g->stream, b->d_x, b->d_y, np, g->d_rp,
-                       g->cursor.as<int32_t>(), b->d_gout, b->d_gyb, b->d_gyl);
   BLP_HIP(hipGetLastError());
   if ((rc = timer_end(b->t_group, g->stream, bt0))) return rc;
   if ((rc = timer_end(g, K_GROUP, t0))) return rc;
