@@ -134,6 +134,14 @@ def cpu_baseline(G, ex_x, ex_y, target_s=15.0):
                       (pu, su, tu, ru, pb, sb, tb, rb)}
 
 
+def _build_elems(G, x):
+    """sum over distinct sources x of sum_{z in N(x)} |N(z)|: elements read to build the H2 bitmaps."""
+    d = G.hop1_size.astype(np.int64)
+    src = np.unique(x)
+    csum = np.concatenate([[0], np.cumsum(d[G.col_idx])])
+    return int((csum[G.row_ptr[src + 1]] - csum[G.row_ptr[src]]).sum())
+
+
 def _dense_edges(G):
     """Edge list (dense ids, each undirected edge once, self-loops restored) from the CSR."""
     rows = np.repeat(np.arange(G.n, dtype=np.int32), np.diff(G.row_ptr))
@@ -173,6 +181,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--user-mask", type=int, default=7, help="methods of the user pass (1 CN, 2 J, 4 AA)")
     args = ap.parse_args()
 
     dist = Dist()
@@ -191,7 +200,7 @@ def main():
 
     passes = []
     if args.sides in ("both", "user"):
-        passes.append(("user", G.batch(ex_x, ex_y), blp.CN | blp.JACCARD | blp.ADAMIC))
+        passes.append(("user", G.batch(ex_x, ex_y), args.user_mask))
     if args.sides in ("both", "business"):
         passes.append(("business", G.batch(ex_y, ex_x), blp.CN | blp.JACCARD))
     for name, bt, _ in passes:
@@ -248,6 +257,9 @@ def main():
             "parallelism": "replicas x%d (graph replicated, users split, no collective)" % dist.world,
         },
         "kernels_ms": ktimes,
+        "work": {name: {"build_elems": _build_elems(G, xs_), "scan_elems": int(G.hop1_size[ys_].astype(np.int64).sum()),
+                        "hits": int(res[name]["cn"].astype(np.int64).sum()), "sources": int(len(np.unique(xs_)))}
+                 for name, xs_, ys_ in [("user", ex_x, ex_y), ("business", ex_y, ex_x)] if name in res},
     }
     # roofline of the dominant kernel: the user-side scorer (falls back to the first pass)
     name0, bt0, mask0 = passes[0]

@@ -22,6 +22,12 @@ int hip_fail(hipError_t e, const char* what, const char* file, int line);
     if (_e != hipSuccess) return ::blp::hip_fail(_e, #call, __FILE__, __LINE__); \
   } while (0)
 
+#define BLP_HIP_OR(call, handler)                                              \
+  do {                                                                          \
+    hipError_t _e = (call);                                                     \
+    if (_e != hipSuccess) return handler(::blp::hip_fail(_e, #call, __FILE__, __LINE__)); \
+  } while (0)
+
 #define BLP_CHECK(cond, code, msg)       \
   do {                                   \
     if (!(cond)) return ::blp::fail((code), (msg)); \
@@ -61,6 +67,12 @@ struct blp_graph {
   int64_t* d_rp = nullptr;   // [n+1]
   int32_t* d_ci = nullptr;   // [nnz]
   long long* d_aaw_fx = nullptr;  // [n] Adamic-Adar weight per node, fixed point 2^-40 (or null)
+  // dense-row index: rows dense enough in their id range also stored as bitmaps (hot.hip)
+  int32_t* d_hot_idx = nullptr;  // [n] hot row number or -1
+  void* d_hot_tab = nullptr;     // [n_hot] blp::HotRow
+  uint32_t* d_hot_pool = nullptr;
+  int64_t n_hot = 0, hot_pool_words = 0;
+  std::vector<int32_t> h_hot_idx;
   // host mirrors used only for launch planning (bitmap universe bounds)
   std::vector<int64_t> h_rp;
   std::vector<int32_t> h_ci;
@@ -70,6 +82,14 @@ struct blp_graph {
 };
 
 namespace blp {
+// One dense row: bits [128 * vlo, 128 * (vlo + nvec)) of N(v) at pool words [4*vec_off, ...).
+struct HotRow {
+  int64_t vec_off;
+  int32_t vlo;
+  int32_t nvec;
+};
+int build_hot_index(blp_graph* g);
+void free_hot_index(blp_graph* g);
 int timer_begin(blp_graph* g, int k, hipEvent_t* start);
 int timer_end(blp_graph* g, int k, hipEvent_t start);
 int timers_collect(blp_graph* g);

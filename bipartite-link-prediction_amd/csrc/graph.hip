@@ -222,6 +222,7 @@ int blp_graph_create(const int64_t* row_ptr, const int32_t* col_idx, int64_t n, 
     return cleanup(rc);
   g->h_rp.assign(row_ptr, row_ptr + n + 1);
   g->h_ci.assign(col_idx, col_idx + nnz);
+  if ((rc = build_hot_index(g)) != BLP_OK) return cleanup(rc);
   *out = g;
   return BLP_OK;
 }
@@ -236,6 +237,7 @@ int blp_graph_destroy(blp_graph* g) {
   g->cursor.release();
   g->active.release();
   g->scratch.release();
+  free_hot_index(g);
   if (g->d_rp) (void)hipFree(g->d_rp);
   if (g->d_ci) (void)hipFree(g->d_ci);
   if (g->d_aaw_fx) (void)hipFree(g->d_aaw_fx);

@@ -51,6 +51,7 @@ struct Misc {
 //                       off/cnt, grouped pair metadata (caller index, N(y) start and length)
 //   5. scan_ex          of the per-bucket active-source counts
 //   6. k_active_write   the active-source list in ascending id order
+constexpr int HOT_LIST = 64;    // dense rows OR-ed per source (more: all rows go sparse)
 constexpr int GP_BLOCK = 1024;  // passes 1 and 3
 constexpr int GB_BLOCK = 256;   // passes 4 and 6
 constexpr int NB_MAX = 4096;    // buckets
@@ -299,16 +300,16 @@ __device__ inline void mp_fetch(const int32_t* __restrict__ ci, const int64_t* s
 
 // Set the bits of every element of the ns segments (rows of ci) inside [c0, c0 + width).
 // Software-pipelined: the loads of step i+1 are in flight while step i's atomics issue.
-template <int BLOCK, int K>
+template <int NT, int K>
 __device__ inline void mp_build(const int32_t* __restrict__ ci, const int64_t* s_start, const int32_t* s_off, int ns,
-                                int64_t c0, int64_t width, uint32_t* bm) {
+                                int64_t c0, int64_t width, uint32_t* bm, int tid) {
   const int T = s_off[ns];
-  constexpr int STEP = BLOCK * K;
+  constexpr int STEP = NT * K;
   int w[K], sk[K];
-  mp_fetch<K>(ci, s_start, s_off, ns, T, (int)threadIdx.x * K, w, sk);
+  mp_fetch<K>(ci, s_start, s_off, ns, T, tid * K, w, sk);
   for (int base = 0; base < T; base += STEP) {
     int wn[K], skn[K];
-    mp_fetch<K>(ci, s_start, s_off, ns, T, base + STEP + (int)threadIdx.x * K, wn, skn);
+    mp_fetch<K>(ci, s_start, s_off, ns, T, base + STEP + tid * K, wn, skn);
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       const int64_t r = (int64_t)w[k] - c0;
@@ -321,17 +322,17 @@ __device__ inline void mp_build(const int32_t* __restrict__ ci, const int64_t* s
 
 // Test every element of the ns segments against the bitmap; per-segment hit counts and
 // fixed-point Adamic-Adar sums accumulate into s_cn / s_aa (LDS). Pipelined like mp_build.
-template <int BLOCK, int K, bool AA>
+template <int NT, int K, bool AA>
 __device__ inline void mp_scan(const int32_t* __restrict__ ci, const long long* __restrict__ aaw, const int64_t* s_start,
                                const int32_t* s_off, int ns, int64_t c0, int64_t width, const uint32_t* bm,
-                               uint32_t* s_cn, unsigned long long* s_aa) {
+                               uint32_t* s_cn, unsigned long long* s_aa, int tid) {
   const int T = s_off[ns];
-  constexpr int STEP = BLOCK * K;
+  constexpr int STEP = NT * K;
   int w[K], sk[K];
-  mp_fetch<K>(ci, s_start, s_off, ns, T, (int)threadIdx.x * K, w, sk);
+  mp_fetch<K>(ci, s_start, s_off, ns, T, tid * K, w, sk);
   for (int base = 0; base < T; base += STEP) {
     int wn[K], skn[K];
-    mp_fetch<K>(ci, s_start, s_off, ns, T, base + STEP + (int)threadIdx.x * K, wn, skn);
+    mp_fetch<K>(ci, s_start, s_off, ns, T, base + STEP + tid * K, wn, skn);
     bool hit[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -377,13 +378,14 @@ __device__ inline void mp_scan(const int32_t* __restrict__ ci, const long long* 
 // Load the rows of N(x)[k0, k0 + ns) as segments: start / exclusive offsets (s_off[ns] = total).
 template <int BLOCK>
 __device__ inline void load_row_segments(const int64_t* __restrict__ rp, const int32_t* __restrict__ ci, int64_t k0,
-                                         int ns, int64_t* s_start, int32_t* s_off, int* red) {
+                                         int ns, int64_t* s_start, int32_t* s_off, int* red,
+                                         const int32_t* __restrict__ skip = nullptr) {
   int len = 0;
   if ((int)threadIdx.x < ns) {
     const int z = ci[k0 + threadIdx.x];
     const int64_t st = rp[z];
     s_start[threadIdx.x] = st;
-    len = (int)(rp[z + 1] - st);
+    len = (skip && skip[z] >= 0) ? 0 : (int)(rp[z + 1] - st);  // dense rows were OR-ed in already
   }
   int tot;
   const int ex = block_exscan<BLOCK>(len, red, &tot);
@@ -422,7 +424,7 @@ __global__ __launch_bounds__(BLOCK) void k_heavy(HeavyArgs h) {
   for (int64_t k0 = it.kb; k0 < it.ke; k0 += SEG) {
     const int ns = (int)min<int64_t>(SEG, it.ke - k0);
     load_row_segments<BLOCK>(h.rp, h.ci, k0, ns, s_start, s_off, red);
-    mp_build<BLOCK, K>(h.ci, s_start, s_off, ns, h.lo, h.width, bm);
+    mp_build<BLOCK, K>(h.ci, s_start, s_off, ns, h.lo, h.width, bm, threadIdx.x);
     __syncthreads();
   }
   uint32_t* dst = h.heavy_bm + (int64_t)it.slot * h.hb_words;
@@ -443,6 +445,9 @@ struct ScoreArgs {
   const int32_t* g_out;    // grouped position -> caller index
   const int64_t* g_yb;     // grouped position -> start of N(y) in ci
   const int32_t* g_yl;     // grouped position -> |N(y)|
+  const int32_t* hot_idx;     // per node: dense-row number or -1 (null: no dense rows)
+  const blp::HotRow* hot_tab;
+  const uint4* hot_pool;
   const int32_t* heavy_slot;  // per node: pre-built bitmap slot or -1 (null: none)
   const uint32_t* heavy_bm;
   int64_t hb_words;
@@ -481,6 +486,8 @@ __global__ __launch_bounds__(BLOCK) void k_score(ScoreArgs a) {
   __shared__ unsigned long long red64[NW];
   __shared__ int red[NW];
   __shared__ int s_src;
+  __shared__ int s_nhot;
+  __shared__ blp::HotRow s_hot[HOT_LIST];
 
   const int64_t CAP_BITS = a.cap_bits;
   const int64_t span = a.hi - a.lo;
@@ -518,13 +525,41 @@ __global__ __launch_bounds__(BLOCK) void k_score(ScoreArgs a) {
           for (int i = threadIdx.x; i < nw4; i += BLOCK) bm4[i] = src4[i];
           __syncthreads();
         } else {
-          // 1. clear, 2. mark N(N(x)) ∩ [c0, c1) through merge-path row segments
-          for (int i = threadIdx.x; i < nw4; i += BLOCK) bm4[i] = make_uint4(0, 0, 0, 0);
+          // 1. the dense rows of N(x) initialise the bitmap (their OR, 16-byte vectors), then
+          // 2. the sparse rows mark N(N(x)) ∩ [c0, c1) through merge-path row segments
+          if (threadIdx.x == 0) s_nhot = 0;
+          __syncthreads();
+          if (a.hot_idx) {
+            for (int64_t k = xb + threadIdx.x; k < xe; k += BLOCK) {
+              const int hi = a.hot_idx[a.ci[k]];
+              if (hi >= 0) {
+                const int slot = atomicAdd(&s_nhot, 1);
+                if (slot < HOT_LIST) s_hot[slot] = a.hot_tab[hi];
+              }
+            }
+          }
+          __syncthreads();
+          const int nhot = s_nhot <= HOT_LIST ? s_nhot : 0;  // overflow: every row goes sparse
+          const int64_t q0 = c0 >> 7;
+          for (int q = threadIdx.x; q < nw4; q += BLOCK) {
+            uint4 v = make_uint4(0, 0, 0, 0);
+            for (int r = 0; r < nhot; ++r) {
+              const int64_t qq = q0 + q - s_hot[r].vlo;
+              if (qq >= 0 && qq < s_hot[r].nvec) {
+                const uint4 p = a.hot_pool[s_hot[r].vec_off + qq];
+                v.x |= p.x;
+                v.y |= p.y;
+                v.z |= p.z;
+                v.w |= p.w;
+              }
+            }
+            bm4[q] = v;
+          }
           __syncthreads();
           for (int64_t k0 = xb; k0 < xe; k0 += SEG) {
             const int ns = (int)min<int64_t>(SEG, xe - k0);
-            load_row_segments<BLOCK>(a.rp, a.ci, k0, ns, s_start, s_off, red);
-            mp_build<BLOCK, K>(a.ci, s_start, s_off, ns, c0, width, bm);
+            load_row_segments<BLOCK>(a.rp, a.ci, k0, ns, s_start, s_off, red, nhot ? a.hot_idx : nullptr);
+            mp_build<BLOCK, K>(a.ci, s_start, s_off, ns, c0, width, bm, threadIdx.x);
             __syncthreads();
           }
         }
@@ -563,9 +598,9 @@ __global__ __launch_bounds__(BLOCK) void k_score(ScoreArgs a) {
           if (threadIdx.x == 0) s_off[ns] = tot;
           __syncthreads();
           if (want_a)
-            mp_scan<BLOCK, K, true>(a.ci, a.aaw, s_start, s_off, ns, c0, width, bm, s_cn, s_aa);
+            mp_scan<BLOCK, K, true>(a.ci, a.aaw, s_start, s_off, ns, c0, width, bm, s_cn, s_aa, threadIdx.x);
           else
-            mp_scan<BLOCK, K, false>(a.ci, a.aaw, s_start, s_off, ns, c0, width, bm, s_cn, s_aa);
+            mp_scan<BLOCK, K, false>(a.ci, a.aaw, s_start, s_off, ns, c0, width, bm, s_cn, s_aa, threadIdx.x);
           __syncthreads();
           for (int t = threadIdx.x; t < ns; t += BLOCK) {
             const int p = a.g_out[pbeg + sb + t];
@@ -593,6 +628,154 @@ __global__ __launch_bounds__(BLOCK) void k_score(ScoreArgs a) {
     }
   }
 }
+
+// ------------------------------------------------------------------ wave-per-source scorer
+// For small node universes (the business side of a review graph: H2(v) ⊂ businesses) the
+// per-source work is ~2K elements, so a workgroup-wide pass is all barrier and latency.
+// Here every wave owns a bitmap slice and a segment area in LDS and runs its sources alone:
+// no block barriers, ~10 sources in flight per CU, same merge-path loops with 64 threads.
+constexpr int WSEG = 64;  // segments per wave chunk: one per lane
+
+__device__ inline void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+__device__ inline int wave_exscan(int v, int lane, int* total) {
+  int inc = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int t = __shfl_up(inc, d, 64);
+    if (lane >= d) inc += t;
+  }
+  *total = __shfl(inc, 63, 64);
+  return inc - v;
+}
+
+template <typename T>
+__device__ inline T wave_sum(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <int WAVES, int WCAP, int K>
+__global__ __launch_bounds__(WAVES * 64) void k_score_wave(ScoreArgs a) {
+  __shared__ uint32_t bm_all[WAVES][WCAP];
+  __shared__ int64_t st_all[WAVES][WSEG];
+  __shared__ int32_t of_all[WAVES][WSEG + 1];
+  __shared__ uint32_t cn_all[WAVES][WSEG];
+  __shared__ unsigned long long aa_all[WAVES][WSEG];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint32_t* bm = bm_all[wid];
+  uint4* bm4 = reinterpret_cast<uint4*>(bm);
+  int64_t* s_start = st_all[wid];
+  int32_t* s_off = of_all[wid];
+  uint32_t* s_cn = cn_all[wid];
+  unsigned long long* s_aa = aa_all[wid];
+  const int64_t c0 = a.lo;
+  const int64_t width = a.hi - a.lo;  // <= WCAP * 32 (checked by the host)
+  const int nw4 = (int)((((width + 31) >> 5) + 3) >> 2);
+  const bool want_j = (a.mask & BLP_JACCARD) != 0;
+  const bool want_a = (a.mask & BLP_ADAMIC) != 0;
+  const int n_active = a.misc->n_active;
+  for (;;) {
+    int first = 0;
+    if (lane == 0) first = atomicAdd(&a.misc->queue, a.dq);
+    first = __shfl(first, 0, 64);
+    if (first >= n_active) break;
+    const int last_s = min(n_active, first + a.dq);
+    for (int s = first; s < last_s; ++s) {
+      const int x = a.active[s];
+      const int pbeg = a.off[x], pcnt = a.cnt[x];
+      const int64_t xb = a.rp[x], xe = a.rp[x + 1];
+      const int hslot = a.heavy_slot ? a.heavy_slot[x] : -1;
+      if (hslot >= 0) {
+        const uint4* src4 = reinterpret_cast<const uint4*>(a.heavy_bm + (int64_t)hslot * a.hb_words);
+        for (int i = lane; i < nw4; i += 64) bm4[i] = src4[i];
+        wave_sync();
+      } else {
+        for (int i = lane; i < nw4; i += 64) bm4[i] = make_uint4(0, 0, 0, 0);
+        wave_sync();
+        for (int64_t k0 = xb; k0 < xe; k0 += WSEG) {
+          const int ns = (int)min<int64_t>(WSEG, xe - k0);
+          int len = 0;
+          if (lane < ns) {
+            const int z = a.ci[k0 + lane];
+            const int64_t st = a.rp[z];
+            s_start[lane] = st;
+            len = (int)(a.rp[z + 1] - st);
+          }
+          int tot;
+          const int ex = wave_exscan(len, lane, &tot);
+          if (lane < ns) s_off[lane] = ex;
+          if (lane == 0) s_off[ns] = tot;
+          wave_sync();
+          mp_build<64, K>(a.ci, s_start, s_off, ns, c0, width, bm, lane);
+          wave_sync();
+        }
+      }
+      // exact distance 2: drop x and N(x) where they fall inside the universe
+      const int64_t nx_lo = xe > xb ? a.ci[xb] : 0, nx_hi = xe > xb ? a.ci[xe - 1] : -1;
+      if (nx_hi >= c0 && nx_lo < c0 + width) {
+        for (int64_t k = xb + lane; k < xe; k += 64) {
+          const int64_t r = (int64_t)a.ci[k] - c0;
+          if (r >= 0 && r < width) atomicAnd(&bm[r >> 5], ~(1u << (r & 31)));
+        }
+      }
+      if (lane == 0 && x >= c0 && x < c0 + width) atomicAnd(&bm[(x - c0) >> 5], ~(1u << ((x - c0) & 31)));
+      wave_sync();
+      unsigned long long h2 = 0;
+      if (want_j) {
+        unsigned long long pc = 0;
+        for (int i = lane; i < nw4; i += 64) {
+          const uint4 q = bm4[i];
+          pc += __popc(q.x) + __popc(q.y) + __popc(q.z) + __popc(q.w);
+        }
+        h2 = wave_sum(pc);
+      }
+      for (int sb = 0; sb < pcnt; sb += WSEG) {
+        const int ns = min(WSEG, pcnt - sb);
+        int len = 0;
+        if (lane < ns) {
+          const int gp = pbeg + sb + lane;
+          s_start[lane] = a.g_yb[gp];
+          len = a.g_yl[gp];
+          s_cn[lane] = 0;
+          s_aa[lane] = 0;
+        }
+        int tot;
+        const int ex = wave_exscan(len, lane, &tot);
+        if (lane < ns) s_off[lane] = ex;
+        if (lane == 0) s_off[ns] = tot;
+        wave_sync();
+        if (want_a)
+          mp_scan<64, K, true>(a.ci, a.aaw, s_start, s_off, ns, c0, width, bm, s_cn, s_aa, lane);
+        else
+          mp_scan<64, K, false>(a.ci, a.aaw, s_start, s_off, ns, c0, width, bm, s_cn, s_aa, lane);
+        wave_sync();
+        if (lane < ns) {
+          const int p = a.g_out[pbeg + sb + lane];
+          const unsigned c = s_cn[lane];
+          a.cn[p] = c;
+          if (want_a) a.aa[p] = (double)s_aa[lane] * (1.0 / blp::AA_SCALE);
+          if (want_j) {
+            const long long uni = (long long)h2 + len - (long long)c;
+            if (uni <= 0) {
+              a.jac[p] = __builtin_nan("");
+              atomicOr(&a.misc->zero_div, 1);
+            } else {
+              a.jac[p] = (double)c / (double)uni;
+            }
+          }
+        }
+        wave_sync();
+      }
+    }
+  }
+}
+
+constexpr int W_WAVES = 2, W_CAP = 3328;  // 13 KiB of bitmap per wave (106,496 node ids)
 
 enum Variant { V_SMALL = 0, V_MED = 1, V_LARGE = 2 };
 // LDS bitmap words (16 / 64 / 136 KiB), threads per block, pair/row segments per chunk
@@ -626,6 +809,8 @@ struct blp_batch {
   int variant = V_SMALL;
   int chunks = 1;
   int dq = 1;
+  bool use_hot = false;  // some source has a dense row in N(x)
+  bool wave = false;     // wave-per-source scorer
   int shift = 10, nb = 1, nblk = 1;
   int32_t xlo = 0;
   int64_t xspan = 0;
@@ -702,6 +887,8 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   std::vector<int32_t> srcs;
   std::vector<int64_t> work;
   int64_t scan_work = 0;
+  bool any_hot = false;
+  const int32_t* hot = g->h_hot_idx.empty() ? nullptr : g->h_hot_idx.data();
   for (int64_t i = 0; i < n_pairs; ++i) {
     const int32_t xi = x[i], yi = y[i];
     if (xi < 0 || xi >= n || yi < 0 || yi >= n) return fail(BLP_E_ARG, "blp_batch_create: node id out of range");
@@ -717,6 +904,7 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
       for (int64_t k = rp[xi]; k < rp[xi + 1]; ++k) {
         const int32_t z = ci[k];
         wsum += rp[z + 1] - rp[z];
+        any_hot |= hot && hot[z] >= 0;
         if (rp[z + 1] > rp[z]) {
           lo = std::min<int64_t>(lo, ci[rp[z]]);
           hi = std::max<int64_t>(hi, (int64_t)ci[rp[z + 1] - 1] + 1);
@@ -726,12 +914,14 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
     }
   }
   if (lo > hi) lo = hi = 0;
+  lo &= ~int64_t(127);  // 128-bit aligned so dense rows map onto whole 16-byte LDS vectors
   blp_batch* b = new blp_batch();
   b->g = g;
   b->n_pairs = n_pairs;
   b->lo = lo;
   b->hi = hi;
   b->n_sources = (int64_t)srcs.size();
+  b->use_hot = any_hot;
   const int64_t span = hi - lo;
   if (span <= variant_cap_bits(V_SMALL))
     b->variant = V_SMALL;
@@ -751,8 +941,15 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   };
   int rc = set_device(g);
   if (rc) return bail(rc);
+  b->wave = span <= (int64_t)W_CAP * 32 && b->chunks == 1 && !getenv("BLP_NO_WAVE");
   int per_cu = 1;
-  if ((rc = variant_occupancy(b->variant, &per_cu))) return bail(rc);
+  if (b->wave) {
+    BLP_HIP_OR(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_score_wave<W_WAVES, W_CAP, 8>, W_WAVES * 64, 0),
+               bail);
+    per_cu = std::max(per_cu, 1) * W_WAVES;  // workers are waves
+  } else if ((rc = variant_occupancy(b->variant, &per_cu))) {
+    return bail(rc);
+  }
   const int64_t n_wg = (int64_t)g->n_cu * per_cu;
   b->dq = (int)std::max<int64_t>(1, std::min<int64_t>(8, b->n_sources / (n_wg * 16)));
   // ---- heavy sources: build work far above the per-workgroup share goes to k_heavy
@@ -845,7 +1042,7 @@ int blp_batch_plan(const blp_batch* b, int64_t* lo, int64_t* hi, int* chunks, in
   if (lo) *lo = b->lo;
   if (hi) *hi = b->hi;
   if (chunks) *chunks = b->chunks;
-  if (block) *block = variant_block(b->variant);
+  if (block) *block = b->wave ? 64 : variant_block(b->variant);
   if (heavy) *heavy = (int)b->n_heavy;
   return BLP_OK;
 }
@@ -944,6 +1141,9 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   a.g_out = b->d_gout;
   a.g_yb = b->d_gyb;
   a.g_yl = b->d_gyl;
+  a.hot_idx = b->use_hot ? g->d_hot_idx : nullptr;
+  a.hot_tab = (const HotRow*)g->d_hot_tab;
+  a.hot_pool = (const uint4*)g->d_hot_pool;
   a.heavy_slot = b->d_heavy_slot;
   a.heavy_bm = b->d_heavy_bm;
   a.hb_words = b->hb_words;
@@ -956,7 +1156,14 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   a.cap_bits = b->cap_bits;
   a.mask = mask | BLP_CN;  // counts are always produced (Jaccard needs them)
   a.dq = b->dq;
-  if (np) {
+  if (np && b->wave) {
+    int per_cu = 1;
+    BLP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_score_wave<W_WAVES, W_CAP, 8>, W_WAVES * 64, 0));
+    a.hot_idx = nullptr;  // the wave kernel builds every row sparsely
+    hipLaunchKernelGGL((k_score_wave<W_WAVES, W_CAP, 8>), dim3(g->n_cu * std::max(per_cu, 1)), dim3(W_WAVES * 64), 0,
+                       g->stream, a);
+    BLP_HIP(hipGetLastError());
+  } else if (np) {
     int per_cu = 1;
     if ((rc = variant_occupancy(b->variant, &per_cu))) return rc;
     if (b->variant == V_SMALL)

@@ -45,12 +45,15 @@ def _check_against_oracle(ga, gb, x, y, mask=7):
     return G
 
 
+@pytest.mark.parametrize("no_wave", [False, True])
 @pytest.mark.parametrize("n_users,n_bus,n_draws,seed", [
-    (2000, 300, 20000, 0),     # small universe: SMALL variant, user side
-    (30000, 2000, 150000, 1),  # MED variant
-    (300000, 5000, 600000, 2), # LARGE variant, long rows (popular businesses)
+    (2000, 300, 20000, 0),     # small universe: wave kernel (or SMALL block variant)
+    (30000, 2000, 150000, 1),  # wave kernel (or MED block variant)
+    (300000, 5000, 600000, 2), # LARGE block variant, long rows (popular businesses)
 ])
-def test_user_and_business_side_vs_oracle(gpu, n_users, n_bus, n_draws, seed):
+def test_user_and_business_side_vs_oracle(gpu, n_users, n_bus, n_draws, seed, no_wave, monkeypatch):
+    if no_wave:
+        monkeypatch.setenv("BLP_NO_WAVE", "1")
     rng = np.random.default_rng(seed)
     a, b = bipartite_edges(rng, n_users, n_bus, n_draws)
     G = blp.DeviceGraph(a, b)
@@ -79,6 +82,12 @@ def test_general_graph_exact_distance(gpu):
     {"BLP_HEAVY_WORK": "50"},                           # heavy sources pre-built by k_heavy
     {"BLP_HEAVY_WORK": "1"},                            # one row per heavy item
     {"BLP_CHUNK_BITS": "2048", "BLP_HEAVY_WORK": "50"}, # multi-chunk disables the heavy path
+    {"BLP_HOT_MIN": "8"},                               # dense-row index OR-ed into H2
+    {"BLP_HOT_MIN": "8", "BLP_CHUNK_BITS": "1024"},     # dense rows across bitmap chunks
+    {"BLP_HOT_MIN": "8", "BLP_HEAVY_WORK": "50"},
+    {"BLP_HOT_MIN": "1", "BLP_HOT_DENSITY": "100000000"},  # > HOT_LIST dense rows: sparse fallback
+    {"BLP_NO_WAVE": "1"},                               # block kernels on a small universe
+    {"BLP_NO_WAVE": "1", "BLP_HEAVY_WORK": "50", "BLP_HOT_MIN": "8"},
 ])
 def test_kernel_paths_vs_oracle(gpu, knobs, monkeypatch):
     for k, v in knobs.items():
