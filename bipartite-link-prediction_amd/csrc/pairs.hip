@@ -951,10 +951,15 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
     return bail(rc);
   }
   const int64_t n_wg = (int64_t)g->n_cu * per_cu;
-  b->dq = (int)std::max<int64_t>(1, std::min<int64_t>(8, b->n_sources / (n_wg * 16)));
+  // sources per dequeue: the active list is in id order, which need not be balanced; keep it 1
+  // unless there are very many light sources per worker
+  b->dq = (int)std::max<int64_t>(1, std::min<int64_t>(8, b->n_sources / (n_wg * 64)));
+  if (const char* e = getenv("BLP_DQ")) b->dq = std::max(1, atoi(e));  // tuning knob
   // ---- heavy sources: build work far above the per-workgroup share goes to k_heavy
   const int64_t total_work = std::accumulate(work.begin(), work.end(), (int64_t)0) + scan_work;
-  int64_t item_work = std::max<int64_t>(16384, total_work / std::max<int64_t>(n_wg, 1));
+  // a wave is ~16x slower on one source than a 1024-thread block: split much earlier there
+  int64_t item_work = b->wave ? std::max<int64_t>(4096, total_work / std::max<int64_t>(4 * n_wg, 1))
+                              : std::max<int64_t>(16384, total_work / std::max<int64_t>(n_wg, 1));
   if (const char* e = getenv("BLP_HEAVY_WORK")) item_work = std::max<int64_t>(1, atoll(e));  // test knob
   std::vector<int32_t> heavy_slot;
   std::vector<HeavyItem> items;
@@ -1160,8 +1165,12 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
     int per_cu = 1;
     BLP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_score_wave<W_WAVES, W_CAP, 8>, W_WAVES * 64, 0));
     a.hot_idx = nullptr;  // the wave kernel builds every row sparsely
-    hipLaunchKernelGGL((k_score_wave<W_WAVES, W_CAP, 8>), dim3(g->n_cu * std::max(per_cu, 1)), dim3(W_WAVES * 64), 0,
-                       g->stream, a);
+    const dim3 grid(g->n_cu * std::max(per_cu, 1)), block(W_WAVES * 64);
+    static const int wk = getenv("BLP_WAVE_K") ? atoi(getenv("BLP_WAVE_K")) : 8;  // tuning knob
+    if (wk == 4)
+      hipLaunchKernelGGL((k_score_wave<W_WAVES, W_CAP, 4>), grid, block, 0, g->stream, a);
+    else
+      hipLaunchKernelGGL((k_score_wave<W_WAVES, W_CAP, 8>), grid, block, 0, g->stream, a);
     BLP_HIP(hipGetLastError());
   } else if (np) {
     int per_cu = 1;
