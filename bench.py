@@ -99,6 +99,24 @@ def alg_bytes(G, x, y, mask, cn=None):
     return int(per_src + per_pair)
 
 
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary of this bench
+    (profiles/*.json written by profiles/summarize.py from separate rocprofv3 --pmc
+    FETCH_SIZE / WRITE_SIZE passes; 2 x FETCH_SIZE + WRITE_SIZE per MI355X_MICROARCH.md)."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_bench.json")), key=os.path.getmtime)
+    for f in reversed(files):
+        try:
+            rows = json.load(open(f))
+        except Exception:
+            continue
+        for r in rows if isinstance(rows, list) else []:
+            if kernel in r.get("kernel", "") and r.get("hbm_bytes_corrected"):
+                return float(r["hbm_bytes_corrected"]), os.path.relpath(f, ROOT)
+    return None, None
+
+
 def cpu_baseline(G, ex_x, ex_y, target_s=15.0):
     """C oracle (oracle/oracle.c), 1 thread, on a bounded sample of the same workload:
     all pairs of a subset of the example users (user side) and all pairs of a subset of
@@ -267,9 +285,12 @@ def main():
     xs, ys = (ex_x, ex_y) if name0 == "user" else (ex_y, ex_x)
     byts = alg_bytes(G, xs, ys, mask0, cn0)
     sec = ktimes[name0]["score_ms"] / 1e3
+    kname = "k_score<1024, 34816, 512, 8>" if bt0.plan()["block"] == 1024 else "k_score_wave<2, 3328, 8>"
+    traffic, tsrc = pmc_traffic(kname)
     out["roofline"] = {"bound": "hbm", "achieved": byts / sec / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                       "frac": byts / sec / 1e9 / HBM_PEAK_GBS, "traffic": None,
-                       "kernel": "k_score<1024,36864> (%s side)" % name0, "alg_bytes_per_launch": byts}
+                       "frac": byts / sec / 1e9 / HBM_PEAK_GBS, "traffic": traffic,
+                       "kernel": "%s (%s side)" % (kname, name0), "alg_bytes_per_launch": byts,
+                       "traffic_source": tsrc}
     if dist.rank == 0 and not args.no_parity and args.sides == "both":
         out["parity"] = parity_check(G, ex_x, ex_y, res["user"], res["business"])
         import importlib
