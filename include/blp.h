@@ -42,6 +42,7 @@ extern "C" {
 
 typedef struct blp_graph blp_graph;
 typedef struct blp_batch blp_batch;
+typedef struct blp_svd blp_svd;
 
 /* ---------------------------------------------------------------- runtime */
 const char* blp_last_error(void);
@@ -127,6 +128,26 @@ int blp_batch_stats_reset(blp_batch* b);
 int blp_hop3_sample(blp_graph* g, const int32_t* src, int64_t n_src, const int32_t* pos_off,
                     const int32_t* pos_y, double rate, uint64_t seed, int32_t* out_x,
                     int32_t* out_y, uint8_t* out_label, int64_t cap, int64_t* n_out);
+
+/* ---------------------------------------------------------------- truncated-SVD scorer
+ * Replaces the reconstruction of svd.svd_user_business (svd.py:25-30): the host keeps the
+ * reference's factorisation (svd.py:24, scipy ARPACK svds) and hands over us = u * s
+ * (n_rows x k, row-major) and v = vt^T (n_cols x k, row-major), both fp64.
+ *   blp_svd_score_pairs: out[i] = us[rows[i]] . v[cols[i]]       == np.dot(us[row], vt[:, col])
+ *   blp_svd_topk:        for each selected user, the `topk` best columns over ALL businesses
+ *                        (fp64 MFMA tiles, fused top-k; score descending then column ascending),
+ *                        optionally skipping a per-user sorted exclusion list (ex_off/ex_col,
+ *                        CSR over the selected users; NULL for none). Missing slots: col -1. */
+int blp_svd_create(const double* us, int64_t n_rows, const double* v, int64_t n_cols, int k,
+                   int device, blp_svd** out);
+int blp_svd_destroy(blp_svd* h);
+int blp_svd_score_pairs(blp_svd* h, const int32_t* rows, const int32_t* cols, int64_t n, double* out);
+int blp_svd_score_pairs_device(blp_svd* h, const int32_t* d_rows, const int32_t* d_cols, int64_t n,
+                               double* d_out);
+int blp_svd_topk(blp_svd* h, const int32_t* users, int64_t n_users, const int64_t* ex_off,
+                 const int32_t* ex_col, int topk, int32_t* out_cols, double* out_scores);
+int blp_svd_stats(blp_svd* h, int which, double* total_ms, int64_t* launches); /* 0 pairs, 1 top-k */
+int blp_svd_sync(blp_svd* h);
 
 /* ---------------------------------------------------------------- stats
  * Per-kernel device time (ms, HIP events on the handle's stream) accumulated since the

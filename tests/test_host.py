@@ -1,0 +1,117 @@
+"""Host-side logic on CPU (no GPU): libblp's host helpers, the id map, SNAP degree rules,
+the score-file assembly, the svd.py matrix build, and the C-ABI symbol table."""
+import ctypes
+import math
+import os
+import re
+import shutil
+
+import numpy as np
+import pytest
+
+import blp
+import blp_oracle as O
+import coracle
+import similarity
+import svd as S
+from helpers import (B_FILES, GOLDEN, METHODS, SIM_CASES, U_FILES, assert_same_scores, dense_edges, golden, load,
+                     read_edges)
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_library_exports_every_declared_symbol():
+    hdr = open(os.path.join(ROOT, "include", "blp.h")).read()
+    names = set(re.findall(r"^\s*(?:int|const char\*)\s+(blp_\w+)\s*\(", hdr, re.M))
+    assert len(names) >= 20
+    L = blp.lib()
+    missing = [n for n in sorted(names) if not hasattr(L, n)]
+    assert not missing, missing
+
+
+def test_edge_list_parser_matches_snap_text_rules(tmp_path):
+    p = tmp_path / "g.txt"
+    p.write_text("# header\n1 2\n3\t4 extra\n\n5\n  6   7\n#8 9\n-1 +10\n")
+    a, b = blp.parse_edge_list(str(p))
+    assert a.tolist() == [1, 3, 6, -1] and b.tolist() == [2, 4, 7, 10]
+    for case in SIM_CASES:
+        a, b = blp.parse_edge_list(os.path.join(GOLDEN, case, "graph.txt"))
+        ra, rb = read_edges(os.path.join(GOLDEN, case, "graph.txt"))
+        assert a.tolist() == ra.tolist() and b.tolist() == rb.tolist()
+
+
+@pytest.mark.parametrize("case", SIM_CASES + ["hop3"])
+def test_host_graph_matches_snap_semantics(case):
+    path = os.path.join(GOLDEN, case, "graph.txt")
+    adj = O.load_edge_list(path)
+    G = blp.HostGraph(*blp.parse_edge_list(path))
+    assert sorted(G.node_ids.tolist()) == sorted(adj)
+    for v, nbrs in adj.items():
+        d = G.dense([v])[0]
+        row = G.node_ids[G.col_idx[G.row_ptr[d]:G.row_ptr[d + 1]]]
+        assert set(row.tolist()) == nbrs - {v}               # CSR: hop-1 set (self-loop not stored)
+        assert G.degree[d] == O.degree(adj, v)                # SNAP GetDeg counts a self-loop once
+        exp_w = math.log(O.degree(adj, v)) ** -1 if O.degree(adj, v) > 1 else 0.0
+        assert G.aa_weight[d] == exp_w                        # bit-identical AA term
+    ids, present = G.lookup(np.array([10**9, -5]))
+    assert not present.any() and (ids == -1).all()
+
+
+@pytest.mark.parametrize("case", SIM_CASES)
+def test_score_file_assembly_matches_reference(case):
+    """similarity.py's dict/JSON contract, fed with oracle scores (GPU-free)."""
+    path = os.path.join(GOLDEN, case, "graph.txt")
+    ex = golden(case, "examples.json")
+    G = blp.HostGraph(*blp.parse_edge_list(path))
+    _, _, ui, vi = similarity.flatten_examples(ex)
+    du, pu = G.lookup(ui)
+    dv, pv = G.lookup(vi)
+    present = pu & pv
+    a, b = read_edges(path)
+    ids, da, db = dense_edges(a, b)
+    og = coracle.OracleGraph(len(ids), da, db)
+    xo = np.searchsorted(ids, G.node_ids[du[present]])
+    yo = np.searchsorted(ids, G.node_ids[dv[present]])
+    for side, files, table in ((0, U_FILES, similarity._U_BITS), (1, B_FILES, similarity._B_BITS)):
+        x, y = (xo, yo) if side == 0 else (yo, xo)
+        cn, jac, aa, _ = og.score_pairs(x, y, 7) if len(x) else (np.zeros(0, np.uint32),) * 4
+        scores = {"cn": cn, "jaccard": jac, "adamic": aa}
+        for m, f in zip(METHODS, files):
+            got = similarity.assemble(ex, similarity._values(table.get(m, 0), present, scores))
+            assert_same_scores(got, golden(case, f), m)
+
+
+def test_unknown_method_writes_only_missing_zeros():
+    ex = golden("edge", "examples.json")
+    present = np.array([True] * 26)
+    present[4] = False
+    vals = similarity._values(0, present, {})
+    assert vals.count(0) == 1 and vals.count(None) == 25
+
+
+@pytest.mark.parametrize("split", ["train", "test"])
+def test_svd_matrix_build(split, tmp_path, monkeypatch):
+    shutil.copytree(os.path.join(GOLDEN, "bip", split), tmp_path / "data" / split)
+    monkeypatch.chdir(tmp_path)
+    users, bus, ex, ur, bc, M = S.user_business_matrix(split)
+    assert users == list(load(os.path.join(GOLDEN, "bip", split, "user.json")))
+    edges = {(l.split()[0], l.split()[1]) for l in open(os.path.join(GOLDEN, "bip", split, "graph.txt"))}
+    assert M.nnz == len(edges) and set(M.data.tolist()) == {1.0}
+    for u, b in list(edges)[:50]:
+        assert M[ur[u], bc[b]] == 1.0
+
+
+def test_svd_dead_code_raises_like_reference(tmp_path, monkeypatch):
+    shutil.copytree(os.path.join(GOLDEN, "bip", "train"), tmp_path / "data" / "train")
+    monkeypatch.chdir(tmp_path)
+    with pytest.raises(IndexError):
+        S.svd("train")
+
+
+def test_engine_fails_loudly_without_library(monkeypatch):
+    from blp import _lib
+
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setattr(_lib, "LIB_PATH", "/nonexistent/libblp.so")
+    with pytest.raises(_lib.BLPUnavailable):
+        _lib.lib()
