@@ -43,6 +43,7 @@ extern "C" {
 typedef struct blp_graph blp_graph;
 typedef struct blp_batch blp_batch;
 typedef struct blp_svd blp_svd;
+typedef struct blp_walk blp_walk;
 
 /* ---------------------------------------------------------------- runtime */
 const char* blp_last_error(void);
@@ -148,6 +149,20 @@ int blp_svd_topk(blp_svd* h, const int32_t* users, int64_t n_users, const int64_
                  const int32_t* ex_col, int topk, int32_t* out_cols, double* out_scores);
 int blp_svd_stats(blp_svd* h, int which, double* total_ms, int64_t* launches); /* 0 pairs, 1 top-k */
 int blp_svd_sync(blp_svd* h);
+
+/* ---------------------------------------------------------------- damped random walks
+ * Replaces random_walks.run_random_walk(s) (random_walks.py:9-53): p <- scale * (p . T) for
+ * `iterations` steps from e_start (the reference: scale = 1 - jump_p = 0.8, 10 steps).
+ * The matrix is handed over as W = T^T in CSR (row j: entries T[i, j] for every i), so a step
+ * is p'[j] = scale * sum_e W[j, e] p[col e]. blp_walk_run walks many starts (32 at a time)
+ * and returns q_out[k] = p_{q_start[k]}[q_node[k]]; queries grouped by start.            */
+int blp_walk_create(const int64_t* row_ptr, const int32_t* col, const double* val, int64_t n,
+                    int device, blp_walk** out);
+int blp_walk_destroy(blp_walk* w);
+int blp_walk_run(blp_walk* w, const int32_t* starts, int64_t n_starts, int iterations, double scale,
+                 const int32_t* q_start, const int32_t* q_node, int64_t n_q, double* q_out);
+int blp_walk_run_dense(blp_walk* w, int32_t start, int iterations, double scale, double* p_out);
+int blp_walk_stats(blp_walk* w, double* total_ms, int64_t* launches);
 
 /* ---------------------------------------------------------------- stats
  * Per-kernel device time (ms, HIP events on the handle's stream) accumulated since the

@@ -115,3 +115,22 @@ def test_engine_fails_loudly_without_library(monkeypatch):
     monkeypatch.setattr(_lib, "LIB_PATH", "/nonexistent/libblp.so")
     with pytest.raises(_lib.BLPUnavailable):
         _lib.lib()
+
+
+@pytest.mark.parametrize("case", ["bip/train", "general"])
+def test_walk_transition_matrix_matches_networkx(case):
+    """random_walks.py:14,26-29 built with networkx (the reference's own construction)."""
+    import networkx as nx
+    import random_walks as RW
+
+    path = os.path.join(GOLDEN, case, "graph.txt")
+    G = nx.read_edgelist(path, nodetype=int)
+    A = nx.to_scipy_sparse_array(G, format="csr").astype(float)
+    rs = np.asarray(A.sum(axis=1)).ravel()
+    T = (np.diag(1.0 / rs) @ A.toarray())
+    order, (rp, ci, val, n) = RW.transition_pull_csr(path)
+    assert order.tolist() == list(G.nodes())
+    W = np.zeros((n, n))
+    for j in range(n):
+        W[j, ci[rp[j]:rp[j + 1]]] = val[rp[j]:rp[j + 1]]
+    np.testing.assert_allclose(W.T, T, rtol=1e-15, atol=0)
