@@ -233,9 +233,10 @@ def run_svd(args):
         cols, scores = S.topk(users, args.topk, exclude=(ex_off, ex_col))
     blp.device_sync(dev)
     wall = time.perf_counter() - t_start
+    dist.barrier()
     ms1, n1 = S.stats(1)
     kern_s = (ms1 - ms0) / 1e3 / max(n1 - n0, 1)
-    t_max = dist.max(kern_s)
+    t_max = dist.max(wall) / args.steps
     scored = len(users) * B
     flops = 2.0 * len(users) * B * 64
     # candidate-pair reconstruction (svd.py:28-30 shape): 750 random businesses per user
@@ -262,15 +263,147 @@ def run_svd(args):
                                "top-%d (own reviews excluded); factorisation on host (scipy ARPACK svds) %.1fs, not in "
                                "the step" % (M.nnz, len(users), args.topk, fact_s),
                    "global_batch": int(dist.sum(scored)), "parallelism": "replicas x%d" % dist.world},
-        "roofline": {"bound": "mfma", "achieved": flops / t_max / 1e12, "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
-                     "frac": flops / t_max / 1e12 / FP64_MFMA_PEAK_TFS, "traffic": None,
-                     "kernel": "k_svd_topk<64> + k_svd_merge"},
-        "wall_ms_per_step": 1e3 * wall / args.steps,
+        "roofline": {"bound": "mfma", "achieved": flops / kern_s / 1e12, "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                     "frac": flops / kern_s / 1e12 / FP64_MFMA_PEAK_TFS, "traffic": None,
+                     "kernel": "k_svd_topk<64> + k_svd_merge", "kernel_ms": 1e3 * kern_s},
         "pairs_kernel": {"pairs": int(len(pr)), "ms": 1e3 * pair_s, "pairs_per_s": len(pr) / pair_s,
                          "alg_GBps": pair_bytes / pair_s / 1e9},
         "parity": {"topk_users_checked": 64, "exact": bool(ok)},
         "factorization_s": fact_s,
     }
+    if dist.rank == 0:
+        print(json.dumps(out), flush=True)
+
+
+def topk_alg_bytes(G, src, h2_sum, push_sum, k, n_methods):
+    """SURVEY.md §8(d) "Full-candidate top-k (user)": per user the H2 bytes
+    (16 + 4 d_u + sum_{b in N(u)} (16 + 4 d_b)) + sum_{w in H2(u)} (16 + 4 d_w) + 12 k per list.
+    The last sum comes from the kernel's own work counters (sum |H2|, sum |N(w)|)."""
+    d = G.hop1_size.astype(np.int64)
+    csum = np.concatenate([[0], np.cumsum(d[G.col_idx])])
+    nbr = csum[G.row_ptr[src + 1]] - csum[G.row_ptr[src]]
+    h2_bytes = int((16 + 4 * d[src] + 16 * d[src] + 4 * nbr).sum())
+    return h2_bytes + 16 * h2_sum + 4 * push_sum + 12 * k * n_methods * len(src)
+
+
+def _oracle_graph(G):
+    """C oracle over the same edges, on the engine's dense ids (identity id maps)."""
+    import coracle
+
+    ident = np.arange(G.n, dtype=np.int32)
+    return coracle.OracleGraph(G.n, *_dense_edges(G)), ident, ident
+
+
+def topk_parity(G, src, k, res, n_users=3):
+    """Not timed: for a few users the C oracle enumerates the exact hop-3 set, scores every
+    candidate and sorts (score desc, id asc); Jaccard lists must match exactly, Adamic-Adar
+    lists must carry the pair kernel's values and agree with the oracle's float sums."""
+    og, to_o, from_o = _oracle_graph(G)
+    pick = np.random.default_rng(5).choice(len(src), n_users, replace=False)
+    ok_j = ok_a = ok_n = True
+    for i in pick:
+        x = to_o[src[i]]
+        _, mem = og.hop3([x])
+        xs = np.full(len(mem), x, np.int32)
+        _, jac, aa, _ = og.score_pairs(xs, mem, 7, nthreads=8)
+        dense = from_o[mem]
+        ok_n &= bool(res["ncand"][i] == len(mem))
+        o = np.lexsort((dense, -jac))[:k]
+        ok_j &= bool(np.array_equal(res["jaccard"][0][i][:len(o)], dense[o]) and
+                     np.array_equal(res["jaccard"][1][i][:len(o)], jac[o]))
+        cols, sc = res["adamic_adar"][0][i], res["adamic_adar"][1][i]
+        v = cols >= 0
+        pair = G.score_pairs(np.full(int(v.sum()), src[i], np.int32), cols[v], 7)["adamic"]
+        ok_a &= bool(np.array_equal(pair, sc[v]))
+        # the k-th value may tie within float rounding; compare the value lists to 1e-9
+        ok_a &= bool(np.allclose(np.sort(aa)[::-1][:int(v.sum())], sc[v], rtol=1e-9, atol=0))
+    return {"users_checked": int(n_users), "jaccard_exact": ok_j, "adamic_pair_kernel_equal_and_oracle_1e-9": ok_a,
+            "n_candidates_exact": ok_n}
+
+
+def topk_cpu_baseline(G, src, k, target_s=15.0):
+    """C oracle, 1 thread: exact hop-3 candidates of a few users (og_hop3), every candidate
+    scored (og_score_pairs: CN, Jaccard, Adamic-Adar), top-k by sort; candidate pairs/s."""
+    og, to_oracle, _ = _oracle_graph(G)
+    done, spent, used = 0, 0.0, 0
+    while spent < target_s and used < len(src):
+        x = to_oracle[src[used]]
+        used += 1
+        t = time.perf_counter()
+        counts, members = og.hop3([x])
+        xs = np.full(len(members), x, np.int32)
+        cn, jac, aa, _ = og.score_pairs(xs, members, 7, nthreads=1)
+        for sc in (jac, aa):
+            np.lexsort((members, -sc))[:k]
+        spent += time.perf_counter() - t
+        done += len(members)
+    return {"value": done / spent, "unit": "pairs/s", "cores": 1, "kind": "port",
+            "sample": "C oracle (oracle/oracle.c), 1 thread: exact hop-3 candidate set of %d users (%d pairs) "
+                      "scored with CN+Jaccard+AA and sorted for top-%d, %.1fs" % (used, done, k, spent)}
+
+
+def run_topk(args):
+    """Config 3 (BASELINE.json configs[2]): the config-2 graph; for 10K users per GPU EVERY
+    exact-distance-3 business is scored with Jaccard and Adamic-Adar and the top-k kept
+    (k = 20, eval.py:10). One step = one blp_topk_run over all users. value = candidate
+    pairs scored (sum |H3(u)|) per second."""
+    from blp.topk import TopK
+
+    dist = Dist()
+    dev = dist.local
+    blp.lib()
+    U, B, D = synth.CONFIGS[args.config]
+    t0 = time.time()
+    a, b = synth.review_edges(U, B, D, seed=0)
+    G = blp.DeviceGraph(a, b, device=dev)
+    del a, b
+    log("graph: %d nodes, %d unique edges, built in %.1fs" % (G.n, G.nnz // 2, time.time() - t0))
+    G.n_users_hint = U  # the same users make_examples samples for config 2
+    src = synth.sample_users(G, args.users, seed=dist.rank)
+    t0 = time.time()
+    T = TopK(G, "user")
+    T.set_sources(src)
+    log("top-k engine: %s in %.1fs" % (T.info(), time.time() - t0))
+    mask = blp.JACCARD | blp.ADAMIC
+    for _ in range(args.warmup):
+        T.run(args.topk, mask)
+    blp.device_sync(dev)
+    T.stats_reset()
+    dist.barrier()
+    blp.device_sync(dev)
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        T.run(args.topk, mask)
+    blp.device_sync(dev)
+    t_local = time.perf_counter() - t_start
+    dist.barrier()
+    t_max = dist.max(t_local) / args.steps
+    kms, kn = T.stats(0)
+    kern_s = kms / 1e3 / max(kn, 1)
+    cols_j, sc_j, ncand = T.fetch("jaccard")
+    cols_a, sc_a, _ = T.fetch("adamic_adar")
+    pairs = int(ncand.sum())
+    h2_sum, push_sum = T.stats(3)[1], T.stats(4)[1]
+    hash_src, direct_src = T.stats(1)[1], T.stats(2)[1]
+    byts = topk_alg_bytes(G, src, h2_sum, push_sum, args.topk, 2)
+    out = {
+        "metric": METRIC, "value": dist.sum(pairs) / t_max, "unit": "pairs/s", "n_gpus": dist.world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * t_max, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "int32", "data": "synthetic",
+        "config": {"workload": "config3: config-2 graph (%d unique edges); %d users/GPU, every exact hop-3 business "
+                               "scored (Jaccard + Adamic-Adar), top-%d per method" % (G.nnz // 2, len(src), args.topk),
+                   "pairs_per_gpu": pairs, "global_batch": int(dist.sum(pairs)),
+                   "parallelism": "replicas x%d (graph replicated, users split, no collective)" % dist.world},
+        "roofline": {"bound": "hbm", "achieved": byts / kern_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": byts / kern_s / 1e9 / HBM_PEAK_GBS, "traffic": pmc_traffic("k_topk")[0],
+                     "kernel": "k_topk", "kernel_ms": 1e3 * kern_s, "alg_bytes_per_launch": byts},
+        "work": {"sum_h2": h2_sum, "sum_push": push_sum, "aa_hash_sources": hash_src, "aa_direct_sources": direct_src},
+    }
+    if dist.rank == 0 and not args.no_parity:
+        out["parity"] = topk_parity(G, src, args.topk, {"jaccard": (cols_j, sc_j), "adamic_adar": (cols_a, sc_a),
+                                                        "ncand": ncand})
+    if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = topk_cpu_baseline(G, src, args.topk, args.cpu_seconds)
     if dist.rank == 0:
         print(json.dumps(out), flush=True)
 
@@ -288,12 +421,15 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--user-mask", type=int, default=7, help="methods of the user pass (1 CN, 2 J, 4 AA)")
-    ap.add_argument("--mode", default="similarity", choices=["similarity", "svd"],
-                    help="similarity: config 2 (default); svd: config 4 rank-64 truncated-SVD scorer")
+    ap.add_argument("--mode", default="similarity", choices=["similarity", "topk", "svd"],
+                    help="similarity: config 2 (default); topk: config 3 full-candidate Jaccard + Adamic-Adar "
+                         "top-k; svd: config 4 rank-64 truncated-SVD scorer")
     ap.add_argument("--topk", type=int, default=20)
     args = ap.parse_args()
     if args.mode == "svd":
         return run_svd(args)
+    if args.mode == "topk":
+        return run_topk(args)
 
     dist = Dist()
     dev = dist.local

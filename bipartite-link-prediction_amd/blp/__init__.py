@@ -6,9 +6,10 @@ scripts; the reference-named modules (similarity, svd, random_walks, util, eval,
 dataset_maker) one directory up are the drop-in call surface.
 """
 from ._lib import ADAMIC, CN, JACCARD, BLPError, BLPUnavailable, device_count, device_sync, lib, version
+from .topk import TopK
 from .graph import DeviceGraph, HostGraph, LoadEdgeList, PairBatch, load_edge_list, parse_edge_list
 
 __all__ = [
     "ADAMIC", "CN", "JACCARD", "BLPError", "BLPUnavailable", "DeviceGraph", "HostGraph", "LoadEdgeList",
-    "PairBatch", "device_count", "device_sync", "lib", "load_edge_list", "parse_edge_list", "version",
+    "PairBatch", "TopK", "device_count", "device_sync", "lib", "load_edge_list", "parse_edge_list", "version",
 ]

@@ -61,6 +61,7 @@ class HostGraph:
         u0 = np.unique(a_ids)
         u1 = np.setdiff1d(np.unique(b_ids), u0, assume_unique=True)
         self.node_ids = np.concatenate([u0, u1])  # dense id -> original id
+        self.n_col0 = len(u0)  # dense ids [0, n_col0) appear in column 0 (users of a graph.txt)
         self.n = len(self.node_ids)
         if self.n >= 2**31 - 1:
             raise ValueError("too many nodes for int32 dense ids")

@@ -1,0 +1,811 @@
+// Full-candidate top-k (BASELINE.json configs[2], "config 3"; SURVEY.md §8(b) blp_topk,
+// §8(d) "Full-candidate top-k").
+//
+// For every source x (a user on the user side) ALL targets b at exact distance 3 are scored
+// with the reference's measures -- common_neighbors / jaccard / adamic_adar of
+// (H2(x), N(b)), similarity.py:108-126 -- and the k best are kept per method (score
+// descending, then dense target id ascending; the reference has no top-k).
+// In a bipartite graph the distance-3 targets are exactly the targets with CN(x,b) > 0
+// outside N(x), so the whole candidate set is one push over the A^T A projection:
+//
+//     CN(x, b) = #{ w in H2(x) : b in N(w) }.
+//
+// One workgroup per source (dequeued). H2(x) is never materialised: the pairs (b', w) with
+// b' in N(x), w in N(b') are walked, and w is pushed only from b' = min(N(w) ∩ N(x))
+// ("ownership"), so each w in H2(x) is pushed exactly once (duplicates cost one scan of the
+// short row N(w)). The targets are renumbered by degree (descending) so the per-target
+// counters can be tiered in LDS: CN <= deg(b), hence a target of degree <= 255 gets a u8
+// counter, <= 65535 a u16, else a u32 (config 3: 100K businesses -> 114 KB, one pass).
+//
+// Adamic-Adar: every w that reaches a distance-3 target has degree >= 2, so
+// CN * wmin <= AA <= CN * wmax with the extreme weights of such w. From the CN counts the
+// candidates that can still reach the k-th AA lower bound are collected (usually a few
+// hundred), and one more push accumulates their exact fixed-point sums (the pair kernel's
+// arithmetic, so the values are bit-identical to blp_score_pairs). When the candidates do
+// not fit, the source falls back to chunked direct fixed-point accumulation.
+#include <algorithm>
+#include <cmath>
+#include <climits>
+#include <cstdlib>
+#include <cstring>
+#include <thread>
+
+#include "blp_internal.h"
+
+namespace {
+
+constexpr int TK_NT = 512;
+constexpr int TK_SEL = 1024;          // selection buffer entries (also the AA hash table)
+constexpr int TK_HCAP = TK_SEL / 2;   // AA candidates handled by the hash (load <= 1/2)
+constexpr int TK_SEG = 256;           // N(x) entries staged per batch
+constexpr int TK_FILT = 128;          // words of the N'(x) membership filter (4096 bits)
+constexpr int TK_ACC_WORDS = 36224;   // counter space: 141.5 KiB
+constexpr int TK_KMAX = 256;
+constexpr uint32_t TK_EMPTY = 0xFFFFFFFFu;
+
+// Counter chunk over permuted target ids [c0, c1): [c0, b32) u32, [b32, b16) u16 packed
+// two per word from word w16, [b16, c1) u8 packed four per word from word w8.
+struct TkChunk {
+  int64_t c0, c1, b32, b16;
+  int32_t w16, w8;
+};
+
+struct TkArgs {
+  const int64_t* rp;
+  const int32_t* ci;
+  const int32_t* pci;  // source-side rows with permuted target ids, sorted; row w at pci + rp[w] - pbase
+  int64_t pbase;
+  const int32_t* perm;  // [T] target (dense id - tlo) -> permuted id
+  const int32_t* inv;   // [T] permuted id -> dense target id
+  const int32_t* tdeg;  // [T] |N(b)| by permuted id
+  const long long* aaw; // Adamic-Adar weights, fixed point (dense ids)
+  const int32_t* src;
+  int n_src;
+  int64_t tlo, T;
+  const TkChunk* chunks;
+  int n_chunks;
+  int64_t aa_chunk;  // targets per direct-AA chunk (u64 each)
+  int k;
+  uint32_t mask;
+  double ratio;  // wmin / wmax over sources of degree >= 2 (fixed point)
+  int hcap;      // AA candidates allowed on the hash path (<= TK_HCAP)
+  unsigned long long* keys;  // [3][n_src][k]
+  int32_t* cols;             // [3][n_src][k]
+  int64_t* ncand;            // [n_src]
+  unsigned long long* counters;  // [0] queue, [1] AA hash path, [2] AA direct path, [3] sum |H2|, [4] sum of |N(w)| over H2
+};
+
+struct TkShared {
+  uint32_t acc[TK_ACC_WORDS];
+  unsigned long long key[TK_SEL];
+  int32_t col[TK_SEL];
+  int64_t seg_rs[TK_SEG];
+  int64_t seg_off[TK_SEG + 1];
+  int32_t seg_p[TK_SEG];
+  uint32_t filt[TK_FILT];
+  long long red[TK_NT / 64];
+  unsigned long long thr_key;
+  int thr_col, have_thr, n, item;
+  int nv[3];
+};
+
+__device__ inline uint32_t filt_bit(int32_t e) { return ((uint32_t)e * 2654435761u) >> 20; }
+
+__device__ inline bool better(unsigned long long ka, int ca, unsigned long long kb, int cb) {
+  return ka > kb || (ka == kb && ca < cb);
+}
+
+__device__ inline void acc_add(uint32_t* acc, const TkChunk& c, int64_t p) {
+  if (p < c.b32) {
+    atomicAdd(&acc[p - c.c0], 1u);
+  } else if (p < c.b16) {
+    const int64_t i = p - c.b32;
+    atomicAdd(&acc[c.w16 + (i >> 1)], 1u << ((i & 1) << 4));
+  } else {
+    const int64_t i = p - c.b16;
+    atomicAdd(&acc[c.w8 + (i >> 2)], 1u << ((i & 3) << 3));
+  }
+}
+
+__device__ inline uint32_t acc_get(const uint32_t* acc, const TkChunk& c, int64_t p) {
+  if (p < c.b32) return acc[p - c.c0];
+  if (p < c.b16) {
+    const int64_t i = p - c.b32;
+    return (acc[c.w16 + (i >> 1)] >> ((i & 1) << 4)) & 0xFFFFu;
+  }
+  const int64_t i = p - c.b16;
+  return (acc[c.w8 + (i >> 2)] >> ((i & 3) << 3)) & 0xFFu;
+}
+
+__device__ inline void acc_clear(uint32_t* acc, const TkChunk& c, int64_t p) {
+  if (p < c.b32) {
+    acc[p - c.c0] = 0;
+  } else if (p < c.b16) {
+    const int64_t i = p - c.b32;
+    atomicAnd(&acc[c.w16 + (i >> 1)], ~(0xFFFFu << ((i & 1) << 4)));
+  } else {
+    const int64_t i = p - c.b16;
+    atomicAnd(&acc[c.w8 + (i >> 2)], ~(0xFFu << ((i & 3) << 3)));
+  }
+}
+
+__device__ inline int hash_slot(int32_t p) { return (int)(((uint32_t)p * 2654435761u) >> 22); }  // 10 bits
+
+__device__ long long block_sum(TkShared& s, long long v) {
+  for (int d = 32; d > 0; d >>= 1) v += __shfl_down(v, d, 64);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) s.red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  long long t = 0;
+  for (int w = 0; w < TK_NT / 64; ++w) t += s.red[w];
+  return t;
+}
+
+// is permuted target e in N'(x)?  filter bit, then binary search of x's sorted permuted row
+__device__ inline bool in_row_x(const TkShared& s, const int32_t* rowx, int du, int32_t e) {
+  const uint32_t b = filt_bit(e);
+  if (!((s.filt[b >> 5] >> (b & 31)) & 1u)) return false;
+  int lo = 0, hi = du;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (rowx[mid] < e) lo = mid + 1; else hi = mid;
+  }
+  return lo < du && rowx[lo] == e;
+}
+
+// MODE 0: CN counts into the tiered counters of chunk c (and |H2(x)| when count_h2)
+// MODE 1: exact AA of the hashed candidates (counter >= thr) into s.key[slot]
+// MODE 2: direct AA fixed-point sums of targets [c0, c1) into the u64 view of s.acc
+template <int MODE>
+__device__ long long push_pass(const TkArgs& a, TkShared& s, int x, int64_t xb, int du, const int32_t* rowx,
+                               const TkChunk& c, uint32_t thr, int64_t d0, int64_t d1, bool count_h2,
+                               long long* pushed = nullptr) {
+  long long h2 = 0, npush = 0;
+  unsigned long long* acc64 = reinterpret_cast<unsigned long long*>(s.acc);
+  const int tid = threadIdx.x;
+  for (int s0 = 0; s0 < du; s0 += TK_SEG) {
+    const int ns = min(TK_SEG, du - s0);
+    __syncthreads();  // the previous batch's readers are done with the segment table
+    long long len = 0;
+    if (tid < ns) {
+      const int b = a.ci[xb + s0 + tid];
+      const int64_t rs = a.rp[b];
+      len = a.rp[b + 1] - rs;
+      s.seg_rs[tid] = rs;
+      s.seg_p[tid] = a.perm[b - a.tlo];
+    }
+    // exclusive scan of the segment lengths (ns <= TK_SEG <= TK_NT)
+    {
+      long long inc = len;
+      const int lane = tid & 63, wid = tid >> 6;
+      for (int d = 1; d < 64; d <<= 1) {
+        const long long t = __shfl_up(inc, d, 64);
+        if (lane >= d) inc += t;
+      }
+      if (lane == 63) s.red[wid] = inc;
+      __syncthreads();
+      long long base = 0;
+      for (int w = 0; w < wid; ++w) base += s.red[w];
+      if (tid < ns) s.seg_off[tid] = base + inc - len;
+      if (tid == TK_NT - 1) s.seg_off[ns] = base + inc;  // total (threads >= ns carry len 0)
+      __syncthreads();
+    }
+    const int64_t E = s.seg_off[ns];
+    int sg = 0;
+    for (int64_t idx = tid; idx < E; idx += TK_NT) {
+      while (s.seg_off[sg + 1] <= idx) ++sg;
+      const int w = a.ci[s.seg_rs[sg] + (idx - s.seg_off[sg])];
+      if (w == x) continue;
+      const int32_t pp = s.seg_p[sg];
+      const int64_t r0 = a.rp[w];
+      const int len_w = (int)(a.rp[w + 1] - r0);
+      const int32_t* roww = a.pci + (r0 - a.pbase);
+      bool owned = true;
+      for (int j = 0; j < len_w; ++j) {
+        const int32_t e = roww[j];
+        if (e >= pp) break;
+        if (in_row_x(s, rowx, du, e)) {
+          owned = false;
+          break;
+        }
+      }
+      if (!owned) continue;
+      if (MODE == 0) {
+        if (count_h2) {
+          ++h2;
+          npush += len_w;
+        }
+        for (int j = 0; j < len_w; ++j) {
+          const int32_t e = roww[j];
+          if (e >= c.c0 && e < c.c1) acc_add(s.acc, c, e);
+        }
+      } else if (MODE == 1) {
+        const unsigned long long wfx = (unsigned long long)a.aaw[w];
+        for (int j = 0; j < len_w; ++j) {
+          const int32_t e = roww[j];
+          if (acc_get(s.acc, c, e) >= thr) {
+            int h = hash_slot(e);
+            while (s.col[h] != e) h = (h + 1) & (TK_SEL - 1);
+            atomicAdd(&s.key[h], wfx);
+          }
+        }
+      } else {
+        const unsigned long long wfx = (unsigned long long)a.aaw[w];
+        for (int j = 0; j < len_w; ++j) {
+          const int32_t e = roww[j];
+          if (e >= d0 && e < d1) atomicAdd(&acc64[e - d0], wfx);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (pushed) *pushed = npush;
+  return h2;
+}
+
+// Sort s.key/s.col[0, TK_SEL) best-first (bitonic), keep min(n, k); update the threshold.
+__device__ void compact(const TkArgs& a, TkShared& s, int n) {
+  const int tid = threadIdx.x;
+  for (int i = n + tid; i < TK_SEL; i += TK_NT) {
+    s.key[i] = 0;
+    s.col[i] = 0x7FFFFFFF;
+  }
+  __syncthreads();
+  int size_lim = 2;
+  while (size_lim < n) size_lim <<= 1;  // entries past n are padding; sort the smallest power of two
+  for (int size = 2; size <= size_lim; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int t = tid; t < size_lim / 2; t += TK_NT) {
+        const int i = 2 * t - (t & (stride - 1));
+        const int j = i + stride;
+        const bool desc = ((i & size) == 0) || size == size_lim;
+        const unsigned long long ki = s.key[i], kj = s.key[j];
+        const int ci = s.col[i], cj = s.col[j];
+        const bool sw = desc ? better(kj, cj, ki, ci) : better(ki, ci, kj, cj);
+        if (sw) {
+          s.key[i] = kj;
+          s.key[j] = ki;
+          s.col[i] = cj;
+          s.col[j] = ci;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  if (tid == 0) {
+    const int keep = min(n, a.k);
+    s.n = keep;
+    if (keep == a.k) {
+      s.thr_key = s.key[keep - 1];
+      s.thr_col = s.col[keep - 1];
+      s.have_thr = 1;
+    }
+  }
+  __syncthreads();
+}
+
+__device__ void sel_begin(const TkArgs& a, TkShared& s, int m, int it) {
+  const int nv = s.nv[m];
+  const size_t base = ((size_t)m * a.n_src + it) * a.k;
+  for (int i = threadIdx.x; i < nv; i += TK_NT) {
+    s.key[i] = a.keys[base + i];
+    s.col[i] = a.cols[base + i];
+  }
+  if (threadIdx.x == 0) {
+    s.n = nv;
+    s.have_thr = nv == a.k;
+    if (nv == a.k) {
+      s.thr_key = a.keys[base + nv - 1];
+      s.thr_col = a.cols[base + nv - 1];
+    }
+  }
+  __syncthreads();
+}
+
+__device__ void sel_end(const TkArgs& a, TkShared& s, int m, int it) {
+  compact(a, s, s.n);
+  const int nv = s.n;
+  const size_t base = ((size_t)m * a.n_src + it) * a.k;
+  for (int i = threadIdx.x; i < nv; i += TK_NT) {
+    a.keys[base + i] = s.key[i];
+    a.cols[base + i] = s.col[i];
+  }
+  if (threadIdx.x == 0) s.nv[m] = nv;
+  __syncthreads();
+}
+
+__device__ inline void sel_offer(TkShared& s, bool ok, unsigned long long key, int col) {
+  if (ok && (!s.have_thr || better(key, col, s.thr_key, s.thr_col))) {
+    const int slot = atomicAdd(&s.n, 1);
+    s.key[slot] = key;
+    s.col[slot] = col;
+  }
+}
+
+__device__ inline void sel_round_end(const TkArgs& a, TkShared& s) {
+  __syncthreads();
+  const int n = s.n;
+  __syncthreads();
+  if (n > TK_SEL - TK_NT) compact(a, s, n);
+}
+
+// METHOD 0: CN key; 1: Jaccard key (fp64 bits); the counters of chunk c
+template <int METHOD>
+__device__ long long sel_counts(const TkArgs& a, TkShared& s, int it, const TkChunk& c, long long h2, bool count) {
+  sel_begin(a, s, METHOD, it);
+  long long nc = 0;
+  for (int64_t base = c.c0; base < c.c1; base += TK_NT) {
+    const int64_t p = base + threadIdx.x;
+    bool ok = false;
+    unsigned long long key = 0;
+    int col = 0;
+    if (p < c.c1) {
+      const uint32_t cnt = acc_get(s.acc, c, p);
+      ok = cnt > 0;
+      if (ok) {
+        nc += count;
+        if (METHOD == 0) {
+          key = cnt;
+        } else {
+          const double jac = (double)cnt / (double)(h2 + (long long)a.tdeg[p] - (long long)cnt);
+          key = (unsigned long long)__double_as_longlong(jac);
+        }
+        col = a.inv[p];
+      }
+    }
+    sel_offer(s, ok, key, col);
+    sel_round_end(a, s);
+  }
+  sel_end(a, s, METHOD, it);
+  return nc;
+}
+
+__global__ __launch_bounds__(TK_NT) void k_topk(TkArgs a) {
+  __shared__ TkShared s;
+  const int tid = threadIdx.x;
+  unsigned long long* acc64 = reinterpret_cast<unsigned long long*>(s.acc);
+  for (;;) {
+    __syncthreads();
+    if (tid == 0) s.item = (int)atomicAdd(&a.counters[0], 1ull);
+    __syncthreads();
+    const int it = s.item;
+    if (it >= a.n_src) break;
+    const int x = a.src[it];
+    const int64_t xb = a.rp[x];
+    const int du = (int)(a.rp[x + 1] - xb);
+    const int32_t* rowx = a.pci + (xb - a.pbase);
+    for (int i = tid; i < TK_FILT; i += TK_NT) s.filt[i] = 0;
+    if (tid < 3) s.nv[tid] = 0;
+    __syncthreads();
+    for (int j = tid; j < du; j += TK_NT) {
+      const uint32_t b = filt_bit(rowx[j]);
+      atomicOr(&s.filt[b >> 5], 1u << (b & 31));
+    }
+    __syncthreads();
+    const bool want_cn = a.mask & (BLP_CN | BLP_ADAMIC), want_j = a.mask & BLP_JACCARD,
+               want_aa = a.mask & BLP_ADAMIC;
+    long long h2 = 0, ncand = 0;
+    for (int ci = 0; ci < a.n_chunks; ++ci) {
+      const TkChunk c = a.chunks[ci];
+      const int words = (int)(c.w8 + ((c.c1 - c.b16) + 3) / 4);
+      for (int i = tid; i < words; i += TK_NT) s.acc[i] = 0;
+      __syncthreads();
+      long long np = 0;
+      const long long h = push_pass<0>(a, s, x, xb, du, rowx, c, 0, 0, 0, ci == 0, &np);
+      if (ci == 0) {
+        h2 = block_sum(s, h);
+        np = block_sum(s, np);
+        if (tid == 0) {
+          atomicAdd(&a.counters[3], (unsigned long long)h2);
+          atomicAdd(&a.counters[4], (unsigned long long)np);
+        }
+      }
+      for (int j = tid; j < du; j += TK_NT) {
+        const int32_t e = rowx[j];
+        if (e >= c.c0 && e < c.c1) acc_clear(s.acc, c, e);
+      }
+      __syncthreads();
+      if (want_cn) ncand += sel_counts<0>(a, s, it, c, h2, true);
+      if (want_j) ncand += sel_counts<1>(a, s, it, c, h2, !want_cn);
+    }
+    ncand = block_sum(s, ncand);
+    if (want_aa && ncand > 0) {
+      bool done = false;
+      if (a.n_chunks == 1) {
+        const TkChunk c = a.chunks[0];
+        uint32_t thr = 1;
+        if (s.nv[0] == a.k) {
+          const unsigned long long cnt_k = a.keys[((size_t)0 * a.n_src + it) * a.k + a.k - 1];
+          thr = (uint32_t)max(1.0, floor((double)cnt_k * a.ratio * (1.0 - 1e-9)));
+        }
+        long long nc = 0;
+        for (int64_t p = c.c0 + tid; p < c.c1; p += TK_NT) nc += acc_get(s.acc, c, p) >= thr;
+        nc = block_sum(s, nc);
+        if (nc <= a.hcap) {
+          for (int i = tid; i < TK_SEL; i += TK_NT) {
+            s.col[i] = (int32_t)TK_EMPTY;
+            s.key[i] = 0;
+          }
+          __syncthreads();
+          for (int64_t p = c.c0 + tid; p < c.c1; p += TK_NT) {
+            if (acc_get(s.acc, c, p) >= thr) {
+              int h = hash_slot((int32_t)p);
+              while (atomicCAS(&s.col[h], (int32_t)TK_EMPTY, (int32_t)p) != (int32_t)TK_EMPTY) h = (h + 1) & (TK_SEL - 1);
+            }
+          }
+          __syncthreads();
+          push_pass<1>(a, s, x, xb, du, rowx, c, thr, 0, 0, false);
+          // hash slots -> selection entries (key = AA fixed point, col = dense target id)
+          unsigned long long kv[TK_SEL / TK_NT];
+          int cv[TK_SEL / TK_NT];
+          for (int r = 0; r < TK_SEL / TK_NT; ++r) {
+            const int i = tid + r * TK_NT;
+            const int32_t p = s.col[i];
+            kv[r] = p == (int32_t)TK_EMPTY ? 0ull : s.key[i];
+            cv[r] = p == (int32_t)TK_EMPTY ? 0x7FFFFFFF : a.inv[p];
+          }
+          __syncthreads();
+          for (int r = 0; r < TK_SEL / TK_NT; ++r) {
+            s.key[tid + r * TK_NT] = kv[r];
+            s.col[tid + r * TK_NT] = cv[r];
+          }
+          if (tid == 0) {
+            s.have_thr = 0;
+            s.n = TK_SEL;
+          }
+          __syncthreads();
+          compact(a, s, TK_SEL);
+          {
+            // entries with key 0 are empty slots sorted last; at most nc are real
+            const int nv = min((int)nc, a.k);
+            const size_t base = ((size_t)2 * a.n_src + it) * a.k;
+            for (int i = tid; i < nv; i += TK_NT) {
+              a.keys[base + i] = s.key[i];
+              a.cols[base + i] = s.col[i];
+            }
+            if (tid == 0) s.nv[2] = nv;
+            __syncthreads();
+          }
+          if (tid == 0) atomicAdd(&a.counters[1], 1ull);
+          done = true;
+        }
+      }
+      if (!done) {
+        for (int64_t d0 = 0; d0 < a.T; d0 += a.aa_chunk) {
+          const int64_t d1 = min(a.T, d0 + a.aa_chunk);
+          for (int64_t i = tid; i < d1 - d0; i += TK_NT) acc64[i] = 0;
+          __syncthreads();
+          push_pass<2>(a, s, x, xb, du, rowx, a.chunks[0], 0, d0, d1, false);
+          for (int j = tid; j < du; j += TK_NT) {
+            const int32_t e = rowx[j];
+            if (e >= d0 && e < d1) acc64[e - d0] = 0;
+          }
+          __syncthreads();
+          sel_begin(a, s, 2, it);
+          for (int64_t base = d0; base < d1; base += TK_NT) {
+            const int64_t p = base + tid;
+            const unsigned long long v = p < d1 ? acc64[p - d0] : 0ull;
+            sel_offer(s, v > 0, v, v > 0 ? a.inv[p] : 0);
+            sel_round_end(a, s);
+          }
+          sel_end(a, s, 2, it);
+        }
+        if (tid == 0) atomicAdd(&a.counters[2], 1ull);
+      }
+    }
+    // pad the unused tail of each list
+    for (int m = 0; m < 3; ++m) {
+      const size_t base = ((size_t)m * a.n_src + it) * a.k;
+      for (int i = s.nv[m] + tid; i < a.k; i += TK_NT) {
+        a.keys[base + i] = 0;
+        a.cols[base + i] = -1;
+      }
+    }
+    if (tid == 0) a.ncand[it] = ncand;
+  }
+}
+
+}  // namespace
+
+using namespace blp;
+
+struct blp_topk {
+  blp_graph* g = nullptr;
+  int64_t slo = 0, shi = 0, tlo = 0, thi = 0, T = 0;
+  int64_t pbase = 0;
+  int64_t n32 = 0, n16 = 0;  // tier boundaries in permuted order
+  int64_t acc_words = TK_ACC_WORDS;
+  double ratio = 0.0;
+  bool have_aa = false;
+  std::vector<TkChunk> chunks;
+  int64_t aa_chunk = 0;
+  DevBuf perm, inv, tdeg, pci, d_chunks, src, keys, cols, ncand, counters;
+  int64_t n_src = 0;
+  int k = 0;
+  uint32_t mask = 0;
+  bool ran = false;
+  KernelTimer timer;
+};
+
+namespace {
+
+int64_t env_i64(const char* name, int64_t dflt) {
+  const char* v = getenv(name);
+  return (v && *v) ? atoll(v) : dflt;
+}
+
+int64_t chunk_words(const blp_topk* t, int64_t c0, int64_t c1) {
+  const int64_t b32 = std::min(std::max(t->n32, c0), c1), b16 = std::min(std::max(t->n16, c0), c1);
+  return (b32 - c0) + (b16 - b32 + 1) / 2 + (c1 - b16 + 3) / 4;
+}
+
+void plan_chunks(blp_topk* t) {
+  t->chunks.clear();
+  int64_t c0 = 0;
+  do {
+    int64_t lo = c0 + 1, hi = t->T;  // largest c1 in [c0+1, T] that fits
+    if (hi <= c0) hi = c0 + 1;
+    while (lo < hi) {
+      const int64_t mid = lo + (hi - lo + 1) / 2;
+      if (chunk_words(t, c0, mid) <= t->acc_words) lo = mid; else hi = mid - 1;
+    }
+    const int64_t c1 = std::min<int64_t>(lo, std::max<int64_t>(t->T, c0 + 1));
+    TkChunk c{};
+    c.c0 = c0;
+    c.c1 = c1;
+    c.b32 = std::min(std::max(t->n32, c0), c1);
+    c.b16 = std::min(std::max(t->n16, c0), c1);
+    c.w16 = (int32_t)(c.b32 - c0);
+    c.w8 = (int32_t)(c.w16 + (c.b16 - c.b32 + 1) / 2);
+    t->chunks.push_back(c);
+    c0 = c1;
+  } while (c0 < t->T);
+  t->aa_chunk = t->acc_words / 2;
+}
+
+}  // namespace
+
+extern "C" int blp_topk_create(blp_graph* g, int64_t src_lo, int64_t src_hi, int64_t tgt_lo, int64_t tgt_hi,
+                               blp_topk** out) {
+  BLP_CHECK(g && out, BLP_E_ARG, "blp_topk_create: bad arguments");
+  BLP_CHECK(0 <= src_lo && src_lo <= src_hi && src_hi <= g->n && 0 <= tgt_lo && tgt_lo < tgt_hi && tgt_hi <= g->n,
+            BLP_E_ARG, "blp_topk_create: bad id ranges");
+  BLP_CHECK(src_hi <= tgt_lo || tgt_hi <= src_lo, BLP_E_ARG, "blp_topk_create: source and target ranges overlap");
+  const int64_t* rp = g->h_rp.data();
+  const int32_t* ci = g->h_ci.data();
+  // bipartite check: every source row points into the targets and every target row into the sources
+  for (int64_t v = src_lo; v < src_hi; ++v)
+    for (int64_t e = rp[v]; e < rp[v + 1]; ++e)
+      if (ci[e] < tgt_lo || ci[e] >= tgt_hi)
+        return fail(BLP_E_UNSUP, "blp_topk_create: graph is not bipartite between the given ranges");
+  for (int64_t v = tgt_lo; v < tgt_hi; ++v)
+    for (int64_t e = rp[v]; e < rp[v + 1]; ++e)
+      if (ci[e] < src_lo || ci[e] >= src_hi)
+        return fail(BLP_E_UNSUP, "blp_topk_create: graph is not bipartite between the given ranges");
+  int rc = set_device(g);
+  if (rc) return rc;
+  auto* t = new blp_topk();
+  t->g = g;
+  t->slo = src_lo;
+  t->shi = src_hi;
+  t->tlo = tgt_lo;
+  t->thi = tgt_hi;
+  t->T = tgt_hi - tgt_lo;
+  t->pbase = rp[src_lo];
+  const int64_t T = t->T;
+  std::vector<int32_t> order(T), perm(T), inv(T), tdeg(T);
+  for (int64_t i = 0; i < T; ++i) order[i] = (int32_t)i;
+  std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
+    return rp[tgt_lo + a + 1] - rp[tgt_lo + a] > rp[tgt_lo + b + 1] - rp[tgt_lo + b];
+  });
+  for (int64_t j = 0; j < T; ++j) {
+    perm[order[j]] = (int32_t)j;
+    inv[j] = (int32_t)(tgt_lo + order[j]);
+    tdeg[j] = (int32_t)(rp[tgt_lo + order[j] + 1] - rp[tgt_lo + order[j]]);
+  }
+  // counter tiers: CN(x, b) <= |N(b)|, so |N(b)| <= 255 fits a u8 and <= 65535 a u16.
+  // BLP_TOPK_T8 / BLP_TOPK_T16 lower the limits and BLP_TOPK_ACC_WORDS the counter space
+  // (test knobs for the u32 tier and the multi-chunk path).
+  const int64_t t8 = std::min<int64_t>(255, env_i64("BLP_TOPK_T8", 255));
+  const int64_t t16 = std::min<int64_t>(65535, env_i64("BLP_TOPK_T16", 65535));
+  t->acc_words = std::max<int64_t>(64, std::min<int64_t>(TK_ACC_WORDS, env_i64("BLP_TOPK_ACC_WORDS", TK_ACC_WORDS)));
+  t->n32 = 0;
+  while (t->n32 < T && tdeg[t->n32] > t16) ++t->n32;
+  t->n16 = t->n32;
+  while (t->n16 < T && tdeg[t->n16] > t8) ++t->n16;
+  // source rows with permuted target ids, each sorted (multi-threaded)
+  const int64_t m = rp[src_hi] - t->pbase;
+  std::vector<int32_t> pci(std::max<int64_t>(m, 1));
+  {
+    const int nth = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<std::thread> th;
+    const int64_t nrows = src_hi - src_lo;
+    for (int q = 0; q < nth; ++q) {
+      th.emplace_back([&, q]() {
+        const int64_t r0 = src_lo + nrows * q / nth, r1 = src_lo + nrows * (q + 1) / nth;
+        for (int64_t v = r0; v < r1; ++v) {
+          int32_t* row = pci.data() + (rp[v] - t->pbase);
+          const int64_t len = rp[v + 1] - rp[v];
+          for (int64_t e = 0; e < len; ++e) row[e] = perm[ci[rp[v] + e] - tgt_lo];
+          std::sort(row, row + len);
+        }
+      });
+    }
+    for (auto& h : th) h.join();
+  }
+  // Adamic-Adar weight bounds over the sources that can reach a distance-3 target (degree >= 2)
+  if (g->d_aaw_fx && src_hi > src_lo) {
+    std::vector<long long> w(src_hi - src_lo);
+    BLP_HIP_OR(hipMemcpy(w.data(), g->d_aaw_fx + src_lo, 8 * w.size(), hipMemcpyDeviceToHost),
+               [&](int r) { delete t; return r; });
+    long long wmin = LLONG_MAX, wmax = 0;
+    for (int64_t v = src_lo; v < src_hi; ++v)
+      if (rp[v + 1] - rp[v] >= 2) {
+        wmin = std::min(wmin, w[v - src_lo]);
+        wmax = std::max(wmax, w[v - src_lo]);
+      }
+    t->have_aa = true;
+    t->ratio = wmax > 0 ? (double)wmin / (double)wmax : 1.0;
+  }
+  plan_chunks(t);
+  auto up = [&](DevBuf& b, const void* h, size_t bytes) -> int {
+    int r = b.reserve(bytes);
+    if (r) return r;
+    BLP_HIP(hipMemcpy(b.p, h, bytes, hipMemcpyHostToDevice));
+    return BLP_OK;
+  };
+  if ((rc = up(t->perm, perm.data(), 4 * T)) || (rc = up(t->inv, inv.data(), 4 * T)) ||
+      (rc = up(t->tdeg, tdeg.data(), 4 * T)) || (rc = up(t->pci, pci.data(), 4 * pci.size())) ||
+      (rc = up(t->d_chunks, t->chunks.data(), sizeof(TkChunk) * t->chunks.size())) ||
+      (rc = t->counters.reserve(64))) {
+    blp_topk_destroy(t);
+    return rc;
+  }
+  *out = t;
+  return BLP_OK;
+}
+
+extern "C" int blp_topk_destroy(blp_topk* t) {
+  if (!t) return BLP_OK;
+  (void)set_device(t->g);
+  for (DevBuf* b : {&t->perm, &t->inv, &t->tdeg, &t->pci, &t->d_chunks, &t->src, &t->keys, &t->cols, &t->ncand,
+                    &t->counters})
+    b->release();
+  timer_release(t->timer);
+  delete t;
+  return BLP_OK;
+}
+
+extern "C" int blp_topk_info(const blp_topk* t, int64_t* n_chunks, int64_t* tier32, int64_t* tier16) {
+  BLP_CHECK(t, BLP_E_ARG, "blp_topk_info: null handle");
+  if (n_chunks) *n_chunks = (int64_t)t->chunks.size();
+  if (tier32) *tier32 = t->n32;
+  if (tier16) *tier16 = t->n16 - t->n32;
+  return BLP_OK;
+}
+
+extern "C" int blp_topk_set_sources(blp_topk* t, const int32_t* src, int64_t n_src) {
+  BLP_CHECK(t && n_src >= 0 && (n_src == 0 || src), BLP_E_ARG, "blp_topk_set_sources: bad arguments");
+  BLP_CHECK(n_src < (int64_t(1) << 31), BLP_E_ARG, "blp_topk_set_sources: too many sources");
+  for (int64_t i = 0; i < n_src; ++i)
+    BLP_CHECK(src[i] >= t->slo && src[i] < t->shi, BLP_E_ARG, "blp_topk_set_sources: source id outside the source range");
+  int rc = set_device(t->g);
+  if (rc) return rc;
+  if ((rc = t->src.reserve(4 * std::max<int64_t>(n_src, 1)))) return rc;
+  if (n_src) BLP_HIP(hipMemcpy(t->src.p, src, 4 * n_src, hipMemcpyHostToDevice));
+  t->n_src = n_src;
+  t->ran = false;
+  return BLP_OK;
+}
+
+extern "C" int blp_topk_run(blp_topk* t, int k, uint32_t mask) {
+  BLP_CHECK(t && k >= 1 && k <= TK_KMAX, BLP_E_ARG, "blp_topk_run: k must be in [1, 256]");
+  BLP_CHECK(mask && !(mask & ~7u), BLP_E_ARG, "blp_topk_run: bad method mask");
+  BLP_CHECK(!(mask & BLP_ADAMIC) || t->have_aa, BLP_E_STATE, "blp_topk_run: graph has no Adamic-Adar weights");
+  int rc = set_device(t->g);
+  if (rc) return rc;
+  const size_t nk = (size_t)std::max<int64_t>(t->n_src, 1) * k;
+  if ((rc = t->keys.reserve(3 * nk * 8)) || (rc = t->cols.reserve(3 * nk * 4)) ||
+      (rc = t->ncand.reserve(8 * std::max<int64_t>(t->n_src, 1))))
+    return rc;
+  hipStream_t st = t->g->stream;
+  BLP_HIP(hipMemsetAsync(t->counters.p, 0, 64, st));
+  TkArgs a{};
+  a.rp = t->g->d_rp;
+  a.ci = t->g->d_ci;
+  a.pci = t->pci.as<int32_t>();
+  a.pbase = t->pbase;
+  a.perm = t->perm.as<int32_t>();
+  a.inv = t->inv.as<int32_t>();
+  a.tdeg = t->tdeg.as<int32_t>();
+  a.aaw = t->g->d_aaw_fx;
+  a.src = t->src.as<int32_t>();
+  a.n_src = (int)t->n_src;
+  a.tlo = t->tlo;
+  a.T = t->T;
+  a.chunks = t->d_chunks.as<TkChunk>();
+  a.n_chunks = (int)t->chunks.size();
+  a.aa_chunk = t->aa_chunk;
+  a.k = k;
+  a.mask = mask;
+  a.ratio = t->ratio;
+  a.hcap = (int)std::max<int64_t>(0, std::min<int64_t>(TK_HCAP, env_i64("BLP_TOPK_HCAP", TK_HCAP)));
+  a.keys = t->keys.as<unsigned long long>();
+  a.cols = t->cols.as<int32_t>();
+  a.ncand = t->ncand.as<int64_t>();
+  a.counters = t->counters.as<unsigned long long>();
+  hipEvent_t t0;
+  if ((rc = timer_begin(t->timer, st, &t0))) return rc;
+  if (t->n_src) {
+    const int grid = (int)std::min<int64_t>(t->g->n_cu, t->n_src);
+    hipLaunchKernelGGL(k_topk, dim3(grid), dim3(TK_NT), 0, st, a);
+    BLP_HIP(hipGetLastError());
+  }
+  if ((rc = timer_end(t->timer, st, t0))) return rc;
+  t->k = k;
+  t->mask = mask;
+  t->ran = true;
+  return BLP_OK;
+}
+
+extern "C" int blp_topk_fetch(blp_topk* t, uint32_t method, int32_t* cols, double* scores, int64_t* n_cand) {
+  BLP_CHECK(t && t->ran, BLP_E_STATE, "blp_topk_fetch: no completed run");
+  BLP_CHECK(method == BLP_CN || method == BLP_JACCARD || method == BLP_ADAMIC, BLP_E_ARG,
+            "blp_topk_fetch: method must be one of BLP_CN, BLP_JACCARD, BLP_ADAMIC");
+  BLP_CHECK(t->mask & method, BLP_E_STATE, "blp_topk_fetch: method was not requested in the run");
+  int rc = set_device(t->g);
+  if (rc) return rc;
+  BLP_HIP(hipStreamSynchronize(t->g->stream));
+  const int m = method == BLP_CN ? 0 : method == BLP_JACCARD ? 1 : 2;
+  const size_t nk = (size_t)t->n_src * t->k;
+  if (nk && (cols || scores)) {
+    std::vector<unsigned long long> keys(nk);
+    std::vector<int32_t> c(nk);
+    BLP_HIP(hipMemcpy(keys.data(), t->keys.as<unsigned long long>() + m * nk, 8 * nk, hipMemcpyDeviceToHost));
+    BLP_HIP(hipMemcpy(c.data(), t->cols.as<int32_t>() + m * nk, 4 * nk, hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < nk; ++i) {
+      if (cols) cols[i] = c[i];
+      if (scores) {
+        double v = 0.0;
+        if (c[i] >= 0) {
+          if (m == 0) v = (double)keys[i];
+          else if (m == 1) { memcpy(&v, &keys[i], 8); }
+          else v = (double)(long long)keys[i] * (1.0 / AA_SCALE);
+        }
+        scores[i] = v;
+      }
+    }
+  }
+  if (n_cand && t->n_src) BLP_HIP(hipMemcpy(n_cand, t->ncand.p, 8 * t->n_src, hipMemcpyDeviceToHost));
+  return BLP_OK;
+}
+
+extern "C" int blp_topk_stats(blp_topk* t, int which, double* total_ms, int64_t* launches) {
+  BLP_CHECK(t && which >= 0 && which <= 4, BLP_E_ARG, "blp_topk_stats: bad arguments");
+  int rc = set_device(t->g);
+  if (rc) return rc;
+  if (which == 0) {
+    if ((rc = timer_collect(t->timer))) return rc;
+    if (total_ms) *total_ms = t->timer.total_ms;
+    if (launches) *launches = t->timer.launches;
+    return BLP_OK;
+  }
+  // 1 / 2: sources whose AA went through the candidate hash / direct accumulation;
+  // 3: sum of |H2(x)|; 4: sum over x and w in H2(x) of |N(w)| (the push volume of one pass)
+  BLP_HIP(hipStreamSynchronize(t->g->stream));
+  unsigned long long c[8];
+  BLP_HIP(hipMemcpy(c, t->counters.p, 64, hipMemcpyDeviceToHost));
+  if (total_ms) *total_ms = 0.0;
+  if (launches) *launches = (int64_t)c[which];
+  return BLP_OK;
+}
+
+extern "C" int blp_topk_stats_reset(blp_topk* t) {
+  BLP_CHECK(t, BLP_E_ARG, "blp_topk_stats_reset: null handle");
+  int rc = set_device(t->g);
+  if (rc) return rc;
+  if ((rc = timer_collect(t->timer))) return rc;
+  t->timer.total_ms = 0.0;
+  t->timer.launches = 0;
+  return BLP_OK;
+}

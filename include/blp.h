@@ -44,6 +44,7 @@ typedef struct blp_graph blp_graph;
 typedef struct blp_batch blp_batch;
 typedef struct blp_svd blp_svd;
 typedef struct blp_walk blp_walk;
+typedef struct blp_topk blp_topk;
 
 /* ---------------------------------------------------------------- runtime */
 const char* blp_last_error(void);
@@ -129,6 +130,34 @@ int blp_batch_stats_reset(blp_batch* b);
 int blp_hop3_sample(blp_graph* g, const int32_t* src, int64_t n_src, const int32_t* pos_off,
                     const int32_t* pos_y, double rate, uint64_t seed, int32_t* out_x,
                     int32_t* out_y, uint8_t* out_label, int64_t cap, int64_t* n_out);
+
+/* ---------------------------------------------------------------- full-candidate top-k
+ * BASELINE.json configs[2] ("Jaccard + Adamic-Adar full-candidate top-k"; SURVEY.md §8(b)
+ * blp_topk). The reference scores only the sampled pairs of examples.json; this scores, for
+ * each source x, EVERY target b at exact distance 3 (the complete candidate set
+ * GetNodesAtHop(G,x,3) that dataset_maker.py:139 samples from) with similarity.py's
+ * common_neighbors / jaccard / adamic_adar of (H2(x), N(b)) (similarity.py:108-126, the
+ * user-side orientation of :20-61) and keeps the k best per method: score descending, then
+ * dense target id ascending. Scores are bit-identical to blp_score_pairs on the same pair.
+ * The graph must be bipartite between [src_lo, src_hi) and [tgt_lo, tgt_hi) (BLP_E_UNSUP
+ * otherwise); both ranges are dense ids (users / businesses of a reference graph.txt).
+ *   blp_topk_create:      builds the degree-ordered target numbering and permuted source rows.
+ *   blp_topk_set_sources: uploads the sources (kept in HBM across runs).
+ *   blp_topk_run:         k in [1, 256], mask of BLP_CN | BLP_JACCARD | BLP_ADAMIC; async.
+ *   blp_topk_fetch:       one method's [n_src][k] lists (col -1 / score 0 past the end) and
+ *                         n_cand[i] = |H3(src[i])|, the number of candidates scored.
+ *   blp_topk_stats:       which 0: kernel ms/launches; 1 / 2: sources whose Adamic-Adar took
+ *                         the candidate-hash / direct-accumulation path (in *launches);
+ *                         3: sum of |H2(x)|; 4: sum over x and w in H2(x) of |N(w)| (work). */
+int blp_topk_create(blp_graph* g, int64_t src_lo, int64_t src_hi, int64_t tgt_lo, int64_t tgt_hi,
+                    blp_topk** out);
+int blp_topk_destroy(blp_topk* t);
+int blp_topk_info(const blp_topk* t, int64_t* n_chunks, int64_t* tier32, int64_t* tier16);
+int blp_topk_set_sources(blp_topk* t, const int32_t* src, int64_t n_src);
+int blp_topk_run(blp_topk* t, int k, uint32_t mask);
+int blp_topk_fetch(blp_topk* t, uint32_t method, int32_t* cols, double* scores, int64_t* n_cand);
+int blp_topk_stats(blp_topk* t, int which, double* total_ms, int64_t* launches);
+int blp_topk_stats_reset(blp_topk* t);
 
 /* ---------------------------------------------------------------- truncated-SVD scorer
  * Replaces the reconstruction of svd.svd_user_business (svd.py:25-30): the host keeps the

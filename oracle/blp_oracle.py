@@ -210,3 +210,45 @@ def precision_at(examples, predictions, k=20):
 def hop3_candidates(adj, u):
     """dataset_maker.py:138-139: snap.GetNodesAtHop(G, u, 3)."""
     return nodes_at_hop(adj, u, 3)
+
+
+# --------------------------------------------------------------------------- full-candidate top-k
+AA_SCALE = 2.0 ** 40  # the engine's fixed-point Adamic-Adar unit (exact integer sums)
+
+
+def aa_fixed(h2, nb, adj):
+    """adamic_adar(h2, nb, G) (similarity.py:116-126) summed in 2^-40 fixed point: each term
+    (log deg)^-1 is rounded to the nearest 2^-40 (half-even, as llrint) and the integers are
+    added, so the sum is independent of set order (the reference's own order is Python set
+    order; the two agree to ~1e-12 relative)."""
+    fx = 0
+    for w in h2.intersection(nb):
+        d = degree(adj, w)
+        if d > 1:
+            fx += round(math.log(d) ** -1 * AA_SCALE)
+    return fx
+
+
+def topk_full_candidates(adj, x, k, method):
+    """BASELINE.json configs[2]: score EVERY node b at exact distance 3 of x (the candidate
+    set dataset_maker.py:139 samples from) with similarity.py's measure of (H2(x), N(b))
+    (similarity.py:48-58 orientation: H2 of the source, hop-1 set of the candidate) and keep
+    the k best: score descending, then node id ascending. The reference has no top-k; this
+    composes its scorers. Returns ([(b, score)], n_candidates)."""
+    h2 = nodes_at_hop(adj, x, 2)
+    cands = nodes_at_hop(adj, x, 3)
+    rows = []
+    for b in cands:
+        nb = nodes_at_hop(adj, b, 1)
+        if method == "common_neighbors":
+            s = common_neighbors(h2, nb)
+            key = s
+        elif method == "jaccard":
+            s = jaccard(h2, nb)
+            key = s
+        else:
+            key = aa_fixed(h2, nb, adj)
+            s = key / AA_SCALE
+        rows.append((-key, b, s))
+    rows.sort()
+    return [(b, s) for _, b, s in rows[:k]], len(cands)

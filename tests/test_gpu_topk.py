@@ -1,0 +1,155 @@
+"""GPU full-candidate top-k (BASELINE.json configs[2]) vs the oracle.
+
+The oracle (oracle/blp_oracle.topk_full_candidates) scores every exact-distance-3 candidate
+with the reference's set formulas (similarity.py:108-126) and sorts by (score desc, id asc).
+Bit-exact bars: CN and Jaccard lists (ids and scores), |H3| counts, and Adamic-Adar in the
+engine's 2^-40 fixed point (order-independent, equal to blp_score_pairs' values); the
+fixed-point sums agree with the reference's float sums to 1e-9 relative (checked below).
+The reference itself has no top-k: the composition is "parity unpinned" beyond its scorers.
+"""
+import math
+
+import numpy as np
+import pytest
+
+import blp
+import blp_oracle as bo
+from helpers import bipartite_edges
+
+pytestmark = pytest.mark.gpu
+
+METHODS = ["common_neighbors", "jaccard", "adamic_adar"]
+ALL = blp.CN | blp.JACCARD | blp.ADAMIC
+
+
+def adj_of(a, b):
+    adj = {}
+    for x, y in zip(a.tolist(), b.tolist()):
+        adj.setdefault(x, set()).add(y)
+        adj.setdefault(y, set()).add(x)
+    return adj
+
+
+def check_against_oracle(G, T, adj, src, k, mask=ALL, methods=METHODS):
+    res = T(src, k=k, mask=mask)
+    for m in methods:
+        cols, scores, ncand = res[m]
+        for i, x in enumerate(src):
+            exp, n_exp = bo.topk_full_candidates(adj, int(G.node_ids[x]), k, m)
+            assert ncand[i] == n_exp, (m, i)
+            got_ids = [int(G.node_ids[c]) for c in cols[i] if c >= 0]
+            assert got_ids == [b for b, _ in exp], (m, i, got_ids[:5], exp[:5])
+            assert np.all(cols[i][len(exp):] == -1)
+            got_s = scores[i][: len(exp)].tolist()
+            assert got_s == [s for _, s in exp], (m, i)
+    return res
+
+
+@pytest.fixture(scope="module")
+def small(gpu):
+    rng = np.random.default_rng(3)
+    a, b = bipartite_edges(rng, 3000, 300, 20000)
+    G = blp.DeviceGraph(a, b, device=gpu)
+    return G, adj_of(a, b), rng
+
+
+def test_topk_all_methods_match_oracle(small):
+    G, adj, rng = small
+    T = blp.TopK(G, "user")
+    src = rng.choice(G.n_col0, 40, replace=False)
+    check_against_oracle(G, T, adj, src, 20)
+
+
+def test_topk_u32_tier_and_multi_chunk(small, monkeypatch):
+    """Tiny tier limits force u32/u16 counters; a tiny counter space forces many chunks (and
+    the direct Adamic-Adar path)."""
+    G, adj, rng = small
+    src = rng.choice(G.n_col0, 16, replace=False)
+    monkeypatch.setenv("BLP_TOPK_T8", "20")
+    monkeypatch.setenv("BLP_TOPK_T16", "60")
+    T = blp.TopK(G, "user")
+    info = T.info()
+    assert info["chunks"] == 1 and info["tier32"] > 0 and info["tier16"] > 0
+    check_against_oracle(G, T, adj, src, 20)
+    monkeypatch.setenv("BLP_TOPK_ACC_WORDS", "40")
+    T2 = blp.TopK(G, "user")
+    assert T2.info()["chunks"] >= 3
+    check_against_oracle(G, T2, adj, src, 20)
+    assert T2.stats(2)[1] == len(src)  # every source took the direct Adamic-Adar path
+
+
+def test_topk_aa_direct_path_matches_hash_path(small, monkeypatch):
+    G, adj, rng = small
+    src = rng.choice(G.n_col0, 32, replace=False)
+    T = blp.TopK(G, "user")
+    r1 = T(src, k=15, mask=blp.ADAMIC)["adamic_adar"]
+    assert T.stats(1)[1] > 0
+    monkeypatch.setenv("BLP_TOPK_HCAP", "0")
+    r2 = T(src, k=15, mask=blp.ADAMIC)["adamic_adar"]
+    assert T.stats(2)[1] == len(src)
+    for x, y in zip(r1, r2):
+        assert np.array_equal(x, y)
+
+
+def test_topk_scores_equal_pair_scorer(small):
+    """Top-k scores are the pair kernel's values bit-for-bit; AA within 1e-9 of float sums."""
+    G, adj, rng = small
+    src = rng.choice(G.n_col0, 24, replace=False)
+    res = blp.TopK(G, "user")(src, k=25, mask=ALL)
+    for m, key in (("common_neighbors", "cn"), ("jaccard", "jaccard"), ("adamic_adar", "adamic")):
+        cols, scores, _ = res[m]
+        ok = cols >= 0
+        x = np.repeat(src, cols.shape[1]).reshape(cols.shape)[ok]
+        pair = G.score_pairs(x, cols[ok], 7)[key]
+        assert np.array_equal(pair.astype(np.float64), scores[ok]), m
+    cols, scores, _ = res["adamic_adar"]
+    for i, x in enumerate(src[:6]):
+        h2 = bo.nodes_at_hop(adj, int(G.node_ids[x]), 2)
+        for c, s in zip(cols[i], scores[i]):
+            if c >= 0:
+                ref = bo.adamic_adar(h2, bo.nodes_at_hop(adj, int(G.node_ids[c]), 1), adj)
+                assert math.isclose(s, ref, rel_tol=1e-9)
+
+
+def test_topk_business_side(small):
+    G, adj, rng = small
+    T = blp.TopK(G, "business")
+    src = G.n_col0 + rng.choice(G.n - G.n_col0, 12, replace=False)
+    check_against_oracle(G, T, adj, src, 10)
+
+
+def test_topk_edge_cases(gpu):
+    # user 0 shares business 10 with user 1, who also reviewed 11 and 12; user 2 is alone on 13
+    a = np.array([0, 1, 1, 1, 2, 3, 3], np.int64)
+    b = np.array([10, 10, 11, 12, 13, 11, 12], np.int64)
+    G = blp.DeviceGraph(a, b, device=gpu)
+    adj = adj_of(a, b)
+    T = blp.TopK(G, "user")
+    src = G.dense([0, 1, 2, 3])
+    res = check_against_oracle(G, T, adj, src, 5)
+    cols, _, ncand = res["jaccard"]
+    assert ncand.tolist() == [2, 0, 0, 1]  # user 1: 11/12 are its own businesses
+    assert (cols[2] == -1).all()
+    check_against_oracle(G, T, adj, src, 1)  # k = 1 (ties broken by id)
+
+
+def test_topk_rejects_non_bipartite(gpu):
+    a = np.array([0, 1, 2], np.int64)
+    b = np.array([1, 2, 0], np.int64)  # triangle: column-0 ids also appear in column 1
+    G = blp.DeviceGraph(a, b, device=gpu)
+    with pytest.raises(blp.BLPError):
+        blp.TopK(G, "user")
+
+
+def test_topk_repeat_is_deterministic(small):
+    G, adj, rng = small
+    src = rng.choice(G.n_col0, 64, replace=False)
+    T = blp.TopK(G, "user")
+    T.set_sources(src)
+    outs = []
+    for _ in range(2):
+        T.run(20, ALL)
+        outs.append([T.fetch(m) for m in METHODS])
+    for r1, r2 in zip(*outs):
+        for x, y in zip(r1, r2):
+            assert np.array_equal(x, y)

@@ -219,3 +219,27 @@ def test_c_oracle_matches_python_oracle_random(edges, seed):
         assert cn[i] == O.common_neighbors(h2, n1)
         assert jac[i] == O.jaccard(h2, n1)
         assert math.isclose(aa[i], O.adamic_adar(h2, n1, adj), rel_tol=1e-12, abs_tol=1e-300)
+
+
+@pytest.mark.parametrize("split", ["bip/train", "bip/test"])
+def test_topk_oracle_composes_reference_scorers(split):
+    """The full-candidate top-k oracle (config 3) scores each distance-3 candidate with the
+    reference's own formulas: every (user, business) pair of the golden examples that is a
+    distance-3 candidate gets the reference's CN / Jaccard exactly and its Adamic-Adar to 1e-9."""
+    adj = O.load_edge_list(os.path.join(GOLDEN, split, "graph.txt"))
+    ex = golden(split, "examples.json")
+    ref = {m: golden(split, f) for m, f in zip(METHODS, U_FILES)}
+    checked = 0
+    for u in list(ex)[:12]:
+        if int(u) not in adj:
+            continue
+        tops = {m: dict(O.topk_full_candidates(adj, int(u), 10**9, m)[0]) for m in METHODS}
+        for b in ex[u]:
+            if int(b) in tops["jaccard"]:
+                assert tops["common_neighbors"][int(b)] == ref["common_neighbors"][u][b]
+                assert tops["jaccard"][int(b)] == ref["jaccard"][u][b]
+                assert math.isclose(tops["adamic_adar"][int(b)], ref["adamic_adar"][u][b], rel_tol=1e-9)
+                checked += 1
+        ranked = O.topk_full_candidates(adj, int(u), 10**9, "jaccard")[0]
+        assert ranked == sorted(ranked, key=lambda t: (-t[1], t[0]))
+    assert checked > 20
