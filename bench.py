@@ -364,7 +364,7 @@ def run_topk(args):
     T = TopK(G, "user")
     T.set_sources(src)
     log("top-k engine: %s in %.1fs" % (T.info(), time.time() - t0))
-    mask = blp.JACCARD | blp.ADAMIC
+    mask = args.topk_mask
     for _ in range(args.warmup):
         T.run(args.topk, mask)
     blp.device_sync(dev)
@@ -380,18 +380,20 @@ def run_topk(args):
     t_max = dist.max(t_local) / args.steps
     kms, kn = T.stats(0)
     kern_s = kms / 1e3 / max(kn, 1)
-    cols_j, sc_j, ncand = T.fetch("jaccard")
-    cols_a, sc_a, _ = T.fetch("adamic_adar")
+    first = [m for m, bit in (("common_neighbors", 1), ("jaccard", 2), ("adamic_adar", 4)) if mask & bit][0]
+    ncand = T.fetch(first)[2]
     pairs = int(ncand.sum())
     h2_sum, push_sum = T.stats(3)[1], T.stats(4)[1]
     hash_src, direct_src = T.stats(1)[1], T.stats(2)[1]
-    byts = topk_alg_bytes(G, src, h2_sum, push_sum, args.topk, 2)
+    byts = topk_alg_bytes(G, src, h2_sum, push_sum, args.topk, bin(mask).count("1"))
     out = {
         "metric": METRIC, "value": dist.sum(pairs) / t_max, "unit": "pairs/s", "n_gpus": dist.world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * t_max, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "int32", "data": "synthetic",
         "config": {"workload": "config3: config-2 graph (%d unique edges); %d users/GPU, every exact hop-3 business "
-                               "scored (Jaccard + Adamic-Adar), top-%d per method" % (G.nnz // 2, len(src), args.topk),
+                               "scored (%s), top-%d per method" % (G.nnz // 2, len(src), "+".join(
+                                   n for n, bit in (("CN", 1), ("Jaccard", 2), ("Adamic-Adar", 4)) if mask & bit),
+                                   args.topk),
                    "pairs_per_gpu": pairs, "global_batch": int(dist.sum(pairs)),
                    "parallelism": "replicas x%d (graph replicated, users split, no collective)" % dist.world},
         "roofline": {"bound": "hbm", "achieved": byts / kern_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -399,7 +401,9 @@ def run_topk(args):
                      "kernel": "k_topk", "kernel_ms": 1e3 * kern_s, "alg_bytes_per_launch": byts},
         "work": {"sum_h2": h2_sum, "sum_push": push_sum, "aa_hash_sources": hash_src, "aa_direct_sources": direct_src},
     }
-    if dist.rank == 0 and not args.no_parity:
+    if dist.rank == 0 and not args.no_parity and mask == blp.JACCARD | blp.ADAMIC:
+        cols_j, sc_j, _ = T.fetch("jaccard")
+        cols_a, sc_a, _ = T.fetch("adamic_adar")
         out["parity"] = topk_parity(G, src, args.topk, {"jaccard": (cols_j, sc_j), "adamic_adar": (cols_a, sc_a),
                                                         "ncand": ncand})
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:
@@ -425,6 +429,7 @@ def main():
                     help="similarity: config 2 (default); topk: config 3 full-candidate Jaccard + Adamic-Adar "
                          "top-k; svd: config 4 rank-64 truncated-SVD scorer")
     ap.add_argument("--topk", type=int, default=20)
+    ap.add_argument("--topk-mask", type=int, default=6, help="methods of --mode topk (default Jaccard + AA)")
     args = ap.parse_args()
     if args.mode == "svd":
         return run_svd(args)

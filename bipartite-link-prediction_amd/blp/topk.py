@@ -15,7 +15,7 @@ _P, _I64, _I32, _U32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_u
 _PI64 = ctypes.POINTER(ctypes.c_int64)
 _lib.register("blp_topk_create", [_P, _I64, _I64, _I64, _I64, ctypes.POINTER(ctypes.c_void_p)])
 _lib.register("blp_topk_destroy", [_P])
-_lib.register("blp_topk_info", [_P, _PI64, _PI64, _PI64])
+_lib.register("blp_topk_info", [_P, _PI64, _PI64, _PI64, _PI64])
 _lib.register("blp_topk_set_sources", [_P, _P, _I64])
 _lib.register("blp_topk_run", [_P, _I32, _U32])
 _lib.register("blp_topk_fetch", [_P, _U32, _P, _P, _P])
@@ -46,9 +46,9 @@ class TopK:
         self.mask = 0
 
     def info(self):
-        a, b, c = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
-        check(lib().blp_topk_info(self.handle, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
-        return {"chunks": a.value, "tier32": b.value, "tier16": c.value}
+        a, b, c, d = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        check(lib().blp_topk_info(self.handle, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c), ctypes.byref(d)))
+        return {"chunks": a.value, "tier32": b.value, "tier16": c.value, "wedge_entries": d.value}
 
     def set_sources(self, src):
         self.src = _lib.as_i32(src)

@@ -39,8 +39,9 @@ constexpr int TK_SEL = 1024;          // selection buffer entries (also the AA h
 constexpr int TK_HCAP = TK_SEL / 2;   // AA candidates handled by the hash (load <= 1/2)
 constexpr int TK_SEG = 256;           // N(x) entries staged per batch
 constexpr int TK_FILT = 128;          // words of the N'(x) membership filter (4096 bits)
-constexpr int TK_ACC_WORDS = 36224;   // counter space: 141.5 KiB
+constexpr int TK_ACC_WORDS = 35712;   // counter space: 139.5 KiB
 constexpr int TK_KMAX = 256;
+constexpr int TK_RB = 16;           // row entries loaded up front per element
 constexpr uint32_t TK_EMPTY = 0xFFFFFFFFu;
 
 // Counter chunk over permuted target ids [c0, c1): [c0, b32) u32, [b32, b16) u16 packed
@@ -58,7 +59,10 @@ struct TkArgs {
   const int32_t* perm;  // [T] target (dense id - tlo) -> permuted id
   const int32_t* inv;   // [T] permuted id -> dense target id
   const int32_t* tdeg;  // [T] |N(b)| by permuted id
-  const long long* aaw; // Adamic-Adar weights, fixed point (dense ids)
+  const long long* wtab;  // Adamic-Adar weight (fixed point) of a source by its degree
+  const int64_t* x2_off;  // [target-side CSR entries + 1] start of each wedge row in x2 (or null)
+  const int32_t* x2;      // wedge rows: for each target b' and member w of N(b'), N'(w)
+  int64_t kbase;          // rp[tlo]
   const int32_t* src;
   int n_src;
   int64_t tlo, T;
@@ -80,6 +84,7 @@ struct TkShared {
   unsigned long long key[TK_SEL];
   int32_t col[TK_SEL];
   int64_t seg_rs[TK_SEG];
+  int64_t seg_kx[TK_SEG];
   int64_t seg_off[TK_SEG + 1];
   int32_t seg_p[TK_SEG];
   uint32_t filt[TK_FILT];
@@ -173,6 +178,14 @@ __device__ long long push_pass(const TkArgs& a, TkShared& s, int x, int64_t xb, 
       len = a.rp[b + 1] - rs;
       s.seg_rs[tid] = rs;
       s.seg_p[tid] = a.perm[b - a.tlo];
+      if (a.x2) {  // position of x in N(b') (sorted): its own wedge is skipped
+        int64_t lo = rs, hi = rs + len;
+        while (lo < hi) {
+          const int64_t mid = (lo + hi) >> 1;
+          if (a.ci[mid] < x) lo = mid + 1; else hi = mid;
+        }
+        s.seg_kx[tid] = lo;
+      }
     }
     // exclusive scan of the segment lengths (ns <= TK_SEG <= TK_NT)
     {
@@ -191,23 +204,53 @@ __device__ long long push_pass(const TkArgs& a, TkShared& s, int x, int64_t xb, 
       __syncthreads();
     }
     const int64_t E = s.seg_off[ns];
+    // Software-pipelined walk. Element idx of the batch is (segment b', i-th member w of
+    // N(b')); its row N'(w) is located either through the expanded wedge array (x2: the rows
+    // of N(b')'s members stored back to back, read sequentially) or through rp[w]. The next
+    // element's row bounds are fetched while the current row is processed, and the first
+    // TK_RB entries of a row are loaded as independent predicated loads (rows are short).
+    const int32_t* base = a.x2 ? a.x2 : a.pci;
     int sg = 0;
-    for (int64_t idx = tid; idx < E; idx += TK_NT) {
-      while (s.seg_off[sg + 1] <= idx) ++sg;
-      const int w = a.ci[s.seg_rs[sg] + (idx - s.seg_off[sg])];
-      if (w == x) continue;
-      const int32_t pp = s.seg_p[sg];
-      const int64_t r0 = a.rp[w];
-      const int len_w = (int)(a.rp[w + 1] - r0);
-      const int32_t* roww = a.pci + (r0 - a.pbase);
+    auto fetch = [&](int64_t id, int64_t& r0, int64_t& r1, int32_t& pp) -> bool {
+      while (s.seg_off[sg + 1] <= id) ++sg;
+      const int64_t k = s.seg_rs[sg] + (id - s.seg_off[sg]);
+      pp = s.seg_p[sg];
+      if (a.x2) {
+        if (k == s.seg_kx[sg]) return true;  // x itself
+        r0 = a.x2_off[k - a.kbase];
+        r1 = a.x2_off[k - a.kbase + 1];
+        return false;
+      }
+      const int w = a.ci[k];
+      if (w == x) return true;
+      r0 = a.rp[w] - a.pbase;
+      r1 = a.rp[w + 1] - a.pbase;
+      return false;
+    };
+    int64_t idx = tid, r0n = 0, r1n = 0;
+    int32_t ppn = 0;
+    bool skipn = true;
+    if (idx < E) skipn = fetch(idx, r0n, r1n, ppn);
+    while (idx < E) {
+      const bool skip = skipn;
+      const int64_t r0 = r0n;
+      const int len_w = (int)(r1n - r0n);
+      const int32_t pp = ppn;
+      const int32_t* roww = base + r0;
+      int32_t e[TK_RB];
+#pragma unroll
+      for (int j = 0; j < TK_RB; ++j) e[j] = (!skip && j < len_w) ? roww[j] : 0x7FFFFFFF;
+      idx += TK_NT;
+      if (idx < E) skipn = fetch(idx, r0n, r1n, ppn);
+      if (skip) continue;
       bool owned = true;
-      for (int j = 0; j < len_w; ++j) {
-        const int32_t e = roww[j];
-        if (e >= pp) break;
-        if (in_row_x(s, rowx, du, e)) {
-          owned = false;
-          break;
-        }
+#pragma unroll
+      for (int j = 0; j < TK_RB; ++j)
+        if (e[j] < pp && in_row_x(s, rowx, du, e[j])) owned = false;
+      for (int j = TK_RB; j < len_w && owned; ++j) {
+        const int32_t ej = roww[j];
+        if (ej >= pp) break;
+        if (in_row_x(s, rowx, du, ej)) owned = false;
       }
       if (!owned) continue;
       if (MODE == 0) {
@@ -215,25 +258,34 @@ __device__ long long push_pass(const TkArgs& a, TkShared& s, int x, int64_t xb, 
           ++h2;
           npush += len_w;
         }
-        for (int j = 0; j < len_w; ++j) {
-          const int32_t e = roww[j];
-          if (e >= c.c0 && e < c.c1) acc_add(s.acc, c, e);
+#pragma unroll
+        for (int j = 0; j < TK_RB; ++j)
+          if (j < len_w && e[j] >= c.c0 && e[j] < c.c1) acc_add(s.acc, c, e[j]);
+        for (int j = TK_RB; j < len_w; ++j) {
+          const int32_t ej = roww[j];
+          if (ej >= c.c0 && ej < c.c1) acc_add(s.acc, c, ej);
         }
       } else if (MODE == 1) {
-        const unsigned long long wfx = (unsigned long long)a.aaw[w];
-        for (int j = 0; j < len_w; ++j) {
-          const int32_t e = roww[j];
-          if (acc_get(s.acc, c, e) >= thr) {
-            int h = hash_slot(e);
-            while (s.col[h] != e) h = (h + 1) & (TK_SEL - 1);
+        const unsigned long long wfx = (unsigned long long)a.wtab[len_w];
+        auto push1 = [&](int32_t ej) {
+          if (acc_get(s.acc, c, ej) >= thr) {
+            int h = hash_slot(ej);
+            while (s.col[h] != ej) h = (h + 1) & (TK_SEL - 1);
             atomicAdd(&s.key[h], wfx);
           }
-        }
+        };
+#pragma unroll
+        for (int j = 0; j < TK_RB; ++j)
+          if (j < len_w) push1(e[j]);
+        for (int j = TK_RB; j < len_w; ++j) push1(roww[j]);
       } else {
-        const unsigned long long wfx = (unsigned long long)a.aaw[w];
-        for (int j = 0; j < len_w; ++j) {
-          const int32_t e = roww[j];
-          if (e >= d0 && e < d1) atomicAdd(&acc64[e - d0], wfx);
+        const unsigned long long wfx = (unsigned long long)a.wtab[len_w];
+#pragma unroll
+        for (int j = 0; j < TK_RB; ++j)
+          if (j < len_w && e[j] >= d0 && e[j] < d1) atomicAdd(&acc64[e[j] - d0], wfx);
+        for (int j = TK_RB; j < len_w; ++j) {
+          const int32_t ej = roww[j];
+          if (ej >= d0 && ej < d1) atomicAdd(&acc64[ej - d0], wfx);
         }
       }
     }
@@ -519,7 +571,8 @@ struct blp_topk {
   bool have_aa = false;
   std::vector<TkChunk> chunks;
   int64_t aa_chunk = 0;
-  DevBuf perm, inv, tdeg, pci, d_chunks, src, keys, cols, ncand, counters;
+  DevBuf perm, inv, tdeg, pci, d_chunks, src, keys, cols, ncand, counters, wtab, x2_off, x2;
+  int64_t kbase = 0, x2_entries = -1;
   int64_t n_src = 0;
   int k = 0;
   uint32_t mask = 0;
@@ -633,20 +686,63 @@ extern "C" int blp_topk_create(blp_graph* g, int64_t src_lo, int64_t src_hi, int
     }
     for (auto& h : th) h.join();
   }
-  // Adamic-Adar weight bounds over the sources that can reach a distance-3 target (degree >= 2)
+  // Adamic-Adar: a source's weight depends on its degree only (bipartite: no self-loops), so
+  // the kernel reads it from a per-degree table; the bounds use the sources of degree >= 2
+  // (the only ones that reach a distance-3 target).
+  int64_t maxdeg = 0;
+  for (int64_t v = src_lo; v < src_hi; ++v) maxdeg = std::max<int64_t>(maxdeg, rp[v + 1] - rp[v]);
+  std::vector<long long> wtab(maxdeg + 1, 0);
   if (g->d_aaw_fx && src_hi > src_lo) {
     std::vector<long long> w(src_hi - src_lo);
     BLP_HIP_OR(hipMemcpy(w.data(), g->d_aaw_fx + src_lo, 8 * w.size(), hipMemcpyDeviceToHost),
                [&](int r) { delete t; return r; });
     long long wmin = LLONG_MAX, wmax = 0;
-    for (int64_t v = src_lo; v < src_hi; ++v)
-      if (rp[v + 1] - rp[v] >= 2) {
+    for (int64_t v = src_lo; v < src_hi; ++v) {
+      const int64_t d = rp[v + 1] - rp[v];
+      wtab[d] = w[v - src_lo];
+      if (d >= 2) {
         wmin = std::min(wmin, w[v - src_lo]);
         wmax = std::max(wmax, w[v - src_lo]);
       }
+    }
     t->have_aa = true;
     t->ratio = wmax > 0 ? (double)wmin / (double)wmax : 1.0;
   }
+  // Expanded wedge rows: for every target b' (CSR order) and member w of N(b'), N'(w) stored
+  // back to back (sum over sources of deg^2 entries). A source's walk then reads each N(b')'s
+  // wedges sequentially instead of chasing rp[w] -> N(w) per member. Skipped above a memory
+  // budget (BLP_TOPK_EXPAND_MB, default 16 GiB) or with BLP_TOPK_EXPAND=0.
+  const int64_t kbase = rp[tgt_lo], mt = rp[tgt_hi] - kbase;
+  std::vector<int64_t> x2_off;
+  std::vector<int32_t> x2;
+  {
+    int64_t total = 0;
+    for (int64_t v = src_lo; v < src_hi; ++v) total += (rp[v + 1] - rp[v]) * (rp[v + 1] - rp[v]);
+    const int64_t budget = env_i64("BLP_TOPK_EXPAND_MB", 16384) << 20;
+    if (env_i64("BLP_TOPK_EXPAND", 1) != 0 && 4 * total <= budget) {
+      x2_off.resize(mt + 1);
+      x2_off[0] = 0;
+      for (int64_t i = 0; i < mt; ++i) {
+        const int32_t w = ci[kbase + i];
+        x2_off[i + 1] = x2_off[i] + (rp[w + 1] - rp[w]);
+      }
+      x2.resize(std::max<int64_t>(x2_off[mt], 1));
+      const int nth = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+      std::vector<std::thread> th;
+      for (int q = 0; q < nth; ++q) {
+        th.emplace_back([&, q]() {
+          for (int64_t i = mt * q / nth; i < mt * (q + 1) / nth; ++i) {
+            const int32_t w = ci[kbase + i];
+            const int32_t* row = pci.data() + (rp[w] - t->pbase);
+            std::copy(row, row + (rp[w + 1] - rp[w]), x2.data() + x2_off[i]);
+          }
+        });
+      }
+      for (auto& h : th) h.join();
+    }
+  }
+  t->kbase = kbase;
+  t->x2_entries = x2.empty() ? -1 : x2_off[mt];
   plan_chunks(t);
   auto up = [&](DevBuf& b, const void* h, size_t bytes) -> int {
     int r = b.reserve(bytes);
@@ -657,6 +753,9 @@ extern "C" int blp_topk_create(blp_graph* g, int64_t src_lo, int64_t src_hi, int
   if ((rc = up(t->perm, perm.data(), 4 * T)) || (rc = up(t->inv, inv.data(), 4 * T)) ||
       (rc = up(t->tdeg, tdeg.data(), 4 * T)) || (rc = up(t->pci, pci.data(), 4 * pci.size())) ||
       (rc = up(t->d_chunks, t->chunks.data(), sizeof(TkChunk) * t->chunks.size())) ||
+      (rc = up(t->wtab, wtab.data(), 8 * wtab.size())) ||
+      (!x2.empty() && ((rc = up(t->x2_off, x2_off.data(), 8 * x2_off.size())) ||
+                       (rc = up(t->x2, x2.data(), 4 * x2.size())))) ||
       (rc = t->counters.reserve(64))) {
     blp_topk_destroy(t);
     return rc;
@@ -669,15 +768,17 @@ extern "C" int blp_topk_destroy(blp_topk* t) {
   if (!t) return BLP_OK;
   (void)set_device(t->g);
   for (DevBuf* b : {&t->perm, &t->inv, &t->tdeg, &t->pci, &t->d_chunks, &t->src, &t->keys, &t->cols, &t->ncand,
-                    &t->counters})
+                    &t->counters, &t->wtab, &t->x2_off, &t->x2})
     b->release();
   timer_release(t->timer);
   delete t;
   return BLP_OK;
 }
 
-extern "C" int blp_topk_info(const blp_topk* t, int64_t* n_chunks, int64_t* tier32, int64_t* tier16) {
+extern "C" int blp_topk_info(const blp_topk* t, int64_t* n_chunks, int64_t* tier32, int64_t* tier16,
+                             int64_t* wedge_entries) {
   BLP_CHECK(t, BLP_E_ARG, "blp_topk_info: null handle");
+  if (wedge_entries) *wedge_entries = t->x2_entries;
   if (n_chunks) *n_chunks = (int64_t)t->chunks.size();
   if (tier32) *tier32 = t->n32;
   if (tier16) *tier16 = t->n16 - t->n32;
@@ -718,7 +819,10 @@ extern "C" int blp_topk_run(blp_topk* t, int k, uint32_t mask) {
   a.perm = t->perm.as<int32_t>();
   a.inv = t->inv.as<int32_t>();
   a.tdeg = t->tdeg.as<int32_t>();
-  a.aaw = t->g->d_aaw_fx;
+  a.wtab = t->wtab.as<long long>();
+  a.x2_off = t->x2_entries >= 0 ? t->x2_off.as<int64_t>() : nullptr;
+  a.x2 = t->x2_entries >= 0 ? t->x2.as<int32_t>() : nullptr;
+  a.kbase = t->kbase;
   a.src = t->src.as<int32_t>();
   a.n_src = (int)t->n_src;
   a.tlo = t->tlo;

@@ -141,7 +141,9 @@ int blp_hop3_sample(blp_graph* g, const int32_t* src, int64_t n_src, const int32
  * dense target id ascending. Scores are bit-identical to blp_score_pairs on the same pair.
  * The graph must be bipartite between [src_lo, src_hi) and [tgt_lo, tgt_hi) (BLP_E_UNSUP
  * otherwise); both ranges are dense ids (users / businesses of a reference graph.txt).
- *   blp_topk_create:      builds the degree-ordered target numbering and permuted source rows.
+ *   blp_topk_create:      builds the degree-ordered target numbering, the permuted source rows
+ *                         and (memory permitting) the expanded wedge rows; blp_topk_info
+ *                         reports the counter chunks, tier sizes and wedge entries (-1: none).
  *   blp_topk_set_sources: uploads the sources (kept in HBM across runs).
  *   blp_topk_run:         k in [1, 256], mask of BLP_CN | BLP_JACCARD | BLP_ADAMIC; async.
  *   blp_topk_fetch:       one method's [n_src][k] lists (col -1 / score 0 past the end) and
@@ -152,7 +154,8 @@ int blp_hop3_sample(blp_graph* g, const int32_t* src, int64_t n_src, const int32
 int blp_topk_create(blp_graph* g, int64_t src_lo, int64_t src_hi, int64_t tgt_lo, int64_t tgt_hi,
                     blp_topk** out);
 int blp_topk_destroy(blp_topk* t);
-int blp_topk_info(const blp_topk* t, int64_t* n_chunks, int64_t* tier32, int64_t* tier16);
+int blp_topk_info(const blp_topk* t, int64_t* n_chunks, int64_t* tier32, int64_t* tier16,
+                  int64_t* wedge_entries);
 int blp_topk_set_sources(blp_topk* t, const int32_t* src, int64_t n_src);
 int blp_topk_run(blp_topk* t, int k, uint32_t mask);
 int blp_topk_fetch(blp_topk* t, uint32_t method, int32_t* cols, double* scores, int64_t* n_cand);

@@ -53,9 +53,13 @@ def small(gpu):
     return G, adj_of(a, b), rng
 
 
-def test_topk_all_methods_match_oracle(small):
+@pytest.mark.parametrize("expand", ["1", "0"])
+def test_topk_all_methods_match_oracle(small, monkeypatch, expand):
+    """Both row layouts: expanded wedge rows (default) and the rp[w] -> N(w) walk."""
     G, adj, rng = small
+    monkeypatch.setenv("BLP_TOPK_EXPAND", expand)
     T = blp.TopK(G, "user")
+    assert (T.info()["wedge_entries"] > 0) == (expand == "1")
     src = rng.choice(G.n_col0, 40, replace=False)
     check_against_oracle(G, T, adj, src, 20)
 
