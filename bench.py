@@ -41,41 +41,7 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
-class Dist:
-    """torch.distributed (gloo, CPU tensors) only for the barrier and max-over-ranks."""
-
-    def __init__(self):
-        self.world = int(os.environ.get("WORLD_SIZE", "1"))
-        self.rank = int(os.environ.get("RANK", "0"))
-        self.local = int(os.environ.get("LOCAL_RANK", "0"))
-        self.pg = None
-        if self.world > 1:
-            import torch.distributed as td
-
-            td.init_process_group("gloo")
-            self.td = td
-
-    def barrier(self):
-        if self.world > 1:
-            self.td.barrier()
-
-    def max(self, v):
-        if self.world == 1:
-            return v
-        import torch
-
-        t = torch.tensor([float(v)], dtype=torch.float64)
-        self.td.all_reduce(t, op=self.td.ReduceOp.MAX)
-        return float(t.item())
-
-    def sum(self, v):
-        if self.world == 1:
-            return v
-        import torch
-
-        t = torch.tensor([float(v)], dtype=torch.float64)
-        self.td.all_reduce(t, op=self.td.ReduceOp.SUM)
-        return float(t.item())
+from blp.dist import Dist  # noqa: E402  (torch.distributed plumbing: barrier, max/sum, exchange)
 
 
 def alg_bytes(G, x, y, mask, cn=None):
@@ -412,6 +378,104 @@ def run_topk(args):
         print(json.dumps(out), flush=True)
 
 
+XGMI_LINK_GBS = 153.0  # per-direction xGMI link rate (MI355X_MICROARCH.md), 7 links per GPU
+
+
+def run_sharded(args):
+    """Config 5 (BASELINE.json configs[4]): row-block sharded ingest. Rank r generates only the
+    edges of its user block, ONE RCCL all-gather over xGMI gives every rank the full edge list
+    in HBM, libblp builds the CSR on the device, and each rank scores its own users' pairs
+    (rank-local, no further collective). The exchange is timed apart from the scoring step;
+    value = candidate pairs scored per second over all ranks (weak scaling)."""
+    from blp import dist as bd
+
+    d = Dist(exchange=True)
+    dev = d.local
+    blp.lib()
+    U, B, D = synth.CONFIGS[args.config]
+    blocks = bd.user_blocks(U, d.world)
+    lo, hi = int(blocks[d.rank]), int(blocks[d.rank + 1])
+    t0 = time.time()
+    u, b = bd.block_review_edges(U, B, D, lo, hi, seed=0)
+    gen_s = time.time() - t0
+    log("rank %d: users [%d, %d), %d draws generated in %.1fs" % (d.rank, lo, hi, len(u), gen_s))
+    import torch
+
+    torch.cuda.set_device(dev)
+    d.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    a_all, b_all, counts = bd.allgather_edges(d, u, b)
+    torch.cuda.synchronize()
+    exch_local = time.perf_counter() - t0
+    d.barrier()
+    exch_s = d.max(exch_local)
+    recv_bytes = 8 * (sum(counts) - counts[d.rank])
+    del u, b
+    t0 = time.perf_counter()
+    G = blp.DeviceGraph.from_device_edges(a_all.data_ptr(), b_all.data_ptr(), len(a_all), U + B, U, device=dev)
+    build_s = time.perf_counter() - t0
+    del a_all, b_all
+    torch.cuda.empty_cache()
+    log("rank %d: graph %d nodes, %d unique edges; exchange %.2fs (%.2f GB in), device CSR + upload %.1fs" %
+        (d.rank, G.n, G.nnz // 2, exch_local, recv_bytes / 1e9, build_s))
+    rng = np.random.default_rng(d.rank)
+    mine = np.arange(lo, hi)
+    mine = mine[G.hop1_size[lo:hi] > 0]
+    src = np.sort(rng.choice(mine, size=min(args.users, len(mine)), replace=False)).astype(np.int32)
+    ex_x, ex_y = synth.uniform_examples(G, src, rate=args.rate, seed=d.rank)
+    passes = [("user", G.batch(ex_x, ex_y), args.user_mask)]
+    if args.sides == "both":
+        passes.append(("business", G.batch(ex_y, ex_x), blp.CN | blp.JACCARD))
+    for name, bt, _ in passes:
+        log("plan %s: %s" % (name, bt.plan()))
+    for _ in range(args.warmup):
+        for _, bt, mask in passes:
+            bt.score(mask)
+    blp.device_sync(dev)
+    for _, bt, _ in passes:
+        bt.stats_reset()
+    d.barrier()
+    blp.device_sync(dev)
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        for _, bt, mask in passes:
+            bt.score(mask)
+    blp.device_sync(dev)
+    t_local = time.perf_counter() - t_start
+    d.barrier()
+    t_max = d.max(t_local)
+    pairs_total = d.sum(len(ex_x))
+    name0, bt0, mask0 = passes[0]
+    ms, n = bt0.stats(0)
+    sec = ms / 1e3 / max(n, 1)
+    cn0 = bt0.fetch(mask0)["cn"]
+    byts = alg_bytes(G, ex_x, ex_y, mask0, cn0)
+    # ring all-gather: each rank receives (G-1)/G of the data; bound by one link per direction
+    xgmi_bound_s = recv_bytes / (XGMI_LINK_GBS * 1e9) if d.world > 1 else 0.0
+    out = {
+        "metric": METRIC, "value": pairs_total * args.steps / t_max, "unit": "pairs/s", "n_gpus": d.world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * t_max / args.steps,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int32", "data": "synthetic",
+        "config": {"workload": "config5-style row-block sharded: %d users x %d businesses, %d draws (%d unique edges); "
+                               "%d users/GPU from the rank's own block, businesses outside N(u) kept at %g; step = %s"
+                               % (U, B, D, G.nnz // 2, len(src), args.rate,
+                                  "user side CN+J+AA + business side CN+J" if args.sides == "both" else "user side"),
+                   "pairs_per_gpu": int(len(ex_x)), "global_batch": int(pairs_total),
+                   "parallelism": "row-block sharded ingest x%d + RCCL all-gather (%s), rank-local scoring"
+                                  % (d.world, d.backend or "single rank")},
+        "exchange": {"seconds": exch_s, "bytes_in_per_rank": int(recv_bytes),
+                     "GBps_in_per_rank": recv_bytes / exch_s / 1e9 if exch_s > 0 and recv_bytes else None,
+                     "xgmi_one_link_bound_s": xgmi_bound_s, "device_csr_build_s": build_s, "generate_s": gen_s},
+        "roofline": {"bound": "hbm", "achieved": byts / sec / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": byts / sec / 1e9 / HBM_PEAK_GBS, "traffic": None, "kernel": "user-side scorer",
+                     "plan": bt0.plan()},
+    }
+    if d.rank == 0:
+        print(json.dumps(out), flush=True)
+    d.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -425,9 +489,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--user-mask", type=int, default=7, help="methods of the user pass (1 CN, 2 J, 4 AA)")
-    ap.add_argument("--mode", default="similarity", choices=["similarity", "topk", "svd"],
+    ap.add_argument("--mode", default="similarity", choices=["similarity", "topk", "svd", "sharded"],
                     help="similarity: config 2 (default); topk: config 3 full-candidate Jaccard + Adamic-Adar "
-                         "top-k; svd: config 4 rank-64 truncated-SVD scorer")
+                         "top-k; svd: config 4 rank-64 truncated-SVD scorer; sharded: config 5 row-block "
+                         "sharded ingest + RCCL all-gather, then rank-local scoring (--config c5)")
     ap.add_argument("--topk", type=int, default=20)
     ap.add_argument("--topk-mask", type=int, default=6, help="methods of --mode topk (default Jaccard + AA)")
     args = ap.parse_args()
@@ -435,6 +500,8 @@ def main():
         return run_svd(args)
     if args.mode == "topk":
         return run_topk(args)
+    if args.mode == "sharded":
+        return run_sharded(args)
 
     dist = Dist()
     dev = dist.local

@@ -45,6 +45,7 @@ SIGNATURES = {
     "blp_device_sync": [_I32],
     "blp_edges_parse": [ctypes.c_char_p, _I32, _I32, _P, _P, ctypes.POINTER(ctypes.c_int64)],
     "blp_csr_from_edges": [_I64, _I64, _P, _P, _P, _P, _P, ctypes.POINTER(ctypes.c_int64)],
+    "blp_csr_from_edges_device": [_I32, _P, _P, _I64, _I64, _P, _P, _P, ctypes.POINTER(ctypes.c_int64)],
     "blp_graph_create": [_P, _P, _I64, _P, _I32, _PP],
     "blp_graph_destroy": [_P],
     "blp_graph_info": [_P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),

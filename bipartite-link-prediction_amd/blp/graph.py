@@ -76,12 +76,29 @@ class HostGraph:
         nnz = ctypes.c_int64(0)
         check(lib().blp_csr_from_edges(self.n, len(da), ptr(da), ptr(db), ptr(rp), ptr(ci), ptr(sl),
                                        ctypes.byref(nnz)))
+        self._set_csr(rp, ci[: nnz.value].copy(), sl[: self.n], aa)
+
+    def _set_csr(self, rp, ci, sl, aa):
         self.row_ptr = rp
-        self.col_idx = ci[: nnz.value].copy()
-        self.self_loop = sl[: self.n]
+        self.col_idx = ci
+        self.self_loop = sl
         self.hop1_size = np.diff(rp)  # |GetNodesAtHop(v, 1)|
         self.degree = self.hop1_size + self.self_loop  # SNAP GetDeg
         self.aa_weight = aa_weights_from_degree(self.degree) if aa else None
+
+    @classmethod
+    def from_csr(cls, row_ptr, col_idx, self_loop, n_col0, aa=True):
+        """A graph whose node ids are already dense (id i = dense id i): the CSR of
+        blp_csr_from_edges(_device), e.g. built on the GPU after the multi-GPU exchange."""
+        g = cls.__new__(cls)
+        g.n = len(row_ptr) - 1
+        g.node_ids = np.arange(g.n, dtype=np.int64)
+        g.n_col0 = int(n_col0)
+        g._sort = g.node_ids
+        g._sorted_ids = g.node_ids
+        g.n_edges_in = None
+        g._set_csr(np.asarray(row_ptr, np.int64), np.asarray(col_idx, np.int32), np.asarray(self_loop, np.uint8), aa)
+        return g
 
     @property
     def nnz(self):
@@ -128,6 +145,27 @@ class DeviceGraph(HostGraph):
 
     def __init__(self, a_ids, b_ids, device=0, aa=True):
         HostGraph.__init__(self, a_ids, b_ids, aa=aa)
+        self._upload(device, aa)
+
+    @classmethod
+    def from_csr(cls, row_ptr, col_idx, self_loop, n_col0, device=0, aa=True):
+        g = HostGraph.from_csr.__func__(cls, row_ptr, col_idx, self_loop, n_col0, aa)
+        g._upload(device, aa)
+        return g
+
+    @classmethod
+    def from_device_edges(cls, a_ptr, b_ptr, m, n, n_col0, device=0, aa=True):
+        """Build the CSR on `device` from device-resident int32 endpoints (m edges, dense ids in
+        [0, n)) -- the multi-GPU ingest path (blp.dist.allgather_edges) -- and upload it."""
+        rp = np.zeros(n + 1, np.int64)
+        ci = np.empty(max(2 * m, 1), np.int32)
+        sl = np.zeros(max(n, 1), np.uint8)
+        nnz = ctypes.c_int64(0)
+        check(lib().blp_csr_from_edges_device(device, ctypes.c_void_p(a_ptr), ctypes.c_void_p(b_ptr), m, n, ptr(rp),
+                                              ptr(ci), ptr(sl), ctypes.byref(nnz)))
+        return cls.from_csr(rp, ci[: nnz.value], sl[:n], n_col0, device=device, aa=aa)
+
+    def _upload(self, device, aa):
         self.device = device
         h = ctypes.c_void_p()
         check(lib().blp_graph_create(ptr(self.row_ptr), ptr(self.col_idx), self.n,

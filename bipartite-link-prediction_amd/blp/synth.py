@@ -78,3 +78,22 @@ def make_examples(G, users, businesses, draws, n_users=10_000, rate=0.01, seed=0
     nu, nb = heldout_edges(users, businesses, draws, seed=seed + 1, zipf=zipf)
     pos_off, pos_y = positives_csr(G, src, nu, nb)
     return G.hop3_sample(src, pos_off, pos_y, rate=rate, seed=seed)
+
+
+def uniform_examples(G, src, rate=0.01, seed=0):
+    """Candidate pairs for graphs too large for exact hop-3 enumeration per source (config 5:
+    H3(u) is nearly every business): each business outside N(u) is kept with probability
+    `rate`, uniformly -- the distribution dataset_maker.py:143 draws from when H3(u) covers
+    the business set. Labels are not produced (no held-out draw at this scale)."""
+    rng = np.random.default_rng(seed)
+    n0 = G.n_col0
+    nb = G.n - n0
+    xs, ys = [], []
+    for x in src:
+        k = rng.binomial(nb, rate)
+        cand = np.unique(rng.integers(0, nb, k)) + n0
+        own = G.col_idx[G.row_ptr[x]:G.row_ptr[x + 1]]
+        cand = cand[~np.isin(cand, own)]
+        xs.append(np.full(len(cand), x, np.int32))
+        ys.append(cand.astype(np.int32))
+    return np.concatenate(xs), np.concatenate(ys)

@@ -300,7 +300,7 @@ __device__ inline void mp_fetch(const int32_t* __restrict__ ci, const int64_t* s
 
 // Set the bits of every element of the ns segments (rows of ci) inside [c0, c0 + width).
 // Software-pipelined: the loads of step i+1 are in flight while step i's atomics issue.
-template <int NT, int K>
+template <int NT, int K, bool GLOBAL = false>
 __device__ inline void mp_build(const int32_t* __restrict__ ci, const int64_t* s_start, const int32_t* s_off, int ns,
                                 int64_t c0, int64_t width, uint32_t* bm, int tid) {
   const int T = s_off[ns];
@@ -313,7 +313,12 @@ __device__ inline void mp_build(const int32_t* __restrict__ ci, const int64_t* s
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       const int64_t r = (int64_t)w[k] - c0;
-      if (w[k] >= 0 && r >= 0 && r < width) atomicOr(&bm[r >> 5], 1u << (r & 31));
+      if (w[k] >= 0 && r >= 0 && r < width) {
+        if (GLOBAL)  // the workgroup's private HBM bitmap: the OR is done in the XCD's L2
+          __hip_atomic_fetch_or(&bm[r >> 5], 1u << (r & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        else
+          atomicOr(&bm[r >> 5], 1u << (r & 31));
+      }
     }
 #pragma unroll
     for (int k = 0; k < K; ++k) w[k] = wn[k];
@@ -629,6 +634,107 @@ __global__ __launch_bounds__(BLOCK) void k_score(ScoreArgs a) {
   }
 }
 
+// ------------------------------------------------------------------ HBM-bitmap scorer
+// Universes wider than one workgroup's LDS (config 5: H2(u) over 50M users = 6.25 MB) would
+// need one full H2 rebuild per LDS chunk. Here every workgroup owns a private bitmap slot in
+// HBM covering the whole universe: it is built once per source with workgroup-scope atomics
+// (performed in the XCD's L2 -- no cross-XCD coherence is needed for private data), then, after
+// an agent-scope fence (drains the stores, invalidates the CU's L1), popcounted and scanned with
+// plain loads. Same merge-path build / scan loops and pair bookkeeping as k_score.
+template <int BLOCK, int SEG, int K>
+__global__ __launch_bounds__(BLOCK) void k_score_global(ScoreArgs a, uint32_t* gbm, int64_t gwords) {
+  constexpr int NW = BLOCK / 64;
+  __shared__ int64_t s_start[SEG];
+  __shared__ int32_t s_off[SEG + 1];
+  __shared__ uint32_t s_cn[SEG];
+  __shared__ unsigned long long s_aa[SEG];
+  __shared__ unsigned long long red64[NW];
+  __shared__ int red[NW];
+  __shared__ int s_src;
+  uint32_t* bm = gbm + (int64_t)blockIdx.x * gwords;
+  uint4* bm4 = reinterpret_cast<uint4*>(bm);
+  const int64_t nw4 = gwords >> 2;
+  const int64_t c0 = a.lo, width = a.hi - a.lo;
+  const bool want_j = (a.mask & BLP_JACCARD) != 0;
+  const bool want_a = (a.mask & BLP_ADAMIC) != 0;
+  const int n_active = a.misc->n_active;
+  for (;;) {
+    if (threadIdx.x == 0) s_src = atomicAdd(&a.misc->queue, a.dq);
+    __syncthreads();
+    const int s_first = s_src;
+    __syncthreads();
+    if (s_first >= n_active) break;
+    const int s_last = min(n_active, s_first + a.dq);
+    for (int s = s_first; s < s_last; ++s) {
+      const int x = a.active[s];
+      const int pbeg = a.off[x], pcnt = a.cnt[x];
+      const int64_t xb = a.rp[x], xe = a.rp[x + 1];
+      for (int64_t i = threadIdx.x; i < nw4; i += BLOCK) bm4[i] = make_uint4(0, 0, 0, 0);
+      __threadfence();
+      __syncthreads();
+      for (int64_t k0 = xb; k0 < xe; k0 += SEG) {
+        const int ns = (int)min<int64_t>(SEG, xe - k0);
+        load_row_segments<BLOCK>(a.rp, a.ci, k0, ns, s_start, s_off, red, nullptr);
+        mp_build<BLOCK, K, true>(a.ci, s_start, s_off, ns, c0, width, bm, threadIdx.x);
+        __syncthreads();
+      }
+      for (int64_t k = xb + threadIdx.x; k <= xe; k += BLOCK) {  // drop N(x) and x itself
+        const int64_t r = (k == xe ? (int64_t)x : (int64_t)a.ci[k]) - c0;
+        if (r >= 0 && r < width)
+          __hip_atomic_fetch_and(&bm[r >> 5], ~(1u << (r & 31)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      __threadfence();
+      __syncthreads();
+      unsigned long long h2 = 0;
+      if (want_j) {
+        unsigned long long pc = 0;
+        for (int64_t i = threadIdx.x; i < nw4; i += BLOCK) {
+          const uint4 q = bm4[i];
+          pc += __popc(q.x) + __popc(q.y) + __popc(q.z) + __popc(q.w);
+        }
+        h2 = block_sum_u64<BLOCK>(pc, red64);
+      }
+      for (int sb = 0; sb < pcnt; sb += SEG) {
+        const int ns = min(SEG, pcnt - sb);
+        int len = 0;
+        if ((int)threadIdx.x < ns) {
+          const int gp = pbeg + sb + threadIdx.x;
+          s_start[threadIdx.x] = a.g_yb[gp];
+          len = a.g_yl[gp];
+          s_cn[threadIdx.x] = 0;
+          s_aa[threadIdx.x] = 0;
+        }
+        int tot;
+        const int ex = block_exscan<BLOCK>(len, red, &tot);
+        if ((int)threadIdx.x < ns) s_off[threadIdx.x] = ex;
+        if (threadIdx.x == 0) s_off[ns] = tot;
+        __syncthreads();
+        if (want_a)
+          mp_scan<BLOCK, K, true>(a.ci, a.aaw, s_start, s_off, ns, c0, width, bm, s_cn, s_aa, threadIdx.x);
+        else
+          mp_scan<BLOCK, K, false>(a.ci, a.aaw, s_start, s_off, ns, c0, width, bm, s_cn, s_aa, threadIdx.x);
+        __syncthreads();
+        for (int t = threadIdx.x; t < ns; t += BLOCK) {
+          const int p = a.g_out[pbeg + sb + t];
+          const unsigned c = s_cn[t];
+          a.cn[p] = c;
+          if (want_a) a.aa[p] = (double)s_aa[t] * (1.0 / blp::AA_SCALE);
+          if (want_j) {
+            const long long uni = (long long)h2 + (s_off[t + 1] - s_off[t]) - (long long)c;
+            if (uni <= 0) {
+              a.jac[p] = __builtin_nan("");
+              atomicOr(&a.misc->zero_div, 1);
+            } else {
+              a.jac[p] = (double)c / (double)uni;
+            }
+          }
+        }
+        __syncthreads();
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------ wave-per-source scorer
 // For small node universes (the business side of a review graph: H2(v) ⊂ businesses) the
 // per-source work is ~2K elements, so a workgroup-wide pass is all barrier and latency.
@@ -782,6 +888,7 @@ enum Variant { V_SMALL = 0, V_MED = 1, V_LARGE = 2 };
 constexpr int CAP_SMALL = 4096, CAP_MED = 16384, CAP_LARGE = 34816;
 constexpr int BLOCK_SMALL = 256, BLOCK_MED = 512, BLOCK_LARGE = 1024;
 constexpr int SEG_SMALL = 256, SEG_MED = 512, SEG_LARGE = 512;
+constexpr int G_BLOCK = 1024, G_SEG = 512;  // HBM-bitmap scorer
 
 inline int variant_block(int v) { return v == V_SMALL ? BLOCK_SMALL : v == V_MED ? BLOCK_MED : BLOCK_LARGE; }
 inline int64_t variant_cap_bits(int v) { return 32ll * (v == V_SMALL ? CAP_SMALL : v == V_MED ? CAP_MED : CAP_LARGE); }
@@ -811,6 +918,9 @@ struct blp_batch {
   int dq = 1;
   bool use_hot = false;  // some source has a dense row in N(x)
   bool wave = false;     // wave-per-source scorer
+  bool global = false;   // HBM-bitmap scorer (universe wider than LDS)
+  uint32_t* d_gbm = nullptr;
+  int64_t gwords = 0, gslots = 0;
   int shift = 10, nb = 1, nblk = 1;
   int32_t xlo = 0;
   int64_t xspan = 0;
@@ -935,13 +1045,17 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
     if (v >= 128 && v % 128 == 0 && v < b->cap_bits) b->cap_bits = v;
   }
   b->chunks = span <= b->cap_bits ? 1 : (int)((span + b->cap_bits - 1) / b->cap_bits);
+  // wider than LDS: one HBM bitmap per workgroup instead of an H2 rebuild per LDS chunk
+  // (BLP_NO_GLOBAL keeps the chunked path, BLP_FORCE_GLOBAL selects HBM on any universe)
+  b->global = (b->chunks > 1 && !getenv("BLP_NO_GLOBAL")) || getenv("BLP_FORCE_GLOBAL");
+  if (b->global) b->chunks = 1;
   auto bail = [&](int rc) {
     blp_batch_destroy(b);
     return rc;
   };
   int rc = set_device(g);
   if (rc) return bail(rc);
-  b->wave = span <= (int64_t)W_CAP * 32 && b->chunks == 1 && !getenv("BLP_NO_WAVE");
+  b->wave = span <= (int64_t)W_CAP * 32 && b->chunks == 1 && !b->global && !getenv("BLP_NO_WAVE");
   int per_cu = 1;
   if (b->wave) {
     BLP_HIP_OR(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_score_wave<W_WAVES, W_CAP, 8>, W_WAVES * 64, 0),
@@ -963,7 +1077,7 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   if (const char* e = getenv("BLP_HEAVY_WORK")) item_work = std::max<int64_t>(1, atoll(e));  // test knob
   std::vector<int32_t> heavy_slot;
   std::vector<HeavyItem> items;
-  if (b->chunks == 1 && span > 0) {
+  if (b->chunks == 1 && span > 0 && !b->global) {
     for (size_t i = 0; i < srcs.size(); ++i) {
       if (work[i] <= 2 * item_work) continue;
       if (heavy_slot.empty()) heavy_slot.assign((size_t)n, -1);
@@ -1001,6 +1115,16 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
     b->nblk = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)g->n_cu * 2, (n_pairs + 4095) / 4096));
     b->per_blk = (n_pairs + b->nblk - 1) / b->nblk;
   }
+  // ---- HBM bitmap slots: one per resident workgroup of k_score_global
+  if (b->global && n_pairs) {
+    int per_cu_g = 1;
+    BLP_HIP_OR(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_g, k_score_global<G_BLOCK, G_SEG, 8>, G_BLOCK, 0),
+               bail);
+    b->gslots = (int64_t)g->n_cu * std::max(per_cu_g, 1);
+    b->gwords = ((span + 31) / 32 + 3) / 4 * 4;
+    if (hipMalloc(&b->d_gbm, 4 * (size_t)b->gwords * b->gslots) != hipSuccess)
+      return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: HBM bitmap slots"));
+  }
   // ---- device buffers
   const size_t np = (size_t)std::max<int64_t>(n_pairs, 1);
   if (hipMalloc(&b->d_x, 4 * np) != hipSuccess || hipMalloc(&b->d_y, 4 * np) != hipSuccess ||
@@ -1035,7 +1159,7 @@ int blp_batch_destroy(blp_batch* b) {
   timer_release(b->t_score);
   timer_release(b->t_group);
   void* ps[] = {b->d_x,    b->d_y,    b->d_cn,   b->d_jac,  b->d_aa,          b->d_gout,        b->d_gyb,
-                b->d_gyl,  b->d_misc, b->d_heavy_slot, b->d_heavy_bm, b->d_heavy_items};
+                b->d_gyl,  b->d_misc, b->d_heavy_slot, b->d_heavy_bm, b->d_heavy_items, b->d_gbm};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   delete b;
@@ -1046,8 +1170,8 @@ int blp_batch_plan(const blp_batch* b, int64_t* lo, int64_t* hi, int* chunks, in
   BLP_CHECK(b, BLP_E_ARG, "blp_batch_plan: null batch");
   if (lo) *lo = b->lo;
   if (hi) *hi = b->hi;
-  if (chunks) *chunks = b->chunks;
-  if (block) *block = b->wave ? 64 : variant_block(b->variant);
+  if (chunks) *chunks = b->global ? 0 : b->chunks;  // 0: HBM-bitmap scorer
+  if (block) *block = b->wave ? 64 : b->global ? G_BLOCK : variant_block(b->variant);
   if (heavy) *heavy = (int)b->n_heavy;
   return BLP_OK;
 }
@@ -1161,7 +1285,12 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   a.cap_bits = b->cap_bits;
   a.mask = mask | BLP_CN;  // counts are always produced (Jaccard needs them)
   a.dq = b->dq;
-  if (np && b->wave) {
+  if (np && b->global) {
+    a.hot_idx = nullptr;
+    hipLaunchKernelGGL((k_score_global<G_BLOCK, G_SEG, 8>), dim3((unsigned)b->gslots), dim3(G_BLOCK), 0, g->stream, a,
+                       b->d_gbm, b->gwords);
+    BLP_HIP(hipGetLastError());
+  } else if (np && b->wave) {
     int per_cu = 1;
     BLP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_score_wave<W_WAVES, W_CAP, 8>, W_WAVES * 64, 0));
     a.hot_idx = nullptr;  // the wave kernel builds every row sparsely

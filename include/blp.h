@@ -64,6 +64,13 @@ int blp_device_sync(int device); /* hipDeviceSynchronize on `device` */
 int blp_csr_from_edges(int64_t n_nodes, int64_t n_edges, const int32_t* a, const int32_t* b,
                        int64_t* row_ptr, int32_t* col_idx, uint8_t* self_loop, int64_t* nnz_out);
 
+/* blp_csr_from_edges_device: the same CSR as blp_csr_from_edges (same outputs, host
+ * buffers), built on device `device` from device-resident endpoints d_a/d_b (m edges, dense
+ * ids) -- e.g. the edge list a rank holds after the RCCL all-gather of the row-block
+ * partials (multi-GPU ingest). Radix sort of 64-bit (row, col) keys.      */
+int blp_csr_from_edges_device(int device, const int32_t* d_a, const int32_t* d_b, int64_t m, int64_t n_nodes,
+                              int64_t* row_ptr, int32_t* col_idx, uint8_t* self_loop, int64_t* nnz_out);
+
 /* blp_edges_parse: SNAP LoadEdgeList's text format (similarity.py:16): one edge per line,
  * whitespace-separated integer columns c0 and c1, lines starting with '#' skipped, lines
  * with too few columns skipped. Two calls: with a == b == NULL it only counts (*m_out);

@@ -78,12 +78,14 @@ def test_general_graph_exact_distance(gpu):
 
 @pytest.mark.parametrize("knobs", [
     {},
-    {"BLP_CHUNK_BITS": "1024"},                         # multi-chunk bitmap universe
+    {"BLP_CHUNK_BITS": "1024"},                         # wider than LDS: HBM-bitmap scorer
+    {"BLP_CHUNK_BITS": "1024", "BLP_NO_GLOBAL": "1"},   # multi-chunk LDS bitmap universe
+    {"BLP_FORCE_GLOBAL": "1"},                          # HBM-bitmap scorer on a small universe
     {"BLP_HEAVY_WORK": "50"},                           # heavy sources pre-built by k_heavy
     {"BLP_HEAVY_WORK": "1"},                            # one row per heavy item
-    {"BLP_CHUNK_BITS": "2048", "BLP_HEAVY_WORK": "50"}, # multi-chunk disables the heavy path
+    {"BLP_CHUNK_BITS": "2048", "BLP_HEAVY_WORK": "50", "BLP_NO_GLOBAL": "1"},  # multi-chunk: no heavy path
     {"BLP_HOT_MIN": "8"},                               # dense-row index OR-ed into H2
-    {"BLP_HOT_MIN": "8", "BLP_CHUNK_BITS": "1024"},     # dense rows across bitmap chunks
+    {"BLP_HOT_MIN": "8", "BLP_CHUNK_BITS": "1024", "BLP_NO_GLOBAL": "1"},  # dense rows across chunks
     {"BLP_HOT_MIN": "8", "BLP_HEAVY_WORK": "50"},
     {"BLP_HOT_MIN": "1", "BLP_HOT_DENSITY": "100000000"},  # > HOT_LIST dense rows: sparse fallback
     {"BLP_NO_WAVE": "1"},                               # block kernels on a small universe
@@ -102,6 +104,8 @@ def test_kernel_paths_vs_oracle(gpu, knobs, monkeypatch):
     _check_against_oracle(a, b, y, x)
     if "BLP_HEAVY_WORK" in knobs and "BLP_CHUNK_BITS" not in knobs:
         assert G.batch(y, x).plan()["heavy"] > 0
+    if "BLP_FORCE_GLOBAL" in knobs or ("BLP_CHUNK_BITS" in knobs and "BLP_NO_GLOBAL" not in knobs):
+        assert G.batch(x, y).plan()["chunks"] == 0  # HBM-bitmap scorer
 
 
 def test_many_pairs_per_source_vs_oracle(gpu):
