@@ -34,21 +34,23 @@
 
 namespace {
 
-constexpr int TK_NT = 512;
-constexpr int TK_SEL = 1024;          // selection buffer entries (also the AA hash table)
+constexpr int TK_NT = 1024;
+constexpr int TK_SEL = 2048;          // selection buffer entries (also the AA hash table)
 constexpr int TK_HCAP = TK_SEL / 2;   // AA candidates handled by the hash (load <= 1/2)
 constexpr int TK_SEG = 256;           // N(x) entries staged per batch
 constexpr int TK_FILT = 128;          // words of the N'(x) membership filter (4096 bits)
-constexpr int TK_ACC_WORDS = 35712;   // counter space: 139.5 KiB
+constexpr int TK_ACC_WORDS = 32768;   // counter space: 128 KiB
 constexpr int TK_KMAX = 256;
-constexpr int TK_RB = 16;           // row entries loaded up front per element
+constexpr int TK_RB = 8;           // row entries loaded up front per element
 constexpr uint32_t TK_EMPTY = 0xFFFFFFFFu;
 
-// Counter chunk over permuted target ids [c0, c1): [c0, b32) u32, [b32, b16) u16 packed
-// two per word from word w16, [b16, c1) u8 packed four per word from word w8.
+// Counter layout: permuted target p has a byte address -- 4p for the u32 tier (p < n32),
+// A16 + 2(p - n32) for the u16 tier (p < n16), A8 + (p - n16) for the u8 tier -- increasing in
+// p, so the rows store addresses (order and ownership tests are unchanged) and a push is one
+// shift-add with no tier branch. A chunk is the permuted range [c0, c1) = addresses [a0, a1),
+// a0 4-aligned, counted in LDS words from a0.
 struct TkChunk {
-  int64_t c0, c1, b32, b16;
-  int32_t w16, w8;
+  int64_t c0, c1, a0, a1;
 };
 
 struct TkArgs {
@@ -56,7 +58,8 @@ struct TkArgs {
   const int32_t* ci;
   const int32_t* pci;  // source-side rows with permuted target ids, sorted; row w at pci + rp[w] - pbase
   int64_t pbase;
-  const int32_t* perm;  // [T] target (dense id - tlo) -> permuted id
+  const int32_t* paddr; // [T] target (dense id - tlo) -> counter byte address of its permuted id
+  int64_t n32, n16, A16, A8;  // counter tiers (see TkChunk)
   const int32_t* inv;   // [T] permuted id -> dense target id
   const int32_t* tdeg;  // [T] |N(b)| by permuted id
   const long long* wtab;  // Adamic-Adar weight (fixed point) of a source by its degree
@@ -100,41 +103,35 @@ __device__ inline bool better(unsigned long long ka, int ca, unsigned long long 
   return ka > kb || (ka == kb && ca < cb);
 }
 
-__device__ inline void acc_add(uint32_t* acc, const TkChunk& c, int64_t p) {
-  if (p < c.b32) {
-    atomicAdd(&acc[p - c.c0], 1u);
-  } else if (p < c.b16) {
-    const int64_t i = p - c.b32;
-    atomicAdd(&acc[c.w16 + (i >> 1)], 1u << ((i & 1) << 4));
-  } else {
-    const int64_t i = p - c.b16;
-    atomicAdd(&acc[c.w8 + (i >> 2)], 1u << ((i & 3) << 3));
-  }
+__device__ inline int64_t addr_of(const TkArgs& a, int64_t p) {
+  return p < a.n32 ? 4 * p : p < a.n16 ? a.A16 + 2 * (p - a.n32) : a.A8 + (p - a.n16);
 }
 
-__device__ inline uint32_t acc_get(const uint32_t* acc, const TkChunk& c, int64_t p) {
-  if (p < c.b32) return acc[p - c.c0];
-  if (p < c.b16) {
-    const int64_t i = p - c.b32;
-    return (acc[c.w16 + (i >> 1)] >> ((i & 1) << 4)) & 0xFFFFu;
-  }
-  const int64_t i = p - c.b16;
-  return (acc[c.w8 + (i >> 2)] >> ((i & 3) << 3)) & 0xFFu;
+__device__ inline int64_t p_of(const TkArgs& a, int64_t e) {
+  return e < a.A16 ? e >> 2 : e < a.A8 ? a.n32 + ((e - a.A16) >> 1) : a.n16 + (e - a.A8);
 }
 
-__device__ inline void acc_clear(uint32_t* acc, const TkChunk& c, int64_t p) {
-  if (p < c.b32) {
-    acc[p - c.c0] = 0;
-  } else if (p < c.b16) {
-    const int64_t i = p - c.b32;
-    atomicAnd(&acc[c.w16 + (i >> 1)], ~(0xFFFFu << ((i & 1) << 4)));
-  } else {
-    const int64_t i = p - c.b16;
-    atomicAnd(&acc[c.w8 + (i >> 2)], ~(0xFFu << ((i & 3) << 3)));
-  }
+__device__ inline uint32_t width_mask(const TkArgs& a, int64_t e) {
+  return e < a.A16 ? 0xFFFFFFFFu : e < a.A8 ? 0xFFFFu : 0xFFu;
 }
 
-__device__ inline int hash_slot(int32_t p) { return (int)(((uint32_t)p * 2654435761u) >> 22); }  // 10 bits
+__device__ inline void acc_add(uint32_t* acc, const TkChunk& c, int64_t e) {
+  const int64_t off = e - c.a0;
+  atomicAdd(&acc[off >> 2], 1u << ((off & 3) << 3));
+}
+
+__device__ inline uint32_t acc_get(const TkArgs& a, const uint32_t* acc, const TkChunk& c, int64_t e) {
+  const int64_t off = e - c.a0;
+  return (acc[off >> 2] >> ((off & 3) << 3)) & width_mask(a, e);
+}
+
+__device__ inline void acc_clear(const TkArgs& a, uint32_t* acc, const TkChunk& c, int64_t e) {
+  const int64_t off = e - c.a0;
+  atomicAnd(&acc[off >> 2], ~(width_mask(a, e) << ((off & 3) << 3)));
+}
+
+constexpr int TK_HBITS = 11;  // log2(TK_SEL)
+__device__ inline int hash_slot(int32_t e) { return (int)(((uint32_t)e * 2654435761u) >> (32 - TK_HBITS)); }
 
 __device__ long long block_sum(TkShared& s, long long v) {
   for (int d = 32; d > 0; d >>= 1) v += __shfl_down(v, d, 64);
@@ -177,7 +174,7 @@ __device__ long long push_pass(const TkArgs& a, TkShared& s, int x, int64_t xb, 
       const int64_t rs = a.rp[b];
       len = a.rp[b + 1] - rs;
       s.seg_rs[tid] = rs;
-      s.seg_p[tid] = a.perm[b - a.tlo];
+      s.seg_p[tid] = a.paddr[b - a.tlo];
       if (a.x2) {  // position of x in N(b') (sorted): its own wedge is skipped
         int64_t lo = rs, hi = rs + len;
         while (lo < hi) {
@@ -260,15 +257,15 @@ __device__ long long push_pass(const TkArgs& a, TkShared& s, int x, int64_t xb, 
         }
 #pragma unroll
         for (int j = 0; j < TK_RB; ++j)
-          if (j < len_w && e[j] >= c.c0 && e[j] < c.c1) acc_add(s.acc, c, e[j]);
+          if (j < len_w && e[j] >= c.a0 && e[j] < c.a1) acc_add(s.acc, c, e[j]);
         for (int j = TK_RB; j < len_w; ++j) {
           const int32_t ej = roww[j];
-          if (ej >= c.c0 && ej < c.c1) acc_add(s.acc, c, ej);
+          if (ej >= c.a0 && ej < c.a1) acc_add(s.acc, c, ej);
         }
       } else if (MODE == 1) {
         const unsigned long long wfx = (unsigned long long)a.wtab[len_w];
         auto push1 = [&](int32_t ej) {
-          if (acc_get(s.acc, c, ej) >= thr) {
+          if (acc_get(a, s.acc, c, ej) >= thr) {
             int h = hash_slot(ej);
             while (s.col[h] != ej) h = (h + 1) & (TK_SEL - 1);
             atomicAdd(&s.key[h], wfx);
@@ -281,11 +278,13 @@ __device__ long long push_pass(const TkArgs& a, TkShared& s, int x, int64_t xb, 
       } else {
         const unsigned long long wfx = (unsigned long long)a.wtab[len_w];
 #pragma unroll
-        for (int j = 0; j < TK_RB; ++j)
-          if (j < len_w && e[j] >= d0 && e[j] < d1) atomicAdd(&acc64[e[j] - d0], wfx);
+        for (int j = 0; j < TK_RB; ++j) {
+          const int64_t p = p_of(a, e[j]);
+          if (j < len_w && p >= d0 && p < d1) atomicAdd(&acc64[p - d0], wfx);
+        }
         for (int j = TK_RB; j < len_w; ++j) {
-          const int32_t ej = roww[j];
-          if (ej >= d0 && ej < d1) atomicAdd(&acc64[ej - d0], wfx);
+          const int64_t p = p_of(a, roww[j]);
+          if (p >= d0 && p < d1) atomicAdd(&acc64[p - d0], wfx);
         }
       }
     }
@@ -392,7 +391,7 @@ __device__ long long sel_counts(const TkArgs& a, TkShared& s, int it, const TkCh
     unsigned long long key = 0;
     int col = 0;
     if (p < c.c1) {
-      const uint32_t cnt = acc_get(s.acc, c, p);
+      const uint32_t cnt = acc_get(a, s.acc, c, addr_of(a, p));
       ok = cnt > 0;
       if (ok) {
         nc += count;
@@ -439,7 +438,7 @@ __global__ __launch_bounds__(TK_NT) void k_topk(TkArgs a) {
     long long h2 = 0, ncand = 0;
     for (int ci = 0; ci < a.n_chunks; ++ci) {
       const TkChunk c = a.chunks[ci];
-      const int words = (int)(c.w8 + ((c.c1 - c.b16) + 3) / 4);
+      const int words = (int)((c.a1 - c.a0 + 3) >> 2);
       for (int i = tid; i < words; i += TK_NT) s.acc[i] = 0;
       __syncthreads();
       long long np = 0;
@@ -454,7 +453,7 @@ __global__ __launch_bounds__(TK_NT) void k_topk(TkArgs a) {
       }
       for (int j = tid; j < du; j += TK_NT) {
         const int32_t e = rowx[j];
-        if (e >= c.c0 && e < c.c1) acc_clear(s.acc, c, e);
+        if (e >= c.a0 && e < c.a1) acc_clear(a, s.acc, c, e);
       }
       __syncthreads();
       if (want_cn) ncand += sel_counts<0>(a, s, it, c, h2, true);
@@ -471,7 +470,7 @@ __global__ __launch_bounds__(TK_NT) void k_topk(TkArgs a) {
           thr = (uint32_t)max(1.0, floor((double)cnt_k * a.ratio * (1.0 - 1e-9)));
         }
         long long nc = 0;
-        for (int64_t p = c.c0 + tid; p < c.c1; p += TK_NT) nc += acc_get(s.acc, c, p) >= thr;
+        for (int64_t p = c.c0 + tid; p < c.c1; p += TK_NT) nc += acc_get(a, s.acc, c, addr_of(a, p)) >= thr;
         nc = block_sum(s, nc);
         if (nc <= a.hcap) {
           for (int i = tid; i < TK_SEL; i += TK_NT) {
@@ -480,9 +479,10 @@ __global__ __launch_bounds__(TK_NT) void k_topk(TkArgs a) {
           }
           __syncthreads();
           for (int64_t p = c.c0 + tid; p < c.c1; p += TK_NT) {
-            if (acc_get(s.acc, c, p) >= thr) {
-              int h = hash_slot((int32_t)p);
-              while (atomicCAS(&s.col[h], (int32_t)TK_EMPTY, (int32_t)p) != (int32_t)TK_EMPTY) h = (h + 1) & (TK_SEL - 1);
+            const int32_t e = (int32_t)addr_of(a, p);
+            if (acc_get(a, s.acc, c, e) >= thr) {
+              int h = hash_slot(e);
+              while (atomicCAS(&s.col[h], (int32_t)TK_EMPTY, e) != (int32_t)TK_EMPTY) h = (h + 1) & (TK_SEL - 1);
             }
           }
           __syncthreads();
@@ -492,9 +492,9 @@ __global__ __launch_bounds__(TK_NT) void k_topk(TkArgs a) {
           int cv[TK_SEL / TK_NT];
           for (int r = 0; r < TK_SEL / TK_NT; ++r) {
             const int i = tid + r * TK_NT;
-            const int32_t p = s.col[i];
-            kv[r] = p == (int32_t)TK_EMPTY ? 0ull : s.key[i];
-            cv[r] = p == (int32_t)TK_EMPTY ? 0x7FFFFFFF : a.inv[p];
+            const int32_t e = s.col[i];
+            kv[r] = e == (int32_t)TK_EMPTY ? 0ull : s.key[i];
+            cv[r] = e == (int32_t)TK_EMPTY ? 0x7FFFFFFF : a.inv[p_of(a, e)];
           }
           __syncthreads();
           for (int r = 0; r < TK_SEL / TK_NT; ++r) {
@@ -529,8 +529,8 @@ __global__ __launch_bounds__(TK_NT) void k_topk(TkArgs a) {
           __syncthreads();
           push_pass<2>(a, s, x, xb, du, rowx, a.chunks[0], 0, d0, d1, false);
           for (int j = tid; j < du; j += TK_NT) {
-            const int32_t e = rowx[j];
-            if (e >= d0 && e < d1) acc64[e - d0] = 0;
+            const int64_t p = p_of(a, rowx[j]);
+            if (p >= d0 && p < d1) acc64[p - d0] = 0;
           }
           __syncthreads();
           sel_begin(a, s, 2, it);
@@ -566,6 +566,7 @@ struct blp_topk {
   int64_t slo = 0, shi = 0, tlo = 0, thi = 0, T = 0;
   int64_t pbase = 0;
   int64_t n32 = 0, n16 = 0;  // tier boundaries in permuted order
+  int64_t A16 = 0, A8 = 0;   // byte addresses where the u16 / u8 tiers start
   int64_t acc_words = TK_ACC_WORDS;
   double ratio = 0.0;
   bool have_aa = false;
@@ -587,10 +588,11 @@ int64_t env_i64(const char* name, int64_t dflt) {
   return (v && *v) ? atoll(v) : dflt;
 }
 
-int64_t chunk_words(const blp_topk* t, int64_t c0, int64_t c1) {
-  const int64_t b32 = std::min(std::max(t->n32, c0), c1), b16 = std::min(std::max(t->n16, c0), c1);
-  return (b32 - c0) + (b16 - b32 + 1) / 2 + (c1 - b16 + 3) / 4;
+int64_t host_addr(const blp_topk* t, int64_t p) {
+  return p < t->n32 ? 4 * p : p < t->n16 ? t->A16 + 2 * (p - t->n32) : t->A8 + (p - t->n16);
 }
+
+int64_t chunk_words(const blp_topk* t, int64_t c0, int64_t c1) { return (host_addr(t, c1) - host_addr(t, c0) + 3) / 4; }
 
 void plan_chunks(blp_topk* t) {
   t->chunks.clear();
@@ -602,14 +604,13 @@ void plan_chunks(blp_topk* t) {
       const int64_t mid = lo + (hi - lo + 1) / 2;
       if (chunk_words(t, c0, mid) <= t->acc_words) lo = mid; else hi = mid - 1;
     }
-    const int64_t c1 = std::min<int64_t>(lo, std::max<int64_t>(t->T, c0 + 1));
+    int64_t c1 = std::min<int64_t>(lo, std::max<int64_t>(t->T, c0 + 1));
+    while (c1 < t->T && c1 > c0 + 1 && host_addr(t, c1) % 4) --c1;  // next chunk starts on a word
     TkChunk c{};
     c.c0 = c0;
     c.c1 = c1;
-    c.b32 = std::min(std::max(t->n32, c0), c1);
-    c.b16 = std::min(std::max(t->n16, c0), c1);
-    c.w16 = (int32_t)(c.b32 - c0);
-    c.w8 = (int32_t)(c.w16 + (c.b16 - c.b32 + 1) / 2);
+    c.a0 = host_addr(t, c0);
+    c.a1 = host_addr(t, c1);
     t->chunks.push_back(c);
     c0 = c1;
   } while (c0 < t->T);
@@ -666,6 +667,14 @@ extern "C" int blp_topk_create(blp_graph* g, int64_t src_lo, int64_t src_hi, int
   while (t->n32 < T && tdeg[t->n32] > t16) ++t->n32;
   t->n16 = t->n32;
   while (t->n16 < T && tdeg[t->n16] > t8) ++t->n16;
+  t->A16 = 4 * t->n32;
+  t->A8 = (t->A16 + 2 * (t->n16 - t->n32) + 3) / 4 * 4;
+  if (host_addr(t, T) >= (int64_t(1) << 31)) {
+    delete t;
+    return fail(BLP_E_UNSUP, "blp_topk_create: too many targets");
+  }
+  std::vector<int32_t> paddr(T);
+  for (int64_t i = 0; i < T; ++i) paddr[i] = (int32_t)host_addr(t, perm[i]);
   // source rows with permuted target ids, each sorted (multi-threaded)
   const int64_t m = rp[src_hi] - t->pbase;
   std::vector<int32_t> pci(std::max<int64_t>(m, 1));
@@ -679,7 +688,7 @@ extern "C" int blp_topk_create(blp_graph* g, int64_t src_lo, int64_t src_hi, int
         for (int64_t v = r0; v < r1; ++v) {
           int32_t* row = pci.data() + (rp[v] - t->pbase);
           const int64_t len = rp[v + 1] - rp[v];
-          for (int64_t e = 0; e < len; ++e) row[e] = perm[ci[rp[v] + e] - tgt_lo];
+          for (int64_t e = 0; e < len; ++e) row[e] = paddr[ci[rp[v] + e] - tgt_lo];
           std::sort(row, row + len);
         }
       });
@@ -750,7 +759,7 @@ extern "C" int blp_topk_create(blp_graph* g, int64_t src_lo, int64_t src_hi, int
     BLP_HIP(hipMemcpy(b.p, h, bytes, hipMemcpyHostToDevice));
     return BLP_OK;
   };
-  if ((rc = up(t->perm, perm.data(), 4 * T)) || (rc = up(t->inv, inv.data(), 4 * T)) ||
+  if ((rc = up(t->perm, paddr.data(), 4 * T)) || (rc = up(t->inv, inv.data(), 4 * T)) ||
       (rc = up(t->tdeg, tdeg.data(), 4 * T)) || (rc = up(t->pci, pci.data(), 4 * pci.size())) ||
       (rc = up(t->d_chunks, t->chunks.data(), sizeof(TkChunk) * t->chunks.size())) ||
       (rc = up(t->wtab, wtab.data(), 8 * wtab.size())) ||
@@ -816,7 +825,11 @@ extern "C" int blp_topk_run(blp_topk* t, int k, uint32_t mask) {
   a.ci = t->g->d_ci;
   a.pci = t->pci.as<int32_t>();
   a.pbase = t->pbase;
-  a.perm = t->perm.as<int32_t>();
+  a.paddr = t->perm.as<int32_t>();
+  a.n32 = t->n32;
+  a.n16 = t->n16;
+  a.A16 = t->A16;
+  a.A8 = t->A8;
   a.inv = t->inv.as<int32_t>();
   a.tdeg = t->tdeg.as<int32_t>();
   a.wtab = t->wtab.as<long long>();
