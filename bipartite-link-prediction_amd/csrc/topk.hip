@@ -72,6 +72,8 @@ struct TkArgs {
   const TkChunk* chunks;
   int n_chunks;
   int64_t aa_chunk;  // targets per direct-AA chunk (u64 each)
+  int64_t H, AH;     // fused AA: the H most popular targets (addresses < AH) get u64 sums in the count pass
+  int64_t h_word;    // ... stored at LDS word h_word (8-byte aligned, after the chunk's counters)
   int k;
   uint32_t mask;
   double ratio;  // wmin / wmax over sources of degree >= 2 (fixed point)
@@ -79,7 +81,7 @@ struct TkArgs {
   unsigned long long* keys;  // [3][n_src][k]
   int32_t* cols;             // [3][n_src][k]
   int64_t* ncand;            // [n_src]
-  unsigned long long* counters;  // [0] queue, [1] AA hash path, [2] AA direct path, [3] sum |H2|, [4] sum of |N(w)| over H2
+  unsigned long long* counters;  // [0] queue, [1] AA hash path, [2] AA direct path, [3] sum |H2|, [4] sum of |N(w)| over H2, [5] AA fused path
 };
 
 struct TkShared {
@@ -156,6 +158,7 @@ __device__ inline bool in_row_x(const TkShared& s, const int32_t* rowx, int du, 
 }
 
 // MODE 0: CN counts into the tiered counters of chunk c (and |H2(x)| when count_h2)
+// MODE 3: MODE 0 plus the fixed-point AA sums of the H most popular targets (fused AA)
 // MODE 1: exact AA of the hashed candidates (counter >= thr) into s.key[slot]
 // MODE 2: direct AA fixed-point sums of targets [c0, c1) into the u64 view of s.acc
 template <int MODE>
@@ -250,7 +253,18 @@ __device__ long long push_pass(const TkArgs& a, TkShared& s, int x, int64_t xb, 
         if (in_row_x(s, rowx, du, ej)) owned = false;
       }
       if (!owned) continue;
-      if (MODE == 0) {
+      if (MODE == 3) {
+        unsigned long long* aah = acc64 + (a.h_word >> 1);
+        const unsigned long long wfx = (unsigned long long)a.wtab[len_w];
+#pragma unroll
+        for (int j = 0; j < TK_RB; ++j)
+          if (j < len_w && e[j] < a.AH) atomicAdd(&aah[p_of(a, e[j])], wfx);
+        for (int j = TK_RB; j < len_w; ++j) {
+          const int32_t ej = roww[j];
+          if (ej < a.AH) atomicAdd(&aah[p_of(a, ej)], wfx);
+        }
+      }
+      if (MODE == 0 || MODE == 3) {
         if (count_h2) {
           ++h2;
           npush += len_w;
@@ -438,11 +452,13 @@ __global__ __launch_bounds__(TK_NT) void k_topk(TkArgs a) {
     long long h2 = 0, ncand = 0;
     for (int ci = 0; ci < a.n_chunks; ++ci) {
       const TkChunk c = a.chunks[ci];
-      const int words = (int)((c.a1 - c.a0 + 3) >> 2);
+      const bool fused = want_aa && a.H > 0 && a.n_chunks == 1;
+      const int words = fused ? (int)(a.h_word + 2 * a.H) : (int)((c.a1 - c.a0 + 3) >> 2);
       for (int i = tid; i < words; i += TK_NT) s.acc[i] = 0;
       __syncthreads();
       long long np = 0;
-      const long long h = push_pass<0>(a, s, x, xb, du, rowx, c, 0, 0, 0, ci == 0, &np);
+      const long long h = fused ? push_pass<3>(a, s, x, xb, du, rowx, c, 0, 0, 0, ci == 0, &np)
+                                : push_pass<0>(a, s, x, xb, du, rowx, c, 0, 0, 0, ci == 0, &np);
       if (ci == 0) {
         h2 = block_sum(s, h);
         np = block_sum(s, np);
@@ -469,10 +485,29 @@ __global__ __launch_bounds__(TK_NT) void k_topk(TkArgs a) {
           const unsigned long long cnt_k = a.keys[((size_t)0 * a.n_src + it) * a.k + a.k - 1];
           thr = (uint32_t)max(1.0, floor((double)cnt_k * a.ratio * (1.0 - 1e-9)));
         }
-        long long nc = 0;
-        for (int64_t p = c.c0 + tid; p < c.c1; p += TK_NT) nc += acc_get(a, s.acc, c, addr_of(a, p)) >= thr;
+        long long nc = 0, nc_out = 0;
+        for (int64_t p = c.c0 + tid; p < c.c1; p += TK_NT) {
+          const bool hit = acc_get(a, s.acc, c, addr_of(a, p)) >= thr;
+          nc += hit;
+          nc_out += hit && p >= a.H;
+        }
         nc = block_sum(s, nc);
-        if (nc <= a.hcap) {
+        nc_out = block_sum(s, nc_out);
+        if (a.H > 0 && nc_out == 0) {
+          // every target that can reach the top k is one of the H fused ones: their exact
+          // sums are already in LDS (the candidates are the targets with a count)
+          const unsigned long long* aah = acc64 + (a.h_word >> 1);
+          sel_begin(a, s, 2, it);
+          for (int64_t base = 0; base < a.H; base += TK_NT) {
+            const int64_t p = base + tid;
+            const bool ok = p < a.H && acc_get(a, s.acc, c, addr_of(a, p)) > 0;
+            sel_offer(s, ok, ok ? aah[p] : 0ull, ok ? a.inv[p] : 0);
+            sel_round_end(a, s);
+          }
+          sel_end(a, s, 2, it);
+          if (tid == 0) atomicAdd(&a.counters[5], 1ull);
+          done = true;
+        } else if (nc <= a.hcap) {
           for (int i = tid; i < TK_SEL; i += TK_NT) {
             s.col[i] = (int32_t)TK_EMPTY;
             s.key[i] = 0;
@@ -567,6 +602,7 @@ struct blp_topk {
   int64_t pbase = 0;
   int64_t n32 = 0, n16 = 0;  // tier boundaries in permuted order
   int64_t A16 = 0, A8 = 0;   // byte addresses where the u16 / u8 tiers start
+  int64_t H = 0, AH = 0, h_word = 0;  // fused AA targets
   int64_t acc_words = TK_ACC_WORDS;
   double ratio = 0.0;
   bool have_aa = false;
@@ -615,6 +651,13 @@ void plan_chunks(blp_topk* t) {
     c0 = c1;
   } while (c0 < t->T);
   t->aa_chunk = t->acc_words / 2;
+  // fused AA (single counter chunk): the most popular targets get u64 sums in the spare words
+  t->H = 0;
+  if (t->chunks.size() == 1 && !env_i64("BLP_TOPK_NO_FUSE", 0)) {
+    t->h_word = (chunk_words(t, 0, t->T) + 1) / 2 * 2;
+    t->H = std::max<int64_t>(0, std::min<int64_t>(t->T, (t->acc_words - t->h_word) / 2));
+  }
+  t->AH = t->H > 0 ? host_addr(t, t->H) : 0;
 }
 
 }  // namespace
@@ -826,6 +869,9 @@ extern "C" int blp_topk_run(blp_topk* t, int k, uint32_t mask) {
   a.pci = t->pci.as<int32_t>();
   a.pbase = t->pbase;
   a.paddr = t->perm.as<int32_t>();
+  a.H = (mask & BLP_ADAMIC) ? t->H : 0;
+  a.AH = t->AH;
+  a.h_word = t->h_word;
   a.n32 = t->n32;
   a.n16 = t->n16;
   a.A16 = t->A16;
@@ -898,7 +944,7 @@ extern "C" int blp_topk_fetch(blp_topk* t, uint32_t method, int32_t* cols, doubl
 }
 
 extern "C" int blp_topk_stats(blp_topk* t, int which, double* total_ms, int64_t* launches) {
-  BLP_CHECK(t && which >= 0 && which <= 4, BLP_E_ARG, "blp_topk_stats: bad arguments");
+  BLP_CHECK(t && which >= 0 && which <= 5, BLP_E_ARG, "blp_topk_stats: bad arguments");
   int rc = set_device(t->g);
   if (rc) return rc;
   if (which == 0) {
@@ -908,7 +954,8 @@ extern "C" int blp_topk_stats(blp_topk* t, int which, double* total_ms, int64_t*
     return BLP_OK;
   }
   // 1 / 2: sources whose AA went through the candidate hash / direct accumulation;
-  // 3: sum of |H2(x)|; 4: sum over x and w in H2(x) of |N(w)| (the push volume of one pass)
+  // 3: sum of |H2(x)|; 4: sum over x and w in H2(x) of |N(w)| (the push volume of one pass);
+  // 5: sources whose AA top-k came straight from the fused sums
   BLP_HIP(hipStreamSynchronize(t->g->stream));
   unsigned long long c[8];
   BLP_HIP(hipMemcpy(c, t->counters.p, 64, hipMemcpyDeviceToHost));

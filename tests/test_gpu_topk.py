@@ -82,17 +82,31 @@ def test_topk_u32_tier_and_multi_chunk(small, monkeypatch):
     assert T2.stats(2)[1] == len(src)  # every source took the direct Adamic-Adar path
 
 
-def test_topk_aa_direct_path_matches_hash_path(small, monkeypatch):
+def test_topk_unfused_matches_oracle(small, monkeypatch):
+    G, adj, rng = small
+    monkeypatch.setenv("BLP_TOPK_NO_FUSE", "1")
+    T = blp.TopK(G, "user")
+    src = rng.choice(G.n_col0, 24, replace=False)
+    check_against_oracle(G, T, adj, src, 20)
+
+
+def test_topk_aa_paths_agree(small, monkeypatch):
+    """Adamic-Adar top-k through the fused sums (default on this graph), the candidate hash
+    and the direct chunked accumulation: identical lists."""
     G, adj, rng = small
     src = rng.choice(G.n_col0, 32, replace=False)
     T = blp.TopK(G, "user")
-    r1 = T(src, k=15, mask=blp.ADAMIC)["adamic_adar"]
-    assert T.stats(1)[1] > 0
+    r0 = T(src, k=15, mask=blp.ADAMIC)["adamic_adar"]
+    assert T.stats(5)[1] == len(src)  # fused
+    monkeypatch.setenv("BLP_TOPK_NO_FUSE", "1")
+    T1 = blp.TopK(G, "user")
+    r1 = T1(src, k=15, mask=blp.ADAMIC)["adamic_adar"]
+    assert T1.stats(1)[1] > 0 and T1.stats(5)[1] == 0  # candidate hash
     monkeypatch.setenv("BLP_TOPK_HCAP", "0")
-    r2 = T(src, k=15, mask=blp.ADAMIC)["adamic_adar"]
-    assert T.stats(2)[1] == len(src)
-    for x, y in zip(r1, r2):
-        assert np.array_equal(x, y)
+    r2 = T1(src, k=15, mask=blp.ADAMIC)["adamic_adar"]
+    assert T1.stats(2)[1] == len(src)  # direct
+    for x, y, z in zip(r0, r1, r2):
+        assert np.array_equal(x, y) and np.array_equal(x, z)
 
 
 def test_topk_scores_equal_pair_scorer(small):
