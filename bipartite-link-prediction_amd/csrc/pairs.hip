@@ -1055,7 +1055,10 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   };
   int rc = set_device(g);
   if (rc) return bail(rc);
-  b->wave = span <= (int64_t)W_CAP * 32 && b->chunks == 1 && !b->global && !getenv("BLP_NO_WAVE");
+  // wave-per-source scorer: opt-in (BLP_WAVE=1). With heavy sources split finely the block
+  // kernels are faster on the business side of config 2 (1.46 vs 2.01 ms, profiles/probe_sides.py)
+  b->wave = span <= (int64_t)W_CAP * 32 && b->chunks == 1 && !b->global && getenv("BLP_WAVE") &&
+            !getenv("BLP_NO_WAVE");
   int per_cu = 1;
   if (b->wave) {
     BLP_HIP_OR(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_score_wave<W_WAVES, W_CAP, 8>, W_WAVES * 64, 0),
@@ -1073,7 +1076,7 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   const int64_t total_work = std::accumulate(work.begin(), work.end(), (int64_t)0) + scan_work;
   // a wave is ~16x slower on one source than a 1024-thread block: split much earlier there
   int64_t item_work = b->wave ? std::max<int64_t>(4096, total_work / std::max<int64_t>(4 * n_wg, 1))
-                              : std::max<int64_t>(16384, total_work / std::max<int64_t>(n_wg, 1));
+                              : std::max<int64_t>(16384, total_work / std::max<int64_t>(4 * n_wg, 1));
   if (const char* e = getenv("BLP_HEAVY_WORK")) item_work = std::max<int64_t>(1, atoll(e));  // test knob
   std::vector<int32_t> heavy_slot;
   std::vector<HeavyItem> items;

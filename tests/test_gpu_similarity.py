@@ -45,15 +45,15 @@ def _check_against_oracle(ga, gb, x, y, mask=7):
     return G
 
 
-@pytest.mark.parametrize("no_wave", [False, True])
+@pytest.mark.parametrize("wave", [False, True])
 @pytest.mark.parametrize("n_users,n_bus,n_draws,seed", [
     (2000, 300, 20000, 0),     # small universe: wave kernel (or SMALL block variant)
     (30000, 2000, 150000, 1),  # wave kernel (or MED block variant)
     (300000, 5000, 600000, 2), # LARGE block variant, long rows (popular businesses)
 ])
-def test_user_and_business_side_vs_oracle(gpu, n_users, n_bus, n_draws, seed, no_wave, monkeypatch):
-    if no_wave:
-        monkeypatch.setenv("BLP_NO_WAVE", "1")
+def test_user_and_business_side_vs_oracle(gpu, n_users, n_bus, n_draws, seed, wave, monkeypatch):
+    if wave:
+        monkeypatch.setenv("BLP_WAVE", "1")  # opt-in wave-per-source scorer
     rng = np.random.default_rng(seed)
     a, b = bipartite_edges(rng, n_users, n_bus, n_draws)
     G = blp.DeviceGraph(a, b)
@@ -88,8 +88,8 @@ def test_general_graph_exact_distance(gpu):
     {"BLP_HOT_MIN": "8", "BLP_CHUNK_BITS": "1024", "BLP_NO_GLOBAL": "1"},  # dense rows across chunks
     {"BLP_HOT_MIN": "8", "BLP_HEAVY_WORK": "50"},
     {"BLP_HOT_MIN": "1", "BLP_HOT_DENSITY": "100000000"},  # > HOT_LIST dense rows: sparse fallback
-    {"BLP_NO_WAVE": "1"},                               # block kernels on a small universe
-    {"BLP_NO_WAVE": "1", "BLP_HEAVY_WORK": "50", "BLP_HOT_MIN": "8"},
+    {"BLP_WAVE": "1"},                                  # wave-per-source scorer (opt-in)
+    {"BLP_WAVE": "1", "BLP_HEAVY_WORK": "50", "BLP_HOT_MIN": "8"},
 ])
 def test_kernel_paths_vs_oracle(gpu, knobs, monkeypatch):
     for k, v in knobs.items():
