@@ -64,7 +64,7 @@ def run_evaluation(examples, methods, precision_at=20, data_dir="./data/test/", 
     curve_args = []
     results = {}
     for i, method in enumerate(methods):
-        predictions = util.load_json(data_dir + method + ".json")
+        predictions = util.load_scores(data_dir + method + ".json")  # the .npz sidecar when present (util.write_sidecar)
         all_ys, all_ps = [], []
         for u in predictions:
             for b in predictions[u]:

@@ -110,7 +110,7 @@ def score_examples(examples, G, side, mask):
     return present, scores
 
 
-def _run_side(examples, G, methods, outfiles, table, side):
+def _run_side(examples, G, methods, outfiles, table, side, sidecar=False):
     mask = method_mask(methods, table)
     present, scores = score_examples(examples, G, side, mask | blp.CN)
     results = []
@@ -118,35 +118,38 @@ def _run_side(examples, G, methods, outfiles, table, side):
         sim = assemble(examples, _values(table.get(m, 0), present, scores))
         if f is not None:
             util.write_json(sim, f)
+            if sidecar:
+                util.write_sidecar(sim, f)
         results.append(sim)
     return results
 
 
 # ----------------------------------------------------------------------------- reference API
-def main(example_file, graph_file, u_methods, u_outfiles, b_methods, b_outfiles):
-    """similarity.main (similarity.py:11-18)."""
+def main(example_file, graph_file, u_methods, u_outfiles, b_methods, b_outfiles, *, sidecar=False):
+    """similarity.main (similarity.py:11-18). ``sidecar=True`` also writes each score file's
+    binary twin ``<file>.npz`` (util.write_sidecar)."""
     datetime.datetime.now()
     print("Loading examples...")
     examples = util.load_json(example_file)
     print("Loading graph...")
     G = blp.load_edge_list(graph_file)
-    users(examples, G, u_methods, u_outfiles)
-    business(examples, G, b_methods, b_outfiles)
+    users(examples, G, u_methods, u_outfiles, sidecar=sidecar)
+    business(examples, G, b_methods, b_outfiles, sidecar=sidecar)
 
 
-def users(examples, G, methods, outfiles):
+def users(examples, G, methods, outfiles, *, sidecar=False):
     """similarity.users (similarity.py:20-61): x = user (exact 2-hop set), y = business."""
     print("Scoring user side on the device...")
-    return _run_side(examples, G, methods, outfiles, _U_BITS, side=0)
+    return _run_side(examples, G, methods, outfiles, _U_BITS, side=0, sidecar=sidecar)
 
 
-def business(examples, G, methods, outfiles, *, fix_adamic=False):
+def business(examples, G, methods, outfiles, *, fix_adamic=False, sidecar=False):
     """similarity.business (similarity.py:63-106): x = business (exact 2-hop set), y = user."""
     print("Scoring business side on the device...")
     table = dict(_B_BITS)
     if fix_adamic:
         table["adamic_adar"] = blp.ADAMIC
-    return _run_side(examples, G, methods, outfiles, table, side=1)
+    return _run_side(examples, G, methods, outfiles, table, side=1, sidecar=sidecar)
 
 
 # Scalar set-level definitions (similarity.py:108-126), kept for API compatibility with

@@ -27,6 +27,41 @@ def write_json(d, fname):
         f.write(json.dumps(d))
 
 
+def write_sidecar(d, fname):
+    """Binary sidecar of a score file: ``fname + '.npz'`` with the same pairs and values as
+    ``write_json(d, fname)``: int64 ``users`` / ``businesses``, float64
+    ``scores`` and a bool ``is_int`` (JSON ints: CN counts and the reference's int 0s), in
+    the dict's order. Loads in milliseconds where json.loads of million-pair files takes
+    seconds; ``load_scores`` reads it back as the same dict."""
+    import numpy as np
+
+    us, bs, vals, ints = [], [], [], []
+    for u, inner in d.items():
+        for b, v in inner.items():
+            us.append(int(u))
+            bs.append(int(b))
+            vals.append(float(v))
+            ints.append(isinstance(v, int) and not isinstance(v, bool))
+    np.savez(fname + ".npz", users=np.array(us, np.int64), businesses=np.array(bs, np.int64),
+             scores=np.array(vals, np.float64), is_int=np.array(ints, bool))
+
+
+def load_scores(fname):
+    """The score dict of ``fname``: from its binary sidecar when present, else the JSON."""
+    import os
+
+    import numpy as np
+
+    side = fname + ".npz"
+    if not os.path.exists(side):
+        return load_json(fname)
+    z = np.load(side)
+    out = {}
+    for u, b, v, i in zip(z["users"].tolist(), z["businesses"].tolist(), z["scores"].tolist(), z["is_int"].tolist()):
+        out.setdefault(str(u), {})[str(b)] = int(v) if i else v
+    return out
+
+
 def load_json_lines(fname):
     """Yields one JSON object per line of fname (util.py:24-28)."""
     with open(fname) as f:

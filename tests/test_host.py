@@ -134,3 +134,20 @@ def test_walk_transition_matrix_matches_networkx(case):
     for j in range(n):
         W[j, ci[rp[j]:rp[j + 1]]] = val[rp[j]:rp[j + 1]]
     np.testing.assert_allclose(W.T, T, rtol=1e-15, atol=0)
+
+
+@pytest.mark.parametrize("case,name", [("bip/test", "u_adamic.json"), ("bip/test", "u_cn.json"),
+                                       ("edge", "u_jaccard.json")])
+def test_sidecar_round_trips_the_score_file(case, name, tmp_path):
+    """util.write_sidecar / load_scores: the binary twin of a reference
+    score file reads back as the identical dict (keys, order, int/float types, values)."""
+    import util
+
+    ref = golden(case, name)
+    f = str(tmp_path / name)
+    util.write_sidecar(ref, f)
+    got = util.load_scores(f)
+    assert list(got) == list(ref)
+    for u in ref:
+        assert list(got[u].items()) == list(ref[u].items())
+        assert [type(v) for v in got[u].values()] == [type(v) for v in ref[u].values()]
