@@ -2,10 +2,12 @@
 
 ``svd_user_business(data_dir, k=50)`` (svd.py:7-31) keeps the reference's steps: rows and
 columns in user.json / business.json key order (svd.py:9-14), the binary user x business
-matrix from graph.txt (svd.py:16-21), ``scipy.sparse.linalg.svds(M, k)`` on the host
-(svd.py:24 -- the reference's own factorisation), ``us = u * s``
-(svd.py:25); every candidate pair's ``np.dot(us[row], vt[:, col])`` (svd.py:28-30) is
-computed by libblp's fp64 kernel, and the scores are written to ./data/<dir>/svd.json.
+matrix from graph.txt (svd.py:16-21), the rank-k factorisation of svd.py:24-25 --
+``blp.factor.svds`` on the GPU (block subspace iteration, agrees with ARPACK to ~1e-13 of
+the score scale) for matrices with at least 256 rows and columns, the reference's own
+``scipy.sparse.linalg.svds`` for smaller ones (a 128-column block does not fit them) -- and
+every candidate pair's ``np.dot(us[row], vt[:, col])`` (svd.py:28-30) computed by libblp's
+fp64 kernel; the scores are written to ./data/<dir>/svd.json.
 ``svd_topk`` is new: the full-candidate ranking (every business per user) on fp64 MFMA.
 """
 import numpy as np
@@ -36,12 +38,26 @@ def user_business_matrix(data_dir):
     return users, businesses, examples, user_to_row, business_to_column, M
 
 
-def svd_user_business(data_dir, k=50, device=0):
+def factorize(M, k, factor="auto", device=0):
+    """svd.py:24-25 -> (us = u * s, vt). factor: 'gpu' (blp.factor.svds), 'host' (scipy
+    ARPACK, the reference's numeric) or 'auto' (gpu when M has >= 256 rows and columns and
+    k < 128)."""
+    from blp import factor as F
+
+    if factor == "auto":
+        factor = "gpu" if min(M.shape) >= 256 and k < F.block_width() else "host"
+    if factor == "gpu":
+        us, s, v = F.svds(M, k=k, device=device, return_us=True)
+        return us, np.ascontiguousarray(v.T)
+    u, s, vt = sparse.linalg.svds(M, k=k)
+    return u * s, vt
+
+
+def svd_user_business(data_dir, k=50, device=0, factor="auto"):
     print("Loading data and building user-business matrix...")
     users, businesses, examples, user_to_row, business_to_column, M = user_business_matrix(data_dir)
     print("Computing singular value decomposition...")
-    u, s, vt = sparse.linalg.svds(M, k=k)
-    us = u * s
+    us, vt = factorize(M, k, factor, device)
     print("Writing results...")
     scores = score_examples(examples, us, vt, user_to_row, business_to_column, device=device)
     i = 0

@@ -189,6 +189,28 @@ int blp_svd_topk(blp_svd* h, const int32_t* users, int64_t n_users, const int64_
 int blp_svd_stats(blp_svd* h, int which, double* total_ms, int64_t* launches); /* 0 pairs, 1 top-k */
 int blp_svd_sync(blp_svd* h);
 
+/* ---------------------------------------------------------------- truncated-SVD factorisation
+ * Replaces scipy.sparse.linalg.svds(M, k) (svd.py:24) on a binary n_rows x n_cols CSR matrix:
+ * block subspace iteration with Rayleigh-Ritz on a P-column fp64 block (P =
+ * blp_fact_block_width(), 128). The device runs the SpMMs, Gram products and block updates;
+ * the caller (blp.factor.svds) does the P x P Cholesky / eigen solves and the iteration
+ * control. Blocks are row-major [rows][P] host arrays at the boundary.
+ *   blp_fact_step:    Z = M Q, W = M^T Z, S = Q^T W (S returned, P x P)
+ *   blp_fact_gram_w:  G = W^T W
+ *   blp_fact_apply_w: W R -> Q (to_q) or back into W
+ *   blp_fact_extract: us = Z V[:, :k] (= U S), v = Q V[:, :k]                             */
+typedef struct blp_fact blp_fact;
+int blp_fact_create(const int64_t* row_ptr, const int32_t* col_idx, int64_t n_rows, int64_t n_cols, int device,
+                    blp_fact** out);
+int blp_fact_destroy(blp_fact* f);
+int blp_fact_block_width(void);
+int blp_fact_set_q(blp_fact* f, const double* q);
+int blp_fact_step(blp_fact* f, double* S);
+int blp_fact_gram_w(blp_fact* f, double* G);
+int blp_fact_apply_w(blp_fact* f, const double* R, int to_q);
+int blp_fact_extract(blp_fact* f, const double* V, int k, double* us, double* v);
+int blp_fact_stats(blp_fact* f, int which, double* total_ms, int64_t* launches); /* 0 SpMM, 1 dense */
+
 /* ---------------------------------------------------------------- damped random walks
  * Replaces random_walks.run_random_walk(s) (random_walks.py:9-53): p <- scale * (p . T) for
  * `iterations` steps from e_start (the reference: scale = 1 - jump_p = 0.8, 10 steps).
