@@ -1,5 +1,6 @@
 """Device-resident truncated-SVD factors: reconstruction of svd.py:25-30 on the GPU."""
 import ctypes
+import time
 
 import numpy as np
 
@@ -95,6 +96,7 @@ class FactorStats:
         self.spmm_ms = 0.0
         self.dense_ms = 0.0
         self.ritz = None
+        self.create_s = 0.0
 
 
 def _sym(S):
@@ -126,19 +128,23 @@ def svds(M, k=6, tol=1e-12, max_iter=400, seed=0, device=0, stats=None, return_u
     rp = np.ascontiguousarray(M.indptr, np.int64)
     ci = np.ascontiguousarray(M.indices, np.int32)
     h = ctypes.c_void_p()
+    t_create = time.perf_counter()
     check(lib().blp_fact_create(ptr(rp), ptr(ci), n_rows, n_cols, device, ctypes.byref(h)))
     st = stats if stats is not None else FactorStats()
     try:
+        # a Gaussian start block: the first step's W = M^T M Q0 is orthonormalised on the device
+        # like every later one (only span(Q0) matters); its Ritz values are not used
+        st.create_s = time.perf_counter() - t_create
         rng = np.random.default_rng(seed)
-        q, _ = np.linalg.qr(rng.standard_normal((n_cols, Pw)))
-        check(lib().blp_fact_set_q(h, ptr(np.ascontiguousarray(q))))
+        q = rng.standard_normal((n_cols, Pw)) / np.sqrt(n_cols)
+        check(lib().blp_fact_set_q(h, ptr(q)))
         S = np.empty((Pw, Pw))
         G = np.empty((Pw, Pw))
         prev = None
         for it in range(1, max_iter + 1):
             check(lib().blp_fact_step(h, ptr(S)))
             lam = np.sort(np.linalg.eigvalsh(_sym(S)))[::-1][:k]
-            if prev is not None and st.converged_at is None and np.max(np.abs(lam - prev) / np.abs(lam)) < tol:
+            if it > 1 and prev is not None and st.converged_at is None and np.max(np.abs(lam - prev) / np.abs(lam)) < tol:
                 st.converged_at = it
             prev = lam
             st.iterations = it
