@@ -11,6 +11,7 @@
 // distance-3 marks over [lo3, hi3). Positives are emitted first (in the caller's order),
 // then the sampled negatives in ascending dense id.
 #include <algorithm>
+#include <cstdlib>
 
 #include "blp_internal.h"
 
@@ -51,8 +52,40 @@ __device__ inline bool keep_negative(uint64_t seed, int u, int b, double rate) {
 
 __device__ inline bool bit_test(const uint32_t* bm, int64_t r) { return (bm[r >> 5] >> (r & 31)) & 1u; }
 
-__global__ __launch_bounds__(H_BLOCK) void k_hop3(Hop3Args a) {
-  __shared__ uint32_t lds[H_WORDS];
+// The two bitmaps live in LDS, or -- universes wider than LDS (configs 4/5) -- in a private
+// HBM slot per workgroup: workgroup-scope atomics (done in the XCD's L2) and agent-scope fences
+// between phases (drain the stores, invalidate the CU's L1), as k_score_global (pairs.hip).
+template <bool G>
+__device__ inline void bit_or(uint32_t* p, uint32_t v) {
+  if (G)
+    __hip_atomic_fetch_or(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  else
+    atomicOr(p, v);
+}
+
+template <bool G>
+__device__ inline void bit_and(uint32_t* p, uint32_t v) {
+  if (G)
+    __hip_atomic_fetch_and(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  else
+    atomicAnd(p, v);
+}
+
+template <bool G>
+__device__ inline void phase_sync() {
+  if (G) __threadfence();
+  __syncthreads();
+}
+
+template <bool G>
+__global__ __launch_bounds__(H_BLOCK) void k_hop3(Hop3Args a, uint32_t* gbm, int64_t gwords) {
+  uint32_t* lds;
+  if constexpr (G) {
+    lds = gbm + (int64_t)blockIdx.x * gwords;
+  } else {
+    __shared__ uint32_t lds_bm[H_WORDS];
+    lds = lds_bm;
+  }
   __shared__ int s_item;
   __shared__ unsigned s_warp[H_BLOCK / 64];
   __shared__ unsigned long long s_base;
@@ -63,27 +96,27 @@ __global__ __launch_bounds__(H_BLOCK) void k_hop3(Hop3Args a) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   for (;;) {
     if (threadIdx.x == 0) s_item = (int)atomicAdd(&a.counters[0], 1ull);
-    __syncthreads();
+    phase_sync<G>();
     const int it = s_item;
     if (it >= a.n_src) break;
     const int x = a.src[it];
     for (int i = threadIdx.x; i < a.w2 + w3; i += H_BLOCK) lds[i] = 0;
-    __syncthreads();
+    phase_sync<G>();
     const int64_t xb = a.rp[x], xe = a.rp[x + 1];
     // H2 marks: N(N(x)); one wave per z, lanes stride the row
     for (int64_t k = xb + wid; k < xe; k += H_BLOCK / 64) {
       const int z = a.ci[k];
       for (int64_t e = a.rp[z] + lane; e < a.rp[z + 1]; e += 64) {
         const int64_t r = (int64_t)a.ci[e] - a.lo2;
-        if (r >= 0 && r < span2) atomicOr(&bm2[r >> 5], 1u << (r & 31));
+        if (r >= 0 && r < span2) bit_or<G>(&bm2[r >> 5], 1u << (r & 31));
       }
     }
-    __syncthreads();
+    phase_sync<G>();
     for (int64_t k = xb + threadIdx.x; k <= xe; k += H_BLOCK) {
       const int64_t r = (k == xe ? (int64_t)x : (int64_t)a.ci[k]) - a.lo2;
-      if (r >= 0 && r < span2) atomicAnd(&bm2[r >> 5], ~(1u << (r & 31)));
+      if (r >= 0 && r < span2) bit_and<G>(&bm2[r >> 5], ~(1u << (r & 31)));
     }
-    __syncthreads();
+    phase_sync<G>();
     // distance-3 marks: N(H2(x)); each thread walks the set bits of its H2 words
     for (int wi = threadIdx.x; wi < a.w2; wi += H_BLOCK) {
       uint32_t bits = bm2[wi];
@@ -93,23 +126,23 @@ __global__ __launch_bounds__(H_BLOCK) void k_hop3(Hop3Args a) {
         const int w = (int)(a.lo2 + (int64_t)wi * 32 + t);
         for (int64_t e = a.rp[w]; e < a.rp[w + 1]; ++e) {
           const int64_t r = (int64_t)a.ci[e] - a.lo3;
-          if (r >= 0 && r < span3) atomicOr(&bm3[r >> 5], 1u << (r & 31));
+          if (r >= 0 && r < span3) bit_or<G>(&bm3[r >> 5], 1u << (r & 31));
         }
       }
     }
-    __syncthreads();
+    phase_sync<G>();
     // exact distance: drop x, N(x) and H2(x) from the distance-3 marks
     for (int64_t k = xb + threadIdx.x; k <= xe; k += H_BLOCK) {
       const int64_t r = (k == xe ? (int64_t)x : (int64_t)a.ci[k]) - a.lo3;
-      if (r >= 0 && r < span3) atomicAnd(&bm3[r >> 5], ~(1u << (r & 31)));
+      if (r >= 0 && r < span3) bit_and<G>(&bm3[r >> 5], ~(1u << (r & 31)));
     }
     // H2 ∩ [lo3, hi3) (general graphs only: the ranges are disjoint for bipartite files)
     {
       const int64_t olo = max(a.lo2, a.lo3), ohi = min(a.hi2, a.hi3);
       for (int64_t v = olo + threadIdx.x; v < ohi; v += H_BLOCK)
-        if (bit_test(bm2, v - a.lo2)) atomicAnd(&bm3[(v - a.lo3) >> 5], ~(1u << ((v - a.lo3) & 31)));
+        if (bit_test(bm2, v - a.lo2)) bit_and<G>(&bm3[(v - a.lo3) >> 5], ~(1u << ((v - a.lo3) & 31)));
     }
-    __syncthreads();
+    phase_sync<G>();
     // positives first (caller order), cleared from the candidate marks
     const int pb = a.pos_off[it], pe = a.pos_off[it + 1];
     if (threadIdx.x == 0) {
@@ -126,7 +159,7 @@ __global__ __launch_bounds__(H_BLOCK) void k_hop3(Hop3Args a) {
         }
       }
     }
-    __syncthreads();
+    phase_sync<G>();
     // sampled negatives: per-thread contiguous word ranges keep ascending id order
     const int per = (w3 + H_BLOCK - 1) / H_BLOCK;
     const int w_beg = min(w3, (int)threadIdx.x * per), w_end = min(w3, w_beg + per);
@@ -146,7 +179,7 @@ __global__ __launch_bounds__(H_BLOCK) void k_hop3(Hop3Args a) {
       if (lane >= d) inc += t;
     }
     if (lane == 63) s_warp[wid] = inc;
-    __syncthreads();
+    phase_sync<G>();
     if (threadIdx.x == 0) {
       unsigned run = 0;
       for (int w = 0; w < H_BLOCK / 64; ++w) {
@@ -156,7 +189,7 @@ __global__ __launch_bounds__(H_BLOCK) void k_hop3(Hop3Args a) {
       }
       s_base = atomicAdd(&a.counters[1], (unsigned long long)run);
     }
-    __syncthreads();
+    phase_sync<G>();
     unsigned long long o = s_base + s_warp[wid] + inc - mine;
     for (int wi = w_beg; wi < w_end; ++wi) {
       uint32_t bits = bm3[wi];
@@ -174,7 +207,7 @@ __global__ __launch_bounds__(H_BLOCK) void k_hop3(Hop3Args a) {
         }
       }
     }
-    __syncthreads();
+    phase_sync<G>();
   }
 }
 
@@ -213,19 +246,18 @@ extern "C" int blp_hop3_sample(blp_graph* g, const int32_t* src, int64_t n_src, 
     }
   if (lo3 > hi3) lo3 = hi3 = 0;
   const int64_t w2 = (((hi2 - lo2) + 31) / 32 + 3) / 4 * 4, w3 = ((hi3 - lo3) + 31) / 32;
-  if (w2 + w3 > H_WORDS)
-    return fail(BLP_E_UNSUP, "blp_hop3_sample: 2-hop + 3-hop universes exceed one workgroup's LDS (" +
-                                 std::to_string(hi2 - lo2) + " + " + std::to_string(hi3 - lo3) + " nodes)");
+  const bool global = w2 + w3 > H_WORDS || getenv("BLP_HOP3_FORCE_GLOBAL");
+  const int64_t gwords = (w2 + w3 + 3) / 4 * 4;
   for (int64_t i = 0; i < (n_src ? pos_off[n_src] : 0); ++i)
     BLP_CHECK(pos_y[i] >= 0 && pos_y[i] < n, BLP_E_ARG, "blp_hop3_sample: positive id out of range");
   int rc = set_device(g);
   if (rc) return rc;
   Hop3Args a{};
   void *d_src = nullptr, *d_off = nullptr, *d_pos = nullptr, *d_cnt = nullptr, *d_x = nullptr, *d_y = nullptr,
-       *d_l = nullptr;
+       *d_l = nullptr, *d_gbm = nullptr;
   const int64_t npos = n_src ? pos_off[n_src] : 0;
   auto cleanup = [&]() {
-    for (void* p : {d_src, d_off, d_pos, d_cnt, d_x, d_y, d_l})
+    for (void* p : {d_src, d_off, d_pos, d_cnt, d_x, d_y, d_l, d_gbm})
       if (p) (void)hipFree(p);
   };
   auto hip = [&](hipError_t e, const char* what) {
@@ -243,6 +275,7 @@ extern "C" int blp_hop3_sample(blp_graph* g, const int32_t* src, int64_t n_src, 
   if ((rc = hip(hipMalloc(&d_x, 4 * dcap), "hipMalloc"))) return rc;
   if ((rc = hip(hipMalloc(&d_y, 4 * dcap), "hipMalloc"))) return rc;
   if ((rc = hip(hipMalloc(&d_l, dcap), "hipMalloc"))) return rc;
+  if (global && (rc = hip(hipMalloc(&d_gbm, 4 * (size_t)gwords * g->n_cu), "hipMalloc (HBM bitmaps)"))) return rc;
   if (n_src) {
     if ((rc = hip(hipMemcpy(d_src, src, 4 * n_src, hipMemcpyHostToDevice), "hipMemcpy"))) return rc;
     if ((rc = hip(hipMemcpy(d_off, pos_off, 4 * (n_src + 1), hipMemcpyHostToDevice), "hipMemcpy"))) return rc;
@@ -270,7 +303,10 @@ extern "C" int blp_hop3_sample(blp_graph* g, const int32_t* src, int64_t n_src, 
   hipEvent_t t0;
   if ((rc = timer_begin(g, K_HOP3, &t0))) return cleanup(), rc;
   if (n_src) {
-    hipLaunchKernelGGL(k_hop3, dim3(g->n_cu), dim3(H_BLOCK), 0, g->stream, a);
+    if (global)
+      hipLaunchKernelGGL(k_hop3<true>, dim3(g->n_cu), dim3(H_BLOCK), 0, g->stream, a, (uint32_t*)d_gbm, gwords);
+    else
+      hipLaunchKernelGGL(k_hop3<false>, dim3(g->n_cu), dim3(H_BLOCK), 0, g->stream, a, (uint32_t*)nullptr, gwords);
     if ((rc = hip(hipGetLastError(), "k_hop3 launch"))) return rc;
   }
   if ((rc = timer_end(g, K_HOP3, t0))) return cleanup(), rc;

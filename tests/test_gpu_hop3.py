@@ -38,8 +38,10 @@ def test_hop3_matches_reference_fixture(gpu):
         assert got[u] == {b: l for b, l in ex[u].items()}
 
 
-@pytest.mark.parametrize("seed", [0, 1])
-def test_hop3_sets_vs_oracle(gpu, seed):
+@pytest.mark.parametrize("seed,hbm", [(0, False), (1, False), (0, True)])
+def test_hop3_sets_vs_oracle(gpu, seed, hbm, monkeypatch):
+    if hbm:  # the HBM-bitmap variant (universes wider than LDS: configs 4/5)
+        monkeypatch.setenv("BLP_HOP3_FORCE_GLOBAL", "1")
     rng = np.random.default_rng(seed)
     a, b = bipartite_edges(rng, 40000, 3000, 250000)
     G = blp.DeviceGraph(a, b)
