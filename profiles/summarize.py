@@ -46,7 +46,7 @@ def main():
         k["write_kb"] = w["avg_kb"] if w else None
         if f and w:
             k["hbm_bytes_corrected"] = 2 * f["avg_kb"] * 1024 + w["avg_kb"] * 1024
-    here = os.path.dirname(os.path.abspath(__file__))
+    here = os.environ.get("PROFILE_OUT") or os.path.dirname(os.path.abspath(__file__))
     with open(os.path.join(here, name + ".json"), "w") as fh:
         json.dump(ks, fh, indent=1)
     lines = ["# %s — rocprofv3 --kernel-trace --stats (+ separate FETCH_SIZE / WRITE_SIZE passes)" % name, "",
