@@ -160,7 +160,7 @@ __global__ __launch_bounds__(GB_BLOCK) void k_bucket_group(const int32_t* __rest
                                                            int32_t xlo, int64_t xspan, int64_t np, int32_t* __restrict__ off,
                                                            int32_t* __restrict__ cnt, int32_t* __restrict__ bucket_active,
                                                            int32_t* __restrict__ g_out, int64_t* __restrict__ g_yb,
-                                                           int32_t* __restrict__ g_yl) {
+                                                           int32_t* __restrict__ g_yl, int32_t* __restrict__ g_y) {
   constexpr int PER = KEYS / GB_BLOCK;
   __shared__ int h[KEYS];
   __shared__ int red[GB_BLOCK / 64];
@@ -203,6 +203,7 @@ __global__ __launch_bounds__(GB_BLOCK) void k_bucket_group(const int32_t* __rest
     g_out[pos] = i;
     g_yb[pos] = st;
     g_yl[pos] = (int32_t)(rp[yi + 1] - st);
+    if (g_y) g_y[pos] = yi;
   }
 }
 
@@ -735,6 +736,206 @@ __global__ __launch_bounds__(BLOCK) void k_score_global(ScoreArgs a, uint32_t* g
   }
 }
 
+// ------------------------------------------------------------------ chunk-parallel scorer
+// Universes between one and eight 512K-bit chunks (the user side of config 2: 1M users). A
+// 125 KB bitmap would hold one workgroup per CU (16 waves) and the scorer is latency-bound, so
+// the universe is cut into C chunks of 64 KB bitmaps and every (source, chunk) is an
+// independent item: two workgroups per CU (32 waves). Rows are sorted, so a chunk reads only
+// its slice of each row N(z) / N(y) -- the slice bounds come from a per-row split table, and
+// no element is read twice. Items are source-major (both chunks of a source run at the same
+// time on different CUs and share its rows in L2). Partial counts, fixed-point AA sums and
+// |H2| partials go to HBM; k_split_combine adds them and computes Jaccard.
+__global__ void k_row_splits(const int64_t* __restrict__ rp, const int32_t* __restrict__ ci, int64_t n, int64_t lo,
+                             int64_t cap_bits, int C, int32_t* __restrict__ rsplit) {
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = rp[v], e = rp[v + 1];
+    for (int c = 0; c <= C; ++c) {
+      const int64_t bound = c == C ? INT64_MAX : lo + c * cap_bits;
+      int64_t l = b, h = e;
+      while (l < h) {
+        const int64_t m = (l + h) >> 1;
+        if (ci[m] < bound) l = m + 1; else h = m;
+      }
+      rsplit[v * (C + 1) + c] = (int32_t)(l - b);
+    }
+  }
+}
+
+template <int BLOCK, int CAP_WORDS, int SEG, int K>
+__global__ __launch_bounds__(BLOCK, 8) void k_score_split(ScoreArgs a, const int32_t* __restrict__ g_y,
+                                                       const int32_t* __restrict__ rsplit, int C,
+                                                       uint32_t* __restrict__ pcn, unsigned long long* __restrict__ paa,
+                                                       uint32_t* __restrict__ ph2, int64_t np) {
+  constexpr int NW = BLOCK / 64;
+  __shared__ uint32_t bm[CAP_WORDS];
+  __shared__ int64_t s_start[SEG];
+  __shared__ int32_t s_off[SEG + 1];
+  __shared__ uint32_t s_cn[SEG];
+  __shared__ unsigned long long s_aa[SEG];
+  __shared__ unsigned long long red64[NW];
+  __shared__ int red[NW];
+  __shared__ int s_item;
+  __shared__ int s_nhot;
+  __shared__ blp::HotRow s_hot[HOT_LIST];
+  const int64_t CAP_BITS = a.cap_bits;
+  const bool want_j = (a.mask & BLP_JACCARD) != 0;
+  const bool want_a = (a.mask & BLP_ADAMIC) != 0;
+  uint4* bm4 = reinterpret_cast<uint4*>(bm);
+  const int64_t n_items = (int64_t)a.misc->n_active * C;
+  for (;;) {
+    if (threadIdx.x == 0) s_item = atomicAdd(&a.misc->queue, 1);
+    __syncthreads();
+    const int64_t item = s_item;
+    __syncthreads();
+    if (item >= n_items) break;
+    const int s = (int)(item / C), c = (int)(item % C);
+    const int x = a.active[s];
+    const int pbeg = a.off[x], pcnt = a.cnt[x];
+    const int64_t xb = a.rp[x], xe = a.rp[x + 1];
+    const int hslot = a.heavy_slot ? a.heavy_slot[x] : -1;
+    const int64_t c0 = a.lo + (int64_t)c * CAP_BITS;
+    const int64_t width = max<int64_t>(min(a.hi, c0 + CAP_BITS) - c0, 0);
+    const int nw4 = (int)((((width + 31) >> 5) + 3) >> 2);
+    if (hslot >= 0) {
+      const uint4* src4 = reinterpret_cast<const uint4*>(a.heavy_bm + (int64_t)hslot * a.hb_words + ((c0 - a.lo) >> 5));
+      for (int i = threadIdx.x; i < nw4; i += BLOCK) bm4[i] = src4[i];
+      __syncthreads();
+    } else {
+      if (threadIdx.x == 0) s_nhot = 0;
+      __syncthreads();
+      if (a.hot_idx) {
+        for (int64_t k = xb + threadIdx.x; k < xe; k += BLOCK) {
+          const int hi = a.hot_idx[a.ci[k]];
+          if (hi >= 0) {
+            const int slot = atomicAdd(&s_nhot, 1);
+            if (slot < HOT_LIST) s_hot[slot] = a.hot_tab[hi];
+          }
+        }
+      }
+      __syncthreads();
+      const int nhot = s_nhot <= HOT_LIST ? s_nhot : 0;
+      const int64_t q0 = c0 >> 7;
+      for (int q = threadIdx.x; q < nw4; q += BLOCK) {
+        uint4 v = make_uint4(0, 0, 0, 0);
+        for (int r = 0; r < nhot; ++r) {
+          const int64_t qq = q0 + q - s_hot[r].vlo;
+          if (qq >= 0 && qq < s_hot[r].nvec) {
+            const uint4 pv = a.hot_pool[s_hot[r].vec_off + qq];
+            v.x |= pv.x;
+            v.y |= pv.y;
+            v.z |= pv.z;
+            v.w |= pv.w;
+          }
+        }
+        bm4[q] = v;
+      }
+      __syncthreads();
+      for (int64_t k0 = xb; k0 < xe; k0 += SEG) {
+        const int ns = (int)min<int64_t>(SEG, xe - k0);
+        int len = 0;
+        if ((int)threadIdx.x < ns) {
+          const int z = a.ci[k0 + threadIdx.x];
+          const int32_t* sp = rsplit + (int64_t)z * (C + 1) + c;
+          s_start[threadIdx.x] = a.rp[z] + sp[0];
+          len = (nhot && a.hot_idx[z] >= 0) ? 0 : sp[1] - sp[0];  // dense rows were OR-ed in
+        }
+        int tot;
+        const int ex = block_exscan<BLOCK>(len, red, &tot);
+        if ((int)threadIdx.x < ns) s_off[threadIdx.x] = ex;
+        if (threadIdx.x == 0) s_off[ns] = tot;
+        __syncthreads();
+        mp_build<BLOCK, K>(a.ci, s_start, s_off, ns, c0, width, bm, threadIdx.x);
+        __syncthreads();
+      }
+    }
+    // exact distance 2 inside this chunk: drop x and N(x)
+    const int64_t nx_lo = xe > xb ? a.ci[xb] : 0, nx_hi = xe > xb ? a.ci[xe - 1] : -1;
+    if (nx_hi >= c0 && nx_lo < c0 + width) {
+      for (int64_t k = xb + threadIdx.x; k < xe; k += BLOCK) {
+        const int64_t r = (int64_t)a.ci[k] - c0;
+        if (r >= 0 && r < width) atomicAnd(&bm[r >> 5], ~(1u << (r & 31)));
+      }
+    }
+    if (threadIdx.x == 0 && x >= c0 && x < c0 + width) atomicAnd(&bm[(x - c0) >> 5], ~(1u << ((x - c0) & 31)));
+    __syncthreads();
+    if (want_j) {
+      unsigned long long pc = 0;
+      for (int i = threadIdx.x; i < nw4; i += BLOCK) {
+        const uint4 q = bm4[i];
+        pc += __popc(q.x) + __popc(q.y) + __popc(q.z) + __popc(q.w);
+      }
+      const unsigned long long h2 = block_sum_u64<BLOCK>(pc, red64);
+      if (threadIdx.x == 0) ph2[(int64_t)x * C + c] = (uint32_t)h2;
+    }
+    for (int sb = 0; sb < pcnt; sb += SEG) {
+      const int ns = min(SEG, pcnt - sb);
+      int len = 0;
+      if ((int)threadIdx.x < ns) {
+        const int gp = pbeg + sb + threadIdx.x;
+        const int32_t* sp = rsplit + (int64_t)g_y[gp] * (C + 1) + c;
+        s_start[threadIdx.x] = a.g_yb[gp] + sp[0];
+        len = sp[1] - sp[0];
+        s_cn[threadIdx.x] = 0;
+        s_aa[threadIdx.x] = 0;
+      }
+      int tot;
+      const int ex = block_exscan<BLOCK>(len, red, &tot);
+      if ((int)threadIdx.x < ns) s_off[threadIdx.x] = ex;
+      if (threadIdx.x == 0) s_off[ns] = tot;
+      __syncthreads();
+      if (want_a)
+        mp_scan<BLOCK, K, true>(a.ci, a.aaw, s_start, s_off, ns, c0, width, bm, s_cn, s_aa, threadIdx.x);
+      else
+        mp_scan<BLOCK, K, false>(a.ci, a.aaw, s_start, s_off, ns, c0, width, bm, s_cn, s_aa, threadIdx.x);
+      __syncthreads();
+      for (int t = threadIdx.x; t < ns; t += BLOCK) {
+        const int64_t gp = pbeg + sb + t;
+        pcn[(int64_t)c * np + gp] = s_cn[t];
+        if (want_a) paa[(int64_t)c * np + gp] = s_aa[t];
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// one wave per active source: sum the chunk partials of each of its pairs, then Jaccard
+__global__ __launch_bounds__(256) void k_split_combine(ScoreArgs a, int C, const uint32_t* __restrict__ pcn,
+                                                      const unsigned long long* __restrict__ paa,
+                                                      const uint32_t* __restrict__ ph2, int64_t np) {
+  const int lane = threadIdx.x & 63;
+  const int n_active = a.misc->n_active;
+  const bool want_j = (a.mask & BLP_JACCARD) != 0;
+  const bool want_a = (a.mask & BLP_ADAMIC) != 0;
+  for (int s = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; s < n_active; s += (gridDim.x * blockDim.x) >> 6) {
+    const int x = a.active[s];
+    long long h2 = 0;
+    if (want_j)
+      for (int c = 0; c < C; ++c) h2 += ph2[(int64_t)x * C + c];
+    const int pbeg = a.off[x], pcnt = a.cnt[x];
+    for (int t = lane; t < pcnt; t += 64) {
+      const int64_t gp = pbeg + t;
+      unsigned cn = 0;
+      unsigned long long aa = 0;
+      for (int c = 0; c < C; ++c) {
+        cn += pcn[(int64_t)c * np + gp];
+        if (want_a) aa += paa[(int64_t)c * np + gp];
+      }
+      const int p = a.g_out[gp];
+      a.cn[p] = cn;
+      if (want_a) a.aa[p] = (double)aa * (1.0 / blp::AA_SCALE);
+      if (want_j) {
+        const long long uni = h2 + a.g_yl[gp] - (long long)cn;
+        if (uni <= 0) {
+          a.jac[p] = __builtin_nan("");
+          atomicOr(&a.misc->zero_div, 1);
+        } else {
+          a.jac[p] = (double)cn / (double)uni;
+        }
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------ wave-per-source scorer
 // For small node universes (the business side of a review graph: H2(v) ⊂ businesses) the
 // per-source work is ~2K elements, so a workgroup-wide pass is all barrier and latency.
@@ -889,6 +1090,7 @@ constexpr int CAP_SMALL = 4096, CAP_MED = 16384, CAP_LARGE = 34816;
 constexpr int BLOCK_SMALL = 256, BLOCK_MED = 512, BLOCK_LARGE = 1024;
 constexpr int SEG_SMALL = 256, SEG_MED = 512, SEG_LARGE = 512;
 constexpr int G_BLOCK = 1024, G_SEG = 512;  // HBM-bitmap scorer
+constexpr int S_BLOCK = 1024, S_CAP = 16384, S_SEG = 512;  // chunk-parallel scorer: 64 KiB chunks, 2 blocks / CU
 
 inline int variant_block(int v) { return v == V_SMALL ? BLOCK_SMALL : v == V_MED ? BLOCK_MED : BLOCK_LARGE; }
 inline int64_t variant_cap_bits(int v) { return 32ll * (v == V_SMALL ? CAP_SMALL : v == V_MED ? CAP_MED : CAP_LARGE); }
@@ -919,6 +1121,12 @@ struct blp_batch {
   bool use_hot = false;  // some source has a dense row in N(x)
   bool wave = false;     // wave-per-source scorer
   bool global = false;   // HBM-bitmap scorer (universe wider than LDS)
+  int split = 0;         // chunk-parallel scorer: universe cut into `split` LDS chunks, 2 workgroups / CU
+  int32_t* d_gy = nullptr;     // grouped position -> y (split mode)
+  int32_t* d_rsplit = nullptr; // [n][split + 1] row offsets where neighbour ids cross chunk boundaries
+  uint32_t* d_pcn = nullptr;   // [split][n_pairs] partial counts
+  unsigned long long* d_paa = nullptr;  // [split][n_pairs] partial fixed-point AA
+  uint32_t* d_ph2 = nullptr;   // [n][split] partial |H2|
   uint32_t* d_gbm = nullptr;
   int64_t gwords = 0, gslots = 0;
   int shift = 10, nb = 1, nblk = 1;
@@ -1045,9 +1253,26 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
     if (v >= 128 && v % 128 == 0 && v < b->cap_bits) b->cap_bits = v;
   }
   b->chunks = span <= b->cap_bits ? 1 : (int)((span + b->cap_bits - 1) / b->cap_bits);
+  // wider than one LDS bitmap, up to eight 512K-bit chunks: chunk-parallel scorer, (source,
+  // chunk) items on 64 KiB bitmaps, two workgroups per CU -- 5.7x the HBM-bitmap scorer on
+  // the 2M-user universe of config 4 (BLP_NO_SPLIT: off; BLP_SPLIT=C: force C chunks)
+  {
+    const int64_t sbits = 32ll * S_CAP;
+    int C = 0;
+    if (const char* e = getenv("BLP_SPLIT"))
+      C = std::max(0, std::min(8, atoi(e)));
+    else if (span > variant_cap_bits(V_LARGE) && span <= 8 * sbits && !getenv("BLP_NO_SPLIT"))
+      C = (int)((span + sbits - 1) / sbits);
+    if (C >= 2 && span > 0) {
+      b->split = C;
+      b->cap_bits = ((span + C - 1) / C + 127) / 128 * 128;
+      b->chunks = 1;
+      b->variant = V_LARGE;  // k_heavy's LDS capacity
+    }
+  }
   // wider than LDS: one HBM bitmap per workgroup instead of an H2 rebuild per LDS chunk
   // (BLP_NO_GLOBAL keeps the chunked path, BLP_FORCE_GLOBAL selects HBM on any universe)
-  b->global = (b->chunks > 1 && !getenv("BLP_NO_GLOBAL")) || getenv("BLP_FORCE_GLOBAL");
+  b->global = !b->split && ((b->chunks > 1 && !getenv("BLP_NO_GLOBAL")) || getenv("BLP_FORCE_GLOBAL"));
   if (b->global) b->chunks = 1;
   auto bail = [&](int rc) {
     blp_batch_destroy(b);
@@ -1057,13 +1282,16 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   if (rc) return bail(rc);
   // wave-per-source scorer: opt-in (BLP_WAVE=1). With heavy sources split finely the block
   // kernels are faster on the business side of config 2 (1.46 vs 2.01 ms, profiles/probe_sides.py)
-  b->wave = span <= (int64_t)W_CAP * 32 && b->chunks == 1 && !b->global && getenv("BLP_WAVE") &&
+  b->wave = span <= (int64_t)W_CAP * 32 && b->chunks == 1 && !b->global && !b->split && getenv("BLP_WAVE") &&
             !getenv("BLP_NO_WAVE");
   int per_cu = 1;
   if (b->wave) {
     BLP_HIP_OR(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_score_wave<W_WAVES, W_CAP, 8>, W_WAVES * 64, 0),
                bail);
     per_cu = std::max(per_cu, 1) * W_WAVES;  // workers are waves
+  } else if (b->split) {
+    BLP_HIP_OR(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_score_split<S_BLOCK, S_CAP, S_SEG, 8>,
+                                                            S_BLOCK, 0), bail);
   } else if ((rc = variant_occupancy(b->variant, &per_cu))) {
     return bail(rc);
   }
@@ -1080,7 +1308,7 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   if (const char* e = getenv("BLP_HEAVY_WORK")) item_work = std::max<int64_t>(1, atoll(e));  // test knob
   std::vector<int32_t> heavy_slot;
   std::vector<HeavyItem> items;
-  if (b->chunks == 1 && span > 0 && !b->global) {
+  if (b->chunks == 1 && span > 0 && !b->global && (!b->split || span <= variant_cap_bits(V_LARGE))) {
     for (size_t i = 0; i < srcs.size(); ++i) {
       if (work[i] <= 2 * item_work) continue;
       if (heavy_slot.empty()) heavy_slot.assign((size_t)n, -1);
@@ -1117,6 +1345,20 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
     if (b->shift > 15 || b->nb > NB_MAX) return bail(fail(BLP_E_UNSUP, "blp_batch_create: source id range too wide"));
     b->nblk = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)g->n_cu * 2, (n_pairs + 4095) / 4096));
     b->per_blk = (n_pairs + b->nblk - 1) / b->nblk;
+  }
+  // ---- chunk-parallel scorer: per-row chunk offsets and partial-result buffers
+  if (b->split && n_pairs) {
+    const int C = b->split;
+    if (hipMalloc(&b->d_gy, 4 * (size_t)n_pairs) != hipSuccess ||
+        hipMalloc(&b->d_rsplit, 4 * (size_t)n * (C + 1)) != hipSuccess ||
+        hipMalloc(&b->d_pcn, 4 * (size_t)n_pairs * C) != hipSuccess ||
+        hipMalloc(&b->d_paa, 8 * (size_t)n_pairs * C) != hipSuccess ||
+        hipMalloc(&b->d_ph2, 4 * (size_t)n * C) != hipSuccess)
+      return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: split buffers"));
+    hipLaunchKernelGGL(k_row_splits, dim3(2048), dim3(256), 0, g->stream, g->d_rp, g->d_ci, n, b->lo, b->cap_bits, C,
+                       b->d_rsplit);
+    BLP_HIP_OR(hipGetLastError(), bail);
+    BLP_HIP_OR(hipStreamSynchronize(g->stream), bail);
   }
   // ---- HBM bitmap slots: one per resident workgroup of k_score_global
   if (b->global && n_pairs) {
@@ -1162,7 +1404,7 @@ int blp_batch_destroy(blp_batch* b) {
   timer_release(b->t_score);
   timer_release(b->t_group);
   void* ps[] = {b->d_x,    b->d_y,    b->d_cn,   b->d_jac,  b->d_aa,          b->d_gout,        b->d_gyb,
-                b->d_gyl,  b->d_misc, b->d_heavy_slot, b->d_heavy_bm, b->d_heavy_items, b->d_gbm};
+                b->d_gyl,  b->d_misc, b->d_heavy_slot, b->d_heavy_bm, b->d_heavy_items, b->d_gbm, b->d_gy, b->d_rsplit, b->d_pcn, b->d_paa, b->d_ph2};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   delete b;
@@ -1173,8 +1415,8 @@ int blp_batch_plan(const blp_batch* b, int64_t* lo, int64_t* hi, int* chunks, in
   BLP_CHECK(b, BLP_E_ARG, "blp_batch_plan: null batch");
   if (lo) *lo = b->lo;
   if (hi) *hi = b->hi;
-  if (chunks) *chunks = b->global ? 0 : b->chunks;  // 0: HBM-bitmap scorer
-  if (block) *block = b->wave ? 64 : b->global ? G_BLOCK : variant_block(b->variant);
+  if (chunks) *chunks = b->global ? 0 : b->split ? -b->split : b->chunks;  // 0: HBM bitmap; -C: chunk-parallel
+  if (block) *block = b->wave ? 64 : b->global ? G_BLOCK : b->split ? S_BLOCK : variant_block(b->variant);
   if (heavy) *heavy = (int)b->n_heavy;
   return BLP_OK;
 }
@@ -1218,7 +1460,7 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   hipLaunchKernelGGL(k_bucket_group<K>, dim3(b->nb), dim3(GB_BLOCK), 0, g->stream, b->d_x, b->d_y, g->d_rp, tmp, hoff, \
                      b->nblk, b->nb, b->shift, b->xlo, b->xspan, np, g->off.as<int32_t>(), g->cnt.as<int32_t>(), bact,  \
                      b->d_gout,                                                                                       \
-                     b->d_gyb, b->d_gyl)
+                     b->d_gyb, b->d_gyl, b->d_gy)
     if (keys <= 256)
       BLP_GROUP_LAUNCH(256);
     else if (keys <= 1024)
@@ -1288,7 +1530,16 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   a.cap_bits = b->cap_bits;
   a.mask = mask | BLP_CN;  // counts are always produced (Jaccard needs them)
   a.dq = b->dq;
-  if (np && b->global) {
+  if (np && b->split) {
+    int per_cu = 1;
+    BLP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_score_split<S_BLOCK, S_CAP, S_SEG, 8>, S_BLOCK, 0));
+    hipLaunchKernelGGL((k_score_split<S_BLOCK, S_CAP, S_SEG, 8>), dim3(g->n_cu * std::max(per_cu, 1)), dim3(S_BLOCK), 0,
+                       g->stream, a, b->d_gy, b->d_rsplit, b->split, b->d_pcn, b->d_paa, b->d_ph2, np);
+    BLP_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_split_combine, dim3(g->n_cu * 8), dim3(256), 0, g->stream, a, b->split, b->d_pcn, b->d_paa,
+                       b->d_ph2, np);
+    BLP_HIP(hipGetLastError());
+  } else if (np && b->global) {
     a.hot_idx = nullptr;
     hipLaunchKernelGGL((k_score_global<G_BLOCK, G_SEG, 8>), dim3((unsigned)b->gslots), dim3(G_BLOCK), 0, g->stream, a,
                        b->d_gbm, b->gwords);

@@ -24,10 +24,10 @@ def main():
         else:
             cur.append(a)
     groups.append(cur)
-    U, B, D = synth.CONFIGS["c2"]
+    U, B, D = synth.CONFIGS[os.environ.get("PROBE_CONFIG", "c2")]
     a, b = synth.review_edges(U, B, D, seed=0)
     G = blp.DeviceGraph(a, b)
-    x, y, _ = synth.make_examples(G, U, B, D, n_users=10000, rate=0.01, seed=0)
+    x, y, _ = synth.make_examples(G, U, B, D, n_users=int(os.environ.get("PROBE_USERS", "10000")), rate=0.01, seed=0)
     xs, ys = (x, y) if side == "user" else (y, x)
     for knobs in groups:
         saved = dict(os.environ)

@@ -81,6 +81,9 @@ def test_general_graph_exact_distance(gpu):
     {"BLP_CHUNK_BITS": "1024"},                         # wider than LDS: HBM-bitmap scorer
     {"BLP_CHUNK_BITS": "1024", "BLP_NO_GLOBAL": "1"},   # multi-chunk LDS bitmap universe
     {"BLP_FORCE_GLOBAL": "1"},                          # HBM-bitmap scorer on a small universe
+    {"BLP_SPLIT": "3"},                                 # chunk-parallel scorer, 3 chunks
+    {"BLP_SPLIT": "8", "BLP_HEAVY_WORK": "50"},         # ... 8 chunks, heavy sources pre-built
+    {"BLP_SPLIT": "2", "BLP_HOT_MIN": "8"},             # ... dense rows OR-ed per chunk
     {"BLP_HEAVY_WORK": "50"},                           # heavy sources pre-built by k_heavy
     {"BLP_HEAVY_WORK": "1"},                            # one row per heavy item
     {"BLP_CHUNK_BITS": "2048", "BLP_HEAVY_WORK": "50", "BLP_NO_GLOBAL": "1"},  # multi-chunk: no heavy path
@@ -106,6 +109,8 @@ def test_kernel_paths_vs_oracle(gpu, knobs, monkeypatch):
         assert G.batch(y, x).plan()["heavy"] > 0
     if "BLP_FORCE_GLOBAL" in knobs or ("BLP_CHUNK_BITS" in knobs and "BLP_NO_GLOBAL" not in knobs):
         assert G.batch(x, y).plan()["chunks"] == 0  # HBM-bitmap scorer
+    if "BLP_SPLIT" in knobs:
+        assert G.batch(x, y).plan()["chunks"] == -int(knobs["BLP_SPLIT"])  # chunk-parallel scorer
 
 
 def test_many_pairs_per_source_vs_oracle(gpu):
