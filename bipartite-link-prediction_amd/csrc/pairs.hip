@@ -745,9 +745,10 @@ __global__ __launch_bounds__(BLOCK) void k_score_global(ScoreArgs a, uint32_t* g
 // no element is read twice. Items are source-major (both chunks of a source run at the same
 // time on different CUs and share its rows in L2). Partial counts, fixed-point AA sums and
 // |H2| partials go to HBM; k_split_combine adds them and computes Jaccard.
-__global__ void k_row_splits(const int64_t* __restrict__ rp, const int32_t* __restrict__ ci, int64_t n, int64_t lo,
-                             int64_t cap_bits, int C, int32_t* __restrict__ rsplit) {
-  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x) {
+__global__ void k_row_splits(const int64_t* __restrict__ rp, const int32_t* __restrict__ ci, int64_t v0, int64_t n,
+                             int64_t lo, int64_t cap_bits, int C, int32_t* __restrict__ rsplit) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t v = v0 + i;
     const int64_t b = rp[v], e = rp[v + 1];
     for (int c = 0; c <= C; ++c) {
       const int64_t bound = c == C ? INT64_MAX : lo + c * cap_bits;
@@ -756,14 +757,14 @@ __global__ void k_row_splits(const int64_t* __restrict__ rp, const int32_t* __re
         const int64_t m = (l + h) >> 1;
         if (ci[m] < bound) l = m + 1; else h = m;
       }
-      rsplit[v * (C + 1) + c] = (int32_t)(l - b);
+      rsplit[i * (C + 1) + c] = (int32_t)(l - b);
     }
   }
 }
 
 template <int BLOCK, int CAP_WORDS, int SEG, int K>
 __global__ __launch_bounds__(BLOCK, 8) void k_score_split(ScoreArgs a, const int32_t* __restrict__ g_y,
-                                                       const int32_t* __restrict__ rsplit, int C,
+                                                       const int32_t* __restrict__ rsplit, int64_t rs_lo, int C,
                                                        uint32_t* __restrict__ pcn, unsigned long long* __restrict__ paa,
                                                        uint32_t* __restrict__ ph2, int64_t np) {
   constexpr int NW = BLOCK / 64;
@@ -835,7 +836,7 @@ __global__ __launch_bounds__(BLOCK, 8) void k_score_split(ScoreArgs a, const int
         int len = 0;
         if ((int)threadIdx.x < ns) {
           const int z = a.ci[k0 + threadIdx.x];
-          const int32_t* sp = rsplit + (int64_t)z * (C + 1) + c;
+          const int32_t* sp = rsplit + ((int64_t)z - rs_lo) * (C + 1) + c;
           s_start[threadIdx.x] = a.rp[z] + sp[0];
           len = (nhot && a.hot_idx[z] >= 0) ? 0 : sp[1] - sp[0];  // dense rows were OR-ed in
         }
@@ -865,14 +866,14 @@ __global__ __launch_bounds__(BLOCK, 8) void k_score_split(ScoreArgs a, const int
         pc += __popc(q.x) + __popc(q.y) + __popc(q.z) + __popc(q.w);
       }
       const unsigned long long h2 = block_sum_u64<BLOCK>(pc, red64);
-      if (threadIdx.x == 0) ph2[(int64_t)x * C + c] = (uint32_t)h2;
+      if (threadIdx.x == 0) ph2[(int64_t)s * C + c] = (uint32_t)h2;
     }
     for (int sb = 0; sb < pcnt; sb += SEG) {
       const int ns = min(SEG, pcnt - sb);
       int len = 0;
       if ((int)threadIdx.x < ns) {
         const int gp = pbeg + sb + threadIdx.x;
-        const int32_t* sp = rsplit + (int64_t)g_y[gp] * (C + 1) + c;
+        const int32_t* sp = rsplit + ((int64_t)g_y[gp] - rs_lo) * (C + 1) + c;
         s_start[threadIdx.x] = a.g_yb[gp] + sp[0];
         len = sp[1] - sp[0];
         s_cn[threadIdx.x] = 0;
@@ -910,7 +911,7 @@ __global__ __launch_bounds__(256) void k_split_combine(ScoreArgs a, int C, const
     const int x = a.active[s];
     long long h2 = 0;
     if (want_j)
-      for (int c = 0; c < C; ++c) h2 += ph2[(int64_t)x * C + c];
+      for (int c = 0; c < C; ++c) h2 += ph2[(int64_t)s * C + c];
     const int pbeg = a.off[x], pcnt = a.cnt[x];
     for (int t = lane; t < pcnt; t += 64) {
       const int64_t gp = pbeg + t;
@@ -1091,6 +1092,7 @@ constexpr int BLOCK_SMALL = 256, BLOCK_MED = 512, BLOCK_LARGE = 1024;
 constexpr int SEG_SMALL = 256, SEG_MED = 512, SEG_LARGE = 512;
 constexpr int G_BLOCK = 1024, G_SEG = 512;  // HBM-bitmap scorer
 constexpr int S_BLOCK = 1024, S_CAP = 16384, S_SEG = 512;  // chunk-parallel scorer: 64 KiB chunks, 2 blocks / CU
+constexpr int S_MAX_CHUNKS = 128;                          // up to 67M-node universes (config 5: 50M users)
 
 inline int variant_block(int v) { return v == V_SMALL ? BLOCK_SMALL : v == V_MED ? BLOCK_MED : BLOCK_LARGE; }
 inline int64_t variant_cap_bits(int v) { return 32ll * (v == V_SMALL ? CAP_SMALL : v == V_MED ? CAP_MED : CAP_LARGE); }
@@ -1122,6 +1124,7 @@ struct blp_batch {
   bool wave = false;     // wave-per-source scorer
   bool global = false;   // HBM-bitmap scorer (universe wider than LDS)
   int split = 0;         // chunk-parallel scorer: universe cut into `split` LDS chunks, 2 workgroups / CU
+  int64_t rs_lo = 0;     // first node of the split table
   int32_t* d_gy = nullptr;     // grouped position -> y (split mode)
   int32_t* d_rsplit = nullptr; // [n][split + 1] row offsets where neighbour ids cross chunk boundaries
   uint32_t* d_pcn = nullptr;   // [split][n_pairs] partial counts
@@ -1206,6 +1209,7 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   std::vector<int64_t> work;
   int64_t scan_work = 0;
   bool any_hot = false;
+  int64_t rows_lo = INT64_MAX, rows_hi = INT64_MIN;  // nodes whose rows are read (the y and the z in N(x))
   const int32_t* hot = g->h_hot_idx.empty() ? nullptr : g->h_hot_idx.data();
   for (int64_t i = 0; i < n_pairs; ++i) {
     const int32_t xi = x[i], yi = y[i];
@@ -1215,6 +1219,8 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
       hi = std::max<int64_t>(hi, (int64_t)ci[rp[yi + 1] - 1] + 1);
     }
     scan_work += rp[yi + 1] - rp[yi];
+    rows_lo = std::min<int64_t>(rows_lo, yi);
+    rows_hi = std::max<int64_t>(rows_hi, (int64_t)yi + 1);
     if (!seen[xi]) {
       seen[xi] = 1;
       srcs.push_back(xi);
@@ -1222,6 +1228,8 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
       for (int64_t k = rp[xi]; k < rp[xi + 1]; ++k) {
         const int32_t z = ci[k];
         wsum += rp[z + 1] - rp[z];
+        rows_lo = std::min<int64_t>(rows_lo, z);
+        rows_hi = std::max<int64_t>(rows_hi, (int64_t)z + 1);
         any_hot |= hot && hot[z] >= 0;
         if (rp[z + 1] > rp[z]) {
           lo = std::min<int64_t>(lo, ci[rp[z]]);
@@ -1260,8 +1268,8 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
     const int64_t sbits = 32ll * S_CAP;
     int C = 0;
     if (const char* e = getenv("BLP_SPLIT"))
-      C = std::max(0, std::min(8, atoi(e)));
-    else if (span > variant_cap_bits(V_LARGE) && span <= 8 * sbits && !getenv("BLP_NO_SPLIT"))
+      C = std::max(0, std::min(S_MAX_CHUNKS, atoi(e)));
+    else if (span > variant_cap_bits(V_LARGE) && span <= S_MAX_CHUNKS * sbits && !getenv("BLP_NO_SPLIT"))
       C = (int)((span + sbits - 1) / sbits);
     if (C >= 2 && span > 0) {
       b->split = C;
@@ -1349,14 +1357,16 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   // ---- chunk-parallel scorer: per-row chunk offsets and partial-result buffers
   if (b->split && n_pairs) {
     const int C = b->split;
+    b->rs_lo = rows_lo;
+    const int64_t nrows = std::max<int64_t>(rows_hi - rows_lo, 1);
     if (hipMalloc(&b->d_gy, 4 * (size_t)n_pairs) != hipSuccess ||
-        hipMalloc(&b->d_rsplit, 4 * (size_t)n * (C + 1)) != hipSuccess ||
+        hipMalloc(&b->d_rsplit, 4 * (size_t)nrows * (C + 1)) != hipSuccess ||
         hipMalloc(&b->d_pcn, 4 * (size_t)n_pairs * C) != hipSuccess ||
         hipMalloc(&b->d_paa, 8 * (size_t)n_pairs * C) != hipSuccess ||
-        hipMalloc(&b->d_ph2, 4 * (size_t)n * C) != hipSuccess)
+        hipMalloc(&b->d_ph2, 4 * (size_t)std::max<int64_t>(b->n_sources, 1) * C) != hipSuccess)
       return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: split buffers"));
-    hipLaunchKernelGGL(k_row_splits, dim3(2048), dim3(256), 0, g->stream, g->d_rp, g->d_ci, n, b->lo, b->cap_bits, C,
-                       b->d_rsplit);
+    hipLaunchKernelGGL(k_row_splits, dim3(2048), dim3(256), 0, g->stream, g->d_rp, g->d_ci, rows_lo, nrows, b->lo,
+                       b->cap_bits, C, b->d_rsplit);
     BLP_HIP_OR(hipGetLastError(), bail);
     BLP_HIP_OR(hipStreamSynchronize(g->stream), bail);
   }
@@ -1534,7 +1544,7 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
     int per_cu = 1;
     BLP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_score_split<S_BLOCK, S_CAP, S_SEG, 8>, S_BLOCK, 0));
     hipLaunchKernelGGL((k_score_split<S_BLOCK, S_CAP, S_SEG, 8>), dim3(g->n_cu * std::max(per_cu, 1)), dim3(S_BLOCK), 0,
-                       g->stream, a, b->d_gy, b->d_rsplit, b->split, b->d_pcn, b->d_paa, b->d_ph2, np);
+                       g->stream, a, b->d_gy, b->d_rsplit, b->rs_lo, b->split, b->d_pcn, b->d_paa, b->d_ph2, np);
     BLP_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_split_combine, dim3(g->n_cu * 8), dim3(256), 0, g->stream, a, b->split, b->d_pcn, b->d_paa,
                        b->d_ph2, np);
