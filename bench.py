@@ -44,6 +44,12 @@ def log(*a):
 from blp.dist import Dist  # noqa: E402  (torch.distributed plumbing: barrier, max/sum, exchange)
 
 
+def _device(dist):
+    """The rank's GPU: LOCAL_RANK (one process per GPU). BLP_DEVICE overrides it -- used only
+    to rehearse the multi-rank path with several ranks on a one-GPU box."""
+    return int(os.environ.get("BLP_DEVICE", dist.local))
+
+
 def alg_bytes(G, x, y, mask, cn=None):
     """SURVEY.md §8(d) algorithmic bytes of one scorer pass over pairs (x -> y).
 
@@ -167,7 +173,7 @@ def run_svd(args):
     from blp.factor import DeviceSVD
 
     dist = Dist()
-    dev = dist.local
+    dev = _device(dist)
     blp.lib()
     U, B, D = synth.CONFIGS["c4"]
     t0 = time.time()
@@ -343,7 +349,7 @@ def run_topk(args):
     from blp.topk import TopK
 
     dist = Dist()
-    dev = dist.local
+    dev = _device(dist)
     blp.lib()
     U, B, D = synth.CONFIGS[args.config]
     t0 = time.time()
@@ -417,7 +423,7 @@ def run_sharded(args):
     from blp import dist as bd
 
     d = Dist(exchange=True)
-    dev = d.local
+    dev = _device(d)
     blp.lib()
     U, B, D = synth.CONFIGS[args.config]
     blocks = bd.user_blocks(U, d.world)
@@ -439,6 +445,8 @@ def run_sharded(args):
     exch_s = d.max(exch_local)
     recv_bytes = 8 * (sum(counts) - counts[d.rank])
     del u, b
+    if not a_all.is_cuda:  # gloo exchange (rehearsal without RCCL): the partials arrive on the host
+        a_all, b_all = a_all.to("cuda:%d" % dev), b_all.to("cuda:%d" % dev)
     t0 = time.perf_counter()
     G = blp.DeviceGraph.from_device_edges(a_all.data_ptr(), b_all.data_ptr(), len(a_all), U + B, U, device=dev)
     build_s = time.perf_counter() - t0
@@ -531,7 +539,7 @@ def main():
         return run_sharded(args)
 
     dist = Dist()
-    dev = dist.local
+    dev = _device(dist)
     blp.lib()
     U, B, D = synth.CONFIGS[args.config]
     t0 = time.time()
