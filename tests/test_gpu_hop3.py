@@ -95,3 +95,23 @@ def test_general_graph_hop3_vs_oracle(gpu):
         got = np.sort(G.node_ids[y[x == s]])
         np.testing.assert_array_equal(got, ids[members[k:k + counts[i]]])
         k += counts[i]
+
+
+def test_dataset_maker_drop_in_matches_reference(gpu, tmp_path):
+    """dataset_maker.make_examples (dataset_maker.py:80-159) on the reference fixture's graph
+    with negative_sample_rate=1.0 and every eligible user: the written examples.json equals
+    the reference's (exact hop-3 candidate sets and labels)."""
+    import json
+    import shutil
+
+    import dataset_maker
+
+    d = os.path.join(GOLDEN, "hop3")
+    for f in ("graph.txt", "new_edges.txt"):
+        shutil.copy(os.path.join(d, f), tmp_path / f)
+    a, b = read_edges(os.path.join(d, "graph.txt"))
+    (tmp_path / "review.json").write_text(json.dumps({str(u): {} for u in np.unique(a)}))
+    got = dataset_maker.make_examples(str(tmp_path) + "/", n_users=10**9, negative_sample_rate=1.0)
+    ref = load(os.path.join(d, "examples.json"))
+    assert {u: v for u, v in ref.items() if v} == got
+    assert json.loads((tmp_path / "examples.json").read_text()) == got
