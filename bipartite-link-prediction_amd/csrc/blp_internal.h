@@ -88,6 +88,11 @@ struct HotRow {
   int32_t vlo;
   int32_t nvec;
 };
+// Four consecutive column ids loaded as one 16-byte vector at 4-byte alignment (gfx950 global
+// loads accept unaligned dwordx4).
+struct __attribute__((aligned(4))) U4a {
+  int32_t x, y, z, w;
+};
 int build_hot_index(blp_graph* g);
 void free_hot_index(blp_graph* g);
 int timer_begin(blp_graph* g, int k, hipEvent_t* start);

@@ -281,6 +281,22 @@ __device__ inline void mp_fetch(const int32_t* __restrict__ ci, const int64_t* s
   int s = seg_search(s_off, ns, f0);
   int next = s_off[s + 1];
   int64_t pos = s_start[s] + (f0 - s_off[s]);
+  if (f0 + K <= next) {
+    // all K elements in one row (the common case on long rows): K/4 16-byte loads, which
+    // gfx950 serves at 4-byte alignment, instead of K dword loads
+    const blp::U4a* p = reinterpret_cast<const blp::U4a*>(ci + pos);
+#pragma unroll
+    for (int j = 0; j < K / 4; ++j) {
+      const blp::U4a v = p[j];
+      w[4 * j] = v.x;
+      w[4 * j + 1] = v.y;
+      w[4 * j + 2] = v.z;
+      w[4 * j + 3] = v.w;
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) sk[k] = s;
+    return;
+  }
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const int f = f0 + k;
@@ -327,7 +343,9 @@ __device__ inline void mp_build(const int32_t* __restrict__ ci, const int64_t* s
 }
 
 // Test every element of the ns segments against the bitmap; per-segment hit counts and
-// fixed-point Adamic-Adar sums accumulate into s_cn / s_aa (LDS). Pipelined like mp_build.
+// fixed-point Adamic-Adar sums accumulate into s_cn / s_aa (LDS). Pipelined like mp_build;
+// the weight gathers of a step are issued BEFORE the next step's loads, so waiting for them
+// (vmcnt counts in issue order) does not also wait for the prefetch.
 template <int NT, int K, bool AA>
 __device__ inline void mp_scan(const int32_t* __restrict__ ci, const long long* __restrict__ aaw, const int64_t* s_start,
                                const int32_t* s_off, int ns, int64_t c0, int64_t width, const uint32_t* bm,
@@ -337,8 +355,6 @@ __device__ inline void mp_scan(const int32_t* __restrict__ ci, const long long* 
   int w[K], sk[K];
   mp_fetch<K>(ci, s_start, s_off, ns, T, tid * K, w, sk);
   for (int base = 0; base < T; base += STEP) {
-    int wn[K], skn[K];
-    mp_fetch<K>(ci, s_start, s_off, ns, T, base + STEP + tid * K, wn, skn);
     bool hit[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -350,6 +366,8 @@ __device__ inline void mp_scan(const int32_t* __restrict__ ci, const long long* 
 #pragma unroll
       for (int k = 0; k < K; ++k) wt[k] = hit[k] ? aaw[w[k]] : 0ll;
     }
+    int wn[K], skn[K];
+    mp_fetch<K>(ci, s_start, s_off, ns, T, base + STEP + tid * K, wn, skn);
     int cur = sk[0];
     unsigned c = 0;
     unsigned long long acc = 0;
@@ -1519,6 +1537,7 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   a.rp = g->d_rp;
   a.ci = g->d_ci;
   a.aaw = g->d_aaw_fx;
+
   a.off = g->off.as<int32_t>();
   a.cnt = g->cnt.as<int32_t>();
   a.active = g->active.as<int32_t>();
