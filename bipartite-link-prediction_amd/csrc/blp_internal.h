@@ -67,6 +67,11 @@ struct blp_graph {
   int64_t* d_rp = nullptr;   // [n+1]
   int32_t* d_ci = nullptr;   // [nnz]
   long long* d_aaw_fx = nullptr;  // [n] Adamic-Adar weight per node, fixed point 2^-40 (or null)
+  // weight-coded copy of d_ci for the scorers: ci | code(ci) << id_bits, code 1..255 naming
+  // one of the graph's most used weights (d_wtab[code]), 0 = look up d_aaw_fx (or null)
+  int32_t* d_ci_w = nullptr;
+  int id_bits = 31;
+  long long* d_wtab = nullptr;  // [256]; d_wtab[0] = 0
   // dense-row index: rows dense enough in their id range also stored as bitmaps (hot.hip)
   int32_t* d_hot_idx = nullptr;  // [n] hot row number or -1
   void* d_hot_tab = nullptr;     // [n_hot] blp::HotRow

@@ -8,8 +8,21 @@
 #include <cmath>
 #include <cstring>
 #include <mutex>
+#include <unordered_map>
 
 #include "blp_internal.h"
+
+namespace {
+
+__global__ void k_code_ids(const int32_t* __restrict__ ci, int64_t nnz, const uint8_t* __restrict__ ncode, int bits,
+                           int32_t* __restrict__ out) {
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < nnz; e += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t v = ci[e];
+    out[e] = v | (int32_t)((uint32_t)ncode[v] << bits);
+  }
+}
+
+}  // namespace
 
 namespace blp {
 
@@ -117,6 +130,54 @@ int timers_collect(blp_graph* g) {
   return BLP_OK;
 }
 
+// Weight-coded column ids: the scorers' Adamic-Adar term of a common neighbour w is a
+// per-node weight (similarity.py:121-125, a function of deg(w)). Instead of gathering aaw[w]
+// per hit, the id stream itself carries a code in its free high bits: codes 1..255 go to the
+// distinct weights with the most occurrences in col_idx (on a review graph the few distinct
+// user degrees cover every user), code 0 means "gather aaw". Only when the ids leave at least
+// one free bit below the sign bit.
+int build_weight_codes(blp_graph* g, const int64_t* row_ptr, const std::vector<long long>& fx) {
+  const int64_t n = g->n, nnz = g->nnz;
+  int bits = 1;
+  while (bits < 31 && (int64_t(1) << bits) < n) ++bits;
+  const int cbits = std::min(8, 31 - bits);
+  int max_codes = (1 << cbits) - 1;
+  if (const char* e = getenv("BLP_WCODES")) max_codes = std::min(max_codes, std::max(0, atoi(e)));  // test knob
+  std::vector<long long> wtab(256, 0);
+  BLP_HIP(hipMalloc(&g->d_wtab, sizeof(long long) * 256));  // always: code 0 reads wtab[0]
+  BLP_HIP(hipMemcpy(g->d_wtab, wtab.data(), sizeof(long long) * 256, hipMemcpyHostToDevice));
+  if (max_codes <= 0 || nnz == 0) return BLP_OK;
+  std::unordered_map<long long, int64_t> uses;
+  for (int64_t i = 0; i < n; ++i) uses[fx[i]] += row_ptr[i + 1] - row_ptr[i];
+  std::vector<std::pair<int64_t, long long>> order;
+  order.reserve(uses.size());
+  for (const auto& kv : uses)
+    if (kv.second > 0) order.emplace_back(-kv.second, kv.first);
+  std::sort(order.begin(), order.end());
+  std::unordered_map<long long, int> code;
+  for (size_t j = 0; j < order.size() && (int)j < max_codes; ++j) {
+    wtab[j + 1] = order[j].second;
+    code[order[j].second] = (int)j + 1;
+  }
+  std::vector<uint8_t> ncode((size_t)n, 0);
+  for (int64_t i = 0; i < n; ++i) {
+    const auto it = code.find(fx[i]);
+    if (it != code.end()) ncode[i] = (uint8_t)it->second;
+  }
+  uint8_t* d_ncode = nullptr;
+  BLP_HIP(hipMemcpy(g->d_wtab, wtab.data(), sizeof(long long) * 256, hipMemcpyHostToDevice));
+  BLP_HIP(hipMalloc(&g->d_ci_w, sizeof(int32_t) * nnz));
+  BLP_HIP(hipMalloc(&d_ncode, (size_t)n));
+  BLP_HIP(hipMemcpy(d_ncode, ncode.data(), (size_t)n, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(k_code_ids, dim3((unsigned)std::min<int64_t>((nnz + 255) / 256, 1 << 20)), dim3(256), 0, g->stream,
+                     g->d_ci, nnz, d_ncode, bits, g->d_ci_w);
+  BLP_HIP(hipGetLastError());
+  BLP_HIP(hipStreamSynchronize(g->stream));
+  BLP_HIP(hipFree(d_ncode));
+  g->id_bits = bits;
+  return BLP_OK;
+}
+
 }  // namespace blp
 
 using namespace blp;
@@ -216,6 +277,7 @@ int blp_graph_create(const int64_t* row_ptr, const int32_t* col_idx, int64_t n, 
            for (int64_t i = 0; i < n; ++i) fx[i] = llrint(aaw[i] * AA_SCALE);
            BLP_HIP(hipMalloc(&g->d_aaw_fx, sizeof(long long) * std::max<int64_t>(n, 1)));
            if (n) BLP_HIP(hipMemcpy(g->d_aaw_fx, fx.data(), sizeof(long long) * n, hipMemcpyHostToDevice));
+           if ((rc = build_weight_codes(g, row_ptr, fx)) != BLP_OK) return rc;
          }
          return BLP_OK;
        }()) != BLP_OK)
@@ -241,6 +303,8 @@ int blp_graph_destroy(blp_graph* g) {
   if (g->d_rp) (void)hipFree(g->d_rp);
   if (g->d_ci) (void)hipFree(g->d_ci);
   if (g->d_aaw_fx) (void)hipFree(g->d_aaw_fx);
+  if (g->d_ci_w) (void)hipFree(g->d_ci_w);
+  if (g->d_wtab) (void)hipFree(g->d_wtab);
   if (g->stream) (void)hipStreamDestroy(g->stream);
   delete g;
   return BLP_OK;

@@ -255,9 +255,9 @@ __device__ inline int block_exscan(int v, int* red, int* total) {
   return base + inc - v;
 }
 
-// last s in [0, ns) with off[s] <= f (requires off[0] <= f < off[ns])
-__device__ inline int seg_search(const int32_t* off, int ns, int f) {
-  int lo = 0, hi = ns;
+// last s in [lo, hi) with off[s] <= f (requires off[lo] <= f < off[hi])
+__device__ inline int seg_search(const int32_t* off, int ns, int f, int lo = 0, int hi = -1) {
+  if (hi < 0) hi = ns;
   while (hi - lo > 1) {
     const int mid = (lo + hi) >> 1;
     if (off[mid] <= f)
@@ -268,17 +268,42 @@ __device__ inline int seg_search(const int32_t* off, int ns, int f) {
   return lo;
 }
 
+// Segment hint table of a batch of segments: hint[j] = segment of element min(j << shift,
+// T - 1), for j <= ((T - 1) >> shift) + 1. A merge-path step then binary-searches only
+// [hint[f0 >> shift], hint[(f0 >> shift) + 1]] -- one or two LDS round trips on long rows
+// instead of log2(ns) dependent ones, which are most of a step's latency. Built once per
+// batch (every thread one search at most), ending with a barrier. Returns shift, or -1 (no
+// hint) when the batch is a single block step anyway.
+template <int BLOCK, int CAP>
+__device__ inline int build_hint(const int32_t* s_off, int ns, int step, int32_t* hint) {
+  const int T = s_off[ns];
+  if (CAP < 4 || T <= step) return -1;
+  int shift = 0;
+  while (((T - 1) >> shift) + 2 > CAP) ++shift;
+  const int nh = ((T - 1) >> shift) + 1;
+  for (int j = threadIdx.x; j <= nh; j += BLOCK) hint[j] = seg_search(s_off, ns, min(j << shift, T - 1));
+  __syncthreads();
+  return shift;
+}
+
 // Fetch one merge-path step: the K consecutive elements [f0, f0 + K) of the concatenated
-// segments (w = node id or -1, sk = segment or -1). One LDS binary search per K elements.
+// segments (w = node id or -1, sk = segment or -1). One LDS binary search per K elements
+// (narrowed by the hint table when given: shift >= 0).
 template <int K>
 __device__ inline void mp_fetch(const int32_t* __restrict__ ci, const int64_t* s_start, const int32_t* s_off, int ns,
-                                int T, int f0, int* w, int* sk) {
+                                int T, int f0, int* w, int* sk, const int32_t* hint = nullptr, int shift = -1) {
   if (f0 >= T) {
 #pragma unroll
     for (int k = 0; k < K; ++k) w[k] = sk[k] = -1;
     return;
   }
-  int s = seg_search(s_off, ns, f0);
+  int s;
+  if (shift >= 0) {
+    const int g = f0 >> shift;
+    s = seg_search(s_off, ns, f0, hint[g], hint[g + 1] + 1);
+  } else {
+    s = seg_search(s_off, ns, f0);
+  }
   int next = s_off[s + 1];
   int64_t pos = s_start[s] + (f0 - s_off[s]);
   if (f0 + K <= next) {
@@ -317,20 +342,29 @@ __device__ inline void mp_fetch(const int32_t* __restrict__ ci, const int64_t* s
 
 // Set the bits of every element of the ns segments (rows of ci) inside [c0, c0 + width).
 // Software-pipelined: the loads of step i+1 are in flight while step i's atomics issue.
+// ci may be the weight-coded copy of the column ids (ScoreArgs::cw): ids are ci & idmask.
+// Offset of element value v (an id, possibly weight-coded, or -1 = no element) in the chunk
+// [c0, c0 + width): one unsigned compare "< width" then tests both validity and range. keep =
+// idmask | sign bit, so -1 maps to >= 2^31 - c0 > width (c0 <= idmask, width < 2^31).
+__device__ inline uint32_t in_chunk(int v, uint32_t keep, uint32_t c0u) { return ((uint32_t)v & keep) - c0u; }
+
 template <int NT, int K, bool GLOBAL = false>
-__device__ inline void mp_build(const int32_t* __restrict__ ci, const int64_t* s_start, const int32_t* s_off, int ns,
-                                int64_t c0, int64_t width, uint32_t* bm, int tid) {
+__device__ inline void mp_build(const int32_t* __restrict__ ci, uint32_t idmask, const int64_t* s_start,
+                                const int32_t* s_off, int ns, int64_t c0, int64_t width, uint32_t* bm, int tid,
+                                const int32_t* hint = nullptr, int shift = -1) {
   const int T = s_off[ns];
   constexpr int STEP = NT * K;
+  const uint32_t keep = idmask | 0x80000000u, c0u = (uint32_t)c0, wu = (uint32_t)width;
   int w[K], sk[K];
-  mp_fetch<K>(ci, s_start, s_off, ns, T, tid * K, w, sk);
+  mp_fetch<K>(ci, s_start, s_off, ns, T, tid * K, w, sk, hint, shift);
   for (int base = 0; base < T; base += STEP) {
     int wn[K], skn[K];
-    mp_fetch<K>(ci, s_start, s_off, ns, T, base + STEP + tid * K, wn, skn);
+    mp_fetch<K>(ci, s_start, s_off, ns, T, base + STEP + tid * K, wn, skn, hint, shift);
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      const int64_t r = (int64_t)w[k] - c0;
-      if (w[k] >= 0 && r >= 0 && r < width) {
+      // one unsigned compare tests validity and range (see in_chunk)
+      const uint32_t r = in_chunk(w[k], keep, c0u);
+      if (r < wu) {
         if (GLOBAL)  // the workgroup's private HBM bitmap: the OR is done in the XCD's L2
           __hip_atomic_fetch_or(&bm[r >> 5], 1u << (r & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         else
@@ -346,50 +380,83 @@ __device__ inline void mp_build(const int32_t* __restrict__ ci, const int64_t* s
 // fixed-point Adamic-Adar sums accumulate into s_cn / s_aa (LDS). Pipelined like mp_build;
 // the weight gathers of a step are issued BEFORE the next step's loads, so waiting for them
 // (vmcnt counts in issue order) does not also wait for the prefetch.
+// ci may be the weight-coded copy (ScoreArgs::cw): an element is id | code << idbits; code c
+// > 0 has the weight wtab[c], code 0 falls back to the per-node table aaw[id].
+
 template <int NT, int K, bool AA>
-__device__ inline void mp_scan(const int32_t* __restrict__ ci, const long long* __restrict__ aaw, const int64_t* s_start,
+__device__ inline void mp_scan(const int32_t* __restrict__ ci, uint32_t idmask, int idbits,
+                               const long long* __restrict__ aaw, const long long* wtab, const int64_t* s_start,
                                const int32_t* s_off, int ns, int64_t c0, int64_t width, const uint32_t* bm,
-                               uint32_t* s_cn, unsigned long long* s_aa, int tid) {
+                               uint32_t* s_cn, unsigned long long* s_aa, int tid, const int32_t* hint = nullptr,
+                               int shift = -1) {
   const int T = s_off[ns];
   constexpr int STEP = NT * K;
+  const uint32_t keep = idmask | 0x80000000u, c0u = (uint32_t)c0, wu = (uint32_t)width;
   int w[K], sk[K];
-  mp_fetch<K>(ci, s_start, s_off, ns, T, tid * K, w, sk);
+  mp_fetch<K>(ci, s_start, s_off, ns, T, tid * K, w, sk, hint, shift);
   for (int base = 0; base < T; base += STEP) {
+    // the bitmap words and (AA) the code weights wtab[code] are read together, so one LDS
+    // round trip serves both; hits with code 0 then gather aaw, before the next step's loads
+    // are issued (rare on a coded id stream)
     bool hit[K];
+    long long wt[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      const int64_t r = (int64_t)w[k] - c0;
-      hit[k] = w[k] >= 0 && r >= 0 && r < width && ((bm[r >> 5] >> (r & 31)) & 1u);
+      const uint32_t r = in_chunk(w[k], keep, c0u);
+      const uint32_t word = bm[(r < wu ? r : 0u) >> 5];
+      if (AA) wt[k] = wtab[((uint32_t)w[k] >> idbits) & 255u];
+      hit[k] = r < wu && ((word >> (r & 31)) & 1u);
     }
-    long long wt[K];
     if (AA) {
+      bool any_esc = false;
 #pragma unroll
-      for (int k = 0; k < K; ++k) wt[k] = hit[k] ? aaw[w[k]] : 0ll;
+      for (int k = 0; k < K; ++k) any_esc |= hit[k] && ((uint32_t)w[k] >> idbits) == 0u;
+      if (any_esc) {
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+          if (hit[k] && ((uint32_t)w[k] >> idbits) == 0u) wt[k] = aaw[w[k] & idmask];
+      }
+#pragma unroll
+      for (int k = 0; k < K; ++k) wt[k] = hit[k] ? wt[k] : 0ll;
     }
     int wn[K], skn[K];
-    mp_fetch<K>(ci, s_start, s_off, ns, T, base + STEP + tid * K, wn, skn);
-    int cur = sk[0];
-    unsigned c = 0;
-    unsigned long long acc = 0;
+    mp_fetch<K>(ci, s_start, s_off, ns, T, base + STEP + tid * K, wn, skn, hint, shift);
+    if (sk[0] == sk[K - 1]) {  // the K elements in one segment (or none valid): one run
+      unsigned c = 0;
+      unsigned long long acc = 0;
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-      if (sk[k] != cur) {
-        if (c) {
-          atomicAdd(&s_cn[cur], c);
-          if (AA) atomicAdd(&s_aa[cur], acc);
-        }
-        cur = sk[k];
-        c = 0;
-        acc = 0;
-      }
-      if (hit[k]) {
-        ++c;
+      for (int k = 0; k < K; ++k) {
+        c += hit[k] ? 1u : 0u;
         if (AA) acc += (unsigned long long)wt[k];
       }
-    }
-    if (c && cur >= 0) {
-      atomicAdd(&s_cn[cur], c);
-      if (AA) atomicAdd(&s_aa[cur], acc);
+      if (c) {
+        atomicAdd(&s_cn[sk[0]], c);
+        if (AA) atomicAdd(&s_aa[sk[0]], acc);
+      }
+    } else {
+      int cur = sk[0];
+      unsigned c = 0;
+      unsigned long long acc = 0;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        if (sk[k] != cur) {
+          if (c) {
+            atomicAdd(&s_cn[cur], c);
+            if (AA) atomicAdd(&s_aa[cur], acc);
+          }
+          cur = sk[k];
+          c = 0;
+          acc = 0;
+        }
+        if (hit[k]) {
+          ++c;
+          if (AA) acc += (unsigned long long)wt[k];
+        }
+      }
+      if (c && cur >= 0) {
+        atomicAdd(&s_cn[cur], c);
+        if (AA) atomicAdd(&s_aa[cur], acc);
+      }
     }
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -448,7 +515,7 @@ __global__ __launch_bounds__(BLOCK) void k_heavy(HeavyArgs h) {
   for (int64_t k0 = it.kb; k0 < it.ke; k0 += SEG) {
     const int ns = (int)min<int64_t>(SEG, it.ke - k0);
     load_row_segments<BLOCK>(h.rp, h.ci, k0, ns, s_start, s_off, red);
-    mp_build<BLOCK, K>(h.ci, s_start, s_off, ns, h.lo, h.width, bm, threadIdx.x);
+    mp_build<BLOCK, K>(h.ci, 0x7fffffffu, s_start, s_off, ns, h.lo, h.width, bm, threadIdx.x);
     __syncthreads();
   }
   uint32_t* dst = h.heavy_bm + (int64_t)it.slot * h.hb_words;
@@ -463,6 +530,10 @@ struct ScoreArgs {
   const int64_t* rp;
   const int32_t* ci;
   const long long* aaw;    // fixed-point Adamic-Adar weights
+  const int32_t* cw;       // column ids streamed by build / scan: id | weight code << idbits
+  uint32_t idmask;
+  int idbits;
+  const long long* wtab;   // [256] fixed-point weight per code (code 0: use aaw)
   const int32_t* off;      // per node: first grouped position of its pairs
   const int32_t* cnt;      // per node: number of pairs with that source
   const int32_t* active;   // active sources
@@ -512,7 +583,13 @@ __global__ __launch_bounds__(BLOCK) void k_score(ScoreArgs a) {
   __shared__ int s_src;
   __shared__ int s_nhot;
   __shared__ blp::HotRow s_hot[HOT_LIST];
+  __shared__ long long s_wtab[256];
+  // hint table where the LDS allows it (the 64 KiB-bitmap variant keeps 2 workgroups per CU)
+  constexpr int HC = CAP_WORDS >= 34816 ? 2048 : CAP_WORDS >= 16384 ? 1 : 512;
+  __shared__ int32_t s_hint[HC];
 
+  if (a.wtab)  // visible after the first barrier
+    for (int i = threadIdx.x; i < 256; i += BLOCK) s_wtab[i] = a.wtab[i];
   const int64_t CAP_BITS = a.cap_bits;
   const int64_t span = a.hi - a.lo;
   const int nchunks = span <= CAP_BITS ? 1 : (int)((span + CAP_BITS - 1) / CAP_BITS);
@@ -583,7 +660,8 @@ __global__ __launch_bounds__(BLOCK) void k_score(ScoreArgs a) {
           for (int64_t k0 = xb; k0 < xe; k0 += SEG) {
             const int ns = (int)min<int64_t>(SEG, xe - k0);
             load_row_segments<BLOCK>(a.rp, a.ci, k0, ns, s_start, s_off, red, nhot ? a.hot_idx : nullptr);
-            mp_build<BLOCK, K>(a.ci, s_start, s_off, ns, c0, width, bm, threadIdx.x);
+            const int shift = build_hint<BLOCK, HC>(s_off, ns, BLOCK * K, s_hint);
+            mp_build<BLOCK, K>(a.cw, a.idmask, s_start, s_off, ns, c0, width, bm, threadIdx.x, s_hint, shift);
             __syncthreads();
           }
         }
@@ -621,10 +699,13 @@ __global__ __launch_bounds__(BLOCK) void k_score(ScoreArgs a) {
           if ((int)threadIdx.x < ns) s_off[threadIdx.x] = ex;
           if (threadIdx.x == 0) s_off[ns] = tot;
           __syncthreads();
+          const int shift = build_hint<BLOCK, HC>(s_off, ns, BLOCK * K, s_hint);
           if (want_a)
-            mp_scan<BLOCK, K, true>(a.ci, a.aaw, s_start, s_off, ns, c0, width, bm, s_cn, s_aa, threadIdx.x);
+            mp_scan<BLOCK, K, true>(a.cw, a.idmask, a.idbits, a.aaw, s_wtab, s_start, s_off, ns, c0, width, bm, s_cn,
+                                    s_aa, threadIdx.x, s_hint, shift);
           else
-            mp_scan<BLOCK, K, false>(a.ci, a.aaw, s_start, s_off, ns, c0, width, bm, s_cn, s_aa, threadIdx.x);
+            mp_scan<BLOCK, K, false>(a.cw, a.idmask, a.idbits, a.aaw, s_wtab, s_start, s_off, ns, c0, width, bm, s_cn,
+                                     s_aa, threadIdx.x, s_hint, shift);
           __syncthreads();
           for (int t = threadIdx.x; t < ns; t += BLOCK) {
             const int p = a.g_out[pbeg + sb + t];
@@ -694,7 +775,7 @@ __global__ __launch_bounds__(BLOCK) void k_score_global(ScoreArgs a, uint32_t* g
       for (int64_t k0 = xb; k0 < xe; k0 += SEG) {
         const int ns = (int)min<int64_t>(SEG, xe - k0);
         load_row_segments<BLOCK>(a.rp, a.ci, k0, ns, s_start, s_off, red, nullptr);
-        mp_build<BLOCK, K, true>(a.ci, s_start, s_off, ns, c0, width, bm, threadIdx.x);
+        mp_build<BLOCK, K, true>(a.cw, a.idmask, s_start, s_off, ns, c0, width, bm, threadIdx.x);
         __syncthreads();
       }
       for (int64_t k = xb + threadIdx.x; k <= xe; k += BLOCK) {  // drop N(x) and x itself
@@ -729,9 +810,9 @@ __global__ __launch_bounds__(BLOCK) void k_score_global(ScoreArgs a, uint32_t* g
         if (threadIdx.x == 0) s_off[ns] = tot;
         __syncthreads();
         if (want_a)
-          mp_scan<BLOCK, K, true>(a.ci, a.aaw, s_start, s_off, ns, c0, width, bm, s_cn, s_aa, threadIdx.x);
+          mp_scan<BLOCK, K, true>(a.cw, a.idmask, a.idbits, a.aaw, a.wtab, s_start, s_off, ns, c0, width, bm, s_cn, s_aa, threadIdx.x);
         else
-          mp_scan<BLOCK, K, false>(a.ci, a.aaw, s_start, s_off, ns, c0, width, bm, s_cn, s_aa, threadIdx.x);
+          mp_scan<BLOCK, K, false>(a.cw, a.idmask, a.idbits, a.aaw, a.wtab, s_start, s_off, ns, c0, width, bm, s_cn, s_aa, threadIdx.x);
         __syncthreads();
         for (int t = threadIdx.x; t < ns; t += BLOCK) {
           const int p = a.g_out[pbeg + sb + t];
@@ -863,7 +944,7 @@ __global__ __launch_bounds__(BLOCK, 8) void k_score_split(ScoreArgs a, const int
         if ((int)threadIdx.x < ns) s_off[threadIdx.x] = ex;
         if (threadIdx.x == 0) s_off[ns] = tot;
         __syncthreads();
-        mp_build<BLOCK, K>(a.ci, s_start, s_off, ns, c0, width, bm, threadIdx.x);
+        mp_build<BLOCK, K>(a.cw, a.idmask, s_start, s_off, ns, c0, width, bm, threadIdx.x);
         __syncthreads();
       }
     }
@@ -903,9 +984,9 @@ __global__ __launch_bounds__(BLOCK, 8) void k_score_split(ScoreArgs a, const int
       if (threadIdx.x == 0) s_off[ns] = tot;
       __syncthreads();
       if (want_a)
-        mp_scan<BLOCK, K, true>(a.ci, a.aaw, s_start, s_off, ns, c0, width, bm, s_cn, s_aa, threadIdx.x);
+        mp_scan<BLOCK, K, true>(a.cw, a.idmask, a.idbits, a.aaw, a.wtab, s_start, s_off, ns, c0, width, bm, s_cn, s_aa, threadIdx.x);
       else
-        mp_scan<BLOCK, K, false>(a.ci, a.aaw, s_start, s_off, ns, c0, width, bm, s_cn, s_aa, threadIdx.x);
+        mp_scan<BLOCK, K, false>(a.cw, a.idmask, a.idbits, a.aaw, a.wtab, s_start, s_off, ns, c0, width, bm, s_cn, s_aa, threadIdx.x);
       __syncthreads();
       for (int t = threadIdx.x; t < ns; t += BLOCK) {
         const int64_t gp = pbeg + sb + t;
@@ -1037,7 +1118,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_score_wave(ScoreArgs a) {
           if (lane < ns) s_off[lane] = ex;
           if (lane == 0) s_off[ns] = tot;
           wave_sync();
-          mp_build<64, K>(a.ci, s_start, s_off, ns, c0, width, bm, lane);
+          mp_build<64, K>(a.cw, a.idmask, s_start, s_off, ns, c0, width, bm, lane);
           wave_sync();
         }
       }
@@ -1076,9 +1157,9 @@ __global__ __launch_bounds__(WAVES * 64) void k_score_wave(ScoreArgs a) {
         if (lane == 0) s_off[ns] = tot;
         wave_sync();
         if (want_a)
-          mp_scan<64, K, true>(a.ci, a.aaw, s_start, s_off, ns, c0, width, bm, s_cn, s_aa, lane);
+          mp_scan<64, K, true>(a.cw, a.idmask, a.idbits, a.aaw, a.wtab, s_start, s_off, ns, c0, width, bm, s_cn, s_aa, lane);
         else
-          mp_scan<64, K, false>(a.ci, a.aaw, s_start, s_off, ns, c0, width, bm, s_cn, s_aa, lane);
+          mp_scan<64, K, false>(a.cw, a.idmask, a.idbits, a.aaw, a.wtab, s_start, s_off, ns, c0, width, bm, s_cn, s_aa, lane);
         wave_sync();
         if (lane < ns) {
           const int p = a.g_out[pbeg + sb + lane];
@@ -1273,6 +1354,10 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
     b->variant = V_MED;
   else
     b->variant = V_LARGE;
+  if (const char* e = getenv("BLP_VARIANT")) {  // test knob: a wider LDS variant than needed
+    const int v = atoi(e);
+    if (v > b->variant && v <= V_LARGE) b->variant = v;
+  }
   b->cap_bits = variant_cap_bits(b->variant);
   if (const char* e = getenv("BLP_CHUNK_BITS")) {  // test knob: force multi-chunk on small graphs
     int64_t v = atoll(e);
@@ -1537,6 +1622,11 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   a.rp = g->d_rp;
   a.ci = g->d_ci;
   a.aaw = g->d_aaw_fx;
+  const bool coded = g->d_ci_w && !getenv("BLP_NO_WCODES");  // tuning knob
+  a.cw = coded ? g->d_ci_w : g->d_ci;
+  a.idbits = coded ? g->id_bits : 31;
+  a.idmask = (uint32_t)((1ull << a.idbits) - 1);
+  a.wtab = g->d_wtab;
 
   a.off = g->off.as<int32_t>();
   a.cnt = g->cnt.as<int32_t>();

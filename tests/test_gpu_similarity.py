@@ -94,6 +94,15 @@ def test_general_graph_exact_distance(gpu):
     {"BLP_HOT_MIN": "1", "BLP_HOT_DENSITY": "100000000"},  # > HOT_LIST dense rows: sparse fallback
     {"BLP_WAVE": "1"},                                  # wave-per-source scorer (opt-in)
     {"BLP_WAVE": "1", "BLP_HEAVY_WORK": "50", "BLP_HOT_MIN": "8"},
+    {"BLP_VARIANT": "1"},                               # 64 KiB-bitmap scorer (no hint table)
+    {"BLP_VARIANT": "2"},                               # 136 KiB-bitmap scorer
+    {"BLP_WCODES": "0"},                                # every AA weight gathered per node
+    {"BLP_WCODES": "3"},                                # coded and gathered weights mixed
+    {"BLP_NO_WCODES": "1"},                             # scorers on the plain id stream
+    {"BLP_WCODES": "3", "BLP_SPLIT": "3"},
+    {"BLP_WCODES": "3", "BLP_FORCE_GLOBAL": "1"},
+    {"BLP_WCODES": "3", "BLP_WAVE": "1"},
+    {"BLP_WCODES": "3", "BLP_HEAVY_WORK": "50", "BLP_HOT_MIN": "8"},
 ])
 def test_kernel_paths_vs_oracle(gpu, knobs, monkeypatch):
     for k, v in knobs.items():
@@ -114,8 +123,12 @@ def test_kernel_paths_vs_oracle(gpu, knobs, monkeypatch):
         assert G.batch(x, y).plan()["chunks"] == -int(knobs["BLP_SPLIT"])  # chunk-parallel scorer
 
 
-def test_many_pairs_per_source_vs_oracle(gpu):
-    # > SEG pairs per source and > SEG rows in N(x): the segment-chunk loops
+@pytest.mark.parametrize("variant", [None, "1", "2"])
+def test_many_pairs_per_source_vs_oracle(gpu, variant, monkeypatch):
+    # > SEG pairs per source and > SEG rows in N(x): the segment-chunk loops; batches of more
+    # than one block step: the segment hint tables
+    if variant:
+        monkeypatch.setenv("BLP_VARIANT", variant)
     rng = np.random.default_rng(12)
     a, b = bipartite_edges(rng, 20000, 1500, 200000)
     G = blp.DeviceGraph(a, b)
