@@ -166,7 +166,8 @@ int build_weight_codes(blp_graph* g, const int64_t* row_ptr, const std::vector<l
   }
   uint8_t* d_ncode = nullptr;
   BLP_HIP(hipMemcpy(g->d_wtab, wtab.data(), sizeof(long long) * 256, hipMemcpyHostToDevice));
-  BLP_HIP(hipMalloc(&g->d_ci_w, sizeof(int32_t) * nnz));
+  BLP_HIP(hipMalloc(&g->d_ci_w, sizeof(int32_t) * (nnz + 16)));
+  BLP_HIP(hipMemset(g->d_ci_w, 0, sizeof(int32_t) * (nnz + 16)));
   BLP_HIP(hipMalloc(&d_ncode, (size_t)n));
   BLP_HIP(hipMemcpy(d_ncode, ncode.data(), (size_t)n, hipMemcpyHostToDevice));
   hipLaunchKernelGGL(k_code_ids, dim3((unsigned)std::min<int64_t>((nnz + 255) / 256, 1 << 20)), dim3(256), 0, g->stream,
@@ -269,7 +270,9 @@ int blp_graph_create(const int64_t* row_ptr, const int32_t* col_idx, int64_t n, 
   if ((rc = [&]() -> int {
          BLP_HIP(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
          BLP_HIP(hipMalloc(&g->d_rp, sizeof(int64_t) * (n + 1)));
-         BLP_HIP(hipMalloc(&g->d_ci, sizeof(int32_t) * std::max<int64_t>(nnz, 1)));
+         // padded: the scorers read short rows in 16-byte vectors, up to 3 ids past a row
+         BLP_HIP(hipMalloc(&g->d_ci, sizeof(int32_t) * (nnz + 16)));
+         BLP_HIP(hipMemset(g->d_ci, 0, sizeof(int32_t) * (nnz + 16)));
          BLP_HIP(hipMemcpy(g->d_rp, row_ptr, sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice));
          if (nnz) BLP_HIP(hipMemcpy(g->d_ci, col_idx, sizeof(int32_t) * nnz, hipMemcpyHostToDevice));
          if (aaw) {

@@ -142,20 +142,25 @@ __global__ __launch_bounds__(GP_BLOCK) void k_bucket_hist(const int32_t* __restr
   for (int i = threadIdx.x; i < nb; i += GP_BLOCK) hist[(int64_t)i * nblk + blockIdx.x] = h[i];
 }
 
-__global__ __launch_bounds__(GP_BLOCK) void k_bucket_scatter(const int32_t* __restrict__ x, int64_t np, int32_t xlo,
-                                                             int shift, int nb, int nblk, int64_t per_blk,
-                                                             const int32_t* __restrict__ hoff, int32_t* __restrict__ tmp) {
+// The pair itself (caller index, x, y) moves into bucket order, so the group kernel reads
+// its bucket contiguously instead of gathering x[i] / y[i] at random caller positions.
+__global__ __launch_bounds__(GP_BLOCK) void k_bucket_scatter(const int32_t* __restrict__ x, const int32_t* __restrict__ y,
+                                                             int64_t np, int32_t xlo, int shift, int nb, int nblk,
+                                                             int64_t per_blk, const int32_t* __restrict__ hoff,
+                                                             int4* __restrict__ tmp) {
   __shared__ int cur[NB_MAX];
   for (int i = threadIdx.x; i < nb; i += GP_BLOCK) cur[i] = hoff[(int64_t)i * nblk + blockIdx.x];
   __syncthreads();
   const int64_t b0 = (int64_t)blockIdx.x * per_blk, b1 = min(np, b0 + per_blk);
-  for (int64_t i = b0 + threadIdx.x; i < b1; i += GP_BLOCK) tmp[atomicAdd(&cur[(x[i] - xlo) >> shift], 1)] = (int32_t)i;
+  for (int64_t i = b0 + threadIdx.x; i < b1; i += GP_BLOCK) {
+    const int xi = x[i];
+    tmp[atomicAdd(&cur[(xi - xlo) >> shift], 1)] = make_int4((int32_t)i, xi, y[i], 0);
+  }
 }
 
 // One block per bucket of KEYS consecutive node ids.
 template <int KEYS>
-__global__ __launch_bounds__(GB_BLOCK) void k_bucket_group(const int32_t* __restrict__ x, const int32_t* __restrict__ y,
-                                                           const int64_t* __restrict__ rp, const int32_t* __restrict__ tmp,
+__global__ __launch_bounds__(GB_BLOCK) void k_bucket_group(const int64_t* __restrict__ rp, const int4* __restrict__ tmp,
                                                            const int32_t* __restrict__ hoff, int nblk, int nb, int shift,
                                                            int32_t xlo, int64_t xspan, int64_t np, int32_t* __restrict__ off,
                                                            int32_t* __restrict__ cnt, int32_t* __restrict__ bucket_active,
@@ -171,7 +176,7 @@ __global__ __launch_bounds__(GB_BLOCK) void k_bucket_group(const int32_t* __rest
   const int be = b + 1 < nb ? hoff[(int64_t)(b + 1) * nblk] : (int)np;
   for (int i = threadIdx.x; i < KEYS; i += GB_BLOCK) h[i] = 0;
   __syncthreads();
-  for (int k = bs + threadIdx.x; k < be; k += GB_BLOCK) atomicAdd(&h[x[tmp[k]] - k0], 1);
+  for (int k = bs + threadIdx.x; k < be; k += GB_BLOCK) atomicAdd(&h[tmp[k].y - k0], 1);
   __syncthreads();
   int v = 0, act = 0;
   for (int q = 0; q < PER; ++q) {
@@ -196,9 +201,10 @@ __global__ __launch_bounds__(GB_BLOCK) void k_bucket_group(const int32_t* __rest
   if (threadIdx.x == 0) bucket_active[b] = acts;
   __syncthreads();
   for (int k = bs + threadIdx.x; k < be; k += GB_BLOCK) {
-    const int i = tmp[k];
-    const int pos = bs + atomicAdd(&h[x[i] - k0], 1);
-    const int yi = y[i];
+    const int4 t = tmp[k];
+    const int i = t.x;
+    const int pos = bs + atomicAdd(&h[t.y - k0], 1);
+    const int yi = t.z;
     const int64_t st = rp[yi];
     g_out[pos] = i;
     g_yb[pos] = st;
@@ -289,9 +295,11 @@ __device__ inline int build_hint(const int32_t* s_off, int ns, int step, int32_t
 // Fetch one merge-path step: the K consecutive elements [f0, f0 + K) of the concatenated
 // segments (w = node id or -1, sk = segment or -1). One LDS binary search per K elements
 // (narrowed by the hint table when given: shift >= 0).
+// s_slot (packed scorer): sk also carries the segment's bitmap slot, s | s_slot[s] << 16.
 template <int K>
 __device__ inline void mp_fetch(const int32_t* __restrict__ ci, const int64_t* s_start, const int32_t* s_off, int ns,
-                                int T, int f0, int* w, int* sk, const int32_t* hint = nullptr, int shift = -1) {
+                                int T, int f0, int* w, int* sk, const int32_t* hint = nullptr, int shift = -1,
+                                const int32_t* s_slot = nullptr) {
   if (f0 >= T) {
 #pragma unroll
     for (int k = 0; k < K; ++k) w[k] = sk[k] = -1;
@@ -318,10 +326,12 @@ __device__ inline void mp_fetch(const int32_t* __restrict__ ci, const int64_t* s
       w[4 * j + 2] = v.z;
       w[4 * j + 3] = v.w;
     }
+    const int sv = s_slot ? s | s_slot[s] << 16 : s;
 #pragma unroll
-    for (int k = 0; k < K; ++k) sk[k] = s;
+    for (int k = 0; k < K; ++k) sk[k] = sv;
     return;
   }
+  int sv = s_slot ? s | s_slot[s] << 16 : s;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const int f = f0 + k;
@@ -332,10 +342,11 @@ __device__ inline void mp_fetch(const int32_t* __restrict__ ci, const int64_t* s
         ++s;
         next = s_off[s + 1];
         pos = s_start[s];
+        sv = s_slot ? s | s_slot[s] << 16 : s;
       }
       w[k] = ci[pos];
       ++pos;
-      sk[k] = s;
+      sk[k] = sv;
     }
   }
 }
@@ -348,31 +359,39 @@ __device__ inline void mp_fetch(const int32_t* __restrict__ ci, const int64_t* s
 // idmask | sign bit, so -1 maps to >= 2^31 - c0 > width (c0 <= idmask, width < 2^31).
 __device__ inline uint32_t in_chunk(int v, uint32_t keep, uint32_t c0u) { return ((uint32_t)v & keep) - c0u; }
 
+// s_slot (packed scorer, GLOBAL false): segment s marks slot s_slot[s] of the bitmap, whose
+// bits start at s_slot[s] * slot_bits.
 template <int NT, int K, bool GLOBAL = false>
 __device__ inline void mp_build(const int32_t* __restrict__ ci, uint32_t idmask, const int64_t* s_start,
                                 const int32_t* s_off, int ns, int64_t c0, int64_t width, uint32_t* bm, int tid,
-                                const int32_t* hint = nullptr, int shift = -1) {
+                                const int32_t* hint = nullptr, int shift = -1, const int32_t* s_slot = nullptr,
+                                uint32_t slot_bits = 0) {
   const int T = s_off[ns];
   constexpr int STEP = NT * K;
   const uint32_t keep = idmask | 0x80000000u, c0u = (uint32_t)c0, wu = (uint32_t)width;
   int w[K], sk[K];
-  mp_fetch<K>(ci, s_start, s_off, ns, T, tid * K, w, sk, hint, shift);
+  mp_fetch<K>(ci, s_start, s_off, ns, T, tid * K, w, sk, hint, shift, s_slot);
   for (int base = 0; base < T; base += STEP) {
     int wn[K], skn[K];
-    mp_fetch<K>(ci, s_start, s_off, ns, T, base + STEP + tid * K, wn, skn, hint, shift);
+    mp_fetch<K>(ci, s_start, s_off, ns, T, base + STEP + tid * K, wn, skn, hint, shift, s_slot);
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       // one unsigned compare tests validity and range (see in_chunk)
       const uint32_t r = in_chunk(w[k], keep, c0u);
       if (r < wu) {
-        if (GLOBAL)  // the workgroup's private HBM bitmap: the OR is done in the XCD's L2
+        if (GLOBAL) {  // the workgroup's private HBM bitmap: the OR is done in the XCD's L2
           __hip_atomic_fetch_or(&bm[r >> 5], 1u << (r & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        else
-          atomicOr(&bm[r >> 5], 1u << (r & 31));
+        } else {
+          const uint32_t rr = s_slot ? r + ((uint32_t)sk[k] >> 16) * slot_bits : r;
+          atomicOr(&bm[rr >> 5], 1u << (rr & 31));
+        }
       }
     }
 #pragma unroll
-    for (int k = 0; k < K; ++k) w[k] = wn[k];
+    for (int k = 0; k < K; ++k) {
+      w[k] = wn[k];
+      sk[k] = skn[k];
+    }
   }
 }
 
@@ -388,12 +407,12 @@ __device__ inline void mp_scan(const int32_t* __restrict__ ci, uint32_t idmask, 
                                const long long* __restrict__ aaw, const long long* wtab, const int64_t* s_start,
                                const int32_t* s_off, int ns, int64_t c0, int64_t width, const uint32_t* bm,
                                uint32_t* s_cn, unsigned long long* s_aa, int tid, const int32_t* hint = nullptr,
-                               int shift = -1) {
+                               int shift = -1, const int32_t* s_slot = nullptr, uint32_t slot_bits = 0) {
   const int T = s_off[ns];
   constexpr int STEP = NT * K;
   const uint32_t keep = idmask | 0x80000000u, c0u = (uint32_t)c0, wu = (uint32_t)width;
   int w[K], sk[K];
-  mp_fetch<K>(ci, s_start, s_off, ns, T, tid * K, w, sk, hint, shift);
+  mp_fetch<K>(ci, s_start, s_off, ns, T, tid * K, w, sk, hint, shift, s_slot);
   for (int base = 0; base < T; base += STEP) {
     // the bitmap words and (AA) the code weights wtab[code] are read together, so one LDS
     // round trip serves both; hits with code 0 then gather aaw, before the next step's loads
@@ -402,10 +421,12 @@ __device__ inline void mp_scan(const int32_t* __restrict__ ci, uint32_t idmask, 
     long long wt[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      const uint32_t r = in_chunk(w[k], keep, c0u);
-      const uint32_t word = bm[(r < wu ? r : 0u) >> 5];
+      uint32_t r = in_chunk(w[k], keep, c0u);
+      const bool in = r < wu;
+      if (s_slot) r += ((uint32_t)sk[k] >> 16) * slot_bits;
+      const uint32_t word = bm[(in ? r : 0u) >> 5];
       if (AA) wt[k] = wtab[((uint32_t)w[k] >> idbits) & 255u];
-      hit[k] = r < wu && ((word >> (r & 31)) & 1u);
+      hit[k] = in && ((word >> (r & 31)) & 1u);
     }
     if (AA) {
       bool any_esc = false;
@@ -420,7 +441,7 @@ __device__ inline void mp_scan(const int32_t* __restrict__ ci, uint32_t idmask, 
       for (int k = 0; k < K; ++k) wt[k] = hit[k] ? wt[k] : 0ll;
     }
     int wn[K], skn[K];
-    mp_fetch<K>(ci, s_start, s_off, ns, T, base + STEP + tid * K, wn, skn, hint, shift);
+    mp_fetch<K>(ci, s_start, s_off, ns, T, base + STEP + tid * K, wn, skn, hint, shift, s_slot);
     if (sk[0] == sk[K - 1]) {  // the K elements in one segment (or none valid): one run
       unsigned c = 0;
       unsigned long long acc = 0;
@@ -430,8 +451,8 @@ __device__ inline void mp_scan(const int32_t* __restrict__ ci, uint32_t idmask, 
         if (AA) acc += (unsigned long long)wt[k];
       }
       if (c) {
-        atomicAdd(&s_cn[sk[0]], c);
-        if (AA) atomicAdd(&s_aa[sk[0]], acc);
+        atomicAdd(&s_cn[sk[0] & 0xffff], c);
+        if (AA) atomicAdd(&s_aa[sk[0] & 0xffff], acc);
       }
     } else {
       int cur = sk[0];
@@ -441,8 +462,8 @@ __device__ inline void mp_scan(const int32_t* __restrict__ ci, uint32_t idmask, 
       for (int k = 0; k < K; ++k) {
         if (sk[k] != cur) {
           if (c) {
-            atomicAdd(&s_cn[cur], c);
-            if (AA) atomicAdd(&s_aa[cur], acc);
+            atomicAdd(&s_cn[cur & 0xffff], c);
+            if (AA) atomicAdd(&s_aa[cur & 0xffff], acc);
           }
           cur = sk[k];
           c = 0;
@@ -454,8 +475,8 @@ __device__ inline void mp_scan(const int32_t* __restrict__ ci, uint32_t idmask, 
         }
       }
       if (c && cur >= 0) {
-        atomicAdd(&s_cn[cur], c);
-        if (AA) atomicAdd(&s_aa[cur], acc);
+        atomicAdd(&s_cn[cur & 0xffff], c);
+        if (AA) atomicAdd(&s_aa[cur & 0xffff], acc);
       }
     }
 #pragma unroll
@@ -463,6 +484,79 @@ __device__ inline void mp_scan(const int32_t* __restrict__ ci, uint32_t idmask, 
       w[k] = wn[k];
       sk[k] = skn[k];
     }
+  }
+}
+
+// Short rows (every row of the batch at most SHORT_MAX ids -- the business side, whose rows
+// are user rows Γ(w)): one thread per segment reads its whole row with up to SHORT_MAX / 4
+// 16-byte loads, all issued before any is used. No merge-path search and no row crossings,
+// whose dependent LDS round trips dominate a merge-path step when rows average ~10 ids;
+// the cost is idle lanes beside the longest row of the wave. ci is padded past nnz.
+constexpr int SHORT_MAX = 32;
+
+__device__ inline int row_load(const int32_t* __restrict__ ci, int64_t st, int len, int* e) {
+  const blp::U4a* p = reinterpret_cast<const blp::U4a*>(ci + st);
+#pragma unroll
+  for (int q = 0; q < SHORT_MAX / 4; ++q) {
+    if (4 * q < len) {
+      const blp::U4a v = p[q];
+      e[4 * q] = v.x;
+      e[4 * q + 1] = v.y;
+      e[4 * q + 2] = v.z;
+      e[4 * q + 3] = v.w;
+    }
+  }
+  return len;
+}
+
+template <int NT>
+__device__ inline void row_build(const int32_t* __restrict__ ci, uint32_t idmask, const int64_t* s_start,
+                                 const int32_t* s_off, int ns, int64_t c0, int64_t width, uint32_t* bm, int tid,
+                                 const int32_t* s_slot = nullptr, uint32_t slot_bits = 0) {
+  const uint32_t keep = idmask | 0x80000000u, c0u = (uint32_t)c0, wu = (uint32_t)width;
+  for (int t = tid; t < ns; t += NT) {
+    int e[SHORT_MAX];
+    const int len = row_load(ci, s_start[t], s_off[t + 1] - s_off[t], e);
+    const uint32_t base = s_slot ? (uint32_t)s_slot[t] * slot_bits : 0u;
+#pragma unroll
+    for (int k = 0; k < SHORT_MAX; ++k) {
+      if (k < len) {
+        const uint32_t r = in_chunk(e[k], keep, c0u);
+        if (r < wu) atomicOr(&bm[(r + base) >> 5], 1u << ((r + base) & 31));
+      }
+    }
+  }
+}
+
+template <int NT, bool AA>
+__device__ inline void row_scan(const int32_t* __restrict__ ci, uint32_t idmask, int idbits,
+                                const long long* __restrict__ aaw, const long long* wtab, const int64_t* s_start,
+                                const int32_t* s_off, int ns, int64_t c0, int64_t width, const uint32_t* bm,
+                                uint32_t* s_cn, unsigned long long* s_aa, int tid, const int32_t* s_slot = nullptr,
+                                uint32_t slot_bits = 0) {
+  const uint32_t keep = idmask | 0x80000000u, c0u = (uint32_t)c0, wu = (uint32_t)width;
+  for (int t = tid; t < ns; t += NT) {  // the thread owns segment t: plain adds, no atomics
+    int e[SHORT_MAX];
+    const int len = row_load(ci, s_start[t], s_off[t + 1] - s_off[t], e);
+    const uint32_t base = s_slot ? (uint32_t)s_slot[t] * slot_bits : 0u;
+    unsigned c = 0;
+    unsigned long long acc = 0;
+#pragma unroll
+    for (int k = 0; k < SHORT_MAX; ++k) {
+      if (k < len) {
+        const uint32_t r = in_chunk(e[k], keep, c0u);
+        const uint32_t rb = r + base;
+        const uint32_t word = bm[(r < wu ? rb : 0u) >> 5];
+        const bool hit = r < wu && ((word >> (rb & 31)) & 1u);
+        c += hit ? 1u : 0u;
+        if (AA && hit) {
+          const uint32_t code = ((uint32_t)e[k] >> idbits) & 255u;
+          acc += (unsigned long long)(code ? wtab[code] : aaw[e[k] & idmask]);
+        }
+      }
+    }
+    s_cn[t] += c;
+    if (AA) s_aa[t] += acc;
   }
 }
 
@@ -554,6 +648,7 @@ struct ScoreArgs {
   int64_t cap_bits;  // bitmap bits per chunk (<= template capacity; lowered only by tests)
   uint32_t mask;
   int dq;            // sources per dequeue
+  int short_rows;    // bit 0: every build row <= SHORT_MAX ids, bit 1: every scan row (row_build / row_scan)
 };
 
 template <int BLOCK>
@@ -570,8 +665,29 @@ __device__ inline unsigned long long block_sum_u64(unsigned long long v, unsigne
   return t;
 }
 
+#ifdef BLP_PROF
+__device__ unsigned long long g_prof[16];
+#define PROF_INIT                          \
+  unsigned long long prof_t0 = clock64();  \
+  unsigned long long prof_acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+#define PROF(i)                                \
+  {                                            \
+    const unsigned long long t1_ = clock64();  \
+    prof_acc[i] += t1_ - prof_t0;              \
+    prof_t0 = t1_;                             \
+  }
+#define PROF_FLUSH                                                         \
+  if (threadIdx.x == 0)                                                    \
+    for (int i_ = 0; i_ < 9; ++i_) atomicAdd(&g_prof[i_], prof_acc[i_]);
+#else
+#define PROF_INIT
+#define PROF(i)
+#define PROF_FLUSH
+#endif
+
 template <int BLOCK, int CAP_WORDS, int SEG, int K>
 __global__ __launch_bounds__(BLOCK) void k_score(ScoreArgs a) {
+  static_assert(SEG <= BLOCK, "one pair segment per thread in the output loop");
   constexpr int NW = BLOCK / 64;
   __shared__ uint32_t bm[CAP_WORDS];
   __shared__ int64_t s_start[SEG];
@@ -598,12 +714,19 @@ __global__ __launch_bounds__(BLOCK) void k_score(ScoreArgs a) {
   uint4* bm4 = reinterpret_cast<uint4*>(bm);
   const int n_active = a.misc->n_active;
 
+  PROF_INIT
+  // dequeue one ahead: the next source's atomic is in flight while this one is scored
+  int nxt = threadIdx.x == 0 ? atomicAdd(&a.misc->queue, a.dq) : 0;
   for (;;) {
-    if (threadIdx.x == 0) s_src = atomicAdd(&a.misc->queue, a.dq);
+    if (threadIdx.x == 0) {
+      s_src = nxt;
+      if (nxt < n_active) nxt = atomicAdd(&a.misc->queue, a.dq);
+    }
     __syncthreads();
     const int s_first = s_src;
     __syncthreads();
     if (s_first >= n_active) break;
+    PROF(0)
     const int s_last = min(n_active, s_first + a.dq);
     for (int s = s_first; s < s_last; ++s) {
       const int x = a.active[s];
@@ -613,6 +736,7 @@ __global__ __launch_bounds__(BLOCK) void k_score(ScoreArgs a) {
       // value range of N(x) (rows are sorted): distance-1 removal is skipped when disjoint
       const int64_t nx_lo = xe > xb ? a.ci[xb] : 0, nx_hi = xe > xb ? a.ci[xe - 1] : -1;
       unsigned long long h2 = 0;
+      PROF(1)
 
       for (int ch = 0; ch < nchunks; ++ch) {
         const int64_t c0 = a.lo + (int64_t)ch * CAP_BITS;
@@ -657,14 +781,20 @@ __global__ __launch_bounds__(BLOCK) void k_score(ScoreArgs a) {
             bm4[q] = v;
           }
           __syncthreads();
+          PROF(2)
           for (int64_t k0 = xb; k0 < xe; k0 += SEG) {
             const int ns = (int)min<int64_t>(SEG, xe - k0);
             load_row_segments<BLOCK>(a.rp, a.ci, k0, ns, s_start, s_off, red, nhot ? a.hot_idx : nullptr);
-            const int shift = build_hint<BLOCK, HC>(s_off, ns, BLOCK * K, s_hint);
-            mp_build<BLOCK, K>(a.cw, a.idmask, s_start, s_off, ns, c0, width, bm, threadIdx.x, s_hint, shift);
+            if (a.short_rows & 1) {
+              row_build<BLOCK>(a.cw, a.idmask, s_start, s_off, ns, c0, width, bm, threadIdx.x);
+            } else {
+              const int shift = build_hint<BLOCK, HC>(s_off, ns, BLOCK * K, s_hint);
+              mp_build<BLOCK, K>(a.cw, a.idmask, s_start, s_off, ns, c0, width, bm, threadIdx.x, s_hint, shift);
+            }
             __syncthreads();
           }
         }
+        PROF(3)
         // 3. exact distance 2: drop x (distance 0) and N(x) (distance 1)
         if (nx_hi >= c0 && nx_lo < c1) {
           for (int64_t k = xb + threadIdx.x; k < xe; k += BLOCK) {
@@ -674,6 +804,7 @@ __global__ __launch_bounds__(BLOCK) void k_score(ScoreArgs a) {
         }
         if (threadIdx.x == 0 && x >= c0 && x < c1) atomicAnd(&bm[(x - c0) >> 5], ~(1u << ((x - c0) & 31)));
         __syncthreads();
+        PROF(4)
         // 4. |H2(x) ∩ chunk|
         if (want_j) {
           unsigned long long pc = 0;
@@ -683,14 +814,16 @@ __global__ __launch_bounds__(BLOCK) void k_score(ScoreArgs a) {
           }
           h2 += block_sum_u64<BLOCK>(pc, red64);
         }
+        PROF(5)
         // 5. scan N(y) of every pair of x, SEG pairs at a time
         for (int sb = 0; sb < pcnt; sb += SEG) {
           const int ns = min(SEG, pcnt - sb);
-          int len = 0;
+          int len = 0, pout = 0;
           if ((int)threadIdx.x < ns) {
             const int gp = pbeg + sb + threadIdx.x;
             s_start[threadIdx.x] = a.g_yb[gp];
             len = a.g_yl[gp];
+            pout = a.g_out[gp];  // used after the scan: its latency hides behind it
             s_cn[threadIdx.x] = 0;
             s_aa[threadIdx.x] = 0;
           }
@@ -699,16 +832,27 @@ __global__ __launch_bounds__(BLOCK) void k_score(ScoreArgs a) {
           if ((int)threadIdx.x < ns) s_off[threadIdx.x] = ex;
           if (threadIdx.x == 0) s_off[ns] = tot;
           __syncthreads();
-          const int shift = build_hint<BLOCK, HC>(s_off, ns, BLOCK * K, s_hint);
-          if (want_a)
-            mp_scan<BLOCK, K, true>(a.cw, a.idmask, a.idbits, a.aaw, s_wtab, s_start, s_off, ns, c0, width, bm, s_cn,
-                                    s_aa, threadIdx.x, s_hint, shift);
-          else
-            mp_scan<BLOCK, K, false>(a.cw, a.idmask, a.idbits, a.aaw, s_wtab, s_start, s_off, ns, c0, width, bm, s_cn,
-                                     s_aa, threadIdx.x, s_hint, shift);
+          PROF(6)
+          if (a.short_rows & 2) {
+            if (want_a)
+              row_scan<BLOCK, true>(a.cw, a.idmask, a.idbits, a.aaw, s_wtab, s_start, s_off, ns, c0, width, bm, s_cn,
+                                    s_aa, threadIdx.x);
+            else
+              row_scan<BLOCK, false>(a.cw, a.idmask, a.idbits, a.aaw, s_wtab, s_start, s_off, ns, c0, width, bm, s_cn,
+                                     s_aa, threadIdx.x);
+          } else {
+            const int shift = build_hint<BLOCK, HC>(s_off, ns, BLOCK * K, s_hint);
+            if (want_a)
+              mp_scan<BLOCK, K, true>(a.cw, a.idmask, a.idbits, a.aaw, s_wtab, s_start, s_off, ns, c0, width, bm, s_cn,
+                                      s_aa, threadIdx.x, s_hint, shift);
+            else
+              mp_scan<BLOCK, K, false>(a.cw, a.idmask, a.idbits, a.aaw, s_wtab, s_start, s_off, ns, c0, width, bm,
+                                       s_cn, s_aa, threadIdx.x, s_hint, shift);
+          }
           __syncthreads();
-          for (int t = threadIdx.x; t < ns; t += BLOCK) {
-            const int p = a.g_out[pbeg + sb + t];
+          PROF(7)
+          for (int t = threadIdx.x; t < ns; t += BLOCK) {  // ns <= SEG <= BLOCK: t == threadIdx.x
+            const int p = pout;
             unsigned c = s_cn[t];
             double av = (double)s_aa[t] * (1.0 / blp::AA_SCALE);
             if (ch > 0) {
@@ -728,8 +872,237 @@ __global__ __launch_bounds__(BLOCK) void k_score(ScoreArgs a) {
             }
           }
           __syncthreads();
+          PROF(8)
         }
       }
+    }
+  }
+  PROF_FLUSH
+}
+
+// ------------------------------------------------------------------ packed scorer
+// Small universes (the business side of a review graph: H2(v) over 100K businesses is
+// 12.5 KiB) use a tenth of a 136 KiB LDS bitmap, and each source is then a short chain of
+// dependent round trips (dequeue, N(x) rows, build, popcount, pair segments, scan, outputs)
+// that 16 waves cannot hide. Here a workgroup dequeues a GROUP of up to n_slots sources and
+// runs every phase once for the whole group: each source owns a bitmap slot of slot_words
+// words; the build's row segments and the scan's pair segments carry their slot (mp_fetch
+// packs it into the segment id). Same exact-distance rule and pair bookkeeping as k_score.
+constexpr int PK_MAX = 32;  // sources per group
+constexpr int PK_HINT = 1024;
+
+// last i in [0, n) with off[i] <= g (off[0] = 0 <= g < off[n]); n <= PK_MAX
+__device__ inline int group_find(const int* off, int n, int g) {
+  int lo = 0, hi = n;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (off[mid] <= g)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  return lo;
+}
+
+template <int BLOCK, int CAP_WORDS, int SEG, int K>
+__global__ __launch_bounds__(BLOCK) void k_score_pack(ScoreArgs a, int slot_words, const int2* __restrict__ groups,
+                                                      int n_groups) {
+  __shared__ uint32_t bm[CAP_WORDS];
+  __shared__ int64_t s_start[SEG];
+  __shared__ int32_t s_off[SEG + 1];
+  __shared__ int32_t s_slot[SEG];
+  __shared__ uint32_t s_cn[SEG];
+  __shared__ unsigned long long s_aa[SEG];
+  __shared__ int32_t s_gp[SEG];
+  __shared__ int32_t s_hint[PK_HINT];
+  __shared__ long long s_wtab[256];
+  __shared__ int red[BLOCK / 64];
+  __shared__ int s_x[PK_MAX], s_heavy[PK_MAX], s_pb[PK_MAX];
+  __shared__ int64_t s_xb[PK_MAX];
+  __shared__ int s_roff[PK_MAX + 1], s_doff[PK_MAX + 1], s_poff[PK_MAX + 1];
+  __shared__ unsigned s_h2[PK_MAX];
+  __shared__ int s_first;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const bool want_j = (a.mask & BLP_JACCARD) != 0;
+  const bool want_a = (a.mask & BLP_ADAMIC) != 0;
+  const int64_t span = a.hi - a.lo;
+  const uint32_t slot_bits = 32u * (uint32_t)slot_words;
+  const int sw4 = slot_words >> 2;
+  uint4* bm4 = reinterpret_cast<uint4*>(bm);
+  const int n_active = a.misc->n_active;
+  if (a.wtab)  // visible after the first barrier
+    for (int i = tid; i < 256; i += BLOCK) s_wtab[i] = a.wtab[i];
+
+  for (;;) {
+    if (tid == 0) {
+      const int gi = atomicAdd(&a.misc->queue, 1);
+      s_first = gi < n_groups ? gi : -1;
+    }
+    __syncthreads();
+    const int gi = s_first;
+    if (gi < 0) break;
+    const int2 gr = groups[gi];
+    const int first = gr.x;
+    const int ng = min(gr.y, n_active) - first;  // n_active equals the planned source count
+    // 0. group table (first wave): sources, their row / removal / pair offsets
+    if (tid < 64) {
+      int nrow = 0, ndrop = 0, npair = 0;
+      if (lane < ng) {
+        const int x = a.active[first + lane];
+        const int64_t xb = a.rp[x], xe = a.rp[x + 1];
+        const int hs = a.heavy_slot ? a.heavy_slot[x] : -1;
+        // N(x) intersects the universe? (rows are sorted; bipartite sides are disjoint)
+        const bool meet = xe > xb && (int64_t)a.ci[xe - 1] >= a.lo && (int64_t)a.ci[xb] < a.hi;
+        s_x[lane] = x;
+        s_xb[lane] = xb;
+        s_heavy[lane] = hs;
+        s_pb[lane] = a.off[x];
+        s_h2[lane] = 0;
+        nrow = hs >= 0 ? 0 : (int)(xe - xb);
+        ndrop = meet ? (int)(xe - xb) : 0;
+        npair = a.cnt[x];
+      }
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int r1 = __shfl_up(nrow, d, 64), r2 = __shfl_up(ndrop, d, 64), r3 = __shfl_up(npair, d, 64);
+        if (lane >= d) {
+          nrow += r1;
+          ndrop += r2;
+          npair += r3;
+        }
+      }
+      if (lane < ng) {  // inclusive -> offsets [lane + 1]
+        s_roff[lane + 1] = nrow;
+        s_doff[lane + 1] = ndrop;
+        s_poff[lane + 1] = npair;
+      }
+      if (lane == 0) s_roff[0] = s_doff[0] = s_poff[0] = 0;
+    }
+    __syncthreads();
+    // 1. slots: zero, or the bitmap k_heavy pre-built for a heavy source
+    for (int q = tid; q < ng * sw4; q += BLOCK) {
+      const int i = q / sw4;
+      const int hs = s_heavy[i];
+      bm4[q] = hs >= 0 ? reinterpret_cast<const uint4*>(a.heavy_bm + (int64_t)hs * a.hb_words)[q - i * sw4]
+                       : make_uint4(0, 0, 0, 0);
+    }
+    __syncthreads();
+    // 2. build: the rows of every (non-heavy) source's N(x), SEG rows at a time
+    const int R = s_roff[ng];
+    for (int k0 = 0; k0 < R; k0 += SEG) {
+      const int ns = min(SEG, R - k0);
+      int len = 0;
+      if (tid < ns) {
+        const int gi = k0 + tid;
+        const int i = group_find(s_roff, ng, gi);
+        const int z = a.ci[s_xb[i] + (gi - s_roff[i])];
+        const int64_t st = a.rp[z];
+        s_start[tid] = st;
+        s_slot[tid] = i;
+        len = (int)(a.rp[z + 1] - st);
+      }
+      int tot;
+      const int ex = block_exscan<BLOCK>(len, red, &tot);
+      if (tid < ns) s_off[tid] = ex;
+      if (tid == 0) s_off[ns] = tot;
+      __syncthreads();
+      if (a.short_rows & 1) {
+        row_build<BLOCK>(a.cw, a.idmask, s_start, s_off, ns, a.lo, span, bm, tid, s_slot, slot_bits);
+      } else {
+        const int shift = build_hint<BLOCK, PK_HINT>(s_off, ns, BLOCK * K, s_hint);
+        mp_build<BLOCK, K>(a.cw, a.idmask, s_start, s_off, ns, a.lo, span, bm, tid, s_hint, shift, s_slot, slot_bits);
+      }
+      __syncthreads();
+    }
+    // 3. exact distance 2: drop x (distance 0) and N(x) (distance 1) from each slot
+    for (int gi = tid; gi < s_doff[ng]; gi += BLOCK) {
+      const int i = group_find(s_doff, ng, gi);
+      const int64_t r = (int64_t)a.ci[s_xb[i] + (gi - s_doff[i])] - a.lo;
+      if (r >= 0 && r < span) {
+        const uint32_t rr = (uint32_t)i * slot_bits + (uint32_t)r;
+        atomicAnd(&bm[rr >> 5], ~(1u << (rr & 31)));
+      }
+    }
+    if (tid < ng) {
+      const int64_t r = (int64_t)s_x[tid] - a.lo;
+      if (r >= 0 && r < span) {
+        const uint32_t rr = (uint32_t)tid * slot_bits + (uint32_t)r;
+        atomicAnd(&bm[rr >> 5], ~(1u << (rr & 31)));
+      }
+    }
+    __syncthreads();
+    // 4. |H2(x)| per slot
+    if (want_j) {
+      int cur = -1;
+      unsigned pc = 0;
+      for (int q = tid; q < ng * sw4; q += BLOCK) {
+        const int i = q / sw4;
+        if (i != cur) {
+          if (pc) atomicAdd(&s_h2[cur], pc);
+          cur = i;
+          pc = 0;
+        }
+        const uint4 v = bm4[q];
+        pc += __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);
+      }
+      if (pc) atomicAdd(&s_h2[cur], pc);
+      __syncthreads();
+    }
+    // 5. scan N(y) of every pair of the group, SEG pairs at a time
+    const int P = s_poff[ng];
+    for (int sb = 0; sb < P; sb += SEG) {
+      const int ns = min(SEG, P - sb);
+      int len = 0;
+      if (tid < ns) {
+        const int gi = sb + tid;
+        const int i = group_find(s_poff, ng, gi);
+        const int gp = s_pb[i] + (gi - s_poff[i]);
+        s_start[tid] = a.g_yb[gp];
+        s_slot[tid] = i;
+        s_gp[tid] = gp;
+        len = a.g_yl[gp];
+        s_cn[tid] = 0;
+        s_aa[tid] = 0;
+      }
+      int tot;
+      const int ex = block_exscan<BLOCK>(len, red, &tot);
+      if (tid < ns) s_off[tid] = ex;
+      if (tid == 0) s_off[ns] = tot;
+      __syncthreads();
+      if (a.short_rows & 2) {
+        if (want_a)
+          row_scan<BLOCK, true>(a.cw, a.idmask, a.idbits, a.aaw, s_wtab, s_start, s_off, ns, a.lo, span, bm, s_cn, s_aa,
+                                tid, s_slot, slot_bits);
+        else
+          row_scan<BLOCK, false>(a.cw, a.idmask, a.idbits, a.aaw, s_wtab, s_start, s_off, ns, a.lo, span, bm, s_cn,
+                                 s_aa, tid, s_slot, slot_bits);
+      } else {
+        const int shift = build_hint<BLOCK, PK_HINT>(s_off, ns, BLOCK * K, s_hint);
+        if (want_a)
+          mp_scan<BLOCK, K, true>(a.cw, a.idmask, a.idbits, a.aaw, s_wtab, s_start, s_off, ns, a.lo, span, bm, s_cn,
+                                  s_aa, tid, s_hint, shift, s_slot, slot_bits);
+        else
+          mp_scan<BLOCK, K, false>(a.cw, a.idmask, a.idbits, a.aaw, s_wtab, s_start, s_off, ns, a.lo, span, bm, s_cn,
+                                   s_aa, tid, s_hint, shift, s_slot, slot_bits);
+      }
+      __syncthreads();
+      if (tid < ns) {
+        const int p = a.g_out[s_gp[tid]];
+        const unsigned c = s_cn[tid];
+        a.cn[p] = c;
+        if (want_a) a.aa[p] = (double)s_aa[tid] * (1.0 / blp::AA_SCALE);
+        if (want_j) {
+          const long long uni = (long long)s_h2[s_slot[tid]] + (s_off[tid + 1] - s_off[tid]) - (long long)c;
+          if (uni <= 0) {
+            a.jac[p] = __builtin_nan("");
+            atomicOr(&a.misc->zero_div, 1);
+          } else {
+            a.jac[p] = (double)c / (double)uni;  // correctly rounded, as Python's float division
+          }
+        }
+      }
+      __syncthreads();
     }
   }
 }
@@ -1118,7 +1491,10 @@ __global__ __launch_bounds__(WAVES * 64) void k_score_wave(ScoreArgs a) {
           if (lane < ns) s_off[lane] = ex;
           if (lane == 0) s_off[ns] = tot;
           wave_sync();
-          mp_build<64, K>(a.cw, a.idmask, s_start, s_off, ns, c0, width, bm, lane);
+          if (a.short_rows & 1)
+            row_build<64>(a.cw, a.idmask, s_start, s_off, ns, c0, width, bm, lane);
+          else
+            mp_build<64, K>(a.cw, a.idmask, s_start, s_off, ns, c0, width, bm, lane);
           wave_sync();
         }
       }
@@ -1143,11 +1519,12 @@ __global__ __launch_bounds__(WAVES * 64) void k_score_wave(ScoreArgs a) {
       }
       for (int sb = 0; sb < pcnt; sb += WSEG) {
         const int ns = min(WSEG, pcnt - sb);
-        int len = 0;
+        int len = 0, pout = 0;
         if (lane < ns) {
           const int gp = pbeg + sb + lane;
           s_start[lane] = a.g_yb[gp];
           len = a.g_yl[gp];
+          pout = a.g_out[gp];
           s_cn[lane] = 0;
           s_aa[lane] = 0;
         }
@@ -1156,13 +1533,23 @@ __global__ __launch_bounds__(WAVES * 64) void k_score_wave(ScoreArgs a) {
         if (lane < ns) s_off[lane] = ex;
         if (lane == 0) s_off[ns] = tot;
         wave_sync();
-        if (want_a)
-          mp_scan<64, K, true>(a.cw, a.idmask, a.idbits, a.aaw, a.wtab, s_start, s_off, ns, c0, width, bm, s_cn, s_aa, lane);
-        else
-          mp_scan<64, K, false>(a.cw, a.idmask, a.idbits, a.aaw, a.wtab, s_start, s_off, ns, c0, width, bm, s_cn, s_aa, lane);
+        if (a.short_rows & 2) {
+          if (want_a)
+            row_scan<64, true>(a.cw, a.idmask, a.idbits, a.aaw, a.wtab, s_start, s_off, ns, c0, width, bm, s_cn, s_aa,
+                               lane);
+          else
+            row_scan<64, false>(a.cw, a.idmask, a.idbits, a.aaw, a.wtab, s_start, s_off, ns, c0, width, bm, s_cn, s_aa,
+                                lane);
+        } else if (want_a) {
+          mp_scan<64, K, true>(a.cw, a.idmask, a.idbits, a.aaw, a.wtab, s_start, s_off, ns, c0, width, bm, s_cn, s_aa,
+                               lane);
+        } else {
+          mp_scan<64, K, false>(a.cw, a.idmask, a.idbits, a.aaw, a.wtab, s_start, s_off, ns, c0, width, bm, s_cn, s_aa,
+                                lane);
+        }
         wave_sync();
         if (lane < ns) {
-          const int p = a.g_out[pbeg + sb + lane];
+          const int p = pout;
           const unsigned c = s_cn[lane];
           a.cn[p] = c;
           if (want_a) a.aa[p] = (double)s_aa[lane] * (1.0 / blp::AA_SCALE);
@@ -1190,6 +1577,7 @@ constexpr int CAP_SMALL = 4096, CAP_MED = 16384, CAP_LARGE = 34816;
 constexpr int BLOCK_SMALL = 256, BLOCK_MED = 512, BLOCK_LARGE = 1024;
 constexpr int SEG_SMALL = 256, SEG_MED = 512, SEG_LARGE = 512;
 constexpr int G_BLOCK = 1024, G_SEG = 512;  // HBM-bitmap scorer
+constexpr int PK_BLOCK = 1024, PK_SEG = 512;  // packed scorer
 constexpr int S_BLOCK = 1024, S_CAP = 16384, S_SEG = 512;  // chunk-parallel scorer: 64 KiB chunks, 2 blocks / CU
 constexpr int S_MAX_CHUNKS = 128;                          // up to 67M-node universes (config 5: 50M users)
 
@@ -1221,6 +1609,11 @@ struct blp_batch {
   int dq = 1;
   bool use_hot = false;  // some source has a dense row in N(x)
   bool wave = false;     // wave-per-source scorer
+  int short_rows = 0;    // ScoreArgs::short_rows
+  int pack = 0;          // packed scorer: sources per workgroup group (0: off)
+  int slot_words = 0;    // packed scorer: bitmap words per source
+  int n_groups = 0;      // packed scorer: groups of consecutive active sources, heaviest first
+  int2* d_groups = nullptr;
   bool global = false;   // HBM-bitmap scorer (universe wider than LDS)
   int split = 0;         // chunk-parallel scorer: universe cut into `split` LDS chunks, 2 workgroups / CU
   int64_t rs_lo = 0;     // first node of the split table
@@ -1306,7 +1699,7 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   std::vector<uint8_t> seen((size_t)n, 0);
   std::vector<int32_t> srcs;
   std::vector<int64_t> work;
-  int64_t scan_work = 0;
+  int64_t scan_work = 0, max_scan_row = 0, max_build_row = 0;
   bool any_hot = false;
   int64_t rows_lo = INT64_MAX, rows_hi = INT64_MIN;  // nodes whose rows are read (the y and the z in N(x))
   const int32_t* hot = g->h_hot_idx.empty() ? nullptr : g->h_hot_idx.data();
@@ -1318,6 +1711,7 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
       hi = std::max<int64_t>(hi, (int64_t)ci[rp[yi + 1] - 1] + 1);
     }
     scan_work += rp[yi + 1] - rp[yi];
+    max_scan_row = std::max<int64_t>(max_scan_row, rp[yi + 1] - rp[yi]);
     rows_lo = std::min<int64_t>(rows_lo, yi);
     rows_hi = std::max<int64_t>(rows_hi, (int64_t)yi + 1);
     if (!seen[xi]) {
@@ -1327,6 +1721,7 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
       for (int64_t k = rp[xi]; k < rp[xi + 1]; ++k) {
         const int32_t z = ci[k];
         wsum += rp[z + 1] - rp[z];
+        max_build_row = std::max<int64_t>(max_build_row, rp[z + 1] - rp[z]);
         rows_lo = std::min<int64_t>(rows_lo, z);
         rows_hi = std::max<int64_t>(rows_hi, (int64_t)z + 1);
         any_hot |= hot && hot[z] >= 0;
@@ -1347,6 +1742,8 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   b->hi = hi;
   b->n_sources = (int64_t)srcs.size();
   b->use_hot = any_hot;
+  if (!getenv("BLP_NO_SHORT"))  // tuning knob
+    b->short_rows = (max_build_row <= SHORT_MAX ? 1 : 0) | (max_scan_row <= SHORT_MAX ? 2 : 0);
   const int64_t span = hi - lo;
   if (span <= variant_cap_bits(V_SMALL))
     b->variant = V_SMALL;
@@ -1395,8 +1792,22 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   // kernels are faster on the business side of config 2 (1.46 vs 2.01 ms, profiles/probe_sides.py)
   b->wave = span <= (int64_t)W_CAP * 32 && b->chunks == 1 && !b->global && !b->split && getenv("BLP_WAVE") &&
             !getenv("BLP_NO_WAVE");
+  // small universe, many sources: the packed scorer (groups of sources, one LDS slot each)
+  {
+    const int64_t sw = ((span + 31) / 32 + 3) / 4 * 4;
+    const int slots = (int)std::min<int64_t>(PK_MAX, sw ? CAP_LARGE / sw : 0);
+    const bool fit = b->chunks == 1 && !b->global && !b->split && !b->wave && span > 0 && slots >= 2;
+    if (fit && getenv("BLP_PACK")) {  // opt-in: slower than per-source k_score on config 2 (1.80 vs 1.53 ms)
+      b->pack = slots;
+      if (const char* e = getenv("BLP_PACK")) b->pack = std::max(1, std::min(slots, atoi(e)));  // test knob
+      b->slot_words = (int)sw;
+    }
+  }
   int per_cu = 1;
-  if (b->wave) {
+  if (b->pack) {
+    BLP_HIP_OR(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_score_pack<PK_BLOCK, CAP_LARGE, PK_SEG, 8>,
+                                                            PK_BLOCK, 0), bail);
+  } else if (b->wave) {
     BLP_HIP_OR(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_score_wave<W_WAVES, W_CAP, 8>, W_WAVES * 64, 0),
                bail);
     per_cu = std::max(per_cu, 1) * W_WAVES;  // workers are waves
@@ -1409,7 +1820,8 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   const int64_t n_wg = (int64_t)g->n_cu * per_cu;
   // sources per dequeue: the active list is in id order, which need not be balanced; keep it 1
   // unless there are very many light sources per worker
-  b->dq = (int)std::max<int64_t>(1, std::min<int64_t>(8, b->n_sources / (n_wg * 64)));
+  // (two once a worker has ~64+ sources: the business side of config 2, 1.44 -> 1.30 ms)
+  b->dq = b->n_sources >= n_wg * 64 ? (int)std::max<int64_t>(2, std::min<int64_t>(8, b->n_sources / (n_wg * 64))) : 1;
   if (const char* e = getenv("BLP_DQ")) b->dq = std::max(1, atoi(e));  // tuning knob
   // ---- heavy sources: build work far above the per-workgroup share goes to k_heavy
   const int64_t total_work = std::accumulate(work.begin(), work.end(), (int64_t)0) + scan_work;
@@ -1438,6 +1850,41 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
     }
   }
   b->n_heavy_items = (int64_t)items.size();
+  // ---- packed scorer groups: consecutive sources of the device's active list (id order),
+  // closed at n_slots sources or ~1/8 of a workgroup's share of the work, then dequeued
+  // heaviest first (the popular sources of a skewed graph would otherwise form a few slow
+  // groups at the front)
+  if (b->pack && n_pairs) {
+    std::vector<int32_t> order(srcs.size());
+    std::iota(order.begin(), order.end(), 0);
+    std::sort(order.begin(), order.end(), [&](int32_t i, int32_t j) { return srcs[i] < srcs[j]; });
+    std::vector<int32_t> pos((size_t)n, -1);
+    for (size_t i = 0; i < srcs.size(); ++i) pos[srcs[i]] = (int32_t)i;
+    std::vector<int64_t> w_src(srcs.size(), 2048);  // fixed per-source cost, in elements
+    for (size_t i = 0; i < srcs.size(); ++i)
+      w_src[i] += (heavy_slot.empty() || heavy_slot[srcs[i]] < 0) ? work[i] : b->hb_words;
+    for (int64_t i = 0; i < n_pairs; ++i) w_src[pos[x[i]]] += rp[y[i] + 1] - rp[y[i]];
+    const int64_t tot = std::accumulate(w_src.begin(), w_src.end(), (int64_t)0);
+    const int64_t target = std::max<int64_t>(1, tot / std::max<int64_t>(1, n_wg * 8));
+    std::vector<std::pair<int64_t, int2>> grp;
+    int32_t g0 = 0;
+    int64_t acc = 0;
+    for (int32_t k = 0; k < (int32_t)order.size(); ++k) {
+      acc += w_src[order[k]];
+      if (k + 1 - g0 == b->pack || acc >= target || k + 1 == (int32_t)order.size()) {
+        grp.push_back({acc, make_int2(g0, k + 1)});
+        g0 = k + 1;
+        acc = 0;
+      }
+    }
+    std::stable_sort(grp.begin(), grp.end(), [](const auto& u, const auto& v) { return u.first > v.first; });
+    std::vector<int2> gs(grp.size());
+    for (size_t i = 0; i < grp.size(); ++i) gs[i] = grp[i].second;
+    b->n_groups = (int)gs.size();
+    if (hipMalloc(&b->d_groups, sizeof(int2) * gs.size()) != hipSuccess ||
+        hipMemcpy(b->d_groups, gs.data(), sizeof(int2) * gs.size(), hipMemcpyHostToDevice) != hipSuccess)
+      return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: group table"));
+  }
   b->hb_words = ((span + 31) / 32 + 3) / 4 * 4;
   // ---- grouping geometry: buckets of 2^shift node ids, at most NB_MAX buckets
   {
@@ -1517,7 +1964,7 @@ int blp_batch_destroy(blp_batch* b) {
   timer_release(b->t_score);
   timer_release(b->t_group);
   void* ps[] = {b->d_x,    b->d_y,    b->d_cn,   b->d_jac,  b->d_aa,          b->d_gout,        b->d_gyb,
-                b->d_gyl,  b->d_misc, b->d_heavy_slot, b->d_heavy_bm, b->d_heavy_items, b->d_gbm, b->d_gy, b->d_rsplit, b->d_pcn, b->d_paa, b->d_ph2};
+                b->d_gyl,  b->d_misc, b->d_heavy_slot, b->d_heavy_bm, b->d_heavy_items, b->d_gbm, b->d_gy, b->d_rsplit, b->d_pcn, b->d_paa, b->d_ph2, b->d_groups};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   delete b;
@@ -1531,6 +1978,21 @@ int blp_batch_plan(const blp_batch* b, int64_t* lo, int64_t* hi, int* chunks, in
   if (chunks) *chunks = b->global ? 0 : b->split ? -b->split : b->chunks;  // 0: HBM bitmap; -C: chunk-parallel
   if (block) *block = b->wave ? 64 : b->global ? G_BLOCK : b->split ? S_BLOCK : variant_block(b->variant);
   if (heavy) *heavy = (int)b->n_heavy;
+  return BLP_OK;
+}
+
+#ifdef BLP_PROF
+int blp_prof_read(unsigned long long* out) {  // experiment builds only: per-phase clock sums, then reset
+  BLP_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * 16));
+  unsigned long long z[16] = {0};
+  BLP_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z)));
+  return BLP_OK;
+}
+#endif
+
+int blp_batch_slots(const blp_batch* b, int* slots) {
+  BLP_CHECK(b && slots, BLP_E_ARG, "blp_batch_slots: bad arguments");
+  *slots = b->pack;
   return BLP_OK;
 }
 
@@ -1548,14 +2010,14 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   if ((rc = g->off.reserve(4 * (n + 1)))) return rc;
   if ((rc = g->active.reserve(4 * (n + 1)))) return rc;
   // scratch: hist | hoff | tiles | bucket_active | abase | tmp
-  const int64_t sc_ints = 2 * nh + std::max(tiles_h, tiles_b) + 1 + 2 * (int64_t)b->nb + np;
+  const int64_t sc_ints = 2 * nh + std::max(tiles_h, tiles_b) + 1 + 2 * (int64_t)b->nb + 4 * np;
   if ((rc = g->scratch.reserve(4 * (sc_ints + 16)))) return rc;
   int32_t* hist = g->scratch.as<int32_t>();
   int32_t* hoff = hist + nh;
   int32_t* tiles = hoff + nh;
   int32_t* bact = tiles + std::max(tiles_h, tiles_b) + 1;
   int32_t* abase = bact + b->nb;
-  int32_t* tmp = abase + b->nb;
+  int4* tmp = reinterpret_cast<int4*>((reinterpret_cast<uintptr_t>(abase + b->nb) + 15) & ~uintptr_t(15));
   hipEvent_t t0, bt0;
   if ((rc = timer_begin(g, K_GROUP, &t0))) return rc;
   if ((rc = timer_begin(b->t_group, g->stream, &bt0))) return rc;
@@ -1566,11 +2028,11 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
     hipLaunchKernelGGL(k_scan_sum, dim3((unsigned)tiles_h), dim3(SCAN_BLOCK), 0, g->stream, hist, nh, tiles);
     hipLaunchKernelGGL(k_scan_mid, dim3(1), dim3(SCAN_BLOCK), 0, g->stream, tiles, tiles_h, (int32_t*)nullptr);
     hipLaunchKernelGGL(k_scan_out, dim3((unsigned)tiles_h), dim3(SCAN_BLOCK), 0, g->stream, hist, nh, tiles, hoff);
-    hipLaunchKernelGGL(k_bucket_scatter, dim3(b->nblk), dim3(GP_BLOCK), 0, g->stream, b->d_x, np, b->xlo, b->shift,
-                       b->nb, b->nblk, b->per_blk, hoff, tmp);
+    hipLaunchKernelGGL(k_bucket_scatter, dim3(b->nblk), dim3(GP_BLOCK), 0, g->stream, b->d_x, b->d_y, np, b->xlo,
+                       b->shift, b->nb, b->nblk, b->per_blk, hoff, tmp);
     const int keys = 1 << b->shift;
 #define BLP_GROUP_LAUNCH(K)                                                                                         \
-  hipLaunchKernelGGL(k_bucket_group<K>, dim3(b->nb), dim3(GB_BLOCK), 0, g->stream, b->d_x, b->d_y, g->d_rp, tmp, hoff, \
+  hipLaunchKernelGGL(k_bucket_group<K>, dim3(b->nb), dim3(GB_BLOCK), 0, g->stream, g->d_rp, tmp, hoff,               \
                      b->nblk, b->nb, b->shift, b->xlo, b->xspan, np, g->off.as<int32_t>(), g->cnt.as<int32_t>(), bact,  \
                      b->d_gout,                                                                                       \
                      b->d_gyb, b->d_gyl, b->d_gy)
@@ -1649,6 +2111,7 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   a.cap_bits = b->cap_bits;
   a.mask = mask | BLP_CN;  // counts are always produced (Jaccard needs them)
   a.dq = b->dq;
+  a.short_rows = b->short_rows;
   if (np && b->split) {
     int per_cu = 1;
     BLP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_score_split<S_BLOCK, S_CAP, S_SEG, 8>, S_BLOCK, 0));
@@ -1657,6 +2120,13 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
     BLP_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_split_combine, dim3(g->n_cu * 8), dim3(256), 0, g->stream, a, b->split, b->d_pcn, b->d_paa,
                        b->d_ph2, np);
+    BLP_HIP(hipGetLastError());
+  } else if (np && b->pack) {
+    int per_cu = 1;
+    BLP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_score_pack<PK_BLOCK, CAP_LARGE, PK_SEG, 8>, PK_BLOCK,
+                                                         0));
+    hipLaunchKernelGGL((k_score_pack<PK_BLOCK, CAP_LARGE, PK_SEG, 8>), dim3(g->n_cu * std::max(per_cu, 1)),
+                       dim3(PK_BLOCK), 0, g->stream, a, b->slot_words, b->d_groups, b->n_groups);
     BLP_HIP(hipGetLastError());
   } else if (np && b->global) {
     a.hot_idx = nullptr;

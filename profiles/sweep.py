@@ -46,11 +46,26 @@ for s in settings:
         for _, bt, m in passes:
             bt.score(m)
     blp.device_sync(0)
+    prof = None
+    if os.environ.get("SWEEP_PROF"):  # experiment build with -DBLP_PROF: per-phase clocks of k_score
+        import ctypes
+        L = blp._lib.lib()
+        buf = (ctypes.c_ulonglong * 16)()
+        L.blp_prof_read(buf)  # reset
+        for name, bt, m in passes:
+            L.blp_prof_read(buf)
+            bt.score(m)
+            blp.device_sync(0)
+            L.blp_prof_read(buf)
+            tot = sum(buf[:9]) or 1
+            print(json.dumps({"phases_" + name: [round(buf[i] / tot, 3) for i in range(9)], "clk": tot}), flush=True)
     row = {"setting": s, "graph_s": round(tg, 2)}
     res = {}
     for name, bt, m in passes:
         ms, n = bt.stats(0)
         row[name + "_ms"] = round(ms / max(n, 1), 4)
+        gms, gn = bt.stats(1)
+        row[name + "_group_ms"] = round(gms / max(gn, 1), 4)
         res[name] = bt.fetch(m)
     if ref is None:
         ref = res
