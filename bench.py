@@ -77,7 +77,7 @@ def pmc_traffic(kernel):
     FETCH_SIZE / WRITE_SIZE passes; 2 x FETCH_SIZE + WRITE_SIZE per MI355X_MICROARCH.md)."""
     import glob
 
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_bench.json")), key=os.path.getmtime)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_bench.json")))  # rNN_vM: newest last
     for f in reversed(files):
         try:
             rows = json.load(open(f))
