@@ -267,10 +267,7 @@ class PairBatch:
         ch, blk, hv = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         check(lib().blp_batch_plan(self.handle, ctypes.byref(lo), ctypes.byref(hi), ctypes.byref(ch),
                                    ctypes.byref(blk), ctypes.byref(hv)))
-        sl = ctypes.c_int()
-        check(lib().blp_batch_slots(self.handle, ctypes.byref(sl)))
-        return {"lo": lo.value, "hi": hi.value, "chunks": ch.value, "block": blk.value, "heavy": hv.value,
-                "slots": sl.value}
+        return {"lo": lo.value, "hi": hi.value, "chunks": ch.value, "block": blk.value, "heavy": hv.value}
 
     def score(self, mask=7):
         check(lib().blp_batch_score(self.graph.handle, self.handle, mask))

@@ -295,11 +295,9 @@ __device__ inline int build_hint(const int32_t* s_off, int ns, int step, int32_t
 // Fetch one merge-path step: the K consecutive elements [f0, f0 + K) of the concatenated
 // segments (w = node id or -1, sk = segment or -1). One LDS binary search per K elements
 // (narrowed by the hint table when given: shift >= 0).
-// s_slot (packed scorer): sk also carries the segment's bitmap slot, s | s_slot[s] << 16.
 template <int K>
 __device__ inline void mp_fetch(const int32_t* __restrict__ ci, const int64_t* s_start, const int32_t* s_off, int ns,
-                                int T, int f0, int* w, int* sk, const int32_t* hint = nullptr, int shift = -1,
-                                const int32_t* s_slot = nullptr) {
+                                int T, int f0, int* w, int* sk, const int32_t* hint = nullptr, int shift = -1) {
   if (f0 >= T) {
 #pragma unroll
     for (int k = 0; k < K; ++k) w[k] = sk[k] = -1;
@@ -326,12 +324,10 @@ __device__ inline void mp_fetch(const int32_t* __restrict__ ci, const int64_t* s
       w[4 * j + 2] = v.z;
       w[4 * j + 3] = v.w;
     }
-    const int sv = s_slot ? s | s_slot[s] << 16 : s;
 #pragma unroll
-    for (int k = 0; k < K; ++k) sk[k] = sv;
+    for (int k = 0; k < K; ++k) sk[k] = s;
     return;
   }
-  int sv = s_slot ? s | s_slot[s] << 16 : s;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const int f = f0 + k;
@@ -342,11 +338,10 @@ __device__ inline void mp_fetch(const int32_t* __restrict__ ci, const int64_t* s
         ++s;
         next = s_off[s + 1];
         pos = s_start[s];
-        sv = s_slot ? s | s_slot[s] << 16 : s;
       }
       w[k] = ci[pos];
       ++pos;
-      sk[k] = sv;
+      sk[k] = s;
     }
   }
 }
@@ -359,32 +354,27 @@ __device__ inline void mp_fetch(const int32_t* __restrict__ ci, const int64_t* s
 // idmask | sign bit, so -1 maps to >= 2^31 - c0 > width (c0 <= idmask, width < 2^31).
 __device__ inline uint32_t in_chunk(int v, uint32_t keep, uint32_t c0u) { return ((uint32_t)v & keep) - c0u; }
 
-// s_slot (packed scorer, GLOBAL false): segment s marks slot s_slot[s] of the bitmap, whose
-// bits start at s_slot[s] * slot_bits.
 template <int NT, int K, bool GLOBAL = false>
 __device__ inline void mp_build(const int32_t* __restrict__ ci, uint32_t idmask, const int64_t* s_start,
                                 const int32_t* s_off, int ns, int64_t c0, int64_t width, uint32_t* bm, int tid,
-                                const int32_t* hint = nullptr, int shift = -1, const int32_t* s_slot = nullptr,
-                                uint32_t slot_bits = 0) {
+                                const int32_t* hint = nullptr, int shift = -1) {
   const int T = s_off[ns];
   constexpr int STEP = NT * K;
   const uint32_t keep = idmask | 0x80000000u, c0u = (uint32_t)c0, wu = (uint32_t)width;
   int w[K], sk[K];
-  mp_fetch<K>(ci, s_start, s_off, ns, T, tid * K, w, sk, hint, shift, s_slot);
+  mp_fetch<K>(ci, s_start, s_off, ns, T, tid * K, w, sk, hint, shift);
   for (int base = 0; base < T; base += STEP) {
     int wn[K], skn[K];
-    mp_fetch<K>(ci, s_start, s_off, ns, T, base + STEP + tid * K, wn, skn, hint, shift, s_slot);
+    mp_fetch<K>(ci, s_start, s_off, ns, T, base + STEP + tid * K, wn, skn, hint, shift);
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       // one unsigned compare tests validity and range (see in_chunk)
       const uint32_t r = in_chunk(w[k], keep, c0u);
       if (r < wu) {
-        if (GLOBAL) {  // the workgroup's private HBM bitmap: the OR is done in the XCD's L2
+        if (GLOBAL)  // the workgroup's private HBM bitmap: the OR is done in the XCD's L2
           __hip_atomic_fetch_or(&bm[r >> 5], 1u << (r & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        } else {
-          const uint32_t rr = s_slot ? r + ((uint32_t)sk[k] >> 16) * slot_bits : r;
-          atomicOr(&bm[rr >> 5], 1u << (rr & 31));
-        }
+        else
+          atomicOr(&bm[r >> 5], 1u << (r & 31));
       }
     }
 #pragma unroll
@@ -407,12 +397,12 @@ __device__ inline void mp_scan(const int32_t* __restrict__ ci, uint32_t idmask, 
                                const long long* __restrict__ aaw, const long long* wtab, const int64_t* s_start,
                                const int32_t* s_off, int ns, int64_t c0, int64_t width, const uint32_t* bm,
                                uint32_t* s_cn, unsigned long long* s_aa, int tid, const int32_t* hint = nullptr,
-                               int shift = -1, const int32_t* s_slot = nullptr, uint32_t slot_bits = 0) {
+                               int shift = -1) {
   const int T = s_off[ns];
   constexpr int STEP = NT * K;
   const uint32_t keep = idmask | 0x80000000u, c0u = (uint32_t)c0, wu = (uint32_t)width;
   int w[K], sk[K];
-  mp_fetch<K>(ci, s_start, s_off, ns, T, tid * K, w, sk, hint, shift, s_slot);
+  mp_fetch<K>(ci, s_start, s_off, ns, T, tid * K, w, sk, hint, shift);
   for (int base = 0; base < T; base += STEP) {
     // the bitmap words and (AA) the code weights wtab[code] are read together, so one LDS
     // round trip serves both; hits with code 0 then gather aaw, before the next step's loads
@@ -421,9 +411,8 @@ __device__ inline void mp_scan(const int32_t* __restrict__ ci, uint32_t idmask, 
     long long wt[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      uint32_t r = in_chunk(w[k], keep, c0u);
+      const uint32_t r = in_chunk(w[k], keep, c0u);
       const bool in = r < wu;
-      if (s_slot) r += ((uint32_t)sk[k] >> 16) * slot_bits;
       const uint32_t word = bm[(in ? r : 0u) >> 5];
       if (AA) wt[k] = wtab[((uint32_t)w[k] >> idbits) & 255u];
       hit[k] = in && ((word >> (r & 31)) & 1u);
@@ -441,7 +430,7 @@ __device__ inline void mp_scan(const int32_t* __restrict__ ci, uint32_t idmask, 
       for (int k = 0; k < K; ++k) wt[k] = hit[k] ? wt[k] : 0ll;
     }
     int wn[K], skn[K];
-    mp_fetch<K>(ci, s_start, s_off, ns, T, base + STEP + tid * K, wn, skn, hint, shift, s_slot);
+    mp_fetch<K>(ci, s_start, s_off, ns, T, base + STEP + tid * K, wn, skn, hint, shift);
     if (sk[0] == sk[K - 1]) {  // the K elements in one segment (or none valid): one run
       unsigned c = 0;
       unsigned long long acc = 0;
@@ -451,8 +440,8 @@ __device__ inline void mp_scan(const int32_t* __restrict__ ci, uint32_t idmask, 
         if (AA) acc += (unsigned long long)wt[k];
       }
       if (c) {
-        atomicAdd(&s_cn[sk[0] & 0xffff], c);
-        if (AA) atomicAdd(&s_aa[sk[0] & 0xffff], acc);
+        atomicAdd(&s_cn[sk[0]], c);
+        if (AA) atomicAdd(&s_aa[sk[0]], acc);
       }
     } else {
       int cur = sk[0];
@@ -462,8 +451,8 @@ __device__ inline void mp_scan(const int32_t* __restrict__ ci, uint32_t idmask, 
       for (int k = 0; k < K; ++k) {
         if (sk[k] != cur) {
           if (c) {
-            atomicAdd(&s_cn[cur & 0xffff], c);
-            if (AA) atomicAdd(&s_aa[cur & 0xffff], acc);
+            atomicAdd(&s_cn[cur], c);
+            if (AA) atomicAdd(&s_aa[cur], acc);
           }
           cur = sk[k];
           c = 0;
@@ -475,8 +464,8 @@ __device__ inline void mp_scan(const int32_t* __restrict__ ci, uint32_t idmask, 
         }
       }
       if (c && cur >= 0) {
-        atomicAdd(&s_cn[cur & 0xffff], c);
-        if (AA) atomicAdd(&s_aa[cur & 0xffff], acc);
+        atomicAdd(&s_cn[cur], c);
+        if (AA) atomicAdd(&s_aa[cur], acc);
       }
     }
 #pragma unroll
@@ -511,18 +500,16 @@ __device__ inline int row_load(const int32_t* __restrict__ ci, int64_t st, int l
 
 template <int NT>
 __device__ inline void row_build(const int32_t* __restrict__ ci, uint32_t idmask, const int64_t* s_start,
-                                 const int32_t* s_off, int ns, int64_t c0, int64_t width, uint32_t* bm, int tid,
-                                 const int32_t* s_slot = nullptr, uint32_t slot_bits = 0) {
+                                 const int32_t* s_off, int ns, int64_t c0, int64_t width, uint32_t* bm, int tid) {
   const uint32_t keep = idmask | 0x80000000u, c0u = (uint32_t)c0, wu = (uint32_t)width;
   for (int t = tid; t < ns; t += NT) {
     int e[SHORT_MAX];
     const int len = row_load(ci, s_start[t], s_off[t + 1] - s_off[t], e);
-    const uint32_t base = s_slot ? (uint32_t)s_slot[t] * slot_bits : 0u;
 #pragma unroll
     for (int k = 0; k < SHORT_MAX; ++k) {
       if (k < len) {
         const uint32_t r = in_chunk(e[k], keep, c0u);
-        if (r < wu) atomicOr(&bm[(r + base) >> 5], 1u << ((r + base) & 31));
+        if (r < wu) atomicOr(&bm[r >> 5], 1u << (r & 31));
       }
     }
   }
@@ -532,22 +519,19 @@ template <int NT, bool AA>
 __device__ inline void row_scan(const int32_t* __restrict__ ci, uint32_t idmask, int idbits,
                                 const long long* __restrict__ aaw, const long long* wtab, const int64_t* s_start,
                                 const int32_t* s_off, int ns, int64_t c0, int64_t width, const uint32_t* bm,
-                                uint32_t* s_cn, unsigned long long* s_aa, int tid, const int32_t* s_slot = nullptr,
-                                uint32_t slot_bits = 0) {
+                                uint32_t* s_cn, unsigned long long* s_aa, int tid) {
   const uint32_t keep = idmask | 0x80000000u, c0u = (uint32_t)c0, wu = (uint32_t)width;
   for (int t = tid; t < ns; t += NT) {  // the thread owns segment t: plain adds, no atomics
     int e[SHORT_MAX];
     const int len = row_load(ci, s_start[t], s_off[t + 1] - s_off[t], e);
-    const uint32_t base = s_slot ? (uint32_t)s_slot[t] * slot_bits : 0u;
     unsigned c = 0;
     unsigned long long acc = 0;
 #pragma unroll
     for (int k = 0; k < SHORT_MAX; ++k) {
       if (k < len) {
         const uint32_t r = in_chunk(e[k], keep, c0u);
-        const uint32_t rb = r + base;
-        const uint32_t word = bm[(r < wu ? rb : 0u) >> 5];
-        const bool hit = r < wu && ((word >> (rb & 31)) & 1u);
+        const uint32_t word = bm[(r < wu ? r : 0u) >> 5];
+        const bool hit = r < wu && ((word >> (r & 31)) & 1u);
         c += hit ? 1u : 0u;
         if (AA && hit) {
           const uint32_t code = ((uint32_t)e[k] >> idbits) & 255u;
@@ -878,233 +862,6 @@ __global__ __launch_bounds__(BLOCK) void k_score(ScoreArgs a) {
     }
   }
   PROF_FLUSH
-}
-
-// ------------------------------------------------------------------ packed scorer
-// Small universes (the business side of a review graph: H2(v) over 100K businesses is
-// 12.5 KiB) use a tenth of a 136 KiB LDS bitmap, and each source is then a short chain of
-// dependent round trips (dequeue, N(x) rows, build, popcount, pair segments, scan, outputs)
-// that 16 waves cannot hide. Here a workgroup dequeues a GROUP of up to n_slots sources and
-// runs every phase once for the whole group: each source owns a bitmap slot of slot_words
-// words; the build's row segments and the scan's pair segments carry their slot (mp_fetch
-// packs it into the segment id). Same exact-distance rule and pair bookkeeping as k_score.
-constexpr int PK_MAX = 32;  // sources per group
-constexpr int PK_HINT = 1024;
-
-// last i in [0, n) with off[i] <= g (off[0] = 0 <= g < off[n]); n <= PK_MAX
-__device__ inline int group_find(const int* off, int n, int g) {
-  int lo = 0, hi = n;
-  while (hi - lo > 1) {
-    const int mid = (lo + hi) >> 1;
-    if (off[mid] <= g)
-      lo = mid;
-    else
-      hi = mid;
-  }
-  return lo;
-}
-
-template <int BLOCK, int CAP_WORDS, int SEG, int K>
-__global__ __launch_bounds__(BLOCK) void k_score_pack(ScoreArgs a, int slot_words, const int2* __restrict__ groups,
-                                                      int n_groups) {
-  __shared__ uint32_t bm[CAP_WORDS];
-  __shared__ int64_t s_start[SEG];
-  __shared__ int32_t s_off[SEG + 1];
-  __shared__ int32_t s_slot[SEG];
-  __shared__ uint32_t s_cn[SEG];
-  __shared__ unsigned long long s_aa[SEG];
-  __shared__ int32_t s_gp[SEG];
-  __shared__ int32_t s_hint[PK_HINT];
-  __shared__ long long s_wtab[256];
-  __shared__ int red[BLOCK / 64];
-  __shared__ int s_x[PK_MAX], s_heavy[PK_MAX], s_pb[PK_MAX];
-  __shared__ int64_t s_xb[PK_MAX];
-  __shared__ int s_roff[PK_MAX + 1], s_doff[PK_MAX + 1], s_poff[PK_MAX + 1];
-  __shared__ unsigned s_h2[PK_MAX];
-  __shared__ int s_first;
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const bool want_j = (a.mask & BLP_JACCARD) != 0;
-  const bool want_a = (a.mask & BLP_ADAMIC) != 0;
-  const int64_t span = a.hi - a.lo;
-  const uint32_t slot_bits = 32u * (uint32_t)slot_words;
-  const int sw4 = slot_words >> 2;
-  uint4* bm4 = reinterpret_cast<uint4*>(bm);
-  const int n_active = a.misc->n_active;
-  if (a.wtab)  // visible after the first barrier
-    for (int i = tid; i < 256; i += BLOCK) s_wtab[i] = a.wtab[i];
-
-  for (;;) {
-    if (tid == 0) {
-      const int gi = atomicAdd(&a.misc->queue, 1);
-      s_first = gi < n_groups ? gi : -1;
-    }
-    __syncthreads();
-    const int gi = s_first;
-    if (gi < 0) break;
-    const int2 gr = groups[gi];
-    const int first = gr.x;
-    const int ng = min(gr.y, n_active) - first;  // n_active equals the planned source count
-    // 0. group table (first wave): sources, their row / removal / pair offsets
-    if (tid < 64) {
-      int nrow = 0, ndrop = 0, npair = 0;
-      if (lane < ng) {
-        const int x = a.active[first + lane];
-        const int64_t xb = a.rp[x], xe = a.rp[x + 1];
-        const int hs = a.heavy_slot ? a.heavy_slot[x] : -1;
-        // N(x) intersects the universe? (rows are sorted; bipartite sides are disjoint)
-        const bool meet = xe > xb && (int64_t)a.ci[xe - 1] >= a.lo && (int64_t)a.ci[xb] < a.hi;
-        s_x[lane] = x;
-        s_xb[lane] = xb;
-        s_heavy[lane] = hs;
-        s_pb[lane] = a.off[x];
-        s_h2[lane] = 0;
-        nrow = hs >= 0 ? 0 : (int)(xe - xb);
-        ndrop = meet ? (int)(xe - xb) : 0;
-        npair = a.cnt[x];
-      }
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const int r1 = __shfl_up(nrow, d, 64), r2 = __shfl_up(ndrop, d, 64), r3 = __shfl_up(npair, d, 64);
-        if (lane >= d) {
-          nrow += r1;
-          ndrop += r2;
-          npair += r3;
-        }
-      }
-      if (lane < ng) {  // inclusive -> offsets [lane + 1]
-        s_roff[lane + 1] = nrow;
-        s_doff[lane + 1] = ndrop;
-        s_poff[lane + 1] = npair;
-      }
-      if (lane == 0) s_roff[0] = s_doff[0] = s_poff[0] = 0;
-    }
-    __syncthreads();
-    // 1. slots: zero, or the bitmap k_heavy pre-built for a heavy source
-    for (int q = tid; q < ng * sw4; q += BLOCK) {
-      const int i = q / sw4;
-      const int hs = s_heavy[i];
-      bm4[q] = hs >= 0 ? reinterpret_cast<const uint4*>(a.heavy_bm + (int64_t)hs * a.hb_words)[q - i * sw4]
-                       : make_uint4(0, 0, 0, 0);
-    }
-    __syncthreads();
-    // 2. build: the rows of every (non-heavy) source's N(x), SEG rows at a time
-    const int R = s_roff[ng];
-    for (int k0 = 0; k0 < R; k0 += SEG) {
-      const int ns = min(SEG, R - k0);
-      int len = 0;
-      if (tid < ns) {
-        const int gi = k0 + tid;
-        const int i = group_find(s_roff, ng, gi);
-        const int z = a.ci[s_xb[i] + (gi - s_roff[i])];
-        const int64_t st = a.rp[z];
-        s_start[tid] = st;
-        s_slot[tid] = i;
-        len = (int)(a.rp[z + 1] - st);
-      }
-      int tot;
-      const int ex = block_exscan<BLOCK>(len, red, &tot);
-      if (tid < ns) s_off[tid] = ex;
-      if (tid == 0) s_off[ns] = tot;
-      __syncthreads();
-      if (a.short_rows & 1) {
-        row_build<BLOCK>(a.cw, a.idmask, s_start, s_off, ns, a.lo, span, bm, tid, s_slot, slot_bits);
-      } else {
-        const int shift = build_hint<BLOCK, PK_HINT>(s_off, ns, BLOCK * K, s_hint);
-        mp_build<BLOCK, K>(a.cw, a.idmask, s_start, s_off, ns, a.lo, span, bm, tid, s_hint, shift, s_slot, slot_bits);
-      }
-      __syncthreads();
-    }
-    // 3. exact distance 2: drop x (distance 0) and N(x) (distance 1) from each slot
-    for (int gi = tid; gi < s_doff[ng]; gi += BLOCK) {
-      const int i = group_find(s_doff, ng, gi);
-      const int64_t r = (int64_t)a.ci[s_xb[i] + (gi - s_doff[i])] - a.lo;
-      if (r >= 0 && r < span) {
-        const uint32_t rr = (uint32_t)i * slot_bits + (uint32_t)r;
-        atomicAnd(&bm[rr >> 5], ~(1u << (rr & 31)));
-      }
-    }
-    if (tid < ng) {
-      const int64_t r = (int64_t)s_x[tid] - a.lo;
-      if (r >= 0 && r < span) {
-        const uint32_t rr = (uint32_t)tid * slot_bits + (uint32_t)r;
-        atomicAnd(&bm[rr >> 5], ~(1u << (rr & 31)));
-      }
-    }
-    __syncthreads();
-    // 4. |H2(x)| per slot
-    if (want_j) {
-      int cur = -1;
-      unsigned pc = 0;
-      for (int q = tid; q < ng * sw4; q += BLOCK) {
-        const int i = q / sw4;
-        if (i != cur) {
-          if (pc) atomicAdd(&s_h2[cur], pc);
-          cur = i;
-          pc = 0;
-        }
-        const uint4 v = bm4[q];
-        pc += __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);
-      }
-      if (pc) atomicAdd(&s_h2[cur], pc);
-      __syncthreads();
-    }
-    // 5. scan N(y) of every pair of the group, SEG pairs at a time
-    const int P = s_poff[ng];
-    for (int sb = 0; sb < P; sb += SEG) {
-      const int ns = min(SEG, P - sb);
-      int len = 0;
-      if (tid < ns) {
-        const int gi = sb + tid;
-        const int i = group_find(s_poff, ng, gi);
-        const int gp = s_pb[i] + (gi - s_poff[i]);
-        s_start[tid] = a.g_yb[gp];
-        s_slot[tid] = i;
-        s_gp[tid] = gp;
-        len = a.g_yl[gp];
-        s_cn[tid] = 0;
-        s_aa[tid] = 0;
-      }
-      int tot;
-      const int ex = block_exscan<BLOCK>(len, red, &tot);
-      if (tid < ns) s_off[tid] = ex;
-      if (tid == 0) s_off[ns] = tot;
-      __syncthreads();
-      if (a.short_rows & 2) {
-        if (want_a)
-          row_scan<BLOCK, true>(a.cw, a.idmask, a.idbits, a.aaw, s_wtab, s_start, s_off, ns, a.lo, span, bm, s_cn, s_aa,
-                                tid, s_slot, slot_bits);
-        else
-          row_scan<BLOCK, false>(a.cw, a.idmask, a.idbits, a.aaw, s_wtab, s_start, s_off, ns, a.lo, span, bm, s_cn,
-                                 s_aa, tid, s_slot, slot_bits);
-      } else {
-        const int shift = build_hint<BLOCK, PK_HINT>(s_off, ns, BLOCK * K, s_hint);
-        if (want_a)
-          mp_scan<BLOCK, K, true>(a.cw, a.idmask, a.idbits, a.aaw, s_wtab, s_start, s_off, ns, a.lo, span, bm, s_cn,
-                                  s_aa, tid, s_hint, shift, s_slot, slot_bits);
-        else
-          mp_scan<BLOCK, K, false>(a.cw, a.idmask, a.idbits, a.aaw, s_wtab, s_start, s_off, ns, a.lo, span, bm, s_cn,
-                                   s_aa, tid, s_hint, shift, s_slot, slot_bits);
-      }
-      __syncthreads();
-      if (tid < ns) {
-        const int p = a.g_out[s_gp[tid]];
-        const unsigned c = s_cn[tid];
-        a.cn[p] = c;
-        if (want_a) a.aa[p] = (double)s_aa[tid] * (1.0 / blp::AA_SCALE);
-        if (want_j) {
-          const long long uni = (long long)s_h2[s_slot[tid]] + (s_off[tid + 1] - s_off[tid]) - (long long)c;
-          if (uni <= 0) {
-            a.jac[p] = __builtin_nan("");
-            atomicOr(&a.misc->zero_div, 1);
-          } else {
-            a.jac[p] = (double)c / (double)uni;  // correctly rounded, as Python's float division
-          }
-        }
-      }
-      __syncthreads();
-    }
-  }
 }
 
 // ------------------------------------------------------------------ HBM-bitmap scorer
@@ -1577,7 +1334,6 @@ constexpr int CAP_SMALL = 4096, CAP_MED = 16384, CAP_LARGE = 34816;
 constexpr int BLOCK_SMALL = 256, BLOCK_MED = 512, BLOCK_LARGE = 1024;
 constexpr int SEG_SMALL = 256, SEG_MED = 512, SEG_LARGE = 512;
 constexpr int G_BLOCK = 1024, G_SEG = 512;  // HBM-bitmap scorer
-constexpr int PK_BLOCK = 1024, PK_SEG = 512;  // packed scorer
 constexpr int S_BLOCK = 1024, S_CAP = 16384, S_SEG = 512;  // chunk-parallel scorer: 64 KiB chunks, 2 blocks / CU
 constexpr int S_MAX_CHUNKS = 128;                          // up to 67M-node universes (config 5: 50M users)
 
@@ -1610,10 +1366,6 @@ struct blp_batch {
   bool use_hot = false;  // some source has a dense row in N(x)
   bool wave = false;     // wave-per-source scorer
   int short_rows = 0;    // ScoreArgs::short_rows
-  int pack = 0;          // packed scorer: sources per workgroup group (0: off)
-  int slot_words = 0;    // packed scorer: bitmap words per source
-  int n_groups = 0;      // packed scorer: groups of consecutive active sources, heaviest first
-  int2* d_groups = nullptr;
   bool global = false;   // HBM-bitmap scorer (universe wider than LDS)
   int split = 0;         // chunk-parallel scorer: universe cut into `split` LDS chunks, 2 workgroups / CU
   int64_t rs_lo = 0;     // first node of the split table
@@ -1792,22 +1544,8 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   // kernels are faster on the business side of config 2 (1.46 vs 2.01 ms, profiles/probe_sides.py)
   b->wave = span <= (int64_t)W_CAP * 32 && b->chunks == 1 && !b->global && !b->split && getenv("BLP_WAVE") &&
             !getenv("BLP_NO_WAVE");
-  // small universe, many sources: the packed scorer (groups of sources, one LDS slot each)
-  {
-    const int64_t sw = ((span + 31) / 32 + 3) / 4 * 4;
-    const int slots = (int)std::min<int64_t>(PK_MAX, sw ? CAP_LARGE / sw : 0);
-    const bool fit = b->chunks == 1 && !b->global && !b->split && !b->wave && span > 0 && slots >= 2;
-    if (fit && getenv("BLP_PACK")) {  // opt-in: slower than per-source k_score on config 2 (1.80 vs 1.53 ms)
-      b->pack = slots;
-      if (const char* e = getenv("BLP_PACK")) b->pack = std::max(1, std::min(slots, atoi(e)));  // test knob
-      b->slot_words = (int)sw;
-    }
-  }
   int per_cu = 1;
-  if (b->pack) {
-    BLP_HIP_OR(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_score_pack<PK_BLOCK, CAP_LARGE, PK_SEG, 8>,
-                                                            PK_BLOCK, 0), bail);
-  } else if (b->wave) {
+  if (b->wave) {
     BLP_HIP_OR(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_score_wave<W_WAVES, W_CAP, 8>, W_WAVES * 64, 0),
                bail);
     per_cu = std::max(per_cu, 1) * W_WAVES;  // workers are waves
@@ -1850,41 +1588,6 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
     }
   }
   b->n_heavy_items = (int64_t)items.size();
-  // ---- packed scorer groups: consecutive sources of the device's active list (id order),
-  // closed at n_slots sources or ~1/8 of a workgroup's share of the work, then dequeued
-  // heaviest first (the popular sources of a skewed graph would otherwise form a few slow
-  // groups at the front)
-  if (b->pack && n_pairs) {
-    std::vector<int32_t> order(srcs.size());
-    std::iota(order.begin(), order.end(), 0);
-    std::sort(order.begin(), order.end(), [&](int32_t i, int32_t j) { return srcs[i] < srcs[j]; });
-    std::vector<int32_t> pos((size_t)n, -1);
-    for (size_t i = 0; i < srcs.size(); ++i) pos[srcs[i]] = (int32_t)i;
-    std::vector<int64_t> w_src(srcs.size(), 2048);  // fixed per-source cost, in elements
-    for (size_t i = 0; i < srcs.size(); ++i)
-      w_src[i] += (heavy_slot.empty() || heavy_slot[srcs[i]] < 0) ? work[i] : b->hb_words;
-    for (int64_t i = 0; i < n_pairs; ++i) w_src[pos[x[i]]] += rp[y[i] + 1] - rp[y[i]];
-    const int64_t tot = std::accumulate(w_src.begin(), w_src.end(), (int64_t)0);
-    const int64_t target = std::max<int64_t>(1, tot / std::max<int64_t>(1, n_wg * 8));
-    std::vector<std::pair<int64_t, int2>> grp;
-    int32_t g0 = 0;
-    int64_t acc = 0;
-    for (int32_t k = 0; k < (int32_t)order.size(); ++k) {
-      acc += w_src[order[k]];
-      if (k + 1 - g0 == b->pack || acc >= target || k + 1 == (int32_t)order.size()) {
-        grp.push_back({acc, make_int2(g0, k + 1)});
-        g0 = k + 1;
-        acc = 0;
-      }
-    }
-    std::stable_sort(grp.begin(), grp.end(), [](const auto& u, const auto& v) { return u.first > v.first; });
-    std::vector<int2> gs(grp.size());
-    for (size_t i = 0; i < grp.size(); ++i) gs[i] = grp[i].second;
-    b->n_groups = (int)gs.size();
-    if (hipMalloc(&b->d_groups, sizeof(int2) * gs.size()) != hipSuccess ||
-        hipMemcpy(b->d_groups, gs.data(), sizeof(int2) * gs.size(), hipMemcpyHostToDevice) != hipSuccess)
-      return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: group table"));
-  }
   b->hb_words = ((span + 31) / 32 + 3) / 4 * 4;
   // ---- grouping geometry: buckets of 2^shift node ids, at most NB_MAX buckets
   {
@@ -1964,7 +1667,7 @@ int blp_batch_destroy(blp_batch* b) {
   timer_release(b->t_score);
   timer_release(b->t_group);
   void* ps[] = {b->d_x,    b->d_y,    b->d_cn,   b->d_jac,  b->d_aa,          b->d_gout,        b->d_gyb,
-                b->d_gyl,  b->d_misc, b->d_heavy_slot, b->d_heavy_bm, b->d_heavy_items, b->d_gbm, b->d_gy, b->d_rsplit, b->d_pcn, b->d_paa, b->d_ph2, b->d_groups};
+                b->d_gyl,  b->d_misc, b->d_heavy_slot, b->d_heavy_bm, b->d_heavy_items, b->d_gbm, b->d_gy, b->d_rsplit, b->d_pcn, b->d_paa, b->d_ph2};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   delete b;
@@ -1990,11 +1693,7 @@ int blp_prof_read(unsigned long long* out) {  // experiment builds only: per-pha
 }
 #endif
 
-int blp_batch_slots(const blp_batch* b, int* slots) {
-  BLP_CHECK(b && slots, BLP_E_ARG, "blp_batch_slots: bad arguments");
-  *slots = b->pack;
-  return BLP_OK;
-}
+
 
 int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   BLP_CHECK(g && b && b->g == g, BLP_E_ARG, "blp_batch_score: graph/batch mismatch");
@@ -2120,13 +1819,6 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
     BLP_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_split_combine, dim3(g->n_cu * 8), dim3(256), 0, g->stream, a, b->split, b->d_pcn, b->d_paa,
                        b->d_ph2, np);
-    BLP_HIP(hipGetLastError());
-  } else if (np && b->pack) {
-    int per_cu = 1;
-    BLP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_score_pack<PK_BLOCK, CAP_LARGE, PK_SEG, 8>, PK_BLOCK,
-                                                         0));
-    hipLaunchKernelGGL((k_score_pack<PK_BLOCK, CAP_LARGE, PK_SEG, 8>), dim3(g->n_cu * std::max(per_cu, 1)),
-                       dim3(PK_BLOCK), 0, g->stream, a, b->slot_words, b->d_groups, b->n_groups);
     BLP_HIP(hipGetLastError());
   } else if (np && b->global) {
     a.hot_idx = nullptr;

@@ -119,10 +119,6 @@ int blp_batch_destroy(blp_batch* b);
  * block, number of heavy sources pre-built across workgroups. For tests and DESIGN.md.     */
 int blp_batch_plan(const blp_batch* b, int64_t* lo, int64_t* hi, int* chunks, int* block,
                    int* heavy);
-/* Packed scorer: sources per workgroup group, one LDS bitmap slot each (0: not packed). A
- * universe at most half the LDS bitmap with many sources (the business side of a review
- * graph) is scored group by group; results are identical.                                 */
-int blp_batch_slots(const blp_batch* b, int* slots);
 
 /* Per-batch device time of the last/accumulated blp_batch_score calls (HIP events on the
  * graph stream): which 0 = scorer kernel, 1 = grouping kernels. Reset with blp_batch_stats_reset. */

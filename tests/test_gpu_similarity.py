@@ -94,10 +94,6 @@ def test_general_graph_exact_distance(gpu):
     {"BLP_HOT_MIN": "1", "BLP_HOT_DENSITY": "100000000"},  # > HOT_LIST dense rows: sparse fallback
     {"BLP_WAVE": "1"},                                  # wave-per-source scorer (opt-in)
     {"BLP_WAVE": "1", "BLP_HEAVY_WORK": "50", "BLP_HOT_MIN": "8"},
-    {"BLP_PACK": "32"},                                 # packed scorer: source groups, one slot each
-    {"BLP_PACK": "3"},
-    {"BLP_PACK": "5", "BLP_HEAVY_WORK": "50"},          # ... with heavy sources' pre-built slots
-    {"BLP_PACK": "4", "BLP_WCODES": "3"},
     {"BLP_VARIANT": "1"},                               # 64 KiB-bitmap scorer (no hint table)
     {"BLP_VARIANT": "2"},                               # 136 KiB-bitmap scorer
     {"BLP_WCODES": "0"},                                # every AA weight gathered per node
@@ -125,17 +121,13 @@ def test_kernel_paths_vs_oracle(gpu, knobs, monkeypatch):
         assert G.batch(x, y).plan()["chunks"] == 0  # HBM-bitmap scorer
     if "BLP_SPLIT" in knobs:
         assert G.batch(x, y).plan()["chunks"] == -int(knobs["BLP_SPLIT"])  # chunk-parallel scorer
-    if "BLP_PACK" in knobs:
-        assert G.batch(y, x).plan()["slots"] == int(knobs["BLP_PACK"])
 
 
-@pytest.mark.parametrize("variant", [None, "1", "2", "pack"])
+@pytest.mark.parametrize("variant", [None, "1", "2"])
 def test_many_pairs_per_source_vs_oracle(gpu, variant, monkeypatch):
     # > SEG pairs per source and > SEG rows in N(x): the segment-chunk loops; batches of more
     # than one block step: the segment hint tables
-    if variant == "pack":
-        monkeypatch.setenv("BLP_PACK", "4")
-    elif variant:
+    if variant:
         monkeypatch.setenv("BLP_VARIANT", variant)
     rng = np.random.default_rng(12)
     a, b = bipartite_edges(rng, 20000, 1500, 200000)
