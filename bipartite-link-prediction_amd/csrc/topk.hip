@@ -237,9 +237,18 @@ __device__ long long push_pass(const TkArgs& a, TkShared& s, int x, int64_t xb, 
       const int len_w = (int)(r1n - r0n);
       const int32_t pp = ppn;
       const int32_t* roww = base + r0;
+      // the first TK_RB entries as 16-byte vectors (rows are padded past their ends)
       int32_t e[TK_RB];
+      const blp::U4a* rv = reinterpret_cast<const blp::U4a*>(roww);
 #pragma unroll
-      for (int j = 0; j < TK_RB; ++j) e[j] = (!skip && j < len_w) ? roww[j] : 0x7FFFFFFF;
+      for (int q = 0; q < TK_RB / 4; ++q) {
+        blp::U4a v = {0x7FFFFFFF, 0x7FFFFFFF, 0x7FFFFFFF, 0x7FFFFFFF};
+        if (!skip && 4 * q < len_w) v = rv[q];
+        e[4 * q] = 4 * q < len_w ? v.x : 0x7FFFFFFF;
+        e[4 * q + 1] = 4 * q + 1 < len_w ? v.y : 0x7FFFFFFF;
+        e[4 * q + 2] = 4 * q + 2 < len_w ? v.z : 0x7FFFFFFF;
+        e[4 * q + 3] = 4 * q + 3 < len_w ? v.w : 0x7FFFFFFF;
+      }
       idx += TK_NT;
       if (idx < E) skipn = fetch(idx, r0n, r1n, ppn);
       if (skip) continue;
@@ -720,7 +729,7 @@ extern "C" int blp_topk_create(blp_graph* g, int64_t src_lo, int64_t src_hi, int
   for (int64_t i = 0; i < T; ++i) paddr[i] = (int32_t)host_addr(t, perm[i]);
   // source rows with permuted target ids, each sorted (multi-threaded)
   const int64_t m = rp[src_hi] - t->pbase;
-  std::vector<int32_t> pci(std::max<int64_t>(m, 1));
+  std::vector<int32_t> pci(m + TK_RB, 0x7FFFFFFF);  // padded: rows are read in 16-byte vectors
   {
     const int nth = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     std::vector<std::thread> th;
@@ -778,7 +787,7 @@ extern "C" int blp_topk_create(blp_graph* g, int64_t src_lo, int64_t src_hi, int
         const int32_t w = ci[kbase + i];
         x2_off[i + 1] = x2_off[i] + (rp[w + 1] - rp[w]);
       }
-      x2.resize(std::max<int64_t>(x2_off[mt], 1));
+      x2.resize(x2_off[mt] + TK_RB, 0x7FFFFFFF);  // padded like pci
       const int nth = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
       std::vector<std::thread> th;
       for (int q = 0; q < nth; ++q) {
