@@ -58,6 +58,10 @@ struct KernelTimer {
 
 }  // namespace blp
 
+namespace blp {
+constexpr int64_t CI_PAD = 16;  // ids of zero padding before and after d_ci / d_ci_w
+}
+
 struct blp_graph {
   int device = 0;
   int n_cu = 256;
@@ -65,7 +69,7 @@ struct blp_graph {
   int64_t n = 0;    // nodes
   int64_t nnz = 0;  // stored CSR entries (both directions, no self-loops)
   int64_t* d_rp = nullptr;   // [n+1]
-  int32_t* d_ci = nullptr;   // [nnz]
+  int32_t* d_ci = nullptr;   // [nnz], CI_PAD readable ids on each side
   long long* d_aaw_fx = nullptr;  // [n] Adamic-Adar weight per node, fixed point 2^-40 (or null)
   // weight-coded copy of d_ci for the scorers: ci | code(ci) << id_bits, code 1..255 naming
   // one of the graph's most used weights (d_wtab[code]), 0 = look up d_aaw_fx (or null)

@@ -166,8 +166,9 @@ int build_weight_codes(blp_graph* g, const int64_t* row_ptr, const std::vector<l
   }
   uint8_t* d_ncode = nullptr;
   BLP_HIP(hipMemcpy(g->d_wtab, wtab.data(), sizeof(long long) * 256, hipMemcpyHostToDevice));
-  BLP_HIP(hipMalloc(&g->d_ci_w, sizeof(int32_t) * (nnz + 16)));
-  BLP_HIP(hipMemset(g->d_ci_w, 0, sizeof(int32_t) * (nnz + 16)));
+  BLP_HIP(hipMalloc(&g->d_ci_w, sizeof(int32_t) * (nnz + 2 * CI_PAD)));
+  BLP_HIP(hipMemset(g->d_ci_w, 0, sizeof(int32_t) * (nnz + 2 * CI_PAD)));
+  g->d_ci_w += CI_PAD;
   BLP_HIP(hipMalloc(&d_ncode, (size_t)n));
   BLP_HIP(hipMemcpy(d_ncode, ncode.data(), (size_t)n, hipMemcpyHostToDevice));
   hipLaunchKernelGGL(k_code_ids, dim3((unsigned)std::min<int64_t>((nnz + 255) / 256, 1 << 20)), dim3(256), 0, g->stream,
@@ -270,9 +271,11 @@ int blp_graph_create(const int64_t* row_ptr, const int32_t* col_idx, int64_t n, 
   if ((rc = [&]() -> int {
          BLP_HIP(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
          BLP_HIP(hipMalloc(&g->d_rp, sizeof(int64_t) * (n + 1)));
-         // padded: the scorers read short rows in 16-byte vectors, up to 3 ids past a row
-         BLP_HIP(hipMalloc(&g->d_ci, sizeof(int32_t) * (nnz + 16)));
-         BLP_HIP(hipMemset(g->d_ci, 0, sizeof(int32_t) * (nnz + 16)));
+         // padded on both sides (CI_PAD ids): the scorers read rows in 16-byte vectors, up to
+         // 15 ids past a row end or before a row start
+         BLP_HIP(hipMalloc(&g->d_ci, sizeof(int32_t) * (nnz + 2 * CI_PAD)));
+         BLP_HIP(hipMemset(g->d_ci, 0, sizeof(int32_t) * (nnz + 2 * CI_PAD)));
+         g->d_ci += CI_PAD;
          BLP_HIP(hipMemcpy(g->d_rp, row_ptr, sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice));
          if (nnz) BLP_HIP(hipMemcpy(g->d_ci, col_idx, sizeof(int32_t) * nnz, hipMemcpyHostToDevice));
          if (aaw) {
@@ -304,9 +307,9 @@ int blp_graph_destroy(blp_graph* g) {
   g->scratch.release();
   free_hot_index(g);
   if (g->d_rp) (void)hipFree(g->d_rp);
-  if (g->d_ci) (void)hipFree(g->d_ci);
+  if (g->d_ci) (void)hipFree(g->d_ci - CI_PAD);
   if (g->d_aaw_fx) (void)hipFree(g->d_aaw_fx);
-  if (g->d_ci_w) (void)hipFree(g->d_ci_w);
+  if (g->d_ci_w) (void)hipFree(g->d_ci_w - CI_PAD);
   if (g->d_wtab) (void)hipFree(g->d_wtab);
   if (g->stream) (void)hipStreamDestroy(g->stream);
   delete g;

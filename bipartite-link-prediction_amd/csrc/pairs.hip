@@ -28,6 +28,13 @@
 
 #include "blp_internal.h"
 
+#ifndef BLP_RC
+#define BLP_RC 1  // row-chunk loops in the large-universe k_score (0: merge-path loops)
+#endif
+#ifndef BLP_PP
+#define BLP_PP 1  // ping-pong merge-path loops in k_score (0: the single-buffer mp_build / mp_scan)
+#endif
+
 namespace {
 
 constexpr int SCAN_BLOCK = 256;
@@ -476,6 +483,376 @@ __device__ inline void mp_scan(const int32_t* __restrict__ ci, uint32_t idmask, 
   }
 }
 
+// ------------------------------------------------------------------ ping-pong merge-path loops
+// mp_build / mp_scan keep one step of prefetch in a register copy (w = wn at the loop end).
+// The copy needs the prefetched data, and mp_fetch issues 0, K/4 or K loads depending on the
+// lane's path, so the compiler's wait before a use is vmcnt(0): each step's global latency is
+// exposed and only the 16 waves of the CU hide it. Here two register buffers alternate (the
+// loop is unrolled by two, no copies), and every fetch issues exactly 2 * K/4 16-byte loads
+// on every path, so the wait before a step's use is vmcnt(2 * K/4): the other buffer's loads
+// stay in flight while the step's LDS work runs.
+//
+// One fetch covers elements [f0, f0 + K): the lane's first row from f0 (vector a), and the
+// first non-empty row after it (vector b), read from rem1 ids BEFORE that row's start so that
+// element k is a[k] for k < rem1 and b[k] otherwise (ci carries CI_PAD ids of padding on
+// both sides). The selection happens at use (PPStep::id), so nothing waits on the loads at
+// fetch time. Elements in a third row (only when a row is shorter than K) are handed to
+// `rare` at once with plain loads.
+// s_waitcnt vmcnt(0) (gfx9 encoding: expcnt and lgkmcnt at their maxima). Each ping-pong loop
+// leaves one unused fetch in flight on exit; draining it there keeps the compiler's pending-
+// load bookkeeping clean at the next loop's header, where it would otherwise insert waits
+// for registers it reuses -- waits that, vmcnt being a counter, stall on the live buffer.
+__device__ inline void vm_drain() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
+template <int K>
+struct PPStep {
+  int va[K], vb[K];
+  int s1, s2, rem1, limb, lim;  // segments, elements in s1, elements in s1 + s2, valid elements
+  __device__ inline int id(int k) const { return k >= lim ? -1 : k < rem1 ? va[k] : k < limb ? vb[k] : -1; }
+  // Mark every loaded register as used here, on every path: the compiler then waits for the
+  // whole step at once (vmcnt = the other buffer's loads) and knows them complete afterwards;
+  // otherwise a register some path never reads stays "pending" into the next iteration,
+  // where reusing it costs a wait on the live buffer.
+  __device__ inline void land() const {
+#pragma unroll
+    for (int k = 0; k < K; ++k) asm volatile("" ::"v"(va[k]), "v"(vb[k]));
+  }
+};
+
+template <int K, typename Rare>
+__device__ inline void pp_fetch(const int32_t* __restrict__ ci, const int64_t* s_start, const int32_t* s_off, int ns,
+                                int T, int f0, const int32_t* hint, int shift, PPStep<K>& st, Rare rare) {
+  int64_t p1 = 0, p2 = 0;
+  int n2 = 0;
+  st.s1 = -1;
+  st.s2 = -1;
+  st.rem1 = 0;
+  const bool valid = f0 < T;
+  if (valid) {
+    int s;
+    if (shift >= 0) {
+      const int g = f0 >> shift;
+      s = seg_search(s_off, ns, f0, hint[g], hint[g + 1] + 1);
+    } else {
+      s = seg_search(s_off, ns, f0);
+    }
+    const int next = s_off[s + 1];
+    st.s1 = s;
+    st.rem1 = next - f0;
+    p1 = s_start[s] + (f0 - s_off[s]);
+    p2 = p1;
+    if (st.rem1 < K && next < T) {
+      int t = s + 1;
+      while (s_off[t + 1] == next) ++t;  // skip empty rows; one with elements exists (next < T)
+      st.s2 = t;
+      n2 = s_off[t + 1];
+      p2 = s_start[t] - st.rem1;
+    }
+  }
+  const blp::U4a* q1 = reinterpret_cast<const blp::U4a*>(ci + p1);
+  const blp::U4a* q2 = reinterpret_cast<const blp::U4a*>(ci + p2);
+#pragma unroll
+  for (int j = 0; j < K / 4; ++j) {
+    const blp::U4a v = q1[j];
+    st.va[4 * j] = v.x;
+    st.va[4 * j + 1] = v.y;
+    st.va[4 * j + 2] = v.z;
+    st.va[4 * j + 3] = v.w;
+  }
+#pragma unroll
+  for (int j = 0; j < K / 4; ++j) {
+    const blp::U4a v = q2[j];
+    st.vb[4 * j] = v.x;
+    st.vb[4 * j + 1] = v.y;
+    st.vb[4 * j + 2] = v.z;
+    st.vb[4 * j + 3] = v.w;
+  }
+  st.limb = st.s2 >= 0 ? n2 - f0 : 0;
+  st.lim = valid ? min(T - f0, K) : 0;
+  if (st.s2 >= 0 && st.limb < st.lim) {  // a third row: rows shorter than K only
+    int t = st.s2;
+    for (int f = f0 + st.limb; f < f0 + st.lim; ++f) {
+      while (s_off[t + 1] <= f) ++t;
+      rare(ci[s_start[t] + (f - s_off[t])], t);
+    }
+  }
+}
+
+// Build: set the bits of every element of the ns segments inside [c0, c0 + width).
+template <int NT, int K>
+__device__ inline void pp_build(const int32_t* __restrict__ ci, uint32_t idmask, const int64_t* s_start,
+                                const int32_t* s_off, int ns, int64_t c0, int64_t width, uint32_t* bm, int tid,
+                                const int32_t* hint, int shift) {
+  const int T = s_off[ns];
+  constexpr int STEP = NT * K;
+  const uint32_t keep = idmask | 0x80000000u, c0u = (uint32_t)c0, wu = (uint32_t)width;
+  auto mark = [&](int v) {
+    const uint32_t r = in_chunk(v, keep, c0u);
+    if (r < wu) atomicOr(&bm[r >> 5], 1u << (r & 31));
+  };
+  auto rare = [&](int v, int) { mark(v); };
+  auto proc = [&](const PPStep<K>& st) {
+    st.land();
+#pragma unroll
+    for (int k = 0; k < K; ++k) mark(st.id(k));
+  };
+  // no exit from the middle of the body: a path leaving with B in flight would merge into the
+  // loop header's pending-load state (the waits of the next loop would stall on live loads)
+  const int nsteps = (T + STEP - 1) / STEP;
+  PPStep<K> A, B;
+  vm_drain();  // nothing older than A may look pending at the loop header
+  pp_fetch<K>(ci, s_start, s_off, ns, T, tid * K, hint, shift, A, rare);
+  for (int i = 0; i + 1 < nsteps; i += 2) {
+    pp_fetch<K>(ci, s_start, s_off, ns, T, (i + 1) * STEP + tid * K, hint, shift, B, rare);
+    proc(A);
+    pp_fetch<K>(ci, s_start, s_off, ns, T, (i + 2) * STEP + tid * K, hint, shift, A, rare);  // may be past T
+    proc(B);
+  }
+  if (nsteps & 1) proc(A);
+  vm_drain();
+}
+
+// Scan: test every element against the bitmap; hits accumulate per segment into s_cn / s_aa.
+// A step's elements lie in at most two segments (s1: k < rem1, s2: the rest), so a step ends
+// with at most two pairs of LDS atomics.
+template <int NT, int K, bool AA>
+__device__ inline void pp_scan(const int32_t* __restrict__ ci, uint32_t idmask, int idbits,
+                               const long long* __restrict__ aaw, const long long* wtab, const int64_t* s_start,
+                               const int32_t* s_off, int ns, int64_t c0, int64_t width, const uint32_t* bm,
+                               uint32_t* s_cn, unsigned long long* s_aa, int tid, const int32_t* hint, int shift) {
+  const int T = s_off[ns];
+  constexpr int STEP = NT * K;
+  const uint32_t keep = idmask | 0x80000000u, c0u = (uint32_t)c0, wu = (uint32_t)width;
+  auto rare = [&](int v, int seg) {
+    const uint32_t r = in_chunk(v, keep, c0u);
+    if (r < wu && ((bm[r >> 5] >> (r & 31)) & 1u)) {
+      atomicAdd(&s_cn[seg], 1u);
+      if (AA) {
+        const uint32_t code = ((uint32_t)v >> idbits) & 255u;
+        atomicAdd(&s_aa[seg], (unsigned long long)(code ? wtab[code] : aaw[v & idmask]));
+      }
+    }
+  };
+  auto proc = [&](const PPStep<K>& st) {
+    st.land();
+    int w[K];
+    bool hit[K];
+    long long wt[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      w[k] = st.id(k);
+      const uint32_t r = in_chunk(w[k], keep, c0u);
+      const bool in = r < wu;
+      const uint32_t word = bm[(in ? r : 0u) >> 5];
+      if (AA) wt[k] = wtab[((uint32_t)w[k] >> idbits) & 255u];
+      hit[k] = in && ((word >> (r & 31)) & 1u);
+    }
+    if (AA) {
+      bool any_esc = false;
+#pragma unroll
+      for (int k = 0; k < K; ++k) any_esc |= hit[k] && ((uint32_t)w[k] >> idbits) == 0u;
+      if (any_esc) {  // code-0 ids: gather the per-node weight (rare on a coded id stream)
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+          if (hit[k] && ((uint32_t)w[k] >> idbits) == 0u) wt[k] = aaw[w[k] & idmask];
+      }
+    }
+    unsigned c1 = 0, c2 = 0;
+    unsigned long long x1 = 0, x2 = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const unsigned h = hit[k] ? 1u : 0u;
+      const unsigned long long v = (AA && hit[k]) ? (unsigned long long)wt[k] : 0ull;
+      if (k < st.rem1) {
+        c1 += h;
+        x1 += v;
+      } else {
+        c2 += h;
+        x2 += v;
+      }
+    }
+    if (c1) {
+      atomicAdd(&s_cn[st.s1], c1);
+      if (AA) atomicAdd(&s_aa[st.s1], x1);
+    }
+    if (c2) {
+      atomicAdd(&s_cn[st.s2], c2);
+      if (AA) atomicAdd(&s_aa[st.s2], x2);
+    }
+  };
+  // no exit from the middle of the body: a path leaving with B in flight would merge into the
+  // loop header's pending-load state (the waits of the next loop would stall on live loads)
+  const int nsteps = (T + STEP - 1) / STEP;
+  PPStep<K> A, B;
+  vm_drain();  // nothing older than A may look pending at the loop header
+  pp_fetch<K>(ci, s_start, s_off, ns, T, tid * K, hint, shift, A, rare);
+  for (int i = 0; i + 1 < nsteps; i += 2) {
+    pp_fetch<K>(ci, s_start, s_off, ns, T, (i + 1) * STEP + tid * K, hint, shift, B, rare);
+    proc(A);
+    pp_fetch<K>(ci, s_start, s_off, ns, T, (i + 2) * STEP + tid * K, hint, shift, A, rare);  // may be past T
+    proc(B);
+  }
+  if (nsteps & 1) proc(A);
+  vm_drain();
+}
+
+// ------------------------------------------------------------------ row-chunk loops
+// The merge-path step of pp_* may straddle rows, which costs every element a three-way select
+// (own row / next row / past the end) and every step two segment atomics. Measured on the
+// config-2 user side, the scorer is VALU-issue bound (25 % of wave cycles issuing with 4 waves
+// per SIMD; ~28 VALU instructions per scanned element), so here the unit of work is a row
+// CHUNK instead: row s of length L is cut into ceil(L / K) chunks of K ids, the chunks of a
+// batch are numbered through (s_coff: exclusive chunk prefix per row), and a lane-step takes
+// one chunk. Its K ids come from one row (K/4 16-byte loads; the last chunk of a row reads up
+// to K-1 ids past it, masked by the count), so a step has one segment, one pair of atomics,
+// and an element costs ~9 VALU (CN) + ~7 (AA). Padding: one short row wastes K - L lanes.
+// Same two-buffer pipeline and vmcnt discipline as pp_*.
+template <int K>
+struct RCStep {
+  int v[K];
+  int s, cnt;  // row (segment) and valid ids of the chunk (0: none)
+  __device__ inline void land() const {
+#pragma unroll
+    for (int k = 0; k < K; ++k) asm volatile("" ::"v"(v[k]));
+  }
+};
+
+template <int K>
+__device__ inline void rc_fetch(const int32_t* __restrict__ ci, const int64_t* s_start, const int32_t* s_off,
+                                const int32_t* s_coff, int ns, int TC, int c, const int32_t* hint, int shift,
+                                RCStep<K>& st) {
+  int64_t pos = 0;
+  st.s = 0;
+  st.cnt = 0;
+  if (c < TC) {
+    int s;
+    if (shift >= 0) {
+      const int g = c >> shift;
+      s = seg_search(s_coff, ns, c, hint[g], hint[g + 1] + 1);
+    } else {
+      s = seg_search(s_coff, ns, c);
+    }
+    const int o = (c - s_coff[s]) * K;
+    st.s = s;
+    st.cnt = min(K, s_off[s + 1] - s_off[s] - o);
+    pos = s_start[s] + o;
+  }
+  const blp::U4a* q = reinterpret_cast<const blp::U4a*>(ci + pos);
+#pragma unroll
+  for (int j = 0; j < K / 4; ++j) {
+    const blp::U4a x = q[j];
+    st.v[4 * j] = x.x;
+    st.v[4 * j + 1] = x.y;
+    st.v[4 * j + 2] = x.z;
+    st.v[4 * j + 3] = x.w;
+  }
+}
+
+// Two-buffer driver: steps of NT chunks; proc(step) after the next step's loads are issued.
+template <int NT, int K, typename Proc>
+__device__ inline void rc_loop(const int32_t* __restrict__ ci, const int64_t* s_start, const int32_t* s_off,
+                               const int32_t* s_coff, int ns, int tid, const int32_t* hint, int shift, Proc proc) {
+  const int TC = s_coff[ns];
+  const int nsteps = (TC + NT - 1) / NT;
+  RCStep<K> A, B;
+  vm_drain();
+  rc_fetch<K>(ci, s_start, s_off, s_coff, ns, TC, tid, hint, shift, A);
+  for (int i = 0; i + 1 < nsteps; i += 2) {
+    rc_fetch<K>(ci, s_start, s_off, s_coff, ns, TC, (i + 1) * NT + tid, hint, shift, B);
+    proc(A);
+    rc_fetch<K>(ci, s_start, s_off, s_coff, ns, TC, (i + 2) * NT + tid, hint, shift, A);  // may be past TC
+    proc(B);
+  }
+  if (nsteps & 1) proc(A);
+  vm_drain();
+}
+
+// LDS bitmap layout for the row-chunk loops: CAP words of bits, then RC_SAFE: one word that
+// stays zero (scan lookups of out-of-chunk ids are clamped to it), then 32 per-lane dummy
+// words that absorb the build's ORs of out-of-chunk / padding ids without a branch.
+constexpr int RC_EXTRA_WORDS = 36;
+
+template <int NT, int K>
+__device__ inline void rc_build(const int32_t* __restrict__ ci, uint32_t idmask, const int64_t* s_start,
+                                const int32_t* s_off, const int32_t* s_coff, int ns, int64_t c0, int64_t width,
+                                uint32_t* bm, int cap_words, int tid, const int32_t* hint, int shift) {
+  const uint32_t keep = idmask | 0x80000000u, c0u = (uint32_t)c0, wu = (uint32_t)width;
+  const uint32_t dummy = (uint32_t)(cap_words + 1 + (tid & 31)) << 5;
+  auto proc = [&](const RCStep<K>& st) {
+    st.land();
+#pragma unroll
+    for (int k = 0; k < K; ++k) {  // branch-free: '&' not '&&' (no exec-mask blocks per id)
+      const uint32_t r = ((uint32_t)st.v[k] & keep) - c0u;
+      const uint32_t rr = ((k < st.cnt) & (r < wu)) ? r : dummy;
+      atomicOr(&bm[rr >> 5], 1u << (rr & 31));
+    }
+  };
+  rc_loop<NT, K>(ci, s_start, s_off, s_coff, ns, tid, hint, shift, proc);
+}
+
+template <int NT, int K, bool AA>
+__device__ inline void rc_scan(const int32_t* __restrict__ ci, uint32_t idmask, int idbits,
+                               const long long* __restrict__ aaw, const long long* wtab, const int64_t* s_start,
+                               const int32_t* s_off, const int32_t* s_coff, int ns, int64_t c0, int64_t width,
+                               const uint32_t* bm, int cap_words, uint32_t* s_cn, unsigned long long* s_aa, int tid,
+                               const int32_t* hint, int shift) {
+  const uint32_t keep = idmask | 0x80000000u, c0u = (uint32_t)c0, wu = (uint32_t)width;
+  const uint32_t safe = (uint32_t)cap_words << 5;
+  // Branch-free phases, so the scheduler can issue all K bitmap reads (and weight reads)
+  // before the first use: one LDS round trip per step instead of one per id.
+  auto proc = [&](const RCStep<K>& st) {
+    st.land();
+    uint32_t rr[K], wd[K];
+    long long wt[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const uint32_t r = ((uint32_t)st.v[k] & keep) - c0u;
+      rr[k] = ((k < st.cnt) & (r < wu)) ? r : safe;
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) wd[k] = bm[rr[k] >> 5];
+    if (AA) {
+#pragma unroll
+      for (int k = 0; k < K; ++k) wt[k] = wtab[((uint32_t)st.v[k] >> idbits) & 255u];
+    }
+    uint32_t hm = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) hm |= ((wd[k] >> (rr[k] & 31)) & 1u) << k;
+    if (hm) {
+      if (AA) {
+        unsigned long long acc = 0;
+        uint32_t esc = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          const bool h = (hm >> k) & 1u;
+          acc += h ? (unsigned long long)wt[k] : 0ull;
+          esc |= (h & ((((uint32_t)st.v[k] >> idbits) & 255u) == 0u)) ? 1u << k : 0u;
+        }
+        if (esc) {  // code-0 ids: the per-node weight (rare on a coded id stream)
+#pragma unroll
+          for (int k = 0; k < K; ++k)
+            if ((esc >> k) & 1u) acc += (unsigned long long)aaw[st.v[k] & idmask];
+        }
+        atomicAdd(&s_aa[st.s], acc);
+      }
+      atomicAdd(&s_cn[st.s], (unsigned)__popc(hm));
+    }
+  };
+  rc_loop<NT, K>(ci, s_start, s_off, s_coff, ns, tid, hint, shift, proc);
+}
+
+// Chunk prefix of a batch whose element offsets s_off[0..ns] are in LDS: s_coff[t] = sum of
+// ceil(len / K) over rows < t; s_coff[ns] = total. Ends with a barrier.
+template <int BLOCK, int K>
+__device__ inline void rc_chunk_offsets(const int32_t* s_off, int ns, int32_t* s_coff, int* red) {
+  const int nc = (int)threadIdx.x < ns ? (s_off[threadIdx.x + 1] - s_off[threadIdx.x] + K - 1) / K : 0;
+  int tot;
+  const int ex = block_exscan<BLOCK>(nc, red, &tot);
+  if ((int)threadIdx.x < ns) s_coff[threadIdx.x] = ex;
+  if (threadIdx.x == 0) s_coff[ns] = tot;
+  __syncthreads();
+}
+
 // Short rows (every row of the batch at most SHORT_MAX ids -- the business side, whose rows
 // are user rows Γ(w)): one thread per segment reads its whole row with up to SHORT_MAX / 4
 // 16-byte loads, all issued before any is used. No merge-path search and no row crossings,
@@ -673,7 +1050,10 @@ template <int BLOCK, int CAP_WORDS, int SEG, int K>
 __global__ __launch_bounds__(BLOCK) void k_score(ScoreArgs a) {
   static_assert(SEG <= BLOCK, "one pair segment per thread in the output loop");
   constexpr int NW = BLOCK / 64;
-  __shared__ uint32_t bm[CAP_WORDS];
+  // row-chunk loops (rc_*) for the large-universe variant; the others keep the merge-path loops
+  constexpr bool RC = BLP_RC && CAP_WORDS >= 34816;
+  __shared__ uint32_t bm[CAP_WORDS + (RC ? RC_EXTRA_WORDS : 0)];
+  __shared__ int32_t s_coff[RC ? SEG + 1 : 1];
   __shared__ int64_t s_start[SEG];
   __shared__ int32_t s_off[SEG + 1];
   __shared__ uint32_t s_cn[SEG];
@@ -685,11 +1065,13 @@ __global__ __launch_bounds__(BLOCK) void k_score(ScoreArgs a) {
   __shared__ blp::HotRow s_hot[HOT_LIST];
   __shared__ long long s_wtab[256];
   // hint table where the LDS allows it (the 64 KiB-bitmap variant keeps 2 workgroups per CU)
-  constexpr int HC = CAP_WORDS >= 34816 ? 2048 : CAP_WORDS >= 16384 ? 1 : 512;
+  constexpr int HC = CAP_WORDS >= 34816 ? (RC ? 1536 : 2048) : CAP_WORDS >= 16384 ? 1 : 512;
   __shared__ int32_t s_hint[HC];
 
   if (a.wtab)  // visible after the first barrier
     for (int i = threadIdx.x; i < 256; i += BLOCK) s_wtab[i] = a.wtab[i];
+  if (RC)  // the zero word and the build's dummy words past the bitmap
+    for (int i = threadIdx.x; i < RC_EXTRA_WORDS; i += BLOCK) bm[CAP_WORDS + i] = 0;
   const int64_t CAP_BITS = a.cap_bits;
   const int64_t span = a.hi - a.lo;
   const int nchunks = span <= CAP_BITS ? 1 : (int)((span + CAP_BITS - 1) / CAP_BITS);
@@ -771,9 +1153,18 @@ __global__ __launch_bounds__(BLOCK) void k_score(ScoreArgs a) {
             load_row_segments<BLOCK>(a.rp, a.ci, k0, ns, s_start, s_off, red, nhot ? a.hot_idx : nullptr);
             if (a.short_rows & 1) {
               row_build<BLOCK>(a.cw, a.idmask, s_start, s_off, ns, c0, width, bm, threadIdx.x);
+            } else if (RC) {
+              rc_chunk_offsets<BLOCK, K>(s_off, ns, s_coff, red);
+              const int shift = build_hint<BLOCK, HC>(s_coff, ns, BLOCK, s_hint);
+              rc_build<BLOCK, K>(a.cw, a.idmask, s_start, s_off, s_coff, ns, c0, width, bm, CAP_WORDS, threadIdx.x,
+                                 s_hint, shift);
             } else {
               const int shift = build_hint<BLOCK, HC>(s_off, ns, BLOCK * K, s_hint);
+#if BLP_PP
+              pp_build<BLOCK, K>(a.cw, a.idmask, s_start, s_off, ns, c0, width, bm, threadIdx.x, s_hint, shift);
+#else
               mp_build<BLOCK, K>(a.cw, a.idmask, s_start, s_off, ns, c0, width, bm, threadIdx.x, s_hint, shift);
+#endif
             }
             __syncthreads();
           }
@@ -824,14 +1215,32 @@ __global__ __launch_bounds__(BLOCK) void k_score(ScoreArgs a) {
             else
               row_scan<BLOCK, false>(a.cw, a.idmask, a.idbits, a.aaw, s_wtab, s_start, s_off, ns, c0, width, bm, s_cn,
                                      s_aa, threadIdx.x);
+          } else if (RC) {
+            rc_chunk_offsets<BLOCK, K>(s_off, ns, s_coff, red);
+            const int shift = build_hint<BLOCK, HC>(s_coff, ns, BLOCK, s_hint);
+            if (want_a)
+              rc_scan<BLOCK, K, true>(a.cw, a.idmask, a.idbits, a.aaw, s_wtab, s_start, s_off, s_coff, ns, c0, width,
+                                      bm, CAP_WORDS, s_cn, s_aa, threadIdx.x, s_hint, shift);
+            else
+              rc_scan<BLOCK, K, false>(a.cw, a.idmask, a.idbits, a.aaw, s_wtab, s_start, s_off, s_coff, ns, c0, width,
+                                       bm, CAP_WORDS, s_cn, s_aa, threadIdx.x, s_hint, shift);
           } else {
             const int shift = build_hint<BLOCK, HC>(s_off, ns, BLOCK * K, s_hint);
+#if BLP_PP
+            if (want_a)
+              pp_scan<BLOCK, K, true>(a.cw, a.idmask, a.idbits, a.aaw, s_wtab, s_start, s_off, ns, c0, width, bm, s_cn,
+                                      s_aa, threadIdx.x, s_hint, shift);
+            else
+              pp_scan<BLOCK, K, false>(a.cw, a.idmask, a.idbits, a.aaw, s_wtab, s_start, s_off, ns, c0, width, bm,
+                                       s_cn, s_aa, threadIdx.x, s_hint, shift);
+#else
             if (want_a)
               mp_scan<BLOCK, K, true>(a.cw, a.idmask, a.idbits, a.aaw, s_wtab, s_start, s_off, ns, c0, width, bm, s_cn,
                                       s_aa, threadIdx.x, s_hint, shift);
             else
               mp_scan<BLOCK, K, false>(a.cw, a.idmask, a.idbits, a.aaw, s_wtab, s_start, s_off, ns, c0, width, bm,
                                        s_cn, s_aa, threadIdx.x, s_hint, shift);
+#endif
           }
           __syncthreads();
           PROF(7)

@@ -95,7 +95,13 @@ def test_general_graph_exact_distance(gpu):
     {"BLP_WAVE": "1"},                                  # wave-per-source scorer (opt-in)
     {"BLP_WAVE": "1", "BLP_HEAVY_WORK": "50", "BLP_HOT_MIN": "8"},
     {"BLP_VARIANT": "1"},                               # 64 KiB-bitmap scorer (no hint table)
-    {"BLP_VARIANT": "2"},                               # 136 KiB-bitmap scorer
+    {"BLP_VARIANT": "2"},                               # 136 KiB-bitmap scorer (row-chunk loops)
+    {"BLP_VARIANT": "2", "BLP_NO_SHORT": "1"},          # ... short rows through the row-chunk loops
+    {"BLP_VARIANT": "2", "BLP_KPT": "4"},               # ... 4-id chunks
+    {"BLP_VARIANT": "2", "BLP_KPT": "16"},              # ... 16-id chunks
+    {"BLP_VARIANT": "2", "BLP_WCODES": "3"},            # ... coded and gathered weights mixed
+    {"BLP_VARIANT": "2", "BLP_HOT_MIN": "8"},           # ... dense rows skipped: empty build rows
+    {"BLP_VARIANT": "2", "BLP_CHUNK_BITS": "1024", "BLP_NO_GLOBAL": "1"},  # ... several LDS chunks
     {"BLP_WCODES": "0"},                                # every AA weight gathered per node
     {"BLP_WCODES": "3"},                                # coded and gathered weights mixed
     {"BLP_NO_WCODES": "1"},                             # scorers on the plain id stream
