@@ -1132,19 +1132,51 @@ __global__ __launch_bounds__(BLOCK) void k_score(ScoreArgs a) {
           __syncthreads();
           const int nhot = s_nhot <= HOT_LIST ? s_nhot : 0;  // overflow: every row goes sparse
           const int64_t q0 = c0 >> 7;
-          for (int q = threadIdx.x; q < nw4; q += BLOCK) {
-            uint4 v = make_uint4(0, 0, 0, 0);
+          if (RC) {
+            // every thread owns QPT vectors of the bitmap and ORs each dense row into registers:
+            // a row's QPT loads are all in flight at once (one L2 round trip per row, not per
+            // vector). Large variant only: the extra registers would cost the small variants a
+            // wave per SIMD.
+            constexpr int QPT = (CAP_WORDS / 4 + BLOCK - 1) / BLOCK;
+            uint4 acc[QPT];
+#pragma unroll
+            for (int j = 0; j < QPT; ++j) acc[j] = make_uint4(0, 0, 0, 0);
             for (int r = 0; r < nhot; ++r) {
-              const int64_t qq = q0 + q - s_hot[r].vlo;
-              if (qq >= 0 && qq < s_hot[r].nvec) {
-                const uint4 p = a.hot_pool[s_hot[r].vec_off + qq];
-                v.x |= p.x;
-                v.y |= p.y;
-                v.z |= p.z;
-                v.w |= p.w;
+              const blp::HotRow h = s_hot[r];
+              const uint4* row = a.hot_pool + h.vec_off;
+#pragma unroll
+              for (int j = 0; j < QPT; ++j) {
+                const int q = threadIdx.x + j * BLOCK;
+                const int64_t qq = q0 + q - h.vlo;
+                if (q < nw4 && qq >= 0 && qq < h.nvec) {
+                  const uint4 p = row[qq];
+                  acc[j].x |= p.x;
+                  acc[j].y |= p.y;
+                  acc[j].z |= p.z;
+                  acc[j].w |= p.w;
+                }
               }
             }
-            bm4[q] = v;
+#pragma unroll
+            for (int j = 0; j < QPT; ++j) {
+              const int q = threadIdx.x + j * BLOCK;
+              if (q < nw4) bm4[q] = acc[j];
+            }
+          } else {
+            for (int q = threadIdx.x; q < nw4; q += BLOCK) {
+              uint4 v = make_uint4(0, 0, 0, 0);
+              for (int r = 0; r < nhot; ++r) {
+                const int64_t qq = q0 + q - s_hot[r].vlo;
+                if (qq >= 0 && qq < s_hot[r].nvec) {
+                  const uint4 p = a.hot_pool[s_hot[r].vec_off + qq];
+                  v.x |= p.x;
+                  v.y |= p.y;
+                  v.z |= p.z;
+                  v.w |= p.w;
+                }
+              }
+              bm4[q] = v;
+            }
           }
           __syncthreads();
           PROF(2)
