@@ -220,6 +220,73 @@ __global__ __launch_bounds__(GB_BLOCK) void k_bucket_group(const int64_t* __rest
   }
 }
 
+// ---- grouping of a pair list that arrives already grouped by source (x non-decreasing, as
+// similarity.users walks examples.json: every user's businesses together, similarity.py:
+// 30-32): the runs of equal x ARE the groups, so instead of the bucket sort one pass finds
+// the run heads (tile counts -> scan -> writes) and the grouped order is the caller's own.
+__device__ inline bool run_head(const int32_t* __restrict__ x, int64_t i) { return i == 0 || x[i] != x[i - 1]; }
+
+__global__ __launch_bounds__(SCAN_BLOCK) void k_run_count(const int32_t* __restrict__ x, int64_t np,
+                                                          int32_t* __restrict__ tile_cnt) {
+  __shared__ int red[SCAN_BLOCK / 64];
+  const int64_t base = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)threadIdx.x * SCAN_ITEMS;
+  int v = 0;
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; ++k) v += (base + k < np && run_head(x, base + k)) ? 1 : 0;
+  int tot;
+  block_exscan_i<SCAN_BLOCK>(v, red, &tot);
+  if (threadIdx.x == 0) tile_cnt[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(SCAN_BLOCK) void k_run_write(const int32_t* __restrict__ x, const int32_t* __restrict__ y,
+                                                          int64_t np, const int64_t* __restrict__ rp,
+                                                          const int32_t* __restrict__ tile_off, int32_t* __restrict__ active,
+                                                          int32_t* __restrict__ off, int32_t* __restrict__ g_out,
+                                                          int64_t* __restrict__ g_yb, int32_t* __restrict__ g_yl,
+                                                          int32_t* __restrict__ g_y) {
+  __shared__ int red[SCAN_BLOCK / 64];
+  const int64_t t0 = (int64_t)blockIdx.x * SCAN_TILE;
+  for (int j = threadIdx.x; j < SCAN_TILE; j += SCAN_BLOCK) {  // per-pair metadata, coalesced
+    const int64_t i = t0 + j;
+    if (i < np) {
+      const int yi = y[i];
+      const int64_t st = rp[yi];
+      g_out[i] = (int32_t)i;
+      g_yb[i] = st;
+      g_yl[i] = (int32_t)(rp[yi + 1] - st);
+      if (g_y) g_y[i] = yi;
+    }
+  }
+  const int64_t base = t0 + (int64_t)threadIdx.x * SCAN_ITEMS;
+  bool h[SCAN_ITEMS];
+  int v = 0;
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; ++k) {
+    h[k] = base + k < np && run_head(x, base + k);
+    v += h[k] ? 1 : 0;
+  }
+  int tot;
+  int o = block_exscan_i<SCAN_BLOCK>(v, red, &tot) + tile_off[blockIdx.x];
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; ++k)
+    if (h[k]) {
+      const int xi = x[base + k];
+      active[o++] = xi;
+      off[xi] = (int32_t)(base + k);
+    }
+}
+
+// cnt of every run from the next run's head (after k_run_write: off[] of all heads)
+__global__ void k_run_cnt(const int32_t* __restrict__ active, const int32_t* __restrict__ n_active, int64_t np,
+                          const int32_t* __restrict__ off, int32_t* __restrict__ cnt) {
+  const int na = *n_active;
+  for (int a = blockIdx.x * blockDim.x + threadIdx.x; a < na; a += gridDim.x * blockDim.x) {
+    const int xa = active[a];
+    const int nxt = a + 1 < na ? off[active[a + 1]] : (int)np;
+    cnt[xa] = nxt - off[xa];
+  }
+}
+
 template <int KEYS>
 __global__ __launch_bounds__(GB_BLOCK) void k_active_write(const int32_t* __restrict__ cnt,
                                                            const int32_t* __restrict__ abase, int shift, int32_t xlo,
@@ -740,7 +807,11 @@ __device__ inline void rc_fetch(const int32_t* __restrict__ ci, const int64_t* s
   const blp::U4a* q = reinterpret_cast<const blp::U4a*>(ci + pos);
 #pragma unroll
   for (int j = 0; j < K / 4; ++j) {
+#ifdef BLP_EXP_NOLOAD  // timing experiment only: no global loads, fake ids
+    const blp::U4a x{(int)pos + 4 * j, (int)pos + 4 * j + 1, (int)pos + 4 * j + 2, (int)pos + 4 * j + 3};
+#else
     const blp::U4a x = q[j];
+#endif
     st.v[4 * j] = x.x;
     st.v[4 * j + 1] = x.y;
     st.v[4 * j + 2] = x.z;
@@ -802,6 +873,15 @@ __device__ inline void rc_scan(const int32_t* __restrict__ ci, uint32_t idmask, 
   // before the first use: one LDS round trip per step instead of one per id.
   auto proc = [&](const RCStep<K>& st) {
     st.land();
+#ifdef BLP_EXP_NOPROC  // timing experiment only: consume the ids without the bitmap work
+    {
+      uint32_t x = 0;
+#pragma unroll
+      for (int k = 0; k < K; ++k) x += (uint32_t)st.v[k];
+      if (x == 0x12345u) atomicAdd(&s_cn[st.s], 1u);
+      return;
+    }
+#endif
     uint32_t rr[K], wd[K];
     long long wt[K];
 #pragma unroll
@@ -1823,6 +1903,7 @@ struct blp_batch {
   int64_t per_blk = 1;
   int64_t cap_bits = 0;
   int64_t n_sources = 0;
+  bool runs = false;  // pairs arrive grouped by source (x non-decreasing): run-head grouping
   blp::KernelTimer t_score, t_group;
 };
 
@@ -1894,11 +1975,13 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   std::vector<int64_t> work;
   int64_t scan_work = 0, max_scan_row = 0, max_build_row = 0;
   bool any_hot = false;
+  bool runs = !getenv("BLP_NO_RUNS");  // x non-decreasing: grouped by run heads (BLP_NO_RUNS: bucket sort)
   int64_t rows_lo = INT64_MAX, rows_hi = INT64_MIN;  // nodes whose rows are read (the y and the z in N(x))
   const int32_t* hot = g->h_hot_idx.empty() ? nullptr : g->h_hot_idx.data();
   for (int64_t i = 0; i < n_pairs; ++i) {
     const int32_t xi = x[i], yi = y[i];
     if (xi < 0 || xi >= n || yi < 0 || yi >= n) return fail(BLP_E_ARG, "blp_batch_create: node id out of range");
+    runs = runs && (i == 0 || x[i - 1] <= xi);
     if (rp[yi + 1] > rp[yi]) {
       lo = std::min<int64_t>(lo, ci[rp[yi]]);
       hi = std::max<int64_t>(hi, (int64_t)ci[rp[yi + 1] - 1] + 1);
@@ -1931,6 +2014,7 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   blp_batch* b = new blp_batch();
   b->g = g;
   b->n_pairs = n_pairs;
+  b->runs = runs;
   b->lo = lo;
   b->hi = hi;
   b->n_sources = (int64_t)srcs.size();
@@ -2162,7 +2246,17 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   if ((rc = timer_begin(g, K_GROUP, &t0))) return rc;
   if ((rc = timer_begin(b->t_group, g->stream, &bt0))) return rc;
   BLP_HIP(hipMemsetAsync(b->d_misc, 0, sizeof(Misc), g->stream));
-  if (np) {
+  if (np && b->runs) {
+    const int64_t tiles = (np + SCAN_TILE - 1) / SCAN_TILE;
+    int32_t* rtile = reinterpret_cast<int32_t*>(tmp);  // the bucket sort's pair buffer is free here
+    hipLaunchKernelGGL(k_run_count, dim3((unsigned)tiles), dim3(SCAN_BLOCK), 0, g->stream, b->d_x, np, rtile);
+    hipLaunchKernelGGL(k_scan_mid, dim3(1), dim3(SCAN_BLOCK), 0, g->stream, rtile, tiles, &b->d_misc->n_active);
+    hipLaunchKernelGGL(k_run_write, dim3((unsigned)tiles), dim3(SCAN_BLOCK), 0, g->stream, b->d_x, b->d_y, np, g->d_rp,
+                       rtile, g->active.as<int32_t>(), g->off.as<int32_t>(), b->d_gout, b->d_gyb, b->d_gyl,
+                       b->d_gy);
+    hipLaunchKernelGGL(k_run_cnt, dim3(1024), dim3(256), 0, g->stream, g->active.as<int32_t>(), &b->d_misc->n_active,
+                       np, g->off.as<int32_t>(), g->cnt.as<int32_t>());
+  } else if (np) {
     hipLaunchKernelGGL(k_bucket_hist, dim3(b->nblk), dim3(GP_BLOCK), 0, g->stream, b->d_x, np, b->xlo, b->shift, b->nb,
                        b->nblk, b->per_blk, hist);
     hipLaunchKernelGGL(k_scan_sum, dim3((unsigned)tiles_h), dim3(SCAN_BLOCK), 0, g->stream, hist, nh, tiles);

@@ -42,6 +42,13 @@ def _check_against_oracle(ga, gb, x, y, mask=7):
     if mask & blp.ADAMIC:
         np.testing.assert_allclose(got["adamic"], aa, rtol=1e-9, atol=0)
         assert np.array_equal(got["adamic"] == 0, aa == 0)
+    # the same pairs grouped by source (x non-decreasing): the run-head grouping path; the
+    # fixed-point sums make every score independent of pair order, so results are identical
+    order = np.argsort(x, kind="stable")
+    got_sorted = G.score_pairs(x[order], y[order], mask)
+    for k, v in got.items():
+        if v is not None:
+            np.testing.assert_array_equal(got_sorted[k], v[order])
     return G
 
 
@@ -144,6 +151,20 @@ def test_many_pairs_per_source_vs_oracle(gpu, variant, monkeypatch):
     y = rng.integers(nu, G.n, len(x)).astype(np.int32)
     _check_against_oracle(a, b, x, y)
     _check_against_oracle(a, b, y, x)   # popular businesses: N(x) has thousands of rows
+
+
+def test_single_run_and_tile_edges(gpu):
+    # grouped input: one source for every pair, and run heads on scan-tile boundaries
+    rng = np.random.default_rng(14)
+    a, b = bipartite_edges(rng, 20000, 1500, 200000)
+    G = blp.DeviceGraph(a, b)
+    nu = G.n - len(np.unique(b))
+    y = rng.integers(nu, G.n, 5000).astype(np.int32)
+    _check_against_oracle(a, b, np.full(len(y), rng.integers(0, nu), np.int32), y)
+    x = np.sort(rng.choice(nu, 4096 * 3 + 7, replace=True)).astype(np.int32)
+    x[4095:4097] = x[4094] + np.array([0, 1])  # heads at and around a tile boundary
+    x = np.maximum.accumulate(x)
+    _check_against_oracle(a, b, x, rng.integers(nu, G.n, len(x)).astype(np.int32))
 
 
 def test_unsorted_pair_order_vs_oracle(gpu):
