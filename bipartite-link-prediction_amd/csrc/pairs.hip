@@ -287,6 +287,8 @@ __global__ void k_run_cnt(const int32_t* __restrict__ active, const int32_t* __r
   }
 }
 
+constexpr int DQ_MAX = 8;  // sources per dequeue (blp_batch::dq)
+
 template <int KEYS>
 __global__ __launch_bounds__(GB_BLOCK) void k_active_write(const int32_t* __restrict__ cnt,
                                                            const int32_t* __restrict__ abase, int shift, int32_t xlo,
@@ -2085,7 +2087,7 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   // unless there are very many light sources per worker
   // (two once a worker has ~64+ sources: the business side of config 2, 1.44 -> 1.30 ms)
   b->dq = b->n_sources >= n_wg * 64 ? (int)std::max<int64_t>(2, std::min<int64_t>(8, b->n_sources / (n_wg * 64))) : 1;
-  if (const char* e = getenv("BLP_DQ")) b->dq = std::max(1, atoi(e));  // tuning knob
+  if (const char* e = getenv("BLP_DQ")) b->dq = std::min(DQ_MAX, std::max(1, atoi(e)));  // tuning knob
   // ---- heavy sources: build work far above the per-workgroup share goes to k_heavy
   const int64_t total_work = std::accumulate(work.begin(), work.end(), (int64_t)0) + scan_work;
   // a wave is ~16x slower on one source than a 1024-thread block: split much earlier there
