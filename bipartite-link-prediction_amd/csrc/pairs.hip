@@ -144,7 +144,18 @@ __global__ __launch_bounds__(GP_BLOCK) void k_bucket_hist(const int32_t* __restr
   for (int i = threadIdx.x; i < nb; i += GP_BLOCK) h[i] = 0;
   __syncthreads();
   const int64_t b0 = (int64_t)blockIdx.x * per_blk, b1 = min(np, b0 + per_blk);
-  for (int64_t i = b0 + threadIdx.x; i < b1; i += GP_BLOCK) atomicAdd(&h[(x[i] - xlo) >> shift], 1);
+  constexpr int U = 4;
+  for (int64_t r = b0; r < b1; r += U * GP_BLOCK) {
+    int xv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = r + u * GP_BLOCK + threadIdx.x;
+      xv[u] = i < b1 ? x[i] : INT32_MIN;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (xv[u] != INT32_MIN) atomicAdd(&h[(xv[u] - xlo) >> shift], 1);
+  }
   __syncthreads();
   for (int i = threadIdx.x; i < nb; i += GP_BLOCK) hist[(int64_t)i * nblk + blockIdx.x] = h[i];
 }
@@ -159,9 +170,21 @@ __global__ __launch_bounds__(GP_BLOCK) void k_bucket_scatter(const int32_t* __re
   for (int i = threadIdx.x; i < nb; i += GP_BLOCK) cur[i] = hoff[(int64_t)i * nblk + blockIdx.x];
   __syncthreads();
   const int64_t b0 = (int64_t)blockIdx.x * per_blk, b1 = min(np, b0 + per_blk);
-  for (int64_t i = b0 + threadIdx.x; i < b1; i += GP_BLOCK) {
-    const int xi = x[i];
-    tmp[atomicAdd(&cur[(xi - xlo) >> shift], 1)] = make_int4((int32_t)i, xi, y[i], 0);
+  constexpr int U = 4;  // U pairs per thread per round: loads and LDS atomics overlap
+  for (int64_t r = b0; r < b1; r += U * GP_BLOCK) {
+    int xv[U], yv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = r + u * GP_BLOCK + threadIdx.x;
+      xv[u] = i < b1 ? x[i] : INT32_MIN;
+      yv[u] = i < b1 ? y[i] : 0;
+    }
+    int pos[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) pos[u] = xv[u] != INT32_MIN ? atomicAdd(&cur[(xv[u] - xlo) >> shift], 1) : -1;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (pos[u] >= 0) tmp[pos[u]] = make_int4((int32_t)(r + u * GP_BLOCK + threadIdx.x), xv[u], yv[u], 0);
   }
 }
 
@@ -207,16 +230,32 @@ __global__ __launch_bounds__(GB_BLOCK) void k_bucket_group(const int64_t* __rest
   }
   if (threadIdx.x == 0) bucket_active[b] = acts;
   __syncthreads();
-  for (int k = bs + threadIdx.x; k < be; k += GB_BLOCK) {
-    const int4 t = tmp[k];
-    const int i = t.x;
-    const int pos = bs + atomicAdd(&h[t.y - k0], 1);
-    const int yi = t.z;
-    const int64_t st = rp[yi];
-    g_out[pos] = i;
-    g_yb[pos] = st;
-    g_yl[pos] = (int32_t)(rp[yi + 1] - st);
-    if (g_y) g_y[pos] = yi;
+  // U pairs per thread per round: their loads, gathers and LDS atomics overlap
+  constexpr int U = 4;
+  for (int k0r = bs; k0r < be; k0r += U * GB_BLOCK) {
+    int4 t[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = k0r + u * GB_BLOCK + threadIdx.x;
+      t[u] = k < be ? tmp[k] : make_int4(-1, 0, 0, 0);
+    }
+    int64_t st[U], en[U];
+    int pos[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      st[u] = rp[t[u].z];
+      en[u] = rp[t[u].z + 1];
+      pos[u] = t[u].x >= 0 ? bs + atomicAdd(&h[t[u].y - k0], 1) : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (t[u].x >= 0) {
+        g_out[pos[u]] = t[u].x;
+        g_yb[pos[u]] = st[u];
+        g_yl[pos[u]] = (int32_t)(en[u] - st[u]);
+        if (g_y) g_y[pos[u]] = t[u].z;
+      }
+    }
   }
 }
 
@@ -246,15 +285,28 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_run_write(const int32_t* __restr
                                                           int32_t* __restrict__ g_y) {
   __shared__ int red[SCAN_BLOCK / 64];
   const int64_t t0 = (int64_t)blockIdx.x * SCAN_TILE;
-  for (int j = threadIdx.x; j < SCAN_TILE; j += SCAN_BLOCK) {  // per-pair metadata, coalesced
-    const int64_t i = t0 + j;
+  // per-pair metadata, coalesced; the tile's y loads, then its row_ptr gathers, all in flight
+  constexpr int PT = SCAN_TILE / SCAN_BLOCK;
+  int yv[PT];
+#pragma unroll
+  for (int q = 0; q < PT; ++q) {
+    const int64_t i = t0 + q * SCAN_BLOCK + threadIdx.x;
+    yv[q] = i < np ? y[i] : 0;
+  }
+  int64_t st[PT], en[PT];
+#pragma unroll
+  for (int q = 0; q < PT; ++q) {
+    st[q] = rp[yv[q]];
+    en[q] = rp[yv[q] + 1];
+  }
+#pragma unroll
+  for (int q = 0; q < PT; ++q) {
+    const int64_t i = t0 + q * SCAN_BLOCK + threadIdx.x;
     if (i < np) {
-      const int yi = y[i];
-      const int64_t st = rp[yi];
       g_out[i] = (int32_t)i;
-      g_yb[i] = st;
-      g_yl[i] = (int32_t)(rp[yi + 1] - st);
-      if (g_y) g_y[i] = yi;
+      g_yb[i] = st[q];
+      g_yl[i] = (int32_t)(en[q] - st[q]);
+      if (g_y) g_y[i] = yv[q];
     }
   }
   const int64_t base = t0 + (int64_t)threadIdx.x * SCAN_ITEMS;
