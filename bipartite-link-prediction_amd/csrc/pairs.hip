@@ -31,6 +31,9 @@
 #ifndef BLP_RC
 #define BLP_RC 1  // row-chunk loops in the large-universe k_score (0: merge-path loops)
 #endif
+#ifndef BLP_SHORT_MINB
+#define BLP_SHORT_MINB 5  // short-row scorer: >= 5 workgroups of 256 per CU (<= 96 VGPRs)
+#endif
 #ifndef BLP_PP
 #define BLP_PP 1  // ping-pong merge-path loops in k_score (0: the single-buffer mp_build / mp_scan)
 #endif
@@ -1180,8 +1183,11 @@ __device__ unsigned long long g_prof[16];
 #define PROF_FLUSH
 #endif
 
-template <int BLOCK, int CAP_WORDS, int SEG, int K>
-__global__ __launch_bounds__(BLOCK) void k_score(ScoreArgs a) {
+// SHORT: every build and scan row of the batch has at most SHORT_MAX ids (the business side of
+// a review graph: user rows), so only the row-per-thread loops are compiled in -- fewer
+// registers and no hint table, hence more resident workgroups for these latency-bound sources.
+template <int BLOCK, int CAP_WORDS, int SEG, int K, bool SHORT = false>
+__global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(ScoreArgs a) {
   static_assert(SEG <= BLOCK, "one pair segment per thread in the output loop");
   constexpr int NW = BLOCK / 64;
   // row-chunk loops (rc_*) for the large-universe variant; the others keep the merge-path loops
@@ -1199,7 +1205,7 @@ __global__ __launch_bounds__(BLOCK) void k_score(ScoreArgs a) {
   __shared__ blp::HotRow s_hot[HOT_LIST];
   __shared__ long long s_wtab[256];
   // hint table where the LDS allows it (the 64 KiB-bitmap variant keeps 2 workgroups per CU)
-  constexpr int HC = CAP_WORDS >= 34816 ? (RC ? 1536 : 2048) : CAP_WORDS >= 16384 ? 1 : 512;
+  constexpr int HC = SHORT ? 1 : CAP_WORDS >= 34816 ? (RC ? 1536 : 2048) : CAP_WORDS >= 16384 ? 1 : 512;
   __shared__ int32_t s_hint[HC];
 
   if (a.wtab)  // visible after the first barrier
@@ -1317,20 +1323,22 @@ __global__ __launch_bounds__(BLOCK) void k_score(ScoreArgs a) {
           for (int64_t k0 = xb; k0 < xe; k0 += SEG) {
             const int ns = (int)min<int64_t>(SEG, xe - k0);
             load_row_segments<BLOCK>(a.rp, a.ci, k0, ns, s_start, s_off, red, nhot ? a.hot_idx : nullptr);
-            if (a.short_rows & 1) {
+            if (SHORT || (a.short_rows & 1)) {
               row_build<BLOCK>(a.cw, a.idmask, s_start, s_off, ns, c0, width, bm, threadIdx.x);
-            } else if (RC) {
-              rc_chunk_offsets<BLOCK, K>(s_off, ns, s_coff, red);
-              const int shift = build_hint<BLOCK, HC>(s_coff, ns, BLOCK, s_hint);
-              rc_build<BLOCK, K>(a.cw, a.idmask, s_start, s_off, s_coff, ns, c0, width, bm, CAP_WORDS, threadIdx.x,
-                                 s_hint, shift);
-            } else {
-              const int shift = build_hint<BLOCK, HC>(s_off, ns, BLOCK * K, s_hint);
+            } else if constexpr (!SHORT) {
+              if (RC) {
+                rc_chunk_offsets<BLOCK, K>(s_off, ns, s_coff, red);
+                const int shift = build_hint<BLOCK, HC>(s_coff, ns, BLOCK, s_hint);
+                rc_build<BLOCK, K>(a.cw, a.idmask, s_start, s_off, s_coff, ns, c0, width, bm, CAP_WORDS, threadIdx.x,
+                                   s_hint, shift);
+              } else {
+                const int shift = build_hint<BLOCK, HC>(s_off, ns, BLOCK * K, s_hint);
 #if BLP_PP
-              pp_build<BLOCK, K>(a.cw, a.idmask, s_start, s_off, ns, c0, width, bm, threadIdx.x, s_hint, shift);
+                pp_build<BLOCK, K>(a.cw, a.idmask, s_start, s_off, ns, c0, width, bm, threadIdx.x, s_hint, shift);
 #else
-              mp_build<BLOCK, K>(a.cw, a.idmask, s_start, s_off, ns, c0, width, bm, threadIdx.x, s_hint, shift);
+                mp_build<BLOCK, K>(a.cw, a.idmask, s_start, s_off, ns, c0, width, bm, threadIdx.x, s_hint, shift);
 #endif
+              }
             }
             __syncthreads();
           }
@@ -1374,13 +1382,14 @@ __global__ __launch_bounds__(BLOCK) void k_score(ScoreArgs a) {
           if (threadIdx.x == 0) s_off[ns] = tot;
           __syncthreads();
           PROF(6)
-          if (a.short_rows & 2) {
+          if (SHORT || (a.short_rows & 2)) {
             if (want_a)
               row_scan<BLOCK, true>(a.cw, a.idmask, a.idbits, a.aaw, s_wtab, s_start, s_off, ns, c0, width, bm, s_cn,
                                     s_aa, threadIdx.x);
             else
               row_scan<BLOCK, false>(a.cw, a.idmask, a.idbits, a.aaw, s_wtab, s_start, s_off, ns, c0, width, bm, s_cn,
                                      s_aa, threadIdx.x);
+          } else if constexpr (SHORT) {
           } else if (RC) {
             rc_chunk_offsets<BLOCK, K>(s_off, ns, s_coff, red);
             const int shift = build_hint<BLOCK, HC>(s_coff, ns, BLOCK, s_hint);
@@ -2424,6 +2433,13 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
       hipLaunchKernelGGL((k_score_wave<W_WAVES, W_CAP, 4>), grid, block, 0, g->stream, a);
     else
       hipLaunchKernelGGL((k_score_wave<W_WAVES, W_CAP, 8>), grid, block, 0, g->stream, a);
+    BLP_HIP(hipGetLastError());
+  } else if (np && b->variant == V_SMALL && b->short_rows == 3 && !getenv("BLP_NO_SHORT_KERNEL")) {
+    int per_cu = 1;
+    BLP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &per_cu, k_score<BLOCK_SMALL, CAP_SMALL, SEG_SMALL, 8, true>, BLOCK_SMALL, 0));
+    hipLaunchKernelGGL((k_score<BLOCK_SMALL, CAP_SMALL, SEG_SMALL, 8, true>), dim3(g->n_cu * std::max(per_cu, 1)),
+                       dim3(BLOCK_SMALL), 0, g->stream, a);
     BLP_HIP(hipGetLastError());
   } else if (np) {
     int per_cu = 1;
