@@ -32,7 +32,7 @@
 #define BLP_RC 1  // row-chunk loops in the large-universe k_score (0: merge-path loops)
 #endif
 #ifndef BLP_SHORT_MINB
-#define BLP_SHORT_MINB 5  // short-row scorer: >= 5 workgroups of 256 per CU (<= 96 VGPRs)
+#define BLP_SHORT_MINB 7  // short-row scorer: >= 7 workgroups of 256 per CU (<= 72 VGPRs)
 #endif
 #ifndef BLP_PP
 #define BLP_PP 1  // ping-pong merge-path loops in k_score (0: the single-buffer mp_build / mp_scan)
@@ -996,12 +996,16 @@ __device__ inline void rc_chunk_offsets(const int32_t* s_off, int ns, int32_t* s
 // whose dependent LDS round trips dominate a merge-path step when rows average ~10 ids;
 // the cost is idle lanes beside the longest row of the wave. ci is padded past nnz.
 constexpr int SHORT_MAX = 32;
+constexpr int SHORT_PART = 16;  // ids held in registers at a time (a row up to SHORT_MAX: two parts)
 
-__device__ inline int row_load(const int32_t* __restrict__ ci, int64_t st, int len, int* e) {
-  const blp::U4a* p = reinterpret_cast<const blp::U4a*>(ci + st);
+// Part [h, h + SHORT_PART) of a row of len ids: up to SHORT_PART / 4 16-byte loads, all issued
+// before any id is used. Rows of a review graph's users average ~10 ids, so the second part is
+// rare; holding one part keeps the scorer inside 64 VGPRs (8 workgroups of 256 per CU).
+__device__ inline void row_part(const int32_t* __restrict__ ci, int64_t st, int len, int h, int* e) {
+  const blp::U4a* p = reinterpret_cast<const blp::U4a*>(ci + st + h);
 #pragma unroll
-  for (int q = 0; q < SHORT_MAX / 4; ++q) {
-    if (4 * q < len) {
+  for (int q = 0; q < SHORT_PART / 4; ++q) {
+    if (h + 4 * q < len) {
       const blp::U4a v = p[q];
       e[4 * q] = v.x;
       e[4 * q + 1] = v.y;
@@ -1009,7 +1013,6 @@ __device__ inline int row_load(const int32_t* __restrict__ ci, int64_t st, int l
       e[4 * q + 3] = v.w;
     }
   }
-  return len;
 }
 
 template <int NT>
@@ -1017,13 +1020,17 @@ __device__ inline void row_build(const int32_t* __restrict__ ci, uint32_t idmask
                                  const int32_t* s_off, int ns, int64_t c0, int64_t width, uint32_t* bm, int tid) {
   const uint32_t keep = idmask | 0x80000000u, c0u = (uint32_t)c0, wu = (uint32_t)width;
   for (int t = tid; t < ns; t += NT) {
-    int e[SHORT_MAX];
-    const int len = row_load(ci, s_start[t], s_off[t + 1] - s_off[t], e);
+    const int64_t st = s_start[t];
+    const int len = s_off[t + 1] - s_off[t];
+    for (int h = 0; h < len; h += SHORT_PART) {
+      int e[SHORT_PART];
+      row_part(ci, st, len, h, e);
 #pragma unroll
-    for (int k = 0; k < SHORT_MAX; ++k) {
-      if (k < len) {
-        const uint32_t r = in_chunk(e[k], keep, c0u);
-        if (r < wu) atomicOr(&bm[r >> 5], 1u << (r & 31));
+      for (int k = 0; k < SHORT_PART; ++k) {
+        if (h + k < len) {
+          const uint32_t r = in_chunk(e[k], keep, c0u);
+          if (r < wu) atomicOr(&bm[r >> 5], 1u << (r & 31));
+        }
       }
     }
   }
@@ -1036,20 +1043,24 @@ __device__ inline void row_scan(const int32_t* __restrict__ ci, uint32_t idmask,
                                 uint32_t* s_cn, unsigned long long* s_aa, int tid) {
   const uint32_t keep = idmask | 0x80000000u, c0u = (uint32_t)c0, wu = (uint32_t)width;
   for (int t = tid; t < ns; t += NT) {  // the thread owns segment t: plain adds, no atomics
-    int e[SHORT_MAX];
-    const int len = row_load(ci, s_start[t], s_off[t + 1] - s_off[t], e);
+    const int64_t st = s_start[t];
+    const int len = s_off[t + 1] - s_off[t];
     unsigned c = 0;
     unsigned long long acc = 0;
+    for (int h = 0; h < len; h += SHORT_PART) {
+      int e[SHORT_PART];
+      row_part(ci, st, len, h, e);
 #pragma unroll
-    for (int k = 0; k < SHORT_MAX; ++k) {
-      if (k < len) {
-        const uint32_t r = in_chunk(e[k], keep, c0u);
-        const uint32_t word = bm[(r < wu ? r : 0u) >> 5];
-        const bool hit = r < wu && ((word >> (r & 31)) & 1u);
-        c += hit ? 1u : 0u;
-        if (AA && hit) {
-          const uint32_t code = ((uint32_t)e[k] >> idbits) & 255u;
-          acc += (unsigned long long)(code ? wtab[code] : aaw[e[k] & idmask]);
+      for (int k = 0; k < SHORT_PART; ++k) {
+        if (h + k < len) {
+          const uint32_t r = in_chunk(e[k], keep, c0u);
+          const uint32_t word = bm[(r < wu ? r : 0u) >> 5];
+          const bool hit = r < wu && ((word >> (r & 31)) & 1u);
+          c += hit ? 1u : 0u;
+          if (AA && hit) {
+            const uint32_t code = ((uint32_t)e[k] >> idbits) & 255u;
+            acc += (unsigned long long)(code ? wtab[code] : aaw[e[k] & idmask]);
+          }
         }
       }
     }
@@ -1186,29 +1197,36 @@ __device__ unsigned long long g_prof[16];
 // SHORT: every build and scan row of the batch has at most SHORT_MAX ids (the business side of
 // a review graph: user rows), so only the row-per-thread loops are compiled in -- fewer
 // registers and no hint table, hence more resident workgroups for these latency-bound sources.
-template <int BLOCK, int CAP_WORDS, int SEG, int K, bool SHORT = false>
+// The SHORT bitmap is dynamic LDS sized to the batch's universe (12.5 KiB for 100K
+// businesses), and SAA = false (no Adamic-Adar: the reference's business pass) drops the
+// fixed-point sums and the weight table: ~16.5 KiB per workgroup in all, so registers, not
+// LDS, bound the residency (BLP_SHORT_MINB workgroups per CU).
+extern __shared__ uint4 blp_dyn_lds[];
+
+template <int BLOCK, int CAP_WORDS, int SEG, int K, bool SHORT = false, bool SAA = true>
 __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(ScoreArgs a) {
   static_assert(SEG <= BLOCK, "one pair segment per thread in the output loop");
   constexpr int NW = BLOCK / 64;
   // row-chunk loops (rc_*) for the large-universe variant; the others keep the merge-path loops
   constexpr bool RC = BLP_RC && CAP_WORDS >= 34816;
-  __shared__ uint32_t bm[CAP_WORDS + (RC ? RC_EXTRA_WORDS : 0)];
+  __shared__ uint32_t bm_st[SHORT ? 4 : CAP_WORDS + (RC ? RC_EXTRA_WORDS : 0)];
+  uint32_t* bm = SHORT ? reinterpret_cast<uint32_t*>(blp_dyn_lds) : bm_st;
   __shared__ int32_t s_coff[RC ? SEG + 1 : 1];
   __shared__ int64_t s_start[SEG];
   __shared__ int32_t s_off[SEG + 1];
   __shared__ uint32_t s_cn[SEG];
-  __shared__ unsigned long long s_aa[SEG];
+  __shared__ unsigned long long s_aa[SAA ? SEG : 1];
   __shared__ unsigned long long red64[NW];
   __shared__ int red[NW];
   __shared__ int s_src;
   __shared__ int s_nhot;
-  __shared__ blp::HotRow s_hot[HOT_LIST];
-  __shared__ long long s_wtab[256];
+  __shared__ blp::HotRow s_hot[SHORT ? 1 : HOT_LIST];
+  __shared__ long long s_wtab[SAA ? 256 : 1];
   // hint table where the LDS allows it (the 64 KiB-bitmap variant keeps 2 workgroups per CU)
   constexpr int HC = SHORT ? 1 : CAP_WORDS >= 34816 ? (RC ? 1536 : 2048) : CAP_WORDS >= 16384 ? 1 : 512;
   __shared__ int32_t s_hint[HC];
 
-  if (a.wtab)  // visible after the first barrier
+  if (SAA && a.wtab)  // visible after the first barrier
     for (int i = threadIdx.x; i < 256; i += BLOCK) s_wtab[i] = a.wtab[i];
   if (RC)  // the zero word and the build's dummy words past the bitmap
     for (int i = threadIdx.x; i < RC_EXTRA_WORDS; i += BLOCK) bm[CAP_WORDS + i] = 0;
@@ -1216,7 +1234,7 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
   const int64_t span = a.hi - a.lo;
   const int nchunks = span <= CAP_BITS ? 1 : (int)((span + CAP_BITS - 1) / CAP_BITS);
   const bool want_j = (a.mask & BLP_JACCARD) != 0;
-  const bool want_a = (a.mask & BLP_ADAMIC) != 0;
+  const bool want_a = SAA && (a.mask & BLP_ADAMIC) != 0;
   uint4* bm4 = reinterpret_cast<uint4*>(bm);
   const int n_active = a.misc->n_active;
 
@@ -1260,7 +1278,7 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
           // 2. the sparse rows mark N(N(x)) ∩ [c0, c1) through merge-path row segments
           if (threadIdx.x == 0) s_nhot = 0;
           __syncthreads();
-          if (a.hot_idx) {
+          if (!SHORT && a.hot_idx) {  // short rows are never dense
             for (int64_t k = xb + threadIdx.x; k < xe; k += BLOCK) {
               const int hi = a.hot_idx[a.ci[k]];
               if (hi >= 0) {
@@ -1270,7 +1288,7 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
             }
           }
           __syncthreads();
-          const int nhot = s_nhot <= HOT_LIST ? s_nhot : 0;  // overflow: every row goes sparse
+          const int nhot = !SHORT && s_nhot <= HOT_LIST ? s_nhot : 0;  // overflow: every row goes sparse
           const int64_t q0 = c0 >> 7;
           if (RC) {
             // every thread owns QPT vectors of the bitmap and ORs each dense row into registers:
@@ -1374,7 +1392,7 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
             len = a.g_yl[gp];
             pout = a.g_out[gp];  // used after the scan: its latency hides behind it
             s_cn[threadIdx.x] = 0;
-            s_aa[threadIdx.x] = 0;
+            if (SAA) s_aa[threadIdx.x] = 0;
           }
           int tot;
           const int ex = block_exscan<BLOCK>(len, red, &tot);
@@ -1383,8 +1401,8 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
           __syncthreads();
           PROF(6)
           if (SHORT || (a.short_rows & 2)) {
-            if (want_a)
-              row_scan<BLOCK, true>(a.cw, a.idmask, a.idbits, a.aaw, s_wtab, s_start, s_off, ns, c0, width, bm, s_cn,
+            if (SAA && want_a)
+              row_scan<BLOCK, SAA>(a.cw, a.idmask, a.idbits, a.aaw, s_wtab, s_start, s_off, ns, c0, width, bm, s_cn,
                                     s_aa, threadIdx.x);
             else
               row_scan<BLOCK, false>(a.cw, a.idmask, a.idbits, a.aaw, s_wtab, s_start, s_off, ns, c0, width, bm, s_cn,
@@ -1422,7 +1440,7 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
           for (int t = threadIdx.x; t < ns; t += BLOCK) {  // ns <= SEG <= BLOCK: t == threadIdx.x
             const int p = pout;
             unsigned c = s_cn[t];
-            double av = (double)s_aa[t] * (1.0 / blp::AA_SCALE);
+            double av = SAA ? (double)s_aa[t] * (1.0 / blp::AA_SCALE) : 0.0;
             if (ch > 0) {
               c += a.cn[p];
               if (want_a) av += a.aa[p];
@@ -2016,6 +2034,22 @@ static int launch_score(blp_graph* g, const ScoreArgs& a, int per_cu) {
   return BLP_OK;
 }
 
+// Short-row scorer (every build and scan row <= SHORT_MAX ids), SAA: Adamic-Adar compiled in.
+// Many light sources per workgroup: at least two per dequeue, so the one queue head is not the
+// limit (one device-scope atomic word saturates near 90 dequeues per microsecond).
+template <bool SAA>
+static int launch_short(blp_graph* g, const blp_batch* b, ScoreArgs a, size_t dyn) {
+  auto kern = k_score<BLOCK_SMALL, CAP_SMALL, SEG_SMALL, 8, true, SAA>;
+  int per_cu = 1;
+  BLP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, BLOCK_SMALL, dyn));
+  const int64_t n_wg = (int64_t)g->n_cu * std::max(per_cu, 1);
+  if (!getenv("BLP_DQ") && b->n_sources >= n_wg * 16) a.dq = std::max(a.dq, 2);
+  hipLaunchKernelGGL((k_score<BLOCK_SMALL, CAP_SMALL, SEG_SMALL, 8, true, SAA>), dim3((unsigned)n_wg),
+                     dim3(BLOCK_SMALL), dyn, g->stream, a);
+  BLP_HIP(hipGetLastError());
+  return BLP_OK;
+}
+
 template <int BLOCK, int CAP, int SEG>
 static int launch_heavy(blp_graph* g, const HeavyArgs& h, int64_t n_items) {
   hipLaunchKernelGGL((k_heavy<BLOCK, CAP, SEG>), dim3((unsigned)n_items), dim3(BLOCK), 0, g->stream, h);
@@ -2435,12 +2469,9 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
       hipLaunchKernelGGL((k_score_wave<W_WAVES, W_CAP, 8>), grid, block, 0, g->stream, a);
     BLP_HIP(hipGetLastError());
   } else if (np && b->variant == V_SMALL && b->short_rows == 3 && !getenv("BLP_NO_SHORT_KERNEL")) {
-    int per_cu = 1;
-    BLP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &per_cu, k_score<BLOCK_SMALL, CAP_SMALL, SEG_SMALL, 8, true>, BLOCK_SMALL, 0));
-    hipLaunchKernelGGL((k_score<BLOCK_SMALL, CAP_SMALL, SEG_SMALL, 8, true>), dim3(g->n_cu * std::max(per_cu, 1)),
-                       dim3(BLOCK_SMALL), 0, g->stream, a);
-    BLP_HIP(hipGetLastError());
+    // bitmap in dynamic LDS, sized to the universe (whole 16-byte vectors)
+    const size_t dyn = 4 * (size_t)std::max<int64_t>(4, ((b->hi - b->lo + 31) / 32 + 3) / 4 * 4);
+    if ((rc = (mask & BLP_ADAMIC) ? launch_short<true>(g, b, a, dyn) : launch_short<false>(g, b, a, dyn))) return rc;
   } else if (np) {
     int per_cu = 1;
     if ((rc = variant_occupancy(b->variant, &per_cu))) return rc;
