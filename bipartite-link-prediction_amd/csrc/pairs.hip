@@ -1986,6 +1986,10 @@ struct blp_batch {
   int64_t n_sources = 0;
   bool runs = false;  // pairs arrive grouped by source (x non-decreasing): run-head grouping
   blp::KernelTimer t_score, t_group;
+  // the batch's own stream and grouping scratch: batches of one graph (the user and the
+  // business pass of similarity.main) run concurrently, one filling the other's tail
+  hipStream_t stream = nullptr;
+  blp::DevBuf cnt, off, active, scratch;
 };
 
 using namespace blp;
@@ -2021,15 +2025,15 @@ static int variant_occupancy(int v, int* per_cu) {
 }
 
 template <int BLOCK, int CAP, int SEG>
-static int launch_score(blp_graph* g, const ScoreArgs& a, int per_cu) {
+static int launch_score(blp_graph* g, hipStream_t st, const ScoreArgs& a, int per_cu) {
   const dim3 grid(g->n_cu * per_cu), block(BLOCK);
   const int k = kpt_choice();
   if (k == 4)
-    hipLaunchKernelGGL((k_score<BLOCK, CAP, SEG, 4>), grid, block, 0, g->stream, a);
+    hipLaunchKernelGGL((k_score<BLOCK, CAP, SEG, 4>), grid, block, 0, st, a);
   else if (k == 16)
-    hipLaunchKernelGGL((k_score<BLOCK, CAP, SEG, 16>), grid, block, 0, g->stream, a);
+    hipLaunchKernelGGL((k_score<BLOCK, CAP, SEG, 16>), grid, block, 0, st, a);
   else
-    hipLaunchKernelGGL((k_score<BLOCK, CAP, SEG, 8>), grid, block, 0, g->stream, a);
+    hipLaunchKernelGGL((k_score<BLOCK, CAP, SEG, 8>), grid, block, 0, st, a);
   BLP_HIP(hipGetLastError());
   return BLP_OK;
 }
@@ -2045,14 +2049,14 @@ static int launch_short(blp_graph* g, const blp_batch* b, ScoreArgs a, size_t dy
   const int64_t n_wg = (int64_t)g->n_cu * std::max(per_cu, 1);
   if (!getenv("BLP_DQ") && b->n_sources >= n_wg * 16) a.dq = std::max(a.dq, 2);
   hipLaunchKernelGGL((k_score<BLOCK_SMALL, CAP_SMALL, SEG_SMALL, 8, true, SAA>), dim3((unsigned)n_wg),
-                     dim3(BLOCK_SMALL), dyn, g->stream, a);
+                     dim3(BLOCK_SMALL), dyn, b->stream, a);
   BLP_HIP(hipGetLastError());
   return BLP_OK;
 }
 
 template <int BLOCK, int CAP, int SEG>
-static int launch_heavy(blp_graph* g, const HeavyArgs& h, int64_t n_items) {
-  hipLaunchKernelGGL((k_heavy<BLOCK, CAP, SEG>), dim3((unsigned)n_items), dim3(BLOCK), 0, g->stream, h);
+static int launch_heavy(hipStream_t st, const HeavyArgs& h, int64_t n_items) {
+  hipLaunchKernelGGL((k_heavy<BLOCK, CAP, SEG>), dim3((unsigned)n_items), dim3(BLOCK), 0, st, h);
   BLP_HIP(hipGetLastError());
   return BLP_OK;
 }
@@ -2162,6 +2166,8 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   };
   int rc = set_device(g);
   if (rc) return bail(rc);
+  BLP_HIP_OR(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking), bail);
+  BLP_HIP_OR(hipStreamSynchronize(g->stream), bail);  // the graph's own uploads are complete
   // wave-per-source scorer: opt-in (BLP_WAVE=1). With heavy sources split finely the block
   // kernels are faster on the business side of config 2 (1.46 vs 2.01 ms, profiles/probe_sides.py)
   b->wave = span <= (int64_t)W_CAP * 32 && b->chunks == 1 && !b->global && !b->split && getenv("BLP_WAVE") &&
@@ -2286,8 +2292,14 @@ int blp_batch_destroy(blp_batch* b) {
   if (!b) return BLP_OK;
   if (b->g) (void)hipSetDevice(b->g->device);
   if (b->g && b->g->stream) (void)hipStreamSynchronize(b->g->stream);
+  if (b->stream) (void)hipStreamSynchronize(b->stream);
   timer_release(b->t_score);
   timer_release(b->t_group);
+  b->cnt.release();
+  b->off.release();
+  b->active.release();
+  b->scratch.release();
+  if (b->stream) (void)hipStreamDestroy(b->stream);
   void* ps[] = {b->d_x,    b->d_y,    b->d_cn,   b->d_jac,  b->d_aa,          b->d_gout,        b->d_gyb,
                 b->d_gyl,  b->d_misc, b->d_heavy_slot, b->d_heavy_bm, b->d_heavy_items, b->d_gbm, b->d_gy, b->d_rsplit, b->d_pcn, b->d_paa, b->d_ph2};
   for (void* p : ps)
@@ -2327,44 +2339,44 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   const int64_t n = g->n, np = b->n_pairs;
   const int64_t nh = (int64_t)b->nb * b->nblk;
   const int64_t tiles_h = (nh + SCAN_TILE - 1) / SCAN_TILE, tiles_b = (b->nb + SCAN_TILE - 1) / SCAN_TILE;
-  if ((rc = g->cnt.reserve(4 * (n + 1)))) return rc;
-  if ((rc = g->off.reserve(4 * (n + 1)))) return rc;
-  if ((rc = g->active.reserve(4 * (n + 1)))) return rc;
+  if ((rc = b->cnt.reserve(4 * (n + 1)))) return rc;
+  if ((rc = b->off.reserve(4 * (n + 1)))) return rc;
+  if ((rc = b->active.reserve(4 * (n + 1)))) return rc;
   // scratch: hist | hoff | tiles | bucket_active | abase | tmp
   const int64_t sc_ints = 2 * nh + std::max(tiles_h, tiles_b) + 1 + 2 * (int64_t)b->nb + 4 * np;
-  if ((rc = g->scratch.reserve(4 * (sc_ints + 16)))) return rc;
-  int32_t* hist = g->scratch.as<int32_t>();
+  if ((rc = b->scratch.reserve(4 * (sc_ints + 16)))) return rc;
+  int32_t* hist = b->scratch.as<int32_t>();
   int32_t* hoff = hist + nh;
   int32_t* tiles = hoff + nh;
   int32_t* bact = tiles + std::max(tiles_h, tiles_b) + 1;
   int32_t* abase = bact + b->nb;
   int4* tmp = reinterpret_cast<int4*>((reinterpret_cast<uintptr_t>(abase + b->nb) + 15) & ~uintptr_t(15));
   hipEvent_t t0, bt0;
-  if ((rc = timer_begin(g, K_GROUP, &t0))) return rc;
-  if ((rc = timer_begin(b->t_group, g->stream, &bt0))) return rc;
-  BLP_HIP(hipMemsetAsync(b->d_misc, 0, sizeof(Misc), g->stream));
+  if ((rc = timer_begin(g->timers[K_GROUP], b->stream, &t0))) return rc;
+  if ((rc = timer_begin(b->t_group, b->stream, &bt0))) return rc;
+  BLP_HIP(hipMemsetAsync(b->d_misc, 0, sizeof(Misc), b->stream));
   if (np && b->runs) {
     const int64_t tiles = (np + SCAN_TILE - 1) / SCAN_TILE;
     int32_t* rtile = reinterpret_cast<int32_t*>(tmp);  // the bucket sort's pair buffer is free here
-    hipLaunchKernelGGL(k_run_count, dim3((unsigned)tiles), dim3(SCAN_BLOCK), 0, g->stream, b->d_x, np, rtile);
-    hipLaunchKernelGGL(k_scan_mid, dim3(1), dim3(SCAN_BLOCK), 0, g->stream, rtile, tiles, &b->d_misc->n_active);
-    hipLaunchKernelGGL(k_run_write, dim3((unsigned)tiles), dim3(SCAN_BLOCK), 0, g->stream, b->d_x, b->d_y, np, g->d_rp,
-                       rtile, g->active.as<int32_t>(), g->off.as<int32_t>(), b->d_gout, b->d_gyb, b->d_gyl,
+    hipLaunchKernelGGL(k_run_count, dim3((unsigned)tiles), dim3(SCAN_BLOCK), 0, b->stream, b->d_x, np, rtile);
+    hipLaunchKernelGGL(k_scan_mid, dim3(1), dim3(SCAN_BLOCK), 0, b->stream, rtile, tiles, &b->d_misc->n_active);
+    hipLaunchKernelGGL(k_run_write, dim3((unsigned)tiles), dim3(SCAN_BLOCK), 0, b->stream, b->d_x, b->d_y, np, g->d_rp,
+                       rtile, b->active.as<int32_t>(), b->off.as<int32_t>(), b->d_gout, b->d_gyb, b->d_gyl,
                        b->d_gy);
-    hipLaunchKernelGGL(k_run_cnt, dim3(1024), dim3(256), 0, g->stream, g->active.as<int32_t>(), &b->d_misc->n_active,
-                       np, g->off.as<int32_t>(), g->cnt.as<int32_t>());
+    hipLaunchKernelGGL(k_run_cnt, dim3(1024), dim3(256), 0, b->stream, b->active.as<int32_t>(), &b->d_misc->n_active,
+                       np, b->off.as<int32_t>(), b->cnt.as<int32_t>());
   } else if (np) {
-    hipLaunchKernelGGL(k_bucket_hist, dim3(b->nblk), dim3(GP_BLOCK), 0, g->stream, b->d_x, np, b->xlo, b->shift, b->nb,
+    hipLaunchKernelGGL(k_bucket_hist, dim3(b->nblk), dim3(GP_BLOCK), 0, b->stream, b->d_x, np, b->xlo, b->shift, b->nb,
                        b->nblk, b->per_blk, hist);
-    hipLaunchKernelGGL(k_scan_sum, dim3((unsigned)tiles_h), dim3(SCAN_BLOCK), 0, g->stream, hist, nh, tiles);
-    hipLaunchKernelGGL(k_scan_mid, dim3(1), dim3(SCAN_BLOCK), 0, g->stream, tiles, tiles_h, (int32_t*)nullptr);
-    hipLaunchKernelGGL(k_scan_out, dim3((unsigned)tiles_h), dim3(SCAN_BLOCK), 0, g->stream, hist, nh, tiles, hoff);
-    hipLaunchKernelGGL(k_bucket_scatter, dim3(b->nblk), dim3(GP_BLOCK), 0, g->stream, b->d_x, b->d_y, np, b->xlo,
+    hipLaunchKernelGGL(k_scan_sum, dim3((unsigned)tiles_h), dim3(SCAN_BLOCK), 0, b->stream, hist, nh, tiles);
+    hipLaunchKernelGGL(k_scan_mid, dim3(1), dim3(SCAN_BLOCK), 0, b->stream, tiles, tiles_h, (int32_t*)nullptr);
+    hipLaunchKernelGGL(k_scan_out, dim3((unsigned)tiles_h), dim3(SCAN_BLOCK), 0, b->stream, hist, nh, tiles, hoff);
+    hipLaunchKernelGGL(k_bucket_scatter, dim3(b->nblk), dim3(GP_BLOCK), 0, b->stream, b->d_x, b->d_y, np, b->xlo,
                        b->shift, b->nb, b->nblk, b->per_blk, hoff, tmp);
     const int keys = 1 << b->shift;
 #define BLP_GROUP_LAUNCH(K)                                                                                         \
-  hipLaunchKernelGGL(k_bucket_group<K>, dim3(b->nb), dim3(GB_BLOCK), 0, g->stream, g->d_rp, tmp, hoff,               \
-                     b->nblk, b->nb, b->shift, b->xlo, b->xspan, np, g->off.as<int32_t>(), g->cnt.as<int32_t>(), bact,  \
+  hipLaunchKernelGGL(k_bucket_group<K>, dim3(b->nb), dim3(GB_BLOCK), 0, b->stream, g->d_rp, tmp, hoff,               \
+                     b->nblk, b->nb, b->shift, b->xlo, b->xspan, np, b->off.as<int32_t>(), b->cnt.as<int32_t>(), bact,  \
                      b->d_gout,                                                                                       \
                      b->d_gyb, b->d_gyl, b->d_gy)
     if (keys <= 256)
@@ -2376,13 +2388,13 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
     else
       BLP_GROUP_LAUNCH(32768);
 #undef BLP_GROUP_LAUNCH
-    hipLaunchKernelGGL(k_scan_sum, dim3((unsigned)tiles_b), dim3(SCAN_BLOCK), 0, g->stream, bact, (int64_t)b->nb, tiles);
-    hipLaunchKernelGGL(k_scan_mid, dim3(1), dim3(SCAN_BLOCK), 0, g->stream, tiles, tiles_b, &b->d_misc->n_active);
-    hipLaunchKernelGGL(k_scan_out, dim3((unsigned)tiles_b), dim3(SCAN_BLOCK), 0, g->stream, bact, (int64_t)b->nb, tiles,
+    hipLaunchKernelGGL(k_scan_sum, dim3((unsigned)tiles_b), dim3(SCAN_BLOCK), 0, b->stream, bact, (int64_t)b->nb, tiles);
+    hipLaunchKernelGGL(k_scan_mid, dim3(1), dim3(SCAN_BLOCK), 0, b->stream, tiles, tiles_b, &b->d_misc->n_active);
+    hipLaunchKernelGGL(k_scan_out, dim3((unsigned)tiles_b), dim3(SCAN_BLOCK), 0, b->stream, bact, (int64_t)b->nb, tiles,
                        abase);
 #define BLP_ACTIVE_LAUNCH(K)                                                                                   \
-  hipLaunchKernelGGL(k_active_write<K>, dim3(b->nb), dim3(GB_BLOCK), 0, g->stream, g->cnt.as<int32_t>(), abase, b->shift, \
-                     b->xlo, b->xspan, g->active.as<int32_t>())
+  hipLaunchKernelGGL(k_active_write<K>, dim3(b->nb), dim3(GB_BLOCK), 0, b->stream, b->cnt.as<int32_t>(), abase, b->shift, \
+                     b->xlo, b->xspan, b->active.as<int32_t>())
     if (keys <= 256)
       BLP_ACTIVE_LAUNCH(256);
     else if (keys <= 1024)
@@ -2394,21 +2406,21 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
 #undef BLP_ACTIVE_LAUNCH
   }
   BLP_HIP(hipGetLastError());
-  if ((rc = timer_end(b->t_group, g->stream, bt0))) return rc;
-  if ((rc = timer_end(g, K_GROUP, t0))) return rc;
+  if ((rc = timer_end(b->t_group, b->stream, bt0))) return rc;
+  if ((rc = timer_end(g->timers[K_GROUP], b->stream, t0))) return rc;
 
   hipEvent_t t1, bt1;
-  if ((rc = timer_begin(g, K_SCORE, &t1))) return rc;
-  if ((rc = timer_begin(b->t_score, g->stream, &bt1))) return rc;
+  if ((rc = timer_begin(g->timers[K_SCORE], b->stream, &t1))) return rc;
+  if ((rc = timer_begin(b->t_score, b->stream, &bt1))) return rc;
   if (b->n_heavy) {
-    BLP_HIP(hipMemsetAsync(b->d_heavy_bm, 0, 4 * b->hb_words * b->n_heavy, g->stream));
+    BLP_HIP(hipMemsetAsync(b->d_heavy_bm, 0, 4 * b->hb_words * b->n_heavy, b->stream));
     HeavyArgs h{g->d_rp, g->d_ci, b->d_heavy_items, b->d_heavy_bm, b->hb_words, b->lo, b->hi - b->lo};
     if (b->variant == V_SMALL)
-      rc = launch_heavy<BLOCK_SMALL, CAP_SMALL, SEG_SMALL>(g, h, b->n_heavy_items);
+      rc = launch_heavy<BLOCK_SMALL, CAP_SMALL, SEG_SMALL>(b->stream, h, b->n_heavy_items);
     else if (b->variant == V_MED)
-      rc = launch_heavy<BLOCK_MED, CAP_MED, SEG_MED>(g, h, b->n_heavy_items);
+      rc = launch_heavy<BLOCK_MED, CAP_MED, SEG_MED>(b->stream, h, b->n_heavy_items);
     else
-      rc = launch_heavy<BLOCK_LARGE, CAP_LARGE, SEG_LARGE>(g, h, b->n_heavy_items);
+      rc = launch_heavy<BLOCK_LARGE, CAP_LARGE, SEG_LARGE>(b->stream, h, b->n_heavy_items);
     if (rc) return rc;
   }
   ScoreArgs a;
@@ -2421,9 +2433,9 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   a.idmask = (uint32_t)((1ull << a.idbits) - 1);
   a.wtab = g->d_wtab;
 
-  a.off = g->off.as<int32_t>();
-  a.cnt = g->cnt.as<int32_t>();
-  a.active = g->active.as<int32_t>();
+  a.off = b->off.as<int32_t>();
+  a.cnt = b->cnt.as<int32_t>();
+  a.active = b->active.as<int32_t>();
   a.g_out = b->d_gout;
   a.g_yb = b->d_gyb;
   a.g_yl = b->d_gyl;
@@ -2447,14 +2459,14 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
     int per_cu = 1;
     BLP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_score_split<S_BLOCK, S_CAP, S_SEG, 8>, S_BLOCK, 0));
     hipLaunchKernelGGL((k_score_split<S_BLOCK, S_CAP, S_SEG, 8>), dim3(g->n_cu * std::max(per_cu, 1)), dim3(S_BLOCK), 0,
-                       g->stream, a, b->d_gy, b->d_rsplit, b->rs_lo, b->split, b->d_pcn, b->d_paa, b->d_ph2, np);
+                       b->stream, a, b->d_gy, b->d_rsplit, b->rs_lo, b->split, b->d_pcn, b->d_paa, b->d_ph2, np);
     BLP_HIP(hipGetLastError());
-    hipLaunchKernelGGL(k_split_combine, dim3(g->n_cu * 8), dim3(256), 0, g->stream, a, b->split, b->d_pcn, b->d_paa,
+    hipLaunchKernelGGL(k_split_combine, dim3(g->n_cu * 8), dim3(256), 0, b->stream, a, b->split, b->d_pcn, b->d_paa,
                        b->d_ph2, np);
     BLP_HIP(hipGetLastError());
   } else if (np && b->global) {
     a.hot_idx = nullptr;
-    hipLaunchKernelGGL((k_score_global<G_BLOCK, G_SEG, 8>), dim3((unsigned)b->gslots), dim3(G_BLOCK), 0, g->stream, a,
+    hipLaunchKernelGGL((k_score_global<G_BLOCK, G_SEG, 8>), dim3((unsigned)b->gslots), dim3(G_BLOCK), 0, b->stream, a,
                        b->d_gbm, b->gwords);
     BLP_HIP(hipGetLastError());
   } else if (np && b->wave) {
@@ -2464,9 +2476,9 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
     const dim3 grid(g->n_cu * std::max(per_cu, 1)), block(W_WAVES * 64);
     static const int wk = getenv("BLP_WAVE_K") ? atoi(getenv("BLP_WAVE_K")) : 8;  // tuning knob
     if (wk == 4)
-      hipLaunchKernelGGL((k_score_wave<W_WAVES, W_CAP, 4>), grid, block, 0, g->stream, a);
+      hipLaunchKernelGGL((k_score_wave<W_WAVES, W_CAP, 4>), grid, block, 0, b->stream, a);
     else
-      hipLaunchKernelGGL((k_score_wave<W_WAVES, W_CAP, 8>), grid, block, 0, g->stream, a);
+      hipLaunchKernelGGL((k_score_wave<W_WAVES, W_CAP, 8>), grid, block, 0, b->stream, a);
     BLP_HIP(hipGetLastError());
   } else if (np && b->variant == V_SMALL && b->short_rows == 3 && !getenv("BLP_NO_SHORT_KERNEL")) {
     // bitmap in dynamic LDS, sized to the universe (whole 16-byte vectors)
@@ -2476,15 +2488,15 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
     int per_cu = 1;
     if ((rc = variant_occupancy(b->variant, &per_cu))) return rc;
     if (b->variant == V_SMALL)
-      rc = launch_score<BLOCK_SMALL, CAP_SMALL, SEG_SMALL>(g, a, per_cu);
+      rc = launch_score<BLOCK_SMALL, CAP_SMALL, SEG_SMALL>(g, b->stream, a, per_cu);
     else if (b->variant == V_MED)
-      rc = launch_score<BLOCK_MED, CAP_MED, SEG_MED>(g, a, per_cu);
+      rc = launch_score<BLOCK_MED, CAP_MED, SEG_MED>(g, b->stream, a, per_cu);
     else
-      rc = launch_score<BLOCK_LARGE, CAP_LARGE, SEG_LARGE>(g, a, per_cu);
+      rc = launch_score<BLOCK_LARGE, CAP_LARGE, SEG_LARGE>(g, b->stream, a, per_cu);
     if (rc) return rc;
   }
-  if ((rc = timer_end(b->t_score, g->stream, bt1))) return rc;
-  return timer_end(g, K_SCORE, t1);
+  if ((rc = timer_end(b->t_score, b->stream, bt1))) return rc;
+  return timer_end(g->timers[K_SCORE], b->stream, t1);
 }
 
 int blp_batch_stats(blp_batch* b, int which, double* total_ms, int64_t* launches) {
@@ -2514,7 +2526,7 @@ int blp_batch_fetch(blp_graph* g, blp_batch* b, uint32_t* cn, double* jac, doubl
   BLP_CHECK(g && b && b->g == g, BLP_E_ARG, "blp_batch_fetch: graph/batch mismatch");
   int rc = set_device(g);
   if (rc) return rc;
-  BLP_HIP(hipStreamSynchronize(g->stream));
+  BLP_HIP(hipStreamSynchronize(b->stream));
   const int64_t np = b->n_pairs;
   Misc m;
   BLP_HIP(hipMemcpy(&m, b->d_misc, sizeof(Misc), hipMemcpyDeviceToHost));

@@ -108,8 +108,11 @@ int blp_score_pairs(blp_graph* g, int side, uint32_t mask, const int32_t* pair_u
 
 /* Device-resident batch (bench / repeated scoring). blp_batch_create copies the pairs to
  * HBM and plans the launch (bitmap universe, variant). blp_batch_score enqueues one full
- * pass on the graph's stream: group pairs by source on the device, score, write results in
- * the caller's pair order into device buffers. blp_batch_fetch copies results to the host. */
+ * pass on the batch's own stream (returns at once): group pairs by source on the device,
+ * score, write results in the caller's pair order into device buffers. Batches of one graph
+ * run concurrently (similarity.main's user and business passes overlap on the device).
+ * blp_batch_fetch waits for the batch and copies results to the host; blp_device_sync waits
+ * for every batch of the device. */
 int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n_pairs,
                      blp_batch** out);
 int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask);
@@ -121,7 +124,7 @@ int blp_batch_plan(const blp_batch* b, int64_t* lo, int64_t* hi, int* chunks, in
                    int* heavy);
 
 /* Per-batch device time of the last/accumulated blp_batch_score calls (HIP events on the
- * graph stream): which 0 = scorer kernel, 1 = grouping kernels. Reset with blp_batch_stats_reset. */
+ * batch stream): which 0 = scorer kernel, 1 = grouping kernels. Reset with blp_batch_stats_reset. */
 int blp_batch_stats(blp_batch* b, int which, double* total_ms, int64_t* launches);
 int blp_batch_stats_reset(blp_batch* b);
 
