@@ -77,7 +77,13 @@ def pmc_traffic(kernel):
     FETCH_SIZE / WRITE_SIZE passes; 2 x FETCH_SIZE + WRITE_SIZE per MI355X_MICROARCH.md)."""
     import glob
 
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_bench.json")))  # rNN_vM: newest last
+    import re
+
+    def version(f):  # rNN_vM_bench.json: newest (round, version) last
+        m = re.search(r"r(\d+)_v(\d+)_bench\.json$", f)
+        return (int(m.group(1)), int(m.group(2))) if m else (-1, -1)
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_v*_bench.json")), key=version)
     for f in reversed(files):
         try:
             rows = json.load(open(f))
@@ -524,6 +530,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--user-mask", type=int, default=7, help="methods of the user pass (1 CN, 2 J, 4 AA)")
+    ap.add_argument("--business-first", action="store_true", help="enqueue the business pass before the user pass")
     ap.add_argument("--mode", default="similarity", choices=["similarity", "topk", "svd", "sharded"],
                     help="similarity: config 2 (default); topk: config 3 full-candidate Jaccard + Adamic-Adar "
                          "top-k; svd: config 4 rank-64 truncated-SVD scorer; sharded: config 5 row-block "
@@ -557,12 +564,14 @@ def main():
         passes.append(("user", G.batch(ex_x, ex_y), args.user_mask))
     if args.sides in ("both", "business"):
         passes.append(("business", G.batch(ex_y, ex_x), blp.CN | blp.JACCARD))
+    if args.business_first:  # enqueue order of the two concurrent passes
+        passes.reverse()
     for name, bt, _ in passes:
         log("plan %s: %s" % (name, bt.plan()))
 
+    step = [(bt, mask) for _, bt, mask in passes]  # one concurrent step (blp_batches_score)
     for _ in range(args.warmup):
-        for _, bt, mask in passes:
-            bt.score(mask)
+        G.score_batches(step)
     blp.device_sync(dev)
     for _, bt, _ in passes:
         bt.stats_reset()
@@ -571,8 +580,7 @@ def main():
     blp.device_sync(dev)
     t_start = time.perf_counter()
     for _ in range(args.steps):
-        for _, bt, mask in passes:
-            bt.score(mask)
+        G.score_batches(step)
     blp.device_sync(dev)
     t_local = time.perf_counter() - t_start
     dist.barrier()
@@ -616,12 +624,12 @@ def main():
                  for name, xs_, ys_ in [("user", ex_x, ex_y), ("business", ex_y, ex_x)] if name in res},
     }
     # roofline of the dominant kernel: the user-side scorer (falls back to the first pass)
-    name0, bt0, mask0 = passes[0]
+    name0, bt0, mask0 = sorted(passes, key=lambda p: p[0] != "user")[0]
     cn0 = res[name0]["cn"]
     xs, ys = (ex_x, ex_y) if name0 == "user" else (ex_y, ex_x)
     byts = alg_bytes(G, xs, ys, mask0, cn0)
     sec = ktimes[name0]["score_ms"] / 1e3
-    kname = "k_score<1024, 34816, 512, 8>" if bt0.plan()["block"] == 1024 else "k_score_wave<2, 3328, 8>"
+    kname = "k_score<1024, 34816, 512, 8, false, true>" if bt0.plan()["block"] == 1024 else "k_score_wave<2, 3328, 8>"
     traffic, tsrc = pmc_traffic(kname)
     out["roofline"] = {"bound": "hbm", "achieved": byts / sec / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                        "frac": byts / sec / 1e9 / HBM_PEAK_GBS, "traffic": traffic,

@@ -54,6 +54,7 @@ SIGNATURES = {
     "blp_score_pairs": [_P, _I32, _U32, _P, _P, _I64, _P, _P, _P],
     "blp_batch_create": [_P, _P, _P, _I64, _PP],
     "blp_batch_score": [_P, _P, _U32],
+    "blp_batches_score": [_P, _I32, _P, _P],
     "blp_batch_fetch": [_P, _P, _P, _P, _P],
     "blp_batch_destroy": [_P],
     "blp_batch_plan": [_P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),

@@ -204,6 +204,14 @@ class DeviceGraph(HostGraph):
     def batch(self, x, y):
         return PairBatch(self, x, y)
 
+    def score_batches(self, items):
+        """Enqueue several batches of this graph as one concurrent step (blp_batches_score).
+        items: [(PairBatch, mask), ...]; returns at once, fetch() waits."""
+        n = len(items)
+        hs = (ctypes.c_void_p * max(n, 1))(*[b.handle for b, _ in items])
+        ms = (ctypes.c_uint32 * max(n, 1))(*[int(m) for _, m in items])
+        check(lib().blp_batches_score(self.handle, n, hs, ms))
+
     def hop3_sample(self, src, pos_off=None, pos_y=None, rate=0.01, seed=0):
         """Exact-distance-3 candidates of each source, sampled (dataset_maker.py:137-144).
 

@@ -110,9 +110,28 @@ def score_examples(examples, G, side, mask):
     return present, scores
 
 
-def _run_side(examples, G, methods, outfiles, table, side, sidecar=False):
+def score_both_sides(examples, G, u_mask, b_mask):
+    """Both passes of similarity.main in one device step: the user-side and the business-side
+    batches are enqueued together (blp_batches_score) and run concurrently.
+
+    Returns (present mask over the flattened pairs, user-side scores, business-side scores)."""
+    _, _, u_ids, v_ids = flatten_examples(examples)
+    du, pu = G.lookup(u_ids)
+    dv, pv = G.lookup(v_ids)
+    present = pu & pv
+    ub = G.batch(du[present], dv[present])
+    bb = G.batch(dv[present], du[present])
+    try:
+        G.score_batches([(ub, u_mask), (bb, b_mask)])
+        return present, ub.fetch(u_mask), bb.fetch(b_mask)
+    finally:
+        ub.close()
+        bb.close()
+
+
+def _run_side(examples, G, methods, outfiles, table, side, sidecar=False, scored=None):
     mask = method_mask(methods, table)
-    present, scores = score_examples(examples, G, side, mask | blp.CN)
+    present, scores = scored if scored is not None else score_examples(examples, G, side, mask | blp.CN)
     results = []
     for m, f in zip(methods, outfiles):
         sim = assemble(examples, _values(table.get(m, 0), present, scores))
@@ -133,8 +152,12 @@ def main(example_file, graph_file, u_methods, u_outfiles, b_methods, b_outfiles,
     examples = util.load_json(example_file)
     print("Loading graph...")
     G = blp.load_edge_list(graph_file)
-    users(examples, G, u_methods, u_outfiles, sidecar=sidecar)
-    business(examples, G, b_methods, b_outfiles, sidecar=sidecar)
+    # both passes in one concurrent device step, then the files in the reference's order
+    print("Scoring user and business sides on the device...")
+    present, u_scores, b_scores = score_both_sides(examples, G, method_mask(u_methods, _U_BITS) | blp.CN,
+                                                   method_mask(b_methods, _B_BITS) | blp.CN)
+    _run_side(examples, G, u_methods, u_outfiles, _U_BITS, 0, sidecar, scored=(present, u_scores))
+    _run_side(examples, G, b_methods, b_outfiles, dict(_B_BITS), 1, sidecar, scored=(present, b_scores))
 
 
 def users(examples, G, methods, outfiles, *, sidecar=False):

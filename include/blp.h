@@ -118,6 +118,10 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
 int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask);
 int blp_batch_fetch(blp_graph* g, blp_batch* b, uint32_t* cn, double* jac, double* aa);
 int blp_batch_destroy(blp_batch* b);
+/* Enqueue blp_batch_score for n batches of one graph at once (one similarity.main step: the
+ * user and the business pass). They run concurrently; a large-universe (user-side) batch is
+ * held to a share of the CUs so the other passes run beside it rather than after it. */
+int blp_batches_score(blp_graph* g, int n, blp_batch* const* batches, const uint32_t* masks);
 /* Launch plan actually used: universe lo/hi (bitmap range), bitmap chunks, threads per
  * block, number of heavy sources pre-built across workgroups. For tests and DESIGN.md.     */
 int blp_batch_plan(const blp_batch* b, int64_t* lo, int64_t* hi, int* chunks, int* block,
