@@ -1,7 +1,9 @@
 """Tuning sweep (not a test, not the bench): build the config-2 graph and examples once, then
 for each env setting (JSON list of dicts in SWEEP, read when the graph / batch is created)
 re-create the device graph and batches and time the user and business scorers with the
-library's own HIP-event timers. Every setting's CN / Jaccard / AA must equal the first's.
+library's own HIP-event timers, each pass alone (batches have their own streams and would
+otherwise overlap). SWEEP_STEP=1 also times the co-scheduled step (blp_batches_score, wall).
+Every setting's CN / Jaccard / AA must equal the first's.
 
   SWEEP='[{}, {"BLP_HOT_DENSITY": "32"}]' python profiles/sweep.py
 """
@@ -42,10 +44,18 @@ for s in settings:
     blp.device_sync(0)
     for _, bt, _ in passes:
         bt.stats_reset()
-    for _ in range(steps):
-        for _, bt, m in passes:
+    for _, bt, m in passes:  # each pass alone
+        for _ in range(steps):
             bt.score(m)
-    blp.device_sync(0)
+        blp.device_sync(0)
+    iso = {name: (bt.stats(0), bt.stats(1)) for name, bt, _ in passes}
+    step_ms = None
+    if os.environ.get("SWEEP_STEP"):
+        t = time.perf_counter()
+        for _ in range(steps):
+            G.score_batches([(bt, m) for _, bt, m in passes])
+        blp.device_sync(0)
+        step_ms = (time.perf_counter() - t) / steps * 1e3
     prof = None
     if os.environ.get("SWEEP_PROF"):  # experiment build with -DBLP_PROF: per-phase clocks of k_score
         import ctypes
@@ -60,11 +70,12 @@ for s in settings:
             tot = sum(buf[:9]) or 1
             print(json.dumps({"phases_" + name: [round(buf[i] / tot, 3) for i in range(9)], "clk": tot}), flush=True)
     row = {"setting": s, "graph_s": round(tg, 2)}
+    if step_ms is not None:
+        row["step_ms"] = round(step_ms, 4)
     res = {}
     for name, bt, m in passes:
-        ms, n = bt.stats(0)
+        (ms, n), (gms, gn) = iso[name]
         row[name + "_ms"] = round(ms / max(n, 1), 4)
-        gms, gn = bt.stats(1)
         row[name + "_group_ms"] = round(gms / max(gn, 1), 4)
         res[name] = bt.fetch(m)
     if ref is None:
