@@ -118,18 +118,6 @@ __device__ inline void tk_compact(double* top_s, int* top_c, double* buf_s, int*
   __builtin_amdgcn_wave_barrier();
 }
 
-__device__ inline bool excluded(const TopkArgs& a, int64_t u, int col) {
-  if (!a.ex_off) return false;
-  int64_t lo = a.ex_off[u], hi = a.ex_off[u + 1];
-  while (lo < hi) {
-    const int64_t mid = (lo + hi) >> 1;
-    const int c = a.ex_col[mid];
-    if (c == col) return true;
-    if (c < col) lo = mid + 1; else hi = mid;
-  }
-  return false;
-}
-
 template <int KPAD>
 __global__ __launch_bounds__(TK_WAVES * 64) void k_svd_topk(TopkArgs a) {
   __shared__ double s_top[TK_WAVES][16][TK_MAX];
@@ -166,6 +154,18 @@ __global__ __launch_bounds__(TK_WAVES * 64) void k_svd_topk(TopkArgs a) {
     for (int s = 0; s < KS; ++s) af[s] = row >= 0 ? a.us[row * KPAD + 4 * s + (lane >> 4)] : 0.0;
   }
   const int my_row = lane >> 4;  // the C/D rows of this lane are my_row + 4 r
+  // Exclusions (the user's own reviews, sorted): lane r < 16 walks row r's list alongside the
+  // tiles (ex_p = position, ex_n = next excluded column) and publishes a 16-bit mask of the
+  // tile's excluded columns; a global load happens only when a tile holds one (~deg times per
+  // row), instead of a binary search per threshold-passing score.
+  int64_t ex_p = 0, ex_e = 0;
+  int ex_n = INT32_MAX;
+  if (a.ex_off && lane < 16 && u0 + lane < a.n_users) {
+    ex_p = a.ex_off[u0 + lane];
+    ex_e = a.ex_off[u0 + lane + 1];
+    while (ex_p < ex_e && a.ex_col[ex_p] < cb) ++ex_p;
+    ex_n = ex_p < ex_e ? a.ex_col[ex_p] : INT32_MAX;
+  }
   // B[k = 4 s + (lane >> 4)][j = lane & 15] = Vt[k][c0 + j]  (padded columns are zero);
   // the next tile's fragments are in flight while this tile's MFMA chain runs
   const double* vt_lane = a.vt + (int64_t)(lane >> 4) * a.ncol_pad + (lane & 15);
@@ -183,12 +183,18 @@ __global__ __launch_bounds__(TK_WAVES * 64) void k_svd_topk(TopkArgs a) {
     for (int s = 0; s < KS; ++s) d = __builtin_amdgcn_mfma_f64_16x16x4f64(af[s], bf[s], d, 0, 0, 0);
 #pragma unroll
     for (int s = 0; s < KS; ++s) bf[s] = nb[s];
+    unsigned exm = 0;  // lane r < 16: excluded columns of row r in this tile
+    while (ex_n < c0 + 16) {
+      if (ex_n >= c0) exm |= 1u << (ex_n - c0);  // (a duplicate or out-of-order id is skipped)
+      ex_n = ++ex_p < ex_e ? a.ex_col[ex_p] : INT32_MAX;
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = my_row + 4 * r;
       const double sc = d[r];
-      if (col < ce && u0 + row < a.n_users && better(sc, col, s_th[w][row], s_thc[w][row]) &&
-          !excluded(a, u0 + row, col)) {
+      const unsigned rm = (unsigned)__shfl((int)exm, row, 64);
+      if (col < ce && u0 + row < a.n_users && !((rm >> (lane & 15)) & 1u) &&
+          better(sc, col, s_th[w][row], s_thc[w][row])) {
         const int slot = atomicAdd(&s_nb[w][row], 1);
         s_buf[w][row][slot] = sc;
         s_bufc[w][row][slot] = col;
@@ -196,10 +202,15 @@ __global__ __launch_bounds__(TK_WAVES * 64) void k_svd_topk(TopkArgs a) {
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    // compact rows whose buffer could overflow on the next tile
-    for (int row = 0; row < 16; ++row) {
+    // compact rows whose buffer could overflow on the next tile (one LDS read and a ballot
+    // find them; the loop visits only those rows)
+    const int my_nb = lane < 16 ? s_nb[w][lane] : 0;
+    unsigned long long due = __ballot(lane < 16 && (my_nb > TK_BUF - 16 || (c0 + 16 >= ce && my_nb > 0)));
+    while (due) {
+      const int row = __builtin_ctzll(due);
+      due &= due - 1;
       const int nb = s_nb[w][row];
-      if (nb > TK_BUF - 16 || (c0 + 16 >= ce && nb > 0)) {
+      {
         tk_compact(s_top[w][row], s_topc[w][row], s_buf[w][row], s_bufc[w][row], nb, topk, lane, &s_th[w][row],
                    &s_thc[w][row]);
         if (lane == 0) s_nb[w][row] = 0;
