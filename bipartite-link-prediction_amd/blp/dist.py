@@ -15,6 +15,7 @@ torch is plumbing here (process group, device buffers for the collective); the g
 every kernel live in libblp.so.
 """
 import os
+import sys
 
 import numpy as np
 
@@ -35,16 +36,27 @@ class Dist:
             import torch.distributed as td
 
             self.td = td
-            if exchange and os.environ.get("BLP_EXCHANGE_BACKEND", "nccl") == "nccl":
-                import torch
+            # gloo's C++ layer prints its connection banner on stdout; the bench's stdout is
+            # its one JSON line, so stdout is pointed at stderr while the groups form
+            sys.stdout.flush()
+            saved = os.dup(1)
+            os.dup2(2, 1)
+            try:
+                if exchange and os.environ.get("BLP_EXCHANGE_BACKEND", "nccl") == "nccl":
+                    import torch
 
-                torch.cuda.set_device(self.local)
-                td.init_process_group("nccl")
-                self.cpu_group = td.new_group(backend="gloo")
-                self.backend = "nccl"
-            else:
-                td.init_process_group("gloo")
-                self.backend = "gloo"
+                    torch.cuda.set_device(self.local)
+                    td.init_process_group("nccl")
+                    self.cpu_group = td.new_group(backend="gloo")
+                    self.backend = "nccl"
+                else:
+                    td.init_process_group("gloo")
+                    self.backend = "gloo"
+                td.barrier(group=self.cpu_group)  # every rank connected before stdout returns
+            finally:
+                sys.stdout.flush()
+                os.dup2(saved, 1)
+                os.close(saved)
         else:
             self.backend = None
 
