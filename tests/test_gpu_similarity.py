@@ -225,3 +225,29 @@ def test_business_fix_adamic_matches_oracle(gpu):
     adj = O.load_edge_list(os.path.join(d, "graph.txt"))
     exp = O.business(ex, adj, [O.BUGGY_B_ADAMIC])[0]
     assert_same_scores(got, exp, "adamic_adar")
+
+
+@pytest.mark.parametrize("variant", [None, "2"])
+def test_coscheduled_passes_match_single_passes(gpu, variant, monkeypatch):
+    # blp_batches_score: the user and business passes of one step run concurrently on their
+    # own streams (the large-universe scorer held to a share of the CUs); results must equal
+    # each pass scored alone, repeated steps included
+    if variant:
+        monkeypatch.setenv("BLP_VARIANT", variant)  # the large-universe block scorer on this graph
+    rng = np.random.default_rng(21)
+    a, b = bipartite_edges(rng, 20000, 1500, 200000)
+    G = blp.DeviceGraph(a, b)
+    nu = G.n - len(np.unique(b))
+    x = np.repeat(rng.choice(nu, 300, replace=False), 40).astype(np.int32)
+    y = rng.integers(nu, G.n, len(x)).astype(np.int32)
+    alone_u = G.score_pairs(x, y, 7)
+    alone_b = G.score_pairs(y, x, 3)
+    ub, bb = G.batch(x, y), G.batch(y, x)
+    for _ in range(3):
+        G.score_batches([(ub, 7), (bb, 3)])
+    got_u, got_b = ub.fetch(7), bb.fetch(3)
+    for k in ("cn", "jaccard", "adamic"):
+        np.testing.assert_array_equal(got_u[k], alone_u[k])
+    for k in ("cn", "jaccard"):
+        np.testing.assert_array_equal(got_b[k], alone_b[k])
+    _check_against_oracle(a, b, x, y)
