@@ -1991,6 +1991,7 @@ struct blp_batch {
   hipStream_t stream = nullptr;
   blp::DevBuf cnt, off, active, scratch;
   int cus = 0;  // CUs the persistent block scorer may occupy (0: all; set by blp_batches_score)
+  int64_t work_elems = 0;  // planned build + scan elements (co-scheduling estimate)
 };
 
 using namespace blp;
@@ -2193,6 +2194,7 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   if (const char* e = getenv("BLP_DQ")) b->dq = std::min(DQ_MAX, std::max(1, atoi(e)));  // tuning knob
   // ---- heavy sources: build work far above the per-workgroup share goes to k_heavy
   const int64_t total_work = std::accumulate(work.begin(), work.end(), (int64_t)0) + scan_work;
+  b->work_elems = total_work;
   // a wave is ~16x slower on one source than a 1024-thread block: split much earlier there
   int64_t item_work = b->wave ? std::max<int64_t>(4096, total_work / std::max<int64_t>(4 * n_wg, 1))
                               : std::max<int64_t>(16384, total_work / std::max<int64_t>(4 * n_wg, 1));
@@ -2503,26 +2505,38 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
 
 // Several passes of one step enqueued together (similarity.main: the user and the business
 // pass), each on its own stream. A large-universe batch (one 160 KiB-LDS workgroup per CU,
-// the user side) holds every CU it lands on until it ends, so beside short-row batches it is
-// given a share of the CUs and the short-row scorer and the grouping kernels run on the rest
-// from the start, instead of queueing behind it. Share: 3/4 of the CUs (BLP_COSCHED_CUS
-// overrides) -- config 2 on MI355X: 2.93 ms per step with all CUs, 2.69 ms at 192 of 256
-// (160: 2.96, 176: 2.79, 224: 2.87, 240: 3.03).
+// the user side) holds every CU it lands on until it ends, so beside other batches it is given
+// a share of the CUs and the short-row scorer and the grouping kernels run on the rest from
+// the start, instead of queueing behind it.
+//
+// Share = n_cu * t_L / (t_L + KAPPA * t_O), clamped to [n_cu / 2, n_cu], from per-batch time
+// estimates: planned elements / rate (large-universe scorer ~1.2e9 elements per ms, others
+// ~1.8e8) + ~3.9e-8 ms per pair of bucket grouping for the others. KAPPA = 0.38: a
+// latency-bound short-row pass does the same work in fewer CU-milliseconds on a few CUs
+// than spread over the chip. Calibrated on config 2 (MI355X): the estimate gives 192 of 256
+// CUs, the measured optimum (2.73 ms per step; all CUs 2.93, 160: 2.96, 176: 2.79, 208:
+// 2.78, 224: 2.87, 240: 3.03). A small second pass leaves the large one (nearly) the whole
+// chip. BLP_COSCHED_CUS overrides the share.
 int blp_batches_score(blp_graph* g, int n, blp_batch* const* bs, const uint32_t* masks) {
   BLP_CHECK(g && n >= 0 && (n == 0 || (bs && masks)), BLP_E_ARG, "blp_batches_score: bad arguments");
-  bool any_large = false, any_other = false;
+  auto is_large = [](const blp_batch* b) { return b->variant == V_LARGE && !b->split && !b->global && !b->wave; };
+  double t_large = 0.0, t_other = 0.0;
   for (int i = 0; i < n; ++i) {
     BLP_CHECK(bs[i] && bs[i]->g == g, BLP_E_ARG, "blp_batches_score: graph/batch mismatch");
-    const bool large = bs[i]->variant == V_LARGE && !bs[i]->split && !bs[i]->global && !bs[i]->wave;
-    any_large |= large;
-    any_other |= !large;
+    if (is_large(bs[i]))
+      t_large += (double)bs[i]->work_elems / 1.2e9;
+    else
+      t_other += (double)bs[i]->work_elems / 1.8e8 + 3.9e-8 * (double)bs[i]->n_pairs;
   }
-  int share = g->n_cu * 3 / 4;
+  int share = g->n_cu;
+  if (t_large > 0.0 && t_other > 0.0) {
+    const double f = t_large / (t_large + 0.38 * t_other);
+    share = std::max(g->n_cu / 2, std::min(g->n_cu, (int)std::lround(f * g->n_cu / 8.0) * 8));
+  }
   if (const char* e = getenv("BLP_COSCHED_CUS")) share = atoi(e);  // tuning knob
   for (int i = 0; i < n; ++i) {
     blp_batch* b = bs[i];
-    const bool large = b->variant == V_LARGE && !b->split && !b->global && !b->wave;
-    b->cus = (large && any_large && any_other) ? share : 0;
+    b->cus = is_large(b) && t_other > 0.0 ? share : 0;
     const int rc = blp_batch_score(g, b, masks[i]);
     b->cus = 0;
     if (rc) return rc;
