@@ -85,8 +85,6 @@ struct blp_graph {
   // host mirrors used only for launch planning (bitmap universe bounds)
   std::vector<int64_t> h_rp;
   std::vector<int32_t> h_ci;
-  // grouping scratch (per handle, reused by every batch)
-  blp::DevBuf cnt, off, cursor, active, scratch;
   blp::KernelTimer timers[blp::K_COUNT];
 };
 

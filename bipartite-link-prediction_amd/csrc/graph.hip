@@ -300,11 +300,6 @@ int blp_graph_destroy(blp_graph* g) {
   (void)hipSetDevice(g->device);
   if (g->stream) (void)hipStreamSynchronize(g->stream);
   for (auto& t : g->timers) timer_release(t);
-  g->cnt.release();
-  g->off.release();
-  g->cursor.release();
-  g->active.release();
-  g->scratch.release();
   free_hot_index(g);
   if (g->d_rp) (void)hipFree(g->d_rp);
   if (g->d_ci) (void)hipFree(g->d_ci - CI_PAD);
