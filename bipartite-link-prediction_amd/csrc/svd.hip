@@ -59,7 +59,9 @@ __global__ __launch_bounds__(256) void k_svd_pairs(const double* __restrict__ us
 // ---------------------------------------------------------------- dense top-k
 constexpr int TK_WAVES = 4;        // waves per block; each owns 16 users
 constexpr int TK_MAX = 32;         // largest top-k
-constexpr int TK_BUF = 48;         // candidate buffer per user (+16 per tile at most)
+constexpr int TK_BUF = 16;         // compaction once a user's buffer holds more (+16 per tile at most:
+                                   // TK_MAX + TK_BUF + 16 <= 64 entries, one per lane)
+constexpr int TK_GROUP = 16;       // tiles per LDS exclusion-mask refill
 
 struct TopkArgs {
   const double* us;        // [n_rows][kpad]
@@ -78,148 +80,229 @@ struct TopkArgs {
 // better = higher score, then lower column
 __device__ inline bool better(double s, int c, double t, int tc) { return s > t || (s == t && c < tc); }
 
-// Keep the best `topk` of top[0..topk) + buf[0..nb) in top (wave-cooperative rank select).
-__device__ inline void tk_compact(double* top_s, int* top_c, double* buf_s, int* buf_c, int nb, int topk, int lane,
-                                  double* th_s, int* th_c) {
-  const int n = topk + nb;
-  double vs[2];
-  int vc[2], rk[2];
-  for (int q = 0; q < 2; ++q) {
-    const int i = lane + 64 * q;
-    vs[q] = -DBL_MAX;
-    vc[q] = INT32_MAX;
-    rk[q] = INT32_MAX;
-    if (i < n) {
-      vs[q] = i < topk ? top_s[i] : buf_s[i - topk];
-      vc[q] = i < topk ? top_c[i] : buf_c[i - topk];
-      int r = 0;
-      for (int j = 0; j < n; ++j) {
-        const double s = j < topk ? top_s[j] : buf_s[j - topk];
-        const int c = j < topk ? top_c[j] : buf_c[j - topk];
-        r += better(s, c, vs[q], vc[q]) || (s == vs[q] && c == vc[q] && j < i);
-      }
-      rk[q] = r;
-    }
+// Keep the best `topk` of top[0..topk) + buf[0..nb) in top: one entry per lane (topk + nb <=
+// 64), a 64-lane bitonic sort through cross-lane shuffles (21 compare-exchange stages, no
+// LDS traffic beyond the loads and the stores), better-first; the k-th entry becomes the
+// row's threshold.
+__device__ inline void tk_compact(double* top_s, int* top_c, const double* buf_s, const int* buf_c, int nb, int topk,
+                                  int lane, double* th_s, int* th_c) {
+  double v = -DBL_MAX;
+  int c = INT32_MAX;
+  if (lane < topk) {
+    v = top_s[lane];
+    c = top_c[lane];
+  } else if (lane < topk + nb) {
+    v = buf_s[lane - topk];
+    c = buf_c[lane - topk];
   }
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  for (int q = 0; q < 2; ++q)
-    if (rk[q] < topk) {
-      top_s[rk[q]] = vs[q];
-      top_c[rk[q]] = vc[q];
+#pragma unroll
+  for (int k2 = 2; k2 <= 64; k2 <<= 1)
+#pragma unroll
+    for (int j = k2 >> 1; j > 0; j >>= 1) {
+      const double pv = __shfl_xor(v, j, 64);
+      const int pc = __shfl_xor(c, j, 64);
+      const bool first = ((lane & j) == 0) == ((lane & k2) == 0);  // this lane keeps the better one
+      if (first == better(pv, pc, v, c)) {
+        v = pv;
+        c = pc;
+      }
     }
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  __builtin_amdgcn_wave_barrier();
+  const double tv = __shfl(v, topk - 1, 64);
+  const int tc = __shfl(c, topk - 1, 64);
+  if (lane < topk) {
+    top_s[lane] = v;
+    top_c[lane] = c;
+  }
   if (lane == 0) {
-    *th_s = top_s[topk - 1];
-    *th_c = top_c[topk - 1];
+    *th_s = tv;
+    *th_c = tc;
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
 }
 
-template <int KPAD>
-__global__ __launch_bounds__(TK_WAVES * 64) void k_svd_topk(TopkArgs a) {
-  __shared__ double s_top[TK_WAVES][16][TK_MAX];
-  __shared__ int s_topc[TK_WAVES][16][TK_MAX];
-  __shared__ double s_buf[TK_WAVES][16][TK_BUF + 16];
-  __shared__ int s_bufc[TK_WAVES][16][TK_BUF + 16];
-  __shared__ int s_nb[TK_WAVES][16];
-  __shared__ double s_th[TK_WAVES][16];
-  __shared__ int s_thc[TK_WAVES][16];
+// RT row tiles per wave (16 RT users): every B fragment fetched feeds RT MFMA chains, so the
+// Vt stream per score is 8 KiB / (256 RT) -- RT = 2 halves the L2/MALL traffic of RT = 1.
+// EXP = 1 (timing experiment only, BLP_SVD_EXP=1): the MFMA chains and fragment loads without
+// the top-k epilogue (results are NOT valid)
+template <int KPAD, int RT, int WAVES, int EXP = 0>
+__global__ __launch_bounds__(WAVES * 64) void k_svd_topk(TopkArgs a) {
+  constexpr int R = 16 * RT;  // users per wave
+  __shared__ double s_top[WAVES][R][TK_MAX];
+  __shared__ int s_topc[WAVES][R][TK_MAX];
+  __shared__ double s_buf[WAVES][R][TK_BUF + 16];
+  __shared__ int s_bufc[WAVES][R][TK_BUF + 16];
+  __shared__ int s_nb[WAVES][R];
+  __shared__ double s_th[WAVES][R];
+  __shared__ int s_thc[WAVES][R];
+  __shared__ unsigned short s_exm[WAVES][R][TK_GROUP];
   constexpr int KS = KPAD / 4;  // MFMA k-steps
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t u0 = ((int64_t)blockIdx.x * TK_WAVES + w) * 16;
+  const int64_t u0 = ((int64_t)blockIdx.x * WAVES + w) * R;
   if (u0 >= a.n_users) return;  // whole wave idle (no block barriers below)
   const int chunk = blockIdx.y;
   const int64_t cb = (int64_t)chunk * a.chunk, ce = min(a.n_cols, cb + a.chunk);
   const int topk = a.topk;
-  for (int i = lane; i < 16 * TK_MAX; i += 64) {
+  for (int i = lane; i < R * TK_MAX; i += 64) {
     s_top[w][i / TK_MAX][i % TK_MAX] = -DBL_MAX;
     s_topc[w][i / TK_MAX][i % TK_MAX] = INT32_MAX;
   }
-  if (lane < 16) {
+  if (lane < R) {
     s_nb[w][lane] = 0;
     s_th[w][lane] = -DBL_MAX;
     s_thc[w][lane] = INT32_MAX;
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
-  // A fragments: A[i = lane & 15][k = 4 s + (lane >> 4)] = US[users[u0 + i]][k]
-  double af[KS];
-  {
-    const int64_t ui = u0 + (lane & 15);
+  // A fragments of tile t: A[i = lane & 15][k = 4 s + (lane >> 4)] = US[users[u0 + 16 t + i]][k]
+  double af[RT][KS];
+#pragma unroll
+  for (int t = 0; t < RT; ++t) {
+    const int64_t ui = u0 + 16 * t + (lane & 15);
     const int64_t row = ui < a.n_users ? a.users[ui] : -1;
 #pragma unroll
-    for (int s = 0; s < KS; ++s) af[s] = row >= 0 ? a.us[row * KPAD + 4 * s + (lane >> 4)] : 0.0;
+    for (int s = 0; s < KS; ++s) af[t][s] = row >= 0 ? a.us[row * KPAD + 4 * s + (lane >> 4)] : 0.0;
   }
-  const int my_row = lane >> 4;  // the C/D rows of this lane are my_row + 4 r
-  // Exclusions (the user's own reviews, sorted): lane r < 16 walks row r's list alongside the
-  // tiles (ex_p = position, ex_n = next excluded column) and publishes a 16-bit mask of the
-  // tile's excluded columns; a global load happens only when a tile holds one (~deg times per
-  // row), instead of a binary search per threshold-passing score.
+  const int my_row = lane >> 4;  // the C/D rows of this lane in tile t are 16 t + my_row + 4 r
+  // Exclusions (the user's own reviews, sorted): every TK_GROUP tiles, lane r < R writes row
+  // r's excluded columns of the next TK_GROUP * 16 columns into an LDS mask (one 16-bit word
+  // per tile), reading its sorted list 4 entries at a time; each tile then takes its mask with
+  // one LDS read. The global loads (and their vmcnt wait, which also waits for the B fragments
+  // in flight: vmcnt counts in issue order) happen once per group, not inside the tile loop.
   int64_t ex_p = 0, ex_e = 0;
-  int ex_n = INT32_MAX;
-  if (a.ex_off && lane < 16 && u0 + lane < a.n_users) {
+  if (a.ex_off && lane < R && u0 + lane < a.n_users) {
     ex_p = a.ex_off[u0 + lane];
     ex_e = a.ex_off[u0 + lane + 1];
     while (ex_p < ex_e && a.ex_col[ex_p] < cb) ++ex_p;
-    ex_n = ex_p < ex_e ? a.ex_col[ex_p] : INT32_MAX;
   }
-  // B[k = 4 s + (lane >> 4)][j = lane & 15] = Vt[k][c0 + j]  (padded columns are zero);
-  // the next tile's fragments are in flight while this tile's MFMA chain runs
-  const double* vt_lane = a.vt + (int64_t)(lane >> 4) * a.ncol_pad + (lane & 15);
-  double bf[KS];
+  auto ex_group = [&](int64_t g0) __attribute__((always_inline)) {
+    if (lane < R) {
 #pragma unroll
-  for (int s = 0; s < KS; ++s) bf[s] = vt_lane[(int64_t)(4 * s) * a.ncol_pad + cb];
-  for (int64_t c0 = cb; c0 < ce; c0 += 16) {
-    double4_t d = {0.0, 0.0, 0.0, 0.0};
-    const int col = (int)(c0 + (lane & 15));
-    const int64_t cn = c0 + 16 < ce ? c0 + 16 : c0;
-    double nb[KS];
+      for (int q = 0; q < TK_GROUP; ++q) s_exm[w][lane][q] = 0;
+      const int64_t g1 = g0 + 16 * TK_GROUP;
+      while (ex_p < ex_e) {
+        int v[4];
 #pragma unroll
-    for (int s = 0; s < KS; ++s) nb[s] = vt_lane[(int64_t)(4 * s) * a.ncol_pad + cn];
+        for (int q = 0; q < 4; ++q) v[q] = ex_p + q < ex_e ? a.ex_col[ex_p + q] : INT32_MAX;
+        int used = 0;
 #pragma unroll
-    for (int s = 0; s < KS; ++s) d = __builtin_amdgcn_mfma_f64_16x16x4f64(af[s], bf[s], d, 0, 0, 0);
-#pragma unroll
-    for (int s = 0; s < KS; ++s) bf[s] = nb[s];
-    unsigned exm = 0;  // lane r < 16: excluded columns of row r in this tile
-    while (ex_n < c0 + 16) {
-      if (ex_n >= c0) exm |= 1u << (ex_n - c0);  // (a duplicate or out-of-order id is skipped)
-      ex_n = ++ex_p < ex_e ? a.ex_col[ex_p] : INT32_MAX;
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = my_row + 4 * r;
-      const double sc = d[r];
-      const unsigned rm = (unsigned)__shfl((int)exm, row, 64);
-      if (col < ce && u0 + row < a.n_users && !((rm >> (lane & 15)) & 1u) &&
-          better(sc, col, s_th[w][row], s_thc[w][row])) {
-        const int slot = atomicAdd(&s_nb[w][row], 1);
-        s_buf[w][row][slot] = sc;
-        s_bufc[w][row][slot] = col;
+        for (int q = 0; q < 4; ++q)
+          if (v[q] < g1) {  // sorted: a prefix of the four
+            ++used;
+            if (v[q] >= g0) s_exm[w][lane][(v[q] - g0) >> 4] |= (unsigned short)(1u << ((v[q] - g0) & 15));
+          }
+        ex_p += used;
+        if (used < 4) break;
       }
     }
+  };
+  // B[k = 4 s + (lane >> 4)][j = lane & 15] = Vt[k][c0 + j]  (padded columns are zero).
+  // Two fragment sets alternate (tiles c0 and c0 + 16): the loads of one tile are issued a
+  // whole tile (16 dependent MFMAs) before its chain needs them, and no register copy sits
+  // between a load and its use (a copy made the compiler wait on the just-issued loads at
+  // the end of every tile: vmcnt(0), i.e. no prefetch at all).
+  const double* vt_lane = a.vt + (int64_t)(lane >> 4) * a.ncol_pad + (lane & 15);
+  double th[RT][4];  // thresholds of this lane's C/D rows (mirrors s_th / s_thc)
+  int thc[RT][4];
+#pragma unroll
+  for (int t = 0; t < RT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      th[t][r] = -DBL_MAX;
+      thc[t][r] = INT32_MAX;
+    }
+  auto load_b = [&](double* bf, int64_t c) __attribute__((always_inline)) {
+#pragma unroll
+    for (int s = 0; s < KS; ++s) bf[s] = vt_lane[(int64_t)(4 * s) * a.ncol_pad + c];
+    // keep the scheduler from sinking these loads into the previous tile's MFMA chain (it
+    // does so to shorten live ranges, which brings the wait back)
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto tile = [&](int64_t c0, const double* bf) __attribute__((always_inline)) {
+    double4_t d[RT];
+#pragma unroll
+    for (int t = 0; t < RT; ++t) d[t] = double4_t{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+      for (int t = 0; t < RT; ++t) d[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[t][s], bf[s], d[t], 0, 0, 0);
+    const int col = (int)(c0 + (lane & 15));
+    if (EXP == 1) {
+#pragma unroll
+      for (int t = 0; t < RT; ++t) th[t][0] += d[t][0] + d[t][1] + d[t][2] + d[t][3];
+      return;
+    }
+    // lane r < R: excluded columns of row r in this tile
+    const unsigned exm = a.ex_off && lane < R ? s_exm[w][lane][((c0 - cb) >> 4) % TK_GROUP] : 0u;
+    // Thresholds live in registers (they change only when a row is compacted), so a tile
+    // whose scores all fall below them costs a few VALU compares and one ballot: no LDS
+    // round trip, no cross-lane shuffle unless the tile holds an excluded column.
+    const bool anyex = __ballot(exm != 0) != 0;  // wave-uniform
+    bool pass[RT][4];
+    bool anyp = false;
+#pragma unroll
+    for (int t = 0; t < RT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * t + my_row + 4 * r;
+        bool ok = col < ce && u0 + row < a.n_users && better(d[t][r], col, th[t][r], thc[t][r]);
+        if (anyex) {
+          const unsigned rm = (unsigned)__shfl((int)exm, row, 64);
+          ok = ok && !((rm >> (lane & 15)) & 1u);
+        }
+        pass[t][r] = ok;
+        anyp |= ok;
+      }
+    const bool last = c0 + 16 >= ce;
+    if (__ballot(anyp) == 0 && !last) return;  // wave-uniform: nothing enters any list
+#pragma unroll
+    for (int t = 0; t < RT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (pass[t][r]) {
+          const int row = 16 * t + my_row + 4 * r;
+          const int slot = atomicAdd(&s_nb[w][row], 1);
+          s_buf[w][row][slot] = d[t][r];
+          s_bufc[w][row][slot] = col;
+        }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
     // compact rows whose buffer could overflow on the next tile (one LDS read and a ballot
     // find them; the loop visits only those rows)
-    const int my_nb = lane < 16 ? s_nb[w][lane] : 0;
-    unsigned long long due = __ballot(lane < 16 && (my_nb > TK_BUF - 16 || (c0 + 16 >= ce && my_nb > 0)));
+    const int my_nb = lane < R ? s_nb[w][lane] : 0;
+    unsigned long long due = __ballot(lane < R && (my_nb > TK_BUF || (last && my_nb > 0)));
+    if (!due) return;
     while (due) {
       const int row = __builtin_ctzll(due);
       due &= due - 1;
       const int nb = s_nb[w][row];
-      {
-        tk_compact(s_top[w][row], s_topc[w][row], s_buf[w][row], s_bufc[w][row], nb, topk, lane, &s_th[w][row],
-                   &s_thc[w][row]);
-        if (lane == 0) s_nb[w][row] = 0;
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-      }
+      tk_compact(s_top[w][row], s_topc[w][row], s_buf[w][row], s_bufc[w][row], nb, topk, lane, &s_th[w][row],
+                 &s_thc[w][row]);
+      if (lane == 0) s_nb[w][row] = 0;
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
     }
+#pragma unroll
+    for (int t = 0; t < RT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        th[t][r] = s_th[w][16 * t + my_row + 4 * r];
+        thc[t][r] = s_thc[w][16 * t + my_row + 4 * r];
+      }
+  };
+  double b0[KS], b1[KS];
+  load_b(b0, cb);
+  for (int64_t c0 = cb; c0 < ce; c0 += 32) {
+    if (a.ex_off && ((c0 - cb) >> 4) % TK_GROUP == 0) ex_group(c0);  // (TK_GROUP is even)
+    const int64_t c1 = c0 + 16;
+    load_b(b1, c1 < ce ? c1 : c0);  // (past the chunk: a harmless re-read)
+    tile(c0, b0);
+    if (c1 >= ce) break;
+    load_b(b0, c1 + 16 < ce ? c1 + 16 : c1);
+    tile(c1, b1);
   }
-  for (int i = lane; i < 16 * topk; i += 64) {
+  if (EXP == 1 && th[0][0] == 1.2345e300) a.part_score[0] = th[0][0];  // keeps the chains live
+  for (int i = lane; i < R * topk; i += 64) {
     const int row = i / topk, q = i % topk;
     const int64_t u = u0 + row;
     if (u < a.n_users) {
@@ -357,8 +440,34 @@ int blp_svd_topk(blp_svd* h, const int32_t* users, int64_t n_users, const int64_
     BLP_CHECK(users[i] >= 0 && users[i] < h->n_rows, BLP_E_ARG, "blp_svd_topk: user row out of range");
   BLP_HIP(hipSetDevice(h->device));
   // chunks: enough blocks to fill the chip, >= 16 tiles each
-  const int64_t ublocks = (n_users + 16 * TK_WAVES - 1) / (16 * TK_WAVES);
-  int n_chunks = (int)std::max<int64_t>(1, std::min<int64_t>((h->n_cu * 8 + ublocks - 1) / ublocks, h->ncol_pad / 256));
+  // default: one 16-user tile per wave, 4 waves per block. Measured alternatives (config 4):
+  // BLP_SVD_RT=2 (two tiles per wave, 2 waves per block, same LDS: 1 wave per SIMD) 15.4 ms
+  // against 10.0 ms; two accumulation chains per tile (halving the dependent MFMA chain)
+  // 10.2 ms
+  const char* rt_env = getenv("BLP_SVD_RT");
+  const int rt = rt_env && atoi(rt_env) == 2 ? 2 : 1;
+  const int waves = rt == 1 ? TK_WAVES : TK_WAVES / 2;
+  const int64_t upb = 16 * rt * waves;  // users per block
+  const int64_t ublocks = (n_users + upb - 1) / upb;
+  // Column chunks: just enough (user block, chunk) blocks to occupy every block slot of the
+  // chip ONCE. Each chunk restarts its users' top-k lists from an empty threshold, and the
+  // insertions a list takes grow as C k (1 + ln(N / (C k))) over C chunks (config 4: 14
+  // chunks 10.0 ms, 3 chunks 7.2 ms), so more chunks than slots only cost.
+  const void* kfn = nullptr;
+#define BLP_SVD_FN(KP) \
+  kfn = rt == 1 ? (const void*)&k_svd_topk<KP, 1, TK_WAVES> : (const void*)&k_svd_topk<KP, 2, TK_WAVES / 2>;
+  switch (h->kpad) {
+    case 16: BLP_SVD_FN(16); break;
+    case 32: BLP_SVD_FN(32); break;
+    case 48: BLP_SVD_FN(48); break;
+    case 64: BLP_SVD_FN(64); break;
+    default: BLP_SVD_FN(128); break;
+  }
+#undef BLP_SVD_FN
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, waves * 64, 0) != hipSuccess || per_cu < 1) per_cu = 1;
+  int n_chunks = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)h->n_cu * per_cu / ublocks, h->ncol_pad / 256));
+  if (const char* e = getenv("BLP_SVD_CHUNKS")) n_chunks = std::max(1, std::min(atoi(e), (int)std::max<int64_t>(1, h->ncol_pad / 256)));
   const int64_t chunk = ((h->n_cols + n_chunks - 1) / n_chunks + 15) / 16 * 16;
   n_chunks = (int)((h->n_cols + chunk - 1) / chunk);
   const int64_t nex = ex_off ? ex_off[n_users] : 0;
@@ -386,14 +495,22 @@ int blp_svd_topk(blp_svd* h, const int32_t* users, int64_t n_users, const int64_
   hipEvent_t t0;
   int rc = timer_begin(h->t_topk, h->stream, &t0);
   if (rc) return cleanup(), rc;
-  const dim3 grid((unsigned)ublocks, (unsigned)n_chunks), block(TK_WAVES * 64);
+  const dim3 grid((unsigned)ublocks, (unsigned)n_chunks), block(waves * 64);
+#define BLP_SVD_TOPK(KP)                                                                        \
+  if (getenv("BLP_SVD_EXP"))                                                                    \
+    hipLaunchKernelGGL((k_svd_topk<KP, 1, TK_WAVES, 1>), grid, block, 0, h->stream, a);         \
+  else if (rt == 1)                                                                             \
+    hipLaunchKernelGGL((k_svd_topk<KP, 1, TK_WAVES>), grid, block, 0, h->stream, a);            \
+  else                                                                                          \
+    hipLaunchKernelGGL((k_svd_topk<KP, 2, TK_WAVES / 2>), grid, block, 0, h->stream, a);
   switch (h->kpad) {
-    case 16: hipLaunchKernelGGL(k_svd_topk<16>, grid, block, 0, h->stream, a); break;
-    case 32: hipLaunchKernelGGL(k_svd_topk<32>, grid, block, 0, h->stream, a); break;
-    case 48: hipLaunchKernelGGL(k_svd_topk<48>, grid, block, 0, h->stream, a); break;
-    case 64: hipLaunchKernelGGL(k_svd_topk<64>, grid, block, 0, h->stream, a); break;
-    default: hipLaunchKernelGGL(k_svd_topk<128>, grid, block, 0, h->stream, a); break;
+    case 16: BLP_SVD_TOPK(16); break;
+    case 32: BLP_SVD_TOPK(32); break;
+    case 48: BLP_SVD_TOPK(48); break;
+    case 64: BLP_SVD_TOPK(64); break;
+    default: BLP_SVD_TOPK(128); break;
   }
+#undef BLP_SVD_TOPK
   hipLaunchKernelGGL(k_svd_merge, dim3((unsigned)n_users), dim3(64), 0, h->stream, (const double*)d_ps,
                      (const int32_t*)d_pc, n_users, n_chunks, topk, (double*)d_os, (int32_t*)d_oc);
   if (hipGetLastError() != hipSuccess) {
