@@ -204,6 +204,11 @@ __global__ __launch_bounds__(WAVES * 64) void k_svd_topk(TopkArgs a) {
   const double* vt_lane = a.vt + (int64_t)(lane >> 4) * a.ncol_pad + (lane & 15);
   double th[RT][4];  // thresholds of this lane's C/D rows (mirrors s_th / s_thc)
   int thc[RT][4];
+  bool rowok[RT][4];  // the row is a real user (the last wave may be partial)
+#pragma unroll
+  for (int t = 0; t < RT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) rowok[t][r] = u0 + 16 * t + my_row + 4 * r < a.n_users;
 #pragma unroll
   for (int t = 0; t < RT; ++t)
 #pragma unroll
@@ -238,6 +243,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_svd_topk(TopkArgs a) {
     // whose scores all fall below them costs a few VALU compares and one ballot: no LDS
     // round trip, no cross-lane shuffle unless the tile holds an excluded column.
     const bool anyex = __ballot(exm != 0) != 0;  // wave-uniform
+    const bool colok = col < ce;
     bool pass[RT][4];
     bool anyp = false;
 #pragma unroll
@@ -245,7 +251,9 @@ __global__ __launch_bounds__(WAVES * 64) void k_svd_topk(TopkArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = 16 * t + my_row + 4 * r;
-        bool ok = col < ce && u0 + row < a.n_users && better(d[t][r], col, th[t][r], thc[t][r]);
+        // non-short-circuit: compares and mask ANDs, no branches
+        const double sc = d[t][r];
+        bool ok = colok & rowok[t][r] & ((sc > th[t][r]) | ((sc == th[t][r]) & (col < thc[t][r])));
         if (anyex) {
           const unsigned rm = (unsigned)__shfl((int)exm, row, 64);
           ok = ok && !((rm >> (lane & 15)) & 1u);
