@@ -71,7 +71,7 @@ def alg_bytes(G, x, y, mask, cn=None):
     return int(per_src + per_pair)
 
 
-def pmc_traffic(kernel):
+def pmc_traffic(kernel, pattern="r*_v*_bench.json"):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary of this bench
     (profiles/*.json written by profiles/summarize.py from separate rocprofv3 --pmc
     FETCH_SIZE / WRITE_SIZE passes; 2 x FETCH_SIZE + WRITE_SIZE per MI355X_MICROARCH.md)."""
@@ -80,10 +80,10 @@ def pmc_traffic(kernel):
     import re
 
     def version(f):  # rNN_vM_bench.json: newest (round, version) last
-        m = re.search(r"r(\d+)_v(\d+)_bench\.json$", f)
+        m = re.search(r"r(\d+)_v(\d+)_[a-z0-9_]+\.json$", f)
         return (int(m.group(1)), int(m.group(2))) if m else (-1, -1)
 
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_v*_bench.json")), key=version)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)), key=version)
     for f in reversed(files):
         try:
             rows = json.load(open(f))
@@ -253,6 +253,7 @@ def run_svd(args):
     for i in range(64):
         full[i, ex_col[ex_off[i]:ex_off[i + 1]]] = -np.inf
     ok = all(np.array_equal(np.lexsort((np.arange(B), -full[i]))[:args.topk], cols[i]) for i in range(64))
+    svd_traffic, svd_tsrc = pmc_traffic("k_svd_topk", "r*_v*_svd_c4.json")  # HBM bytes per launch (PMC)
     out = {
         "metric": METRIC, "value": dist.sum(scored) / t_max, "unit": "pairs/s", "n_gpus": dist.world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * t_max, "higher_is_better": True,
@@ -263,8 +264,9 @@ def run_svd(args):
                                "%.2fs, not in the step" % (M.nnz, len(users), args.topk, fact_s),
                    "global_batch": int(dist.sum(scored)), "parallelism": "replicas x%d" % dist.world},
         "roofline": {"bound": "mfma", "achieved": flops / kern_s / 1e12, "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
-                     "frac": flops / kern_s / 1e12 / FP64_MFMA_PEAK_TFS, "traffic": None,
-                     "kernel": "k_svd_topk<64> + k_svd_merge", "kernel_ms": 1e3 * kern_s},
+                     "frac": flops / kern_s / 1e12 / FP64_MFMA_PEAK_TFS, "traffic": svd_traffic,
+                     "kernel": "k_svd_topk<64> + k_svd_merge", "kernel_ms": 1e3 * kern_s,
+                     "traffic_source": svd_tsrc},
         "pairs_kernel": {"pairs": int(len(pr)), "ms": 1e3 * pair_s, "pairs_per_s": len(pr) / pair_s,
                          "alg_GBps": pair_bytes / pair_s / 1e9},
         "parity": {"topk_users_checked": 64, "exact": bool(ok)},
