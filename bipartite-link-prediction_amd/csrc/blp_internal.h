@@ -82,6 +82,12 @@ struct blp_graph {
   uint32_t* d_hot_pool = nullptr;
   int64_t n_hot = 0, hot_pool_words = 0;
   std::vector<int32_t> h_hot_idx;
+  // wedge rows (wedge.hip): for every node x whose neighbours' rows all hold <= SHORT_ROW_MAX
+  // ids, the rows N(z), z in N(x), back to back (d_wedge[4 d_wp[x] .. 4 d_wp[x + 1]), padded to
+  // whole 16-byte vectors with a repeat of the row's last id); null when over budget
+  int64_t* d_wp = nullptr;    // [n + 1], in 16-byte vectors
+  int32_t* d_wedge = nullptr;
+  int64_t wedge_vecs = 0;
   // host mirrors used only for launch planning (bitmap universe bounds)
   std::vector<int64_t> h_rp;
   std::vector<int32_t> h_ci;
@@ -100,7 +106,10 @@ struct HotRow {
 struct __attribute__((aligned(4))) U4a {
   int32_t x, y, z, w;
 };
+constexpr int SHORT_ROW_MAX = 32;  // the short-row scorer's row bound (pairs.hip SHORT_MAX)
 int build_hot_index(blp_graph* g);
+int build_wedge_index(blp_graph* g);
+void free_wedge_index(blp_graph* g);
 void free_hot_index(blp_graph* g);
 int timer_begin(blp_graph* g, int k, hipEvent_t* start);
 int timer_end(blp_graph* g, int k, hipEvent_t start);

@@ -291,6 +291,7 @@ int blp_graph_create(const int64_t* row_ptr, const int32_t* col_idx, int64_t n, 
   g->h_rp.assign(row_ptr, row_ptr + n + 1);
   g->h_ci.assign(col_idx, col_idx + nnz);
   if ((rc = build_hot_index(g)) != BLP_OK) return cleanup(rc);
+  if ((rc = build_wedge_index(g)) != BLP_OK) return cleanup(rc);
   *out = g;
   return BLP_OK;
 }
@@ -301,6 +302,7 @@ int blp_graph_destroy(blp_graph* g) {
   if (g->stream) (void)hipStreamSynchronize(g->stream);
   for (auto& t : g->timers) timer_release(t);
   free_hot_index(g);
+  free_wedge_index(g);
   if (g->d_rp) (void)hipFree(g->d_rp);
   if (g->d_ci) (void)hipFree(g->d_ci - CI_PAD);
   if (g->d_aaw_fx) (void)hipFree(g->d_aaw_fx);

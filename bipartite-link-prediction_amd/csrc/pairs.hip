@@ -995,7 +995,7 @@ __device__ inline void rc_chunk_offsets(const int32_t* s_off, int ns, int32_t* s
 // 16-byte loads, all issued before any is used. No merge-path search and no row crossings,
 // whose dependent LDS round trips dominate a merge-path step when rows average ~10 ids;
 // the cost is idle lanes beside the longest row of the wave. ci is padded past nnz.
-constexpr int SHORT_MAX = 32;
+constexpr int SHORT_MAX = blp::SHORT_ROW_MAX;
 constexpr int SHORT_PART = 16;  // ids held in registers at a time (a row up to SHORT_MAX: two parts)
 
 // Part [h, h + SHORT_PART) of a row of len ids: up to SHORT_PART / 4 16-byte loads, all issued
@@ -1158,6 +1158,8 @@ struct ScoreArgs {
   uint32_t mask;
   int dq;            // sources per dequeue
   int short_rows;    // bit 0: every build row <= SHORT_MAX ids, bit 1: every scan row (row_build / row_scan)
+  const int64_t* wp;    // wedge rows (wedge.hip; short-row scorer only, null: build from CSR)
+  const uint4* wedge;
 };
 
 template <int BLOCK>
@@ -1338,6 +1340,23 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
           }
           __syncthreads();
           PROF(2)
+          if (SHORT && a.wp) {
+            // N(N(x)) from x's wedge row: one contiguous range, two 16-byte vectors per thread
+            // in flight, no row_ptr round trip and no idle lanes beside long rows
+            const int64_t wb = a.wp[x], we = a.wp[x + 1];
+            const uint32_t keep = a.idmask | 0x80000000u, c0u = (uint32_t)c0, wu = (uint32_t)width;
+            for (int64_t q = wb + threadIdx.x; q < we; q += 2 * BLOCK) {
+              const uint4 v0 = a.wedge[q];
+              const uint4 v1 = q + BLOCK < we ? a.wedge[q + BLOCK] : v0;  // (a repeat ORs nothing new)
+              const uint32_t ids[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+              for (int k = 0; k < 8; ++k) {
+                const uint32_t r = in_chunk((int)ids[k], keep, c0u);
+                if (r < wu) atomicOr(&bm[r >> 5], 1u << (r & 31));
+              }
+            }
+            __syncthreads();
+          } else
           for (int64_t k0 = xb; k0 < xe; k0 += SEG) {
             const int ns = (int)min<int64_t>(SEG, xe - k0);
             load_row_segments<BLOCK>(a.rp, a.ci, k0, ns, s_start, s_off, red, nhot ? a.hot_idx : nullptr);
@@ -2428,6 +2447,8 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
     if (rc) return rc;
   }
   ScoreArgs a;
+  a.wp = nullptr;
+  a.wedge = nullptr;
   a.rp = g->d_rp;
   a.ci = g->d_ci;
   a.aaw = g->d_aaw_fx;
@@ -2487,6 +2508,10 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   } else if (np && b->variant == V_SMALL && b->short_rows == 3 && !getenv("BLP_NO_SHORT_KERNEL")) {
     // bitmap in dynamic LDS, sized to the universe (whole 16-byte vectors)
     const size_t dyn = 4 * (size_t)std::max<int64_t>(4, ((b->hi - b->lo + 31) / 32 + 3) / 4 * 4);
+    if (g->d_wp && !getenv("BLP_NO_WEDGE")) {  // tuning knob: BLP_NO_WEDGE builds from CSR
+      a.wp = g->d_wp;
+      a.wedge = reinterpret_cast<const uint4*>(g->d_wedge);
+    }
     if ((rc = (mask & BLP_ADAMIC) ? launch_short<true>(g, b, a, dyn) : launch_short<false>(g, b, a, dyn))) return rc;
   } else if (np) {
     int per_cu = 1;

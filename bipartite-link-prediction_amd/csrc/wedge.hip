@@ -1,0 +1,83 @@
+// Wedge rows (libblp.so): a second layout of the graph for the short-row scorer.
+//
+// Building H2(x) (similarity.py:74 GetNodesAtHop(v, 2) on the business side) from CSR takes
+// three dependent round trips per source -- N(x), then row_ptr[z] for every z in N(x), then
+// the rows N(z) -- and one thread per row, idle beside the longest row of its wave. For a node
+// whose neighbours' rows are all short (<= SHORT_ROW_MAX ids: every business of a review
+// graph, whose members are users with a few reviews each) the rows N(z), z in N(x), are also
+// stored back to back, so the build reads one contiguous range with 16-byte vectors spread
+// over the whole workgroup. The volume is sum over eligible x of sum_{z in N(x)} |N(z)| (the
+// business side's build elements: 108.8M ids, 435 MB at config 2); it is skipped above
+// BLP_WEDGE_MAX_X x nnz ids (default 8) or with BLP_WEDGE=0. Duplicate ids are harmless:
+// the build ORs them into a bitmap, so the padding repeats the last id.
+#include <algorithm>
+#include <cstdlib>
+#include <thread>
+#include <vector>
+
+#include "blp_internal.h"
+
+namespace blp {
+
+int build_wedge_index(blp_graph* g) {
+  if (const char* e = getenv("BLP_WEDGE"))
+    if (atoi(e) == 0) return BLP_OK;
+  const int64_t n = g->n;
+  const int64_t* rp = g->h_rp.data();
+  const int32_t* ci = g->h_ci.data();
+  if (n == 0 || g->nnz == 0) return BLP_OK;
+  std::vector<int64_t> wp((size_t)n + 1, 0);
+  int64_t total = 0;
+  for (int64_t x = 0; x < n; ++x) {
+    wp[x] = total;
+    int64_t len = 0;
+    bool ok = true;
+    for (int64_t k = rp[x]; k < rp[x + 1]; ++k) {
+      const int64_t d = rp[ci[k] + 1] - rp[ci[k]];
+      if (d > SHORT_ROW_MAX) {
+        ok = false;
+        break;
+      }
+      len += d;
+    }
+    total += ok ? (len + 3) / 4 : 0;
+  }
+  wp[n] = total;
+  double max_x = 8.0;
+  if (const char* e = getenv("BLP_WEDGE_MAX_X")) max_x = atof(e);
+  if (total == 0 || (double)(4 * total) > max_x * (double)g->nnz || 4 * total >= (int64_t(1) << 34)) return BLP_OK;
+  std::vector<int32_t> w((size_t)(4 * total));
+  const int nt = (int)std::max<unsigned>(1, std::min<unsigned>(16, std::thread::hardware_concurrency()));
+  std::vector<std::thread> th;
+  for (int t = 0; t < nt; ++t)
+    th.emplace_back([&, t]() {
+      for (int64_t x = t; x < n; x += nt) {
+        int64_t pos = 4 * wp[x];
+        const int64_t end = 4 * wp[x + 1];
+        if (pos == end) continue;
+        for (int64_t k = rp[x]; k < rp[x + 1]; ++k) {
+          const int32_t z = ci[k];
+          for (int64_t j = rp[z]; j < rp[z + 1]; ++j) w[pos++] = ci[j];
+        }
+        const int32_t last = w[pos - 1];
+        while (pos < end) w[pos++] = last;
+      }
+    });
+  for (auto& t : th) t.join();
+  BLP_HIP(hipMalloc(&g->d_wp, sizeof(int64_t) * (n + 1)));
+  BLP_HIP(hipMalloc(&g->d_wedge, sizeof(int32_t) * 4 * total));
+  BLP_HIP(hipMemcpy(g->d_wp, wp.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice));
+  BLP_HIP(hipMemcpy(g->d_wedge, w.data(), sizeof(int32_t) * 4 * total, hipMemcpyHostToDevice));
+  g->wedge_vecs = total;
+  return BLP_OK;
+}
+
+void free_wedge_index(blp_graph* g) {
+  if (g->d_wp) (void)hipFree(g->d_wp);
+  if (g->d_wedge) (void)hipFree(g->d_wedge);
+  g->d_wp = nullptr;
+  g->d_wedge = nullptr;
+  g->wedge_vecs = 0;
+}
+
+}  // namespace blp
