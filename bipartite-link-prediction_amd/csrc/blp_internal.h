@@ -88,6 +88,7 @@ struct blp_graph {
   int64_t* d_wp = nullptr;    // [n + 1], in 16-byte vectors
   int32_t* d_wedge = nullptr;
   int64_t wedge_vecs = 0;
+  std::vector<int64_t> h_wp;  // host copy of d_wp (heavy-source planning)
   // host mirrors used only for launch planning (bitmap universe bounds)
   std::vector<int64_t> h_rp;
   std::vector<int32_t> h_ci;

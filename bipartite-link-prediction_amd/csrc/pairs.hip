@@ -1091,7 +1091,7 @@ __device__ inline void load_row_segments(const int64_t* __restrict__ rp, const i
 // ------------------------------------------------------------------ heavy-source pre-build
 struct HeavyItem {
   int32_t slot;
-  int32_t pad;
+  int32_t wedge;   // 0: [kb, ke) are CSR positions of N(x); 1: 16-byte vectors of x's wedge row
   int64_t kb, ke;  // rows N(x) = ci[kb, ke) handled by this item
 };
 
@@ -1102,6 +1102,7 @@ struct HeavyArgs {
   uint32_t* heavy_bm;  // [slots][hb_words]
   int64_t hb_words;
   int64_t lo, width;
+  const uint4* wedge;  // wedge rows (wedge.hip), for items with wedge = 1
 };
 
 template <int BLOCK, int CAP_WORDS, int SEG>
@@ -1115,6 +1116,20 @@ __global__ __launch_bounds__(BLOCK) void k_heavy(HeavyArgs h) {
   const int nw = (int)((h.width + 31) >> 5);
   for (int i = threadIdx.x; i < nw; i += BLOCK) bm[i] = 0;
   __syncthreads();
+  if (it.wedge) {  // a slice of x's wedge row: contiguous vectors, two per thread in flight
+    const uint32_t c0u = (uint32_t)h.lo, wu = (uint32_t)h.width;
+    for (int64_t q = it.kb + threadIdx.x; q < it.ke; q += 2 * BLOCK) {
+      const uint4 v0 = h.wedge[q];
+      const uint4 v1 = q + BLOCK < it.ke ? h.wedge[q + BLOCK] : v0;
+      const uint32_t ids[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t r = in_chunk((int)ids[k], 0x7fffffffu | 0x80000000u, c0u);
+        if (r < wu) atomicOr(&bm[r >> 5], 1u << (r & 31));
+      }
+    }
+    __syncthreads();
+  } else
   for (int64_t k0 = it.kb; k0 < it.ke; k0 += SEG) {
     const int ns = (int)min<int64_t>(SEG, it.ke - k0);
     load_row_segments<BLOCK>(h.rp, h.ci, k0, ns, s_start, s_off, red);
@@ -2220,6 +2235,9 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   if (const char* e = getenv("BLP_HEAVY_WORK")) item_work = std::max<int64_t>(1, atoll(e));  // test knob
   std::vector<int32_t> heavy_slot;
   std::vector<HeavyItem> items;
+  // every source's rows are short and the graph holds wedge rows: heavy sources are split into
+  // slices of their wedge rows (the short-row scorer's layout)
+  const bool wedge_items = (b->short_rows & 1) && g->d_wp && !getenv("BLP_NO_WEDGE");
   if (b->chunks == 1 && span > 0 && !b->global && (!b->split || span <= variant_cap_bits(V_LARGE))) {
     for (size_t i = 0; i < srcs.size(); ++i) {
       if (work[i] <= 2 * item_work) continue;
@@ -2227,6 +2245,11 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
       const int32_t xs = srcs[i];
       const int32_t slot = (int32_t)b->n_heavy++;
       heavy_slot[xs] = slot;
+      if (wedge_items) {  // slices of x's wedge row, item_work ids each
+        const int64_t wb = g->h_wp[xs], we = g->h_wp[xs + 1], step = std::max<int64_t>(1, item_work / 4);
+        for (int64_t q = wb; q < we; q += step) items.push_back(HeavyItem{slot, 1, q, std::min(we, q + step)});
+        continue;
+      }
       int64_t acc = 0, kb = rp[xs];
       for (int64_t k = rp[xs]; k < rp[xs + 1]; ++k) {
         acc += rp[ci[k] + 1] - rp[ci[k]];
@@ -2437,7 +2460,8 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   if ((rc = timer_begin(b->t_score, b->stream, &bt1))) return rc;
   if (b->n_heavy) {
     BLP_HIP(hipMemsetAsync(b->d_heavy_bm, 0, 4 * b->hb_words * b->n_heavy, b->stream));
-    HeavyArgs h{g->d_rp, g->d_ci, b->d_heavy_items, b->d_heavy_bm, b->hb_words, b->lo, b->hi - b->lo};
+    HeavyArgs h{g->d_rp, g->d_ci, b->d_heavy_items, b->d_heavy_bm, b->hb_words, b->lo, b->hi - b->lo,
+                reinterpret_cast<const uint4*>(g->d_wedge)};
     if (b->variant == V_SMALL)
       rc = launch_heavy<BLOCK_SMALL, CAP_SMALL, SEG_SMALL>(b->stream, h, b->n_heavy_items);
     else if (b->variant == V_MED)

@@ -69,6 +69,7 @@ int build_wedge_index(blp_graph* g) {
   BLP_HIP(hipMemcpy(g->d_wp, wp.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice));
   BLP_HIP(hipMemcpy(g->d_wedge, w.data(), sizeof(int32_t) * 4 * total, hipMemcpyHostToDevice));
   g->wedge_vecs = total;
+  g->h_wp = std::move(wp);
   return BLP_OK;
 }
 
@@ -78,6 +79,7 @@ void free_wedge_index(blp_graph* g) {
   g->d_wp = nullptr;
   g->d_wedge = nullptr;
   g->wedge_vecs = 0;
+  g->h_wp.clear();
 }
 
 }  // namespace blp
