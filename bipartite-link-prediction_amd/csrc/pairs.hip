@@ -209,7 +209,21 @@ __global__ __launch_bounds__(GB_BLOCK) void k_bucket_group(const int64_t* __rest
   const int be = b + 1 < nb ? hoff[(int64_t)(b + 1) * nblk] : (int)np;
   for (int i = threadIdx.x; i < KEYS; i += GB_BLOCK) h[i] = 0;
   __syncthreads();
-  for (int k = bs + threadIdx.x; k < be; k += GB_BLOCK) atomicAdd(&h[tmp[k].y - k0], 1);
+  {  // counting pass: UC independent loads in flight per thread, then their LDS atomics (one
+     // dependent round trip per UC pairs, not per pair: the bucket's ~5K pairs took 19)
+    constexpr int UC = 8;
+    for (int kr = bs; kr < be; kr += UC * GB_BLOCK) {
+      int xv[UC];
+#pragma unroll
+      for (int u = 0; u < UC; ++u) {
+        const int k = kr + u * GB_BLOCK + threadIdx.x;
+        xv[u] = k < be ? tmp[k].y : INT32_MIN;
+      }
+#pragma unroll
+      for (int u = 0; u < UC; ++u)
+        if (xv[u] != INT32_MIN) atomicAdd(&h[xv[u] - k0], 1);
+    }
+  }
   __syncthreads();
   int v = 0, act = 0;
   for (int q = 0; q < PER; ++q) {
@@ -234,7 +248,10 @@ __global__ __launch_bounds__(GB_BLOCK) void k_bucket_group(const int64_t* __rest
   if (threadIdx.x == 0) bucket_active[b] = acts;
   __syncthreads();
   // U pairs per thread per round: their loads, gathers and LDS atomics overlap
-  constexpr int U = 4;
+#ifndef BLP_GROUP_U
+#define BLP_GROUP_U 4
+#endif
+  constexpr int U = BLP_GROUP_U;
   for (int k0r = bs; k0r < be; k0r += U * GB_BLOCK) {
     int4 t[U];
 #pragma unroll
