@@ -117,6 +117,11 @@ def test_general_graph_exact_distance(gpu):
     {"BLP_WCODES": "3", "BLP_FORCE_GLOBAL": "1"},
     {"BLP_WCODES": "3", "BLP_WAVE": "1"},
     {"BLP_WCODES": "3", "BLP_HEAVY_WORK": "50", "BLP_HOT_MIN": "8"},
+    {"BLP_NO_WEDGE": "1"},                              # short-row build from CSR, not wedge rows
+    {"BLP_NO_WEDGE": "1", "BLP_HEAVY_WORK": "50"},      # ... heavy items as CSR ranges
+    {"BLP_WEDGE": "0", "BLP_HEAVY_WORK": "50"},         # graph built without wedge rows
+    {"BLP_WEDGE_MAX_X": "0.5"},                         # wedge rows over budget: not built
+    {"BLP_HEAVY_WORK": "7"},                            # wedge slices of 1 vector, uneven tails
 ])
 def test_kernel_paths_vs_oracle(gpu, knobs, monkeypatch):
     for k, v in knobs.items():
