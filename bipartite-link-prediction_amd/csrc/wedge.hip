@@ -26,28 +26,41 @@ int build_wedge_index(blp_graph* g) {
   const int64_t* rp = g->h_rp.data();
   const int32_t* ci = g->h_ci.data();
   if (n == 0 || g->nnz == 0) return BLP_OK;
-  std::vector<int64_t> wp((size_t)n + 1, 0);
-  int64_t total = 0;
-  for (int64_t x = 0; x < n; ++x) {
-    wp[x] = total;
-    int64_t len = 0;
-    bool ok = true;
-    for (int64_t k = rp[x]; k < rp[x + 1]; ++k) {
-      const int64_t d = rp[ci[k] + 1] - rp[ci[k]];
-      if (d > SHORT_ROW_MAX) {
-        ok = false;
-        break;
-      }
-      len += d;
-    }
-    total += ok ? (len + 3) / 4 : 0;
-  }
-  wp[n] = total;
   double max_x = 8.0;
   if (const char* e = getenv("BLP_WEDGE_MAX_X")) max_x = atof(e);
-  if (total == 0 || (double)(4 * total) > max_x * (double)g->nnz || 4 * total >= (int64_t(1) << 34)) return BLP_OK;
-  std::vector<int32_t> w((size_t)(4 * total));
+  const double budget = std::min(max_x * (double)g->nnz, (double)(int64_t(1) << 34));
+  // per-node volume: one degree lookup per CSR entry, 16 threads (2B entries at config 5)
   const int nt = (int)std::max<unsigned>(1, std::min<unsigned>(16, std::thread::hardware_concurrency()));
+  std::vector<int64_t> wp((size_t)n + 1, 0);  // per-node vector counts, then offsets
+  {
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t)
+      th.emplace_back([&, t]() {
+        for (int64_t x = t; x < n; x += nt) {
+          int64_t len = 0;
+          bool ok = true;
+          for (int64_t k = rp[x]; k < rp[x + 1]; ++k) {
+            const int64_t d = rp[ci[k] + 1] - rp[ci[k]];
+            if (d > SHORT_ROW_MAX) {
+              ok = false;
+              break;
+            }
+            len += d;
+          }
+          wp[x] = ok ? (len + 3) / 4 : 0;
+        }
+      });
+    for (auto& t : th) t.join();
+  }
+  int64_t total = 0;
+  for (int64_t x = 0; x < n; ++x) {
+    const int64_t c = wp[x];
+    wp[x] = total;
+    total += c;
+  }
+  wp[n] = total;
+  if (total == 0 || (double)(4 * total) > budget) return BLP_OK;
+  std::vector<int32_t> w((size_t)(4 * total));
   std::vector<std::thread> th;
   for (int t = 0; t < nt; ++t)
     th.emplace_back([&, t]() {
