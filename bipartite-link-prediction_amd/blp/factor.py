@@ -12,6 +12,7 @@ _lib.register("blp_svd_create", [_P, _I64, _P, _I64, _I32, _I32, ctypes.POINTER(
 _lib.register("blp_svd_destroy", [_P])
 _lib.register("blp_svd_score_pairs", [_P, _P, _P, _I64, _P])
 _lib.register("blp_svd_score_pairs_device", [_P, _P, _P, _I64, _P])
+_lib.register("blp_svd_topk_device", [_P, _P, _I64, _P, _P, _I32, _P, _P])
 _lib.register("blp_svd_topk", [_P, _P, _I64, _P, _P, _I32, _P, _P])
 _lib.register("blp_svd_stats", [_P, _I32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)])
 _lib.register("blp_svd_sync", [_P])
@@ -64,6 +65,19 @@ class DeviceSVD:
             ec = _lib.as_i32(exclude[1] if len(exclude[1]) else np.zeros(1, np.int32))
         check(lib().blp_svd_topk(self.handle, ptr(users), len(users), ptr(eo), ptr(ec), topk, ptr(oc), ptr(os_)))
         return oc, os_
+
+    def topk_device(self, users, topk, out_cols, out_scores, exclude=None):
+        """blp_svd_topk_device: every argument a device-resident torch tensor on this handle's
+        device (users int32 [n]; exclude (int64 offsets [n+1], int32 cols) or None; out_cols
+        int32 [n, topk], out_scores float64 [n, topk]). Enqueued on the handle's stream without a
+        sync (sync() waits)."""
+        eo = exclude[0].data_ptr() if exclude is not None else None
+        ec = exclude[1].data_ptr() if exclude is not None else None
+        check(lib().blp_svd_topk_device(self.handle, users.data_ptr(), users.numel(), eo, ec, topk,
+                                        out_cols.data_ptr(), out_scores.data_ptr()))
+
+    def sync(self):
+        check(lib().blp_svd_sync(self.handle))
 
     def stats(self, which=0):
         ms = ctypes.c_double(0)

@@ -28,6 +28,9 @@ struct blp_svd {
   double* d_v = nullptr;   // [n_cols][kpad]
   double* d_vt = nullptr;  // [kpad][ncol_pad]
   blp::KernelTimer t_pairs, t_topk;
+  double* d_ps = nullptr;  // top-k scratch: per (user, chunk) partial lists, part_cap entries
+  int32_t* d_pc = nullptr;
+  int64_t part_cap = 0;
 };
 
 namespace {
@@ -391,7 +394,7 @@ int blp_svd_destroy(blp_svd* h) {
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   timer_release(h->t_pairs);
   timer_release(h->t_topk);
-  for (void* p : {(void*)h->d_us, (void*)h->d_v, (void*)h->d_vt})
+  for (void* p : {(void*)h->d_us, (void*)h->d_v, (void*)h->d_vt, (void*)h->d_ps, (void*)h->d_pc})
     if (p) (void)hipFree(p);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
@@ -438,14 +441,10 @@ int blp_svd_score_pairs(blp_svd* h, const int32_t* rows, const int32_t* cols, in
   return rc;
 }
 
-int blp_svd_topk(blp_svd* h, const int32_t* users, int64_t n_users, const int64_t* ex_off, const int32_t* ex_col,
-                 int topk, int32_t* out_cols, double* out_scores) {
-  BLP_CHECK(h && users && n_users > 0 && topk > 0 && topk <= TK_MAX && out_cols && out_scores, BLP_E_ARG,
-            "blp_svd_topk: bad arguments");
-  BLP_CHECK(h->kpad == 16 || h->kpad == 32 || h->kpad == 48 || h->kpad == 64 || h->kpad == 128, BLP_E_UNSUP,
-            "blp_svd_topk: k must pad to 16/32/48/64/128");
-  for (int64_t i = 0; i < n_users; ++i)
-    BLP_CHECK(users[i] >= 0 && users[i] < h->n_rows, BLP_E_ARG, "blp_svd_topk: user row out of range");
+// Enqueue the top-k of device-resident inputs on the handle's stream; the per-chunk partial
+// lists live in handle-owned scratch (grown on demand, freed with the handle).
+static int svd_topk_enqueue(blp_svd* h, const int32_t* d_users, int64_t n_users, const int64_t* d_exo,
+                            const int32_t* d_exc, int topk, int32_t* d_oc, double* d_os) {
   BLP_HIP(hipSetDevice(h->device));
   // chunks: enough blocks to fill the chip, >= 16 tiles each
   // default: one 16-user tile per wave, 4 waves per block. Measured alternatives (config 4):
@@ -478,31 +477,22 @@ int blp_svd_topk(blp_svd* h, const int32_t* users, int64_t n_users, const int64_
   if (const char* e = getenv("BLP_SVD_CHUNKS")) n_chunks = std::max(1, std::min(atoi(e), (int)std::max<int64_t>(1, h->ncol_pad / 256)));
   const int64_t chunk = ((h->n_cols + n_chunks - 1) / n_chunks + 15) / 16 * 16;
   n_chunks = (int)((h->n_cols + chunk - 1) / chunk);
-  const int64_t nex = ex_off ? ex_off[n_users] : 0;
-  void *d_users = nullptr, *d_exo = nullptr, *d_exc = nullptr, *d_ps = nullptr, *d_pc = nullptr, *d_os = nullptr,
-       *d_oc = nullptr;
-  auto cleanup = [&]() {
-    for (void* p : {d_users, d_exo, d_exc, d_ps, d_pc, d_os, d_oc})
-      if (p) (void)hipFree(p);
-  };
   const int64_t np = n_users * n_chunks * topk;
-  if (hipMalloc(&d_users, 4 * n_users) != hipSuccess || hipMalloc(&d_ps, 8 * np) != hipSuccess ||
-      hipMalloc(&d_pc, 4 * np) != hipSuccess || hipMalloc(&d_os, 8 * n_users * topk) != hipSuccess ||
-      hipMalloc(&d_oc, 4 * n_users * topk) != hipSuccess ||
-      (ex_off && (hipMalloc(&d_exo, 8 * (n_users + 1)) != hipSuccess || hipMalloc(&d_exc, 4 * std::max<int64_t>(nex, 1)) != hipSuccess))) {
-    cleanup();
-    return fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_svd_topk: hipMalloc failed");
+  if (np > h->part_cap) {
+    if (h->d_ps) (void)hipFree(h->d_ps);
+    if (h->d_pc) (void)hipFree(h->d_pc);
+    h->d_ps = nullptr;
+    h->d_pc = nullptr;
+    h->part_cap = 0;
+    if (hipMalloc(&h->d_ps, 8 * np) != hipSuccess || hipMalloc(&h->d_pc, 4 * np) != hipSuccess)
+      return fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_svd_topk: partial buffers");
+    h->part_cap = np;
   }
-  (void)hipMemcpy(d_users, users, 4 * n_users, hipMemcpyHostToDevice);
-  if (ex_off) {
-    (void)hipMemcpy(d_exo, ex_off, 8 * (n_users + 1), hipMemcpyHostToDevice);
-    if (nex) (void)hipMemcpy(d_exc, ex_col, 4 * nex, hipMemcpyHostToDevice);
-  }
-  TopkArgs a{h->d_us, h->d_vt, (const int32_t*)d_users, (const int64_t*)d_exo, (const int32_t*)d_exc, n_users,
-             h->n_cols, h->ncol_pad, h->kpad, topk, chunk, n_chunks, (double*)d_ps, (int32_t*)d_pc};
+  TopkArgs a{h->d_us, h->d_vt, d_users, d_exo, d_exc, n_users, h->n_cols, h->ncol_pad, h->kpad, topk, chunk, n_chunks,
+             h->d_ps, h->d_pc};
   hipEvent_t t0;
   int rc = timer_begin(h->t_topk, h->stream, &t0);
-  if (rc) return cleanup(), rc;
+  if (rc) return rc;
   const dim3 grid((unsigned)ublocks, (unsigned)n_chunks), block(waves * 64);
 #define BLP_SVD_TOPK(KP)                                                                        \
   if (getenv("BLP_SVD_EXP"))                                                                    \
@@ -519,13 +509,51 @@ int blp_svd_topk(blp_svd* h, const int32_t* users, int64_t n_users, const int64_
     default: BLP_SVD_TOPK(128); break;
   }
 #undef BLP_SVD_TOPK
-  hipLaunchKernelGGL(k_svd_merge, dim3((unsigned)n_users), dim3(64), 0, h->stream, (const double*)d_ps,
-                     (const int32_t*)d_pc, n_users, n_chunks, topk, (double*)d_os, (int32_t*)d_oc);
-  if (hipGetLastError() != hipSuccess) {
+  hipLaunchKernelGGL(k_svd_merge, dim3((unsigned)n_users), dim3(64), 0, h->stream, h->d_ps, h->d_pc, n_users,
+                     n_chunks, topk, d_os, d_oc);
+  if (hipGetLastError() != hipSuccess) return fail(BLP_E_HIP_BASE, "blp_svd_topk: launch failed");
+  return timer_end(h->t_topk, h->stream, t0);
+}
+
+int blp_svd_topk_device(blp_svd* h, const int32_t* d_users, int64_t n_users, const int64_t* d_ex_off,
+                        const int32_t* d_ex_col, int topk, int32_t* d_out_cols, double* d_out_scores) {
+  BLP_CHECK(h && d_users && n_users > 0 && topk > 0 && topk <= TK_MAX && d_out_cols && d_out_scores &&
+                (!d_ex_off == !d_ex_col),
+            BLP_E_ARG, "blp_svd_topk_device: bad arguments");
+  BLP_CHECK(h->kpad == 16 || h->kpad == 32 || h->kpad == 48 || h->kpad == 64 || h->kpad == 128, BLP_E_UNSUP,
+            "blp_svd_topk_device: k must pad to 16/32/48/64/128");
+  return svd_topk_enqueue(h, d_users, n_users, d_ex_off, d_ex_col, topk, d_out_cols, d_out_scores);
+}
+
+int blp_svd_topk(blp_svd* h, const int32_t* users, int64_t n_users, const int64_t* ex_off, const int32_t* ex_col,
+                 int topk, int32_t* out_cols, double* out_scores) {
+  BLP_CHECK(h && users && n_users > 0 && topk > 0 && topk <= TK_MAX && out_cols && out_scores, BLP_E_ARG,
+            "blp_svd_topk: bad arguments");
+  BLP_CHECK(h->kpad == 16 || h->kpad == 32 || h->kpad == 48 || h->kpad == 64 || h->kpad == 128, BLP_E_UNSUP,
+            "blp_svd_topk: k must pad to 16/32/48/64/128");
+  for (int64_t i = 0; i < n_users; ++i)
+    BLP_CHECK(users[i] >= 0 && users[i] < h->n_rows, BLP_E_ARG, "blp_svd_topk: user row out of range");
+  BLP_HIP(hipSetDevice(h->device));
+  const int64_t nex = ex_off ? ex_off[n_users] : 0;
+  void *d_users = nullptr, *d_exo = nullptr, *d_exc = nullptr, *d_os = nullptr, *d_oc = nullptr;
+  auto cleanup = [&]() {
+    for (void* p : {d_users, d_exo, d_exc, d_os, d_oc})
+      if (p) (void)hipFree(p);
+  };
+  if (hipMalloc(&d_users, 4 * n_users) != hipSuccess || hipMalloc(&d_os, 8 * n_users * topk) != hipSuccess ||
+      hipMalloc(&d_oc, 4 * n_users * topk) != hipSuccess ||
+      (ex_off && (hipMalloc(&d_exo, 8 * (n_users + 1)) != hipSuccess || hipMalloc(&d_exc, 4 * std::max<int64_t>(nex, 1)) != hipSuccess))) {
     cleanup();
-    return fail(BLP_E_HIP_BASE, "blp_svd_topk: launch failed");
+    return fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_svd_topk: hipMalloc failed");
   }
-  if ((rc = timer_end(h->t_topk, h->stream, t0))) return cleanup(), rc;
+  (void)hipMemcpy(d_users, users, 4 * n_users, hipMemcpyHostToDevice);
+  if (ex_off) {
+    (void)hipMemcpy(d_exo, ex_off, 8 * (n_users + 1), hipMemcpyHostToDevice);
+    if (nex) (void)hipMemcpy(d_exc, ex_col, 4 * nex, hipMemcpyHostToDevice);
+  }
+  int rc = svd_topk_enqueue(h, (const int32_t*)d_users, n_users, (const int64_t*)d_exo, (const int32_t*)d_exc, topk,
+                            (int32_t*)d_oc, (double*)d_os);
+  if (rc) return cleanup(), rc;
   if (hipStreamSynchronize(h->stream) != hipSuccess ||
       hipMemcpy(out_scores, d_os, 8 * n_users * topk, hipMemcpyDeviceToHost) != hipSuccess ||
       hipMemcpy(out_cols, d_oc, 4 * n_users * topk, hipMemcpyDeviceToHost) != hipSuccess) {

@@ -193,6 +193,10 @@ int blp_svd_score_pairs_device(blp_svd* h, const int32_t* d_rows, const int32_t*
                                double* d_out);
 int blp_svd_topk(blp_svd* h, const int32_t* users, int64_t n_users, const int64_t* ex_off,
                  const int32_t* ex_col, int topk, int32_t* out_cols, double* out_scores);
+/* blp_svd_topk on device pointers (users, exclusion CSR or NULLs, outputs), enqueued on the
+ * handle's stream without a sync (blp_svd_sync waits); rows are not range-checked here. */
+int blp_svd_topk_device(blp_svd* h, const int32_t* d_users, int64_t n_users, const int64_t* d_ex_off,
+                        const int32_t* d_ex_col, int topk, int32_t* d_out_cols, double* d_out_scores);
 int blp_svd_stats(blp_svd* h, int which, double* total_ms, int64_t* launches); /* 0 pairs, 1 top-k */
 int blp_svd_sync(blp_svd* h);
 

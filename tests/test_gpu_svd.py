@@ -106,3 +106,29 @@ def test_topk_ties_and_exclusions(gpu):
     small = DeviceSVD(us, v[:10])
     c2, _ = small.topk(users[:3], 15)
     assert (c2[:, 10:] == -1).all() and (c2[:, :10] >= 0).all()
+
+
+def test_topk_device_matches_host_entry(gpu):
+    """blp_svd_topk_device (device-resident inputs and outputs, handle-owned scratch) gives
+    the lists of blp_svd_topk, with and without exclusions, across calls of different sizes."""
+    import torch
+
+    rng = np.random.default_rng(5)
+    us = rng.standard_normal((300, 64))
+    v = rng.standard_normal((2000, 64))
+    dev = DeviceSVD(us, v)
+    cuda = torch.device("cuda", 0)
+    for n in (40, 150, 7):  # the scratch grows, then is reused
+        users = rng.choice(300, n, replace=False).astype(np.int32)
+        excl = [np.sort(rng.choice(2000, 12, replace=False)) for _ in users]
+        off = np.r_[0, np.cumsum([len(e) for e in excl])].astype(np.int64)
+        col = np.concatenate(excl).astype(np.int32)
+        for ex in (None, (off, col)):
+            hc, hs = dev.topk(users, 20, exclude=ex)
+            dc = torch.empty((n, 20), dtype=torch.int32, device=cuda)
+            ds = torch.empty((n, 20), dtype=torch.float64, device=cuda)
+            dex = None if ex is None else (torch.from_numpy(off).to(cuda), torch.from_numpy(col).to(cuda))
+            dev.topk_device(torch.from_numpy(users).to(cuda), 20, dc, ds, exclude=dex)
+            dev.sync()
+            np.testing.assert_array_equal(dc.cpu().numpy(), hc)
+            np.testing.assert_array_equal(ds.cpu().numpy(), hs)
