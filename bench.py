@@ -95,16 +95,13 @@ def pmc_traffic(kernel, pattern="r*_v*_bench.json"):
     return None, None
 
 
-def cpu_baseline(G, ex_x, ex_y, target_s=15.0):
+def cpu_baseline(og, ex_x, ex_y, target_s=15.0):
     """C oracle (oracle/oracle.c), 1 thread, on a bounded sample of the same workload:
     all pairs of a subset of the example users (user side) and all pairs of a subset of
     the candidate businesses (business side); rate = 1 / (1/r_user + 1/r_business)."""
-    import coracle
-
-    og = coracle.OracleGraph(G.n, *_dense_edges(G))
     rng = np.random.default_rng(123)
 
-    def side_rate(src_arr, dst_arr, mask, budget, nthreads=1):
+    def side_rate(src_arr, dst_arr, mask, budget):
         srcs = np.unique(src_arr)
         rng.shuffle(srcs)
         k = max(1, min(len(srcs), 8))
@@ -114,7 +111,7 @@ def cpu_baseline(G, ex_x, ex_y, target_s=15.0):
             used += len(pick)
             sel = np.isin(src_arr, pick)
             t = time.perf_counter()
-            og.score_pairs(src_arr[sel], dst_arr[sel], mask, nthreads=nthreads)
+            og.score_pairs(src_arr[sel], dst_arr[sel], mask, nthreads=1)
             spent += time.perf_counter() - t
             done_pairs += int(sel.sum())
             k = min(k * 2, 4096)
@@ -123,19 +120,81 @@ def cpu_baseline(G, ex_x, ex_y, target_s=15.0):
     ru, pu, su, tu = side_rate(ex_x, ex_y, 7, target_s / 2)
     rb, pb, sb, tb = side_rate(ex_y, ex_x, 3, target_s / 2)
     rate = 1.0 / (1.0 / ru + 1.0 / rb)
-    # the same restatement on the host's cores (OpenMP, dynamic per source),
-    # so the GPU ratio is not only against one thread.
-    nt = max(1, int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0)))
-    mu, mpu, msu, mtu = side_rate(ex_x, ex_y, 7, target_s / 4, nthreads=nt)
-    mb, mpb, msb, mtb = side_rate(ex_y, ex_x, 3, target_s / 4, nthreads=nt)
-    multi = {"value": 1.0 / (1.0 / mu + 1.0 / mb), "unit": "pairs/s", "cores": nt, "kind": "port",
-             "sample": "C oracle, %d OpenMP threads: user side %d pairs of %d users in %.1fs, business side "
-                       "%d pairs of %d businesses in %.1fs; combined = harmonic" % (nt, mpu, msu, mtu, mpb, msb, mtb)}
-    return {"value": rate, "unit": "pairs/s", "cores": 1, "kind": "port", "multicore": multi,
+    return {"value": rate, "unit": "pairs/s", "cores": 1, "kind": "port",
             "sample": "C oracle (oracle/oracle.c, reference algorithm: per-source exact BFS 2-hop set, per-pair "
                       "N(y) scan), 1 thread: user side %d pairs of %d users in %.1fs (%.0f pairs/s), business "
                       "side %d pairs of %d businesses in %.1fs (%.0f pairs/s); combined = harmonic" %
                       (pu, su, tu, ru, pb, sb, tb, rb)}
+
+
+def oracle_full(og, ex_x, ex_y):
+    """Every pair of the step scored by the C oracle on all of this host's cores (OpenMP,
+    dynamic per source): the full-workload parity reference AND the multicore CPU baseline
+    (SURVEY.md §8(d)(ii)). Same arithmetic as similarity.py:108-126."""
+    nt = max(1, int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0)))
+    t0 = time.perf_counter()
+    ucn, ujac, uaa, _ = og.score_pairs(ex_x, ex_y, 7, nthreads=nt)
+    tu = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    bcn, bjac, _, _ = og.score_pairs(ex_y, ex_x, 3, nthreads=nt)
+    tb = time.perf_counter() - t0
+    res = {"user": {"cn": ucn, "jaccard": ujac, "adamic": uaa}, "business": {"cn": bcn, "jaccard": bjac}}
+    multi = {"value": len(ex_x) / (tu + tb), "unit": "pairs/s", "cores": nt, "kind": "port",
+             "sample": "C oracle, %d OpenMP threads, the WHOLE step: user side %d pairs (CN+J+AA) in %.2fs, business "
+                       "side %d pairs (CN+J) in %.2fs" % (nt, len(ex_x), tu, len(ex_x), tb)}
+    return res, multi
+
+
+def merge_ties(v, rel=1e-12):
+    """Scores equal to `rel` (relative) mapped to one value: the Adamic-Adar sums of pairs
+    with the same common-neighbour weights are equal in exact arithmetic. The engine's
+    fixed-point sums keep them exactly equal; a float sum in set order (the reference's and
+    the oracle's) splits them by a last bit, which breaks ROC ties arbitrarily."""
+    v = np.asarray(v, np.float64)
+    if len(v) == 0:
+        return v
+    u = np.unique(v)
+    new_group = np.r_[True, np.diff(u) > rel * np.abs(u[1:])]
+    rep = u[np.flatnonzero(new_group)][np.cumsum(new_group) - 1]
+    return rep[np.searchsorted(u, v)]
+
+
+def full_parity(ex_l, gpu, ora):
+    """All pairs of both sides: CN and Jaccard bit-exact, Adamic-Adar within 1e-9 relative
+    (fixed-point vs the oracle's float sum; north star bar 1e-5); AUC (eval.py:26) of the GPU
+    scores and of the oracle scores side by side -- identical for CN/Jaccard. For Adamic-Adar
+    the float sums' order breaks exact ties by a last bit, so the AUCs are compared with
+    equal-to-1e-12 scores merged into one tie on both sides (merge_ties); the raw oracle AUC
+    is reported beside it."""
+    import importlib
+
+    ev = importlib.import_module("eval")
+    out = {"pairs_checked": int(len(ex_l)) * 2, "pairs_per_side": int(len(ex_l))}
+    ok = True
+    auc = {}
+    for side, keys in (("user", ("cn", "jaccard", "adamic")), ("business", ("cn", "jaccard"))):
+        for k in keys:
+            g, o = gpu[side][k], ora[side][k]
+            if k == "adamic":
+                same = bool(np.allclose(g, o, rtol=1e-9, atol=0) and np.array_equal(g == 0, o == 0))
+                worst = float(np.max(np.abs(g - o) / np.maximum(np.abs(o), 1e-300))) if len(o) else 0.0
+                out["%s_%s_max_rel_err" % (side[0], k)] = worst
+            else:
+                same = bool(np.array_equal(g, o))
+            out["%s_%s_%s" % (side[0], k, "within_1e-9" if k == "adamic" else "exact")] = same
+            ok &= same
+            name = "%s_%s" % (side[0], {"cn": "cn", "jaccard": "jaccard", "adamic": "adamic"}[k])
+            ag, ao = ev.roc_auc(ex_l, g), ev.roc_auc(ex_l, o)
+            auc[name] = {"gpu": ag, "oracle": ao}
+            if k == "adamic":
+                ag, ao = ev.roc_auc(ex_l, merge_ties(g)), ev.roc_auc(ex_l, merge_ties(o))
+                auc[name].update({"gpu_ties_merged_1e-12": ag, "oracle_ties_merged_1e-12": ao})
+            auc[name]["equal"] = bool(ag == ao)
+            ok &= ag == ao
+    out["auc"] = auc
+    out["auc_equal"] = all(v["equal"] for v in auc.values())
+    out["ok"] = bool(ok)
+    return out
 
 
 def _build_elems(G, x):
@@ -154,23 +213,6 @@ def _dense_edges(G):
     b = G.col_idx[keep]
     loops = np.flatnonzero(G.self_loop).astype(np.int32)
     return np.concatenate([a, loops]), np.concatenate([b, loops])
-
-
-def parity_check(G, ex_x, ex_y, ures, bres, n_users=40):
-    """Spot-check a sample of example users (both sides) against the C oracle (not timed)."""
-    import coracle
-
-    og = coracle.OracleGraph(G.n, *_dense_edges(G))
-    rng = np.random.default_rng(7)
-    pick = rng.choice(np.unique(ex_x), size=min(n_users, len(np.unique(ex_x))), replace=False)
-    sel = np.isin(ex_x, pick)
-    cn, jac, aa, _ = og.score_pairs(ex_x[sel], ex_y[sel], 7, nthreads=8)
-    ok_u = (np.array_equal(ures["cn"][sel], cn) and np.array_equal(ures["jaccard"][sel], jac)
-            and np.allclose(ures["adamic"][sel], aa, rtol=1e-9, atol=0))
-    bcn, bjac, _, _ = og.score_pairs(ex_y[sel], ex_x[sel], 3, nthreads=8)
-    ok_b = np.array_equal(bres["cn"][sel], bcn) and np.array_equal(bres["jaccard"][sel], bjac)
-    return {"checked_pairs": int(sel.sum()), "users": int(len(pick)), "user_side_exact": bool(ok_u),
-            "business_side_exact": bool(ok_b)}
 
 
 FP64_MFMA_PEAK_TFS = 78.6  # MI355X FP64 matrix peak (AMD spec; MI355X_MICROARCH.md lists no FP64 rate)
@@ -263,11 +305,16 @@ def run_svd(args):
     p1, q1 = S.stats(0)
     pair_s = (p1 - p0) / 1e3 / max(q1 - q0, 1)
     pair_bytes = len(users) * 64 * 8 + len(pr) * (64 * 8 + 8 + 8)
-    # parity spot check of the top-k on 64 users (fp64 numpy on the same factors)
-    full = us[users[:64]] @ vt_g
-    for i in range(64):
-        full[i, ex_col[ex_off[i]:ex_off[i + 1]]] = -np.inf
-    ok = all(np.array_equal(np.lexsort((np.arange(B), -full[i]))[:args.topk], cols[i]) for i in range(64))
+    # parity of the top-k on >= 1000 users: fp64 numpy on the same factors, 64 users per chunk
+    n_chk = min(len(users), args.svd_parity_users)
+    ok = True
+    for c0 in range(0, n_chk, 64):
+        c1 = min(n_chk, c0 + 64)
+        full = us[users[c0:c1]] @ vt_g
+        for i in range(c0, c1):
+            full[i - c0, ex_col[ex_off[i]:ex_off[i + 1]]] = -np.inf
+            ok &= bool(np.array_equal(np.lexsort((np.arange(B), -full[i - c0]))[:args.topk], cols[i]))
+    del full
     svd_traffic, svd_tsrc = pmc_traffic("k_svd_topk", "r*_v*_svd_c4.json")  # HBM bytes per launch (PMC)
     out = {
         "metric": METRIC, "value": dist.sum(scored) / t_max, "unit": "pairs/s", "n_gpus": dist.world,
@@ -284,7 +331,7 @@ def run_svd(args):
                      "traffic_source": svd_tsrc},
         "pairs_kernel": {"pairs": int(len(pr)), "ms": 1e3 * pair_s, "pairs_per_s": len(pr) / pair_s,
                          "alg_GBps": pair_bytes / pair_s / 1e9},
-        "parity": {"topk_users_checked": 64, "exact": bool(ok), "host_entry_point_same": host_same},
+        "parity": {"topk_users_checked": int(n_chk), "exact": bool(ok), "host_entry_point_same": host_same},
         "factorization": {"gpu_s": fact_s, "create_s": st.create_s, "iterations": st.iterations,
                           "ritz_settled_at": st.converged_at,
                           "spmm_ms": st.spmm_ms, "dense_ms": st.dense_ms},
@@ -292,11 +339,15 @@ def run_svd(args):
     if arpack_s is not None:
         # the reference's own factorisation (svd.py:24) on the host, and the agreement of the
         # two rank-64 reconstructions on random (user, business) pairs
+        import blp_oracle
+
         ref = np.einsum("ij,ji->i", (uu * ss)[pr[:200000]], vt[:, pc[:200000]])
         got = np.einsum("ij,ji->i", us[pr[:200000]], vt_g[:, pc[:200000]])
-        out["factorization"].update({
-            "host_arpack_s": arpack_s, "speedup": arpack_s / fact_s,
-            "max_abs_diff_over_scale": float(np.max(np.abs(got - ref)) / np.max(np.abs(ref)))})
+        cdeg = np.diff(M.tocsc().indptr)
+        zero = (deg[pr[:200000]] == 0) | (cdeg[pc[:200000]] == 0)
+        out["factorization"].update({"host_arpack_s": arpack_s, "speedup": arpack_s / fact_s})
+        # per-entry 1e-5 relative, exact-zero rule for empty rows/columns, near-zero floor
+        out["parity"]["gpu_factor_vs_arpack"] = blp_oracle.svd_entry_parity(got, ref, zero)
         out["cpu_baseline"] = {"value": arpack_s, "unit": "s per rank-64 factorisation", "cores": os.cpu_count(),
                                "kind": "reference",
                                "sample": "scipy.sparse.linalg.svds(M, k=64) on the same 2M x 200K matrix (svd.py:24, "
@@ -324,31 +375,39 @@ def _oracle_graph(G):
     return coracle.OracleGraph(G.n, *_dense_edges(G)), ident, ident
 
 
-def topk_parity(G, src, k, res, n_users=3):
-    """Not timed: for a few users the C oracle enumerates the exact hop-3 set, scores every
-    candidate and sorts (score desc, id asc); Jaccard lists must match exactly, Adamic-Adar
-    lists must carry the pair kernel's values and agree with the oracle's float sums."""
+def topk_parity(G, src, k, res, n_users=200):
+    """Not timed: for `n_users` users the C oracle enumerates the exact hop-3 set, scores every
+    candidate (all host cores) and sorts (score desc, id asc); the Jaccard lists must match
+    exactly, the Adamic-Adar lists must carry the pair kernel's values and agree with the
+    oracle's float sums to 1e-9, and |H3(u)| must equal the kernel's candidate count."""
     og, to_o, from_o = _oracle_graph(G)
-    pick = np.random.default_rng(5).choice(len(src), n_users, replace=False)
-    ok_j = ok_a = ok_n = True
-    for i in pick:
-        x = to_o[src[i]]
-        _, mem = og.hop3([x])
-        xs = np.full(len(mem), x, np.int32)
-        _, jac, aa, _ = og.score_pairs(xs, mem, 7, nthreads=8)
-        dense = from_o[mem]
-        ok_n &= bool(res["ncand"][i] == len(mem))
-        o = np.lexsort((dense, -jac))[:k]
+    nt = max(1, len(os.sched_getaffinity(0)))
+    pick = np.sort(np.random.default_rng(5).choice(len(src), min(n_users, len(src)), replace=False))
+    xs_o = to_o[src[pick]]
+    counts, mem = og.hop3(xs_o)
+    xrep = np.repeat(xs_o, counts).astype(np.int32)
+    _, jac, aa, _ = og.score_pairs(xrep, mem, 7, nthreads=nt)
+    starts = np.r_[0, np.cumsum(counts)]
+    ok_j = ok_a = True
+    ok_n = bool(np.array_equal(res["ncand"][pick], counts))
+    pair_x, pair_y, pair_v = [], [], []
+    for j, i in enumerate(pick):
+        s_, e_ = starts[j], starts[j + 1]
+        dense = from_o[mem[s_:e_]]
+        o = np.lexsort((dense, -jac[s_:e_]))[:k]
         ok_j &= bool(np.array_equal(res["jaccard"][0][i][:len(o)], dense[o]) and
-                     np.array_equal(res["jaccard"][1][i][:len(o)], jac[o]))
+                     np.array_equal(res["jaccard"][1][i][:len(o)], jac[s_:e_][o]))
         cols, sc = res["adamic_adar"][0][i], res["adamic_adar"][1][i]
         v = cols >= 0
-        pair = G.score_pairs(np.full(int(v.sum()), src[i], np.int32), cols[v], 7)["adamic"]
-        ok_a &= bool(np.array_equal(pair, sc[v]))
+        pair_x.append(np.full(int(v.sum()), src[i], np.int32))
+        pair_y.append(cols[v])
+        pair_v.append(sc[v])
         # the k-th value may tie within float rounding; compare the value lists to 1e-9
-        ok_a &= bool(np.allclose(np.sort(aa)[::-1][:int(v.sum())], sc[v], rtol=1e-9, atol=0))
-    return {"users_checked": int(n_users), "jaccard_exact": ok_j, "adamic_pair_kernel_equal_and_oracle_1e-9": ok_a,
-            "n_candidates_exact": ok_n}
+        ok_a &= bool(np.allclose(np.sort(aa[s_:e_])[::-1][:int(v.sum())], sc[v], rtol=1e-9, atol=0))
+    pair = G.score_pairs(np.concatenate(pair_x), np.concatenate(pair_y), 7)["adamic"]
+    ok_a &= bool(np.array_equal(pair, np.concatenate(pair_v)))
+    return {"users_checked": int(len(pick)), "candidates_checked": int(counts.sum()), "jaccard_exact": ok_j,
+            "adamic_pair_kernel_equal_and_oracle_1e-9": ok_a, "n_candidates_exact": ok_n}
 
 
 def topk_cpu_baseline(G, src, k, target_s=15.0):
@@ -479,12 +538,22 @@ def run_sharded(args):
     if not a_all.is_cuda:  # gloo exchange (rehearsal without RCCL): the partials arrive on the host
         a_all, b_all = a_all.to("cuda:%d" % dev), b_all.to("cuda:%d" % dev)
     t0 = time.perf_counter()
+    # the CSR is built in HBM from the gathered endpoints and stays there (no host round trip)
     G = blp.DeviceGraph.from_device_edges(a_all.data_ptr(), b_all.data_ptr(), len(a_all), U + B, U, device=dev)
     build_s = time.perf_counter() - t0
     del a_all, b_all
     torch.cuda.empty_cache()
-    log("rank %d: graph %d nodes, %d unique edges; exchange %.2fs (%.2f GB in), device CSR + upload %.1fs" %
-        (d.rank, G.n, G.nnz // 2, exch_local, recv_bytes / 1e9, build_s))
+    log("rank %d: graph %d nodes, %d unique edges; exchange %.2fs (%.2f GB in), device CSR build %.1fs %s" %
+        (d.rank, G.n, G.nnz // 2, exch_local, recv_bytes / 1e9, build_s, G.build_times))
+    # scoring ownership: contiguous user blocks balanced by WORK (SURVEY.md §8(e) step 1:
+    # sum_{b in N(u)} d_b per user, from the full CSR every rank now holds -- identical on all ranks)
+    end_u = int(G.row_ptr[U])  # user rows come first: only their entries are summed
+    csum = np.zeros(end_u + 1, np.int64)
+    np.cumsum(G.hop1_size[G.col_idx[:end_u]], out=csum[1:])
+    work = (csum[G.row_ptr[1:U + 1]] - csum[G.row_ptr[:U]]).astype(np.float64)
+    del csum
+    sblocks = bd.user_blocks(U, d.world, work)
+    lo, hi = int(sblocks[d.rank]), int(sblocks[d.rank + 1])
     rng = np.random.default_rng(d.rank)
     mine = np.arange(lo, hi)
     mine = mine[G.hop1_size[lo:hi] > 0]
@@ -532,7 +601,11 @@ def run_sharded(args):
                                   % (d.world, d.backend or "single rank")},
         "exchange": {"seconds": exch_s, "bytes_in_per_rank": int(recv_bytes),
                      "GBps_in_per_rank": recv_bytes / exch_s / 1e9 if exch_s > 0 and recv_bytes else None,
-                     "xgmi_one_link_bound_s": xgmi_bound_s, "device_csr_build_s": build_s, "generate_s": gen_s},
+                     "xgmi_one_link_bound_s": xgmi_bound_s, "device_csr_build_s": build_s, "generate_s": gen_s,
+                     "device_csr_phases_s": G.build_times,
+                     "scoring_blocks": "work-balanced (sum of d_b over N(u)); block work max/mean %.3f" %
+                                       (max(work[sblocks[r]:sblocks[r + 1]].sum() for r in range(d.world)) /
+                                        (work.sum() / d.world))},
         "roofline": {"bound": "hbm", "achieved": byts / sec / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": byts / sec / 1e9 / HBM_PEAK_GBS, "traffic": None, "kernel": "user-side scorer",
                      "plan": bt0.plan()},
@@ -540,6 +613,35 @@ def run_sharded(args):
     if d.rank == 0:
         print(json.dumps(out), flush=True)
     d.close()
+
+
+def _free_port():
+    import socket
+
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    return port
+
+
+def relaunch_if_needed(args):
+    """`python bench.py --gpus N` with N > 1 and no torchrun environment: start N ranks under
+    torch.distributed.run as a CHILD process (nothing here has touched the GPU yet) and exit
+    with its status. Under torchrun (the driver's own launch), WORLD_SIZE must equal --gpus."""
+    world = os.environ.get("WORLD_SIZE")
+    if world is None:
+        if args.gpus <= 1:
+            return
+        import subprocess
+
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % args.gpus,
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+               os.path.abspath(__file__)] + sys.argv[1:]
+        log("launching %d ranks: %s" % (args.gpus, " ".join(cmd)))
+        sys.exit(subprocess.call(cmd))
+    if int(world) != args.gpus:
+        sys.exit("bench.py: WORLD_SIZE=%s but --gpus %d" % (world, args.gpus))
 
 
 def main():
@@ -561,8 +663,10 @@ def main():
                          "top-k; svd: config 4 rank-64 truncated-SVD scorer; sharded: config 5 row-block "
                          "sharded ingest + RCCL all-gather, then rank-local scoring (--config c5)")
     ap.add_argument("--topk", type=int, default=20)
+    ap.add_argument("--svd-parity-users", type=int, default=1000, help="--mode svd: users whose top-k is checked")
     ap.add_argument("--topk-mask", type=int, default=6, help="methods of --mode topk (default Jaccard + AA)")
     args = ap.parse_args()
+    relaunch_if_needed(args)
     if args.mode == "svd":
         return run_svd(args)
     if args.mode == "topk":
@@ -658,20 +762,20 @@ def main():
     traffic, tsrc = pmc_traffic(kname)
     out["roofline"] = {"bound": "hbm", "achieved": byts / sec / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                        "frac": byts / sec / 1e9 / HBM_PEAK_GBS, "traffic": traffic,
+                       # the counters' HBM-side bytes over the same kernel time: what DRAM actually moved
+                       "frac_dram": (traffic / sec / 1e9 / HBM_PEAK_GBS) if traffic else None,
                        "kernel": "%s (%s side)" % (kname, name0), "alg_bytes_per_launch": byts,
                        "traffic_source": tsrc}
-    if dist.rank == 0 and not args.no_parity and args.sides == "both":
-        out["parity"] = parity_check(G, ex_x, ex_y, res["user"], res["business"])
-        import importlib
+    if dist.rank == 0 and args.sides == "both" and not (args.no_parity and args.no_cpu_baseline):
+        import coracle
 
-        sys.path.insert(0, os.path.join(ROOT, "bipartite-link-prediction_amd"))
-        ev = importlib.import_module("eval")
-        out["auc"] = {"u_cn": ev.roc_auc(ex_l, res["user"]["cn"]), "u_jaccard": ev.roc_auc(ex_l, res["user"]["jaccard"]),
-                      "u_adamic": ev.roc_auc(ex_l, res["user"]["adamic"]),
-                      "b_cn": ev.roc_auc(ex_l, res["business"]["cn"]),
-                      "b_jaccard": ev.roc_auc(ex_l, res["business"]["jaccard"])}
-    if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline and args.sides == "both":
-        out["cpu_baseline"] = cpu_baseline(G, ex_x, ex_y, args.cpu_seconds)
+        og = coracle.OracleGraph(G.n, *_dense_edges(G))
+        ora, multi = oracle_full(og, ex_x, ex_y)
+        if not args.no_parity:
+            out["parity"] = full_parity(ex_l, res, ora)
+        if dist.world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(og, ex_x, ex_y, args.cpu_seconds)
+            out["cpu_baseline"]["multicore"] = multi
     if dist.rank == 0:
         print(json.dumps(out), flush=True)
 

@@ -47,10 +47,16 @@ SIGNATURES = {
     "blp_csr_from_edges": [_I64, _I64, _P, _P, _P, _P, _P, ctypes.POINTER(ctypes.c_int64)],
     "blp_csr_from_edges_device": [_I32, _P, _P, _I64, _I64, _P, _P, _P, ctypes.POINTER(ctypes.c_int64)],
     "blp_graph_create": [_P, _P, _I64, _P, _I32, _PP],
+    "blp_csr_build_device": [_I32, _P, _P, _I64, _I64, _PP],
+    "blp_csr_info": [_P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)],
+    "blp_csr_fetch": [_P, _P, _P, _P],
+    "blp_csr_destroy": [_P],
+    "blp_graph_create_from_csr": [_P, _P, _P, _P, _PP],
     "blp_graph_destroy": [_P],
     "blp_graph_info": [_P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
                        ctypes.POINTER(ctypes.c_int)],
     "blp_graph_sync": [_P],
+    "blp_graph_aa_shift": [_P, ctypes.POINTER(ctypes.c_int)],
     "blp_score_pairs": [_P, _I32, _U32, _P, _P, _I64, _P, _P, _P],
     "blp_batch_create": [_P, _P, _P, _I64, _PP],
     "blp_batch_score": [_P, _P, _U32],

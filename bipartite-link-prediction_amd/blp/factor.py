@@ -16,6 +16,7 @@ _lib.register("blp_svd_topk_device", [_P, _P, _I64, _P, _P, _I32, _P, _P])
 _lib.register("blp_svd_topk", [_P, _P, _I64, _P, _P, _I32, _P, _P])
 _lib.register("blp_svd_stats", [_P, _I32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)])
 _lib.register("blp_svd_sync", [_P])
+_lib.register("blp_svd_stream_join", [_P, _P, _I32])
 
 
 class DeviceSVD:
@@ -28,6 +29,7 @@ class DeviceSVD:
             raise ValueError("factors must be (n_rows, k) and (n_cols, k)")
         self.n_rows, self.k = self.us.shape
         self.n_cols = self.v.shape[0]
+        self.device = device
         h = ctypes.c_void_p()
         check(lib().blp_svd_create(ptr(self.us), self.n_rows, ptr(self.v), self.n_cols, self.k, device,
                                    ctypes.byref(h)))
@@ -69,12 +71,39 @@ class DeviceSVD:
     def topk_device(self, users, topk, out_cols, out_scores, exclude=None):
         """blp_svd_topk_device: every argument a device-resident torch tensor on this handle's
         device (users int32 [n]; exclude (int64 offsets [n+1], int32 cols) or None; out_cols
-        int32 [n, topk], out_scores float64 [n, topk]). Enqueued on the handle's stream without a
-        sync (sync() waits)."""
-        eo = exclude[0].data_ptr() if exclude is not None else None
-        ec = exclude[1].data_ptr() if exclude is not None else None
-        check(lib().blp_svd_topk_device(self.handle, users.data_ptr(), users.numel(), eo, ec, topk,
+        int32 [n, topk], out_scores float64 [n, topk]), all contiguous.
+
+        Stream contract: the handle's stream first waits for the work queued so far on torch's
+        current stream (so inputs made by torch kernels are complete), and torch's current
+        stream then waits for the top-k (so the outputs are complete before torch reads,
+        reuses or frees them). Returns without a host sync (sync() waits)."""
+        import torch
+
+        dev = torch.device("cuda", self.device)
+        n = users.numel()
+
+        def want(t, name, dtype, shape):
+            if not isinstance(t, torch.Tensor) or t.device != dev or t.dtype != dtype or not t.is_contiguous() \
+                    or tuple(t.shape) != tuple(shape):
+                raise ValueError("topk_device: %s must be a contiguous %s tensor of shape %s on %s (got %s)" % (
+                    name, dtype, tuple(shape), dev, (getattr(t, "dtype", type(t)), tuple(getattr(t, "shape", ())),
+                                                   getattr(t, "device", None))))
+
+        if not 1 <= int(topk) <= 256:
+            raise ValueError("topk_device: topk must be in [1, 256]")
+        want(users, "users", torch.int32, (n,))
+        want(out_cols, "out_cols", torch.int32, (n, topk))
+        want(out_scores, "out_scores", torch.float64, (n, topk))
+        eo = ec = None
+        if exclude is not None:
+            want(exclude[0], "exclude offsets", torch.int64, (n + 1,))
+            want(exclude[1], "exclude cols", torch.int32, (exclude[1].numel(),))
+            eo, ec = exclude[0].data_ptr(), exclude[1].data_ptr()
+        cur = torch.cuda.current_stream(dev).cuda_stream
+        check(lib().blp_svd_stream_join(self.handle, cur, 1))
+        check(lib().blp_svd_topk_device(self.handle, users.data_ptr(), n, eo, ec, topk,
                                         out_cols.data_ptr(), out_scores.data_ptr()))
+        check(lib().blp_svd_stream_join(self.handle, cur, 0))
 
     def sync(self):
         check(lib().blp_svd_sync(self.handle))
@@ -158,7 +187,10 @@ def svds(M, k=6, tol=1e-12, max_iter=400, seed=0, device=0, stats=None, return_u
         for it in range(1, max_iter + 1):
             check(lib().blp_fact_step(h, ptr(S)))
             lam = np.sort(np.linalg.eigvalsh(_sym(S)))[::-1][:k]
-            if it > 1 and prev is not None and st.converged_at is None and np.max(np.abs(lam - prev) / np.abs(lam)) < tol:
+            # relative change, with the denominator floored at eps * lam_1: a zero Ritz value
+            # (rank(M) < k) must not turn the test into NaN and run all max_iter iterations
+            den = np.maximum(np.abs(lam), np.finfo(np.float64).eps * max(abs(lam[0]), np.finfo(np.float64).tiny))
+            if it > 1 and prev is not None and st.converged_at is None and np.max(np.abs(lam - prev) / den) < tol:
                 st.converged_at = it
             prev = lam
             st.iterations = it
@@ -174,6 +206,9 @@ def svds(M, k=6, tol=1e-12, max_iter=400, seed=0, device=0, stats=None, return_u
                 R = np.linalg.cholesky(Gs).T  # upper: G = R^T R
                 Rinv = np.ascontiguousarray(np.linalg.inv(R))
                 check(lib().blp_fact_apply_w(h, ptr(Rinv), 1 if rep == 1 else 0))
+        if st.converged_at is None:
+            raise RuntimeError("blp.factor.svds: the top-%d Ritz values did not settle to %g within %d iterations; "
+                               "raise max_iter or use scipy.sparse.linalg.svds" % (k, tol, max_iter))
         lam_all, V = np.linalg.eigh(_sym(S))
         order = np.argsort(-lam_all)
         Vd = np.zeros((Pw, Pw))

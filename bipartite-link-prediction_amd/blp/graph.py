@@ -155,15 +155,46 @@ class DeviceGraph(HostGraph):
 
     @classmethod
     def from_device_edges(cls, a_ptr, b_ptr, m, n, n_col0, device=0, aa=True):
-        """Build the CSR on `device` from device-resident int32 endpoints (m edges, dense ids in
-        [0, n)) -- the multi-GPU ingest path (blp.dist.allgather_edges) -- and upload it."""
-        rp = np.zeros(n + 1, np.int64)
-        ci = np.empty(max(2 * m, 1), np.int32)
-        sl = np.zeros(max(n, 1), np.uint8)
-        nnz = ctypes.c_int64(0)
-        check(lib().blp_csr_from_edges_device(device, ctypes.c_void_p(a_ptr), ctypes.c_void_p(b_ptr), m, n, ptr(rp),
-                                              ptr(ci), ptr(sl), ctypes.byref(nnz)))
-        return cls.from_csr(rp, ci[: nnz.value], sl[:n], n_col0, device=device, aa=aa)
+        """The multi-GPU ingest path (blp.dist.allgather_edges): build the CSR on `device` from
+        device-resident int32 endpoints (m edges, dense ids in [0, n)) and keep it there
+        (blp_csr_build_device -> blp_graph_create_from_csr: no host-to-device upload). The host
+        half (id map, degrees, Adamic-Adar weights with the reference's math.log) comes from
+        one device-to-host copy of the CSR, which the handle borrows as its planning mirror.
+        ``build_times`` records the phases."""
+        import time
+
+        L = lib()
+        t = {}
+        t0 = time.perf_counter()
+        c = ctypes.c_void_p()
+        check(L.blp_csr_build_device(device, ctypes.c_void_p(a_ptr), ctypes.c_void_p(b_ptr), m, n, ctypes.byref(c)))
+        t["device_csr_s"] = time.perf_counter() - t0
+        try:
+            nn, nnz = ctypes.c_int64(), ctypes.c_int64()
+            check(L.blp_csr_info(c, ctypes.byref(nn), ctypes.byref(nnz)))
+            t0 = time.perf_counter()
+            rp = np.empty(n + 1, np.int64)
+            ci = np.empty(max(nnz.value, 1), np.int32)
+            sl = np.empty(max(n, 1), np.uint8)
+            check(L.blp_csr_fetch(c, ptr(rp), ptr(ci), ptr(sl)))
+            t["fetch_s"] = time.perf_counter() - t0
+            t0 = time.perf_counter()
+            g = HostGraph.from_csr.__func__(cls, rp, ci[: nnz.value], sl[:n], n_col0, aa)
+            t["host_half_s"] = time.perf_counter() - t0
+            t0 = time.perf_counter()
+            h = ctypes.c_void_p()
+            check(L.blp_graph_create_from_csr(c, ptr(g.row_ptr), ptr(ci), ptr(g.aa_weight) if aa else None,
+                                              ctypes.byref(h)))
+            c = None  # consumed
+            t["graph_create_s"] = time.perf_counter() - t0
+        finally:
+            if c is not None:
+                L.blp_csr_destroy(c)
+        g._mirror = ci  # the handle borrows row_ptr / col_idx (their full allocations)
+        g.device = device
+        g.handle = h
+        g.build_times = t
+        return g
 
     def _upload(self, device, aa):
         self.device = device
@@ -171,6 +202,13 @@ class DeviceGraph(HostGraph):
         check(lib().blp_graph_create(ptr(self.row_ptr), ptr(self.col_idx), self.n,
                                      ptr(self.aa_weight) if aa else None, device, ctypes.byref(h)))
         self.handle = h
+
+    @property
+    def aa_shift(self):
+        """Fixed-point scale (2^-shift) of the Adamic-Adar sums (blp_graph_aa_shift)."""
+        v = ctypes.c_int(0)
+        check(lib().blp_graph_aa_shift(self.handle, ctypes.byref(v)))
+        return v.value
 
     # ------------------------------------------------------------------ lifecycle
     def close(self):

@@ -42,9 +42,13 @@ struct DevBuf {
   template <class T> T* as() const { return reinterpret_cast<T*>(p); }
 };
 
-// Adamic-Adar terms are summed in 2^-40 fixed point: exact, order-independent integer sums
-// (the reference's own order is Python set order); |term| <= 1/ln 2 < 2^1.
-constexpr double AA_SCALE = 1099511627776.0;  // 2^40
+// Adamic-Adar terms are summed in 2^-s fixed point: exact, order-independent integer sums
+// (the reference's own order is Python set order); |term| <= 1/ln 2 < 2^1. s = AA_SHIFT (40)
+// unless the graph could overflow a signed 64-bit sum at that scale: blp_graph_create bounds
+// every pair's sum by max_row_len * (max_weight * 2^s + 1/2) and lowers s until the bound is
+// below 2^63 (blp_graph::aa_shift). CN <= |N(y)| <= max_row_len < 2^31 and weight < 2^0.53
+// keep s >= 31 on any graph an int32 CSR can hold.
+constexpr int AA_SHIFT = 40;
 
 enum KernelId { K_SCORE = 0, K_GROUP = 1, K_SVD_PAIRS = 2, K_SVD_TOPK = 3, K_WALK = 4, K_HOP3 = 5, K_COUNT = 6 };
 
@@ -70,7 +74,8 @@ struct blp_graph {
   int64_t nnz = 0;  // stored CSR entries (both directions, no self-loops)
   int64_t* d_rp = nullptr;   // [n+1]
   int32_t* d_ci = nullptr;   // [nnz], CI_PAD readable ids on each side
-  long long* d_aaw_fx = nullptr;  // [n] Adamic-Adar weight per node, fixed point 2^-40 (or null)
+  long long* d_aaw_fx = nullptr;  // [n] Adamic-Adar weight per node, fixed point 2^-aa_shift (or null)
+  int aa_shift = blp::AA_SHIFT;   // fixed-point scale of d_aaw_fx (overflow guard, blp_internal.h)
   // weight-coded copy of d_ci for the scorers: ci | code(ci) << id_bits, code 1..255 naming
   // one of the graph's most used weights (d_wtab[code]), 0 = look up d_aaw_fx (or null)
   int32_t* d_ci_w = nullptr;
@@ -89,9 +94,13 @@ struct blp_graph {
   int32_t* d_wedge = nullptr;
   int64_t wedge_vecs = 0;
   std::vector<int64_t> h_wp;  // host copy of d_wp (heavy-source planning)
-  // host mirrors used only for launch planning (bitmap universe bounds)
+  // host mirrors used for launch planning (bitmap universe bounds) and the host-built indexes:
+  // owned copies (blp_graph_create), or the caller's buffers (blp_graph_create_from_csr, which
+  // requires them to outlive the handle)
   std::vector<int64_t> h_rp;
   std::vector<int32_t> h_ci;
+  const int64_t* hrp = nullptr;
+  const int32_t* hci = nullptr;
   blp::KernelTimer timers[blp::K_COUNT];
 };
 
@@ -109,6 +118,7 @@ struct __attribute__((aligned(4))) U4a {
 };
 constexpr int SHORT_ROW_MAX = 32;  // the short-row scorer's row bound (pairs.hip SHORT_MAX)
 int build_hot_index(blp_graph* g);
+int graph_finish(blp_graph* g, const double* aaw);
 int build_wedge_index(blp_graph* g);
 void free_wedge_index(blp_graph* g);
 void free_hot_index(blp_graph* g);

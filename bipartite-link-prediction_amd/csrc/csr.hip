@@ -56,32 +56,64 @@ __global__ void k_low_halves(const uint64_t* keys, int64_t nnz, int32_t* ci) {
 
 using namespace blp;
 
-extern "C" int blp_csr_from_edges_device(int device, const int32_t* d_a, const int32_t* d_b, int64_t m, int64_t n,
-                                         int64_t* row_ptr, int32_t* col_idx, uint8_t* self_loop, int64_t* nnz_out) {
-  BLP_CHECK(n >= 0 && m >= 0 && row_ptr && nnz_out && (m == 0 || (d_a && d_b && col_idx)), BLP_E_ARG,
-            "blp_csr_from_edges_device: bad arguments");
-  BLP_CHECK(n < (int64_t(1) << 31), BLP_E_ARG, "blp_csr_from_edges_device: n_nodes must fit int32");
+// A CSR built on the device and kept there (blp_csr_build_device): the row offsets, the
+// padded column ids (CI_PAD ids of zeros on each side, the layout blp_graph uses) and the
+// self-loop flags. blp_graph_create_from_csr adopts the buffers; no host round trip.
+struct blp_csr {
+  int device = 0;
+  int64_t n = 0, nnz = 0;
+  int64_t* d_rp = nullptr;   // [n + 1]
+  int32_t* d_ci = nullptr;   // [nnz], CI_PAD ids readable on each side (allocation starts at d_ci - CI_PAD)
+  uint8_t* d_self = nullptr; // [max(n, 1)]
+};
+
+extern "C" int blp_csr_destroy(blp_csr* c) {
+  if (!c) return BLP_OK;
+  (void)hipSetDevice(c->device);
+  if (c->d_rp) (void)hipFree(c->d_rp);
+  if (c->d_ci) (void)hipFree(c->d_ci - CI_PAD);
+  if (c->d_self) (void)hipFree(c->d_self);
+  delete c;
+  return BLP_OK;
+}
+
+extern "C" int blp_csr_build_device(int device, const int32_t* d_a, const int32_t* d_b, int64_t m, int64_t n,
+                                    blp_csr** out) {
+  BLP_CHECK(out && n >= 0 && m >= 0 && (m == 0 || (d_a && d_b)), BLP_E_ARG, "blp_csr_build_device: bad arguments");
+  BLP_CHECK(n < (int64_t(1) << 31), BLP_E_ARG, "blp_csr_build_device: n_nodes must fit int32");
+  int ndev = 0;
+  BLP_HIP(hipGetDeviceCount(&ndev));
+  BLP_CHECK(device >= 0 && device < ndev, BLP_E_ARG, "blp_csr_build_device: no such device");
   BLP_HIP(hipSetDevice(device));
+  // the endpoints come from another stream (the RCCL all-gather, a torch copy): a one-off
+  // ingest step, so wait for everything queued on the device rather than ask for a stream
+  BLP_HIP(hipDeviceSynchronize());
   hipStream_t st = nullptr;
   BLP_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-  DevBuf keys, sorted, temp, rp, selfb, flag, nsel;
+  blp_csr* c = new blp_csr();
+  c->device = device;
+  c->n = n;
+  DevBuf keys, sorted, temp, flag, nsel;
   auto done = [&](int rc) {
-    for (DevBuf* b : {&keys, &sorted, &temp, &rp, &selfb, &flag, &nsel}) b->release();
+    for (DevBuf* b : {&keys, &sorted, &temp, &flag, &nsel}) b->release();
+    (void)hipStreamSynchronize(st);
     (void)hipStreamDestroy(st);
+    if (rc != BLP_OK) blp_csr_destroy(c);
     return rc;
   };
   int rc;
   const int64_t mk = 2 * m;
-  if ((rc = keys.reserve(8 * std::max<int64_t>(mk, 1))) || (rc = sorted.reserve(8 * std::max<int64_t>(mk, 1))) ||
-      (rc = rp.reserve(8 * (n + 1))) || (rc = selfb.reserve(std::max<int64_t>(n, 1))) || (rc = flag.reserve(4)) ||
-      (rc = nsel.reserve(8)))
-    return done(rc);
-  BLP_HIP_OR(hipMemsetAsync(selfb.p, 0, std::max<int64_t>(n, 1), st), done);
+  BLP_HIP_OR(hipMalloc(&c->d_rp, 8 * (n + 1)), done);
+  BLP_HIP_OR(hipMalloc(&c->d_self, std::max<int64_t>(n, 1)), done);
+  if ((rc = flag.reserve(4)) || (rc = nsel.reserve(8))) return done(rc);
+  BLP_HIP_OR(hipMemsetAsync(c->d_self, 0, std::max<int64_t>(n, 1), st), done);
   BLP_HIP_OR(hipMemsetAsync(flag.p, 0, 4, st), done);
+  BLP_HIP_OR(hipMemsetAsync(c->d_rp, 0, 8 * (n + 1), st), done);
   int64_t nnz = 0;
   if (m) {
-    hipLaunchKernelGGL(k_edge_keys, dim3(4096), dim3(256), 0, st, d_a, d_b, m, n, keys.as<uint64_t>(),
-                       selfb.as<uint8_t>(), flag.as<int>());
+    if ((rc = keys.reserve(8 * mk)) || (rc = sorted.reserve(8 * mk))) return done(rc);
+    hipLaunchKernelGGL(k_edge_keys, dim3(4096), dim3(256), 0, st, d_a, d_b, m, n, keys.as<uint64_t>(), c->d_self,
+                       flag.as<int>());
     BLP_HIP_OR(hipGetLastError(), done);
     // sort only the bits that carry ids: 32 + ceil(log2 n) (KEY_NONE has them all set)
     int idbits = 1;
@@ -104,25 +136,84 @@ extern "C" int blp_csr_from_edges_device(int device, const int32_t* d_a, const i
     BLP_HIP_OR(hipMemcpyAsync(&nu, nsel.p, 8, hipMemcpyDeviceToHost, st), done);
     BLP_HIP_OR(hipMemcpyAsync(&bad, flag.p, 4, hipMemcpyDeviceToHost, st), done);
     BLP_HIP_OR(hipStreamSynchronize(st), done);
-    if (bad) return done(fail(BLP_E_ARG, "blp_csr_from_edges_device: node id out of range"));
+    if (bad) return done(fail(BLP_E_ARG, "blp_csr_build_device: node id out of range"));
     nnz = nu;
     if (nnz > 0) {  // a trailing KEY_NONE (self-loops present) is not an entry
       uint64_t last = 0;
-      BLP_HIP_OR(hipMemcpy(&last, keys.as<uint64_t>() + nnz - 1, 8, hipMemcpyDeviceToHost), done);
+      BLP_HIP_OR(hipMemcpyAsync(&last, keys.as<uint64_t>() + nnz - 1, 8, hipMemcpyDeviceToHost, st), done);
+      BLP_HIP_OR(hipStreamSynchronize(st), done);
       if (last == KEY_NONE) --nnz;
     }
-    hipLaunchKernelGGL(k_row_ptr, dim3(2048), dim3(256), 0, st, keys.as<uint64_t>(), nnz, n, rp.as<int64_t>());
+    sorted.release();
+    temp.release();
+    hipLaunchKernelGGL(k_row_ptr, dim3(2048), dim3(256), 0, st, keys.as<uint64_t>(), nnz, n, c->d_rp);
     BLP_HIP_OR(hipGetLastError(), done);
-    // the low halves go into the (now free) sort buffer, then to the host
-    hipLaunchKernelGGL(k_low_halves, dim3(4096), dim3(256), 0, st, keys.as<uint64_t>(), nnz, sorted.as<int32_t>());
-    BLP_HIP_OR(hipGetLastError(), done);
-    BLP_HIP_OR(hipMemcpyAsync(row_ptr, rp.p, 8 * (n + 1), hipMemcpyDeviceToHost, st), done);
-    if (nnz) BLP_HIP_OR(hipMemcpyAsync(col_idx, sorted.p, 4 * nnz, hipMemcpyDeviceToHost, st), done);
-  } else {
-    for (int64_t i = 0; i <= n; ++i) row_ptr[i] = 0;
   }
-  if (self_loop && n) BLP_HIP_OR(hipMemcpyAsync(self_loop, selfb.p, n, hipMemcpyDeviceToHost, st), done);
+  BLP_HIP_OR(hipMalloc(&c->d_ci, sizeof(int32_t) * (nnz + 2 * CI_PAD)), done);
+  c->d_ci += CI_PAD;
+  BLP_HIP_OR(hipMemsetAsync(c->d_ci - CI_PAD, 0, sizeof(int32_t) * (nnz + 2 * CI_PAD), st), done);
+  if (nnz) {
+    hipLaunchKernelGGL(k_low_halves, dim3(4096), dim3(256), 0, st, keys.as<uint64_t>(), nnz, c->d_ci);
+    BLP_HIP_OR(hipGetLastError(), done);
+  }
   BLP_HIP_OR(hipStreamSynchronize(st), done);
-  *nnz_out = nnz;
+  c->nnz = nnz;
+  *out = c;
   return done(BLP_OK);
+}
+
+extern "C" int blp_csr_info(const blp_csr* c, int64_t* n_nodes, int64_t* nnz) {
+  BLP_CHECK(c, BLP_E_ARG, "blp_csr_info: null csr");
+  if (n_nodes) *n_nodes = c->n;
+  if (nnz) *nnz = c->nnz;
+  return BLP_OK;
+}
+
+extern "C" int blp_csr_fetch(const blp_csr* c, int64_t* row_ptr, int32_t* col_idx, uint8_t* self_loop) {
+  BLP_CHECK(c, BLP_E_ARG, "blp_csr_fetch: null csr");
+  BLP_HIP(hipSetDevice(c->device));
+  if (row_ptr) BLP_HIP(hipMemcpy(row_ptr, c->d_rp, 8 * (c->n + 1), hipMemcpyDeviceToHost));
+  if (col_idx && c->nnz) BLP_HIP(hipMemcpy(col_idx, c->d_ci, 4 * c->nnz, hipMemcpyDeviceToHost));
+  if (self_loop && c->n) BLP_HIP(hipMemcpy(self_loop, c->d_self, c->n, hipMemcpyDeviceToHost));
+  return BLP_OK;
+}
+
+extern "C" int blp_graph_create_from_csr(blp_csr* c, const int64_t* row_ptr, const int32_t* col_idx,
+                                         const double* aaw, blp_graph** out) {
+  BLP_CHECK(c && out && row_ptr && (c->nnz == 0 || col_idx), BLP_E_ARG, "blp_graph_create_from_csr: bad arguments");
+  BLP_CHECK(row_ptr[c->n] == c->nnz, BLP_E_ARG, "blp_graph_create_from_csr: host mirror does not match the csr");
+  BLP_HIP(hipSetDevice(c->device));
+  blp_graph* g = new blp_graph();
+  g->device = c->device;
+  g->n = c->n;
+  g->nnz = c->nnz;
+  g->hrp = row_ptr;  // borrowed: the caller keeps them alive and unchanged for the graph's lifetime
+  g->hci = col_idx;
+  g->d_rp = c->d_rp;  // the device CSR, adopted once everything derived from it is built
+  g->d_ci = c->d_ci;
+  int rc = graph_finish(g, aaw);
+  if (rc != BLP_OK) {
+    g->d_rp = nullptr;  // c still owns its buffers: the caller may retry or destroy it
+    g->d_ci = nullptr;
+    blp_graph_destroy(g);
+    return rc;
+  }
+  c->d_rp = nullptr;  // c is consumed
+  c->d_ci = nullptr;
+  blp_csr_destroy(c);
+  *out = g;
+  return BLP_OK;
+}
+
+extern "C" int blp_csr_from_edges_device(int device, const int32_t* d_a, const int32_t* d_b, int64_t m, int64_t n,
+                                         int64_t* row_ptr, int32_t* col_idx, uint8_t* self_loop, int64_t* nnz_out) {
+  BLP_CHECK(n >= 0 && m >= 0 && row_ptr && nnz_out && (m == 0 || (d_a && d_b && col_idx)), BLP_E_ARG,
+            "blp_csr_from_edges_device: bad arguments");
+  blp_csr* c = nullptr;
+  int rc = blp_csr_build_device(device, d_a, d_b, m, n, &c);
+  if (rc) return rc;
+  rc = blp_csr_fetch(c, row_ptr, col_idx, self_loop);
+  if (!rc) *nnz_out = c->nnz;
+  blp_csr_destroy(c);
+  return rc;
 }

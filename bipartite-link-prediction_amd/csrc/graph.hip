@@ -180,6 +180,47 @@ int build_weight_codes(blp_graph* g, const int64_t* row_ptr, const std::vector<l
   return BLP_OK;
 }
 
+// Overflow guard of the fixed-point Adamic-Adar sums (blp_internal.h): the largest shift
+// s <= AA_SHIFT (or BLP_AA_SHIFT, a test knob that may ask for more) such that no pair's sum
+// can reach 2^63: a pair's common neighbours are members of one row N(y), so the sum is at
+// most max_row_len terms of at most llrint(max_weight * 2^s) <= max_weight * 2^s + 1/2.
+int aa_fixed_shift(const int64_t* row_ptr, const double* aaw, int64_t n) {
+  int64_t dmax = 0;
+  double wmax = 0.0;
+  for (int64_t i = 0; i < n; ++i) {
+    dmax = std::max<int64_t>(dmax, row_ptr[i + 1] - row_ptr[i]);
+    wmax = std::max(wmax, std::fabs(aaw[i]));
+  }
+  int s = AA_SHIFT;
+  if (const char* e = getenv("BLP_AA_SHIFT")) s = std::max(0, std::min(62, atoi(e)));
+  const double lim = std::ldexp(1.0, 63) * (1.0 - 1e-12);
+  while (s > 0 && (double)dmax * (wmax * std::ldexp(1.0, s) + 0.5) >= lim) --s;
+  return s;
+}
+
+// Everything a graph handle derives from its CSR once g->d_rp / g->d_ci (device) and
+// g->hrp / g->hci (host mirrors) are in place: stream, CU count, fixed-point Adamic-Adar
+// weights and the weight-coded id stream, the dense-row index and the wedge rows.
+int graph_finish(blp_graph* g, const double* aaw) {
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, g->device) == hipSuccess) g->n_cu = prop.multiProcessorCount;
+  if (!g->stream) BLP_HIP(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
+  const int64_t n = g->n;
+  if (aaw) {
+    g->aa_shift = aa_fixed_shift(g->hrp, aaw, n);
+    const double scale = std::ldexp(1.0, g->aa_shift);
+    std::vector<long long> fx((size_t)n);
+    for (int64_t i = 0; i < n; ++i) fx[i] = llrint(aaw[i] * scale);
+    BLP_HIP(hipMalloc(&g->d_aaw_fx, sizeof(long long) * std::max<int64_t>(n, 1)));
+    if (n) BLP_HIP(hipMemcpy(g->d_aaw_fx, fx.data(), sizeof(long long) * n, hipMemcpyHostToDevice));
+    int rc = build_weight_codes(g, g->hrp, fx);
+    if (rc != BLP_OK) return rc;
+  }
+  int rc = build_hot_index(g);
+  if (rc != BLP_OK) return rc;
+  return build_wedge_index(g);
+}
+
 }  // namespace blp
 
 using namespace blp;
@@ -262,14 +303,7 @@ int blp_graph_create(const int64_t* row_ptr, const int32_t* col_idx, int64_t n, 
   g->n = n;
   g->nnz = nnz;
   int rc = BLP_OK;
-  auto cleanup = [&](int code) {
-    blp_graph_destroy(g);
-    return code;
-  };
-  hipDeviceProp_t prop;
-  if (hipGetDeviceProperties(&prop, device) == hipSuccess) g->n_cu = prop.multiProcessorCount;
   if ((rc = [&]() -> int {
-         BLP_HIP(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
          BLP_HIP(hipMalloc(&g->d_rp, sizeof(int64_t) * (n + 1)));
          // padded on both sides (CI_PAD ids): the scorers read rows in 16-byte vectors, up to
          // 15 ids past a row end or before a row start
@@ -278,20 +312,19 @@ int blp_graph_create(const int64_t* row_ptr, const int32_t* col_idx, int64_t n, 
          g->d_ci += CI_PAD;
          BLP_HIP(hipMemcpy(g->d_rp, row_ptr, sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice));
          if (nnz) BLP_HIP(hipMemcpy(g->d_ci, col_idx, sizeof(int32_t) * nnz, hipMemcpyHostToDevice));
-         if (aaw) {
-           std::vector<long long> fx((size_t)n);
-           for (int64_t i = 0; i < n; ++i) fx[i] = llrint(aaw[i] * AA_SCALE);
-           BLP_HIP(hipMalloc(&g->d_aaw_fx, sizeof(long long) * std::max<int64_t>(n, 1)));
-           if (n) BLP_HIP(hipMemcpy(g->d_aaw_fx, fx.data(), sizeof(long long) * n, hipMemcpyHostToDevice));
-           if ((rc = build_weight_codes(g, row_ptr, fx)) != BLP_OK) return rc;
-         }
          return BLP_OK;
-       }()) != BLP_OK)
-    return cleanup(rc);
+       }()) != BLP_OK) {
+    blp_graph_destroy(g);
+    return rc;
+  }
   g->h_rp.assign(row_ptr, row_ptr + n + 1);
   g->h_ci.assign(col_idx, col_idx + nnz);
-  if ((rc = build_hot_index(g)) != BLP_OK) return cleanup(rc);
-  if ((rc = build_wedge_index(g)) != BLP_OK) return cleanup(rc);
+  g->hrp = g->h_rp.data();
+  g->hci = g->h_ci.data();
+  if ((rc = graph_finish(g, aaw)) != BLP_OK) {
+    blp_graph_destroy(g);
+    return rc;
+  }
   *out = g;
   return BLP_OK;
 }
@@ -310,6 +343,12 @@ int blp_graph_destroy(blp_graph* g) {
   if (g->d_wtab) (void)hipFree(g->d_wtab);
   if (g->stream) (void)hipStreamDestroy(g->stream);
   delete g;
+  return BLP_OK;
+}
+
+int blp_graph_aa_shift(const blp_graph* g, int* shift) {
+  BLP_CHECK(g && shift, BLP_E_ARG, "blp_graph_aa_shift: bad arguments");
+  *shift = g->aa_shift;
   return BLP_OK;
 }
 

@@ -33,8 +33,8 @@ int build_hot_index(blp_graph* g) {
   int64_t hot_min = 2048, density = 64;
   if (const char* e = getenv("BLP_HOT_MIN")) hot_min = std::max<int64_t>(1, atoll(e));
   if (const char* e = getenv("BLP_HOT_DENSITY")) density = std::max<int64_t>(1, atoll(e));
-  const int64_t* rp = g->h_rp.data();
-  const int32_t* ci = g->h_ci.data();
+  const int64_t* rp = g->hrp;
+  const int32_t* ci = g->hci;
   std::vector<int32_t> idx((size_t)g->n, -1), rows;
   std::vector<HotRow> tab;
   int64_t vecs = 0;

@@ -1192,6 +1192,7 @@ struct ScoreArgs {
   int short_rows;    // bit 0: every build row <= SHORT_MAX ids, bit 1: every scan row (row_build / row_scan)
   const int64_t* wp;    // wedge rows (wedge.hip; short-row scorer only, null: build from CSR)
   const uint4* wedge;
+  double aa_inv;        // 2^-aa_shift: fixed-point Adamic-Adar sum -> double (blp_graph::aa_shift)
 };
 
 template <int BLOCK>
@@ -1491,7 +1492,7 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
           for (int t = threadIdx.x; t < ns; t += BLOCK) {  // ns <= SEG <= BLOCK: t == threadIdx.x
             const int p = pout;
             unsigned c = s_cn[t];
-            double av = SAA ? (double)s_aa[t] * (1.0 / blp::AA_SCALE) : 0.0;
+            double av = SAA ? (double)s_aa[t] * a.aa_inv : 0.0;
             if (ch > 0) {
               c += a.cn[p];
               if (want_a) av += a.aa[p];
@@ -1601,7 +1602,7 @@ __global__ __launch_bounds__(BLOCK) void k_score_global(ScoreArgs a, uint32_t* g
           const int p = a.g_out[pbeg + sb + t];
           const unsigned c = s_cn[t];
           a.cn[p] = c;
-          if (want_a) a.aa[p] = (double)s_aa[t] * (1.0 / blp::AA_SCALE);
+          if (want_a) a.aa[p] = (double)s_aa[t] * a.aa_inv;
           if (want_j) {
             const long long uni = (long long)h2 + (s_off[t + 1] - s_off[t]) - (long long)c;
             if (uni <= 0) {
@@ -1805,7 +1806,7 @@ __global__ __launch_bounds__(256) void k_split_combine(ScoreArgs a, int C, const
       }
       const int p = a.g_out[gp];
       a.cn[p] = cn;
-      if (want_a) a.aa[p] = (double)aa * (1.0 / blp::AA_SCALE);
+      if (want_a) a.aa[p] = (double)aa * a.aa_inv;
       if (want_j) {
         const long long uni = h2 + a.g_yl[gp] - (long long)cn;
         if (uni <= 0) {
@@ -1962,7 +1963,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_score_wave(ScoreArgs a) {
           const int p = pout;
           const unsigned c = s_cn[lane];
           a.cn[p] = c;
-          if (want_a) a.aa[p] = (double)s_aa[lane] * (1.0 / blp::AA_SCALE);
+          if (want_a) a.aa[p] = (double)s_aa[lane] * a.aa_inv;
           if (want_j) {
             const long long uni = (long long)h2 + len - (long long)c;
             if (uni <= 0) {
@@ -2121,8 +2122,8 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   BLP_CHECK(g && out && n_pairs >= 0 && (n_pairs == 0 || (x && y)), BLP_E_ARG, "blp_batch_create: bad arguments");
   BLP_CHECK(n_pairs < (int64_t(1) << 31) - 1, BLP_E_ARG, "blp_batch_create: at most 2^31-2 pairs per batch");
   const int64_t n = g->n;
-  const int64_t* rp = g->h_rp.data();
-  const int32_t* ci = g->h_ci.data();
+  const int64_t* rp = g->hrp;
+  const int32_t* ci = g->hci;
   // ---- plan: node universe touched by H2(x) and N(y); per-source build work
   int64_t lo = INT64_MAX, hi = INT64_MIN;
   std::vector<uint8_t> seen((size_t)n, 0);
@@ -2493,6 +2494,7 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   a.rp = g->d_rp;
   a.ci = g->d_ci;
   a.aaw = g->d_aaw_fx;
+  a.aa_inv = std::ldexp(1.0, -g->aa_shift);
   const bool coded = g->d_ci_w && !getenv("BLP_NO_WCODES");  // tuning knob
   a.cw = coded ? g->d_ci_w : g->d_ci;
   a.idbits = coded ? g->id_bits : 31;

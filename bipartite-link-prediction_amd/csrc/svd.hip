@@ -28,6 +28,7 @@ struct blp_svd {
   double* d_v = nullptr;   // [n_cols][kpad]
   double* d_vt = nullptr;  // [kpad][ncol_pad]
   blp::KernelTimer t_pairs, t_topk;
+  hipEvent_t join_ev = nullptr;  // blp_svd_stream_join
   double* d_ps = nullptr;  // top-k scratch: per (user, chunk) partial lists, part_cap entries
   int32_t* d_pc = nullptr;
   int64_t part_cap = 0;
@@ -78,6 +79,7 @@ struct TopkArgs {
   int n_chunks;
   double* part_score;      // [n_users][n_chunks][topk]
   int32_t* part_col;
+  int64_t n_rows;          // rows of us: a selected row outside [0, n_rows) reads no memory
 };
 
 // better = higher score, then lower column
@@ -162,7 +164,8 @@ __global__ __launch_bounds__(WAVES * 64) void k_svd_topk(TopkArgs a) {
 #pragma unroll
   for (int t = 0; t < RT; ++t) {
     const int64_t ui = u0 + 16 * t + (lane & 15);
-    const int64_t row = ui < a.n_users ? a.users[ui] : -1;
+    int64_t row = ui < a.n_users ? a.users[ui] : -1;
+    if (row >= a.n_rows) row = -1;  // device-side guard (blp_svd_topk_device does not range-check)
 #pragma unroll
     for (int s = 0; s < KS; ++s) af[t][s] = row >= 0 ? a.us[row * KPAD + 4 * s + (lane >> 4)] : 0.0;
   }
@@ -394,6 +397,7 @@ int blp_svd_destroy(blp_svd* h) {
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   timer_release(h->t_pairs);
   timer_release(h->t_topk);
+  if (h->join_ev) (void)hipEventDestroy(h->join_ev);
   for (void* p : {(void*)h->d_us, (void*)h->d_v, (void*)h->d_vt, (void*)h->d_ps, (void*)h->d_pc})
     if (p) (void)hipFree(p);
   if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -489,7 +493,7 @@ static int svd_topk_enqueue(blp_svd* h, const int32_t* d_users, int64_t n_users,
     h->part_cap = np;
   }
   TopkArgs a{h->d_us, h->d_vt, d_users, d_exo, d_exc, n_users, h->n_cols, h->ncol_pad, h->kpad, topk, chunk, n_chunks,
-             h->d_ps, h->d_pc};
+             h->d_ps, h->d_pc, h->n_rows};
   hipEvent_t t0;
   int rc = timer_begin(h->t_topk, h->stream, &t0);
   if (rc) return rc;
@@ -572,6 +576,21 @@ int blp_svd_stats(blp_svd* h, int which, double* total_ms, int64_t* launches) {
   if (rc) return rc;
   if (total_ms) *total_ms = t.total_ms;
   if (launches) *launches = t.launches;
+  return BLP_OK;
+}
+
+int blp_svd_stream_join(blp_svd* h, void* stream, int handle_waits) {
+  BLP_CHECK(h, BLP_E_ARG, "blp_svd_stream_join: null handle");
+  BLP_HIP(hipSetDevice(h->device));
+  if (!h->join_ev) BLP_HIP(hipEventCreateWithFlags(&h->join_ev, hipEventDisableTiming));
+  hipStream_t other = (hipStream_t)stream;
+  if (handle_waits) {
+    BLP_HIP(hipEventRecord(h->join_ev, other));
+    BLP_HIP(hipStreamWaitEvent(h->stream, h->join_ev, 0));
+  } else {
+    BLP_HIP(hipEventRecord(h->join_ev, h->stream));
+    BLP_HIP(hipStreamWaitEvent(other, h->join_ev, 0));
+  }
   return BLP_OK;
 }
 

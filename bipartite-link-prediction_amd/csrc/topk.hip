@@ -677,8 +677,8 @@ extern "C" int blp_topk_create(blp_graph* g, int64_t src_lo, int64_t src_hi, int
   BLP_CHECK(0 <= src_lo && src_lo <= src_hi && src_hi <= g->n && 0 <= tgt_lo && tgt_lo < tgt_hi && tgt_hi <= g->n,
             BLP_E_ARG, "blp_topk_create: bad id ranges");
   BLP_CHECK(src_hi <= tgt_lo || tgt_hi <= src_lo, BLP_E_ARG, "blp_topk_create: source and target ranges overlap");
-  const int64_t* rp = g->h_rp.data();
-  const int32_t* ci = g->h_ci.data();
+  const int64_t* rp = g->hrp;
+  const int32_t* ci = g->hci;
   // bipartite check: every source row points into the targets and every target row into the sources
   for (int64_t v = src_lo; v < src_hi; ++v)
     for (int64_t e = rp[v]; e < rp[v + 1]; ++e)
@@ -942,7 +942,7 @@ extern "C" int blp_topk_fetch(blp_topk* t, uint32_t method, int32_t* cols, doubl
         if (c[i] >= 0) {
           if (m == 0) v = (double)keys[i];
           else if (m == 1) { memcpy(&v, &keys[i], 8); }
-          else v = (double)(long long)keys[i] * (1.0 / AA_SCALE);
+          else v = (double)(long long)keys[i] * std::ldexp(1.0, -t->g->aa_shift);
         }
         scores[i] = v;
       }

@@ -23,8 +23,8 @@ int build_wedge_index(blp_graph* g) {
   if (const char* e = getenv("BLP_WEDGE"))
     if (atoi(e) == 0) return BLP_OK;
   const int64_t n = g->n;
-  const int64_t* rp = g->h_rp.data();
-  const int32_t* ci = g->h_ci.data();
+  const int64_t* rp = g->hrp;
+  const int32_t* ci = g->hci;
   if (n == 0 || g->nnz == 0) return BLP_OK;
   double max_x = 8.0;
   if (const char* e = getenv("BLP_WEDGE_MAX_X")) max_x = atof(e);

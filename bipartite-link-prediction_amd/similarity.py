@@ -1,6 +1,9 @@
 """Drop-in for the reference's similarity.py, computed by the HIP engine (libblp.so).
 
-Same call surface (similarity.py:11-126) and the same score files, bit-for-bit in value:
+Same call surface (similarity.py:11-126) and the same score files: common_neighbors and
+jaccard bit-exact, adamic_adar within ~1e-12 absolute (an exact, order-independent
+2^-40 fixed-point sum of the reference's float terms; the reference sums in Python set
+order, so its own last bits depend on that order):
 
 * ``main(example_file, graph_file, u_methods, u_outfiles, b_methods, b_outfiles)``
 * ``users(examples, G, methods, outfiles)`` / ``business(examples, G, methods, outfiles)``

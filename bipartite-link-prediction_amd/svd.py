@@ -44,11 +44,17 @@ def factorize(M, k, factor="auto", device=0):
     k < 128)."""
     from blp import factor as F
 
-    if factor == "auto":
+    auto = factor == "auto"
+    if auto:
         factor = "gpu" if min(M.shape) >= 256 and k < F.block_width() else "host"
     if factor == "gpu":
-        us, s, v = F.svds(M, k=k, device=device, return_us=True)
-        return us, np.ascontiguousarray(v.T)
+        try:
+            us, s, v = F.svds(M, k=k, device=device, return_us=True)
+            return us, np.ascontiguousarray(v.T)
+        except RuntimeError as e:  # Ritz values did not settle: 'auto' takes the reference's ARPACK
+            if not auto or isinstance(e, (blp.BLPError, blp.BLPUnavailable)):
+                raise
+            print("GPU factorisation did not converge (%s); using scipy.sparse.linalg.svds" % e)
     u, s, vt = sparse.linalg.svds(M, k=k)
     return u * s, vt
 

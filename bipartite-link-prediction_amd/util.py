@@ -22,9 +22,14 @@ def load_json(fname):
 
 
 def write_json(d, fname):
-    """Writes dictionary d to fname (util.py:18-21)."""
+    """Writes dictionary d to fname (util.py:18-21). A binary sidecar left beside an older
+    version of the file is removed (it would describe the old scores)."""
+    import os
+
     with open(fname, "w") as f:
         f.write(json.dumps(d))
+    if os.path.exists(fname + ".npz"):
+        os.unlink(fname + ".npz")
 
 
 def write_sidecar(d, fname):
@@ -32,7 +37,11 @@ def write_sidecar(d, fname):
     ``write_json(d, fname)``: int64 ``users`` / ``businesses``, float64
     ``scores`` and a bool ``is_int`` (JSON ints: CN counts and the reference's int 0s), in
     the dict's order. Loads in milliseconds where json.loads of million-pair files takes
-    seconds; ``load_scores`` reads it back as the same dict."""
+    seconds; ``load_scores`` reads it back as the same dict. The sidecar records the size
+    and mtime of the JSON it describes (``json_stat``): ``load_scores`` ignores it once the
+    JSON has been rewritten by anything else (e.g. the reference's own scripts)."""
+    import os
+
     import numpy as np
 
     us, bs, vals, ints = [], [], [], []
@@ -43,7 +52,18 @@ def write_sidecar(d, fname):
             vals.append(float(v))
             ints.append(isinstance(v, int) and not isinstance(v, bool))
     np.savez(fname + ".npz", users=np.array(us, np.int64), businesses=np.array(bs, np.int64),
-             scores=np.array(vals, np.float64), is_int=np.array(ints, bool))
+             scores=np.array(vals, np.float64), is_int=np.array(ints, bool), json_stat=_json_stat(fname))
+
+
+def _json_stat(fname):
+    import os
+
+    import numpy as np
+
+    if not os.path.exists(fname):
+        return np.array([-1, -1], np.int64)
+    st = os.stat(fname)
+    return np.array([st.st_size, st.st_mtime_ns], np.int64)
 
 
 def load_scores(fname):
@@ -56,6 +76,9 @@ def load_scores(fname):
     if not os.path.exists(side):
         return load_json(fname)
     z = np.load(side)
+    if os.path.exists(fname) and ("json_stat" not in z.files or
+                                  not np.array_equal(z["json_stat"], _json_stat(fname))):
+        return load_json(fname)  # stale: the JSON changed after the sidecar was written
     out = {}
     for u, b, v, i in zip(z["users"].tolist(), z["businesses"].tolist(), z["scores"].tolist(), z["is_int"].tolist()):
         out.setdefault(str(u), {})[str(b)] = int(v) if i else v

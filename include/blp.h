@@ -71,6 +71,25 @@ int blp_csr_from_edges(int64_t n_nodes, int64_t n_edges, const int32_t* a, const
 int blp_csr_from_edges_device(int device, const int32_t* d_a, const int32_t* d_b, int64_t m, int64_t n_nodes,
                               int64_t* row_ptr, int32_t* col_idx, uint8_t* self_loop, int64_t* nnz_out);
 
+/* Device-resident CSR (multi-GPU ingest without a host round trip).
+ * blp_csr_build_device: the same CSR as blp_csr_from_edges_device, kept in HBM in the layout
+ *   blp_graph uses (row offsets int64, column ids int32, self-loop flags). It first waits for
+ *   all work queued on `device` (the endpoints may come from the RCCL all-gather's stream).
+ * blp_csr_info / blp_csr_fetch: sizes, and device-to-host copies (any pointer may be NULL).
+ * blp_graph_create_from_csr: a graph handle over that device CSR (no upload). row_ptr /
+ *   col_idx are the host mirror of the same CSR (from blp_csr_fetch); unlike
+ *   blp_graph_create, the handle BORROWS them: the caller keeps them alive and unchanged
+ *   until blp_graph_destroy. On success the csr is consumed (do not destroy it); on failure
+ *   it is left intact. aaw as for blp_graph_create.                                       */
+typedef struct blp_csr blp_csr;
+int blp_csr_build_device(int device, const int32_t* d_a, const int32_t* d_b, int64_t m, int64_t n_nodes,
+                         blp_csr** out);
+int blp_csr_info(const blp_csr* c, int64_t* n_nodes, int64_t* nnz);
+int blp_csr_fetch(const blp_csr* c, int64_t* row_ptr, int32_t* col_idx, uint8_t* self_loop);
+int blp_csr_destroy(blp_csr* c);
+int blp_graph_create_from_csr(blp_csr* c, const int64_t* row_ptr, const int32_t* col_idx, const double* aaw,
+                              blp_graph** out);
+
 /* blp_edges_parse: SNAP LoadEdgeList's text format (similarity.py:16): one edge per line,
  * whitespace-separated integer columns c0 and c1, lines starting with '#' skipped, lines
  * with too few columns skipped. Two calls: with a == b == NULL it only counts (*m_out);
@@ -87,6 +106,10 @@ int blp_graph_create(const int64_t* row_ptr, const int32_t* col_idx, int64_t n_n
 int blp_graph_destroy(blp_graph* g);
 int blp_graph_info(const blp_graph* g, int64_t* n_nodes, int64_t* nnz, int* device);
 int blp_graph_sync(blp_graph* g); /* wait for all work queued on the handle's stream */
+/* Fixed-point scale of the Adamic-Adar sums: terms are llrint(w * 2^shift), summed exactly
+ * in 64-bit integers. shift = 40 unless the graph's bound (max row length x max weight)
+ * could overflow a 64-bit sum, in which case blp_graph_create lowers it (overflow guard). */
+int blp_graph_aa_shift(const blp_graph* g, int* shift);
 
 /* ---------------------------------------------------------------- pair scoring
  * Replaces the hot loops of similarity.users (similarity.py:20-61) and similarity.business
@@ -194,9 +217,17 @@ int blp_svd_score_pairs_device(blp_svd* h, const int32_t* d_rows, const int32_t*
 int blp_svd_topk(blp_svd* h, const int32_t* users, int64_t n_users, const int64_t* ex_off,
                  const int32_t* ex_col, int topk, int32_t* out_cols, double* out_scores);
 /* blp_svd_topk on device pointers (users, exclusion CSR or NULLs, outputs), enqueued on the
- * handle's stream without a sync (blp_svd_sync waits); rows are not range-checked here. */
+ * handle's stream without a sync (blp_svd_sync waits). Rows are not range-checked on the host;
+ * the kernel treats a row outside [0, n_rows) as an all-zero row (no out-of-bounds read).
+ * Ordering contract: the handle's stream is its own (non-blocking). A caller whose inputs
+ * are produced on another stream, or who reads / frees the outputs on another stream, joins
+ * the streams with blp_svd_stream_join: handle_waits = 1 makes the handle's stream wait for
+ * the work queued so far on `stream` (call before blp_svd_topk_device); 0 makes `stream`
+ * wait for the handle's work queued so far (call after). `stream` is a hipStream_t passed
+ * as void* (NULL = the device's null stream). */
 int blp_svd_topk_device(blp_svd* h, const int32_t* d_users, int64_t n_users, const int64_t* d_ex_off,
                         const int32_t* d_ex_col, int topk, int32_t* d_out_cols, double* d_out_scores);
+int blp_svd_stream_join(blp_svd* h, void* stream, int handle_waits);
 int blp_svd_stats(blp_svd* h, int which, double* total_ms, int64_t* launches); /* 0 pairs, 1 top-k */
 int blp_svd_sync(blp_svd* h);
 

@@ -148,6 +148,38 @@ def svd_pair_scores(us, vt, rows, cols):
 
 
 # --------------------------------------------------------------------------- random_walks.py
+def svd_entry_parity(got, ref, structural_zero, rtol=1e-5, floor_frac=1e-6, zero_atol_frac=1e-12):
+    """Per-entry comparison of two rank-k reconstructions (SURVEY.md §7 hard part 3; the
+    north star's 1e-5 relative bar on svd.py:28-30 scores).
+
+    * structural zeros -- pairs whose user row or business column of M is empty, so
+      us[row] . vt[:, col] is 0 in exact arithmetic: `got` must be exactly 0.0 and `ref`
+      within zero_atol_frac * scale (ARPACK's vectors of an empty row are 0 up to rounding);
+    * every other entry: |got - ref| <= rtol * max(|ref|, floor), floor = floor_frac * scale
+      (scale = max |ref|). The floor is the near-zero rule: an entry that cancels to below
+      one millionth of the score scale carries no relative digits in either factorisation.
+    Returns a dict with the verdict, the worst entry and the band counts."""
+    got = np.asarray(got, np.float64)
+    ref = np.asarray(ref, np.float64)
+    z = np.asarray(structural_zero, bool)
+    scale = float(np.max(np.abs(ref))) if len(ref) else 0.0
+    floor = floor_frac * scale
+    zero_ok = bool(np.all(got[z] == 0.0) and np.all(np.abs(ref[z]) <= zero_atol_frac * scale))
+    nz = ~z
+    den = np.maximum(np.abs(ref[nz]), floor) if nz.any() else np.zeros(0)
+    err = np.abs(got[nz] - ref[nz]) / np.where(den > 0, den, 1.0)
+    worst = int(np.argmax(err)) if len(err) else -1
+    idx = np.flatnonzero(nz)
+    return {
+        "entries": int(len(ref)), "structural_zeros": int(z.sum()), "structural_zeros_exact": zero_ok,
+        "near_zero_band": int(np.sum(np.abs(ref[nz]) < floor)), "rtol": rtol, "floor": floor,
+        "worst_rel_err": float(err[worst]) if worst >= 0 else 0.0,
+        "worst_entry": {"index": int(idx[worst]), "got": float(got[idx[worst]]), "ref": float(ref[idx[worst]])}
+        if worst >= 0 else None,
+        "ok": bool(zero_ok and (len(err) == 0 or err[worst] <= rtol)),
+    }
+
+
 def random_walk_scores(edges, examples, iterations=10, jump_p=0.2):
     """random_walks.py:9-53 restated densely (small graphs only).
 

@@ -39,6 +39,31 @@ def test_reconstruction_matches_arpack(gpu, k):
     assert np.allclose(gvt @ gvt.T, np.eye(k), atol=1e-10)
 
 
+@pytest.mark.parametrize("k", [16, 64])
+def test_per_entry_parity_vs_arpack(gpu, k):
+    """Every reconstructed entry of the GPU factorisation (the svd.py default) against the
+    reference's ARPACK factorisation at 1e-5 relative per entry, with the exact-zero rule
+    for empty rows / columns and the near-zero floor (blp_oracle.svd_entry_parity)."""
+    import blp_oracle as O
+
+    M, rng = _matrix(5, 6000, 700, 60000)
+    # users and businesses with no reviews: their scores are exactly 0 (structural zeros)
+    M = sp.vstack([M, sp.csr_matrix((40, M.shape[1]))]).tocsr()
+    M = sp.hstack([M, sp.csr_matrix((M.shape[0], 9))]).tocsr()
+    u, s, vt = spla.svds(M, k=k)
+    ref_us = u * s
+    gus, gs, gv = factor.svds(M, k=k, device=gpu, return_us=True)
+    rows = np.r_[rng.integers(0, M.shape[0], 30000), np.arange(M.shape[0] - 40, M.shape[0])]
+    cols = np.r_[rng.integers(0, M.shape[1], 30000), rng.integers(0, M.shape[1], 40)]
+    cols[:50] = M.shape[1] - 1 - np.arange(50) % 9  # some empty columns
+    ref = np.einsum("ij,ji->i", ref_us[rows], vt[:, cols])
+    got = np.einsum("ij,ij->i", gus[rows], gv[cols])
+    zero = (np.diff(M.indptr)[rows] == 0) | (np.diff(M.tocsc().indptr)[cols] == 0)
+    r = O.svd_entry_parity(got, ref, zero)
+    assert r["structural_zeros"] >= 80
+    assert r["ok"], r
+
+
 def test_return_us_layout_and_determinism(gpu):
     M, _ = _matrix(2, 5000, 600, 50000)
     us1, s1, v1 = factor.svds(M, k=32, device=gpu, return_us=True)

@@ -1,0 +1,208 @@
+"""GPU parity of the config-5 ingest path: device-resident endpoints ->
+blp_csr_build_device -> blp_graph_create_from_csr (DeviceGraph.from_device_edges), against
+the host CSR builder (blp_csr_from_edges, SNAP LoadEdgeList semantics, similarity.py:16)
+and the C oracle; then the sharded-universe scorers on the resulting graph. Marked `gpu`.
+
+The exchange itself (blp.dist.allgather_edges) runs here at world 1 on the device, and at
+world 2 with two processes sharing the one GPU (gloo carries the exchange; the RCCL leg
+needs two GPUs and runs in the driver's multi-GPU bench)."""
+import ctypes
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import blp
+import coracle
+from blp import dist as bd
+from helpers import bipartite_edges, dense_edges
+
+pytestmark = pytest.mark.gpu
+
+
+def _host_csr(n, a, b):
+    A = np.ascontiguousarray(a, np.int32)
+    B = np.ascontiguousarray(b, np.int32)
+    rp = np.zeros(n + 1, np.int64)
+    ci = np.empty(max(2 * len(A), 1), np.int32)
+    sl = np.zeros(max(n, 1), np.uint8)
+    nnz = ctypes.c_int64(0)
+    P = blp._lib.ptr
+    blp._lib.check(blp.lib().blp_csr_from_edges(n, len(A), P(A), P(B), P(rp), P(ci), P(sl), ctypes.byref(nnz)))
+    return rp, ci[: nnz.value], sl[:n]
+
+
+def _on_device(*arrs):
+    import torch
+
+    out = [torch.from_numpy(np.ascontiguousarray(x, np.int32)).cuda() for x in arrs]
+    return out
+
+
+def _messy_edges(rng, n_users, n_bus, draws):
+    """Review edges plus duplicates, reversed duplicates and self-loops (dense ids)."""
+    u, b = bipartite_edges(rng, n_users, n_bus, draws)
+    k = draws // 10
+    i = rng.integers(0, draws, k)
+    loops = rng.integers(0, n_users + n_bus, 25)
+    a = np.concatenate([u, u[i], b[i[: k // 2]], loops])
+    c = np.concatenate([b, b[i], u[i[: k // 2]], loops])
+    perm = rng.permutation(len(a))
+    return a[perm], c[perm]
+
+
+@pytest.mark.parametrize("seed,n_users,n_bus,draws", [(0, 3000, 200, 20000), (1, 200000, 6000, 900000)])
+def test_device_csr_equals_host_csr(gpu, seed, n_users, n_bus, draws):
+    rng = np.random.default_rng(seed)
+    a, c = _messy_edges(rng, n_users, n_bus, draws)
+    n = n_users + n_bus
+    rp, ci, sl = _host_csr(n, a, c)
+    da, dc = _on_device(a, c)
+    G = blp.DeviceGraph.from_device_edges(da.data_ptr(), dc.data_ptr(), len(a), n, n_users, device=gpu)
+    assert np.array_equal(G.row_ptr, rp) and np.array_equal(G.col_idx, ci) and np.array_equal(G.self_loop, sl)
+    assert sl.sum() > 0 and G.nnz == len(ci)
+    assert set(G.build_times) == {"device_csr_s", "fetch_s", "host_half_s", "graph_create_s"}
+    # the older entry point (host outputs) is the same builder
+    rp2 = np.zeros(n + 1, np.int64)
+    ci2 = np.empty(2 * len(a), np.int32)
+    sl2 = np.zeros(n, np.uint8)
+    nnz = ctypes.c_int64(0)
+    P = blp._lib.ptr
+    blp._lib.check(blp.lib().blp_csr_from_edges_device(gpu, ctypes.c_void_p(da.data_ptr()), ctypes.c_void_p(
+        dc.data_ptr()), len(a), n, P(rp2), P(ci2), P(sl2), ctypes.byref(nnz)))
+    assert np.array_equal(rp2, rp) and np.array_equal(ci2[: nnz.value], ci) and np.array_equal(sl2, sl)
+
+
+def test_device_csr_rejects_out_of_range_ids(gpu):
+    a = np.array([0, 1, 5], np.int32)
+    c = np.array([3, 2, 9], np.int32)  # 9 >= n
+    da, dc = _on_device(a, c)
+    with pytest.raises(blp.BLPError) as e:
+        blp.DeviceGraph.from_device_edges(da.data_ptr(), dc.data_ptr(), 3, 8, 4, device=gpu)
+    assert e.value.code == -1  # BLP_E_ARG
+    a[2] = -1
+    c[2] = 3
+    da, dc = _on_device(a, c)
+    with pytest.raises(blp.BLPError) as e:
+        blp.DeviceGraph.from_device_edges(da.data_ptr(), dc.data_ptr(), 3, 8, 4, device=gpu)
+    assert e.value.code == -1
+
+
+def test_device_csr_empty_and_loops_only(gpu):
+    da, dc = _on_device(np.array([2, 2], np.int32), np.array([2, 2], np.int32))
+    G = blp.DeviceGraph.from_device_edges(da.data_ptr(), dc.data_ptr(), 2, 5, 3, device=gpu)
+    assert G.nnz == 0 and G.row_ptr.tolist() == [0] * 6 and G.self_loop.tolist() == [0, 0, 1, 0, 0]
+    assert G.degree.tolist() == [0, 0, 1, 0, 0]
+
+
+@pytest.mark.parametrize("knobs", [{}, {"BLP_SPLIT": "3"}, {"BLP_FORCE_GLOBAL": "1"}])
+def test_device_graph_scores_match_oracle(gpu, knobs, monkeypatch):
+    """Scores on the adopted device CSR: the default plan, the chunk-parallel scorer (the
+    config-5 user side) and the HBM-bitmap scorer, vs the C oracle and vs a host-built graph."""
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    rng = np.random.default_rng(5)
+    n_users, n_bus = 40000, 1200
+    a, c = _messy_edges(rng, n_users, n_bus, 300000)
+    n = n_users + n_bus
+    da, dc = _on_device(a, c)
+    G = blp.DeviceGraph.from_device_edges(da.data_ptr(), dc.data_ptr(), len(a), n, n_users, device=gpu)
+    users = rng.choice(np.flatnonzero(G.hop1_size[:n_users] > 0), 120, replace=False)
+    x = np.repeat(users, 25).astype(np.int32)
+    y = rng.integers(n_users, n, len(x)).astype(np.int32)
+    y = y[G.hop1_size[y] > 0]
+    x = x[: len(y)]
+    ids, oa, ob = dense_edges(a, c)
+    og = coracle.OracleGraph(len(ids), oa, ob)
+    for xs, ys, mask in ((x, y, 7), (y, x, 3)):
+        got = G.score_pairs(xs, ys, mask)
+        cn, jac, aa, _ = og.score_pairs(np.searchsorted(ids, xs), np.searchsorted(ids, ys), mask, nthreads=8)
+        np.testing.assert_array_equal(got["cn"], cn)
+        np.testing.assert_array_equal(got["jaccard"], jac)
+        if mask & blp.ADAMIC:
+            np.testing.assert_allclose(got["adamic"], aa, rtol=1e-9, atol=0)
+    if "BLP_SPLIT" in knobs:
+        assert G.batch(x, y).plan()["chunks"] == -3
+    if "BLP_FORCE_GLOBAL" in knobs:
+        assert G.batch(x, y).plan()["chunks"] == 0
+    # the same graph built from host arrays scores identically (Adamic-Adar included)
+    H = blp.DeviceGraph.from_csr(G.row_ptr.copy(), G.col_idx.copy(), G.self_loop.copy(), n_users, device=gpu)
+    for k, v in G.score_pairs(x, y, 7).items():
+        np.testing.assert_array_equal(v, H.score_pairs(x, y, 7)[k])
+
+
+def test_allgather_world1_on_device(gpu, monkeypatch):
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        monkeypatch.delenv(k, raising=False)
+    U, B, D = 5000, 300, 40000
+    d = bd.Dist(exchange=True)
+    u, b = bd.block_review_edges(U, B, D, 0, U, seed=3)
+    a_all, b_all, counts = bd.allgather_edges(d, u, b)
+    assert a_all.is_cuda and counts == [len(u)]
+    G = blp.DeviceGraph.from_device_edges(a_all.data_ptr(), b_all.data_ptr(), len(a_all), U + B, U, device=gpu)
+    rp, ci, _ = _host_csr(U + B, u, b)
+    assert np.array_equal(G.row_ptr, rp) and np.array_equal(G.col_idx, ci)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+U2, B2, D2 = 30000, 800, 200000
+
+
+def _rank(rank, world, port, outdir):
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(rank),
+                       "WORLD_SIZE": str(world), "LOCAL_RANK": "0", "BLP_EXCHANGE_BACKEND": "gloo"})
+    d = bd.Dist(exchange=True)
+    blocks = bd.user_blocks(U2, world)
+    u, b = bd.block_review_edges(U2, B2, D2, blocks[rank], blocks[rank + 1], seed=9)
+    a_all, b_all, counts = bd.allgather_edges(d, u, b)
+    a_dev, b_dev = a_all.to("cuda:0"), b_all.to("cuda:0")
+    G = blp.DeviceGraph.from_device_edges(a_dev.data_ptr(), b_dev.data_ptr(), len(a_dev), U2 + B2, U2, device=0)
+    mine = np.arange(blocks[rank], blocks[rank + 1])
+    src = np.random.default_rng(rank).choice(mine[G.hop1_size[mine] > 0], 40, replace=False)
+    x = np.repeat(src, 20).astype(np.int32)
+    y = np.random.default_rng(rank + 10).integers(U2, U2 + B2, len(x)).astype(np.int32)
+    r = G.score_pairs(x, y, 7)
+    np.savez(os.path.join(outdir, "r%d.npz" % rank), rp=G.row_ptr, ci=G.col_idx, u=u, b=b, x=x, y=y, **r)
+    G.close()
+    d.barrier()
+    d.close()
+
+
+def test_two_ranks_share_the_gpu(gpu, tmp_path):
+    """World 2 on one GPU: each rank generates its user block, the exchange gives both the
+    union, each builds the device graph and scores its own users: CSRs equal the union's host
+    CSR on both ranks, scores equal the oracle."""
+    import torch.multiprocessing as mp
+
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=_rank, args=(r, 2, port, str(tmp_path))) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(110)
+    codes = [p.exitcode for p in procs]
+    for p in procs:
+        if p.exitcode is None:
+            p.kill()
+    assert codes == [0, 0], codes
+    res = [np.load(os.path.join(tmp_path, "r%d.npz" % r)) for r in range(2)]
+    u = np.concatenate([r["u"] for r in res])
+    b = np.concatenate([r["b"] for r in res])
+    rp, ci, _ = _host_csr(U2 + B2, u, b)
+    ids, oa, ob = dense_edges(u, b)
+    og = coracle.OracleGraph(len(ids), oa, ob)
+    for r in res:
+        assert np.array_equal(r["rp"], rp) and np.array_equal(r["ci"], ci)
+        cn, jac, aa, _ = og.score_pairs(np.searchsorted(ids, r["x"]), np.searchsorted(ids, r["y"]), 7)
+        np.testing.assert_array_equal(r["cn"], cn)
+        np.testing.assert_array_equal(r["jaccard"], jac)
+        np.testing.assert_allclose(r["adamic"], aa, rtol=1e-9, atol=0)

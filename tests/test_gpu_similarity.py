@@ -256,3 +256,33 @@ def test_coscheduled_passes_match_single_passes(gpu, variant, monkeypatch):
     for k in ("cn", "jaccard"):
         np.testing.assert_array_equal(got_b[k], alone_b[k])
     _check_against_oracle(a, b, x, y)
+
+
+@pytest.mark.parametrize("request_shift", [62, 50])
+def test_adamic_fixed_point_overflow_guard(gpu, request_shift, monkeypatch):
+    """The Adamic-Adar sums are 64-bit fixed point. Asking for a scale that would wrap them on
+    this graph (BLP_AA_SHIFT, a test knob; the default is 2^40) must make blp_graph_create lower
+    the scale until max_row_len x max_weight fits: results then still match the oracle, for
+    both sides and the top-k engine. Without the guard, 2^62 wraps on the first hub."""
+    monkeypatch.setenv("BLP_AA_SHIFT", str(request_shift))
+    rng = np.random.default_rng(31)
+    a, b = bipartite_edges(rng, 30000, 800, 240000)
+    G = blp.DeviceGraph(a, b)
+    dmax = int(G.hop1_size.max())
+    wmax = float(G.aa_weight.max())
+    s = G.aa_shift
+    assert s <= request_shift
+    assert dmax * (wmax * 2.0**s + 0.5) < 2.0**63                 # the bound holds
+    if dmax * (wmax * 2.0**request_shift) >= 2.0**63:
+        assert s < request_shift                                   # and the guard engaged
+    nu = G.n - len(np.unique(b))
+    x = np.repeat(rng.choice(nu, 150, replace=False), 30).astype(np.int32)
+    y = rng.integers(nu, G.n, len(x)).astype(np.int32)
+    _check_against_oracle(a, b, x, y)
+    _check_against_oracle(a, b, y, x)
+
+
+def test_adamic_default_scale_is_2_pow_40(gpu):
+    rng = np.random.default_rng(2)
+    a, b = bipartite_edges(rng, 2000, 300, 20000)
+    assert blp.DeviceGraph(a, b).aa_shift == 40

@@ -243,3 +243,32 @@ def test_topk_oracle_composes_reference_scorers(split):
         ranked = O.topk_full_candidates(adj, int(u), 10**9, "jaccard")[0]
         assert ranked == sorted(ranked, key=lambda t: (-t[1], t[0]))
     assert checked > 20
+
+
+def test_svd_entry_parity_rule():
+    """The per-entry SVD comparator: two ARPACK runs from different starts pass; a perturbed
+    entry, a non-zero structural zero and a wrong near-zero entry fail."""
+    import scipy.sparse as sp
+    import scipy.sparse.linalg as spla
+
+    rng = np.random.default_rng(0)
+    M = sp.random(400, 300, density=0.03, random_state=1, format="csr")
+    M.data[:] = 1.0
+    M = sp.vstack([M, sp.csr_matrix((5, 300))]).tocsr()
+    u1, s1, vt1 = spla.svds(M, k=10, v0=rng.standard_normal(min(M.shape)))
+    u2, s2, vt2 = spla.svds(M, k=10, v0=rng.standard_normal(min(M.shape)))
+    rows = np.r_[rng.integers(0, 400, 3000), np.arange(400, 405)]
+    cols = rng.integers(0, 300, len(rows))
+    a = np.einsum("ij,ji->i", (u1 * s1)[rows], vt1[:, cols])
+    b = np.einsum("ij,ji->i", (u2 * s2)[rows], vt2[:, cols])
+    zero = np.diff(M.indptr)[rows] == 0
+    a[zero] = 0.0
+    assert O.svd_entry_parity(a, b, zero)["ok"]
+    bad = a.copy()
+    i = int(np.argmax(np.abs(b)))
+    bad[i] *= 1 + 1e-4
+    r = O.svd_entry_parity(bad, b, zero)
+    assert not r["ok"] and r["worst_entry"]["index"] == i
+    bad = a.copy()
+    bad[np.flatnonzero(zero)[0]] = 1e-300
+    assert not O.svd_entry_parity(bad, b, zero)["ok"]
