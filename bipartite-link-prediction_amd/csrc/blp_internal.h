@@ -42,13 +42,43 @@ struct DevBuf {
   template <class T> T* as() const { return reinterpret_cast<T*>(p); }
 };
 
-// Adamic-Adar terms are summed in 2^-s fixed point: exact, order-independent integer sums
-// (the reference's own order is Python set order); |term| <= 1/ln 2 < 2^1. s = AA_SHIFT (40)
-// unless the graph could overflow a signed 64-bit sum at that scale: blp_graph_create bounds
-// every pair's sum by max_row_len * (max_weight * 2^s + 1/2) and lowers s until the bound is
-// below 2^63 (blp_graph::aa_shift). CN <= |N(y)| <= max_row_len < 2^31 and weight < 2^0.53
-// keep s >= 31 on any graph an int32 CSR can hold.
-constexpr int AA_SHIFT = 40;
+// Adamic-Adar sums are EXACT. A term w = (log deg)^-1 (similarity.py:121-125) is a double in
+// [2^-5, 2) for any degree an int32 CSR can hold, so W = w * 2^58 is an integer below 2^59 with
+// no rounding at all. A pair's sum S = Σ W over its CN common neighbours is carried in two u64
+// words that any order of addition leaves identical:
+//   lo = Σ W mod 2^64 (wrapping adds)      hi = Σ (W >> 32) (exact: < CN * 2^27 < 2^58)
+// S - hi * 2^32 = Σ (W mod 2^32) < CN * 2^32 < 2^63, so S = hi * 2^32 + (lo - hi * 2^32 mod 2^64)
+// exactly (aa_exact below), and the score is S * 2^-58 rounded once to the nearest double:
+// the correctly rounded sum of the reference's own terms, which is what math.fsum returns. The
+// reference adds the same terms in Python set order (one rounding per add), so it agrees to a
+// few ulps; the oracle's fsum agrees bit for bit, and so do the AUCs computed from them.
+constexpr int AA_SHIFT = 58;
+constexpr double AA_WMAX = 64.0;  // custom weight tables: [0, 64) keeps W < 2^64 and the bounds above
+
+// S = hi * 2^32 + r as a 128-bit integer (hi64:lo64), from the two accumulator words.
+__host__ __device__ inline void aa_exact(unsigned long long lo, unsigned long long hi, unsigned long long* s_hi,
+                                         unsigned long long* s_lo) {
+  const unsigned long long a = hi << 32;  // hi * 2^32 mod 2^64; the 128-bit low word of S is lo itself
+  *s_lo = lo;
+  *s_hi = (hi >> 32) + (lo < a ? 1ull : 0ull);
+}
+
+// Correctly rounded (nearest-even) conversion of the 128-bit integer hi64:lo64 to double.
+__host__ __device__ inline double u128_to_double(unsigned long long h, unsigned long long l) {
+  if (h == 0) return (double)l;  // u64 -> f64 rounds once
+  const int lz = __builtin_clzll(h);
+  unsigned long long m = lz ? (h << lz) | (l >> (64 - lz)) : h;  // top 64 significant bits
+  const unsigned long long rest = lz ? l << lz : l;                // bits below them
+  m |= rest != 0 ? 1ull : 0ull;  // sticky: bit 0 lies far below the rounding position (bit 10)
+  return __builtin_ldexp((double)m, 64 - lz);
+}
+
+// Adamic-Adar score of one accumulator pair: S * 2^-58, correctly rounded.
+__host__ __device__ inline double aa_value(unsigned long long lo, unsigned long long hi) {
+  unsigned long long sh, sl;
+  aa_exact(lo, hi, &sh, &sl);
+  return __builtin_ldexp(u128_to_double(sh, sl), -AA_SHIFT);
+}
 
 enum KernelId { K_SCORE = 0, K_GROUP = 1, K_SVD_PAIRS = 2, K_SVD_TOPK = 3, K_WALK = 4, K_HOP3 = 5, K_COUNT = 6 };
 
@@ -74,8 +104,7 @@ struct blp_graph {
   int64_t nnz = 0;  // stored CSR entries (both directions, no self-loops)
   int64_t* d_rp = nullptr;   // [n+1]
   int32_t* d_ci = nullptr;   // [nnz], CI_PAD readable ids on each side
-  long long* d_aaw_fx = nullptr;  // [n] Adamic-Adar weight per node, fixed point 2^-aa_shift (or null)
-  int aa_shift = blp::AA_SHIFT;   // fixed-point scale of d_aaw_fx (overflow guard, blp_internal.h)
+  long long* d_aaw_fx = nullptr;  // [n] Adamic-Adar weight per node, W = w * 2^58 (exact; or null)
   // weight-coded copy of d_ci for the scorers: ci | code(ci) << id_bits, code 1..255 naming
   // one of the graph's most used weights (d_wtab[code]), 0 = look up d_aaw_fx (or null)
   int32_t* d_ci_w = nullptr;

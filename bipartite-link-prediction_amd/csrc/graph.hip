@@ -180,22 +180,19 @@ int build_weight_codes(blp_graph* g, const int64_t* row_ptr, const std::vector<l
   return BLP_OK;
 }
 
-// Overflow guard of the fixed-point Adamic-Adar sums (blp_internal.h): the largest shift
-// s <= AA_SHIFT (or BLP_AA_SHIFT, a test knob that may ask for more) such that no pair's sum
-// can reach 2^63: a pair's common neighbours are members of one row N(y), so the sum is at
-// most max_row_len terms of at most llrint(max_weight * 2^s) <= max_weight * 2^s + 1/2.
-int aa_fixed_shift(const int64_t* row_ptr, const double* aaw, int64_t n) {
-  int64_t dmax = 0;
-  double wmax = 0.0;
+// Adamic-Adar weights as integers W = w * 2^58 (blp_internal.h). Every weight the reference
+// produces, (log d)^-1 for 2 <= d < 2^31, lies in [2^-5, 2) and converts exactly; a custom table
+// must hold weights in [0, 64) (smaller weights than 2^-6 round to the 2^-58 grid once, here).
+int aa_weights_fixed(const double* aaw, int64_t n, std::vector<long long>& fx) {
+  const double scale = std::ldexp(1.0, AA_SHIFT);
+  fx.resize((size_t)n);
   for (int64_t i = 0; i < n; ++i) {
-    dmax = std::max<int64_t>(dmax, row_ptr[i + 1] - row_ptr[i]);
-    wmax = std::max(wmax, std::fabs(aaw[i]));
+    const double w = aaw[i];
+    if (!(w >= 0.0 && w < AA_WMAX))
+      return fail(BLP_E_ARG, "blp_graph_create: aa_weight entries must lie in [0, 64) (node " + std::to_string(i) + ")");
+    fx[i] = (long long)(unsigned long long)std::nearbyint(w * scale);
   }
-  int s = AA_SHIFT;
-  if (const char* e = getenv("BLP_AA_SHIFT")) s = std::max(0, std::min(62, atoi(e)));
-  const double lim = std::ldexp(1.0, 63) * (1.0 - 1e-12);
-  while (s > 0 && (double)dmax * (wmax * std::ldexp(1.0, s) + 0.5) >= lim) --s;
-  return s;
+  return BLP_OK;
 }
 
 // Everything a graph handle derives from its CSR once g->d_rp / g->d_ci (device) and
@@ -207,10 +204,8 @@ int graph_finish(blp_graph* g, const double* aaw) {
   if (!g->stream) BLP_HIP(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
   const int64_t n = g->n;
   if (aaw) {
-    g->aa_shift = aa_fixed_shift(g->hrp, aaw, n);
-    const double scale = std::ldexp(1.0, g->aa_shift);
-    std::vector<long long> fx((size_t)n);
-    for (int64_t i = 0; i < n; ++i) fx[i] = llrint(aaw[i] * scale);
+    std::vector<long long> fx;
+    if (int rc = aa_weights_fixed(aaw, n, fx)) return rc;
     BLP_HIP(hipMalloc(&g->d_aaw_fx, sizeof(long long) * std::max<int64_t>(n, 1)));
     if (n) BLP_HIP(hipMemcpy(g->d_aaw_fx, fx.data(), sizeof(long long) * n, hipMemcpyHostToDevice));
     int rc = build_weight_codes(g, g->hrp, fx);
@@ -348,7 +343,7 @@ int blp_graph_destroy(blp_graph* g) {
 
 int blp_graph_aa_shift(const blp_graph* g, int* shift) {
   BLP_CHECK(g && shift, BLP_E_ARG, "blp_graph_aa_shift: bad arguments");
-  *shift = g->aa_shift;
+  *shift = AA_SHIFT;  // fixed: W = w * 2^58 (exact sums, blp_internal.h)
   return BLP_OK;
 }
 

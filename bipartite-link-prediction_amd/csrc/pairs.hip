@@ -21,7 +21,7 @@
 //              segment loops: the rows of a chunk are concatenated, every thread takes K
 //              consecutive elements (K independent loads in flight), one LDS binary search per
 //              K elements maps an element to its row. Short and very long rows cost the same.
-// Adamic-Adar terms are summed in 2^-40 fixed point (exact integer adds in any order).
+// Adamic-Adar sums are exact (two-word integer sums of w * 2^58, any order; blp_internal.h).
 #include <algorithm>
 #include <cmath>
 #include <numeric>
@@ -502,6 +502,18 @@ __device__ inline void mp_fetch(const int32_t* __restrict__ ci, const int64_t* s
 // idmask | sign bit, so -1 maps to >= 2^31 - c0 > width (c0 <= idmask, width < 2^31).
 __device__ inline uint32_t in_chunk(int v, uint32_t keep, uint32_t c0u) { return ((uint32_t)v & keep) - c0u; }
 
+// Exact Adamic-Adar accumulation (blp_internal.h): a term W adds to the wrapping low word and
+// its high half to the exact high word. LDS accumulators are interleaved: s_aa[2 t] = lo,
+// s_aa[2 t + 1] = hi for segment t.
+__device__ inline void aa_term(unsigned long long& lo, unsigned long long& hi, unsigned long long w) {
+  lo += w;
+  hi += w >> 32;
+}
+__device__ inline void aa_push(unsigned long long* s_aa, int t, unsigned long long lo, unsigned long long hi) {
+  atomicAdd(&s_aa[2 * t], lo);
+  atomicAdd(&s_aa[2 * t + 1], hi);
+}
+
 template <int NT, int K, bool GLOBAL = false>
 __device__ inline void mp_build(const int32_t* __restrict__ ci, uint32_t idmask, const int64_t* s_start,
                                 const int32_t* s_off, int ns, int64_t c0, int64_t width, uint32_t* bm, int tid,
@@ -581,39 +593,40 @@ __device__ inline void mp_scan(const int32_t* __restrict__ ci, uint32_t idmask, 
     mp_fetch<K>(ci, s_start, s_off, ns, T, base + STEP + tid * K, wn, skn, hint, shift);
     if (sk[0] == sk[K - 1]) {  // the K elements in one segment (or none valid): one run
       unsigned c = 0;
-      unsigned long long acc = 0;
+      unsigned long long acc = 0, acch = 0;
 #pragma unroll
       for (int k = 0; k < K; ++k) {
         c += hit[k] ? 1u : 0u;
-        if (AA) acc += (unsigned long long)wt[k];
+        if (AA) aa_term(acc, acch, (unsigned long long)wt[k]);
       }
       if (c) {
         atomicAdd(&s_cn[sk[0]], c);
-        if (AA) atomicAdd(&s_aa[sk[0]], acc);
+        if (AA) aa_push(s_aa, sk[0], acc, acch);
       }
     } else {
       int cur = sk[0];
       unsigned c = 0;
-      unsigned long long acc = 0;
+      unsigned long long acc = 0, acch = 0;
 #pragma unroll
       for (int k = 0; k < K; ++k) {
         if (sk[k] != cur) {
           if (c) {
             atomicAdd(&s_cn[cur], c);
-            if (AA) atomicAdd(&s_aa[cur], acc);
+            if (AA) aa_push(s_aa, cur, acc, acch);
           }
           cur = sk[k];
           c = 0;
           acc = 0;
+          acch = 0;
         }
         if (hit[k]) {
           ++c;
-          if (AA) acc += (unsigned long long)wt[k];
+          if (AA) aa_term(acc, acch, (unsigned long long)wt[k]);
         }
       }
       if (c && cur >= 0) {
         atomicAdd(&s_cn[cur], c);
-        if (AA) atomicAdd(&s_aa[cur], acc);
+        if (AA) aa_push(s_aa, cur, acc, acch);
       }
     }
 #pragma unroll
@@ -770,7 +783,8 @@ __device__ inline void pp_scan(const int32_t* __restrict__ ci, uint32_t idmask, 
       atomicAdd(&s_cn[seg], 1u);
       if (AA) {
         const uint32_t code = ((uint32_t)v >> idbits) & 255u;
-        atomicAdd(&s_aa[seg], (unsigned long long)(code ? wtab[code] : aaw[v & idmask]));
+        const unsigned long long w = (unsigned long long)(code ? wtab[code] : aaw[v & idmask]);
+        aa_push(s_aa, seg, w, w >> 32);
       }
     }
   };
@@ -799,26 +813,26 @@ __device__ inline void pp_scan(const int32_t* __restrict__ ci, uint32_t idmask, 
       }
     }
     unsigned c1 = 0, c2 = 0;
-    unsigned long long x1 = 0, x2 = 0;
+    unsigned long long x1 = 0, x2 = 0, h1 = 0, h2 = 0;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       const unsigned h = hit[k] ? 1u : 0u;
       const unsigned long long v = (AA && hit[k]) ? (unsigned long long)wt[k] : 0ull;
       if (k < st.rem1) {
         c1 += h;
-        x1 += v;
+        aa_term(x1, h1, v);
       } else {
         c2 += h;
-        x2 += v;
+        aa_term(x2, h2, v);
       }
     }
     if (c1) {
       atomicAdd(&s_cn[st.s1], c1);
-      if (AA) atomicAdd(&s_aa[st.s1], x1);
+      if (AA) aa_push(s_aa, st.s1, x1, h1);
     }
     if (c2) {
       atomicAdd(&s_cn[st.s2], c2);
-      if (AA) atomicAdd(&s_aa[st.s2], x2);
+      if (AA) aa_push(s_aa, st.s2, x2, h2);
     }
   };
   // no exit from the middle of the body: a path leaving with B in flight would merge into the
@@ -974,20 +988,20 @@ __device__ inline void rc_scan(const int32_t* __restrict__ ci, uint32_t idmask, 
     for (int k = 0; k < K; ++k) hm |= ((wd[k] >> (rr[k] & 31)) & 1u) << k;
     if (hm) {
       if (AA) {
-        unsigned long long acc = 0;
+        unsigned long long acc = 0, acch = 0;
         uint32_t esc = 0;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
           const bool h = (hm >> k) & 1u;
-          acc += h ? (unsigned long long)wt[k] : 0ull;
+          aa_term(acc, acch, h ? (unsigned long long)wt[k] : 0ull);
           esc |= (h & ((((uint32_t)st.v[k] >> idbits) & 255u) == 0u)) ? 1u << k : 0u;
         }
         if (esc) {  // code-0 ids: the per-node weight (rare on a coded id stream)
 #pragma unroll
           for (int k = 0; k < K; ++k)
-            if ((esc >> k) & 1u) acc += (unsigned long long)aaw[st.v[k] & idmask];
+            if ((esc >> k) & 1u) aa_term(acc, acch, (unsigned long long)aaw[st.v[k] & idmask]);
         }
-        atomicAdd(&s_aa[st.s], acc);
+        aa_push(s_aa, st.s, acc, acch);
       }
       atomicAdd(&s_cn[st.s], (unsigned)__popc(hm));
     }
@@ -1063,7 +1077,7 @@ __device__ inline void row_scan(const int32_t* __restrict__ ci, uint32_t idmask,
     const int64_t st = s_start[t];
     const int len = s_off[t + 1] - s_off[t];
     unsigned c = 0;
-    unsigned long long acc = 0;
+    unsigned long long acc = 0, acch = 0;
     for (int h = 0; h < len; h += SHORT_PART) {
       int e[SHORT_PART];
       row_part(ci, st, len, h, e);
@@ -1076,13 +1090,16 @@ __device__ inline void row_scan(const int32_t* __restrict__ ci, uint32_t idmask,
           c += hit ? 1u : 0u;
           if (AA && hit) {
             const uint32_t code = ((uint32_t)e[k] >> idbits) & 255u;
-            acc += (unsigned long long)(code ? wtab[code] : aaw[e[k] & idmask]);
+            aa_term(acc, acch, (unsigned long long)(code ? wtab[code] : aaw[e[k] & idmask]));
           }
         }
       }
     }
     s_cn[t] += c;
-    if (AA) s_aa[t] += acc;
+    if (AA) {
+      s_aa[2 * t] += acc;
+      s_aa[2 * t + 1] += acch;
+    }
   }
 }
 
@@ -1192,7 +1209,7 @@ struct ScoreArgs {
   int short_rows;    // bit 0: every build row <= SHORT_MAX ids, bit 1: every scan row (row_build / row_scan)
   const int64_t* wp;    // wedge rows (wedge.hip; short-row scorer only, null: build from CSR)
   const uint4* wedge;
-  double aa_inv;        // 2^-aa_shift: fixed-point Adamic-Adar sum -> double (blp_graph::aa_shift)
+  unsigned long long* aa_part;  // [2 n_pairs] exact AA words carried between LDS chunks (k_score, chunks > 1)
 };
 
 template <int BLOCK>
@@ -1243,14 +1260,14 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
   static_assert(SEG <= BLOCK, "one pair segment per thread in the output loop");
   constexpr int NW = BLOCK / 64;
   // row-chunk loops (rc_*) for the large-universe variant; the others keep the merge-path loops
-  constexpr bool RC = BLP_RC && CAP_WORDS >= 34816;
+  constexpr bool RC = BLP_RC && CAP_WORDS > 16384;  // the large variant
   __shared__ uint32_t bm_st[SHORT ? 4 : CAP_WORDS + (RC ? RC_EXTRA_WORDS : 0)];
   uint32_t* bm = SHORT ? reinterpret_cast<uint32_t*>(blp_dyn_lds) : bm_st;
   __shared__ int32_t s_coff[RC ? SEG + 1 : 1];
   __shared__ int64_t s_start[SEG];
   __shared__ int32_t s_off[SEG + 1];
   __shared__ uint32_t s_cn[SEG];
-  __shared__ unsigned long long s_aa[SAA ? SEG : 1];
+  __shared__ unsigned long long s_aa[SAA ? 2 * SEG : 1];  // exact AA words, interleaved (aa_push)
   __shared__ unsigned long long red64[NW];
   __shared__ int red[NW];
   __shared__ int s_src;
@@ -1258,7 +1275,7 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
   __shared__ blp::HotRow s_hot[SHORT ? 1 : HOT_LIST];
   __shared__ long long s_wtab[SAA ? 256 : 1];
   // hint table where the LDS allows it (the 64 KiB-bitmap variant keeps 2 workgroups per CU)
-  constexpr int HC = SHORT ? 1 : CAP_WORDS >= 34816 ? (RC ? 1536 : 2048) : CAP_WORDS >= 16384 ? 1 : 512;
+  constexpr int HC = SHORT ? 1 : CAP_WORDS > 16384 ? (RC ? 1536 : 2048) : CAP_WORDS >= 16384 ? 1 : 512;
   __shared__ int32_t s_hint[HC];
 
   if (SAA && a.wtab)  // visible after the first barrier
@@ -1444,7 +1461,10 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
             len = a.g_yl[gp];
             pout = a.g_out[gp];  // used after the scan: its latency hides behind it
             s_cn[threadIdx.x] = 0;
-            if (SAA) s_aa[threadIdx.x] = 0;
+            if (SAA) {
+              s_aa[2 * threadIdx.x] = 0;
+              s_aa[2 * threadIdx.x + 1] = 0;
+            }
           }
           int tot;
           const int ex = block_exscan<BLOCK>(len, red, &tot);
@@ -1492,13 +1512,21 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
           for (int t = threadIdx.x; t < ns; t += BLOCK) {  // ns <= SEG <= BLOCK: t == threadIdx.x
             const int p = pout;
             unsigned c = s_cn[t];
-            double av = SAA ? (double)s_aa[t] * a.aa_inv : 0.0;
-            if (ch > 0) {
-              c += a.cn[p];
-              if (want_a) av += a.aa[p];
-            }
+            if (ch > 0) c += a.cn[p];
             a.cn[p] = c;
-            if (want_a) a.aa[p] = av;
+            if (SAA && want_a) {
+              unsigned long long lo = s_aa[2 * t], hi = s_aa[2 * t + 1];
+              if (ch > 0) {  // the exact words of the earlier chunks
+                lo += a.aa_part[2 * (int64_t)p];
+                hi += a.aa_part[2 * (int64_t)p + 1];
+              }
+              if (last) {
+                a.aa[p] = blp::aa_value(lo, hi);
+              } else {
+                a.aa_part[2 * (int64_t)p] = lo;
+                a.aa_part[2 * (int64_t)p + 1] = hi;
+              }
+            }
             if (want_j && last) {
               const long long uni = (long long)h2 + (s_off[t + 1] - s_off[t]) - (long long)c;
               if (uni <= 0) {
@@ -1531,7 +1559,7 @@ __global__ __launch_bounds__(BLOCK) void k_score_global(ScoreArgs a, uint32_t* g
   __shared__ int64_t s_start[SEG];
   __shared__ int32_t s_off[SEG + 1];
   __shared__ uint32_t s_cn[SEG];
-  __shared__ unsigned long long s_aa[SEG];
+  __shared__ unsigned long long s_aa[2 * SEG];
   __shared__ unsigned long long red64[NW];
   __shared__ int red[NW];
   __shared__ int s_src;
@@ -1586,7 +1614,8 @@ __global__ __launch_bounds__(BLOCK) void k_score_global(ScoreArgs a, uint32_t* g
           s_start[threadIdx.x] = a.g_yb[gp];
           len = a.g_yl[gp];
           s_cn[threadIdx.x] = 0;
-          s_aa[threadIdx.x] = 0;
+          s_aa[2 * threadIdx.x] = 0;
+          s_aa[2 * threadIdx.x + 1] = 0;
         }
         int tot;
         const int ex = block_exscan<BLOCK>(len, red, &tot);
@@ -1602,7 +1631,7 @@ __global__ __launch_bounds__(BLOCK) void k_score_global(ScoreArgs a, uint32_t* g
           const int p = a.g_out[pbeg + sb + t];
           const unsigned c = s_cn[t];
           a.cn[p] = c;
-          if (want_a) a.aa[p] = (double)s_aa[t] * a.aa_inv;
+          if (want_a) a.aa[p] = blp::aa_value(s_aa[2 * t], s_aa[2 * t + 1]);
           if (want_j) {
             const long long uni = (long long)h2 + (s_off[t + 1] - s_off[t]) - (long long)c;
             if (uni <= 0) {
@@ -1655,7 +1684,7 @@ __global__ __launch_bounds__(BLOCK, 8) void k_score_split(ScoreArgs a, const int
   __shared__ int64_t s_start[SEG];
   __shared__ int32_t s_off[SEG + 1];
   __shared__ uint32_t s_cn[SEG];
-  __shared__ unsigned long long s_aa[SEG];
+  __shared__ unsigned long long s_aa[2 * SEG];
   __shared__ unsigned long long red64[NW];
   __shared__ int red[NW];
   __shared__ int s_item;
@@ -1760,7 +1789,8 @@ __global__ __launch_bounds__(BLOCK, 8) void k_score_split(ScoreArgs a, const int
         s_start[threadIdx.x] = a.g_yb[gp] + sp[0];
         len = sp[1] - sp[0];
         s_cn[threadIdx.x] = 0;
-        s_aa[threadIdx.x] = 0;
+        s_aa[2 * threadIdx.x] = 0;
+        s_aa[2 * threadIdx.x + 1] = 0;
       }
       int tot;
       const int ex = block_exscan<BLOCK>(len, red, &tot);
@@ -1775,7 +1805,10 @@ __global__ __launch_bounds__(BLOCK, 8) void k_score_split(ScoreArgs a, const int
       for (int t = threadIdx.x; t < ns; t += BLOCK) {
         const int64_t gp = pbeg + sb + t;
         pcn[(int64_t)c * np + gp] = s_cn[t];
-        if (want_a) paa[(int64_t)c * np + gp] = s_aa[t];
+        if (want_a) {  // exact AA words of this chunk
+          paa[2 * ((int64_t)c * np + gp)] = s_aa[2 * t];
+          paa[2 * ((int64_t)c * np + gp) + 1] = s_aa[2 * t + 1];
+        }
       }
       __syncthreads();
     }
@@ -1799,14 +1832,17 @@ __global__ __launch_bounds__(256) void k_split_combine(ScoreArgs a, int C, const
     for (int t = lane; t < pcnt; t += 64) {
       const int64_t gp = pbeg + t;
       unsigned cn = 0;
-      unsigned long long aa = 0;
+      unsigned long long lo = 0, hi = 0;
       for (int c = 0; c < C; ++c) {
         cn += pcn[(int64_t)c * np + gp];
-        if (want_a) aa += paa[(int64_t)c * np + gp];
+        if (want_a) {
+          lo += paa[2 * ((int64_t)c * np + gp)];
+          hi += paa[2 * ((int64_t)c * np + gp) + 1];
+        }
       }
       const int p = a.g_out[gp];
       a.cn[p] = cn;
-      if (want_a) a.aa[p] = (double)aa * a.aa_inv;
+      if (want_a) a.aa[p] = blp::aa_value(lo, hi);
       if (want_j) {
         const long long uni = h2 + a.g_yl[gp] - (long long)cn;
         if (uni <= 0) {
@@ -1856,7 +1892,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_score_wave(ScoreArgs a) {
   __shared__ int64_t st_all[WAVES][WSEG];
   __shared__ int32_t of_all[WAVES][WSEG + 1];
   __shared__ uint32_t cn_all[WAVES][WSEG];
-  __shared__ unsigned long long aa_all[WAVES][WSEG];
+  __shared__ unsigned long long aa_all[WAVES][2 * WSEG];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   uint32_t* bm = bm_all[wid];
   uint4* bm4 = reinterpret_cast<uint4*>(bm);
@@ -1937,7 +1973,8 @@ __global__ __launch_bounds__(WAVES * 64) void k_score_wave(ScoreArgs a) {
           len = a.g_yl[gp];
           pout = a.g_out[gp];
           s_cn[lane] = 0;
-          s_aa[lane] = 0;
+          s_aa[2 * lane] = 0;
+          s_aa[2 * lane + 1] = 0;
         }
         int tot;
         const int ex = wave_exscan(len, lane, &tot);
@@ -1963,7 +2000,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_score_wave(ScoreArgs a) {
           const int p = pout;
           const unsigned c = s_cn[lane];
           a.cn[p] = c;
-          if (want_a) a.aa[p] = (double)s_aa[lane] * a.aa_inv;
+          if (want_a) a.aa[p] = blp::aa_value(s_aa[2 * lane], s_aa[2 * lane + 1]);
           if (want_j) {
             const long long uni = (long long)h2 + len - (long long)c;
             if (uni <= 0) {
@@ -1984,7 +2021,7 @@ constexpr int W_WAVES = 2, W_CAP = 3328;  // 13 KiB of bitmap per wave (106,496 
 
 enum Variant { V_SMALL = 0, V_MED = 1, V_LARGE = 2 };
 // LDS bitmap words (16 / 64 / 136 KiB), threads per block, pair/row segments per chunk
-constexpr int CAP_SMALL = 4096, CAP_MED = 16384, CAP_LARGE = 34816;
+constexpr int CAP_SMALL = 4096, CAP_MED = 16384, CAP_LARGE = 33792;  // 1.08M bits: fits 160 KiB with the exact AA words
 constexpr int BLOCK_SMALL = 256, BLOCK_MED = 512, BLOCK_LARGE = 1024;
 constexpr int SEG_SMALL = 256, SEG_MED = 512, SEG_LARGE = 512;
 constexpr int G_BLOCK = 1024, G_SEG = 512;  // HBM-bitmap scorer
@@ -2026,7 +2063,8 @@ struct blp_batch {
   int32_t* d_gy = nullptr;     // grouped position -> y (split mode)
   int32_t* d_rsplit = nullptr; // [n][split + 1] row offsets where neighbour ids cross chunk boundaries
   uint32_t* d_pcn = nullptr;   // [split][n_pairs] partial counts
-  unsigned long long* d_paa = nullptr;  // [split][n_pairs] partial fixed-point AA
+  unsigned long long* d_paa = nullptr;  // [split][n_pairs][2] partial exact AA words
+  unsigned long long* d_aa_part = nullptr;  // [n_pairs][2] exact AA words between LDS chunks (chunks > 1)
   uint32_t* d_ph2 = nullptr;   // [n][split] partial |H2|
   uint32_t* d_gbm = nullptr;
   int64_t gwords = 0, gslots = 0;
@@ -2307,7 +2345,7 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
     if (hipMalloc(&b->d_gy, 4 * (size_t)n_pairs) != hipSuccess ||
         hipMalloc(&b->d_rsplit, 4 * (size_t)nrows * (C + 1)) != hipSuccess ||
         hipMalloc(&b->d_pcn, 4 * (size_t)n_pairs * C) != hipSuccess ||
-        hipMalloc(&b->d_paa, 8 * (size_t)n_pairs * C) != hipSuccess ||
+        hipMalloc(&b->d_paa, 16 * (size_t)n_pairs * C) != hipSuccess ||
         hipMalloc(&b->d_ph2, 4 * (size_t)std::max<int64_t>(b->n_sources, 1) * C) != hipSuccess)
       return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: split buffers"));
     hipLaunchKernelGGL(k_row_splits, dim3(2048), dim3(256), 0, g->stream, g->d_rp, g->d_ci, rows_lo, nrows, b->lo,
@@ -2332,6 +2370,8 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
       hipMalloc(&b->d_aa, 8 * np) != hipSuccess || hipMalloc(&b->d_gout, 4 * np) != hipSuccess ||
       hipMalloc(&b->d_gyb, 8 * np) != hipSuccess || hipMalloc(&b->d_gyl, 4 * np) != hipSuccess ||
       hipMalloc(&b->d_misc, sizeof(Misc)) != hipSuccess)
+    return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: hipMalloc failed"));
+  if (b->chunks > 1 && hipMalloc(&b->d_aa_part, 16 * np) != hipSuccess)
     return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: hipMalloc failed"));
   if (n_pairs) {
     if (hipMemcpy(b->d_x, x, 4 * n_pairs, hipMemcpyHostToDevice) != hipSuccess ||
@@ -2365,7 +2405,7 @@ int blp_batch_destroy(blp_batch* b) {
   b->scratch.release();
   if (b->stream) (void)hipStreamDestroy(b->stream);
   void* ps[] = {b->d_x,    b->d_y,    b->d_cn,   b->d_jac,  b->d_aa,          b->d_gout,        b->d_gyb,
-                b->d_gyl,  b->d_misc, b->d_heavy_slot, b->d_heavy_bm, b->d_heavy_items, b->d_gbm, b->d_gy, b->d_rsplit, b->d_pcn, b->d_paa, b->d_ph2};
+                b->d_gyl,  b->d_misc, b->d_heavy_slot, b->d_heavy_bm, b->d_heavy_items, b->d_gbm, b->d_gy, b->d_rsplit, b->d_pcn, b->d_paa, b->d_ph2, b->d_aa_part};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   delete b;
@@ -2494,7 +2534,7 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   a.rp = g->d_rp;
   a.ci = g->d_ci;
   a.aaw = g->d_aaw_fx;
-  a.aa_inv = std::ldexp(1.0, -g->aa_shift);
+  a.aa_part = b->d_aa_part;
   const bool coded = g->d_ci_w && !getenv("BLP_NO_WCODES");  // tuning knob
   a.cw = coded ? g->d_ci_w : g->d_ci;
   a.idbits = coded ? g->id_bits : 31;

@@ -20,9 +20,10 @@
 // Adamic-Adar: every w that reaches a distance-3 target has degree >= 2, so
 // CN * wmin <= AA <= CN * wmax with the extreme weights of such w. From the CN counts the
 // candidates that can still reach the k-th AA lower bound are collected (usually a few
-// hundred), and one more push accumulates their exact fixed-point sums (the pair kernel's
-// arithmetic, so the values are bit-identical to blp_score_pairs). When the candidates do
-// not fit, the source falls back to chunked direct fixed-point accumulation.
+// hundred), and one more push accumulates their exact sums (the pair kernel's two-word integer
+// arithmetic, blp_internal.h, so the values are bit-identical to blp_score_pairs). When the
+// candidates do not fit, the source falls back to chunked direct accumulation. AA selection
+// keys are the bits of the correctly rounded double (monotone for non-negative doubles).
 #include <algorithm>
 #include <cmath>
 #include <climits>
@@ -36,7 +37,8 @@ namespace {
 
 constexpr int TK_NT = 1024;
 constexpr int TK_SEL = 2048;          // selection buffer entries (also the AA hash table)
-constexpr int TK_HCAP = TK_SEL / 2;   // AA candidates handled by the hash (load <= 1/2)
+constexpr int TK_AH = TK_SEL / 2;     // AA hash slots: two u64 words each in s.key (exact sums)
+constexpr int TK_HCAP = TK_AH / 2;    // AA candidates handled by the hash (load <= 1/2)
 constexpr int TK_SEG = 256;           // N(x) entries staged per batch
 constexpr int TK_FILT = 128;          // words of the N'(x) membership filter (4096 bits)
 constexpr int TK_ACC_WORDS = 32768;   // counter space: 128 KiB
@@ -71,8 +73,8 @@ struct TkArgs {
   int64_t tlo, T;
   const TkChunk* chunks;
   int n_chunks;
-  int64_t aa_chunk;  // targets per direct-AA chunk (u64 each)
-  int64_t H, AH;     // fused AA: the H most popular targets (addresses < AH) get u64 sums in the count pass
+  int64_t aa_chunk;  // targets per direct-AA chunk (two u64 words each)
+  int64_t H, AH;     // fused AA: the H most popular targets (addresses < AH) get exact sums in the count pass
   int64_t h_word;    // ... stored at LDS word h_word (8-byte aligned, after the chunk's counters)
   int k;
   uint32_t mask;
@@ -132,8 +134,19 @@ __device__ inline void acc_clear(const TkArgs& a, uint32_t* acc, const TkChunk& 
   atomicAnd(&acc[off >> 2], ~(width_mask(a, e) << ((off & 3) << 3)));
 }
 
-constexpr int TK_HBITS = 11;  // log2(TK_SEL)
+constexpr int TK_HBITS = 10;  // log2(TK_AH)
 __device__ inline int hash_slot(int32_t e) { return (int)(((uint32_t)e * 2654435761u) >> (32 - TK_HBITS)); }
+
+// one term W into target t's exact AA words (lo wrapping, hi = sum of W >> 32)
+__device__ inline void aa_push2(unsigned long long* w2, int64_t t, unsigned long long W) {
+  atomicAdd(&w2[2 * t], W);
+  atomicAdd(&w2[2 * t + 1], W >> 32);
+}
+
+// selection key of an exact AA word pair: the bits of the correctly rounded double
+__device__ inline unsigned long long aa_key(const unsigned long long* w2, int64_t t) {
+  return (unsigned long long)__double_as_longlong(blp::aa_value(w2[2 * t], w2[2 * t + 1]));
+}
 
 __device__ long long block_sum(TkShared& s, long long v) {
   for (int d = 32; d > 0; d >>= 1) v += __shfl_down(v, d, 64);
@@ -158,9 +171,10 @@ __device__ inline bool in_row_x(const TkShared& s, const int32_t* rowx, int du, 
 }
 
 // MODE 0: CN counts into the tiered counters of chunk c (and |H2(x)| when count_h2)
-// MODE 3: MODE 0 plus the fixed-point AA sums of the H most popular targets (fused AA)
-// MODE 1: exact AA of the hashed candidates (counter >= thr) into s.key[slot]
-// MODE 2: direct AA fixed-point sums of targets [c0, c1) into the u64 view of s.acc
+// MODE 3: MODE 0 plus the exact AA words of the H most popular targets (fused AA)
+// MODE 1: exact AA of the hashed candidates (counter >= thr) into s.key[2 slot], s.key[2 slot + 1]
+// MODE 2: direct exact AA words of targets [c0, c1) into the u64 view of s.acc
+// (two words per target: the wrapping sum of W and the sum of W >> 32, blp_internal.h)
 template <int MODE>
 __device__ long long push_pass(const TkArgs& a, TkShared& s, int x, int64_t xb, int du, const int32_t* rowx,
                                const TkChunk& c, uint32_t thr, int64_t d0, int64_t d1, bool count_h2,
@@ -267,10 +281,10 @@ __device__ long long push_pass(const TkArgs& a, TkShared& s, int x, int64_t xb, 
         const unsigned long long wfx = (unsigned long long)a.wtab[len_w];
 #pragma unroll
         for (int j = 0; j < TK_RB; ++j)
-          if (j < len_w && e[j] < a.AH) atomicAdd(&aah[p_of(a, e[j])], wfx);
+          if (j < len_w && e[j] < a.AH) aa_push2(aah, p_of(a, e[j]), wfx);
         for (int j = TK_RB; j < len_w; ++j) {
           const int32_t ej = roww[j];
-          if (ej < a.AH) atomicAdd(&aah[p_of(a, ej)], wfx);
+          if (ej < a.AH) aa_push2(aah, p_of(a, ej), wfx);
         }
       }
       if (MODE == 0 || MODE == 3) {
@@ -290,8 +304,8 @@ __device__ long long push_pass(const TkArgs& a, TkShared& s, int x, int64_t xb, 
         auto push1 = [&](int32_t ej) {
           if (acc_get(a, s.acc, c, ej) >= thr) {
             int h = hash_slot(ej);
-            while (s.col[h] != ej) h = (h + 1) & (TK_SEL - 1);
-            atomicAdd(&s.key[h], wfx);
+            while (s.col[h] != ej) h = (h + 1) & (TK_AH - 1);
+            aa_push2(s.key, h, wfx);
           }
         };
 #pragma unroll
@@ -303,11 +317,11 @@ __device__ long long push_pass(const TkArgs& a, TkShared& s, int x, int64_t xb, 
 #pragma unroll
         for (int j = 0; j < TK_RB; ++j) {
           const int64_t p = p_of(a, e[j]);
-          if (j < len_w && p >= d0 && p < d1) atomicAdd(&acc64[p - d0], wfx);
+          if (j < len_w && p >= d0 && p < d1) aa_push2(acc64, p - d0, wfx);
         }
         for (int j = TK_RB; j < len_w; ++j) {
           const int64_t p = p_of(a, roww[j]);
-          if (p >= d0 && p < d1) atomicAdd(&acc64[p - d0], wfx);
+          if (p >= d0 && p < d1) aa_push2(acc64, p - d0, wfx);
         }
       }
     }
@@ -462,7 +476,7 @@ __global__ __launch_bounds__(TK_NT) void k_topk(TkArgs a) {
     for (int ci = 0; ci < a.n_chunks; ++ci) {
       const TkChunk c = a.chunks[ci];
       const bool fused = want_aa && a.H > 0 && a.n_chunks == 1;
-      const int words = fused ? (int)(a.h_word + 2 * a.H) : (int)((c.a1 - c.a0 + 3) >> 2);
+      const int words = fused ? (int)(a.h_word + 4 * a.H) : (int)((c.a1 - c.a0 + 3) >> 2);
       for (int i = tid; i < words; i += TK_NT) s.acc[i] = 0;
       __syncthreads();
       long long np = 0;
@@ -510,7 +524,7 @@ __global__ __launch_bounds__(TK_NT) void k_topk(TkArgs a) {
           for (int64_t base = 0; base < a.H; base += TK_NT) {
             const int64_t p = base + tid;
             const bool ok = p < a.H && acc_get(a, s.acc, c, addr_of(a, p)) > 0;
-            sel_offer(s, ok, ok ? aah[p] : 0ull, ok ? a.inv[p] : 0);
+            sel_offer(s, ok, ok ? aa_key(aah, p) : 0ull, ok ? a.inv[p] : 0);
             sel_round_end(a, s);
           }
           sel_end(a, s, 2, it);
@@ -526,18 +540,18 @@ __global__ __launch_bounds__(TK_NT) void k_topk(TkArgs a) {
             const int32_t e = (int32_t)addr_of(a, p);
             if (acc_get(a, s.acc, c, e) >= thr) {
               int h = hash_slot(e);
-              while (atomicCAS(&s.col[h], (int32_t)TK_EMPTY, e) != (int32_t)TK_EMPTY) h = (h + 1) & (TK_SEL - 1);
+              while (atomicCAS(&s.col[h], (int32_t)TK_EMPTY, e) != (int32_t)TK_EMPTY) h = (h + 1) & (TK_AH - 1);
             }
           }
           __syncthreads();
           push_pass<1>(a, s, x, xb, du, rowx, c, thr, 0, 0, false);
-          // hash slots -> selection entries (key = AA fixed point, col = dense target id)
+          // hash slots -> selection entries (key = bits of the exact AA double, col = dense target id)
           unsigned long long kv[TK_SEL / TK_NT];
           int cv[TK_SEL / TK_NT];
           for (int r = 0; r < TK_SEL / TK_NT; ++r) {
             const int i = tid + r * TK_NT;
-            const int32_t e = s.col[i];
-            kv[r] = e == (int32_t)TK_EMPTY ? 0ull : s.key[i];
+            const int32_t e = i < TK_AH ? s.col[i] : (int32_t)TK_EMPTY;
+            kv[r] = e == (int32_t)TK_EMPTY ? 0ull : aa_key(s.key, i);
             cv[r] = e == (int32_t)TK_EMPTY ? 0x7FFFFFFF : a.inv[p_of(a, e)];
           }
           __syncthreads();
@@ -569,18 +583,18 @@ __global__ __launch_bounds__(TK_NT) void k_topk(TkArgs a) {
       if (!done) {
         for (int64_t d0 = 0; d0 < a.T; d0 += a.aa_chunk) {
           const int64_t d1 = min(a.T, d0 + a.aa_chunk);
-          for (int64_t i = tid; i < d1 - d0; i += TK_NT) acc64[i] = 0;
+          for (int64_t i = tid; i < 2 * (d1 - d0); i += TK_NT) acc64[i] = 0;
           __syncthreads();
           push_pass<2>(a, s, x, xb, du, rowx, a.chunks[0], 0, d0, d1, false);
           for (int j = tid; j < du; j += TK_NT) {
             const int64_t p = p_of(a, rowx[j]);
-            if (p >= d0 && p < d1) acc64[p - d0] = 0;
+            if (p >= d0 && p < d1) acc64[2 * (p - d0)] = acc64[2 * (p - d0) + 1] = 0;
           }
           __syncthreads();
           sel_begin(a, s, 2, it);
           for (int64_t base = d0; base < d1; base += TK_NT) {
             const int64_t p = base + tid;
-            const unsigned long long v = p < d1 ? acc64[p - d0] : 0ull;
+            const unsigned long long v = p < d1 ? aa_key(acc64, p - d0) : 0ull;
             sel_offer(s, v > 0, v, v > 0 ? a.inv[p] : 0);
             sel_round_end(a, s);
           }
@@ -659,12 +673,12 @@ void plan_chunks(blp_topk* t) {
     t->chunks.push_back(c);
     c0 = c1;
   } while (c0 < t->T);
-  t->aa_chunk = t->acc_words / 2;
-  // fused AA (single counter chunk): the most popular targets get u64 sums in the spare words
+  t->aa_chunk = t->acc_words / 4;
+  // fused AA (single counter chunk): the most popular targets get exact word pairs in the spare words
   t->H = 0;
   if (t->chunks.size() == 1 && !env_i64("BLP_TOPK_NO_FUSE", 0)) {
     t->h_word = (chunk_words(t, 0, t->T) + 1) / 2 * 2;
-    t->H = std::max<int64_t>(0, std::min<int64_t>(t->T, (t->acc_words - t->h_word) / 2));
+    t->H = std::max<int64_t>(0, std::min<int64_t>(t->T, (t->acc_words - t->h_word) / 4));
   }
   t->AH = t->H > 0 ? host_addr(t, t->H) : 0;
 }
@@ -942,7 +956,7 @@ extern "C" int blp_topk_fetch(blp_topk* t, uint32_t method, int32_t* cols, doubl
         if (c[i] >= 0) {
           if (m == 0) v = (double)keys[i];
           else if (m == 1) { memcpy(&v, &keys[i], 8); }
-          else v = (double)(long long)keys[i] * std::ldexp(1.0, -t->g->aa_shift);
+          else memcpy(&v, &keys[i], 8);  // AA: the exact sum's double (blp_internal.h)
         }
         scores[i] = v;
       }

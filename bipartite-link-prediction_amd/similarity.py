@@ -1,9 +1,10 @@
 """Drop-in for the reference's similarity.py, computed by the HIP engine (libblp.so).
 
 Same call surface (similarity.py:11-126) and the same score files: common_neighbors and
-jaccard bit-exact, adamic_adar within ~1e-12 absolute (an exact, order-independent
-2^-40 fixed-point sum of the reference's float terms; the reference sums in Python set
-order, so its own last bits depend on that order):
+jaccard bit-exact; adamic_adar is the correctly rounded sum of the reference's own float
+terms (exact integer sums on the device, rounded once: math.fsum of the same terms). The
+reference adds those terms in Python set order with a rounding per add, so its last bits
+depend on that order and differ from this value by a few ulps (~1e-15 relative):
 
 * ``main(example_file, graph_file, u_methods, u_outfiles, b_methods, b_outfiles)``
 * ``users(examples, G, methods, outfiles)`` / ``business(examples, G, methods, outfiles)``

@@ -245,20 +245,17 @@ def hop3_candidates(adj, u):
 
 
 # --------------------------------------------------------------------------- full-candidate top-k
-AA_SCALE = 2.0 ** 40  # the engine's fixed-point Adamic-Adar unit (exact integer sums)
-
-
-def aa_fixed(h2, nb, adj):
-    """adamic_adar(h2, nb, G) (similarity.py:116-126) summed in 2^-40 fixed point: each term
-    (log deg)^-1 is rounded to the nearest 2^-40 (half-even, as llrint) and the integers are
-    added, so the sum is independent of set order (the reference's own order is Python set
-    order; the two agree to ~1e-12 relative)."""
-    fx = 0
-    for w in h2.intersection(nb):
+def adamic_adar_exact(s1, s2, adj):
+    """adamic_adar (similarity.py:116-126) with the terms added exactly and rounded once
+    (math.fsum): the value the engine returns (blp_internal.h). The reference adds the same
+    terms in Python set order with a rounding per add, so it agrees to a few ulps; keeps the
+    reference's int 0 when nothing is added."""
+    terms = []
+    for w in s1.intersection(s2):
         d = degree(adj, w)
         if d > 1:
-            fx += round(math.log(d) ** -1 * AA_SCALE)
-    return fx
+            terms.append(math.log(d) ** -1)
+    return math.fsum(terms) if terms else 0
 
 
 def topk_full_candidates(adj, x, k, method):
@@ -279,8 +276,8 @@ def topk_full_candidates(adj, x, k, method):
             s = jaccard(h2, nb)
             key = s
         else:
-            key = aa_fixed(h2, nb, adj)
-            s = key / AA_SCALE
+            s = adamic_adar_exact(h2, nb, adj)
+            key = s
         rows.append((-key, b, s))
     rows.sort()
     return [(b, s) for _, b, s in rows[:k]], len(cands)

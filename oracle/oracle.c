@@ -12,6 +12,11 @@
  *                      marker set; per pair |H2(x) ∩ N(y)| (:113-114), the Jaccard quotient
  *                      float(|∩|)/float(|∪|) (:108-111) and the Adamic-Adar sum of
  *                      (log deg)^-1 over deg > 1 (:116-126), N(y) = GetNodesAtHop(y,1) (:41/:85).
+ *                      The Adamic-Adar terms are added exactly (128-bit integer in units of
+ *                      2^-58: every term (log d)^-1 in [2^-5, 2) is such an integer) and the
+ *                      sum is rounded once: the correctly rounded sum, math.fsum of the same
+ *                      terms. The reference adds them in Python set order, rounding at every
+ *                      add, and so differs from it by a few ulps at most.
  *   - og_hop3:         dataset_maker.py:139 GetNodesAtHop(G,u,3) candidate sets.
  * Pinned against tests/golden (reference outputs) by tests/test_oracle.py.
  */
@@ -143,14 +148,14 @@ int og_score_pairs(const og_graph* g, int64_t np, const int32_t* xs, const int32
                 int64_t p = perm[k];
                 int32_t y = ys[p];
                 uint32_t c = 0;
-                double s = 0.0;
+                unsigned __int128 s = 0; /* exact, units of 2^-58 */
                 int64_t hop1 = g->deg[y] - g->self[y];
                 for (int64_t e = g->rp[y]; e < g->rp[y + 1]; ++e) {
                     int32_t w = g->ci[e];
                     if (w == y) continue;
                     if (dist[w] == 2) {
                         ++c;
-                        if (g->deg[w] > 1) s += pow(log((double)g->deg[w]), -1.0);
+                        if (g->deg[w] > 1) s += (uint64_t)ldexp(pow(log((double)g->deg[w]), -1.0), 58);
                     }
                 }
                 if (mask & 1u) cn[p] = c;
@@ -162,7 +167,7 @@ int og_score_pairs(const og_graph* g, int64_t np, const int32_t* xs, const int32
                     } else
                         jac[p] = (double)c / (double)uni;
                 }
-                if (mask & 4u) aa[p] = s;
+                if (mask & 4u) aa[p] = ldexp((double)s, -58); /* one rounding: nearest even */
                 if (h2out) h2out[p] = (uint32_t)h2;
             }
             for (int64_t i = 0; i < nv; ++i) dist[visited[i]] = -1;

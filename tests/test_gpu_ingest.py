@@ -121,7 +121,7 @@ def test_device_graph_scores_match_oracle(gpu, knobs, monkeypatch):
         np.testing.assert_array_equal(got["cn"], cn)
         np.testing.assert_array_equal(got["jaccard"], jac)
         if mask & blp.ADAMIC:
-            np.testing.assert_allclose(got["adamic"], aa, rtol=1e-9, atol=0)
+            np.testing.assert_array_equal(got["adamic"], aa)  # exact sums: bit-exact
     if "BLP_SPLIT" in knobs:
         assert G.batch(x, y).plan()["chunks"] == -3
     if "BLP_FORCE_GLOBAL" in knobs:
@@ -205,4 +205,4 @@ def test_two_ranks_share_the_gpu(gpu, tmp_path):
         cn, jac, aa, _ = og.score_pairs(np.searchsorted(ids, r["x"]), np.searchsorted(ids, r["y"]), 7)
         np.testing.assert_array_equal(r["cn"], cn)
         np.testing.assert_array_equal(r["jaccard"], jac)
-        np.testing.assert_allclose(r["adamic"], aa, rtol=1e-9, atol=0)
+        np.testing.assert_array_equal(r["adamic"], aa)  # exact sums: bit-exact

@@ -40,10 +40,9 @@ def _check_against_oracle(ga, gb, x, y, mask=7):
     if mask & blp.JACCARD:
         np.testing.assert_array_equal(got["jaccard"], jac)  # bit-exact
     if mask & blp.ADAMIC:
-        np.testing.assert_allclose(got["adamic"], aa, rtol=1e-9, atol=0)
-        assert np.array_equal(got["adamic"] == 0, aa == 0)
+        np.testing.assert_array_equal(got["adamic"], aa)  # exact sums on both sides: bit-exact
     # the same pairs grouped by source (x non-decreasing): the run-head grouping path; the
-    # fixed-point sums make every score independent of pair order, so results are identical
+    # exact sums make every score independent of pair order, so results are identical
     order = np.argsort(x, kind="stable")
     got_sorted = G.score_pairs(x[order], y[order], mask)
     for k, v in got.items():
@@ -258,31 +257,55 @@ def test_coscheduled_passes_match_single_passes(gpu, variant, monkeypatch):
     _check_against_oracle(a, b, x, y)
 
 
-@pytest.mark.parametrize("request_shift", [62, 50])
-def test_adamic_fixed_point_overflow_guard(gpu, request_shift, monkeypatch):
-    """The Adamic-Adar sums are 64-bit fixed point. Asking for a scale that would wrap them on
-    this graph (BLP_AA_SHIFT, a test knob; the default is 2^40) must make blp_graph_create lower
-    the scale until max_row_len x max_weight fits: results then still match the oracle, for
-    both sides and the top-k engine. Without the guard, 2^62 wraps on the first hub."""
-    monkeypatch.setenv("BLP_AA_SHIFT", str(request_shift))
+def test_adamic_exact_on_hub_pairs(gpu):
+    """Adamic-Adar sums are exact (two-word integer sums of w * 2^58, blp_internal.h), so a pair
+    with ~100K common neighbours -- far past where a 64-bit 2^-40 fixed point would wrap
+    (Σw >= 2^23) for larger hubs -- still equals the correctly rounded sum of the reference's
+    terms: math.fsum of (log deg)^-1 over H2(x) ∩ N(y) (similarity.py:116-126), bit for bit."""
     rng = np.random.default_rng(31)
-    a, b = bipartite_edges(rng, 30000, 800, 240000)
+    # two hub businesses reviewed by most of 120K users, plus background reviews
+    nu = 120000
+    users = np.arange(nu)
+    a = np.concatenate([users, users[: nu * 9 // 10], rng.integers(0, nu, 200000)])
+    b = np.concatenate([np.full(nu, nu), np.full(nu * 9 // 10, nu + 1), nu + 2 + rng.integers(0, 500, 200000)])
     G = blp.DeviceGraph(a, b)
-    dmax = int(G.hop1_size.max())
-    wmax = float(G.aa_weight.max())
-    s = G.aa_shift
-    assert s <= request_shift
-    assert dmax * (wmax * 2.0**s + 0.5) < 2.0**63                 # the bound holds
-    if dmax * (wmax * 2.0**request_shift) >= 2.0**63:
-        assert s < request_shift                                   # and the guard engaged
-    nu = G.n - len(np.unique(b))
-    x = np.repeat(rng.choice(nu, 150, replace=False), 30).astype(np.int32)
-    y = rng.integers(nu, G.n, len(x)).astype(np.int32)
-    _check_against_oracle(a, b, x, y)
-    _check_against_oracle(a, b, y, x)
+    x = G.dense(np.array([0, 1, 2, 3], np.int64)).astype(np.int32)   # users
+    y = G.dense(np.array([nu + 1, nu + 1, nu, nu + 2], np.int64)).astype(np.int32)  # hub targets
+    got = G.score_pairs(x, y, 7)
+    assert got["cn"].min() > 50000
+    _check_against_oracle(a, b, x, y)  # bit-exact vs the C oracle's 128-bit sums
+    # the same value from math.fsum over the reference's own terms
+    deg = G.degree
+    for i in range(len(x)):
+        h2 = set(np.flatnonzero(_h2_mask(G, int(x[i]))))
+        nb = set(G.col_idx[G.row_ptr[y[i]]:G.row_ptr[y[i] + 1]].tolist())
+        terms = [math.log(int(deg[w])) ** -1 for w in h2 & nb if deg[w] > 1]
+        assert got["adamic"][i] == math.fsum(terms)
 
 
-def test_adamic_default_scale_is_2_pow_40(gpu):
+def _h2_mask(G, x):
+    """Exact distance-2 membership of every dense node (host-side BFS over the CSR mirror)."""
+    rp, ci = G.row_ptr, G.col_idx
+    d1 = ci[rp[x]:rp[x + 1]]
+    m = np.zeros(G.n, bool)
+    for z in d1:
+        m[ci[rp[z]:rp[z + 1]]] = True
+    m[d1] = False
+    m[x] = False
+    return m
+
+
+def test_adamic_scale_and_weight_range(gpu):
     rng = np.random.default_rng(2)
     a, b = bipartite_edges(rng, 2000, 300, 20000)
-    assert blp.DeviceGraph(a, b).aa_shift == 40
+    G = blp.DeviceGraph(a, b)
+    assert G.aa_shift == 58
+    # a custom weight table outside [0, 64) is refused (exactness bound, blp_internal.h)
+    from blp._lib import lib, ptr
+    import ctypes
+    for bad in (-1.0, 64.0, float("nan")):
+        w = np.array(G.aa_weight, np.float64)
+        w[3] = bad
+        h = ctypes.c_void_p()
+        rc = lib().blp_graph_create(ptr(G.row_ptr), ptr(G.col_idx), G.n, ptr(w), 0, ctypes.byref(h))
+        assert rc == -1 and "aa_weight" in lib().blp_last_error().decode()  # BLP_E_ARG

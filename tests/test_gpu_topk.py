@@ -110,7 +110,8 @@ def test_topk_aa_paths_agree(small, monkeypatch):
 
 
 def test_topk_scores_equal_pair_scorer(small):
-    """Top-k scores are the pair kernel's values bit-for-bit; AA within 1e-9 of float sums."""
+    """Top-k scores are the pair kernel's values bit-for-bit; AA equals math.fsum of the
+    reference's terms exactly and the reference's own set-order float sum to 1e-12."""
     G, adj, rng = small
     src = rng.choice(G.n_col0, 24, replace=False)
     res = blp.TopK(G, "user")(src, k=25, mask=ALL)
@@ -125,8 +126,9 @@ def test_topk_scores_equal_pair_scorer(small):
         h2 = bo.nodes_at_hop(adj, int(G.node_ids[x]), 2)
         for c, s in zip(cols[i], scores[i]):
             if c >= 0:
-                ref = bo.adamic_adar(h2, bo.nodes_at_hop(adj, int(G.node_ids[c]), 1), adj)
-                assert math.isclose(s, ref, rel_tol=1e-9)
+                nb = bo.nodes_at_hop(adj, int(G.node_ids[c]), 1)
+                assert s == bo.adamic_adar_exact(h2, nb, adj)
+                assert math.isclose(s, bo.adamic_adar(h2, nb, adj), rel_tol=1e-12)
 
 
 def test_topk_business_side(small):

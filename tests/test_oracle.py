@@ -58,7 +58,7 @@ def test_c_oracle_matches_reference_similarity(case):
         u, v = us[i], vs[i]
         assert ucn[k] == ref["ucn"][u][v]
         assert ujac[k] == ref["ujac"][u][v]
-        assert math.isclose(uaa[k], ref["uaa"][u][v], rel_tol=1e-12)
+        assert math.isclose(uaa[k], ref["uaa"][u][v], rel_tol=1e-12)  # set-order sum vs exact
         assert bcn[k] == ref["bcn"][u][v]
         assert bjac[k] == ref["bjac"][u][v]
         k += 1
@@ -219,6 +219,7 @@ def test_c_oracle_matches_python_oracle_random(edges, seed):
         assert cn[i] == O.common_neighbors(h2, n1)
         assert jac[i] == O.jaccard(h2, n1)
         assert math.isclose(aa[i], O.adamic_adar(h2, n1, adj), rel_tol=1e-12, abs_tol=1e-300)
+        assert aa[i] == O.adamic_adar_exact(h2, n1, adj)  # 128-bit sum == math.fsum, bit for bit
 
 
 @pytest.mark.parametrize("split", ["bip/train", "bip/test"])
@@ -272,3 +273,29 @@ def test_svd_entry_parity_rule():
     bad = a.copy()
     bad[np.flatnonzero(zero)[0]] = 1e-300
     assert not O.svd_entry_parity(bad, b, zero)["ok"]
+
+
+def test_exact_adamic_sum_on_many_terms():
+    """The C oracle's 128-bit Adamic-Adar sum equals math.fsum of the reference's terms on a pair
+    with 20K common neighbours of mixed degree (where naive float addition drifts by many ulps)."""
+    rng = np.random.default_rng(5)
+    n_users = 20000
+    users = np.arange(n_users)
+    extra_b = 2 + rng.integers(0, 3000, 60000)
+    a = np.concatenate([users, users, rng.integers(0, n_users, 60000)])
+    b = np.concatenate([np.zeros(n_users, np.int64), np.ones(n_users, np.int64), extra_b]) + n_users
+    ids, da, db = dense_edges(a, b)
+    g = coracle.OracleGraph(len(ids), da, db)
+    x = np.searchsorted(ids, [0, 7]).astype(np.int32)
+    y = np.searchsorted(ids, [n_users + 1, n_users + 1]).astype(np.int32)
+    cn, _, aa, _ = g.score_pairs(x, y, 7)
+    adj = {}
+    for p, q in zip(a.tolist(), b.tolist()):
+        adj.setdefault(p, set()).add(q)
+        adj.setdefault(q, set()).add(p)
+    for i, u in enumerate([0, 7]):
+        h2 = O.nodes_at_hop(adj, u, 2)
+        n1 = O.nodes_at_hop(adj, n_users + 1, 1)
+        assert cn[i] == len(h2 & n1) > 19000
+        assert aa[i] == O.adamic_adar_exact(h2, n1, adj)
+        assert math.isclose(aa[i], O.adamic_adar(h2, n1, adj), rel_tol=1e-12)
