@@ -272,7 +272,7 @@ def test_adamic_exact_on_hub_pairs(gpu):
     x = G.dense(np.array([0, 1, 2, 3], np.int64)).astype(np.int32)   # users
     y = G.dense(np.array([nu + 1, nu + 1, nu, nu + 2], np.int64)).astype(np.int32)  # hub targets
     got = G.score_pairs(x, y, 7)
-    assert got["cn"].min() > 50000
+    assert got["cn"][:3].min() > 100000  # hub pairs
     _check_against_oracle(a, b, x, y)  # bit-exact vs the C oracle's 128-bit sums
     # the same value from math.fsum over the reference's own terms
     deg = G.degree
