@@ -593,6 +593,101 @@ def run_sharded(args):
     d.close()
 
 
+def run_e2e(args):
+    """Config 1 (Yelp-sized synthetic, BASELINE.json configs[0]) and config 2 end to end: the
+    drop-in similarity.main (similarity.py:11-18) from graph.txt + examples.json to the six
+    JSON files (parse + id lookup + device step + dict assembly + json.dumps, util.py:18-21),
+    one run, phases timed. Beside it: the device-only step on the same pairs, the C oracle's
+    reference-algorithm scoring of every pair (1 thread and all host threads), and every
+    score file checked against the oracle (CN / Jaccard / Adamic-Adar bit-exact)."""
+    import importlib
+    import shutil
+    import tempfile
+
+    import pandas as pd
+
+    import coracle
+
+    sim = importlib.import_module("similarity")
+    util = importlib.import_module("util")
+    dist = Dist()
+    dev = _device(dist)
+    blp.lib()
+    U, B, D = synth.CONFIGS[args.config]
+    work = tempfile.mkdtemp(prefix="blp_e2e_", dir=os.environ.get("TMPDIR", "/tmp"))
+    try:
+        t0 = time.time()
+        a, b = synth.review_edges(U, B, D, seed=0)
+        gpath = os.path.join(work, "graph.txt")
+        pd.DataFrame({"u": a, "b": b}).to_csv(gpath, sep="\t", header=False, index=False)
+        G = blp.DeviceGraph(a, b, device=dev)
+        del a, b
+        ex_x, ex_y, ex_l = synth.make_examples(G, U, B, D, n_users=args.users, rate=args.rate, seed=0)
+        uid, bid = G.node_ids[ex_x].tolist(), G.node_ids[ex_y].tolist()
+        examples = {}
+        for u, v, l in zip(uid, bid, ex_l.tolist()):
+            examples.setdefault(str(u), {})[str(v)] = int(l)
+        epath = os.path.join(work, "examples.json")
+        util.write_json(examples, epath)
+        log("e2e inputs: %d edges in graph.txt (%.0f MB), %d pairs of %d users, in %.1fs" %
+            (D, os.path.getsize(gpath) / 2**20, len(ex_x), len(examples), time.time() - t0))
+        # the device-only step on the same pairs (both passes, concurrent), for reference
+        ub, bb = G.batch(ex_x, ex_y), G.batch(ex_y, ex_x)
+        step = [(ub, 7), (bb, 3)]
+        G.score_batches(step)
+        blp.device_sync(dev)
+        t = time.perf_counter()
+        for _ in range(5):
+            G.score_batches(step)
+        blp.device_sync(dev)
+        dev_ms = (time.perf_counter() - t) / 5 * 1e3
+        og = coracle.OracleGraph(G.n, *_dense_edges(G))
+        ub.close()
+        bb.close()
+        G.close()
+        del G
+        # timed: similarity.main end to end
+        uf = [os.path.join(work, f) for f in ("u_cn.json", "u_jaccard.json", "u_adamic.json")]
+        bf = [os.path.join(work, f) for f in ("b_cn.json", "b_jaccard.json", "b_adamic.json")]
+        methods = ["common_neighbors", "jaccard", "adamic_adar"]
+        ph = {}
+        t = time.perf_counter()
+        sim.main(epath, gpath, methods, uf, methods, bf, timings=ph)
+        e2e = time.perf_counter() - t
+        n = ph["pairs"]
+        # the C oracle (reference algorithm) on every pair of both sides
+        cpu = {}
+        nt = max(1, len(os.sched_getaffinity(0)))
+        for threads in (1, nt):
+            t = time.perf_counter()
+            ucn, ujac, uaa, _ = og.score_pairs(ex_x, ex_y, 7, nthreads=threads)
+            bcn, bjac, _, _ = og.score_pairs(ex_y, ex_x, 3, nthreads=threads)
+            cpu["%dt" % threads] = {"seconds": time.perf_counter() - t, "pairs_per_s": n / (time.perf_counter() - t)}
+        # every score file against the oracle, in the files' own order (= examples order)
+        par = {}
+        for f, want in ((uf[0], ucn), (uf[1], ujac), (uf[2], uaa), (bf[0], bcn), (bf[1], bjac)):
+            got = [v for u in util.load_json(f).values() for v in u.values()]
+            w = want.tolist()
+            if f.endswith("_adamic.json"):
+                w = [0 if x == 0.0 else x for x in w]
+            par[os.path.basename(f)] = bool(got == w and all(type(g) is type(x) for g, x in zip(got, w)))
+        out = {"metric": "similarity.main end to end (graph.txt -> 6 JSON files), pairs/s", "value": n / e2e,
+               "unit": "pairs/s", "n_gpus": 1, "higher_is_better": True, "data": "synthetic",
+               "config": {"workload": "%s: synthetic %d users x %d businesses, %d draws; %d example users, hop-3 "
+                                      "candidates kept at %g; u_methods = b_methods = CN, Jaccard, AA (the reference's "
+                                      "__main__ call, similarity.py:129-135)" % (args.config, U, B, D, len(examples),
+                                                                                  args.rate), "pairs": n},
+               "e2e_s": e2e, "phases_s": {k: v for k, v in ph.items() if k != "pairs"},
+               "device_step_ms": dev_ms, "device_pairs_per_s": n / (dev_ms / 1e3),
+               "cpu_reference_algorithm": {"kind": "port", "what": "C oracle scoring of every pair of both sides "
+                                           "(graph already built; no file I/O)", **cpu},
+               "files_equal_oracle": par, "ok": all(par.values())}
+        if dist.rank == 0:
+            print(json.dumps(out), flush=True)
+    finally:
+        shutil.rmtree(work, ignore_errors=True)
+
+
 def _free_port():
     import socket
 
@@ -636,10 +731,11 @@ def main():
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--user-mask", type=int, default=7, help="methods of the user pass (1 CN, 2 J, 4 AA)")
     ap.add_argument("--business-first", action="store_true", help="enqueue the business pass before the user pass")
-    ap.add_argument("--mode", default="similarity", choices=["similarity", "topk", "svd", "sharded"],
+    ap.add_argument("--mode", default="similarity", choices=["similarity", "topk", "svd", "sharded", "e2e"],
                     help="similarity: config 2 (default); topk: config 3 full-candidate Jaccard + Adamic-Adar "
                          "top-k; svd: config 4 rank-64 truncated-SVD scorer; sharded: config 5 row-block "
-                         "sharded ingest + RCCL all-gather, then rank-local scoring (--config c5)")
+                         "sharded ingest + RCCL all-gather, then rank-local scoring (--config c5); e2e: "
+                         "similarity.main from graph.txt to the 6 files (--config yelp = config 1, or c2)")
     ap.add_argument("--topk", type=int, default=20)
     ap.add_argument("--svd-parity-users", type=int, default=1000, help="--mode svd: users whose top-k is checked")
     ap.add_argument("--topk-mask", type=int, default=6, help="methods of --mode topk (default Jaccard + AA)")
@@ -651,6 +747,8 @@ def main():
         return run_topk(args)
     if args.mode == "sharded":
         return run_sharded(args)
+    if args.mode == "e2e":
+        return run_e2e(args)
 
     dist = Dist()
     dev = _device(dist)

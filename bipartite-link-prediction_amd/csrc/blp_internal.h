@@ -53,14 +53,16 @@ struct DevBuf {
 // reference adds the same terms in Python set order (one rounding per add), so it agrees to a
 // few ulps; the oracle's fsum agrees bit for bit, and so do the AUCs computed from them.
 constexpr int AA_SHIFT = 58;
-constexpr double AA_WMAX = 64.0;  // custom weight tables: [0, 64) keeps W < 2^64 and the bounds above
+constexpr double AA_WMAX = 2.0;  // custom weight tables: [0, 2) keeps W < 2^59 (the scorers' 32-bit step sums of W >> 32)
 
-// S = hi * 2^32 + r as a 128-bit integer (hi64:lo64), from the two accumulator words.
+// S = hi * 2^32 + r as a 128-bit integer (hi64:lo64), from the two accumulator words. More
+// generally the high word may count units of 2^hs (hs in [32, 63]) as long as hi * 2^hs <= S and
+// S - hi * 2^hs < 2^64: the packed layout of the row-chunk scan (pairs.hip rc_scan) uses hs = 40.
 __host__ __device__ inline void aa_exact(unsigned long long lo, unsigned long long hi, unsigned long long* s_hi,
-                                         unsigned long long* s_lo) {
-  const unsigned long long a = hi << 32;  // hi * 2^32 mod 2^64; the 128-bit low word of S is lo itself
+                                         unsigned long long* s_lo, int hs = 32) {
+  const unsigned long long a = hi << hs;  // hi * 2^hs mod 2^64; the 128-bit low word of S is lo itself
   *s_lo = lo;
-  *s_hi = (hi >> 32) + (lo < a ? 1ull : 0ull);
+  *s_hi = (hi >> (64 - hs)) + (lo < a ? 1ull : 0ull);
 }
 
 // Correctly rounded (nearest-even) conversion of the 128-bit integer hi64:lo64 to double.
@@ -74,9 +76,9 @@ __host__ __device__ inline double u128_to_double(unsigned long long h, unsigned 
 }
 
 // Adamic-Adar score of one accumulator pair: S * 2^-58, correctly rounded.
-__host__ __device__ inline double aa_value(unsigned long long lo, unsigned long long hi) {
+__host__ __device__ inline double aa_value(unsigned long long lo, unsigned long long hi, int hs = 32) {
   unsigned long long sh, sl;
-  aa_exact(lo, hi, &sh, &sl);
+  aa_exact(lo, hi, &sh, &sl, hs);
   return __builtin_ldexp(u128_to_double(sh, sl), -AA_SHIFT);
 }
 

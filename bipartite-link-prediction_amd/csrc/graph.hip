@@ -182,14 +182,14 @@ int build_weight_codes(blp_graph* g, const int64_t* row_ptr, const std::vector<l
 
 // Adamic-Adar weights as integers W = w * 2^58 (blp_internal.h). Every weight the reference
 // produces, (log d)^-1 for 2 <= d < 2^31, lies in [2^-5, 2) and converts exactly; a custom table
-// must hold weights in [0, 64) (smaller weights than 2^-6 round to the 2^-58 grid once, here).
+// must hold weights in [0, 2) (smaller weights than 2^-6 round to the 2^-58 grid once, here).
 int aa_weights_fixed(const double* aaw, int64_t n, std::vector<long long>& fx) {
   const double scale = std::ldexp(1.0, AA_SHIFT);
   fx.resize((size_t)n);
   for (int64_t i = 0; i < n; ++i) {
     const double w = aaw[i];
     if (!(w >= 0.0 && w < AA_WMAX))
-      return fail(BLP_E_ARG, "blp_graph_create: aa_weight entries must lie in [0, 64) (node " + std::to_string(i) + ")");
+      return fail(BLP_E_ARG, "blp_graph_create: aa_weight entries must lie in [0, 2) (node " + std::to_string(i) + ")");
     fx[i] = (long long)(unsigned long long)std::nearbyint(w * scale);
   }
   return BLP_OK;

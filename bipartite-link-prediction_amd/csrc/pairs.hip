@@ -949,12 +949,20 @@ __device__ inline void rc_build(const int32_t* __restrict__ ci, uint32_t idmask,
   rc_loop<NT, K>(ci, s_start, s_off, s_coff, ns, tid, hint, shift, proc);
 }
 
+// Packed exact-AA layout (packed = true, one LDS chunk): per segment t, s_aa[2 t] = Σ W (wrapping)
+// and s_aa[2 t + 1] = (Σ_steps (Σ_step (W >> 32)) >> 8) << PK_CN_BITS | cn -- the high word in
+// units of 2^40 shares the count's atomic, so a step issues the same two LDS atomics as a CN +
+// 64-bit sum. Valid while cn < 2^PK_CN_BITS (a chunk holds < 2^21 nodes) : each step's high part
+// undercounts S by < 2^40 + K * 2^32, so S - hi * 2^40 < cn * 2^41 < 2^64 (blp::aa_exact, hs = 40).
+constexpr int PK_CN_BITS = 21;
+constexpr int PK_HS = 40;
+
 template <int NT, int K, bool AA>
 __device__ inline void rc_scan(const int32_t* __restrict__ ci, uint32_t idmask, int idbits,
                                const long long* __restrict__ aaw, const long long* wtab, const int64_t* s_start,
                                const int32_t* s_off, const int32_t* s_coff, int ns, int64_t c0, int64_t width,
                                const uint32_t* bm, int cap_words, uint32_t* s_cn, unsigned long long* s_aa, int tid,
-                               const int32_t* hint, int shift) {
+                               const int32_t* hint, int shift, bool packed = false) {
   const uint32_t keep = idmask | 0x80000000u, c0u = (uint32_t)c0, wu = (uint32_t)width;
   const uint32_t safe = (uint32_t)cap_words << 5;
   // Branch-free phases, so the scheduler can issue all K bitmap reads (and weight reads)
@@ -988,18 +996,30 @@ __device__ inline void rc_scan(const int32_t* __restrict__ ci, uint32_t idmask, 
     for (int k = 0; k < K; ++k) hm |= ((wd[k] >> (rr[k] & 31)) & 1u) << k;
     if (hm) {
       if (AA) {
-        unsigned long long acc = 0, acch = 0;
-        uint32_t esc = 0;
+        // the step's high words fit 32 bits: K <= 16 terms of W >> 32 < 2^27 (W < 2^59)
+        unsigned long long acc = 0;
+        uint32_t acch = 0, esc = 0;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
           const bool h = (hm >> k) & 1u;
-          aa_term(acc, acch, h ? (unsigned long long)wt[k] : 0ull);
+          const unsigned long long w = h ? (unsigned long long)wt[k] : 0ull;
+          acc += w;
+          acch += (uint32_t)(w >> 32);
           esc |= (h & ((((uint32_t)st.v[k] >> idbits) & 255u) == 0u)) ? 1u << k : 0u;
         }
         if (esc) {  // code-0 ids: the per-node weight (rare on a coded id stream)
 #pragma unroll
           for (int k = 0; k < K; ++k)
-            if ((esc >> k) & 1u) aa_term(acc, acch, (unsigned long long)aaw[st.v[k] & idmask]);
+            if ((esc >> k) & 1u) {
+              const unsigned long long w = (unsigned long long)aaw[st.v[k] & idmask];
+              acc += w;
+              acch += (uint32_t)(w >> 32);
+            }
+        }
+        if (packed) {
+          atomicAdd(&s_aa[2 * st.s], acc);
+          atomicAdd(&s_aa[2 * st.s + 1], ((unsigned long long)(acch >> (PK_HS - 32)) << PK_CN_BITS) | (unsigned)__popc(hm));
+          return;
         }
         aa_push(s_aa, st.s, acc, acch);
       }
@@ -1287,6 +1307,8 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
   const int nchunks = span <= CAP_BITS ? 1 : (int)((span + CAP_BITS - 1) / CAP_BITS);
   const bool want_j = (a.mask & BLP_JACCARD) != 0;
   const bool want_a = SAA && (a.mask & BLP_ADAMIC) != 0;
+  // packed count + high word (rc_scan): row-chunk scans of a one-chunk universe (< 2^21 nodes)
+  const bool packed = RC && want_a && nchunks == 1 && !(a.short_rows & 2) && CAP_BITS < (1 << PK_CN_BITS);
   uint4* bm4 = reinterpret_cast<uint4*>(bm);
   const int n_active = a.misc->n_active;
 
@@ -1485,7 +1507,7 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
             const int shift = build_hint<BLOCK, HC>(s_coff, ns, BLOCK, s_hint);
             if (want_a)
               rc_scan<BLOCK, K, true>(a.cw, a.idmask, a.idbits, a.aaw, s_wtab, s_start, s_off, s_coff, ns, c0, width,
-                                      bm, CAP_WORDS, s_cn, s_aa, threadIdx.x, s_hint, shift);
+                                      bm, CAP_WORDS, s_cn, s_aa, threadIdx.x, s_hint, shift, packed);
             else
               rc_scan<BLOCK, K, false>(a.cw, a.idmask, a.idbits, a.aaw, s_wtab, s_start, s_off, s_coff, ns, c0, width,
                                        bm, CAP_WORDS, s_cn, s_aa, threadIdx.x, s_hint, shift);
@@ -1511,10 +1533,12 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
           PROF(7)
           for (int t = threadIdx.x; t < ns; t += BLOCK) {  // ns <= SEG <= BLOCK: t == threadIdx.x
             const int p = pout;
-            unsigned c = s_cn[t];
+            unsigned c = packed ? (unsigned)(s_aa[2 * t + 1] & ((1u << PK_CN_BITS) - 1)) : s_cn[t];
             if (ch > 0) c += a.cn[p];
             a.cn[p] = c;
-            if (SAA && want_a) {
+            if (SAA && want_a && packed) {
+              a.aa[p] = blp::aa_value(s_aa[2 * t], s_aa[2 * t + 1] >> PK_CN_BITS, PK_HS);
+            } else if (SAA && want_a) {
               unsigned long long lo = s_aa[2 * t], hi = s_aa[2 * t + 1];
               if (ch > 0) {  // the exact words of the earlier chunks
                 lo += a.aa_part[2 * (int64_t)p];

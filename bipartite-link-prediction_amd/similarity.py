@@ -148,20 +148,31 @@ def _run_side(examples, G, methods, outfiles, table, side, sidecar=False, scored
 
 
 # ----------------------------------------------------------------------------- reference API
-def main(example_file, graph_file, u_methods, u_outfiles, b_methods, b_outfiles, *, sidecar=False):
+def main(example_file, graph_file, u_methods, u_outfiles, b_methods, b_outfiles, *, sidecar=False, timings=None):
     """similarity.main (similarity.py:11-18). ``sidecar=True`` also writes each score file's
-    binary twin ``<file>.npz`` (util.write_sidecar)."""
+    binary twin ``<file>.npz`` (util.write_sidecar). ``timings``: an optional dict that receives
+    the wall time of each phase in seconds (examples, graph, score, files)."""
+    import time
+
+    clock = time.perf_counter
+    t = clock()
     datetime.datetime.now()
     print("Loading examples...")
     examples = util.load_json(example_file)
+    t_ex = clock()
     print("Loading graph...")
     G = blp.load_edge_list(graph_file)
+    t_g = clock()
     # both passes in one concurrent device step, then the files in the reference's order
     print("Scoring user and business sides on the device...")
     present, u_scores, b_scores = score_both_sides(examples, G, method_mask(u_methods, _U_BITS) | blp.CN,
                                                    method_mask(b_methods, _B_BITS) | blp.CN)
+    t_s = clock()
     _run_side(examples, G, u_methods, u_outfiles, _U_BITS, 0, sidecar, scored=(present, u_scores))
     _run_side(examples, G, b_methods, b_outfiles, dict(_B_BITS), 1, sidecar, scored=(present, b_scores))
+    if timings is not None:
+        timings.update({"examples": t_ex - t, "graph": t_g - t_ex, "score": t_s - t_g, "files": clock() - t_s,
+                        "pairs": int(present.sum())})
 
 
 def users(examples, G, methods, outfiles, *, sidecar=False):
