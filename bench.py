@@ -657,7 +657,7 @@ def run_e2e(args):
         n = ph["pairs"]
         # the C oracle (reference algorithm) on every pair of both sides
         cpu = {}
-        nt = max(1, len(os.sched_getaffinity(0)))
+        nt = max(1, int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0)))
         for threads in (1, nt):
             t = time.perf_counter()
             ucn, ujac, uaa, _ = og.score_pairs(ex_x, ex_y, 7, nthreads=threads)
