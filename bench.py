@@ -357,7 +357,7 @@ def topk_parity(G, src, k, res, n_users=200):
     exactly, so must the Adamic-Adar lists (exact sums on both sides; their values also equal
     the pair kernel's), and |H3(u)| must equal the kernel's candidate count."""
     og, to_o, from_o = _oracle_graph(G)
-    nt = max(1, len(os.sched_getaffinity(0)))
+    nt = max(1, int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0)))
     pick = np.sort(np.random.default_rng(5).choice(len(src), min(n_users, len(src)), replace=False))
     xs_o = to_o[src[pick]]
     counts, mem = og.hop3(xs_o)

@@ -2047,9 +2047,9 @@ enum Variant { V_SMALL = 0, V_MED = 1, V_LARGE = 2 };
 // LDS bitmap words (16 / 64 / 136 KiB), threads per block, pair/row segments per chunk
 constexpr int CAP_SMALL = 4096, CAP_MED = 16384, CAP_LARGE = 33792;  // 1.08M bits: fits 160 KiB with the exact AA words
 constexpr int BLOCK_SMALL = 256, BLOCK_MED = 512, BLOCK_LARGE = 1024;
-constexpr int SEG_SMALL = 256, SEG_MED = 512, SEG_LARGE = 512;
+constexpr int SEG_SMALL = 256, SEG_MED = 384, SEG_LARGE = 512;  // MED: two 512-thread workgroups per CU (<= 80 KiB LDS)
 constexpr int G_BLOCK = 1024, G_SEG = 512;  // HBM-bitmap scorer
-constexpr int S_BLOCK = 1024, S_CAP = 16384, S_SEG = 512;  // chunk-parallel scorer: 64 KiB chunks, 2 blocks / CU
+constexpr int S_BLOCK = 1024, S_CAP = 16384, S_SEG = 448;  // chunk-parallel scorer: 64 KiB chunks, 2 blocks / CU (<= 80 KiB LDS each)
 constexpr int S_MAX_CHUNKS = 128;                          // up to 67M-node universes (config 5: 50M users)
 
 inline int variant_block(int v) { return v == V_SMALL ? BLOCK_SMALL : v == V_MED ? BLOCK_MED : BLOCK_LARGE; }

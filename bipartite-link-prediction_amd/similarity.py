@@ -32,6 +32,7 @@ import numpy as np
 
 import blp
 import util
+from blp import scorefile
 
 BUGGY_B_ADAMIC = "Beginning adamic adar coefficient computation"  # similarity.py:102
 _U_BITS = {"common_neighbors": blp.CN, "jaccard": blp.JACCARD, "adamic_adar": blp.ADAMIC}
@@ -120,6 +121,10 @@ def score_both_sides(examples, G, u_mask, b_mask):
 
     Returns (present mask over the flattened pairs, user-side scores, business-side scores)."""
     _, _, u_ids, v_ids = flatten_examples(examples)
+    return _score_both_ids(G, u_ids, v_ids, u_mask, b_mask)
+
+
+def _score_both_ids(G, u_ids, v_ids, u_mask, b_mask):
     du, pu = G.lookup(u_ids)
     dv, pv = G.lookup(v_ids)
     present = pu & pv
@@ -147,6 +152,27 @@ def _run_side(examples, G, methods, outfiles, table, side, sidecar=False, scored
     return results
 
 
+def _write_side(ex, methods, outfiles, table, present, scores):
+    """The score files of one side straight from the device arrays (util.write_json's text)."""
+    import os
+
+    pres = None if present.all() else present
+    for m, f in zip(methods, outfiles):
+        if f is None:
+            continue
+        bit = table.get(m, 0)
+        if bit == blp.CN:
+            ex.write(f, scorefile.U32, pres, scores["cn"])
+        elif bit == blp.JACCARD:
+            ex.write(f, scorefile.F64, pres, scores["jaccard"])
+        elif bit == blp.ADAMIC:
+            ex.write(f, scorefile.F64_INT0, pres, scores["adamic"])
+        else:  # a method the reference does not match: only missing-node zeros
+            ex.write(f, scorefile.NONE, pres)
+        if os.path.exists(f + ".npz"):  # as util.write_json: a stale sidecar goes
+            os.unlink(f + ".npz")
+
+
 # ----------------------------------------------------------------------------- reference API
 def main(example_file, graph_file, u_methods, u_outfiles, b_methods, b_outfiles, *, sidecar=False, timings=None):
     """similarity.main (similarity.py:11-18). ``sidecar=True`` also writes each score file's
@@ -158,18 +184,30 @@ def main(example_file, graph_file, u_methods, u_outfiles, b_methods, b_outfiles,
     t = clock()
     datetime.datetime.now()
     print("Loading examples...")
-    examples = util.load_json(example_file)
+    # examples.json of the reference's shape is read natively into flat arrays (anything else:
+    # json.loads, as util.load_json); the score files are then written natively with the same
+    # text json.dumps gives (blp/scorefile.py). With sidecar=True the dict path runs.
+    ex = None if sidecar else scorefile.Examples.load(example_file)
+    examples = util.load_json(example_file) if ex is None else None
     t_ex = clock()
     print("Loading graph...")
     G = blp.load_edge_list(graph_file)
     t_g = clock()
     # both passes in one concurrent device step, then the files in the reference's order
     print("Scoring user and business sides on the device...")
-    present, u_scores, b_scores = score_both_sides(examples, G, method_mask(u_methods, _U_BITS) | blp.CN,
-                                                   method_mask(b_methods, _B_BITS) | blp.CN)
+    masks = method_mask(u_methods, _U_BITS) | blp.CN, method_mask(b_methods, _B_BITS) | blp.CN
+    if ex is None:
+        present, u_scores, b_scores = score_both_sides(examples, G, *masks)
+    else:
+        present, u_scores, b_scores = _score_both_ids(G, ex.pair_user, ex.pair_business, *masks)
     t_s = clock()
-    _run_side(examples, G, u_methods, u_outfiles, _U_BITS, 0, sidecar, scored=(present, u_scores))
-    _run_side(examples, G, b_methods, b_outfiles, dict(_B_BITS), 1, sidecar, scored=(present, b_scores))
+    if ex is None:
+        _run_side(examples, G, u_methods, u_outfiles, _U_BITS, 0, sidecar, scored=(present, u_scores))
+        _run_side(examples, G, b_methods, b_outfiles, dict(_B_BITS), 1, sidecar, scored=(present, b_scores))
+    else:
+        _write_side(ex, u_methods, u_outfiles, _U_BITS, present, u_scores)
+        _write_side(ex, b_methods, b_outfiles, _B_BITS, present, b_scores)
+        ex.close()
     if timings is not None:
         timings.update({"examples": t_ex - t, "graph": t_g - t_ex, "score": t_s - t_g, "files": clock() - t_s,
                         "pairs": int(present.sum())})

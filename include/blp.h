@@ -101,14 +101,43 @@ int blp_edges_parse(const char* path, int c0, int c1, int64_t* a, int64_t* b, in
  * aa_weight[n_nodes]: per-node Adamic-Adar term, (log deg)^-1 for SNAP degree > 1 else 0,
  * computed by the caller with the reference's own arithmetic (similarity.py:121-125);
  * may be NULL when BLP_ADAMIC is never requested.                                        */
+/* ---- score-file I/O of similarity.main (similarity.py:11-18; util.py:12-21) ----------------
+ * blp_examples_parse: examples.json of the reference's shape -- {"user": {"business": label}},
+ *   integer-valued keys without escapes, scalar labels, no duplicate keys -- into flat arrays
+ *   (json.loads + the per-pair walk of similarity.py:22-32). Anything else is BLP_E_UNSUP: the
+ *   caller then uses json.loads, so results never depend on which path ran.
+ * blp_examples_ids: per-pair int(user key) / int(business key) (file order) and the pair
+ *   offsets of each user ([n_users + 1]); any pointer may be NULL.
+ * blp_scores_write: one score file with exactly the text json.dumps({u: {b: v}}) writes
+ *   (util.py:18-21): keys as they appear in examples.json, values in file order. present[i]
+ *   (NULL: all) marks pairs whose nodes are both in the graph; absent pairs get the int 0
+ *   (similarity.py:59-60, 104-105). values holds one entry per PRESENT pair:
+ *     BLP_SCORE_U32       uint32 counts, JSON ints (common_neighbors)
+ *     BLP_SCORE_F64       doubles in Python repr (jaccard)
+ *     BLP_SCORE_F64_INT0  doubles, 0.0 written as the int 0 (adamic_adar, similarity.py:118)
+ *     BLP_SCORE_NONE      values unused: only absent pairs are written (a method string the
+ *                         reference does not match, e.g. the b_adamic bug, similarity.py:102) */
+typedef struct blp_examples blp_examples;
+#define BLP_SCORE_U32 0
+#define BLP_SCORE_F64 1
+#define BLP_SCORE_F64_INT0 2
+#define BLP_SCORE_NONE 3
+int blp_examples_parse(const char* path, blp_examples** out);
+int blp_examples_info(const blp_examples* e, int64_t* n_users, int64_t* n_pairs);
+int blp_examples_ids(const blp_examples* e, int64_t* pair_user, int64_t* pair_business, int64_t* user_off);
+int blp_examples_destroy(blp_examples* e);
+int blp_scores_write(const blp_examples* e, const char* path, int kind, const uint8_t* present, const void* values,
+                     int64_t n_values);
+
 int blp_graph_create(const int64_t* row_ptr, const int32_t* col_idx, int64_t n_nodes,
                      const double* aa_weight, int device, blp_graph** out);
 int blp_graph_destroy(blp_graph* g);
 int blp_graph_info(const blp_graph* g, int64_t* n_nodes, int64_t* nnz, int* device);
 int blp_graph_sync(blp_graph* g); /* wait for all work queued on the handle's stream */
-/* Fixed-point scale of the Adamic-Adar sums: terms are llrint(w * 2^shift), summed exactly
- * in 64-bit integers. shift = 40 unless the graph's bound (max row length x max weight)
- * could overflow a 64-bit sum, in which case blp_graph_create lowers it (overflow guard). */
+/* Fixed-point scale of the Adamic-Adar terms: W = w * 2^shift with shift = 58, exact for every
+ * weight the reference produces ((log d)^-1 in [2^-5, 2)); a pair's sum is carried exactly in
+ * two 64-bit words and rounded once to the nearest double, i.e. the correctly rounded sum of
+ * the reference's terms (math.fsum). aa_weight entries must lie in [0, 2) (else BLP_E_ARG).   */
 int blp_graph_aa_shift(const blp_graph* g, int* shift);
 
 /* ---------------------------------------------------------------- pair scoring

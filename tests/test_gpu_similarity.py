@@ -27,6 +27,22 @@ def test_main_writes_reference_files(gpu, case, tmp_path):
         assert_same_scores(load(str(tmp_path / f)), golden(case, f), m)
 
 
+@pytest.mark.parametrize("case", SIM_CASES)
+def test_main_native_files_equal_dict_path(gpu, case, tmp_path):
+    """similarity.main's native path (examples parsed into arrays, files written by
+    blp_scores_write) produces byte-identical files to the dict + json.dumps path (which
+    sidecar=True selects), including missing-node zeros and the b_adamic bug file."""
+    d = os.path.join(GOLDEN, case)
+    out = {}
+    for mode in ("native", "dict"):
+        uf = [str(tmp_path / (mode + f)) for f in U_FILES]
+        bf = [str(tmp_path / (mode + f)) for f in B_FILES]
+        similarity.main(os.path.join(d, "examples.json"), os.path.join(d, "graph.txt"), METHODS, uf, METHODS, bf,
+                        sidecar=(mode == "dict"))
+        out[mode] = [open(f).read() for f in uf + bf]
+    assert out["native"] == out["dict"]
+
+
 def _check_against_oracle(ga, gb, x, y, mask=7):
     """Device scores of dense-id pairs vs the C oracle on the same edge list."""
     G = blp.DeviceGraph(ga, gb)
