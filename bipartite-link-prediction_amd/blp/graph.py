@@ -110,6 +110,16 @@ class HostGraph:
         ids = np.asarray(ids, dtype=np.int64)
         if self.n == 0:
             return np.full(len(ids), -1, np.int32), np.zeros(len(ids), bool)
+        lo, span = int(self._sorted_ids[0]), int(self._sorted_ids[-1]) - int(self._sorted_ids[0]) + 1
+        if span <= max(4 * self.n, 1 << 20):  # compact id space: one direct table gather
+            tab = getattr(self, "_direct", None)
+            if tab is None:
+                tab = self._direct = np.full(span, -1, np.int32)
+                tab[self._sorted_ids - lo] = self._sort
+            off = ids - lo
+            ok = (off >= 0) & (off < span)
+            dense = np.where(ok, tab[np.where(ok, off, 0)], -1).astype(np.int32)
+            return dense, dense >= 0
         pos = np.searchsorted(self._sorted_ids, ids)
         pos = np.minimum(pos, self.n - 1)
         present = self._sorted_ids[pos] == ids
