@@ -1197,6 +1197,44 @@ __global__ __launch_bounds__(BLOCK) void k_heavy(HeavyArgs h) {
   }
 }
 
+// ------------------------------------------------------------------ source records
+// Everything the short-row scorer needs about an active source before its first global read of
+// row data, gathered once per step after grouping: one 64-byte record per active source (read
+// with scalar loads) instead of the dependent chain active[s] -> off / cnt / rp / wp / heavy ->
+// ci[rp] (three round trips per source on the latency-bound business side).
+struct SrcRec {
+  int32_t x, pbeg, pcnt, hslot;
+  int64_t xb, xe;  // N(x) = ci[xb, xe)
+  int64_t wb, we;  // wedge row of x, in 16-byte vectors (wb == we: none)
+  int32_t nx_lo, nx_hi;  // first and last id of N(x) (nx_hi < nx_lo: empty)
+  int32_t pad[2];
+};
+static_assert(sizeof(SrcRec) == 64, "one 64-byte record per source");
+
+__global__ void k_source_records(const int32_t* __restrict__ active, const Misc* __restrict__ misc,
+                                 const int32_t* __restrict__ off, const int32_t* __restrict__ cnt,
+                                 const int64_t* __restrict__ rp, const int32_t* __restrict__ ci,
+                                 const int32_t* __restrict__ heavy_slot, const int64_t* __restrict__ wp,
+                                 SrcRec* __restrict__ rec) {
+  const int na = misc->n_active;
+  for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < na; s += gridDim.x * blockDim.x) {
+    const int x = active[s];
+    SrcRec r;
+    r.x = x;
+    r.pbeg = off[x];
+    r.pcnt = cnt[x];
+    r.hslot = heavy_slot ? heavy_slot[x] : -1;
+    r.xb = rp[x];
+    r.xe = rp[x + 1];
+    r.wb = wp ? wp[x] : 0;
+    r.we = wp ? wp[x + 1] : 0;
+    r.nx_lo = r.xe > r.xb ? ci[r.xb] : 0;
+    r.nx_hi = r.xe > r.xb ? ci[r.xe - 1] : -1;
+    r.pad[0] = r.pad[1] = 0;
+    rec[s] = r;
+  }
+}
+
 // ------------------------------------------------------------------ scorer
 struct ScoreArgs {
   const int64_t* rp;
@@ -1230,6 +1268,7 @@ struct ScoreArgs {
   const int64_t* wp;    // wedge rows (wedge.hip; short-row scorer only, null: build from CSR)
   const uint4* wedge;
   unsigned long long* aa_part;  // [2 n_pairs] exact AA words carried between LDS chunks (k_score, chunks > 1)
+  const SrcRec* rec;            // per active source (short-row scorer; null: gather from active[])
 };
 
 template <int BLOCK>
@@ -1327,12 +1366,37 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
     PROF(0)
     const int s_last = min(n_active, s_first + a.dq);
     for (int s = s_first; s < s_last; ++s) {
-      const int x = a.active[s];
-      const int pbeg = a.off[x], pcnt = a.cnt[x];
-      const int64_t xb = a.rp[x], xe = a.rp[x + 1];
-      const int hslot = a.heavy_slot ? a.heavy_slot[x] : -1;
-      // value range of N(x) (rows are sorted): distance-1 removal is skipped when disjoint
-      const int64_t nx_lo = xe > xb ? a.ci[xb] : 0, nx_hi = xe > xb ? a.ci[xe - 1] : -1;
+      int x, pbeg, pcnt, hslot;
+      int64_t xb, xe, wb = 0, we = 0, nx_lo, nx_hi;
+      if constexpr (SHORT) {  // one record per source (s is uniform)
+        // uniform: kept in scalar registers (the VGPR budget of 7 workgroups per CU is tight)
+        const SrcRec& r = a.rec[__builtin_amdgcn_readfirstlane(s)];
+        auto u32 = [](int32_t v) { return (int32_t)__builtin_amdgcn_readfirstlane(v); };
+        auto u64 = [](int64_t v) {
+          return (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(v >> 32)) << 32) |
+                           (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)v));
+        };
+        x = u32(r.x);
+        pbeg = u32(r.pbeg);
+        pcnt = u32(r.pcnt);
+        hslot = u32(r.hslot);
+        xb = u64(r.xb);
+        xe = u64(r.xe);
+        wb = u64(r.wb);
+        we = u64(r.we);
+        nx_lo = u32(r.nx_lo);
+        nx_hi = u32(r.nx_hi);
+      } else {
+        x = a.active[s];
+        pbeg = a.off[x];
+        pcnt = a.cnt[x];
+        xb = a.rp[x];
+        xe = a.rp[x + 1];
+        hslot = a.heavy_slot ? a.heavy_slot[x] : -1;
+        // value range of N(x) (rows are sorted): distance-1 removal is skipped when disjoint
+        nx_lo = xe > xb ? a.ci[xb] : 0;
+        nx_hi = xe > xb ? a.ci[xe - 1] : -1;
+      }
       unsigned long long h2 = 0;
       PROF(1)
 
@@ -1415,7 +1479,6 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
           if (SHORT && a.wp) {
             // N(N(x)) from x's wedge row: one contiguous range, two 16-byte vectors per thread
             // in flight, no row_ptr round trip and no idle lanes beside long rows
-            const int64_t wb = a.wp[x], we = a.wp[x + 1];
             const uint32_t keep = a.idmask | 0x80000000u, c0u = (uint32_t)c0, wu = (uint32_t)width;
             for (int64_t q = wb + threadIdx.x; q < we; q += 2 * BLOCK) {
               const uint4 v0 = a.wedge[q];
@@ -2105,10 +2168,17 @@ struct blp_batch {
   hipStream_t stream = nullptr;
   blp::DevBuf cnt, off, active, scratch;
   int cus = 0;  // CUs the persistent block scorer may occupy (0: all; set by blp_batches_score)
+  SrcRec* d_rec = nullptr;  // [n_sources] source records of the short-row scorer (or null)
   int64_t work_elems = 0;  // planned build + scan elements (co-scheduling estimate)
 };
 
 using namespace blp;
+
+// the short-row scorer (k_score<..., SHORT = true>) takes the batch
+static bool short_kernel(const blp_batch* b) {
+  return b->variant == V_SMALL && b->short_rows == 3 && !b->wave && !b->global && !b->split &&
+         !getenv("BLP_NO_SHORT_KERNEL");
+}
 
 // elements per thread per merge-path step (template; BLP_KPT=4|8|16 selects another build)
 static int kpt_choice() {
@@ -2397,6 +2467,9 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
     return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: hipMalloc failed"));
   if (b->chunks > 1 && hipMalloc(&b->d_aa_part, 16 * np) != hipSuccess)
     return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: hipMalloc failed"));
+  if (short_kernel(b) &&
+      hipMalloc(&b->d_rec, sizeof(SrcRec) * (size_t)std::max<int64_t>(b->n_sources, 1)) != hipSuccess)
+    return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: hipMalloc failed"));
   if (n_pairs) {
     if (hipMemcpy(b->d_x, x, 4 * n_pairs, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(b->d_y, y, 4 * n_pairs, hipMemcpyHostToDevice) != hipSuccess)
@@ -2429,7 +2502,7 @@ int blp_batch_destroy(blp_batch* b) {
   b->scratch.release();
   if (b->stream) (void)hipStreamDestroy(b->stream);
   void* ps[] = {b->d_x,    b->d_y,    b->d_cn,   b->d_jac,  b->d_aa,          b->d_gout,        b->d_gyb,
-                b->d_gyl,  b->d_misc, b->d_heavy_slot, b->d_heavy_bm, b->d_heavy_items, b->d_gbm, b->d_gy, b->d_rsplit, b->d_pcn, b->d_paa, b->d_ph2, b->d_aa_part};
+                b->d_gyl,  b->d_misc, b->d_heavy_slot, b->d_heavy_bm, b->d_heavy_items, b->d_gbm, b->d_gy, b->d_rsplit, b->d_pcn, b->d_paa, b->d_ph2, b->d_aa_part, b->d_rec};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   delete b;
@@ -2559,6 +2632,7 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   a.ci = g->d_ci;
   a.aaw = g->d_aaw_fx;
   a.aa_part = b->d_aa_part;
+  a.rec = nullptr;
   const bool coded = g->d_ci_w && !getenv("BLP_NO_WCODES");  // tuning knob
   a.cw = coded ? g->d_ci_w : g->d_ci;
   a.idbits = coded ? g->id_bits : 31;
@@ -2612,12 +2686,19 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
     else
       hipLaunchKernelGGL((k_score_wave<W_WAVES, W_CAP, 8>), grid, block, 0, b->stream, a);
     BLP_HIP(hipGetLastError());
-  } else if (np && b->variant == V_SMALL && b->short_rows == 3 && !getenv("BLP_NO_SHORT_KERNEL")) {
+  } else if (np && short_kernel(b)) {
     // bitmap in dynamic LDS, sized to the universe (whole 16-byte vectors)
     const size_t dyn = 4 * (size_t)std::max<int64_t>(4, ((b->hi - b->lo + 31) / 32 + 3) / 4 * 4);
     if (g->d_wp && !getenv("BLP_NO_WEDGE")) {  // tuning knob: BLP_NO_WEDGE builds from CSR
       a.wp = g->d_wp;
       a.wedge = reinterpret_cast<const uint4*>(g->d_wedge);
+    }
+    if (b->d_rec) {  // one record per active source (after grouping, on the batch stream)
+      hipLaunchKernelGGL(k_source_records, dim3((unsigned)std::min<int64_t>((b->n_sources + 255) / 256, 2048)),
+                         dim3(256), 0, b->stream, a.active, b->d_misc, a.off, a.cnt, g->d_rp, g->d_ci, b->d_heavy_slot,
+                         a.wp, b->d_rec);
+      BLP_HIP(hipGetLastError());
+      a.rec = b->d_rec;
     }
     if ((rc = (mask & BLP_ADAMIC) ? launch_short<true>(g, b, a, dyn) : launch_short<false>(g, b, a, dyn))) return rc;
   } else if (np) {
