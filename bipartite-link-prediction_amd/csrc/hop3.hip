@@ -77,6 +77,80 @@ __device__ inline void phase_sync() {
   __syncthreads();
 }
 
+// Emission of one source's candidates (after the exact distance-3 marks are final in bm3):
+// positives first, in the caller's order, cleared from the marks; then the sampled negatives,
+// each thread a contiguous word range so the ids come out ascending.
+template <bool G, int NT>
+__device__ inline void emit(const Hop3Args& a, int it, int x, uint32_t* bm3, int w3, int64_t span3, unsigned* s_warp,
+                            unsigned long long* s_base_p) {
+  unsigned long long& s_base = *s_base_p;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  // positives first (caller order), cleared from the candidate marks
+  const int pb = a.pos_off[it], pe = a.pos_off[it + 1];
+  if (threadIdx.x == 0) {
+    for (int k = pb; k < pe; ++k) {
+      const int64_t r = (int64_t)a.pos_y[k] - a.lo3;
+      if (r >= 0 && r < span3 && bit_test(bm3, r)) {
+        bm3[r >> 5] &= ~(1u << (r & 31));
+        const unsigned long long o = atomicAdd(&a.counters[1], 1ull);
+        if ((int64_t)o < a.cap) {
+          a.out_x[o] = x;
+          a.out_y[o] = a.pos_y[k];
+          a.out_label[o] = 1;
+        }
+      }
+    }
+  }
+  phase_sync<G>();
+  // sampled negatives: per-thread contiguous word ranges keep ascending id order
+  const int per = (w3 + NT - 1) / NT;
+  const int w_beg = min(w3, (int)threadIdx.x * per), w_end = min(w3, w_beg + per);
+  unsigned mine = 0;
+  for (int wi = w_beg; wi < w_end; ++wi) {
+    uint32_t bits = bm3[wi];
+    while (bits) {
+      const int t = __ffs(bits) - 1;
+      bits &= bits - 1;
+      if (keep_negative(a.seed, x, (int)(a.lo3 + (int64_t)wi * 32 + t), a.rate)) ++mine;
+    }
+  }
+  // block exclusive scan of the per-thread counts
+  unsigned inc = mine;
+  for (int d = 1; d < 64; d <<= 1) {
+    const unsigned t = __shfl_up(inc, d, 64);
+    if (lane >= d) inc += t;
+  }
+  if (lane == 63) s_warp[wid] = inc;
+  phase_sync<G>();
+  if (threadIdx.x == 0) {
+    unsigned run = 0;
+    for (int w = 0; w < NT / 64; ++w) {
+      const unsigned t = s_warp[w];
+      s_warp[w] = run;
+      run += t;
+    }
+    s_base = atomicAdd(&a.counters[1], (unsigned long long)run);
+  }
+  phase_sync<G>();
+  unsigned long long o = s_base + s_warp[wid] + inc - mine;
+  for (int wi = w_beg; wi < w_end; ++wi) {
+    uint32_t bits = bm3[wi];
+    while (bits) {
+      const int t = __ffs(bits) - 1;
+      bits &= bits - 1;
+      const int b = (int)(a.lo3 + (int64_t)wi * 32 + t);
+      if (keep_negative(a.seed, x, b, a.rate)) {
+        if ((int64_t)o < a.cap) {
+          a.out_x[o] = x;
+          a.out_y[o] = b;
+          a.out_label[o] = 0;
+        }
+        ++o;
+      }
+    }
+  }
+}
+
 template <bool G>
 __global__ __launch_bounds__(H_BLOCK) void k_hop3(Hop3Args a, uint32_t* gbm, int64_t gwords) {
   uint32_t* lds;
@@ -143,71 +217,115 @@ __global__ __launch_bounds__(H_BLOCK) void k_hop3(Hop3Args a, uint32_t* gbm, int
         if (bit_test(bm2, v - a.lo2)) bit_and<G>(&bm3[(v - a.lo3) >> 5], ~(1u << ((v - a.lo3) & 31)));
     }
     phase_sync<G>();
-    // positives first (caller order), cleared from the candidate marks
-    const int pb = a.pos_off[it], pe = a.pos_off[it + 1];
-    if (threadIdx.x == 0) {
-      for (int k = pb; k < pe; ++k) {
-        const int64_t r = (int64_t)a.pos_y[k] - a.lo3;
-        if (r >= 0 && r < span3 && bit_test(bm3, r)) {
-          bm3[r >> 5] &= ~(1u << (r & 31));
-          const unsigned long long o = atomicAdd(&a.counters[1], 1ull);
-          if ((int64_t)o < a.cap) {
-            a.out_x[o] = x;
-            a.out_y[o] = a.pos_y[k];
-            a.out_label[o] = 1;
+    emit<G, H_BLOCK>(a, it, x, bm3, w3, span3, s_warp, &s_base);
+    phase_sync<G>();
+  }
+}
+
+// Wedge-row variant (bipartite review graphs; the graph's wedge index, wedge.hip): for a user
+// x, N(N(N(x))) = the union over b in N(x) of b's wedge row (the rows N(z), z in N(b), stored
+// back to back), so the distance-3 marks come from contiguous 16-byte vectors -- no H2 bitmap,
+// no per-member row_ptr gathers and no one-id-per-load row walks (the row walk of k_hop3 moved
+// 2-4x its algorithmic bytes). Exact distance 3 = marks minus N(x): x and every distance-2 node
+// lie in N(N(x)), whose id range the host checked to be disjoint from the marks' range.
+// Work items are chunks of HW_CH vectors of one wedge row, one wave each, four vectors per lane
+// in flight; the mark bitmap is dynamic LDS sized to the target range.
+constexpr int HW_BLOCK = 1024;
+constexpr int HW_SEG = 1024;  // N(x) entries per batch
+constexpr int HW_CH = 1024;   // wedge vectors per work item
+extern __shared__ uint32_t hw_dyn[];
+
+__device__ inline int hw_exscan(int v, int* red, int* total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int inc = v;
+  for (int d = 1; d < 64; d <<= 1) {
+    const int t = __shfl_up(inc, d, 64);
+    if (lane >= d) inc += t;
+  }
+  if (lane == 63) red[wid] = inc;
+  __syncthreads();
+  int base = 0, tot = 0;
+  for (int w = 0; w < HW_BLOCK / 64; ++w) {
+    base += w < wid ? red[w] : 0;
+    tot += red[w];
+  }
+  __syncthreads();
+  *total = tot;
+  return base + inc - v;
+}
+
+__global__ __launch_bounds__(HW_BLOCK) void k_hop3_wedge(Hop3Args a, const int64_t* __restrict__ wp,
+                                                         const uint4* __restrict__ wedge) {
+  __shared__ int64_t s_ws[HW_SEG];
+  __shared__ int32_t s_wl[HW_SEG];
+  __shared__ int32_t s_co[HW_SEG + 1];
+  __shared__ int red[HW_BLOCK / 64];
+  __shared__ int s_item;
+  __shared__ unsigned s_warp[HW_BLOCK / 64];
+  __shared__ unsigned long long s_base;
+  uint32_t* bm3 = hw_dyn;
+  const int64_t span3 = a.hi3 - a.lo3;
+  const int w3 = (int)((span3 + 31) >> 5);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const uint32_t c0u = (uint32_t)a.lo3, wu = (uint32_t)span3;
+  for (;;) {
+    if (threadIdx.x == 0) s_item = (int)atomicAdd(&a.counters[0], 1ull);
+    __syncthreads();
+    const int it = s_item;
+    if (it >= a.n_src) break;
+    const int x = a.src[it];
+    for (int i = threadIdx.x; i < w3; i += HW_BLOCK) bm3[i] = 0;
+    const int64_t xb = a.rp[x], xe = a.rp[x + 1];
+    __syncthreads();
+    for (int64_t k0 = xb; k0 < xe; k0 += HW_SEG) {
+      const int ns = (int)min<int64_t>(HW_SEG, xe - k0);
+      int nch = 0;
+      if ((int)threadIdx.x < ns) {
+        const int b = a.ci[k0 + threadIdx.x];
+        const int64_t ws = wp[b], we = wp[b + 1];
+        s_ws[threadIdx.x] = ws;
+        s_wl[threadIdx.x] = (int)(we - ws);
+        nch = (int)((we - ws + HW_CH - 1) / HW_CH);
+      }
+      int tot;
+      const int ex = hw_exscan(nch, red, &tot);
+      if ((int)threadIdx.x < ns) s_co[threadIdx.x] = ex;
+      if (threadIdx.x == 0) s_co[ns] = tot;
+      __syncthreads();
+      for (int item = wid; item < tot; item += HW_BLOCK / 64) {
+        int lo = 0, hi = ns;  // the row of this item: last lo with s_co[lo] <= item
+        while (hi - lo > 1) {
+          const int mid = (lo + hi) >> 1;
+          if (s_co[mid] <= item) lo = mid; else hi = mid;
+        }
+        const int64_t row_end = s_ws[lo] + s_wl[lo];
+        const int64_t base = s_ws[lo] + (int64_t)(item - s_co[lo]) * HW_CH;
+        const int64_t end = min(base + HW_CH, row_end);
+        for (int64_t q = base + lane; q < end; q += 4 * 64) {
+          uint4 v[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) v[u] = wedge[q + 64 * u < end ? q + 64 * u : q];  // a repeat ORs nothing new
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const uint32_t ids[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+              const uint32_t r = ids[c] - c0u;
+              if (r < wu) atomicOr(&bm3[r >> 5], 1u << (r & 31));
+            }
           }
         }
       }
+      __syncthreads();
     }
-    phase_sync<G>();
-    // sampled negatives: per-thread contiguous word ranges keep ascending id order
-    const int per = (w3 + H_BLOCK - 1) / H_BLOCK;
-    const int w_beg = min(w3, (int)threadIdx.x * per), w_end = min(w3, w_beg + per);
-    unsigned mine = 0;
-    for (int wi = w_beg; wi < w_end; ++wi) {
-      uint32_t bits = bm3[wi];
-      while (bits) {
-        const int t = __ffs(bits) - 1;
-        bits &= bits - 1;
-        if (keep_negative(a.seed, x, (int)(a.lo3 + (int64_t)wi * 32 + t), a.rate)) ++mine;
-      }
+    // exact distance 3: drop N(x) (distance 1); x and H2(x) lie outside [lo3, hi3)
+    for (int64_t k = xb + threadIdx.x; k < xe; k += HW_BLOCK) {
+      const uint32_t r = (uint32_t)a.ci[k] - c0u;
+      if (r < wu) atomicAnd(&bm3[r >> 5], ~(1u << (r & 31)));
     }
-    // block exclusive scan of the per-thread counts
-    unsigned inc = mine;
-    for (int d = 1; d < 64; d <<= 1) {
-      const unsigned t = __shfl_up(inc, d, 64);
-      if (lane >= d) inc += t;
-    }
-    if (lane == 63) s_warp[wid] = inc;
-    phase_sync<G>();
-    if (threadIdx.x == 0) {
-      unsigned run = 0;
-      for (int w = 0; w < H_BLOCK / 64; ++w) {
-        const unsigned t = s_warp[w];
-        s_warp[w] = run;
-        run += t;
-      }
-      s_base = atomicAdd(&a.counters[1], (unsigned long long)run);
-    }
-    phase_sync<G>();
-    unsigned long long o = s_base + s_warp[wid] + inc - mine;
-    for (int wi = w_beg; wi < w_end; ++wi) {
-      uint32_t bits = bm3[wi];
-      while (bits) {
-        const int t = __ffs(bits) - 1;
-        bits &= bits - 1;
-        const int b = (int)(a.lo3 + (int64_t)wi * 32 + t);
-        if (keep_negative(a.seed, x, b, a.rate)) {
-          if ((int64_t)o < a.cap) {
-            a.out_x[o] = x;
-            a.out_y[o] = b;
-            a.out_label[o] = 0;
-          }
-          ++o;
-        }
-      }
-    }
-    phase_sync<G>();
+    __syncthreads();
+    emit<false, HW_BLOCK>(a, it, x, bm3, w3, span3, s_warp, &s_base);
+    __syncthreads();
   }
 }
 
@@ -247,6 +365,15 @@ extern "C" int blp_hop3_sample(blp_graph* g, const int32_t* src, int64_t n_src, 
   if (lo3 > hi3) lo3 = hi3 = 0;
   const int64_t w2 = (((hi2 - lo2) + 31) / 32 + 3) / 4 * 4, w3 = ((hi3 - lo3) + 31) / 32;
   const bool global = w2 + w3 > H_WORDS || getenv("BLP_HOP3_FORCE_GLOBAL");
+  // wedge-row path: every target range disjoint from N(N(x))'s, every b in N(x) holding a
+  // wedge row (or no members), and the mark bitmap within LDS (BLP_HOP3_NO_WEDGE: off)
+  bool wedge = g->d_wp && !getenv("BLP_HOP3_NO_WEDGE") && (hi2 <= lo3 || hi3 <= lo2) &&
+               (size_t)4 * w3 + 20480 <= 160 * 1024;
+  for (int64_t i = 0; wedge && i < n_src; ++i)
+    for (int64_t k = rp[src[i]]; k < rp[src[i] + 1] && wedge; ++k) {
+      const int32_t b = ci[k];
+      wedge = g->h_wp[b + 1] > g->h_wp[b] || rp[b + 1] == rp[b];
+    }
   const int64_t gwords = (w2 + w3 + 3) / 4 * 4;
   for (int64_t i = 0; i < (n_src ? pos_off[n_src] : 0); ++i)
     BLP_CHECK(pos_y[i] >= 0 && pos_y[i] < n, BLP_E_ARG, "blp_hop3_sample: positive id out of range");
@@ -275,7 +402,8 @@ extern "C" int blp_hop3_sample(blp_graph* g, const int32_t* src, int64_t n_src, 
   if ((rc = hip(hipMalloc(&d_x, 4 * dcap), "hipMalloc"))) return rc;
   if ((rc = hip(hipMalloc(&d_y, 4 * dcap), "hipMalloc"))) return rc;
   if ((rc = hip(hipMalloc(&d_l, dcap), "hipMalloc"))) return rc;
-  if (global && (rc = hip(hipMalloc(&d_gbm, 4 * (size_t)gwords * g->n_cu), "hipMalloc (HBM bitmaps)"))) return rc;
+  if (global && !wedge && (rc = hip(hipMalloc(&d_gbm, 4 * (size_t)gwords * g->n_cu), "hipMalloc (HBM bitmaps)")))
+    return rc;
   if (n_src) {
     if ((rc = hip(hipMemcpy(d_src, src, 4 * n_src, hipMemcpyHostToDevice), "hipMemcpy"))) return rc;
     if ((rc = hip(hipMemcpy(d_off, pos_off, 4 * (n_src + 1), hipMemcpyHostToDevice), "hipMemcpy"))) return rc;
@@ -302,7 +430,15 @@ extern "C" int blp_hop3_sample(blp_graph* g, const int32_t* src, int64_t n_src, 
   a.counters = (unsigned long long*)d_cnt;
   hipEvent_t t0;
   if ((rc = timer_begin(g, K_HOP3, &t0))) return cleanup(), rc;
-  if (n_src) {
+  if (n_src && wedge) {
+    const size_t dyn = 4 * (size_t)std::max<int64_t>(w3, 1);
+    int per_cu = 1;
+    if ((rc = hip(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_hop3_wedge, HW_BLOCK, dyn), "occupancy")))
+      return rc;
+    hipLaunchKernelGGL(k_hop3_wedge, dim3(g->n_cu * std::max(per_cu, 1)), dim3(HW_BLOCK), dyn, g->stream, a,
+                       (const int64_t*)g->d_wp, (const uint4*)g->d_wedge);
+    if ((rc = hip(hipGetLastError(), "k_hop3_wedge launch"))) return rc;
+  } else if (n_src) {
     if (global)
       hipLaunchKernelGGL(k_hop3<true>, dim3(g->n_cu), dim3(H_BLOCK), 0, g->stream, a, (uint32_t*)d_gbm, gwords);
     else

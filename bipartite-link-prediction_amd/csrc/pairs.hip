@@ -908,11 +908,33 @@ __device__ inline void rc_fetch(const int32_t* __restrict__ ci, const int64_t* s
 }
 
 // Two-buffer driver: steps of NT chunks; proc(step) after the next step's loads are issued.
+// BLP_RC3: three buffers, two steps of loads in flight while one is processed.
+#ifndef BLP_RC3
+#define BLP_RC3 0
+#endif
 template <int NT, int K, typename Proc>
 __device__ inline void rc_loop(const int32_t* __restrict__ ci, const int64_t* s_start, const int32_t* s_off,
                                const int32_t* s_coff, int ns, int tid, const int32_t* hint, int shift, Proc proc) {
   const int TC = s_coff[ns];
   const int nsteps = (TC + NT - 1) / NT;
+#if BLP_RC3
+  RCStep<K> A, B, C;
+  vm_drain();
+  rc_fetch<K>(ci, s_start, s_off, s_coff, ns, TC, tid, hint, shift, A);
+  rc_fetch<K>(ci, s_start, s_off, s_coff, ns, TC, NT + tid, hint, shift, B);  // may be past TC
+  int i = 0;
+  for (; i + 2 < nsteps; i += 3) {
+    rc_fetch<K>(ci, s_start, s_off, s_coff, ns, TC, (i + 2) * NT + tid, hint, shift, C);
+    proc(A);
+    rc_fetch<K>(ci, s_start, s_off, s_coff, ns, TC, (i + 3) * NT + tid, hint, shift, A);
+    proc(B);
+    rc_fetch<K>(ci, s_start, s_off, s_coff, ns, TC, (i + 4) * NT + tid, hint, shift, B);
+    proc(C);
+  }
+  if (i < nsteps) proc(A);
+  if (i + 1 < nsteps) proc(B);
+  vm_drain();
+#else
   RCStep<K> A, B;
   vm_drain();
   rc_fetch<K>(ci, s_start, s_off, s_coff, ns, TC, tid, hint, shift, A);
@@ -924,6 +946,7 @@ __device__ inline void rc_loop(const int32_t* __restrict__ ci, const int64_t* s_
   }
   if (nsteps & 1) proc(A);
   vm_drain();
+#endif
 }
 
 // LDS bitmap layout for the row-chunk loops: CAP words of bits, then RC_SAFE: one word that

@@ -38,9 +38,13 @@ def test_hop3_matches_reference_fixture(gpu):
         assert got[u] == {b: l for b, l in ex[u].items()}
 
 
-@pytest.mark.parametrize("seed,hbm", [(0, False), (1, False), (0, True)])
-def test_hop3_sets_vs_oracle(gpu, seed, hbm, monkeypatch):
-    if hbm:  # the HBM-bitmap variant (universes wider than LDS: configs 4/5)
+@pytest.mark.parametrize("seed,mode", [(0, "wedge"), (1, "wedge"), (0, "lds"), (1, "lds"), (0, "hbm")])
+def test_hop3_sets_vs_oracle(gpu, seed, mode, monkeypatch):
+    """wedge: marks from the graph's wedge rows (default on review graphs); lds: H2 bitmap then
+    N(H2) row walks in LDS; hbm: the same in per-workgroup HBM bitmaps (configs 4/5)."""
+    if mode != "wedge":
+        monkeypatch.setenv("BLP_HOP3_NO_WEDGE", "1")
+    if mode == "hbm":
         monkeypatch.setenv("BLP_HOP3_FORCE_GLOBAL", "1")
     rng = np.random.default_rng(seed)
     a, b = bipartite_edges(rng, 40000, 3000, 250000)
@@ -115,3 +119,26 @@ def test_dataset_maker_drop_in_matches_reference(gpu, tmp_path):
     ref = load(os.path.join(d, "examples.json"))
     assert {u: v for u, v in ref.items() if v} == got
     assert json.loads((tmp_path / "examples.json").read_text()) == got
+
+
+@pytest.mark.parametrize("long_rows", [False, True])
+def test_hop3_wedge_and_row_walk_agree(gpu, long_rows, monkeypatch):
+    """The wedge-row path and the row-walk path emit identical (x, y, label) lists, positives
+    and sampled negatives included. With users of > 32 reviews some businesses have no wedge
+    row and the launch falls back to the row walk (same output either way)."""
+    rng = np.random.default_rng(11)
+    a, b = bipartite_edges(rng, 30000, 2000, 200000)
+    if long_rows:  # a few heavy users: their businesses get no wedge row
+        heavy = rng.choice(30000, 20, replace=False)
+        a = np.concatenate([a, np.repeat(heavy, 60)])
+        b = np.concatenate([b, 30000 + rng.integers(0, 2000, 20 * 60)])
+    G = blp.DeviceGraph(a, b)
+    nu = G.n - len(np.unique(b))
+    src = np.sort(rng.choice(nu, 120, replace=False)).astype(np.int32)
+    pos_off = np.arange(0, 2 * len(src) + 1, 2, dtype=np.int32)
+    pos_y = rng.integers(nu, G.n, 2 * len(src)).astype(np.int32)
+    got = G.hop3_sample(src, pos_off, pos_y, rate=0.05, seed=4)
+    monkeypatch.setenv("BLP_HOP3_NO_WEDGE", "1")
+    ref = G.hop3_sample(src, pos_off, pos_y, rate=0.05, seed=4)
+    for p, q in zip(got, ref):
+        np.testing.assert_array_equal(p, q)
