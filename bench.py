@@ -127,7 +127,7 @@ def cpu_baseline(og, ex_x, ex_y, target_s=15.0):
                       (pu, su, tu, ru, pb, sb, tb, rb)}
 
 
-def oracle_full(og, ex_x, ex_y):
+def oracle_full(og, ex_x, ex_y, b_mask=3):
     """Every pair of the step scored by the C oracle on all of this host's cores (OpenMP,
     dynamic per source): the full-workload parity reference AND the multicore CPU baseline
     (SURVEY.md §8(d)(ii)). Same arithmetic as similarity.py:108-126."""
@@ -136,9 +136,11 @@ def oracle_full(og, ex_x, ex_y):
     ucn, ujac, uaa, _ = og.score_pairs(ex_x, ex_y, 7, nthreads=nt)
     tu = time.perf_counter() - t0
     t0 = time.perf_counter()
-    bcn, bjac, _, _ = og.score_pairs(ex_y, ex_x, 3, nthreads=nt)
+    bcn, bjac, baa, _ = og.score_pairs(ex_y, ex_x, b_mask, nthreads=nt)
     tb = time.perf_counter() - t0
     res = {"user": {"cn": ucn, "jaccard": ujac, "adamic": uaa}, "business": {"cn": bcn, "jaccard": bjac}}
+    if b_mask & 4:
+        res["business"]["adamic"] = baa
     multi = {"value": len(ex_x) / (tu + tb), "unit": "pairs/s", "cores": nt, "kind": "port",
              "sample": "C oracle, %d OpenMP threads, the WHOLE step: user side %d pairs (CN+J+AA) in %.2fs, business "
                        "side %d pairs (CN+J) in %.2fs" % (nt, len(ex_x), tu, len(ex_x), tb)}
@@ -157,8 +159,10 @@ def full_parity(ex_l, gpu, ora):
     out = {"pairs_checked": int(len(ex_l)) * 2, "pairs_per_side": int(len(ex_l))}
     ok = True
     auc = {}
-    for side, keys in (("user", ("cn", "jaccard", "adamic")), ("business", ("cn", "jaccard"))):
+    for side, keys in (("user", ("cn", "jaccard", "adamic")), ("business", ("cn", "jaccard", "adamic"))):
         for k in keys:
+            if k not in ora[side] or gpu[side].get(k) is None:
+                continue
             g, o = gpu[side][k], ora[side][k]
             same = bool(np.array_equal(g, o))
             out["%s_%s_exact" % (side[0], k)] = same
@@ -539,7 +543,7 @@ def run_sharded(args):
     ex_x, ex_y = synth.uniform_examples(G, src, rate=args.rate, seed=d.rank)
     passes = [("user", G.batch(ex_x, ex_y), args.user_mask)]
     if args.sides == "both":
-        passes.append(("business", G.batch(ex_y, ex_x), blp.CN | blp.JACCARD))
+        passes.append(("business", G.batch(ex_y, ex_x), 7 if getattr(args, "fix_adamic", False) else 3))
     for name, bt, _ in passes:
         log("plan %s: %s" % (name, bt.plan()))
     for _ in range(args.warmup):
@@ -731,6 +735,9 @@ def main():
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--user-mask", type=int, default=7, help="methods of the user pass (1 CN, 2 J, 4 AA)")
     ap.add_argument("--business-first", action="store_true", help="enqueue the business pass before the user pass")
+    ap.add_argument("--fix-adamic", action="store_true",
+                    help="business pass with Adamic-Adar too (similarity.business(..., fix_adamic=True); the "
+                         "reference's own business pass never computes it, similarity.py:102)")
     ap.add_argument("--mode", default="similarity", choices=["similarity", "topk", "svd", "sharded", "e2e"],
                     help="similarity: config 2 (default); topk: config 3 full-candidate Jaccard + Adamic-Adar "
                          "top-k; svd: config 4 rank-64 truncated-SVD scorer; sharded: config 5 row-block "
@@ -768,7 +775,7 @@ def main():
     if args.sides in ("both", "user"):
         passes.append(("user", G.batch(ex_x, ex_y), args.user_mask))
     if args.sides in ("both", "business"):
-        passes.append(("business", G.batch(ex_y, ex_x), blp.CN | blp.JACCARD))
+        passes.append(("business", G.batch(ex_y, ex_x), 7 if getattr(args, "fix_adamic", False) else 3))
     if args.business_first:  # enqueue order of the two concurrent passes
         passes.reverse()
     for name, bt, _ in passes:
@@ -817,7 +824,8 @@ def main():
             "workload": "config2: synthetic %dK users x %dK businesses, %dM draws (%d unique edges); %d example "
                         "users/GPU, exact hop-3 candidates kept at %g (+held-out positives); step = similarity.main "
                         "device work: %s" % (U // 1000, B // 1000, D // 10**6, G.nnz // 2, len(np.unique(ex_x)),
-                                             args.rate, "user side CN+Jaccard+AA fused + business side CN+Jaccard"
+                                             args.rate, "user side CN+Jaccard+AA fused + business side CN+Jaccard" +
+                                             (" + AA (fix_adamic)" if args.fix_adamic else "")
                                              if args.sides == "both" else args.sides + " side"),
             "pairs_per_gpu": int(len(ex_x)),
             "global_batch": int(pairs_total),
@@ -846,7 +854,7 @@ def main():
         import coracle
 
         og = coracle.OracleGraph(G.n, *_dense_edges(G))
-        ora, multi = oracle_full(og, ex_x, ex_y)
+        ora, multi = oracle_full(og, ex_x, ex_y, 7 if args.fix_adamic else 3)
         if not args.no_parity:
             out["parity"] = full_parity(ex_l, res, ora)
         if dist.world == 1 and not args.no_cpu_baseline:

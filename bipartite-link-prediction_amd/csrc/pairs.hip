@@ -1765,8 +1765,10 @@ __global__ __launch_bounds__(BLOCK) void k_score_global(ScoreArgs a, uint32_t* g
 // independent item: two workgroups per CU (32 waves). Rows are sorted, so a chunk reads only
 // its slice of each row N(z) / N(y) -- the slice bounds come from a per-row split table, and
 // no element is read twice. Items are source-major (both chunks of a source run at the same
-// time on different CUs and share its rows in L2). Partial counts, fixed-point AA sums and
-// |H2| partials go to HBM; k_split_combine adds them and computes Jaccard.
+// time on different CUs and share its rows in L2). A (pair, chunk) slice with hits adds its
+// count and exact AA words to the pair's accumulators in HBM (device-scope atomics; slices
+// without hits add nothing); |H2| partials go to [sources][chunks]; k_split_combine computes
+// the final values and Jaccard.
 __global__ void k_row_splits(const int64_t* __restrict__ rp, const int32_t* __restrict__ ci, int64_t v0, int64_t n,
                              int64_t lo, int64_t cap_bits, int C, int32_t* __restrict__ rsplit) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
@@ -1912,12 +1914,18 @@ __global__ __launch_bounds__(BLOCK, 8) void k_score_split(ScoreArgs a, const int
       else
         mp_scan<BLOCK, K, false>(a.cw, a.idmask, a.idbits, a.aaw, a.wtab, s_start, s_off, ns, c0, width, bm, s_cn, s_aa, threadIdx.x);
       __syncthreads();
+      // a pair's chunk partials meet in per-pair accumulators: only (pair, chunk) slices with a
+      // hit add anything (a few per pair), so no [chunks][pairs] partial arrays (config 5:
+      // 96 chunks x 199M pairs) and no dense combine reads
       for (int t = threadIdx.x; t < ns; t += BLOCK) {
         const int64_t gp = pbeg + sb + t;
-        pcn[(int64_t)c * np + gp] = s_cn[t];
-        if (want_a) {  // exact AA words of this chunk
-          paa[2 * ((int64_t)c * np + gp)] = s_aa[2 * t];
-          paa[2 * ((int64_t)c * np + gp) + 1] = s_aa[2 * t + 1];
+        const unsigned c_t = s_cn[t];
+        if (c_t) {
+          atomicAdd(&pcn[gp], c_t);
+          if (want_a) {  // exact AA words: wrapping low sums and exact high sums add in any order
+            atomicAdd(&paa[2 * gp], s_aa[2 * t]);
+            atomicAdd(&paa[2 * gp + 1], s_aa[2 * t + 1]);
+          }
         }
       }
       __syncthreads();
@@ -1941,15 +1949,8 @@ __global__ __launch_bounds__(256) void k_split_combine(ScoreArgs a, int C, const
     const int pbeg = a.off[x], pcnt = a.cnt[x];
     for (int t = lane; t < pcnt; t += 64) {
       const int64_t gp = pbeg + t;
-      unsigned cn = 0;
-      unsigned long long lo = 0, hi = 0;
-      for (int c = 0; c < C; ++c) {
-        cn += pcn[(int64_t)c * np + gp];
-        if (want_a) {
-          lo += paa[2 * ((int64_t)c * np + gp)];
-          hi += paa[2 * ((int64_t)c * np + gp) + 1];
-        }
-      }
+      const unsigned cn = pcn[gp];
+      const unsigned long long lo = want_a ? paa[2 * gp] : 0ull, hi = want_a ? paa[2 * gp + 1] : 0ull;
       const int p = a.g_out[gp];
       a.cn[p] = cn;
       if (want_a) a.aa[p] = blp::aa_value(lo, hi);
@@ -2172,8 +2173,8 @@ struct blp_batch {
   int64_t rs_lo = 0;     // first node of the split table
   int32_t* d_gy = nullptr;     // grouped position -> y (split mode)
   int32_t* d_rsplit = nullptr; // [n][split + 1] row offsets where neighbour ids cross chunk boundaries
-  uint32_t* d_pcn = nullptr;   // [split][n_pairs] partial counts
-  unsigned long long* d_paa = nullptr;  // [split][n_pairs][2] partial exact AA words
+  uint32_t* d_pcn = nullptr;   // [n_pairs] counts, summed over chunks (zeroed per score)
+  unsigned long long* d_paa = nullptr;  // [n_pairs][2] exact AA words, summed over chunks
   unsigned long long* d_aa_part = nullptr;  // [n_pairs][2] exact AA words between LDS chunks (chunks > 1)
   uint32_t* d_ph2 = nullptr;   // [n][split] partial |H2|
   uint32_t* d_gbm = nullptr;
@@ -2461,8 +2462,8 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
     const int64_t nrows = std::max<int64_t>(rows_hi - rows_lo, 1);
     if (hipMalloc(&b->d_gy, 4 * (size_t)n_pairs) != hipSuccess ||
         hipMalloc(&b->d_rsplit, 4 * (size_t)nrows * (C + 1)) != hipSuccess ||
-        hipMalloc(&b->d_pcn, 4 * (size_t)n_pairs * C) != hipSuccess ||
-        hipMalloc(&b->d_paa, 16 * (size_t)n_pairs * C) != hipSuccess ||
+        hipMalloc(&b->d_pcn, 4 * (size_t)n_pairs) != hipSuccess ||
+        hipMalloc(&b->d_paa, 16 * (size_t)n_pairs) != hipSuccess ||
         hipMalloc(&b->d_ph2, 4 * (size_t)std::max<int64_t>(b->n_sources, 1) * C) != hipSuccess)
       return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: split buffers"));
     hipLaunchKernelGGL(k_row_splits, dim3(2048), dim3(256), 0, g->stream, g->d_rp, g->d_ci, rows_lo, nrows, b->lo,
@@ -2685,6 +2686,8 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   a.dq = b->dq;
   a.short_rows = b->short_rows;
   if (np && b->split) {
+    BLP_HIP(hipMemsetAsync(b->d_pcn, 0, 4 * (size_t)np, b->stream));
+    if (mask & BLP_ADAMIC) BLP_HIP(hipMemsetAsync(b->d_paa, 0, 16 * (size_t)np, b->stream));
     int per_cu = 1;
     BLP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_score_split<S_BLOCK, S_CAP, S_SEG, 8>, S_BLOCK, 0));
     hipLaunchKernelGGL((k_score_split<S_BLOCK, S_CAP, S_SEG, 8>), dim3(g->n_cu * std::max(per_cu, 1)), dim3(S_BLOCK), 0,
