@@ -505,13 +505,26 @@ __device__ inline uint32_t in_chunk(int v, uint32_t keep, uint32_t c0u) { return
 // Exact Adamic-Adar accumulation (blp_internal.h): a term W adds to the wrapping low word and
 // its high half to the exact high word. LDS accumulators are interleaved: s_aa[2 t] = lo,
 // s_aa[2 t + 1] = hi for segment t.
-__device__ inline void aa_term(unsigned long long& lo, unsigned long long& hi, unsigned long long w) {
-  lo += w;
-  hi += w >> 32;
-}
 __device__ inline void aa_push(unsigned long long* s_aa, int t, unsigned long long lo, unsigned long long hi) {
   atomicAdd(&s_aa[2 * t], lo);
   atomicAdd(&s_aa[2 * t + 1], hi);
+}
+
+// Packed layout (see rc_scan): the high word in units of 2^PK_HS shares the count's word.
+constexpr int PK_CN_BITS = 21;
+constexpr int PK_HS = 40;
+// One scan run's contribution: count c, low sum lo, high-word sum hh (a run spans <= 32 terms of
+// W >> 32 < 2^27, so hh fits 32 bits). Packed: two atomics; else the count and the two words.
+template <bool AA, bool PK>
+__device__ inline void scan_push(uint32_t* s_cn, unsigned long long* s_aa, int seg, unsigned c, unsigned long long lo,
+                                 uint32_t hh) {
+  if (PK) {
+    atomicAdd(&s_aa[2 * seg], lo);
+    atomicAdd(&s_aa[2 * seg + 1], ((unsigned long long)(hh >> (PK_HS - 32)) << PK_CN_BITS) | c);
+  } else {
+    atomicAdd(&s_cn[seg], c);
+    if (AA) aa_push(s_aa, seg, lo, (unsigned long long)hh);
+  }
 }
 
 template <int NT, int K, bool GLOBAL = false>
@@ -552,7 +565,7 @@ __device__ inline void mp_build(const int32_t* __restrict__ ci, uint32_t idmask,
 // ci may be the weight-coded copy (ScoreArgs::cw): an element is id | code << idbits; code c
 // > 0 has the weight wtab[c], code 0 falls back to the per-node table aaw[id].
 
-template <int NT, int K, bool AA>
+template <int NT, int K, bool AA, bool PK = false>
 __device__ inline void mp_scan(const int32_t* __restrict__ ci, uint32_t idmask, int idbits,
                                const long long* __restrict__ aaw, const long long* wtab, const int64_t* s_start,
                                const int32_t* s_off, int ns, int64_t c0, int64_t width, const uint32_t* bm,
@@ -593,27 +606,26 @@ __device__ inline void mp_scan(const int32_t* __restrict__ ci, uint32_t idmask, 
     mp_fetch<K>(ci, s_start, s_off, ns, T, base + STEP + tid * K, wn, skn, hint, shift);
     if (sk[0] == sk[K - 1]) {  // the K elements in one segment (or none valid): one run
       unsigned c = 0;
-      unsigned long long acc = 0, acch = 0;
+      unsigned long long acc = 0;
+      uint32_t acch = 0;
 #pragma unroll
       for (int k = 0; k < K; ++k) {
         c += hit[k] ? 1u : 0u;
-        if (AA) aa_term(acc, acch, (unsigned long long)wt[k]);
+        if (AA) {
+          acc += (unsigned long long)wt[k];
+          acch += (uint32_t)((unsigned long long)wt[k] >> 32);
+        }
       }
-      if (c) {
-        atomicAdd(&s_cn[sk[0]], c);
-        if (AA) aa_push(s_aa, sk[0], acc, acch);
-      }
+      if (c) scan_push<AA, PK>(s_cn, s_aa, sk[0], c, acc, acch);
     } else {
       int cur = sk[0];
       unsigned c = 0;
-      unsigned long long acc = 0, acch = 0;
+      unsigned long long acc = 0;
+      uint32_t acch = 0;
 #pragma unroll
       for (int k = 0; k < K; ++k) {
         if (sk[k] != cur) {
-          if (c) {
-            atomicAdd(&s_cn[cur], c);
-            if (AA) aa_push(s_aa, cur, acc, acch);
-          }
+          if (c) scan_push<AA, PK>(s_cn, s_aa, cur, c, acc, acch);
           cur = sk[k];
           c = 0;
           acc = 0;
@@ -621,13 +633,13 @@ __device__ inline void mp_scan(const int32_t* __restrict__ ci, uint32_t idmask, 
         }
         if (hit[k]) {
           ++c;
-          if (AA) aa_term(acc, acch, (unsigned long long)wt[k]);
+          if (AA) {
+            acc += (unsigned long long)wt[k];
+            acch += (uint32_t)((unsigned long long)wt[k] >> 32);
+          }
         }
       }
-      if (c && cur >= 0) {
-        atomicAdd(&s_cn[cur], c);
-        if (AA) aa_push(s_aa, cur, acc, acch);
-      }
+      if (c && cur >= 0) scan_push<AA, PK>(s_cn, s_aa, cur, c, acc, acch);
     }
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -813,26 +825,29 @@ __device__ inline void pp_scan(const int32_t* __restrict__ ci, uint32_t idmask, 
       }
     }
     unsigned c1 = 0, c2 = 0;
-    unsigned long long x1 = 0, x2 = 0, h1 = 0, h2 = 0;
+    unsigned long long x1 = 0, x2 = 0;
+    uint32_t h1 = 0, h2 = 0;  // <= K terms of W >> 32 < 2^27 each
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       const unsigned h = hit[k] ? 1u : 0u;
       const unsigned long long v = (AA && hit[k]) ? (unsigned long long)wt[k] : 0ull;
       if (k < st.rem1) {
         c1 += h;
-        aa_term(x1, h1, v);
+        x1 += v;
+        h1 += (uint32_t)(v >> 32);
       } else {
         c2 += h;
-        aa_term(x2, h2, v);
+        x2 += v;
+        h2 += (uint32_t)(v >> 32);
       }
     }
     if (c1) {
       atomicAdd(&s_cn[st.s1], c1);
-      if (AA) aa_push(s_aa, st.s1, x1, h1);
+      if (AA) aa_push(s_aa, st.s1, x1, (unsigned long long)h1);
     }
     if (c2) {
       atomicAdd(&s_cn[st.s2], c2);
-      if (AA) aa_push(s_aa, st.s2, x2, h2);
+      if (AA) aa_push(s_aa, st.s2, x2, (unsigned long long)h2);
     }
   };
   // no exit from the middle of the body: a path leaving with B in flight would merge into the
@@ -977,8 +992,6 @@ __device__ inline void rc_build(const int32_t* __restrict__ ci, uint32_t idmask,
 // units of 2^40 shares the count's atomic, so a step issues the same two LDS atomics as a CN +
 // 64-bit sum. Valid while cn < 2^PK_CN_BITS (a chunk holds < 2^21 nodes) : each step's high part
 // undercounts S by < 2^40 + K * 2^32, so S - hi * 2^40 < cn * 2^41 < 2^64 (blp::aa_exact, hs = 40).
-constexpr int PK_CN_BITS = 21;
-constexpr int PK_HS = 40;
 
 template <int NT, int K, bool AA>
 __device__ inline void rc_scan(const int32_t* __restrict__ ci, uint32_t idmask, int idbits,
@@ -1120,7 +1133,8 @@ __device__ inline void row_scan(const int32_t* __restrict__ ci, uint32_t idmask,
     const int64_t st = s_start[t];
     const int len = s_off[t + 1] - s_off[t];
     unsigned c = 0;
-    unsigned long long acc = 0, acch = 0;
+    unsigned long long acc = 0;
+    uint32_t acch = 0;  // a row holds <= SHORT_MAX = 32 terms of W >> 32 < 2^27
     for (int h = 0; h < len; h += SHORT_PART) {
       int e[SHORT_PART];
       row_part(ci, st, len, h, e);
@@ -1133,7 +1147,9 @@ __device__ inline void row_scan(const int32_t* __restrict__ ci, uint32_t idmask,
           c += hit ? 1u : 0u;
           if (AA && hit) {
             const uint32_t code = ((uint32_t)e[k] >> idbits) & 255u;
-            aa_term(acc, acch, (unsigned long long)(code ? wtab[code] : aaw[e[k] & idmask]));
+            const unsigned long long w = (unsigned long long)(code ? wtab[code] : aaw[e[k] & idmask]);
+            acc += w;
+            acch += (uint32_t)(w >> 32);
           }
         }
       }
@@ -1909,8 +1925,10 @@ __global__ __launch_bounds__(BLOCK, 8) void k_score_split(ScoreArgs a, const int
       if ((int)threadIdx.x < ns) s_off[threadIdx.x] = ex;
       if (threadIdx.x == 0) s_off[ns] = tot;
       __syncthreads();
+      // Adamic-Adar: packed count + high word (a chunk holds < 2^21 nodes), converted per slice
       if (want_a)
-        mp_scan<BLOCK, K, true>(a.cw, a.idmask, a.idbits, a.aaw, a.wtab, s_start, s_off, ns, c0, width, bm, s_cn, s_aa, threadIdx.x);
+        mp_scan<BLOCK, K, true, true>(a.cw, a.idmask, a.idbits, a.aaw, a.wtab, s_start, s_off, ns, c0, width, bm, s_cn,
+                                      s_aa, threadIdx.x);
       else
         mp_scan<BLOCK, K, false>(a.cw, a.idmask, a.idbits, a.aaw, a.wtab, s_start, s_off, ns, c0, width, bm, s_cn, s_aa, threadIdx.x);
       __syncthreads();
@@ -1919,12 +1937,16 @@ __global__ __launch_bounds__(BLOCK, 8) void k_score_split(ScoreArgs a, const int
       // 96 chunks x 199M pairs) and no dense combine reads
       for (int t = threadIdx.x; t < ns; t += BLOCK) {
         const int64_t gp = pbeg + sb + t;
-        const unsigned c_t = s_cn[t];
+        const unsigned c_t = want_a ? (unsigned)(s_aa[2 * t + 1] & ((1u << PK_CN_BITS) - 1)) : s_cn[t];
         if (c_t) {
           atomicAdd(&pcn[gp], c_t);
-          if (want_a) {  // exact AA words: wrapping low sums and exact high sums add in any order
-            atomicAdd(&paa[2 * gp], s_aa[2 * t]);
-            atomicAdd(&paa[2 * gp + 1], s_aa[2 * t + 1]);
+          if (want_a) {
+            // the slice's exact 128-bit sum S from (lo, hi in 2^40 units), re-expressed as
+            // (S mod 2^64, S >> 32): these add across slices like the two-word form (hs = 32)
+            unsigned long long sh, sl;
+            blp::aa_exact(s_aa[2 * t], s_aa[2 * t + 1] >> PK_CN_BITS, &sh, &sl, PK_HS);
+            atomicAdd(&paa[2 * gp], sl);
+            atomicAdd(&paa[2 * gp + 1], (sh << 32) | (sl >> 32));
           }
         }
       }
