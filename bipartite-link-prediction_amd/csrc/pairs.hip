@@ -518,9 +518,11 @@ constexpr int PK_HS = 40;
 template <bool AA, bool PK>
 __device__ inline void scan_push(uint32_t* s_cn, unsigned long long* s_aa, int seg, unsigned c, unsigned long long lo,
                                  uint32_t hh) {
-  if (PK) {
+  if (PK && AA) {
     atomicAdd(&s_aa[2 * seg], lo);
     atomicAdd(&s_aa[2 * seg + 1], ((unsigned long long)(hh >> (PK_HS - 32)) << PK_CN_BITS) | c);
+  } else if (PK) {  // counts only, in the packed word
+    atomicAdd(&s_aa[2 * seg + 1], (unsigned long long)c);
   } else {
     atomicAdd(&s_cn[seg], c);
     if (AA) aa_push(s_aa, seg, lo, (unsigned long long)hh);
@@ -1811,8 +1813,7 @@ __global__ __launch_bounds__(BLOCK, 8) void k_score_split(ScoreArgs a, const int
   __shared__ uint32_t bm[CAP_WORDS];
   __shared__ int64_t s_start[SEG];
   __shared__ int32_t s_off[SEG + 1];
-  __shared__ uint32_t s_cn[SEG];
-  __shared__ unsigned long long s_aa[2 * SEG];
+  __shared__ unsigned long long s_aa[2 * SEG];  // packed: [2t] Σ W, [2t + 1] high word << 21 | count
   __shared__ unsigned long long red64[NW];
   __shared__ int red[NW];
   __shared__ int s_item;
@@ -1916,7 +1917,6 @@ __global__ __launch_bounds__(BLOCK, 8) void k_score_split(ScoreArgs a, const int
         const int32_t* sp = rsplit + ((int64_t)g_y[gp] - rs_lo) * (C + 1) + c;
         s_start[threadIdx.x] = a.g_yb[gp] + sp[0];
         len = sp[1] - sp[0];
-        s_cn[threadIdx.x] = 0;
         s_aa[2 * threadIdx.x] = 0;
         s_aa[2 * threadIdx.x + 1] = 0;
       }
@@ -1925,19 +1925,20 @@ __global__ __launch_bounds__(BLOCK, 8) void k_score_split(ScoreArgs a, const int
       if ((int)threadIdx.x < ns) s_off[threadIdx.x] = ex;
       if (threadIdx.x == 0) s_off[ns] = tot;
       __syncthreads();
-      // Adamic-Adar: packed count + high word (a chunk holds < 2^21 nodes), converted per slice
+      // packed count + high word (a chunk holds < 2^21 nodes), converted per slice below
       if (want_a)
-        mp_scan<BLOCK, K, true, true>(a.cw, a.idmask, a.idbits, a.aaw, a.wtab, s_start, s_off, ns, c0, width, bm, s_cn,
-                                      s_aa, threadIdx.x);
+        mp_scan<BLOCK, K, true, true>(a.cw, a.idmask, a.idbits, a.aaw, a.wtab, s_start, s_off, ns, c0, width, bm,
+                                      nullptr, s_aa, threadIdx.x);
       else
-        mp_scan<BLOCK, K, false>(a.cw, a.idmask, a.idbits, a.aaw, a.wtab, s_start, s_off, ns, c0, width, bm, s_cn, s_aa, threadIdx.x);
+        mp_scan<BLOCK, K, false, true>(a.cw, a.idmask, a.idbits, a.aaw, a.wtab, s_start, s_off, ns, c0, width, bm,
+                                       nullptr, s_aa, threadIdx.x);
       __syncthreads();
       // a pair's chunk partials meet in per-pair accumulators: only (pair, chunk) slices with a
       // hit add anything (a few per pair), so no [chunks][pairs] partial arrays (config 5:
       // 96 chunks x 199M pairs) and no dense combine reads
       for (int t = threadIdx.x; t < ns; t += BLOCK) {
         const int64_t gp = pbeg + sb + t;
-        const unsigned c_t = want_a ? (unsigned)(s_aa[2 * t + 1] & ((1u << PK_CN_BITS) - 1)) : s_cn[t];
+        const unsigned c_t = (unsigned)(s_aa[2 * t + 1] & ((1u << PK_CN_BITS) - 1));
         if (c_t) {
           atomicAdd(&pcn[gp], c_t);
           if (want_a) {
@@ -2157,8 +2158,9 @@ enum Variant { V_SMALL = 0, V_MED = 1, V_LARGE = 2 };
 constexpr int CAP_SMALL = 4096, CAP_MED = 16384, CAP_LARGE = 33792;  // 1.08M bits: fits 160 KiB with the exact AA words
 constexpr int BLOCK_SMALL = 256, BLOCK_MED = 512, BLOCK_LARGE = 1024;
 constexpr int SEG_SMALL = 256, SEG_MED = 384, SEG_LARGE = 512;  // MED: two 512-thread workgroups per CU (<= 80 KiB LDS)
+constexpr int SEG_MED_NOAA = 512;  // MED without Adamic-Adar (no AA words, no weight table in LDS)
 constexpr int G_BLOCK = 1024, G_SEG = 512;  // HBM-bitmap scorer
-constexpr int S_BLOCK = 1024, S_CAP = 16384, S_SEG = 448;  // chunk-parallel scorer: 64 KiB chunks, 2 blocks / CU (<= 80 KiB LDS each)
+constexpr int S_BLOCK = 1024, S_CAP = 16384, S_SEG = 512;  // chunk-parallel scorer: 64 KiB chunks, 2 blocks / CU (<= 80 KiB LDS each)
 constexpr int S_MAX_CHUNKS = 128;                          // up to 67M-node universes (config 5: 50M users)
 
 inline int variant_block(int v) { return v == V_SMALL ? BLOCK_SMALL : v == V_MED ? BLOCK_MED : BLOCK_LARGE; }
@@ -2256,17 +2258,17 @@ static int variant_occupancy(int v, int* per_cu) {
   return score_occupancy<BLOCK_LARGE, CAP_LARGE, SEG_LARGE>(per_cu);
 }
 
-template <int BLOCK, int CAP, int SEG>
+template <int BLOCK, int CAP, int SEG, bool SAA = true>
 static int launch_score(blp_graph* g, hipStream_t st, const ScoreArgs& a, int per_cu, int cus) {
   if (cus <= 0 || cus > g->n_cu) cus = g->n_cu;
   const dim3 grid(cus * per_cu), block(BLOCK);
   const int k = kpt_choice();
   if (k == 4)
-    hipLaunchKernelGGL((k_score<BLOCK, CAP, SEG, 4>), grid, block, 0, st, a);
+    hipLaunchKernelGGL((k_score<BLOCK, CAP, SEG, 4, false, SAA>), grid, block, 0, st, a);
   else if (k == 16)
-    hipLaunchKernelGGL((k_score<BLOCK, CAP, SEG, 16>), grid, block, 0, st, a);
+    hipLaunchKernelGGL((k_score<BLOCK, CAP, SEG, 16, false, SAA>), grid, block, 0, st, a);
   else
-    hipLaunchKernelGGL((k_score<BLOCK, CAP, SEG, 8>), grid, block, 0, st, a);
+    hipLaunchKernelGGL((k_score<BLOCK, CAP, SEG, 8, false, SAA>), grid, block, 0, st, a);
   BLP_HIP(hipGetLastError());
   return BLP_OK;
 }
@@ -2755,7 +2757,8 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
     if (b->variant == V_SMALL)
       rc = launch_score<BLOCK_SMALL, CAP_SMALL, SEG_SMALL>(g, b->stream, a, per_cu, b->cus);
     else if (b->variant == V_MED)
-      rc = launch_score<BLOCK_MED, CAP_MED, SEG_MED>(g, b->stream, a, per_cu, b->cus);
+      rc = (mask & BLP_ADAMIC) ? launch_score<BLOCK_MED, CAP_MED, SEG_MED>(g, b->stream, a, per_cu, b->cus)
+                               : launch_score<BLOCK_MED, CAP_MED, SEG_MED_NOAA, false>(g, b->stream, a, per_cu, b->cus);
     else
       rc = launch_score<BLOCK_LARGE, CAP_LARGE, SEG_LARGE>(g, b->stream, a, per_cu, b->cus);
     if (rc) return rc;
