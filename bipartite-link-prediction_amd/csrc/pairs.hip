@@ -1310,6 +1310,7 @@ struct ScoreArgs {
   const uint4* wedge;
   unsigned long long* aa_part;  // [2 n_pairs] exact AA words carried between LDS chunks (k_score, chunks > 1)
   const SrcRec* rec;            // per active source (short-row scorer; null: gather from active[])
+  int sched;                    // short-row scorer: 1 = claims dealt round-robin (BLP_STATIC), 0 = dequeued
 };
 
 template <int BLOCK>
@@ -1393,16 +1394,24 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
   const int n_active = a.misc->n_active;
 
   PROF_INIT
-  // dequeue one ahead: the next source's atomic is in flight while this one is scored
-  int nxt = threadIdx.x == 0 ? atomicAdd(&a.misc->queue, a.dq) : 0;
+  // dequeue one ahead: the next source's atomic is in flight while this one is scored.
+  // a.sched (short-row scorer, BLP_STATIC): claims dealt round-robin instead, no atomics.
+  const bool dealt = SHORT && a.sched;
+  int nxt = dealt ? (int)blockIdx.x * a.dq : threadIdx.x == 0 ? atomicAdd(&a.misc->queue, a.dq) : 0;
   for (;;) {
-    if (threadIdx.x == 0) {
-      s_src = nxt;
-      if (nxt < n_active) nxt = atomicAdd(&a.misc->queue, a.dq);
+    int s_first;
+    if (dealt) {
+      s_first = nxt;
+      nxt += (int)gridDim.x * a.dq;
+    } else {
+      if (threadIdx.x == 0) {
+        s_src = nxt;
+        if (nxt < n_active) nxt = atomicAdd(&a.misc->queue, a.dq);
+      }
+      __syncthreads();
+      s_first = s_src;
+      __syncthreads();
     }
-    __syncthreads();
-    const int s_first = s_src;
-    __syncthreads();
     if (s_first >= n_active) break;
     PROF(0)
     const int s_last = min(n_active, s_first + a.dq);
@@ -1455,18 +1464,20 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
         } else {
           // 1. the dense rows of N(x) initialise the bitmap (their OR, 16-byte vectors), then
           // 2. the sparse rows mark N(N(x)) ∩ [c0, c1) through merge-path row segments
-          if (threadIdx.x == 0) s_nhot = 0;
-          __syncthreads();
-          if (!SHORT && a.hot_idx) {  // short rows are never dense
-            for (int64_t k = xb + threadIdx.x; k < xe; k += BLOCK) {
-              const int hi = a.hot_idx[a.ci[k]];
-              if (hi >= 0) {
-                const int slot = atomicAdd(&s_nhot, 1);
-                if (slot < HOT_LIST) s_hot[slot] = a.hot_tab[hi];
+          if constexpr (!SHORT) {  // short rows are never dense: the bitmap is only zeroed
+            if (threadIdx.x == 0) s_nhot = 0;
+            __syncthreads();
+            if (a.hot_idx) {
+              for (int64_t k = xb + threadIdx.x; k < xe; k += BLOCK) {
+                const int hi = a.hot_idx[a.ci[k]];
+                if (hi >= 0) {
+                  const int slot = atomicAdd(&s_nhot, 1);
+                  if (slot < HOT_LIST) s_hot[slot] = a.hot_tab[hi];
+                }
               }
             }
+            __syncthreads();
           }
-          __syncthreads();
           const int nhot = !SHORT && s_nhot <= HOT_LIST ? s_nhot : 0;  // overflow: every row goes sparse
           const int64_t q0 = c0 >> 7;
           if (RC) {
@@ -2681,6 +2692,7 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   a.aaw = g->d_aaw_fx;
   a.aa_part = b->d_aa_part;
   a.rec = nullptr;
+  a.sched = getenv("BLP_STATIC") ? atoi(getenv("BLP_STATIC")) : 0;  // tuning knob
   const bool coded = g->d_ci_w && !getenv("BLP_NO_WCODES");  // tuning knob
   a.cw = coded ? g->d_ci_w : g->d_ci;
   a.idbits = coded ? g->id_bits : 31;
