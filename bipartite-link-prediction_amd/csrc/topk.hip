@@ -43,7 +43,10 @@ constexpr int TK_SEG = 256;           // N(x) entries staged per batch
 constexpr int TK_FILT = 128;          // words of the N'(x) membership filter (4096 bits)
 constexpr int TK_ACC_WORDS = 32768;   // counter space: 128 KiB
 constexpr int TK_KMAX = 256;
-constexpr int TK_RB = 8;           // row entries loaded up front per element
+#ifndef BLP_TK_RB
+#define BLP_TK_RB 8
+#endif
+constexpr int TK_RB = BLP_TK_RB;   // row entries loaded up front per element (16-byte vectors)
 constexpr uint32_t TK_EMPTY = 0xFFFFFFFFu;
 
 // Counter layout: permuted target p has a byte address -- 4p for the u32 tier (p < n32),
