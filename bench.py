@@ -763,19 +763,25 @@ def main():
     U, B, D = synth.CONFIGS[args.config]
     t0 = time.time()
     a, b = synth.review_edges(U, B, D, seed=0)
-    G = blp.DeviceGraph(a, b, device=dev)
+    t_gen = time.time() - t0
+    t0 = time.time()
+    G = blp.DeviceGraph(a, b, device=dev)  # CSR, weights, coded ids, dense-row index, wedge rows
+    t_graph = time.time() - t0
     del a, b
-    log("graph: %d nodes, %d unique edges, built in %.1fs" % (G.n, G.nnz // 2, time.time() - t0))
+    log("graph: %d nodes, %d unique edges, generated in %.1fs, built in %.1fs" % (G.n, G.nnz // 2, t_gen, t_graph))
     t0 = time.time()
     ex_x, ex_y, ex_l = synth.make_examples(G, U, B, D, n_users=args.users, rate=args.rate, seed=dist.rank)
+    t_ex = time.time() - t0
     log("examples: %d pairs for %d users (%d positives) in %.1fs" %
-        (len(ex_x), len(np.unique(ex_x)), int(ex_l.sum()), time.time() - t0))
+        (len(ex_x), len(np.unique(ex_x)), int(ex_l.sum()), t_ex))
 
     passes = []
+    t0 = time.time()
     if args.sides in ("both", "user"):
         passes.append(("user", G.batch(ex_x, ex_y), args.user_mask))
     if args.sides in ("both", "business"):
         passes.append(("business", G.batch(ex_y, ex_x), 7 if getattr(args, "fix_adamic", False) else 3))
+    t_batch = time.time() - t0
     if args.business_first:  # enqueue order of the two concurrent passes
         passes.reverse()
     for name, bt, _ in passes:
@@ -832,6 +838,10 @@ def main():
             "parallelism": "replicas x%d (graph replicated, users split, no collective)" % dist.world,
         },
         "kernels_ms": ktimes,
+        # outside the timed step (once per graph / per example set), reported for completeness
+        "setup_s": {"edge_generation": round(t_gen, 3), "graph_build": round(t_graph, 3),
+                    "examples_hop3": round(t_ex, 3),
+                    "batch_create": round(t_batch, 3)},
         "work": {name: {"build_elems": _build_elems(G, xs_), "scan_elems": int(G.hop1_size[ys_].astype(np.int64).sum()),
                         "hits": int(res[name]["cn"].astype(np.int64).sum()), "sources": int(len(np.unique(xs_)))}
                  for name, xs_, ys_ in [("user", ex_x, ex_y), ("business", ex_y, ex_x)] if name in res},
