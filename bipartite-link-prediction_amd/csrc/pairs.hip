@@ -34,6 +34,9 @@
 #ifndef BLP_SHORT_MINB
 #define BLP_SHORT_MINB 7  // short-row scorer: >= 7 workgroups of 256 per CU (<= 72 VGPRs)
 #endif
+#ifndef BLP_PF
+#define BLP_PF 1  // short-row scorer: first pair segment's metadata loaded before the H2 build
+#endif
 #ifndef BLP_PP
 #define BLP_PP 1  // ping-pong merge-path loops in k_score (0: the single-buffer mp_build / mp_scan)
 #endif
@@ -1448,6 +1451,16 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
         nx_hi = xe > xb ? a.ci[xe - 1] : -1;
       }
       unsigned long long h2 = 0;
+      // short-row scorer (BLP_PF): the first pair segment's metadata is loaded now, so its
+      // latency overlaps the H2 build instead of following it
+      int64_t pf_start = 0;
+      int pf_len = 0, pf_out = 0;
+      if (SHORT && BLP_PF && (int)threadIdx.x < min(SEG, pcnt)) {
+        const int gp = pbeg + threadIdx.x;
+        pf_start = a.g_yb[gp];
+        pf_len = a.g_yl[gp];
+        pf_out = a.g_out[gp];
+      }
       PROF(1)
 
       for (int ch = 0; ch < nchunks; ++ch) {
@@ -1592,7 +1605,18 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
         for (int sb = 0; sb < pcnt; sb += SEG) {
           const int ns = min(SEG, pcnt - sb);
           int len = 0, pout = 0;
-          if ((int)threadIdx.x < ns) {
+          if (SHORT && BLP_PF && sb == 0) {
+            if ((int)threadIdx.x < ns) {
+              s_start[threadIdx.x] = pf_start;
+              len = pf_len;
+              pout = pf_out;
+              s_cn[threadIdx.x] = 0;
+              if (SAA) {
+                s_aa[2 * threadIdx.x] = 0;
+                s_aa[2 * threadIdx.x + 1] = 0;
+              }
+            }
+          } else if ((int)threadIdx.x < ns) {
             const int gp = pbeg + sb + threadIdx.x;
             s_start[threadIdx.x] = a.g_yb[gp];
             len = a.g_yl[gp];
