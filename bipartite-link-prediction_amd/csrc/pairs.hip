@@ -37,6 +37,12 @@
 #ifndef BLP_PF
 #define BLP_PF 1  // short-row scorer: first pair segment's metadata loaded before the H2 build
 #endif
+#ifndef BLP_PFL
+#define BLP_PFL 1  // the same for the large-universe row-chunk scorer
+#endif
+#ifndef BLP_PFN
+#define BLP_PFN 1  // ... and every later segment's metadata during the previous segment's scan
+#endif
 #ifndef BLP_PP
 #define BLP_PP 1  // ping-pong merge-path loops in k_score (0: the single-buffer mp_build / mp_scan)
 #endif
@@ -1455,7 +1461,8 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
       // latency overlaps the H2 build instead of following it
       int64_t pf_start = 0;
       int pf_len = 0, pf_out = 0;
-      if (SHORT && BLP_PF && (int)threadIdx.x < min(SEG, pcnt)) {
+      constexpr bool PF = SHORT ? BLP_PF : (RC && BLP_PFL);
+      if (PF && nchunks == 1 && (int)threadIdx.x < min(SEG, pcnt)) {
         const int gp = pbeg + threadIdx.x;
         pf_start = a.g_yb[gp];
         pf_len = a.g_yl[gp];
@@ -1602,10 +1609,11 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
         }
         PROF(5)
         // 5. scan N(y) of every pair of x, SEG pairs at a time
+        bool have_pf = PF && nchunks == 1;  // segment sb's metadata is in pf_* (loaded earlier)
         for (int sb = 0; sb < pcnt; sb += SEG) {
           const int ns = min(SEG, pcnt - sb);
           int len = 0, pout = 0;
-          if (SHORT && BLP_PF && sb == 0) {
+          if (have_pf) {
             if ((int)threadIdx.x < ns) {
               s_start[threadIdx.x] = pf_start;
               len = pf_len;
@@ -1632,6 +1640,14 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
           if ((int)threadIdx.x < ns) s_off[threadIdx.x] = ex;
           if (threadIdx.x == 0) s_off[ns] = tot;
           __syncthreads();
+          // the next segment's metadata, in flight during this segment's scan (BLP_PFN)
+          have_pf = PF && !SHORT && BLP_PFN && nchunks == 1 && sb + SEG < pcnt;
+          if (have_pf && (int)threadIdx.x < min(SEG, pcnt - sb - SEG)) {
+            const int gp = pbeg + sb + SEG + threadIdx.x;
+            pf_start = a.g_yb[gp];
+            pf_len = a.g_yl[gp];
+            pf_out = a.g_out[gp];
+          }
           PROF(6)
           if (SHORT || (a.short_rows & 2)) {
             if (SAA && want_a)
