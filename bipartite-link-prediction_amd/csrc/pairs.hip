@@ -1856,7 +1856,7 @@ __global__ void k_row_splits(const int64_t* __restrict__ rp, const int32_t* __re
 }
 
 template <int BLOCK, int CAP_WORDS, int SEG, int K>
-__global__ __launch_bounds__(BLOCK, 8) void k_score_split(ScoreArgs a, const int32_t* __restrict__ g_y,
+__global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_split(ScoreArgs a, const int32_t* __restrict__ g_y,
                                                        const int32_t* __restrict__ rsplit, int64_t rs_lo, int C,
                                                        uint32_t* __restrict__ pcn, unsigned long long* __restrict__ paa,
                                                        uint32_t* __restrict__ ph2, int64_t np) {
@@ -2212,6 +2212,7 @@ constexpr int SEG_SMALL = 256, SEG_MED = 384, SEG_LARGE = 512;  // MED: two 512-
 constexpr int SEG_MED_NOAA = 512;  // MED without Adamic-Adar (no AA words, no weight table in LDS)
 constexpr int G_BLOCK = 1024, G_SEG = 512;  // HBM-bitmap scorer
 constexpr int S_BLOCK = 1024, S_CAP = 16384, S_SEG = 512;  // chunk-parallel scorer: 64 KiB chunks, 2 blocks / CU (<= 80 KiB LDS each)
+constexpr int S_CAP_BIG = 32768;  // ... or 128 KiB chunks, 1 block / CU: half the (pair, chunk) slices (BLP_SPLIT_BIG)
 constexpr int S_MAX_CHUNKS = 128;                          // up to 67M-node universes (config 5: 50M users)
 
 inline int variant_block(int v) { return v == V_SMALL ? BLOCK_SMALL : v == V_MED ? BLOCK_MED : BLOCK_LARGE; }
@@ -2245,6 +2246,7 @@ struct blp_batch {
   int short_rows = 0;    // ScoreArgs::short_rows
   bool global = false;   // HBM-bitmap scorer (universe wider than LDS)
   int split = 0;         // chunk-parallel scorer: universe cut into `split` LDS chunks, 2 workgroups / CU
+  bool split_big = false;  // ... 128 KiB chunks, one workgroup per CU
   int64_t rs_lo = 0;     // first node of the split table
   int32_t* d_gy = nullptr;     // grouped position -> y (split mode)
   int32_t* d_rsplit = nullptr; // [n][split + 1] row offsets where neighbour ids cross chunk boundaries
@@ -2429,7 +2431,8 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   // chunk) items on 64 KiB bitmaps, two workgroups per CU -- 5.7x the HBM-bitmap scorer on
   // the 2M-user universe of config 4 (BLP_NO_SPLIT: off; BLP_SPLIT=C: force C chunks)
   {
-    const int64_t sbits = 32ll * S_CAP;
+    b->split_big = getenv("BLP_SPLIT_BIG") && atoi(getenv("BLP_SPLIT_BIG")) > 0;  // tuning knob
+    const int64_t sbits = 32ll * (b->split_big ? S_CAP_BIG : S_CAP);
     int C = 0;
     if (const char* e = getenv("BLP_SPLIT"))
       C = std::max(0, std::min(S_MAX_CHUNKS, atoi(e)));
@@ -2765,9 +2768,15 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
     BLP_HIP(hipMemsetAsync(b->d_pcn, 0, 4 * (size_t)np, b->stream));
     if (mask & BLP_ADAMIC) BLP_HIP(hipMemsetAsync(b->d_paa, 0, 16 * (size_t)np, b->stream));
     int per_cu = 1;
-    BLP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_score_split<S_BLOCK, S_CAP, S_SEG, 8>, S_BLOCK, 0));
-    hipLaunchKernelGGL((k_score_split<S_BLOCK, S_CAP, S_SEG, 8>), dim3(g->n_cu * std::max(per_cu, 1)), dim3(S_BLOCK), 0,
-                       b->stream, a, b->d_gy, b->d_rsplit, b->rs_lo, b->split, b->d_pcn, b->d_paa, b->d_ph2, np);
+    if (b->split_big) {
+      BLP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_score_split<S_BLOCK, S_CAP_BIG, S_SEG, 8>, S_BLOCK, 0));
+      hipLaunchKernelGGL((k_score_split<S_BLOCK, S_CAP_BIG, S_SEG, 8>), dim3(g->n_cu * std::max(per_cu, 1)), dim3(S_BLOCK),
+                         0, b->stream, a, b->d_gy, b->d_rsplit, b->rs_lo, b->split, b->d_pcn, b->d_paa, b->d_ph2, np);
+    } else {
+      BLP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_score_split<S_BLOCK, S_CAP, S_SEG, 8>, S_BLOCK, 0));
+      hipLaunchKernelGGL((k_score_split<S_BLOCK, S_CAP, S_SEG, 8>), dim3(g->n_cu * std::max(per_cu, 1)), dim3(S_BLOCK), 0,
+                         b->stream, a, b->d_gy, b->d_rsplit, b->rs_lo, b->split, b->d_pcn, b->d_paa, b->d_ph2, np);
+    }
     BLP_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_split_combine, dim3(g->n_cu * 8), dim3(256), 0, b->stream, a, b->split, b->d_pcn, b->d_paa,
                        b->d_ph2, np);
