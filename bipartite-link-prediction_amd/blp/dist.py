@@ -114,16 +114,23 @@ def block_review_edges(users, businesses, draws, lo, hi, seed=0, zipf=0.8):
     The union over a partition is a graph of the same distribution (not the same sample as
     the single-process generator)."""
     n = int(round(draws * (hi - lo) / float(users)))
-    rng = np.random.default_rng([seed, lo, hi])
     p = synth.popularity(businesses, zipf)
     cdf = np.cumsum(p)
     u = np.empty(n, np.int64)
     b = np.empty(n, np.int64)
-    step = 50_000_000
-    for s in range(0, n, step):
-        e = min(n, s + step)
+    step = 25_000_000
+
+    def chunk(i):  # each chunk its own seeded stream: the result does not depend on the thread count
+        s, e = i * step, min(n, (i + 1) * step)
+        rng = np.random.default_rng([seed, lo, hi, i])
         u[s:e] = rng.integers(lo, hi, e - s)
         b[s:e] = np.minimum(np.searchsorted(cdf, rng.random(e - s)), businesses - 1) + users
+
+    from concurrent.futures import ThreadPoolExecutor
+
+    workers = max(1, min(16, len(os.sched_getaffinity(0))))
+    with ThreadPoolExecutor(workers) as ex:  # numpy's bulk draws and searchsorted release the GIL
+        list(ex.map(chunk, range((n + step - 1) // step)))
     return u, b
 
 
