@@ -2212,7 +2212,7 @@ constexpr int SEG_SMALL = 256, SEG_MED = 384, SEG_LARGE = 512;  // MED: two 512-
 constexpr int SEG_MED_NOAA = 512;  // MED without Adamic-Adar (no AA words, no weight table in LDS)
 constexpr int G_BLOCK = 1024, G_SEG = 512;  // HBM-bitmap scorer
 constexpr int S_BLOCK = 1024, S_CAP = 16384, S_SEG = 512;  // chunk-parallel scorer: 64 KiB chunks, 2 blocks / CU (<= 80 KiB LDS each)
-constexpr int S_CAP_BIG = 32768;  // ... or 128 KiB chunks, 1 block / CU: half the (pair, chunk) slices (BLP_SPLIT_BIG)
+constexpr int S_CAP_BIG = 32768;  // ... or 128 KiB chunks, 1 block / CU: half the (pair, chunk) slices (wide universes)
 constexpr int S_MAX_CHUNKS = 128;                          // up to 67M-node universes (config 5: 50M users)
 
 inline int variant_block(int v) { return v == V_SMALL ? BLOCK_SMALL : v == V_MED ? BLOCK_MED : BLOCK_LARGE; }
@@ -2431,7 +2431,13 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   // chunk) items on 64 KiB bitmaps, two workgroups per CU -- 5.7x the HBM-bitmap scorer on
   // the 2M-user universe of config 4 (BLP_NO_SPLIT: off; BLP_SPLIT=C: force C chunks)
   {
-    b->split_big = getenv("BLP_SPLIT_BIG") && atoi(getenv("BLP_SPLIT_BIG")) > 0;  // tuning knob
+    // universes of more than 16 small chunks (config 5: 96) take 128 KiB chunks: a (pair, chunk)
+    // slice's fixed cost -- its metadata, row-split lookups and exscan -- dominates there (5 ids
+    // per slice at config 5), and halving the slices beats the second workgroup per CU
+    // (config 5: 1.77 -> 1.07 s per step; config 4's 4 chunks stay small: its step is faster
+    // with two workgroups per CU beside the business pass). BLP_SPLIT_BIG=0/1 forces.
+    b->split_big = span > 16 * 32ll * S_CAP;
+    if (const char* e = getenv("BLP_SPLIT_BIG")) b->split_big = atoi(e) > 0;  // tuning knob
     const int64_t sbits = 32ll * (b->split_big ? S_CAP_BIG : S_CAP);
     int C = 0;
     if (const char* e = getenv("BLP_SPLIT"))
