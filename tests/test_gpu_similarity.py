@@ -107,6 +107,8 @@ def test_general_graph_exact_distance(gpu):
     {"BLP_SPLIT": "8", "BLP_HEAVY_WORK": "50"},         # ... 8 chunks, heavy sources pre-built
     {"BLP_SPLIT": "2", "BLP_HOT_MIN": "8"},             # ... dense rows OR-ed per chunk
     {"BLP_SPLIT": "40"},                                # ... many chunks, some empty
+    {"BLP_SPLIT": "3", "BLP_SPLIT_BIG": "1"},           # ... 128 KiB chunks, one workgroup per CU
+    {"BLP_SPLIT": "24", "BLP_SPLIT_BIG": "1"},          # ... same, many chunks
     {"BLP_HEAVY_WORK": "50"},                           # heavy sources pre-built by k_heavy
     {"BLP_HEAVY_WORK": "1"},                            # one row per heavy item
     {"BLP_CHUNK_BITS": "2048", "BLP_HEAVY_WORK": "50", "BLP_NO_GLOBAL": "1"},  # multi-chunk: no heavy path
