@@ -1070,6 +1070,10 @@ __device__ inline void rc_scan(const int32_t* __restrict__ ci, uint32_t idmask, 
         }
         aa_push(s_aa, st.s, acc, acch);
       }
+      if (!AA && packed) {  // counts only, in the packed word (the chunk-parallel scorer)
+        atomicAdd(&s_aa[2 * st.s + 1], (unsigned long long)__popc(hm));
+        return;
+      }
       atomicAdd(&s_cn[st.s], (unsigned)__popc(hm));
     }
   };
@@ -1861,9 +1865,14 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
                                                        uint32_t* __restrict__ pcn, unsigned long long* __restrict__ paa,
                                                        uint32_t* __restrict__ ph2, int64_t np) {
   constexpr int NW = BLOCK / 64;
-  __shared__ uint32_t bm[CAP_WORDS];
+  // 128 KiB chunks (one workgroup per CU) use the row-chunk loops of the large scorer
+  constexpr bool RCS = BLP_RC && CAP_WORDS > 16384;
+  constexpr int HCS = RCS ? 1536 : 1;
+  __shared__ uint32_t bm[CAP_WORDS + (RCS ? RC_EXTRA_WORDS : 0)];
   __shared__ int64_t s_start[SEG];
   __shared__ int32_t s_off[SEG + 1];
+  __shared__ int32_t s_coff[RCS ? SEG + 1 : 1];
+  __shared__ int32_t s_hint[HCS];
   __shared__ unsigned long long s_aa[2 * SEG];  // packed: [2t] Σ W, [2t + 1] high word << 21 | count
   __shared__ unsigned long long red64[NW];
   __shared__ int red[NW];
@@ -1874,6 +1883,8 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
   const bool want_j = (a.mask & BLP_JACCARD) != 0;
   const bool want_a = (a.mask & BLP_ADAMIC) != 0;
   uint4* bm4 = reinterpret_cast<uint4*>(bm);
+  if (RCS)  // the zero word and the build's dummy words past the bitmap
+    for (int i = threadIdx.x; i < RC_EXTRA_WORDS; i += BLOCK) bm[CAP_WORDS + i] = 0;
   const int64_t n_items = (int64_t)a.misc->n_active * C;
   for (;;) {
     if (threadIdx.x == 0) s_item = atomicAdd(&a.misc->queue, 1);
@@ -1937,7 +1948,14 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
         if ((int)threadIdx.x < ns) s_off[threadIdx.x] = ex;
         if (threadIdx.x == 0) s_off[ns] = tot;
         __syncthreads();
-        mp_build<BLOCK, K>(a.cw, a.idmask, s_start, s_off, ns, c0, width, bm, threadIdx.x);
+        if constexpr (RCS) {
+          rc_chunk_offsets<BLOCK, K>(s_off, ns, s_coff, red);
+          const int shift = build_hint<BLOCK, HCS>(s_coff, ns, BLOCK, s_hint);
+          rc_build<BLOCK, K>(a.cw, a.idmask, s_start, s_off, s_coff, ns, c0, width, bm, CAP_WORDS, threadIdx.x, s_hint,
+                             shift);
+        } else {
+          mp_build<BLOCK, K>(a.cw, a.idmask, s_start, s_off, ns, c0, width, bm, threadIdx.x);
+        }
         __syncthreads();
       }
     }
@@ -1977,12 +1995,22 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
       if (threadIdx.x == 0) s_off[ns] = tot;
       __syncthreads();
       // packed count + high word (a chunk holds < 2^21 nodes), converted per slice below
-      if (want_a)
+      if constexpr (RCS) {
+        rc_chunk_offsets<BLOCK, K>(s_off, ns, s_coff, red);
+        const int shift = build_hint<BLOCK, HCS>(s_coff, ns, BLOCK, s_hint);
+        if (want_a)
+          rc_scan<BLOCK, K, true>(a.cw, a.idmask, a.idbits, a.aaw, a.wtab, s_start, s_off, s_coff, ns, c0, width, bm,
+                                  CAP_WORDS, nullptr, s_aa, threadIdx.x, s_hint, shift, true);
+        else
+          rc_scan<BLOCK, K, false>(a.cw, a.idmask, a.idbits, a.aaw, a.wtab, s_start, s_off, s_coff, ns, c0, width, bm,
+                                   CAP_WORDS, nullptr, s_aa, threadIdx.x, s_hint, shift, true);
+      } else if (want_a) {
         mp_scan<BLOCK, K, true, true>(a.cw, a.idmask, a.idbits, a.aaw, a.wtab, s_start, s_off, ns, c0, width, bm,
                                       nullptr, s_aa, threadIdx.x);
-      else
+      } else {
         mp_scan<BLOCK, K, false, true>(a.cw, a.idmask, a.idbits, a.aaw, a.wtab, s_start, s_off, ns, c0, width, bm,
                                        nullptr, s_aa, threadIdx.x);
+      }
       __syncthreads();
       // a pair's chunk partials meet in per-pair accumulators: only (pair, chunk) slices with a
       // hit add anything (a few per pair), so no [chunks][pairs] partial arrays (config 5:
@@ -2431,12 +2459,12 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   // chunk) items on 64 KiB bitmaps, two workgroups per CU -- 5.7x the HBM-bitmap scorer on
   // the 2M-user universe of config 4 (BLP_NO_SPLIT: off; BLP_SPLIT=C: force C chunks)
   {
-    // universes of more than 16 small chunks (config 5: 96) take 128 KiB chunks: a (pair, chunk)
-    // slice's fixed cost -- its metadata, row-split lookups and exscan -- dominates there (5 ids
-    // per slice at config 5), and halving the slices beats the second workgroup per CU
-    // (config 5: 1.77 -> 1.07 s per step; config 4's 4 chunks stay small: its step is faster
-    // with two workgroups per CU beside the business pass). BLP_SPLIT_BIG=0/1 forces.
-    b->split_big = span > 16 * 32ll * S_CAP;
+    // 128 KiB chunks, one workgroup per CU, row-chunk loops: a (pair, chunk) slice's fixed cost
+    // -- its metadata, row-split lookups and exscan -- dominates the chunk-parallel scorer (5 ids
+    // per slice at config 5), and halving the slices beats a second workgroup per CU. Config 5:
+    // 1.77 s per step with 64 KiB chunks on both sides, 1.07 s with 128 KiB chunks (both
+    // sides). BLP_SPLIT_BIG=0 keeps 64 KiB chunks, two workgroups per CU.
+    b->split_big = true;
     if (const char* e = getenv("BLP_SPLIT_BIG")) b->split_big = atoi(e) > 0;  // tuning knob
     const int64_t sbits = 32ll * (b->split_big ? S_CAP_BIG : S_CAP);
     int C = 0;
