@@ -861,8 +861,8 @@ def main():
                        "kernel": "%s (%s side)" % (kname, name0), "alg_bytes_per_launch": byts,
                        "traffic_source": tsrc,
                        # what the counters name as the bound ("What bounds the user scorer")
-                       "limiter": "latency: waves wait 57% of cycles; VALU <= 53%, LDS 34% busy (45% of it bank "
-                                  "conflicts), L2 hit 17%, DRAM side 0.32 of peak (profiles/r02_v3_bench_pmc.txt)"}
+                       "limiter": "latency: waves wait 56% of cycles; VALU <= 53%, LDS 34% busy (45% of it bank "
+                                  "conflicts), L2 hit 17%, DRAM side 0.32 of peak (profiles/r02_v4_bench_pmc.txt)"}
     if dist.rank == 0 and args.sides == "both" and not (args.no_parity and args.no_cpu_baseline):
         import coracle
 
