@@ -48,6 +48,7 @@ SIGNATURES = {
     "blp_csr_from_edges_device": [_I32, _P, _P, _I64, _I64, _P, _P, _P, ctypes.POINTER(ctypes.c_int64)],
     "blp_graph_create": [_P, _P, _I64, _P, _I32, _PP],
     "blp_csr_build_device": [_I32, _P, _P, _I64, _I64, _PP],
+    "blp_csr_build_host": [_I32, _P, _P, _I64, _I64, _PP],
     "blp_csr_info": [_P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)],
     "blp_csr_fetch": [_P, _P, _P, _P],
     "blp_csr_destroy": [_P],

@@ -16,6 +16,7 @@
 """
 import ctypes
 import math
+import os
 
 import numpy as np
 
@@ -46,6 +47,19 @@ def aa_weights_from_degree(deg):
     return table[inv]
 
 
+def _unique(x):
+    """np.unique(x) for an int64 array; one presence table instead of a sort when the id span
+    is compact (graph.txt ids usually are)."""
+    if len(x) == 0:
+        return np.unique(x)
+    lo, hi = int(x.min()), int(x.max())
+    if hi - lo + 1 > max(4 * len(x), 1 << 20):
+        return np.unique(x)
+    seen = np.zeros(hi - lo + 1, bool)
+    seen[x - lo] = True
+    return np.flatnonzero(seen).astype(np.int64) + lo
+
+
 class HostGraph:
     """Host half of the graph: id map, CSR, SNAP degrees, Adamic-Adar weights.
 
@@ -58,18 +72,7 @@ class HostGraph:
         b_ids = np.asarray(b_ids, dtype=np.int64)
         if len(a_ids) != len(b_ids):
             raise ValueError("edge endpoint arrays differ in length")
-        u0 = np.unique(a_ids)
-        u1 = np.setdiff1d(np.unique(b_ids), u0, assume_unique=True)
-        self.node_ids = np.concatenate([u0, u1])  # dense id -> original id
-        self.n_col0 = len(u0)  # dense ids [0, n_col0) appear in column 0 (users of a graph.txt)
-        self.n = len(self.node_ids)
-        if self.n >= 2**31 - 1:
-            raise ValueError("too many nodes for int32 dense ids")
-        self._sort = np.argsort(self.node_ids, kind="stable")
-        self._sorted_ids = self.node_ids[self._sort]
-        da = self.dense(a_ids)
-        db = self.dense(b_ids)
-        self.n_edges_in = len(a_ids)
+        da, db = self._ids(a_ids, b_ids)
         rp = np.zeros(self.n + 1, np.int64)
         ci = np.empty(max(2 * len(da), 1), np.int32)
         sl = np.zeros(max(self.n, 1), np.uint8)
@@ -77,6 +80,21 @@ class HostGraph:
         check(lib().blp_csr_from_edges(self.n, len(da), ptr(da), ptr(db), ptr(rp), ptr(ci), ptr(sl),
                                        ctypes.byref(nnz)))
         self._set_csr(rp, ci[: nnz.value].copy(), sl[: self.n], aa)
+
+    def _ids(self, a_ids, b_ids):
+        """The id map (dense ids: column-0 ids ascending, then the other ids ascending) and the
+        edge list over dense ids."""
+        u0 = _unique(a_ids)
+        u1 = np.setdiff1d(_unique(b_ids), u0, assume_unique=True)
+        self.node_ids = np.concatenate([u0, u1])  # dense id -> original id
+        self.n_col0 = len(u0)  # dense ids [0, n_col0) appear in column 0 (users of a graph.txt)
+        self.n = len(self.node_ids)
+        if self.n >= 2**31 - 1:
+            raise ValueError("too many nodes for int32 dense ids")
+        self._sort = np.argsort(self.node_ids, kind="stable")
+        self._sorted_ids = self.node_ids[self._sort]
+        self.n_edges_in = len(a_ids)
+        return self.dense(a_ids), self.dense(b_ids)
 
     def _set_csr(self, rp, ci, sl, aa):
         self.row_ptr = rp
@@ -154,8 +172,21 @@ class DeviceGraph(HostGraph):
     """
 
     def __init__(self, a_ids, b_ids, device=0, aa=True):
-        HostGraph.__init__(self, a_ids, b_ids, aa=aa)
-        self._upload(device, aa)
+        a_ids = np.asarray(a_ids, dtype=np.int64)
+        b_ids = np.asarray(b_ids, dtype=np.int64)
+        if len(a_ids) != len(b_ids):
+            raise ValueError("edge endpoint arrays differ in length")
+        if len(a_ids) == 0 or len(a_ids) < int(os.environ.get("BLP_DEVICE_CSR_MIN", 1 << 16)):
+            HostGraph.__init__(self, a_ids, b_ids, aa=aa)
+            self._upload(device, aa)
+            return
+        # large edge lists: the CSR is built on the device (blp_csr_build_host: upload, radix
+        # sort of the directed (row, col) keys, unique) and the host mirror fetched back --
+        # the same CSR as blp_csr_from_edges (tests/test_gpu_ingest.py)
+        da, db = self._ids(a_ids, b_ids)
+        c = ctypes.c_void_p()
+        check(lib().blp_csr_build_host(device, ptr(da), ptr(db), len(da), self.n, ctypes.byref(c)))
+        self._adopt_csr(c, device, aa)
 
     @classmethod
     def from_csr(cls, row_ptr, col_idx, self_loop, n_col0, device=0, aa=True):
@@ -173,15 +204,32 @@ class DeviceGraph(HostGraph):
         ``build_times`` records the phases."""
         import time
 
-        L = lib()
-        t = {}
         t0 = time.perf_counter()
         c = ctypes.c_void_p()
-        check(L.blp_csr_build_device(device, ctypes.c_void_p(a_ptr), ctypes.c_void_p(b_ptr), m, n, ctypes.byref(c)))
-        t["device_csr_s"] = time.perf_counter() - t0
+        check(lib().blp_csr_build_device(device, ctypes.c_void_p(a_ptr), ctypes.c_void_p(b_ptr), m, n,
+                                         ctypes.byref(c)))
+        t_csr = time.perf_counter() - t0
+        g = cls.__new__(cls)
+        g.node_ids = np.arange(n, dtype=np.int64)  # ids already dense
+        g.n_col0 = int(n_col0)
+        g._sort = g.node_ids
+        g._sorted_ids = g.node_ids
+        g.n_edges_in = None
+        g._adopt_csr(c, device, aa)
+        g.build_times["device_csr_s"] = t_csr
+        return g
+
+    def _adopt_csr(self, c, device, aa):
+        """Host half from one device-to-host copy of the device CSR `c`, then the graph handle
+        over it (blp_graph_create_from_csr, which consumes `c` and borrows the host mirror)."""
+        import time
+
+        L = lib()
+        t = {}
         try:
             nn, nnz = ctypes.c_int64(), ctypes.c_int64()
             check(L.blp_csr_info(c, ctypes.byref(nn), ctypes.byref(nnz)))
+            n = nn.value
             t0 = time.perf_counter()
             rp = np.empty(n + 1, np.int64)
             ci = np.empty(max(nnz.value, 1), np.int32)
@@ -189,22 +237,22 @@ class DeviceGraph(HostGraph):
             check(L.blp_csr_fetch(c, ptr(rp), ptr(ci), ptr(sl)))
             t["fetch_s"] = time.perf_counter() - t0
             t0 = time.perf_counter()
-            g = HostGraph.from_csr.__func__(cls, rp, ci[: nnz.value], sl[:n], n_col0, aa)
+            self.n = n
+            self._set_csr(rp, ci[: nnz.value], sl[:n], aa)
             t["host_half_s"] = time.perf_counter() - t0
             t0 = time.perf_counter()
             h = ctypes.c_void_p()
-            check(L.blp_graph_create_from_csr(c, ptr(g.row_ptr), ptr(ci), ptr(g.aa_weight) if aa else None,
+            check(L.blp_graph_create_from_csr(c, ptr(self.row_ptr), ptr(ci), ptr(self.aa_weight) if aa else None,
                                               ctypes.byref(h)))
             c = None  # consumed
             t["graph_create_s"] = time.perf_counter() - t0
         finally:
             if c is not None:
                 L.blp_csr_destroy(c)
-        g._mirror = ci  # the handle borrows row_ptr / col_idx (their full allocations)
-        g.device = device
-        g.handle = h
-        g.build_times = t
-        return g
+        self._mirror = ci  # the handle borrows row_ptr / col_idx (their full allocations)
+        self.device = device
+        self.handle = h
+        self.build_times = t
 
     def _upload(self, device, aa):
         self.device = device

@@ -162,6 +162,31 @@ extern "C" int blp_csr_build_device(int device, const int32_t* d_a, const int32_
   return done(BLP_OK);
 }
 
+// Host-resident endpoints (similarity.main's graph.txt load): upload, then the device build.
+extern "C" int blp_csr_build_host(int device, const int32_t* a, const int32_t* b, int64_t m, int64_t n, blp_csr** out) {
+  BLP_CHECK(out && m >= 0 && (m == 0 || (a && b)), BLP_E_ARG, "blp_csr_build_host: bad arguments");
+  int ndev = 0;
+  BLP_HIP(hipGetDeviceCount(&ndev));
+  BLP_CHECK(device >= 0 && device < ndev, BLP_E_ARG, "blp_csr_build_host: no such device");
+  BLP_HIP(hipSetDevice(device));
+  DevBuf da, db;
+  int rc;
+  if ((rc = da.reserve(4 * std::max<int64_t>(m, 1))) || (rc = db.reserve(4 * std::max<int64_t>(m, 1)))) return rc;
+  if (m) {
+    hipError_t e = hipMemcpy(da.p, a, 4 * m, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(db.p, b, 4 * m, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      da.release();
+      db.release();
+      return hip_fail(e, "hipMemcpy (edge upload)", __FILE__, __LINE__);
+    }
+  }
+  rc = blp_csr_build_device(device, da.as<int32_t>(), db.as<int32_t>(), m, n, out);
+  da.release();
+  db.release();
+  return rc;
+}
+
 extern "C" int blp_csr_info(const blp_csr* c, int64_t* n_nodes, int64_t* nnz) {
   BLP_CHECK(c, BLP_E_ARG, "blp_csr_info: null csr");
   if (n_nodes) *n_nodes = c->n;

@@ -84,6 +84,9 @@ int blp_csr_from_edges_device(int device, const int32_t* d_a, const int32_t* d_b
 typedef struct blp_csr blp_csr;
 int blp_csr_build_device(int device, const int32_t* d_a, const int32_t* d_b, int64_t m, int64_t n_nodes,
                          blp_csr** out);
+/* blp_csr_build_host: blp_csr_build_device from host-resident endpoints (uploaded first), e.g.
+ * the dense ids of a parsed graph.txt: the single-GPU load path of DeviceGraph.            */
+int blp_csr_build_host(int device, const int32_t* a, const int32_t* b, int64_t m, int64_t n_nodes, blp_csr** out);
 int blp_csr_info(const blp_csr* c, int64_t* n_nodes, int64_t* nnz);
 int blp_csr_fetch(const blp_csr* c, int64_t* row_ptr, int32_t* col_idx, uint8_t* self_loop);
 int blp_csr_destroy(blp_csr* c);

@@ -132,6 +132,39 @@ def test_device_graph_scores_match_oracle(gpu, knobs, monkeypatch):
         np.testing.assert_array_equal(v, H.score_pairs(x, y, 7)[k])
 
 
+@pytest.mark.parametrize("seed,sparse_ids", [(0, False), (1, True)])
+def test_device_graph_from_ids_device_csr(gpu, seed, sparse_ids, monkeypatch):
+    """DeviceGraph(a_ids, b_ids) -- similarity.main's graph.txt load -- builds large edge lists'
+    CSR on the device (blp_csr_build_host): id map, CSR, degrees, weights and scores equal the
+    host-CSR build of the same ids (duplicates, reversed duplicates, self-loops included)."""
+    rng = np.random.default_rng(seed)
+    n_users, n_bus = 30000, 900
+    a, c = _messy_edges(rng, n_users, n_bus, 200000)
+    if sparse_ids:  # original ids far apart: the sorted unique path and the searchsorted lookup
+        a = a.astype(np.int64) * 7919 + 10**9
+        c = c.astype(np.int64) * 7919 + 10**9
+    else:
+        a = a.astype(np.int64) + 12
+        c = c.astype(np.int64) + 12
+    monkeypatch.setenv("BLP_DEVICE_CSR_MIN", str(1 << 40))
+    H = blp.DeviceGraph(a, c, device=gpu)
+    monkeypatch.setenv("BLP_DEVICE_CSR_MIN", "1")
+    G = blp.DeviceGraph(a, c, device=gpu)
+    assert hasattr(G, "build_times") and not hasattr(H, "build_times")
+    for k in ("node_ids", "row_ptr", "col_idx", "self_loop", "degree", "aa_weight"):
+        assert np.array_equal(getattr(G, k), getattr(H, k)), k
+    assert G.n_col0 == H.n_col0 and G.n == H.n and G.self_loop.sum() > 0
+    users = rng.choice(G.node_ids[: G.n_col0][G.hop1_size[: G.n_col0] > 0], 60, replace=False)
+    x = np.repeat(G.dense(users), 20).astype(np.int32)
+    y = rng.integers(G.n_col0, G.n, len(x)).astype(np.int32)
+    y = y[G.hop1_size[y] > 0]
+    x = x[: len(y)]
+    for xs, ys, mask in ((x, y, 7), (y, x, 7)):
+        rg, rh = G.score_pairs(xs, ys, mask), H.score_pairs(xs, ys, mask)
+        for k in rg:
+            np.testing.assert_array_equal(rg[k], rh[k])
+
+
 def test_allgather_world1_on_device(gpu, monkeypatch):
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         monkeypatch.delenv(k, raising=False)

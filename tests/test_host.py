@@ -151,3 +151,15 @@ def test_sidecar_round_trips_the_score_file(case, name, tmp_path):
     for u in ref:
         assert list(got[u].items()) == list(ref[u].items())
         assert [type(v) for v in got[u].values()] == [type(v) for v in ref[u].values()]
+
+
+@pytest.mark.parametrize("span", [50, 10**6, 10**12])
+def test_unique_ids_match_numpy(span):
+    """blp.graph._unique (presence table for compact id spans) == np.unique."""
+    from blp.graph import _unique
+
+    rng = np.random.default_rng(span % 97)
+    for n in (0, 1, 1000, 200000):
+        x = rng.integers(-5, span, n).astype(np.int64) + 3
+        assert np.array_equal(_unique(x), np.unique(x))
+        assert _unique(x).dtype == np.int64
