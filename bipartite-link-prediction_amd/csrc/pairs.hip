@@ -25,6 +25,7 @@
 #include <algorithm>
 #include <cmath>
 #include <numeric>
+#include <thread>
 
 #include "blp_internal.h"
 
@@ -2385,47 +2386,80 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   const int64_t n = g->n;
   const int64_t* rp = g->hrp;
   const int32_t* ci = g->hci;
-  // ---- plan: node universe touched by H2(x) and N(y); per-source build work
-  int64_t lo = INT64_MAX, hi = INT64_MIN;
-  std::vector<uint8_t> seen((size_t)n, 0);
-  std::vector<int32_t> srcs;
-  std::vector<int64_t> work;
-  int64_t scan_work = 0, max_scan_row = 0, max_build_row = 0;
-  bool any_hot = false;
-  bool runs = !getenv("BLP_NO_RUNS");  // x non-decreasing: grouped by run heads (BLP_NO_RUNS: bucket sort)
-  int64_t rows_lo = INT64_MAX, rows_hi = INT64_MIN;  // nodes whose rows are read (the y and the z in N(x))
-  const int32_t* hot = g->h_hot_idx.empty() ? nullptr : g->h_hot_idx.data();
-  for (int64_t i = 0; i < n_pairs; ++i) {
-    const int32_t xi = x[i], yi = y[i];
-    if (xi < 0 || xi >= n || yi < 0 || yi >= n) return fail(BLP_E_ARG, "blp_batch_create: node id out of range");
-    runs = runs && (i == 0 || x[i - 1] <= xi);
-    if (rp[yi + 1] > rp[yi]) {
-      lo = std::min<int64_t>(lo, ci[rp[yi]]);
-      hi = std::max<int64_t>(hi, (int64_t)ci[rp[yi + 1] - 1] + 1);
+  // ---- plan: node universe touched by H2(x) and N(y); per-source build work. The pair and
+  // source loops gather rows at random (row_ptr / col_idx of the host mirror): several threads
+  // for large batches (the business side of config 2: 0.26 s on one thread).
+  struct Acc {
+    int64_t lo = INT64_MAX, hi = INT64_MIN, scan = 0, max_scan = 0, max_build = 0;
+    int64_t rows_lo = INT64_MAX, rows_hi = INT64_MIN;  // nodes whose rows are read (the y and the z in N(x))
+    bool bad = false, runs = true, any_hot = false;
+    void row(const int64_t* rp, const int32_t* ci, int64_t v) {
+      if (rp[v + 1] > rp[v]) {
+        lo = std::min<int64_t>(lo, ci[rp[v]]);
+        hi = std::max<int64_t>(hi, (int64_t)ci[rp[v + 1] - 1] + 1);
+      }
+      rows_lo = std::min<int64_t>(rows_lo, v);
+      rows_hi = std::max<int64_t>(rows_hi, v + 1);
     }
-    scan_work += rp[yi + 1] - rp[yi];
-    max_scan_row = std::max<int64_t>(max_scan_row, rp[yi + 1] - rp[yi]);
-    rows_lo = std::min<int64_t>(rows_lo, yi);
-    rows_hi = std::max<int64_t>(rows_hi, (int64_t)yi + 1);
-    if (!seen[xi]) {
-      seen[xi] = 1;
-      srcs.push_back(xi);
+    void merge(const Acc& o) {
+      lo = std::min(lo, o.lo), hi = std::max(hi, o.hi), scan += o.scan, max_scan = std::max(max_scan, o.max_scan);
+      max_build = std::max(max_build, o.max_build), rows_lo = std::min(rows_lo, o.rows_lo);
+      rows_hi = std::max(rows_hi, o.rows_hi), bad |= o.bad, runs &= o.runs, any_hot |= o.any_hot;
+    }
+  };
+  const int32_t* hot = g->h_hot_idx.empty() ? nullptr : g->h_hot_idx.data();
+  auto parallel = [](int64_t count, int64_t min_per_thread, auto body) {  // body(acc, begin, end)
+    const int nt = (int)std::max<int64_t>(1, std::min<int64_t>({16, (int64_t)std::thread::hardware_concurrency(),
+                                                                  count / std::max<int64_t>(min_per_thread, 1)}));
+    std::vector<Acc> acc(nt);
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) th.emplace_back(body, std::ref(acc[t]), count * t / nt, count * (t + 1) / nt);
+    body(acc[0], 0, count / nt);
+    for (auto& h : th) h.join();
+    for (int t = 1; t < nt; ++t) acc[0].merge(acc[t]);
+    return acc[0];
+  };
+  Acc A = parallel(n_pairs, 1 << 18, [&](Acc& a, int64_t i0, int64_t i1) {
+    for (int64_t i = i0; i < i1; ++i) {
+      const int32_t xi = x[i], yi = y[i];
+      if (xi < 0 || xi >= n || yi < 0 || yi >= n) {
+        a.bad = true;
+        return;
+      }
+      a.runs = a.runs && (i == 0 || x[i - 1] <= xi);
+      a.scan += rp[yi + 1] - rp[yi];
+      a.max_scan = std::max<int64_t>(a.max_scan, rp[yi + 1] - rp[yi]);
+      a.row(rp, ci, yi);
+    }
+  });
+  if (A.bad) return fail(BLP_E_ARG, "blp_batch_create: node id out of range");
+  std::vector<uint8_t> seen((size_t)n, 0);
+  std::vector<int32_t> srcs;  // in order of first appearance
+  for (int64_t i = 0; i < n_pairs; ++i)
+    if (!seen[x[i]]) {
+      seen[x[i]] = 1;
+      srcs.push_back(x[i]);
+    }
+  std::vector<int64_t> work(srcs.size());
+  A.merge(parallel((int64_t)srcs.size(), 1 << 12, [&](Acc& a, int64_t s0, int64_t s1) {
+    for (int64_t s = s0; s < s1; ++s) {
+      const int32_t xi = srcs[s];
       int64_t wsum = 0;
       for (int64_t k = rp[xi]; k < rp[xi + 1]; ++k) {
         const int32_t z = ci[k];
         wsum += rp[z + 1] - rp[z];
-        max_build_row = std::max<int64_t>(max_build_row, rp[z + 1] - rp[z]);
-        rows_lo = std::min<int64_t>(rows_lo, z);
-        rows_hi = std::max<int64_t>(rows_hi, (int64_t)z + 1);
-        any_hot |= hot && hot[z] >= 0;
-        if (rp[z + 1] > rp[z]) {
-          lo = std::min<int64_t>(lo, ci[rp[z]]);
-          hi = std::max<int64_t>(hi, (int64_t)ci[rp[z + 1] - 1] + 1);
-        }
+        a.max_build = std::max<int64_t>(a.max_build, rp[z + 1] - rp[z]);
+        a.any_hot |= hot && hot[z] >= 0;
+        a.row(rp, ci, z);
       }
-      work.push_back(wsum);
+      work[s] = wsum;
     }
-  }
+  }));
+  int64_t lo = A.lo, hi = A.hi;
+  const int64_t scan_work = A.scan, max_scan_row = A.max_scan, max_build_row = A.max_build;
+  const bool any_hot = A.any_hot;
+  bool runs = A.runs && !getenv("BLP_NO_RUNS");  // x non-decreasing: grouped by run heads (BLP_NO_RUNS: bucket sort)
+  const int64_t rows_lo = A.rows_lo, rows_hi = A.rows_hi;
   if (lo > hi) lo = hi = 0;
   lo &= ~int64_t(127);  // 128-bit aligned so dense rows map onto whole 16-byte LDS vectors
   blp_batch* b = new blp_batch();
