@@ -183,10 +183,16 @@ class DeviceGraph(HostGraph):
         # large edge lists: the CSR is built on the device (blp_csr_build_host: upload, radix
         # sort of the directed (row, col) keys, unique) and the host mirror fetched back --
         # the same CSR as blp_csr_from_edges (tests/test_gpu_ingest.py)
+        import time
+
+        t0 = time.perf_counter()
         da, db = self._ids(a_ids, b_ids)
+        t1 = time.perf_counter()
         c = ctypes.c_void_p()
         check(lib().blp_csr_build_host(device, ptr(da), ptr(db), len(da), self.n, ctypes.byref(c)))
+        t2 = time.perf_counter()
         self._adopt_csr(c, device, aa)
+        self.build_times.update({"id_map_s": t1 - t0, "device_csr_s": t2 - t1})
 
     @classmethod
     def from_csr(cls, row_ptr, col_idx, self_loop, n_col0, device=0, aa=True):

@@ -335,18 +335,43 @@ int blp_scores_write(const blp_examples* x, const char* path, int kind, const ui
   for (unsigned t = 1; t < nt; ++t) th.emplace_back(work, t);
   work(0);
   for (auto& h : th) h.join();
-  FILE* f = fopen(path, "wb");
-  if (!f) return fail(BLP_E_ARG, std::string("blp_scores_write: cannot open ") + path);
-  bool ok = fputc('{', f) != EOF;
+  // "{" part ", " part ... "}": every slice written at its own offset, concurrently (one
+  // sequential fwrite of ~200 MB per file at config 2 dominated the file phase)
+  const int fd = open(path, O_WRONLY | O_CREAT | O_TRUNC, 0666);
+  if (fd < 0) return fail(BLP_E_ARG, std::string("blp_scores_write: cannot open ") + path);
+  std::vector<int64_t> at(nt, 0);
+  int64_t pos = 1;
   bool any = false;
-  for (unsigned t = 0; t < nt && ok; ++t) {
+  for (unsigned t = 0; t < nt; ++t) {
     if (!nonempty[t]) continue;
-    if (any) ok = fwrite(", ", 1, 2, f) == 2;
-    ok = ok && fwrite(part[t].data(), 1, part[t].size(), f) == part[t].size();
+    if (any) pos += 2;
+    at[t] = pos;
+    pos += (int64_t)part[t].size();
     any = true;
   }
-  ok = ok && fputc('}', f) != EOF;
-  ok = (fclose(f) == 0) && ok;
+  auto put = [fd](const char* p, int64_t len, int64_t off) {
+    while (len > 0) {
+      const ssize_t w = pwrite(fd, p, (size_t)std::min<int64_t>(len, int64_t(1) << 30), (off_t)off);
+      if (w <= 0) return false;
+      p += w, len -= w, off += w;
+    }
+    return true;
+  };
+  std::vector<uint8_t> wok(nt, 1);
+  th.clear();
+  bool sep = false;
+  for (unsigned t = 0; t < nt; ++t) {
+    if (!nonempty[t]) continue;
+    const bool with_sep = sep;
+    sep = true;
+    th.emplace_back([&, t, with_sep]() {
+      wok[t] = (!with_sep || put(", ", 2, at[t] - 2)) && put(part[t].data(), (int64_t)part[t].size(), at[t]);
+    });
+  }
+  bool ok = put("{", 1, 0) && put("}", 1, pos);
+  for (auto& h : th) h.join();
+  for (unsigned t = 0; t < nt; ++t) ok = ok && wok[t];
+  ok = (close(fd) == 0) && ok;
   return ok ? BLP_OK : fail(BLP_E_ARG, std::string("blp_scores_write: write failed: ") + path);
 }
 
