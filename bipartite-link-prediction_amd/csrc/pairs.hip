@@ -1880,10 +1880,14 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
   __shared__ int s_item;
   __shared__ int s_nhot;
   __shared__ blp::HotRow s_hot[HOT_LIST];
+  __shared__ long long s_wtab[RCS ? 256 : 1];  // code weights in LDS (the 64 KiB variant has no room)
   const int64_t CAP_BITS = a.cap_bits;
   const bool want_j = (a.mask & BLP_JACCARD) != 0;
   const bool want_a = (a.mask & BLP_ADAMIC) != 0;
   uint4* bm4 = reinterpret_cast<uint4*>(bm);
+  if (RCS && a.wtab)  // visible after the first barrier
+    for (int i = threadIdx.x; i < 256; i += BLOCK) s_wtab[i] = a.wtab[i];
+  const long long* wtab = RCS ? s_wtab : a.wtab;
   if (RCS)  // the zero word and the build's dummy words past the bitmap
     for (int i = threadIdx.x; i < RC_EXTRA_WORDS; i += BLOCK) bm[CAP_WORDS + i] = 0;
   const int64_t n_items = (int64_t)a.misc->n_active * C;
@@ -2000,10 +2004,10 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
         rc_chunk_offsets<BLOCK, K>(s_off, ns, s_coff, red);
         const int shift = build_hint<BLOCK, HCS>(s_coff, ns, BLOCK, s_hint);
         if (want_a)
-          rc_scan<BLOCK, K, true>(a.cw, a.idmask, a.idbits, a.aaw, a.wtab, s_start, s_off, s_coff, ns, c0, width, bm,
+          rc_scan<BLOCK, K, true>(a.cw, a.idmask, a.idbits, a.aaw, wtab, s_start, s_off, s_coff, ns, c0, width, bm,
                                   CAP_WORDS, nullptr, s_aa, threadIdx.x, s_hint, shift, true);
         else
-          rc_scan<BLOCK, K, false>(a.cw, a.idmask, a.idbits, a.aaw, a.wtab, s_start, s_off, s_coff, ns, c0, width, bm,
+          rc_scan<BLOCK, K, false>(a.cw, a.idmask, a.idbits, a.aaw, wtab, s_start, s_off, s_coff, ns, c0, width, bm,
                                    CAP_WORDS, nullptr, s_aa, threadIdx.x, s_hint, shift, true);
       } else if (want_a) {
         mp_scan<BLOCK, K, true, true>(a.cw, a.idmask, a.idbits, a.aaw, a.wtab, s_start, s_off, ns, c0, width, bm,
