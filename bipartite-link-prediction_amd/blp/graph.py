@@ -42,6 +42,12 @@ def aa_weights_from_degree(deg):
     out = np.zeros(len(deg), np.float64)
     if len(deg) == 0:
         return out
+    dmax = int(deg.max())
+    if int(deg.min()) >= 0 and dmax <= max(4 * len(deg), 1 << 20):  # one table over 0..max degree
+        table = np.zeros(dmax + 1, np.float64)
+        for d in np.flatnonzero(np.bincount(deg)):
+            table[d] = (math.log(int(d)) ** -1) if d > 1 else 0.0
+        return table[deg]
     uniq, inv = np.unique(deg, return_inverse=True)
     table = np.array([(math.log(int(d)) ** -1) if d > 1 else 0.0 for d in uniq], np.float64)
     return table[inv]
