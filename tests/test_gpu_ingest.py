@@ -165,6 +165,42 @@ def test_device_graph_from_ids_device_csr(gpu, seed, sparse_ids, monkeypatch):
             np.testing.assert_array_equal(rg[k], rh[k])
 
 
+def test_csr_build_host_entry_point(gpu):
+    """blp_csr_build_host: host endpoints -> device CSR, equal to the host builder; empty edge
+    lists and self-loop-only lists; out-of-range ids rejected with BLP_E_ARG."""
+    L, P = blp.lib(), blp._lib.ptr
+
+    def build(a, c, n):
+        A = np.ascontiguousarray(a, np.int32)
+        C = np.ascontiguousarray(c, np.int32)
+        h = ctypes.c_void_p()
+        blp._lib.check(L.blp_csr_build_host(gpu, P(A) if len(A) else None, P(C) if len(C) else None, len(A), n,
+                                            ctypes.byref(h)))
+        try:
+            nn, nnz = ctypes.c_int64(), ctypes.c_int64()
+            blp._lib.check(L.blp_csr_info(h, ctypes.byref(nn), ctypes.byref(nnz)))
+            rp = np.empty(n + 1, np.int64)
+            ci = np.empty(max(nnz.value, 1), np.int32)
+            sl = np.empty(max(n, 1), np.uint8)
+            blp._lib.check(L.blp_csr_fetch(h, P(rp), P(ci), P(sl)))
+            return rp, ci[: nnz.value], sl[:n]
+        finally:
+            L.blp_csr_destroy(h)
+
+    rng = np.random.default_rng(11)
+    a, c = _messy_edges(rng, 5000, 300, 40000)
+    got = build(a, c, 5300)
+    for g_, e_ in zip(got, _host_csr(5300, a, c)):
+        assert np.array_equal(g_, e_)
+    rp, ci, sl = build([], [], 4)
+    assert rp.tolist() == [0] * 5 and len(ci) == 0 and sl.tolist() == [0] * 4
+    rp, ci, sl = build([1, 3], [1, 3], 4)
+    assert rp.tolist() == [0] * 5 and sl.tolist() == [0, 1, 0, 1]
+    with pytest.raises(blp.BLPError) as e:
+        build([0, 7], [1, 2], 5)
+    assert e.value.code == -1
+
+
 def test_allgather_world1_on_device(gpu, monkeypatch):
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         monkeypatch.delenv(k, raising=False)
