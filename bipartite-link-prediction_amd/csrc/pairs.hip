@@ -209,7 +209,7 @@ __global__ __launch_bounds__(GB_BLOCK) void k_bucket_group(const int64_t* __rest
                                                            int32_t* __restrict__ cnt, int32_t* __restrict__ bucket_active,
                                                            int32_t* __restrict__ g_out, int64_t* __restrict__ g_yb,
                                                            int32_t* __restrict__ g_yl, int32_t* __restrict__ g_y) {
-  constexpr int PER = KEYS / GB_BLOCK;
+  constexpr int PER = KEYS >= GB_BLOCK ? KEYS / GB_BLOCK : 1;  // KEYS < GB_BLOCK: threads >= KEYS idle
   __shared__ int h[KEYS];
   __shared__ int red[GB_BLOCK / 64];
   const int b = blockIdx.x;
@@ -237,7 +237,8 @@ __global__ __launch_bounds__(GB_BLOCK) void k_bucket_group(const int64_t* __rest
   __syncthreads();
   int v = 0, act = 0;
   for (int q = 0; q < PER; ++q) {
-    const int c = h[threadIdx.x * PER + q];
+    const int j = threadIdx.x * PER + q;
+    const int c = j < KEYS ? h[j] : 0;
     v += c;
     act += c > 0;
   }
@@ -245,7 +246,7 @@ __global__ __launch_bounds__(GB_BLOCK) void k_bucket_group(const int64_t* __rest
   int o = block_exscan_i<GB_BLOCK>(v, red, &tot);
   int acts;
   block_exscan_i<GB_BLOCK>(act, red, &acts);
-  for (int q = 0; q < PER; ++q) {
+  for (int q = 0; q < PER && threadIdx.x * PER + q < KEYS; ++q) {
     const int j = threadIdx.x * PER + q;
     const int c = h[j];
     if (j < nk) {
@@ -375,7 +376,7 @@ template <int KEYS>
 __global__ __launch_bounds__(GB_BLOCK) void k_active_write(const int32_t* __restrict__ cnt,
                                                            const int32_t* __restrict__ abase, int shift, int32_t xlo,
                                                            int64_t xspan, int32_t* __restrict__ active) {
-  constexpr int PER = KEYS / GB_BLOCK;
+  constexpr int PER = KEYS >= GB_BLOCK ? KEYS / GB_BLOCK : 1;  // j < nk <= KEYS guards the rest
   __shared__ int red[GB_BLOCK / 64];
   const int b = blockIdx.x;
   const int64_t k0 = (int64_t)xlo + ((int64_t)b << shift);
@@ -2754,7 +2755,9 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
                      b->nblk, b->nb, b->shift, b->xlo, b->xspan, np, b->off.as<int32_t>(), b->cnt.as<int32_t>(), bact,  \
                      b->d_gout,                                                                                       \
                      b->d_gyb, b->d_gyl, b->d_gy)
-    if (keys <= 256)
+    if (keys <= 64)  // 272 bytes of LDS: fits beside a 160 KiB large-scorer workgroup
+      BLP_GROUP_LAUNCH(64);
+    else if (keys <= 256)
       BLP_GROUP_LAUNCH(256);
     else if (keys <= 1024)
       BLP_GROUP_LAUNCH(1024);
@@ -2770,7 +2773,9 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
 #define BLP_ACTIVE_LAUNCH(K)                                                                                   \
   hipLaunchKernelGGL(k_active_write<K>, dim3(b->nb), dim3(GB_BLOCK), 0, b->stream, b->cnt.as<int32_t>(), abase, b->shift, \
                      b->xlo, b->xspan, b->active.as<int32_t>())
-    if (keys <= 256)
+    if (keys <= 64)  // 272 bytes of LDS: fits beside a 160 KiB large-scorer workgroup
+      BLP_ACTIVE_LAUNCH(64);
+    else if (keys <= 256)
       BLP_ACTIVE_LAUNCH(256);
     else if (keys <= 1024)
       BLP_ACTIVE_LAUNCH(1024);

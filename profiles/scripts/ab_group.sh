@@ -4,6 +4,8 @@
 set -o pipefail
 mkdir -p gpurun_out
 cd "$GRAFT_REPO_ROOT" || exit 1
+timeout -k 10 300 python -u -m pytest tests/test_gpu_similarity.py -x -q --timeout 120 --timeout-method thread > gpurun_out/ab_group_tests.log 2>&1 || { tail -30 gpurun_out/ab_group_tests.log; exit 1; }
+tail -1 gpurun_out/ab_group_tests.log
 run() {  # name, lib, extra args
   BLP_LIB=$PWD/bipartite-link-prediction_amd/blp/$2 timeout -k 10 300 python bench.py --no-cpu-baseline "${@:3}" \
     > gpurun_out/ab_$1.json 2> gpurun_out/ab_$1.err || { tail -30 gpurun_out/ab_$1.err; exit 1; }
