@@ -425,8 +425,16 @@ template <int METHOD>
 __device__ long long sel_counts(const TkArgs& a, TkShared& s, int it, const TkChunk& c, long long h2, bool count) {
   sel_begin(a, s, METHOD, it);
   long long nc = 0;
-  for (int64_t base = c.c0; base < c.c1; base += TK_NT) {
-    const int64_t p = base + threadIdx.x;
+  // the next round's target ids (and degrees) are loaded while this round is offered: each
+  // round ends in barriers, so a load issued in the round that uses it costs a full L2 round
+  // trip per round (~100 rounds per method at config 3)
+  int64_t p = c.c0 + threadIdx.x;
+  int inv_c = p < c.c1 ? a.inv[p] : 0;
+  int deg_c = METHOD == 1 && p < c.c1 ? a.tdeg[p] : 0;
+  for (int64_t base = c.c0; base < c.c1; base += TK_NT, p += TK_NT) {
+    const int64_t pn = p + TK_NT;
+    const int inv_n = pn < c.c1 ? a.inv[pn] : 0;
+    const int deg_n = METHOD == 1 && pn < c.c1 ? a.tdeg[pn] : 0;
     bool ok = false;
     unsigned long long key = 0;
     int col = 0;
@@ -438,28 +446,52 @@ __device__ long long sel_counts(const TkArgs& a, TkShared& s, int it, const TkCh
         if (METHOD == 0) {
           key = cnt;
         } else {
-          const double jac = (double)cnt / (double)(h2 + (long long)a.tdeg[p] - (long long)cnt);
+          const double jac = (double)cnt / (double)(h2 + (long long)deg_c - (long long)cnt);
           key = (unsigned long long)__double_as_longlong(jac);
         }
-        col = a.inv[p];
+        col = inv_c;
       }
     }
     sel_offer(s, ok, key, col);
     sel_round_end(a, s);
+    inv_c = inv_n;
+    deg_c = deg_n;
   }
   sel_end(a, s, METHOD, it);
   return nc;
 }
 
+#ifdef BLP_PROF  // experiment builds only: per-phase clock sums of thread 0 (blp_topk_prof_read)
+__device__ unsigned long long g_tkprof[16];
+#define TKP_INIT                          \
+  unsigned long long tkp_t0 = clock64();  \
+  unsigned long long tkp_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define TKP(i)                                 \
+  {                                            \
+    const unsigned long long t1_ = clock64();  \
+    tkp_acc[i] += t1_ - tkp_t0;                \
+    tkp_t0 = t1_;                              \
+  }
+#define TKP_FLUSH \
+  if (tid == 0)   \
+    for (int i_ = 0; i_ < 8; ++i_) atomicAdd(&g_tkprof[i_], tkp_acc[i_]);
+#else
+#define TKP_INIT
+#define TKP(i)
+#define TKP_FLUSH
+#endif
+
 __global__ __launch_bounds__(TK_NT) void k_topk(TkArgs a) {
   __shared__ TkShared s;
   const int tid = threadIdx.x;
   unsigned long long* acc64 = reinterpret_cast<unsigned long long*>(s.acc);
+  TKP_INIT
   for (;;) {
     __syncthreads();
     if (tid == 0) s.item = (int)atomicAdd(&a.counters[0], 1ull);
     __syncthreads();
     const int it = s.item;
+    TKP(0)
     if (it >= a.n_src) break;
     const int x = a.src[it];
     const int64_t xb = a.rp[x];
@@ -482,9 +514,11 @@ __global__ __launch_bounds__(TK_NT) void k_topk(TkArgs a) {
       const int words = fused ? (int)(a.h_word + 4 * a.H) : (int)((c.a1 - c.a0 + 3) >> 2);
       for (int i = tid; i < words; i += TK_NT) s.acc[i] = 0;
       __syncthreads();
+      TKP(1)
       long long np = 0;
       const long long h = fused ? push_pass<3>(a, s, x, xb, du, rowx, c, 0, 0, 0, ci == 0, &np)
                                 : push_pass<0>(a, s, x, xb, du, rowx, c, 0, 0, 0, ci == 0, &np);
+      TKP(2)
       if (ci == 0) {
         h2 = block_sum(s, h);
         np = block_sum(s, np);
@@ -500,6 +534,7 @@ __global__ __launch_bounds__(TK_NT) void k_topk(TkArgs a) {
       __syncthreads();
       if (want_cn) ncand += sel_counts<0>(a, s, it, c, h2, true);
       if (want_j) ncand += sel_counts<1>(a, s, it, c, h2, !want_cn);
+      TKP(3)
     }
     ncand = block_sum(s, ncand);
     if (want_aa && ncand > 0) {
@@ -533,6 +568,7 @@ __global__ __launch_bounds__(TK_NT) void k_topk(TkArgs a) {
           sel_end(a, s, 2, it);
           if (tid == 0) atomicAdd(&a.counters[5], 1ull);
           done = true;
+          TKP(4)
         } else if (nc <= a.hcap) {
           for (int i = tid; i < TK_SEL; i += TK_NT) {
             s.col[i] = (int32_t)TK_EMPTY;
@@ -581,6 +617,7 @@ __global__ __launch_bounds__(TK_NT) void k_topk(TkArgs a) {
           }
           if (tid == 0) atomicAdd(&a.counters[1], 1ull);
           done = true;
+          TKP(5)
         }
       }
       if (!done) {
@@ -604,6 +641,7 @@ __global__ __launch_bounds__(TK_NT) void k_topk(TkArgs a) {
           sel_end(a, s, 2, it);
         }
         if (tid == 0) atomicAdd(&a.counters[2], 1ull);
+        TKP(6)
       }
     }
     // pad the unused tail of each list
@@ -615,12 +653,23 @@ __global__ __launch_bounds__(TK_NT) void k_topk(TkArgs a) {
       }
     }
     if (tid == 0) a.ncand[it] = ncand;
+    TKP(7)
   }
+  TKP_FLUSH
 }
 
 }  // namespace
 
 using namespace blp;
+
+#ifdef BLP_PROF
+extern "C" int blp_topk_prof_read(unsigned long long* out) {  // experiment builds only; then reset
+  BLP_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tkprof), sizeof(unsigned long long) * 16));
+  unsigned long long z[16] = {0};
+  BLP_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_tkprof), z, sizeof(z)));
+  return BLP_OK;
+}
+#endif
 
 struct blp_topk {
   blp_graph* g = nullptr;
