@@ -425,6 +425,8 @@ template <int METHOD>
 __device__ long long sel_counts(const TkArgs& a, TkShared& s, int it, const TkChunk& c, long long h2, bool count) {
   sel_begin(a, s, METHOD, it);
   long long nc = 0;
+  if (count)  // targets with a count (the chunk's share of |H3(x)|): all of them, before the pruned walk
+    for (int64_t q = c.c0 + threadIdx.x; q < c.c1; q += TK_NT) nc += acc_get(a, s.acc, c, addr_of(a, q)) > 0;
   // the next round's target ids (and degrees) are loaded while this round is offered: each
   // round ends in barriers, so a load issued in the round that uses it costs a full L2 round
   // trip per round (~100 rounds per method at config 3)
@@ -442,7 +444,6 @@ __device__ long long sel_counts(const TkArgs& a, TkShared& s, int it, const TkCh
       const uint32_t cnt = acc_get(a, s.acc, c, addr_of(a, p));
       ok = cnt > 0;
       if (ok) {
-        nc += count;
         if (METHOD == 0) {
           key = cnt;
         } else {
@@ -456,6 +457,19 @@ __device__ long long sel_counts(const TkArgs& a, TkShared& s, int it, const TkCh
     sel_round_end(a, s);
     inv_c = inv_n;
     deg_c = deg_n;
+    // Pruning: targets are in degree order (descending), and a target of degree d scores at
+    // most CN = d, Jaccard = d / |H2| (once d <= |H2|; c / (|H2| + d - c) grows with c <= d,
+    // and the rounded quotients keep that order). Once that bound is below the current k-th
+    // key -- strictly, so no tie can still win on the id -- no later target can enter the list.
+    // The decision is uniform: shared threshold, the same degree load in every thread.
+    const int64_t pn0 = base + TK_NT;
+    if (pn0 < c.c1 && s.have_thr) {
+      const long long d = a.tdeg[pn0];
+      const bool stop = METHOD == 0 ? (unsigned long long)d < s.thr_key
+                                    : h2 > 0 && d <= h2 &&
+                                          (unsigned long long)__double_as_longlong((double)d / (double)h2) < s.thr_key;
+      if (stop) break;
+    }
   }
   sel_end(a, s, METHOD, it);
   return nc;

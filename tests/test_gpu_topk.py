@@ -82,6 +82,24 @@ def test_topk_u32_tier_and_multi_chunk(small, monkeypatch):
     assert T2.stats(2)[1] == len(src)  # every source took the direct Adamic-Adar path
 
 
+@pytest.mark.parametrize("acc_words", [None, "600"])
+def test_topk_selection_pruning_many_targets(gpu, monkeypatch, acc_words):
+    """More targets than one selection round (1,024): the CN and Jaccard walks stop once the
+    degree bound falls below the k-th key. Many equal degrees and equal counts (ties broken by
+    id), k = 1, 5 and 20; with a small counter space the bound is applied per chunk."""
+    rng = np.random.default_rng(21)
+    a, b = bipartite_edges(rng, 20000, 5000, 120000, zipf=0.5)
+    G = blp.DeviceGraph(a, b, device=gpu)
+    adj = adj_of(a, b)
+    if acc_words:
+        monkeypatch.setenv("BLP_TOPK_ACC_WORDS", acc_words)
+    T = blp.TopK(G, "user")
+    assert (T.info()["chunks"] > 1) == (acc_words is not None)
+    src = rng.choice(np.flatnonzero(G.hop1_size[: G.n_col0] > 1), 12, replace=False)
+    for k in (1, 5, 20):
+        check_against_oracle(G, T, adj, src, k, mask=blp.CN | blp.JACCARD, methods=METHODS[:2])
+
+
 def test_topk_unfused_matches_oracle(small, monkeypatch):
     G, adj, rng = small
     monkeypatch.setenv("BLP_TOPK_NO_FUSE", "1")
