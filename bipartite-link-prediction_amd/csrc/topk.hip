@@ -67,6 +67,8 @@ struct TkArgs {
   int64_t n32, n16, A16, A8;  // counter tiers (see TkChunk)
   const int32_t* inv;   // [T] permuted id -> dense target id
   const int32_t* tdeg;  // [T] |N(b)| by permuted id
+  const int32_t* ge;    // [ge_n] ge[d] = number of targets of degree >= d (a prefix of the permuted order)
+  int64_t ge_n;
   const long long* wtab;  // Adamic-Adar weight (fixed point) of a source by its degree
   const int64_t* x2_off;  // [target-side CSR entries + 1] start of each wedge row in x2 (or null)
   const int32_t* x2;      // wedge rows: for each target b' and member w of N(b'), N'(w)
@@ -561,7 +563,9 @@ __global__ __launch_bounds__(TK_NT) void k_topk(TkArgs a) {
           thr = (uint32_t)max(1.0, floor((double)cnt_k * a.ratio * (1.0 - 1e-9)));
         }
         long long nc = 0, nc_out = 0;
-        for (int64_t p = c.c0 + tid; p < c.c1; p += TK_NT) {
+        // a count >= thr needs degree >= thr: only the prefix of the degree order can qualify
+        const int64_t pcut = min(c.c1, thr < a.ge_n ? (int64_t)a.ge[thr] : (int64_t)0);
+        for (int64_t p = c.c0 + tid; p < pcut; p += TK_NT) {
           const bool hit = acc_get(a, s.acc, c, addr_of(a, p)) >= thr;
           nc += hit;
           nc_out += hit && p >= a.H;
@@ -589,7 +593,7 @@ __global__ __launch_bounds__(TK_NT) void k_topk(TkArgs a) {
             s.key[i] = 0;
           }
           __syncthreads();
-          for (int64_t p = c.c0 + tid; p < c.c1; p += TK_NT) {
+          for (int64_t p = c.c0 + tid; p < pcut; p += TK_NT) {
             const int32_t e = (int32_t)addr_of(a, p);
             if (acc_get(a, s.acc, c, e) >= thr) {
               int h = hash_slot(e);
@@ -692,12 +696,13 @@ struct blp_topk {
   int64_t n32 = 0, n16 = 0;  // tier boundaries in permuted order
   int64_t A16 = 0, A8 = 0;   // byte addresses where the u16 / u8 tiers start
   int64_t H = 0, AH = 0, h_word = 0;  // fused AA targets
+  int64_t ge_n = 0;                   // entries of ge (degree -> prefix length)
   int64_t acc_words = TK_ACC_WORDS;
   double ratio = 0.0;
   bool have_aa = false;
   std::vector<TkChunk> chunks;
   int64_t aa_chunk = 0;
-  DevBuf perm, inv, tdeg, pci, d_chunks, src, keys, cols, ncand, counters, wtab, x2_off, x2;
+  DevBuf perm, inv, tdeg, ge, pci, d_chunks, src, keys, cols, ncand, counters, wtab, x2_off, x2;
   int64_t kbase = 0, x2_entries = -1;
   int64_t n_src = 0;
   int k = 0;
@@ -884,6 +889,13 @@ extern "C" int blp_topk_create(blp_graph* g, int64_t src_lo, int64_t src_hi, int
   }
   t->kbase = kbase;
   t->x2_entries = x2.empty() ? -1 : x2_off[mt];
+  // ge[d] = targets of degree >= d, d in [0, max degree + 1] (degrees are non-increasing in p)
+  std::vector<int32_t> ge((size_t)(T ? tdeg[0] : 0) + 2, 0);
+  for (int64_t d = 0, j = T; d < (int64_t)ge.size(); ++d) {
+    while (j > 0 && tdeg[j - 1] < d) --j;
+    ge[d] = (int32_t)j;
+  }
+  t->ge_n = (int64_t)ge.size();
   plan_chunks(t);
   auto up = [&](DevBuf& b, const void* h, size_t bytes) -> int {
     int r = b.reserve(bytes);
@@ -892,7 +904,7 @@ extern "C" int blp_topk_create(blp_graph* g, int64_t src_lo, int64_t src_hi, int
     return BLP_OK;
   };
   if ((rc = up(t->perm, paddr.data(), 4 * T)) || (rc = up(t->inv, inv.data(), 4 * T)) ||
-      (rc = up(t->tdeg, tdeg.data(), 4 * T)) || (rc = up(t->pci, pci.data(), 4 * pci.size())) ||
+      (rc = up(t->tdeg, tdeg.data(), 4 * T)) || (rc = up(t->ge, ge.data(), 4 * ge.size())) || (rc = up(t->pci, pci.data(), 4 * pci.size())) ||
       (rc = up(t->d_chunks, t->chunks.data(), sizeof(TkChunk) * t->chunks.size())) ||
       (rc = up(t->wtab, wtab.data(), 8 * wtab.size())) ||
       (!x2.empty() && ((rc = up(t->x2_off, x2_off.data(), 8 * x2_off.size())) ||
@@ -908,7 +920,7 @@ extern "C" int blp_topk_create(blp_graph* g, int64_t src_lo, int64_t src_hi, int
 extern "C" int blp_topk_destroy(blp_topk* t) {
   if (!t) return BLP_OK;
   (void)set_device(t->g);
-  for (DevBuf* b : {&t->perm, &t->inv, &t->tdeg, &t->pci, &t->d_chunks, &t->src, &t->keys, &t->cols, &t->ncand,
+  for (DevBuf* b : {&t->perm, &t->inv, &t->tdeg, &t->ge, &t->pci, &t->d_chunks, &t->src, &t->keys, &t->cols, &t->ncand,
                     &t->counters, &t->wtab, &t->x2_off, &t->x2})
     b->release();
   timer_release(t->timer);
@@ -967,6 +979,8 @@ extern "C" int blp_topk_run(blp_topk* t, int k, uint32_t mask) {
   a.A8 = t->A8;
   a.inv = t->inv.as<int32_t>();
   a.tdeg = t->tdeg.as<int32_t>();
+  a.ge = t->ge.as<int32_t>();
+  a.ge_n = t->ge_n;
   a.wtab = t->wtab.as<long long>();
   a.x2_off = t->x2_entries >= 0 ? t->x2_off.as<int64_t>() : nullptr;
   a.x2 = t->x2_entries >= 0 ? t->x2.as<int32_t>() : nullptr;
