@@ -54,6 +54,7 @@ SIGNATURES = {
     "blp_csr_destroy": [_P],
     "blp_graph_create_from_csr": [_P, _P, _P, _P, _PP],
     "blp_graph_destroy": [_P],
+    "blp_graph_wedge": [_P, ctypes.POINTER(ctypes.c_int64), _P, _P],
     "blp_graph_info": [_P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
                        ctypes.POINTER(ctypes.c_int)],
     "blp_graph_sync": [_P],

@@ -19,36 +19,49 @@
 
 namespace {
 
-// One wave per node x: the rows N(z), z in N(x), back to back from the device CSR. The wave
-// takes 64 of x's neighbours at a time (their row offsets in one load), then copies their rows
-// one after another, one id per lane (rows hold <= SHORT_ROW_MAX < 64 ids), and pads the last
-// vector with a repeat of the last id.
-__global__ __launch_bounds__(256) void k_wedge_fill(const int64_t* __restrict__ rp, const int32_t* __restrict__ ci,
-                                                    const int64_t* __restrict__ wp, int64_t n, int32_t* __restrict__ w) {
-  const int lane = threadIdx.x & 63;
-  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
-  for (int64_t x = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); x < n; x += nwaves) {
-    int64_t pos = 4 * wp[x];
+// One workgroup per node x: the rows N(z), z in N(x), back to back from the device CSR. Each
+// round takes 256 of x's neighbours, one per thread: a block scan of their row lengths gives
+// every row its offset, then each thread copies its own row (<= SHORT_ROW_MAX ids). The last
+// vector is padded with a repeat of the last id. (One wave per node walking N(x) serially took
+// 86 ms at config 2: the most reviewed business alone has ~10^5 neighbours.)
+constexpr int WF_BLOCK = 256;
+__global__ __launch_bounds__(WF_BLOCK) void k_wedge_fill(const int64_t* __restrict__ rp, const int32_t* __restrict__ ci,
+                                                         const int64_t* __restrict__ wp, int64_t n, int32_t* __restrict__ w) {
+  __shared__ int red[WF_BLOCK / 64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int64_t x = blockIdx.x; x < n; x += gridDim.x) {
+    int64_t base = 4 * wp[x];
     const int64_t end = 4 * wp[x + 1];
-    if (pos == end) continue;
+    if (base == end) continue;  // uniform over the block
     const int64_t kb = rp[x], ke = rp[x + 1];
-    int32_t last = 0;
-    for (int64_t k0 = kb; k0 < ke; k0 += 64) {
-      const bool in = k0 + lane < ke;
-      const int32_t z = in ? ci[k0 + lane] : 0;
+    for (int64_t k0 = kb; k0 < ke; k0 += WF_BLOCK) {
+      const int64_t k = k0 + threadIdx.x;
+      const bool in = k < ke;
+      const int32_t z = in ? ci[k] : 0;
       const int64_t zb = in ? rp[z] : 0;
       const int d = in ? (int)(rp[z + 1] - zb) : 0;
-      const int cnt = (int)min<int64_t>(64, ke - k0);
-      for (int j = 0; j < cnt; ++j) {
-        const int64_t b = __shfl(zb, j, 64);
-        const int dj = __shfl(d, j, 64);
-        const int32_t v = lane < dj ? ci[b + lane] : 0;
-        if (lane < dj) w[pos + lane] = v;
-        if (dj) last = __shfl(v, dj - 1, 64);
-        pos += dj;
+      int inc = d;  // block exclusive scan of d
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += t;
       }
+      if (lane == 63) red[wid] = inc;
+      __syncthreads();
+      int before = 0, tot = 0;
+#pragma unroll
+      for (int q = 0; q < WF_BLOCK / 64; ++q) {
+        before += q < wid ? red[q] : 0;
+        tot += red[q];
+      }
+      __syncthreads();  // red is reused by the next round
+      const int64_t at = base + before + inc - d;
+      for (int j = 0; j < d; ++j) w[at + j] = ci[zb + j];
+      base += tot;
     }
-    if (lane < end - pos) w[pos + lane] = last;
+    __syncthreads();  // the block's row writes are visible to the block
+    if (threadIdx.x < end - base) w[base + threadIdx.x] = w[base - 1];
+    __syncthreads();
   }
 }
 
@@ -102,7 +115,7 @@ int build_wedge_index(blp_graph* g) {
   BLP_HIP(hipMalloc(&g->d_wp, sizeof(int64_t) * (n + 1)));
   BLP_HIP(hipMalloc(&g->d_wedge, sizeof(int32_t) * 4 * total));
   BLP_HIP(hipMemcpy(g->d_wp, wp.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice));
-  hipLaunchKernelGGL(k_wedge_fill, dim3((unsigned)std::min<int64_t>(8192, (n + 3) / 4)), dim3(256), 0, g->stream,
+  hipLaunchKernelGGL(k_wedge_fill, dim3((unsigned)std::min<int64_t>(16384, n)), dim3(WF_BLOCK), 0, g->stream,
                      g->d_rp, g->d_ci, g->d_wp, n, g->d_wedge);
   BLP_HIP(hipGetLastError());
   BLP_HIP(hipStreamSynchronize(g->stream));
@@ -121,3 +134,17 @@ void free_wedge_index(blp_graph* g) {
 }
 
 }  // namespace blp
+
+// The wedge-row index of a graph (tests and tools): its vector count (-1: not built), and
+// optionally the offsets [n + 1] (in 16-byte vectors) and the ids [4 * n_vecs].
+extern "C" int blp_graph_wedge(const blp_graph* g, int64_t* n_vecs, int64_t* wp, int32_t* wedge) {
+  BLP_CHECK(g && n_vecs, BLP_E_ARG, "blp_graph_wedge: bad arguments");
+  *n_vecs = g->d_wp ? g->wedge_vecs : -1;
+  if (!g->d_wp) return BLP_OK;
+  BLP_HIP(hipSetDevice(g->device));
+  if (wp) BLP_HIP(hipMemcpy(wp, g->d_wp, sizeof(int64_t) * (g->n + 1), hipMemcpyDeviceToHost));
+  if (wedge && g->wedge_vecs)
+    BLP_HIP(hipMemcpy(wedge, g->d_wedge, sizeof(int32_t) * 4 * g->wedge_vecs, hipMemcpyDeviceToHost));
+  return BLP_OK;
+}
+

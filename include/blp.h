@@ -135,6 +135,11 @@ int blp_scores_write(const blp_examples* e, const char* path, int kind, const ui
 int blp_graph_create(const int64_t* row_ptr, const int32_t* col_idx, int64_t n_nodes,
                      const double* aa_weight, int device, blp_graph** out);
 int blp_graph_destroy(blp_graph* g);
+/* blp_graph_wedge: the graph's wedge-row index (the short-row scorer's second layout: for
+ * each node x whose neighbours' rows are all short, the rows N(z), z in N(x), back to back,
+ * padded to whole 16-byte vectors with a repeat of the last id). *n_vecs = its size in vectors
+ * (-1: not built); wp [n + 1] (vector offsets) and wedge [4 * n_vecs] may be NULL.         */
+int blp_graph_wedge(const blp_graph* g, int64_t* n_vecs, int64_t* wp, int32_t* wedge);
 int blp_graph_info(const blp_graph* g, int64_t* n_nodes, int64_t* nnz, int* device);
 int blp_graph_sync(blp_graph* g); /* wait for all work queued on the handle's stream */
 /* Fixed-point scale of the Adamic-Adar terms: W = w * 2^shift with shift = 58, exact for every

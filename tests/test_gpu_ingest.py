@@ -201,6 +201,40 @@ def test_csr_build_host_entry_point(gpu):
     assert e.value.code == -1
 
 
+@pytest.mark.parametrize("device_csr", [False, True])
+def test_wedge_rows_equal_host_construction(gpu, device_csr, monkeypatch):
+    """The wedge-row index (gathered on the device, k_wedge_fill) equals its definition built
+    here from the CSR: for every node whose neighbours' rows all hold <= 32 ids, the rows N(z),
+    z in N(x), back to back, padded to whole vectors with the last id. Businesses here have
+    ~400 neighbours, so one node spans several 256-neighbour rounds."""
+    monkeypatch.setenv("BLP_DEVICE_CSR_MIN", "1" if device_csr else str(1 << 40))
+    rng = np.random.default_rng(17)
+    a, c = bipartite_edges(rng, 3000, 100, 40000)
+    G = blp.DeviceGraph(a, c, device=gpu)
+    nv = ctypes.c_int64()
+    blp._lib.check(blp.lib().blp_graph_wedge(G.handle, ctypes.byref(nv), None, None))
+    assert nv.value > 0
+    wp = np.empty(G.n + 1, np.int64)
+    wd = np.empty(4 * nv.value, np.int32)
+    blp._lib.check(blp.lib().blp_graph_wedge(G.handle, ctypes.byref(nv), blp._lib.ptr(wp), blp._lib.ptr(wd)))
+    rp, ci = G.row_ptr, G.col_idx
+    deg = np.diff(rp)
+    exp_wp = [0]
+    exp = []
+    for x in range(G.n):
+        nb = ci[rp[x]: rp[x + 1]]
+        row = []
+        if len(nb) and deg[nb].max() <= 32:
+            for z in nb:
+                row.extend(ci[rp[z]: rp[z + 1]].tolist())
+            row.extend([row[-1]] * (-len(row) % 4))
+        exp.extend(row)
+        exp_wp.append(exp_wp[-1] + len(row) // 4)
+    assert np.array_equal(wp, np.array(exp_wp, np.int64))
+    assert np.array_equal(wd, np.array(exp, np.int32))
+    assert deg[G.n_col0:].max() > 256
+
+
 def test_allgather_world1_on_device(gpu, monkeypatch):
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         monkeypatch.delenv(k, raising=False)
