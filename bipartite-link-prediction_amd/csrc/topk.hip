@@ -153,7 +153,7 @@ __device__ inline unsigned long long aa_key(const unsigned long long* w2, int64_
   return (unsigned long long)__double_as_longlong(blp::aa_value(w2[2 * t], w2[2 * t + 1]));
 }
 
-__device__ long long block_sum(TkShared& s, long long v) {
+__device__ __attribute__((always_inline)) long long block_sum(TkShared& s, long long v) {
   for (int d = 32; d > 0; d >>= 1) v += __shfl_down(v, d, 64);
   __syncthreads();
   if ((threadIdx.x & 63) == 0) s.red[threadIdx.x >> 6] = v;
@@ -175,13 +175,16 @@ __device__ inline bool in_row_x(const TkShared& s, const int32_t* rowx, int du, 
   return lo < du && rowx[lo] == e;
 }
 
+// Every helper that takes TkShared& is forced inline: an out-of-line copy (the compiler made one
+// of push_pass<2> when the kernel grew) reaches LDS through generic pointers with flat
+// instructions and a call stack in scratch, and that build faulted.
 // MODE 0: CN counts into the tiered counters of chunk c (and |H2(x)| when count_h2)
 // MODE 3: MODE 0 plus the exact AA words of the H most popular targets (fused AA)
 // MODE 1: exact AA of the hashed candidates (counter >= thr) into s.key[2 slot], s.key[2 slot + 1]
 // MODE 2: direct exact AA words of targets [c0, c1) into the u64 view of s.acc
 // (two words per target: the wrapping sum of W and the sum of W >> 32, blp_internal.h)
 template <int MODE>
-__device__ long long push_pass(const TkArgs& a, TkShared& s, int x, int64_t xb, int du, const int32_t* rowx,
+__device__ __attribute__((always_inline)) long long push_pass(const TkArgs& a, TkShared& s, int x, int64_t xb, int du, const int32_t* rowx,
                                const TkChunk& c, uint32_t thr, int64_t d0, int64_t d1, bool count_h2,
                                long long* pushed = nullptr) {
   long long h2 = 0, npush = 0;
@@ -337,7 +340,7 @@ __device__ long long push_pass(const TkArgs& a, TkShared& s, int x, int64_t xb, 
 }
 
 // Sort s.key/s.col[0, TK_SEL) best-first (bitonic), keep min(n, k); update the threshold.
-__device__ void compact(const TkArgs& a, TkShared& s, int n) {
+__device__ __attribute__((always_inline)) void compact(const TkArgs& a, TkShared& s, int n) {
   const int tid = threadIdx.x;
   for (int i = n + tid; i < TK_SEL; i += TK_NT) {
     s.key[i] = 0;
@@ -377,7 +380,7 @@ __device__ void compact(const TkArgs& a, TkShared& s, int n) {
   __syncthreads();
 }
 
-__device__ void sel_begin(const TkArgs& a, TkShared& s, int m, int it) {
+__device__ __attribute__((always_inline)) void sel_begin(const TkArgs& a, TkShared& s, int m, int it) {
   const int nv = s.nv[m];
   const size_t base = ((size_t)m * a.n_src + it) * a.k;
   for (int i = threadIdx.x; i < nv; i += TK_NT) {
@@ -395,7 +398,7 @@ __device__ void sel_begin(const TkArgs& a, TkShared& s, int m, int it) {
   __syncthreads();
 }
 
-__device__ void sel_end(const TkArgs& a, TkShared& s, int m, int it) {
+__device__ __attribute__((always_inline)) void sel_end(const TkArgs& a, TkShared& s, int m, int it) {
   compact(a, s, s.n);
   const int nv = s.n;
   const size_t base = ((size_t)m * a.n_src + it) * a.k;
@@ -424,7 +427,7 @@ __device__ inline void sel_round_end(const TkArgs& a, TkShared& s) {
 
 // METHOD 0: CN key; 1: Jaccard key (fp64 bits); the counters of chunk c
 template <int METHOD>
-__device__ long long sel_counts(const TkArgs& a, TkShared& s, int it, const TkChunk& c, long long h2, bool count) {
+__device__ __attribute__((always_inline)) long long sel_counts(const TkArgs& a, TkShared& s, int it, const TkChunk& c, long long h2, bool count) {
   sel_begin(a, s, METHOD, it);
   long long nc = 0;
   if (count)  // targets with a count (the chunk's share of |H3(x)|): all of them, before the pruned walk
