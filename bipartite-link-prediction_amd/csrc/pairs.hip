@@ -759,7 +759,7 @@ __device__ inline void pp_fetch(const int32_t* __restrict__ ci, const int64_t* s
 
 // Build: set the bits of every element of the ns segments inside [c0, c0 + width).
 template <int NT, int K>
-__device__ inline void pp_build(const int32_t* __restrict__ ci, uint32_t idmask, const int64_t* s_start,
+__device__ __attribute__((always_inline)) inline void pp_build(const int32_t* __restrict__ ci, uint32_t idmask, const int64_t* s_start,
                                 const int32_t* s_off, int ns, int64_t c0, int64_t width, uint32_t* bm, int tid,
                                 const int32_t* hint, int shift) {
   const int T = s_off[ns];
@@ -795,7 +795,7 @@ __device__ inline void pp_build(const int32_t* __restrict__ ci, uint32_t idmask,
 // A step's elements lie in at most two segments (s1: k < rem1, s2: the rest), so a step ends
 // with at most two pairs of LDS atomics.
 template <int NT, int K, bool AA>
-__device__ inline void pp_scan(const int32_t* __restrict__ ci, uint32_t idmask, int idbits,
+__device__ __attribute__((always_inline)) inline void pp_scan(const int32_t* __restrict__ ci, uint32_t idmask, int idbits,
                                const long long* __restrict__ aaw, const long long* wtab, const int64_t* s_start,
                                const int32_t* s_off, int ns, int64_t c0, int64_t width, const uint32_t* bm,
                                uint32_t* s_cn, unsigned long long* s_aa, int tid, const int32_t* hint, int shift) {
