@@ -2370,6 +2370,7 @@ static int launch_short(blp_graph* g, const blp_batch* b, ScoreArgs a, size_t dy
   BLP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, BLOCK_SMALL, dyn));
   const int64_t n_wg = (int64_t)g->n_cu * std::max(per_cu, 1);
   if (!getenv("BLP_DQ") && b->n_sources >= n_wg * 16) a.dq = std::max(a.dq, 2);
+  if (const char* e = getenv("BLP_DQ_SHORT")) a.dq = std::min(DQ_MAX, std::max(1, atoi(e)));  // tuning knob
   hipLaunchKernelGGL((k_score<BLOCK_SMALL, CAP_SMALL, SEG_SMALL, 8, true, SAA>), dim3((unsigned)n_wg),
                      dim3(BLOCK_SMALL), dyn, b->stream, a);
   BLP_HIP(hipGetLastError());
