@@ -71,28 +71,42 @@ def alg_bytes(G, x, y, mask, cn=None):
     return int(per_src + per_pair)
 
 
-def pmc_traffic(kernel, pattern="r*_v*_bench.json"):
-    """HBM bytes per launch of `kernel` from the newest committed PMC summary of this bench
-    (profiles/*.json written by profiles/summarize.py from separate rocprofv3 --pmc
-    FETCH_SIZE / WRITE_SIZE passes; 2 x FETCH_SIZE + WRITE_SIZE per MI355X_MICROARCH.md)."""
+def pmc_fields(kernel, pattern, sec=None):
+    """HBM-side bytes per launch of `kernel` from the newest committed PMC summary matching
+    `pattern` under profiles/ (written by profiles/summarize.py from separate rocprofv3 --pmc
+    FETCH_SIZE / WRITE_SIZE passes of the same command): newest round first (rNN_ prefix),
+    then the highest _vM, then the name. Reported side by side, because MI355X_MICROARCH.md
+    (HBM) calibrates FETCH_SIZE only for wide coalesced streaming reads (exactly half the
+    bytes) and these kernels also gather:
+      traffic      = 2 x FETCH_SIZE + WRITE_SIZE (the guide's streaming correction)
+      traffic_raw  = FETCH_SIZE + WRITE_SIZE     (uncorrected)
+    frac_dram (over the same kernel time `sec`) is given for both; traffic_source names the
+    file and its measured kernel time (avg over its launches)."""
     import glob
-
     import re
 
-    def version(f):  # rNN_vM_bench.json: newest (round, version) last
-        m = re.search(r"r(\d+)_v(\d+)_[a-z0-9_]+\.json$", f)
-        return (int(m.group(1)), int(m.group(2))) if m else (-1, -1)
+    def key(f):
+        b = os.path.basename(f)
+        r = re.match(r"r(\d+)_", b)
+        v = re.search(r"_v(\d+)", b)
+        return (int(r.group(1)) if r else -1, int(v.group(1)) if v else -1, b)
 
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)), key=version)
-    for f in reversed(files):
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)), key=key, reverse=True):
         try:
             rows = json.load(open(f))
         except Exception:
             continue
         for r in rows if isinstance(rows, list) else []:
-            if kernel in r.get("kernel", "") and r.get("hbm_bytes_corrected"):
-                return float(r["hbm_bytes_corrected"]), os.path.relpath(f, ROOT)
-    return None, None
+            if kernel in r.get("kernel", "") and r.get("fetch_kb_raw") and r.get("write_kb") is not None:
+                fetch, write = 1024.0 * r["fetch_kb_raw"], 1024.0 * r["write_kb"]
+                out = {"traffic": 2 * fetch + write, "traffic_raw": fetch + write,
+                       "traffic_source": "%s (kernel avg %.3f ms there)" % (os.path.relpath(f, ROOT),
+                                                                             r["avg_us"] / 1e3)}
+                if sec:
+                    out["frac_dram"] = out["traffic"] / sec / 1e9 / HBM_PEAK_GBS
+                    out["frac_dram_raw"] = out["traffic_raw"] / sec / 1e9 / HBM_PEAK_GBS
+                return out
+    return {"traffic": None, "traffic_source": "no committed PMC summary for %s matching profiles/%s" % (kernel, pattern)}
 
 
 def cpu_baseline(og, ex_x, ex_y, target_s=15.0):
@@ -195,7 +209,11 @@ def _dense_edges(G):
     return np.concatenate([a, loops]), np.concatenate([b, loops])
 
 
-FP64_MFMA_PEAK_TFS = 78.6  # MI355X FP64 matrix peak (AMD spec; MI355X_MICROARCH.md lists no FP64 rate)
+# FP64 MFMA ceiling, MEASURED on this chip (MI355X_MICROARCH.md lists no FP64 rate): the probe
+# profiles/scripts/mfma_f64_peak.hip sustains 75 TF/s of v_mfma_f64_16x16x4f64 with independent
+# accumulation chains on every SIMD (profiles/r01_mfma_f64_peak.txt); AMD's spec value is 78.6.
+FP64_MFMA_PEAK_TFS = 75.0
+FP64_MFMA_PEAK_SOURCE = "measured: profiles/r01_mfma_f64_peak.txt (v_mfma_f64_16x16x4f64, independent chains)"
 
 
 def run_svd(args):
@@ -295,7 +313,8 @@ def run_svd(args):
             full[i - c0, ex_col[ex_off[i]:ex_off[i + 1]]] = -np.inf
             ok &= bool(np.array_equal(np.lexsort((np.arange(B), -full[i - c0]))[:args.topk], cols[i]))
     del full
-    svd_traffic, svd_tsrc = pmc_traffic("k_svd_topk", "r*_v*_svd_c4.json")  # HBM bytes per launch (PMC)
+    svd_pmc = pmc_fields("k_svd_topk", "r*_svd_c4*.json")  # HBM bytes per launch (PMC)
+    svd_pmc.pop("frac_dram", None)
     out = {
         "metric": METRIC, "value": dist.sum(scored) / t_max, "unit": "pairs/s", "n_gpus": dist.world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * t_max, "higher_is_better": True,
@@ -306,9 +325,9 @@ def run_svd(args):
                                "%.2fs, not in the step" % (M.nnz, len(users), args.topk, fact_s),
                    "global_batch": int(dist.sum(scored)), "parallelism": "replicas x%d" % dist.world},
         "roofline": {"bound": "mfma", "achieved": flops / kern_s / 1e12, "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
-                     "frac": flops / kern_s / 1e12 / FP64_MFMA_PEAK_TFS, "traffic": svd_traffic,
-                     "kernel": "k_svd_topk<64> + k_svd_merge", "kernel_ms": 1e3 * kern_s,
-                     "traffic_source": svd_tsrc},
+                     "frac": flops / kern_s / 1e12 / FP64_MFMA_PEAK_TFS, "peak_source": FP64_MFMA_PEAK_SOURCE,
+                     "frac_of_spec_78.6": flops / kern_s / 1e12 / 78.6,
+                     "kernel": "k_svd_topk<64> + k_svd_merge", "kernel_ms": 1e3 * kern_s, **svd_pmc},
         "pairs_kernel": {"pairs": int(len(pr)), "ms": 1e3 * pair_s, "pairs_per_s": len(pr) / pair_s,
                          "alg_GBps": pair_bytes / pair_s / 1e9},
         "parity": {"topk_users_checked": int(n_chk), "exact": bool(ok), "host_entry_point_same": host_same},
@@ -468,8 +487,8 @@ def run_topk(args):
                    "pairs_per_gpu": pairs, "global_batch": int(dist.sum(pairs)),
                    "parallelism": "replicas x%d (graph replicated, users split, no collective)" % dist.world},
         "roofline": {"bound": "hbm", "achieved": byts / kern_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": byts / kern_s / 1e9 / HBM_PEAK_GBS, "traffic": pmc_traffic("k_topk")[0],
-                     "kernel": "k_topk", "kernel_ms": 1e3 * kern_s, "alg_bytes_per_launch": byts},
+                     "frac": byts / kern_s / 1e9 / HBM_PEAK_GBS, "kernel": "k_topk", "kernel_ms": 1e3 * kern_s,
+                     "alg_bytes_per_launch": byts, **pmc_fields("k_topk", "r*_topk_*.json", kern_s)},
         "work": {"sum_h2": h2_sum, "sum_push": push_sum, "aa_hash_sources": hash_src, "aa_direct_sources": direct_src},
     }
     if dist.rank == 0 and not args.no_parity and mask == blp.JACCARD | blp.ADAMIC:
@@ -494,7 +513,9 @@ def run_sharded(args):
     value = candidate pairs scored per second over all ranks (weak scaling)."""
     from blp import dist as bd
 
-    d = Dist(exchange=True)
+    # the process group is formed even for one rank, so the exchange below is RCCL's own
+    # all_gather_into_tensor at every world size (dist.py, allgather_edges)
+    d = Dist(exchange=True, collective_at_world1=not args.no_collective_at_world1)
     dev = _device(d)
     blp.lib()
     U, B, D = synth.CONFIGS[args.config]
@@ -516,6 +537,7 @@ def run_sharded(args):
     d.barrier()
     exch_s = d.max(exch_local)
     recv_bytes = 8 * (sum(counts) - counts[d.rank])
+    gathered_bytes = 8 * max(counts) * d.world  # the all-gather's output tensor (padded partials)
     del u, b
     if not a_all.is_cuda:  # gloo exchange (rehearsal without RCCL): the partials arrive on the host
         a_all, b_all = a_all.to("cuda:%d" % dev), b_all.to("cuda:%d" % dev)
@@ -581,7 +603,9 @@ def run_sharded(args):
                    "pairs_per_gpu": int(len(ex_x)), "global_batch": int(pairs_total),
                    "parallelism": "row-block sharded ingest x%d + RCCL all-gather (%s), rank-local scoring"
                                   % (d.world, d.backend or "single rank")},
-        "exchange": {"seconds": exch_s, "bytes_in_per_rank": int(recv_bytes),
+        "exchange": {"backend": d.backend, "collective": "all_gather_into_tensor" if d.td is not None else None,
+                     "gathered_bytes_per_rank": int(gathered_bytes),
+                     "seconds": exch_s, "bytes_in_per_rank": int(recv_bytes),
                      "GBps_in_per_rank": recv_bytes / exch_s / 1e9 if exch_s > 0 and recv_bytes else None,
                      "xgmi_one_link_bound_s": xgmi_bound_s, "device_csr_build_s": build_s, "generate_s": gen_s,
                      "device_csr_phases_s": G.build_times,
@@ -589,12 +613,76 @@ def run_sharded(args):
                                        (max(work[sblocks[r]:sblocks[r + 1]].sum() for r in range(d.world)) /
                                         (work.sum() / d.world))},
         "roofline": {"bound": "hbm", "achieved": byts / sec / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": byts / sec / 1e9 / HBM_PEAK_GBS, "traffic": None, "kernel": "user-side scorer",
-                     "plan": bt0.plan()},
+                     "frac": byts / sec / 1e9 / HBM_PEAK_GBS, "kernel": "user-side scorer (%s)" % C5_KERNEL,
+                     "kernel_ms": 1e3 * sec, "alg_bytes_per_launch": byts, "plan": bt0.plan()},
     }
+    out["roofline"].update(pmc_fields(C5_KERNEL, "r*_c5_*.json", sec))
+    if not args.no_parity:
+        out["parity"] = sharded_parity(args, d, U, B, D, passes, ex_x, ex_y)
     if d.rank == 0:
         print(json.dumps(out), flush=True)
     d.close()
+
+
+C5_KERNEL = "k_score_split"
+
+
+def sharded_parity(args, d, U, B, D, passes, ex_x, ex_y):
+    """Config 5 at its own scale, not timed: on every rank, all pairs of `--parity-sources`
+    sampled user sources (user pass, CN + Jaccard + Adamic-Adar) and as many sampled business
+    sources (business pass, CN + Jaccard) are gathered to rank 0, which regenerates the union
+    of every rank's edge partial independently of the exchange (block_review_edges, the same
+    seeds), builds the C oracle's graph over the full 1B edges (oracle.c og_create: SNAP
+    LoadEdgeList semantics) and scores them with the reference algorithm
+    (similarity.py:20-106 / :108-126). Bit-exact: CN, the Jaccard quotient and the correctly
+    rounded Adamic-Adar sum."""
+    import coracle
+
+    from blp import dist as bd
+
+    rng = np.random.default_rng(100 + d.rank)
+    mine = {}
+    for name, bt, mask in passes:
+        xs, ys = (ex_x, ex_y) if name == "user" else (ex_y, ex_x)
+        srcs = np.unique(xs)
+        pick = rng.choice(srcs, size=min(args.parity_sources, len(srcs)), replace=False)
+        sel = np.flatnonzero(np.isin(xs, pick))
+        res = bt.fetch(mask)
+        mine[name] = {"x": xs[sel], "y": ys[sel], "mask": mask,
+                      **{k: v[sel] for k, v in res.items() if v is not None}}
+    allr = [mine]
+    if d.world > 1:
+        allr = [None] * d.world if d.rank == 0 else None
+        d.td.gather_object(mine, allr, dst=0, group=d.cpu_group)
+    if d.rank != 0:
+        return None
+    t0 = time.time()
+    blocks = bd.user_blocks(U, d.world)
+    parts = [bd.block_review_edges(U, B, D, int(blocks[r]), int(blocks[r + 1]), seed=0) for r in range(d.world)]
+    a = np.concatenate([p[0] for p in parts]).astype(np.int32)
+    b = np.concatenate([p[1] for p in parts]).astype(np.int32)
+    del parts
+    og = coracle.OracleGraph(U + B, a, b)
+    del a, b
+    build_s = time.time() - t0
+    nt = max(1, int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0)))
+    out = {"ranks_checked": len(allr), "oracle_graph_build_s": round(build_s, 1), "ok": True}
+    t0 = time.time()
+    for name in mine:
+        n_pairs = n_src = 0
+        same = {}
+        for r in allr:
+            m = r[name]
+            cn, jac, aa, _ = og.score_pairs(m["x"], m["y"], m["mask"], nthreads=nt)
+            for k, want in (("cn", cn), ("jaccard", jac), ("adamic", aa)):
+                if k in m:
+                    same[k] = same.get(k, True) and bool(np.array_equal(m[k], want))
+            n_pairs += len(m["x"])
+            n_src += len(np.unique(m["x"]))
+        out[name] = {"sources": n_src, "pairs": n_pairs, **{k + "_exact": v for k, v in same.items()}}
+        out["ok"] &= all(same.values()) and n_pairs > 0
+    out["oracle_score_s"] = round(time.time() - t0, 1)
+    return out
 
 
 def run_e2e(args):
@@ -743,6 +831,10 @@ def main():
                          "top-k; svd: config 4 rank-64 truncated-SVD scorer; sharded: config 5 row-block "
                          "sharded ingest + RCCL all-gather, then rank-local scoring (--config c5); e2e: "
                          "similarity.main from graph.txt to the 6 files (--config yelp = config 1, or c2)")
+    ap.add_argument("--parity-sources", type=int, default=50,
+                    help="--mode sharded: sampled sources per side and rank checked against the C oracle")
+    ap.add_argument("--no-collective-at-world1", action="store_true",
+                    help="--mode sharded: at one rank, skip the process group (no RCCL call; the local partial)")
     ap.add_argument("--topk", type=int, default=20)
     ap.add_argument("--svd-parity-users", type=int, default=1000, help="--mode svd: users whose top-k is checked")
     ap.add_argument("--topk-mask", type=int, default=6, help="methods of --mode topk (default Jaccard + AA)")
@@ -853,13 +945,11 @@ def main():
     byts = alg_bytes(G, xs, ys, mask0, cn0)
     sec = ktimes[name0]["score_ms"] / 1e3
     kname = "k_score<1024, 33792, 512, 8, false, true>" if bt0.plan()["block"] == 1024 else "k_score_wave<2, 3328, 8>"
-    traffic, tsrc = pmc_traffic(kname)
     out["roofline"] = {"bound": "hbm", "achieved": byts / sec / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                       "frac": byts / sec / 1e9 / HBM_PEAK_GBS, "traffic": traffic,
+                       "frac": byts / sec / 1e9 / HBM_PEAK_GBS,
                        # the counters' HBM-side bytes over the same kernel time: what DRAM actually moved
-                       "frac_dram": (traffic / sec / 1e9 / HBM_PEAK_GBS) if traffic else None,
+                       **pmc_fields(kname, "r*_v*_bench.json", sec),
                        "kernel": "%s (%s side)" % (kname, name0), "alg_bytes_per_launch": byts,
-                       "traffic_source": tsrc,
                        # what the counters name as the bound ("What bounds the user scorer")
                        "limiter": "latency: waves wait 56% of cycles; VALU <= 53%, LDS 34% busy (45% of it bank "
                                   "conflicts), L2 hit 17%, DRAM side 0.32 of peak (profiles/r02_v4_bench_pmc.txt)"}

@@ -25,14 +25,24 @@ from . import synth
 class Dist:
     """Rank / world from the torchrun environment; CPU (gloo) reductions; optional RCCL group."""
 
-    def __init__(self, exchange=False):
+    def __init__(self, exchange=False, collective_at_world1=False):
+        """exchange: form the RCCL group the config-5 exchange uses (BLP_EXCHANGE_BACKEND=gloo
+        rehearses it over gloo instead). collective_at_world1: form the process group even
+        for a single rank, so the exchange runs the real collective (RCCL's all-gather over
+        one rank) rather than returning the local partial -- the code path of N ranks,
+        exercised on a one-GPU box."""
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
         self.exchange = exchange
         self.td = None
         self.cpu_group = None
-        if self.world > 1:
+        if self.world == 1 and exchange and collective_at_world1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
+        if self.world > 1 or (exchange and collective_at_world1):
             import torch.distributed as td
 
             self.td = td
@@ -91,8 +101,18 @@ class Dist:
         return [int(t.item()) for t in out]
 
     def close(self):
-        if self.world > 1 and self.td.is_initialized():
+        if self.td is not None and self.td.is_initialized():
             self.td.destroy_process_group()
+
+
+def _free_port():
+    import socket
+
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    return port
 
 
 def user_blocks(n_users, world, work=None):
@@ -151,7 +171,7 @@ def allgather_edges(dist, a_local, b_local):
     if len(a_local):
         mine[0, : len(a_local)] = torch.as_tensor(np.asarray(a_local, np.int32)).to(dev)
         mine[1, : len(b_local)] = torch.as_tensor(np.asarray(b_local, np.int32)).to(dev)
-    if dist.world == 1:
+    if dist.td is None:  # a single rank without a process group: nothing to exchange
         return mine[0, : counts[0]].contiguous(), mine[1, : counts[0]].contiguous(), counts
     out = torch.empty((dist.world, 2, max(mx, 1)), dtype=torch.int32, device=dev)
     if dist.backend == "nccl":

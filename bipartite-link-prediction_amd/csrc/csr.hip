@@ -77,17 +77,19 @@ extern "C" int blp_csr_destroy(blp_csr* c) {
   return BLP_OK;
 }
 
-extern "C" int blp_csr_build_device(int device, const int32_t* d_a, const int32_t* d_b, int64_t m, int64_t n,
-                                    blp_csr** out) {
+// sync_device: the endpoints come from another stream (the RCCL all-gather, a torch copy), so
+// wait for everything queued on the device first (a one-off ingest step). blp_csr_build_host's
+// uploads are synchronous already and skip it, so a graph load never waits for other graphs'
+// batches still running on the device.
+static int csr_build(int device, const int32_t* d_a, const int32_t* d_b, int64_t m, int64_t n, blp_csr** out,
+                     bool sync_device) {
   BLP_CHECK(out && n >= 0 && m >= 0 && (m == 0 || (d_a && d_b)), BLP_E_ARG, "blp_csr_build_device: bad arguments");
   BLP_CHECK(n < (int64_t(1) << 31), BLP_E_ARG, "blp_csr_build_device: n_nodes must fit int32");
   int ndev = 0;
   BLP_HIP(hipGetDeviceCount(&ndev));
   BLP_CHECK(device >= 0 && device < ndev, BLP_E_ARG, "blp_csr_build_device: no such device");
   BLP_HIP(hipSetDevice(device));
-  // the endpoints come from another stream (the RCCL all-gather, a torch copy): a one-off
-  // ingest step, so wait for everything queued on the device rather than ask for a stream
-  BLP_HIP(hipDeviceSynchronize());
+  if (sync_device) BLP_HIP(hipDeviceSynchronize());
   hipStream_t st = nullptr;
   BLP_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
   blp_csr* c = new blp_csr();
@@ -162,6 +164,11 @@ extern "C" int blp_csr_build_device(int device, const int32_t* d_a, const int32_
   return done(BLP_OK);
 }
 
+extern "C" int blp_csr_build_device(int device, const int32_t* d_a, const int32_t* d_b, int64_t m, int64_t n,
+                                    blp_csr** out) {
+  return csr_build(device, d_a, d_b, m, n, out, true);
+}
+
 // Host-resident endpoints (similarity.main's graph.txt load): upload, then the device build.
 extern "C" int blp_csr_build_host(int device, const int32_t* a, const int32_t* b, int64_t m, int64_t n, blp_csr** out) {
   BLP_CHECK(out && m >= 0 && (m == 0 || (a && b)), BLP_E_ARG, "blp_csr_build_host: bad arguments");
@@ -181,7 +188,7 @@ extern "C" int blp_csr_build_host(int device, const int32_t* a, const int32_t* b
       return hip_fail(e, "hipMemcpy (edge upload)", __FILE__, __LINE__);
     }
   }
-  rc = blp_csr_build_device(device, da.as<int32_t>(), db.as<int32_t>(), m, n, out);
+  rc = csr_build(device, da.as<int32_t>(), db.as<int32_t>(), m, n, out, false);  // uploads were synchronous
   da.release();
   db.release();
   return rc;

@@ -923,11 +923,7 @@ __device__ inline void rc_fetch(const int32_t* __restrict__ ci, const int64_t* s
   const blp::U4a* q = reinterpret_cast<const blp::U4a*>(ci + pos);
 #pragma unroll
   for (int j = 0; j < K / 4; ++j) {
-#ifdef BLP_EXP_NOLOAD  // timing experiment only: no global loads, fake ids
-    const blp::U4a x{(int)pos + 4 * j, (int)pos + 4 * j + 1, (int)pos + 4 * j + 2, (int)pos + 4 * j + 3};
-#else
     const blp::U4a x = q[j];
-#endif
     st.v[4 * j] = x.x;
     st.v[4 * j + 1] = x.y;
     st.v[4 * j + 2] = x.z;
@@ -1018,15 +1014,6 @@ __device__ inline void rc_scan(const int32_t* __restrict__ ci, uint32_t idmask, 
   // before the first use: one LDS round trip per step instead of one per id.
   auto proc = [&](const RCStep<K>& st) {
     st.land();
-#ifdef BLP_EXP_NOPROC  // timing experiment only: consume the ids without the bitmap work
-    {
-      uint32_t x = 0;
-#pragma unroll
-      for (int k = 0; k < K; ++k) x += (uint32_t)st.v[k];
-      if (x == 0x12345u) atomicAdd(&s_cn[st.s], 1u);
-      return;
-    }
-#endif
     uint32_t rr[K], wd[K];
     long long wt[K];
 #pragma unroll
@@ -2304,6 +2291,7 @@ struct blp_batch {
   blp::DevBuf cnt, off, active, scratch;
   int cus = 0;  // CUs the persistent block scorer may occupy (0: all; set by blp_batches_score)
   SrcRec* d_rec = nullptr;  // [n_sources] source records of the short-row scorer (or null)
+  bool use_short = false;   // the short-row scorer takes this batch (decided once, at create)
   int64_t work_elems = 0;  // planned build + scan elements (co-scheduling estimate)
 };
 
@@ -2643,7 +2631,8 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
     return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: hipMalloc failed"));
   if (b->chunks > 1 && hipMalloc(&b->d_aa_part, 16 * np) != hipSuccess)
     return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: hipMalloc failed"));
-  if (short_kernel(b) &&
+  b->use_short = short_kernel(b);  // fixed here: d_rec's allocation and the launch must agree
+  if (b->use_short &&
       hipMalloc(&b->d_rec, sizeof(SrcRec) * (size_t)std::max<int64_t>(b->n_sources, 1)) != hipSuccess)
     return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: hipMalloc failed"));
   if (n_pairs) {
@@ -2875,7 +2864,7 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
     else
       hipLaunchKernelGGL((k_score_wave<W_WAVES, W_CAP, 8>), grid, block, 0, b->stream, a);
     BLP_HIP(hipGetLastError());
-  } else if (np && short_kernel(b)) {
+  } else if (np && b->use_short) {
     // bitmap in dynamic LDS, sized to the universe (whole 16-byte vectors)
     const size_t dyn = 4 * (size_t)std::max<int64_t>(4, ((b->hi - b->lo + 31) / 32 + 3) / 4 * 4);
     if (g->d_wp && !getenv("BLP_NO_WEDGE")) {  // tuning knob: BLP_NO_WEDGE builds from CSR

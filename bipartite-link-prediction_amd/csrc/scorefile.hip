@@ -86,16 +86,41 @@ bool int_key(Cursor& c, int64_t* off, int32_t* len, int64_t* id, const char* bas
   return true;
 }
 
-// a scalar value (the label): number, true, false or null
+// a scalar value (the label) exactly as json.loads accepts it: a JSON number
+// -?(0|[1-9][0-9]*)(.[0-9]+)?([eE][+-]?[0-9]+)?, true, false, null, or Python's extra
+// literals NaN, Infinity, -Infinity. Anything else is refused (BLP_E_UNSUP), so the json.loads
+// path raises on it as the reference does.
 bool skip_scalar(Cursor& c) {
   c.ws();
-  const char* s = c.p;
-  while (c.p < c.e && *c.p != ',' && *c.p != '}' && *c.p != ' ' && *c.p != '\n' && *c.p != '\r' && *c.p != '\t') {
-    const char ch = *c.p;
-    if (ch == '{' || ch == '[' || ch == '"') return false;
+  auto lit = [&](const char* w) {
+    const size_t n = strlen(w);
+    if ((size_t)(c.e - c.p) >= n && memcmp(c.p, w, n) == 0) {
+      c.p += n;
+      return true;
+    }
+    return false;
+  };
+  if (lit("true") || lit("false") || lit("null") || lit("NaN") || lit("Infinity") || lit("-Infinity")) return true;
+  auto digit = [&]() { return c.p < c.e && *c.p >= '0' && *c.p <= '9'; };
+  if (c.p < c.e && *c.p == '-') ++c.p;
+  if (!digit()) return false;
+  if (*c.p == '0') {
     ++c.p;
+  } else {
+    while (digit()) ++c.p;
   }
-  return c.p > s;
+  if (c.p < c.e && *c.p == '.') {
+    ++c.p;
+    if (!digit()) return false;
+    while (digit()) ++c.p;
+  }
+  if (c.p < c.e && (*c.p == 'e' || *c.p == 'E')) {
+    ++c.p;
+    if (c.p < c.e && (*c.p == '+' || *c.p == '-')) ++c.p;
+    if (!digit()) return false;
+    while (digit()) ++c.p;
+  }
+  return true;
 }
 
 int parse(blp_examples* x) {
@@ -146,7 +171,11 @@ int parse(blp_examples* x) {
     const int64_t b = x->u_off[u], e = x->u_off[u + 1];
     ord.resize(e - b);
     for (int64_t k = b; k < e; ++k) ord[k - b] = k;
-    std::sort(ord.begin(), ord.end(), [&](int64_t i, int64_t j) { return x->v_id[i] < x->v_id[j]; });
+    // by (id, key bytes): equal keys are then adjacent even where keys of one id differ ("5", "05")
+    std::sort(ord.begin(), ord.end(), [&](int64_t i, int64_t j) {
+      if (x->v_id[i] != x->v_id[j]) return x->v_id[i] < x->v_id[j];
+      return view(x->v_key[i], x->v_len[i]) < view(x->v_key[j], x->v_len[j]);
+    });
     for (size_t k = 1; k < ord.size(); ++k)
       if (x->v_id[ord[k]] == x->v_id[ord[k - 1]] &&
           view(x->v_key[ord[k]], x->v_len[ord[k]]) == view(x->v_key[ord[k - 1]], x->v_len[ord[k - 1]]))

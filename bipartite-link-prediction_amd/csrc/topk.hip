@@ -46,6 +46,9 @@ constexpr int TK_KMAX = 256;
 #ifndef BLP_TK_RB
 #define BLP_TK_RB 8
 #endif
+#ifndef BLP_TK_TAIL16
+#define BLP_TK_TAIL16 0  // 1: row entries past the first TK_RB read as 16-byte vectors (4 per load)
+#endif
 constexpr int TK_RB = BLP_TK_RB;   // row entries loaded up front per element (16-byte vectors)
 constexpr uint32_t TK_EMPTY = 0xFFFFFFFFu;
 
@@ -89,7 +92,30 @@ struct TkArgs {
   int32_t* cols;             // [3][n_src][k]
   int64_t* ncand;            // [n_src]
   unsigned long long* counters;  // [0] queue, [1] AA hash path, [2] AA direct path, [3] sum |H2|, [4] sum of |N(w)| over H2, [5] AA fused path
+  int64_t acc_words;  // counter words in use (<= TK_ACC_WORDS; test knob BLP_TOPK_ACC_WORDS)
+  int64_t pci_len, x2_len;  // entries of pci / x2 including their padding (BLP_DEBUG bounds)
 };
+
+// BLP_DEBUG builds (make debug -> libblp_debug.so): every LDS index and every row read of the
+// walk is checked against its bound before the access; a violation is counted, the first one
+// recorded (site, value, bound) and the access skipped, so the check never faults the GPU.
+// blp_topk_run then fails with the record (BLP_E_STATE). Release builds compile the checks out.
+#ifdef BLP_DEBUG
+__device__ long long g_tk_dbg[4];  // violations, first site, its value, its bound
+__device__ inline bool tk_ok(bool ok, int site, long long v, long long bound) {
+  if (!ok && atomicAdd((unsigned long long*)&g_tk_dbg[0], 1ull) == 0ull) {
+    g_tk_dbg[1] = site;
+    g_tk_dbg[2] = v;
+    g_tk_dbg[3] = bound;
+  }
+  return ok;
+}
+#define TK_OK(cond, site, v, bound) tk_ok((cond), (site), (long long)(v), (long long)(bound))
+#else
+#define TK_OK(cond, site, v, bound) ((void)(v), true)
+#endif
+// sites: 1 acc_add, 2 acc_get, 3 acc_clear, 4 fused AA word, 5 hash AA word, 6 direct AA word,
+// 7 segment index, 8 16-byte row read, 9 row entry read, 10 selection slot, 11 hash probe length
 
 struct TkShared {
   uint32_t acc[TK_ACC_WORDS];
@@ -124,19 +150,21 @@ __device__ inline uint32_t width_mask(const TkArgs& a, int64_t e) {
   return e < a.A16 ? 0xFFFFFFFFu : e < a.A8 ? 0xFFFFu : 0xFFu;
 }
 
-__device__ inline void acc_add(uint32_t* acc, const TkChunk& c, int64_t e) {
+__device__ inline void acc_add(const TkArgs& a, uint32_t* acc, const TkChunk& c, int64_t e) {
   const int64_t off = e - c.a0;
-  atomicAdd(&acc[off >> 2], 1u << ((off & 3) << 3));
+  if (TK_OK(off >= 0 && (off >> 2) < a.acc_words, 1, off, a.acc_words)) atomicAdd(&acc[off >> 2], 1u << ((off & 3) << 3));
 }
 
 __device__ inline uint32_t acc_get(const TkArgs& a, const uint32_t* acc, const TkChunk& c, int64_t e) {
   const int64_t off = e - c.a0;
+  if (!TK_OK(off >= 0 && (off >> 2) < a.acc_words, 2, off, a.acc_words)) return 0;
   return (acc[off >> 2] >> ((off & 3) << 3)) & width_mask(a, e);
 }
 
 __device__ inline void acc_clear(const TkArgs& a, uint32_t* acc, const TkChunk& c, int64_t e) {
   const int64_t off = e - c.a0;
-  atomicAnd(&acc[off >> 2], ~(width_mask(a, e) << ((off & 3) << 3)));
+  if (TK_OK(off >= 0 && (off >> 2) < a.acc_words, 3, off, a.acc_words))
+    atomicAnd(&acc[off >> 2], ~(width_mask(a, e) << ((off & 3) << 3)));
 }
 
 constexpr int TK_HBITS = 10;  // log2(TK_AH)
@@ -232,9 +260,12 @@ __device__ __attribute__((always_inline)) long long push_pass(const TkArgs& a, T
     // element's row bounds are fetched while the current row is processed, and the first
     // TK_RB entries of a row are loaded as independent predicated loads (rows are short).
     const int32_t* base = a.x2 ? a.x2 : a.pci;
+    const int64_t base_len = a.x2 ? a.x2_len : a.pci_len;  // entries incl. padding (BLP_DEBUG bound)
+    (void)base_len;
     int sg = 0;
     auto fetch = [&](int64_t id, int64_t& r0, int64_t& r1, int32_t& pp) -> bool {
       while (s.seg_off[sg + 1] <= id) ++sg;
+      if (!TK_OK(sg < ns, 7, sg, ns)) return true;
       const int64_t k = s.seg_rs[sg] + (id - s.seg_off[sg]);
       pp = s.seg_p[sg];
       if (a.x2) {
@@ -265,7 +296,7 @@ __device__ __attribute__((always_inline)) long long push_pass(const TkArgs& a, T
 #pragma unroll
       for (int q = 0; q < TK_RB / 4; ++q) {
         blp::U4a v = {0x7FFFFFFF, 0x7FFFFFFF, 0x7FFFFFFF, 0x7FFFFFFF};
-        if (!skip && 4 * q < len_w) v = rv[q];
+        if (!skip && 4 * q < len_w && TK_OK(r0 >= 0 && r0 + 4 * q + 4 <= base_len, 8, r0 + 4 * q + 4, base_len)) v = rv[q];
         e[4 * q] = 4 * q < len_w ? v.x : 0x7FFFFFFF;
         e[4 * q + 1] = 4 * q + 1 < len_w ? v.y : 0x7FFFFFFF;
         e[4 * q + 2] = 4 * q + 2 < len_w ? v.z : 0x7FFFFFFF;
@@ -274,26 +305,54 @@ __device__ __attribute__((always_inline)) long long push_pass(const TkArgs& a, T
       idx += TK_NT;
       if (idx < E) skipn = fetch(idx, r0n, r1n, ppn);
       if (skip) continue;
+      // row entry j >= TK_RB (bounds-checked in BLP_DEBUG builds)
+      auto entry = [&](int j) -> int32_t {
+        return TK_OK(r0 + j < base_len, 9, r0 + j, base_len) ? roww[j] : 0x7FFFFFFF;
+      };
+      // the entries past the first TK_RB, four at a time as 16-byte vectors (BLP_TK_TAIL16): the
+      // last vector reads up to 3 entries past the row, inside the next row or the array padding
+      auto tail4 = [&](int j, int32_t* t) {
+        blp::U4a v = {0x7FFFFFFF, 0x7FFFFFFF, 0x7FFFFFFF, 0x7FFFFFFF};
+        if (TK_OK(r0 + j + 4 <= base_len, 8, r0 + j + 4, base_len)) v = *reinterpret_cast<const blp::U4a*>(roww + j);
+        t[0] = v.x;
+        t[1] = j + 1 < len_w ? v.y : 0x7FFFFFFF;
+        t[2] = j + 2 < len_w ? v.z : 0x7FFFFFFF;
+        t[3] = j + 3 < len_w ? v.w : 0x7FFFFFFF;
+      };
+      (void)tail4;
       bool owned = true;
 #pragma unroll
       for (int j = 0; j < TK_RB; ++j)
         if (e[j] < pp && in_row_x(s, rowx, du, e[j])) owned = false;
+#if BLP_TK_TAIL16
+      for (int j = TK_RB; j < len_w && owned; j += 4) {
+        int32_t t[4];
+        tail4(j, t);
+        if (t[0] >= pp) break;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (t[q] < pp && in_row_x(s, rowx, du, t[q])) owned = false;
+        if (t[3] >= pp) break;
+      }
+#else
       for (int j = TK_RB; j < len_w && owned; ++j) {
-        const int32_t ej = roww[j];
+        const int32_t ej = entry(j);
         if (ej >= pp) break;
         if (in_row_x(s, rowx, du, ej)) owned = false;
       }
+#endif
       if (!owned) continue;
       if (MODE == 3) {
         unsigned long long* aah = acc64 + (a.h_word >> 1);
         const unsigned long long wfx = (unsigned long long)a.wtab[len_w];
-#pragma unroll
+        auto push3 = [&](int32_t ej) {
+          const int64_t t = p_of(a, ej);
+          if (ej < a.AH && TK_OK(t >= 0 && (a.h_word >> 1) + 2 * t + 1 < a.acc_words / 2, 4, t, a.acc_words))
+            aa_push2(aah, t, wfx);
+        };
         for (int j = 0; j < TK_RB; ++j)
-          if (j < len_w && e[j] < a.AH) aa_push2(aah, p_of(a, e[j]), wfx);
-        for (int j = TK_RB; j < len_w; ++j) {
-          const int32_t ej = roww[j];
-          if (ej < a.AH) aa_push2(aah, p_of(a, ej), wfx);
-        }
+          if (j < len_w) push3(e[j]);
+        for (int j = TK_RB; j < len_w; ++j) push3(entry(j));
       }
       if (MODE == 0 || MODE == 3) {
         if (count_h2) {
@@ -302,35 +361,48 @@ __device__ __attribute__((always_inline)) long long push_pass(const TkArgs& a, T
         }
 #pragma unroll
         for (int j = 0; j < TK_RB; ++j)
-          if (j < len_w && e[j] >= c.a0 && e[j] < c.a1) acc_add(s.acc, c, e[j]);
-        for (int j = TK_RB; j < len_w; ++j) {
-          const int32_t ej = roww[j];
-          if (ej >= c.a0 && ej < c.a1) acc_add(s.acc, c, ej);
+          if (j < len_w && e[j] >= c.a0 && e[j] < c.a1) acc_add(a, s.acc, c, e[j]);
+#if BLP_TK_TAIL16
+        for (int j = TK_RB; j < len_w; j += 4) {
+          int32_t t[4];
+          tail4(j, t);
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (t[q] >= c.a0 && t[q] < c.a1) acc_add(a, s.acc, c, t[q]);
         }
+#else
+        for (int j = TK_RB; j < len_w; ++j) {
+          const int32_t ej = entry(j);
+          if (ej >= c.a0 && ej < c.a1) acc_add(a, s.acc, c, ej);
+        }
+#endif
       } else if (MODE == 1) {
         const unsigned long long wfx = (unsigned long long)a.wtab[len_w];
         auto push1 = [&](int32_t ej) {
           if (acc_get(a, s.acc, c, ej) >= thr) {
-            int h = hash_slot(ej);
-            while (s.col[h] != ej) h = (h + 1) & (TK_AH - 1);
-            aa_push2(s.key, h, wfx);
+            int h = hash_slot(ej), probes = 0;
+            while (s.col[h] != ej) {
+              ++probes;
+              if (!TK_OK(probes < TK_AH, 11, probes, TK_AH)) break;
+              h = (h + 1) & (TK_AH - 1);
+            }
+            if (s.col[h] == ej && TK_OK(2 * h + 1 < TK_SEL, 5, h, TK_SEL)) aa_push2(s.key, h, wfx);
           }
         };
 #pragma unroll
         for (int j = 0; j < TK_RB; ++j)
           if (j < len_w) push1(e[j]);
-        for (int j = TK_RB; j < len_w; ++j) push1(roww[j]);
+        for (int j = TK_RB; j < len_w; ++j) push1(entry(j));
       } else {
         const unsigned long long wfx = (unsigned long long)a.wtab[len_w];
+        auto push2 = [&](int64_t p) {
+          if (p >= d0 && p < d1 && TK_OK(2 * (p - d0) + 1 < a.acc_words / 2, 6, p - d0, a.acc_words / 4))
+            aa_push2(acc64, p - d0, wfx);
+        };
 #pragma unroll
-        for (int j = 0; j < TK_RB; ++j) {
-          const int64_t p = p_of(a, e[j]);
-          if (j < len_w && p >= d0 && p < d1) aa_push2(acc64, p - d0, wfx);
-        }
-        for (int j = TK_RB; j < len_w; ++j) {
-          const int64_t p = p_of(a, roww[j]);
-          if (p >= d0 && p < d1) aa_push2(acc64, p - d0, wfx);
-        }
+        for (int j = 0; j < TK_RB; ++j)
+          if (j < len_w) push2(p_of(a, e[j]));
+        for (int j = TK_RB; j < len_w; ++j) push2(p_of(a, entry(j)));
       }
     }
   }
@@ -413,8 +485,10 @@ __device__ __attribute__((always_inline)) void sel_end(const TkArgs& a, TkShared
 __device__ inline void sel_offer(TkShared& s, bool ok, unsigned long long key, int col) {
   if (ok && (!s.have_thr || better(key, col, s.thr_key, s.thr_col))) {
     const int slot = atomicAdd(&s.n, 1);
-    s.key[slot] = key;
-    s.col[slot] = col;
+    if (TK_OK(slot < TK_SEL, 10, slot, TK_SEL)) {
+      s.key[slot] = key;
+      s.col[slot] = col;
+    }
   }
 }
 
@@ -599,8 +673,12 @@ __global__ __launch_bounds__(TK_NT) void k_topk(TkArgs a) {
           for (int64_t p = c.c0 + tid; p < pcut; p += TK_NT) {
             const int32_t e = (int32_t)addr_of(a, p);
             if (acc_get(a, s.acc, c, e) >= thr) {
-              int h = hash_slot(e);
-              while (atomicCAS(&s.col[h], (int32_t)TK_EMPTY, e) != (int32_t)TK_EMPTY) h = (h + 1) & (TK_AH - 1);
+              int h = hash_slot(e), probes = 0;
+              while (atomicCAS(&s.col[h], (int32_t)TK_EMPTY, e) != (int32_t)TK_EMPTY) {
+                ++probes;
+                if (!TK_OK(probes < TK_AH, 11, probes, TK_AH)) break;
+                h = (h + 1) & (TK_AH - 1);
+              }
             }
           }
           __syncthreads();
@@ -649,7 +727,8 @@ __global__ __launch_bounds__(TK_NT) void k_topk(TkArgs a) {
           push_pass<2>(a, s, x, xb, du, rowx, a.chunks[0], 0, d0, d1, false);
           for (int j = tid; j < du; j += TK_NT) {
             const int64_t p = p_of(a, rowx[j]);
-            if (p >= d0 && p < d1) acc64[2 * (p - d0)] = acc64[2 * (p - d0) + 1] = 0;
+            if (p >= d0 && p < d1 && TK_OK(2 * (p - d0) + 1 < a.acc_words / 2, 6, p - d0, a.acc_words / 4))
+              acc64[2 * (p - d0)] = acc64[2 * (p - d0) + 1] = 0;
           }
           __syncthreads();
           sel_begin(a, s, 2, it);
@@ -707,6 +786,7 @@ struct blp_topk {
   int64_t aa_chunk = 0;
   DevBuf perm, inv, tdeg, ge, pci, d_chunks, src, keys, cols, ncand, counters, wtab, x2_off, x2;
   int64_t kbase = 0, x2_entries = -1;
+  int64_t pci_n = 0, x2_n = 0;  // entries uploaded to pci / x2, padding included
   int64_t n_src = 0;
   int k = 0;
   uint32_t mask = 0;
@@ -892,6 +972,8 @@ extern "C" int blp_topk_create(blp_graph* g, int64_t src_lo, int64_t src_hi, int
   }
   t->kbase = kbase;
   t->x2_entries = x2.empty() ? -1 : x2_off[mt];
+  t->pci_n = (int64_t)pci.size();
+  t->x2_n = (int64_t)x2.size();
   // ge[d] = targets of degree >= d, d in [0, max degree + 1] (degrees are non-increasing in p)
   std::vector<int32_t> ge((size_t)(T ? tdeg[0] : 0) + 2, 0);
   for (int64_t d = 0, j = T; d < (int64_t)ge.size(); ++d) {
@@ -1003,6 +1085,9 @@ extern "C" int blp_topk_run(blp_topk* t, int k, uint32_t mask) {
   a.cols = t->cols.as<int32_t>();
   a.ncand = t->ncand.as<int64_t>();
   a.counters = t->counters.as<unsigned long long>();
+  a.acc_words = t->acc_words;
+  a.pci_len = t->pci_n;
+  a.x2_len = t->x2_n;
   hipEvent_t t0;
   if ((rc = timer_begin(t->timer, st, &t0))) return rc;
   if (t->n_src) {
@@ -1011,6 +1096,21 @@ extern "C" int blp_topk_run(blp_topk* t, int k, uint32_t mask) {
     BLP_HIP(hipGetLastError());
   }
   if ((rc = timer_end(t->timer, st, t0))) return rc;
+#ifdef BLP_DEBUG
+  {  // the walk's bound checks (see TK_OK): any violation fails the run
+    long long dbg[4];
+    BLP_HIP(hipStreamSynchronize(st));
+    BLP_HIP(hipMemcpyFromSymbol(dbg, HIP_SYMBOL(g_tk_dbg), sizeof(dbg)));
+    if (dbg[0]) {
+      const long long z[4] = {0, 0, 0, 0};
+      BLP_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_tk_dbg), z, sizeof(z)));
+      char msg[160];
+      snprintf(msg, sizeof msg, "blp_topk_run [BLP_DEBUG]: %lld bound violations; first at site %lld: %lld vs bound %lld",
+               dbg[0], dbg[1], dbg[2], dbg[3]);
+      return fail(BLP_E_STATE, msg);
+    }
+  }
+#endif
   t->k = k;
   t->mask = mask;
   t->ran = true;

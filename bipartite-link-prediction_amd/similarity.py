@@ -187,27 +187,33 @@ def main(example_file, graph_file, u_methods, u_outfiles, b_methods, b_outfiles,
     # examples.json of the reference's shape is read natively into flat arrays (anything else:
     # json.loads, as util.load_json); the score files are then written natively with the same
     # text json.dumps gives (blp/scorefile.py). With sidecar=True the dict path runs.
-    ex = None if sidecar else scorefile.Examples.load(example_file)
+    import os
+
+    # a missing or unreadable file raises what util.load_json raises (IOError / FileNotFoundError)
+    ex = None if sidecar or not os.path.isfile(example_file) else scorefile.Examples.load(example_file)
     examples = util.load_json(example_file) if ex is None else None
-    t_ex = clock()
-    print("Loading graph...")
-    G = blp.load_edge_list(graph_file)
-    t_g = clock()
-    # both passes in one concurrent device step, then the files in the reference's order
-    print("Scoring user and business sides on the device...")
-    masks = method_mask(u_methods, _U_BITS) | blp.CN, method_mask(b_methods, _B_BITS) | blp.CN
-    if ex is None:
-        present, u_scores, b_scores = score_both_sides(examples, G, *masks)
-    else:
-        present, u_scores, b_scores = _score_both_ids(G, ex.pair_user, ex.pair_business, *masks)
-    t_s = clock()
-    if ex is None:
-        _run_side(examples, G, u_methods, u_outfiles, _U_BITS, 0, sidecar, scored=(present, u_scores))
-        _run_side(examples, G, b_methods, b_outfiles, dict(_B_BITS), 1, sidecar, scored=(present, b_scores))
-    else:
-        _write_side(ex, u_methods, u_outfiles, _U_BITS, present, u_scores)
-        _write_side(ex, b_methods, b_outfiles, _B_BITS, present, b_scores)
-        ex.close()
+    try:
+        t_ex = clock()
+        print("Loading graph...")
+        G = blp.load_edge_list(graph_file)
+        t_g = clock()
+        # both passes in one concurrent device step, then the files in the reference's order
+        print("Scoring user and business sides on the device...")
+        masks = method_mask(u_methods, _U_BITS) | blp.CN, method_mask(b_methods, _B_BITS) | blp.CN
+        if ex is None:
+            present, u_scores, b_scores = score_both_sides(examples, G, *masks)
+        else:
+            present, u_scores, b_scores = _score_both_ids(G, ex.pair_user, ex.pair_business, *masks)
+        t_s = clock()
+        if ex is None:
+            _run_side(examples, G, u_methods, u_outfiles, _U_BITS, 0, sidecar, scored=(present, u_scores))
+            _run_side(examples, G, b_methods, b_outfiles, dict(_B_BITS), 1, sidecar, scored=(present, b_scores))
+        else:
+            _write_side(ex, u_methods, u_outfiles, _U_BITS, present, u_scores)
+            _write_side(ex, b_methods, b_outfiles, _B_BITS, present, b_scores)
+    finally:
+        if ex is not None:
+            ex.close()
     if timings is not None:
         timings.update({"examples": t_ex - t, "graph": t_g - t_ex, "score": t_s - t_g, "files": clock() - t_s,
                         "pairs": int(present.sum())})

@@ -1,0 +1,48 @@
+"""Headline-size parity in the GPU suite (BASELINE.json configs[1], "config 2"): the full
+1M-user x 100K-business, 10M-draw graph the bench scores, a slice of its example users, both
+passes of similarity.main enqueued as one co-scheduled step (blp_batches_score) exactly as the
+bench's timed step runs them, checked bit-exact against the C oracle (the reference algorithm,
+similarity.py:20-106, :108-126). The user pass must take the LARGE block variant
+(k_score<1024, 33792, ...>: one LDS bitmap over the 1M-user universe) with its co-scheduled
+CU share -- the kernel and geometry of the headline number. Marked `gpu`."""
+import os
+
+import numpy as np
+import pytest
+
+import blp
+import coracle
+from blp import synth
+from helpers import dense_edges
+
+pytestmark = pytest.mark.gpu
+
+
+def test_config2_slice_both_sides_coscheduled(gpu):
+    U, B, D = synth.CONFIGS["c2"]
+    a, b = synth.review_edges(U, B, D, seed=0)
+    G = blp.DeviceGraph(a, b, device=gpu)
+    ex_x, ex_y, ex_l = synth.make_examples(G, U, B, D, n_users=220, rate=0.01, seed=7)
+    assert len(ex_x) >= 150_000 and len(np.unique(ex_x)) == 220
+    ub, bb = G.batch(ex_x, ex_y), G.batch(ex_y, ex_x)
+    plan = ub.plan()
+    assert plan["block"] == 1024 and plan["chunks"] == 1 and plan["hi"] - plan["lo"] > 33792 * 16, plan
+    G.score_batches([(ub, 7), (bb, 3)])  # the bench's step: both passes concurrent, user pass on its CU share
+    got_u, got_b = ub.fetch(7), bb.fetch(3)
+    ids, oa, ob = dense_edges(a, b)
+    og = coracle.OracleGraph(len(ids), oa, ob)
+    xo = np.searchsorted(ids, G.node_ids[ex_x])
+    yo = np.searchsorted(ids, G.node_ids[ex_y])
+    nt = max(1, len(os.sched_getaffinity(0)))
+    cn, jac, aa, _ = og.score_pairs(xo, yo, 7, nthreads=nt)
+    np.testing.assert_array_equal(got_u["cn"], cn)
+    np.testing.assert_array_equal(got_u["jaccard"], jac)
+    np.testing.assert_array_equal(got_u["adamic"], aa)
+    cn, jac, _, _ = og.score_pairs(yo, xo, 3, nthreads=nt)
+    np.testing.assert_array_equal(got_b["cn"], cn)
+    np.testing.assert_array_equal(got_b["jaccard"], jac)
+    # a repeated step is bit-identical (order-independent exact arithmetic)
+    G.score_batches([(ub, 7), (bb, 3)])
+    again = ub.fetch(7)
+    for k in ("cn", "jaccard", "adamic"):
+        np.testing.assert_array_equal(again[k], got_u[k])

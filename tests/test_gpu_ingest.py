@@ -3,9 +3,10 @@ blp_csr_build_device -> blp_graph_create_from_csr (DeviceGraph.from_device_edges
 the host CSR builder (blp_csr_from_edges, SNAP LoadEdgeList semantics, similarity.py:16)
 and the C oracle; then the sharded-universe scorers on the resulting graph. Marked `gpu`.
 
-The exchange itself (blp.dist.allgather_edges) runs here at world 1 on the device, and at
-world 2 with two processes sharing the one GPU (gloo carries the exchange; the RCCL leg
-needs two GPUs and runs in the driver's multi-GPU bench)."""
+The exchange itself (blp.dist.allgather_edges) runs here three ways: at world 1 on the
+device without a process group; through RCCL (backend "nccl", all_gather_into_tensor) over a
+one-rank process group, the same code N ranks run; and at world 2 with two processes sharing
+the one GPU (gloo carries that exchange: RCCL refuses two ranks on one device)."""
 import ctypes
 import os
 import socket
@@ -277,6 +278,55 @@ def _rank(rank, world, port, outdir):
     G.close()
     d.barrier()
     d.close()
+
+
+def _rccl_world1(port, outdir):
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": "0", "WORLD_SIZE": "1",
+                       "LOCAL_RANK": "0", "BLP_EXCHANGE_BACKEND": "nccl"})
+    d = bd.Dist(exchange=True, collective_at_world1=True)
+    assert d.backend == "nccl" and d.td is not None
+    u, b = bd.block_review_edges(U2, B2, D2, 0, U2, seed=9)
+    a_all, b_all, counts = bd.allgather_edges(d, u, b)  # RCCL all_gather_into_tensor over one rank
+    assert a_all.is_cuda and counts == [len(u)]
+    G = blp.DeviceGraph.from_device_edges(a_all.data_ptr(), b_all.data_ptr(), len(a_all), U2 + B2, U2, device=0)
+    src = np.random.default_rng(3).choice(np.flatnonzero(G.hop1_size[:U2] > 0), 40, replace=False)
+    x = np.repeat(src, 20).astype(np.int32)
+    y = np.random.default_rng(4).integers(U2, U2 + B2, len(x)).astype(np.int32)
+    r = G.score_pairs(x, y, 7)
+    rb = G.score_pairs(y, x, 7)
+    np.savez(os.path.join(outdir, "w1.npz"), rp=G.row_ptr, ci=G.col_idx, u=u, b=b, x=x, y=y, backend=d.backend,
+             **r, **{"b_" + k: v for k, v in rb.items()})
+    G.close()
+    d.barrier()
+    d.close()
+
+
+def test_rccl_allgather_world1(gpu, tmp_path):
+    """The config-5 exchange through RCCL itself (backend "nccl", all_gather_into_tensor),
+    run over a one-rank process group on the one-GPU box: the gathered device partials build
+    the device CSR (equal to the host CSR of the edges) and both sides' scores equal the oracle
+    (dist.py allgather_edges; similarity.py:20-106)."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    p = ctx.Process(target=_rccl_world1, args=(_free_port(), str(tmp_path)))
+    p.start()
+    p.join(110)
+    if p.exitcode is None:
+        p.kill()
+    assert p.exitcode == 0, p.exitcode
+    r = np.load(os.path.join(tmp_path, "w1.npz"))
+    assert str(r["backend"]) == "nccl"
+    rp, ci, _ = _host_csr(U2 + B2, r["u"], r["b"])
+    assert np.array_equal(r["rp"], rp) and np.array_equal(r["ci"], ci)
+    ids, oa, ob = dense_edges(r["u"], r["b"])
+    og = coracle.OracleGraph(len(ids), oa, ob)
+    xs, ys = np.searchsorted(ids, r["x"]), np.searchsorted(ids, r["y"])
+    for pre, (sx, sy) in (("", (xs, ys)), ("b_", (ys, xs))):
+        cn, jac, aa, _ = og.score_pairs(sx, sy, 7)
+        np.testing.assert_array_equal(r[pre + "cn"], cn)
+        np.testing.assert_array_equal(r[pre + "jaccard"], jac)
+        np.testing.assert_array_equal(r[pre + "adamic"], aa)
 
 
 def test_two_ranks_share_the_gpu(gpu, tmp_path):

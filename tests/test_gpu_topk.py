@@ -2,9 +2,10 @@
 
 The oracle (oracle/blp_oracle.topk_full_candidates) scores every exact-distance-3 candidate
 with the reference's set formulas (similarity.py:108-126) and sorts by (score desc, id asc).
-Bit-exact bars: CN and Jaccard lists (ids and scores), |H3| counts, and Adamic-Adar in the
-engine's 2^-40 fixed point (order-independent, equal to blp_score_pairs' values); the
-fixed-point sums agree with the reference's float sums to 1e-9 relative (checked below).
+Bit-exact bars: CN and Jaccard lists (ids and scores), |H3| counts, and Adamic-Adar as the
+correctly rounded sum of the reference's own terms (exact two-word integer sums of
+w * 2^58, blp_internal.h; equal to blp_score_pairs' values and to math.fsum of the terms),
+within a few ulps of the reference's set-order float sums (checked below).
 The reference itself has no top-k: the composition is "parity unpinned" beyond its scorers.
 """
 import math

@@ -163,3 +163,11 @@ def test_unique_ids_match_numpy(span):
         x = rng.integers(-5, span, n).astype(np.int64) + 3
         assert np.array_equal(_unique(x), np.unique(x))
         assert _unique(x).dtype == np.int64
+
+
+def test_main_missing_examples_raises_like_reference(tmp_path):
+    """similarity.main on a missing examples.json raises what the reference's util.load_json
+    (open()) raises -- FileNotFoundError, an IOError -- before any device work."""
+    with pytest.raises(FileNotFoundError):
+        similarity.main(str(tmp_path / "nope.json"), str(tmp_path / "graph.txt"), METHODS,
+                        [None] * 3, METHODS, [None] * 3)

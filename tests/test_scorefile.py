@@ -71,6 +71,11 @@ def test_parse_matches_json_loads(tmp_path):
     '{"1": {"2": [1]}}',            # nested value
     '{"1": {"2": 1, "2": 0}}',      # duplicate inner key (json.loads: first position, last value)
     '{"1": {"2": 1}, "1": {"3": 0}}',  # duplicate outer key
+    '{"1": {"5": 1, "05": 0, "5": 0}}',  # duplicate key of one id interleaved with another spelling
+    '{"1": {"2": abc}}',            # not a JSON value (json.loads raises)
+    '{"1": {"2": 1.2.3}}',
+    '{"1": {"2": tru}}',
+    '{"1": {"2": 01}}',             # leading zero: not JSON
     '[1, 2]',
     '{"1": {"2": 1}} x',
 ])
@@ -78,6 +83,16 @@ def test_parse_refuses_other_shapes(tmp_path, text):
     p = tmp_path / "e.json"
     p.write_text(text)
     assert scorefile.Examples.load(str(p)) is None
+
+
+@pytest.mark.parametrize("label", ["1", "0", "-1", "0.5", "1e3", "-2.5E-7", "true", "false", "null", "NaN", "Infinity",
+                                   "-Infinity"])
+def test_parse_accepts_json_scalars(tmp_path, label):
+    """Every label json.loads accepts (numbers, literals, Python's NaN / Infinity) parses natively."""
+    p = tmp_path / "e.json"
+    p.write_text('{"1": {"2": %s, "3": 0}}' % label)
+    ex = scorefile.Examples.load(str(p))
+    assert ex is not None and ex.n_pairs == 2
 
 
 @pytest.mark.parametrize("kind", ["cn", "jaccard", "adamic", "none"])
