@@ -421,7 +421,7 @@ __device__ inline int block_exscan(int v, int* red, int* total) {
 }
 
 // last s in [lo, hi) with off[s] <= f (requires off[lo] <= f < off[hi])
-__device__ inline int seg_search(const int32_t* off, int ns, int f, int lo = 0, int hi = -1) {
+__device__ __attribute__((always_inline)) inline int seg_search(const int32_t* off, int ns, int f, int lo = 0, int hi = -1) {
   if (hi < 0) hi = ns;
   while (hi - lo > 1) {
     const int mid = (lo + hi) >> 1;
@@ -440,7 +440,7 @@ __device__ inline int seg_search(const int32_t* off, int ns, int f, int lo = 0, 
 // batch (every thread one search at most), ending with a barrier. Returns shift, or -1 (no
 // hint) when the batch is a single block step anyway.
 template <int BLOCK, int CAP>
-__device__ inline int build_hint(const int32_t* s_off, int ns, int step, int32_t* hint) {
+__device__ __attribute__((always_inline)) inline int build_hint(const int32_t* s_off, int ns, int step, int32_t* hint) {
   const int T = s_off[ns];
   if (CAP < 4 || T <= step) return -1;
   int shift = 0;
@@ -455,7 +455,7 @@ __device__ inline int build_hint(const int32_t* s_off, int ns, int step, int32_t
 // segments (w = node id or -1, sk = segment or -1). One LDS binary search per K elements
 // (narrowed by the hint table when given: shift >= 0).
 template <int K>
-__device__ inline void mp_fetch(const int32_t* __restrict__ ci, const int64_t* s_start, const int32_t* s_off, int ns,
+__device__ __attribute__((always_inline)) inline void mp_fetch(const int32_t* __restrict__ ci, const int64_t* s_start, const int32_t* s_off, int ns,
                                 int T, int f0, int* w, int* sk, const int32_t* hint = nullptr, int shift = -1) {
   if (f0 >= T) {
 #pragma unroll
@@ -541,7 +541,7 @@ __device__ inline void scan_push(uint32_t* s_cn, unsigned long long* s_aa, int s
 }
 
 template <int NT, int K, bool GLOBAL = false>
-__device__ inline void mp_build(const int32_t* __restrict__ ci, uint32_t idmask, const int64_t* s_start,
+__device__ __attribute__((always_inline)) inline void mp_build(const int32_t* __restrict__ ci, uint32_t idmask, const int64_t* s_start,
                                 const int32_t* s_off, int ns, int64_t c0, int64_t width, uint32_t* bm, int tid,
                                 const int32_t* hint = nullptr, int shift = -1) {
   const int T = s_off[ns];
@@ -579,7 +579,7 @@ __device__ inline void mp_build(const int32_t* __restrict__ ci, uint32_t idmask,
 // > 0 has the weight wtab[c], code 0 falls back to the per-node table aaw[id].
 
 template <int NT, int K, bool AA, bool PK = false>
-__device__ inline void mp_scan(const int32_t* __restrict__ ci, uint32_t idmask, int idbits,
+__device__ __attribute__((always_inline)) inline void mp_scan(const int32_t* __restrict__ ci, uint32_t idmask, int idbits,
                                const long long* __restrict__ aaw, const long long* wtab, const int64_t* s_start,
                                const int32_t* s_off, int ns, int64_t c0, int64_t width, const uint32_t* bm,
                                uint32_t* s_cn, unsigned long long* s_aa, int tid, const int32_t* hint = nullptr,
@@ -901,7 +901,7 @@ struct RCStep {
 };
 
 template <int K>
-__device__ inline void rc_fetch(const int32_t* __restrict__ ci, const int64_t* s_start, const int32_t* s_off,
+__device__ __attribute__((always_inline)) inline void rc_fetch(const int32_t* __restrict__ ci, const int64_t* s_start, const int32_t* s_off,
                                 const int32_t* s_coff, int ns, int TC, int c, const int32_t* hint, int shift,
                                 RCStep<K>& st) {
   int64_t pos = 0;
@@ -931,13 +931,91 @@ __device__ inline void rc_fetch(const int32_t* __restrict__ ci, const int64_t* s
   }
 }
 
+// Wave-contiguous row-chunk loops (BLP_RCW): each wave takes one contiguous run of the batch's
+// chunks, 64 per step (lane l: chunk cb + 64 i + l), instead of the block taking 1024 chunks per
+// step. A lane's chunks then stay in one row for |row| / 512 steps, so (1) its row is cached in
+// registers (RCSeg) and the LDS binary search runs only when the lane crosses into a new row, and
+// (2) rc_scan sums a lane's hits in registers across those steps and issues its LDS atomics once
+// per row instead of once per step (the 64 lanes of a wave on one long row hit ONE LDS address,
+// a 64-way conflict per atomic). Loads stay coalesced: the 64 lanes of a step read 64
+// consecutive chunks.
+#ifndef BLP_RCW
+#define BLP_RCW 1
+#endif
+struct RCSeg {
+  int s, c0, c1, len;  // cached row: chunks [c0, c1), len ids from start
+  int64_t start;
+};
+
+template <int K>
+__device__ __attribute__((always_inline)) inline void rcw_fetch(const int32_t* __restrict__ ci, const int64_t* s_start, const int32_t* s_off,
+                                 const int32_t* s_coff, int ns, int ce, int c, const int32_t* hint, int shift,
+                                 RCSeg& g, RCStep<K>& st) {
+  int64_t pos = 0;
+  st.s = 0;
+  st.cnt = 0;
+  if (c < ce) {
+    if (c >= g.c1) {  // a lane's chunks only increase: search past the cached row
+      int s;
+      if (shift >= 0) {
+        const int h = c >> shift;
+        s = seg_search(s_coff, ns, c, max(hint[h], g.s), hint[h + 1] + 1);
+      } else {
+        s = seg_search(s_coff, ns, c, g.s);
+      }
+      g.s = s;
+      g.c0 = s_coff[s];
+      g.c1 = s_coff[s + 1];
+      g.start = s_start[s];
+      g.len = s_off[s + 1] - s_off[s];
+    }
+    const int o = (c - g.c0) * K;
+    st.s = g.s;
+    st.cnt = min(K, g.len - o);
+    pos = g.start + o;
+  }
+  const blp::U4a* q = reinterpret_cast<const blp::U4a*>(ci + pos);
+#pragma unroll
+  for (int j = 0; j < K / 4; ++j) {
+    const blp::U4a x = q[j];
+    st.v[4 * j] = x.x;
+    st.v[4 * j + 1] = x.y;
+    st.v[4 * j + 2] = x.z;
+    st.v[4 * j + 3] = x.w;
+  }
+}
+
+template <int NT, int K, typename Proc>
+__device__ __attribute__((always_inline)) inline void rcw_loop(const int32_t* __restrict__ ci, const int64_t* s_start, const int32_t* s_off,
+                                const int32_t* s_coff, int ns, int tid, const int32_t* hint, int shift, Proc proc) {
+  constexpr int NWV = NT / 64;
+  const int TC = s_coff[ns];
+  const int lane = tid & 63, w = tid >> 6;
+  const int per_w = ((TC + 63) / 64 + NWV - 1) / NWV;  // steps per wave (= the block loop's step count)
+  const int cb = w * per_w * 64;
+  const int ce = min(TC, cb + per_w * 64);
+  const int nsteps = ce > cb ? (ce - cb + 63) / 64 : 0;  // wave-uniform; proc has no barrier
+  RCSeg g{0, 0, 0, 0, 0};
+  RCStep<K> A, B;
+  vm_drain();
+  rcw_fetch<K>(ci, s_start, s_off, s_coff, ns, ce, cb + lane, hint, shift, g, A);
+  for (int i = 0; i + 1 < nsteps; i += 2) {
+    rcw_fetch<K>(ci, s_start, s_off, s_coff, ns, ce, cb + (i + 1) * 64 + lane, hint, shift, g, B);
+    proc(A);
+    rcw_fetch<K>(ci, s_start, s_off, s_coff, ns, ce, cb + (i + 2) * 64 + lane, hint, shift, g, A);  // may be past ce
+    proc(B);
+  }
+  if (nsteps & 1) proc(A);
+  vm_drain();
+}
+
 // Two-buffer driver: steps of NT chunks; proc(step) after the next step's loads are issued.
 // BLP_RC3: three buffers, two steps of loads in flight while one is processed.
 #ifndef BLP_RC3
 #define BLP_RC3 0
 #endif
 template <int NT, int K, typename Proc>
-__device__ inline void rc_loop(const int32_t* __restrict__ ci, const int64_t* s_start, const int32_t* s_off,
+__device__ __attribute__((always_inline)) inline void rc_loop(const int32_t* __restrict__ ci, const int64_t* s_start, const int32_t* s_off,
                                const int32_t* s_coff, int ns, int tid, const int32_t* hint, int shift, Proc proc) {
   const int TC = s_coff[ns];
   const int nsteps = (TC + NT - 1) / NT;
@@ -979,7 +1057,7 @@ __device__ inline void rc_loop(const int32_t* __restrict__ ci, const int64_t* s_
 constexpr int RC_EXTRA_WORDS = 36;
 
 template <int NT, int K>
-__device__ inline void rc_build(const int32_t* __restrict__ ci, uint32_t idmask, const int64_t* s_start,
+__device__ __attribute__((always_inline)) inline void rc_build(const int32_t* __restrict__ ci, uint32_t idmask, const int64_t* s_start,
                                 const int32_t* s_off, const int32_t* s_coff, int ns, int64_t c0, int64_t width,
                                 uint32_t* bm, int cap_words, int tid, const int32_t* hint, int shift) {
   const uint32_t keep = idmask | 0x80000000u, c0u = (uint32_t)c0, wu = (uint32_t)width;
@@ -993,7 +1071,10 @@ __device__ inline void rc_build(const int32_t* __restrict__ ci, uint32_t idmask,
       atomicOr(&bm[rr >> 5], 1u << (rr & 31));
     }
   };
-  rc_loop<NT, K>(ci, s_start, s_off, s_coff, ns, tid, hint, shift, proc);
+  if (BLP_RCW)
+    rcw_loop<NT, K>(ci, s_start, s_off, s_coff, ns, tid, hint, shift, proc);
+  else
+    rc_loop<NT, K>(ci, s_start, s_off, s_coff, ns, tid, hint, shift, proc);
 }
 
 // Packed exact-AA layout (packed = true, one LDS chunk): per segment t, s_aa[2 t] = Σ W (wrapping)
@@ -1003,13 +1084,34 @@ __device__ inline void rc_build(const int32_t* __restrict__ ci, uint32_t idmask,
 // undercounts S by < 2^40 + K * 2^32, so S - hi * 2^40 < cn * 2^41 < 2^64 (blp::aa_exact, hs = 40).
 
 template <int NT, int K, bool AA>
-__device__ inline void rc_scan(const int32_t* __restrict__ ci, uint32_t idmask, int idbits,
+__device__ __attribute__((always_inline)) inline void rc_scan(const int32_t* __restrict__ ci, uint32_t idmask, int idbits,
                                const long long* __restrict__ aaw, const long long* wtab, const int64_t* s_start,
                                const int32_t* s_off, const int32_t* s_coff, int ns, int64_t c0, int64_t width,
                                const uint32_t* bm, int cap_words, uint32_t* s_cn, unsigned long long* s_aa, int tid,
                                const int32_t* hint, int shift, bool packed = false) {
   const uint32_t keep = idmask | 0x80000000u, c0u = (uint32_t)c0, wu = (uint32_t)width;
   const uint32_t safe = (uint32_t)cap_words << 5;
+  // BLP_RCW: the lane's sums for its current row, flushed to LDS when the row changes (and at
+  // the end); the same additions as the per-step atomics, so the LDS totals are identical.
+  // packed AA: lo = Σ W, hi = Σ_steps ((Σ_step W >> 32) >> 8) << PK_CN_BITS | cn; other AA:
+  // lo = Σ W, hi = Σ (W >> 32); counts in cn (or in hi's low bits when packed).
+  int acc_s = -1;
+  uint32_t acc_c = 0;
+  unsigned long long acc_lo = 0, acc_hi = 0;
+  auto flush = [&]() {
+    if (acc_c == 0) return;
+    if (AA && packed) {
+      atomicAdd(&s_aa[2 * acc_s], acc_lo);
+      atomicAdd(&s_aa[2 * acc_s + 1], acc_hi);
+    } else if (AA) {
+      aa_push(s_aa, acc_s, acc_lo, acc_hi);
+      atomicAdd(&s_cn[acc_s], acc_c);
+    } else if (packed) {
+      atomicAdd(&s_aa[2 * acc_s + 1], (unsigned long long)acc_c);
+    } else {
+      atomicAdd(&s_cn[acc_s], acc_c);
+    }
+  };
   // Branch-free phases, so the scheduler can issue all K bitmap reads (and weight reads)
   // before the first use: one LDS round trip per step instead of one per id.
   auto proc = [&](const RCStep<K>& st) {
@@ -1052,12 +1154,34 @@ __device__ inline void rc_scan(const int32_t* __restrict__ ci, uint32_t idmask, 
               acch += (uint32_t)(w >> 32);
             }
         }
+        if (BLP_RCW) {
+          if (st.s != acc_s) {
+            flush();
+            acc_s = st.s;
+            acc_c = 0;
+            acc_lo = acc_hi = 0;
+          }
+          acc_c += (unsigned)__popc(hm);
+          acc_lo += acc;
+          acc_hi += packed ? ((unsigned long long)(acch >> (PK_HS - 32)) << PK_CN_BITS) | (unsigned)__popc(hm)
+                           : (unsigned long long)acch;
+          return;
+        }
         if (packed) {
           atomicAdd(&s_aa[2 * st.s], acc);
           atomicAdd(&s_aa[2 * st.s + 1], ((unsigned long long)(acch >> (PK_HS - 32)) << PK_CN_BITS) | (unsigned)__popc(hm));
           return;
         }
         aa_push(s_aa, st.s, acc, acch);
+      }
+      if (BLP_RCW) {
+        if (st.s != acc_s) {
+          flush();
+          acc_s = st.s;
+          acc_c = 0;
+        }
+        acc_c += (unsigned)__popc(hm);
+        return;
       }
       if (!AA && packed) {  // counts only, in the packed word (the chunk-parallel scorer)
         atomicAdd(&s_aa[2 * st.s + 1], (unsigned long long)__popc(hm));
@@ -1066,13 +1190,18 @@ __device__ inline void rc_scan(const int32_t* __restrict__ ci, uint32_t idmask, 
       atomicAdd(&s_cn[st.s], (unsigned)__popc(hm));
     }
   };
-  rc_loop<NT, K>(ci, s_start, s_off, s_coff, ns, tid, hint, shift, proc);
+  if (BLP_RCW) {
+    rcw_loop<NT, K>(ci, s_start, s_off, s_coff, ns, tid, hint, shift, proc);
+    flush();
+  } else {
+    rc_loop<NT, K>(ci, s_start, s_off, s_coff, ns, tid, hint, shift, proc);
+  }
 }
 
 // Chunk prefix of a batch whose element offsets s_off[0..ns] are in LDS: s_coff[t] = sum of
 // ceil(len / K) over rows < t; s_coff[ns] = total. Ends with a barrier.
 template <int BLOCK, int K>
-__device__ inline void rc_chunk_offsets(const int32_t* s_off, int ns, int32_t* s_coff, int* red) {
+__device__ __attribute__((always_inline)) inline void rc_chunk_offsets(const int32_t* s_off, int ns, int32_t* s_coff, int* red) {
   const int nc = (int)threadIdx.x < ns ? (s_off[threadIdx.x + 1] - s_off[threadIdx.x] + K - 1) / K : 0;
   int tot;
   const int ex = block_exscan<BLOCK>(nc, red, &tot);
@@ -1107,7 +1236,7 @@ __device__ inline void row_part(const int32_t* __restrict__ ci, int64_t st, int 
 }
 
 template <int NT>
-__device__ inline void row_build(const int32_t* __restrict__ ci, uint32_t idmask, const int64_t* s_start,
+__device__ __attribute__((always_inline)) inline void row_build(const int32_t* __restrict__ ci, uint32_t idmask, const int64_t* s_start,
                                  const int32_t* s_off, int ns, int64_t c0, int64_t width, uint32_t* bm, int tid) {
   const uint32_t keep = idmask | 0x80000000u, c0u = (uint32_t)c0, wu = (uint32_t)width;
   for (int t = tid; t < ns; t += NT) {
@@ -1128,7 +1257,7 @@ __device__ inline void row_build(const int32_t* __restrict__ ci, uint32_t idmask
 }
 
 template <int NT, bool AA>
-__device__ inline void row_scan(const int32_t* __restrict__ ci, uint32_t idmask, int idbits,
+__device__ __attribute__((always_inline)) inline void row_scan(const int32_t* __restrict__ ci, uint32_t idmask, int idbits,
                                 const long long* __restrict__ aaw, const long long* wtab, const int64_t* s_start,
                                 const int32_t* s_off, int ns, int64_t c0, int64_t width, const uint32_t* bm,
                                 uint32_t* s_cn, unsigned long long* s_aa, int tid) {
@@ -1168,7 +1297,7 @@ __device__ inline void row_scan(const int32_t* __restrict__ ci, uint32_t idmask,
 
 // Load the rows of N(x)[k0, k0 + ns) as segments: start / exclusive offsets (s_off[ns] = total).
 template <int BLOCK>
-__device__ inline void load_row_segments(const int64_t* __restrict__ rp, const int32_t* __restrict__ ci, int64_t k0,
+__device__ __attribute__((always_inline)) inline void load_row_segments(const int64_t* __restrict__ rp, const int32_t* __restrict__ ci, int64_t k0,
                                          int ns, int64_t* s_start, int32_t* s_off, int* red,
                                          const int32_t* __restrict__ skip = nullptr) {
   int len = 0;

@@ -47,7 +47,7 @@ constexpr int TK_KMAX = 256;
 #define BLP_TK_RB 8
 #endif
 #ifndef BLP_TK_TAIL16
-#define BLP_TK_TAIL16 0  // 1: row entries past the first TK_RB read as 16-byte vectors (4 per load)
+#define BLP_TK_TAIL16 1  // row entries past the first TK_RB read as 16-byte vectors (4 per load); 0: one by one
 #endif
 constexpr int TK_RB = BLP_TK_RB;   // row entries loaded up front per element (16-byte vectors)
 constexpr uint32_t TK_EMPTY = 0xFFFFFFFFu;
