@@ -104,6 +104,7 @@ struct blp_graph {
   hipStream_t stream = nullptr;
   int64_t n = 0;    // nodes
   int64_t nnz = 0;  // stored CSR entries (both directions, no self-loops)
+  int64_t max_row = 0;  // longest CSR row (graph_finish)
   int64_t* d_rp = nullptr;   // [n+1]
   int32_t* d_ci = nullptr;   // [nnz], CI_PAD readable ids on each side
   long long* d_aaw_fx = nullptr;  // [n] Adamic-Adar weight per node, W = w * 2^58 (exact; or null)

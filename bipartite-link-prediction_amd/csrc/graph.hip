@@ -203,6 +203,8 @@ int graph_finish(blp_graph* g, const double* aaw) {
   if (hipGetDeviceProperties(&prop, g->device) == hipSuccess) g->n_cu = prop.multiProcessorCount;
   if (!g->stream) BLP_HIP(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
   const int64_t n = g->n;
+  g->max_row = 0;
+  for (int64_t v = 0; v < n; ++v) g->max_row = std::max<int64_t>(g->max_row, g->hrp[v + 1] - g->hrp[v]);
   if (aaw) {
     std::vector<long long> fx;
     if (int rc = aa_weights_fixed(aaw, n, fx)) return rc;

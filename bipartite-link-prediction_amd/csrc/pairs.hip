@@ -1210,6 +1210,43 @@ __device__ __attribute__((always_inline)) inline void rc_chunk_offsets(const int
   __syncthreads();
 }
 
+// Element AND chunk offsets of a batch of ns segments (thread t < ns holds segment t's length) in
+// ONE block scan: the pair (len, ceil(len / K)) packed in 64 bits -- the low half never carries
+// into the high one, a batch holds < 2^31 ids -- instead of a scan for s_off followed by
+// rc_chunk_offsets' scan for s_coff: three barriers fewer per batch. Ends with a barrier.
+template <int BLOCK, int K>
+__device__ __attribute__((always_inline)) inline void seg_offsets(int len, int ns, int32_t* s_off, int32_t* s_coff,
+                                                                  unsigned long long* red64) {
+  constexpr int NW = BLOCK / 64;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const unsigned long long v = ((unsigned long long)(uint32_t)len << 32) | (uint32_t)((len + K - 1) / K);
+  unsigned long long inc = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const unsigned long long t = __shfl_up(inc, d, 64);
+    if (lane >= d) inc += t;
+  }
+  if (lane == 63) red64[wid] = inc;
+  __syncthreads();
+  unsigned long long base = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    const unsigned long long t = red64[w];
+    base += w < wid ? t : 0ull;
+    tot += t;
+  }
+  const unsigned long long ex = base + inc - v;
+  if ((int)threadIdx.x < ns) {
+    s_off[threadIdx.x] = (int32_t)(ex >> 32);
+    s_coff[threadIdx.x] = (int32_t)(uint32_t)ex;
+  }
+  if (threadIdx.x == 0) {
+    s_off[ns] = (int32_t)(tot >> 32);
+    s_coff[ns] = (int32_t)(uint32_t)tot;
+  }
+  __syncthreads();  // also orders red64's reads before its next use
+}
+
 // Short rows (every row of the batch at most SHORT_MAX ids -- the business side, whose rows
 // are user rows Γ(w)): one thread per segment reads its whole row with up to SHORT_MAX / 4
 // 16-byte loads, all issued before any is used. No merge-path search and no row crossings,
@@ -1688,6 +1725,21 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
           } else
           for (int64_t k0 = xb; k0 < xe; k0 += SEG) {
             const int ns = (int)min<int64_t>(SEG, xe - k0);
+            if (RC && !(a.short_rows & 1)) {  // row-chunk build: element and chunk offsets in one scan
+              int len = 0;
+              if ((int)threadIdx.x < ns) {
+                const int z = a.ci[k0 + threadIdx.x];
+                const int64_t st = a.rp[z];
+                s_start[threadIdx.x] = st;
+                len = (nhot && a.hot_idx[z] >= 0) ? 0 : (int)(a.rp[z + 1] - st);  // dense rows were OR-ed in
+              }
+              seg_offsets<BLOCK, K>(len, ns, s_off, s_coff, red64);
+              const int shift = build_hint<BLOCK, HC>(s_coff, ns, BLOCK, s_hint);
+              rc_build<BLOCK, K>(a.cw, a.idmask, s_start, s_off, s_coff, ns, c0, width, bm, CAP_WORDS, threadIdx.x,
+                                 s_hint, shift);
+              __syncthreads();
+              continue;
+            }
             load_row_segments<BLOCK>(a.rp, a.ci, k0, ns, s_start, s_off, red, nhot ? a.hot_idx : nullptr);
             if (SHORT || (a.short_rows & 1)) {
               row_build<BLOCK>(a.cw, a.idmask, s_start, s_off, ns, c0, width, bm, threadIdx.x);
@@ -1757,11 +1809,16 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
               s_aa[2 * threadIdx.x + 1] = 0;
             }
           }
-          int tot;
-          const int ex = block_exscan<BLOCK>(len, red, &tot);
-          if ((int)threadIdx.x < ns) s_off[threadIdx.x] = ex;
-          if (threadIdx.x == 0) s_off[ns] = tot;
-          __syncthreads();
+          const bool rcs = RC && !(a.short_rows & 2);  // row-chunk scan: element and chunk offsets in one scan
+          if (rcs) {
+            seg_offsets<BLOCK, K>(len, ns, s_off, s_coff, red64);
+          } else {
+            int tot;
+            const int ex = block_exscan<BLOCK>(len, red, &tot);
+            if ((int)threadIdx.x < ns) s_off[threadIdx.x] = ex;
+            if (threadIdx.x == 0) s_off[ns] = tot;
+            __syncthreads();
+          }
           // the next segment's metadata, in flight during this segment's scan (BLP_PFN)
           have_pf = PF && !SHORT && BLP_PFN && nchunks == 1 && sb + SEG < pcnt;
           if (have_pf && (int)threadIdx.x < min(SEG, pcnt - sb - SEG)) {
@@ -1780,8 +1837,7 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
                                      s_aa, threadIdx.x);
           } else if constexpr (SHORT) {
           } else if (RC) {
-            rc_chunk_offsets<BLOCK, K>(s_off, ns, s_coff, red);
-            const int shift = build_hint<BLOCK, HC>(s_coff, ns, BLOCK, s_hint);
+            const int shift = build_hint<BLOCK, HC>(s_coff, ns, BLOCK, s_hint);  // s_coff: seg_offsets above
             if (want_a)
               rc_scan<BLOCK, K, true>(a.cw, a.idmask, a.idbits, a.aaw, s_wtab, s_start, s_off, s_coff, ns, c0, width,
                                       bm, CAP_WORDS, s_cn, s_aa, threadIdx.x, s_hint, shift, packed);
@@ -1977,11 +2033,13 @@ __global__ void k_row_splits(const int64_t* __restrict__ rp, const int32_t* __re
   }
 }
 
+constexpr int SPLIT_CN_BITS = 24;  // k_score_split pk24: count field of the packed per-pair word
+
 template <int BLOCK, int CAP_WORDS, int SEG, int K>
 __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_split(ScoreArgs a, const int32_t* __restrict__ g_y,
                                                        const int32_t* __restrict__ rsplit, int64_t rs_lo, int C,
                                                        uint32_t* __restrict__ pcn, unsigned long long* __restrict__ paa,
-                                                       uint32_t* __restrict__ ph2, int64_t np) {
+                                                       uint32_t* __restrict__ ph2, int64_t np, int pk24) {
   constexpr int NW = BLOCK / 64;
   // 128 KiB chunks (one workgroup per CU) use the row-chunk loops of the large scorer
   constexpr bool RCS = BLP_RC && CAP_WORDS > 16384;
@@ -2100,25 +2158,47 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
       const unsigned long long h2 = block_sum_u64<BLOCK>(pc, red64);
       if (threadIdx.x == 0) ph2[(int64_t)s * C + c] = (uint32_t)h2;
     }
+    // Pair-batch metadata: the pair's y and row start (chunk-independent), then its slice bounds
+    // for chunk c from the split table. The next batch's y / row start are loaded during this
+    // batch's offsets, its slice bounds right after this batch's scan, so each batch starts with
+    // its metadata in registers instead of two dependent global round trips.
+    int pf_y = 0;
+    int64_t pf_yb = 0;
+    int pf_s0 = 0, pf_s1 = 0;
+    if ((int)threadIdx.x < min(SEG, pcnt)) {
+      const int gp = pbeg + threadIdx.x;
+      pf_y = g_y[gp];
+      pf_yb = a.g_yb[gp];
+      const int32_t* sp = rsplit + ((int64_t)pf_y - rs_lo) * (C + 1) + c;
+      pf_s0 = sp[0];
+      pf_s1 = sp[1];
+    }
     for (int sb = 0; sb < pcnt; sb += SEG) {
       const int ns = min(SEG, pcnt - sb);
       int len = 0;
       if ((int)threadIdx.x < ns) {
-        const int gp = pbeg + sb + threadIdx.x;
-        const int32_t* sp = rsplit + ((int64_t)g_y[gp] - rs_lo) * (C + 1) + c;
-        s_start[threadIdx.x] = a.g_yb[gp] + sp[0];
-        len = sp[1] - sp[0];
+        s_start[threadIdx.x] = pf_yb + pf_s0;
+        len = pf_s1 - pf_s0;
         s_aa[2 * threadIdx.x] = 0;
         s_aa[2 * threadIdx.x + 1] = 0;
       }
-      int tot;
-      const int ex = block_exscan<BLOCK>(len, red, &tot);
-      if ((int)threadIdx.x < ns) s_off[threadIdx.x] = ex;
-      if (threadIdx.x == 0) s_off[ns] = tot;
-      __syncthreads();
+      const int ns_next = min(SEG, pcnt - sb - SEG);  // <= 0: last batch
+      if constexpr (RCS) {
+        seg_offsets<BLOCK, K>(len, ns, s_off, s_coff, red64);
+      } else {
+        int tot;
+        const int ex = block_exscan<BLOCK>(len, red, &tot);
+        if ((int)threadIdx.x < ns) s_off[threadIdx.x] = ex;
+        if (threadIdx.x == 0) s_off[ns] = tot;
+        __syncthreads();
+      }
+      if ((int)threadIdx.x < ns_next) {
+        const int gp = pbeg + sb + SEG + threadIdx.x;
+        pf_y = g_y[gp];
+        pf_yb = a.g_yb[gp];
+      }
       // packed count + high word (a chunk holds < 2^21 nodes), converted per slice below
       if constexpr (RCS) {
-        rc_chunk_offsets<BLOCK, K>(s_off, ns, s_coff, red);
         const int shift = build_hint<BLOCK, HCS>(s_coff, ns, BLOCK, s_hint);
         if (want_a)
           rc_scan<BLOCK, K, true>(a.cw, a.idmask, a.idbits, a.aaw, wtab, s_start, s_off, s_coff, ns, c0, width, bm,
@@ -2133,22 +2213,36 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
         mp_scan<BLOCK, K, false, true>(a.cw, a.idmask, a.idbits, a.aaw, a.wtab, s_start, s_off, ns, c0, width, bm,
                                        nullptr, s_aa, threadIdx.x);
       }
+      if ((int)threadIdx.x < ns_next) {  // the next batch's slice bounds, in flight over the output phase
+        const int32_t* sp = rsplit + ((int64_t)pf_y - rs_lo) * (C + 1) + c;
+        pf_s0 = sp[0];
+        pf_s1 = sp[1];
+      }
       __syncthreads();
       // a pair's chunk partials meet in per-pair accumulators: only (pair, chunk) slices with a
-      // hit add anything (a few per pair), so no [chunks][pairs] partial arrays (config 5:
-      // 96 chunks x 199M pairs) and no dense combine reads
+      // hit add anything, so no [chunks][pairs] partial arrays (config 5: 48 chunks x 199M
+      // pairs) and no dense combine reads. With Adamic-Adar and every scanned row shorter than
+      // 2^24 (pk24), two atomics per slice: paa[2p] += S mod 2^64 and paa[2p + 1] +=
+      // (S >> 52) << 24 | count -- exact (blp::aa_exact with hs = 52: the 2^52 remainders of at
+      // most C < 2^12 slices sum below 2^64; S >> 52 <= count * 2^7 per slice, so the high field
+      // stays below 2^40); otherwise the count, S mod 2^64 and S >> 32 in three.
       for (int t = threadIdx.x; t < ns; t += BLOCK) {
         const int64_t gp = pbeg + sb + t;
         const unsigned c_t = (unsigned)(s_aa[2 * t + 1] & ((1u << PK_CN_BITS) - 1));
         if (c_t) {
-          atomicAdd(&pcn[gp], c_t);
           if (want_a) {
-            // the slice's exact 128-bit sum S from (lo, hi in 2^40 units), re-expressed as
-            // (S mod 2^64, S >> 32): these add across slices like the two-word form (hs = 32)
+            // the slice's exact 128-bit sum S from (lo, hi in 2^40 units)
             unsigned long long sh, sl;
             blp::aa_exact(s_aa[2 * t], s_aa[2 * t + 1] >> PK_CN_BITS, &sh, &sl, PK_HS);
             atomicAdd(&paa[2 * gp], sl);
-            atomicAdd(&paa[2 * gp + 1], (sh << 32) | (sl >> 32));
+            if (pk24) {
+              atomicAdd(&paa[2 * gp + 1], (((sh << 12) | (sl >> 52)) << SPLIT_CN_BITS) | c_t);
+            } else {
+              atomicAdd(&pcn[gp], c_t);
+              atomicAdd(&paa[2 * gp + 1], (sh << 32) | (sl >> 32));
+            }
+          } else {
+            atomicAdd(&pcn[gp], c_t);
           }
         }
       }
@@ -2160,7 +2254,7 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
 // one wave per active source: sum the chunk partials of each of its pairs, then Jaccard
 __global__ __launch_bounds__(256) void k_split_combine(ScoreArgs a, int C, const uint32_t* __restrict__ pcn,
                                                       const unsigned long long* __restrict__ paa,
-                                                      const uint32_t* __restrict__ ph2, int64_t np) {
+                                                      const uint32_t* __restrict__ ph2, int64_t np, int pk24) {
   const int lane = threadIdx.x & 63;
   const int n_active = a.misc->n_active;
   const bool want_j = (a.mask & BLP_JACCARD) != 0;
@@ -2173,11 +2267,11 @@ __global__ __launch_bounds__(256) void k_split_combine(ScoreArgs a, int C, const
     const int pbeg = a.off[x], pcnt = a.cnt[x];
     for (int t = lane; t < pcnt; t += 64) {
       const int64_t gp = pbeg + t;
-      const unsigned cn = pcn[gp];
       const unsigned long long lo = want_a ? paa[2 * gp] : 0ull, hi = want_a ? paa[2 * gp + 1] : 0ull;
+      const unsigned cn = pk24 ? (unsigned)(hi & ((1u << SPLIT_CN_BITS) - 1)) : pcn[gp];
       const int p = a.g_out[gp];
       a.cn[p] = cn;
-      if (want_a) a.aa[p] = blp::aa_value(lo, hi);
+      if (want_a) a.aa[p] = pk24 ? blp::aa_value(lo, hi >> SPLIT_CN_BITS, 52) : blp::aa_value(lo, hi);
       if (want_j) {
         const long long uni = h2 + a.g_yl[gp] - (long long)cn;
         if (uni <= 0) {
@@ -2961,21 +3055,23 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   a.dq = b->dq;
   a.short_rows = b->short_rows;
   if (np && b->split) {
-    BLP_HIP(hipMemsetAsync(b->d_pcn, 0, 4 * (size_t)np, b->stream));
+    // AA counts ride in the packed per-pair word while every row (hence every count) < 2^24
+    const int pk24 = (mask & BLP_ADAMIC) && g->max_row < (int64_t(1) << SPLIT_CN_BITS) && !getenv("BLP_SPLIT_NOPK");
+    if (!pk24) BLP_HIP(hipMemsetAsync(b->d_pcn, 0, 4 * (size_t)np, b->stream));
     if (mask & BLP_ADAMIC) BLP_HIP(hipMemsetAsync(b->d_paa, 0, 16 * (size_t)np, b->stream));
     int per_cu = 1;
     if (b->split_big) {
       BLP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_score_split<S_BLOCK, S_CAP_BIG, S_SEG, 8>, S_BLOCK, 0));
       hipLaunchKernelGGL((k_score_split<S_BLOCK, S_CAP_BIG, S_SEG, 8>), dim3(g->n_cu * std::max(per_cu, 1)), dim3(S_BLOCK),
-                         0, b->stream, a, b->d_gy, b->d_rsplit, b->rs_lo, b->split, b->d_pcn, b->d_paa, b->d_ph2, np);
+                         0, b->stream, a, b->d_gy, b->d_rsplit, b->rs_lo, b->split, b->d_pcn, b->d_paa, b->d_ph2, np, pk24);
     } else {
       BLP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_score_split<S_BLOCK, S_CAP, S_SEG, 8>, S_BLOCK, 0));
       hipLaunchKernelGGL((k_score_split<S_BLOCK, S_CAP, S_SEG, 8>), dim3(g->n_cu * std::max(per_cu, 1)), dim3(S_BLOCK), 0,
-                         b->stream, a, b->d_gy, b->d_rsplit, b->rs_lo, b->split, b->d_pcn, b->d_paa, b->d_ph2, np);
+                         b->stream, a, b->d_gy, b->d_rsplit, b->rs_lo, b->split, b->d_pcn, b->d_paa, b->d_ph2, np, pk24);
     }
     BLP_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_split_combine, dim3(g->n_cu * 8), dim3(256), 0, b->stream, a, b->split, b->d_pcn, b->d_paa,
-                       b->d_ph2, np);
+                       b->d_ph2, np, pk24);
     BLP_HIP(hipGetLastError());
   } else if (np && b->global) {
     a.hot_idx = nullptr;

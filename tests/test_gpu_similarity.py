@@ -104,6 +104,8 @@ def test_general_graph_exact_distance(gpu):
     {"BLP_CHUNK_BITS": "1024", "BLP_NO_GLOBAL": "1"},   # multi-chunk LDS bitmap universe
     {"BLP_FORCE_GLOBAL": "1"},                          # HBM-bitmap scorer on a small universe
     {"BLP_SPLIT": "3"},                                 # chunk-parallel scorer, 3 chunks
+    {"BLP_SPLIT": "3", "BLP_SPLIT_NOPK": "1"},          # ... per-pair count in its own word (rows >= 2^24)
+    {"BLP_SPLIT": "5", "BLP_SPLIT_BIG": "1", "BLP_SPLIT_NOPK": "1"},
     {"BLP_SPLIT": "8", "BLP_HEAVY_WORK": "50"},         # ... 8 chunks, heavy sources pre-built
     {"BLP_SPLIT": "2", "BLP_HOT_MIN": "8"},             # ... dense rows OR-ed per chunk
     {"BLP_SPLIT": "40"},                                # ... many chunks, some empty
@@ -159,11 +161,17 @@ def test_kernel_paths_vs_oracle(gpu, knobs, monkeypatch):
         assert G.batch(x, y).plan()["chunks"] == -int(knobs["BLP_SPLIT"])  # chunk-parallel scorer
 
 
-@pytest.mark.parametrize("variant", [None, "1", "2"])
+@pytest.mark.parametrize("variant", [None, "1", "2", "split", "split_big", "split_nopk"])
 def test_many_pairs_per_source_vs_oracle(gpu, variant, monkeypatch):
     # > SEG pairs per source and > SEG rows in N(x): the segment-chunk loops; batches of more
-    # than one block step: the segment hint tables
-    if variant:
+    # than one block step: the segment hint tables. Chunk-parallel scorer: several pair batches
+    # per (source, chunk) item, so the next batch's metadata comes from the in-flight prefetch
+    knobs = {"split": {"BLP_SPLIT": "3"}, "split_big": {"BLP_SPLIT": "4", "BLP_SPLIT_BIG": "1"},
+             "split_nopk": {"BLP_SPLIT": "4", "BLP_SPLIT_BIG": "1", "BLP_SPLIT_NOPK": "1"}}
+    if variant in knobs:
+        for k, v in knobs[variant].items():
+            monkeypatch.setenv(k, v)
+    elif variant:
         monkeypatch.setenv("BLP_VARIANT", variant)
     rng = np.random.default_rng(12)
     a, b = bipartite_edges(rng, 20000, 1500, 200000)
