@@ -14,12 +14,29 @@ Two modes, both with no collective on the scoring data path:
 torch is plumbing here (process group, device buffers for the collective); the graph and
 every kernel live in libblp.so.
 """
+import contextlib
 import os
 import sys
 
 import numpy as np
 
 from . import synth
+
+
+@contextlib.contextmanager
+def stdout_to_stderr():
+    """Point file descriptor 1 at stderr: gloo's connection banner and RCCL's version banner
+    (printed when its communicator forms, at the first collective) go to stdout from C++, and
+    the bench's stdout is its one JSON line."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        yield
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
 
 
 class Dist:
@@ -48,10 +65,7 @@ class Dist:
             self.td = td
             # gloo's C++ layer prints its connection banner on stdout; the bench's stdout is
             # its one JSON line, so stdout is pointed at stderr while the groups form
-            sys.stdout.flush()
-            saved = os.dup(1)
-            os.dup2(2, 1)
-            try:
+            with stdout_to_stderr():
                 if exchange and os.environ.get("BLP_EXCHANGE_BACKEND", "nccl") == "nccl":
                     import torch
 
@@ -63,10 +77,6 @@ class Dist:
                     td.init_process_group("gloo")
                     self.backend = "gloo"
                 td.barrier(group=self.cpu_group)  # every rank connected before stdout returns
-            finally:
-                sys.stdout.flush()
-                os.dup2(saved, 1)
-                os.close(saved)
         else:
             self.backend = None
 
@@ -175,7 +185,9 @@ def allgather_edges(dist, a_local, b_local):
         return mine[0, : counts[0]].contiguous(), mine[1, : counts[0]].contiguous(), counts
     out = torch.empty((dist.world, 2, max(mx, 1)), dtype=torch.int32, device=dev)
     if dist.backend == "nccl":
-        dist.td.all_gather_into_tensor(out, mine)
+        with stdout_to_stderr():  # the communicator forms here (RCCL's banner)
+            dist.td.all_gather_into_tensor(out, mine)
+            torch.cuda.synchronize(dev)
     else:
         dist.td.all_gather(list(out.unbind(0)), mine, group=dist.cpu_group)
     a = torch.cat([out[r, 0, : counts[r]] for r in range(dist.world)])

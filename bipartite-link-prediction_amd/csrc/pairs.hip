@@ -940,7 +940,7 @@ __device__ __attribute__((always_inline)) inline void rc_fetch(const int32_t* __
 // a 64-way conflict per atomic). Loads stay coalesced: the 64 lanes of a step read 64
 // consecutive chunks.
 #ifndef BLP_RCW
-#define BLP_RCW 1
+#define BLP_RCW 0
 #endif
 struct RCSeg {
   int s, c0, c1, len;  // cached row: chunks [c0, c1), len ids from start
