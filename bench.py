@@ -769,7 +769,8 @@ def run_e2e(args):
                                       "candidates kept at %g; u_methods = b_methods = CN, Jaccard, AA (the reference's "
                                       "__main__ call, similarity.py:129-135)" % (args.config, U, B, D, len(examples),
                                                                                   args.rate), "pairs": n},
-               "e2e_s": e2e, "phases_s": {k: v for k, v in ph.items() if k != "pairs"},
+               "e2e_s": e2e, "phases_s": {k: v for k, v in ph.items() if k not in ("pairs", "graph_detail")},
+               "graph_phase_detail_s": ph.get("graph_detail"),
                "device_step_ms": dev_ms, "device_pairs_per_s": n / (dev_ms / 1e3),
                "cpu_reference_algorithm": {"kind": "port", "what": "C oracle scoring of every pair of both sides "
                                            "(graph already built; no file I/O)", **cpu},

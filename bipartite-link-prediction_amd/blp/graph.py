@@ -419,8 +419,15 @@ class PairBatch:
 
 def load_edge_list(path, c0=0, c1=1, device=0):
     """snap.LoadEdgeList(snap.PUNGraph, path, c0, c1) -> DeviceGraph (similarity.py:16)."""
+    import time
+
+    t0 = time.perf_counter()
     a, b = parse_edge_list(path, c0, c1)
-    return DeviceGraph(a, b, device=device)
+    t1 = time.perf_counter()
+    G = DeviceGraph(a, b, device=device)
+    if getattr(G, "build_times", None) is not None:
+        G.build_times["parse_s"] = t1 - t0
+    return G
 
 
 LoadEdgeList = load_edge_list

@@ -124,15 +124,33 @@ def score_both_sides(examples, G, u_mask, b_mask):
     return _score_both_ids(G, u_ids, v_ids, u_mask, b_mask)
 
 
-def _score_both_ids(G, u_ids, v_ids, u_mask, b_mask):
+def _score_both_ids(G, u_ids, v_ids, u_mask, b_mask, timings=None):
+    """Id lookup, the two batches (created concurrently: blp_batch_create's host planning
+    releases the GIL), one concurrent device step, and the results; phase times into
+    ``timings`` (score_lookup, score_create, score_device, score_fetch) when given."""
+    import time
+    from concurrent.futures import ThreadPoolExecutor
+
+    t0 = time.perf_counter()
     du, pu = G.lookup(u_ids)
     dv, pv = G.lookup(v_ids)
     present = pu & pv
-    ub = G.batch(du[present], dv[present])
-    bb = G.batch(dv[present], du[present])
+    xs, ys = (du, dv) if present.all() else (du[present], dv[present])
+    t1 = time.perf_counter()
+    with ThreadPoolExecutor(1) as pool:
+        fb = pool.submit(G.batch, ys, xs)
+        ub = G.batch(xs, ys)
+        bb = fb.result()
     try:
+        t2 = time.perf_counter()
         G.score_batches([(ub, u_mask), (bb, b_mask)])
-        return present, ub.fetch(u_mask), bb.fetch(b_mask)
+        blp.device_sync(G.device)  # the batches run on their own streams
+        t3 = time.perf_counter()
+        res = present, ub.fetch(u_mask), bb.fetch(b_mask)
+        if timings is not None:
+            timings.update({"score_lookup": t1 - t0, "score_create": t2 - t1, "score_device": t3 - t2,
+                            "score_fetch": time.perf_counter() - t3})
+        return res
     finally:
         ub.close()
         bb.close()
@@ -188,22 +206,39 @@ def main(example_file, graph_file, u_methods, u_outfiles, b_methods, b_outfiles,
     # json.loads, as util.load_json); the score files are then written natively with the same
     # text json.dumps gives (blp/scorefile.py). With sidecar=True the dict path runs.
     import os
+    from concurrent.futures import ThreadPoolExecutor
 
-    # a missing or unreadable file raises what util.load_json raises (IOError / FileNotFoundError)
-    ex = None if sidecar or not os.path.isfile(example_file) else scorefile.Examples.load(example_file)
-    examples = util.load_json(example_file) if ex is None else None
+    def load_examples():
+        # a missing or unreadable file raises what util.load_json raises (IOError / FileNotFoundError)
+        e = None if sidecar or not os.path.isfile(example_file) else scorefile.Examples.load(example_file)
+        return e, (util.load_json(example_file) if e is None else None)
+
+    if not os.path.isfile(example_file):
+        load_examples()  # raises (before any device work, as the reference does)
+    # examples.json is parsed on a second thread while the graph loads (both native calls release
+    # the GIL); a third starts the HIP runtime, whose first call costs a few tenths of a second
+    pool = ThreadPoolExecutor(2)
+    fut_ex = pool.submit(load_examples)
+    pool.submit(blp.device_sync, 0)
+    ex = None
     try:
-        t_ex = clock()
         print("Loading graph...")
-        G = blp.load_edge_list(graph_file)
+        try:
+            G = blp.load_edge_list(graph_file)
+        except BaseException:
+            if fut_ex.exception() is not None:  # the reference reports the examples file first
+                raise fut_ex.exception()
+            raise
         t_g = clock()
+        ex, examples = fut_ex.result()
+        t_ex = clock()
         # both passes in one concurrent device step, then the files in the reference's order
         print("Scoring user and business sides on the device...")
         masks = method_mask(u_methods, _U_BITS) | blp.CN, method_mask(b_methods, _B_BITS) | blp.CN
         if ex is None:
             present, u_scores, b_scores = score_both_sides(examples, G, *masks)
         else:
-            present, u_scores, b_scores = _score_both_ids(G, ex.pair_user, ex.pair_business, *masks)
+            present, u_scores, b_scores = _score_both_ids(G, ex.pair_user, ex.pair_business, *masks, timings=timings)
         t_s = clock()
         if ex is None:
             _run_side(examples, G, u_methods, u_outfiles, _U_BITS, 0, sidecar, scored=(present, u_scores))
@@ -212,11 +247,17 @@ def main(example_file, graph_file, u_methods, u_outfiles, b_methods, b_outfiles,
             _write_side(ex, u_methods, u_outfiles, _U_BITS, present, u_scores)
             _write_side(ex, b_methods, b_outfiles, _B_BITS, present, b_scores)
     finally:
+        pool.shutdown(wait=True)
+        if ex is None and fut_ex.done() and fut_ex.exception() is None:
+            ex = fut_ex.result()[0]
         if ex is not None:
             ex.close()
     if timings is not None:
-        timings.update({"examples": t_ex - t, "graph": t_g - t_ex, "score": t_s - t_g, "files": clock() - t_s,
+        # examples and graph load concurrently: "graph" is the graph load, "examples" the extra
+        # wait for examples.json after it
+        timings.update({"graph": t_g - t, "examples": t_ex - t_g, "score": t_s - t_ex, "files": clock() - t_s,
                         "pairs": int(present.sum())})
+        timings["graph_detail"] = dict(getattr(G, "build_times", None) or {})
 
 
 def users(examples, G, methods, outfiles, *, sidecar=False):
