@@ -23,6 +23,14 @@ import numpy as np
 from . import _lib
 from ._lib import check, lib, ptr
 
+_I64P = ctypes.POINTER(ctypes.c_int64)
+_lib.register("blp_edges_load", [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)])
+_lib.register("blp_edges_info", [ctypes.c_void_p, _I64P, _I64P, _I64P, _I64P, _I64P])
+_lib.register("blp_edges_fetch", [ctypes.c_void_p] * 7)
+_lib.register("blp_edges_destroy", [ctypes.c_void_p])
+_lib.register("blp_ids_lookup", [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64,
+                                 ctypes.c_void_p])
+
 
 def parse_edge_list(path, c0=0, c1=1):
     """graph.txt -> (a, b) int64 arrays (SNAP LoadEdgeList text semantics)."""
@@ -79,6 +87,10 @@ class HostGraph:
         if len(a_ids) != len(b_ids):
             raise ValueError("edge endpoint arrays differ in length")
         da, db = self._ids(a_ids, b_ids)
+        self._host_csr(da, db, aa)
+
+    def _host_csr(self, da, db, aa):
+        """The CSR of the dense edge list on the host (blp_csr_from_edges)."""
         rp = np.zeros(self.n + 1, np.int64)
         ci = np.empty(max(2 * len(da), 1), np.int32)
         sl = np.zeros(max(self.n, 1), np.uint8)
@@ -86,6 +98,36 @@ class HostGraph:
         check(lib().blp_csr_from_edges(self.n, len(da), ptr(da), ptr(db), ptr(rp), ptr(ci), ptr(sl),
                                        ctypes.byref(nnz)))
         self._set_csr(rp, ci[: nnz.value].copy(), sl[: self.n], aa)
+
+    def _set_ids(self, node_ids, n_col0, id_lo, id_map, n_edges_in):
+        """The id map as blp_edges_load built it natively (same order as _ids): a dense table
+        id_map[id - id_lo] answers every lookup."""
+        self.node_ids = node_ids
+        self.n_col0 = int(n_col0)
+        self.n = len(node_ids)
+        self._id_lo = int(id_lo)
+        self._id_map = id_map
+        self.n_edges_in = n_edges_in
+
+    @property
+    def _sort(self):  # dense ids in original-id order (the searchsorted lookup of sparse id spaces)
+        if getattr(self, "_sort_", None) is None:
+            self._sort_ = np.argsort(self.node_ids, kind="stable")
+        return self._sort_
+
+    @_sort.setter
+    def _sort(self, v):
+        self._sort_ = v
+
+    @property
+    def _sorted_ids(self):
+        if getattr(self, "_sorted_ids_", None) is None:
+            self._sorted_ids_ = self.node_ids[self._sort]
+        return self._sorted_ids_
+
+    @_sorted_ids.setter
+    def _sorted_ids(self, v):
+        self._sorted_ids_ = v
 
     def _ids(self, a_ids, b_ids):
         """The id map (dense ids: column-0 ids ascending, then the other ids ascending) and the
@@ -134,6 +176,12 @@ class HostGraph:
         ids = np.asarray(ids, dtype=np.int64)
         if self.n == 0:
             return np.full(len(ids), -1, np.int32), np.zeros(len(ids), bool)
+        if getattr(self, "_id_map", None) is not None:  # native table lookup (multi-threaded)
+            ids = np.ascontiguousarray(ids)
+            dense = np.empty(len(ids), np.int32)
+            check(lib().blp_ids_lookup(ptr(self._id_map), self._id_lo, len(self._id_map), ptr(ids), len(ids),
+                                       ptr(dense)))
+            return dense, dense >= 0
         lo, span = int(self._sorted_ids[0]), int(self._sorted_ids[-1]) - int(self._sorted_ids[0]) + 1
         if span <= max(4 * self.n, 1 << 20):  # compact id space: one direct table gather
             tab = getattr(self, "_direct", None)
@@ -182,23 +230,39 @@ class DeviceGraph(HostGraph):
         b_ids = np.asarray(b_ids, dtype=np.int64)
         if len(a_ids) != len(b_ids):
             raise ValueError("edge endpoint arrays differ in length")
-        if len(a_ids) == 0 or len(a_ids) < int(os.environ.get("BLP_DEVICE_CSR_MIN", 1 << 16)):
-            HostGraph.__init__(self, a_ids, b_ids, aa=aa)
-            self._upload(device, aa)
-            return
-        # large edge lists: the CSR is built on the device (blp_csr_build_host: upload, radix
-        # sort of the directed (row, col) keys, unique) and the host mirror fetched back --
-        # the same CSR as blp_csr_from_edges (tests/test_gpu_ingest.py)
         import time
 
         t0 = time.perf_counter()
         da, db = self._ids(a_ids, b_ids)
-        t1 = time.perf_counter()
+        self._build(da, db, device, aa)
+        self.build_times["id_map_s"] = time.perf_counter() - t0 - self.build_times.get("total_s", 0.0)
+
+    def _build(self, da, db, device, aa):
+        """CSR + graph handle from dense endpoints (the id map is set)."""
+        import time
+
+        t0 = time.perf_counter()
+        if len(da) == 0 or len(da) < int(os.environ.get("BLP_DEVICE_CSR_MIN", 1 << 16)):
+            self._host_csr(da, db, aa)
+            self._upload(device, aa)
+            self.build_times = {"total_s": time.perf_counter() - t0}
+            return
+        # large edge lists: the CSR is built on the device (blp_csr_build_host: upload, radix
+        # sort of the directed (row, col) keys, unique) and the host mirror fetched back --
+        # the same CSR as blp_csr_from_edges (tests/test_gpu_ingest.py)
         c = ctypes.c_void_p()
         check(lib().blp_csr_build_host(device, ptr(da), ptr(db), len(da), self.n, ctypes.byref(c)))
-        t2 = time.perf_counter()
+        t1 = time.perf_counter()
         self._adopt_csr(c, device, aa)
-        self.build_times.update({"id_map_s": t1 - t0, "device_csr_s": t2 - t1})
+        self.build_times.update({"device_csr_s": t1 - t0, "total_s": time.perf_counter() - t0})
+
+    @classmethod
+    def from_dense(cls, da, db, node_ids, n_col0, id_lo, id_map, device=0, aa=True):
+        """A graph from dense endpoints plus the id map blp_edges_load built natively."""
+        g = cls.__new__(cls)
+        g._set_ids(node_ids, n_col0, id_lo, id_map, len(da))
+        g._build(da, db, device, aa)
+        return g
 
     @classmethod
     def from_csr(cls, row_ptr, col_idx, self_loop, n_col0, device=0, aa=True):
@@ -418,15 +482,37 @@ class PairBatch:
 
 
 def load_edge_list(path, c0=0, c1=1, device=0):
-    """snap.LoadEdgeList(snap.PUNGraph, path, c0, c1) -> DeviceGraph (similarity.py:16)."""
+    """snap.LoadEdgeList(snap.PUNGraph, path, c0, c1) -> DeviceGraph (similarity.py:16).
+
+    The file is parsed once (multi-threaded) and, for a compact id space, mapped to dense ids
+    natively (blp_edges_load); otherwise the raw endpoints go through HostGraph._ids."""
     import time
 
     t0 = time.perf_counter()
-    a, b = parse_edge_list(path, c0, c1)
-    t1 = time.perf_counter()
-    G = DeviceGraph(a, b, device=device)
-    if getattr(G, "build_times", None) is not None:
-        G.build_times["parse_s"] = t1 - t0
+    L = lib()
+    h = ctypes.c_void_p()
+    bpath = path.encode() if isinstance(path, str) else path
+    check(L.blp_edges_load(bpath, c0, c1, ctypes.byref(h)))
+    try:
+        m, n, n0, lo, span = (ctypes.c_int64() for _ in range(5))
+        check(L.blp_edges_info(h, *(ctypes.byref(v) for v in (m, n, n0, lo, span))))
+        if span.value > 0:
+            da = np.empty(m.value, np.int32)
+            db = np.empty(m.value, np.int32)
+            node_ids = np.empty(n.value, np.int64)
+            id_map = np.empty(span.value, np.int32)
+            check(L.blp_edges_fetch(h, None, None, ptr(da), ptr(db), ptr(node_ids), ptr(id_map)))
+            t1 = time.perf_counter()
+            G = DeviceGraph.from_dense(da, db, node_ids, n0.value, lo.value, id_map, device=device)
+        else:
+            a = np.empty(m.value, np.int64)
+            b = np.empty(m.value, np.int64)
+            check(L.blp_edges_fetch(h, ptr(a), ptr(b), None, None, None, None))
+            t1 = time.perf_counter()
+            G = DeviceGraph(a, b, device=device)
+    finally:
+        L.blp_edges_destroy(h)
+    G.build_times["parse_and_id_map_s"] = t1 - t0
     return G
 
 

@@ -6,6 +6,8 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
+#include <climits>
 #include <thread>
 #include <vector>
 
@@ -58,11 +60,11 @@ inline bool parse_line(const char* p, const char* e, int c0, int c1, int64_t* va
   return ga && gb;
 }
 
-}  // namespace
 
-extern "C" int blp_edges_parse(const char* path, int c0, int c1, int64_t* a, int64_t* b, int64_t* m_out) {
+// Parse the file once into per-thread slices (file order within and across slices).
+int parse_slices(const char* path, int c0, int c1, std::vector<Slice>& sl) {
   using namespace blp;
-  BLP_CHECK(path && m_out && c0 >= 0 && c1 >= 0, BLP_E_ARG, "blp_edges_parse: bad arguments");
+  BLP_CHECK(path && c0 >= 0 && c1 >= 0, BLP_E_ARG, "blp_edges_parse: bad arguments");
   int fd = open(path, O_RDONLY);
   if (fd < 0) return fail(BLP_E_ARG, std::string("blp_edges_parse: cannot open ") + path);
   struct stat st;
@@ -88,10 +90,12 @@ extern "C" int blp_edges_parse(const char* path, int c0, int c1, int64_t* a, int
     while (c < size && data[c - 1] != '\n') ++c;
     cut[t] = c;
   }
-  std::vector<Slice> sl(nt);
+  sl.assign(nt, Slice{});
   auto work = [&](unsigned t) {
     const char* p = data + cut[t];
     const char* end = data + cut[t + 1];
+    sl[t].a.reserve((cut[t + 1] - cut[t]) / 12 + 16);
+    sl[t].b.reserve((cut[t + 1] - cut[t]) / 12 + 16);
     while (p < end) {
       const char* e = p;
       while (e < end && *e != '\n') ++e;
@@ -111,17 +115,186 @@ extern "C" int blp_edges_parse(const char* path, int c0, int c1, int64_t* a, int
   for (auto& x : th) x.join();
   if (data) munmap((void*)data, size);
   close(fd);
+  return BLP_OK;
+}
+
+// f(t, lo, hi) over [0, n) cut into `nt` ranges, on nt threads
+template <class F>
+void par_for(int64_t n, unsigned nt, F f) {
+  if (n < (1 << 16)) nt = 1;
+  std::vector<std::thread> th;
+  for (unsigned t = 1; t < nt; ++t) th.emplace_back(f, t, n * t / nt, n * (t + 1) / nt);
+  f(0u, (int64_t)0, n / nt);
+  for (auto& x : th) x.join();
+}
+
+unsigned n_threads() { return std::max(1u, std::min(16u, std::thread::hardware_concurrency())); }
+
+}  // namespace
+
+// A parsed edge list and, when the id space is compact, its dense id map: ids seen in column
+// 0 ascending, then the ids seen only in column 1 ascending (blp/graph.py HostGraph._ids; a
+// reference bipartite graph.txt puts users in one dense range and businesses in another).
+struct blp_edges {
+  std::vector<Slice> sl;
   int64_t m = 0;
-  for (auto& s : sl) m += (int64_t)s.a.size();
+  int64_t n = 0, n_col0 = 0, lo = 0, span = 0;  // span == 0: no dense map (sparse id space)
+  std::vector<int32_t> map;                       // [span] dense id of id lo + i, or -1
+  std::vector<int64_t> node_ids;                  // [n] dense id -> original id
+};
+
+using namespace blp;
+
+extern "C" int blp_edges_parse(const char* path, int c0, int c1, int64_t* a, int64_t* b, int64_t* m_out) {
+  BLP_CHECK(m_out, BLP_E_ARG, "blp_edges_parse: bad arguments");
+  std::vector<Slice> sl;
+  if (int rc = parse_slices(path, c0, c1, sl)) return rc;
+  int64_t m = 0;
+  for (auto& x : sl) m += (int64_t)x.a.size();
   if (a && b) {
     BLP_CHECK(*m_out >= m, BLP_E_ARG, "blp_edges_parse: output arrays too small");
     int64_t k = 0;
-    for (auto& s : sl) {
-      std::copy(s.a.begin(), s.a.end(), a + k);
-      std::copy(s.b.begin(), s.b.end(), b + k);
-      k += (int64_t)s.a.size();
+    for (auto& x : sl) {
+      std::copy(x.a.begin(), x.a.end(), a + k);
+      std::copy(x.b.begin(), x.b.end(), b + k);
+      k += (int64_t)x.a.size();
     }
   }
   *m_out = m;
+  return BLP_OK;
+}
+
+extern "C" int blp_edges_load(const char* path, int c0, int c1, blp_edges** out) {
+  BLP_CHECK(out, BLP_E_ARG, "blp_edges_load: null out");
+  auto* e = new blp_edges();
+  if (int rc = parse_slices(path, c0, c1, e->sl)) {
+    delete e;
+    return rc;
+  }
+  const unsigned nt = (unsigned)e->sl.size();
+  std::vector<int64_t> base(nt + 1, 0);
+  for (unsigned t = 0; t < nt; ++t) base[t + 1] = base[t] + (int64_t)e->sl[t].a.size();
+  e->m = base[nt];
+  if (e->m) {
+    std::vector<int64_t> mn(nt, INT64_MAX), mx(nt, INT64_MIN);
+    std::vector<std::thread> th;
+    auto mm = [&](unsigned t) {
+      for (size_t i = 0; i < e->sl[t].a.size(); ++i) {
+        mn[t] = std::min({mn[t], e->sl[t].a[i], e->sl[t].b[i]});
+        mx[t] = std::max({mx[t], e->sl[t].a[i], e->sl[t].b[i]});
+      }
+    };
+    for (unsigned t = 1; t < nt; ++t) th.emplace_back(mm, t);
+    mm(0);
+    for (auto& x : th) x.join();
+    const int64_t lo = *std::min_element(mn.begin(), mn.end()), hi = *std::max_element(mx.begin(), mx.end());
+    const int64_t span = hi - lo + 1;
+    if (span > 0 && span <= std::max<int64_t>(4 * e->m, 1 << 20) && span < (int64_t(1) << 31)) {
+      // presence per column (byte flags: concurrent stores of the same value only)
+      std::vector<uint8_t> in0(span, 0), in1(span, 0);
+      th.clear();
+      auto mark = [&](unsigned t) {
+        for (size_t i = 0; i < e->sl[t].a.size(); ++i) {
+          in0[e->sl[t].a[i] - lo] = 1;
+          in1[e->sl[t].b[i] - lo] = 1;
+        }
+      };
+      for (unsigned t = 1; t < nt; ++t) th.emplace_back(mark, t);
+      mark(0);
+      for (auto& x : th) x.join();
+      // ranks: column-0 ids first, then column-1-only ids, each ascending (block counts + prefix)
+      const unsigned nb = n_threads();
+      std::vector<int64_t> c0n(nb + 1, 0), c1n(nb + 1, 0);
+      par_for(span, nb, [&](unsigned t, int64_t b0, int64_t b1) {
+        int64_t x = 0, y = 0;
+        for (int64_t i = b0; i < b1; ++i) {
+          x += in0[i];
+          y += (int)(in0[i] == 0) & (int)(in1[i] != 0);
+        }
+        c0n[t + 1] = x;
+        c1n[t + 1] = y;
+      });
+      const unsigned used = span < (1 << 16) ? 1u : nb;
+      for (unsigned t = 0; t < used; ++t) {
+        c0n[t + 1] += c0n[t];
+        c1n[t + 1] += c1n[t];
+      }
+      e->lo = lo;
+      e->span = span;
+      e->n_col0 = c0n[used];
+      e->n = e->n_col0 + c1n[used];
+      e->map.assign(span, -1);
+      e->node_ids.resize(e->n);
+      par_for(span, nb, [&](unsigned t, int64_t b0, int64_t b1) {
+        int64_t r0 = c0n[t], r1 = e->n_col0 + c1n[t];
+        for (int64_t i = b0; i < b1; ++i) {
+          if (in0[i]) {
+            e->map[i] = (int32_t)r0;
+            e->node_ids[r0++] = lo + i;
+          } else if (in1[i]) {
+            e->map[i] = (int32_t)r1;
+            e->node_ids[r1++] = lo + i;
+          }
+        }
+      });
+    }
+  }
+  *out = e;
+  return BLP_OK;
+}
+
+extern "C" int blp_edges_info(const blp_edges* e, int64_t* m, int64_t* n_nodes, int64_t* n_col0, int64_t* id_lo,
+                              int64_t* id_span) {
+  BLP_CHECK(e, BLP_E_ARG, "blp_edges_info: null handle");
+  if (m) *m = e->m;
+  if (n_nodes) *n_nodes = e->n;
+  if (n_col0) *n_col0 = e->n_col0;
+  if (id_lo) *id_lo = e->lo;
+  if (id_span) *id_span = e->span;
+  return BLP_OK;
+}
+
+extern "C" int blp_edges_fetch(const blp_edges* e, int64_t* a, int64_t* b, int32_t* da, int32_t* db, int64_t* node_ids,
+                               int32_t* id_map) {
+  BLP_CHECK(e, BLP_E_ARG, "blp_edges_fetch: null handle");
+  BLP_CHECK(e->span > 0 || !(da || db || node_ids || id_map), BLP_E_STATE,
+            "blp_edges_fetch: no dense id map (sparse id space): fetch a / b only");
+  const unsigned nt = (unsigned)e->sl.size();
+  std::vector<int64_t> base(nt + 1, 0);
+  for (unsigned t = 0; t < nt; ++t) base[t + 1] = base[t] + (int64_t)e->sl[t].a.size();
+  std::vector<std::thread> th;
+  auto work = [&](unsigned t) {
+    const Slice& x = e->sl[t];
+    const int64_t k = base[t];
+    for (size_t i = 0; i < x.a.size(); ++i) {
+      if (a) a[k + i] = x.a[i];
+      if (b) b[k + i] = x.b[i];
+      if (da) da[k + i] = e->map[x.a[i] - e->lo];
+      if (db) db[k + i] = e->map[x.b[i] - e->lo];
+    }
+  };
+  for (unsigned t = 1; t < nt; ++t) th.emplace_back(work, t);
+  work(0);
+  for (auto& x : th) x.join();
+  if (node_ids) std::copy(e->node_ids.begin(), e->node_ids.end(), node_ids);
+  if (id_map) std::copy(e->map.begin(), e->map.end(), id_map);
+  return BLP_OK;
+}
+
+extern "C" int blp_edges_destroy(blp_edges* e) {
+  delete e;
+  return BLP_OK;
+}
+
+// ids -> dense ids through a dense map (blp_edges_fetch's id_map): -1 for ids outside the graph
+extern "C" int blp_ids_lookup(const int32_t* id_map, int64_t id_lo, int64_t id_span, const int64_t* ids, int64_t n,
+                              int32_t* dense) {
+  BLP_CHECK(id_map && n >= 0 && (n == 0 || (ids && dense)), BLP_E_ARG, "blp_ids_lookup: bad arguments");
+  par_for(n, n_threads(), [&](unsigned, int64_t b0, int64_t b1) {
+    for (int64_t i = b0; i < b1; ++i) {
+      const int64_t o = ids[i] - id_lo;
+      dense[i] = (o >= 0 && o < id_span) ? id_map[o] : -1;
+    }
+  });
   return BLP_OK;
 }

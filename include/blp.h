@@ -100,6 +100,22 @@ int blp_graph_create_from_csr(blp_csr* c, const int64_t* row_ptr, const int32_t*
  * call (the OS page cache serves the second read).                                       */
 int blp_edges_parse(const char* path, int c0, int c1, int64_t* a, int64_t* b, int64_t* m_out);
 
+/* blp_edges_load: the same parse, once, into a handle, plus -- when the id space is compact
+ * (max - min < 4 * edges or 2^20) -- the dense id map of the engine's graph (similarity.py:16
+ * node ids; blp/graph.py HostGraph._ids): ids seen in column c0 ascending, then ids seen only
+ * in column c1 ascending. blp_edges_info reports id_span == 0 when there is no map.
+ * blp_edges_fetch copies any of: raw endpoints a / b (int64, file order), dense endpoints
+ * da / db (int32), node_ids[n_nodes] (dense -> original id) and id_map[id_span] (original id
+ * id_lo + i -> dense id or -1). blp_ids_lookup maps ids through id_map (-1: not in the graph),
+ * the membership test of similarity.py:22-26 / :66-70. Host-only, multi-threaded.          */
+typedef struct blp_edges blp_edges;
+int blp_edges_load(const char* path, int c0, int c1, blp_edges** out);
+int blp_edges_info(const blp_edges* e, int64_t* m, int64_t* n_nodes, int64_t* n_col0, int64_t* id_lo, int64_t* id_span);
+int blp_edges_fetch(const blp_edges* e, int64_t* a, int64_t* b, int32_t* da, int32_t* db, int64_t* node_ids,
+                    int32_t* id_map);
+int blp_edges_destroy(blp_edges* e);
+int blp_ids_lookup(const int32_t* id_map, int64_t id_lo, int64_t id_span, const int64_t* ids, int64_t n, int32_t* dense);
+
 /* Upload a CSR (from blp_csr_from_edges or equivalent) to device `device`.
  * aa_weight[n_nodes]: per-node Adamic-Adar term, (log deg)^-1 for SNAP degree > 1 else 0,
  * computed by the caller with the reference's own arithmetic (similarity.py:121-125);

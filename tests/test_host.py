@@ -171,3 +171,72 @@ def test_main_missing_examples_raises_like_reference(tmp_path):
     with pytest.raises(FileNotFoundError):
         similarity.main(str(tmp_path / "nope.json"), str(tmp_path / "graph.txt"), METHODS,
                         [None] * 3, METHODS, [None] * 3)
+
+
+def _native_edges(path):
+    L = blp.lib()
+    from blp import graph as bg  # noqa: F401  (registers the blp_edges_* signatures)
+
+    h = ctypes.c_void_p()
+    blp._lib.check(L.blp_edges_load(str(path).encode(), 0, 1, ctypes.byref(h)))
+    try:
+        m, n, n0, lo, span = (ctypes.c_int64() for _ in range(5))
+        blp._lib.check(L.blp_edges_info(h, *(ctypes.byref(v) for v in (m, n, n0, lo, span))))
+        a = np.empty(m.value, np.int64)
+        b = np.empty(m.value, np.int64)
+        out = {"m": m.value, "n": n.value, "n_col0": n0.value, "lo": lo.value, "span": span.value, "a": a, "b": b}
+        P = blp._lib.ptr
+        if span.value:
+            out.update(da=np.empty(m.value, np.int32), db=np.empty(m.value, np.int32),
+                       node_ids=np.empty(n.value, np.int64), id_map=np.empty(span.value, np.int32))
+            blp._lib.check(L.blp_edges_fetch(h, P(a), P(b), P(out["da"]), P(out["db"]), P(out["node_ids"]),
+                                             P(out["id_map"])))
+        else:
+            blp._lib.check(L.blp_edges_fetch(h, P(a), P(b), None, None, None, None))
+        return out
+    finally:
+        L.blp_edges_destroy(h)
+
+
+@pytest.mark.parametrize("kind", ["golden", "compact", "negative", "sparse"])
+def test_native_edge_load_equals_host_id_map(tmp_path, kind):
+    """blp_edges_load (one threaded parse + the dense id map, similarity.py:16) gives the same
+    endpoints as blp_edges_parse and the same id map as HostGraph._ids: column-0 ids ascending,
+    then column-1-only ids ascending; dense lookups agree with HostGraph.lookup, absent ids -1."""
+    rng = np.random.default_rng(3)
+    if kind == "golden":
+        path = os.path.join(GOLDEN, "bip", "train", "graph.txt")
+    else:
+        if kind == "compact":
+            a = rng.integers(0, 5000, 300000)
+            b = rng.integers(5000, 5600, 300000)
+        elif kind == "negative":
+            a = rng.integers(-3000, 3000, 300000)
+            b = rng.integers(-3000, 3000, 300000)
+        else:
+            a = rng.integers(0, 10**12, 1000) * 7
+            b = rng.integers(0, 10**12, 1000) * 11
+        a[:5] = b[:5]  # self-loops
+        path = tmp_path / "graph.txt"
+        with open(path, "w") as f:
+            f.write("# comment\n")
+            f.write("".join("%d\t%d\n" % (x, y) for x, y in zip(a, b)))
+    got = _native_edges(path)
+    ra, rb = blp.parse_edge_list(str(path))
+    np.testing.assert_array_equal(got["a"], ra)
+    np.testing.assert_array_equal(got["b"], rb)
+    H = blp.HostGraph(ra, rb)
+    if kind == "sparse":
+        assert got["span"] == 0
+        return
+    assert got["span"] > 0 and got["n"] == H.n and got["n_col0"] == H.n_col0
+    np.testing.assert_array_equal(got["node_ids"], H.node_ids)
+    np.testing.assert_array_equal(got["da"], H.dense(ra))
+    np.testing.assert_array_equal(got["db"], H.dense(rb))
+    probe = np.concatenate([ra[:1000], rb[:1000], [got["lo"] - 1, got["lo"] + got["span"], 10**15, -10**15]])
+    probe = np.ascontiguousarray(probe, np.int64)
+    dense = np.empty(len(probe), np.int32)
+    blp._lib.check(blp.lib().blp_ids_lookup(blp._lib.ptr(got["id_map"]), got["lo"], got["span"],
+                                            blp._lib.ptr(probe), len(probe), blp._lib.ptr(dense)))
+    exp, _ = H.lookup(probe)
+    np.testing.assert_array_equal(dense, exp)
