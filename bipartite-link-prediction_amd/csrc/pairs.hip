@@ -1134,26 +1134,23 @@ __device__ __attribute__((always_inline)) inline void rc_scan(const int32_t* __r
     for (int k = 0; k < K; ++k) hm |= ((wd[k] >> (rr[k] & 31)) & 1u) << k;
     if (hm) {
       if (AA) {
-        // the step's high words fit 32 bits: K <= 16 terms of W >> 32 < 2^27 (W < 2^59)
+        // the step's sum is exact in one u64: K <= 16 terms W < 2^59. Its high part acc >> 32
+        // (< 2^31) is the step's high-word contribution: hi * 2^32 <= S and S - hi * 2^32 <
+        // (steps with a hit) * 2^32 <= cn * 2^32 (blp::aa_exact); packed, acc >> 40 in 2^40 units
         unsigned long long acc = 0;
-        uint32_t acch = 0, esc = 0;
+        uint32_t esc = 0;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
           const bool h = (hm >> k) & 1u;
-          const unsigned long long w = h ? (unsigned long long)wt[k] : 0ull;
-          acc += w;
-          acch += (uint32_t)(w >> 32);
+          acc += h ? (unsigned long long)wt[k] : 0ull;
           esc |= (h & ((((uint32_t)st.v[k] >> idbits) & 255u) == 0u)) ? 1u << k : 0u;
         }
         if (esc) {  // code-0 ids: the per-node weight (rare on a coded id stream)
 #pragma unroll
           for (int k = 0; k < K; ++k)
-            if ((esc >> k) & 1u) {
-              const unsigned long long w = (unsigned long long)aaw[st.v[k] & idmask];
-              acc += w;
-              acch += (uint32_t)(w >> 32);
-            }
+            if ((esc >> k) & 1u) acc += (unsigned long long)aaw[st.v[k] & idmask];
         }
+        const uint32_t acch = (uint32_t)(acc >> 32);
         if (BLP_RCW) {
           if (st.s != acc_s) {
             flush();
