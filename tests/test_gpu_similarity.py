@@ -110,6 +110,8 @@ def test_general_graph_exact_distance(gpu):
     {"BLP_SPLIT": "2", "BLP_HOT_MIN": "8"},             # ... dense rows OR-ed per chunk
     {"BLP_SPLIT": "40"},                                # ... many chunks, some empty
     {"BLP_SPLIT": "3", "BLP_SPLIT_BIG": "1"},           # ... 128 KiB chunks, one workgroup per CU
+    {"BLP_SPLIT": "3", "BLP_SPLIT_BIG": "1", "BLP_SPLIT_SHORT": "0"},  # ... no thread-per-slice short path
+    {"BLP_SPLIT": "2", "BLP_SPLIT_BIG": "1", "BLP_SPLIT_SHORT": "4"},  # ... short path only below 5 ids
     {"BLP_SPLIT": "24", "BLP_SPLIT_BIG": "1"},          # ... same, many chunks
     {"BLP_HEAVY_WORK": "50"},                           # heavy sources pre-built by k_heavy
     {"BLP_HEAVY_WORK": "1"},                            # one row per heavy item
@@ -161,13 +163,14 @@ def test_kernel_paths_vs_oracle(gpu, knobs, monkeypatch):
         assert G.batch(x, y).plan()["chunks"] == -int(knobs["BLP_SPLIT"])  # chunk-parallel scorer
 
 
-@pytest.mark.parametrize("variant", [None, "1", "2", "split", "split_big", "split_nopk"])
+@pytest.mark.parametrize("variant", [None, "1", "2", "split", "split_big", "split_nopk", "split_noshort"])
 def test_many_pairs_per_source_vs_oracle(gpu, variant, monkeypatch):
     # > SEG pairs per source and > SEG rows in N(x): the segment-chunk loops; batches of more
     # than one block step: the segment hint tables. Chunk-parallel scorer: several pair batches
     # per (source, chunk) item, so the next batch's metadata comes from the in-flight prefetch
     knobs = {"split": {"BLP_SPLIT": "3"}, "split_big": {"BLP_SPLIT": "4", "BLP_SPLIT_BIG": "1"},
-             "split_nopk": {"BLP_SPLIT": "4", "BLP_SPLIT_BIG": "1", "BLP_SPLIT_NOPK": "1"}}
+             "split_nopk": {"BLP_SPLIT": "4", "BLP_SPLIT_BIG": "1", "BLP_SPLIT_NOPK": "1"},
+             "split_noshort": {"BLP_SPLIT": "4", "BLP_SPLIT_BIG": "1", "BLP_SPLIT_SHORT": "0"}}
     if variant in knobs:
         for k, v in knobs[variant].items():
             monkeypatch.setenv(k, v)
