@@ -44,6 +44,9 @@
 #ifndef BLP_PFN
 #define BLP_PFN 1  // ... and every later segment's metadata during the previous segment's scan
 #endif
+#ifndef BLP_SHORT_FAST
+#define BLP_SHORT_FAST 1  // short-row scorer: thread-owned pair rows, no per-batch offset scan (0: the batch loop)
+#endif
 #ifndef BLP_PP
 #define BLP_PP 1  // ping-pong merge-path loops in k_score (0: the single-buffer mp_build / mp_scan)
 #endif
@@ -1759,6 +1762,103 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
           }
         }
         PROF(3)
+        if constexpr (SHORT && BLP_SHORT_FAST) {
+          {  // (the host gives this kernel one-chunk universes only: short_kernel)
+            // Short-row scorer, one chunk: the pairs' rows are thread-owned (SEG == BLOCK), so
+            // after H2(x) is final each thread scans its pair's row and writes the scores itself
+            // -- no offset scan, no LDS accumulators, no barrier per pair batch. x's own bit is
+            // left out of the popcount and cleared between the reduction's two barriers.
+            static_assert(!SHORT || SEG == BLOCK, "one pair per thread");
+            if (nx_hi >= c0 && nx_lo < c1) {  // N(x) inside the universe (general graphs)
+              for (int64_t k = xb + threadIdx.x; k < xe; k += BLOCK) {
+                const int64_t r = (int64_t)a.ci[k] - c0;
+                if (r >= 0 && r < width) atomicAnd(&bm[r >> 5], ~(1u << (r & 31)));
+              }
+              __syncthreads();
+            }
+            const bool x_in = x >= c0 && x < c1;
+            const int64_t xr = x - c0;
+            {
+              unsigned long long pc = 0;
+              if (want_j)
+                for (int i = threadIdx.x; i < nw4; i += BLOCK) {
+                  uint4 q = bm4[i];
+                  if (x_in && i == (int)(xr >> 7)) {  // x is not in H2(x)
+                    const uint32_t m = ~(1u << (xr & 31));
+                    const int j = (int)((xr >> 5) & 3);
+                    q.x &= j == 0 ? m : ~0u;
+                    q.y &= j == 1 ? m : ~0u;
+                    q.z &= j == 2 ? m : ~0u;
+                    q.w &= j == 3 ? m : ~0u;
+                  }
+                  pc += __popc(q.x) + __popc(q.y) + __popc(q.z) + __popc(q.w);
+                }
+              for (int o = 32; o > 0; o >>= 1) pc += __shfl_xor(pc, o, 64);
+              if ((threadIdx.x & 63) == 0) red64[threadIdx.x >> 6] = pc;
+              __syncthreads();  // every popcount read is done
+              if (threadIdx.x == 0 && x_in) atomicAnd(&bm[xr >> 5], ~(1u << (xr & 31)));
+#pragma unroll
+              for (int w = 0; w < NW; ++w) h2 += red64[w];
+              __syncthreads();  // x's bit cleared before any scan; red64 free again
+            }
+            PROF(5)
+            const uint32_t keep = a.idmask | 0x80000000u, wu = (uint32_t)width;
+            const uint32_t c0u = (uint32_t)c0;
+            for (int sb = 0; sb < pcnt; sb += SEG) {
+              const int t = sb + (int)threadIdx.x;
+              if (t >= pcnt) break;
+              int64_t st;
+              int len, p;
+              if (PF && sb == 0) {
+                st = pf_start;
+                len = pf_len;
+                p = pf_out;
+              } else {
+                const int gp = pbeg + t;
+                st = a.g_yb[gp];
+                len = a.g_yl[gp];
+                p = a.g_out[gp];
+              }
+              unsigned c = 0;
+              unsigned long long acc = 0;
+              uint32_t acch = 0;  // <= SHORT_MAX = 32 terms of W >> 32 < 2^27
+              for (int h = 0; h < len; h += SHORT_PART) {
+                int e[SHORT_PART];
+                row_part(a.cw, st, len, h, e);
+#pragma unroll
+                for (int k = 0; k < SHORT_PART; ++k) {
+                  if (h + k < len) {
+                    const uint32_t r = in_chunk(e[k], keep, c0u);
+                    const uint32_t word = bm[(r < wu ? r : 0u) >> 5];
+                    const bool hit = r < wu && ((word >> (r & 31)) & 1u);
+                    c += hit ? 1u : 0u;
+                    if (SAA && want_a && hit) {
+                      const uint32_t code = ((uint32_t)e[k] >> a.idbits) & 255u;
+                      const unsigned long long w = (unsigned long long)(code ? s_wtab[code] : a.aaw[e[k] & a.idmask]);
+                      acc += w;
+                      acch += (uint32_t)(w >> 32);
+                    }
+                  }
+                }
+              }
+              a.cn[p] = c;
+              if (SAA && want_a) a.aa[p] = blp::aa_value(acc, acch);
+              if (want_j) {
+                const long long uni = (long long)h2 + len - (long long)c;
+                if (uni <= 0) {
+                  a.jac[p] = __builtin_nan("");
+                  atomicOr(&a.misc->zero_div, 1);
+                } else {
+                  a.jac[p] = (double)c / (double)uni;  // correctly rounded, as Python's float division
+                }
+              }
+            }
+            __syncthreads();  // every row scanned before the next source rebuilds the bitmap
+            PROF(8)
+            continue;
+          }
+        }
+        if constexpr (!(SHORT && BLP_SHORT_FAST)) {
         // 3. exact distance 2: drop x (distance 0) and N(x) (distance 1)
         if (nx_hi >= c0 && nx_lo < c1) {
           for (int64_t k = xb + threadIdx.x; k < xe; k += BLOCK) {
@@ -1894,6 +1994,7 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
           __syncthreads();
           PROF(8)
         }
+        }  // !(SHORT && BLP_SHORT_FAST)
       }
     }
   }
@@ -2552,7 +2653,7 @@ using namespace blp;
 
 // the short-row scorer (k_score<..., SHORT = true>) takes the batch
 static bool short_kernel(const blp_batch* b) {
-  return b->variant == V_SMALL && b->short_rows == 3 && !b->wave && !b->global && !b->split &&
+  return b->variant == V_SMALL && b->short_rows == 3 && b->chunks == 1 && !b->wave && !b->global && !b->split &&
          !getenv("BLP_NO_SHORT_KERNEL");
 }
 
