@@ -865,8 +865,9 @@ def main():
     t0 = time.time()
     ex_x, ex_y, ex_l = synth.make_examples(G, U, B, D, n_users=args.users, rate=args.rate, seed=dist.rank)
     t_ex = time.time() - t0
-    log("examples: %d pairs for %d users (%d positives) in %.1fs" %
-        (len(ex_x), len(np.unique(ex_x)), int(ex_l.sum()), t_ex))
+    hop3_ms, hop3_n = G.stats(blp._lib.K_HOP3)  # the candidate kernel (k_hop3_wedge), HIP events
+    log("examples: %d pairs for %d users (%d positives) in %.1fs (hop-3 kernel %.2f ms)" %
+        (len(ex_x), len(np.unique(ex_x)), int(ex_l.sum()), t_ex, hop3_ms / max(hop3_n, 1)))
 
     passes = []
     t0 = time.time()
@@ -933,7 +934,7 @@ def main():
         "kernels_ms": ktimes,
         # outside the timed step (once per graph / per example set), reported for completeness
         "setup_s": {"edge_generation": round(t_gen, 3), "graph_build": round(t_graph, 3),
-                    "examples_hop3": round(t_ex, 3),
+                    "examples_hop3": round(t_ex, 3), "hop3_kernel_ms": round(hop3_ms / max(hop3_n, 1), 3),
                     "batch_create": round(t_batch, 3)},
         "work": {name: {"build_elems": _build_elems(G, xs_), "scan_elems": int(G.hop1_size[ys_].astype(np.int64).sum()),
                         "hits": int(res[name]["cn"].astype(np.int64).sum()), "sources": int(len(np.unique(xs_)))}

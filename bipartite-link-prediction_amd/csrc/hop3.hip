@@ -15,6 +15,10 @@
 
 #include "blp_internal.h"
 
+#ifndef BLP_HOP3_TEST
+#define BLP_HOP3_TEST 1  // k_hop3_wedge: read a word before OR-ing into it (0: OR every id)
+#endif
+
 namespace {
 
 constexpr int H_BLOCK = 1024;
@@ -305,6 +309,26 @@ __global__ __launch_bounds__(HW_BLOCK) void k_hop3_wedge(Hop3Args a, const int64
           uint4 v[4];
 #pragma unroll
           for (int u = 0; u < 4; ++u) v[u] = wedge[q + 64 * u < end ? q + 64 * u : q];  // a repeat ORs nothing new
+#if BLP_HOP3_TEST
+          // Read before OR: the wedge rows repeat the popular targets in nearly every row, so
+          // their words are set early and most ORs would be redundant -- and the 64 lanes of an
+          // OR to one hot word serialise on its bank. Reads of one address broadcast, so the
+          // words are read first (all 16 in one LDS round trip) and only lanes whose bit is
+          // still clear OR it in (a stale read only costs a redundant, harmless OR).
+          uint32_t rr[16], wd[16];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            rr[4 * u] = v[u].x - c0u;
+            rr[4 * u + 1] = v[u].y - c0u;
+            rr[4 * u + 2] = v[u].z - c0u;
+            rr[4 * u + 3] = v[u].w - c0u;
+          }
+#pragma unroll
+          for (int c = 0; c < 16; ++c) wd[c] = bm3[(rr[c] < wu ? rr[c] : 0u) >> 5];
+#pragma unroll
+          for (int c = 0; c < 16; ++c)
+            if (rr[c] < wu && !((wd[c] >> (rr[c] & 31)) & 1u)) atomicOr(&bm3[rr[c] >> 5], 1u << (rr[c] & 31));
+#else
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const uint32_t ids[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
@@ -314,6 +338,7 @@ __global__ __launch_bounds__(HW_BLOCK) void k_hop3_wedge(Hop3Args a, const int64
               if (r < wu) atomicOr(&bm3[r >> 5], 1u << (r & 31));
             }
           }
+#endif
         }
       }
       __syncthreads();
