@@ -44,8 +44,11 @@
 #ifndef BLP_PFN
 #define BLP_PFN 1  // ... and every later segment's metadata during the previous segment's scan
 #endif
-#ifndef BLP_SHORT_FAST
-#define BLP_SHORT_FAST 1  // short-row scorer: thread-owned pair rows, no per-batch offset scan (0: the batch loop)
+#ifndef BLP_SEGOFF
+#define BLP_SEGOFF 1  // large scorer: element and chunk offsets of a batch in one fused scan (0: two scans)
+#endif
+#ifndef BLP_AA64
+#define BLP_AA64 1  // rc_scan: a step's Adamic-Adar terms summed in one u64 (0: separate high-word sum)
 #endif
 #ifndef BLP_PP
 #define BLP_PP 1  // ping-pong merge-path loops in k_score (0: the single-buffer mp_build / mp_scan)
@@ -62,6 +65,7 @@ struct Misc {
   int queue;
   int zero_div;
   int pad;
+  int qh[8];  // k_score_split: one queue head per XCD group (sources s = g mod 8)
 };
 
 // ------------------------------------------------------------------ grouping kernels
@@ -1141,19 +1145,25 @@ __device__ __attribute__((always_inline)) inline void rc_scan(const int32_t* __r
         // (< 2^31) is the step's high-word contribution: hi * 2^32 <= S and S - hi * 2^32 <
         // (steps with a hit) * 2^32 <= cn * 2^32 (blp::aa_exact); packed, acc >> 40 in 2^40 units
         unsigned long long acc = 0;
-        uint32_t esc = 0;
+        uint32_t esc = 0, acch = 0;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
           const bool h = (hm >> k) & 1u;
-          acc += h ? (unsigned long long)wt[k] : 0ull;
+          const unsigned long long w = h ? (unsigned long long)wt[k] : 0ull;
+          acc += w;
+          if (!BLP_AA64) acch += (uint32_t)(w >> 32);
           esc |= (h & ((((uint32_t)st.v[k] >> idbits) & 255u) == 0u)) ? 1u << k : 0u;
         }
         if (esc) {  // code-0 ids: the per-node weight (rare on a coded id stream)
 #pragma unroll
           for (int k = 0; k < K; ++k)
-            if ((esc >> k) & 1u) acc += (unsigned long long)aaw[st.v[k] & idmask];
+            if ((esc >> k) & 1u) {
+              const unsigned long long w = (unsigned long long)aaw[st.v[k] & idmask];
+              acc += w;
+              if (!BLP_AA64) acch += (uint32_t)(w >> 32);
+            }
         }
-        const uint32_t acch = (uint32_t)(acc >> 32);
+        if (BLP_AA64) acch = (uint32_t)(acc >> 32);
         if (BLP_RCW) {
           if (st.s != acc_s) {
             flush();
@@ -1725,7 +1735,7 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
           } else
           for (int64_t k0 = xb; k0 < xe; k0 += SEG) {
             const int ns = (int)min<int64_t>(SEG, xe - k0);
-            if (RC && !(a.short_rows & 1)) {  // row-chunk build: element and chunk offsets in one scan
+            if (RC && BLP_SEGOFF && !(a.short_rows & 1)) {  // row-chunk build: element and chunk offsets in one scan
               int len = 0;
               if ((int)threadIdx.x < ns) {
                 const int z = a.ci[k0 + threadIdx.x];
@@ -1762,103 +1772,6 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
           }
         }
         PROF(3)
-        if constexpr (SHORT && BLP_SHORT_FAST) {
-          {  // (the host gives this kernel one-chunk universes only: short_kernel)
-            // Short-row scorer, one chunk: the pairs' rows are thread-owned (SEG == BLOCK), so
-            // after H2(x) is final each thread scans its pair's row and writes the scores itself
-            // -- no offset scan, no LDS accumulators, no barrier per pair batch. x's own bit is
-            // left out of the popcount and cleared between the reduction's two barriers.
-            static_assert(!SHORT || SEG == BLOCK, "one pair per thread");
-            if (nx_hi >= c0 && nx_lo < c1) {  // N(x) inside the universe (general graphs)
-              for (int64_t k = xb + threadIdx.x; k < xe; k += BLOCK) {
-                const int64_t r = (int64_t)a.ci[k] - c0;
-                if (r >= 0 && r < width) atomicAnd(&bm[r >> 5], ~(1u << (r & 31)));
-              }
-              __syncthreads();
-            }
-            const bool x_in = x >= c0 && x < c1;
-            const int64_t xr = x - c0;
-            {
-              unsigned long long pc = 0;
-              if (want_j)
-                for (int i = threadIdx.x; i < nw4; i += BLOCK) {
-                  uint4 q = bm4[i];
-                  if (x_in && i == (int)(xr >> 7)) {  // x is not in H2(x)
-                    const uint32_t m = ~(1u << (xr & 31));
-                    const int j = (int)((xr >> 5) & 3);
-                    q.x &= j == 0 ? m : ~0u;
-                    q.y &= j == 1 ? m : ~0u;
-                    q.z &= j == 2 ? m : ~0u;
-                    q.w &= j == 3 ? m : ~0u;
-                  }
-                  pc += __popc(q.x) + __popc(q.y) + __popc(q.z) + __popc(q.w);
-                }
-              for (int o = 32; o > 0; o >>= 1) pc += __shfl_xor(pc, o, 64);
-              if ((threadIdx.x & 63) == 0) red64[threadIdx.x >> 6] = pc;
-              __syncthreads();  // every popcount read is done
-              if (threadIdx.x == 0 && x_in) atomicAnd(&bm[xr >> 5], ~(1u << (xr & 31)));
-#pragma unroll
-              for (int w = 0; w < NW; ++w) h2 += red64[w];
-              __syncthreads();  // x's bit cleared before any scan; red64 free again
-            }
-            PROF(5)
-            const uint32_t keep = a.idmask | 0x80000000u, wu = (uint32_t)width;
-            const uint32_t c0u = (uint32_t)c0;
-            for (int sb = 0; sb < pcnt; sb += SEG) {
-              const int t = sb + (int)threadIdx.x;
-              if (t >= pcnt) break;
-              int64_t st;
-              int len, p;
-              if (PF && sb == 0) {
-                st = pf_start;
-                len = pf_len;
-                p = pf_out;
-              } else {
-                const int gp = pbeg + t;
-                st = a.g_yb[gp];
-                len = a.g_yl[gp];
-                p = a.g_out[gp];
-              }
-              unsigned c = 0;
-              unsigned long long acc = 0;
-              uint32_t acch = 0;  // <= SHORT_MAX = 32 terms of W >> 32 < 2^27
-              for (int h = 0; h < len; h += SHORT_PART) {
-                int e[SHORT_PART];
-                row_part(a.cw, st, len, h, e);
-#pragma unroll
-                for (int k = 0; k < SHORT_PART; ++k) {
-                  if (h + k < len) {
-                    const uint32_t r = in_chunk(e[k], keep, c0u);
-                    const uint32_t word = bm[(r < wu ? r : 0u) >> 5];
-                    const bool hit = r < wu && ((word >> (r & 31)) & 1u);
-                    c += hit ? 1u : 0u;
-                    if (SAA && want_a && hit) {
-                      const uint32_t code = ((uint32_t)e[k] >> a.idbits) & 255u;
-                      const unsigned long long w = (unsigned long long)(code ? s_wtab[code] : a.aaw[e[k] & a.idmask]);
-                      acc += w;
-                      acch += (uint32_t)(w >> 32);
-                    }
-                  }
-                }
-              }
-              a.cn[p] = c;
-              if (SAA && want_a) a.aa[p] = blp::aa_value(acc, acch);
-              if (want_j) {
-                const long long uni = (long long)h2 + len - (long long)c;
-                if (uni <= 0) {
-                  a.jac[p] = __builtin_nan("");
-                  atomicOr(&a.misc->zero_div, 1);
-                } else {
-                  a.jac[p] = (double)c / (double)uni;  // correctly rounded, as Python's float division
-                }
-              }
-            }
-            __syncthreads();  // every row scanned before the next source rebuilds the bitmap
-            PROF(8)
-            continue;
-          }
-        }
-        if constexpr (!(SHORT && BLP_SHORT_FAST)) {
         // 3. exact distance 2: drop x (distance 0) and N(x) (distance 1)
         if (nx_hi >= c0 && nx_lo < c1) {
           for (int64_t k = xb + threadIdx.x; k < xe; k += BLOCK) {
@@ -1906,7 +1819,7 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
               s_aa[2 * threadIdx.x + 1] = 0;
             }
           }
-          const bool rcs = RC && !(a.short_rows & 2);  // row-chunk scan: element and chunk offsets in one scan
+          const bool rcs = RC && BLP_SEGOFF && !(a.short_rows & 2);  // row-chunk scan: offsets in one scan
           if (rcs) {
             seg_offsets<BLOCK, K>(len, ns, s_off, s_coff, red64);
           } else {
@@ -1934,6 +1847,7 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
                                      s_aa, threadIdx.x);
           } else if constexpr (SHORT) {
           } else if (RC) {
+            if (!rcs) rc_chunk_offsets<BLOCK, K>(s_off, ns, s_coff, red);
             const int shift = build_hint<BLOCK, HC>(s_coff, ns, BLOCK, s_hint);  // s_coff: seg_offsets above
             if (want_a)
               rc_scan<BLOCK, K, true>(a.cw, a.idmask, a.idbits, a.aaw, s_wtab, s_start, s_off, s_coff, ns, c0, width,
@@ -1994,7 +1908,6 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
           __syncthreads();
           PROF(8)
         }
-        }  // !(SHORT && BLP_SHORT_FAST)
       }
     }
   }
@@ -2150,7 +2063,7 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
   __shared__ unsigned long long s_aa[2 * SEG];  // packed: [2t] Σ W, [2t + 1] high word << 21 | count
   __shared__ unsigned long long red64[NW];
   __shared__ int red[NW];
-  __shared__ int s_item;
+  __shared__ int64_t s_item;
   __shared__ int s_nhot;
   __shared__ blp::HotRow s_hot[HOT_LIST];
   __shared__ long long s_wtab[RCS ? 256 : 1];  // code weights in LDS (the 64 KiB variant has no room)
@@ -2163,13 +2076,34 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
   const long long* wtab = RCS ? s_wtab : a.wtab;
   if (RCS)  // the zero word and the build's dummy words past the bitmap
     for (int i = threadIdx.x; i < RC_EXTRA_WORDS; i += BLOCK) bm[CAP_WORDS + i] = 0;
-  const int64_t n_items = (int64_t)a.misc->n_active * C;
+  const int n_src = a.misc->n_active;
+  // Items (source, chunk) are claimed per XCD group: workgroups b and b + 8 share an XCD (and its
+  // L2; a placement observation, used for speed only), group g = b mod 8 takes the sources
+  // s = g (mod 8), all C chunks of a source in a row, so the C workgroups scanning one source's
+  // pair rows chunk by chunk do it on one XCD, close in time, and share those rows in its L2
+  // instead of fetching each 128-byte line into several L2s. A group whose sources are done
+  // takes items of the next group (queue heads misc->qh[g]). BLP_SPLIT_ONEQ: one global queue.
+  const int grp = a.sched ? 0 : (int)(blockIdx.x & 7);
+  const int ngrp = a.sched ? 1 : 8;
+  int gq = 0;  // thread 0: groups found empty so far
   for (;;) {
-    if (threadIdx.x == 0) s_item = atomicAdd(&a.misc->queue, 1);
+    if (threadIdx.x == 0) {
+      s_item = -1;
+      while (gq < ngrp) {
+        const int g = (grp + gq) % ngrp;
+        const int64_t n_g = n_src > g ? (n_src - g + ngrp - 1) / ngrp : 0;
+        const int k = atomicAdd(&a.misc->qh[g], 1);
+        if ((int64_t)k < n_g * C) {
+          s_item = (int64_t)(g + (int64_t)ngrp * (k / C)) * C + k % C;
+          break;
+        }
+        ++gq;
+      }
+    }
     __syncthreads();
     const int64_t item = s_item;
     __syncthreads();
-    if (item >= n_items) break;
+    if (item < 0) break;
     const int s = (int)(item / C), c = (int)(item % C);
     const int x = a.active[s];
     const int pbeg = a.off[x], pcnt = a.cnt[x];
@@ -2653,7 +2587,7 @@ using namespace blp;
 
 // the short-row scorer (k_score<..., SHORT = true>) takes the batch
 static bool short_kernel(const blp_batch* b) {
-  return b->variant == V_SMALL && b->short_rows == 3 && b->chunks == 1 && !b->wave && !b->global && !b->split &&
+  return b->variant == V_SMALL && b->short_rows == 3 && !b->wave && !b->global && !b->split &&
          !getenv("BLP_NO_SHORT_KERNEL");
 }
 
@@ -3190,6 +3124,7 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
     const int pk24 = (mask & BLP_ADAMIC) && g->max_row < (int64_t(1) << SPLIT_CN_BITS) && !getenv("BLP_SPLIT_NOPK");
     // slices of <= short_max ids scanned by their pair's thread (128 KiB chunks; BLP_SPLIT_SHORT=0: off)
     const int short_max = std::min(SHORT_PART, getenv("BLP_SPLIT_SHORT") ? atoi(getenv("BLP_SPLIT_SHORT")) : SHORT_PART);
+    a.sched = getenv("BLP_SPLIT_ONEQ") ? 1 : 0;  // k_score_split: 1 = one global item queue (no XCD groups)
     if (!pk24) BLP_HIP(hipMemsetAsync(b->d_pcn, 0, 4 * (size_t)np, b->stream));
     if (mask & BLP_ADAMIC) BLP_HIP(hipMemsetAsync(b->d_paa, 0, 16 * (size_t)np, b->stream));
     int per_cu = 1;

@@ -112,6 +112,7 @@ def test_general_graph_exact_distance(gpu):
     {"BLP_SPLIT": "3", "BLP_SPLIT_BIG": "1"},           # ... 128 KiB chunks, one workgroup per CU
     {"BLP_SPLIT": "3", "BLP_SPLIT_BIG": "1", "BLP_SPLIT_SHORT": "0"},  # ... no thread-per-slice short path
     {"BLP_SPLIT": "2", "BLP_SPLIT_BIG": "1", "BLP_SPLIT_SHORT": "4"},  # ... short path only below 5 ids
+    {"BLP_SPLIT": "3", "BLP_SPLIT_BIG": "1", "BLP_SPLIT_ONEQ": "1"},   # ... one item queue (no XCD groups)
     {"BLP_SPLIT": "24", "BLP_SPLIT_BIG": "1"},          # ... same, many chunks
     {"BLP_HEAVY_WORK": "50"},                           # heavy sources pre-built by k_heavy
     {"BLP_HEAVY_WORK": "1"},                            # one row per heavy item
