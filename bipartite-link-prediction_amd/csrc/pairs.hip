@@ -44,12 +44,6 @@
 #ifndef BLP_PFN
 #define BLP_PFN 1  // ... and every later segment's metadata during the previous segment's scan
 #endif
-#ifndef BLP_SEGOFF
-#define BLP_SEGOFF 0  // large scorer: 1 = element and chunk offsets in one fused scan (measured slower: 2.30 vs 2.20 ms)
-#endif
-#ifndef BLP_AA64
-#define BLP_AA64 0  // rc_scan: 1 = a step's Adamic-Adar terms summed in one u64 (measured: no gain)
-#endif
 #ifndef BLP_PP
 #define BLP_PP 1  // ping-pong merge-path loops in k_score (0: the single-buffer mp_build / mp_scan)
 #endif
@@ -938,84 +932,6 @@ __device__ __attribute__((always_inline)) inline void rc_fetch(const int32_t* __
   }
 }
 
-// Wave-contiguous row-chunk loops (BLP_RCW): each wave takes one contiguous run of the batch's
-// chunks, 64 per step (lane l: chunk cb + 64 i + l), instead of the block taking 1024 chunks per
-// step. A lane's chunks then stay in one row for |row| / 512 steps, so (1) its row is cached in
-// registers (RCSeg) and the LDS binary search runs only when the lane crosses into a new row, and
-// (2) rc_scan sums a lane's hits in registers across those steps and issues its LDS atomics once
-// per row instead of once per step (the 64 lanes of a wave on one long row hit ONE LDS address,
-// a 64-way conflict per atomic). Loads stay coalesced: the 64 lanes of a step read 64
-// consecutive chunks.
-#ifndef BLP_RCW
-#define BLP_RCW 0
-#endif
-struct RCSeg {
-  int s, c0, c1, len;  // cached row: chunks [c0, c1), len ids from start
-  int64_t start;
-};
-
-template <int K>
-__device__ __attribute__((always_inline)) inline void rcw_fetch(const int32_t* __restrict__ ci, const int64_t* s_start, const int32_t* s_off,
-                                 const int32_t* s_coff, int ns, int ce, int c, const int32_t* hint, int shift,
-                                 RCSeg& g, RCStep<K>& st) {
-  int64_t pos = 0;
-  st.s = 0;
-  st.cnt = 0;
-  if (c < ce) {
-    if (c >= g.c1) {  // a lane's chunks only increase: search past the cached row
-      int s;
-      if (shift >= 0) {
-        const int h = c >> shift;
-        s = seg_search(s_coff, ns, c, max(hint[h], g.s), hint[h + 1] + 1);
-      } else {
-        s = seg_search(s_coff, ns, c, g.s);
-      }
-      g.s = s;
-      g.c0 = s_coff[s];
-      g.c1 = s_coff[s + 1];
-      g.start = s_start[s];
-      g.len = s_off[s + 1] - s_off[s];
-    }
-    const int o = (c - g.c0) * K;
-    st.s = g.s;
-    st.cnt = min(K, g.len - o);
-    pos = g.start + o;
-  }
-  const blp::U4a* q = reinterpret_cast<const blp::U4a*>(ci + pos);
-#pragma unroll
-  for (int j = 0; j < K / 4; ++j) {
-    const blp::U4a x = q[j];
-    st.v[4 * j] = x.x;
-    st.v[4 * j + 1] = x.y;
-    st.v[4 * j + 2] = x.z;
-    st.v[4 * j + 3] = x.w;
-  }
-}
-
-template <int NT, int K, typename Proc>
-__device__ __attribute__((always_inline)) inline void rcw_loop(const int32_t* __restrict__ ci, const int64_t* s_start, const int32_t* s_off,
-                                const int32_t* s_coff, int ns, int tid, const int32_t* hint, int shift, Proc proc) {
-  constexpr int NWV = NT / 64;
-  const int TC = s_coff[ns];
-  const int lane = tid & 63, w = tid >> 6;
-  const int per_w = ((TC + 63) / 64 + NWV - 1) / NWV;  // steps per wave (= the block loop's step count)
-  const int cb = w * per_w * 64;
-  const int ce = min(TC, cb + per_w * 64);
-  const int nsteps = ce > cb ? (ce - cb + 63) / 64 : 0;  // wave-uniform; proc has no barrier
-  RCSeg g{0, 0, 0, 0, 0};
-  RCStep<K> A, B;
-  vm_drain();
-  rcw_fetch<K>(ci, s_start, s_off, s_coff, ns, ce, cb + lane, hint, shift, g, A);
-  for (int i = 0; i + 1 < nsteps; i += 2) {
-    rcw_fetch<K>(ci, s_start, s_off, s_coff, ns, ce, cb + (i + 1) * 64 + lane, hint, shift, g, B);
-    proc(A);
-    rcw_fetch<K>(ci, s_start, s_off, s_coff, ns, ce, cb + (i + 2) * 64 + lane, hint, shift, g, A);  // may be past ce
-    proc(B);
-  }
-  if (nsteps & 1) proc(A);
-  vm_drain();
-}
-
 // Two-buffer driver: steps of NT chunks; proc(step) after the next step's loads are issued.
 // BLP_RC3: three buffers, two steps of loads in flight while one is processed.
 #ifndef BLP_RC3
@@ -1078,10 +994,7 @@ __device__ __attribute__((always_inline)) inline void rc_build(const int32_t* __
       atomicOr(&bm[rr >> 5], 1u << (rr & 31));
     }
   };
-  if (BLP_RCW)
-    rcw_loop<NT, K>(ci, s_start, s_off, s_coff, ns, tid, hint, shift, proc);
-  else
-    rc_loop<NT, K>(ci, s_start, s_off, s_coff, ns, tid, hint, shift, proc);
+  rc_loop<NT, K>(ci, s_start, s_off, s_coff, ns, tid, hint, shift, proc);
 }
 
 // Packed exact-AA layout (packed = true, one LDS chunk): per segment t, s_aa[2 t] = Σ W (wrapping)
@@ -1090,7 +1003,7 @@ __device__ __attribute__((always_inline)) inline void rc_build(const int32_t* __
 // 64-bit sum. Valid while cn < 2^PK_CN_BITS (a chunk holds < 2^21 nodes) : each step's high part
 // undercounts S by < 2^40 + K * 2^32, so S - hi * 2^40 < cn * 2^41 < 2^64 (blp::aa_exact, hs = 40).
 
-template <int NT, int K, bool AA>
+template <int NT, int K, bool AA, bool CS = false>
 __device__ __attribute__((always_inline)) inline void rc_scan(const int32_t* __restrict__ ci, uint32_t idmask, int idbits,
                                const long long* __restrict__ aaw, const long long* wtab, const int64_t* s_start,
                                const int32_t* s_off, const int32_t* s_coff, int ns, int64_t c0, int64_t width,
@@ -1098,33 +1011,12 @@ __device__ __attribute__((always_inline)) inline void rc_scan(const int32_t* __r
                                const int32_t* hint, int shift, bool packed = false) {
   const uint32_t keep = idmask | 0x80000000u, c0u = (uint32_t)c0, wu = (uint32_t)width;
   const uint32_t safe = (uint32_t)cap_words << 5;
-  // BLP_RCW: the lane's sums for its current row, flushed to LDS when the row changes (and at
-  // the end); the same additions as the per-step atomics, so the LDS totals are identical.
-  // packed AA: lo = Σ W, hi = Σ_steps ((Σ_step W >> 32) >> 8) << PK_CN_BITS | cn; other AA:
-  // lo = Σ W, hi = Σ (W >> 32); counts in cn (or in hi's low bits when packed).
-  int acc_s = -1;
-  uint32_t acc_c = 0;
-  unsigned long long acc_lo = 0, acc_hi = 0;
-  auto flush = [&]() {
-    if (acc_c == 0) return;
-    if (AA && packed) {
-      atomicAdd(&s_aa[2 * acc_s], acc_lo);
-      atomicAdd(&s_aa[2 * acc_s + 1], acc_hi);
-    } else if (AA) {
-      aa_push(s_aa, acc_s, acc_lo, acc_hi);
-      atomicAdd(&s_cn[acc_s], acc_c);
-    } else if (packed) {
-      atomicAdd(&s_aa[2 * acc_s + 1], (unsigned long long)acc_c);
-    } else {
-      atomicAdd(&s_cn[acc_s], acc_c);
-    }
-  };
   // Branch-free phases, so the scheduler can issue all K bitmap reads (and weight reads)
   // before the first use: one LDS round trip per step instead of one per id.
   auto proc = [&](const RCStep<K>& st) {
     st.land();
     uint32_t rr[K], wd[K];
-    long long wt[K];
+    long long wt[CS ? 1 : K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       const uint32_t r = ((uint32_t)st.v[k] & keep) - c0u;
@@ -1132,18 +1024,46 @@ __device__ __attribute__((always_inline)) inline void rc_scan(const int32_t* __r
     }
 #pragma unroll
     for (int k = 0; k < K; ++k) wd[k] = bm[rr[k] >> 5];
+    // CS (rows ordered by weight code): the chunk's first code's weight only, read with the words
+    const uint32_t code0 = ((uint32_t)st.v[0] >> idbits) & 255u;
     if (AA) {
 #pragma unroll
-      for (int k = 0; k < K; ++k) wt[k] = wtab[((uint32_t)st.v[k] >> idbits) & 255u];
+      for (int k = 0; k < (CS ? 1 : K); ++k) wt[k] = wtab[CS ? code0 : ((uint32_t)st.v[k] >> idbits) & 255u];
     }
     uint32_t hm = 0;
 #pragma unroll
     for (int k = 0; k < K; ++k) hm |= ((wd[k] >> (rr[k] & 31)) & 1u) << k;
     if (hm) {
-      if (AA) {
-        // the step's sum is exact in one u64: K <= 16 terms W < 2^59. Its high part acc >> 32
-        // (< 2^31) is the step's high-word contribution: hi * 2^32 <= S and S - hi * 2^32 <
-        // (steps with a hit) * 2^32 <= cn * 2^32 (blp::aa_exact); packed, acc >> 40 in 2^40 units
+      if constexpr (AA && CS) {
+        // a full chunk of a code-ordered row whose first and last ids share a (nonzero) code is
+        // all of that code: its hits add count * W, exact (<= K * 2^59 < 2^63); otherwise (a code
+        // boundary, a row's last chunk, code-0 ids) each hit reads its own weight
+        const uint32_t codeL = ((uint32_t)st.v[K - 1] >> idbits) & 255u;
+        unsigned long long acc;
+        uint32_t acch;
+        if ((st.cnt == K) & (code0 == codeL) & (code0 != 0u)) {
+          acc = (unsigned long long)wt[0] * (unsigned)__popc(hm);
+          acch = (uint32_t)(acc >> 32);  // hi * 2^32 <= S_step < (hi + 1) * 2^32 (blp::aa_exact)
+        } else {
+          acc = 0;
+          acch = 0;
+#pragma unroll
+          for (int k = 0; k < K; ++k)
+            if ((hm >> k) & 1u) {
+              const uint32_t code = ((uint32_t)st.v[k] >> idbits) & 255u;
+              const unsigned long long w = (unsigned long long)(code ? wtab[code] : aaw[st.v[k] & idmask]);
+              acc += w;
+              acch += (uint32_t)(w >> 32);
+            }
+        }
+        if (packed) {
+          atomicAdd(&s_aa[2 * st.s], acc);
+          atomicAdd(&s_aa[2 * st.s + 1], ((unsigned long long)(acch >> (PK_HS - 32)) << PK_CN_BITS) | (unsigned)__popc(hm));
+          return;
+        }
+        aa_push(s_aa, st.s, acc, acch);
+      } else if constexpr (AA) {
+        // the step's high words fit 32 bits: K <= 16 terms of W >> 32 < 2^27 (W < 2^59)
         unsigned long long acc = 0;
         uint32_t esc = 0, acch = 0;
 #pragma unroll
@@ -1151,7 +1071,7 @@ __device__ __attribute__((always_inline)) inline void rc_scan(const int32_t* __r
           const bool h = (hm >> k) & 1u;
           const unsigned long long w = h ? (unsigned long long)wt[k] : 0ull;
           acc += w;
-          if (!BLP_AA64) acch += (uint32_t)(w >> 32);
+          acch += (uint32_t)(w >> 32);
           esc |= (h & ((((uint32_t)st.v[k] >> idbits) & 255u) == 0u)) ? 1u << k : 0u;
         }
         if (esc) {  // code-0 ids: the per-node weight (rare on a coded id stream)
@@ -1160,22 +1080,8 @@ __device__ __attribute__((always_inline)) inline void rc_scan(const int32_t* __r
             if ((esc >> k) & 1u) {
               const unsigned long long w = (unsigned long long)aaw[st.v[k] & idmask];
               acc += w;
-              if (!BLP_AA64) acch += (uint32_t)(w >> 32);
+              acch += (uint32_t)(w >> 32);
             }
-        }
-        if (BLP_AA64) acch = (uint32_t)(acc >> 32);
-        if (BLP_RCW) {
-          if (st.s != acc_s) {
-            flush();
-            acc_s = st.s;
-            acc_c = 0;
-            acc_lo = acc_hi = 0;
-          }
-          acc_c += (unsigned)__popc(hm);
-          acc_lo += acc;
-          acc_hi += packed ? ((unsigned long long)(acch >> (PK_HS - 32)) << PK_CN_BITS) | (unsigned)__popc(hm)
-                           : (unsigned long long)acch;
-          return;
         }
         if (packed) {
           atomicAdd(&s_aa[2 * st.s], acc);
@@ -1184,15 +1090,6 @@ __device__ __attribute__((always_inline)) inline void rc_scan(const int32_t* __r
         }
         aa_push(s_aa, st.s, acc, acch);
       }
-      if (BLP_RCW) {
-        if (st.s != acc_s) {
-          flush();
-          acc_s = st.s;
-          acc_c = 0;
-        }
-        acc_c += (unsigned)__popc(hm);
-        return;
-      }
       if (!AA && packed) {  // counts only, in the packed word (the chunk-parallel scorer)
         atomicAdd(&s_aa[2 * st.s + 1], (unsigned long long)__popc(hm));
         return;
@@ -1200,12 +1097,7 @@ __device__ __attribute__((always_inline)) inline void rc_scan(const int32_t* __r
       atomicAdd(&s_cn[st.s], (unsigned)__popc(hm));
     }
   };
-  if (BLP_RCW) {
-    rcw_loop<NT, K>(ci, s_start, s_off, s_coff, ns, tid, hint, shift, proc);
-    flush();
-  } else {
-    rc_loop<NT, K>(ci, s_start, s_off, s_coff, ns, tid, hint, shift, proc);
-  }
+  rc_loop<NT, K>(ci, s_start, s_off, s_coff, ns, tid, hint, shift, proc);
 }
 
 // Chunk prefix of a batch whose element offsets s_off[0..ns] are in LDS: s_coff[t] = sum of
@@ -1460,6 +1352,7 @@ struct ScoreArgs {
   const int32_t* ci;
   const long long* aaw;    // fixed-point Adamic-Adar weights
   const int32_t* cw;       // column ids streamed by build / scan: id | weight code << idbits
+  const int32_t* cws;      // the large scorer's scan stream: cw with rows ordered by code (or cw)
   uint32_t idmask;
   int idbits;
   const long long* wtab;   // [256] fixed-point weight per code (code 0: use aaw)
@@ -1735,21 +1628,6 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
           } else
           for (int64_t k0 = xb; k0 < xe; k0 += SEG) {
             const int ns = (int)min<int64_t>(SEG, xe - k0);
-            if (RC && BLP_SEGOFF && !(a.short_rows & 1)) {  // row-chunk build: element and chunk offsets in one scan
-              int len = 0;
-              if ((int)threadIdx.x < ns) {
-                const int z = a.ci[k0 + threadIdx.x];
-                const int64_t st = a.rp[z];
-                s_start[threadIdx.x] = st;
-                len = (nhot && a.hot_idx[z] >= 0) ? 0 : (int)(a.rp[z + 1] - st);  // dense rows were OR-ed in
-              }
-              seg_offsets<BLOCK, K>(len, ns, s_off, s_coff, red64);
-              const int shift = build_hint<BLOCK, HC>(s_coff, ns, BLOCK, s_hint);
-              rc_build<BLOCK, K>(a.cw, a.idmask, s_start, s_off, s_coff, ns, c0, width, bm, CAP_WORDS, threadIdx.x,
-                                 s_hint, shift);
-              __syncthreads();
-              continue;
-            }
             load_row_segments<BLOCK>(a.rp, a.ci, k0, ns, s_start, s_off, red, nhot ? a.hot_idx : nullptr);
             if (SHORT || (a.short_rows & 1)) {
               row_build<BLOCK>(a.cw, a.idmask, s_start, s_off, ns, c0, width, bm, threadIdx.x);
@@ -1819,16 +1697,11 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
               s_aa[2 * threadIdx.x + 1] = 0;
             }
           }
-          const bool rcs = RC && BLP_SEGOFF && !(a.short_rows & 2);  // row-chunk scan: offsets in one scan
-          if (rcs) {
-            seg_offsets<BLOCK, K>(len, ns, s_off, s_coff, red64);
-          } else {
-            int tot;
-            const int ex = block_exscan<BLOCK>(len, red, &tot);
-            if ((int)threadIdx.x < ns) s_off[threadIdx.x] = ex;
-            if (threadIdx.x == 0) s_off[ns] = tot;
-            __syncthreads();
-          }
+          int tot;
+          const int ex = block_exscan<BLOCK>(len, red, &tot);
+          if ((int)threadIdx.x < ns) s_off[threadIdx.x] = ex;
+          if (threadIdx.x == 0) s_off[ns] = tot;
+          __syncthreads();
           // the next segment's metadata, in flight during this segment's scan (BLP_PFN)
           have_pf = PF && !SHORT && BLP_PFN && nchunks == 1 && sb + SEG < pcnt;
           if (have_pf && (int)threadIdx.x < min(SEG, pcnt - sb - SEG)) {
@@ -1847,9 +1720,12 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
                                      s_aa, threadIdx.x);
           } else if constexpr (SHORT) {
           } else if (RC) {
-            if (!rcs) rc_chunk_offsets<BLOCK, K>(s_off, ns, s_coff, red);
-            const int shift = build_hint<BLOCK, HC>(s_coff, ns, BLOCK, s_hint);  // s_coff: seg_offsets above
-            if (want_a)
+            rc_chunk_offsets<BLOCK, K>(s_off, ns, s_coff, red);
+            const int shift = build_hint<BLOCK, HC>(s_coff, ns, BLOCK, s_hint);
+            if (want_a && a.cws != a.cw)  // code-ordered rows (sort_rows_by_code)
+              rc_scan<BLOCK, K, true, true>(a.cws, a.idmask, a.idbits, a.aaw, s_wtab, s_start, s_off, s_coff, ns, c0,
+                                            width, bm, CAP_WORDS, s_cn, s_aa, threadIdx.x, s_hint, shift, packed);
+            else if (want_a)
               rc_scan<BLOCK, K, true>(a.cw, a.idmask, a.idbits, a.aaw, s_wtab, s_start, s_off, s_coff, ns, c0, width,
                                       bm, CAP_WORDS, s_cn, s_aa, threadIdx.x, s_hint, shift, packed);
             else
@@ -3093,6 +2969,7 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   a.sched = getenv("BLP_STATIC") ? atoi(getenv("BLP_STATIC")) : 0;  // tuning knob
   const bool coded = g->d_ci_w && !getenv("BLP_NO_WCODES");  // tuning knob
   a.cw = coded ? g->d_ci_w : g->d_ci;
+  a.cws = coded && g->d_ci_ws ? g->d_ci_ws : a.cw;  // scan order is free outside the split scorer's slices
   a.idbits = coded ? g->id_bits : 31;
   a.idmask = (uint32_t)((1ull << a.idbits) - 1);
   a.wtab = g->d_wtab;
