@@ -111,7 +111,6 @@ struct blp_graph {
   // weight-coded copy of d_ci for the scorers: ci | code(ci) << id_bits, code 1..255 naming
   // one of the graph's most used weights (d_wtab[code]), 0 = look up d_aaw_fx (or null)
   int32_t* d_ci_w = nullptr;
-  int32_t* d_ci_ws = nullptr;  // d_ci_w with every row ordered by weight code (csr.hip sort_rows_by_code)
   int id_bits = 31;
   long long* d_wtab = nullptr;  // [256]; d_wtab[0] = 0
   // dense-row index: rows dense enough in their id range also stored as bitmaps (hot.hip)
@@ -152,7 +151,6 @@ struct __attribute__((aligned(4))) U4a {
 constexpr int SHORT_ROW_MAX = 32;  // the short-row scorer's row bound (pairs.hip SHORT_MAX)
 int build_hot_index(blp_graph* g);
 int graph_finish(blp_graph* g, const double* aaw);
-int sort_rows_by_code(blp_graph* g, int bits, int cbits);
 int build_wedge_index(blp_graph* g);
 void free_wedge_index(blp_graph* g);
 void free_hot_index(blp_graph* g);

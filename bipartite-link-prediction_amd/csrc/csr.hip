@@ -67,39 +67,6 @@ struct blp_csr {
   uint8_t* d_self = nullptr; // [max(n, 1)]
 };
 
-namespace blp {
-// The weight-coded id stream with every row ordered by weight code (stable: ids ascending within
-// a code) for the large scorer's scan (pairs.hip rc_scan, CS): a K-id chunk whose ids share one
-// code adds count * W with one weight read instead of K. Segmented radix sort of each row on the
-// code bits [bits, bits + cbits), on the graph's stream. Row lengths and offsets are unchanged.
-int sort_rows_by_code(blp_graph* g, int bits, int cbits) {
-  const int64_t n = g->n, nnz = g->nnz;
-  if (!g->d_ci_w || nnz == 0 || nnz >= (int64_t(1) << 30) || n >= (int64_t(1) << 30) || cbits <= 0) return BLP_OK;
-  int32_t* out = nullptr;
-  BLP_HIP(hipMalloc(&out, sizeof(int32_t) * (nnz + 2 * CI_PAD)));
-  BLP_HIP(hipMemsetAsync(out, 0, sizeof(int32_t) * (nnz + 2 * CI_PAD), g->stream));
-  out += CI_PAD;
-  DevBuf temp;
-  size_t tb = 0;
-  hipError_t e = hipcub::DeviceSegmentedRadixSort::SortKeys(nullptr, tb, g->d_ci_w, out, (int)nnz, (int)n, g->d_rp,
-                                                            g->d_rp + 1, bits, bits + cbits, g->stream);
-  int rc = e == hipSuccess ? temp.reserve(std::max<size_t>(tb, 1)) : hip_fail(e, "segmented sort", __FILE__, __LINE__);
-  if (!rc) {
-    e = hipcub::DeviceSegmentedRadixSort::SortKeys(temp.p, tb, g->d_ci_w, out, (int)nnz, (int)n, g->d_rp, g->d_rp + 1,
-                                                   bits, bits + cbits, g->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(g->stream);
-    if (e != hipSuccess) rc = hip_fail(e, "segmented sort", __FILE__, __LINE__);
-  }
-  temp.release();
-  if (rc) {
-    (void)hipFree(out - CI_PAD);
-    return rc;
-  }
-  g->d_ci_ws = out;
-  return BLP_OK;
-}
-}  // namespace blp
-
 extern "C" int blp_csr_destroy(blp_csr* c) {
   if (!c) return BLP_OK;
   (void)hipSetDevice(c->device);

@@ -177,8 +177,7 @@ int build_weight_codes(blp_graph* g, const int64_t* row_ptr, const std::vector<l
   BLP_HIP(hipStreamSynchronize(g->stream));
   BLP_HIP(hipFree(d_ncode));
   g->id_bits = bits;
-  if (getenv("BLP_NO_CSORT")) return BLP_OK;  // tuning knob: scan the id-ordered stream
-  return sort_rows_by_code(g, bits, cbits);
+  return BLP_OK;
 }
 
 // Adamic-Adar weights as integers W = w * 2^58 (blp_internal.h). Every weight the reference
@@ -338,7 +337,6 @@ int blp_graph_destroy(blp_graph* g) {
   if (g->d_ci) (void)hipFree(g->d_ci - CI_PAD);
   if (g->d_aaw_fx) (void)hipFree(g->d_aaw_fx);
   if (g->d_ci_w) (void)hipFree(g->d_ci_w - CI_PAD);
-  if (g->d_ci_ws) (void)hipFree(g->d_ci_ws - CI_PAD);
   if (g->d_wtab) (void)hipFree(g->d_wtab);
   if (g->stream) (void)hipStreamDestroy(g->stream);
   delete g;

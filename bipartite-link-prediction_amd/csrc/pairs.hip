@@ -1003,7 +1003,7 @@ __device__ __attribute__((always_inline)) inline void rc_build(const int32_t* __
 // 64-bit sum. Valid while cn < 2^PK_CN_BITS (a chunk holds < 2^21 nodes) : each step's high part
 // undercounts S by < 2^40 + K * 2^32, so S - hi * 2^40 < cn * 2^41 < 2^64 (blp::aa_exact, hs = 40).
 
-template <int NT, int K, bool AA, bool CS = false>
+template <int NT, int K, bool AA>
 __device__ __attribute__((always_inline)) inline void rc_scan(const int32_t* __restrict__ ci, uint32_t idmask, int idbits,
                                const long long* __restrict__ aaw, const long long* wtab, const int64_t* s_start,
                                const int32_t* s_off, const int32_t* s_coff, int ns, int64_t c0, int64_t width,
@@ -1016,7 +1016,7 @@ __device__ __attribute__((always_inline)) inline void rc_scan(const int32_t* __r
   auto proc = [&](const RCStep<K>& st) {
     st.land();
     uint32_t rr[K], wd[K];
-    long long wt[CS ? 1 : K];
+    long long wt[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       const uint32_t r = ((uint32_t)st.v[k] & keep) - c0u;
@@ -1024,45 +1024,15 @@ __device__ __attribute__((always_inline)) inline void rc_scan(const int32_t* __r
     }
 #pragma unroll
     for (int k = 0; k < K; ++k) wd[k] = bm[rr[k] >> 5];
-    // CS (rows ordered by weight code): the chunk's first code's weight only, read with the words
-    const uint32_t code0 = ((uint32_t)st.v[0] >> idbits) & 255u;
     if (AA) {
 #pragma unroll
-      for (int k = 0; k < (CS ? 1 : K); ++k) wt[k] = wtab[CS ? code0 : ((uint32_t)st.v[k] >> idbits) & 255u];
+      for (int k = 0; k < K; ++k) wt[k] = wtab[((uint32_t)st.v[k] >> idbits) & 255u];
     }
     uint32_t hm = 0;
 #pragma unroll
     for (int k = 0; k < K; ++k) hm |= ((wd[k] >> (rr[k] & 31)) & 1u) << k;
     if (hm) {
-      if constexpr (AA && CS) {
-        // a full chunk of a code-ordered row whose first and last ids share a (nonzero) code is
-        // all of that code: its hits add count * W, exact (<= K * 2^59 < 2^63); otherwise (a code
-        // boundary, a row's last chunk, code-0 ids) each hit reads its own weight
-        const uint32_t codeL = ((uint32_t)st.v[K - 1] >> idbits) & 255u;
-        unsigned long long acc;
-        uint32_t acch;
-        if ((st.cnt == K) & (code0 == codeL) & (code0 != 0u)) {
-          acc = (unsigned long long)wt[0] * (unsigned)__popc(hm);
-          acch = (uint32_t)(acc >> 32);  // hi * 2^32 <= S_step < (hi + 1) * 2^32 (blp::aa_exact)
-        } else {
-          acc = 0;
-          acch = 0;
-#pragma unroll
-          for (int k = 0; k < K; ++k)
-            if ((hm >> k) & 1u) {
-              const uint32_t code = ((uint32_t)st.v[k] >> idbits) & 255u;
-              const unsigned long long w = (unsigned long long)(code ? wtab[code] : aaw[st.v[k] & idmask]);
-              acc += w;
-              acch += (uint32_t)(w >> 32);
-            }
-        }
-        if (packed) {
-          atomicAdd(&s_aa[2 * st.s], acc);
-          atomicAdd(&s_aa[2 * st.s + 1], ((unsigned long long)(acch >> (PK_HS - 32)) << PK_CN_BITS) | (unsigned)__popc(hm));
-          return;
-        }
-        aa_push(s_aa, st.s, acc, acch);
-      } else if constexpr (AA) {
+      if (AA) {
         // the step's high words fit 32 bits: K <= 16 terms of W >> 32 < 2^27 (W < 2^59)
         unsigned long long acc = 0;
         uint32_t esc = 0, acch = 0;
@@ -1352,7 +1322,6 @@ struct ScoreArgs {
   const int32_t* ci;
   const long long* aaw;    // fixed-point Adamic-Adar weights
   const int32_t* cw;       // column ids streamed by build / scan: id | weight code << idbits
-  const int32_t* cws;      // the large scorer's scan stream: cw with rows ordered by code (or cw)
   uint32_t idmask;
   int idbits;
   const long long* wtab;   // [256] fixed-point weight per code (code 0: use aaw)
@@ -1722,10 +1691,7 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
           } else if (RC) {
             rc_chunk_offsets<BLOCK, K>(s_off, ns, s_coff, red);
             const int shift = build_hint<BLOCK, HC>(s_coff, ns, BLOCK, s_hint);
-            if (want_a && a.cws != a.cw)  // code-ordered rows (sort_rows_by_code)
-              rc_scan<BLOCK, K, true, true>(a.cws, a.idmask, a.idbits, a.aaw, s_wtab, s_start, s_off, s_coff, ns, c0,
-                                            width, bm, CAP_WORDS, s_cn, s_aa, threadIdx.x, s_hint, shift, packed);
-            else if (want_a)
+            if (want_a)
               rc_scan<BLOCK, K, true>(a.cw, a.idmask, a.idbits, a.aaw, s_wtab, s_start, s_off, s_coff, ns, c0, width,
                                       bm, CAP_WORDS, s_cn, s_aa, threadIdx.x, s_hint, shift, packed);
             else
@@ -2969,7 +2935,6 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   a.sched = getenv("BLP_STATIC") ? atoi(getenv("BLP_STATIC")) : 0;  // tuning knob
   const bool coded = g->d_ci_w && !getenv("BLP_NO_WCODES");  // tuning knob
   a.cw = coded ? g->d_ci_w : g->d_ci;
-  a.cws = coded && g->d_ci_ws ? g->d_ci_ws : a.cw;  // scan order is free outside the split scorer's slices
   a.idbits = coded ? g->id_bits : 31;
   a.idmask = (uint32_t)((1ull << a.idbits) - 1);
   a.wtab = g->d_wtab;

@@ -118,9 +118,8 @@ def test_general_graph_exact_distance(gpu):
     {"BLP_HEAVY_WORK": "1"},                            # one row per heavy item
     {"BLP_CHUNK_BITS": "2048", "BLP_HEAVY_WORK": "50", "BLP_NO_GLOBAL": "1"},  # multi-chunk: no heavy path
     {"BLP_HOT_MIN": "8"},                               # dense-row index OR-ed into H2
-    {"BLP_NO_CSORT": "1"},                              # scan the id-ordered coded stream (no code-ordered rows)
-    {"BLP_VARIANT": "2"},                               # LARGE variant on the small graph: code-ordered AA scan
-    {"BLP_VARIANT": "2", "BLP_WCODES": "3"},            # ... few codes: code-0 ids inside code-ordered rows
+    {"BLP_VARIANT": "2"},                               # LARGE variant (row-chunk loops) on the small graph
+    {"BLP_VARIANT": "2", "BLP_WCODES": "3"},            # ... few weight codes: code-0 ids gather aaw
     {"BLP_HOT_MIN": "8", "BLP_CHUNK_BITS": "1024", "BLP_NO_GLOBAL": "1"},  # dense rows across chunks
     {"BLP_HOT_MIN": "8", "BLP_HEAVY_WORK": "50"},
     {"BLP_HOT_MIN": "1", "BLP_HOT_DENSITY": "100000000"},  # > HOT_LIST dense rows: sparse fallback
