@@ -46,6 +46,9 @@ constexpr int TK_KMAX = 256;
 #ifndef BLP_TK_RB
 #define BLP_TK_RB 8
 #endif
+#ifndef BLP_TK_FLAT
+#define BLP_TK_FLAT 1  // count passes: the wave's owned rows pushed as one flat run (0: a row per lane)
+#endif
 #ifndef BLP_TK_TAIL16
 #define BLP_TK_TAIL16 1  // row entries past the first TK_RB read as 16-byte vectors (4 per load); 0: one by one
 #endif
@@ -284,6 +287,125 @@ __device__ __attribute__((always_inline)) long long push_pass(const TkArgs& a, T
     int32_t ppn = 0;
     bool skipn = true;
     if (idx < E) skipn = fetch(idx, r0n, r1n, ppn);
+    if constexpr ((MODE == 0 || MODE == 3) && BLP_TK_FLAT) {
+      // Wave-flattened push. A lane still owns one element (b', w) per round and decides its
+      // ownership, but the owned rows of the wave's 64 lanes are then pushed as ONE run: lane l
+      // takes entries [l q, (l + 1) q) of their concatenation (q = ceil(total / 64)). Rows hold
+      // 1..28 ids (~11), so a row per lane left most lanes idle beside the wave's longest row,
+      // and the 64 lanes all pushed their rows' FIRST entries -- the most popular targets, whose
+      // counters share a few LDS words -- in the same instruction. Every count is the same sum.
+      // The wave's row table (start, exclusive prefix, weight) lives in s.key / s.col, which the
+      // count pass does not otherwise use (the selection reloads them afterwards).
+      const int lane = tid & 63, wv = tid >> 6;
+      int64_t* rt_base = reinterpret_cast<int64_t*>(s.key) + wv * 64;
+      unsigned long long* rt_w = s.key + TK_SEL / 2 + wv * 64;
+      int32_t* rt_excl = s.col + wv * 65;
+      unsigned long long* aah = acc64 + (a.h_word >> 1);
+      for (int64_t wb = tid - lane; wb < E; wb += TK_NT) {  // wave-uniform rounds
+        const bool skip = idx >= E || skipn;
+        const int64_t r0 = r0n;
+        const int len_w = skip ? 0 : (int)(r1n - r0n);
+        const int32_t pp = ppn;
+        const int32_t* roww = base + r0;
+        int32_t e[TK_RB];
+        const blp::U4a* rv = reinterpret_cast<const blp::U4a*>(roww);
+#pragma unroll
+        for (int q = 0; q < TK_RB / 4; ++q) {
+          blp::U4a v = {0x7FFFFFFF, 0x7FFFFFFF, 0x7FFFFFFF, 0x7FFFFFFF};
+          if (4 * q < len_w && TK_OK(r0 >= 0 && r0 + 4 * q + 4 <= base_len, 8, r0 + 4 * q + 4, base_len)) v = rv[q];
+          e[4 * q] = 4 * q < len_w ? v.x : 0x7FFFFFFF;
+          e[4 * q + 1] = 4 * q + 1 < len_w ? v.y : 0x7FFFFFFF;
+          e[4 * q + 2] = 4 * q + 2 < len_w ? v.z : 0x7FFFFFFF;
+          e[4 * q + 3] = 4 * q + 3 < len_w ? v.w : 0x7FFFFFFF;
+        }
+        idx += TK_NT;
+        if (idx < E) skipn = fetch(idx, r0n, r1n, ppn);
+        // ownership: no entry of N'(w) below b' is in N'(x)
+        bool owned = !skip;
+#pragma unroll
+        for (int j = 0; j < TK_RB; ++j)
+          if (owned && e[j] < pp && in_row_x(s, rowx, du, e[j])) owned = false;
+        for (int j = TK_RB; j < len_w && owned; j += 4) {
+          blp::U4a v = {0x7FFFFFFF, 0x7FFFFFFF, 0x7FFFFFFF, 0x7FFFFFFF};
+          if (TK_OK(r0 + j + 4 <= base_len, 8, r0 + j + 4, base_len)) v = *reinterpret_cast<const blp::U4a*>(roww + j);
+          const int32_t t[4] = {v.x, j + 1 < len_w ? v.y : 0x7FFFFFFF, j + 2 < len_w ? v.z : 0x7FFFFFFF,
+                                j + 3 < len_w ? v.w : 0x7FFFFFFF};
+          if (t[0] >= pp) break;
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (t[q] < pp && in_row_x(s, rowx, du, t[q])) owned = false;
+          if (t[3] >= pp) break;
+        }
+        const int mylen = owned ? len_w : 0;
+        if (count_h2 && owned) {
+          ++h2;
+          npush += len_w;
+        }
+        int incl = mylen;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+          const int t = __shfl_up(incl, d, 64);
+          if (lane >= d) incl += t;
+        }
+        const int T = __shfl(incl, 63, 64);
+        if (T == 0) continue;  // uniform
+        rt_base[lane] = r0;
+        rt_excl[lane] = incl - mylen;
+        if (lane == 63) rt_excl[64] = T;
+        if (MODE == 3) rt_w[lane] = (unsigned long long)a.wtab[len_w];
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        const int qn = (T + 63) >> 6;
+        const int f0 = lane * qn, f1 = min(T, f0 + qn);
+        if (f0 < f1) {
+          int r = 0, hi = 64;  // the row holding entry f0: last r with excl[r] <= f0
+          while (hi - r > 1) {
+            const int mid = (r + hi) >> 1;
+            if (rt_excl[mid] <= f0) r = mid; else hi = mid;
+          }
+          int rs = rt_excl[r], re = rt_excl[r + 1];
+          int64_t rb = rt_base[r];
+          unsigned long long wr = MODE == 3 ? rt_w[r] : 0ull;
+          for (int f = f0; f < f1; f += 4) {  // four entries' loads in flight per group
+            int64_t ad[4];
+            unsigned long long wu[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const int fu = min(f + u, f1 - 1);  // past the end: a repeat of the last, not pushed
+              while (fu >= re) {
+                ++r;
+                rs = re;
+                re = rt_excl[r + 1];
+                rb = rt_base[r];
+                if (MODE == 3) wr = rt_w[r];
+              }
+              ad[u] = rb + (fu - rs);
+              wu[u] = wr;
+            }
+            int32_t ev[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+              ev[u] = TK_OK(ad[u] >= 0 && ad[u] < base_len, 9, ad[u], base_len) ? base[ad[u]] : 0x7FFFFFFF;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              if (f + u >= f1) break;
+              const int32_t ej = ev[u];
+              if (ej >= c.a0 && ej < c.a1) acc_add(a, s.acc, c, ej);
+              if (MODE == 3 && ej < a.AH) {
+                const int64_t t = p_of(a, ej);
+                if (TK_OK(t >= 0 && (a.h_word >> 1) + 2 * t + 1 < a.acc_words / 2, 4, t, a.acc_words))
+                  aa_push2(aah, t, wu[u]);
+              }
+            }
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();  // the table is rewritten next round
+      }
+      __syncthreads();
+      if (pushed) *pushed = npush;
+      return h2;
+    }
     while (idx < E) {
       const bool skip = skipn;
       const int64_t r0 = r0n;
