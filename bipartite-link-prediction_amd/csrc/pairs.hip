@@ -58,7 +58,7 @@ struct Misc {
   int n_active;
   int queue;
   int zero_div;
-  int pad;
+  int hq;     // k_score_hash's queue head
   int qh[8];  // k_score_split: one queue head per XCD group (sources s = g mod 8)
 };
 
@@ -1892,7 +1892,8 @@ template <int BLOCK, int CAP_WORDS, int SEG, int K>
 __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_split(ScoreArgs a, const int32_t* __restrict__ g_y,
                                                        const int32_t* __restrict__ rsplit, int64_t rs_lo, int C,
                                                        uint32_t* __restrict__ pcn, unsigned long long* __restrict__ paa,
-                                                       uint32_t* __restrict__ ph2, int64_t np, int pk24, int short_max) {
+                                                       uint32_t* __restrict__ ph2, int64_t np, int pk24, int short_max,
+                                                       const uint8_t* __restrict__ hflag, int32_t hxlo) {
   constexpr int NW = BLOCK / 64;
   // 128 KiB chunks (one workgroup per CU) use the row-chunk loops of the large scorer
   constexpr bool RCS = BLP_RC && CAP_WORDS > 16384;
@@ -1948,6 +1949,7 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
     if (item < 0) break;
     const int s = (int)(item / C), c = (int)(item % C);
     const int x = a.active[s];
+    if (hflag && hflag[x - hxlo]) continue;  // uniform: scored by k_score_hash
     const int pbeg = a.off[x], pcnt = a.cnt[x];
     const int64_t xb = a.rp[x], xe = a.rp[x + 1];
     const int hslot = a.heavy_slot ? a.heavy_slot[x] : -1;
@@ -2161,13 +2163,15 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
 // one wave per active source: sum the chunk partials of each of its pairs, then Jaccard
 __global__ __launch_bounds__(256) void k_split_combine(ScoreArgs a, int C, const uint32_t* __restrict__ pcn,
                                                       const unsigned long long* __restrict__ paa,
-                                                      const uint32_t* __restrict__ ph2, int64_t np, int pk24) {
+                                                      const uint32_t* __restrict__ ph2, int64_t np, int pk24,
+                                                      const uint8_t* __restrict__ hflag, int32_t hxlo) {
   const int lane = threadIdx.x & 63;
   const int n_active = a.misc->n_active;
   const bool want_j = (a.mask & BLP_JACCARD) != 0;
   const bool want_a = (a.mask & BLP_ADAMIC) != 0;
   for (int s = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; s < n_active; s += (gridDim.x * blockDim.x) >> 6) {
     const int x = a.active[s];
+    if (hflag && hflag[x - hxlo]) continue;  // scored by k_score_hash
     long long h2 = 0;
     if (want_j)
       for (int c = 0; c < C; ++c) h2 += ph2[(int64_t)s * C + c];
@@ -2189,6 +2193,143 @@ __global__ __launch_bounds__(256) void k_split_combine(ScoreArgs a, int C, const
         }
       }
     }
+  }
+}
+
+// ------------------------------------------------------------------ hash-set scorer
+// Universes wider than LDS (the chunk-parallel scorer's batches) whose source has a SMALL H2: the
+// business side of config 5 (H2(b) = the businesses co-reviewed with b, ~20 |N(b)| ids among 2M)
+// pays the chunk-parallel scorer's per-item costs -- a 128 KiB bitmap zeroed and popcounted,
+// offsets, barriers -- C times for a few thousand ids. Here H2(x) is an open-addressing hash set
+// in LDS (HT slots, linear probing, load <= 1/2: the host routes only sources whose build work,
+// the total length of the rows N(z), z in N(x), is at most HT / 2), built with one CAS per new id;
+// x and N(x) are then tombstoned (exact distance 2) and every pair's N(y) probes the set. One
+// pair per thread, results written directly (cn, Jaccard, exact Adamic-Adar words).
+constexpr uint32_t HS_EMPTY = 0xFFFFFFFFu;
+template <int HT>
+__device__ inline uint32_t hs_slot(uint32_t v) {
+  return (v * 2654435761u) >> (32 - __builtin_ctz(HT));
+}
+
+template <int BLOCK, int HT>
+__global__ __launch_bounds__(BLOCK) void k_score_hash(ScoreArgs a, const uint8_t* __restrict__ hflag, int32_t xlo) {
+  constexpr int NW = BLOCK / 64;
+  static_assert((HT & (HT - 1)) == 0, "HT: a power of two");
+  __shared__ uint32_t tab[HT];
+  __shared__ unsigned long long red64[NW];
+  __shared__ int s_src;
+  const int n_active = a.misc->n_active;
+  const bool want_j = (a.mask & BLP_JACCARD) != 0;
+  const bool want_a = (a.mask & BLP_ADAMIC) != 0;
+  const uint32_t c0u = (uint32_t)a.lo, wu = (uint32_t)(a.hi - a.lo);
+  const uint32_t keep = a.idmask | 0x80000000u;
+  auto find = [&](uint32_t v) -> int {  // slot of v (id - lo) or -1
+    uint32_t h = hs_slot<HT>(v);
+    for (int i = 0; i < HT; ++i) {
+      const uint32_t t = tab[h];
+      if (t == v) return (int)h;
+      if (t == HS_EMPTY) return -1;
+      h = (h + 1) & (HT - 1);
+    }
+    return -1;
+  };
+  for (;;) {
+    if (threadIdx.x == 0) s_src = atomicAdd(&a.misc->hq, 1);
+    __syncthreads();
+    const int si = s_src;
+    __syncthreads();
+    if (si >= n_active) break;
+    const int x = a.active[si];
+    if (!hflag[x - xlo]) continue;  // uniform: the chunk-parallel scorer takes it
+    for (int i = threadIdx.x; i < HT / 4; i += BLOCK) reinterpret_cast<uint4*>(tab)[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
+    __syncthreads();
+    // build: one row N(z) per thread, 16 ids at a time (rows padded past nnz)
+    const int64_t xb = a.rp[x], xe = a.rp[x + 1];
+    unsigned long long added = 0;
+    for (int64_t k = xb + threadIdx.x; k < xe; k += BLOCK) {
+      const int z = a.ci[k];
+      const int64_t st = a.rp[z];
+      const int len = (int)(a.rp[z + 1] - st);
+      for (int h0 = 0; h0 < len; h0 += SHORT_PART) {
+        int e[SHORT_PART];
+        row_part(a.cw, st, len, h0, e);
+#pragma unroll
+        for (int j = 0; j < SHORT_PART; ++j) {
+          const uint32_t v = in_chunk(e[j], keep, c0u);
+          if (h0 + j < len && v < wu) {
+            uint32_t h = hs_slot<HT>(v);
+            for (;;) {
+              const uint32_t t = tab[h];
+              if (t == v) break;
+              if (t == HS_EMPTY) {
+                const uint32_t old = atomicCAS(&tab[h], HS_EMPTY, v);
+                if (old == HS_EMPTY) {
+                  ++added;
+                  break;
+                }
+                if (old == v) break;
+              }
+              h = (h + 1) & (HT - 1);
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+    // exact distance 2: x and N(x) out (tombstones keep the probe chains intact)
+    unsigned long long removed = 0;
+    for (int64_t k = xb - 1 + threadIdx.x; k < xe; k += BLOCK) {
+      const int w = k < xb ? x : a.ci[k];
+      const uint32_t v = (uint32_t)w - c0u;
+      if (v < wu) {
+        const int h = find(v);
+        if (h >= 0) {
+          tab[h] = v | 0x80000000u;
+          ++removed;
+        }
+      }
+    }
+    const unsigned long long h2 = want_j ? block_sum_u64<BLOCK>(added - removed, red64) : 0ull;
+    if (!want_j) __syncthreads();  // tombstones written before any probe
+    // scan: one pair per thread
+    const int pbeg = a.off[x], pcnt = a.cnt[x];
+    for (int t = threadIdx.x; t < pcnt; t += BLOCK) {
+      const int gp = pbeg + t;
+      const int64_t st = a.g_yb[gp];
+      const int len = a.g_yl[gp];
+      const int p = a.g_out[gp];
+      unsigned c = 0;
+      unsigned long long acc = 0, acch = 0;
+      for (int h0 = 0; h0 < len; h0 += SHORT_PART) {
+        int e[SHORT_PART];
+        row_part(a.cw, st, len, h0, e);
+#pragma unroll
+        for (int j = 0; j < SHORT_PART; ++j) {
+          const uint32_t v = in_chunk(e[j], keep, c0u);
+          if (h0 + j < len && v < wu && find(v) >= 0) {
+            ++c;
+            if (want_a) {
+              const uint32_t code = ((uint32_t)e[j] >> a.idbits) & 255u;
+              const unsigned long long w = (unsigned long long)(code ? a.wtab[code] : a.aaw[e[j] & a.idmask]);
+              acc += w;
+              acch += w >> 32;
+            }
+          }
+        }
+      }
+      a.cn[p] = c;
+      if (want_a) a.aa[p] = blp::aa_value(acc, acch);
+      if (want_j) {
+        const long long uni = (long long)h2 + len - (long long)c;
+        if (uni <= 0) {
+          a.jac[p] = __builtin_nan("");
+          atomicOr(&a.misc->zero_div, 1);
+        } else {
+          a.jac[p] = (double)c / (double)uni;  // correctly rounded, as Python's float division
+        }
+      }
+    }
+    __syncthreads();  // every probe done before the next source clears the table
   }
 }
 
@@ -2359,6 +2500,7 @@ enum Variant { V_SMALL = 0, V_MED = 1, V_LARGE = 2 };
 // LDS bitmap words (16 / 64 / 136 KiB), threads per block, pair/row segments per chunk
 constexpr int CAP_SMALL = 4096, CAP_MED = 16384, CAP_LARGE = 33792;  // 1.08M bits: fits 160 KiB with the exact AA words
 constexpr int BLOCK_SMALL = 256, BLOCK_MED = 512, BLOCK_LARGE = 1024;
+constexpr int HS_BLOCK = 512, HS_HT = 16384;  // hash-set scorer: 64 KiB table, two workgroups per CU
 constexpr int SEG_SMALL = 256, SEG_MED = 384, SEG_LARGE = 512;  // MED: two 512-thread workgroups per CU (<= 80 KiB LDS)
 constexpr int SEG_MED_NOAA = 512;  // MED without Adamic-Adar (no AA words, no weight table in LDS)
 constexpr int G_BLOCK = 1024, G_SEG = 512;  // HBM-bitmap scorer
@@ -2421,6 +2563,8 @@ struct blp_batch {
   blp::DevBuf cnt, off, active, scratch;
   int cus = 0;  // CUs the persistent block scorer may occupy (0: all; set by blp_batches_score)
   SrcRec* d_rec = nullptr;  // [n_sources] source records of the short-row scorer (or null)
+  uint8_t* d_hflag = nullptr;  // [xspan] 1: source scored by k_score_hash (split batches; or null)
+  int64_t n_hash = 0;          // such sources
   bool use_short = false;   // the short-row scorer takes this batch (decided once, at create)
   int64_t work_elems = 0;  // planned build + scan elements (co-scheduling estimate)
 };
@@ -2741,6 +2885,24 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
     BLP_HIP_OR(hipGetLastError(), bail);
     BLP_HIP_OR(hipStreamSynchronize(g->stream), bail);
   }
+  // ---- hash-set scorer (split batches): sources whose build work fits half the hash table
+  if (b->split && n_pairs && !getenv("BLP_NO_HASH")) {
+    // work bounds the distinct ids inserted; at most HT - 1 keeps an empty slot, so every insert
+    // and probe chain ends (the knob is clamped: a fuller table is slower, never unbounded)
+    const int64_t want = getenv("BLP_HASH_WORK") ? atoll(getenv("BLP_HASH_WORK")) : HS_HT / 2;
+    const int64_t cap = std::min<int64_t>(std::max<int64_t>(1, want), HS_HT - 1);
+    std::vector<uint8_t> hf((size_t)std::max<int64_t>(b->xspan, 1), 0);
+    for (size_t i = 0; i < srcs.size(); ++i)
+      if (work[i] <= cap) {
+        hf[srcs[i] - b->xlo] = 1;
+        ++b->n_hash;
+      }
+    if (b->n_hash) {
+      if (hipMalloc(&b->d_hflag, hf.size()) != hipSuccess)
+        return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: hash flags"));
+      BLP_HIP_OR(hipMemcpy(b->d_hflag, hf.data(), hf.size(), hipMemcpyHostToDevice), bail);
+    }
+  }
   // ---- HBM bitmap slots: one per resident workgroup of k_score_global
   if (b->global && n_pairs) {
     int per_cu_g = 1;
@@ -2797,7 +2959,7 @@ int blp_batch_destroy(blp_batch* b) {
   b->scratch.release();
   if (b->stream) (void)hipStreamDestroy(b->stream);
   void* ps[] = {b->d_x,    b->d_y,    b->d_cn,   b->d_jac,  b->d_aa,          b->d_gout,        b->d_gyb,
-                b->d_gyl,  b->d_misc, b->d_heavy_slot, b->d_heavy_bm, b->d_heavy_items, b->d_gbm, b->d_gy, b->d_rsplit, b->d_pcn, b->d_paa, b->d_ph2, b->d_aa_part, b->d_rec};
+                b->d_gyl,  b->d_misc, b->d_heavy_slot, b->d_heavy_bm, b->d_heavy_items, b->d_gbm, b->d_gy, b->d_rsplit, b->d_pcn, b->d_paa, b->d_ph2, b->d_aa_part, b->d_rec, b->d_hflag};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   delete b;
@@ -2967,6 +3129,13 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
     // slices of <= short_max ids scanned by their pair's thread (128 KiB chunks; BLP_SPLIT_SHORT=0: off)
     const int short_max = std::min(SHORT_PART, getenv("BLP_SPLIT_SHORT") ? atoi(getenv("BLP_SPLIT_SHORT")) : SHORT_PART);
     a.sched = getenv("BLP_SPLIT_ONEQ") ? 1 : 0;  // k_score_split: 1 = one global item queue (no XCD groups)
+    if (b->d_hflag) {  // small-H2 sources first, on their own hash-set kernel
+      int hcu = 1;
+      BLP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&hcu, k_score_hash<HS_BLOCK, HS_HT>, HS_BLOCK, 0));
+      hipLaunchKernelGGL((k_score_hash<HS_BLOCK, HS_HT>), dim3(g->n_cu * std::max(hcu, 1)), dim3(HS_BLOCK), 0, b->stream, a,
+                         b->d_hflag, (int32_t)b->xlo);
+      BLP_HIP(hipGetLastError());
+    }
     if (!pk24) BLP_HIP(hipMemsetAsync(b->d_pcn, 0, 4 * (size_t)np, b->stream));
     if (mask & BLP_ADAMIC) BLP_HIP(hipMemsetAsync(b->d_paa, 0, 16 * (size_t)np, b->stream));
     int per_cu = 1;
@@ -2974,16 +3143,16 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
       BLP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_score_split<S_BLOCK, S_CAP_BIG, S_SEG, 8>, S_BLOCK, 0));
       hipLaunchKernelGGL((k_score_split<S_BLOCK, S_CAP_BIG, S_SEG, 8>), dim3(g->n_cu * std::max(per_cu, 1)), dim3(S_BLOCK),
                          0, b->stream, a, b->d_gy, b->d_rsplit, b->rs_lo, b->split, b->d_pcn, b->d_paa, b->d_ph2, np, pk24,
-                         short_max);
+                         short_max, b->d_hflag, (int32_t)b->xlo);
     } else {
       BLP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_score_split<S_BLOCK, S_CAP, S_SEG, 8>, S_BLOCK, 0));
       hipLaunchKernelGGL((k_score_split<S_BLOCK, S_CAP, S_SEG, 8>), dim3(g->n_cu * std::max(per_cu, 1)), dim3(S_BLOCK), 0,
                          b->stream, a, b->d_gy, b->d_rsplit, b->rs_lo, b->split, b->d_pcn, b->d_paa, b->d_ph2, np, pk24,
-                         short_max);
+                         short_max, b->d_hflag, (int32_t)b->xlo);
     }
     BLP_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_split_combine, dim3(g->n_cu * 8), dim3(256), 0, b->stream, a, b->split, b->d_pcn, b->d_paa,
-                       b->d_ph2, np, pk24);
+                       b->d_ph2, np, pk24, b->d_hflag, (int32_t)b->xlo);
     BLP_HIP(hipGetLastError());
   } else if (np && b->global) {
     a.hot_idx = nullptr;

@@ -103,17 +103,17 @@ def test_general_graph_exact_distance(gpu):
     {"BLP_CHUNK_BITS": "1024"},                         # wider than LDS: HBM-bitmap scorer
     {"BLP_CHUNK_BITS": "1024", "BLP_NO_GLOBAL": "1"},   # multi-chunk LDS bitmap universe
     {"BLP_FORCE_GLOBAL": "1"},                          # HBM-bitmap scorer on a small universe
-    {"BLP_SPLIT": "3"},                                 # chunk-parallel scorer, 3 chunks
-    {"BLP_SPLIT": "3", "BLP_SPLIT_NOPK": "1"},          # ... per-pair count in its own word (rows >= 2^24)
-    {"BLP_SPLIT": "5", "BLP_SPLIT_BIG": "1", "BLP_SPLIT_NOPK": "1"},
-    {"BLP_SPLIT": "8", "BLP_HEAVY_WORK": "50"},         # ... 8 chunks, heavy sources pre-built
-    {"BLP_SPLIT": "2", "BLP_HOT_MIN": "8"},             # ... dense rows OR-ed per chunk
-    {"BLP_SPLIT": "40"},                                # ... many chunks, some empty
-    {"BLP_SPLIT": "3", "BLP_SPLIT_BIG": "1"},           # ... 128 KiB chunks, one workgroup per CU
-    {"BLP_SPLIT": "3", "BLP_SPLIT_BIG": "1", "BLP_SPLIT_SHORT": "0"},  # ... no thread-per-slice short path
-    {"BLP_SPLIT": "2", "BLP_SPLIT_BIG": "1", "BLP_SPLIT_SHORT": "4"},  # ... short path only below 5 ids
-    {"BLP_SPLIT": "3", "BLP_SPLIT_BIG": "1", "BLP_SPLIT_ONEQ": "1"},   # ... one item queue (no XCD groups)
-    {"BLP_SPLIT": "24", "BLP_SPLIT_BIG": "1"},          # ... same, many chunks
+    {"BLP_SPLIT": "3", "BLP_NO_HASH": "1"},                                 # chunk-parallel scorer, 3 chunks
+    {"BLP_SPLIT": "3", "BLP_SPLIT_NOPK": "1", "BLP_NO_HASH": "1"},          # ... per-pair count in its own word (rows >= 2^24)
+    {"BLP_SPLIT": "5", "BLP_SPLIT_BIG": "1", "BLP_SPLIT_NOPK": "1", "BLP_NO_HASH": "1"},
+    {"BLP_SPLIT": "8", "BLP_HEAVY_WORK": "50", "BLP_NO_HASH": "1"},         # ... 8 chunks, heavy sources pre-built
+    {"BLP_SPLIT": "2", "BLP_HOT_MIN": "8", "BLP_NO_HASH": "1"},             # ... dense rows OR-ed per chunk
+    {"BLP_SPLIT": "40", "BLP_NO_HASH": "1"},                                # ... many chunks, some empty
+    {"BLP_SPLIT": "3", "BLP_SPLIT_BIG": "1", "BLP_NO_HASH": "1"},           # ... 128 KiB chunks, one workgroup per CU
+    {"BLP_SPLIT": "3", "BLP_SPLIT_BIG": "1", "BLP_SPLIT_SHORT": "0", "BLP_NO_HASH": "1"},  # ... no thread-per-slice short path
+    {"BLP_SPLIT": "2", "BLP_SPLIT_BIG": "1", "BLP_SPLIT_SHORT": "4", "BLP_NO_HASH": "1"},  # ... short path only below 5 ids
+    {"BLP_SPLIT": "3", "BLP_SPLIT_BIG": "1", "BLP_SPLIT_ONEQ": "1", "BLP_NO_HASH": "1"},   # ... one item queue (no XCD groups)
+    {"BLP_SPLIT": "24", "BLP_SPLIT_BIG": "1", "BLP_NO_HASH": "1"},          # ... same, many chunks
     {"BLP_HEAVY_WORK": "50"},                           # heavy sources pre-built by k_heavy
     {"BLP_HEAVY_WORK": "1"},                            # one row per heavy item
     {"BLP_CHUNK_BITS": "2048", "BLP_HEAVY_WORK": "50", "BLP_NO_GLOBAL": "1"},  # multi-chunk: no heavy path
@@ -146,6 +146,9 @@ def test_general_graph_exact_distance(gpu):
     {"BLP_WEDGE": "0", "BLP_HEAVY_WORK": "50"},         # graph built without wedge rows
     {"BLP_WEDGE_MAX_X": "0.5"},                         # wedge rows over budget: not built
     {"BLP_HEAVY_WORK": "7"},                            # wedge slices of 1 vector, uneven tails
+    {"BLP_SPLIT": "3", "BLP_SPLIT_BIG": "1", "BLP_HASH_WORK": "600"},  # hash-set scorer for light sources, split for the rest
+    {"BLP_SPLIT": "2", "BLP_SPLIT_BIG": "1", "BLP_HASH_WORK": "100000"},  # every source on the hash-set scorer (knob clamped to HT - 1)
+    {"BLP_SPLIT": "4", "BLP_HASH_WORK": "400"},          # ... beside the 64 KiB chunk scorer
 ])
 def test_kernel_paths_vs_oracle(gpu, knobs, monkeypatch):
     for k, v in knobs.items():
@@ -166,14 +169,15 @@ def test_kernel_paths_vs_oracle(gpu, knobs, monkeypatch):
         assert G.batch(x, y).plan()["chunks"] == -int(knobs["BLP_SPLIT"])  # chunk-parallel scorer
 
 
-@pytest.mark.parametrize("variant", [None, "1", "2", "split", "split_big", "split_nopk", "split_noshort"])
+@pytest.mark.parametrize("variant", [None, "1", "2", "split", "split_big", "split_nopk", "split_noshort", "split_hash"])
 def test_many_pairs_per_source_vs_oracle(gpu, variant, monkeypatch):
     # > SEG pairs per source and > SEG rows in N(x): the segment-chunk loops; batches of more
     # than one block step: the segment hint tables. Chunk-parallel scorer: several pair batches
     # per (source, chunk) item, so the next batch's metadata comes from the in-flight prefetch
-    knobs = {"split": {"BLP_SPLIT": "3"}, "split_big": {"BLP_SPLIT": "4", "BLP_SPLIT_BIG": "1"},
-             "split_nopk": {"BLP_SPLIT": "4", "BLP_SPLIT_BIG": "1", "BLP_SPLIT_NOPK": "1"},
-             "split_noshort": {"BLP_SPLIT": "4", "BLP_SPLIT_BIG": "1", "BLP_SPLIT_SHORT": "0"}}
+    knobs = {"split": {"BLP_SPLIT": "3", "BLP_NO_HASH": "1"}, "split_big": {"BLP_SPLIT": "4", "BLP_SPLIT_BIG": "1", "BLP_NO_HASH": "1"},
+             "split_nopk": {"BLP_SPLIT": "4", "BLP_SPLIT_BIG": "1", "BLP_SPLIT_NOPK": "1", "BLP_NO_HASH": "1"},
+             "split_noshort": {"BLP_SPLIT": "4", "BLP_SPLIT_BIG": "1", "BLP_SPLIT_SHORT": "0", "BLP_NO_HASH": "1"},
+             "split_hash": {"BLP_SPLIT": "4", "BLP_SPLIT_BIG": "1", "BLP_HASH_WORK": "100000"}}
     if variant in knobs:
         for k, v in knobs[variant].items():
             monkeypatch.setenv(k, v)
