@@ -59,6 +59,7 @@ struct Misc {
   int queue;
   int zero_div;
   int hq;     // k_score_hash's queue head
+  int n_items;  // item grouping: items planned by k_item_plan
   int qh[8];  // k_score_split: one queue head per XCD group (sources s = g mod 8)
 };
 
@@ -152,7 +153,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan_out(const int32_t* __restri
 }
 
 __global__ __launch_bounds__(GP_BLOCK) void k_bucket_hist(const int32_t* __restrict__ x, int64_t np, int32_t xlo,
-                                                          int shift, int nb, int nblk, int64_t per_blk,
+                                                          int shift, int bmask, int nb, int nblk, int64_t per_blk,
                                                           int32_t* __restrict__ hist) {
   __shared__ int h[NB_MAX];
   for (int i = threadIdx.x; i < nb; i += GP_BLOCK) h[i] = 0;
@@ -168,7 +169,7 @@ __global__ __launch_bounds__(GP_BLOCK) void k_bucket_hist(const int32_t* __restr
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      if (xv[u] != INT32_MIN) atomicAdd(&h[(xv[u] - xlo) >> shift], 1);
+      if (xv[u] != INT32_MIN) atomicAdd(&h[((xv[u] - xlo) >> shift) & bmask], 1);
   }
   __syncthreads();
   for (int i = threadIdx.x; i < nb; i += GP_BLOCK) hist[(int64_t)i * nblk + blockIdx.x] = h[i];
@@ -177,7 +178,7 @@ __global__ __launch_bounds__(GP_BLOCK) void k_bucket_hist(const int32_t* __restr
 // The pair itself (caller index, x, y) moves into bucket order, so the group kernel reads
 // its bucket contiguously instead of gathering x[i] / y[i] at random caller positions.
 __global__ __launch_bounds__(GP_BLOCK) void k_bucket_scatter(const int32_t* __restrict__ x, const int32_t* __restrict__ y,
-                                                             int64_t np, int32_t xlo, int shift, int nb, int nblk,
+                                                             int64_t np, int32_t xlo, int shift, int bmask, int nb, int nblk,
                                                              int64_t per_blk, const int32_t* __restrict__ hoff,
                                                              int4* __restrict__ tmp) {
   __shared__ int cur[NB_MAX];
@@ -195,7 +196,7 @@ __global__ __launch_bounds__(GP_BLOCK) void k_bucket_scatter(const int32_t* __re
     }
     int pos[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) pos[u] = xv[u] != INT32_MIN ? atomicAdd(&cur[(xv[u] - xlo) >> shift], 1) : -1;
+    for (int u = 0; u < U; ++u) pos[u] = xv[u] != INT32_MIN ? atomicAdd(&cur[((xv[u] - xlo) >> shift) & bmask], 1) : -1;
 #pragma unroll
     for (int u = 0; u < U; ++u)
       if (pos[u] >= 0) tmp[pos[u]] = make_int4((int32_t)(r + u * GP_BLOCK + threadIdx.x), xv[u], yv[u], 0);
@@ -289,6 +290,158 @@ __global__ __launch_bounds__(GB_BLOCK) void k_bucket_group(const int64_t* __rest
       }
     }
   }
+}
+
+// ---- item grouping (the default for pair lists not grouped by source): skew-proof. Measured
+// on config 2's business pass (x = business, Zipf-popular): the bucket of the 64 most popular
+// ids holds ~16% of the 7.55M pairs, so k_bucket_group ran one workgroup over 1.2M pairs
+// (461 us, the rest of the grid idle) and the hist / scatter LDS counters of that bucket
+// serialised. Here buckets INTERLEAVE ids (bucket = v mod nb, key j = v / nb, v = x - xlo) so
+// popular ids land in different buckets, and each bucket's pairs are cut into items of at most
+// GI_PAIRS, one workgroup each: a source with 1M pairs costs 256 workgroups, not one.
+//   k_item_plan   one block: items per bucket, item table (bucket, first, end)
+//   k_item_count  per item: LDS histogram of its keys, one device atomic per (item, key) into cnt
+//   scans         off = exclusive scan of cnt over the id range; active = ids with cnt > 0
+//   k_item_write  per item: the same histogram; per key one device atomic reserves the item's
+//                 run inside [off, off + cnt) (fill), then LDS cursors place every pair
+// Order within one source's group follows item order (not caller order): every grouped pair
+// carries its caller index (g_out), so results do not depend on it.
+constexpr int GI_PAIRS = 4096;
+
+__global__ __launch_bounds__(1024) void k_item_plan(const int32_t* __restrict__ hoff, int nblk, int nb, int64_t np,
+                                                    int32_t* __restrict__ item_b, int32_t* __restrict__ item_s,
+                                                    int32_t* __restrict__ item_e, int32_t* __restrict__ n_items) {
+  __shared__ int red[1024 / 64];
+  int carry = 0;
+  for (int b0 = 0; b0 < nb; b0 += 1024) {
+    const int b = b0 + (int)threadIdx.x;
+    const int s = b < nb ? hoff[(int64_t)b * nblk] : 0;
+    const int e = b < nb ? (b + 1 < nb ? hoff[(int64_t)(b + 1) * nblk] : (int)np) : 0;
+    const int it = (e - s + GI_PAIRS - 1) / GI_PAIRS;
+    int tot;
+    int o = block_exscan_i<1024>(it, red, &tot) + carry;
+    for (int q = 0; q < it; ++q, ++o) {
+      item_b[o] = b;
+      item_s[o] = s + q * GI_PAIRS;
+      item_e[o] = min(e, s + (q + 1) * GI_PAIRS);
+    }
+    carry += tot;
+  }
+  if (threadIdx.x == 0) *n_items = carry;
+}
+
+template <int KEYS>
+__device__ inline void item_hist(const int4* __restrict__ tmp, int s, int e, int32_t xlo, int lognb, int* h) {
+  for (int i = threadIdx.x; i < KEYS; i += GB_BLOCK) h[i] = 0;
+  __syncthreads();
+  constexpr int UC = 4;  // GI_PAIRS / GB_BLOCK = 16 pairs per thread: UC loads in flight
+  for (int kr = s; kr < e; kr += UC * GB_BLOCK) {
+    int xv[UC];
+#pragma unroll
+    for (int u = 0; u < UC; ++u) {
+      const int k = kr + u * GB_BLOCK + (int)threadIdx.x;
+      xv[u] = k < e ? tmp[k].y : INT32_MIN;
+    }
+#pragma unroll
+    for (int u = 0; u < UC; ++u)
+      if (xv[u] != INT32_MIN) atomicAdd(&h[(xv[u] - xlo) >> lognb], 1);
+  }
+  __syncthreads();
+}
+
+template <int KEYS>
+__global__ __launch_bounds__(GB_BLOCK) void k_item_count(const int4* __restrict__ tmp, const int32_t* __restrict__ item_b,
+                                                         const int32_t* __restrict__ item_s,
+                                                         const int32_t* __restrict__ item_e,
+                                                         const int32_t* __restrict__ n_items, int32_t xlo, int lognb,
+                                                         int32_t* __restrict__ cnt) {
+  __shared__ int h[KEYS];
+  const int i = blockIdx.x;
+  if (i >= *n_items) return;  // uniform: the grid is the host's upper bound on items
+  const int b = item_b[i];
+  item_hist<KEYS>(tmp, item_s[i], item_e[i], xlo, lognb, h);
+  for (int j = threadIdx.x; j < KEYS; j += GB_BLOCK)
+    if (h[j]) atomicAdd(&cnt[xlo + b + (j << lognb)], h[j]);
+}
+
+template <int KEYS>
+__global__ __launch_bounds__(GB_BLOCK) void k_item_write(const int64_t* __restrict__ rp, const int4* __restrict__ tmp,
+                                                         const int32_t* __restrict__ item_b,
+                                                         const int32_t* __restrict__ item_s,
+                                                         const int32_t* __restrict__ item_e,
+                                                         const int32_t* __restrict__ n_items, int32_t xlo, int lognb,
+                                                         const int32_t* __restrict__ off, int32_t* __restrict__ fill,
+                                                         int32_t* __restrict__ g_out, int64_t* __restrict__ g_yb,
+                                                         int32_t* __restrict__ g_yl, int32_t* __restrict__ g_y) {
+  __shared__ int h[KEYS];
+  const int i = blockIdx.x;
+  if (i >= *n_items) return;
+  const int b = item_b[i], s = item_s[i], e = item_e[i];
+  item_hist<KEYS>(tmp, s, e, xlo, lognb, h);
+  for (int j = threadIdx.x; j < KEYS; j += GB_BLOCK)
+    if (h[j]) {
+      const int v = b + (j << lognb);
+      h[j] = off[xlo + v] + atomicAdd(&fill[v], h[j]);  // this item's run of source x
+    }
+  __syncthreads();
+  constexpr int U = 4;
+  for (int k0r = s; k0r < e; k0r += U * GB_BLOCK) {
+    int4 t[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = k0r + u * GB_BLOCK + (int)threadIdx.x;
+      t[u] = k < e ? tmp[k] : make_int4(-1, xlo, 0, 0);
+    }
+    int64_t st[U], en[U];
+    int pos[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      st[u] = rp[t[u].z];
+      en[u] = rp[t[u].z + 1];
+      pos[u] = t[u].x >= 0 ? atomicAdd(&h[(t[u].y - xlo) >> lognb], 1) : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (t[u].x >= 0) {
+        g_out[pos[u]] = t[u].x;
+        g_yb[pos[u]] = st[u];
+        g_yl[pos[u]] = (int32_t)(en[u] - st[u]);
+        if (g_y) g_y[pos[u]] = t[u].z;
+      }
+    }
+  }
+}
+
+// active sources = ids with cnt > 0, ascending (tile counts -> scan -> writes)
+__global__ __launch_bounds__(SCAN_BLOCK) void k_nz_count(const int32_t* __restrict__ cnt, int64_t n,
+                                                         int32_t* __restrict__ tile_cnt) {
+  __shared__ int red[SCAN_BLOCK / 64];
+  const int64_t base = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)threadIdx.x * SCAN_ITEMS;
+  int v = 0;
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; ++k) v += (base + k < n && cnt[base + k] > 0) ? 1 : 0;
+  int tot;
+  block_exscan_i<SCAN_BLOCK>(v, red, &tot);
+  if (threadIdx.x == 0) tile_cnt[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(SCAN_BLOCK) void k_nz_write(const int32_t* __restrict__ cnt, int64_t n,
+                                                         const int32_t* __restrict__ tile_off, int32_t xlo,
+                                                         int32_t* __restrict__ active) {
+  __shared__ int red[SCAN_BLOCK / 64];
+  const int64_t base = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)threadIdx.x * SCAN_ITEMS;
+  bool h[SCAN_ITEMS];
+  int v = 0;
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; ++k) {
+    h[k] = base + k < n && cnt[base + k] > 0;
+    v += h[k] ? 1 : 0;
+  }
+  int tot;
+  int o = block_exscan_i<SCAN_BLOCK>(v, red, &tot) + tile_off[blockIdx.x];
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; ++k)
+    if (h[k]) active[o++] = xlo + (int32_t)(base + k);
 }
 
 // ---- grouping of a pair list that arrives already grouped by source (x non-decreasing, as
@@ -2556,6 +2709,7 @@ struct blp_batch {
   int64_t cap_bits = 0;
   int64_t n_sources = 0;
   bool runs = false;  // pairs arrive grouped by source (x non-decreasing): run-head grouping
+  bool items = false;  // item grouping (interleaved buckets cut into GI_PAIRS items); else k_bucket_group
   blp::KernelTimer t_score, t_group;
   // the batch's own stream and grouping scratch: batches of one graph (the user and the
   // business pass of similarity.main) run concurrently, one filling the other's tail
@@ -2862,10 +3016,20 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
     if (srcs.empty()) xlo = xhi = 0;
     b->xlo = xlo;
     b->xspan = (int64_t)xhi - xlo;
-    b->shift = 0;
-    while ((b->xspan >> b->shift) > 2048) ++b->shift;
-    b->nb = (int)std::max<int64_t>(1, (b->xspan + (int64_t(1) << b->shift) - 1) >> b->shift);
-    if (b->shift > 15 || b->nb > NB_MAX) return bail(fail(BLP_E_UNSUP, "blp_batch_create: source id range too wide"));
+    b->items = !getenv("BLP_GROUP_BUCKETS");  // A/B knob: one workgroup per contiguous bucket
+    if (b->items) {
+      // nb = 2^shift interleaved buckets (<= 2048), each with ceil(xspan / nb) keys
+      b->shift = 0;
+      while ((int64_t(1) << b->shift) < std::min<int64_t>(b->xspan, 2048)) ++b->shift;
+      b->nb = 1 << b->shift;
+      if (((b->xspan + b->nb - 1) >> b->shift) > 32768)
+        return bail(fail(BLP_E_UNSUP, "blp_batch_create: source id range too wide"));
+    } else {
+      b->shift = 0;
+      while ((b->xspan >> b->shift) > 2048) ++b->shift;
+      b->nb = (int)std::max<int64_t>(1, (b->xspan + (int64_t(1) << b->shift) - 1) >> b->shift);
+      if (b->shift > 15 || b->nb > NB_MAX) return bail(fail(BLP_E_UNSUP, "blp_batch_create: source id range too wide"));
+    }
     b->nblk = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)g->n_cu * 2, (n_pairs + 4095) / 4096));
     b->per_blk = (n_pairs + b->nblk - 1) / b->nblk;
   }
@@ -3000,8 +3164,11 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   if ((rc = b->cnt.reserve(4 * (n + 1)))) return rc;
   if ((rc = b->off.reserve(4 * (n + 1)))) return rc;
   if ((rc = b->active.reserve(4 * (n + 1)))) return rc;
-  // scratch: hist | hoff | tiles | bucket_active | abase | tmp
-  const int64_t sc_ints = 2 * nh + std::max(tiles_h, tiles_b) + 1 + 2 * (int64_t)b->nb + 4 * np;
+  // scratch: hist | hoff | tiles | bucket_active | abase | tmp [| fill | item table | id-range tiles]
+  const int64_t items_ints = b->items ? b->xspan + 3 * ((np + GI_PAIRS - 1) / GI_PAIRS + b->nb) +
+                                            2 * ((b->xspan + SCAN_TILE - 1) / SCAN_TILE + 1)
+                                      : 0;
+  const int64_t sc_ints = 2 * nh + std::max(tiles_h, tiles_b) + 1 + 2 * (int64_t)b->nb + 4 * np + items_ints;
   if ((rc = b->scratch.reserve(4 * (sc_ints + 16)))) return rc;
   int32_t* hist = b->scratch.as<int32_t>();
   int32_t* hoff = hist + nh;
@@ -3024,48 +3191,87 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
     hipLaunchKernelGGL(k_run_cnt, dim3(1024), dim3(256), 0, b->stream, b->active.as<int32_t>(), &b->d_misc->n_active,
                        np, b->off.as<int32_t>(), b->cnt.as<int32_t>());
   } else if (np) {
-    hipLaunchKernelGGL(k_bucket_hist, dim3(b->nblk), dim3(GP_BLOCK), 0, b->stream, b->d_x, np, b->xlo, b->shift, b->nb,
-                       b->nblk, b->per_blk, hist);
+    // items mode: interleaved buckets (v & (nb - 1)); bucket mode: contiguous (v >> shift)
+    const int hshift = b->items ? 0 : b->shift, bmask = b->items ? b->nb - 1 : -1;
+    hipLaunchKernelGGL(k_bucket_hist, dim3(b->nblk), dim3(GP_BLOCK), 0, b->stream, b->d_x, np, b->xlo, hshift, bmask,
+                       b->nb, b->nblk, b->per_blk, hist);
     hipLaunchKernelGGL(k_scan_sum, dim3((unsigned)tiles_h), dim3(SCAN_BLOCK), 0, b->stream, hist, nh, tiles);
     hipLaunchKernelGGL(k_scan_mid, dim3(1), dim3(SCAN_BLOCK), 0, b->stream, tiles, tiles_h, (int32_t*)nullptr);
     hipLaunchKernelGGL(k_scan_out, dim3((unsigned)tiles_h), dim3(SCAN_BLOCK), 0, b->stream, hist, nh, tiles, hoff);
     hipLaunchKernelGGL(k_bucket_scatter, dim3(b->nblk), dim3(GP_BLOCK), 0, b->stream, b->d_x, b->d_y, np, b->xlo,
-                       b->shift, b->nb, b->nblk, b->per_blk, hoff, tmp);
-    const int keys = 1 << b->shift;
+                       hshift, bmask, b->nb, b->nblk, b->per_blk, hoff, tmp);
+    if (b->items) {
+      const int64_t ub = (np + GI_PAIRS - 1) / GI_PAIRS + b->nb, tx = (b->xspan + SCAN_TILE - 1) / SCAN_TILE;
+      int32_t* fill = reinterpret_cast<int32_t*>(tmp + np);
+      int32_t *it_b = fill + b->xspan, *it_s = it_b + ub, *it_e = it_s + ub, *tx1 = it_e + ub, *tx2 = tx1 + tx + 1;
+      int32_t *cnt = b->cnt.as<int32_t>(), *off = b->off.as<int32_t>();
+      BLP_HIP(hipMemsetAsync(cnt + b->xlo, 0, 4 * (size_t)b->xspan, b->stream));
+      BLP_HIP(hipMemsetAsync(fill, 0, 4 * (size_t)b->xspan, b->stream));
+      hipLaunchKernelGGL(k_item_plan, dim3(1), dim3(1024), 0, b->stream, hoff, b->nblk, b->nb, np, it_b, it_s, it_e,
+                         &b->d_misc->n_items);
+      const int64_t keys = (b->xspan + b->nb - 1) >> b->shift;
+#define BLP_ITEM_LAUNCH(K)                                                                                         \
+  hipLaunchKernelGGL(k_item_count<K>, dim3((unsigned)ub), dim3(GB_BLOCK), 0, b->stream, tmp, it_b, it_s, it_e,     \
+                     &b->d_misc->n_items, b->xlo, b->shift, cnt);                                                   \
+  hipLaunchKernelGGL(k_scan_sum, dim3((unsigned)tx), dim3(SCAN_BLOCK), 0, b->stream, cnt + b->xlo, b->xspan, tx1); \
+  hipLaunchKernelGGL(k_scan_mid, dim3(1), dim3(SCAN_BLOCK), 0, b->stream, tx1, tx, (int32_t*)nullptr);             \
+  hipLaunchKernelGGL(k_scan_out, dim3((unsigned)tx), dim3(SCAN_BLOCK), 0, b->stream, cnt + b->xlo, b->xspan, tx1,  \
+                     off + b->xlo);                                                                                 \
+  hipLaunchKernelGGL(k_nz_count, dim3((unsigned)tx), dim3(SCAN_BLOCK), 0, b->stream, cnt + b->xlo, b->xspan, tx2); \
+  hipLaunchKernelGGL(k_scan_mid, dim3(1), dim3(SCAN_BLOCK), 0, b->stream, tx2, tx, &b->d_misc->n_active);          \
+  hipLaunchKernelGGL(k_nz_write, dim3((unsigned)tx), dim3(SCAN_BLOCK), 0, b->stream, cnt + b->xlo, b->xspan, tx2,  \
+                     b->xlo, b->active.as<int32_t>());                                                              \
+  hipLaunchKernelGGL(k_item_write<K>, dim3((unsigned)ub), dim3(GB_BLOCK), 0, b->stream, g->d_rp, tmp, it_b, it_s,  \
+                     it_e, &b->d_misc->n_items, b->xlo, b->shift, off, fill, b->d_gout, b->d_gyb, b->d_gyl, b->d_gy)
+      if (keys <= 64) {  // 272 bytes of LDS: fits beside a 160 KiB large-scorer workgroup
+        BLP_ITEM_LAUNCH(64);
+      } else if (keys <= 256) {
+        BLP_ITEM_LAUNCH(256);
+      } else if (keys <= 1024) {
+        BLP_ITEM_LAUNCH(1024);
+      } else if (keys <= 4096) {
+        BLP_ITEM_LAUNCH(4096);
+      } else {
+        BLP_ITEM_LAUNCH(32768);
+      }
+#undef BLP_ITEM_LAUNCH
+    } else {
+      const int keys = 1 << b->shift;
 #define BLP_GROUP_LAUNCH(K)                                                                                         \
-  hipLaunchKernelGGL(k_bucket_group<K>, dim3(b->nb), dim3(GB_BLOCK), 0, b->stream, g->d_rp, tmp, hoff,               \
-                     b->nblk, b->nb, b->shift, b->xlo, b->xspan, np, b->off.as<int32_t>(), b->cnt.as<int32_t>(), bact,  \
-                     b->d_gout,                                                                                       \
-                     b->d_gyb, b->d_gyl, b->d_gy)
-    if (keys <= 64)  // 272 bytes of LDS: fits beside a 160 KiB large-scorer workgroup
-      BLP_GROUP_LAUNCH(64);
-    else if (keys <= 256)
-      BLP_GROUP_LAUNCH(256);
-    else if (keys <= 1024)
-      BLP_GROUP_LAUNCH(1024);
-    else if (keys <= 4096)
-      BLP_GROUP_LAUNCH(4096);
-    else
-      BLP_GROUP_LAUNCH(32768);
+    hipLaunchKernelGGL(k_bucket_group<K>, dim3(b->nb), dim3(GB_BLOCK), 0, b->stream, g->d_rp, tmp, hoff,               \
+                       b->nblk, b->nb, b->shift, b->xlo, b->xspan, np, b->off.as<int32_t>(), b->cnt.as<int32_t>(), bact,  \
+                       b->d_gout,                                                                                       \
+                       b->d_gyb, b->d_gyl, b->d_gy)
+      if (keys <= 64)  // 272 bytes of LDS: fits beside a 160 KiB large-scorer workgroup
+        BLP_GROUP_LAUNCH(64);
+      else if (keys <= 256)
+        BLP_GROUP_LAUNCH(256);
+      else if (keys <= 1024)
+        BLP_GROUP_LAUNCH(1024);
+      else if (keys <= 4096)
+        BLP_GROUP_LAUNCH(4096);
+      else
+        BLP_GROUP_LAUNCH(32768);
 #undef BLP_GROUP_LAUNCH
-    hipLaunchKernelGGL(k_scan_sum, dim3((unsigned)tiles_b), dim3(SCAN_BLOCK), 0, b->stream, bact, (int64_t)b->nb, tiles);
-    hipLaunchKernelGGL(k_scan_mid, dim3(1), dim3(SCAN_BLOCK), 0, b->stream, tiles, tiles_b, &b->d_misc->n_active);
-    hipLaunchKernelGGL(k_scan_out, dim3((unsigned)tiles_b), dim3(SCAN_BLOCK), 0, b->stream, bact, (int64_t)b->nb, tiles,
-                       abase);
+      hipLaunchKernelGGL(k_scan_sum, dim3((unsigned)tiles_b), dim3(SCAN_BLOCK), 0, b->stream, bact, (int64_t)b->nb, tiles);
+      hipLaunchKernelGGL(k_scan_mid, dim3(1), dim3(SCAN_BLOCK), 0, b->stream, tiles, tiles_b, &b->d_misc->n_active);
+      hipLaunchKernelGGL(k_scan_out, dim3((unsigned)tiles_b), dim3(SCAN_BLOCK), 0, b->stream, bact, (int64_t)b->nb, tiles,
+                         abase);
 #define BLP_ACTIVE_LAUNCH(K)                                                                                   \
-  hipLaunchKernelGGL(k_active_write<K>, dim3(b->nb), dim3(GB_BLOCK), 0, b->stream, b->cnt.as<int32_t>(), abase, b->shift, \
-                     b->xlo, b->xspan, b->active.as<int32_t>())
-    if (keys <= 64)  // 272 bytes of LDS: fits beside a 160 KiB large-scorer workgroup
-      BLP_ACTIVE_LAUNCH(64);
-    else if (keys <= 256)
-      BLP_ACTIVE_LAUNCH(256);
-    else if (keys <= 1024)
-      BLP_ACTIVE_LAUNCH(1024);
-    else if (keys <= 4096)
-      BLP_ACTIVE_LAUNCH(4096);
-    else
-      BLP_ACTIVE_LAUNCH(32768);
+    hipLaunchKernelGGL(k_active_write<K>, dim3(b->nb), dim3(GB_BLOCK), 0, b->stream, b->cnt.as<int32_t>(), abase, b->shift, \
+                       b->xlo, b->xspan, b->active.as<int32_t>())
+      if (keys <= 64)  // 272 bytes of LDS: fits beside a 160 KiB large-scorer workgroup
+        BLP_ACTIVE_LAUNCH(64);
+      else if (keys <= 256)
+        BLP_ACTIVE_LAUNCH(256);
+      else if (keys <= 1024)
+        BLP_ACTIVE_LAUNCH(1024);
+      else if (keys <= 4096)
+        BLP_ACTIVE_LAUNCH(4096);
+      else
+        BLP_ACTIVE_LAUNCH(32768);
 #undef BLP_ACTIVE_LAUNCH
+    }
   }
   BLP_HIP(hipGetLastError());
   if ((rc = timer_end(b->t_group, b->stream, bt0))) return rc;

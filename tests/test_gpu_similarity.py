@@ -220,6 +220,24 @@ def test_unsorted_pair_order_vs_oracle(gpu):
     _check_against_oracle(a, b, x[perm], y[perm])
 
 
+@pytest.mark.parametrize("mode", ["items", "buckets"])
+def test_skewed_unsorted_grouping_vs_oracle(gpu, mode, monkeypatch):
+    # ungrouped pair lists with one hot source (> several GI_PAIRS items of its own) and a run
+    # of popular neighbouring ids, over a wide id range (hundreds of keys per bucket)
+    if mode == "buckets":
+        monkeypatch.setenv("BLP_GROUP_BUCKETS", "1")
+    rng = np.random.default_rng(15)
+    a, b = bipartite_edges(rng, 300000, 2000, 400000)
+    G = blp.DeviceGraph(a, b)
+    nu = G.n - len(np.unique(b))
+    hot = int(rng.integers(0, nu))
+    x = np.concatenate([np.full(18000, hot), rng.integers(0, 64, 6000), rng.integers(0, nu, 9000)]).astype(np.int32)
+    y = rng.integers(nu, G.n, len(x)).astype(np.int32)
+    perm = rng.permutation(len(x))
+    _check_against_oracle(a, b, x[perm], y[perm])
+    _check_against_oracle(a, b, y[perm], x[perm])
+
+
 def test_batch_repeat_is_deterministic(gpu):
     rng = np.random.default_rng(3)
     a, b = bipartite_edges(rng, 20000, 1000, 100000)
