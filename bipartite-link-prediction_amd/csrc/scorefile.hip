@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <charconv>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <thread>
 #include <unordered_set>
@@ -184,14 +185,15 @@ int parse(blp_examples* x) {
   return BLP_OK;
 }
 
-// Python's repr(float) for a finite double (float_repr_style 'short': Py_DTSF_ADD_DOT_0).
-void put_repr(std::string& o, double v) {
+// Python's repr(float) for a finite double (float_repr_style 'short': Py_DTSF_ADD_DOT_0),
+// written at o (at most 24 bytes); returns the end.
+char* put_repr(char* o, double v) {
   char buf[64];
   const auto r = std::to_chars(buf, buf + sizeof(buf), v, std::chars_format::scientific);
   // buf = [-]d[.ddd]e(+|-)XX : the shortest round-trip digits
   const char* p = buf;
   if (*p == '-') {
-    o.push_back('-');
+    *o++ = '-';
     ++p;
   }
   char dig[32];
@@ -204,30 +206,45 @@ void put_repr(std::string& o, double v) {
   std::from_chars(p + 1 + (p[1] == '+' ? 1 : 0), r.ptr, ex);
   const int decpt = ex + 1;
   if (decpt <= -4 || decpt > 16) {  // exponent notation
-    o.push_back(dig[0]);
+    *o++ = dig[0];
     if (nd > 1) {
-      o.push_back('.');
-      o.append(dig + 1, nd - 1);
+      *o++ = '.';
+      std::memcpy(o, dig + 1, nd - 1);
+      o += nd - 1;
     }
     const int e = decpt - 1;
-    o.push_back('e');
-    o.push_back(e < 0 ? '-' : '+');
+    *o++ = 'e';
+    *o++ = e < 0 ? '-' : '+';
     const int ae = e < 0 ? -e : e;
-    if (ae < 10) o.push_back('0');
-    o += std::to_string(ae);
+    if (ae < 10) *o++ = '0';
+    o = std::to_chars(o, o + 8, ae).ptr;
   } else if (decpt <= 0) {  // 0.000ddd
-    o += "0.";
-    o.append(-decpt, '0');
-    o.append(dig, nd);
+    *o++ = '0';
+    *o++ = '.';
+    std::memset(o, '0', -decpt);
+    o += -decpt;
+    std::memcpy(o, dig, nd);
+    o += nd;
   } else if (decpt >= nd) {  // ddd000.0
-    o.append(dig, nd);
-    o.append(decpt - nd, '0');
-    o += ".0";
+    std::memcpy(o, dig, nd);
+    o += nd;
+    std::memset(o, '0', decpt - nd);
+    o += decpt - nd;
+    *o++ = '.';
+    *o++ = '0';
   } else {
-    o.append(dig, decpt);
-    o.push_back('.');
-    o.append(dig + decpt, nd - decpt);
+    std::memcpy(o, dig, decpt);
+    o += decpt;
+    *o++ = '.';
+    std::memcpy(o, dig + decpt, nd - decpt);
+    o += nd - decpt;
   }
+  return o;
+}
+
+inline char* put_bytes(char* o, const char* s, size_t n) {
+  std::memcpy(o, s, n);
+  return o + n;
 }
 
 }  // namespace
@@ -315,11 +332,18 @@ int blp_scores_write(const blp_examples* x, const char* path, int kind, const ui
   for (unsigned t = 1; t < nt; ++t)
     cut[t] = std::lower_bound(x->u_off.begin(), x->u_off.end(), np * (int64_t)t / nt) - x->u_off.begin();
   for (unsigned t = 1; t <= nt; ++t) cut[t] = std::max(cut[t], cut[t - 1]);
-  std::vector<std::string> part(nt);
+  // each slice formats into its own buffer, sized by a bound: per user its key + 8 bytes,
+  // per pair its key + 6 + a value of at most 24 bytes (repr of a double; 10 digits of a u32)
+  std::vector<std::unique_ptr<char[]>> part(nt);
+  std::vector<int64_t> part_len(nt, 0);
   std::vector<uint8_t> nonempty(nt, 0);
   auto work = [&](unsigned t) {
-    std::string& o = part[t];
-    o.reserve((size_t)(x->u_off[cut[t + 1]] - x->u_off[cut[t]]) * 28 + 64);
+    int64_t bound = 16;
+    for (int64_t u = cut[t]; u < cut[t + 1]; ++u) bound += x->u_len[u] + 8;
+    for (int64_t k = x->u_off[cut[t]]; k < x->u_off[cut[t + 1]]; ++k) bound += x->v_len[k] + 30;
+    part[t].reset(new char[(size_t)bound]);
+    char* const o0 = part[t].get();
+    char* o = o0;
     bool first_user = true;
     for (int64_t u = cut[t]; u < cut[t + 1]; ++u) {
       bool opened = false;
@@ -329,35 +353,36 @@ int blp_scores_write(const blp_examples* x, const char* path, int kind, const ui
         // for a present pair under an unmatched method (defaultdict: no empty user dicts)
         if (kind == BLP_SCORE_NONE && pres) continue;
         if (!opened) {
-          if (!first_user) o += ", ";
+          if (!first_user) o = put_bytes(o, ", ", 2);
           first_user = false;
-          o.push_back('"');
-          o.append(base + x->u_key[u], x->u_len[u]);
-          o += "\": {";
+          *o++ = '"';
+          o = put_bytes(o, base + x->u_key[u], x->u_len[u]);
+          o = put_bytes(o, "\": {", 4);
           opened = true;
         } else {
-          o += ", ";
+          o = put_bytes(o, ", ", 2);
         }
-        o.push_back('"');
-        o.append(base + x->v_key[k], x->v_len[k]);
-        o += "\": ";
+        *o++ = '"';
+        o = put_bytes(o, base + x->v_key[k], x->v_len[k]);
+        o = put_bytes(o, "\": ", 3);
         if (!pres) {
-          o.push_back('0');
+          *o++ = '0';
           continue;
         }
         const int64_t vi = present ? vidx[k] : k;
         if (kind == BLP_SCORE_U32) {
-          o += std::to_string(((const uint32_t*)values)[vi]);
+          o = std::to_chars(o, o + 12, ((const uint32_t*)values)[vi]).ptr;
         } else {
           const double v = ((const double*)values)[vi];
           if (kind == BLP_SCORE_F64_INT0 && v == 0.0)
-            o.push_back('0');  // similarity.py:118: nothing added -> the int 0
+            *o++ = '0';  // similarity.py:118: nothing added -> the int 0
           else
-            put_repr(o, v);
+            o = put_repr(o, v);
         }
       }
-      if (opened) o.push_back('}');
+      if (opened) *o++ = '}';
     }
+    part_len[t] = o - o0;
     nonempty[t] = !first_user;
   };
   std::vector<std::thread> th;
@@ -375,7 +400,7 @@ int blp_scores_write(const blp_examples* x, const char* path, int kind, const ui
     if (!nonempty[t]) continue;
     if (any) pos += 2;
     at[t] = pos;
-    pos += (int64_t)part[t].size();
+    pos += part_len[t];
     any = true;
   }
   auto put = [fd](const char* p, int64_t len, int64_t off) {
@@ -394,7 +419,7 @@ int blp_scores_write(const blp_examples* x, const char* path, int kind, const ui
     const bool with_sep = sep;
     sep = true;
     th.emplace_back([&, t, with_sep]() {
-      wok[t] = (!with_sep || put(", ", 2, at[t] - 2)) && put(part[t].data(), (int64_t)part[t].size(), at[t]);
+      wok[t] = (!with_sep || put(", ", 2, at[t] - 2)) && put(part[t].get(), part_len[t], at[t]);
     });
   }
   bool ok = put("{", 1, 0) && put("}", 1, pos);

@@ -27,6 +27,7 @@ Reference behaviour kept on purpose:
 * the per-pair ``print`` calls of business() (similarity.py:97,100) are not reproduced.
 """
 import datetime
+import os
 
 import numpy as np
 
@@ -170,25 +171,48 @@ def _run_side(examples, G, methods, outfiles, table, side, sidecar=False, scored
     return results
 
 
-def _write_side(ex, methods, outfiles, table, present, scores):
-    """The score files of one side straight from the device arrays (util.write_json's text)."""
+def _write_jobs(ex, methods, outfiles, table, present, scores):
+    """The score files of one side straight from the device arrays (util.write_json's text):
+    one callable per file."""
     import os
 
     pres = None if present.all() else present
+    jobs = []
     for m, f in zip(methods, outfiles):
         if f is None:
             continue
         bit = table.get(m, 0)
         if bit == blp.CN:
-            ex.write(f, scorefile.U32, pres, scores["cn"])
+            args = (scorefile.U32, pres, scores["cn"])
         elif bit == blp.JACCARD:
-            ex.write(f, scorefile.F64, pres, scores["jaccard"])
+            args = (scorefile.F64, pres, scores["jaccard"])
         elif bit == blp.ADAMIC:
-            ex.write(f, scorefile.F64_INT0, pres, scores["adamic"])
+            args = (scorefile.F64_INT0, pres, scores["adamic"])
         else:  # a method the reference does not match: only missing-node zeros
-            ex.write(f, scorefile.NONE, pres)
-        if os.path.exists(f + ".npz"):  # as util.write_json: a stale sidecar goes
-            os.unlink(f + ".npz")
+            args = (scorefile.NONE, pres)
+
+        def job(f=f, args=args):
+            ex.write(f, *args)
+            if os.path.exists(f + ".npz"):  # as util.write_json: a stale sidecar goes
+                os.unlink(f + ".npz")
+        jobs.append(job)
+    return jobs
+
+
+def _write_files(jobs):
+    """Run the file writes concurrently (each native write formats on its own threads and
+    releases the GIL; files on different inodes do not serialise on one inode lock). The
+    contents are what the reference's sequential writes give; a failure raises as there."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    workers = max(1, int(os.environ.get("BLP_FILE_WRITERS", "3")))
+    if workers == 1 or len(jobs) < 2:
+        for j in jobs:
+            j()
+        return
+    with ThreadPoolExecutor(min(workers, len(jobs))) as pool:
+        for fut in [pool.submit(j) for j in jobs]:
+            fut.result()
 
 
 # ----------------------------------------------------------------------------- reference API
@@ -244,8 +268,8 @@ def main(example_file, graph_file, u_methods, u_outfiles, b_methods, b_outfiles,
             _run_side(examples, G, u_methods, u_outfiles, _U_BITS, 0, sidecar, scored=(present, u_scores))
             _run_side(examples, G, b_methods, b_outfiles, dict(_B_BITS), 1, sidecar, scored=(present, b_scores))
         else:
-            _write_side(ex, u_methods, u_outfiles, _U_BITS, present, u_scores)
-            _write_side(ex, b_methods, b_outfiles, _B_BITS, present, b_scores)
+            _write_files(_write_jobs(ex, u_methods, u_outfiles, _U_BITS, present, u_scores) +
+                         _write_jobs(ex, b_methods, b_outfiles, _B_BITS, present, b_scores))
     finally:
         pool.shutdown(wait=True)
         if ex is None and fut_ex.done() and fut_ex.exception() is None:
