@@ -563,8 +563,8 @@ def run_sharded(args):
     mine = mine[G.hop1_size[lo:hi] > 0]
     src = np.sort(rng.choice(mine, size=min(args.users, len(mine)), replace=False)).astype(np.int32)
     ex_x, ex_y = synth.uniform_examples(G, src, rate=args.rate, seed=d.rank)
-    passes = [("user", G.batch(ex_x, ex_y), args.user_mask)]
-    if args.sides == "both":
+    passes = [("user", G.batch(ex_x, ex_y), args.user_mask)] if args.sides != "business" else []
+    if args.sides != "user":
         passes.append(("business", G.batch(ex_y, ex_x), 7 if getattr(args, "fix_adamic", False) else 3))
     for name, bt, _ in passes:
         log("plan %s: %s" % (name, bt.plan()))
@@ -589,7 +589,7 @@ def run_sharded(args):
     ms, n = bt0.stats(0)
     sec = ms / 1e3 / max(n, 1)
     cn0 = bt0.fetch(mask0)["cn"]
-    byts = alg_bytes(G, ex_x, ex_y, mask0, cn0)
+    byts = alg_bytes(G, *((ex_x, ex_y) if name0 == "user" else (ex_y, ex_x)), mask0, cn0)
     # ring all-gather: each rank receives (G-1)/G of the data; bound by one link per direction
     xgmi_bound_s = recv_bytes / (XGMI_LINK_GBS * 1e9) if d.world > 1 else 0.0
     out = {
@@ -599,7 +599,8 @@ def run_sharded(args):
         "config": {"workload": "config5-style row-block sharded: %d users x %d businesses, %d draws (%d unique edges); "
                                "%d users/GPU from the rank's own block, businesses outside N(u) kept at %g; step = %s"
                                % (U, B, D, G.nnz // 2, len(src), args.rate,
-                                  "user side CN+J+AA + business side CN+J" if args.sides == "both" else "user side"),
+                                  "user side CN+J+AA + business side CN+J" if args.sides == "both" else
+                                  args.sides + " side only"),
                    "pairs_per_gpu": int(len(ex_x)), "global_batch": int(pairs_total),
                    "parallelism": "row-block sharded ingest x%d + RCCL all-gather (%s), rank-local scoring"
                                   % (d.world, d.backend or "single rank")},
@@ -613,7 +614,7 @@ def run_sharded(args):
                                        (max(work[sblocks[r]:sblocks[r + 1]].sum() for r in range(d.world)) /
                                         (work.sum() / d.world))},
         "roofline": {"bound": "hbm", "achieved": byts / sec / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": byts / sec / 1e9 / HBM_PEAK_GBS, "kernel": "user-side scorer (%s)" % C5_KERNEL,
+                     "frac": byts / sec / 1e9 / HBM_PEAK_GBS, "kernel": "%s-side scorer (%s)" % (name0, C5_KERNEL),
                      "kernel_ms": 1e3 * sec, "alg_bytes_per_launch": byts, "plan": bt0.plan()},
     }
     out["roofline"].update(pmc_fields(C5_KERNEL, "r*_c5_*.json", sec))

@@ -3140,6 +3140,14 @@ int blp_batch_plan(const blp_batch* b, int64_t* lo, int64_t* hi, int* chunks, in
   return BLP_OK;
 }
 
+int blp_batch_routes(const blp_batch* b, int64_t* n_sources, int64_t* n_hash, int* runs) {
+  BLP_CHECK(b, BLP_E_ARG, "blp_batch_routes: null batch");
+  if (n_sources) *n_sources = b->n_sources;
+  if (n_hash) *n_hash = b->n_hash;
+  if (runs) *runs = b->runs ? 1 : 0;
+  return BLP_OK;
+}
+
 #ifdef BLP_PROF
 int blp_prof_read(unsigned long long* out) {  // experiment builds only: per-phase clock sums, then reset
   BLP_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * 16));
