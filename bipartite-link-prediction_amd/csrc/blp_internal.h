@@ -126,6 +126,11 @@ struct blp_graph {
   int32_t* d_wedge = nullptr;
   int64_t wedge_vecs = 0;
   std::vector<int64_t> h_wp;  // host copy of d_wp (heavy-source planning)
+  // wedge-row bitmaps (hop3.hip): the SET of ids of a long wedge row over the hop-3 mark range
+  // [wbm_lo, wbm_hi), built on the first hop-3 call that needs them; d_wbm_slot[x] = slot or -1
+  int32_t* d_wbm_slot = nullptr;
+  uint32_t* d_wbm_pool = nullptr;  // [slots][wbm_words]
+  int64_t wbm_lo = 0, wbm_hi = 0, wbm_words = 0, wbm_slots = 0;
   // host mirrors used for launch planning (bitmap universe bounds) and the host-built indexes:
   // owned copies (blp_graph_create), or the caller's buffers (blp_graph_create_from_csr, which
   // requires them to outlive the handle)

@@ -40,6 +40,9 @@ struct Hop3Args {
   uint8_t* out_label;
   int64_t cap;
   unsigned long long* counters;  // [0] queue, [1] emitted
+  const int32_t* wbm_slot;       // wedge-row bitmaps (k_hop3_wedge): slot of b or -1; null: none
+  const uint4* wbm_pool;         // [slots][wbm_vecs]
+  int wbm_vecs;
 };
 
 __device__ inline uint64_t mix64(uint64_t z) {
@@ -286,10 +289,17 @@ __global__ __launch_bounds__(HW_BLOCK) void k_hop3_wedge(Hop3Args a, const int64
       int nch = 0;
       if ((int)threadIdx.x < ns) {
         const int b = a.ci[k0 + threadIdx.x];
-        const int64_t ws = wp[b], we = wp[b + 1];
-        s_ws[threadIdx.x] = ws;
-        s_wl[threadIdx.x] = (int)(we - ws);
-        nch = (int)((we - ws + HW_CH - 1) / HW_CH);
+        const int slot = a.wbm_slot ? a.wbm_slot[b] : -1;
+        if (slot >= 0) {  // the row's id set as a bitmap: its words, negative length marks it
+          s_ws[threadIdx.x] = (int64_t)slot * a.wbm_vecs;
+          s_wl[threadIdx.x] = -a.wbm_vecs;
+          nch = (a.wbm_vecs + HW_CH - 1) / HW_CH;
+        } else {
+          const int64_t ws = wp[b], we = wp[b + 1];
+          s_ws[threadIdx.x] = ws;
+          s_wl[threadIdx.x] = (int)(we - ws);
+          nch = (int)((we - ws + HW_CH - 1) / HW_CH);
+        }
       }
       int tot;
       const int ex = hw_exscan(nch, red, &tot);
@@ -301,6 +311,19 @@ __global__ __launch_bounds__(HW_BLOCK) void k_hop3_wedge(Hop3Args a, const int64
         while (hi - lo > 1) {
           const int mid = (lo + hi) >> 1;
           if (s_co[mid] <= item) lo = mid; else hi = mid;
+        }
+        if (s_wl[lo] < 0) {  // a wedge-row bitmap: OR its nonzero words (consecutive: no bank conflicts)
+          const int64_t b0 = s_ws[lo], vb = (int64_t)(item - s_co[lo]) * HW_CH;
+          const int64_t ve = min<int64_t>(vb + HW_CH, -s_wl[lo]);
+          for (int64_t q = vb + lane; q < ve; q += 64) {
+            const uint4 v = a.wbm_pool[b0 + q];
+            uint32_t* d = bm3 + 4 * q;
+            if (v.x) atomicOr(d, v.x);
+            if (v.y) atomicOr(d + 1, v.y);
+            if (v.z) atomicOr(d + 2, v.z);
+            if (v.w) atomicOr(d + 3, v.w);
+          }
+          continue;
         }
         const int64_t row_end = s_ws[lo] + s_wl[lo];
         const int64_t base = s_ws[lo] + (int64_t)(item - s_co[lo]) * HW_CH;
@@ -354,9 +377,91 @@ __global__ __launch_bounds__(HW_BLOCK) void k_hop3_wedge(Hop3Args a, const int64
   }
 }
 
+// Wedge-row bitmaps. A popular business b's wedge row holds |N(z)| ids for each of its
+// members z -- millions at config 2 -- yet only its SET W(b) = N(N(b)) matters for the marks, and
+// that set lives in a range of w3 words (12.5 KB at config 2). Every source reviewing b streamed
+// the whole row (k_hop3_wedge read ~37 GB per call for 0.44 GB of wedge rows). Rows longer than
+// their bitmap are OR-ed once into one bitmap each (this kernel, one workgroup per row); the
+// hop-3 kernel then ORs those words instead. Same set, so the same marks.
+__global__ __launch_bounds__(HW_BLOCK) void k_wbm_fill(const int64_t* __restrict__ wp, const uint4* __restrict__ wedge,
+                                                       const int32_t* __restrict__ rows, int64_t lo3, int64_t span3,
+                                                       int words, uint32_t* __restrict__ pool) {
+  uint32_t* bm = hw_dyn;
+  const int b = rows[blockIdx.x];
+  for (int i = threadIdx.x; i < words; i += HW_BLOCK) bm[i] = 0;
+  __syncthreads();
+  const uint32_t c0u = (uint32_t)lo3, wu = (uint32_t)span3;
+  const int64_t s = wp[b], e = wp[b + 1];
+  for (int64_t q = s + threadIdx.x; q < e; q += 4 * HW_BLOCK) {
+    uint4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = wedge[q + HW_BLOCK * u < e ? q + HW_BLOCK * u : q];  // a repeat ORs nothing new
+    uint32_t rr[16], wd[16];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      rr[4 * u] = v[u].x - c0u;
+      rr[4 * u + 1] = v[u].y - c0u;
+      rr[4 * u + 2] = v[u].z - c0u;
+      rr[4 * u + 3] = v[u].w - c0u;
+    }
+#pragma unroll
+    for (int c = 0; c < 16; ++c) wd[c] = bm[(rr[c] < wu ? rr[c] : 0u) >> 5];
+#pragma unroll
+    for (int c = 0; c < 16; ++c)
+      if (rr[c] < wu && !((wd[c] >> (rr[c] & 31)) & 1u)) atomicOr(&bm[rr[c] >> 5], 1u << (rr[c] & 31));
+  }
+  __syncthreads();
+  uint32_t* dst = pool + (int64_t)blockIdx.x * words;
+  for (int i = threadIdx.x; i < words; i += HW_BLOCK) dst[i] = bm[i];
+}
+
 }  // namespace
 
 using namespace blp;
+
+// Build (or reuse) the graph's wedge-row bitmaps over [lo3, hi3): rows of at least
+// BLP_WBM_MIN_X (default 1) times their bitmap's words, longest first, within BLP_WBM_MB of HBM
+// (default 2048). Enqueued on the graph stream; returns with the fill kernel queued.
+static int ensure_wedge_bitmaps(blp_graph* g, int64_t lo3, int64_t hi3) {
+  const int64_t words = (((hi3 - lo3) + 31) / 32 + 3) / 4 * 4;
+  if (g->wbm_words && g->wbm_lo == lo3 && g->wbm_hi == hi3) return BLP_OK;
+  if (g->d_wbm_slot) (void)hipFree(g->d_wbm_slot);
+  if (g->d_wbm_pool) (void)hipFree(g->d_wbm_pool);
+  g->d_wbm_slot = nullptr;
+  g->d_wbm_pool = nullptr;
+  g->wbm_slots = 0;
+  const double min_x = getenv("BLP_WBM_MIN_X") ? atof(getenv("BLP_WBM_MIN_X")) : 1.0;
+  const int64_t budget = (getenv("BLP_WBM_MB") ? atoll(getenv("BLP_WBM_MB")) : 2048) << 20;
+  std::vector<std::pair<int64_t, int32_t>> rows;  // (ids, b)
+  for (int64_t b = 0; b < g->n; ++b) {
+    const int64_t ids = 4 * (g->h_wp[b + 1] - g->h_wp[b]);
+    if (ids > 0 && (double)ids >= min_x * (double)words) rows.push_back({-ids, (int32_t)b});
+  }
+  std::sort(rows.begin(), rows.end());
+  rows.resize((size_t)std::min<int64_t>((int64_t)rows.size(), budget / (4 * words)));
+  g->wbm_lo = lo3;
+  g->wbm_hi = hi3;
+  g->wbm_words = words;
+  if (rows.empty()) return BLP_OK;
+  std::vector<int32_t> slot((size_t)g->n, -1), order(rows.size());
+  for (size_t i = 0; i < rows.size(); ++i) {
+    slot[rows[i].second] = (int32_t)i;
+    order[i] = rows[i].second;
+  }
+  int32_t* d_rows = nullptr;
+  BLP_HIP(hipMalloc(&g->d_wbm_slot, 4 * (size_t)g->n));
+  BLP_HIP(hipMalloc(&g->d_wbm_pool, 4 * (size_t)words * rows.size()));
+  BLP_HIP(hipMalloc(&d_rows, 4 * rows.size()));
+  BLP_HIP(hipMemcpy(g->d_wbm_slot, slot.data(), 4 * (size_t)g->n, hipMemcpyHostToDevice));
+  BLP_HIP(hipMemcpy(d_rows, order.data(), 4 * order.size(), hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(k_wbm_fill, dim3((unsigned)rows.size()), dim3(HW_BLOCK), 4 * (size_t)words, g->stream,
+                     (const int64_t*)g->d_wp, (const uint4*)g->d_wedge, d_rows, lo3, hi3 - lo3, (int)words, g->d_wbm_pool);
+  BLP_HIP(hipGetLastError());
+  BLP_HIP(hipStreamSynchronize(g->stream));
+  BLP_HIP(hipFree(d_rows));
+  g->wbm_slots = (int64_t)rows.size();
+  return BLP_OK;
+}
 
 extern "C" int blp_hop3_sample(blp_graph* g, const int32_t* src, int64_t n_src, const int32_t* pos_off,
                                const int32_t* pos_y, double rate, uint64_t seed, int32_t* out_x, int32_t* out_y,
@@ -392,8 +497,9 @@ extern "C" int blp_hop3_sample(blp_graph* g, const int32_t* src, int64_t n_src, 
   const bool global = w2 + w3 > H_WORDS || getenv("BLP_HOP3_FORCE_GLOBAL");
   // wedge-row path: every target range disjoint from N(N(x))'s, every b in N(x) holding a
   // wedge row (or no members), and the mark bitmap within LDS (BLP_HOP3_NO_WEDGE: off)
+  const int64_t w3v = (w3 + 3) / 4;  // the mark bitmap in 16-byte vectors (wedge-row bitmaps OR whole vectors)
   bool wedge = g->d_wp && !getenv("BLP_HOP3_NO_WEDGE") && (hi2 <= lo3 || hi3 <= lo2) &&
-               (size_t)4 * w3 + 20480 <= 160 * 1024;
+               (size_t)16 * w3v + 20480 <= 160 * 1024;
   for (int64_t i = 0; wedge && i < n_src; ++i)
     for (int64_t k = rp[src[i]]; k < rp[src[i] + 1] && wedge; ++k) {
       const int32_t b = ci[k];
@@ -456,7 +562,15 @@ extern "C" int blp_hop3_sample(blp_graph* g, const int32_t* src, int64_t n_src, 
   hipEvent_t t0;
   if ((rc = timer_begin(g, K_HOP3, &t0))) return cleanup(), rc;
   if (n_src && wedge) {
-    const size_t dyn = 4 * (size_t)std::max<int64_t>(w3, 1);
+    if (!getenv("BLP_HOP3_NO_WBM")) {
+      if ((rc = ensure_wedge_bitmaps(g, lo3, hi3))) return cleanup(), rc;
+      if (g->wbm_slots) {
+        a.wbm_slot = g->d_wbm_slot;
+        a.wbm_pool = (const uint4*)g->d_wbm_pool;
+        a.wbm_vecs = (int)(g->wbm_words / 4);
+      }
+    }
+    const size_t dyn = 16 * (size_t)std::max<int64_t>(w3v, 1);
     int per_cu = 1;
     if ((rc = hip(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_hop3_wedge, HW_BLOCK, dyn), "occupancy")))
       return rc;

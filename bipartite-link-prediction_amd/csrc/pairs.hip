@@ -412,6 +412,93 @@ __global__ __launch_bounds__(GB_BLOCK) void k_item_write(const int64_t* __restri
   }
 }
 
+// The same write with the item's pairs first ordered by key in LDS (their tmp indices), so each
+// key's run goes out as consecutive positions: the grouped metadata (16-20 B per pair) leaves in
+// whole runs instead of one scattered 4-8 B store per array per pair (k_item_write<64>: 533 us
+// in-step at config 2). KEYS <= 1024 (the three key tables and the index stage fit in 28 KB).
+template <int KEYS>
+__global__ __launch_bounds__(GB_BLOCK) void k_item_write_runs(const int64_t* __restrict__ rp, const int4* __restrict__ tmp,
+                                                              const int32_t* __restrict__ item_b,
+                                                              const int32_t* __restrict__ item_s,
+                                                              const int32_t* __restrict__ item_e,
+                                                              const int32_t* __restrict__ n_items, int32_t xlo, int lognb,
+                                                              const int32_t* __restrict__ off, int32_t* __restrict__ fill,
+                                                              int32_t* __restrict__ g_out, int64_t* __restrict__ g_yb,
+                                                              int32_t* __restrict__ g_yl, int32_t* __restrict__ g_y) {
+  static_assert(KEYS <= 1024, "key tables in LDS");
+  constexpr int PER = KEYS >= GB_BLOCK ? KEYS / GB_BLOCK : 1;
+  __shared__ int h[KEYS];     // counts, then local cursors
+  __shared__ int lofs[KEYS];  // the key's first local position
+  __shared__ int gbase[KEYS]; // ... and its first global position
+  __shared__ int sidx[GI_PAIRS];
+  __shared__ int red[GB_BLOCK / 64];
+  const int i = blockIdx.x;
+  if (i >= *n_items) return;
+  const int b = item_b[i], s = item_s[i], e = item_e[i];
+  item_hist<KEYS>(tmp, s, e, xlo, lognb, h);
+  int v = 0;
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const int j = (int)threadIdx.x * PER + q;
+    v += j < KEYS ? h[j] : 0;
+  }
+  int tot;
+  int o = block_exscan_i<GB_BLOCK>(v, red, &tot);
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const int j = (int)threadIdx.x * PER + q;
+    if (j < KEYS) {
+      const int c = h[j];
+      const int vv = b + (j << lognb);
+      lofs[j] = o;
+      gbase[j] = c ? off[xlo + vv] + atomicAdd(&fill[vv], c) : 0;
+      h[j] = o;
+      o += c;
+    }
+  }
+  __syncthreads();
+  constexpr int U = 4;
+  for (int kr = s; kr < e; kr += U * GB_BLOCK) {  // key order: each pair's tmp index at its local slot
+    int yv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = kr + u * GB_BLOCK + (int)threadIdx.x;
+      yv[u] = k < e ? tmp[k].y : INT32_MIN;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (yv[u] != INT32_MIN) sidx[atomicAdd(&h[(yv[u] - xlo) >> lognb], 1)] = kr + u * GB_BLOCK + (int)threadIdx.x;
+  }
+  __syncthreads();
+  const int n = e - s;
+  for (int pr = 0; pr < n; pr += U * GB_BLOCK) {  // consecutive local slots -> consecutive global positions
+    int4 t[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int p = pr + u * GB_BLOCK + (int)threadIdx.x;
+      t[u] = p < n ? tmp[sidx[p]] : make_int4(-1, xlo, 0, 0);
+    }
+    int64_t st[U], en[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      st[u] = rp[t[u].z];
+      en[u] = rp[t[u].z + 1];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (t[u].x >= 0) {
+        const int p = pr + u * GB_BLOCK + (int)threadIdx.x;
+        const int j = (t[u].y - xlo) >> lognb;
+        const int pos = gbase[j] + (p - lofs[j]);
+        g_out[pos] = t[u].x;
+        g_yb[pos] = st[u];
+        g_yl[pos] = (int32_t)(en[u] - st[u]);
+        if (g_y) g_y[pos] = t[u].z;
+      }
+    }
+  }
+}
+
 // active sources = ids with cnt > 0, ascending (tile counts -> scan -> writes)
 __global__ __launch_bounds__(SCAN_BLOCK) void k_nz_count(const int32_t* __restrict__ cnt, int64_t n,
                                                          int32_t* __restrict__ tile_cnt) {
@@ -3229,8 +3316,13 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   hipLaunchKernelGGL(k_scan_mid, dim3(1), dim3(SCAN_BLOCK), 0, b->stream, tx2, tx, &b->d_misc->n_active);          \
   hipLaunchKernelGGL(k_nz_write, dim3((unsigned)tx), dim3(SCAN_BLOCK), 0, b->stream, cnt + b->xlo, b->xspan, tx2,  \
                      b->xlo, b->active.as<int32_t>());                                                              \
-  hipLaunchKernelGGL(k_item_write<K>, dim3((unsigned)ub), dim3(GB_BLOCK), 0, b->stream, g->d_rp, tmp, it_b, it_s,  \
-                     it_e, &b->d_misc->n_items, b->xlo, b->shift, off, fill, b->d_gout, b->d_gyb, b->d_gyl, b->d_gy)
+  if (K <= 1024 && !getenv("BLP_ITEM_SCATTER"))                                                                      \
+    hipLaunchKernelGGL(k_item_write_runs<(K <= 1024 ? K : 1024)>, dim3((unsigned)ub), dim3(GB_BLOCK), 0, b->stream,  \
+                       g->d_rp, tmp, it_b, it_s, it_e, &b->d_misc->n_items, b->xlo, b->shift, off, fill, b->d_gout,  \
+                       b->d_gyb, b->d_gyl, b->d_gy);                                                                  \
+  else                                                                                                                \
+    hipLaunchKernelGGL(k_item_write<K>, dim3((unsigned)ub), dim3(GB_BLOCK), 0, b->stream, g->d_rp, tmp, it_b, it_s,  \
+                       it_e, &b->d_misc->n_items, b->xlo, b->shift, off, fill, b->d_gout, b->d_gyb, b->d_gyl, b->d_gy)
       if (keys <= 64) {  // 272 bytes of LDS: fits beside a 160 KiB large-scorer workgroup
         BLP_ITEM_LAUNCH(64);
       } else if (keys <= 256) {

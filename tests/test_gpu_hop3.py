@@ -38,11 +38,18 @@ def test_hop3_matches_reference_fixture(gpu):
         assert got[u] == {b: l for b, l in ex[u].items()}
 
 
-@pytest.mark.parametrize("seed,mode", [(0, "wedge"), (1, "wedge"), (0, "lds"), (1, "lds"), (0, "hbm")])
+@pytest.mark.parametrize("seed,mode", [(0, "wedge"), (1, "wedge"), (0, "wedge_rows"), (0, "wedge_bitmaps"),
+                                       (1, "wedge_bitmaps"), (0, "lds"), (1, "lds"), (0, "hbm")])
 def test_hop3_sets_vs_oracle(gpu, seed, mode, monkeypatch):
-    """wedge: marks from the graph's wedge rows (default on review graphs); lds: H2 bitmap then
-    N(H2) row walks in LDS; hbm: the same in per-workgroup HBM bitmaps (configs 4/5)."""
-    if mode != "wedge":
+    """wedge: marks from the graph's wedge rows (default on review graphs), rows longer than
+    their set's bitmap OR-ed as wedge-row bitmaps; wedge_rows: no bitmaps; wedge_bitmaps: every
+    row through its bitmap; lds: H2 bitmap then N(H2) row walks in LDS; hbm: the same in
+    per-workgroup HBM bitmaps (configs 4/5)."""
+    if mode == "wedge_rows":
+        monkeypatch.setenv("BLP_HOP3_NO_WBM", "1")
+    if mode == "wedge_bitmaps":
+        monkeypatch.setenv("BLP_WBM_MIN_X", "0")
+    if not mode.startswith("wedge"):
         monkeypatch.setenv("BLP_HOP3_NO_WEDGE", "1")
     if mode == "hbm":
         monkeypatch.setenv("BLP_HOP3_FORCE_GLOBAL", "1")
@@ -138,7 +145,11 @@ def test_hop3_wedge_and_row_walk_agree(gpu, long_rows, monkeypatch):
     pos_off = np.arange(0, 2 * len(src) + 1, 2, dtype=np.int32)
     pos_y = rng.integers(nu, G.n, 2 * len(src)).astype(np.int32)
     got = G.hop3_sample(src, pos_off, pos_y, rate=0.05, seed=4)
+    sub = G.hop3_sample(src[::3], pos_off[:len(src[::3]) + 1], pos_y, rate=0.05, seed=4)  # bitmaps reused or rebuilt
     monkeypatch.setenv("BLP_HOP3_NO_WEDGE", "1")
+    ref_sub = G.hop3_sample(src[::3], pos_off[:len(src[::3]) + 1], pos_y, rate=0.05, seed=4)
+    for p, q in zip(sub, ref_sub):
+        np.testing.assert_array_equal(p, q)
     ref = G.hop3_sample(src, pos_off, pos_y, rate=0.05, seed=4)
     for p, q in zip(got, ref):
         np.testing.assert_array_equal(p, q)
