@@ -7,7 +7,10 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 #include <climits>
+#include <cstdio>
+#include <cstdlib>
 #include <thread>
 #include <vector>
 
@@ -17,7 +20,30 @@ namespace {
 
 struct Slice {
   std::vector<int64_t> a, b;
+  int64_t mn = INT64_MAX, mx = INT64_MIN;  // over both columns
 };
+
+// "digits ws digits [ws] \n" (the reference's graph.txt line, c0 = 0, c1 = 1) in one pass;
+// false (p untouched) for anything else, which then goes through parse_line.
+inline bool fast_line(const char*& p, const char* end, int64_t* va, int64_t* vb) {
+  const char* q = p;
+  if (q >= end || *q < '0' || *q > '9') return false;
+  int64_t x = 0;
+  int nd = 0;
+  while (q < end && *q >= '0' && *q <= '9' && nd < 18) x = x * 10 + (*q++ - '0'), ++nd;
+  if (q >= end || (*q != ' ' && *q != '\t')) return false;
+  while (q < end && (*q == ' ' || *q == '\t')) ++q;
+  if (q >= end || *q < '0' || *q > '9') return false;
+  int64_t y = 0;
+  nd = 0;
+  while (q < end && *q >= '0' && *q <= '9' && nd < 18) y = y * 10 + (*q++ - '0'), ++nd;
+  while (q < end && (*q == ' ' || *q == '\t' || *q == '\r')) ++q;
+  if (q < end && *q != '\n') return false;
+  *va = x;
+  *vb = y;
+  p = q + 1;
+  return true;
+}
 
 inline bool is_ws(char c) { return c == ' ' || c == '\t' || c == '\r' || c == '\v' || c == '\f'; }
 
@@ -75,7 +101,9 @@ int parse_slices(const char* path, int c0, int c1, std::vector<Slice>& sl) {
   const size_t size = (size_t)st.st_size;
   const char* data = nullptr;
   if (size) {
-    data = (const char*)mmap(nullptr, size, PROT_READ, MAP_PRIVATE, fd, 0);
+    // populated up front: 16 threads faulting the same mapping page by page serialise on the
+    // process's mmap lock
+    data = (const char*)mmap(nullptr, size, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
     if (data == MAP_FAILED) {
       close(fd);
       return fail(BLP_E_ARG, "blp_edges_parse: mmap failed");
@@ -94,20 +122,32 @@ int parse_slices(const char* path, int c0, int c1, std::vector<Slice>& sl) {
   auto work = [&](unsigned t) {
     const char* p = data + cut[t];
     const char* end = data + cut[t + 1];
-    sl[t].a.reserve((cut[t + 1] - cut[t]) / 12 + 16);
-    sl[t].b.reserve((cut[t + 1] - cut[t]) / 12 + 16);
+    Slice& S = sl[t];
+    S.a.reserve((cut[t + 1] - cut[t]) / 12 + 16);
+    S.b.reserve((cut[t + 1] - cut[t]) / 12 + 16);
+    int64_t mn = INT64_MAX, mx = INT64_MIN;
+    const bool fast = c0 == 0 && c1 == 1;
     while (p < end) {
+      int64_t va, vb;
+      if (fast && fast_line(p, end, &va, &vb)) {
+        S.a.push_back(va);
+        S.b.push_back(vb);
+        mn = std::min(mn, std::min(va, vb));
+        mx = std::max(mx, std::max(va, vb));
+        continue;
+      }
       const char* e = p;
       while (e < end && *e != '\n') ++e;
-      if (e > p && *p != '#') {
-        int64_t va, vb;
-        if (parse_line(p, e, c0, c1, &va, &vb)) {
-          sl[t].a.push_back(va);
-          sl[t].b.push_back(vb);
-        }
+      if (e > p && *p != '#' && parse_line(p, e, c0, c1, &va, &vb)) {
+        S.a.push_back(va);
+        S.b.push_back(vb);
+        mn = std::min(mn, std::min(va, vb));
+        mx = std::max(mx, std::max(va, vb));
       }
       p = e + 1;
     }
+    S.mn = mn;
+    S.mx = mx;
   };
   std::vector<std::thread> th;
   for (unsigned t = 1; t < nt; ++t) th.emplace_back(work, t);
@@ -167,6 +207,16 @@ extern "C" int blp_edges_parse(const char* path, int c0, int c1, int64_t* a, int
 extern "C" int blp_edges_load(const char* path, int c0, int c1, blp_edges** out) {
   BLP_CHECK(out, BLP_E_ARG, "blp_edges_load: null out");
   auto* e = new blp_edges();
+  const bool prof = getenv("BLP_INGEST_PROF") != nullptr;
+  auto now = []() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+  double tp = now();
+  auto stamp = [&](const char* what) {
+    if (prof) {
+      const double t = now();
+      fprintf(stderr, "blp_edges_load %s %.4f s\n", what, t - tp);
+      tp = t;
+    }
+  };
   if (int rc = parse_slices(path, c0, c1, e->sl)) {
     delete e;
     return rc;
@@ -176,18 +226,13 @@ extern "C" int blp_edges_load(const char* path, int c0, int c1, blp_edges** out)
   for (unsigned t = 0; t < nt; ++t) base[t + 1] = base[t] + (int64_t)e->sl[t].a.size();
   e->m = base[nt];
   if (e->m) {
-    std::vector<int64_t> mn(nt, INT64_MAX), mx(nt, INT64_MIN);
     std::vector<std::thread> th;
-    auto mm = [&](unsigned t) {
-      for (size_t i = 0; i < e->sl[t].a.size(); ++i) {
-        mn[t] = std::min({mn[t], e->sl[t].a[i], e->sl[t].b[i]});
-        mx[t] = std::max({mx[t], e->sl[t].a[i], e->sl[t].b[i]});
-      }
-    };
-    for (unsigned t = 1; t < nt; ++t) th.emplace_back(mm, t);
-    mm(0);
-    for (auto& x : th) x.join();
-    const int64_t lo = *std::min_element(mn.begin(), mn.end()), hi = *std::max_element(mx.begin(), mx.end());
+    stamp("parse");
+    int64_t lo = INT64_MAX, hi = INT64_MIN;  // tracked by the parse
+    for (const Slice& x : e->sl) {
+      lo = std::min(lo, x.mn);
+      hi = std::max(hi, x.mx);
+    }
     const int64_t span = hi - lo + 1;
     if (span > 0 && span <= std::max<int64_t>(4 * e->m, 1 << 20) && span < (int64_t(1) << 31)) {
       // presence per column (byte flags: concurrent stores of the same value only)
@@ -202,6 +247,7 @@ extern "C" int blp_edges_load(const char* path, int c0, int c1, blp_edges** out)
       for (unsigned t = 1; t < nt; ++t) th.emplace_back(mark, t);
       mark(0);
       for (auto& x : th) x.join();
+      stamp("mark");
       // ranks: column-0 ids first, then column-1-only ids, each ascending (block counts + prefix)
       const unsigned nb = n_threads();
       std::vector<int64_t> c0n(nb + 1, 0), c1n(nb + 1, 0);
@@ -237,6 +283,7 @@ extern "C" int blp_edges_load(const char* path, int c0, int c1, blp_edges** out)
           }
         }
       });
+      stamp("map");
     }
   }
   *out = e;

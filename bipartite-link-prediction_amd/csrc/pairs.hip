@@ -354,14 +354,16 @@ __global__ __launch_bounds__(GB_BLOCK) void k_item_count(const int4* __restrict_
                                                          const int32_t* __restrict__ item_s,
                                                          const int32_t* __restrict__ item_e,
                                                          const int32_t* __restrict__ n_items, int32_t xlo, int lognb,
-                                                         int32_t* __restrict__ cnt) {
+                                                         int32_t* __restrict__ cnt, int32_t* __restrict__ ih) {
   __shared__ int h[KEYS];
   const int i = blockIdx.x;
   if (i >= *n_items) return;  // uniform: the grid is the host's upper bound on items
   const int b = item_b[i];
   item_hist<KEYS>(tmp, item_s[i], item_e[i], xlo, lognb, h);
-  for (int j = threadIdx.x; j < KEYS; j += GB_BLOCK)
+  for (int j = threadIdx.x; j < KEYS; j += GB_BLOCK) {
     if (h[j]) atomicAdd(&cnt[xlo + b + (j << lognb)], h[j]);
+    if (ih) ih[(int64_t)i * KEYS + j] = h[j];  // the item's histogram, for k_item_write_runs
+  }
 }
 
 template <int KEYS>
@@ -412,35 +414,39 @@ __global__ __launch_bounds__(GB_BLOCK) void k_item_write(const int64_t* __restri
   }
 }
 
-// The same write with the item's pairs first ordered by key in LDS (their tmp indices), so each
-// key's run goes out as consecutive positions: the grouped metadata (16-20 B per pair) leaves in
-// whole runs instead of one scattered 4-8 B store per array per pair (k_item_write<64>: 533 us
-// in-step at config 2). KEYS <= 1024 (the three key tables and the index stage fit in 28 KB).
+// The same write with the item's pairs first ordered by key in LDS, so each key's run goes out
+// as consecutive positions: the grouped metadata (16-20 B per pair) leaves in whole runs instead
+// of one scattered 4-8 B store per array per pair (k_item_write<64>: 533 us in-step at config 2).
+// The item's histogram comes from k_item_count (ih) and its records are read ONCE into an LDS
+// stage in key order (k_item_write re-reads the item three times). KEYS <= 1024: 64 KiB of
+// stage + 12 KiB of key tables.
 template <int KEYS>
 __global__ __launch_bounds__(GB_BLOCK) void k_item_write_runs(const int64_t* __restrict__ rp, const int4* __restrict__ tmp,
                                                               const int32_t* __restrict__ item_b,
                                                               const int32_t* __restrict__ item_s,
                                                               const int32_t* __restrict__ item_e,
                                                               const int32_t* __restrict__ n_items, int32_t xlo, int lognb,
+                                                              const int32_t* __restrict__ ih,
                                                               const int32_t* __restrict__ off, int32_t* __restrict__ fill,
                                                               int32_t* __restrict__ g_out, int64_t* __restrict__ g_yb,
                                                               int32_t* __restrict__ g_yl, int32_t* __restrict__ g_y) {
   static_assert(KEYS <= 1024, "key tables in LDS");
   constexpr int PER = KEYS >= GB_BLOCK ? KEYS / GB_BLOCK : 1;
-  __shared__ int h[KEYS];     // counts, then local cursors
-  __shared__ int lofs[KEYS];  // the key's first local position
-  __shared__ int gbase[KEYS]; // ... and its first global position
-  __shared__ int sidx[GI_PAIRS];
+  __shared__ int h[KEYS];      // local cursors
+  __shared__ int lofs[KEYS];   // the key's first local position
+  __shared__ int gbase[KEYS];  // ... and its first global position
+  __shared__ int4 stage[GI_PAIRS];
   __shared__ int red[GB_BLOCK / 64];
   const int i = blockIdx.x;
   if (i >= *n_items) return;
   const int b = item_b[i], s = item_s[i], e = item_e[i];
-  item_hist<KEYS>(tmp, s, e, xlo, lognb, h);
+  int c[PER];
   int v = 0;
 #pragma unroll
   for (int q = 0; q < PER; ++q) {
     const int j = (int)threadIdx.x * PER + q;
-    v += j < KEYS ? h[j] : 0;
+    c[q] = j < KEYS ? ih[(int64_t)i * KEYS + j] : 0;
+    v += c[q];
   }
   int tot;
   int o = block_exscan_i<GB_BLOCK>(v, red, &tot);
@@ -448,26 +454,25 @@ __global__ __launch_bounds__(GB_BLOCK) void k_item_write_runs(const int64_t* __r
   for (int q = 0; q < PER; ++q) {
     const int j = (int)threadIdx.x * PER + q;
     if (j < KEYS) {
-      const int c = h[j];
       const int vv = b + (j << lognb);
       lofs[j] = o;
-      gbase[j] = c ? off[xlo + vv] + atomicAdd(&fill[vv], c) : 0;
+      gbase[j] = c[q] ? off[xlo + vv] + atomicAdd(&fill[vv], c[q]) : 0;
       h[j] = o;
-      o += c;
+      o += c[q];
     }
   }
   __syncthreads();
   constexpr int U = 4;
-  for (int kr = s; kr < e; kr += U * GB_BLOCK) {  // key order: each pair's tmp index at its local slot
-    int yv[U];
+  for (int kr = s; kr < e; kr += U * GB_BLOCK) {  // the item's records, staged in key order
+    int4 t[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int k = kr + u * GB_BLOCK + (int)threadIdx.x;
-      yv[u] = k < e ? tmp[k].y : INT32_MIN;
+      t[u] = k < e ? tmp[k] : make_int4(-1, xlo, 0, 0);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      if (yv[u] != INT32_MIN) sidx[atomicAdd(&h[(yv[u] - xlo) >> lognb], 1)] = kr + u * GB_BLOCK + (int)threadIdx.x;
+      if (t[u].x >= 0) stage[atomicAdd(&h[(t[u].y - xlo) >> lognb], 1)] = t[u];
   }
   __syncthreads();
   const int n = e - s;
@@ -476,7 +481,7 @@ __global__ __launch_bounds__(GB_BLOCK) void k_item_write_runs(const int64_t* __r
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int p = pr + u * GB_BLOCK + (int)threadIdx.x;
-      t[u] = p < n ? tmp[sidx[p]] : make_int4(-1, xlo, 0, 0);
+      t[u] = p < n ? stage[p] : make_int4(-1, xlo, 0, 0);
     }
     int64_t st[U], en[U];
 #pragma unroll
@@ -3260,8 +3265,9 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   if ((rc = b->off.reserve(4 * (n + 1)))) return rc;
   if ((rc = b->active.reserve(4 * (n + 1)))) return rc;
   // scratch: hist | hoff | tiles | bucket_active | abase | tmp [| fill | item table | id-range tiles]
-  const int64_t items_ints = b->items ? b->xspan + 3 * ((np + GI_PAIRS - 1) / GI_PAIRS + b->nb) +
-                                            2 * ((b->xspan + SCAN_TILE - 1) / SCAN_TILE + 1)
+  const int64_t items_ub = (np + GI_PAIRS - 1) / GI_PAIRS + b->nb;
+  const int64_t items_ints = b->items ? b->xspan + 3 * items_ub + 2 * ((b->xspan + SCAN_TILE - 1) / SCAN_TILE + 1) +
+                                            1024 * items_ub
                                       : 0;
   const int64_t sc_ints = 2 * nh + std::max(tiles_h, tiles_b) + 1 + 2 * (int64_t)b->nb + 4 * np + items_ints;
   if ((rc = b->scratch.reserve(4 * (sc_ints + 16)))) return rc;
@@ -3305,9 +3311,11 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
       hipLaunchKernelGGL(k_item_plan, dim3(1), dim3(1024), 0, b->stream, hoff, b->nblk, b->nb, np, it_b, it_s, it_e,
                          &b->d_misc->n_items);
       const int64_t keys = (b->xspan + b->nb - 1) >> b->shift;
+      const bool runs_w = keys <= 1024 && !getenv("BLP_ITEM_SCATTER");
+      int32_t* ih = tx2 + tx + 1;  // [ub][K] item histograms (runs_w)
 #define BLP_ITEM_LAUNCH(K)                                                                                         \
   hipLaunchKernelGGL(k_item_count<K>, dim3((unsigned)ub), dim3(GB_BLOCK), 0, b->stream, tmp, it_b, it_s, it_e,     \
-                     &b->d_misc->n_items, b->xlo, b->shift, cnt);                                                   \
+                     &b->d_misc->n_items, b->xlo, b->shift, cnt, runs_w ? ih : nullptr);                           \
   hipLaunchKernelGGL(k_scan_sum, dim3((unsigned)tx), dim3(SCAN_BLOCK), 0, b->stream, cnt + b->xlo, b->xspan, tx1); \
   hipLaunchKernelGGL(k_scan_mid, dim3(1), dim3(SCAN_BLOCK), 0, b->stream, tx1, tx, (int32_t*)nullptr);             \
   hipLaunchKernelGGL(k_scan_out, dim3((unsigned)tx), dim3(SCAN_BLOCK), 0, b->stream, cnt + b->xlo, b->xspan, tx1,  \
@@ -3316,10 +3324,10 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   hipLaunchKernelGGL(k_scan_mid, dim3(1), dim3(SCAN_BLOCK), 0, b->stream, tx2, tx, &b->d_misc->n_active);          \
   hipLaunchKernelGGL(k_nz_write, dim3((unsigned)tx), dim3(SCAN_BLOCK), 0, b->stream, cnt + b->xlo, b->xspan, tx2,  \
                      b->xlo, b->active.as<int32_t>());                                                              \
-  if (K <= 1024 && !getenv("BLP_ITEM_SCATTER"))                                                                      \
+  if (runs_w)                                                                                                         \
     hipLaunchKernelGGL(k_item_write_runs<(K <= 1024 ? K : 1024)>, dim3((unsigned)ub), dim3(GB_BLOCK), 0, b->stream,  \
-                       g->d_rp, tmp, it_b, it_s, it_e, &b->d_misc->n_items, b->xlo, b->shift, off, fill, b->d_gout,  \
-                       b->d_gyb, b->d_gyl, b->d_gy);                                                                  \
+                       g->d_rp, tmp, it_b, it_s, it_e, &b->d_misc->n_items, b->xlo, b->shift, ih, off, fill,         \
+                       b->d_gout, b->d_gyb, b->d_gyl, b->d_gy);                                                       \
   else                                                                                                                \
     hipLaunchKernelGGL(k_item_write<K>, dim3((unsigned)ub), dim3(GB_BLOCK), 0, b->stream, g->d_rp, tmp, it_b, it_s,  \
                        it_e, &b->d_misc->n_items, b->xlo, b->shift, off, fill, b->d_gout, b->d_gyb, b->d_gyl, b->d_gy)

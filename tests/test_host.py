@@ -38,6 +38,19 @@ def test_edge_list_parser_matches_snap_text_rules(tmp_path):
         a, b = blp.parse_edge_list(os.path.join(GOLDEN, case, "graph.txt"))
         ra, rb = read_edges(os.path.join(GOLDEN, case, "graph.txt"))
         assert a.tolist() == ra.tolist() and b.tolist() == rb.tolist()
+    # > 1 MiB (threaded slices): the one-pass "digits ws digits" lines mixed with every other
+    # shape the SNAP rules accept or skip (CRLF, tabs, extra columns, signs, comments, blanks)
+    rng = np.random.default_rng(9)
+    shapes = ["%d %d\n", "%d\t%d\r\n", "%d  %d extra\n", "-%d +%d\n", "  %d %d\n", "%d\t%d \t\n", "# %d %d\n", "%d\n\n"]
+    lines = []
+    for k in rng.integers(0, len(shapes), 200000):
+        x, y = rng.integers(0, 10**9, 2)
+        lines.append(shapes[k] % ((x,) if shapes[k] == "%d\n\n" else (x, y)))
+    q = tmp_path / "big.txt"
+    q.write_text("".join(lines) + "12 34")  # last line without a newline
+    a, b = blp.parse_edge_list(str(q))
+    ra, rb = read_edges(str(q))
+    assert len(ra) > 100000 and a.tolist() == ra.tolist() and b.tolist() == rb.tolist()
 
 
 @pytest.mark.parametrize("case", SIM_CASES + ["hop3"])
