@@ -21,7 +21,7 @@ q() {  # name, args...
   timeout -k 10 600 python -u bench.py --no-cpu-baseline "$@" > gpurun_out/e11_$n.json 2> gpurun_out/e11_$n.err || { tail -20 gpurun_out/e11_$n.err; return 1; }
   python -c "import json;d=json.load(open('gpurun_out/e11_$n.json'));print('$n', round(d['ms_per_step'],3), d.get('kernels_ms'))"
 }
-q c2 --steps 20 --warmup 3 || exit 1
+q c2bench --steps 20 --warmup 3 || exit 1
 BLP_GROUP_BUCKETS=1 q c2_buckets --steps 20 --warmup 3 --no-parity || exit 1
 q c2_user --steps 20 --warmup 3 --no-parity --sides user || exit 1
 BLP_SPLIT=2 BLP_SPLIT_BIG=0 q c2_user_split2 --steps 20 --warmup 3 --no-parity --sides user || exit 1
