@@ -475,6 +475,7 @@ def run_topk(args):
     pairs = int(ncand.sum())
     h2_sum, push_sum = T.stats(3)[1], T.stats(4)[1]
     hash_src, direct_src = T.stats(1)[1], T.stats(2)[1]
+    pushed, dense_adds = T.stats(6)[1], T.stats(7)[1]
     byts = topk_alg_bytes(G, src, h2_sum, push_sum, args.topk, bin(mask).count("1"))
     out = {
         "metric": METRIC, "value": dist.sum(pairs) / t_max, "unit": "pairs/s", "n_gpus": dist.world,
@@ -489,7 +490,8 @@ def run_topk(args):
         "roofline": {"bound": "hbm", "achieved": byts / kern_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": byts / kern_s / 1e9 / HBM_PEAK_GBS, "kernel": "k_topk", "kernel_ms": 1e3 * kern_s,
                      "alg_bytes_per_launch": byts, **pmc_fields("k_topk", "r*_topk_*.json", kern_s)},
-        "work": {"sum_h2": h2_sum, "sum_push": push_sum, "aa_hash_sources": hash_src, "aa_direct_sources": direct_src},
+        "work": {"sum_h2": h2_sum, "sum_push": push_sum, "pushed": pushed, "dense_target_adds": dense_adds,
+                 "aa_hash_sources": hash_src, "aa_direct_sources": direct_src},
     }
     if dist.rank == 0 and not args.no_parity and mask == blp.JACCARD | blp.ADAMIC:
         cols_j, sc_j, _ = T.fetch("jaccard")

@@ -24,6 +24,18 @@
 // arithmetic, blp_internal.h, so the values are bit-identical to blp_score_pairs). When the
 // candidates do not fit, the source falls back to chunked direct accumulation. AA selection
 // keys are the bits of the correctly rounded double (monotone for non-negative doubles).
+//
+// Dense wedge counts (hot targets). On a Zipf review graph the members of the most popular
+// targets carry most of the push volume (config 3: the ~100 most reviewed businesses, ~85 % of
+// 10.3G pushes per run). For each such target b (a prefix of the degree order) the counts of ALL
+// its members, C_b[t] = |N(b) ∩ N(t)|, and their fused AA words are built once at create
+// (k_tk_dense_fill), with N(b) as a bitmap over the sources. A source x whose N'(x) starts with
+// hot targets b_0 < b_1 < ... (address order) adds C_{b_i} word by word instead of walking N(b_i):
+// first the members of b_i already counted through an earlier b_j are subtracted (N(b_i) ∩
+// ∪_{j<i} N(b_j), from the bitmaps), then C_{b_i} is added, then x's own row is subtracted. Every
+// intermediate count is a count of distinct users reviewing t, so the tiered counters never
+// overflow, and the result is the ownership walk's exactly: a member of a hot b_i is owned by the
+// first hot target that holds it, and the walk of the other targets skips it as before.
 #include <algorithm>
 #include <cmath>
 #include <climits>
@@ -97,6 +109,13 @@ struct TkArgs {
   unsigned long long* counters;  // [0] queue, [1] AA hash path, [2] AA direct path, [3] sum |H2|, [4] sum of |N(w)| over H2, [5] AA fused path
   int64_t acc_words;  // counter words in use (<= TK_ACC_WORDS; test knob BLP_TOPK_ACC_WORDS)
   int64_t pci_len, x2_len;  // entries of pci / x2 including their padding (BLP_DEBUG bounds)
+  // dense wedge counts of the hot targets p < dw_n (single counter chunk; see the header)
+  const uint32_t* dw_cv;            // [dw_n][dw_words] packed counts of all members of N(b)
+  const unsigned long long* dw_ca;  // [dw_n][2 H] their fused AA words (or null)
+  uint32_t* dw_bm;                  // [dw_n][dw_bmw] N(b) over the sources (bit w - slo)
+  long long* dw_info;               // [dw_n][2] |N(b)|, sum of |N(w)| over w in N(b)
+  int dw_n, dw_max;                 // hot targets; at most dw_max of them per source
+  int64_t dw_words, dw_bmw, slo;
 };
 
 // BLP_DEBUG builds (make debug -> libblp_debug.so): every LDS index and every row read of the
@@ -118,7 +137,8 @@ __device__ inline bool tk_ok(bool ok, int site, long long v, long long bound) {
 #define TK_OK(cond, site, v, bound) ((void)(v), true)
 #endif
 // sites: 1 acc_add, 2 acc_get, 3 acc_clear, 4 fused AA word, 5 hash AA word, 6 direct AA word,
-// 7 segment index, 8 16-byte row read, 9 row entry read, 10 selection slot, 11 hash probe length
+// 7 segment index, 8 16-byte row read, 9 row entry read, 10 selection slot, 11 hash probe length,
+// 12 dense: hot target index, 13 dense: member bitmap word, 14 dense: member row read
 
 struct TkShared {
   uint32_t acc[TK_ACC_WORDS];
@@ -133,6 +153,7 @@ struct TkShared {
   unsigned long long thr_key;
   int thr_col, have_thr, n, item;
   int nv[3];
+  int nd;  // hot targets of this source handled by dense_pass
 };
 
 __device__ inline uint32_t filt_bit(int32_t e) { return ((uint32_t)e * 2654435761u) >> 20; }
@@ -179,6 +200,17 @@ __device__ inline void aa_push2(unsigned long long* w2, int64_t t, unsigned long
   atomicAdd(&w2[2 * t + 1], W >> 32);
 }
 
+// removal of one count / one AA term (the inverse of acc_add / aa_push2: wrapping adds of the
+// negation; the removed contribution is always present, so no tier field borrows)
+__device__ inline void acc_sub(const TkArgs& a, uint32_t* acc, int64_t e) {
+  if (TK_OK(e >= 0 && (e >> 2) < a.acc_words, 1, e, a.acc_words)) atomicAdd(&acc[e >> 2], 0u - (1u << ((e & 3) << 3)));
+}
+
+__device__ inline void aa_sub2(unsigned long long* w2, int64_t t, unsigned long long W) {
+  atomicAdd(&w2[2 * t], 0ull - W);
+  atomicAdd(&w2[2 * t + 1], 0ull - (W >> 32));
+}
+
 // selection key of an exact AA word pair: the bits of the correctly rounded double
 __device__ inline unsigned long long aa_key(const unsigned long long* w2, int64_t t) {
   return (unsigned long long)__double_as_longlong(blp::aa_value(w2[2 * t], w2[2 * t + 1]));
@@ -217,7 +249,7 @@ __device__ inline bool in_row_x(const TkShared& s, const int32_t* rowx, int du, 
 template <int MODE>
 __device__ __attribute__((always_inline)) long long push_pass(const TkArgs& a, TkShared& s, int x, int64_t xb, int du, const int32_t* rowx,
                                const TkChunk& c, uint32_t thr, int64_t d0, int64_t d1, bool count_h2,
-                               long long* pushed = nullptr) {
+                               long long* pushed = nullptr, int32_t a_dense = 0) {
   long long h2 = 0, npush = 0;
   unsigned long long* acc64 = reinterpret_cast<unsigned long long*>(s.acc);
   const int tid = threadIdx.x;
@@ -231,6 +263,7 @@ __device__ __attribute__((always_inline)) long long push_pass(const TkArgs& a, T
       len = a.rp[b + 1] - rs;
       s.seg_rs[tid] = rs;
       s.seg_p[tid] = a.paddr[b - a.tlo];
+      if (s.seg_p[tid] < a_dense) len = 0;  // a hot target already counted by dense_pass
       if (a.x2) {  // position of x in N(b') (sorted): its own wedge is skipped
         int64_t lo = rs, hi = rs + len;
         while (lo < hi) {
@@ -696,6 +729,122 @@ __device__ unsigned long long g_tkprof[16];
 #define TKP_FLUSH
 #endif
 
+// Dense counts of the hot prefix of N'(x) (single counter chunk, a0 = 0; header comment). h2 /
+// np / fix receive this thread's share of |H2(x)|, of sum_{w in H2(x)} |N(w)| and of the rows
+// pushed as corrections. Returns the address bound below which the walk skips targets.
+template <bool FUSED>
+__device__ __attribute__((always_inline)) int32_t dense_pass(const TkArgs& a, TkShared& s, int x, int du,
+                                                             const int32_t* rowx, long long& h2, long long& np,
+                                                             long long& fix) {
+  const int tid = threadIdx.x;
+  unsigned long long* aah = reinterpret_cast<unsigned long long*>(s.acc) + (a.h_word >> 1);
+  if (tid == 0) {
+    const int32_t abound = (int32_t)addr_of(a, a.dw_n);
+    int nd = 0;
+    while (nd < du && nd < a.dw_max && rowx[nd] < abound) ++nd;
+    s.nd = nd;
+  }
+  __syncthreads();
+  const int nd = s.nd;
+  if (nd == 0) return 0;
+  const unsigned long long wx = FUSED ? (unsigned long long)a.wtab[du] : 0ull;
+  const int64_t xo = (int64_t)x - a.slo;
+  for (int i = 0; i < nd; ++i) {
+    const int64_t pi = p_of(a, rowx[i]);
+    if (!TK_OK(pi >= 0 && pi < a.dw_n, 12, pi, a.dw_n)) continue;  // uniform
+    if (i > 0) {  // members of b_i counted before through b_0 .. b_{i-1}: remove them once
+      const uint32_t* bi = a.dw_bm + pi * a.dw_bmw;
+      for (int64_t k = tid; k < a.dw_bmw; k += TK_NT) {
+        uint32_t o = 0;
+        for (int j = 0; j < i; ++j) o |= a.dw_bm[p_of(a, rowx[j]) * a.dw_bmw + k];
+        uint32_t m = bi[k] & o;
+        if (k == (xo >> 5)) m &= ~(1u << (xo & 31));  // x is handled below
+        while (m) {
+          const int bit = __ffs(m) - 1;
+          m &= m - 1;
+          const int64_t w = a.slo + 32 * k + bit;
+          const int64_t r0 = a.rp[w] - a.pbase;
+          const int len = (int)(a.rp[w + 1] - a.rp[w]);
+          const unsigned long long ww = FUSED ? (unsigned long long)a.wtab[len] : 0ull;
+          for (int q = 0; q < len; ++q) {
+            const int32_t e = TK_OK(r0 + q >= 0 && r0 + q < a.pci_len, 14, r0 + q, a.pci_len) ? a.pci[r0 + q] : 0;
+            acc_sub(a, s.acc, e);
+            if (FUSED && e < a.AH) aa_sub2(aah, p_of(a, e), ww);
+          }
+          h2 -= 1;
+          np -= len;
+          fix += len;
+        }
+      }
+      __syncthreads();
+    }
+    // every member's counts (and fused AA words), one word per thread
+    const uint32_t* cv = a.dw_cv + pi * a.dw_words;
+    for (int64_t k = tid; k < a.dw_words; k += TK_NT) s.acc[k] += cv[k];
+    if (FUSED) {
+      const unsigned long long* ca = a.dw_ca + pi * 2 * a.H;
+      for (int64_t k = tid; k < 2 * a.H; k += TK_NT) aah[k] += ca[k];
+    }
+    __syncthreads();
+    // x is a member of every b_i but not in H2(x)
+    for (int j = tid; j < du; j += TK_NT) {
+      const int32_t e = rowx[j];
+      acc_sub(a, s.acc, e);
+      if (FUSED && e < a.AH) aa_sub2(aah, p_of(a, e), wx);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      h2 += a.dw_info[2 * pi] - 1;
+      np += a.dw_info[2 * pi + 1] - du;
+      fix += du;
+    }
+  }
+  return rowx[nd - 1] + 1;
+}
+
+// Dense counts of one hot target p (one workgroup): every member w of N(b) pushes N'(w) into LDS
+// counters (and the fused AA words of the H most popular targets), w's bit is set in the member
+// bitmap, and the words go out to dw_cv / dw_ca. dw_bm and dw_info are zeroed before.
+__global__ __launch_bounds__(TK_NT) void k_tk_dense_fill(TkArgs a) {
+  __shared__ uint32_t acc[TK_ACC_WORDS];
+  __shared__ long long red[TK_NT / 64];
+  const int tid = threadIdx.x;
+  const int p = blockIdx.x;
+  for (int64_t i = tid; i < a.acc_words; i += TK_NT) acc[i] = 0;
+  __syncthreads();
+  unsigned long long* aah = reinterpret_cast<unsigned long long*>(acc) + (a.h_word >> 1);
+  const int b = a.inv[p];
+  const int64_t rs = a.rp[b], re = a.rp[b + 1];
+  long long sum = 0;
+  for (int64_t k = rs + tid; k < re; k += TK_NT) {
+    const int w = a.ci[k];
+    const int64_t wo = (int64_t)w - a.slo;
+    atomicOr(&a.dw_bm[(int64_t)p * a.dw_bmw + (wo >> 5)], 1u << (wo & 31));
+    const int64_t r0 = a.rp[w] - a.pbase;
+    const int len = (int)(a.rp[w + 1] - a.rp[w]);
+    const unsigned long long ww = a.H > 0 ? (unsigned long long)a.wtab[len] : 0ull;
+    for (int q = 0; q < len; ++q) {
+      const int32_t e = a.pci[r0 + q];
+      atomicAdd(&acc[e >> 2], 1u << ((e & 3) << 3));
+      if (a.H > 0 && e < a.AH) aa_push2(aah, p_of(a, e), ww);
+    }
+    sum += len;
+  }
+  for (int d = 32; d > 0; d >>= 1) sum += __shfl_down(sum, d, 64);
+  if ((tid & 63) == 0) red[tid >> 6] = sum;
+  __syncthreads();
+  if (tid == 0) {
+    long long t = 0;
+    for (int w = 0; w < TK_NT / 64; ++w) t += red[w];
+    a.dw_info[2 * p] = re - rs;
+    a.dw_info[2 * p + 1] = t;
+  }
+  for (int64_t k = tid; k < a.dw_words; k += TK_NT) const_cast<uint32_t*>(a.dw_cv)[(int64_t)p * a.dw_words + k] = acc[k];
+  if (a.H > 0 && a.dw_ca)
+    for (int64_t k = tid; k < 2 * a.H; k += TK_NT)
+      const_cast<unsigned long long*>(a.dw_ca)[(int64_t)p * 2 * a.H + k] = aah[k];
+}
+
 __global__ __launch_bounds__(TK_NT) void k_topk(TkArgs a) {
   __shared__ TkShared s;
   const int tid = threadIdx.x;
@@ -714,6 +863,7 @@ __global__ __launch_bounds__(TK_NT) void k_topk(TkArgs a) {
     const int32_t* rowx = a.pci + (xb - a.pbase);
     for (int i = tid; i < TK_FILT; i += TK_NT) s.filt[i] = 0;
     if (tid < 3) s.nv[tid] = 0;
+    if (tid == 0) s.nd = 0;
     __syncthreads();
     for (int j = tid; j < du; j += TK_NT) {
       const uint32_t b = filt_bit(rowx[j]);
@@ -730,16 +880,24 @@ __global__ __launch_bounds__(TK_NT) void k_topk(TkArgs a) {
       for (int i = tid; i < words; i += TK_NT) s.acc[i] = 0;
       __syncthreads();
       TKP(1)
-      long long np = 0;
-      const long long h = fused ? push_pass<3>(a, s, x, xb, du, rowx, c, 0, 0, 0, ci == 0, &np)
-                                : push_pass<0>(a, s, x, xb, du, rowx, c, 0, 0, 0, ci == 0, &np);
+      long long np = 0, dh = 0, dnp = 0, dfix = 0;
+      int32_t a_dense = 0;  // hot targets below this address were counted densely
+      if (a.dw_n > 0 && a.n_chunks == 1)
+        a_dense = fused ? dense_pass<true>(a, s, x, du, rowx, dh, dnp, dfix)
+                        : dense_pass<false>(a, s, x, du, rowx, dh, dnp, dfix);
+      const long long h = fused ? push_pass<3>(a, s, x, xb, du, rowx, c, 0, 0, 0, ci == 0, &np, a_dense)
+                                : push_pass<0>(a, s, x, xb, du, rowx, c, 0, 0, 0, ci == 0, &np, a_dense);
       TKP(2)
       if (ci == 0) {
-        h2 = block_sum(s, h);
-        np = block_sum(s, np);
+        h2 = block_sum(s, h + dh);
+        const long long walked = block_sum(s, np);
+        np = block_sum(s, np + dnp);
+        dfix = block_sum(s, dfix);
         if (tid == 0) {
           atomicAdd(&a.counters[3], (unsigned long long)h2);
           atomicAdd(&a.counters[4], (unsigned long long)np);
+          atomicAdd(&a.counters[6], (unsigned long long)(walked + dfix));
+          atomicAdd(&a.counters[7], (unsigned long long)s.nd);
         }
       }
       for (int j = tid; j < du; j += TK_NT) {
@@ -907,6 +1065,8 @@ struct blp_topk {
   std::vector<TkChunk> chunks;
   int64_t aa_chunk = 0;
   DevBuf perm, inv, tdeg, ge, pci, d_chunks, src, keys, cols, ncand, counters, wtab, x2_off, x2;
+  DevBuf dw_cv, dw_ca, dw_bm, dw_info;  // dense counts of the hot targets (see the header comment)
+  int64_t dw_n = 0, dw_words = 0, dw_bmw = 0;
   int64_t kbase = 0, x2_entries = -1;
   int64_t pci_n = 0, x2_n = 0;  // entries uploaded to pci / x2, padding included
   int64_t n_src = 0;
@@ -960,6 +1120,60 @@ void plan_chunks(blp_topk* t) {
 }
 
 }  // namespace
+
+// the kernel arguments of a run (k, mask) of handle t
+static TkArgs topk_args(blp_topk* t, int k, uint32_t mask) {
+  TkArgs a{};
+  a.rp = t->g->d_rp;
+  a.ci = t->g->d_ci;
+  a.pci = t->pci.as<int32_t>();
+  a.pbase = t->pbase;
+  a.paddr = t->perm.as<int32_t>();
+  a.H = (mask & BLP_ADAMIC) ? t->H : 0;
+  a.AH = t->AH;
+  a.h_word = t->h_word;
+  a.n32 = t->n32;
+  a.n16 = t->n16;
+  a.A16 = t->A16;
+  a.A8 = t->A8;
+  a.inv = t->inv.as<int32_t>();
+  a.tdeg = t->tdeg.as<int32_t>();
+  a.ge = t->ge.as<int32_t>();
+  a.ge_n = t->ge_n;
+  a.wtab = t->wtab.as<long long>();
+  a.x2_off = t->x2_entries >= 0 ? t->x2_off.as<int64_t>() : nullptr;
+  a.x2 = t->x2_entries >= 0 ? t->x2.as<int32_t>() : nullptr;
+  a.kbase = t->kbase;
+  a.src = t->src.as<int32_t>();
+  a.n_src = (int)t->n_src;
+  a.tlo = t->tlo;
+  a.T = t->T;
+  a.chunks = t->d_chunks.as<TkChunk>();
+  a.n_chunks = (int)t->chunks.size();
+  a.aa_chunk = t->aa_chunk;
+  a.k = k;
+  a.mask = mask;
+  a.ratio = t->ratio;
+  a.hcap = (int)std::max<int64_t>(0, std::min<int64_t>(TK_HCAP, env_i64("BLP_TOPK_HCAP", TK_HCAP)));
+  a.keys = t->keys.as<unsigned long long>();
+  a.cols = t->cols.as<int32_t>();
+  a.ncand = t->ncand.as<int64_t>();
+  a.counters = t->counters.as<unsigned long long>();
+  a.acc_words = t->acc_words;
+  a.pci_len = t->pci_n;
+  a.x2_len = t->x2_n;
+  a.dw_cv = t->dw_n ? t->dw_cv.as<uint32_t>() : nullptr;
+  a.dw_ca = t->dw_n && a.H > 0 ? t->dw_ca.as<unsigned long long>() : nullptr;
+  a.dw_bm = t->dw_n ? t->dw_bm.as<uint32_t>() : nullptr;
+  a.dw_info = t->dw_n ? t->dw_info.as<long long>() : nullptr;
+  a.dw_n = (int)t->dw_n;
+  a.dw_max = (int)std::max<int64_t>(1, env_i64("BLP_TOPK_DENSE_MAX", 8));
+  if (a.H > 0 && !a.dw_ca) a.dw_n = 0;  // counts without their AA words: walk every target
+  a.dw_words = t->dw_words;
+  a.dw_bmw = t->dw_bmw;
+  a.slo = t->slo;
+  return a;
+}
 
 extern "C" int blp_topk_create(blp_graph* g, int64_t src_lo, int64_t src_hi, int64_t tgt_lo, int64_t tgt_hi,
                                blp_topk** out) {
@@ -1120,6 +1334,42 @@ extern "C" int blp_topk_create(blp_graph* g, int64_t src_lo, int64_t src_hi, int
     blp_topk_destroy(t);
     return rc;
   }
+  // dense counts of the hot targets (header comment): the prefix of the degree order whose
+  // members' rows hold at least BLP_TOPK_DENSE_F (2) times the counter words, within
+  // BLP_TOPK_DENSE_MB (1024) of HBM and 256 targets; one counter chunk only (BLP_TOPK_NO_DENSE=1: off)
+  if (t->chunks.size() == 1 && T > 0 && !env_i64("BLP_TOPK_NO_DENSE", 0)) {
+    const int64_t words = chunk_words(t, 0, T);
+    const double f = getenv("BLP_TOPK_DENSE_F") ? atof(getenv("BLP_TOPK_DENSE_F")) : 2.0;
+    const int64_t bmw = ((src_hi - src_lo + 31) / 32 + 3) / 4 * 4;
+    const int64_t hw = t->have_aa ? 2 * t->H : 0;  // u64 AA words per target
+    const int64_t per = 4 * words + 8 * hw + 4 * bmw;
+    const int64_t cap = std::min<int64_t>(256, (env_i64("BLP_TOPK_DENSE_MB", 1024) << 20) / std::max<int64_t>(per, 1));
+    int64_t n = 0;
+    while (n < std::min<int64_t>(T, cap)) {
+      const int b = inv[n];
+      int64_t sum = 0;
+      for (int64_t e = rp[b]; e < rp[b + 1]; ++e) sum += rp[ci[e] + 1] - rp[ci[e]];
+      if ((double)sum < f * (double)words) break;
+      ++n;
+    }
+    if (n > 0) {
+      auto fail_out = [&](int r) {
+        blp_topk_destroy(t);
+        return r;
+      };
+      if ((rc = t->dw_cv.reserve(4 * words * n)) || (rc = t->dw_bm.reserve(4 * bmw * n)) ||
+          (rc = t->dw_info.reserve(16 * n)) || (hw && (rc = t->dw_ca.reserve(8 * hw * n))))
+        return fail_out(rc);
+      BLP_HIP_OR(hipMemset(t->dw_bm.p, 0, 4 * bmw * n), fail_out);
+      t->dw_n = n;
+      t->dw_words = words;
+      t->dw_bmw = bmw;
+      const TkArgs a = topk_args(t, 1, t->have_aa ? 7u : 3u);
+      hipLaunchKernelGGL(k_tk_dense_fill, dim3((unsigned)n), dim3(TK_NT), 0, g->stream, a);
+      BLP_HIP_OR(hipGetLastError(), fail_out);
+      BLP_HIP_OR(hipStreamSynchronize(g->stream), fail_out);
+    }
+  }
   *out = t;
   return BLP_OK;
 }
@@ -1128,7 +1378,7 @@ extern "C" int blp_topk_destroy(blp_topk* t) {
   if (!t) return BLP_OK;
   (void)set_device(t->g);
   for (DevBuf* b : {&t->perm, &t->inv, &t->tdeg, &t->ge, &t->pci, &t->d_chunks, &t->src, &t->keys, &t->cols, &t->ncand,
-                    &t->counters, &t->wtab, &t->x2_off, &t->x2})
+                    &t->counters, &t->wtab, &t->x2_off, &t->x2, &t->dw_cv, &t->dw_ca, &t->dw_bm, &t->dw_info})
     b->release();
   timer_release(t->timer);
   delete t;
@@ -1171,45 +1421,7 @@ extern "C" int blp_topk_run(blp_topk* t, int k, uint32_t mask) {
     return rc;
   hipStream_t st = t->g->stream;
   BLP_HIP(hipMemsetAsync(t->counters.p, 0, 64, st));
-  TkArgs a{};
-  a.rp = t->g->d_rp;
-  a.ci = t->g->d_ci;
-  a.pci = t->pci.as<int32_t>();
-  a.pbase = t->pbase;
-  a.paddr = t->perm.as<int32_t>();
-  a.H = (mask & BLP_ADAMIC) ? t->H : 0;
-  a.AH = t->AH;
-  a.h_word = t->h_word;
-  a.n32 = t->n32;
-  a.n16 = t->n16;
-  a.A16 = t->A16;
-  a.A8 = t->A8;
-  a.inv = t->inv.as<int32_t>();
-  a.tdeg = t->tdeg.as<int32_t>();
-  a.ge = t->ge.as<int32_t>();
-  a.ge_n = t->ge_n;
-  a.wtab = t->wtab.as<long long>();
-  a.x2_off = t->x2_entries >= 0 ? t->x2_off.as<int64_t>() : nullptr;
-  a.x2 = t->x2_entries >= 0 ? t->x2.as<int32_t>() : nullptr;
-  a.kbase = t->kbase;
-  a.src = t->src.as<int32_t>();
-  a.n_src = (int)t->n_src;
-  a.tlo = t->tlo;
-  a.T = t->T;
-  a.chunks = t->d_chunks.as<TkChunk>();
-  a.n_chunks = (int)t->chunks.size();
-  a.aa_chunk = t->aa_chunk;
-  a.k = k;
-  a.mask = mask;
-  a.ratio = t->ratio;
-  a.hcap = (int)std::max<int64_t>(0, std::min<int64_t>(TK_HCAP, env_i64("BLP_TOPK_HCAP", TK_HCAP)));
-  a.keys = t->keys.as<unsigned long long>();
-  a.cols = t->cols.as<int32_t>();
-  a.ncand = t->ncand.as<int64_t>();
-  a.counters = t->counters.as<unsigned long long>();
-  a.acc_words = t->acc_words;
-  a.pci_len = t->pci_n;
-  a.x2_len = t->x2_n;
+  TkArgs a = topk_args(t, k, mask);
   hipEvent_t t0;
   if ((rc = timer_begin(t->timer, st, &t0))) return rc;
   if (t->n_src) {
@@ -1272,7 +1484,7 @@ extern "C" int blp_topk_fetch(blp_topk* t, uint32_t method, int32_t* cols, doubl
 }
 
 extern "C" int blp_topk_stats(blp_topk* t, int which, double* total_ms, int64_t* launches) {
-  BLP_CHECK(t && which >= 0 && which <= 5, BLP_E_ARG, "blp_topk_stats: bad arguments");
+  BLP_CHECK(t && which >= 0 && which <= 7, BLP_E_ARG, "blp_topk_stats: bad arguments");
   int rc = set_device(t->g);
   if (rc) return rc;
   if (which == 0) {
@@ -1283,7 +1495,8 @@ extern "C" int blp_topk_stats(blp_topk* t, int which, double* total_ms, int64_t*
   }
   // 1 / 2: sources whose AA went through the candidate hash / direct accumulation;
   // 3: sum of |H2(x)|; 4: sum over x and w in H2(x) of |N(w)| (the push volume of one pass);
-  // 5: sources whose AA top-k came straight from the fused sums
+  // 5: sources whose AA top-k came straight from the fused sums; 6: row entries actually pushed by
+  // the count pass (walk + dense corrections); 7: dense target counts added
   BLP_HIP(hipStreamSynchronize(t->g->stream));
   unsigned long long c[8];
   BLP_HIP(hipMemcpy(c, t->counters.p, 64, hipMemcpyDeviceToHost));

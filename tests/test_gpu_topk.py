@@ -101,6 +101,30 @@ def test_topk_selection_pruning_many_targets(gpu, monkeypatch, acc_words):
         check_against_oracle(G, T, adj, src, k, mask=blp.CN | blp.JACCARD, methods=METHODS[:2])
 
 
+@pytest.mark.parametrize("knobs", [
+    {},                                               # dense counts for the hot prefix (default)
+    {"BLP_TOPK_NO_DENSE": "1"},                       # every target walked
+    {"BLP_TOPK_DENSE_MAX": "1"},                      # one dense target per source, the rest walked
+    {"BLP_TOPK_DENSE_MAX": "3"},                      # corrections between dense targets
+    {"BLP_TOPK_DENSE_F": "40"},                       # only the most popular targets dense
+    {"BLP_TOPK_DENSE_MAX": "64", "BLP_TOPK_T8": "20", "BLP_TOPK_T16": "60"},  # all tiers
+    {"BLP_TOPK_DENSE_MAX": "64", "BLP_TOPK_NO_FUSE": "1"},
+])
+def test_topk_dense_counts_match_oracle(small, monkeypatch, knobs):
+    """Hot targets' counts added from their precomputed member counts (minus members already
+    counted through an earlier hot target, minus x) give the walk's lists exactly."""
+    G, adj, rng = small
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    T = blp.TopK(G, "user")
+    src = rng.choice(np.flatnonzero(G.hop1_size[: G.n_col0] > 2), 30, replace=False)
+    check_against_oracle(G, T, adj, src, 20)
+    dense = T.stats(7)[1]
+    assert (dense == 0) == ("BLP_TOPK_NO_DENSE" in knobs)
+    if "BLP_TOPK_DENSE_MAX" in knobs and knobs["BLP_TOPK_DENSE_MAX"] == "1":
+        assert dense <= len(src)
+
+
 def test_topk_unfused_matches_oracle(small, monkeypatch):
     G, adj, rng = small
     monkeypatch.setenv("BLP_TOPK_NO_FUSE", "1")
