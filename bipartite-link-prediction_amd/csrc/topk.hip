@@ -435,9 +435,7 @@ __device__ __attribute__((always_inline)) long long push_pass(const TkArgs& a, T
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();  // the table is rewritten next round
       }
-      __syncthreads();
-      if (pushed) *pushed = npush;
-      return h2;
+      continue;  // the next batch of N(x) (its first barrier orders this batch's pushes)
     }
     while (idx < E) {
       const bool skip = skipn;
@@ -1360,7 +1358,7 @@ extern "C" int blp_topk_create(blp_graph* g, int64_t src_lo, int64_t src_hi, int
       if ((rc = t->dw_cv.reserve(4 * words * n)) || (rc = t->dw_bm.reserve(4 * bmw * n)) ||
           (rc = t->dw_info.reserve(16 * n)) || (hw && (rc = t->dw_ca.reserve(8 * hw * n))))
         return fail_out(rc);
-      BLP_HIP_OR(hipMemset(t->dw_bm.p, 0, 4 * bmw * n), fail_out);
+      BLP_HIP_OR(hipMemsetAsync(t->dw_bm.p, 0, 4 * bmw * n, g->stream), fail_out);  // ordered before the fill
       t->dw_n = n;
       t->dw_words = words;
       t->dw_bmw = bmw;

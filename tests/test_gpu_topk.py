@@ -181,6 +181,23 @@ def test_topk_business_side(small):
     check_against_oracle(G, T, adj, src, 10)
 
 
+@pytest.mark.parametrize("knobs", [{}, {"BLP_TOPK_NO_DENSE": "1"}, {"BLP_TOPK_DENSE_MAX": "2"}])
+def test_topk_sources_with_long_rows(small, monkeypatch, knobs):
+    """Business-side sources with more than one batch of N(x) (TK_SEG = 256 entries): the most
+    reviewed businesses. Every batch must be walked (the flattened push once stopped after the
+    first batch)."""
+    G, adj, rng = small
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    nb = G.n - G.n_col0
+    deg = G.hop1_size[G.n_col0:]
+    top = np.argsort(-deg, kind="stable")[:6]
+    assert deg[top[0]] > 256
+    src = G.n_col0 + np.concatenate([top, rng.choice(nb, 6, replace=False)])
+    T = blp.TopK(G, "business")
+    check_against_oracle(G, T, adj, src, 10)
+
+
 def test_topk_edge_cases(gpu):
     # user 0 shares business 10 with user 1, who also reviewed 11 and 12; user 2 is alone on 13
     a = np.array([0, 1, 1, 1, 2, 3, 3], np.int64)
