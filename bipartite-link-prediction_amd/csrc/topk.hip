@@ -114,6 +114,8 @@ struct TkArgs {
   const unsigned long long* dw_ca;  // [dw_n][2 H] their fused AA words (or null)
   uint32_t* dw_bm;                  // [dw_n][dw_bmw] N(b) over the sources (bit w - slo)
   long long* dw_info;               // [dw_n][2] |N(b)|, sum of |N(w)| over w in N(b)
+  unsigned long long* dw_caf;       // [dw_n][2 T] the members' exact AA words for EVERY target (the
+                                    // hash / direct AA passes; or null: those passes walk every target)
   int dw_n, dw_max;                 // hot targets; at most dw_max of them per source
   int64_t dw_words, dw_bmw, slo;
 };
@@ -730,6 +732,29 @@ __device__ unsigned long long g_tkprof[16];
 // Dense counts of the hot prefix of N'(x) (single counter chunk, a0 = 0; header comment). h2 /
 // np / fix receive this thread's share of |H2(x)|, of sum_{w in H2(x)} |N(w)| and of the rows
 // pushed as corrections. Returns the address bound below which the walk skips targets.
+// The members of hot target b_i (i >= 1) already counted through b_0 .. b_{i-1} -- the bits of
+// N(b_i) AND (N(b_0) OR ... OR N(b_{i-1})), x's bit cleared -- each handed to fn(w, r0, len) by the
+// thread owning its bitmap word (r0: w's row in pci, len = |N(w)|).
+template <class Fn>
+__device__ __attribute__((always_inline)) void dense_overlap(const TkArgs& a, const int32_t* rowx, int i, int x, Fn fn) {
+  const int64_t pi = p_of(a, rowx[i]);
+  const int64_t xo = (int64_t)x - a.slo;
+  const uint32_t* bi = a.dw_bm + pi * a.dw_bmw;
+  for (int64_t k = threadIdx.x; k < a.dw_bmw; k += TK_NT) {
+    uint32_t o = 0;
+    for (int j = 0; j < i; ++j) o |= a.dw_bm[p_of(a, rowx[j]) * a.dw_bmw + k];
+    uint32_t m = bi[k] & o;
+    if (k == (xo >> 5)) m &= ~(1u << (xo & 31));  // x: handled by the caller
+    while (m) {
+      const int bit = __ffs(m) - 1;
+      m &= m - 1;
+      const int64_t w = a.slo + 32 * k + bit;
+      const int64_t r0 = a.rp[w] - a.pbase;
+      fn(w, r0, (int)(a.rp[w + 1] - a.rp[w]));
+    }
+  }
+}
+
 template <bool FUSED>
 __device__ __attribute__((always_inline)) int32_t dense_pass(const TkArgs& a, TkShared& s, int x, int du,
                                                              const int32_t* rowx, long long& h2, long long& np,
@@ -746,34 +771,21 @@ __device__ __attribute__((always_inline)) int32_t dense_pass(const TkArgs& a, Tk
   const int nd = s.nd;
   if (nd == 0) return 0;
   const unsigned long long wx = FUSED ? (unsigned long long)a.wtab[du] : 0ull;
-  const int64_t xo = (int64_t)x - a.slo;
   for (int i = 0; i < nd; ++i) {
     const int64_t pi = p_of(a, rowx[i]);
     if (!TK_OK(pi >= 0 && pi < a.dw_n, 12, pi, a.dw_n)) continue;  // uniform
     if (i > 0) {  // members of b_i counted before through b_0 .. b_{i-1}: remove them once
-      const uint32_t* bi = a.dw_bm + pi * a.dw_bmw;
-      for (int64_t k = tid; k < a.dw_bmw; k += TK_NT) {
-        uint32_t o = 0;
-        for (int j = 0; j < i; ++j) o |= a.dw_bm[p_of(a, rowx[j]) * a.dw_bmw + k];
-        uint32_t m = bi[k] & o;
-        if (k == (xo >> 5)) m &= ~(1u << (xo & 31));  // x is handled below
-        while (m) {
-          const int bit = __ffs(m) - 1;
-          m &= m - 1;
-          const int64_t w = a.slo + 32 * k + bit;
-          const int64_t r0 = a.rp[w] - a.pbase;
-          const int len = (int)(a.rp[w + 1] - a.rp[w]);
-          const unsigned long long ww = FUSED ? (unsigned long long)a.wtab[len] : 0ull;
-          for (int q = 0; q < len; ++q) {
-            const int32_t e = TK_OK(r0 + q >= 0 && r0 + q < a.pci_len, 14, r0 + q, a.pci_len) ? a.pci[r0 + q] : 0;
-            acc_sub(a, s.acc, e);
-            if (FUSED && e < a.AH) aa_sub2(aah, p_of(a, e), ww);
-          }
-          h2 -= 1;
-          np -= len;
-          fix += len;
+      dense_overlap(a, rowx, i, x, [&](int64_t, int64_t r0, int len) {
+        const unsigned long long ww = FUSED ? (unsigned long long)a.wtab[len] : 0ull;
+        for (int q = 0; q < len; ++q) {
+          const int32_t e = TK_OK(r0 + q >= 0 && r0 + q < a.pci_len, 14, r0 + q, a.pci_len) ? a.pci[r0 + q] : 0;
+          acc_sub(a, s.acc, e);
+          if (FUSED && e < a.AH) aa_sub2(aah, p_of(a, e), ww);
         }
-      }
+        h2 -= 1;
+        np -= len;
+        fix += len;
+      });
       __syncthreads();
     }
     // every member's counts (and fused AA words), one word per thread
@@ -800,6 +812,73 @@ __device__ __attribute__((always_inline)) int32_t dense_pass(const TkArgs& a, Tk
   return rowx[nd - 1] + 1;
 }
 
+// The hash AA pass (MODE 1) with the same nd hot targets as the count pass: each hashed
+// candidate t gets sum_i CAF_{b_i}[t] (the exact words of ALL members of b_i), then the members of
+// b_i already counted through an earlier b_j give their term back. x's own term never reaches a
+// candidate (candidates lie outside N'(x)). Returns the walk's skip bound (0: no dense targets).
+__device__ __attribute__((always_inline)) int32_t dense_aa_hash(const TkArgs& a, TkShared& s, int x, const int32_t* rowx) {
+  const int nd = s.nd;
+  if (nd == 0 || !a.dw_caf) return 0;
+  for (int h = threadIdx.x; h < TK_AH; h += TK_NT) {
+    const int32_t e = s.col[h];
+    if (e == (int32_t)TK_EMPTY) continue;
+    const int64_t t = p_of(a, e);
+    unsigned long long lo = 0, hi = 0;
+    for (int i = 0; i < nd; ++i) {
+      const unsigned long long* caf = a.dw_caf + 2 * (p_of(a, rowx[i]) * a.T + t);
+      lo += caf[0];
+      hi += caf[1];
+    }
+    s.key[2 * h] += lo;
+    s.key[2 * h + 1] += hi;
+  }
+  __syncthreads();
+  for (int i = 1; i < nd; ++i)
+    dense_overlap(a, rowx, i, x, [&](int64_t, int64_t r0, int len) {
+      const unsigned long long ww = (unsigned long long)a.wtab[len];
+      for (int q = 0; q < len; ++q) {
+        const int32_t e = a.pci[r0 + q];
+        int h = hash_slot(e);
+        for (int pr = 0; pr < TK_AH; ++pr) {
+          const int32_t c = s.col[h];
+          if (c == e) {
+            aa_sub2(s.key, h, ww);
+            break;
+          }
+          if (c == (int32_t)TK_EMPTY) break;
+          h = (h + 1) & (TK_AH - 1);
+        }
+      }
+    });
+  __syncthreads();
+  return rowx[nd - 1] + 1;
+}
+
+// The direct AA pass (MODE 2), targets [d0, d1) as word pairs in acc64: the same dense
+// contributions for the slice (x's own entries are cleared after the pass anyway).
+__device__ __attribute__((always_inline)) int32_t dense_aa_direct(const TkArgs& a, TkShared& s, int x, const int32_t* rowx,
+                                                                  int64_t d0, int64_t d1) {
+  const int nd = s.nd;
+  if (nd == 0 || !a.dw_caf) return 0;
+  unsigned long long* acc64 = reinterpret_cast<unsigned long long*>(s.acc);
+  for (int64_t q = threadIdx.x; q < 2 * (d1 - d0); q += TK_NT) {
+    unsigned long long v = 0;
+    for (int i = 0; i < nd; ++i) v += a.dw_caf[2 * (p_of(a, rowx[i]) * a.T + d0) + q];
+    acc64[q] += v;
+  }
+  __syncthreads();
+  for (int i = 1; i < nd; ++i)
+    dense_overlap(a, rowx, i, x, [&](int64_t, int64_t r0, int len) {
+      const unsigned long long ww = (unsigned long long)a.wtab[len];
+      for (int q = 0; q < len; ++q) {
+        const int64_t p = p_of(a, a.pci[r0 + q]);
+        if (p >= d0 && p < d1) aa_sub2(acc64, p - d0, ww);
+      }
+    });
+  __syncthreads();
+  return rowx[nd - 1] + 1;
+}
+
 // Dense counts of one hot target p (one workgroup): every member w of N(b) pushes N'(w) into LDS
 // counters (and the fused AA words of the H most popular targets), w's bit is set in the member
 // bitmap, and the words go out to dw_cv / dw_ca. dw_bm and dw_info are zeroed before.
@@ -821,10 +900,14 @@ __global__ __launch_bounds__(TK_NT) void k_tk_dense_fill(TkArgs a) {
     const int64_t r0 = a.rp[w] - a.pbase;
     const int len = (int)(a.rp[w + 1] - a.rp[w]);
     const unsigned long long ww = a.H > 0 ? (unsigned long long)a.wtab[len] : 0ull;
+    unsigned long long* caf = a.dw_caf ? a.dw_caf + 2 * (int64_t)p * a.T : nullptr;
     for (int q = 0; q < len; ++q) {
       const int32_t e = a.pci[r0 + q];
       atomicAdd(&acc[e >> 2], 1u << ((e & 3) << 3));
-      if (a.H > 0 && e < a.AH) aa_push2(aah, p_of(a, e), ww);
+      if (a.H > 0 && e < a.AH)
+        aa_push2(aah, p_of(a, e), ww);
+      else if (caf)
+        aa_push2(caf, p_of(a, e), ww);  // device-scope: the targets outside the fused region
     }
     sum += len;
   }
@@ -839,8 +922,10 @@ __global__ __launch_bounds__(TK_NT) void k_tk_dense_fill(TkArgs a) {
   }
   for (int64_t k = tid; k < a.dw_words; k += TK_NT) const_cast<uint32_t*>(a.dw_cv)[(int64_t)p * a.dw_words + k] = acc[k];
   if (a.H > 0 && a.dw_ca)
-    for (int64_t k = tid; k < 2 * a.H; k += TK_NT)
+    for (int64_t k = tid; k < 2 * a.H; k += TK_NT) {
       const_cast<unsigned long long*>(a.dw_ca)[(int64_t)p * 2 * a.H + k] = aah[k];
+      if (a.dw_caf) a.dw_caf[2 * (int64_t)p * a.T + k] = aah[k];  // the fused targets' words, in CAF too
+    }
 }
 
 __global__ __launch_bounds__(TK_NT) void k_topk(TkArgs a) {
@@ -960,7 +1045,8 @@ __global__ __launch_bounds__(TK_NT) void k_topk(TkArgs a) {
             }
           }
           __syncthreads();
-          push_pass<1>(a, s, x, xb, du, rowx, c, thr, 0, 0, false);
+          const int32_t a_dense1 = dense_aa_hash(a, s, x, rowx);
+          push_pass<1>(a, s, x, xb, du, rowx, c, thr, 0, 0, false, nullptr, a_dense1);
           // hash slots -> selection entries (key = bits of the exact AA double, col = dense target id)
           unsigned long long kv[TK_SEL / TK_NT];
           int cv[TK_SEL / TK_NT];
@@ -1002,7 +1088,8 @@ __global__ __launch_bounds__(TK_NT) void k_topk(TkArgs a) {
           const int64_t d1 = min(a.T, d0 + a.aa_chunk);
           for (int64_t i = tid; i < 2 * (d1 - d0); i += TK_NT) acc64[i] = 0;
           __syncthreads();
-          push_pass<2>(a, s, x, xb, du, rowx, a.chunks[0], 0, d0, d1, false);
+          const int32_t a_dense2 = dense_aa_direct(a, s, x, rowx, d0, d1);
+          push_pass<2>(a, s, x, xb, du, rowx, a.chunks[0], 0, d0, d1, false, nullptr, a_dense2);
           for (int j = tid; j < du; j += TK_NT) {
             const int64_t p = p_of(a, rowx[j]);
             if (p >= d0 && p < d1 && TK_OK(2 * (p - d0) + 1 < a.acc_words / 2, 6, p - d0, a.acc_words / 4))
@@ -1063,7 +1150,7 @@ struct blp_topk {
   std::vector<TkChunk> chunks;
   int64_t aa_chunk = 0;
   DevBuf perm, inv, tdeg, ge, pci, d_chunks, src, keys, cols, ncand, counters, wtab, x2_off, x2;
-  DevBuf dw_cv, dw_ca, dw_bm, dw_info;  // dense counts of the hot targets (see the header comment)
+  DevBuf dw_cv, dw_ca, dw_bm, dw_info, dw_caf;  // dense counts of the hot targets (see the header comment)
   int64_t dw_n = 0, dw_words = 0, dw_bmw = 0;
   int64_t kbase = 0, x2_entries = -1;
   int64_t pci_n = 0, x2_n = 0;  // entries uploaded to pci / x2, padding included
@@ -1113,6 +1200,7 @@ void plan_chunks(blp_topk* t) {
   if (t->chunks.size() == 1 && !env_i64("BLP_TOPK_NO_FUSE", 0)) {
     t->h_word = (chunk_words(t, 0, t->T) + 1) / 2 * 2;
     t->H = std::max<int64_t>(0, std::min<int64_t>(t->T, (t->acc_words - t->h_word) / 4));
+    t->H = std::min<int64_t>(t->H, env_i64("BLP_TOPK_FUSE_H", t->H));  // test knob: fewer fused targets
   }
   t->AH = t->H > 0 ? host_addr(t, t->H) : 0;
 }
@@ -1164,6 +1252,7 @@ static TkArgs topk_args(blp_topk* t, int k, uint32_t mask) {
   a.dw_ca = t->dw_n && a.H > 0 ? t->dw_ca.as<unsigned long long>() : nullptr;
   a.dw_bm = t->dw_n ? t->dw_bm.as<uint32_t>() : nullptr;
   a.dw_info = t->dw_n ? t->dw_info.as<long long>() : nullptr;
+  a.dw_caf = t->dw_n && (mask & BLP_ADAMIC) && t->dw_caf.p ? t->dw_caf.as<unsigned long long>() : nullptr;
   a.dw_n = (int)t->dw_n;
   a.dw_max = (int)std::max<int64_t>(1, env_i64("BLP_TOPK_DENSE_MAX", 8));
   if (a.H > 0 && !a.dw_ca) a.dw_n = 0;  // counts without their AA words: walk every target
@@ -1358,6 +1447,13 @@ extern "C" int blp_topk_create(blp_graph* g, int64_t src_lo, int64_t src_hi, int
       if ((rc = t->dw_cv.reserve(4 * words * n)) || (rc = t->dw_bm.reserve(4 * bmw * n)) ||
           (rc = t->dw_info.reserve(16 * n)) || (hw && (rc = t->dw_ca.reserve(8 * hw * n))))
         return fail_out(rc);
+      // every target's exact AA words of the members (the hash / direct AA passes), within
+      // BLP_TOPK_DENSE_AA_MB (2048) of HBM; without them those passes walk every target
+      const int64_t caf_bytes = 16 * T * n;
+      if (t->have_aa && caf_bytes <= (env_i64("BLP_TOPK_DENSE_AA_MB", 2048) << 20)) {
+        if ((rc = t->dw_caf.reserve(caf_bytes))) return fail_out(rc);
+        BLP_HIP_OR(hipMemsetAsync(t->dw_caf.p, 0, caf_bytes, g->stream), fail_out);
+      }
       BLP_HIP_OR(hipMemsetAsync(t->dw_bm.p, 0, 4 * bmw * n, g->stream), fail_out);  // ordered before the fill
       t->dw_n = n;
       t->dw_words = words;
@@ -1376,7 +1472,8 @@ extern "C" int blp_topk_destroy(blp_topk* t) {
   if (!t) return BLP_OK;
   (void)set_device(t->g);
   for (DevBuf* b : {&t->perm, &t->inv, &t->tdeg, &t->ge, &t->pci, &t->d_chunks, &t->src, &t->keys, &t->cols, &t->ncand,
-                    &t->counters, &t->wtab, &t->x2_off, &t->x2, &t->dw_cv, &t->dw_ca, &t->dw_bm, &t->dw_info})
+                    &t->counters, &t->wtab, &t->x2_off, &t->x2, &t->dw_cv, &t->dw_ca, &t->dw_bm, &t->dw_info,
+                    &t->dw_caf})
     b->release();
   timer_release(t->timer);
   delete t;

@@ -109,6 +109,10 @@ def test_topk_selection_pruning_many_targets(gpu, monkeypatch, acc_words):
     {"BLP_TOPK_DENSE_F": "40"},                       # only the most popular targets dense
     {"BLP_TOPK_DENSE_MAX": "64", "BLP_TOPK_T8": "20", "BLP_TOPK_T16": "60"},  # all tiers
     {"BLP_TOPK_DENSE_MAX": "64", "BLP_TOPK_NO_FUSE": "1"},
+    {"BLP_TOPK_FUSE_H": "20"},                        # AA through the candidate hash, dense words added
+    {"BLP_TOPK_FUSE_H": "20", "BLP_TOPK_HCAP": "0"},  # ... through the direct chunks
+    {"BLP_TOPK_NO_FUSE": "1", "BLP_TOPK_HCAP": "0", "BLP_TOPK_DENSE_MAX": "3"},
+    {"BLP_TOPK_FUSE_H": "20", "BLP_TOPK_DENSE_AA_MB": "0"},  # no dense AA words: those passes walk all
 ])
 def test_topk_dense_counts_match_oracle(small, monkeypatch, knobs):
     """Hot targets' counts added from their precomputed member counts (minus members already
@@ -121,6 +125,10 @@ def test_topk_dense_counts_match_oracle(small, monkeypatch, knobs):
     check_against_oracle(G, T, adj, src, 20)
     dense = T.stats(7)[1]
     assert (dense == 0) == ("BLP_TOPK_NO_DENSE" in knobs)
+    if knobs.get("BLP_TOPK_HCAP") == "0":
+        assert T.stats(2)[1] > 0  # direct AA path taken
+    elif "BLP_TOPK_FUSE_H" in knobs:
+        assert T.stats(1)[1] > 0  # candidate hash path taken
     if "BLP_TOPK_DENSE_MAX" in knobs and knobs["BLP_TOPK_DENSE_MAX"] == "1":
         assert dense <= len(src)
 
