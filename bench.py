@@ -570,9 +570,17 @@ def run_sharded(args):
         passes.append(("business", G.batch(ex_y, ex_x), 7 if getattr(args, "fix_adamic", False) else 3))
     for name, bt, _ in passes:
         log("plan %s: %s" % (name, bt.plan()))
+    # both passes as one concurrent step (blp_batches_score: each chunk-parallel grid on its share
+    # of the CUs); --serial-passes: one after the other
+    def step():
+        if len(passes) > 1 and not args.serial_passes:
+            G.score_batches([(bt, mask) for _, bt, mask in passes])
+        else:
+            for _, bt, mask in passes:
+                bt.score(mask)
+
     for _ in range(args.warmup):
-        for _, bt, mask in passes:
-            bt.score(mask)
+        step()
     blp.device_sync(dev)
     for _, bt, _ in passes:
         bt.stats_reset()
@@ -580,8 +588,7 @@ def run_sharded(args):
     blp.device_sync(dev)
     t_start = time.perf_counter()
     for _ in range(args.steps):
-        for _, bt, mask in passes:
-            bt.score(mask)
+        step()
     blp.device_sync(dev)
     t_local = time.perf_counter() - t_start
     d.barrier()
@@ -835,6 +842,7 @@ def main():
                          "top-k; svd: config 4 rank-64 truncated-SVD scorer; sharded: config 5 row-block "
                          "sharded ingest + RCCL all-gather, then rank-local scoring (--config c5); e2e: "
                          "similarity.main from graph.txt to the 6 files (--config yelp = config 1, or c2)")
+    ap.add_argument("--serial-passes", action="store_true", help="--mode sharded: score the passes one after the other")
     ap.add_argument("--parity-sources", type=int, default=50,
                     help="--mode sharded: sampled sources per side and rank checked against the C oracle")
     ap.add_argument("--no-collective-at-world1", action="store_true",

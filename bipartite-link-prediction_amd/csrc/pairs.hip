@@ -3443,10 +3443,11 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
     // slices of <= short_max ids scanned by their pair's thread (128 KiB chunks; BLP_SPLIT_SHORT=0: off)
     const int short_max = std::min(SHORT_PART, getenv("BLP_SPLIT_SHORT") ? atoi(getenv("BLP_SPLIT_SHORT")) : SHORT_PART);
     a.sched = getenv("BLP_SPLIT_ONEQ") ? 1 : 0;  // k_score_split: 1 = one global item queue (no XCD groups)
+    const int scu = b->cus > 0 ? b->cus : g->n_cu;  // CUs the persistent grids may fill (blp_batches_score)
     if (b->d_hflag) {  // small-H2 sources first, on their own hash-set kernel
       int hcu = 1;
       BLP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&hcu, k_score_hash<HS_BLOCK, HS_HT>, HS_BLOCK, 0));
-      hipLaunchKernelGGL((k_score_hash<HS_BLOCK, HS_HT>), dim3(g->n_cu * std::max(hcu, 1)), dim3(HS_BLOCK), 0, b->stream, a,
+      hipLaunchKernelGGL((k_score_hash<HS_BLOCK, HS_HT>), dim3(scu * std::max(hcu, 1)), dim3(HS_BLOCK), 0, b->stream, a,
                          b->d_hflag, (int32_t)b->xlo);
       BLP_HIP(hipGetLastError());
     }
@@ -3455,12 +3456,12 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
     int per_cu = 1;
     if (b->split_big) {
       BLP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_score_split<S_BLOCK, S_CAP_BIG, S_SEG, 8>, S_BLOCK, 0));
-      hipLaunchKernelGGL((k_score_split<S_BLOCK, S_CAP_BIG, S_SEG, 8>), dim3(g->n_cu * std::max(per_cu, 1)), dim3(S_BLOCK),
+      hipLaunchKernelGGL((k_score_split<S_BLOCK, S_CAP_BIG, S_SEG, 8>), dim3(scu * std::max(per_cu, 1)), dim3(S_BLOCK),
                          0, b->stream, a, b->d_gy, b->d_rsplit, b->rs_lo, b->split, b->d_pcn, b->d_paa, b->d_ph2, np, pk24,
                          short_max, b->d_hflag, (int32_t)b->xlo);
     } else {
       BLP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_score_split<S_BLOCK, S_CAP, S_SEG, 8>, S_BLOCK, 0));
-      hipLaunchKernelGGL((k_score_split<S_BLOCK, S_CAP, S_SEG, 8>), dim3(g->n_cu * std::max(per_cu, 1)), dim3(S_BLOCK), 0,
+      hipLaunchKernelGGL((k_score_split<S_BLOCK, S_CAP, S_SEG, 8>), dim3(scu * std::max(per_cu, 1)), dim3(S_BLOCK), 0,
                          b->stream, a, b->d_gy, b->d_rsplit, b->rs_lo, b->split, b->d_pcn, b->d_paa, b->d_ph2, np, pk24,
                          short_max, b->d_hflag, (int32_t)b->xlo);
     }
@@ -3546,9 +3547,22 @@ int blp_batches_score(blp_graph* g, int n, blp_batch* const* bs, const uint32_t*
     share = std::max(g->n_cu / 2, std::min(g->n_cu, (int)std::lround(f * g->n_cu / 8.0) * 8));
   }
   if (const char* e = getenv("BLP_COSCHED_CUS")) share = atoi(e);  // tuning knob
+  // chunk-parallel batches side by side (config 5's two passes): each persistent grid on a share
+  // of the CUs in proportion to its planned elements, so both run at once (BLP_SPLIT_COSCHED=0: off)
+  int n_split = 0;
+  double w_split = 0.0;
+  for (int i = 0; i < n; ++i)
+    if (bs[i]->split) ++n_split, w_split += (double)bs[i]->work_elems + 1.0;
+  const bool split_share = n_split >= 2 && !(getenv("BLP_SPLIT_COSCHED") && atoi(getenv("BLP_SPLIT_COSCHED")) == 0);
   for (int i = 0; i < n; ++i) {
     blp_batch* b = bs[i];
     b->cus = is_large(b) && t_other > 0.0 ? share : 0;
+    if (split_share && b->split) {
+      const double f = ((double)b->work_elems + 1.0) / w_split;
+      b->cus = std::max(8, std::min(g->n_cu - 8, (int)std::lround(f * g->n_cu / 8.0) * 8));
+      if (const char* e = getenv("BLP_SPLIT_COSCHED_CUS"))  // tuning knob: the FIRST split batch's share
+        b->cus = i == 0 ? atoi(e) : g->n_cu - atoi(e);
+    }
     const int rc = blp_batch_score(g, b, masks[i]);
     b->cus = 0;
     if (rc) return rc;

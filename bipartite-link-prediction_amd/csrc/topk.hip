@@ -899,8 +899,8 @@ __global__ __launch_bounds__(TK_NT) void k_tk_dense_fill(TkArgs a) {
     atomicOr(&a.dw_bm[(int64_t)p * a.dw_bmw + (wo >> 5)], 1u << (wo & 31));
     const int64_t r0 = a.rp[w] - a.pbase;
     const int len = (int)(a.rp[w + 1] - a.rp[w]);
-    const unsigned long long ww = a.H > 0 ? (unsigned long long)a.wtab[len] : 0ull;
     unsigned long long* caf = a.dw_caf ? a.dw_caf + 2 * (int64_t)p * a.T : nullptr;
+    const unsigned long long ww = a.H > 0 || caf ? (unsigned long long)a.wtab[len] : 0ull;
     for (int q = 0; q < len; ++q) {
       const int32_t e = a.pci[r0 + q];
       atomicAdd(&acc[e >> 2], 1u << ((e & 3) << 3));
