@@ -109,6 +109,39 @@ def pmc_fields(kernel, pattern, sec=None):
     return {"traffic": None, "traffic_source": "no committed PMC summary for %s matching profiles/%s" % (kernel, pattern)}
 
 
+def pmc_limiter(kernel, pattern):
+    """What bounds `kernel`, from the newest committed counter summary matching `pattern` under
+    profiles/ (profiles/pmc_report.py output of separate SQ / TCC --pmc passes): the share of
+    wave cycles spent waiting, the share of LDS-active cycles lost to bank conflicts, and the L2
+    hit rate. None when no summary names the kernel."""
+    import glob
+    import re
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)),
+                   key=lambda f: (int((re.match(r"r(\d+)_", os.path.basename(f)) or [0, -1])[1]), f), reverse=True)
+    for f in files:
+        c, cur = {}, None
+        for line in open(f):
+            if not line.startswith(" "):
+                cur = kernel in line
+                continue
+            if cur:
+                parts = line.split()
+                if len(parts) == 2:
+                    c[parts[0]] = float(parts[1])
+        if c.get("SQ_WAVE_CYCLES"):
+            def ratio(a, b):
+                return c.get(a, 0.0) / c[b] if c.get(b) else float("nan")
+            hit = c.get("TCC_HIT_sum", 0.0)
+            miss = c.get("TCC_MISS_sum", 0.0)
+            return ("latency: waves wait %.0f%% of their cycles; %.0f%% of LDS-active cycles are bank conflicts; "
+                    "L2 hit %.0f%% (%s)" % (100 * ratio("SQ_WAIT_ANY", "SQ_WAVE_CYCLES"),
+                                             100 * ratio("SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE"),
+                                             100 * hit / (hit + miss) if hit + miss else float("nan"),
+                                             os.path.relpath(f, ROOT)))
+    return None
+
+
 def cpu_baseline(og, ex_x, ex_y, target_s=15.0):
     """C oracle (oracle/oracle.c), 1 thread, on a bounded sample of the same workload:
     all pairs of a subset of the example users (user side) and all pairs of a subset of
@@ -489,7 +522,8 @@ def run_topk(args):
                    "parallelism": "replicas x%d (graph replicated, users split, no collective)" % dist.world},
         "roofline": {"bound": "hbm", "achieved": byts / kern_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": byts / kern_s / 1e9 / HBM_PEAK_GBS, "kernel": "k_topk", "kernel_ms": 1e3 * kern_s,
-                     "alg_bytes_per_launch": byts, **pmc_fields("k_topk", "r*_topk_*.json", kern_s)},
+                     "alg_bytes_per_launch": byts, **pmc_fields("k_topk", "r*_topk_*.json", kern_s),
+                     "limiter": pmc_limiter("k_topk", "r*_topk_*_pmc.txt")},
         "work": {"sum_h2": h2_sum, "sum_push": push_sum, "pushed": pushed, "dense_target_adds": dense_adds,
                  "aa_hash_sources": hash_src, "aa_direct_sources": direct_src},
     }
@@ -627,6 +661,7 @@ def run_sharded(args):
                      "kernel_ms": 1e3 * sec, "alg_bytes_per_launch": byts, "plan": bt0.plan()},
     }
     out["roofline"].update(pmc_fields(C5_KERNEL, "r*_c5_*.json", sec))
+    out["roofline"]["limiter"] = pmc_limiter(C5_KERNEL, "r*_c5_*_pmc.txt")
     if not args.no_parity:
         out["parity"] = sharded_parity(args, d, U, B, D, passes, ex_x, ex_y)
     if d.rank == 0:
