@@ -604,10 +604,12 @@ def run_sharded(args):
         passes.append(("business", G.batch(ex_y, ex_x), 7 if getattr(args, "fix_adamic", False) else 3))
     for name, bt, _ in passes:
         log("plan %s: %s" % (name, bt.plan()))
-    # both passes as one concurrent step (blp_batches_score: each chunk-parallel grid on its share
-    # of the CUs); --serial-passes: one after the other
+    # each pass on its own stream (they overlap where the grids leave room); --cosched-passes:
+    # blp_batches_score with BLP_SPLIT_COSCHED=1 holds each chunk-parallel grid to a CU share
+    # (measured slower: 1951 / 864 / 903 ms at proportional / 176 / 128 user CUs against 743 ms,
+    # profiles/r03_bench_sharded_c5_cosched*.json)
     def step():
-        if len(passes) > 1 and not args.serial_passes:
+        if len(passes) > 1 and args.cosched_passes:
             G.score_batches([(bt, mask) for _, bt, mask in passes])
         else:
             for _, bt, mask in passes:
@@ -877,7 +879,7 @@ def main():
                          "top-k; svd: config 4 rank-64 truncated-SVD scorer; sharded: config 5 row-block "
                          "sharded ingest + RCCL all-gather, then rank-local scoring (--config c5); e2e: "
                          "similarity.main from graph.txt to the 6 files (--config yelp = config 1, or c2)")
-    ap.add_argument("--serial-passes", action="store_true", help="--mode sharded: score the passes one after the other")
+    ap.add_argument("--cosched-passes", action="store_true", help="--mode sharded: both passes through blp_batches_score")
     ap.add_argument("--parity-sources", type=int, default=50,
                     help="--mode sharded: sampled sources per side and rank checked against the C oracle")
     ap.add_argument("--no-collective-at-world1", action="store_true",

@@ -3547,13 +3547,14 @@ int blp_batches_score(blp_graph* g, int n, blp_batch* const* bs, const uint32_t*
     share = std::max(g->n_cu / 2, std::min(g->n_cu, (int)std::lround(f * g->n_cu / 8.0) * 8));
   }
   if (const char* e = getenv("BLP_COSCHED_CUS")) share = atoi(e);  // tuning knob
-  // chunk-parallel batches side by side (config 5's two passes): each persistent grid on a share
-  // of the CUs in proportion to its planned elements, so both run at once (BLP_SPLIT_COSCHED=0: off)
+  // chunk-parallel batches side by side (config 5's two passes), opt-in (BLP_SPLIT_COSCHED=1): each
+  // persistent grid on a share of the CUs in proportion to its planned elements. Measured slower
+  // than the two grids each on the whole chip (1951 ms per config-5 step against 743 ms).
   int n_split = 0;
   double w_split = 0.0;
   for (int i = 0; i < n; ++i)
     if (bs[i]->split) ++n_split, w_split += (double)bs[i]->work_elems + 1.0;
-  const bool split_share = n_split >= 2 && !(getenv("BLP_SPLIT_COSCHED") && atoi(getenv("BLP_SPLIT_COSCHED")) == 0);
+  const bool split_share = n_split >= 2 && getenv("BLP_SPLIT_COSCHED") && atoi(getenv("BLP_SPLIT_COSCHED")) != 0;
   for (int i = 0; i < n; ++i) {
     blp_batch* b = bs[i];
     b->cus = is_large(b) && t_other > 0.0 ? share : 0;

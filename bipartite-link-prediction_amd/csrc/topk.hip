@@ -1254,7 +1254,7 @@ static TkArgs topk_args(blp_topk* t, int k, uint32_t mask) {
   a.dw_info = t->dw_n ? t->dw_info.as<long long>() : nullptr;
   a.dw_caf = t->dw_n && (mask & BLP_ADAMIC) && t->dw_caf.p ? t->dw_caf.as<unsigned long long>() : nullptr;
   a.dw_n = (int)t->dw_n;
-  a.dw_max = (int)std::max<int64_t>(1, env_i64("BLP_TOPK_DENSE_MAX", 8));
+  a.dw_max = (int)std::max<int64_t>(1, env_i64("BLP_TOPK_DENSE_MAX", 4));
   if (a.H > 0 && !a.dw_ca) a.dw_n = 0;  // counts without their AA words: walk every target
   a.dw_words = t->dw_words;
   a.dw_bmw = t->dw_bmw;
@@ -1422,11 +1422,11 @@ extern "C" int blp_topk_create(blp_graph* g, int64_t src_lo, int64_t src_hi, int
     return rc;
   }
   // dense counts of the hot targets (header comment): the prefix of the degree order whose
-  // members' rows hold at least BLP_TOPK_DENSE_F (2) times the counter words, within
+  // members' rows hold at least BLP_TOPK_DENSE_F (8) times the counter words, within
   // BLP_TOPK_DENSE_MB (1024) of HBM and 256 targets; one counter chunk only (BLP_TOPK_NO_DENSE=1: off)
   if (t->chunks.size() == 1 && T > 0 && !env_i64("BLP_TOPK_NO_DENSE", 0)) {
     const int64_t words = chunk_words(t, 0, T);
-    const double f = getenv("BLP_TOPK_DENSE_F") ? atof(getenv("BLP_TOPK_DENSE_F")) : 2.0;
+    const double f = getenv("BLP_TOPK_DENSE_F") ? atof(getenv("BLP_TOPK_DENSE_F")) : 8.0;
     const int64_t bmw = ((src_hi - src_lo + 31) / 32 + 3) / 4 * 4;
     const int64_t hw = t->have_aa ? 2 * t->H : 0;  // u64 AA words per target
     const int64_t per = 4 * words + 8 * hw + 4 * bmw;
