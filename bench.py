@@ -480,11 +480,13 @@ def run_topk(args):
     a, b = synth.review_edges(U, B, D, seed=0)
     G = blp.DeviceGraph(a, b, device=dev)
     del a, b
-    log("graph: %d nodes, %d unique edges, built in %.1fs" % (G.n, G.nnz // 2, time.time() - t0))
+    graph_s = time.time() - t0
+    log("graph: %d nodes, %d unique edges, built in %.1fs" % (G.n, G.nnz // 2, graph_s))
     G.n_users_hint = U  # the same users make_examples samples for config 2
     src = synth.sample_users(G, args.users, seed=dist.rank)
     t0 = time.time()
-    T = TopK(G, "user")
+    T = TopK(G, "user")  # the handle's graph indexes: permuted rows, wedge rows, hot-target dense counts
+    create_s = time.time() - t0
     T.set_sources(src)
     log("top-k engine: %s in %.1fs" % (T.info(), time.time() - t0))
     mask = args.topk_mask
@@ -526,6 +528,9 @@ def run_topk(args):
                      "limiter": pmc_limiter("k_topk", "r*_topk_*_pmc.txt")},
         "work": {"sum_h2": h2_sum, "sum_push": push_sum, "pushed": pushed, "dense_target_adds": dense_adds,
                  "aa_hash_sources": hash_src, "aa_direct_sources": direct_src},
+        # off the clock, once per graph (independent of the sources): the synthetic graph and the
+        # top-k handle (permuted rows, wedge rows, the hot targets' dense counts)
+        "setup_s": {"graph_build": round(graph_s, 3), "topk_create": round(create_s, 3)},
     }
     if dist.rank == 0 and not args.no_parity and mask == blp.JACCARD | blp.ADAMIC:
         cols_j, sc_j, _ = T.fetch("jaccard")
