@@ -96,6 +96,15 @@ struct KernelTimer {
 
 namespace blp {
 constexpr int64_t CI_PAD = 16;  // ids of zero padding before and after d_ci / d_ci_w
+
+// The id sets of a graph's long wedge rows over [lo, hi): bit i of a slot = id lo + i; words
+// rounded to whole 16-byte vectors; slot[x] (device, and its host copy) = x's slot or -1.
+struct WedgeBitmaps {
+  int64_t lo = 0, hi = 0, words = 0, slots = 0;
+  int32_t* d_slot = nullptr;
+  uint32_t* d_pool = nullptr;
+  std::vector<int32_t> h_slot;
+};
 }
 
 struct blp_graph {
@@ -126,11 +135,10 @@ struct blp_graph {
   int32_t* d_wedge = nullptr;
   int64_t wedge_vecs = 0;
   std::vector<int64_t> h_wp;  // host copy of d_wp (heavy-source planning)
-  // wedge-row bitmaps (hop3.hip): the SET of ids of a long wedge row over the hop-3 mark range
-  // [wbm_lo, wbm_hi), built on the first hop-3 call that needs them; d_wbm_slot[x] = slot or -1
-  int32_t* d_wbm_slot = nullptr;
-  uint32_t* d_wbm_pool = nullptr;  // [slots][wbm_words]
-  int64_t wbm_lo = 0, wbm_hi = 0, wbm_words = 0, wbm_slots = 0;
+  // wedge-row bitmaps (hop3.hip, blp::wedge_bitmaps): the SET of ids of each long wedge row over
+  // an id range [lo, hi), built on first use per range (the hop-3 mark range; the business
+  // batch's universe) and kept with the graph (at most 4 ranges)
+  std::vector<blp::WedgeBitmaps> wbm;
   // host mirrors used for launch planning (bitmap universe bounds) and the host-built indexes:
   // owned copies (blp_graph_create), or the caller's buffers (blp_graph_create_from_csr, which
   // requires them to outlive the handle)
@@ -157,6 +165,9 @@ constexpr int SHORT_ROW_MAX = 32;  // the short-row scorer's row bound (pairs.hi
 int build_hot_index(blp_graph* g);
 int graph_finish(blp_graph* g, const double* aaw);
 int build_wedge_index(blp_graph* g);
+// the graph's wedge-row bitmaps over [lo, hi) (built and cached on first use); null with *rc == 0
+// when there is no wedge index or no cache slot left
+const WedgeBitmaps* wedge_bitmaps(blp_graph* g, int64_t lo, int64_t hi, int* rc);
 void free_wedge_index(blp_graph* g);
 void free_hot_index(blp_graph* g);
 int timer_begin(blp_graph* g, int k, hipEvent_t* start);

@@ -419,49 +419,59 @@ __global__ __launch_bounds__(HW_BLOCK) void k_wbm_fill(const int64_t* __restrict
 
 using namespace blp;
 
-// Build (or reuse) the graph's wedge-row bitmaps over [lo3, hi3): rows of at least
-// BLP_WBM_MIN_X (default 1) times their bitmap's words, longest first, within BLP_WBM_MB of HBM
-// (default 2048). Enqueued on the graph stream; returns with the fill kernel queued.
-static int ensure_wedge_bitmaps(blp_graph* g, int64_t lo3, int64_t hi3) {
-  const int64_t words = (((hi3 - lo3) + 31) / 32 + 3) / 4 * 4;
-  if (g->wbm_words && g->wbm_lo == lo3 && g->wbm_hi == hi3) return BLP_OK;
-  if (g->d_wbm_slot) (void)hipFree(g->d_wbm_slot);
-  if (g->d_wbm_pool) (void)hipFree(g->d_wbm_pool);
-  g->d_wbm_slot = nullptr;
-  g->d_wbm_pool = nullptr;
-  g->wbm_slots = 0;
+// The graph's wedge-row bitmaps over [lo, hi) (blp_internal.h), built on first use: rows of at
+// least BLP_WBM_MIN_X (default 1) times their bitmap's words, longest first, within BLP_WBM_MB of
+// HBM (default 2048) per range; at most 4 ranges are kept per graph.
+namespace blp {
+const WedgeBitmaps* wedge_bitmaps(blp_graph* g, int64_t lo, int64_t hi, int* rc) {
+  *rc = BLP_OK;
+  if (!g->d_wp || hi <= lo) return nullptr;
+  for (const WedgeBitmaps& w : g->wbm)
+    if (w.lo == lo && w.hi == hi) return &w;
+  if (g->wbm.size() >= 4) return nullptr;
+  g->wbm.reserve(4);  // entries never move: batches keep their device pointers
+  const int64_t words = (((hi - lo) + 31) / 32 + 3) / 4 * 4;
   const double min_x = getenv("BLP_WBM_MIN_X") ? atof(getenv("BLP_WBM_MIN_X")) : 1.0;
   const int64_t budget = (getenv("BLP_WBM_MB") ? atoll(getenv("BLP_WBM_MB")) : 2048) << 20;
-  std::vector<std::pair<int64_t, int32_t>> rows;  // (ids, b)
-  for (int64_t b = 0; b < g->n; ++b) {
-    const int64_t ids = 4 * (g->h_wp[b + 1] - g->h_wp[b]);
-    if (ids > 0 && (double)ids >= min_x * (double)words) rows.push_back({-ids, (int32_t)b});
+  std::vector<std::pair<int64_t, int32_t>> rows;  // (-ids, x)
+  for (int64_t x = 0; x < g->n; ++x) {
+    const int64_t ids = 4 * (g->h_wp[x + 1] - g->h_wp[x]);
+    if (ids > 0 && (double)ids >= min_x * (double)words) rows.push_back({-ids, (int32_t)x});
   }
   std::sort(rows.begin(), rows.end());
   rows.resize((size_t)std::min<int64_t>((int64_t)rows.size(), budget / (4 * words)));
-  g->wbm_lo = lo3;
-  g->wbm_hi = hi3;
-  g->wbm_words = words;
-  if (rows.empty()) return BLP_OK;
-  std::vector<int32_t> slot((size_t)g->n, -1), order(rows.size());
+  g->wbm.emplace_back();
+  WedgeBitmaps& w = g->wbm.back();
+  w.lo = lo;
+  w.hi = hi;
+  w.words = words;
+  if (rows.empty()) return &w;
+  w.h_slot.assign((size_t)g->n, -1);
+  std::vector<int32_t> order(rows.size());
   for (size_t i = 0; i < rows.size(); ++i) {
-    slot[rows[i].second] = (int32_t)i;
+    w.h_slot[rows[i].second] = (int32_t)i;
     order[i] = rows[i].second;
   }
   int32_t* d_rows = nullptr;
-  BLP_HIP(hipMalloc(&g->d_wbm_slot, 4 * (size_t)g->n));
-  BLP_HIP(hipMalloc(&g->d_wbm_pool, 4 * (size_t)words * rows.size()));
-  BLP_HIP(hipMalloc(&d_rows, 4 * rows.size()));
-  BLP_HIP(hipMemcpy(g->d_wbm_slot, slot.data(), 4 * (size_t)g->n, hipMemcpyHostToDevice));
-  BLP_HIP(hipMemcpy(d_rows, order.data(), 4 * order.size(), hipMemcpyHostToDevice));
+  auto hip = [&](hipError_t e, const char* what) {
+    if (e != hipSuccess) *rc = hip_fail(e, what, __FILE__, __LINE__);
+    return e == hipSuccess;
+  };
+  if (!hip(hipMalloc(&w.d_slot, 4 * (size_t)g->n), "hipMalloc") ||
+      !hip(hipMalloc(&w.d_pool, 4 * (size_t)words * rows.size()), "hipMalloc (wedge bitmaps)") ||
+      !hip(hipMalloc(&d_rows, 4 * rows.size()), "hipMalloc") ||
+      !hip(hipMemcpy(w.d_slot, w.h_slot.data(), 4 * (size_t)g->n, hipMemcpyHostToDevice), "hipMemcpy") ||
+      !hip(hipMemcpy(d_rows, order.data(), 4 * order.size(), hipMemcpyHostToDevice), "hipMemcpy"))
+    return nullptr;
   hipLaunchKernelGGL(k_wbm_fill, dim3((unsigned)rows.size()), dim3(HW_BLOCK), 4 * (size_t)words, g->stream,
-                     (const int64_t*)g->d_wp, (const uint4*)g->d_wedge, d_rows, lo3, hi3 - lo3, (int)words, g->d_wbm_pool);
-  BLP_HIP(hipGetLastError());
-  BLP_HIP(hipStreamSynchronize(g->stream));
-  BLP_HIP(hipFree(d_rows));
-  g->wbm_slots = (int64_t)rows.size();
-  return BLP_OK;
+                     (const int64_t*)g->d_wp, (const uint4*)g->d_wedge, d_rows, lo, hi - lo, (int)words, w.d_pool);
+  if (!hip(hipGetLastError(), "k_wbm_fill launch") || !hip(hipStreamSynchronize(g->stream), "hipStreamSynchronize"))
+    return nullptr;
+  (void)hipFree(d_rows);
+  w.slots = (int64_t)rows.size();
+  return &w;
 }
+}  // namespace blp
 
 extern "C" int blp_hop3_sample(blp_graph* g, const int32_t* src, int64_t n_src, const int32_t* pos_off,
                                const int32_t* pos_y, double rate, uint64_t seed, int32_t* out_x, int32_t* out_y,
@@ -563,11 +573,12 @@ extern "C" int blp_hop3_sample(blp_graph* g, const int32_t* src, int64_t n_src, 
   if ((rc = timer_begin(g, K_HOP3, &t0))) return cleanup(), rc;
   if (n_src && wedge) {
     if (!getenv("BLP_HOP3_NO_WBM")) {
-      if ((rc = ensure_wedge_bitmaps(g, lo3, hi3))) return cleanup(), rc;
-      if (g->wbm_slots) {
-        a.wbm_slot = g->d_wbm_slot;
-        a.wbm_pool = (const uint4*)g->d_wbm_pool;
-        a.wbm_vecs = (int)(g->wbm_words / 4);
+      const WedgeBitmaps* w = wedge_bitmaps(g, lo3, hi3, &rc);
+      if (rc) return cleanup(), rc;
+      if (w && w->slots) {
+        a.wbm_slot = w->d_slot;
+        a.wbm_pool = (const uint4*)w->d_pool;
+        a.wbm_vecs = (int)(w->words / 4);
       }
     }
     const size_t dyn = 16 * (size_t)std::max<int64_t>(w3v, 1);

@@ -2773,6 +2773,8 @@ struct blp_batch {
   // heavy sources (planned at create)
   int32_t* d_heavy_slot = nullptr;
   uint32_t* d_heavy_bm = nullptr;
+  const int32_t* wbm_slot = nullptr;  // the graph's wedge-row bitmaps over [lo, hi) (or null):
+  const uint32_t* wbm_pool = nullptr; // used as pre-built bitmaps in place of k_heavy's
   HeavyItem* d_heavy_items = nullptr;
   int64_t n_heavy = 0, n_heavy_items = 0, hb_words = 0;
   int64_t lo = 0, hi = 0;
@@ -3097,6 +3099,28 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   }
   b->n_heavy_items = (int64_t)items.size();
   b->hb_words = ((span + 31) / 32 + 3) / 4 * 4;
+  // ---- the graph's wedge-row bitmaps (hop3.hip) over this universe: a source whose wedge row is
+  // at least as long as its bitmap's words copies the bitmap (its id set, 12.5 KB at config 2)
+  // instead of OR-ing the row id by id -- the same slots and copy as k_heavy's pre-built bitmaps,
+  // so those sources need no per-step k_heavy either (BLP_NO_WBM_BATCH=1: off)
+  if (wedge_items && b->chunks == 1 && span > 0 && !b->global && !b->split && !b->wave && !getenv("BLP_NO_WBM_BATCH")) {
+    int rcw = BLP_OK;
+    const WedgeBitmaps* w = wedge_bitmaps(g, lo, hi, &rcw);
+    if (rcw) return bail(rcw);
+    if (w && w->slots && w->words == b->hb_words) {
+      bool covered = true;  // every planned heavy source has a bitmap (the longest rows do)
+      for (size_t i = 0; i < srcs.size() && covered; ++i)
+        covered = heavy_slot.empty() || heavy_slot[srcs[i]] < 0 || w->h_slot[srcs[i]] >= 0;
+      if (covered) {
+        b->wbm_slot = w->d_slot;
+        b->wbm_pool = w->d_pool;
+        b->n_heavy = 0;
+        b->n_heavy_items = 0;
+        items.clear();
+        heavy_slot.clear();
+      }
+    }
+  }
   // ---- grouping geometry: buckets of 2^shift node ids, at most NB_MAX buckets
   {
     // buckets cover the sources' id range [xlo, xhi): ~2K buckets of 2^shift ids each
@@ -3424,8 +3448,8 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   a.hot_idx = b->use_hot ? g->d_hot_idx : nullptr;
   a.hot_tab = (const HotRow*)g->d_hot_tab;
   a.hot_pool = (const uint4*)g->d_hot_pool;
-  a.heavy_slot = b->d_heavy_slot;
-  a.heavy_bm = b->d_heavy_bm;
+  a.heavy_slot = b->wbm_slot ? b->wbm_slot : b->d_heavy_slot;
+  a.heavy_bm = b->wbm_slot ? const_cast<uint32_t*>(b->wbm_pool) : b->d_heavy_bm;
   a.hb_words = b->hb_words;
   a.misc = b->d_misc;
   a.cn = b->d_cn;
@@ -3494,7 +3518,7 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
     }
     if (b->d_rec) {  // one record per active source (after grouping, on the batch stream)
       hipLaunchKernelGGL(k_source_records, dim3((unsigned)std::min<int64_t>((b->n_sources + 255) / 256, 2048)),
-                         dim3(256), 0, b->stream, a.active, b->d_misc, a.off, a.cnt, g->d_rp, g->d_ci, b->d_heavy_slot,
+                         dim3(256), 0, b->stream, a.active, b->d_misc, a.off, a.cnt, g->d_rp, g->d_ci, a.heavy_slot,
                          a.wp, b->d_rec);
       BLP_HIP(hipGetLastError());
       a.rec = b->d_rec;

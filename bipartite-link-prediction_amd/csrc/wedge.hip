@@ -131,11 +131,11 @@ void free_wedge_index(blp_graph* g) {
   g->d_wedge = nullptr;
   g->wedge_vecs = 0;
   g->h_wp.clear();
-  if (g->d_wbm_slot) (void)hipFree(g->d_wbm_slot);
-  if (g->d_wbm_pool) (void)hipFree(g->d_wbm_pool);
-  g->d_wbm_slot = nullptr;
-  g->d_wbm_pool = nullptr;
-  g->wbm_lo = g->wbm_hi = g->wbm_words = g->wbm_slots = 0;
+  for (WedgeBitmaps& w : g->wbm) {
+    if (w.d_slot) (void)hipFree(w.d_slot);
+    if (w.d_pool) (void)hipFree(w.d_pool);
+  }
+  g->wbm.clear();
 }
 
 }  // namespace blp

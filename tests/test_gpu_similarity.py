@@ -146,6 +146,9 @@ def test_general_graph_exact_distance(gpu):
     {"BLP_WEDGE": "0", "BLP_HEAVY_WORK": "50"},         # graph built without wedge rows
     {"BLP_WEDGE_MAX_X": "0.5"},                         # wedge rows over budget: not built
     {"BLP_HEAVY_WORK": "7"},                            # wedge slices of 1 vector, uneven tails
+    {"BLP_HEAVY_WORK": "7", "BLP_NO_WBM_BATCH": "1"},   # ... through k_heavy, not the graph's wedge-row bitmaps
+    {"BLP_NO_WBM_BATCH": "1"},                          # every business source built from its wedge row
+    {"BLP_WBM_MIN_X": "40"},                            # bitmaps for the longest wedge rows only
     {"BLP_SPLIT": "3", "BLP_SPLIT_BIG": "1", "BLP_HASH_WORK": "600"},  # hash-set scorer for light sources, split for the rest
     {"BLP_SPLIT": "2", "BLP_SPLIT_BIG": "1", "BLP_HASH_WORK": "100000"},  # every source on the hash-set scorer (knob clamped to HT - 1)
     {"BLP_SPLIT": "4", "BLP_HASH_WORK": "400"},          # ... beside the 64 KiB chunk scorer
