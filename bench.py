@@ -1005,9 +1005,9 @@ def main():
                        # the counters' HBM-side bytes over the same kernel time: what DRAM actually moved
                        **pmc_fields(kname, "r*_v*_bench.json", sec),
                        "kernel": "%s (%s side)" % (kname, name0), "alg_bytes_per_launch": byts,
-                       # what the counters name as the bound ("What bounds the user scorer")
-                       "limiter": "latency: waves wait 56% of cycles; VALU <= 53%, LDS 34% busy (45% of it bank "
-                                  "conflicts), L2 hit 17%, DRAM side 0.32 of peak (profiles/r02_v4_bench_pmc.txt)"}
+                       # what the counters name as the bound ("What bounds the user scorer"),
+                       # from the newest committed counter summary of this kernel
+                       "limiter": pmc_limiter(kname, "r*_v*_bench_pmc.txt")}
     if dist.rank == 0 and args.sides == "both" and not (args.no_parity and args.no_cpu_baseline):
         import coracle
 
