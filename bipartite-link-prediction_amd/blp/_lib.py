@@ -68,7 +68,8 @@ SIGNATURES = {
     "blp_batch_plan": [_P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
                        ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
                        ctypes.POINTER(ctypes.c_int)],
-    "blp_batch_routes": [_P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int)],
+    "blp_batch_routes": [_P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int),
+                         ctypes.POINTER(ctypes.c_int)],
     "blp_batch_stats": [_P, _I32, _DP, ctypes.POINTER(ctypes.c_int64)],
     "blp_batch_stats_reset": [_P],
     "blp_hop3_sample": [_P, _P, _I64, _P, _P, ctypes.c_double, ctypes.c_uint64, _P, _P, _P, _I64,

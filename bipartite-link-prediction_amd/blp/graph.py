@@ -447,10 +447,12 @@ class PairBatch:
         ch, blk, hv = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         check(lib().blp_batch_plan(self.handle, ctypes.byref(lo), ctypes.byref(hi), ctypes.byref(ch),
                                    ctypes.byref(blk), ctypes.byref(hv)))
-        ns, nh, runs = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int()
-        check(lib().blp_batch_routes(self.handle, ctypes.byref(ns), ctypes.byref(nh), ctypes.byref(runs)))
+        ns, nh, runs, wbm = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int(), ctypes.c_int()
+        check(lib().blp_batch_routes(self.handle, ctypes.byref(ns), ctypes.byref(nh), ctypes.byref(runs),
+                                     ctypes.byref(wbm)))
         return {"lo": lo.value, "hi": hi.value, "chunks": ch.value, "block": blk.value, "heavy": hv.value,
-                "sources": ns.value, "hash_sources": nh.value, "runs": bool(runs.value)}
+                "sources": ns.value, "hash_sources": nh.value, "runs": bool(runs.value),
+                "wedge_bitmaps": bool(wbm.value)}
 
     def score(self, mask=7):
         check(lib().blp_batch_score(self.graph.handle, self.handle, mask))

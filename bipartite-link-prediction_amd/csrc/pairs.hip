@@ -3256,11 +3256,12 @@ int blp_batch_plan(const blp_batch* b, int64_t* lo, int64_t* hi, int* chunks, in
   return BLP_OK;
 }
 
-int blp_batch_routes(const blp_batch* b, int64_t* n_sources, int64_t* n_hash, int* runs) {
+int blp_batch_routes(const blp_batch* b, int64_t* n_sources, int64_t* n_hash, int* runs, int* wedge_bitmaps) {
   BLP_CHECK(b, BLP_E_ARG, "blp_batch_routes: null batch");
   if (n_sources) *n_sources = b->n_sources;
   if (n_hash) *n_hash = b->n_hash;
   if (runs) *runs = b->runs ? 1 : 0;
+  if (wedge_bitmaps) *wedge_bitmaps = b->wbm_slot ? 1 : 0;
   return BLP_OK;
 }
 

@@ -203,8 +203,9 @@ int blp_batches_score(blp_graph* g, int n, blp_batch* const* batches, const uint
 int blp_batch_plan(const blp_batch* b, int64_t* lo, int64_t* hi, int* chunks, int* block,
                    int* heavy);
 /* Source routing of the plan: distinct sources, those on the hash-set scorer (chunk-parallel
- * batches; else 0), and 1 if the pairs arrive grouped by source (run-head grouping).       */
-int blp_batch_routes(const blp_batch* b, int64_t* n_sources, int64_t* n_hash, int* runs);
+ * batches; else 0), 1 if the pairs arrive grouped by source (run-head grouping), and 1 if long
+ * sources copy the graph's wedge-row bitmaps as pre-built H2 sets (short-row batches).      */
+int blp_batch_routes(const blp_batch* b, int64_t* n_sources, int64_t* n_hash, int* runs, int* wedge_bitmaps);
 
 /* Per-batch device time of the last/accumulated blp_batch_score calls (HIP events on the
  * batch stream): which 0 = scorer kernel, 1 = grouping kernels. Reset with blp_batch_stats_reset. */

@@ -165,7 +165,10 @@ def test_kernel_paths_vs_oracle(gpu, knobs, monkeypatch):
     _check_against_oracle(a, b, x, y)
     _check_against_oracle(a, b, y, x)
     if "BLP_HEAVY_WORK" in knobs and "BLP_CHUNK_BITS" not in knobs:
-        assert G.batch(y, x).plan()["heavy"] > 0
+        plan = G.batch(y, x).plan()  # heavy business sources: k_heavy, or the graph's wedge-row bitmaps
+        assert plan["heavy"] > 0 or plan["wedge_bitmaps"]
+        if "BLP_NO_WBM_BATCH" in knobs:
+            assert plan["heavy"] > 0 and not plan["wedge_bitmaps"]
     if "BLP_FORCE_GLOBAL" in knobs or ("BLP_CHUNK_BITS" in knobs and "BLP_NO_GLOBAL" not in knobs):
         assert G.batch(x, y).plan()["chunks"] == 0  # HBM-bitmap scorer
     if "BLP_SPLIT" in knobs:
