@@ -2201,9 +2201,28 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
     const int64_t c0 = a.lo + (int64_t)c * CAP_BITS;
     const int64_t width = max<int64_t>(min(a.hi, c0 + CAP_BITS) - c0, 0);
     const int nw4 = (int)((((width + 31) >> 5) + 3) >> 2);
+    const int64_t wb = a.wp ? a.wp[x] : 0, we = a.wp ? a.wp[x + 1] : 0;
     if (hslot >= 0) {
       const uint4* src4 = reinterpret_cast<const uint4*>(a.heavy_bm + (int64_t)hslot * a.hb_words + ((c0 - a.lo) >> 5));
       for (int i = threadIdx.x; i < nw4; i += BLOCK) bm4[i] = src4[i];
+      __syncthreads();
+    } else if (we > wb) {
+      // x's wedge row (wedge.hip: N(N(x)) back to back, a source whose members' rows are short,
+      // i.e. the business side): one contiguous stream filtered to this chunk, instead of a
+      // row_ptr and two split-table lookups per member for a ~10-id slice
+      for (int i = threadIdx.x; i < nw4; i += BLOCK) bm4[i] = make_uint4(0, 0, 0, 0);
+      __syncthreads();
+      const uint32_t keep = a.idmask | 0x80000000u, c0u = (uint32_t)c0, wu = (uint32_t)width;
+      for (int64_t q = wb + threadIdx.x; q < we; q += 2 * BLOCK) {
+        const uint4 v0 = a.wedge[q];
+        const uint4 v1 = q + BLOCK < we ? a.wedge[q + BLOCK] : v0;  // (a repeat ORs nothing new)
+        const uint32_t ids[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const uint32_t r = in_chunk((int)ids[k], keep, c0u);
+          if (r < wu) atomicOr(&bm[r >> 5], 1u << (r & 31));
+        }
+      }
       __syncthreads();
     } else {
       if (threadIdx.x == 0) s_nhot = 0;
@@ -2488,34 +2507,49 @@ __global__ __launch_bounds__(BLOCK) void k_score_hash(ScoreArgs a, const uint8_t
     if (!hflag[x - xlo]) continue;  // uniform: the chunk-parallel scorer takes it
     for (int i = threadIdx.x; i < HT / 4; i += BLOCK) reinterpret_cast<uint4*>(tab)[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
     __syncthreads();
-    // build: one row N(z) per thread, 16 ids at a time (rows padded past nnz)
+    // build: one row N(z) per thread, 16 ids at a time (rows padded past nnz), or x's wedge row
+    // (N(N(x)) back to back, wedge.hip) 4 ids per 16-byte load over the whole workgroup
     const int64_t xb = a.rp[x], xe = a.rp[x + 1];
     unsigned long long added = 0;
-    for (int64_t k = xb + threadIdx.x; k < xe; k += BLOCK) {
-      const int z = a.ci[k];
-      const int64_t st = a.rp[z];
-      const int len = (int)(a.rp[z + 1] - st);
-      for (int h0 = 0; h0 < len; h0 += SHORT_PART) {
-        int e[SHORT_PART];
-        row_part(a.cw, st, len, h0, e);
+    auto insert = [&](uint32_t v) {
+      uint32_t h = hs_slot<HT>(v);
+      for (;;) {
+        const uint32_t t = tab[h];
+        if (t == v) break;
+        if (t == HS_EMPTY) {
+          const uint32_t old = atomicCAS(&tab[h], HS_EMPTY, v);
+          if (old == HS_EMPTY) {
+            ++added;
+            break;
+          }
+          if (old == v) break;
+        }
+        h = (h + 1) & (HT - 1);
+      }
+    };
+    const int64_t wb = a.wp ? a.wp[x] : 0, we = a.wp ? a.wp[x + 1] : 0;
+    if (we > wb) {
+      for (int64_t q = wb + threadIdx.x; q < we; q += BLOCK) {
+        const uint4 v4 = a.wedge[q];
+        const uint32_t ids[4] = {v4.x, v4.y, v4.z, v4.w};
 #pragma unroll
-        for (int j = 0; j < SHORT_PART; ++j) {
-          const uint32_t v = in_chunk(e[j], keep, c0u);
-          if (h0 + j < len && v < wu) {
-            uint32_t h = hs_slot<HT>(v);
-            for (;;) {
-              const uint32_t t = tab[h];
-              if (t == v) break;
-              if (t == HS_EMPTY) {
-                const uint32_t old = atomicCAS(&tab[h], HS_EMPTY, v);
-                if (old == HS_EMPTY) {
-                  ++added;
-                  break;
-                }
-                if (old == v) break;
-              }
-              h = (h + 1) & (HT - 1);
-            }
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t v = in_chunk((int)ids[j], keep, c0u);
+          if (v < wu) insert(v);
+        }
+      }
+    } else {
+      for (int64_t k = xb + threadIdx.x; k < xe; k += BLOCK) {
+        const int z = a.ci[k];
+        const int64_t st = a.rp[z];
+        const int len = (int)(a.rp[z + 1] - st);
+        for (int h0 = 0; h0 < len; h0 += SHORT_PART) {
+          int e[SHORT_PART];
+          row_part(a.cw, st, len, h0, e);
+#pragma unroll
+          for (int j = 0; j < SHORT_PART; ++j) {
+            const uint32_t v = in_chunk(e[j], keep, c0u);
+            if (h0 + j < len && v < wu) insert(v);
           }
         }
       }
@@ -3468,6 +3502,10 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
     // slices of <= short_max ids scanned by their pair's thread (128 KiB chunks; BLP_SPLIT_SHORT=0: off)
     const int short_max = std::min(SHORT_PART, getenv("BLP_SPLIT_SHORT") ? atoi(getenv("BLP_SPLIT_SHORT")) : SHORT_PART);
     a.sched = getenv("BLP_SPLIT_ONEQ") ? 1 : 0;  // k_score_split: 1 = one global item queue (no XCD groups)
+    if (g->d_wp && !getenv("BLP_NO_WEDGE")) {  // sources with wedge rows build from them (split and hash kernels)
+      a.wp = g->d_wp;
+      a.wedge = reinterpret_cast<const uint4*>(g->d_wedge);
+    }
     const int scu = b->cus > 0 ? b->cus : g->n_cu;  // CUs the persistent grids may fill (blp_batches_score)
     if (b->d_hflag) {  // small-H2 sources first, on their own hash-set kernel
       int hcu = 1;

@@ -65,6 +65,64 @@ __global__ __launch_bounds__(WF_BLOCK) void k_wedge_fill(const int64_t* __restri
   }
 }
 
+// Large graphs (config 5: 2M businesses, 21G wedge ids): one workgroup per node would leave
+// the most reviewed business (11.6M members) on one workgroup for seconds. Items of at most
+// WF_ITEM members of one node instead, each reserving its rows' space in the node's range with
+// one device atomic (cursor[x]): the rows of a node land in item order, which the bitmap builds
+// do not see. k_wedge_pad then repeats the node's first id through its last vector.
+constexpr int WF_ITEM = 4096;
+struct WedgeItem {
+  int64_t k0;   // first CSR entry (member) of the item
+  int32_t x;    // node
+  int32_t cnt;  // members (<= WF_ITEM)
+};
+
+__global__ __launch_bounds__(WF_BLOCK) void k_wedge_fill_items(const int64_t* __restrict__ rp, const int32_t* __restrict__ ci,
+                                                               const int64_t* __restrict__ wp, const WedgeItem* __restrict__ items,
+                                                               int64_t n_items, unsigned long long* __restrict__ cursor,
+                                                               int32_t* __restrict__ w) {
+  __shared__ int red[WF_BLOCK / 64];
+  __shared__ long long s_base;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int64_t it = blockIdx.x; it < n_items; it += gridDim.x) {
+    const WedgeItem item = items[it];
+    for (int m0 = 0; m0 < item.cnt; m0 += WF_BLOCK) {
+      const int m = m0 + (int)threadIdx.x;
+      const bool in = m < item.cnt;
+      const int32_t z = in ? ci[item.k0 + m] : 0;
+      const int64_t zb = in ? rp[z] : 0;
+      const int d = in ? (int)(rp[z + 1] - zb) : 0;
+      int inc = d;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += t;
+      }
+      if (lane == 63) red[wid] = inc;
+      __syncthreads();
+      int before = 0, tot = 0;
+#pragma unroll
+      for (int q = 0; q < WF_BLOCK / 64; ++q) {
+        before += q < wid ? red[q] : 0;
+        tot += red[q];
+      }
+      if (threadIdx.x == 0) s_base = (long long)atomicAdd(&cursor[item.x], (unsigned long long)tot);
+      __syncthreads();
+      const int64_t at = 4 * wp[item.x] + s_base + before + inc - d;
+      for (int j = 0; j < d; ++j) w[at + j] = ci[zb + j];
+      __syncthreads();  // red / s_base are reused by the next round
+    }
+  }
+}
+
+__global__ void k_wedge_pad(const int64_t* __restrict__ wp, const unsigned long long* __restrict__ cursor, int64_t n,
+                            int32_t* __restrict__ w) {
+  for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < n; x += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = 4 * wp[x], e = 4 * wp[x + 1];
+    for (int64_t q = b + (int64_t)cursor[x]; q < e; ++q) w[q] = w[b];  // a repeat ORs nothing new
+  }
+}
+
 }  // namespace
 
 namespace blp {
@@ -76,9 +134,15 @@ int build_wedge_index(blp_graph* g) {
   const int64_t* rp = g->hrp;
   const int32_t* ci = g->hci;
   if (n == 0 || g->nnz == 0) return BLP_OK;
-  double max_x = 8.0;
+  // budget: BLP_WEDGE_MAX_X (16) x nnz ids, and at most 35 % of the free HBM
+  double max_x = 16.0;
   if (const char* e = getenv("BLP_WEDGE_MAX_X")) max_x = atof(e);
-  const double budget = std::min(max_x * (double)g->nnz, (double)(int64_t(1) << 34));
+  size_t free_b = 0, total_b = 0;
+  BLP_HIP(hipMemGetInfo(&free_b, &total_b));
+  const double budget = std::min(max_x * (double)g->nnz, 0.35 * (double)free_b);
+  // members' rows up to BLP_WEDGE_ROW_MAX (64) ids: the short-row scorer's sources (rows <=
+  // SHORT_ROW_MAX) always qualify; the chunk-parallel and hash-set scorers use any wedge row
+  const int64_t row_max = std::max<int64_t>(SHORT_ROW_MAX, getenv("BLP_WEDGE_ROW_MAX") ? atoll(getenv("BLP_WEDGE_ROW_MAX")) : 64);
   // per-node volume: one degree lookup per CSR entry, 16 threads (2B entries at config 5)
   const int nt = (int)std::max<unsigned>(1, std::min<unsigned>(16, std::thread::hardware_concurrency()));
   std::vector<int64_t> wp((size_t)n + 1, 0);  // per-node vector counts, then offsets
@@ -91,7 +155,7 @@ int build_wedge_index(blp_graph* g) {
           bool ok = true;
           for (int64_t k = rp[x]; k < rp[x + 1]; ++k) {
             const int64_t d = rp[ci[k] + 1] - rp[ci[k]];
-            if (d > SHORT_ROW_MAX) {
+            if (d > row_max) {
               ok = false;
               break;
             }
@@ -112,11 +176,44 @@ int build_wedge_index(blp_graph* g) {
   if (total == 0 || (double)(4 * total) > budget) return BLP_OK;
   // the rows themselves are gathered on the device from the CSR already there (435 MB at
   // config 2: a host fill and upload took ~0.2 s)
-  BLP_HIP(hipMalloc(&g->d_wp, sizeof(int64_t) * (n + 1)));
-  BLP_HIP(hipMalloc(&g->d_wedge, sizeof(int32_t) * 4 * total));
+  // an index that does not fit is skipped (every scorer also builds from the CSR)
+  if (hipMalloc(&g->d_wp, sizeof(int64_t) * (n + 1)) != hipSuccess ||
+      hipMalloc(&g->d_wedge, sizeof(int32_t) * 4 * total) != hipSuccess) {
+    (void)hipGetLastError();
+    if (g->d_wp) (void)hipFree(g->d_wp);
+    g->d_wp = nullptr;
+    g->d_wedge = nullptr;
+    return BLP_OK;
+  }
   BLP_HIP(hipMemcpy(g->d_wp, wp.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice));
-  hipLaunchKernelGGL(k_wedge_fill, dim3((unsigned)std::min<int64_t>(16384, n)), dim3(WF_BLOCK), 0, g->stream,
-                     g->d_rp, g->d_ci, g->d_wp, n, g->d_wedge);
+  int64_t max_deg = 0;
+  for (int64_t x = 0; x < n; ++x)
+    if (wp[x + 1] > wp[x]) max_deg = std::max<int64_t>(max_deg, rp[x + 1] - rp[x]);
+  if (max_deg <= 2 * WF_ITEM && !getenv("BLP_WEDGE_ITEMS")) {  // one workgroup per node
+    hipLaunchKernelGGL(k_wedge_fill, dim3((unsigned)std::min<int64_t>(16384, n)), dim3(WF_BLOCK), 0, g->stream,
+                       g->d_rp, g->d_ci, g->d_wp, n, g->d_wedge);
+  } else {  // items of <= WF_ITEM members (hub nodes)
+    std::vector<WedgeItem> items;
+    for (int64_t x = 0; x < n; ++x)
+      if (wp[x + 1] > wp[x])
+        for (int64_t k0 = rp[x]; k0 < rp[x + 1]; k0 += WF_ITEM)
+          items.push_back(WedgeItem{k0, (int32_t)x, (int32_t)std::min<int64_t>(WF_ITEM, rp[x + 1] - k0)});
+    WedgeItem* d_items = nullptr;
+    unsigned long long* d_cursor = nullptr;
+    BLP_HIP(hipMalloc(&d_items, sizeof(WedgeItem) * std::max<size_t>(items.size(), 1)));
+    BLP_HIP(hipMalloc(&d_cursor, 8 * (size_t)n));
+    BLP_HIP(hipMemcpy(d_items, items.data(), sizeof(WedgeItem) * items.size(), hipMemcpyHostToDevice));
+    BLP_HIP(hipMemsetAsync(d_cursor, 0, 8 * (size_t)n, g->stream));
+    hipLaunchKernelGGL(k_wedge_fill_items, dim3((unsigned)std::min<size_t>(65536, std::max<size_t>(items.size(), 1))),
+                       dim3(WF_BLOCK), 0, g->stream, g->d_rp, g->d_ci, g->d_wp, d_items, (int64_t)items.size(), d_cursor,
+                       g->d_wedge);
+    hipLaunchKernelGGL(k_wedge_pad, dim3((unsigned)std::min<int64_t>(8192, (n + 255) / 256)), dim3(256), 0, g->stream,
+                       g->d_wp, d_cursor, n, g->d_wedge);
+    BLP_HIP(hipGetLastError());
+    BLP_HIP(hipStreamSynchronize(g->stream));
+    (void)hipFree(d_items);
+    (void)hipFree(d_cursor);
+  }
   BLP_HIP(hipGetLastError());
   BLP_HIP(hipStreamSynchronize(g->stream));
   g->wedge_vecs = total;

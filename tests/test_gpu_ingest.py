@@ -202,13 +202,17 @@ def test_csr_build_host_entry_point(gpu):
     assert e.value.code == -1
 
 
-@pytest.mark.parametrize("device_csr", [False, True])
-def test_wedge_rows_equal_host_construction(gpu, device_csr, monkeypatch):
+@pytest.mark.parametrize("device_csr,items", [(False, False), (True, False), (True, True)])
+def test_wedge_rows_equal_host_construction(gpu, device_csr, items, monkeypatch):
     """The wedge-row index (gathered on the device, k_wedge_fill) equals its definition built
-    here from the CSR: for every node whose neighbours' rows all hold <= 32 ids, the rows N(z),
+    here from the CSR: for every node whose neighbours' rows all hold <= 64 ids, the rows N(z),
     z in N(x), back to back, padded to whole vectors with the last id. Businesses here have
-    ~400 neighbours, so one node spans several 256-neighbour rounds."""
+    ~400 neighbours, so one node spans several 256-neighbour rounds. items: the hub-node fill
+    (k_wedge_fill_items: items of <= 4096 members, rows of a node in item order, padding a
+    repeat of the node's first stored id) -- the same multiset per node."""
     monkeypatch.setenv("BLP_DEVICE_CSR_MIN", "1" if device_csr else str(1 << 40))
+    if items:
+        monkeypatch.setenv("BLP_WEDGE_ITEMS", "1")
     rng = np.random.default_rng(17)
     a, c = bipartite_edges(rng, 3000, 100, 40000)
     G = blp.DeviceGraph(a, c, device=gpu)
@@ -225,14 +229,20 @@ def test_wedge_rows_equal_host_construction(gpu, device_csr, monkeypatch):
     for x in range(G.n):
         nb = ci[rp[x]: rp[x + 1]]
         row = []
-        if len(nb) and deg[nb].max() <= 32:
+        n_ids = 0
+        if len(nb) and deg[nb].max() <= 64:
             for z in nb:
                 row.extend(ci[rp[z]: rp[z + 1]].tolist())
+            n_ids = len(row)
             row.extend([row[-1]] * (-len(row) % 4))
+        if items and n_ids:
+            got = wd[4 * wp[x]: 4 * wp[x + 1]]
+            assert sorted(got[:n_ids].tolist()) == sorted(row[:n_ids]) and (got[n_ids:] == got[0]).all()
         exp.extend(row)
         exp_wp.append(exp_wp[-1] + len(row) // 4)
     assert np.array_equal(wp, np.array(exp_wp, np.int64))
-    assert np.array_equal(wd, np.array(exp, np.int32))
+    if not items:
+        assert np.array_equal(wd, np.array(exp, np.int32))
     assert deg[G.n_col0:].max() > 256
 
 
