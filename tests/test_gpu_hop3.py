@@ -131,14 +131,14 @@ def test_dataset_maker_drop_in_matches_reference(gpu, tmp_path):
 @pytest.mark.parametrize("long_rows", [False, True])
 def test_hop3_wedge_and_row_walk_agree(gpu, long_rows, monkeypatch):
     """The wedge-row path and the row-walk path emit identical (x, y, label) lists, positives
-    and sampled negatives included. With users of > 32 reviews some businesses have no wedge
+    and sampled negatives included. With users of > 64 reviews some businesses have no wedge
     row and the launch falls back to the row walk (same output either way)."""
     rng = np.random.default_rng(11)
     a, b = bipartite_edges(rng, 30000, 2000, 200000)
     if long_rows:  # a few heavy users: their businesses get no wedge row
         heavy = rng.choice(30000, 20, replace=False)
-        a = np.concatenate([a, np.repeat(heavy, 60)])
-        b = np.concatenate([b, 30000 + rng.integers(0, 2000, 20 * 60)])
+        a = np.concatenate([a, np.repeat(heavy, 90)])
+        b = np.concatenate([b, 30000 + rng.integers(0, 2000, 20 * 90)])
     G = blp.DeviceGraph(a, b)
     nu = G.n - len(np.unique(b))
     src = np.sort(rng.choice(nu, 120, replace=False)).astype(np.int32)
