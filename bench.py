@@ -556,7 +556,10 @@ def run_sharded(args):
 
     # the process group is formed even for one rank, so the exchange below is RCCL's own
     # all_gather_into_tensor at every world size (dist.py, allgather_edges)
-    d = Dist(exchange=True, collective_at_world1=not args.no_collective_at_world1)
+    capi = args.exchange == "capi"
+    # capi: the exchange through libblp's own RCCL communicator (blp_multi_*, multi.hip); the
+    # torch group is then gloo only (barrier, max / sum of the timings)
+    d = Dist(exchange=not capi, collective_at_world1=not args.no_collective_at_world1 and not capi)
     dev = _device(d)
     blp.lib()
     U, B, D = synth.CONFIGS[args.config]
@@ -571,22 +574,42 @@ def run_sharded(args):
     torch.cuda.set_device(dev)
     d.barrier()
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    a_all, b_all, counts = bd.allgather_edges(d, u, b)
-    torch.cuda.synchronize()
-    exch_local = time.perf_counter() - t0
-    d.barrier()
-    exch_s = d.max(exch_local)
-    recv_bytes = 8 * (sum(counts) - counts[d.rank])
-    gathered_bytes = 8 * max(counts) * d.world  # the all-gather's output tensor (padded partials)
-    del u, b
-    if not a_all.is_cuda:  # gloo exchange (rehearsal without RCCL): the partials arrive on the host
-        a_all, b_all = a_all.to("cuda:%d" % dev), b_all.to("cuda:%d" % dev)
-    t0 = time.perf_counter()
-    # the CSR is built in HBM from the gathered endpoints and stays there (no host round trip)
-    G = blp.DeviceGraph.from_device_edges(a_all.data_ptr(), b_all.data_ptr(), len(a_all), U + B, U, device=dev)
-    build_s = time.perf_counter() - t0
-    del a_all, b_all
+    if capi:
+        from blp.multi import Multi
+
+        with bd.stdout_to_stderr():  # RCCL's banner goes to stdout
+            mc = Multi(d.broadcast_bytes(Multi.unique_id() if d.rank == 0 else None), d.world, d.rank, dev)
+        d.barrier()
+        t0 = time.perf_counter()
+        # ONE call: counts + padded partials all-gathered over RCCL, padding dropped, CSR built in HBM
+        c = mc.gather_csr(u.astype(np.int32), b.astype(np.int32), U + B)
+        exch_local = time.perf_counter() - t0
+        d.barrier()
+        exch_s = d.max(exch_local)
+        recv_bytes = mc.bytes_in  # padded partials of the other ranks
+        gathered_bytes = recv_bytes + 8 * len(u)
+        del u, b
+        t0 = time.perf_counter()
+        G = blp.DeviceGraph.from_csr_handle(c, U + B, U, device=dev)
+        build_s = time.perf_counter() - t0
+        mc.close()
+    else:
+        t0 = time.perf_counter()
+        a_all, b_all, counts = bd.allgather_edges(d, u, b)
+        torch.cuda.synchronize()
+        exch_local = time.perf_counter() - t0
+        d.barrier()
+        exch_s = d.max(exch_local)
+        recv_bytes = 8 * (sum(counts) - counts[d.rank])
+        gathered_bytes = 8 * max(counts) * d.world  # the all-gather's output tensor (padded partials)
+        del u, b
+        if not a_all.is_cuda:  # gloo exchange (rehearsal without RCCL): the partials arrive on the host
+            a_all, b_all = a_all.to("cuda:%d" % dev), b_all.to("cuda:%d" % dev)
+        t0 = time.perf_counter()
+        # the CSR is built in HBM from the gathered endpoints and stays there (no host round trip)
+        G = blp.DeviceGraph.from_device_edges(a_all.data_ptr(), b_all.data_ptr(), len(a_all), U + B, U, device=dev)
+        build_s = time.perf_counter() - t0
+        del a_all, b_all
     torch.cuda.empty_cache()
     log("rank %d: graph %d nodes, %d unique edges; exchange %.2fs (%.2f GB in), device CSR build %.1fs %s" %
         (d.rank, G.n, G.nnz // 2, exch_local, recv_bytes / 1e9, build_s, G.build_times))
@@ -632,6 +655,13 @@ def run_sharded(args):
         step()
     blp.device_sync(dev)
     t_local = time.perf_counter() - t_start
+    if os.environ.get("BLP_PROF_READ"):  # experiment library built with -DBLP_PROF: phase clocks
+        import ctypes
+
+        buf = (ctypes.c_ulonglong * 16)()
+        blp.lib().blp_prof_read(buf)
+        v = np.array(buf[:9], np.float64)
+        log("prof %s" % {i: "%.1f%%" % (100 * x / max(v.sum(), 1)) for i, x in enumerate(v)})
     d.barrier()
     t_max = d.max(t_local)
     pairs_total = d.sum(len(ex_x))
@@ -654,7 +684,10 @@ def run_sharded(args):
                    "pairs_per_gpu": int(len(ex_x)), "global_batch": int(pairs_total),
                    "parallelism": "row-block sharded ingest x%d + RCCL all-gather (%s), rank-local scoring"
                                   % (d.world, d.backend or "single rank")},
-        "exchange": {"backend": d.backend, "collective": "all_gather_into_tensor" if d.td is not None else None,
+        "exchange": {"backend": "rccl (libblp blp_multi_gather_csr; seconds include the device CSR build)" if capi
+                     else d.backend,
+                     "collective": "ncclAllGather" if capi else
+                     "all_gather_into_tensor" if d.td is not None else None,
                      "gathered_bytes_per_rank": int(gathered_bytes),
                      "seconds": exch_s, "bytes_in_per_rank": int(recv_bytes),
                      "GBps_in_per_rank": recv_bytes / exch_s / 1e9 if exch_s > 0 and recv_bytes else None,
@@ -887,6 +920,9 @@ def main():
     ap.add_argument("--cosched-passes", action="store_true", help="--mode sharded: both passes through blp_batches_score")
     ap.add_argument("--parity-sources", type=int, default=50,
                     help="--mode sharded: sampled sources per side and rank checked against the C oracle")
+    ap.add_argument("--exchange", choices=["torch", "capi"], default="torch",
+                    help="sharded mode: config 5's exchange through torch.distributed (RCCL) or through "
+                         "libblp's own RCCL communicator (blp_multi_gather_csr)")
     ap.add_argument("--no-collective-at-world1", action="store_true",
                     help="--mode sharded: at one rank, skip the process group (no RCCL call; the local partial)")
     ap.add_argument("--topk", type=int, default=20)

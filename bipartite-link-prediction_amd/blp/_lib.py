@@ -54,6 +54,12 @@ SIGNATURES = {
     "blp_csr_destroy": [_P],
     "blp_graph_create_from_csr": [_P, _P, _P, _P, _PP],
     "blp_graph_destroy": [_P],
+    "blp_multi_unique_id": [_P],
+    "blp_multi_init": [_P, _I32, _I32, _I32, _PP],
+    "blp_multi_info": [_P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)],
+    "blp_multi_gather_csr": [_P, _P, _P, _I64, _I64, _PP, ctypes.POINTER(ctypes.c_int64)],
+    "blp_multi_allreduce": [_P, _DP, _I32],
+    "blp_multi_destroy": [_P],
     "blp_graph_wedge": [_P, ctypes.POINTER(ctypes.c_int64), _P, _P],
     "blp_graph_info": [_P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
                        ctypes.POINTER(ctypes.c_int)],

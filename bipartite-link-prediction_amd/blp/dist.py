@@ -110,6 +110,14 @@ class Dist:
         self.td.all_gather(out, torch.tensor([int(v)], dtype=torch.int64), group=self.cpu_group)
         return [int(t.item()) for t in out]
 
+    def broadcast_bytes(self, b, src=0):
+        """Rank src's bytes on every rank (over the CPU group), e.g. libblp's RCCL id."""
+        if self.world == 1:
+            return b
+        box = [b]
+        self.td.broadcast_object_list(box, src=src, group=self.cpu_group)
+        return box[0]
+
     def close(self):
         if self.td is not None and self.td.is_initialized():
             self.td.destroy_process_group()

@@ -285,6 +285,14 @@ class DeviceGraph(HostGraph):
         check(lib().blp_csr_build_device(device, ctypes.c_void_p(a_ptr), ctypes.c_void_p(b_ptr), m, n,
                                          ctypes.byref(c)))
         t_csr = time.perf_counter() - t0
+        g = cls.from_csr_handle(c, n, n_col0, device, aa)
+        g.build_times["device_csr_s"] = t_csr
+        return g
+
+    @classmethod
+    def from_csr_handle(cls, c, n, n_col0, device=0, aa=True):
+        """A graph over a device CSR handle (blp_csr_build_device / blp_multi_gather_csr output,
+        dense ids in [0, n)); the handle is consumed."""
         g = cls.__new__(cls)
         g.node_ids = np.arange(n, dtype=np.int64)  # ids already dense
         g.n_col0 = int(n_col0)
@@ -292,7 +300,6 @@ class DeviceGraph(HostGraph):
         g._sorted_ids = g.node_ids
         g.n_edges_in = None
         g._adopt_csr(c, device, aa)
-        g.build_times["device_csr_s"] = t_csr
         return g
 
     def _adopt_csr(self, c, device, aa):

@@ -34,6 +34,7 @@ extern "C" {
 #define BLP_E_NOMEM (-3)    /* host allocation failed */
 #define BLP_E_UNSUP (-4)    /* configuration not supported by this build */
 #define BLP_E_ZERODIV (-5)  /* Jaccard union of size 0 (reference raises ZeroDivisionError) */
+#define BLP_E_COMM (-6)     /* a collective failed (RCCL error; blp_multi_*) */
 #define BLP_E_HIP_BASE (-1000)
 
 #define BLP_CN 1u
@@ -92,6 +93,35 @@ int blp_csr_fetch(const blp_csr* c, int64_t* row_ptr, int32_t* col_idx, uint8_t*
 int blp_csr_destroy(blp_csr* c);
 int blp_graph_create_from_csr(blp_csr* c, const int64_t* row_ptr, const int32_t* col_idx, const double* aaw,
                               blp_graph** out);
+
+/* ---------------------------------------------------------------- multi-GPU exchange (config 5)
+ * The reference is single-process (snap.LoadEdgeList, similarity.py:16); its 1B-edge config is
+ * this engine's row-block sharded ingest. These entry points are the exchange
+ * step of blp/dist.py (allgather_edges + DeviceGraph.from_device_edges) with the engine's own
+ * RCCL communicator, for hosts that do not run torch.distributed. One process per GPU.
+ * blp_multi_unique_id: rank 0 creates the communicator id; the host ships its
+ *   BLP_MULTI_ID_BYTES bytes to every rank over any channel (a file, a socket, MPI).
+ * blp_multi_init: every rank joins with the same id (RCCL is loaded at run time: BLP_E_UNSUP
+ *   when librccl.so.1 cannot be loaded; a failing collective returns BLP_E_COMM).
+ * blp_multi_gather_csr: THE exchange. Each rank passes its edge partial (m_r endpoint pairs,
+ *   dense ids in [0, n_nodes), host or device memory); the counts, then the partials padded to
+ *   the largest count, are all-gathered over RCCL, the padding is dropped on the device and the
+ *   union's CSR is built in HBM as blp_csr_build_device does. Every rank gets the same csr; feed
+ *   it to blp_csr_fetch / blp_graph_create_from_csr. *bytes_in (may be NULL): bytes received
+ *   from the other ranks. Collective: every rank must call it.
+ * blp_multi_allreduce: *v = the sum (BLP_MULTI_SUM) or max (BLP_MULTI_MAX) of every rank's *v,
+ *   e.g. the max-over-ranks step time. Collective.                                           */
+#define BLP_MULTI_ID_BYTES 128
+#define BLP_MULTI_SUM 0
+#define BLP_MULTI_MAX 1
+typedef struct blp_multi blp_multi;
+int blp_multi_unique_id(uint8_t* id);
+int blp_multi_init(const uint8_t* id, int world, int rank, int device, blp_multi** out);
+int blp_multi_info(const blp_multi* m, int* world, int* rank, int* device);
+int blp_multi_gather_csr(blp_multi* m, const int32_t* a, const int32_t* b, int64_t m_r, int64_t n_nodes,
+                         blp_csr** out, int64_t* bytes_in);
+int blp_multi_allreduce(blp_multi* m, double* v, int op);
+int blp_multi_destroy(blp_multi* m);
 
 /* blp_edges_parse: SNAP LoadEdgeList's text format (similarity.py:16): one edge per line,
  * whitespace-separated integer columns c0 and c1, lines starting with '#' skipped, lines

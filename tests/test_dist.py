@@ -52,7 +52,8 @@ def _worker(rank, world, port, outdir):
     # the same CSR on every rank, built by the host twin of blp_csr_from_edges_device
     rp, ci = _csr(a_all.numpy(), b_all.numpy())
     np.savez(os.path.join(outdir, "r%d.npz" % rank), rp=rp, ci=ci, u=u, b=b,
-             mx=d.max(rank + 1.5), sm=d.sum(rank + 1), ints=np.array(d.allgather_int(10 * rank + 3)))
+             mx=d.max(rank + 1.5), sm=d.sum(rank + 1), ints=np.array(d.allgather_int(10 * rank + 3)),
+             uid=np.frombuffer(d.broadcast_bytes(bytes(range(128)) if rank == 0 else None), np.uint8))
     d.barrier()
     d.close()
 
@@ -103,3 +104,5 @@ def test_gloo_exchange_gives_every_rank_the_whole_graph(world, tmp_path):
         assert np.array_equal(r["rp"], rp) and np.array_equal(r["ci"], ci)
     assert float(res[0]["mx"]) == world + 0.5 and float(res[1]["sm"]) == sum(range(1, world + 1))
     assert res[1]["ints"].tolist() == [10 * r + 3 for r in range(world)]
+    # rank 0's communicator id (blp_multi_unique_id's 128 bytes) reaches every rank
+    assert all(r["uid"].tolist() == list(range(128)) for r in res)

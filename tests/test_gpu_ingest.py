@@ -369,3 +369,99 @@ def test_two_ranks_share_the_gpu(gpu, tmp_path):
         np.testing.assert_array_equal(r["cn"], cn)
         np.testing.assert_array_equal(r["jaccard"], jac)
         np.testing.assert_array_equal(r["adamic"], aa)  # exact sums: bit-exact
+
+
+def _capi_rank(rank, world, q, outdir, device_ptrs):
+    """One rank of the C-ABI exchange (multi.hip): its user block's edges through
+    blp_multi_gather_csr (libblp's own RCCL communicator), then its users' pairs scored."""
+    import torch
+
+    from blp import multi as bm
+
+    if rank == 0:
+        uid = bm.Multi.unique_id()
+        for _ in range(world - 1):
+            q.put(uid)
+    else:
+        uid = q.get(timeout=60)
+    blocks = bd.user_blocks(U2, world)
+    u, b = bd.block_review_edges(U2, B2, D2, blocks[rank], blocks[rank + 1], seed=9)
+    dev = rank % blp.device_count()  # one GPU per rank where the box has them
+    torch.cuda.set_device(dev)
+    try:
+        m = bm.Multi(uid, world, rank, dev)
+    except blp.BLPError as e:
+        if e.code == -6 and world > 1:  # RCCL refuses several ranks on one GPU
+            open(os.path.join(outdir, "skip%d" % rank), "w").write(str(e))
+            return
+        raise
+    if device_ptrs:
+        ta = torch.as_tensor(u.astype(np.int32)).to("cuda:%d" % dev)
+        tb = torch.as_tensor(b.astype(np.int32)).to("cuda:%d" % dev)
+        G = m.gather_graph(ta.data_ptr(), tb.data_ptr(), U2 + B2, U2, m=len(u))
+    else:
+        G = m.gather_graph(u.astype(np.int32), b.astype(np.int32), U2 + B2, U2)
+    tmax = m.allreduce(rank + 1.5, "max")
+    tsum = m.allreduce(1.0, "sum")
+    mine = np.arange(blocks[rank], blocks[rank + 1])
+    src = np.random.default_rng(rank).choice(mine[G.hop1_size[mine] > 0], 40, replace=False)
+    x = np.repeat(src, 20).astype(np.int32)
+    y = np.random.default_rng(rank + 10).integers(U2, U2 + B2, len(x)).astype(np.int32)
+    r = G.score_pairs(x, y, 7)
+    np.savez(os.path.join(outdir, "c%d.npz" % rank), rp=G.row_ptr, ci=G.col_idx, u=u, b=b, x=x, y=y,
+             bytes_in=m.bytes_in, tmax=tmax, tsum=tsum, **r)
+    G.close()
+    m.close()
+
+
+def _run_capi(world, tmp_path, device_ptrs):
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_capi_rank, args=(r, world, q, str(tmp_path), device_ptrs)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(110)
+    codes = [p.exitcode for p in procs]
+    for p in procs:
+        if p.exitcode is None:
+            p.kill()
+    assert codes == [0] * world, codes
+    if any(os.path.exists(os.path.join(tmp_path, "skip%d" % r)) for r in range(world)):
+        pytest.skip("RCCL: several ranks on one GPU refused (%s)" % open(
+            [os.path.join(tmp_path, "skip%d" % r) for r in range(world)
+             if os.path.exists(os.path.join(tmp_path, "skip%d" % r))][0]).read())
+    res = [np.load(os.path.join(tmp_path, "c%d.npz" % r)) for r in range(world)]
+    u = np.concatenate([r["u"] for r in res])
+    b = np.concatenate([r["b"] for r in res])
+    rp, ci, _ = _host_csr(U2 + B2, u, b)
+    ids, oa, ob = dense_edges(u, b)
+    og = coracle.OracleGraph(len(ids), oa, ob)
+    m_max = max(len(r["u"]) for r in res)
+    for r in res:
+        assert np.array_equal(r["rp"], rp) and np.array_equal(r["ci"], ci)
+        assert int(r["bytes_in"]) == 8 * m_max * (world - 1)
+        assert float(r["tmax"]) == world - 1 + 1.5 and float(r["tsum"]) == world
+        cn, jac, aa, _ = og.score_pairs(np.searchsorted(ids, r["x"]), np.searchsorted(ids, r["y"]), 7)
+        np.testing.assert_array_equal(r["cn"], cn)
+        np.testing.assert_array_equal(r["jaccard"], jac)
+        np.testing.assert_array_equal(r["adamic"], aa)
+
+
+@pytest.mark.parametrize("device_ptrs", [False, True])
+def test_multi_capi_world1(gpu, tmp_path, device_ptrs):
+    """The C-ABI exchange (blp_multi_*: libblp's own RCCL communicator, no torch.distributed)
+    over one rank: host or device partials, the counts and padded partials all-gathered, the
+    CSR built in HBM equals the host CSR of the edges, the all-reduce returns the rank's own
+    value, and the scores equal the oracle (similarity.py:20-106)."""
+    _run_capi(1, tmp_path, device_ptrs)
+
+
+def test_multi_capi_two_ranks(gpu, tmp_path):
+    """World 2 through the C-ABI, rank r on GPU r mod the device count: each rank passes its
+    user block, both get the union's CSR (bytes_in = the other rank's padded partial), the
+    max / sum all-reduces agree, and each rank's scores equal the oracle. On a one-GPU box
+    both ranks share device 0, which RCCL refuses (ncclInvalidUsage): then skipped."""
+    _run_capi(2, tmp_path, False)
