@@ -2174,6 +2174,7 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
   const int grp = a.sched ? 0 : (int)(blockIdx.x & 7);
   const int ngrp = a.sched ? 1 : 8;
   int gq = 0;  // thread 0: groups found empty so far
+  PROF_INIT  // -DBLP_PROF phase clocks: 0 claim, 1 build, 2 popcount, 3 batch to short scan, 4 long scan, 5 partials
   for (;;) {
     if (threadIdx.x == 0) {
       s_item = -1;
@@ -2192,6 +2193,7 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
     const int64_t item = s_item;
     __syncthreads();
     if (item < 0) break;
+    PROF(0)
     const int s = (int)(item / C), c = (int)(item % C);
     const int x = a.active[s];
     if (hflag && hflag[x - hxlo]) continue;  // uniform: scored by k_score_hash
@@ -2279,6 +2281,7 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
         __syncthreads();
       }
     }
+    PROF(1)
     // exact distance 2 inside this chunk: drop x and N(x)
     const int64_t nx_lo = xe > xb ? a.ci[xb] : 0, nx_hi = xe > xb ? a.ci[xe - 1] : -1;
     if (nx_hi >= c0 && nx_lo < c0 + width) {
@@ -2298,6 +2301,7 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
       const unsigned long long h2 = block_sum_u64<BLOCK>(pc, red64);
       if (threadIdx.x == 0) ph2[(int64_t)s * C + c] = (uint32_t)h2;
     }
+    PROF(2)
     // Pair-batch metadata: the pair's y and row start (chunk-independent), then its slice bounds
     // for chunk c from the split table. The next batch's y / row start are loaded during this
     // batch's offsets, its slice bounds right after this batch's scan, so each batch starts with
@@ -2365,6 +2369,7 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
         if (threadIdx.x == 0) s_off[ns] = tot;
         __syncthreads();
       }
+      PROF(3)
       if ((int)threadIdx.x < ns_next) {
         const int gp = pbeg + sb + SEG + threadIdx.x;
         pf_y = g_y[gp];
@@ -2392,6 +2397,7 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
         pf_s1 = sp[1];
       }
       __syncthreads();
+      PROF(4)
       // a pair's chunk partials meet in per-pair accumulators: only (pair, chunk) slices with a
       // hit add anything, so no [chunks][pairs] partial arrays (config 5: 48 chunks x 199M
       // pairs) and no dense combine reads. With Adamic-Adar and every scanned row shorter than
@@ -2420,8 +2426,10 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
         }
       }
       __syncthreads();
+      PROF(5)
     }
   }
+  PROF_FLUSH
 }
 
 // one wave per active source: sum the chunk partials of each of its pairs, then Jaccard
