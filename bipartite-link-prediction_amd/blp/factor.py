@@ -17,6 +17,8 @@ _lib.register("blp_svd_topk", [_P, _P, _I64, _P, _P, _I32, _P, _P])
 _lib.register("blp_svd_stats", [_P, _I32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)])
 _lib.register("blp_svd_sync", [_P])
 _lib.register("blp_svd_stream_join", [_P, _P, _I32])
+_lib.register("blp_svd_set_prune", [_P, _I32])
+_lib.register("blp_svd_tiles", [_P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)])
 
 
 class DeviceSVD:
@@ -107,6 +109,17 @@ class DeviceSVD:
 
     def sync(self):
         check(lib().blp_svd_sync(self.handle))
+
+    def set_prune(self, on=True):
+        """Top-k by norm pruning (the default; same lists) or the dense pass over every pair."""
+        check(lib().blp_svd_set_prune(self.handle, 1 if on else 0))
+
+    def tiles(self):
+        """(MFMA tiles of 16 users x 16 businesses scored, tiles of the dense pass) over the top-k
+        calls since the last tiles() call."""
+        a, b = ctypes.c_int64(0), ctypes.c_int64(0)
+        check(lib().blp_svd_tiles(self.handle, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
 
     def stats(self, which=0):
         ms = ctypes.c_double(0)

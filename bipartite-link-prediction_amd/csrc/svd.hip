@@ -10,8 +10,18 @@
 //                     with a fused running top-k per user (threshold + LDS candidate buffer),
 //                     one partial list per (user, business chunk).
 //   * k_svd_merge  -- merges the per-chunk lists: score descending, then column ascending.
+//   * norm-pruned top-k (default; blp_svd_set_prune): a score is us[u] . v[b], so
+//     |score| <= ||us[u]|| ||v[b]||. The businesses are numbered by ||v[b]|| descending (a
+//     permuted copy of Vt, built once per handle), a first pass scores the first TK_SEED_COLS
+//     of that order for every user, and the rest of the columns go to chunks that take tiles
+//     round-robin (each chunk sees the norms descending) starting from the first pass's k-th
+//     score: a wave stops when the bound of the next tile, ||us[u]|| ||v[c]|| (1 + 1e-9), is
+//     strictly below every one of its 16 users' thresholds, since no later column can enter
+//     a list. Same MFMA dot products, same lists as the dense pass (bit-exact).
 // Factor layout: US [n_rows][kpad] and V [n_cols][kpad] row-major, Vt [kpad][ncol_pad];
 // kpad = k rounded up to 16 (zero padding adds exact zeros to every dot product).
+#include <hipcub/hipcub.hpp>
+
 #include <algorithm>
 #include <cfloat>
 #include <vector>
@@ -32,6 +42,15 @@ struct blp_svd {
   double* d_ps = nullptr;  // top-k scratch: per (user, chunk) partial lists, part_cap entries
   int32_t* d_pc = nullptr;
   int64_t part_cap = 0;
+  // norm-pruned top-k (built on first use): Vt with columns by ||v|| descending, the sorted
+  // norms (zeros past n_cols), the order (sorted position -> column; INT32_MAX past n_cols)
+  int prune = 1;
+  double* d_vtp = nullptr;
+  double* d_vnp = nullptr;
+  int32_t* d_perm = nullptr;
+  unsigned long long* d_tiles = nullptr;  // MFMA tiles scored since the last blp_svd_tiles
+  int64_t tiles_total = 0;                // tiles of the dense pass over the same calls
+  int64_t tiles_dense = 0;                // tiles scored by dense-pass calls
 };
 
 namespace {
@@ -80,6 +99,15 @@ struct TopkArgs {
   double* part_score;      // [n_users][n_chunks][topk]
   int32_t* part_col;
   int64_t n_rows;          // rows of us: a selected row outside [0, n_rows) reads no memory
+  // norm-pruned pass (PR = 1): vt is the norm-sorted copy, perm maps a sorted position to its
+  // column, vnorm the sorted norms; chunk j of the grid takes the tiles col_base + 16 (j + i S),
+  // S = gridDim.y, below n_cols; its list is chunk chunk_base + j of part_*; seeded: start
+  // every user's threshold at the k-th entry of its chunk-0 list (the first pass)
+  const int32_t* perm;
+  const double* vnorm;
+  int64_t col_base;
+  int chunk_base, seeded;  // seeded: lists 0 .. seeded-1 hold the first pass
+  unsigned long long* tiles;  // tiles scored (or null)
 };
 
 // better = higher score, then lower column
@@ -130,7 +158,7 @@ __device__ inline void tk_compact(double* top_s, int* top_c, const double* buf_s
 // Vt stream per score is 8 KiB / (256 RT) -- RT = 2 halves the L2/MALL traffic of RT = 1.
 // EXP = 1 (timing experiment only, BLP_SVD_EXP=1): the MFMA chains and fragment loads without
 // the top-k epilogue (results are NOT valid)
-template <int KPAD, int RT, int WAVES, int EXP = 0>
+template <int KPAD, int RT, int WAVES, int EXP = 0, int PR = 0>
 __global__ __launch_bounds__(WAVES * 64) void k_svd_topk(TopkArgs a) {
   constexpr int R = 16 * RT;  // users per wave
   __shared__ double s_top[WAVES][R][TK_MAX];
@@ -146,7 +174,9 @@ __global__ __launch_bounds__(WAVES * 64) void k_svd_topk(TopkArgs a) {
   const int64_t u0 = ((int64_t)blockIdx.x * WAVES + w) * R;
   if (u0 >= a.n_users) return;  // whole wave idle (no block barriers below)
   const int chunk = blockIdx.y;
-  const int64_t cb = (int64_t)chunk * a.chunk, ce = min(a.n_cols, cb + a.chunk);
+  const int64_t cb = PR ? a.col_base + 16 * (int64_t)chunk : (int64_t)chunk * a.chunk;
+  const int64_t ce = PR ? a.n_cols : min(a.n_cols, cb + a.chunk);
+  const int64_t TS = PR ? 16 * (int64_t)gridDim.y : 16;  // column step between this chunk's tiles
   const int topk = a.topk;
   for (int i = lane; i < R * TK_MAX; i += 64) {
     s_top[w][i / TK_MAX][i % TK_MAX] = -DBL_MAX;
@@ -176,7 +206,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_svd_topk(TopkArgs a) {
   // one LDS read. The global loads (and their vmcnt wait, which also waits for the B fragments
   // in flight: vmcnt counts in issue order) happen once per group, not inside the tile loop.
   int64_t ex_p = 0, ex_e = 0;
-  if (a.ex_off && lane < R && u0 + lane < a.n_users) {
+  if (!PR && a.ex_off && lane < R && u0 + lane < a.n_users) {
     ex_p = a.ex_off[u0 + lane];
     ex_e = a.ex_off[u0 + lane + 1];
     while (ex_p < ex_e && a.ex_col[ex_p] < cb) ++ex_p;
@@ -215,21 +245,63 @@ __global__ __launch_bounds__(WAVES * 64) void k_svd_topk(TopkArgs a) {
   for (int t = 0; t < RT; ++t)
 #pragma unroll
     for (int r = 0; r < 4; ++r) rowok[t][r] = u0 + 16 * t + my_row + 4 * r < a.n_users;
+  double sd[RT][4];  // PR: the first pass's k-th entry of each row (the floor of its threshold)
+  int sdc[RT][4];
 #pragma unroll
   for (int t = 0; t < RT; ++t)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      th[t][r] = -DBL_MAX;
-      thc[t][r] = INT32_MAX;
+      sd[t][r] = -DBL_MAX;
+      sdc[t][r] = INT32_MAX;
+      const int64_t u = u0 + 16 * t + my_row + 4 * r;
+      // the best k-th entry of the first pass's lists: the union of those lists holds topk
+      // entries at least that good, so the final k-th score is never below it
+      for (int j = 0; PR && j < a.seeded && u < a.n_users; ++j) {
+        const int64_t o = (u * a.n_chunks + j) * topk + topk - 1;
+        const double v = a.part_score[o];
+        const int vc = a.part_col[o];
+        if (better(v, vc, sd[t][r], sdc[t][r])) {
+          sd[t][r] = v;
+          sdc[t][r] = vc;
+        }
+      }
+      th[t][r] = sd[t][r];
+      thc[t][r] = sdc[t][r];
     }
-  auto load_b = [&](double* bf, int64_t c) __attribute__((always_inline)) {
+  // PR: ||us[u]|| of this lane's rows (lanes 0-15 hold row lane & 15's sum of squares after the
+  // cross-group reduction) and the rows' exclusion ranges (checked per candidate by search)
+  double un[RT][4];
+  int64_t exb[RT][4], exe[RT][4];
+#pragma unroll
+  for (int t = 0; t < RT; ++t) {
+    double q = 0.0;
+    if (PR) {
+#pragma unroll
+      for (int s = 0; s < KS; ++s) q = fma(af[t][s], af[t][s], q);
+      q += __shfl_xor(q, 16, 64);
+      q += __shfl_xor(q, 32, 64);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 16 * t + my_row + 4 * r;
+      un[t][r] = PR ? sqrt(__shfl(q, row & 15, 64)) : 0.0;
+      exb[t][r] = exe[t][r] = 0;
+      if (PR && a.ex_off && u0 + row < a.n_users) {
+        exb[t][r] = a.ex_off[u0 + row];
+        exe[t][r] = a.ex_off[u0 + row + 1];
+      }
+    }
+  }
+  int pcol0 = 0, pcol1 = 0;  // PR: the columns of the two fragment sets' tiles
+  auto load_b = [&](double* bf, int& pcol, int64_t c) __attribute__((always_inline)) {
 #pragma unroll
     for (int s = 0; s < KS; ++s) bf[s] = vt_lane[(int64_t)(4 * s) * a.ncol_pad + c];
+    if (PR) pcol = a.perm[c + (lane & 15)];
     // keep the scheduler from sinking these loads into the previous tile's MFMA chain (it
     // does so to shorten live ranges, which brings the wait back)
     __builtin_amdgcn_sched_barrier(0);
   };
-  auto tile = [&](int64_t c0, const double* bf) __attribute__((always_inline)) {
+  auto tile = [&](int64_t c0, const double* bf, int pcol) __attribute__((always_inline)) {
     double4_t d[RT];
 #pragma unroll
     for (int t = 0; t < RT; ++t) d[t] = double4_t{0.0, 0.0, 0.0, 0.0};
@@ -237,19 +309,20 @@ __global__ __launch_bounds__(WAVES * 64) void k_svd_topk(TopkArgs a) {
     for (int s = 0; s < KS; ++s)
 #pragma unroll
       for (int t = 0; t < RT; ++t) d[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[t][s], bf[s], d[t], 0, 0, 0);
-    const int col = (int)(c0 + (lane & 15));
+    const int cidx = (int)(c0 + (lane & 15));
+    const int col = PR ? pcol : cidx;  // the business id (lists and ties use it)
     if (EXP == 1) {
 #pragma unroll
       for (int t = 0; t < RT; ++t) th[t][0] += d[t][0] + d[t][1] + d[t][2] + d[t][3];
       return;
     }
     // lane r < R: excluded columns of row r in this tile
-    const unsigned exm = a.ex_off && lane < R ? s_exm[w][lane][((c0 - cb) >> 4) % TK_GROUP] : 0u;
+    const unsigned exm = !PR && a.ex_off && lane < R ? s_exm[w][lane][((c0 - cb) >> 4) % TK_GROUP] : 0u;
     // Thresholds live in registers (they change only when a row is compacted), so a tile
     // whose scores all fall below them costs a few VALU compares and one ballot: no LDS
     // round trip, no cross-lane shuffle unless the tile holds an excluded column.
     const bool anyex = __ballot(exm != 0) != 0;  // wave-uniform
-    const bool colok = col < ce;
+    const bool colok = cidx < ce;
     bool pass[RT][4];
     bool anyp = false;
 #pragma unroll
@@ -264,10 +337,18 @@ __global__ __launch_bounds__(WAVES * 64) void k_svd_topk(TopkArgs a) {
           const unsigned rm = (unsigned)__shfl((int)exm, row, 64);
           ok = ok && !((rm >> (lane & 15)) & 1u);
         }
+        if (PR && ok && exe[t][r] > exb[t][r]) {  // a rare candidate: search the sorted exclusions
+          int64_t lo = exb[t][r], hi = exe[t][r];
+          while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (a.ex_col[mid] < col) lo = mid + 1; else hi = mid;
+          }
+          ok = !(lo < exe[t][r] && a.ex_col[lo] == col);
+        }
         pass[t][r] = ok;
         anyp |= ok;
       }
-    const bool last = c0 + 16 >= ce;
+    const bool last = c0 + TS >= ce;
     if (__ballot(anyp) == 0 && !last) return;  // wave-uniform: nothing enters any list
 #pragma unroll
     for (int t = 0; t < RT; ++t)
@@ -302,40 +383,113 @@ __global__ __launch_bounds__(WAVES * 64) void k_svd_topk(TopkArgs a) {
       for (int r = 0; r < 4; ++r) {
         th[t][r] = s_th[w][16 * t + my_row + 4 * r];
         thc[t][r] = s_thc[w][16 * t + my_row + 4 * r];
+        if (PR && better(sd[t][r], sdc[t][r], th[t][r], thc[t][r])) {  // never below the first pass's
+          th[t][r] = sd[t][r];
+          thc[t][r] = sdc[t][r];
+        }
       }
   };
+  // PR: true when no column from c on can enter any of the wave's lists (wave-uniform)
+  auto pruned = [&](int64_t c) __attribute__((always_inline)) {
+    const double bn = a.vnorm[c] * (1.0 + 1e-9);
+    bool keep = false;
+#pragma unroll
+    for (int t = 0; t < RT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) keep |= rowok[t][r] && !(un[t][r] * bn < th[t][r]);
+    return __ballot(keep) == 0;
+  };
   double b0[KS], b1[KS];
-  load_b(b0, cb);
-  for (int64_t c0 = cb; c0 < ce; c0 += 32) {
-    if (a.ex_off && ((c0 - cb) >> 4) % TK_GROUP == 0) ex_group(c0);  // (TK_GROUP is even)
-    const int64_t c1 = c0 + 16;
-    load_b(b1, c1 < ce ? c1 : c0);  // (past the chunk: a harmless re-read)
-    tile(c0, b0);
+  unsigned long long n_tiles = 0;
+  if (cb < ce) load_b(b0, pcol0, cb);
+  for (int64_t c0 = cb; c0 < ce; c0 += 2 * TS) {
+    if (!PR && a.ex_off && ((c0 - cb) >> 4) % TK_GROUP == 0) ex_group(c0);  // (TK_GROUP is even)
+    const int64_t c1 = c0 + TS;
+    load_b(b1, pcol1, c1 < ce ? c1 : c0);  // (past the chunk: a harmless re-read)
+    if (PR && pruned(c0)) break;
+    tile(c0, b0, pcol0);
+    ++n_tiles;
     if (c1 >= ce) break;
-    load_b(b0, c1 + 16 < ce ? c1 + 16 : c1);
-    tile(c1, b1);
+    load_b(b0, pcol0, c1 + TS < ce ? c1 + TS : c1);
+    if (PR && pruned(c1)) break;
+    tile(c1, b1, pcol1);
+    ++n_tiles;
+  }
+  if (PR) {
+    // a pruned stop leaves buffered candidates: fold them into the lists
+    unsigned long long due = __ballot(lane < R && s_nb[w][lane] > 0);
+    while (due) {
+      const int row = __builtin_ctzll(due);
+      due &= due - 1;
+      tk_compact(s_top[w][row], s_topc[w][row], s_buf[w][row], s_bufc[w][row], s_nb[w][row], topk, lane,
+                 &s_th[w][row], &s_thc[w][row]);
+      if (lane == 0) s_nb[w][row] = 0;
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    }
+    if (a.tiles && lane == 0) atomicAdd(a.tiles, n_tiles);
   }
   if (EXP == 1 && th[0][0] == 1.2345e300) a.part_score[0] = th[0][0];  // keeps the chains live
   for (int i = lane; i < R * topk; i += 64) {
     const int row = i / topk, q = i % topk;
     const int64_t u = u0 + row;
     if (u < a.n_users) {
-      const int64_t o = (u * a.n_chunks + chunk) * topk + q;
+      const int64_t o = (u * a.n_chunks + (PR ? a.chunk_base + chunk : chunk)) * topk + q;
       a.part_score[o] = s_top[w][row][q];
       a.part_col[o] = s_topc[w][row][q];
     }
   }
 }
 
-// One wave per user: best topk of n_chunks * topk partial entries.
+// One wave per user: best topk of n_chunks * topk partial entries. The filled entries (empty
+// slots carry column INT32_MAX; a pruned chunk's list is all empty) are gathered into LDS
+// first and ranked among themselves (columns are distinct across lists: no exact ties);
+// slots past the filled count get (0.0, -1). More than TK_MERGE_CAP filled: rank in place.
+constexpr int TK_MERGE_CAP = 1024;
 __global__ __launch_bounds__(64) void k_svd_merge(const double* __restrict__ ps, const int32_t* __restrict__ pc,
                                                   int64_t n_users, int n_chunks, int topk, double* __restrict__ out_s,
                                                   int32_t* __restrict__ out_c) {
+  __shared__ double m_s[TK_MERGE_CAP];
+  __shared__ int m_c[TK_MERGE_CAP];
+  __shared__ int m_n;
   const int64_t u = blockIdx.x;
   const int lane = threadIdx.x;
   const int n = n_chunks * topk;
   const double* s = ps + u * n;
   const int32_t* c = pc + u * n;
+  if (lane == 0) m_n = 0;
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  for (int i = lane; i < n; i += 64) {
+    const int vc = c[i];
+    if (vc != INT32_MAX) {
+      const int slot = atomicAdd(&m_n, 1);
+      if (slot < TK_MERGE_CAP) {
+        m_s[slot] = s[i];
+        m_c[slot] = vc;
+      }
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  const int m = m_n;
+  if (m <= TK_MERGE_CAP) {
+    for (int i = lane; i < m; i += 64) {
+      const double v = m_s[i];
+      const int vc = m_c[i];
+      int r = 0;
+      for (int j = 0; j < m; ++j) r += better(m_s[j], m_c[j], v, vc);
+      if (r < topk) {
+        out_s[u * topk + r] = v;
+        out_c[u * topk + r] = vc;
+      }
+    }
+    for (int q = m + lane; q < topk; q += 64) {
+      out_s[u * topk + q] = 0.0;
+      out_c[u * topk + q] = -1;
+    }
+    return;
+  }
   for (int i = lane; i < n; i += 64) {
     const double v = s[i];
     const int vc = c[i];
@@ -348,9 +502,87 @@ __global__ __launch_bounds__(64) void k_svd_merge(const double* __restrict__ ps,
   }
 }
 
+// ---------------------------------------------------------------- norm order (pruned top-k)
+constexpr int TK_SEED_COLS = 2048;  // the first pass: this many columns of largest ||v|| per user
+constexpr int TK_PR_CHUNKS = 16;    // chunks of the pruned pass (tiles dealt round-robin)
+constexpr int TK_SEED_CHUNKS = 4;   // chunks of the first pass (its tiles dealt round-robin too)
+
+// key = the bits of ||v[c]|| (non-negative doubles order as their bit patterns), value = c
+__global__ void k_vnorm(const double* __restrict__ v, int64_t n_cols, int kpad, unsigned long long* __restrict__ key,
+                        int32_t* __restrict__ idx) {
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < n_cols; c += (int64_t)gridDim.x * blockDim.x) {
+    double q = 0.0;
+    for (int j = 0; j < kpad; ++j) q = fma(v[c * kpad + j], v[c * kpad + j], q);
+    key[c] = (unsigned long long)__double_as_longlong(sqrt(q));
+    idx[c] = (int32_t)c;
+  }
+}
+
+// sorted position j: the column, its norm and its Vt column (padding past n_cols: zeros)
+__global__ void k_vt_perm(const double* __restrict__ vt, int64_t ncol_pad, int64_t n_cols, int kpad,
+                          const unsigned long long* __restrict__ skey, const int32_t* __restrict__ sidx,
+                          double* __restrict__ vtp, double* __restrict__ vnp, int32_t* __restrict__ perm) {
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < ncol_pad; j += (int64_t)gridDim.x * blockDim.x) {
+    const bool in = j < n_cols;
+    const int32_t c = in ? sidx[j] : INT32_MAX;
+    perm[j] = c;
+    vnp[j] = in ? __longlong_as_double((long long)skey[j]) : 0.0;
+    for (int k = 0; k < kpad; ++k) vtp[k * ncol_pad + j] = in ? vt[k * ncol_pad + c] : 0.0;
+  }
+}
+
 }  // namespace
 
 using namespace blp;
+
+// The norm-ordered copy of the factors (first pruned top-k): a stable descending sort of
+// ||v[c]||, so equal norms keep column order.
+static int svd_prune_prepare(blp_svd* h) {
+  if (h->d_vtp) return BLP_OK;
+  const int64_t n = h->n_cols, np = h->ncol_pad;
+  DevBuf key, idx, skey, sidx, temp;
+  int rc;
+  if ((rc = key.reserve(8 * n)) || (rc = idx.reserve(4 * n)) || (rc = skey.reserve(8 * n)) || (rc = sidx.reserve(4 * n)))
+    return rc;
+  auto done = [&](int r) {
+    (void)hipStreamSynchronize(h->stream);
+    for (DevBuf* b : {&key, &idx, &skey, &sidx, &temp}) b->release();
+    return r;
+  };
+  hipLaunchKernelGGL(k_vnorm, dim3(1024), dim3(256), 0, h->stream, h->d_v, n, h->kpad, key.as<unsigned long long>(),
+                     idx.as<int32_t>());
+  size_t tb = 0;
+  BLP_HIP_OR(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, tb, key.as<unsigned long long>(),
+                                                          skey.as<unsigned long long>(), idx.as<int32_t>(),
+                                                          sidx.as<int32_t>(), (int)n, 0, 64, h->stream), done);
+  if ((rc = temp.reserve(tb))) return done(rc);
+  BLP_HIP_OR(hipcub::DeviceRadixSort::SortPairsDescending(temp.p, tb, key.as<unsigned long long>(),
+                                                          skey.as<unsigned long long>(), idx.as<int32_t>(),
+                                                          sidx.as<int32_t>(), (int)n, 0, 64, h->stream), done);
+  BLP_HIP_OR(hipMalloc(&h->d_vtp, 8 * (size_t)h->kpad * np), done);
+  BLP_HIP_OR(hipMalloc(&h->d_vnp, 8 * (size_t)np), done);
+  BLP_HIP_OR(hipMalloc(&h->d_perm, 4 * (size_t)np), done);
+  BLP_HIP_OR(hipMalloc(&h->d_tiles, 8), done);
+  BLP_HIP_OR(hipMemsetAsync(h->d_tiles, 0, 8, h->stream), done);
+  hipLaunchKernelGGL(k_vt_perm, dim3(1024), dim3(256), 0, h->stream, h->d_vt, np, n, h->kpad,
+                     skey.as<unsigned long long>(), sidx.as<int32_t>(), h->d_vtp, h->d_vnp, h->d_perm);
+  BLP_HIP_OR(hipGetLastError(), done);
+  return done(BLP_OK);
+}
+
+// the two pruned passes: n1 first-pass chunks over the seed columns, n2 chunks over the rest
+template <int KP>
+static void svd_pr_launch(blp_svd* h, const TopkArgs& a, int64_t ublocks, int n1, int n2, int64_t seed_cols) {
+  const dim3 block(TK_WAVES * 64);
+  hipLaunchKernelGGL((k_svd_topk<KP, 1, TK_WAVES, 0, 1>), dim3((unsigned)ublocks, (unsigned)n1), block, 0, h->stream, a);
+  if (!n2) return;
+  TopkArgs b = a;
+  b.n_cols = h->n_cols;
+  b.col_base = seed_cols;
+  b.chunk_base = n1;
+  b.seeded = n1;
+  hipLaunchKernelGGL((k_svd_topk<KP, 1, TK_WAVES, 0, 1>), dim3((unsigned)ublocks, (unsigned)n2), block, 0, h->stream, b);
+}
 
 extern "C" {
 
@@ -398,7 +630,8 @@ int blp_svd_destroy(blp_svd* h) {
   timer_release(h->t_pairs);
   timer_release(h->t_topk);
   if (h->join_ev) (void)hipEventDestroy(h->join_ev);
-  for (void* p : {(void*)h->d_us, (void*)h->d_v, (void*)h->d_vt, (void*)h->d_ps, (void*)h->d_pc})
+  for (void* p : {(void*)h->d_us, (void*)h->d_v, (void*)h->d_vt, (void*)h->d_ps, (void*)h->d_pc, (void*)h->d_vtp,
+                  (void*)h->d_vnp, (void*)h->d_perm, (void*)h->d_tiles})
     if (p) (void)hipFree(p);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
@@ -445,6 +678,51 @@ int blp_svd_score_pairs(blp_svd* h, const int32_t* rows, const int32_t* cols, in
   return rc;
 }
 
+static int part_reserve(blp_svd* h, int64_t np) {
+  if (np <= h->part_cap) return BLP_OK;
+  if (h->d_ps) (void)hipFree(h->d_ps);
+  if (h->d_pc) (void)hipFree(h->d_pc);
+  h->d_ps = nullptr;
+  h->d_pc = nullptr;
+  h->part_cap = 0;
+  if (hipMalloc(&h->d_ps, 8 * np) != hipSuccess || hipMalloc(&h->d_pc, 4 * np) != hipSuccess)
+    return fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_svd_topk: partial buffers");
+  h->part_cap = np;
+  return BLP_OK;
+}
+
+// The norm-pruned top-k: pass 1 scores the TK_SEED_COLS columns of largest ||v|| for every user
+// (lists 0 .. n1-1, its tiles dealt round-robin over n1 chunks), pass 2 deals the remaining tiles
+// round-robin over TK_PR_CHUNKS chunks (lists n1 ..), each starting from the best k-th entry of
+// the first pass's lists and stopping at the norm bound; then the merge.
+static int svd_topk_pruned(blp_svd* h, const int32_t* d_users, int64_t n_users, const int64_t* d_exo,
+                           const int32_t* d_exc, int topk, int32_t* d_oc, double* d_os) {
+  const int64_t ublocks = (n_users + 16 * TK_WAVES - 1) / (16 * TK_WAVES);
+  const int64_t seed_cols = std::min<int64_t>(h->ncol_pad, TK_SEED_COLS);
+  const int64_t rest_tiles = (h->ncol_pad - seed_cols) / 16;
+  const int n2 = (int)std::min<int64_t>(TK_PR_CHUNKS, rest_tiles);
+  const int n1 = (int)std::max<int64_t>(1, std::min<int64_t>(TK_SEED_CHUNKS, seed_cols / 16));
+  const int n_chunks = n1 + n2;
+  int rc = part_reserve(h, n_users * n_chunks * topk);
+  if (rc) return rc;
+  TopkArgs a{h->d_us, h->d_vtp, d_users, d_exo, d_exc, n_users, std::min<int64_t>(h->n_cols, seed_cols), h->ncol_pad,
+             h->kpad, topk, 0, n_chunks, h->d_ps, h->d_pc, h->n_rows, h->d_perm, h->d_vnp, 0, 0, 0, h->d_tiles};
+  hipEvent_t t0;
+  if ((rc = timer_begin(h->t_topk, h->stream, &t0))) return rc;
+  switch (h->kpad) {
+    case 16: svd_pr_launch<16>(h, a, ublocks, n1, n2, seed_cols); break;
+    case 32: svd_pr_launch<32>(h, a, ublocks, n1, n2, seed_cols); break;
+    case 48: svd_pr_launch<48>(h, a, ublocks, n1, n2, seed_cols); break;
+    case 64: svd_pr_launch<64>(h, a, ublocks, n1, n2, seed_cols); break;
+    default: svd_pr_launch<128>(h, a, ublocks, n1, n2, seed_cols); break;
+  }
+  hipLaunchKernelGGL(k_svd_merge, dim3((unsigned)n_users), dim3(64), 0, h->stream, h->d_ps, h->d_pc, n_users,
+                     n_chunks, topk, d_os, d_oc);
+  if (hipGetLastError() != hipSuccess) return fail(BLP_E_HIP_BASE, "blp_svd_topk: launch failed");
+  h->tiles_total += ((n_users + 15) / 16) * (h->ncol_pad / 16);
+  return timer_end(h->t_topk, h->stream, t0);
+}
+
 // Enqueue the top-k of device-resident inputs on the handle's stream; the per-chunk partial
 // lists live in handle-owned scratch (grown on demand, freed with the handle).
 static int svd_topk_enqueue(blp_svd* h, const int32_t* d_users, int64_t n_users, const int64_t* d_exo,
@@ -475,25 +753,26 @@ static int svd_topk_enqueue(blp_svd* h, const int32_t* d_users, int64_t n_users,
     default: BLP_SVD_FN(128); break;
   }
 #undef BLP_SVD_FN
+  const bool prune = h->prune && !getenv("BLP_SVD_EXP");
+  if (prune) {
+    int rc0 = svd_prune_prepare(h);
+    if (rc0) return rc0;
+    return svd_topk_pruned(h, d_users, n_users, d_exo, d_exc, topk, d_oc, d_os);
+  }
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, waves * 64, 0) != hipSuccess || per_cu < 1) per_cu = 1;
   int n_chunks = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)h->n_cu * per_cu / ublocks, h->ncol_pad / 256));
   if (const char* e = getenv("BLP_SVD_CHUNKS")) n_chunks = std::max(1, std::min(atoi(e), (int)std::max<int64_t>(1, h->ncol_pad / 256)));
   const int64_t chunk = ((h->n_cols + n_chunks - 1) / n_chunks + 15) / 16 * 16;
   n_chunks = (int)((h->n_cols + chunk - 1) / chunk);
-  const int64_t np = n_users * n_chunks * topk;
-  if (np > h->part_cap) {
-    if (h->d_ps) (void)hipFree(h->d_ps);
-    if (h->d_pc) (void)hipFree(h->d_pc);
-    h->d_ps = nullptr;
-    h->d_pc = nullptr;
-    h->part_cap = 0;
-    if (hipMalloc(&h->d_ps, 8 * np) != hipSuccess || hipMalloc(&h->d_pc, 4 * np) != hipSuccess)
-      return fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_svd_topk: partial buffers");
-    h->part_cap = np;
+  {
+    int rc0 = part_reserve(h, n_users * n_chunks * topk);
+    if (rc0) return rc0;
   }
   TopkArgs a{h->d_us, h->d_vt, d_users, d_exo, d_exc, n_users, h->n_cols, h->ncol_pad, h->kpad, topk, chunk, n_chunks,
-             h->d_ps, h->d_pc, h->n_rows};
+             h->d_ps, h->d_pc, h->n_rows, nullptr, nullptr, 0, 0, 0, nullptr};
+  h->tiles_total += ((n_users + 15) / 16) * (h->ncol_pad / 16);
+  h->tiles_dense += ((n_users + 15) / 16) * (h->ncol_pad / 16);
   hipEvent_t t0;
   int rc = timer_begin(h->t_topk, h->stream, &t0);
   if (rc) return rc;
@@ -565,6 +844,28 @@ int blp_svd_topk(blp_svd* h, const int32_t* users, int64_t n_users, const int64_
     return fail(BLP_E_HIP_BASE, "blp_svd_topk: execution failed");
   }
   cleanup();
+  return BLP_OK;
+}
+
+int blp_svd_set_prune(blp_svd* h, int on) {
+  BLP_CHECK(h, BLP_E_ARG, "blp_svd_set_prune: null handle");
+  h->prune = on ? 1 : 0;
+  return BLP_OK;
+}
+
+int blp_svd_tiles(blp_svd* h, int64_t* scored, int64_t* dense) {
+  BLP_CHECK(h, BLP_E_ARG, "blp_svd_tiles: null handle");
+  BLP_HIP(hipSetDevice(h->device));
+  BLP_HIP(hipStreamSynchronize(h->stream));
+  unsigned long long v = 0;
+  if (h->d_tiles) {
+    BLP_HIP(hipMemcpy(&v, h->d_tiles, 8, hipMemcpyDeviceToHost));
+    BLP_HIP(hipMemset(h->d_tiles, 0, 8));
+  }
+  if (scored) *scored = (int64_t)v + h->tiles_dense;
+  if (dense) *dense = h->tiles_total;
+  h->tiles_total = 0;
+  h->tiles_dense = 0;
   return BLP_OK;
 }
 

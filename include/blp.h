@@ -315,6 +315,14 @@ int blp_svd_topk(blp_svd* h, const int32_t* users, int64_t n_users, const int64_
 int blp_svd_topk_device(blp_svd* h, const int32_t* d_users, int64_t n_users, const int64_t* d_ex_off,
                         const int32_t* d_ex_col, int topk, int32_t* d_out_cols, double* d_out_scores);
 int blp_svd_stream_join(blp_svd* h, void* stream, int handle_waits);
+/* blp_svd_set_prune: top-k by norm pruning (on = 1, the default) or the dense pass (0). Both
+ * give the same lists: a score is us[u] . v[b], so |score| <= ||us[u]|| ||v[b]||; with the
+ * businesses in ||v|| descending order a block of 16 users stops once that bound falls strictly
+ * below all its users' k-th scores. The dense pass reconstructs every (user, business) score.
+ * blp_svd_tiles: MFMA tiles (16 users x 16 businesses) scored by the top-k calls since the last
+ * call, and the tiles the dense pass would have scored over the same calls (then both reset). */
+int blp_svd_set_prune(blp_svd* h, int on);
+int blp_svd_tiles(blp_svd* h, int64_t* scored, int64_t* dense);
 int blp_svd_stats(blp_svd* h, int which, double* total_ms, int64_t* launches); /* 0 pairs, 1 top-k */
 int blp_svd_sync(blp_svd* h);
 

@@ -81,11 +81,14 @@ def test_topk_vs_numpy(gpu, k, n_cols, topk):
     us = rng.standard_normal((500, k))
     v = rng.standard_normal((n_cols, k))
     users = rng.choice(500, 150, replace=False).astype(np.int32)
-    cols, sc = DeviceSVD(us, v).topk(users, topk)
     full = us[users] @ v.T
     ec, es = _np_topk(full, topk)
-    np.testing.assert_array_equal(cols, ec)
-    np.testing.assert_allclose(sc, es, rtol=1e-12, atol=1e-12)
+    dev = DeviceSVD(us, v)
+    for prune in (True, False):
+        dev.set_prune(prune)
+        cols, sc = dev.topk(users, topk)
+        np.testing.assert_array_equal(cols, ec)
+        np.testing.assert_allclose(sc, es, rtol=1e-12, atol=1e-12)
 
 
 def test_topk_ties_and_exclusions(gpu):
@@ -98,10 +101,12 @@ def test_topk_ties_and_exclusions(gpu):
     excl = [np.sort(rng.choice(500, 30, replace=False)) for _ in users]
     off = np.r_[0, np.cumsum([len(e) for e in excl])]
     dev = DeviceSVD(us, v)
-    cols, sc = dev.topk(users, 20, exclude=(off, np.concatenate(excl)))
     full = us[users] @ v.T
     ec, es = _np_topk(full, 20, excl)
-    np.testing.assert_array_equal(cols, ec)
+    for prune in (True, False):  # equal norms (repeated rows) and equal scores: column order decides
+        dev.set_prune(prune)
+        cols, sc = dev.topk(users, 20, exclude=(off, np.concatenate(excl)))
+        np.testing.assert_array_equal(cols, ec)
     # more requested than available columns: trailing slots are -1
     small = DeviceSVD(us, v[:10])
     c2, _ = small.topk(users[:3], 15)
@@ -132,3 +137,37 @@ def test_topk_device_matches_host_entry(gpu):
             dev.sync()
             np.testing.assert_array_equal(dc.cpu().numpy(), hc)
             np.testing.assert_array_equal(ds.cpu().numpy(), hs)
+
+
+@pytest.mark.parametrize("n_cols,topk", [(30011, 20), (2500, 32), (2048 + 16, 5)])
+def test_topk_pruned_equals_dense(gpu, n_cols, topk):
+    """Norm pruning (blp_svd_set_prune, the default) gives the dense pass's lists bit for bit --
+    scores and columns, with exclusions -- on factors whose column norms are skewed like a
+    review graph's (a few popular businesses carry most of the mass), and scores far fewer
+    MFMA tiles. Sizes: many pruned chunks; seed pass plus a short rest; one tile past the seed."""
+    rng = np.random.default_rng(n_cols)
+    k = 64
+    us = rng.standard_normal((2000, k)) * rng.uniform(0.1, 3.0, (2000, 1))
+    pop = 1.0 / np.arange(1, n_cols + 1) ** 0.8
+    v = rng.standard_normal((n_cols, k)) * pop[rng.permutation(n_cols)][:, None]
+    users = rng.choice(2000, 700, replace=False).astype(np.int32)
+    excl = [np.sort(rng.choice(n_cols, int(rng.integers(0, 60)), replace=False)) for _ in users]
+    off = np.r_[0, np.cumsum([len(e) for e in excl])].astype(np.int64)
+    col = np.concatenate(excl).astype(np.int32)
+    dev = DeviceSVD(us, v)
+    dev.set_prune(False)
+    dc, ds = dev.topk(users, topk, exclude=(off, col))
+    dense_scored, dense_total = dev.tiles()
+    assert dense_scored == dense_total > 0
+    dev.set_prune(True)
+    pc, ps = dev.topk(users, topk, exclude=(off, col))
+    scored, total = dev.tiles()
+    np.testing.assert_array_equal(pc, dc)
+    np.testing.assert_array_equal(ps, ds)
+    assert total == dense_total
+    if n_cols > 20000:
+        assert scored < 0.5 * total, (scored, total)
+    full = us[users] @ v.T
+    ec, es = _np_topk(full, topk, excl)
+    np.testing.assert_array_equal(pc, ec)
+    np.testing.assert_allclose(ps, es, rtol=1e-12, atol=1e-12)
