@@ -366,14 +366,15 @@ def run_svd(args):
     pair_s = (p1 - p0) / 1e3 / max(q1 - q0, 1)
     pair_bytes = len(users) * 64 * 8 + len(pr) * (64 * 8 + 8 + 8)
     # parity of the top-k on >= 1000 users: fp64 numpy on the same factors, 64 users per chunk
-    n_chk = min(len(users), args.svd_parity_users)
+    n_chk = len(users) if args.svd_parity_users <= 0 else min(len(users), args.svd_parity_users)
     ok = True
+    bids = np.arange(B)
     for c0 in range(0, n_chk, 64):
         c1 = min(n_chk, c0 + 64)
         full = us[users[c0:c1]] @ vt_g
         for i in range(c0, c1):
             full[i - c0, ex_col[ex_off[i]:ex_off[i + 1]]] = -np.inf
-            ok &= bool(np.array_equal(np.lexsort((np.arange(B), -full[i - c0]))[:args.topk], cols[i]))
+            ok &= bool(np.array_equal(exact_topk(full[i - c0], bids, args.topk), cols[i]))
     del full
     svd_pmc = pmc_fields("k_svd_topk", "r*_svd_c4*.json")  # HBM bytes per launch (PMC)
     svd_pmc.pop("frac_dram", None)
@@ -437,40 +438,59 @@ def _oracle_graph(G):
     return coracle.OracleGraph(G.n, *_dense_edges(G)), ident, ident
 
 
-def topk_parity(G, src, k, res, n_users=200):
-    """Not timed: for `n_users` users the C oracle enumerates the exact hop-3 set, scores every
-    candidate (all host cores) and sorts (score desc, id asc); the Jaccard lists must match
-    exactly, so must the Adamic-Adar lists (exact sums on both sides; their values also equal
-    the pair kernel's), and |H3(u)| must equal the kernel's candidate count."""
+def exact_topk(scores, ids, k):
+    """Positions of the best k of `scores` (score descending, then id ascending), exactly: the
+    k-th largest value by partition, then a sort of everything at or above it (ties included)."""
+    n = len(scores)
+    if n > k:
+        vk = -np.partition(-scores, k - 1)[k - 1]
+        cand = np.flatnonzero(scores >= vk)
+    else:
+        cand = np.arange(n)
+    return cand[np.lexsort((ids[cand], -scores[cand]))][:k]
+
+
+def topk_parity(G, src, k, res, n_users=200, batch=250):
+    """Not timed: for `n_users` users (all of them with --topk-parity-users 0) the C oracle
+    enumerates the exact hop-3 set, scores every candidate (all host cores) and ranks them
+    (score desc, id asc), `batch` users at a time; the Jaccard lists must match exactly, so must
+    the Adamic-Adar lists (exact sums on both sides; their values also equal the pair
+    kernel's), and |H3(u)| must equal the kernel's candidate count."""
     og, to_o, from_o = _oracle_graph(G)
     nt = max(1, int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0)))
-    pick = np.sort(np.random.default_rng(5).choice(len(src), min(n_users, len(src)), replace=False))
-    xs_o = to_o[src[pick]]
-    counts, mem = og.hop3(xs_o)
-    xrep = np.repeat(xs_o, counts).astype(np.int32)
-    _, jac, aa, _ = og.score_pairs(xrep, mem, 7, nthreads=nt)
-    starts = np.r_[0, np.cumsum(counts)]
-    ok_j = ok_a = True
-    ok_n = bool(np.array_equal(res["ncand"][pick], counts))
+    n_users = len(src) if n_users <= 0 else min(n_users, len(src))
+    pick = np.sort(np.random.default_rng(5).choice(len(src), n_users, replace=False))
+    ok_j = ok_a = ok_n = True
+    n_cand = 0
     pair_x, pair_y, pair_v = [], [], []
-    for j, i in enumerate(pick):
-        s_, e_ = starts[j], starts[j + 1]
-        dense = from_o[mem[s_:e_]]
-        o = np.lexsort((dense, -jac[s_:e_]))[:k]
-        ok_j &= bool(np.array_equal(res["jaccard"][0][i][:len(o)], dense[o]) and
-                     np.array_equal(res["jaccard"][1][i][:len(o)], jac[s_:e_][o]))
-        # Adamic-Adar: exact sums on both sides (blp_internal.h), so the lists match exactly too
-        oa = np.lexsort((dense, -aa[s_:e_]))[:k]
-        ok_a &= bool(np.array_equal(res["adamic_adar"][0][i][:len(oa)], dense[oa]) and
-                     np.array_equal(res["adamic_adar"][1][i][:len(oa)], aa[s_:e_][oa]))
-        cols, sc = res["adamic_adar"][0][i], res["adamic_adar"][1][i]
-        v = cols >= 0
-        pair_x.append(np.full(int(v.sum()), src[i], np.int32))
-        pair_y.append(cols[v])
-        pair_v.append(sc[v])
+    for b0 in range(0, len(pick), batch):
+        pb = pick[b0:b0 + batch]
+        xs_o = to_o[src[pb]]
+        counts, mem = og.hop3(xs_o)
+        n_cand += int(counts.sum())
+        ok_n &= bool(np.array_equal(res["ncand"][pb], counts))
+        xrep = np.repeat(xs_o, counts).astype(np.int32)
+        _, jac, aa, _ = og.score_pairs(xrep, mem, 7, nthreads=nt)
+        starts = np.r_[0, np.cumsum(counts)]
+        for j, i in enumerate(pb):
+            s_, e_ = starts[j], starts[j + 1]
+            dense = from_o[mem[s_:e_]]
+            o = exact_topk(jac[s_:e_], dense, k)
+            ok_j &= bool(np.array_equal(res["jaccard"][0][i][:len(o)], dense[o]) and
+                         np.array_equal(res["jaccard"][1][i][:len(o)], jac[s_:e_][o]))
+            # Adamic-Adar: exact sums on both sides (blp_internal.h), so the lists match exactly too
+            oa = exact_topk(aa[s_:e_], dense, k)
+            ok_a &= bool(np.array_equal(res["adamic_adar"][0][i][:len(oa)], dense[oa]) and
+                         np.array_equal(res["adamic_adar"][1][i][:len(oa)], aa[s_:e_][oa]))
+            cols, sc = res["adamic_adar"][0][i], res["adamic_adar"][1][i]
+            v = cols >= 0
+            pair_x.append(np.full(int(v.sum()), src[i], np.int32))
+            pair_y.append(cols[v])
+            pair_v.append(sc[v])
+        del mem, xrep, jac, aa
     pair = G.score_pairs(np.concatenate(pair_x), np.concatenate(pair_y), 7)["adamic"]
     ok_a &= bool(np.array_equal(pair, np.concatenate(pair_v)))
-    return {"users_checked": int(len(pick)), "candidates_checked": int(counts.sum()), "jaccard_exact": ok_j,
+    return {"users_checked": int(len(pick)), "candidates_checked": n_cand, "jaccard_exact": ok_j,
             "adamic_exact_and_pair_kernel_equal": ok_a, "n_candidates_exact": ok_n}
 
 
@@ -566,7 +586,7 @@ def run_topk(args):
         cols_j, sc_j, _ = T.fetch("jaccard")
         cols_a, sc_a, _ = T.fetch("adamic_adar")
         out["parity"] = topk_parity(G, src, args.topk, {"jaccard": (cols_j, sc_j), "adamic_adar": (cols_a, sc_a),
-                                                        "ncand": ncand})
+                                                        "ncand": ncand}, n_users=args.topk_parity_users)
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = topk_cpu_baseline(G, src, args.topk, args.cpu_seconds)
     if dist.rank == 0:
@@ -956,7 +976,10 @@ def main():
     ap.add_argument("--no-collective-at-world1", action="store_true",
                     help="--mode sharded: at one rank, skip the process group (no RCCL call; the local partial)")
     ap.add_argument("--topk", type=int, default=20)
-    ap.add_argument("--svd-parity-users", type=int, default=1000, help="--mode svd: users whose top-k is checked")
+    ap.add_argument("--svd-parity-users", type=int, default=1000,
+                    help="--mode svd: users whose top-k is checked against numpy (0: every user)")
+    ap.add_argument("--topk-parity-users", type=int, default=200,
+                    help="--mode topk: users whose lists are checked against the C oracle (0: every user)")
     ap.add_argument("--topk-mask", type=int, default=6, help="methods of --mode topk (default Jaccard + AA)")
     args = ap.parse_args()
     relaunch_if_needed(args)
