@@ -1596,6 +1596,7 @@ struct ScoreArgs {
   unsigned long long* aa_part;  // [2 n_pairs] exact AA words carried between LDS chunks (k_score, chunks > 1)
   const SrcRec* rec;            // per active source (short-row scorer; null: gather from active[])
   int sched;                    // short-row scorer: 1 = claims dealt round-robin (BLP_STATIC), 0 = dequeued
+  int4* lq;                     // k_score_split: long-slice queues, SPLIT_LQ entries per workgroup
 };
 
 template <int BLOCK>
@@ -2132,6 +2133,8 @@ __global__ void k_row_splits(const int64_t* __restrict__ rp, const int32_t* __re
 }
 
 constexpr int SPLIT_CN_BITS = 24;  // k_score_split pk24: count field of the packed per-pair word
+constexpr int SPLIT_ROUND = 4;     // k_score_split: 64-pair groups per wave between block syncs
+constexpr int SPLIT_LQ = 16 * SPLIT_ROUND * 64;  // long-slice queue entries per workgroup (16 waves)
 
 template <int BLOCK, int CAP_WORDS, int SEG, int K>
 __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_split(ScoreArgs a, const int32_t* __restrict__ g_y,
@@ -2140,6 +2143,7 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
                                                        uint32_t* __restrict__ ph2, int64_t np, int pk24, int short_max,
                                                        const uint8_t* __restrict__ hflag, int32_t hxlo) {
   constexpr int NW = BLOCK / 64;
+  static_assert(NW * SPLIT_ROUND * 64 <= SPLIT_LQ, "a round's long slices fit the queue");
   // 128 KiB chunks (one workgroup per CU) use the row-chunk loops of the large scorer
   constexpr bool RCS = BLP_RC && CAP_WORDS > 16384;
   constexpr int HCS = RCS ? 1536 : 1;
@@ -2153,6 +2157,7 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
   __shared__ int red[NW];
   __shared__ int64_t s_item;
   __shared__ int s_nhot;
+  __shared__ int s_nl;  // long slices queued in this round
   __shared__ blp::HotRow s_hot[HOT_LIST];
   __shared__ long long s_wtab[RCS ? 256 : 1];  // code weights in LDS (the 64 KiB variant has no room)
   const int64_t CAP_BITS = a.cap_bits;
@@ -2164,6 +2169,7 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
   const long long* wtab = RCS ? s_wtab : a.wtab;
   if (RCS)  // the zero word and the build's dummy words past the bitmap
     for (int i = threadIdx.x; i < RC_EXTRA_WORDS; i += BLOCK) bm[CAP_WORDS + i] = 0;
+  if (threadIdx.x == 0) s_nl = 0;  // visible after the first barrier
   const int n_src = a.misc->n_active;
   // Items (source, chunk) are claimed per XCD group: workgroups b and b + 8 share an XCD (and its
   // L2; a placement observation, used for speed only), group g = b mod 8 takes the sources
@@ -2302,45 +2308,61 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
       if (threadIdx.x == 0) ph2[(int64_t)s * C + c] = (uint32_t)h2;
     }
     PROF(2)
-    // Pair-batch metadata: the pair's y and row start (chunk-independent), then its slice bounds
-    // for chunk c from the split table. The next batch's y / row start are loaded during this
-    // batch's offsets, its slice bounds right after this batch's scan, so each batch starts with
-    // its metadata in registers instead of two dependent global round trips.
-    int pf_y = 0;
-    int64_t pf_yb = 0;
-    int pf_s0 = 0, pf_s1 = 0;
-    if ((int)threadIdx.x < min(SEG, pcnt)) {
-      const int gp = pbeg + threadIdx.x;
-      pf_y = g_y[gp];
-      pf_yb = a.g_yb[gp];
-      const int32_t* sp = rsplit + ((int64_t)pf_y - rs_lo) * (C + 1) + c;
-      pf_s0 = sp[0];
-      pf_s1 = sp[1];
-    }
-    // Short slices (<= short_max ids; 128 KiB chunks): the thread that owns the pair scans its
-    // slice itself -- one part of up to 16 ids in registers, loaded before the batch's offset scan
-    // -- and writes the pair's packed words (lo = Σ W, hi = Σ (W >> 40) << 21 | count: exact, a
-    // slice's 16 terms undercount S by < 2^44) with plain stores; those rows get no chunks in the
-    // row-chunk loop, which then holds only the long slices. At config 5 (48 chunks) ~92% of the
-    // slices are short: no chunk, search, hint or LDS atomic for them.
+    // Pair slices of this chunk, in rounds of NW * SPLIT_ROUND groups of 64 pairs. Within a round
+    // every wave runs its own groups with no block barrier: lane = pair, its y / row start
+    // (coalesced), its slice bounds from the split table, then -- for a short slice (<=
+    // short_max ids; 128 KiB chunks; ~92 % of the slices at config 5) -- one part of up to 16
+    // ids in registers tested against the bitmap, and the slice's partial words sent from
+    // registers; the 16 waves of the CU hide each other's round trips. A long slice is queued
+    // (this workgroup's region of a global queue: row start, length, pair); at the end of the
+    // round the block scans the queued slices together with the row-chunk loops, SEG at a time.
+    // Partial words: lo = S mod 2^64, hi = (S >> 40) << 21 | count (exact: a slice's terms
+    // undercount S by < 2^44).
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t keep = a.idmask | 0x80000000u, c0u = (uint32_t)c0, wu = (uint32_t)width;
-    for (int sb = 0; sb < pcnt; sb += SEG) {
-      const int ns = min(SEG, pcnt - sb);
-      int len = 0;
-      int sv[SHORT_PART];
-      bool shorty = false;
-      if ((int)threadIdx.x < ns) {
-        s_start[threadIdx.x] = pf_yb + pf_s0;
-        len = pf_s1 - pf_s0;
-        shorty = RCS && len <= short_max;
-        if (shorty && len > 0) row_part(a.cw, pf_yb + pf_s0, len, 0, sv);
-        s_aa[2 * threadIdx.x] = 0;
-        s_aa[2 * threadIdx.x + 1] = 0;
+    int4* lq = a.lq + (int64_t)blockIdx.x * SPLIT_LQ;
+    // a (pair, chunk) slice's partial words into the pair's accumulators: only slices with a hit
+    // add anything, so no [chunks][pairs] partial arrays (config 5: 48 chunks x 199M pairs) and
+    // no dense combine reads. With Adamic-Adar and every scanned row shorter than 2^24 (pk24), two
+    // atomics: paa[2p] += S mod 2^64 and paa[2p + 1] += (S >> 52) << 24 | count -- exact
+    // (blp::aa_exact with hs = 52: the 2^52 remainders of at most C < 2^12 slices sum below 2^64;
+    // S >> 52 <= count * 2^7 per slice, so the high field stays below 2^40); otherwise the count,
+    // S mod 2^64 and S >> 32 in three.
+    auto emit = [&](int64_t gp, unsigned long long w0, unsigned long long w1) {
+      const unsigned c_t = (unsigned)(w1 & ((1u << PK_CN_BITS) - 1));
+      if (!c_t) return;
+      if (want_a) {
+        unsigned long long sh, sl;
+        blp::aa_exact(w0, w1 >> PK_CN_BITS, &sh, &sl, PK_HS);
+        atomicAdd(&paa[2 * gp], sl);
+        if (pk24) {
+          atomicAdd(&paa[2 * gp + 1], (((sh << 12) | (sl >> 52)) << SPLIT_CN_BITS) | c_t);
+        } else {
+          atomicAdd(&pcn[gp], c_t);
+          atomicAdd(&paa[2 * gp + 1], (sh << 32) | (sl >> 32));
+        }
+      } else {
+        atomicAdd(&pcn[gp], c_t);
       }
-      const int ns_next = min(SEG, pcnt - sb - SEG);  // <= 0: last batch
-      if constexpr (RCS) {
-        seg_offsets<BLOCK, K>(shorty ? 0 : len, ns, s_off, s_coff, red64);
-        if (shorty && len > 0) {
+    };
+    const int ngr = (pcnt + 63) >> 6;
+    for (int r0 = 0; r0 < ngr; r0 += NW * SPLIT_ROUND) {
+      const int r1 = min(ngr, r0 + NW * SPLIT_ROUND);
+      for (int g = r0 + wv; g < r1; g += NW) {
+        const int q = g * 64 + lane;
+        int len = 0;
+        int64_t st = 0;
+        if (q < pcnt) {
+          const int gp = pbeg + q;
+          const int y = g_y[gp];
+          const int32_t* sp = rsplit + ((int64_t)y - rs_lo) * (C + 1) + c;
+          const int s0 = sp[0];
+          len = sp[1] - s0;
+          st = a.g_yb[gp] + s0;
+        }
+        if (len > 0 && len <= short_max) {
+          int sv[SHORT_PART];
+          row_part(a.cw, st, len, 0, sv);
           uint32_t cnt = 0;
           unsigned long long lo = 0, hi40 = 0;
 #pragma unroll
@@ -2359,74 +2381,55 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
               }
             }
           }
-          s_aa[2 * threadIdx.x] = lo;
-          s_aa[2 * threadIdx.x + 1] = (hi40 << PK_CN_BITS) | cnt;
+          emit(pbeg + q, lo, (hi40 << PK_CN_BITS) | cnt);
+        } else if (len > short_max) {
+          const int slot = atomicAdd(&s_nl, 1);  // < SPLIT_LQ: a round holds NW * SPLIT_ROUND * 64 pairs
+          lq[slot] = make_int4((int32_t)(uint32_t)st, (int32_t)(st >> 32), len, pbeg + q);
         }
-      } else {
-        int tot;
-        const int ex = block_exscan<BLOCK>(len, red, &tot);
-        if ((int)threadIdx.x < ns) s_off[threadIdx.x] = ex;
-        if (threadIdx.x == 0) s_off[ns] = tot;
+      }
+      __syncthreads();
+      PROF(3)
+      const int nl = s_nl;
+      for (int b0 = 0; b0 < nl; b0 += SEG) {  // the round's long slices, block-wide
+        const int ns = min(SEG, nl - b0);
+        int len = 0, gp = 0;
+        if ((int)threadIdx.x < ns) {
+          const int4 e = lq[b0 + threadIdx.x];
+          s_start[threadIdx.x] = (int64_t)(((uint64_t)(uint32_t)e.y << 32) | (uint32_t)e.x);
+          len = e.z;
+          gp = e.w;
+          s_aa[2 * threadIdx.x] = 0;
+          s_aa[2 * threadIdx.x + 1] = 0;
+        }
+        if constexpr (RCS) {
+          seg_offsets<BLOCK, K>(len, ns, s_off, s_coff, red64);
+          const int shift = build_hint<BLOCK, HCS>(s_coff, ns, BLOCK, s_hint);
+          if (want_a)
+            rc_scan<BLOCK, K, true>(a.cw, a.idmask, a.idbits, a.aaw, wtab, s_start, s_off, s_coff, ns, c0, width, bm,
+                                    CAP_WORDS, nullptr, s_aa, threadIdx.x, s_hint, shift, true);
+          else
+            rc_scan<BLOCK, K, false>(a.cw, a.idmask, a.idbits, a.aaw, wtab, s_start, s_off, s_coff, ns, c0, width, bm,
+                                     CAP_WORDS, nullptr, s_aa, threadIdx.x, s_hint, shift, true);
+        } else {
+          int tot;
+          const int ex = block_exscan<BLOCK>(len, red, &tot);
+          if ((int)threadIdx.x < ns) s_off[threadIdx.x] = ex;
+          if (threadIdx.x == 0) s_off[ns] = tot;
+          __syncthreads();
+          if (want_a)
+            mp_scan<BLOCK, K, true, true>(a.cw, a.idmask, a.idbits, a.aaw, a.wtab, s_start, s_off, ns, c0, width, bm,
+                                          nullptr, s_aa, threadIdx.x);
+          else
+            mp_scan<BLOCK, K, false, true>(a.cw, a.idmask, a.idbits, a.aaw, a.wtab, s_start, s_off, ns, c0, width, bm,
+                                           nullptr, s_aa, threadIdx.x);
+        }
+        __syncthreads();
+        if ((int)threadIdx.x < ns) emit(gp, s_aa[2 * threadIdx.x], s_aa[2 * threadIdx.x + 1]);
         __syncthreads();
       }
-      PROF(3)
-      if ((int)threadIdx.x < ns_next) {
-        const int gp = pbeg + sb + SEG + threadIdx.x;
-        pf_y = g_y[gp];
-        pf_yb = a.g_yb[gp];
-      }
-      // packed count + high word (a chunk holds < 2^21 nodes), converted per slice below
-      if constexpr (RCS) {
-        const int shift = build_hint<BLOCK, HCS>(s_coff, ns, BLOCK, s_hint);
-        if (want_a)
-          rc_scan<BLOCK, K, true>(a.cw, a.idmask, a.idbits, a.aaw, wtab, s_start, s_off, s_coff, ns, c0, width, bm,
-                                  CAP_WORDS, nullptr, s_aa, threadIdx.x, s_hint, shift, true);
-        else
-          rc_scan<BLOCK, K, false>(a.cw, a.idmask, a.idbits, a.aaw, wtab, s_start, s_off, s_coff, ns, c0, width, bm,
-                                   CAP_WORDS, nullptr, s_aa, threadIdx.x, s_hint, shift, true);
-      } else if (want_a) {
-        mp_scan<BLOCK, K, true, true>(a.cw, a.idmask, a.idbits, a.aaw, a.wtab, s_start, s_off, ns, c0, width, bm,
-                                      nullptr, s_aa, threadIdx.x);
-      } else {
-        mp_scan<BLOCK, K, false, true>(a.cw, a.idmask, a.idbits, a.aaw, a.wtab, s_start, s_off, ns, c0, width, bm,
-                                       nullptr, s_aa, threadIdx.x);
-      }
-      if ((int)threadIdx.x < ns_next) {  // the next batch's slice bounds, in flight over the output phase
-        const int32_t* sp = rsplit + ((int64_t)pf_y - rs_lo) * (C + 1) + c;
-        pf_s0 = sp[0];
-        pf_s1 = sp[1];
-      }
+      if (threadIdx.x == 0) s_nl = 0;
       __syncthreads();
       PROF(4)
-      // a pair's chunk partials meet in per-pair accumulators: only (pair, chunk) slices with a
-      // hit add anything, so no [chunks][pairs] partial arrays (config 5: 48 chunks x 199M
-      // pairs) and no dense combine reads. With Adamic-Adar and every scanned row shorter than
-      // 2^24 (pk24), two atomics per slice: paa[2p] += S mod 2^64 and paa[2p + 1] +=
-      // (S >> 52) << 24 | count -- exact (blp::aa_exact with hs = 52: the 2^52 remainders of at
-      // most C < 2^12 slices sum below 2^64; S >> 52 <= count * 2^7 per slice, so the high field
-      // stays below 2^40); otherwise the count, S mod 2^64 and S >> 32 in three.
-      for (int t = threadIdx.x; t < ns; t += BLOCK) {
-        const int64_t gp = pbeg + sb + t;
-        const unsigned c_t = (unsigned)(s_aa[2 * t + 1] & ((1u << PK_CN_BITS) - 1));
-        if (c_t) {
-          if (want_a) {
-            // the slice's exact 128-bit sum S from (lo, hi in 2^40 units)
-            unsigned long long sh, sl;
-            blp::aa_exact(s_aa[2 * t], s_aa[2 * t + 1] >> PK_CN_BITS, &sh, &sl, PK_HS);
-            atomicAdd(&paa[2 * gp], sl);
-            if (pk24) {
-              atomicAdd(&paa[2 * gp + 1], (((sh << 12) | (sl >> 52)) << SPLIT_CN_BITS) | c_t);
-            } else {
-              atomicAdd(&pcn[gp], c_t);
-              atomicAdd(&paa[2 * gp + 1], (sh << 32) | (sl >> 32));
-            }
-          } else {
-            atomicAdd(&pcn[gp], c_t);
-          }
-        }
-      }
-      __syncthreads();
-      PROF(5)
     }
   }
   PROF_FLUSH
@@ -2832,6 +2835,7 @@ struct blp_batch {
   int64_t rs_lo = 0;     // first node of the split table
   int32_t* d_gy = nullptr;     // grouped position -> y (split mode)
   int32_t* d_rsplit = nullptr; // [n][split + 1] row offsets where neighbour ids cross chunk boundaries
+  int4* d_lq = nullptr;        // k_score_split's long-slice queues (SPLIT_LQ per resident workgroup)
   uint32_t* d_pcn = nullptr;   // [n_pairs] counts, summed over chunks (zeroed per score)
   unsigned long long* d_paa = nullptr;  // [n_pairs][2] exact AA words, summed over chunks
   unsigned long long* d_aa_part = nullptr;  // [n_pairs][2] exact AA words between LDS chunks (chunks > 1)
@@ -3200,7 +3204,8 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
         hipMalloc(&b->d_rsplit, 4 * (size_t)nrows * (C + 1)) != hipSuccess ||
         hipMalloc(&b->d_pcn, 4 * (size_t)n_pairs) != hipSuccess ||
         hipMalloc(&b->d_paa, 16 * (size_t)n_pairs) != hipSuccess ||
-        hipMalloc(&b->d_ph2, 4 * (size_t)std::max<int64_t>(b->n_sources, 1) * C) != hipSuccess)
+        hipMalloc(&b->d_ph2, 4 * (size_t)std::max<int64_t>(b->n_sources, 1) * C) != hipSuccess ||
+        hipMalloc(&b->d_lq, sizeof(int4) * SPLIT_LQ * (size_t)g->n_cu * 2) != hipSuccess)
       return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: split buffers"));
     hipLaunchKernelGGL(k_row_splits, dim3(2048), dim3(256), 0, g->stream, g->d_rp, g->d_ci, rows_lo, nrows, b->lo,
                        b->cap_bits, C, b->d_rsplit);
@@ -3281,7 +3286,7 @@ int blp_batch_destroy(blp_batch* b) {
   b->scratch.release();
   if (b->stream) (void)hipStreamDestroy(b->stream);
   void* ps[] = {b->d_x,    b->d_y,    b->d_cn,   b->d_jac,  b->d_aa,          b->d_gout,        b->d_gyb,
-                b->d_gyl,  b->d_misc, b->d_heavy_slot, b->d_heavy_bm, b->d_heavy_items, b->d_gbm, b->d_gy, b->d_rsplit, b->d_pcn, b->d_paa, b->d_ph2, b->d_aa_part, b->d_rec, b->d_hflag};
+                b->d_gyl,  b->d_misc, b->d_heavy_slot, b->d_heavy_bm, b->d_heavy_items, b->d_gbm, b->d_gy, b->d_rsplit, b->d_pcn, b->d_paa, b->d_ph2, b->d_aa_part, b->d_rec, b->d_hflag, b->d_lq};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   delete b;
@@ -3510,6 +3515,7 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
     // slices of <= short_max ids scanned by their pair's thread (128 KiB chunks; BLP_SPLIT_SHORT=0: off)
     const int short_max = std::min(SHORT_PART, getenv("BLP_SPLIT_SHORT") ? atoi(getenv("BLP_SPLIT_SHORT")) : SHORT_PART);
     a.sched = getenv("BLP_SPLIT_ONEQ") ? 1 : 0;  // k_score_split: 1 = one global item queue (no XCD groups)
+    a.lq = b->d_lq;
     if (g->d_wp && !getenv("BLP_NO_WEDGE")) {  // sources with wedge rows build from them (split and hash kernels)
       a.wp = g->d_wp;
       a.wedge = reinterpret_cast<const uint4*>(g->d_wedge);
@@ -3527,12 +3533,12 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
     int per_cu = 1;
     if (b->split_big) {
       BLP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_score_split<S_BLOCK, S_CAP_BIG, S_SEG, 8>, S_BLOCK, 0));
-      hipLaunchKernelGGL((k_score_split<S_BLOCK, S_CAP_BIG, S_SEG, 8>), dim3(scu * std::max(per_cu, 1)), dim3(S_BLOCK),
+      hipLaunchKernelGGL((k_score_split<S_BLOCK, S_CAP_BIG, S_SEG, 8>), dim3(scu * std::min(std::max(per_cu, 1), 2)), dim3(S_BLOCK),
                          0, b->stream, a, b->d_gy, b->d_rsplit, b->rs_lo, b->split, b->d_pcn, b->d_paa, b->d_ph2, np, pk24,
                          short_max, b->d_hflag, (int32_t)b->xlo);
     } else {
       BLP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_score_split<S_BLOCK, S_CAP, S_SEG, 8>, S_BLOCK, 0));
-      hipLaunchKernelGGL((k_score_split<S_BLOCK, S_CAP, S_SEG, 8>), dim3(scu * std::max(per_cu, 1)), dim3(S_BLOCK), 0,
+      hipLaunchKernelGGL((k_score_split<S_BLOCK, S_CAP, S_SEG, 8>), dim3(scu * std::min(std::max(per_cu, 1), 2)), dim3(S_BLOCK), 0,
                          b->stream, a, b->d_gy, b->d_rsplit, b->rs_lo, b->split, b->d_pcn, b->d_paa, b->d_ph2, np, pk24,
                          short_max, b->d_hflag, (int32_t)b->xlo);
     }
