@@ -1597,6 +1597,7 @@ struct ScoreArgs {
   const SrcRec* rec;            // per active source (short-row scorer; null: gather from active[])
   int sched;                    // short-row scorer: 1 = claims dealt round-robin (BLP_STATIC), 0 = dequeued
   int4* lq;                     // k_score_split: long-slice queues, SPLIT_LQ entries per workgroup
+  int split_round;              // k_score_split: 64-pair groups per wave per round
 };
 
 template <int BLOCK>
@@ -2133,8 +2134,9 @@ __global__ void k_row_splits(const int64_t* __restrict__ rp, const int32_t* __re
 }
 
 constexpr int SPLIT_CN_BITS = 24;  // k_score_split pk24: count field of the packed per-pair word
-constexpr int SPLIT_ROUND = 4;     // k_score_split: 64-pair groups per wave between block syncs
-constexpr int SPLIT_LQ = 16 * SPLIT_ROUND * 64;  // long-slice queue entries per workgroup (16 waves)
+constexpr int SPLIT_ROUND = 16;      // k_score_split: 64-pair groups per wave between block syncs (default)
+constexpr int SPLIT_ROUND_MAX = 16;  // ... at most (BLP_SPLIT_ROUND; config 5: 4 -> 341, 8 -> 317-324, 16 -> 322 ms)
+constexpr int SPLIT_LQ = 16 * SPLIT_ROUND_MAX * 64;  // long-slice queue entries per workgroup (16 waves)
 
 template <int BLOCK, int CAP_WORDS, int SEG, int K>
 __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_split(ScoreArgs a, const int32_t* __restrict__ g_y,
@@ -2143,7 +2145,7 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
                                                        uint32_t* __restrict__ ph2, int64_t np, int pk24, int short_max,
                                                        const uint8_t* __restrict__ hflag, int32_t hxlo) {
   constexpr int NW = BLOCK / 64;
-  static_assert(NW * SPLIT_ROUND * 64 <= SPLIT_LQ, "a round's long slices fit the queue");
+  static_assert(NW * SPLIT_ROUND_MAX * 64 <= SPLIT_LQ, "a round's long slices fit the queue");
   // 128 KiB chunks (one workgroup per CU) use the row-chunk loops of the large scorer
   constexpr bool RCS = BLP_RC && CAP_WORDS > 16384;
   constexpr int HCS = RCS ? 1536 : 1;
@@ -2346,16 +2348,16 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
       }
     };
     const int ngr = (pcnt + 63) >> 6;
-    for (int r0 = 0; r0 < ngr; r0 += NW * SPLIT_ROUND) {
-      const int r1 = min(ngr, r0 + NW * SPLIT_ROUND);
+    const int rg = NW * a.split_round;
+    for (int r0 = 0; r0 < ngr; r0 += rg) {
+      const int r1 = min(ngr, r0 + rg);
       for (int g = r0 + wv; g < r1; g += NW) {
         const int q = g * 64 + lane;
         int len = 0;
         int64_t st = 0;
         if (q < pcnt) {
           const int gp = pbeg + q;
-          const int y = g_y[gp];
-          const int32_t* sp = rsplit + ((int64_t)y - rs_lo) * (C + 1) + c;
+          const int32_t* sp = rsplit + ((int64_t)g_y[gp] - rs_lo) * (C + 1) + c;
           const int s0 = sp[0];
           len = sp[1] - s0;
           st = a.g_yb[gp] + s0;
@@ -3516,6 +3518,8 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
     const int short_max = std::min(SHORT_PART, getenv("BLP_SPLIT_SHORT") ? atoi(getenv("BLP_SPLIT_SHORT")) : SHORT_PART);
     a.sched = getenv("BLP_SPLIT_ONEQ") ? 1 : 0;  // k_score_split: 1 = one global item queue (no XCD groups)
     a.lq = b->d_lq;
+    a.split_round = std::max(1, std::min(SPLIT_ROUND_MAX, getenv("BLP_SPLIT_ROUND") ? atoi(getenv("BLP_SPLIT_ROUND"))
+                                                                                     : SPLIT_ROUND));  // tuning knob
     if (g->d_wp && !getenv("BLP_NO_WEDGE")) {  // sources with wedge rows build from them (split and hash kernels)
       a.wp = g->d_wp;
       a.wedge = reinterpret_cast<const uint4*>(g->d_wedge);
