@@ -61,6 +61,8 @@ struct Misc {
   int hq;     // k_score_hash's queue head
   int n_items;  // item grouping: items planned by k_item_plan
   int qh[8];  // k_score_split: one queue head per XCD group (sources s = g mod 8)
+  int n_hash_front;  // split batches with hash-routed sources: the active list is partitioned,
+  int n_split_back;  // hash sources in [0, n_hash_front), split sources after (k_hash_partition)
 };
 
 // ------------------------------------------------------------------ grouping kernels
@@ -2142,8 +2144,7 @@ template <int BLOCK, int CAP_WORDS, int SEG, int K>
 __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_split(ScoreArgs a, const int32_t* __restrict__ g_y,
                                                        const int32_t* __restrict__ rsplit, int64_t rs_lo, int C,
                                                        uint32_t* __restrict__ pcn, unsigned long long* __restrict__ paa,
-                                                       uint32_t* __restrict__ ph2, int64_t np, int pk24, int short_max,
-                                                       const uint8_t* __restrict__ hflag, int32_t hxlo) {
+                                                       uint32_t* __restrict__ ph2, int64_t np, int pk24, int short_max) {
   constexpr int NW = BLOCK / 64;
   static_assert(NW * SPLIT_ROUND_MAX * 64 <= SPLIT_LQ, "a round's long slices fit the queue");
   // 128 KiB chunks (one workgroup per CU) use the row-chunk loops of the large scorer
@@ -2172,7 +2173,8 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
   if (RCS)  // the zero word and the build's dummy words past the bitmap
     for (int i = threadIdx.x; i < RC_EXTRA_WORDS; i += BLOCK) bm[CAP_WORDS + i] = 0;
   if (threadIdx.x == 0) s_nl = 0;  // visible after the first barrier
-  const int n_src = a.misc->n_active;
+  const int s_base = a.misc->n_hash_front;  // hash-routed sources (partitioned to the front) are not ours
+  const int n_src = a.misc->n_active - s_base;
   // Items (source, chunk) are claimed per XCD group: workgroups b and b + 8 share an XCD (and its
   // L2; a placement observation, used for speed only), group g = b mod 8 takes the sources
   // s = g (mod 8), all C chunks of a source in a row, so the C workgroups scanning one source's
@@ -2191,7 +2193,8 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
         const int64_t n_g = n_src > g ? (n_src - g + ngrp - 1) / ngrp : 0;
         const int k = atomicAdd(&a.misc->qh[g], 1);
         if ((int64_t)k < n_g * C) {
-          s_item = (int64_t)(g + (int64_t)ngrp * (k / C)) * C + k % C;
+          // BLP_SPLIT_ONEQ=2: chunk-major order (every source's chunk c before any chunk c + 1)
+          s_item = a.sched == 2 ? (int64_t)(k % n_g) * C + k / n_g : (int64_t)(g + (int64_t)ngrp * (k / C)) * C + k % C;
           break;
         }
         ++gq;
@@ -2202,9 +2205,8 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
     __syncthreads();
     if (item < 0) break;
     PROF(0)
-    const int s = (int)(item / C), c = (int)(item % C);
+    const int s = s_base + (int)(item / C), c = (int)(item % C);
     const int x = a.active[s];
-    if (hflag && hflag[x - hxlo]) continue;  // uniform: scored by k_score_hash
     const int pbeg = a.off[x], pcnt = a.cnt[x];
     const int64_t xb = a.rp[x], xe = a.rp[x + 1];
     const int hslot = a.heavy_slot ? a.heavy_slot[x] : -1;
@@ -2440,15 +2442,14 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
 // one wave per active source: sum the chunk partials of each of its pairs, then Jaccard
 __global__ __launch_bounds__(256) void k_split_combine(ScoreArgs a, int C, const uint32_t* __restrict__ pcn,
                                                       const unsigned long long* __restrict__ paa,
-                                                      const uint32_t* __restrict__ ph2, int64_t np, int pk24,
-                                                      const uint8_t* __restrict__ hflag, int32_t hxlo) {
+                                                      const uint32_t* __restrict__ ph2, int64_t np, int pk24) {
   const int lane = threadIdx.x & 63;
   const int n_active = a.misc->n_active;
   const bool want_j = (a.mask & BLP_JACCARD) != 0;
   const bool want_a = (a.mask & BLP_ADAMIC) != 0;
-  for (int s = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; s < n_active; s += (gridDim.x * blockDim.x) >> 6) {
+  const int s_base = a.misc->n_hash_front;  // sources before it were scored by k_score_hash
+  for (int s = s_base + ((blockIdx.x * blockDim.x + threadIdx.x) >> 6); s < n_active; s += (gridDim.x * blockDim.x) >> 6) {
     const int x = a.active[s];
-    if (hflag && hflag[x - hxlo]) continue;  // scored by k_score_hash
     long long h2 = 0;
     if (want_j)
       for (int c = 0; c < C; ++c) h2 += ph2[(int64_t)s * C + c];
@@ -2473,6 +2474,38 @@ __global__ __launch_bounds__(256) void k_split_combine(ScoreArgs a, int C, const
   }
 }
 
+// Split batches with hash-routed sources: one pass partitions the active list so that
+// k_score_hash claims only its own sources from the front and k_score_split / k_split_combine
+// only theirs after them. Each wave moves 64 consecutive entries (ballot, one atomic per list),
+// so neighbouring sources stay neighbours inside a wave's run. Without it both persistent
+// kernels claimed every source and skipped the other's -- three dependent round trips and two
+// block barriers per skipped (source, chunk) item.
+__global__ __launch_bounds__(256) void k_hash_partition(const int32_t* __restrict__ active, Misc* __restrict__ misc,
+                                                        const uint8_t* __restrict__ hflag, int32_t xlo,
+                                                        int32_t* __restrict__ out) {
+  const int n = misc->n_active;
+  const int lane = threadIdx.x & 63;
+  const int nwv = (gridDim.x * blockDim.x) >> 6;
+  for (int base = ((blockIdx.x * blockDim.x + threadIdx.x) >> 6) * 64; base < n; base += nwv * 64) {
+    const int i = base + lane;
+    const int x = i < n ? active[i] : 0;
+    const bool h = i < n && hflag[x - xlo];
+    const unsigned long long hb = __ballot(h), sb = __ballot(i < n && !h);
+    const unsigned long long below = (1ull << lane) - 1;
+    int fh = 0, bs = 0;
+    if (lane == 0) {
+      fh = hb ? atomicAdd(&misc->n_hash_front, __popcll(hb)) : 0;
+      bs = sb ? atomicAdd(&misc->n_split_back, __popcll(sb)) : 0;
+    }
+    fh = __shfl(fh, 0);
+    bs = __shfl(bs, 0);
+    if (h)
+      out[fh + __popcll(hb & below)] = x;
+    else if (i < n)
+      out[n - bs - __popcll(sb) + __popcll(sb & below)] = x;
+  }
+}
+
 // ------------------------------------------------------------------ hash-set scorer
 // Universes wider than LDS (the chunk-parallel scorer's batches) whose source has a SMALL H2: the
 // business side of config 5 (H2(b) = the businesses co-reviewed with b, ~20 |N(b)| ids among 2M)
@@ -2489,13 +2522,13 @@ __device__ inline uint32_t hs_slot(uint32_t v) {
 }
 
 template <int BLOCK, int HT>
-__global__ __launch_bounds__(BLOCK) void k_score_hash(ScoreArgs a, const uint8_t* __restrict__ hflag, int32_t xlo) {
+__global__ __launch_bounds__(BLOCK) void k_score_hash(ScoreArgs a) {
   constexpr int NW = BLOCK / 64;
   static_assert((HT & (HT - 1)) == 0, "HT: a power of two");
   __shared__ uint32_t tab[HT];
   __shared__ unsigned long long red64[NW];
   __shared__ int s_src;
-  const int n_active = a.misc->n_active;
+  const int n_hash = a.misc->n_hash_front;  // the partitioned active list's hash sources come first
   const bool want_j = (a.mask & BLP_JACCARD) != 0;
   const bool want_a = (a.mask & BLP_ADAMIC) != 0;
   const uint32_t c0u = (uint32_t)a.lo, wu = (uint32_t)(a.hi - a.lo);
@@ -2515,9 +2548,8 @@ __global__ __launch_bounds__(BLOCK) void k_score_hash(ScoreArgs a, const uint8_t
     __syncthreads();
     const int si = s_src;
     __syncthreads();
-    if (si >= n_active) break;
+    if (si >= n_hash) break;
     const int x = a.active[si];
-    if (!hflag[x - xlo]) continue;  // uniform: the chunk-parallel scorer takes it
     for (int i = threadIdx.x; i < HT / 4; i += BLOCK) reinterpret_cast<uint4*>(tab)[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
     __syncthreads();
     // build: one row N(z) per thread, 16 ids at a time (rows padded past nnz), or x's wedge row
@@ -2860,6 +2892,7 @@ struct blp_batch {
   int cus = 0;  // CUs the persistent block scorer may occupy (0: all; set by blp_batches_score)
   SrcRec* d_rec = nullptr;  // [n_sources] source records of the short-row scorer (or null)
   uint8_t* d_hflag = nullptr;  // [xspan] 1: source scored by k_score_hash (split batches; or null)
+  int32_t* d_active2 = nullptr;  // the active list partitioned by k_hash_partition (with d_hflag)
   int64_t n_hash = 0;          // such sources
   bool use_short = false;   // the short-row scorer takes this batch (decided once, at create)
   int64_t work_elems = 0;  // planned build + scan elements (co-scheduling estimate)
@@ -3227,7 +3260,8 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
         ++b->n_hash;
       }
     if (b->n_hash) {
-      if (hipMalloc(&b->d_hflag, hf.size()) != hipSuccess)
+      if (hipMalloc(&b->d_hflag, hf.size()) != hipSuccess ||
+          hipMalloc(&b->d_active2, 4 * (hf.size() + 1)) != hipSuccess)
         return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: hash flags"));
       BLP_HIP_OR(hipMemcpy(b->d_hflag, hf.data(), hf.size(), hipMemcpyHostToDevice), bail);
     }
@@ -3288,7 +3322,7 @@ int blp_batch_destroy(blp_batch* b) {
   b->scratch.release();
   if (b->stream) (void)hipStreamDestroy(b->stream);
   void* ps[] = {b->d_x,    b->d_y,    b->d_cn,   b->d_jac,  b->d_aa,          b->d_gout,        b->d_gyb,
-                b->d_gyl,  b->d_misc, b->d_heavy_slot, b->d_heavy_bm, b->d_heavy_items, b->d_gbm, b->d_gy, b->d_rsplit, b->d_pcn, b->d_paa, b->d_ph2, b->d_aa_part, b->d_rec, b->d_hflag, b->d_lq};
+                b->d_gyl,  b->d_misc, b->d_heavy_slot, b->d_heavy_bm, b->d_heavy_items, b->d_gbm, b->d_gy, b->d_rsplit, b->d_pcn, b->d_paa, b->d_ph2, b->d_aa_part, b->d_rec, b->d_hflag, b->d_lq, b->d_active2};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   delete b;
@@ -3516,7 +3550,8 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
     const int pk24 = (mask & BLP_ADAMIC) && g->max_row < (int64_t(1) << SPLIT_CN_BITS) && !getenv("BLP_SPLIT_NOPK");
     // slices of <= short_max ids scanned by their pair's thread (128 KiB chunks; BLP_SPLIT_SHORT=0: off)
     const int short_max = std::min(SHORT_PART, getenv("BLP_SPLIT_SHORT") ? atoi(getenv("BLP_SPLIT_SHORT")) : SHORT_PART);
-    a.sched = getenv("BLP_SPLIT_ONEQ") ? 1 : 0;  // k_score_split: 1 = one global item queue (no XCD groups)
+    // k_score_split: 1 = one global item queue (no XCD groups), 2 = one queue in chunk-major order
+    a.sched = getenv("BLP_SPLIT_ONEQ") ? (atoi(getenv("BLP_SPLIT_ONEQ")) == 2 ? 2 : 1) : 0;
     a.lq = b->d_lq;
     a.split_round = std::max(1, std::min(SPLIT_ROUND_MAX, getenv("BLP_SPLIT_ROUND") ? atoi(getenv("BLP_SPLIT_ROUND"))
                                                                                      : SPLIT_ROUND));  // tuning knob
@@ -3526,10 +3561,13 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
     }
     const int scu = b->cus > 0 ? b->cus : g->n_cu;  // CUs the persistent grids may fill (blp_batches_score)
     if (b->d_hflag) {  // small-H2 sources first, on their own hash-set kernel
+      hipLaunchKernelGGL(k_hash_partition, dim3(g->n_cu * 4), dim3(256), 0, b->stream, a.active, b->d_misc, b->d_hflag,
+                         (int32_t)b->xlo, b->d_active2);
+      BLP_HIP(hipGetLastError());
+      a.active = b->d_active2;
       int hcu = 1;
       BLP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&hcu, k_score_hash<HS_BLOCK, HS_HT>, HS_BLOCK, 0));
-      hipLaunchKernelGGL((k_score_hash<HS_BLOCK, HS_HT>), dim3(scu * std::max(hcu, 1)), dim3(HS_BLOCK), 0, b->stream, a,
-                         b->d_hflag, (int32_t)b->xlo);
+      hipLaunchKernelGGL((k_score_hash<HS_BLOCK, HS_HT>), dim3(scu * std::max(hcu, 1)), dim3(HS_BLOCK), 0, b->stream, a);
       BLP_HIP(hipGetLastError());
     }
     if (!pk24) BLP_HIP(hipMemsetAsync(b->d_pcn, 0, 4 * (size_t)np, b->stream));
@@ -3539,16 +3577,16 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
       BLP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_score_split<S_BLOCK, S_CAP_BIG, S_SEG, 8>, S_BLOCK, 0));
       hipLaunchKernelGGL((k_score_split<S_BLOCK, S_CAP_BIG, S_SEG, 8>), dim3(scu * std::min(std::max(per_cu, 1), 2)), dim3(S_BLOCK),
                          0, b->stream, a, b->d_gy, b->d_rsplit, b->rs_lo, b->split, b->d_pcn, b->d_paa, b->d_ph2, np, pk24,
-                         short_max, b->d_hflag, (int32_t)b->xlo);
+                         short_max);
     } else {
       BLP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_score_split<S_BLOCK, S_CAP, S_SEG, 8>, S_BLOCK, 0));
       hipLaunchKernelGGL((k_score_split<S_BLOCK, S_CAP, S_SEG, 8>), dim3(scu * std::min(std::max(per_cu, 1), 2)), dim3(S_BLOCK), 0,
                          b->stream, a, b->d_gy, b->d_rsplit, b->rs_lo, b->split, b->d_pcn, b->d_paa, b->d_ph2, np, pk24,
-                         short_max, b->d_hflag, (int32_t)b->xlo);
+                         short_max);
     }
     BLP_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_split_combine, dim3(g->n_cu * 8), dim3(256), 0, b->stream, a, b->split, b->d_pcn, b->d_paa,
-                       b->d_ph2, np, pk24, b->d_hflag, (int32_t)b->xlo);
+                       b->d_ph2, np, pk24);
     BLP_HIP(hipGetLastError());
   } else if (np && b->global) {
     a.hot_idx = nullptr;

@@ -113,6 +113,7 @@ def test_general_graph_exact_distance(gpu):
     {"BLP_SPLIT": "3", "BLP_SPLIT_BIG": "1", "BLP_SPLIT_SHORT": "0", "BLP_NO_HASH": "1"},  # ... no thread-per-slice short path
     {"BLP_SPLIT": "2", "BLP_SPLIT_BIG": "1", "BLP_SPLIT_SHORT": "4", "BLP_NO_HASH": "1"},  # ... short path only below 5 ids
     {"BLP_SPLIT": "3", "BLP_SPLIT_BIG": "1", "BLP_SPLIT_ONEQ": "1", "BLP_NO_HASH": "1"},   # ... one item queue (no XCD groups)
+    {"BLP_SPLIT": "3", "BLP_SPLIT_BIG": "1", "BLP_SPLIT_ONEQ": "2", "BLP_NO_HASH": "1"},   # ... one queue, chunk-major
     {"BLP_SPLIT": "24", "BLP_SPLIT_BIG": "1", "BLP_NO_HASH": "1"},          # ... same, many chunks
     {"BLP_SPLIT": "3", "BLP_SPLIT_BIG": "1", "BLP_NO_HASH": "1", "BLP_NO_WEDGE": "1"},  # ... members' rows from the CSR, not wedge rows
     {"BLP_SPLIT": "3", "BLP_SPLIT_BIG": "1", "BLP_HASH_WORK": "600", "BLP_NO_WEDGE": "1"},  # hash-set build from the CSR
