@@ -2516,6 +2516,7 @@ __global__ __launch_bounds__(256) void k_hash_partition(const int32_t* __restric
 // x and N(x) are then tombstoned (exact distance 2) and every pair's N(y) probes the set. One
 // pair per thread, results written directly (cn, Jaccard, exact Adamic-Adar words).
 constexpr uint32_t HS_EMPTY = 0xFFFFFFFFu;
+constexpr int HS_DQ = 4;  // k_score_hash: sources per claim
 template <int HT>
 __device__ inline uint32_t hs_slot(uint32_t v) {
   return (v * 2654435761u) >> (32 - __builtin_ctz(HT));
@@ -2543,18 +2544,36 @@ __global__ __launch_bounds__(BLOCK) void k_score_hash(ScoreArgs a) {
     }
     return -1;
   };
+  // Sources are claimed HS_DQ at a time (one device-scope atomic per HS_DQ sources), and a
+  // source's header -- its rows, its pair range and this thread's first pair -- is loaded before
+  // the table is cleared, so those round trips overlap the clear instead of following the build.
+  int si_next = 0, left = 0;  // uniform over the workgroup
   for (;;) {
-    if (threadIdx.x == 0) s_src = atomicAdd(&a.misc->hq, 1);
-    __syncthreads();
-    const int si = s_src;
-    __syncthreads();
+    if (left == 0) {
+      if (threadIdx.x == 0) s_src = atomicAdd(&a.misc->hq, HS_DQ);
+      __syncthreads();
+      si_next = s_src;
+      left = HS_DQ;
+      __syncthreads();
+    }
+    const int si = si_next++;
+    --left;
     if (si >= n_hash) break;
     const int x = a.active[si];
+    const int64_t xb = a.rp[x], xe = a.rp[x + 1];
+    const int64_t wb = a.wp ? a.wp[x] : 0, we = a.wp ? a.wp[x + 1] : 0;
+    const int pbeg = a.off[x], pcnt = a.cnt[x];
+    int64_t st0 = 0;
+    int len0 = 0, p0 = 0;
+    if ((int)threadIdx.x < pcnt) {
+      st0 = a.g_yb[pbeg + threadIdx.x];
+      len0 = a.g_yl[pbeg + threadIdx.x];
+      p0 = a.g_out[pbeg + threadIdx.x];
+    }
     for (int i = threadIdx.x; i < HT / 4; i += BLOCK) reinterpret_cast<uint4*>(tab)[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
     __syncthreads();
     // build: one row N(z) per thread, 16 ids at a time (rows padded past nnz), or x's wedge row
-    // (N(N(x)) back to back, wedge.hip) 4 ids per 16-byte load over the whole workgroup
-    const int64_t xb = a.rp[x], xe = a.rp[x + 1];
+    // (N(N(x)) back to back, wedge.hip) 4 ids per 16-byte load, two loads in flight per thread
     unsigned long long added = 0;
     auto insert = [&](uint32_t v) {
       uint32_t h = hs_slot<HT>(v);
@@ -2572,13 +2591,13 @@ __global__ __launch_bounds__(BLOCK) void k_score_hash(ScoreArgs a) {
         h = (h + 1) & (HT - 1);
       }
     };
-    const int64_t wb = a.wp ? a.wp[x] : 0, we = a.wp ? a.wp[x + 1] : 0;
     if (we > wb) {
-      for (int64_t q = wb + threadIdx.x; q < we; q += BLOCK) {
-        const uint4 v4 = a.wedge[q];
-        const uint32_t ids[4] = {v4.x, v4.y, v4.z, v4.w};
+      for (int64_t q = wb + threadIdx.x; q < we; q += 2 * BLOCK) {
+        const uint4 v0 = a.wedge[q];
+        const uint4 v1 = q + BLOCK < we ? a.wedge[q + BLOCK] : v0;  // (a repeat inserts nothing new)
+        const uint32_t ids[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < 8; ++j) {
           const uint32_t v = in_chunk((int)ids[j], keep, c0u);
           if (v < wu) insert(v);
         }
@@ -2615,13 +2634,13 @@ __global__ __launch_bounds__(BLOCK) void k_score_hash(ScoreArgs a) {
     }
     const unsigned long long h2 = want_j ? block_sum_u64<BLOCK>(added - removed, red64) : 0ull;
     if (!want_j) __syncthreads();  // tombstones written before any probe
-    // scan: one pair per thread
-    const int pbeg = a.off[x], pcnt = a.cnt[x];
+    // scan: one pair per thread (the first one's metadata came with the header)
     for (int t = threadIdx.x; t < pcnt; t += BLOCK) {
       const int gp = pbeg + t;
-      const int64_t st = a.g_yb[gp];
-      const int len = a.g_yl[gp];
-      const int p = a.g_out[gp];
+      const bool first = t == (int)threadIdx.x;
+      const int64_t st = first ? st0 : a.g_yb[gp];
+      const int len = first ? len0 : a.g_yl[gp];
+      const int p = first ? p0 : a.g_out[gp];
       unsigned c = 0;
       unsigned long long acc = 0, acch = 0;
       for (int h0 = 0; h0 < len; h0 += SHORT_PART) {
