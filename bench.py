@@ -408,15 +408,38 @@ def run_svd(args):
         got = np.einsum("ij,ji->i", us[pr[:200000]], vt_g[:, pc[:200000]])
         cdeg = np.diff(M.tocsc().indptr)
         zero = (deg[pr[:200000]] == 0) | (cdeg[pc[:200000]] == 0)
-        out["factorization"].update({"host_arpack_s": arpack_s, "speedup": arpack_s / fact_s})
+        out["factorization"].update({"host_arpack_s": arpack_s, "speedup": arpack_s / fact_s,
+                                     "host_arpack_note": "scipy.sparse.linalg.svds(M, k=64) on the same matrix "
+                                                         "(svd.py:24, the reference's own call), host BLAS threads"})
         # per-entry 1e-5 relative, exact-zero rule for empty rows/columns, near-zero floor
         out["parity"]["gpu_factor_vs_arpack"] = blp_oracle.svd_entry_parity(got, ref, zero)
-        out["cpu_baseline"] = {"value": arpack_s, "unit": "s per rank-64 factorisation", "cores": os.cpu_count(),
-                               "kind": "reference",
-                               "sample": "scipy.sparse.linalg.svds(M, k=64) on the same 2M x 200K matrix (svd.py:24, "
-                                         "the reference's own call), host BLAS threads"}
+    if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = svd_cpu_baseline(us, vt_g, users, B, args.cpu_seconds)
     if dist.rank == 0:
         print(json.dumps(out), flush=True)
+
+
+def svd_cpu_baseline(us, vt, users, n_cols, target_s=15.0):
+    """The reference's reconstruction loop (svd.py:28-30: examples[u][b] = np.dot(us[row],
+    vt[:, col]) per pair) restated on the same factors, 1 thread, over a bounded sample of the
+    step's own pairs: the sampled users' rows against every business, in the step's order, for
+    about target_s seconds. pairs/s, the unit of the bench line."""
+    done, t0 = 0, time.perf_counter()
+    vt = np.ascontiguousarray(vt)
+    i = 0
+    while time.perf_counter() - t0 < target_s:
+        row = us[users[i % len(users)]]
+        for col in range(0, n_cols, 1):
+            np.dot(row, vt[:, col])
+            done += 1
+            if done % 65536 == 0 and time.perf_counter() - t0 >= target_s:
+                break
+        i += 1
+    spent = time.perf_counter() - t0
+    return {"value": done / spent, "unit": "pairs/s", "cores": 1, "kind": "port",
+            "sample": "svd.py:28-30 restated: np.dot(us[row], vt[:, col]) per (user, business) pair on the step's "
+                      "factors, users in the step's order against every business, 1 thread: %d pairs in %.1fs" %
+                      (done, spent)}
 
 
 def topk_alg_bytes(G, src, h2_sum, push_sum, k, n_methods):
@@ -683,9 +706,9 @@ def run_sharded(args):
     for name, bt, _ in passes:
         log("plan %s: %s" % (name, bt.plan()))
     # each pass on its own stream (they overlap where the grids leave room); --cosched-passes:
-    # blp_batches_score with BLP_SPLIT_COSCHED=1 holds each chunk-parallel grid to a CU share
-    # (measured slower: 1951 / 864 / 903 ms at proportional / 176 / 128 user CUs against 743 ms,
-    # profiles/r03_bench_sharded_c5_cosched*.json)
+    # both through blp_batches_score (holding each chunk-parallel grid to a CU share was measured
+    # slower: 1951 / 864 / 903 ms at proportional / 176 / 128 user CUs against 743 ms,
+    # profiles/r03_bench_sharded_c5_cosched*.json, and was removed)
     def step():
         if len(passes) > 1 and args.cosched_passes:
             G.score_batches([(bt, mask) for _, bt, mask in passes])
@@ -916,6 +939,60 @@ def run_e2e(args):
         shutil.rmtree(work, ignore_errors=True)
 
 
+def exchange_check(dist, dev, a, b, U, B, G, timeout_s=120.0):
+    """One run of the multi-GPU exchange (blp_multi_gather_csr, csrc/multi.hip)
+    after the timed step, over this job's ranks: rank r sends the edges of its user block
+    (user_blocks by count) of the config-2 graph every replica generated; ONE RCCL all-gather
+    moves the counts, then the padded partials; the padding is dropped on the device and the
+    union's CSR is built in HBM. The union is the whole graph, so its CSR must equal the
+    replica's (checked). Reported beside the headline, never part of it. A watchdog bounds the
+    collective: if it has not returned in timeout_s, rank 0 still prints its line (exchange
+    marked as timed out) and every rank exits."""
+    import threading
+
+    from blp import dist as bd
+    from blp.multi import Multi
+
+    lo, hi = (int(v) for v in bd.user_blocks(U, dist.world)[dist.rank:dist.rank + 2])
+    sel = (a >= lo) & (a < hi)
+    pa, pb = a[sel].astype(np.int32), b[sel].astype(np.int32)
+    box = {}
+
+    def run():
+        try:
+            with bd.stdout_to_stderr():  # RCCL's banner goes to stdout
+                uid = dist.broadcast_bytes(Multi.unique_id() if dist.rank == 0 else None)
+                mc = Multi(uid, dist.world, dist.rank, dev)
+            dist.barrier()
+            t0 = time.perf_counter()
+            c = mc.gather_csr(pa, pb, U + B)
+            sec = time.perf_counter() - t0
+            rp, ci = Multi.fetch_csr(c)
+            t_max = mc.allreduce(sec, "max")
+            box["res"] = (mc.bytes_in, sec, t_max, rp, ci)
+            mc.close()
+        except Exception as e:  # reported in the line, the headline stands
+            box["err"] = "%s: %s" % (type(e).__name__, e)
+
+    th = threading.Thread(target=run, daemon=True)
+    th.start()
+    th.join(timeout_s)
+    if th.is_alive():
+        return {"error": "exchange did not return within %.0f s" % timeout_s, "timed_out": True}
+    if "err" in box:
+        return {"error": box["err"]}
+    bytes_in, sec, t_max, rp, ci = box["res"]
+    dense = G.n == U + B and np.array_equal(G.node_ids, np.arange(U + B))
+    same = bool(dense and np.array_equal(rp, G.row_ptr) and np.array_equal(ci, G.col_idx)) if dense else \
+        int(len(ci)) == int(G.nnz)
+    return {"backend": "rccl (libblp blp_multi_gather_csr)", "collective": "ncclAllGather (counts, then padded partials)",
+            "edges_sent": int(sel.sum()), "bytes_in_per_rank": int(bytes_in),
+            "seconds_max_over_ranks": t_max, "seconds_include": "count exchange + all-gather + device CSR build",
+            "GBps_in_per_rank": bytes_in / t_max / 1e9 if t_max > 0 and bytes_in else None,
+            "xgmi_one_link_bound_s": bytes_in / (XGMI_LINK_GBS * 1e9),
+            "union_csr_equals_replica": same}
+
+
 def _free_port():
     import socket
 
@@ -975,6 +1052,8 @@ def main():
                          "libblp's own RCCL communicator (blp_multi_gather_csr)")
     ap.add_argument("--no-collective-at-world1", action="store_true",
                     help="--mode sharded: at one rank, skip the process group (no RCCL call; the local partial)")
+    ap.add_argument("--no-exchange", action="store_true",
+                    help="similarity mode: skip the post-step exchange run (blp_multi_gather_csr over the ranks)")
     ap.add_argument("--topk", type=int, default=20)
     ap.add_argument("--svd-parity-users", type=int, default=1000,
                     help="--mode svd: users whose top-k is checked against numpy (0: every user)")
@@ -1002,7 +1081,6 @@ def main():
     t0 = time.time()
     G = blp.DeviceGraph(a, b, device=dev)  # CSR, weights, coded ids, dense-row index, wedge rows
     t_graph = time.time() - t0
-    del a, b
     log("graph: %d nodes, %d unique edges, generated in %.1fs, built in %.1fs" % (G.n, G.nnz // 2, t_gen, t_graph))
     t0 = time.time()
     ex_x, ex_y, ex_l = synth.make_examples(G, U, B, D, n_users=args.users, rate=args.rate, seed=dist.rank)
@@ -1048,6 +1126,10 @@ def main():
         gms, gn = bt.stats(1)
         ktimes[name] = {"score_ms": ms / max(n, 1), "group_ms": gms / max(gn, 1)}
     res = {name: bt.fetch(mask) for name, bt, mask in passes}
+    # after the timed step: config 5's exchange (blp_multi_gather_csr: counts + padded partials in
+    # ONE RCCL all-gather, CSR built in HBM) over this job's ranks, on the config-2 edge partials
+    exchange = None if args.no_exchange else exchange_check(dist, dev, a, b, U, B, G)
+    del a, b
 
     out = {
         "metric": METRIC,
@@ -1074,6 +1156,7 @@ def main():
             "parallelism": "replicas x%d (graph replicated, users split, no collective)" % dist.world,
         },
         "kernels_ms": ktimes,
+        "exchange": exchange,
         # outside the timed step (once per graph / per example set), reported for completeness
         "setup_s": {"edge_generation": round(t_gen, 3), "graph_build": round(t_graph, 3),
                     "examples_hop3": round(t_ex, 3), "hop3_kernel_ms": round(hop3_ms / max(hop3_n, 1), 3),
@@ -1109,6 +1192,9 @@ def main():
             out["cpu_baseline"]["multicore"] = multi
     if dist.rank == 0:
         print(json.dumps(out), flush=True)
+    if exchange and exchange.get("timed_out"):  # a collective still blocked in RCCL: do not wait for it
+        sys.stdout.flush()
+        os._exit(0)
 
 
 if __name__ == "__main__":

@@ -60,6 +60,7 @@ SIGNATURES = {
     "blp_multi_gather_csr": [_P, _P, _P, _I64, _I64, _PP, ctypes.POINTER(ctypes.c_int64)],
     "blp_multi_allreduce": [_P, _DP, _I32],
     "blp_multi_destroy": [_P],
+    "blp_multi_compact_csr": [_I32, _P, _P, _I32, _I64, _PP, ctypes.POINTER(ctypes.c_int64)],
     "blp_graph_wedge": [_P, ctypes.POINTER(ctypes.c_int64), _P, _P],
     "blp_graph_info": [_P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
                        ctypes.POINTER(ctypes.c_int)],

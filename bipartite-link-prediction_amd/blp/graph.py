@@ -17,6 +17,7 @@
 import ctypes
 import math
 import os
+import weakref
 
 import numpy as np
 
@@ -352,7 +353,15 @@ class DeviceGraph(HostGraph):
         return v.value
 
     # ------------------------------------------------------------------ lifecycle
+    def _adopt(self, child):
+        """Register a handle built on this graph (a pair batch, a top-k engine): it is closed
+        before the graph's own handle, whatever order Python collects them in."""
+        kids = self.__dict__.setdefault("_children", weakref.WeakSet())
+        kids.add(child)
+
     def close(self):
+        for child in list(self.__dict__.get("_children", ())):
+            child.close()
         if getattr(self, "handle", None):
             lib().blp_graph_destroy(self.handle)
             self.handle = None
@@ -448,6 +457,7 @@ class PairBatch:
         h = ctypes.c_void_p()
         check(lib().blp_batch_create(graph.handle, ptr(self.x), ptr(self.y), self.n, ctypes.byref(h)))
         self.handle = h
+        graph._adopt(self)
 
     def plan(self):
         lo, hi = ctypes.c_int64(), ctypes.c_int64()

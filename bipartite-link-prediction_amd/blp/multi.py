@@ -56,6 +56,41 @@ class Multi:
         self.bytes_in = got.value
         return c
 
+    @staticmethod
+    def compact_csr(recv, counts, n, device=0):
+        """The post-gather half of the exchange (blp_multi_compact_csr): recv is an all-gather
+        receive buffer -- an int32 numpy array, or a device pointer -- of len(counts) slots
+        [a | b], each half padded to max(counts); returns (device CSR handle, bytes_in)."""
+        cnt = np.ascontiguousarray(counts, np.int64)
+        if isinstance(recv, np.ndarray):
+            recv = np.ascontiguousarray(recv, np.int32)
+            if recv.size < 2 * int(cnt.max(initial=0)) * len(cnt):
+                raise ValueError("receive buffer smaller than the counts imply")
+            p = recv.ctypes.data
+        else:
+            p = int(recv)
+        c = ctypes.c_void_p()
+        got = ctypes.c_int64()
+        check(lib().blp_multi_compact_csr(int(device), ctypes.c_void_p(p), cnt.ctypes.data_as(ctypes.c_void_p),
+                                          len(cnt), int(n), ctypes.byref(c), ctypes.byref(got)))
+        return c, got.value
+
+    @staticmethod
+    def fetch_csr(c, destroy=True):
+        """(row_ptr int64, col_idx int32) of a device CSR handle (blp_csr_fetch); the handle
+        is destroyed afterwards unless destroy=False."""
+        L = lib()
+        try:
+            nn, nnz = ctypes.c_int64(), ctypes.c_int64()
+            check(L.blp_csr_info(c, ctypes.byref(nn), ctypes.byref(nnz)))
+            rp = np.empty(nn.value + 1, np.int64)
+            ci = np.empty(max(nnz.value, 1), np.int32)
+            check(L.blp_csr_fetch(c, rp.ctypes.data_as(ctypes.c_void_p), ci.ctypes.data_as(ctypes.c_void_p), None))
+            return rp, ci[: nnz.value]
+        finally:
+            if destroy:
+                L.blp_csr_destroy(c)
+
     def gather_graph(self, a, b, n, n_col0, m=None, aa=True):
         """gather_csr, then the graph handle over it (DeviceGraph.from_csr_handle)."""
         from .graph import DeviceGraph

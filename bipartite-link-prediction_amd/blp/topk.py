@@ -40,6 +40,7 @@ class TopK:
         h = ctypes.c_void_p()
         check(lib().blp_topk_create(graph.handle, src[0], src[1], tgt[0], tgt[1], ctypes.byref(h)))
         self.handle = h
+        graph._adopt(self)
         self.src_range, self.tgt_range = src, tgt
         self.n_src = 0
         self.k = None

@@ -5,6 +5,7 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -40,6 +41,13 @@ struct DevBuf {
   int reserve(size_t want);
   void release();
   template <class T> T* as() const { return reinterpret_cast<T*>(p); }
+};
+// A DevBuf freed when it leaves scope (temporaries on paths with early returns).
+struct ScopedBuf : DevBuf {
+  ScopedBuf() = default;
+  ScopedBuf(const ScopedBuf&) = delete;
+  ScopedBuf& operator=(const ScopedBuf&) = delete;
+  ~ScopedBuf() { release(); }
 };
 
 // Adamic-Adar sums are EXACT. A term w = (log deg)^-1 (similarity.py:121-125) is a double in
@@ -139,6 +147,7 @@ struct blp_graph {
   // an id range [lo, hi), built on first use per range (the hop-3 mark range; the business
   // batch's universe) and kept with the graph (at most 4 ranges)
   std::vector<blp::WedgeBitmaps> wbm;
+  std::mutex wbm_mu;  // held across wedge_bitmaps' lookup-or-build (batches are created concurrently)
   // host mirrors used for launch planning (bitmap universe bounds) and the host-built indexes:
   // owned copies (blp_graph_create), or the caller's buffers (blp_graph_create_from_csr, which
   // requires them to outlive the handle)

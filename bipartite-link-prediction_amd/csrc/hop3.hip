@@ -426,6 +426,9 @@ namespace blp {
 const WedgeBitmaps* wedge_bitmaps(blp_graph* g, int64_t lo, int64_t hi, int* rc) {
   *rc = BLP_OK;
   if (!g->d_wp || hi <= lo) return nullptr;
+  // two batches of one graph may be created on two host threads at once (similarity.py's user and
+  // business passes): the whole lookup-or-build is one critical section
+  std::lock_guard<std::mutex> lock(g->wbm_mu);
   for (const WedgeBitmaps& w : g->wbm)
     if (w.lo == lo && w.hi == hi) return &w;
   if (g->wbm.size() >= 4) return nullptr;
@@ -440,36 +443,45 @@ const WedgeBitmaps* wedge_bitmaps(blp_graph* g, int64_t lo, int64_t hi, int* rc)
   }
   std::sort(rows.begin(), rows.end());
   rows.resize((size_t)std::min<int64_t>((int64_t)rows.size(), budget / (4 * words)));
-  g->wbm.emplace_back();
-  WedgeBitmaps& w = g->wbm.back();
+  // built into a local entry; it joins the cache only once complete, so a failure leaves no
+  // half-built entry behind and frees what it allocated
+  WedgeBitmaps w;
   w.lo = lo;
   w.hi = hi;
   w.words = words;
-  if (rows.empty()) return &w;
-  w.h_slot.assign((size_t)g->n, -1);
-  std::vector<int32_t> order(rows.size());
-  for (size_t i = 0; i < rows.size(); ++i) {
-    w.h_slot[rows[i].second] = (int32_t)i;
-    order[i] = rows[i].second;
+  if (!rows.empty()) {
+    w.h_slot.assign((size_t)g->n, -1);
+    std::vector<int32_t> order(rows.size());
+    for (size_t i = 0; i < rows.size(); ++i) {
+      w.h_slot[rows[i].second] = (int32_t)i;
+      order[i] = rows[i].second;
+    }
+    ScopedBuf d_rows;
+    auto hip = [&](hipError_t e, const char* what) {
+      if (e != hipSuccess) *rc = hip_fail(e, what, __FILE__, __LINE__);
+      return e == hipSuccess;
+    };
+    bool ok = hip(hipMalloc(&w.d_slot, 4 * (size_t)g->n), "hipMalloc") &&
+              hip(hipMalloc(&w.d_pool, 4 * (size_t)words * rows.size()), "hipMalloc (wedge bitmaps)");
+    if (ok && (*rc = d_rows.reserve(4 * rows.size())) != BLP_OK) ok = false;
+    ok = ok && hip(hipMemcpy(w.d_slot, w.h_slot.data(), 4 * (size_t)g->n, hipMemcpyHostToDevice), "hipMemcpy") &&
+         hip(hipMemcpy(d_rows.p, order.data(), 4 * order.size(), hipMemcpyHostToDevice), "hipMemcpy");
+    if (ok) {
+      hipLaunchKernelGGL(k_wbm_fill, dim3((unsigned)rows.size()), dim3(HW_BLOCK), 4 * (size_t)words, g->stream,
+                         (const int64_t*)g->d_wp, (const uint4*)g->d_wedge, d_rows.as<int32_t>(), lo, hi - lo,
+                         (int)words, w.d_pool);
+      ok = hip(hipGetLastError(), "k_wbm_fill launch") && hip(hipStreamSynchronize(g->stream), "hipStreamSynchronize");
+    }
+    d_rows.release();
+    if (!ok) {
+      if (w.d_slot) (void)hipFree(w.d_slot);
+      if (w.d_pool) (void)hipFree(w.d_pool);
+      return nullptr;
+    }
+    w.slots = (int64_t)rows.size();
   }
-  int32_t* d_rows = nullptr;
-  auto hip = [&](hipError_t e, const char* what) {
-    if (e != hipSuccess) *rc = hip_fail(e, what, __FILE__, __LINE__);
-    return e == hipSuccess;
-  };
-  if (!hip(hipMalloc(&w.d_slot, 4 * (size_t)g->n), "hipMalloc") ||
-      !hip(hipMalloc(&w.d_pool, 4 * (size_t)words * rows.size()), "hipMalloc (wedge bitmaps)") ||
-      !hip(hipMalloc(&d_rows, 4 * rows.size()), "hipMalloc") ||
-      !hip(hipMemcpy(w.d_slot, w.h_slot.data(), 4 * (size_t)g->n, hipMemcpyHostToDevice), "hipMemcpy") ||
-      !hip(hipMemcpy(d_rows, order.data(), 4 * order.size(), hipMemcpyHostToDevice), "hipMemcpy"))
-    return nullptr;
-  hipLaunchKernelGGL(k_wbm_fill, dim3((unsigned)rows.size()), dim3(HW_BLOCK), 4 * (size_t)words, g->stream,
-                     (const int64_t*)g->d_wp, (const uint4*)g->d_wedge, d_rows, lo, hi - lo, (int)words, w.d_pool);
-  if (!hip(hipGetLastError(), "k_wbm_fill launch") || !hip(hipStreamSynchronize(g->stream), "hipStreamSynchronize"))
-    return nullptr;
-  (void)hipFree(d_rows);
-  w.slots = (int64_t)rows.size();
-  return &w;
+  g->wbm.push_back(std::move(w));
+  return &g->wbm.back();
 }
 }  // namespace blp
 

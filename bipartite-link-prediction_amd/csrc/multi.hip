@@ -159,6 +159,60 @@ extern "C" int blp_multi_allreduce(blp_multi* m, double* v, int op) {
   return BLP_OK;
 }
 
+namespace {
+
+// The post-gather half of the exchange: recv holds `world` slots of [a | b], each half padded to
+// m_max = max(counts) (slot r: rank r's a ids in [0, m_max), its b ids in [m_max, 2 m_max)); the
+// valid prefixes are copied back to back on `st` (device or host recv) and the union's CSR is
+// built in HBM. The padding is never read.
+int compact_csr(int device, hipStream_t st, const int32_t* recv, const int64_t* cnt, int W, int64_t n_nodes,
+                blp_csr** out, int64_t* bytes_in) {
+  int64_t m_max = 0, m_tot = 0;
+  for (int r = 0; r < W; ++r) {
+    BLP_CHECK(cnt[r] >= 0, BLP_E_ARG, "blp_multi_compact_csr: negative count");
+    m_max = std::max(m_max, cnt[r]);
+    m_tot += cnt[r];
+  }
+  BLP_CHECK(m_max == 0 || recv, BLP_E_ARG, "blp_multi_compact_csr: null receive buffer");
+  ScopedBuf ua, ub;
+  int rc;
+  if ((rc = ua.reserve(4 * (size_t)std::max<int64_t>(m_tot, 1))) ||
+      (rc = ub.reserve(4 * (size_t)std::max<int64_t>(m_tot, 1))))
+    return rc;
+  if (m_max > 0) {
+    const hipMemcpyKind k = on_device(recv) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    int64_t off = 0;
+    for (int r = 0; r < W; ++r) {
+      if (!cnt[r]) continue;
+      const int32_t* src = recv + (size_t)r * 2 * m_max;
+      BLP_HIP(hipMemcpyAsync(ua.as<int32_t>() + off, src, 4 * (size_t)cnt[r], k, st));
+      BLP_HIP(hipMemcpyAsync(ub.as<int32_t>() + off, src + m_max, 4 * (size_t)cnt[r], k, st));
+      off += cnt[r];
+    }
+    BLP_HIP(hipStreamSynchronize(st));
+  }
+  rc = blp_csr_build_device(device, ua.as<int32_t>(), ub.as<int32_t>(), m_tot, n_nodes, out);
+  if (rc == BLP_OK && bytes_in) *bytes_in = 8 * m_max * (int64_t)(W - 1);
+  return rc;
+}
+
+}  // namespace
+
+extern "C" int blp_multi_compact_csr(int device, const int32_t* recv, const int64_t* counts, int world, int64_t n_nodes,
+                                     blp_csr** out, int64_t* bytes_in) {
+  BLP_CHECK(counts && out && world >= 1 && n_nodes >= 0, BLP_E_ARG, "blp_multi_compact_csr: bad arguments");
+  int ndev = 0;
+  BLP_HIP(hipGetDeviceCount(&ndev));
+  BLP_CHECK(device >= 0 && device < ndev, BLP_E_ARG, "blp_multi_compact_csr: no such device");
+  BLP_HIP(hipSetDevice(device));
+  hipStream_t st = nullptr;
+  BLP_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  const int rc = compact_csr(device, st, recv, counts, world, n_nodes, out, bytes_in);
+  (void)hipStreamSynchronize(st);
+  (void)hipStreamDestroy(st);
+  return rc;
+}
+
 extern "C" int blp_multi_gather_csr(blp_multi* m, const int32_t* a, const int32_t* b, int64_t m_r, int64_t n_nodes,
                                     blp_csr** out, int64_t* bytes_in) {
   BLP_CHECK(m && out && m_r >= 0 && n_nodes >= 0 && (m_r == 0 || (a && b)), BLP_E_ARG,
@@ -166,10 +220,9 @@ extern "C" int blp_multi_gather_csr(blp_multi* m, const int32_t* a, const int32_
   const Rccl* R = rccl();
   BLP_HIP(hipSetDevice(m->device));
   const int W = m->world;
-  DevBuf send, recv, ua, ub;
+  ScopedBuf send, recv;
   auto done = [&](int rc) {
     (void)hipStreamSynchronize(m->stream);
-    for (DevBuf* x : {&send, &recv, &ua, &ub}) x->release();
     return rc;
   };
   // 1. counts: one int64 per rank
@@ -180,8 +233,6 @@ extern "C" int blp_multi_gather_csr(blp_multi* m, const int32_t* a, const int32_
   BLP_HIP_OR(hipMemcpyAsync(cnt.data(), d_cnt + 1, 8 * (size_t)W, hipMemcpyDeviceToHost, m->stream), done);
   BLP_HIP_OR(hipStreamSynchronize(m->stream), done);
   const int64_t m_max = *std::max_element(cnt.begin(), cnt.end());
-  int64_t m_tot = 0;
-  for (int64_t c : cnt) m_tot += c;
   BLP_CHECK(cnt[m->rank] == m_r, BLP_E_COMM, "blp_multi_gather_csr: count exchange mismatch");
   int rc;
   if (m_max > 0) {
@@ -195,27 +246,8 @@ extern "C" int blp_multi_gather_csr(blp_multi* m, const int32_t* a, const int32_
       BLP_HIP_OR(hipMemcpyAsync(s + m_max, b, 4 * (size_t)m_r, kb, m->stream), done);
     }
     BLP_NCCL_OR(R->all_gather(s, recv.p, 2 * (size_t)m_max, ncclInt32, m->comm, m->stream), done);
-    // 3. drop the padding: each rank's valid prefix, back to back
-    if ((rc = ua.reserve(4 * (size_t)std::max<int64_t>(m_tot, 1))) ||
-        (rc = ub.reserve(4 * (size_t)std::max<int64_t>(m_tot, 1))))
-      return done(rc);
-    int64_t off = 0;
-    for (int r = 0; r < W; ++r) {
-      if (!cnt[r]) continue;
-      const int32_t* src = recv.as<int32_t>() + (size_t)r * 2 * m_max;
-      BLP_HIP_OR(hipMemcpyAsync(ua.as<int32_t>() + off, src, 4 * (size_t)cnt[r], hipMemcpyDeviceToDevice, m->stream),
-                 done);
-      BLP_HIP_OR(hipMemcpyAsync(ub.as<int32_t>() + off, src + m_max, 4 * (size_t)cnt[r], hipMemcpyDeviceToDevice,
-                                m->stream),
-                 done);
-      off += cnt[r];
-    }
-    BLP_HIP_OR(hipStreamSynchronize(m->stream), done);
     send.release();
-    recv.release();
   }
-  // 4. the union's CSR, kept in HBM
-  rc = blp_csr_build_device(m->device, ua.as<int32_t>(), ub.as<int32_t>(), m_tot, n_nodes, out);
-  if (rc == BLP_OK && bytes_in) *bytes_in = 8 * m_max * (int64_t)(W - 1);
-  return done(rc);
+  // 3. drop the padding and build the union's CSR, kept in HBM
+  return done(compact_csr(m->device, m->stream, recv.as<int32_t>(), cnt.data(), W, n_nodes, out, bytes_in));
 }

@@ -63,7 +63,32 @@ struct Misc {
   int qh[8];  // k_score_split: one queue head per XCD group (sources s = g mod 8)
   int n_hash_front;  // split batches with hash-routed sources: the active list is partitioned,
   int n_split_back;  // hash sources in [0, n_hash_front), split sources after (k_hash_partition)
+  long long dbg[4];  // BLP_DEBUG builds: bound violations, first site, its value, its bound (PS_OK)
 };
+
+// BLP_DEBUG builds (make debug -> libblp_debug.so): the scorers' queue claims, queue slots, table
+// probes, split-table rows and output indexes are checked against their bounds before the
+// access; a violation is counted in the batch's Misc, the first one recorded (site, value,
+// bound) and the access skipped, so a check never faults the GPU. blp_batch_fetch then fails
+// with the record (BLP_E_STATE). Release builds compile the checks out. Sites:
+//   1 claimed source index < n_active        2 source id < n_nodes
+//   3 pair range [pbeg, pbeg + pcnt) <= np    4 output index < np
+//   5 long-slice queue slot < SPLIT_LQ        6 long-slice queue region < the allocated workgroups
+//   7 split-table row < its rows              8 hash-set probes < HT (a full table would spin)
+//   9 chunk width <= the bitmap's bits
+#ifdef BLP_DEBUG
+__device__ inline bool ps_ok(Misc* m, bool ok, int site, long long v, long long bound) {
+  if (!ok && atomicAdd(reinterpret_cast<unsigned long long*>(&m->dbg[0]), 1ull) == 0ull) {
+    m->dbg[1] = site;
+    m->dbg[2] = v;
+    m->dbg[3] = bound;
+  }
+  return ok;
+}
+#define PS_OK(m, cond, site, v, bound) ps_ok((m), (cond), (site), (long long)(v), (long long)(bound))
+#else
+#define PS_OK(m, cond, site, v, bound) ((void)(v), true)
+#endif
 
 // ------------------------------------------------------------------ grouping kernels
 // Two-pass MSD bucket sort of the pairs by source x, with every atomic in LDS (a device-
@@ -1180,33 +1205,12 @@ __device__ __attribute__((always_inline)) inline void rc_fetch(const int32_t* __
 }
 
 // Two-buffer driver: steps of NT chunks; proc(step) after the next step's loads are issued.
-// BLP_RC3: three buffers, two steps of loads in flight while one is processed.
-#ifndef BLP_RC3
-#define BLP_RC3 0
-#endif
+// (A third buffer, two steps of loads in flight, measured 2.28 vs 2.26 ms: not kept.)
 template <int NT, int K, typename Proc>
 __device__ __attribute__((always_inline)) inline void rc_loop(const int32_t* __restrict__ ci, const int64_t* s_start, const int32_t* s_off,
                                const int32_t* s_coff, int ns, int tid, const int32_t* hint, int shift, Proc proc) {
   const int TC = s_coff[ns];
   const int nsteps = (TC + NT - 1) / NT;
-#if BLP_RC3
-  RCStep<K> A, B, C;
-  vm_drain();
-  rc_fetch<K>(ci, s_start, s_off, s_coff, ns, TC, tid, hint, shift, A);
-  rc_fetch<K>(ci, s_start, s_off, s_coff, ns, TC, NT + tid, hint, shift, B);  // may be past TC
-  int i = 0;
-  for (; i + 2 < nsteps; i += 3) {
-    rc_fetch<K>(ci, s_start, s_off, s_coff, ns, TC, (i + 2) * NT + tid, hint, shift, C);
-    proc(A);
-    rc_fetch<K>(ci, s_start, s_off, s_coff, ns, TC, (i + 3) * NT + tid, hint, shift, A);
-    proc(B);
-    rc_fetch<K>(ci, s_start, s_off, s_coff, ns, TC, (i + 4) * NT + tid, hint, shift, B);
-    proc(C);
-  }
-  if (i < nsteps) proc(A);
-  if (i + 1 < nsteps) proc(B);
-  vm_drain();
-#else
   RCStep<K> A, B;
   vm_drain();
   rc_fetch<K>(ci, s_start, s_off, s_coff, ns, TC, tid, hint, shift, A);
@@ -1218,7 +1222,6 @@ __device__ __attribute__((always_inline)) inline void rc_loop(const int32_t* __r
   }
   if (nsteps & 1) proc(A);
   vm_drain();
-#endif
 }
 
 // LDS bitmap layout for the row-chunk loops: CAP words of bits, then RC_SAFE: one word that
@@ -1597,9 +1600,10 @@ struct ScoreArgs {
   const uint4* wedge;
   unsigned long long* aa_part;  // [2 n_pairs] exact AA words carried between LDS chunks (k_score, chunks > 1)
   const SrcRec* rec;            // per active source (short-row scorer; null: gather from active[])
-  int sched;                    // short-row scorer: 1 = claims dealt round-robin (BLP_STATIC), 0 = dequeued
   int4* lq;                     // k_score_split: long-slice queues, SPLIT_LQ entries per workgroup
-  int split_round;              // k_score_split: 64-pair groups per wave per round
+  int64_t np, n_nodes;          // pairs and nodes (BLP_DEBUG bounds)
+  int64_t rs_rows;              // rows of the split table (BLP_DEBUG bound)
+  int lq_wgs;                   // workgroups d_lq was sized for (BLP_DEBUG bound)
 };
 
 template <int BLOCK>
@@ -1683,24 +1687,17 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
   const int n_active = a.misc->n_active;
 
   PROF_INIT
-  // dequeue one ahead: the next source's atomic is in flight while this one is scored.
-  // a.sched (short-row scorer, BLP_STATIC): claims dealt round-robin instead, no atomics.
-  const bool dealt = SHORT && a.sched;
-  int nxt = dealt ? (int)blockIdx.x * a.dq : threadIdx.x == 0 ? atomicAdd(&a.misc->queue, a.dq) : 0;
+  // dequeue one ahead: the next source's atomic is in flight while this one is scored
+  int nxt = threadIdx.x == 0 ? atomicAdd(&a.misc->queue, a.dq) : 0;
   for (;;) {
     int s_first;
-    if (dealt) {
-      s_first = nxt;
-      nxt += (int)gridDim.x * a.dq;
-    } else {
-      if (threadIdx.x == 0) {
-        s_src = nxt;
-        if (nxt < n_active) nxt = atomicAdd(&a.misc->queue, a.dq);
-      }
-      __syncthreads();
-      s_first = s_src;
-      __syncthreads();
+    if (threadIdx.x == 0) {
+      s_src = nxt;
+      if (nxt < n_active) nxt = atomicAdd(&a.misc->queue, a.dq);
     }
+    __syncthreads();
+    s_first = s_src;
+    __syncthreads();
     if (s_first >= n_active) break;
     PROF(0)
     const int s_last = min(n_active, s_first + a.dq);
@@ -1727,8 +1724,10 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
         nx_hi = u32(r.nx_hi);
       } else {
         x = a.active[s];
+        if (!PS_OK(a.misc, x >= 0 && x < a.n_nodes, 2, x, a.n_nodes)) continue;  // uniform
         pbeg = a.off[x];
         pcnt = a.cnt[x];
+        if (!PS_OK(a.misc, pbeg >= 0 && (int64_t)pbeg + pcnt <= a.np, 3, (int64_t)pbeg + pcnt, a.np)) continue;
         xb = a.rp[x];
         xe = a.rp[x + 1];
         hslot = a.heavy_slot ? a.heavy_slot[x] : -1;
@@ -1968,6 +1967,7 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
           PROF(7)
           for (int t = threadIdx.x; t < ns; t += BLOCK) {  // ns <= SEG <= BLOCK: t == threadIdx.x
             const int p = pout;
+            if (!PS_OK(a.misc, p >= 0 && p < a.np, 4, p, a.np)) continue;
             unsigned c = packed ? (unsigned)(s_aa[2 * t + 1] & ((1u << PK_CN_BITS) - 1)) : s_cn[t];
             if (ch > 0) c += a.cn[p];
             a.cn[p] = c;
@@ -2136,9 +2136,8 @@ __global__ void k_row_splits(const int64_t* __restrict__ rp, const int32_t* __re
 }
 
 constexpr int SPLIT_CN_BITS = 24;  // k_score_split pk24: count field of the packed per-pair word
-constexpr int SPLIT_ROUND = 16;      // k_score_split: 64-pair groups per wave between block syncs (default)
-constexpr int SPLIT_ROUND_MAX = 16;  // ... at most (BLP_SPLIT_ROUND; config 5: 4 -> 341, 8 -> 317-324, 16 -> 322 ms)
-constexpr int SPLIT_LQ = 16 * SPLIT_ROUND_MAX * 64;  // long-slice queue entries per workgroup (16 waves)
+constexpr int SPLIT_ROUND = 16;  // k_score_split: 64-pair groups per wave between block syncs (config 5: 4 -> 341, 8 -> 317-324, 16 -> 322 ms)
+constexpr int SPLIT_LQ = 16 * SPLIT_ROUND * 64;  // long-slice queue entries per workgroup (16 waves)
 
 template <int BLOCK, int CAP_WORDS, int SEG, int K>
 __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_split(ScoreArgs a, const int32_t* __restrict__ g_y,
@@ -2146,7 +2145,7 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
                                                        uint32_t* __restrict__ pcn, unsigned long long* __restrict__ paa,
                                                        uint32_t* __restrict__ ph2, int64_t np, int pk24, int short_max) {
   constexpr int NW = BLOCK / 64;
-  static_assert(NW * SPLIT_ROUND_MAX * 64 <= SPLIT_LQ, "a round's long slices fit the queue");
+  static_assert(NW * SPLIT_ROUND * 64 <= SPLIT_LQ, "a round's long slices fit the queue");
   // 128 KiB chunks (one workgroup per CU) use the row-chunk loops of the large scorer
   constexpr bool RCS = BLP_RC && CAP_WORDS > 16384;
   constexpr int HCS = RCS ? 1536 : 1;
@@ -2180,9 +2179,10 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
   // s = g (mod 8), all C chunks of a source in a row, so the C workgroups scanning one source's
   // pair rows chunk by chunk do it on one XCD, close in time, and share those rows in its L2
   // instead of fetching each 128-byte line into several L2s. A group whose sources are done
-  // takes items of the next group (queue heads misc->qh[g]). BLP_SPLIT_ONEQ: one global queue.
-  const int grp = a.sched ? 0 : (int)(blockIdx.x & 7);
-  const int ngrp = a.sched ? 1 : 8;
+  // takes items of the next group (queue heads misc->qh[g]). Measured against one global queue
+  // in chunk-major order (every source's chunk c before any chunk c + 1): 326 -> 484 ms.
+  const int grp = (int)(blockIdx.x & 7);
+  constexpr int ngrp = 8;
   int gq = 0;  // thread 0: groups found empty so far
   PROF_INIT  // -DBLP_PROF phase clocks: 0 claim, 1 build, 2 popcount, 3 batch to short scan, 4 long scan, 5 partials
   for (;;) {
@@ -2193,8 +2193,7 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
         const int64_t n_g = n_src > g ? (n_src - g + ngrp - 1) / ngrp : 0;
         const int k = atomicAdd(&a.misc->qh[g], 1);
         if ((int64_t)k < n_g * C) {
-          // BLP_SPLIT_ONEQ=2: chunk-major order (every source's chunk c before any chunk c + 1)
-          s_item = a.sched == 2 ? (int64_t)(k % n_g) * C + k / n_g : (int64_t)(g + (int64_t)ngrp * (k / C)) * C + k % C;
+          s_item = (int64_t)(g + (int64_t)ngrp * (k / C)) * C + k % C;
           break;
         }
         ++gq;
@@ -2206,12 +2205,16 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
     if (item < 0) break;
     PROF(0)
     const int s = s_base + (int)(item / C), c = (int)(item % C);
+    if (!PS_OK(a.misc, s < a.misc->n_active, 1, s, a.misc->n_active)) continue;  // uniform
     const int x = a.active[s];
+    if (!PS_OK(a.misc, x >= 0 && x < a.n_nodes, 2, x, a.n_nodes)) continue;
     const int pbeg = a.off[x], pcnt = a.cnt[x];
+    if (!PS_OK(a.misc, pbeg >= 0 && (int64_t)pbeg + pcnt <= a.np, 3, (int64_t)pbeg + pcnt, a.np)) continue;
     const int64_t xb = a.rp[x], xe = a.rp[x + 1];
     const int hslot = a.heavy_slot ? a.heavy_slot[x] : -1;
     const int64_t c0 = a.lo + (int64_t)c * CAP_BITS;
     const int64_t width = max<int64_t>(min(a.hi, c0 + CAP_BITS) - c0, 0);
+    if (!PS_OK(a.misc, width <= 32ll * CAP_WORDS, 9, width, 32ll * CAP_WORDS)) continue;
     const int nw4 = (int)((((width + 31) >> 5) + 3) >> 2);
     const int64_t wb = a.wp ? a.wp[x] : 0, we = a.wp ? a.wp[x + 1] : 0;
     if (hslot >= 0) {
@@ -2271,9 +2274,13 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
         int len = 0;
         if ((int)threadIdx.x < ns) {
           const int z = a.ci[k0 + threadIdx.x];
-          const int32_t* sp = rsplit + ((int64_t)z - rs_lo) * (C + 1) + c;
-          s_start[threadIdx.x] = a.rp[z] + sp[0];
-          len = (nhot && a.hot_idx[z] >= 0) ? 0 : sp[1] - sp[0];  // dense rows were OR-ed in
+          if (PS_OK(a.misc, (int64_t)z - rs_lo >= 0 && (int64_t)z - rs_lo < a.rs_rows, 7, (int64_t)z - rs_lo, a.rs_rows)) {
+            const int32_t* sp = rsplit + ((int64_t)z - rs_lo) * (C + 1) + c;
+            s_start[threadIdx.x] = a.rp[z] + sp[0];
+            len = (nhot && a.hot_idx[z] >= 0) ? 0 : sp[1] - sp[0];  // dense rows were OR-ed in
+          } else {
+            s_start[threadIdx.x] = 0;
+          }
         }
         int tot;
         const int ex = block_exscan<BLOCK>(len, red, &tot);
@@ -2324,6 +2331,7 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
     // undercount S by < 2^44).
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t keep = a.idmask | 0x80000000u, c0u = (uint32_t)c0, wu = (uint32_t)width;
+    if (!PS_OK(a.misc, (int)blockIdx.x < a.lq_wgs, 6, blockIdx.x, a.lq_wgs)) break;  // uniform
     int4* lq = a.lq + (int64_t)blockIdx.x * SPLIT_LQ;
     // a (pair, chunk) slice's partial words into the pair's accumulators: only slices with a hit
     // add anything, so no [chunks][pairs] partial arrays (config 5: 48 chunks x 199M pairs) and
@@ -2334,7 +2342,7 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
     // S mod 2^64 and S >> 32 in three.
     auto emit = [&](int64_t gp, unsigned long long w0, unsigned long long w1) {
       const unsigned c_t = (unsigned)(w1 & ((1u << PK_CN_BITS) - 1));
-      if (!c_t) return;
+      if (!c_t || !PS_OK(a.misc, gp >= 0 && gp < a.np, 4, gp, a.np)) return;
       if (want_a) {
         unsigned long long sh, sl;
         blp::aa_exact(w0, w1 >> PK_CN_BITS, &sh, &sl, PK_HS);
@@ -2350,7 +2358,7 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
       }
     };
     const int ngr = (pcnt + 63) >> 6;
-    const int rg = NW * a.split_round;
+    const int rg = NW * SPLIT_ROUND;
     for (int r0 = 0; r0 < ngr; r0 += rg) {
       const int r1 = min(ngr, r0 + rg);
       for (int g = r0 + wv; g < r1; g += NW) {
@@ -2359,10 +2367,13 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
         int64_t st = 0;
         if (q < pcnt) {
           const int gp = pbeg + q;
-          const int32_t* sp = rsplit + ((int64_t)g_y[gp] - rs_lo) * (C + 1) + c;
-          const int s0 = sp[0];
-          len = sp[1] - s0;
-          st = a.g_yb[gp] + s0;
+          const int64_t row = (int64_t)g_y[gp] - rs_lo;
+          if (PS_OK(a.misc, row >= 0 && row < a.rs_rows, 7, row, a.rs_rows)) {
+            const int32_t* sp = rsplit + row * (C + 1) + c;
+            const int s0 = sp[0];
+            len = sp[1] - s0;
+            st = a.g_yb[gp] + s0;
+          }
         }
         if (len > 0 && len <= short_max) {
           int sv[SHORT_PART];
@@ -2388,12 +2399,13 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
           emit(pbeg + q, lo, (hi40 << PK_CN_BITS) | cnt);
         } else if (len > short_max) {
           const int slot = atomicAdd(&s_nl, 1);  // < SPLIT_LQ: a round holds NW * SPLIT_ROUND * 64 pairs
-          lq[slot] = make_int4((int32_t)(uint32_t)st, (int32_t)(st >> 32), len, pbeg + q);
+          if (PS_OK(a.misc, slot < SPLIT_LQ, 5, slot, SPLIT_LQ))
+            lq[slot] = make_int4((int32_t)(uint32_t)st, (int32_t)(st >> 32), len, pbeg + q);
         }
       }
       __syncthreads();
       PROF(3)
-      const int nl = s_nl;
+      const int nl = min(s_nl, SPLIT_LQ);
       for (int b0 = 0; b0 < nl; b0 += SEG) {  // the round's long slices, block-wide
         const int ns = min(SEG, nl - b0);
         int len = 0, gp = 0;
@@ -2459,6 +2471,7 @@ __global__ __launch_bounds__(256) void k_split_combine(ScoreArgs a, int C, const
       const unsigned long long lo = want_a ? paa[2 * gp] : 0ull, hi = want_a ? paa[2 * gp + 1] : 0ull;
       const unsigned cn = pk24 ? (unsigned)(hi & ((1u << SPLIT_CN_BITS) - 1)) : pcn[gp];
       const int p = a.g_out[gp];
+      if (!PS_OK(a.misc, p >= 0 && p < a.np, 4, p, a.np)) continue;
       a.cn[p] = cn;
       if (want_a) a.aa[p] = pk24 ? blp::aa_value(lo, hi >> SPLIT_CN_BITS, 52) : blp::aa_value(lo, hi);
       if (want_j) {
@@ -2536,7 +2549,7 @@ __global__ __launch_bounds__(BLOCK) void k_score_hash(ScoreArgs a) {
   const uint32_t keep = a.idmask | 0x80000000u;
   auto find = [&](uint32_t v) -> int {  // slot of v (id - lo) or -1
     uint32_t h = hs_slot<HT>(v);
-    for (int i = 0; i < HT; ++i) {
+    for (int i = 0; i < HT; ++i) {  // bounded: a full table ends the probe
       const uint32_t t = tab[h];
       if (t == v) return (int)h;
       if (t == HS_EMPTY) return -1;
@@ -2560,9 +2573,11 @@ __global__ __launch_bounds__(BLOCK) void k_score_hash(ScoreArgs a) {
     --left;
     if (si >= n_hash) break;
     const int x = a.active[si];
+    if (!PS_OK(a.misc, x >= 0 && x < a.n_nodes, 2, x, a.n_nodes)) continue;  // uniform
     const int64_t xb = a.rp[x], xe = a.rp[x + 1];
     const int64_t wb = a.wp ? a.wp[x] : 0, we = a.wp ? a.wp[x + 1] : 0;
     const int pbeg = a.off[x], pcnt = a.cnt[x];
+    if (!PS_OK(a.misc, pbeg >= 0 && (int64_t)pbeg + pcnt <= a.np, 3, (int64_t)pbeg + pcnt, a.np)) continue;
     int64_t st0 = 0;
     int len0 = 0, p0 = 0;
     if ((int)threadIdx.x < pcnt) {
@@ -2577,7 +2592,9 @@ __global__ __launch_bounds__(BLOCK) void k_score_hash(ScoreArgs a) {
     unsigned long long added = 0;
     auto insert = [&](uint32_t v) {
       uint32_t h = hs_slot<HT>(v);
-      for (;;) {
+      for (int probes = 0;; ++probes) {
+        // the host routes only sources of build work <= HT / 2 (load <= 1/2): a full table is a bug
+        if (!PS_OK(a.misc, probes < HT, 8, probes, HT)) break;
         const uint32_t t = tab[h];
         if (t == v) break;
         if (t == HS_EMPTY) {
@@ -2641,6 +2658,7 @@ __global__ __launch_bounds__(BLOCK) void k_score_hash(ScoreArgs a) {
       const int64_t st = first ? st0 : a.g_yb[gp];
       const int len = first ? len0 : a.g_yl[gp];
       const int p = first ? p0 : a.g_out[gp];
+      if (!PS_OK(a.misc, p >= 0 && p < a.np, 4, p, a.np)) continue;
       unsigned c = 0;
       unsigned long long acc = 0, acch = 0;
       for (int h0 = 0; h0 < len; h0 += SHORT_PART) {
@@ -2676,168 +2694,6 @@ __global__ __launch_bounds__(BLOCK) void k_score_hash(ScoreArgs a) {
   }
 }
 
-// ------------------------------------------------------------------ wave-per-source scorer
-// For small node universes (the business side of a review graph: H2(v) ⊂ businesses) the
-// per-source work is ~2K elements, so a workgroup-wide pass is all barrier and latency.
-// Here every wave owns a bitmap slice and a segment area in LDS and runs its sources alone:
-// no block barriers, ~10 sources in flight per CU, same merge-path loops with 64 threads.
-constexpr int WSEG = 64;  // segments per wave chunk: one per lane
-
-__device__ inline void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-}
-
-__device__ inline int wave_exscan(int v, int lane, int* total) {
-  int inc = v;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int t = __shfl_up(inc, d, 64);
-    if (lane >= d) inc += t;
-  }
-  *total = __shfl(inc, 63, 64);
-  return inc - v;
-}
-
-template <typename T>
-__device__ inline T wave_sum(T v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-
-template <int WAVES, int WCAP, int K>
-__global__ __launch_bounds__(WAVES * 64) void k_score_wave(ScoreArgs a) {
-  __shared__ uint32_t bm_all[WAVES][WCAP];
-  __shared__ int64_t st_all[WAVES][WSEG];
-  __shared__ int32_t of_all[WAVES][WSEG + 1];
-  __shared__ uint32_t cn_all[WAVES][WSEG];
-  __shared__ unsigned long long aa_all[WAVES][2 * WSEG];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  uint32_t* bm = bm_all[wid];
-  uint4* bm4 = reinterpret_cast<uint4*>(bm);
-  int64_t* s_start = st_all[wid];
-  int32_t* s_off = of_all[wid];
-  uint32_t* s_cn = cn_all[wid];
-  unsigned long long* s_aa = aa_all[wid];
-  const int64_t c0 = a.lo;
-  const int64_t width = a.hi - a.lo;  // <= WCAP * 32 (checked by the host)
-  const int nw4 = (int)((((width + 31) >> 5) + 3) >> 2);
-  const bool want_j = (a.mask & BLP_JACCARD) != 0;
-  const bool want_a = (a.mask & BLP_ADAMIC) != 0;
-  const int n_active = a.misc->n_active;
-  for (;;) {
-    int first = 0;
-    if (lane == 0) first = atomicAdd(&a.misc->queue, a.dq);
-    first = __shfl(first, 0, 64);
-    if (first >= n_active) break;
-    const int last_s = min(n_active, first + a.dq);
-    for (int s = first; s < last_s; ++s) {
-      const int x = a.active[s];
-      const int pbeg = a.off[x], pcnt = a.cnt[x];
-      const int64_t xb = a.rp[x], xe = a.rp[x + 1];
-      const int hslot = a.heavy_slot ? a.heavy_slot[x] : -1;
-      if (hslot >= 0) {
-        const uint4* src4 = reinterpret_cast<const uint4*>(a.heavy_bm + (int64_t)hslot * a.hb_words);
-        for (int i = lane; i < nw4; i += 64) bm4[i] = src4[i];
-        wave_sync();
-      } else {
-        for (int i = lane; i < nw4; i += 64) bm4[i] = make_uint4(0, 0, 0, 0);
-        wave_sync();
-        for (int64_t k0 = xb; k0 < xe; k0 += WSEG) {
-          const int ns = (int)min<int64_t>(WSEG, xe - k0);
-          int len = 0;
-          if (lane < ns) {
-            const int z = a.ci[k0 + lane];
-            const int64_t st = a.rp[z];
-            s_start[lane] = st;
-            len = (int)(a.rp[z + 1] - st);
-          }
-          int tot;
-          const int ex = wave_exscan(len, lane, &tot);
-          if (lane < ns) s_off[lane] = ex;
-          if (lane == 0) s_off[ns] = tot;
-          wave_sync();
-          if (a.short_rows & 1)
-            row_build<64>(a.cw, a.idmask, s_start, s_off, ns, c0, width, bm, lane);
-          else
-            mp_build<64, K>(a.cw, a.idmask, s_start, s_off, ns, c0, width, bm, lane);
-          wave_sync();
-        }
-      }
-      // exact distance 2: drop x and N(x) where they fall inside the universe
-      const int64_t nx_lo = xe > xb ? a.ci[xb] : 0, nx_hi = xe > xb ? a.ci[xe - 1] : -1;
-      if (nx_hi >= c0 && nx_lo < c0 + width) {
-        for (int64_t k = xb + lane; k < xe; k += 64) {
-          const int64_t r = (int64_t)a.ci[k] - c0;
-          if (r >= 0 && r < width) atomicAnd(&bm[r >> 5], ~(1u << (r & 31)));
-        }
-      }
-      if (lane == 0 && x >= c0 && x < c0 + width) atomicAnd(&bm[(x - c0) >> 5], ~(1u << ((x - c0) & 31)));
-      wave_sync();
-      unsigned long long h2 = 0;
-      if (want_j) {
-        unsigned long long pc = 0;
-        for (int i = lane; i < nw4; i += 64) {
-          const uint4 q = bm4[i];
-          pc += __popc(q.x) + __popc(q.y) + __popc(q.z) + __popc(q.w);
-        }
-        h2 = wave_sum(pc);
-      }
-      for (int sb = 0; sb < pcnt; sb += WSEG) {
-        const int ns = min(WSEG, pcnt - sb);
-        int len = 0, pout = 0;
-        if (lane < ns) {
-          const int gp = pbeg + sb + lane;
-          s_start[lane] = a.g_yb[gp];
-          len = a.g_yl[gp];
-          pout = a.g_out[gp];
-          s_cn[lane] = 0;
-          s_aa[2 * lane] = 0;
-          s_aa[2 * lane + 1] = 0;
-        }
-        int tot;
-        const int ex = wave_exscan(len, lane, &tot);
-        if (lane < ns) s_off[lane] = ex;
-        if (lane == 0) s_off[ns] = tot;
-        wave_sync();
-        if (a.short_rows & 2) {
-          if (want_a)
-            row_scan<64, true>(a.cw, a.idmask, a.idbits, a.aaw, a.wtab, s_start, s_off, ns, c0, width, bm, s_cn, s_aa,
-                               lane);
-          else
-            row_scan<64, false>(a.cw, a.idmask, a.idbits, a.aaw, a.wtab, s_start, s_off, ns, c0, width, bm, s_cn, s_aa,
-                                lane);
-        } else if (want_a) {
-          mp_scan<64, K, true>(a.cw, a.idmask, a.idbits, a.aaw, a.wtab, s_start, s_off, ns, c0, width, bm, s_cn, s_aa,
-                               lane);
-        } else {
-          mp_scan<64, K, false>(a.cw, a.idmask, a.idbits, a.aaw, a.wtab, s_start, s_off, ns, c0, width, bm, s_cn, s_aa,
-                                lane);
-        }
-        wave_sync();
-        if (lane < ns) {
-          const int p = pout;
-          const unsigned c = s_cn[lane];
-          a.cn[p] = c;
-          if (want_a) a.aa[p] = blp::aa_value(s_aa[2 * lane], s_aa[2 * lane + 1]);
-          if (want_j) {
-            const long long uni = (long long)h2 + len - (long long)c;
-            if (uni <= 0) {
-              a.jac[p] = __builtin_nan("");
-              atomicOr(&a.misc->zero_div, 1);
-            } else {
-              a.jac[p] = (double)c / (double)uni;
-            }
-          }
-        }
-        wave_sync();
-      }
-    }
-  }
-}
-
-constexpr int W_WAVES = 2, W_CAP = 3328;  // 13 KiB of bitmap per wave (106,496 node ids)
 
 enum Variant { V_SMALL = 0, V_MED = 1, V_LARGE = 2 };
 // LDS bitmap words (16 / 64 / 136 KiB), threads per block, pair/row segments per chunk
@@ -2854,6 +2710,64 @@ constexpr int S_MAX_CHUNKS = 128;                          // up to 67M-node uni
 inline int variant_block(int v) { return v == V_SMALL ? BLOCK_SMALL : v == V_MED ? BLOCK_MED : BLOCK_LARGE; }
 inline int64_t variant_cap_bits(int v) { return 32ll * (v == V_SMALL ? CAP_SMALL : v == V_MED ? CAP_MED : CAP_LARGE); }
 
+}  // namespace
+
+namespace {
+// Environment switches of the pair scorers, read ONCE per batch at blp_batch_create (never while
+// scoring): path selectors the tests use to drive every kernel on small graphs, and two tuning
+// overrides. Release behaviour is the all-default struct.
+struct Knobs {
+  bool no_runs = false;          // BLP_NO_RUNS: bucket-sort grouping even for source-grouped lists
+  bool no_short = false;         // BLP_NO_SHORT: row-per-thread loops off
+  bool no_short_kernel = false;  // BLP_NO_SHORT_KERNEL: the short-row scorer off (block scorer instead)
+  int variant = -1;              // BLP_VARIANT: a wider LDS variant than needed
+  int64_t chunk_bits = 0;        // BLP_CHUNK_BITS: force multi-chunk universes on small graphs
+  int split_big = -1;            // BLP_SPLIT_BIG: 128 KiB (1) or 64 KiB (0) chunk-parallel chunks
+  int split = -1;                // BLP_SPLIT: force C chunk-parallel chunks
+  bool no_split = false;         // BLP_NO_SPLIT
+  bool no_global = false;        // BLP_NO_GLOBAL
+  bool force_global = false;     // BLP_FORCE_GLOBAL
+  int64_t heavy_work = -1;       // BLP_HEAVY_WORK: heavy-source item size
+  bool no_wedge = false;         // BLP_NO_WEDGE: build H2 from the CSR, not the wedge rows
+  bool no_wbm_batch = false;     // BLP_NO_WBM_BATCH: no wedge-row bitmaps as pre-built H2 sets
+  bool group_buckets = false;    // BLP_GROUP_BUCKETS: one workgroup per contiguous bucket
+  bool no_hash = false;          // BLP_NO_HASH: no hash-set scorer in split batches
+  int64_t hash_work = -1;        // BLP_HASH_WORK: hash-set routing bound (build ids)
+  bool no_wcodes = false;        // BLP_NO_WCODES: plain ids (per-hit weight gathers)
+  bool split_nopk = false;       // BLP_SPLIT_NOPK: unpacked split partials
+  int split_short = -1;          // BLP_SPLIT_SHORT: register-scanned slice bound (0: off)
+  int cosched_cus = -1;          // BLP_COSCHED_CUS: tuning override of the co-scheduled CU share
+};
+
+Knobs read_knobs() {
+  Knobs k;
+  auto on = [](const char* n) { return getenv(n) != nullptr; };
+  auto num = [](const char* n, long long dflt) {
+    const char* e = getenv(n);
+    return e ? atoll(e) : dflt;
+  };
+  k.no_runs = on("BLP_NO_RUNS");
+  k.no_short = on("BLP_NO_SHORT");
+  k.no_short_kernel = on("BLP_NO_SHORT_KERNEL");
+  k.variant = (int)num("BLP_VARIANT", -1);
+  k.chunk_bits = num("BLP_CHUNK_BITS", 0);
+  k.split_big = (int)num("BLP_SPLIT_BIG", -1);
+  k.split = (int)num("BLP_SPLIT", -1);
+  k.no_split = on("BLP_NO_SPLIT");
+  k.no_global = on("BLP_NO_GLOBAL");
+  k.force_global = on("BLP_FORCE_GLOBAL");
+  k.heavy_work = num("BLP_HEAVY_WORK", -1);
+  k.no_wedge = on("BLP_NO_WEDGE");
+  k.no_wbm_batch = on("BLP_NO_WBM_BATCH");
+  k.group_buckets = on("BLP_GROUP_BUCKETS");
+  k.no_hash = on("BLP_NO_HASH");
+  k.hash_work = num("BLP_HASH_WORK", -1);
+  k.no_wcodes = on("BLP_NO_WCODES");
+  k.split_nopk = on("BLP_SPLIT_NOPK");
+  k.split_short = (int)num("BLP_SPLIT_SHORT", -1);
+  k.cosched_cus = (int)num("BLP_COSCHED_CUS", -1);
+  return k;
+}
 }  // namespace
 
 struct blp_batch {
@@ -2880,12 +2794,12 @@ struct blp_batch {
   int chunks = 1;
   int dq = 1;
   bool use_hot = false;  // some source has a dense row in N(x)
-  bool wave = false;     // wave-per-source scorer
   int short_rows = 0;    // ScoreArgs::short_rows
   bool global = false;   // HBM-bitmap scorer (universe wider than LDS)
   int split = 0;         // chunk-parallel scorer: universe cut into `split` LDS chunks, 2 workgroups / CU
   bool split_big = false;  // ... 128 KiB chunks, one workgroup per CU
   int64_t rs_lo = 0;     // first node of the split table
+  int64_t rs_rows = 0;   // its rows
   int32_t* d_gy = nullptr;     // grouped position -> y (split mode)
   int32_t* d_rsplit = nullptr; // [n][split + 1] row offsets where neighbour ids cross chunk boundaries
   int4* d_lq = nullptr;        // k_score_split's long-slice queues (SPLIT_LQ per resident workgroup)
@@ -2915,38 +2829,21 @@ struct blp_batch {
   int64_t n_hash = 0;          // such sources
   bool use_short = false;   // the short-row scorer takes this batch (decided once, at create)
   int64_t work_elems = 0;  // planned build + scan elements (co-scheduling estimate)
+  Knobs kn;               // environment switches, read once at create
 };
 
 using namespace blp;
 
 // the short-row scorer (k_score<..., SHORT = true>) takes the batch
 static bool short_kernel(const blp_batch* b) {
-  return b->variant == V_SMALL && b->short_rows == 3 && !b->wave && !b->global && !b->split &&
-         !getenv("BLP_NO_SHORT_KERNEL");
-}
-
-// elements per thread per merge-path step (template; BLP_KPT=4|8|16 selects another build)
-static int kpt_choice() {
-  static int k = [] {
-    const char* e = getenv("BLP_KPT");
-    const int v = e ? atoi(e) : 8;
-    return (v == 4 || v == 16) ? v : 8;
-  }();
-  return k;
-}
-
-template <int BLOCK, int CAP, int SEG, int K>
-static int score_occ(int* per_cu) {
-  BLP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, k_score<BLOCK, CAP, SEG, K>, BLOCK, 0));
-  *per_cu = std::max(*per_cu, 1);
-  return BLP_OK;
+  return b->variant == V_SMALL && b->short_rows == 3 && !b->global && !b->split && !b->kn.no_short_kernel;
 }
 
 template <int BLOCK, int CAP, int SEG>
 static int score_occupancy(int* per_cu) {
-  const int k = kpt_choice();
-  return k == 4 ? score_occ<BLOCK, CAP, SEG, 4>(per_cu) : k == 16 ? score_occ<BLOCK, CAP, SEG, 16>(per_cu)
-                                                                  : score_occ<BLOCK, CAP, SEG, 8>(per_cu);
+  BLP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, k_score<BLOCK, CAP, SEG, 8>, BLOCK, 0));
+  *per_cu = std::max(*per_cu, 1);
+  return BLP_OK;
 }
 
 static int variant_occupancy(int v, int* per_cu) {
@@ -2959,13 +2856,7 @@ template <int BLOCK, int CAP, int SEG, bool SAA = true>
 static int launch_score(blp_graph* g, hipStream_t st, const ScoreArgs& a, int per_cu, int cus) {
   if (cus <= 0 || cus > g->n_cu) cus = g->n_cu;
   const dim3 grid(cus * per_cu), block(BLOCK);
-  const int k = kpt_choice();
-  if (k == 4)
-    hipLaunchKernelGGL((k_score<BLOCK, CAP, SEG, 4, false, SAA>), grid, block, 0, st, a);
-  else if (k == 16)
-    hipLaunchKernelGGL((k_score<BLOCK, CAP, SEG, 16, false, SAA>), grid, block, 0, st, a);
-  else
-    hipLaunchKernelGGL((k_score<BLOCK, CAP, SEG, 8, false, SAA>), grid, block, 0, st, a);
+  hipLaunchKernelGGL((k_score<BLOCK, CAP, SEG, 8, false, SAA>), grid, block, 0, st, a);
   BLP_HIP(hipGetLastError());
   return BLP_OK;
 }
@@ -2979,8 +2870,7 @@ static int launch_short(blp_graph* g, const blp_batch* b, ScoreArgs a, size_t dy
   int per_cu = 1;
   BLP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, BLOCK_SMALL, dyn));
   const int64_t n_wg = (int64_t)g->n_cu * std::max(per_cu, 1);
-  if (!getenv("BLP_DQ") && b->n_sources >= n_wg * 16) a.dq = std::max(a.dq, 2);
-  if (const char* e = getenv("BLP_DQ_SHORT")) a.dq = std::min(DQ_MAX, std::max(1, atoi(e)));  // tuning knob
+  if (b->n_sources >= n_wg * 16) a.dq = std::max(a.dq, 2);
   hipLaunchKernelGGL((k_score<BLOCK_SMALL, CAP_SMALL, SEG_SMALL, 8, true, SAA>), dim3((unsigned)n_wg),
                      dim3(BLOCK_SMALL), dyn, b->stream, a);
   BLP_HIP(hipGetLastError());
@@ -3074,7 +2964,8 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   int64_t lo = A.lo, hi = A.hi;
   const int64_t scan_work = A.scan, max_scan_row = A.max_scan, max_build_row = A.max_build;
   const bool any_hot = A.any_hot;
-  bool runs = A.runs && !getenv("BLP_NO_RUNS");  // x non-decreasing: grouped by run heads (BLP_NO_RUNS: bucket sort)
+  const Knobs kn = read_knobs();
+  bool runs = A.runs && !kn.no_runs;  // x non-decreasing: grouped by run heads (BLP_NO_RUNS: bucket sort)
   const int64_t rows_lo = A.rows_lo, rows_hi = A.rows_hi;
   if (lo > hi) lo = hi = 0;
   lo &= ~int64_t(127);  // 128-bit aligned so dense rows map onto whole 16-byte LDS vectors
@@ -3086,7 +2977,8 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   b->hi = hi;
   b->n_sources = (int64_t)srcs.size();
   b->use_hot = any_hot;
-  if (!getenv("BLP_NO_SHORT"))  // tuning knob
+  b->kn = kn;
+  if (!kn.no_short)  // test knob
     b->short_rows = (max_build_row <= SHORT_MAX ? 1 : 0) | (max_scan_row <= SHORT_MAX ? 2 : 0);
   const int64_t span = hi - lo;
   if (span <= variant_cap_bits(V_SMALL))
@@ -3095,15 +2987,10 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
     b->variant = V_MED;
   else
     b->variant = V_LARGE;
-  if (const char* e = getenv("BLP_VARIANT")) {  // test knob: a wider LDS variant than needed
-    const int v = atoi(e);
-    if (v > b->variant && v <= V_LARGE) b->variant = v;
-  }
+  if (kn.variant > b->variant && kn.variant <= V_LARGE) b->variant = kn.variant;  // test knob: a wider LDS variant
   b->cap_bits = variant_cap_bits(b->variant);
-  if (const char* e = getenv("BLP_CHUNK_BITS")) {  // test knob: force multi-chunk on small graphs
-    int64_t v = atoll(e);
-    if (v >= 128 && v % 128 == 0 && v < b->cap_bits) b->cap_bits = v;
-  }
+  if (kn.chunk_bits >= 128 && kn.chunk_bits % 128 == 0 && kn.chunk_bits < b->cap_bits)  // test knob: multi-chunk
+    b->cap_bits = kn.chunk_bits;
   b->chunks = span <= b->cap_bits ? 1 : (int)((span + b->cap_bits - 1) / b->cap_bits);
   // wider than one LDS bitmap, up to eight 512K-bit chunks: chunk-parallel scorer, (source,
   // chunk) items on 64 KiB bitmaps, two workgroups per CU -- 5.7x the HBM-bitmap scorer on
@@ -3115,12 +3002,12 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
     // 1.77 s per step with 64 KiB chunks on both sides, 1.07 s with 128 KiB chunks (both
     // sides). BLP_SPLIT_BIG=0 keeps 64 KiB chunks, two workgroups per CU.
     b->split_big = true;
-    if (const char* e = getenv("BLP_SPLIT_BIG")) b->split_big = atoi(e) > 0;  // tuning knob
+    if (kn.split_big >= 0) b->split_big = kn.split_big > 0;  // test knob
     const int64_t sbits = 32ll * (b->split_big ? S_CAP_BIG : S_CAP);
     int C = 0;
-    if (const char* e = getenv("BLP_SPLIT"))
-      C = std::max(0, std::min(S_MAX_CHUNKS, atoi(e)));
-    else if (span > variant_cap_bits(V_LARGE) && span <= S_MAX_CHUNKS * sbits && !getenv("BLP_NO_SPLIT"))
+    if (kn.split >= 0)
+      C = std::max(0, std::min(S_MAX_CHUNKS, kn.split));
+    else if (span > variant_cap_bits(V_LARGE) && span <= S_MAX_CHUNKS * sbits && !kn.no_split)
       C = (int)((span + sbits - 1) / sbits);
     if (C >= 2 && span > 0) {
       b->split = C;
@@ -3131,7 +3018,7 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   }
   // wider than LDS: one HBM bitmap per workgroup instead of an H2 rebuild per LDS chunk
   // (BLP_NO_GLOBAL keeps the chunked path, BLP_FORCE_GLOBAL selects HBM on any universe)
-  b->global = !b->split && ((b->chunks > 1 && !getenv("BLP_NO_GLOBAL")) || getenv("BLP_FORCE_GLOBAL"));
+  b->global = !b->split && ((b->chunks > 1 && !kn.no_global) || kn.force_global);
   if (b->global) b->chunks = 1;
   auto bail = [&](int rc) {
     blp_batch_destroy(b);
@@ -3141,16 +3028,8 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   if (rc) return bail(rc);
   BLP_HIP_OR(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking), bail);
   BLP_HIP_OR(hipStreamSynchronize(g->stream), bail);  // the graph's own uploads are complete
-  // wave-per-source scorer: opt-in (BLP_WAVE=1). With heavy sources split finely the block
-  // kernels are faster on the business side of config 2 (1.46 vs 2.01 ms, profiles/probe_sides.py)
-  b->wave = span <= (int64_t)W_CAP * 32 && b->chunks == 1 && !b->global && !b->split && getenv("BLP_WAVE") &&
-            !getenv("BLP_NO_WAVE");
   int per_cu = 1;
-  if (b->wave) {
-    BLP_HIP_OR(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_score_wave<W_WAVES, W_CAP, 8>, W_WAVES * 64, 0),
-               bail);
-    per_cu = std::max(per_cu, 1) * W_WAVES;  // workers are waves
-  } else if (b->split) {
+  if (b->split) {
     BLP_HIP_OR(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_score_split<S_BLOCK, S_CAP, S_SEG, 8>,
                                                             S_BLOCK, 0), bail);
   } else if ((rc = variant_occupancy(b->variant, &per_cu))) {
@@ -3160,20 +3039,17 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   // sources per dequeue: the active list is in id order, which need not be balanced; keep it 1
   // unless there are very many light sources per worker
   // (two once a worker has ~64+ sources: the business side of config 2, 1.44 -> 1.30 ms)
-  b->dq = b->n_sources >= n_wg * 64 ? (int)std::max<int64_t>(2, std::min<int64_t>(8, b->n_sources / (n_wg * 64))) : 1;
-  if (const char* e = getenv("BLP_DQ")) b->dq = std::min(DQ_MAX, std::max(1, atoi(e)));  // tuning knob
+  b->dq = b->n_sources >= n_wg * 64 ? (int)std::max<int64_t>(2, std::min<int64_t>(DQ_MAX, b->n_sources / (n_wg * 64))) : 1;
   // ---- heavy sources: build work far above the per-workgroup share goes to k_heavy
   const int64_t total_work = std::accumulate(work.begin(), work.end(), (int64_t)0) + scan_work;
   b->work_elems = total_work;
-  // a wave is ~16x slower on one source than a 1024-thread block: split much earlier there
-  int64_t item_work = b->wave ? std::max<int64_t>(4096, total_work / std::max<int64_t>(4 * n_wg, 1))
-                              : std::max<int64_t>(16384, total_work / std::max<int64_t>(4 * n_wg, 1));
-  if (const char* e = getenv("BLP_HEAVY_WORK")) item_work = std::max<int64_t>(1, atoll(e));  // test knob
+  int64_t item_work = std::max<int64_t>(16384, total_work / std::max<int64_t>(4 * n_wg, 1));
+  if (kn.heavy_work >= 0) item_work = std::max<int64_t>(1, kn.heavy_work);  // test knob
   std::vector<int32_t> heavy_slot;
   std::vector<HeavyItem> items;
   // every source's rows are short and the graph holds wedge rows: heavy sources are split into
   // slices of their wedge rows (the short-row scorer's layout)
-  const bool wedge_items = (b->short_rows & 1) && g->d_wp && !getenv("BLP_NO_WEDGE");
+  const bool wedge_items = (b->short_rows & 1) && g->d_wp && !kn.no_wedge;
   if (b->chunks == 1 && span > 0 && !b->global && (!b->split || span <= variant_cap_bits(V_LARGE))) {
     for (size_t i = 0; i < srcs.size(); ++i) {
       if (work[i] <= 2 * item_work) continue;
@@ -3203,7 +3079,7 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   // at least as long as its bitmap's words copies the bitmap (its id set, 12.5 KB at config 2)
   // instead of OR-ing the row id by id -- the same slots and copy as k_heavy's pre-built bitmaps,
   // so those sources need no per-step k_heavy either (BLP_NO_WBM_BATCH=1: off)
-  if (wedge_items && b->chunks == 1 && span > 0 && !b->global && !b->split && !b->wave && !getenv("BLP_NO_WBM_BATCH")) {
+  if (wedge_items && b->chunks == 1 && span > 0 && !b->global && !b->split && !b->kn.no_wbm_batch) {
     int rcw = BLP_OK;
     const WedgeBitmaps* w = wedge_bitmaps(g, lo, hi, &rcw);
     if (rcw) return bail(rcw);
@@ -3232,7 +3108,7 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
     if (srcs.empty()) xlo = xhi = 0;
     b->xlo = xlo;
     b->xspan = (int64_t)xhi - xlo;
-    b->items = !getenv("BLP_GROUP_BUCKETS");  // A/B knob: one workgroup per contiguous bucket
+    b->items = !kn.group_buckets;  // test knob: one workgroup per contiguous bucket
     if (b->items) {
       // nb = 2^shift interleaved buckets (<= 2048), each with ceil(xspan / nb) keys
       b->shift = 0;
@@ -3254,6 +3130,7 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
     const int C = b->split;
     b->rs_lo = rows_lo;
     const int64_t nrows = std::max<int64_t>(rows_hi - rows_lo, 1);
+    b->rs_rows = nrows;
     if (hipMalloc(&b->d_gy, 4 * (size_t)n_pairs) != hipSuccess ||
         hipMalloc(&b->d_rsplit, 4 * (size_t)nrows * (C + 1)) != hipSuccess ||
         hipMalloc(&b->d_pcn, 4 * (size_t)n_pairs) != hipSuccess ||
@@ -3267,11 +3144,17 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
     BLP_HIP_OR(hipStreamSynchronize(g->stream), bail);
   }
   // ---- hash-set scorer (split batches): sources whose build work fits half the hash table
-  if (b->split && n_pairs && !getenv("BLP_NO_HASH")) {
+  if (b->split && n_pairs && !kn.no_hash) {
     // work bounds the distinct ids inserted; at most HT - 1 keeps an empty slot, so every insert
     // and probe chain ends (the knob is clamped: a fuller table is slower, never unbounded)
-    const int64_t want = getenv("BLP_HASH_WORK") ? atoll(getenv("BLP_HASH_WORK")) : HS_HT / 2;
+    const int64_t want = kn.hash_work >= 0 ? kn.hash_work : HS_HT / 2;
+#ifdef BLP_DEBUG
+    // debug builds take the knob unclamped, so a test can overfill the table and see the probe
+    // bound (PS_OK site 8) report it instead of a spin
+    const int64_t cap = kn.hash_work >= 0 ? kn.hash_work : std::min<int64_t>(std::max<int64_t>(1, want), HS_HT - 1);
+#else
     const int64_t cap = std::min<int64_t>(std::max<int64_t>(1, want), HS_HT - 1);
+#endif
     std::vector<uint8_t> hf((size_t)std::max<int64_t>(b->xspan, 1), 0);
     for (size_t i = 0; i < srcs.size(); ++i)
       if (work[i] <= cap) {
@@ -3309,6 +3192,8 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   if (b->use_short &&
       hipMalloc(&b->d_rec, sizeof(SrcRec) * (size_t)std::max<int64_t>(b->n_sources, 1)) != hipSuccess)
     return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: hipMalloc failed"));
+  if (hipMemset(b->d_misc, 0, sizeof(Misc)) != hipSuccess)  // dbg[] is zeroed here, not per score
+    return bail(fail(BLP_E_HIP_BASE, "blp_batch_create: hipMemset failed"));
   if (n_pairs) {
     if (hipMemcpy(b->d_x, x, 4 * n_pairs, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(b->d_y, y, 4 * n_pairs, hipMemcpyHostToDevice) != hipSuccess)
@@ -3353,7 +3238,7 @@ int blp_batch_plan(const blp_batch* b, int64_t* lo, int64_t* hi, int* chunks, in
   if (lo) *lo = b->lo;
   if (hi) *hi = b->hi;
   if (chunks) *chunks = b->global ? 0 : b->split ? -b->split : b->chunks;  // 0: HBM bitmap; -C: chunk-parallel
-  if (block) *block = b->wave ? 64 : b->global ? G_BLOCK : b->split ? S_BLOCK : variant_block(b->variant);
+  if (block) *block = b->global ? G_BLOCK : b->split ? S_BLOCK : variant_block(b->variant);
   if (heavy) *heavy = (int)b->n_heavy;
   return BLP_OK;
 }
@@ -3407,7 +3292,7 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   hipEvent_t t0, bt0;
   if ((rc = timer_begin(g->timers[K_GROUP], b->stream, &t0))) return rc;
   if ((rc = timer_begin(b->t_group, b->stream, &bt0))) return rc;
-  BLP_HIP(hipMemsetAsync(b->d_misc, 0, sizeof(Misc), b->stream));
+  BLP_HIP(hipMemsetAsync(b->d_misc, 0, offsetof(Misc, dbg), b->stream));  // the debug record persists to fetch
   if (np && b->runs) {
     const int64_t tiles = (np + SCAN_TILE - 1) / SCAN_TILE;
     int32_t* rtile = reinterpret_cast<int32_t*>(tmp);  // the bucket sort's pair buffer is free here
@@ -3438,7 +3323,7 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
       hipLaunchKernelGGL(k_item_plan, dim3(1), dim3(1024), 0, b->stream, hoff, b->nblk, b->nb, np, it_b, it_s, it_e,
                          &b->d_misc->n_items);
       const int64_t keys = (b->xspan + b->nb - 1) >> b->shift;
-      const bool runs_w = keys <= 1024 && !getenv("BLP_ITEM_SCATTER");
+      const bool runs_w = keys <= 1024;
       int32_t* ih = tx2 + tx + 1;  // [ub][K] item histograms (runs_w)
 #define BLP_ITEM_LAUNCH(K)                                                                                         \
   hipLaunchKernelGGL(k_item_count<K>, dim3((unsigned)ub), dim3(GB_BLOCK), 0, b->stream, tmp, it_b, it_s, it_e,     \
@@ -3535,8 +3420,7 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   a.aaw = g->d_aaw_fx;
   a.aa_part = b->d_aa_part;
   a.rec = nullptr;
-  a.sched = getenv("BLP_STATIC") ? atoi(getenv("BLP_STATIC")) : 0;  // tuning knob
-  const bool coded = g->d_ci_w && !getenv("BLP_NO_WCODES");  // tuning knob
+  const bool coded = g->d_ci_w && !b->kn.no_wcodes;  // test knob
   a.cw = coded ? g->d_ci_w : g->d_ci;
   a.idbits = coded ? g->id_bits : 31;
   a.idmask = (uint32_t)((1ull << a.idbits) - 1);
@@ -3564,21 +3448,21 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   a.mask = mask | BLP_CN;  // counts are always produced (Jaccard needs them)
   a.dq = b->dq;
   a.short_rows = b->short_rows;
+  a.np = np;
+  a.n_nodes = g->n;
+  a.rs_rows = b->rs_rows;
+  a.lq_wgs = b->d_lq ? 2 * g->n_cu : 0;
   if (np && b->split) {
     // AA counts ride in the packed per-pair word while every row (hence every count) < 2^24
-    const int pk24 = (mask & BLP_ADAMIC) && g->max_row < (int64_t(1) << SPLIT_CN_BITS) && !getenv("BLP_SPLIT_NOPK");
+    const int pk24 = (mask & BLP_ADAMIC) && g->max_row < (int64_t(1) << SPLIT_CN_BITS) && !b->kn.split_nopk;
     // slices of <= short_max ids scanned by their pair's thread (128 KiB chunks; BLP_SPLIT_SHORT=0: off)
-    const int short_max = std::min(SHORT_PART, getenv("BLP_SPLIT_SHORT") ? atoi(getenv("BLP_SPLIT_SHORT")) : SHORT_PART);
-    // k_score_split: 1 = one global item queue (no XCD groups), 2 = one queue in chunk-major order
-    a.sched = getenv("BLP_SPLIT_ONEQ") ? (atoi(getenv("BLP_SPLIT_ONEQ")) == 2 ? 2 : 1) : 0;
-    a.lq = b->d_lq;
-    a.split_round = std::max(1, std::min(SPLIT_ROUND_MAX, getenv("BLP_SPLIT_ROUND") ? atoi(getenv("BLP_SPLIT_ROUND"))
-                                                                                     : SPLIT_ROUND));  // tuning knob
-    if (g->d_wp && !getenv("BLP_NO_WEDGE")) {  // sources with wedge rows build from them (split and hash kernels)
+    const int short_max = std::min(SHORT_PART, b->kn.split_short >= 0 ? b->kn.split_short : SHORT_PART);
+    if (g->d_wp && !b->kn.no_wedge) {  // sources with wedge rows build from them (split and hash kernels)
       a.wp = g->d_wp;
       a.wedge = reinterpret_cast<const uint4*>(g->d_wedge);
     }
-    const int scu = b->cus > 0 ? b->cus : g->n_cu;  // CUs the persistent grids may fill (blp_batches_score)
+    // CUs the persistent grids may fill (blp_batches_score), within [1, n_cu]: d_lq holds 2 workgroups per CU
+    const int scu = std::max(1, std::min(b->cus > 0 ? b->cus : g->n_cu, g->n_cu));
     if (b->d_hflag) {  // small-H2 sources first, on their own hash-set kernel
       hipLaunchKernelGGL(k_hash_partition, dim3(g->n_cu * 4), dim3(256), 0, b->stream, a.active, b->d_misc, b->d_hflag,
                          (int32_t)b->xlo, b->d_active2);
@@ -3612,21 +3496,10 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
     hipLaunchKernelGGL((k_score_global<G_BLOCK, G_SEG, 8>), dim3((unsigned)b->gslots), dim3(G_BLOCK), 0, b->stream, a,
                        b->d_gbm, b->gwords);
     BLP_HIP(hipGetLastError());
-  } else if (np && b->wave) {
-    int per_cu = 1;
-    BLP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_score_wave<W_WAVES, W_CAP, 8>, W_WAVES * 64, 0));
-    a.hot_idx = nullptr;  // the wave kernel builds every row sparsely
-    const dim3 grid(g->n_cu * std::max(per_cu, 1)), block(W_WAVES * 64);
-    static const int wk = getenv("BLP_WAVE_K") ? atoi(getenv("BLP_WAVE_K")) : 8;  // tuning knob
-    if (wk == 4)
-      hipLaunchKernelGGL((k_score_wave<W_WAVES, W_CAP, 4>), grid, block, 0, b->stream, a);
-    else
-      hipLaunchKernelGGL((k_score_wave<W_WAVES, W_CAP, 8>), grid, block, 0, b->stream, a);
-    BLP_HIP(hipGetLastError());
   } else if (np && b->use_short) {
     // bitmap in dynamic LDS, sized to the universe (whole 16-byte vectors)
     const size_t dyn = 4 * (size_t)std::max<int64_t>(4, ((b->hi - b->lo + 31) / 32 + 3) / 4 * 4);
-    if (g->d_wp && !getenv("BLP_NO_WEDGE")) {  // tuning knob: BLP_NO_WEDGE builds from CSR
+    if (g->d_wp && !b->kn.no_wedge) {  // test knob: BLP_NO_WEDGE builds from CSR
       a.wp = g->d_wp;
       a.wedge = reinterpret_cast<const uint4*>(g->d_wedge);
     }
@@ -3670,7 +3543,7 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
 // chip. BLP_COSCHED_CUS overrides the share.
 int blp_batches_score(blp_graph* g, int n, blp_batch* const* bs, const uint32_t* masks) {
   BLP_CHECK(g && n >= 0 && (n == 0 || (bs && masks)), BLP_E_ARG, "blp_batches_score: bad arguments");
-  auto is_large = [](const blp_batch* b) { return b->variant == V_LARGE && !b->split && !b->global && !b->wave; };
+  auto is_large = [](const blp_batch* b) { return b->variant == V_LARGE && !b->split && !b->global; };
   double t_large = 0.0, t_other = 0.0;
   for (int i = 0; i < n; ++i) {
     BLP_CHECK(bs[i] && bs[i]->g == g, BLP_E_ARG, "blp_batches_score: graph/batch mismatch");
@@ -3684,24 +3557,13 @@ int blp_batches_score(blp_graph* g, int n, blp_batch* const* bs, const uint32_t*
     const double f = t_large / (t_large + 0.38 * t_other);
     share = std::max(g->n_cu / 2, std::min(g->n_cu, (int)std::lround(f * g->n_cu / 8.0) * 8));
   }
-  if (const char* e = getenv("BLP_COSCHED_CUS")) share = atoi(e);  // tuning knob
-  // chunk-parallel batches side by side (config 5's two passes), opt-in (BLP_SPLIT_COSCHED=1): each
-  // persistent grid on a share of the CUs in proportion to its planned elements. Measured slower
-  // than the two grids each on the whole chip (1951 ms per config-5 step against 743 ms).
-  int n_split = 0;
-  double w_split = 0.0;
-  for (int i = 0; i < n; ++i)
-    if (bs[i]->split) ++n_split, w_split += (double)bs[i]->work_elems + 1.0;
-  const bool split_share = n_split >= 2 && getenv("BLP_SPLIT_COSCHED") && atoi(getenv("BLP_SPLIT_COSCHED")) != 0;
+  if (n > 0 && bs[0]->kn.cosched_cus > 0) share = bs[0]->kn.cosched_cus;  // tuning knob (read at create)
+  // chunk-parallel batches (config 5's two passes) each take the whole chip: holding each
+  // persistent grid to a CU share was slower at every share tried (1951 ms per config-5 step in
+  // proportion to planned work, 864 / 903 ms at 176 / 128 user CUs, against 743 ms)
   for (int i = 0; i < n; ++i) {
     blp_batch* b = bs[i];
     b->cus = is_large(b) && t_other > 0.0 ? share : 0;
-    if (split_share && b->split) {
-      const double f = ((double)b->work_elems + 1.0) / w_split;
-      b->cus = std::max(8, std::min(g->n_cu - 8, (int)std::lround(f * g->n_cu / 8.0) * 8));
-      if (const char* e = getenv("BLP_SPLIT_COSCHED_CUS"))  // tuning knob: the FIRST split batch's share
-        b->cus = i == 0 ? atoi(e) : g->n_cu - atoi(e);
-    }
     const int rc = blp_batch_score(g, b, masks[i]);
     b->cus = 0;
     if (rc) return rc;
@@ -3745,6 +3607,16 @@ int blp_batch_fetch(blp_graph* g, blp_batch* b, uint32_t* cn, double* jac, doubl
     if (jac) BLP_HIP(hipMemcpy(jac, b->d_jac, 8 * np, hipMemcpyDeviceToHost));
     if (aa) BLP_HIP(hipMemcpy(aa, b->d_aa, 8 * np, hipMemcpyDeviceToHost));
   }
+#ifdef BLP_DEBUG
+  if (m.dbg[0]) {  // the scorers' bound checks (PS_OK): any violation fails the batch
+    const long long z[4] = {0, 0, 0, 0};
+    BLP_HIP(hipMemcpy(b->d_misc->dbg, z, sizeof(z), hipMemcpyHostToDevice));
+    char msg[160];
+    snprintf(msg, sizeof msg, "blp_batch_fetch [BLP_DEBUG]: %lld bound violations; first at site %lld: %lld vs bound %lld",
+             m.dbg[0], m.dbg[1], m.dbg[2], m.dbg[3]);
+    return fail(BLP_E_STATE, msg);
+  }
+#endif
   if (m.zero_div && jac) return fail(BLP_E_ZERODIV, "float division by zero (Jaccard union is empty)");
   return BLP_OK;
 }

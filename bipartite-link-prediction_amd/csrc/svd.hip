@@ -156,7 +156,7 @@ __device__ inline void tk_compact(double* top_s, int* top_c, const double* buf_s
 
 // RT row tiles per wave (16 RT users): every B fragment fetched feeds RT MFMA chains, so the
 // Vt stream per score is 8 KiB / (256 RT) -- RT = 2 halves the L2/MALL traffic of RT = 1.
-// EXP = 1 (timing experiment only, BLP_SVD_EXP=1): the MFMA chains and fragment loads without
+// EXP = 1 (timing experiment only; no launch site instantiates it): the MFMA chains and fragment loads without
 // the top-k epilogue (results are NOT valid)
 template <int KPAD, int RT, int WAVES, int EXP = 0, int PR = 0>
 __global__ __launch_bounds__(WAVES * 64) void k_svd_topk(TopkArgs a) {
@@ -729,22 +729,18 @@ static int svd_topk_enqueue(blp_svd* h, const int32_t* d_users, int64_t n_users,
                             const int32_t* d_exc, int topk, int32_t* d_oc, double* d_os) {
   BLP_HIP(hipSetDevice(h->device));
   // chunks: enough blocks to fill the chip, >= 16 tiles each
-  // default: one 16-user tile per wave, 4 waves per block. Measured alternatives (config 4):
-  // BLP_SVD_RT=2 (two tiles per wave, 2 waves per block, same LDS: 1 wave per SIMD) 15.4 ms
-  // against 10.0 ms; two accumulation chains per tile (halving the dependent MFMA chain)
-  // 10.2 ms
-  const char* rt_env = getenv("BLP_SVD_RT");
-  const int rt = rt_env && atoi(rt_env) == 2 ? 2 : 1;
-  const int waves = rt == 1 ? TK_WAVES : TK_WAVES / 2;
-  const int64_t upb = 16 * rt * waves;  // users per block
+  // one 16-user tile per wave, 4 waves per block. Measured alternatives (config 4): two tiles
+  // per wave (2 waves per block, same LDS: 1 wave per SIMD) 15.4 ms against 10.0 ms; two
+  // accumulation chains per tile (halving the dependent MFMA chain) 10.2 ms
+  const int waves = TK_WAVES;
+  const int64_t upb = 16 * waves;  // users per block
   const int64_t ublocks = (n_users + upb - 1) / upb;
   // Column chunks: just enough (user block, chunk) blocks to occupy every block slot of the
   // chip ONCE. Each chunk restarts its users' top-k lists from an empty threshold, and the
   // insertions a list takes grow as C k (1 + ln(N / (C k))) over C chunks (config 4: 14
   // chunks 10.0 ms, 3 chunks 7.2 ms), so more chunks than slots only cost.
   const void* kfn = nullptr;
-#define BLP_SVD_FN(KP) \
-  kfn = rt == 1 ? (const void*)&k_svd_topk<KP, 1, TK_WAVES> : (const void*)&k_svd_topk<KP, 2, TK_WAVES / 2>;
+#define BLP_SVD_FN(KP) kfn = (const void*)&k_svd_topk<KP, 1, TK_WAVES>;
   switch (h->kpad) {
     case 16: BLP_SVD_FN(16); break;
     case 32: BLP_SVD_FN(32); break;
@@ -753,8 +749,7 @@ static int svd_topk_enqueue(blp_svd* h, const int32_t* d_users, int64_t n_users,
     default: BLP_SVD_FN(128); break;
   }
 #undef BLP_SVD_FN
-  const bool prune = h->prune && !getenv("BLP_SVD_EXP");
-  if (prune) {
+  if (h->prune) {
     int rc0 = svd_prune_prepare(h);
     if (rc0) return rc0;
     return svd_topk_pruned(h, d_users, n_users, d_exo, d_exc, topk, d_oc, d_os);
@@ -762,7 +757,6 @@ static int svd_topk_enqueue(blp_svd* h, const int32_t* d_users, int64_t n_users,
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, waves * 64, 0) != hipSuccess || per_cu < 1) per_cu = 1;
   int n_chunks = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)h->n_cu * per_cu / ublocks, h->ncol_pad / 256));
-  if (const char* e = getenv("BLP_SVD_CHUNKS")) n_chunks = std::max(1, std::min(atoi(e), (int)std::max<int64_t>(1, h->ncol_pad / 256)));
   const int64_t chunk = ((h->n_cols + n_chunks - 1) / n_chunks + 15) / 16 * 16;
   n_chunks = (int)((h->n_cols + chunk - 1) / chunk);
   {
@@ -777,13 +771,7 @@ static int svd_topk_enqueue(blp_svd* h, const int32_t* d_users, int64_t n_users,
   int rc = timer_begin(h->t_topk, h->stream, &t0);
   if (rc) return rc;
   const dim3 grid((unsigned)ublocks, (unsigned)n_chunks), block(waves * 64);
-#define BLP_SVD_TOPK(KP)                                                                        \
-  if (getenv("BLP_SVD_EXP"))                                                                    \
-    hipLaunchKernelGGL((k_svd_topk<KP, 1, TK_WAVES, 1>), grid, block, 0, h->stream, a);         \
-  else if (rt == 1)                                                                             \
-    hipLaunchKernelGGL((k_svd_topk<KP, 1, TK_WAVES>), grid, block, 0, h->stream, a);            \
-  else                                                                                          \
-    hipLaunchKernelGGL((k_svd_topk<KP, 2, TK_WAVES / 2>), grid, block, 0, h->stream, a);
+#define BLP_SVD_TOPK(KP) hipLaunchKernelGGL((k_svd_topk<KP, 1, TK_WAVES>), grid, block, 0, h->stream, a);
   switch (h->kpad) {
     case 16: BLP_SVD_TOPK(16); break;
     case 32: BLP_SVD_TOPK(32); break;

@@ -198,21 +198,20 @@ int build_wedge_index(blp_graph* g) {
       if (wp[x + 1] > wp[x])
         for (int64_t k0 = rp[x]; k0 < rp[x + 1]; k0 += WF_ITEM)
           items.push_back(WedgeItem{k0, (int32_t)x, (int32_t)std::min<int64_t>(WF_ITEM, rp[x + 1] - k0)});
-    WedgeItem* d_items = nullptr;
-    unsigned long long* d_cursor = nullptr;
-    BLP_HIP(hipMalloc(&d_items, sizeof(WedgeItem) * std::max<size_t>(items.size(), 1)));
-    BLP_HIP(hipMalloc(&d_cursor, 8 * (size_t)n));
-    BLP_HIP(hipMemcpy(d_items, items.data(), sizeof(WedgeItem) * items.size(), hipMemcpyHostToDevice));
-    BLP_HIP(hipMemsetAsync(d_cursor, 0, 8 * (size_t)n, g->stream));
+    ScopedBuf d_items, d_cursor;  // freed on every return
+    int rc;
+    if ((rc = d_items.reserve(sizeof(WedgeItem) * std::max<size_t>(items.size(), 1))) ||
+        (rc = d_cursor.reserve(8 * (size_t)n)))
+      return rc;
+    BLP_HIP(hipMemcpy(d_items.p, items.data(), sizeof(WedgeItem) * items.size(), hipMemcpyHostToDevice));
+    BLP_HIP(hipMemsetAsync(d_cursor.p, 0, 8 * (size_t)n, g->stream));
     hipLaunchKernelGGL(k_wedge_fill_items, dim3((unsigned)std::min<size_t>(65536, std::max<size_t>(items.size(), 1))),
-                       dim3(WF_BLOCK), 0, g->stream, g->d_rp, g->d_ci, g->d_wp, d_items, (int64_t)items.size(), d_cursor,
-                       g->d_wedge);
+                       dim3(WF_BLOCK), 0, g->stream, g->d_rp, g->d_ci, g->d_wp, d_items.as<WedgeItem>(),
+                       (int64_t)items.size(), d_cursor.as<unsigned long long>(), g->d_wedge);
     hipLaunchKernelGGL(k_wedge_pad, dim3((unsigned)std::min<int64_t>(8192, (n + 255) / 256)), dim3(256), 0, g->stream,
-                       g->d_wp, d_cursor, n, g->d_wedge);
+                       g->d_wp, d_cursor.as<unsigned long long>(), n, g->d_wedge);
     BLP_HIP(hipGetLastError());
     BLP_HIP(hipStreamSynchronize(g->stream));
-    (void)hipFree(d_items);
-    (void)hipFree(d_cursor);
   }
   BLP_HIP(hipGetLastError());
   BLP_HIP(hipStreamSynchronize(g->stream));

@@ -110,7 +110,13 @@ int blp_graph_create_from_csr(blp_csr* c, const int64_t* row_ptr, const int32_t*
  *   it to blp_csr_fetch / blp_graph_create_from_csr. *bytes_in (may be NULL): bytes received
  *   from the other ranks. Collective: every rank must call it.
  * blp_multi_allreduce: *v = the sum (BLP_MULTI_SUM) or max (BLP_MULTI_MAX) of every rank's *v,
- *   e.g. the max-over-ranks step time. Collective.                                           */
+ *   e.g. the max-over-ranks step time. Collective.
+ * blp_multi_compact_csr: the post-gather half of blp_multi_gather_csr on its own (not collective):
+ *   recv (host or device) is an all-gather receive buffer of `world` slots, slot r = rank r's a
+ *   ids then its b ids, each half padded to m_max = max(counts); counts[world] (host) are the
+ *   valid prefixes. They are copied back to back on `device` (padding never read) and the
+ *   union's CSR is built in HBM; *bytes_in (may be NULL) = 8 * m_max * (world - 1), what each
+ *   rank received. For hosts that run the collective themselves, and for tests.              */
 #define BLP_MULTI_ID_BYTES 128
 #define BLP_MULTI_SUM 0
 #define BLP_MULTI_MAX 1
@@ -121,6 +127,8 @@ int blp_multi_info(const blp_multi* m, int* world, int* rank, int* device);
 int blp_multi_gather_csr(blp_multi* m, const int32_t* a, const int32_t* b, int64_t m_r, int64_t n_nodes,
                          blp_csr** out, int64_t* bytes_in);
 int blp_multi_allreduce(blp_multi* m, double* v, int op);
+int blp_multi_compact_csr(int device, const int32_t* recv, const int64_t* counts, int world, int64_t n_nodes,
+                          blp_csr** out, int64_t* bytes_in);
 int blp_multi_destroy(blp_multi* m);
 
 /* blp_edges_parse: SNAP LoadEdgeList's text format (similarity.py:16): one edge per line,

@@ -465,3 +465,64 @@ def test_multi_capi_two_ranks(gpu, tmp_path):
     max / sum all-reduces agree, and each rank's scores equal the oracle. On a one-GPU box
     both ranks share device 0, which RCCL refuses (ncclInvalidUsage): then skipped."""
     _run_capi(2, tmp_path, False)
+
+
+@pytest.mark.parametrize("device_recv", [False, True])
+def test_multi_compact_three_ranks(gpu, device_recv):
+    """The post-gather compaction of the C-ABI exchange (blp_multi_compact_csr, the code
+    blp_multi_gather_csr runs after its all-gather) at world 3 on one GPU: an all-gather
+    receive buffer with uneven counts and a zero-count rank, its padding poisoned with
+    out-of-range ids (read, they would fail the CSR build), host or device memory. The CSR
+    equals the host CSR of the union, bytes_in = 8 * m_max * (world - 1), and the scores on it
+    equal the oracle (similarity.py:20-61 over the union graph, similarity.py:16)."""
+    from blp.multi import Multi
+
+    rng = np.random.default_rng(5)
+    n_users, n_bus = 40000, 3000
+    blocks = [0, 15000, 15000, n_users]  # rank 1 owns no users: a zero-count partial
+    parts = []
+    for r in range(3):
+        lo, hi = blocks[r], blocks[r + 1]
+        k = {0: 90000, 1: 0, 2: 170000}[r]
+        u = rng.integers(lo, max(hi, lo + 1), k)
+        b = n_users + np.minimum((rng.pareto(1.2, k) * 40).astype(np.int64), n_bus - 1)
+        parts.append((u.astype(np.int32), b.astype(np.int32)))
+    counts = np.array([len(p[0]) for p in parts], np.int64)
+    m_max = int(counts.max())
+    recv = np.full((3, 2, m_max), 0x7FFFFFF0, np.int32)  # padding: ids far outside [0, n)
+    for r, (u, b) in enumerate(parts):
+        recv[r, 0, : len(u)] = u
+        recv[r, 1, : len(b)] = b
+    n = n_users + n_bus
+    if device_recv:
+        import torch
+
+        t = torch.from_numpy(recv).cuda()
+        c, bytes_in = Multi.compact_csr(t.data_ptr(), counts, n, device=gpu)
+    else:
+        c, bytes_in = Multi.compact_csr(recv, counts, n, device=gpu)
+    assert bytes_in == 8 * m_max * 2
+    G = blp.DeviceGraph.from_csr_handle(c, n, n_users, gpu)
+    ua = np.concatenate([p[0] for p in parts])
+    ub = np.concatenate([p[1] for p in parts])
+    rp, ci, _ = _host_csr(n, ua, ub)
+    assert np.array_equal(G.row_ptr, rp) and np.array_equal(G.col_idx, ci)
+    ids, oa, ob = dense_edges(ua, ub)
+    og = coracle.OracleGraph(len(ids), oa, ob)
+    src = rng.choice(np.unique(ua), 60, replace=False)
+    x = np.repeat(src, 25).astype(np.int32)
+    y = rng.choice(np.unique(ub), len(x)).astype(np.int32)
+    for xs, ys in ((x, y), (y, x)):
+        got = G.score_pairs(xs, ys, 7)
+        cn, jac, aa, _ = og.score_pairs(np.searchsorted(ids, xs), np.searchsorted(ids, ys), 7)
+        np.testing.assert_array_equal(got["cn"], cn)
+        np.testing.assert_array_equal(got["jaccard"], jac)
+        np.testing.assert_array_equal(got["adamic"], aa)
+    G.close()
+
+
+def test_multi_compact_rejects_bad_counts(gpu):
+    from blp.multi import Multi
+
+    with pytest.raises(RuntimeError):
+        Multi.compact_csr(np.zeros(8, np.int32), np.array([2, -1], np.int64), 10, device=gpu)

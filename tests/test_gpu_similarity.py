@@ -67,15 +67,15 @@ def _check_against_oracle(ga, gb, x, y, mask=7):
     return G
 
 
-@pytest.mark.parametrize("wave", [False, True])
+@pytest.mark.parametrize("no_runs", [False, True])
 @pytest.mark.parametrize("n_users,n_bus,n_draws,seed", [
-    (2000, 300, 20000, 0),     # small universe: wave kernel (or SMALL block variant)
-    (30000, 2000, 150000, 1),  # wave kernel (or MED block variant)
+    (2000, 300, 20000, 0),     # small universe: SMALL block variant / short-row scorer
+    (30000, 2000, 150000, 1),  # MED block variant
     (300000, 5000, 600000, 2), # LARGE block variant, long rows (popular businesses)
 ])
-def test_user_and_business_side_vs_oracle(gpu, n_users, n_bus, n_draws, seed, wave, monkeypatch):
-    if wave:
-        monkeypatch.setenv("BLP_WAVE", "1")  # opt-in wave-per-source scorer
+def test_user_and_business_side_vs_oracle(gpu, n_users, n_bus, n_draws, seed, no_runs, monkeypatch):
+    if no_runs:
+        monkeypatch.setenv("BLP_NO_RUNS", "1")  # bucket-sort grouping even for source-grouped lists
     rng = np.random.default_rng(seed)
     a, b = bipartite_edges(rng, n_users, n_bus, n_draws)
     G = blp.DeviceGraph(a, b)
@@ -112,8 +112,6 @@ def test_general_graph_exact_distance(gpu):
     {"BLP_SPLIT": "3", "BLP_SPLIT_BIG": "1", "BLP_NO_HASH": "1"},           # ... 128 KiB chunks, one workgroup per CU
     {"BLP_SPLIT": "3", "BLP_SPLIT_BIG": "1", "BLP_SPLIT_SHORT": "0", "BLP_NO_HASH": "1"},  # ... no thread-per-slice short path
     {"BLP_SPLIT": "2", "BLP_SPLIT_BIG": "1", "BLP_SPLIT_SHORT": "4", "BLP_NO_HASH": "1"},  # ... short path only below 5 ids
-    {"BLP_SPLIT": "3", "BLP_SPLIT_BIG": "1", "BLP_SPLIT_ONEQ": "1", "BLP_NO_HASH": "1"},   # ... one item queue (no XCD groups)
-    {"BLP_SPLIT": "3", "BLP_SPLIT_BIG": "1", "BLP_SPLIT_ONEQ": "2", "BLP_NO_HASH": "1"},   # ... one queue, chunk-major
     {"BLP_SPLIT": "24", "BLP_SPLIT_BIG": "1", "BLP_NO_HASH": "1"},          # ... same, many chunks
     {"BLP_SPLIT": "3", "BLP_SPLIT_BIG": "1", "BLP_NO_HASH": "1", "BLP_NO_WEDGE": "1"},  # ... members' rows from the CSR, not wedge rows
     {"BLP_SPLIT": "3", "BLP_SPLIT_BIG": "1", "BLP_HASH_WORK": "600", "BLP_NO_WEDGE": "1"},  # hash-set build from the CSR
@@ -126,13 +124,9 @@ def test_general_graph_exact_distance(gpu):
     {"BLP_HOT_MIN": "8", "BLP_CHUNK_BITS": "1024", "BLP_NO_GLOBAL": "1"},  # dense rows across chunks
     {"BLP_HOT_MIN": "8", "BLP_HEAVY_WORK": "50"},
     {"BLP_HOT_MIN": "1", "BLP_HOT_DENSITY": "100000000"},  # > HOT_LIST dense rows: sparse fallback
-    {"BLP_WAVE": "1"},                                  # wave-per-source scorer (opt-in)
-    {"BLP_WAVE": "1", "BLP_HEAVY_WORK": "50", "BLP_HOT_MIN": "8"},
     {"BLP_VARIANT": "1"},                               # 64 KiB-bitmap scorer (no hint table)
     {"BLP_VARIANT": "2"},                               # 136 KiB-bitmap scorer (row-chunk loops)
     {"BLP_VARIANT": "2", "BLP_NO_SHORT": "1"},          # ... short rows through the row-chunk loops
-    {"BLP_VARIANT": "2", "BLP_KPT": "4"},               # ... 4-id chunks
-    {"BLP_VARIANT": "2", "BLP_KPT": "16"},              # ... 16-id chunks
     {"BLP_VARIANT": "2", "BLP_WCODES": "3"},            # ... coded and gathered weights mixed
     {"BLP_VARIANT": "2", "BLP_HOT_MIN": "8"},           # ... dense rows skipped: empty build rows
     {"BLP_VARIANT": "2", "BLP_CHUNK_BITS": "1024", "BLP_NO_GLOBAL": "1"},  # ... several LDS chunks
@@ -142,7 +136,6 @@ def test_general_graph_exact_distance(gpu):
     {"BLP_NO_WCODES": "1"},                             # scorers on the plain id stream
     {"BLP_WCODES": "3", "BLP_SPLIT": "3"},
     {"BLP_WCODES": "3", "BLP_FORCE_GLOBAL": "1"},
-    {"BLP_WCODES": "3", "BLP_WAVE": "1"},
     {"BLP_WCODES": "3", "BLP_HEAVY_WORK": "50", "BLP_HOT_MIN": "8"},
     {"BLP_NO_WEDGE": "1"},                              # short-row build from CSR, not wedge rows
     {"BLP_NO_WEDGE": "1", "BLP_HEAVY_WORK": "50"},      # ... heavy items as CSR ranges
@@ -372,3 +365,39 @@ def test_adamic_scale_and_weight_range(gpu):
         h = ctypes.c_void_p()
         rc = lib().blp_graph_create(ptr(G.row_ptr), ptr(G.col_idx), G.n, ptr(w), 0, ctypes.byref(h))
         assert rc == -1 and "aa_weight" in lib().blp_last_error().decode()  # BLP_E_ARG
+
+
+def test_concurrent_short_row_batches_share_wedge_bitmaps(gpu):
+    """similarity.main creates its user and business batches on two host threads at once
+    (similarity._score_both_ids). On a graph where every row is short, BOTH batches take the
+    short-row scorer and ask the graph for its wedge-row bitmaps over their own universe, so
+    the graph's bitmap cache is built from two threads concurrently (blp::wedge_bitmaps holds
+    the graph's lock across lookup-or-build). Repeated on fresh graphs; every batch's scores
+    must equal the oracle (similarity.py:20-106)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    rng = np.random.default_rng(11)
+    seen_wbm = 0
+    for rep in range(6):
+        n_users, n_bus = 300, 200  # ~10 reviews per user, ~15 members per business: every row short
+        u, b = bipartite_edges(rng, n_users, n_bus, 3000, zipf=0.0)
+        G = blp.DeviceGraph(u, b, device=gpu)
+        nu = G.n_col0
+        x = rng.integers(0, nu, 6000).astype(np.int32)
+        y = rng.integers(nu, G.n, len(x)).astype(np.int32)
+        with ThreadPoolExecutor(2) as ex:
+            fu = ex.submit(G.batch, x, y)
+            fb = ex.submit(G.batch, y, x)
+            ub, bb = fu.result(), fb.result()
+        seen_wbm += sum(bt.plan().get("wedge_bitmaps", 0) for bt in (ub, bb))
+        G.score_batches([(ub, 7), (bb, 7)])
+        ids, oa, ob = dense_edges(u, b)
+        og = coracle.OracleGraph(len(ids), oa, ob)
+        for bt, xs, ys in ((ub, x, y), (bb, y, x)):
+            got = bt.fetch(7)
+            cn, jac, aa, _ = og.score_pairs(np.searchsorted(ids, G.node_ids[xs]), np.searchsorted(ids, G.node_ids[ys]), 7)
+            np.testing.assert_array_equal(got["cn"], cn)
+            np.testing.assert_array_equal(got["jaccard"], jac)
+            np.testing.assert_array_equal(got["adamic"], aa)
+        G.close()
+    assert seen_wbm > 0  # the bitmaps were actually in play
