@@ -23,6 +23,7 @@
 //              K elements maps an element to its row. Short and very long rows cost the same.
 // Adamic-Adar sums are exact (two-word integer sums of w * 2^58, any order; blp_internal.h).
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <numeric>
 #include <thread>
@@ -75,7 +76,9 @@ struct Misc {
 //   3 pair range [pbeg, pbeg + pcnt) <= np    4 output index < np
 //   5 long-slice queue slot < SPLIT_LQ        6 long-slice queue region < the allocated workgroups
 //   7 split-table row < its rows              8 hash-set probes < HT (a full table would spin)
-//   9 chunk width <= the bitmap's bits
+//   9 chunk width <= the bitmap's bits      10 a row read [st, st + len) <= nnz (+ padding)
+//  11 wedge-row vectors [wb, we) <= wedge    12 dense row number < n_hot
+//  13 dense-row pool vector < pool vectors
 #ifdef BLP_DEBUG
 __device__ inline bool ps_ok(Misc* m, bool ok, int site, long long v, long long bound) {
   if (!ok && atomicAdd(reinterpret_cast<unsigned long long*>(&m->dbg[0]), 1ull) == 0ull) {
@@ -1603,6 +1606,8 @@ struct ScoreArgs {
   int4* lq;                     // k_score_split: long-slice queues, SPLIT_LQ entries per workgroup
   int64_t np, n_nodes;          // pairs and nodes (BLP_DEBUG bounds)
   int64_t rs_rows;              // rows of the split table (BLP_DEBUG bound)
+  int64_t nnz, wedge_vecs;      // CSR entries, wedge-row vectors (BLP_DEBUG bounds)
+  int64_t n_hot, hot_vecs;      // dense rows, their pool's vectors (BLP_DEBUG bounds)
   int lq_wgs;                   // workgroups d_lq was sized for (BLP_DEBUG bound)
 };
 
@@ -1769,7 +1774,7 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
             if (a.hot_idx) {
               for (int64_t k = xb + threadIdx.x; k < xe; k += BLOCK) {
                 const int hi = a.hot_idx[a.ci[k]];
-                if (hi >= 0) {
+                if (hi >= 0 && PS_OK(a.misc, hi < a.n_hot, 12, hi, a.n_hot)) {
                   const int slot = atomicAdd(&s_nhot, 1);
                   if (slot < HOT_LIST) s_hot[slot] = a.hot_tab[hi];
                 }
@@ -2216,7 +2221,8 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
     const int64_t width = max<int64_t>(min(a.hi, c0 + CAP_BITS) - c0, 0);
     if (!PS_OK(a.misc, width <= 32ll * CAP_WORDS, 9, width, 32ll * CAP_WORDS)) continue;
     const int nw4 = (int)((((width + 31) >> 5) + 3) >> 2);
-    const int64_t wb = a.wp ? a.wp[x] : 0, we = a.wp ? a.wp[x + 1] : 0;
+    int64_t wb = a.wp ? a.wp[x] : 0, we = a.wp ? a.wp[x + 1] : 0;
+    if (!PS_OK(a.misc, wb >= 0 && wb <= we && we <= a.wedge_vecs, 11, we, a.wedge_vecs)) wb = we = 0;
     if (hslot >= 0) {
       const uint4* src4 = reinterpret_cast<const uint4*>(a.heavy_bm + (int64_t)hslot * a.hb_words + ((c0 - a.lo) >> 5));
       for (int i = threadIdx.x; i < nw4; i += BLOCK) bm4[i] = src4[i];
@@ -2245,7 +2251,7 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
       if (a.hot_idx) {
         for (int64_t k = xb + threadIdx.x; k < xe; k += BLOCK) {
           const int hi = a.hot_idx[a.ci[k]];
-          if (hi >= 0) {
+          if (hi >= 0 && PS_OK(a.misc, hi < a.n_hot, 12, hi, a.n_hot)) {
             const int slot = atomicAdd(&s_nhot, 1);
             if (slot < HOT_LIST) s_hot[slot] = a.hot_tab[hi];
           }
@@ -2258,7 +2264,8 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
         uint4 v = make_uint4(0, 0, 0, 0);
         for (int r = 0; r < nhot; ++r) {
           const int64_t qq = q0 + q - s_hot[r].vlo;
-          if (qq >= 0 && qq < s_hot[r].nvec) {
+          if (qq >= 0 && qq < s_hot[r].nvec &&
+              PS_OK(a.misc, s_hot[r].vec_off + qq < a.hot_vecs, 13, s_hot[r].vec_off + qq, a.hot_vecs)) {
             const uint4 pv = a.hot_pool[s_hot[r].vec_off + qq];
             v.x |= pv.x;
             v.y |= pv.y;
@@ -2278,6 +2285,9 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
             const int32_t* sp = rsplit + ((int64_t)z - rs_lo) * (C + 1) + c;
             s_start[threadIdx.x] = a.rp[z] + sp[0];
             len = (nhot && a.hot_idx[z] >= 0) ? 0 : sp[1] - sp[0];  // dense rows were OR-ed in
+            if (!PS_OK(a.misc, sp[0] >= 0 && len >= 0 && s_start[threadIdx.x] + len <= a.nnz, 10,
+                       s_start[threadIdx.x] + len, a.nnz))
+              len = 0;
           } else {
             s_start[threadIdx.x] = 0;
           }
@@ -2373,6 +2383,7 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
             const int s0 = sp[0];
             len = sp[1] - s0;
             st = a.g_yb[gp] + s0;
+            if (!PS_OK(a.misc, s0 >= 0 && len >= 0 && st + len <= a.nnz, 10, st + len, a.nnz)) len = 0;
           }
         }
         if (len > 0 && len <= short_max) {
@@ -2575,7 +2586,8 @@ __global__ __launch_bounds__(BLOCK) void k_score_hash(ScoreArgs a) {
     const int x = a.active[si];
     if (!PS_OK(a.misc, x >= 0 && x < a.n_nodes, 2, x, a.n_nodes)) continue;  // uniform
     const int64_t xb = a.rp[x], xe = a.rp[x + 1];
-    const int64_t wb = a.wp ? a.wp[x] : 0, we = a.wp ? a.wp[x + 1] : 0;
+    int64_t wb = a.wp ? a.wp[x] : 0, we = a.wp ? a.wp[x + 1] : 0;
+    if (!PS_OK(a.misc, wb >= 0 && wb <= we && we <= a.wedge_vecs, 11, we, a.wedge_vecs)) wb = we = 0;
     const int pbeg = a.off[x], pcnt = a.cnt[x];
     if (!PS_OK(a.misc, pbeg >= 0 && (int64_t)pbeg + pcnt <= a.np, 3, (int64_t)pbeg + pcnt, a.np)) continue;
     int64_t st0 = 0;
@@ -2623,7 +2635,8 @@ __global__ __launch_bounds__(BLOCK) void k_score_hash(ScoreArgs a) {
       for (int64_t k = xb + threadIdx.x; k < xe; k += BLOCK) {
         const int z = a.ci[k];
         const int64_t st = a.rp[z];
-        const int len = (int)(a.rp[z + 1] - st);
+        int len = (int)(a.rp[z + 1] - st);
+        if (!PS_OK(a.misc, st >= 0 && len >= 0 && st + len <= a.nnz, 10, st + len, a.nnz)) len = 0;
         for (int h0 = 0; h0 < len; h0 += SHORT_PART) {
           int e[SHORT_PART];
           row_part(a.cw, st, len, h0, e);
@@ -2656,7 +2669,8 @@ __global__ __launch_bounds__(BLOCK) void k_score_hash(ScoreArgs a) {
       const int gp = pbeg + t;
       const bool first = t == (int)threadIdx.x;
       const int64_t st = first ? st0 : a.g_yb[gp];
-      const int len = first ? len0 : a.g_yl[gp];
+      int len = first ? len0 : a.g_yl[gp];
+      if (!PS_OK(a.misc, st >= 0 && len >= 0 && st + len <= a.nnz, 10, st + len, a.nnz)) len = 0;
       const int p = first ? p0 : a.g_out[gp];
       if (!PS_OK(a.misc, p >= 0 && p < a.np, 4, p, a.np)) continue;
       unsigned c = 0;
@@ -2925,6 +2939,16 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
     for (int t = 1; t < nt; ++t) acc[0].merge(acc[t]);
     return acc[0];
   };
+  // BLP_CREATE_PROF=1: the planning stages' wall times on stderr (the e2e score phase)
+  const bool cprof = getenv("BLP_CREATE_PROF") != nullptr;
+  auto ct0 = std::chrono::steady_clock::now();
+  auto stage = [&](const char* what) {
+    if (!cprof) return;
+    const auto t = std::chrono::steady_clock::now();
+    fprintf(stderr, "[blp_batch_create %lld pairs] %-10s %.2f ms\n", (long long)n_pairs, what,
+            std::chrono::duration<double, std::milli>(t - ct0).count());
+    ct0 = t;
+  };
   Acc A = parallel(n_pairs, 1 << 18, [&](Acc& a, int64_t i0, int64_t i1) {
     for (int64_t i = i0; i < i1; ++i) {
       const int32_t xi = x[i], yi = y[i];
@@ -2939,6 +2963,7 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
     }
   });
   if (A.bad) return fail(BLP_E_ARG, "blp_batch_create: node id out of range");
+  stage("pairs");
   std::vector<uint8_t> seen((size_t)n, 0);
   std::vector<int32_t> srcs;  // in order of first appearance
   for (int64_t i = 0; i < n_pairs; ++i)
@@ -2946,6 +2971,7 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
       seen[x[i]] = 1;
       srcs.push_back(x[i]);
     }
+  stage("sources");
   std::vector<int64_t> work(srcs.size());
   A.merge(parallel((int64_t)srcs.size(), 1 << 12, [&](Acc& a, int64_t s0, int64_t s1) {
     for (int64_t s = s0; s < s1; ++s) {
@@ -2961,6 +2987,7 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
       work[s] = wsum;
     }
   }));
+  stage("work");
   int64_t lo = A.lo, hi = A.hi;
   const int64_t scan_work = A.scan, max_scan_row = A.max_scan, max_build_row = A.max_build;
   const bool any_hot = A.any_hot;
@@ -3040,6 +3067,7 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   // unless there are very many light sources per worker
   // (two once a worker has ~64+ sources: the business side of config 2, 1.44 -> 1.30 ms)
   b->dq = b->n_sources >= n_wg * 64 ? (int)std::max<int64_t>(2, std::min<int64_t>(DQ_MAX, b->n_sources / (n_wg * 64))) : 1;
+  stage("stream");
   // ---- heavy sources: build work far above the per-workgroup share goes to k_heavy
   const int64_t total_work = std::accumulate(work.begin(), work.end(), (int64_t)0) + scan_work;
   b->work_elems = total_work;
@@ -3075,6 +3103,7 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   }
   b->n_heavy_items = (int64_t)items.size();
   b->hb_words = ((span + 31) / 32 + 3) / 4 * 4;
+  stage("heavy");
   // ---- the graph's wedge-row bitmaps (hop3.hip) over this universe: a source whose wedge row is
   // at least as long as its bitmap's words copies the bitmap (its id set, 12.5 KB at config 2)
   // instead of OR-ing the row id by id -- the same slots and copy as k_heavy's pre-built bitmaps,
@@ -3097,6 +3126,7 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
       }
     }
   }
+  stage("wbm");
   // ---- grouping geometry: buckets of 2^shift node ids, at most NB_MAX buckets
   {
     // buckets cover the sources' id range [xlo, xhi): ~2K buckets of 2^shift ids each
@@ -3178,6 +3208,7 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
     if (hipMalloc(&b->d_gbm, 4 * (size_t)b->gwords * b->gslots) != hipSuccess)
       return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: HBM bitmap slots"));
   }
+  stage("split");
   // ---- device buffers
   const size_t np = (size_t)std::max<int64_t>(n_pairs, 1);
   if (hipMalloc(&b->d_x, 4 * np) != hipSuccess || hipMalloc(&b->d_y, 4 * np) != hipSuccess ||
@@ -3209,6 +3240,7 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
             hipSuccess)
       return bail(fail(BLP_E_HIP_BASE, "blp_batch_create: upload failed"));
   }
+  stage("buffers");
   *out = b;
   return BLP_OK;
 }
@@ -3412,7 +3444,7 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
       rc = launch_heavy<BLOCK_LARGE, CAP_LARGE, SEG_LARGE>(b->stream, h, b->n_heavy_items);
     if (rc) return rc;
   }
-  ScoreArgs a;
+  ScoreArgs a{};  // value-initialised: a field a path does not set is null / zero, never stale
   a.wp = nullptr;
   a.wedge = nullptr;
   a.rp = g->d_rp;
@@ -3451,12 +3483,18 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   a.np = np;
   a.n_nodes = g->n;
   a.rs_rows = b->rs_rows;
+  a.nnz = g->nnz;
+  a.wedge_vecs = g->wedge_vecs;
+  a.n_hot = g->n_hot;
+  a.hot_vecs = g->hot_pool_words / 4;
   a.lq_wgs = b->d_lq ? 2 * g->n_cu : 0;
   if (np && b->split) {
     // AA counts ride in the packed per-pair word while every row (hence every count) < 2^24
     const int pk24 = (mask & BLP_ADAMIC) && g->max_row < (int64_t(1) << SPLIT_CN_BITS) && !b->kn.split_nopk;
     // slices of <= short_max ids scanned by their pair's thread (128 KiB chunks; BLP_SPLIT_SHORT=0: off)
     const int short_max = std::min(SHORT_PART, b->kn.split_short >= 0 ? b->kn.split_short : SHORT_PART);
+    a.lq = b->d_lq;  // k_score_split's long-slice queues (SPLIT_LQ entries per resident workgroup)
+    BLP_CHECK(a.lq, BLP_E_STATE, "blp_batch_score: split batch without its long-slice queues");
     if (g->d_wp && !b->kn.no_wedge) {  // sources with wedge rows build from them (split and hash kernels)
       a.wp = g->d_wp;
       a.wedge = reinterpret_cast<const uint4*>(g->d_wedge);
