@@ -143,6 +143,11 @@ struct blp_graph {
   int32_t* d_wedge = nullptr;
   int64_t wedge_vecs = 0;
   std::vector<int64_t> h_wp;  // host copy of d_wp (heavy-source planning)
+  // per-node two-hop statistics over N(x) (node2.hip, built on the device): sum of |N(z)|, the id
+  // range of N(N(x)) ([lo2, hi2), lo2 = INT32_MAX when empty), max |N(z)|, bit 0: some z is dense
+  std::vector<unsigned long long> h_w2;
+  std::vector<int32_t> h_lo2, h_hi2, h_maxd;
+  std::vector<uint8_t> h_flag2;
   // wedge-row bitmaps (hop3.hip, blp::wedge_bitmaps): the SET of ids of each long wedge row over
   // an id range [lo, hi), built on first use per range (the hop-3 mark range; the business
   // batch's universe) and kept with the graph (at most 4 ranges)
@@ -174,6 +179,7 @@ constexpr int SHORT_ROW_MAX = 32;  // the short-row scorer's row bound (pairs.hi
 int build_hot_index(blp_graph* g);
 int graph_finish(blp_graph* g, const double* aaw);
 int build_wedge_index(blp_graph* g);
+int build_node2(blp_graph* g);  // after build_hot_index (the dense-row flag)
 // the graph's wedge-row bitmaps over [lo, hi) (built and cached on first use); null with *rc == 0
 // when there is no wedge index or no cache slot left
 const WedgeBitmaps* wedge_bitmaps(blp_graph* g, int64_t lo, int64_t hi, int* rc);

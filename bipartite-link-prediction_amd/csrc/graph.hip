@@ -215,6 +215,7 @@ int graph_finish(blp_graph* g, const double* aaw) {
   }
   int rc = build_hot_index(g);
   if (rc != BLP_OK) return rc;
+  if ((rc = build_node2(g)) != BLP_OK) return rc;
   return build_wedge_index(g);
 }
 

@@ -2973,9 +2973,28 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
     }
   stage("sources");
   std::vector<int64_t> work(srcs.size());
-  A.merge(parallel((int64_t)srcs.size(), 1 << 12, [&](Acc& a, int64_t s0, int64_t s1) {
+  // per source: the graph's two-hop statistics (node2.hip, computed on the device at graph
+  // creation) instead of a walk over N(x) -- the rows N(z) it reads, their id range, the longest
+  const bool have2 = (int64_t)g->h_w2.size() == n;
+  A.merge(parallel((int64_t)srcs.size(), 1 << 14, [&](Acc& a, int64_t s0, int64_t s1) {
     for (int64_t s = s0; s < s1; ++s) {
       const int32_t xi = srcs[s];
+      if (rp[xi + 1] == rp[xi]) {
+        work[s] = 0;
+        continue;
+      }
+      if (have2) {
+        work[s] = (int64_t)g->h_w2[xi];
+        a.max_build = std::max<int64_t>(a.max_build, g->h_maxd[xi]);
+        a.any_hot |= (g->h_flag2[xi] & 1) != 0;
+        if (g->h_lo2[xi] != INT32_MAX) {
+          a.lo = std::min<int64_t>(a.lo, g->h_lo2[xi]);
+          a.hi = std::max<int64_t>(a.hi, g->h_hi2[xi]);
+        }
+        a.rows_lo = std::min<int64_t>(a.rows_lo, ci[rp[xi]]);  // rows are sorted: N(x)'s first and last
+        a.rows_hi = std::max<int64_t>(a.rows_hi, (int64_t)ci[rp[xi + 1] - 1] + 1);
+        continue;
+      }
       int64_t wsum = 0;
       for (int64_t k = rp[xi]; k < rp[xi + 1]; ++k) {
         const int32_t z = ci[k];

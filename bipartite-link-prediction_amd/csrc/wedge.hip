@@ -132,7 +132,6 @@ int build_wedge_index(blp_graph* g) {
     if (atoi(e) == 0) return BLP_OK;
   const int64_t n = g->n;
   const int64_t* rp = g->hrp;
-  const int32_t* ci = g->hci;
   if (n == 0 || g->nnz == 0) return BLP_OK;
   // budget: BLP_WEDGE_MAX_X (16) x nnz ids, and at most 35 % of the free HBM
   double max_x = 16.0;
@@ -143,29 +142,11 @@ int build_wedge_index(blp_graph* g) {
   // members' rows up to BLP_WEDGE_ROW_MAX (64) ids: the short-row scorer's sources (rows <=
   // SHORT_ROW_MAX) always qualify; the chunk-parallel and hash-set scorers use any wedge row
   const int64_t row_max = std::max<int64_t>(SHORT_ROW_MAX, getenv("BLP_WEDGE_ROW_MAX") ? atoll(getenv("BLP_WEDGE_ROW_MAX")) : 64);
-  // per-node volume: one degree lookup per CSR entry, 16 threads (2B entries at config 5)
-  const int nt = (int)std::max<unsigned>(1, std::min<unsigned>(16, std::thread::hardware_concurrency()));
+  // per-node volume: the two-hop statistics of graph_finish (node2.hip, on the device): x holds a
+  // wedge row when every neighbour row is at most row_max ids, of sum |N(z)| ids
   std::vector<int64_t> wp((size_t)n + 1, 0);  // per-node vector counts, then offsets
-  {
-    std::vector<std::thread> th;
-    for (int t = 0; t < nt; ++t)
-      th.emplace_back([&, t]() {
-        for (int64_t x = t; x < n; x += nt) {
-          int64_t len = 0;
-          bool ok = true;
-          for (int64_t k = rp[x]; k < rp[x + 1]; ++k) {
-            const int64_t d = rp[ci[k] + 1] - rp[ci[k]];
-            if (d > row_max) {
-              ok = false;
-              break;
-            }
-            len += d;
-          }
-          wp[x] = ok ? (len + 3) / 4 : 0;
-        }
-      });
-    for (auto& t : th) t.join();
-  }
+  for (int64_t x = 0; x < n; ++x)
+    wp[x] = (rp[x + 1] > rp[x] && g->h_maxd[x] <= row_max) ? ((int64_t)g->h_w2[x] + 3) / 4 : 0;
   int64_t total = 0;
   for (int64_t x = 0; x < n; ++x) {
     const int64_t c = wp[x];

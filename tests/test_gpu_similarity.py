@@ -401,3 +401,75 @@ def test_concurrent_short_row_batches_share_wedge_bitmaps(gpu):
             np.testing.assert_array_equal(got["adamic"], aa)
         G.close()
     assert seen_wbm > 0  # the bitmaps were actually in play
+
+
+def test_node2_planning_with_empty_row_runs(gpu):
+    """The per-node two-hop statistics (node2.hip, computed on the device at graph creation) that
+    blp_batch_create plans from and the wedge index sizes with: a graph whose dense ids hold a
+    run of 200K isolated users between two populated blocks, so one CSR tile spans far more
+    rows than its LDS table (the direct-atomic path). The batch universe equals the host
+    computation over N(y) and N(N(x)), the wedge rows equal their host construction, and the
+    scores equal the oracle (similarity.py:20-106)."""
+    import ctypes
+
+    rng = np.random.default_rng(21)
+    n_users, n_bus = 300_000, 600
+    users = np.concatenate([rng.integers(0, 1000, 6000), rng.integers(200_000, 201_000, 6000)])
+    bus = n_users + (rng.pareto(1.0, len(users)) * 20).astype(np.int64) % n_bus
+    n = n_users + n_bus
+    A = np.ascontiguousarray(users, np.int32)
+    Bv = np.ascontiguousarray(bus, np.int32)
+    rp = np.zeros(n + 1, np.int64)
+    ci = np.empty(2 * len(A), np.int32)
+    sl = np.zeros(n, np.uint8)
+    nnz = ctypes.c_int64(0)
+    P = blp._lib.ptr
+    blp._lib.check(blp.lib().blp_csr_from_edges(n, len(A), P(A), P(Bv), P(rp), P(ci), P(sl), ctypes.byref(nnz)))
+    ci = ci[: nnz.value].copy()
+    G = blp.DeviceGraph.from_csr(rp, ci, sl, n_users, device=gpu)
+    present_u = np.flatnonzero(np.diff(rp)[:n_users] > 0)
+    x = np.repeat(rng.choice(present_u, 80, replace=False), 15).astype(np.int32)
+    y = rng.integers(n_users, n, len(x)).astype(np.int32)
+
+    def universe(xs, ys):
+        lo, hi = 1 << 62, -1
+        for v in np.unique(ys):
+            if rp[v + 1] > rp[v]:
+                lo, hi = min(lo, ci[rp[v]]), max(hi, ci[rp[v + 1] - 1] + 1)
+        for u in np.unique(xs):
+            for z in ci[rp[u]:rp[u + 1]]:
+                if rp[z + 1] > rp[z]:
+                    lo, hi = min(lo, ci[rp[z]]), max(hi, ci[rp[z + 1] - 1] + 1)
+        return lo & ~127, hi
+
+    ids = np.arange(n)
+    og = coracle.OracleGraph(n, A, Bv)
+    for xs, ys in ((x, y), (y, x)):
+        bt = G.batch(xs, ys)
+        plan = bt.plan()
+        assert (plan["lo"], plan["hi"]) == universe(xs, ys), plan
+        bt.score(7)
+        got = bt.fetch(7)
+        cn, jac, aa, _ = og.score_pairs(xs, ys, 7)
+        np.testing.assert_array_equal(got["cn"], cn)
+        np.testing.assert_array_equal(got["jaccard"], jac)
+        np.testing.assert_array_equal(got["adamic"], aa)
+        bt.close()
+    # wedge rows: x holds one when every neighbour row has <= 64 ids (wedge.hip), N(N(x)) back to back
+    nv = ctypes.c_int64(0)
+    blp._lib.check(blp.lib().blp_graph_wedge(G.handle, ctypes.byref(nv), None, None))
+    if nv.value > 0:
+        wp = np.empty(n + 1, np.int64)
+        wedge = np.empty(4 * nv.value, np.int32)
+        blp._lib.check(blp.lib().blp_graph_wedge(G.handle, ctypes.byref(nv), P(wp), P(wedge)))
+        deg = np.diff(rp)
+        for v in rng.choice(n, 400, replace=False):
+            nbr = ci[rp[v]:rp[v + 1]]
+            ok = len(nbr) > 0 and deg[nbr].max() <= 64
+            assert (wp[v + 1] > wp[v]) == ok
+            if ok:
+                want = np.concatenate([ci[rp[z]:rp[z + 1]] for z in nbr])
+                got_w = wedge[4 * wp[v]:4 * wp[v + 1]]
+                np.testing.assert_array_equal(np.unique(got_w), np.unique(want))
+                assert len(got_w) == (len(want) + 3) // 4 * 4
+    G.close()
