@@ -1579,9 +1579,14 @@ extern "C" int blp_topk_fetch(blp_topk* t, uint32_t method, int32_t* cols, doubl
 }
 
 extern "C" int blp_topk_stats(blp_topk* t, int which, double* total_ms, int64_t* launches) {
-  BLP_CHECK(t && which >= 0 && which <= 7, BLP_E_ARG, "blp_topk_stats: bad arguments");
+  BLP_CHECK(t && which >= 0 && which <= 8, BLP_E_ARG, "blp_topk_stats: bad arguments");
   int rc = set_device(t->g);
   if (rc) return rc;
+  if (which == 8) {  // bytes one dense hot-target add reads: its packed counts and fused AA words
+    if (total_ms) *total_ms = 0.0;
+    if (launches) *launches = t->dw_n ? 4 * t->dw_words + (t->have_aa ? 16 * t->H : 0) : 0;
+    return BLP_OK;
+  }
   if (which == 0) {
     if ((rc = timer_collect(t->timer))) return rc;
     if (total_ms) *total_ms = t->timer.total_ms;
@@ -1591,8 +1596,8 @@ extern "C" int blp_topk_stats(blp_topk* t, int which, double* total_ms, int64_t*
   // 1 / 2: sources whose AA went through the candidate hash / direct accumulation;
   // 3: sum of |H2(x)|; 4: sum over x and w in H2(x) of |N(w)| (the push volume of one pass);
   // 5: sources whose AA top-k came straight from the fused sums; 6: row entries actually pushed by
-  // the count pass (walk + dense corrections); 7: dense target counts added
-  BLP_HIP(hipStreamSynchronize(t->g->stream));
+  // the count pass (walk + dense corrections); 7: dense target counts added; 8 (above): bytes read
+  // per dense add  BLP_HIP(hipStreamSynchronize(t->g->stream));
   unsigned long long c[8];
   BLP_HIP(hipMemcpy(c, t->counters.p, 64, hipMemcpyDeviceToHost));
   if (total_ms) *total_ms = 0.0;

@@ -282,7 +282,10 @@ int blp_hop3_sample(blp_graph* g, const int32_t* src, int64_t n_src, const int32
  *                         n_cand[i] = |H3(src[i])|, the number of candidates scored.
  *   blp_topk_stats:       which 0: kernel ms/launches; 1 / 2: sources whose Adamic-Adar took
  *                         the candidate-hash / direct-accumulation path (in *launches);
- *                         3: sum of |H2(x)|; 4: sum over x and w in H2(x) of |N(w)| (work). */
+ *                         3: sum of |H2(x)|; 4: sum over x and w in H2(x) of |N(w)| (work);
+ *                         5: sources whose AA lists came from the fused sums; 6: row entries the
+ *                         count pass pushed (walk + dense corrections); 7: dense hot-target adds;
+ *                         8: bytes one dense add reads (counts + fused AA words).                 */
 int blp_topk_create(blp_graph* g, int64_t src_lo, int64_t src_hi, int64_t tgt_lo, int64_t tgt_hi,
                     blp_topk** out);
 int blp_topk_destroy(blp_topk* t);
