@@ -71,6 +71,9 @@ SIGNATURES = {
     "blp_batch_score": [_P, _P, _U32],
     "blp_batches_score": [_P, _I32, _P, _P],
     "blp_batch_fetch": [_P, _P, _P, _P, _P],
+    "blp_batch_fetch_repr": [_P, _P, _I32, _I32, _P],
+    "blp_repr_format": [_P, _I64, _I32, _P],
+    "blp_repr_format_device": [_I32, _P, _I64, _I32, _P],
     "blp_batch_destroy": [_P],
     "blp_batch_plan": [_P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
                        ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),

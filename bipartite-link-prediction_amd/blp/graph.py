@@ -491,6 +491,13 @@ class PairBatch:
         check(lib().blp_batch_fetch(self.graph.handle, self.handle, ptr(cn), ptr(jac), ptr(aa)))
         return {"cn": cn, "jaccard": jac, "adamic": aa}
 
+    def fetch_repr(self, which, zero_int=False):
+        """The Jaccard (which = JACCARD) or Adamic-Adar (ADAMIC) scores as json.dumps text,
+        formatted on the device: uint8[n, 24], NUL-padded slots (blp_batch_fetch_repr)."""
+        out = np.empty((self.n, 24), np.uint8)
+        check(lib().blp_batch_fetch_repr(self.graph.handle, self.handle, which, int(bool(zero_int)), ptr(out)))
+        return out
+
     def close(self):
         if getattr(self, "handle", None):
             lib().blp_batch_destroy(self.handle)

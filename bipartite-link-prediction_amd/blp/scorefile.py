@@ -19,7 +19,7 @@ _lib.register("blp_examples_ids", [_P, _P, _P, _P])
 _lib.register("blp_examples_destroy", [_P])
 _lib.register("blp_scores_write", [_P, ctypes.c_char_p, ctypes.c_int, _P, _P, ctypes.c_int64])
 
-U32, F64, F64_INT0, NONE = 0, 1, 2, 3  # BLP_SCORE_* (blp.h)
+U32, F64, F64_INT0, NONE, REPR24 = 0, 1, 2, 3, 4  # BLP_SCORE_* (blp.h)
 E_UNSUP = -4
 
 
@@ -47,10 +47,16 @@ class Examples:
         return cls(h)
 
     def write(self, path, kind, present=None, values=None):
-        """One score file; values hold one entry per present pair (uint32 for U32, float64 else)."""
+        """One score file; values hold one entry per present pair (uint32 for U32, a row of the
+        uint8[n, 24] slots of PairBatch.fetch_repr for REPR24, float64 else)."""
         pres = None if present is None else np.ascontiguousarray(present, np.uint8)
         if kind == NONE:
             vals, n = None, 0
+        elif kind == REPR24:
+            vals = np.ascontiguousarray(values, np.uint8)
+            if vals.ndim != 2 or vals.shape[1] != 24:
+                raise ValueError("REPR24 values must be uint8[n, 24] slots")
+            n = len(vals)
         else:
             vals = np.ascontiguousarray(values, np.uint32 if kind == U32 else np.float64)
             n = len(vals)
@@ -66,3 +72,17 @@ class Examples:
             self.close()
         except Exception:
             pass
+
+
+def format_repr(values, zero_int=False):
+    """repr(v) of each double as uint8[n, 24] slots, formatted on the host by the same code the
+    device runs (blp_repr_format; csrc/repr.h)."""
+    v = np.ascontiguousarray(values, np.float64)
+    out = np.zeros((len(v), 24), np.uint8)
+    check(lib().blp_repr_format(ptr(v), len(v), int(bool(zero_int)), ptr(out)))
+    return out
+
+
+def slot_strings(slots):
+    """The text of each 24-byte slot (tests)."""
+    return [bytes(r).rstrip(b"\0").decode() for r in np.asarray(slots, np.uint8)]

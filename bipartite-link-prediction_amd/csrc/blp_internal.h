@@ -3,8 +3,10 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdio>
+#include <cstring>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -180,6 +182,9 @@ int build_hot_index(blp_graph* g);
 int graph_finish(blp_graph* g, const double* aaw);
 int build_wedge_index(blp_graph* g);
 int build_node2(blp_graph* g);  // after build_hot_index (the dense-row flag)
+constexpr int REPR_SLOT_BYTES = 24;  // repr.h REPR_SLOT
+// repr(v) of n device doubles into 24-byte slots at d_out (repr.hip); enqueued on s
+int repr_launch(const double* d_v, int64_t n, bool zero_int, char* d_out, int n_cu, hipStream_t s);
 // the graph's wedge-row bitmaps over [lo, hi) (built and cached on first use); null with *rc == 0
 // when there is no wedge index or no cache slot left
 const WedgeBitmaps* wedge_bitmaps(blp_graph* g, int64_t lo, int64_t hi, int* rc);

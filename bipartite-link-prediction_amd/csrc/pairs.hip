@@ -3678,6 +3678,27 @@ int blp_batch_fetch(blp_graph* g, blp_batch* b, uint32_t* cn, double* jac, doubl
   return BLP_OK;
 }
 
+int blp_batch_fetch_repr(blp_graph* g, blp_batch* b, int which, int zero_int, char* out) {
+  BLP_CHECK(g && b && b->g == g && (which == BLP_JACCARD || which == BLP_ADAMIC), BLP_E_ARG,
+            "blp_batch_fetch_repr: graph/batch mismatch or which is not BLP_JACCARD / BLP_ADAMIC");
+  const int64_t np = b->n_pairs;
+  BLP_CHECK(np == 0 || out, BLP_E_ARG, "blp_batch_fetch_repr: null output");
+  int rc = set_device(g);
+  if (rc) return rc;
+  BLP_HIP(hipStreamSynchronize(b->stream));
+  Misc m;
+  BLP_HIP(hipMemcpy(&m, b->d_misc, sizeof(Misc), hipMemcpyDeviceToHost));
+  if (which == BLP_JACCARD && m.zero_div) return fail(BLP_E_ZERODIV, "float division by zero (Jaccard union is empty)");
+  if (np == 0) return BLP_OK;
+  ScopedBuf slots;
+  if ((rc = slots.reserve((size_t)blp::REPR_SLOT_BYTES * np))) return rc;
+  rc = repr_launch(which == BLP_JACCARD ? b->d_jac : b->d_aa, np, zero_int != 0, slots.as<char>(), g->n_cu, b->stream);
+  if (rc) return rc;
+  BLP_HIP(hipMemcpyAsync(out, slots.p, (size_t)blp::REPR_SLOT_BYTES * np, hipMemcpyDeviceToHost, b->stream));
+  BLP_HIP(hipStreamSynchronize(b->stream));
+  return BLP_OK;
+}
+
 int blp_score_pairs(blp_graph* g, int side, uint32_t mask, const int32_t* pu, const int32_t* pb, int64_t n_pairs,
                     uint32_t* cn, double* jac, double* aa) {
   BLP_CHECK(g && (side == 0 || side == 1), BLP_E_ARG, "blp_score_pairs: bad graph or side");

@@ -309,7 +309,7 @@ int blp_examples_destroy(blp_examples* x) {
 
 int blp_scores_write(const blp_examples* x, const char* path, int kind, const uint8_t* present, const void* values,
                      int64_t n_values) {
-  BLP_CHECK(x && path && kind >= BLP_SCORE_U32 && kind <= BLP_SCORE_NONE, BLP_E_ARG, "blp_scores_write: bad arguments");
+  BLP_CHECK(x && path && kind >= BLP_SCORE_U32 && kind <= BLP_SCORE_REPR24, BLP_E_ARG, "blp_scores_write: bad arguments");
   const int64_t nu = (int64_t)x->u_key.size(), np = (int64_t)x->v_key.size();
   // k-th present pair -> values[k]: the prefix count of present pairs
   std::vector<int64_t> vidx;
@@ -372,6 +372,10 @@ int blp_scores_write(const blp_examples* x, const char* path, int kind, const ui
         const int64_t vi = present ? vidx[k] : k;
         if (kind == BLP_SCORE_U32) {
           o = std::to_chars(o, o + 12, ((const uint32_t*)values)[vi]).ptr;
+        } else if (kind == BLP_SCORE_REPR24) {  // formatted on the device: copy the slot
+          const char* sl = (const char*)values + 24 * vi;
+          std::memcpy(o, sl, 24);  // within the pair's bound (key + 30)
+          o += strnlen(sl, 24);
         } else {
           const double v = ((const double*)values)[vi];
           if (kind == BLP_SCORE_F64_INT0 && v == 0.0)

@@ -125,10 +125,12 @@ def score_both_sides(examples, G, u_mask, b_mask):
     return _score_both_ids(G, u_ids, v_ids, u_mask, b_mask)
 
 
-def _score_both_ids(G, u_ids, v_ids, u_mask, b_mask, timings=None):
+def _score_both_ids(G, u_ids, v_ids, u_mask, b_mask, timings=None, text=False):
     """Id lookup, the two batches (created concurrently: blp_batch_create's host planning
     releases the GIL), one concurrent device step, and the results; phase times into
-    ``timings`` (score_lookup, score_create, score_device, score_fetch) when given."""
+    ``timings`` (score_lookup, score_create, score_device, score_fetch) when given. ``text``:
+    the Jaccard / Adamic-Adar scores come back as their json.dumps text, formatted on the
+    device (PairBatch.fetch_repr: "jaccard_repr" / "adamic_repr" slots), not as doubles."""
     import time
     from concurrent.futures import ThreadPoolExecutor
 
@@ -147,7 +149,10 @@ def _score_both_ids(G, u_ids, v_ids, u_mask, b_mask, timings=None):
         G.score_batches([(ub, u_mask), (bb, b_mask)])
         blp.device_sync(G.device)  # the batches run on their own streams
         t3 = time.perf_counter()
-        res = present, ub.fetch(u_mask), bb.fetch(b_mask)
+        if text:
+            res = present, _fetch_text(ub, u_mask), _fetch_text(bb, b_mask)
+        else:
+            res = present, ub.fetch(u_mask), bb.fetch(b_mask)
         if timings is not None:
             timings.update({"score_lookup": t1 - t0, "score_create": t2 - t1, "score_device": t3 - t2,
                             "score_fetch": time.perf_counter() - t3})
@@ -155,6 +160,17 @@ def _score_both_ids(G, u_ids, v_ids, u_mask, b_mask, timings=None):
     finally:
         ub.close()
         bb.close()
+
+
+def _fetch_text(batch, mask):
+    """Counts as uint32; Jaccard / Adamic-Adar as device-formatted text slots (0.0 as the int 0
+    for Adamic-Adar, similarity.py:118)."""
+    res = batch.fetch(blp.CN)
+    if mask & blp.JACCARD:
+        res["jaccard_repr"] = batch.fetch_repr(blp.JACCARD)
+    if mask & blp.ADAMIC:
+        res["adamic_repr"] = batch.fetch_repr(blp.ADAMIC, zero_int=True)
+    return res
 
 
 def _run_side(examples, G, methods, outfiles, table, side, sidecar=False, scored=None):
@@ -185,9 +201,11 @@ def _write_jobs(ex, methods, outfiles, table, present, scores):
         if bit == blp.CN:
             args = (scorefile.U32, pres, scores["cn"])
         elif bit == blp.JACCARD:
-            args = (scorefile.F64, pres, scores["jaccard"])
+            args = ((scorefile.REPR24, pres, scores["jaccard_repr"]) if "jaccard_repr" in scores
+                    else (scorefile.F64, pres, scores["jaccard"]))
         elif bit == blp.ADAMIC:
-            args = (scorefile.F64_INT0, pres, scores["adamic"])
+            args = ((scorefile.REPR24, pres, scores["adamic_repr"]) if "adamic_repr" in scores
+                    else (scorefile.F64_INT0, pres, scores["adamic"]))
         else:  # a method the reference does not match: only missing-node zeros
             args = (scorefile.NONE, pres)
 
@@ -262,7 +280,8 @@ def main(example_file, graph_file, u_methods, u_outfiles, b_methods, b_outfiles,
         if ex is None:
             present, u_scores, b_scores = score_both_sides(examples, G, *masks)
         else:
-            present, u_scores, b_scores = _score_both_ids(G, ex.pair_user, ex.pair_business, *masks, timings=timings)
+            present, u_scores, b_scores = _score_both_ids(G, ex.pair_user, ex.pair_business, *masks, timings=timings,
+                                                          text=True)
         t_s = clock()
         if ex is None:
             _run_side(examples, G, u_methods, u_outfiles, _U_BITS, 0, sidecar, scored=(present, u_scores))

@@ -173,12 +173,16 @@ int blp_ids_lookup(const int32_t* id_map, int64_t id_lo, int64_t id_span, const 
  *     BLP_SCORE_F64       doubles in Python repr (jaccard)
  *     BLP_SCORE_F64_INT0  doubles, 0.0 written as the int 0 (adamic_adar, similarity.py:118)
  *     BLP_SCORE_NONE      values unused: only absent pairs are written (a method string the
- *                         reference does not match, e.g. the b_adamic bug, similarity.py:102) */
+ *                         reference does not match, e.g. the b_adamic bug, similarity.py:102)
+ *     BLP_SCORE_REPR24    values are 24-byte slots of already formatted text, NUL-padded
+ *                         (blp_batch_fetch_repr / blp_repr_format: the doubles formatted on
+ *                         the device) */
 typedef struct blp_examples blp_examples;
 #define BLP_SCORE_U32 0
 #define BLP_SCORE_F64 1
 #define BLP_SCORE_F64_INT0 2
 #define BLP_SCORE_NONE 3
+#define BLP_SCORE_REPR24 4
 int blp_examples_parse(const char* path, blp_examples** out);
 int blp_examples_info(const blp_examples* e, int64_t* n_users, int64_t* n_pairs);
 int blp_examples_ids(const blp_examples* e, int64_t* pair_user, int64_t* pair_business, int64_t* user_off);
@@ -231,6 +235,17 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
                      blp_batch** out);
 int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask);
 int blp_batch_fetch(blp_graph* g, blp_batch* b, uint32_t* cn, double* jac, double* aa);
+/* blp_batch_fetch_repr: the batch's Jaccard (which = BLP_JACCARD) or Adamic-Adar (BLP_ADAMIC)
+ * scores as the text json.dumps writes for them (Python's repr: shortest round-trip digits),
+ * formatted on the device into out[n_pairs][24] (NUL-padded slots, caller order); zero_int
+ * writes 0.0 as the int 0 (adamic_adar, similarity.py:118). Replaces the host formatting of
+ * util.write_json (util.py:18-21) for similarity.main's score files; BLP_E_ZERODIV as
+ * blp_batch_fetch for an empty Jaccard union. */
+int blp_batch_fetch_repr(blp_graph* g, blp_batch* b, int which, int zero_int, char* out);
+/* The same formatting of n doubles: on the host (blp_repr_format; tests pin it against CPython's
+ * repr) and of device-resident values on device `device` (blp_repr_format_device). */
+int blp_repr_format(const double* values, int64_t n, int zero_int, char* out);
+int blp_repr_format_device(int device, const double* d_values, int64_t n, int zero_int, char* d_out);
 int blp_batch_destroy(blp_batch* b);
 /* Enqueue blp_batch_score for n batches of one graph at once (one similarity.main step: the
  * user and the business pass). They run concurrently; a large-universe (user-side) batch is

@@ -95,7 +95,7 @@ def test_parse_accepts_json_scalars(tmp_path, label):
     assert ex is not None and ex.n_pairs == 2
 
 
-@pytest.mark.parametrize("kind", ["cn", "jaccard", "adamic", "none"])
+@pytest.mark.parametrize("kind", ["cn", "jaccard", "adamic", "none", "jaccard_repr", "adamic_repr"])
 @pytest.mark.parametrize("absent_rate", [0.0, 0.07])
 def test_written_text_equals_json_dumps(tmp_path, kind, absent_rate):
     rng = np.random.default_rng(7)
@@ -118,6 +118,16 @@ def test_written_text_equals_json_dumps(tmp_path, kind, absent_rate):
         scores = {"adamic": a}
         bit, code = similarity.blp.ADAMIC, scorefile.F64_INT0
         vals = a
+    elif kind == "jaccard_repr":  # pre-formatted slots (similarity.main: formatted on the device)
+        scores = {"jaccard": _odd_doubles(rng, k)}
+        bit, code = similarity.blp.JACCARD, scorefile.REPR24
+        vals = scorefile.format_repr(scores["jaccard"])
+    elif kind == "adamic_repr":
+        a = _odd_doubles(rng, k)
+        a[rng.random(k) < 0.2] = 0.0
+        scores = {"adamic": a}
+        bit, code = similarity.blp.ADAMIC, scorefile.REPR24
+        vals = scorefile.format_repr(a, zero_int=True)
     else:
         scores, bit, code, vals = {}, 0, scorefile.NONE, None
     out = str(tmp_path / "out.json")
