@@ -160,9 +160,13 @@ int build_weight_codes(blp_graph* g, const int64_t* row_ptr, const std::vector<l
     code[order[j].second] = (int)j + 1;
   }
   std::vector<uint8_t> ncode((size_t)n, 0);
+  g->h_uncoded.clear();
   for (int64_t i = 0; i < n; ++i) {
     const auto it = code.find(fx[i]);
-    if (it != code.end()) ncode[i] = (uint8_t)it->second;
+    if (it != code.end())
+      ncode[i] = (uint8_t)it->second;
+    else if (row_ptr[i + 1] > row_ptr[i])
+      g->h_uncoded.push_back((int32_t)i);  // its weight is gathered (code 0): scans over it test for escapes
   }
   uint8_t* d_ncode = nullptr;
   BLP_HIP(hipMemcpy(g->d_wtab, wtab.data(), sizeof(long long) * 256, hipMemcpyHostToDevice));

@@ -1256,7 +1256,7 @@ __device__ __attribute__((always_inline)) inline void rc_build(const int32_t* __
 // 64-bit sum. Valid while cn < 2^PK_CN_BITS (a chunk holds < 2^21 nodes) : each step's high part
 // undercounts S by < 2^40 + K * 2^32, so S - hi * 2^40 < cn * 2^41 < 2^64 (blp::aa_exact, hs = 40).
 
-template <int NT, int K, bool AA>
+template <int NT, int K, bool AA, bool ESC = true>
 __device__ __attribute__((always_inline)) inline void rc_scan(const int32_t* __restrict__ ci, uint32_t idmask, int idbits,
                                const long long* __restrict__ aaw, const long long* wtab, const int64_t* s_start,
                                const int32_t* s_off, const int32_t* s_coff, int ns, int64_t c0, int64_t width,
@@ -1286,8 +1286,19 @@ __device__ __attribute__((always_inline)) inline void rc_scan(const int32_t* __r
     for (int k = 0; k < K; ++k) hm |= ((wd[k] >> (rr[k] & 31)) & 1u) << k;
     if (hm) {
       if (AA) {
-        // the step's high words fit 32 bits: K <= 16 terms of W >> 32 < 2^27 (W < 2^59)
         unsigned long long acc = 0;
+        if (!ESC && packed) {
+          // every id of the scan universe carries its weight's code (ESC false: the batch's
+          // range holds no code-0 node): no escape test, and the high field is the step sum's
+          // own >> PK_HS -- K <= 16 terms of W < 2^59 sum below 2^63, and each step undercounts
+          // S by < 2^PK_HS, so S - hi * 2^PK_HS < cn * 2^PK_HS (blp::aa_exact)
+#pragma unroll
+          for (int k = 0; k < K; ++k) acc += ((hm >> k) & 1u) ? (unsigned long long)wt[k] : 0ull;
+          atomicAdd(&s_aa[2 * st.s], acc);
+          atomicAdd(&s_aa[2 * st.s + 1], ((acc >> PK_HS) << PK_CN_BITS) | (unsigned)__popc(hm));
+          return;
+        }
+        // the step's high words fit 32 bits: K <= 16 terms of W >> 32 < 2^27 (W < 2^59)
         uint32_t esc = 0, acch = 0;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
@@ -1609,6 +1620,7 @@ struct ScoreArgs {
   int64_t nnz, wedge_vecs;      // CSR entries, wedge-row vectors (BLP_DEBUG bounds)
   int64_t n_hot, hot_vecs;      // dense rows, their pool's vectors (BLP_DEBUG bounds)
   int lq_wgs;                   // workgroups d_lq was sized for (BLP_DEBUG bound)
+  int all_coded;                // 1: every node of [lo, hi) carries a weight code (no code-0 gathers); 0: unknown
 };
 
 template <int BLOCK>
@@ -1944,7 +1956,10 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
           } else if (RC) {
             rc_chunk_offsets<BLOCK, K>(s_off, ns, s_coff, red);
             const int shift = build_hint<BLOCK, HC>(s_coff, ns, BLOCK, s_hint);
-            if (want_a)
+            if (want_a && packed && a.all_coded)
+              rc_scan<BLOCK, K, true, false>(a.cw, a.idmask, a.idbits, a.aaw, s_wtab, s_start, s_off, s_coff, ns, c0,
+                                             width, bm, CAP_WORDS, s_cn, s_aa, threadIdx.x, s_hint, shift, true);
+            else if (want_a)
               rc_scan<BLOCK, K, true>(a.cw, a.idmask, a.idbits, a.aaw, s_wtab, s_start, s_off, s_coff, ns, c0, width,
                                       bm, CAP_WORDS, s_cn, s_aa, threadIdx.x, s_hint, shift, packed);
             else
@@ -2356,6 +2371,14 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
       if (want_a) {
         unsigned long long sh, sl;
         blp::aa_exact(w0, w1 >> PK_CN_BITS, &sh, &sl, PK_HS);
+#ifdef BLP_EXP_L2ATOM  // experiment only (wrong when a source's chunks span XCDs): atomics in L2
+        if (pk24) {
+          __hip_atomic_fetch_add(&paa[2 * gp], sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          __hip_atomic_fetch_add(&paa[2 * gp + 1], (((sh << 12) | (sl >> 52)) << SPLIT_CN_BITS) | c_t,
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          return;
+        }
+#endif
         atomicAdd(&paa[2 * gp], sl);
         if (pk24) {
           atomicAdd(&paa[2 * gp + 1], (((sh << 12) | (sl >> 52)) << SPLIT_CN_BITS) | c_t);
@@ -3476,6 +3499,10 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   a.idbits = coded ? g->id_bits : 31;
   a.idmask = (uint32_t)((1ull << a.idbits) - 1);
   a.wtab = g->d_wtab;
+  // no code-0 node in the universe: the escape-free packed scan (rc_scan ESC = false)
+  a.all_coded = coded && std::lower_bound(g->h_uncoded.begin(), g->h_uncoded.end(), (int32_t)b->lo) ==
+                             std::lower_bound(g->h_uncoded.begin(), g->h_uncoded.end(),
+                                              (int32_t)std::min<int64_t>(b->hi, INT32_MAX));
 
   a.off = b->off.as<int32_t>();
   a.cnt = b->cnt.as<int32_t>();
