@@ -10,6 +10,8 @@
 #include <mutex>
 #include <unordered_map>
 
+#include <chrono>
+
 #include "blp_internal.h"
 
 namespace {
@@ -203,24 +205,40 @@ int aa_weights_fixed(const double* aaw, int64_t n, std::vector<long long>& fx) {
 // g->hrp / g->hci (host mirrors) are in place: stream, CU count, fixed-point Adamic-Adar
 // weights and the weight-coded id stream, the dense-row index and the wedge rows.
 int graph_finish(blp_graph* g, const double* aaw) {
+  // BLP_GRAPH_PROF: stage wall times on stderr (profiling only; the stages run either way)
+  const bool gprof = getenv("BLP_GRAPH_PROF") != nullptr;
+  auto t_prev = std::chrono::steady_clock::now();
+  auto stage = [&](const char* what) {
+    if (!gprof) return;
+    const auto t = std::chrono::steady_clock::now();
+    fprintf(stderr, "graph_finish %-8s %.3f ms\n", what, std::chrono::duration<double, std::milli>(t - t_prev).count());
+    t_prev = t;
+  };
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, g->device) == hipSuccess) g->n_cu = prop.multiProcessorCount;
   if (!g->stream) BLP_HIP(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
   const int64_t n = g->n;
   g->max_row = 0;
   for (int64_t v = 0; v < n; ++v) g->max_row = std::max<int64_t>(g->max_row, g->hrp[v + 1] - g->hrp[v]);
+  stage("setup");
   if (aaw) {
     std::vector<long long> fx;
     if (int rc = aa_weights_fixed(aaw, n, fx)) return rc;
     BLP_HIP(hipMalloc(&g->d_aaw_fx, sizeof(long long) * std::max<int64_t>(n, 1)));
     if (n) BLP_HIP(hipMemcpy(g->d_aaw_fx, fx.data(), sizeof(long long) * n, hipMemcpyHostToDevice));
+    stage("weights");
     int rc = build_weight_codes(g, g->hrp, fx);
     if (rc != BLP_OK) return rc;
+    stage("codes");
   }
   int rc = build_hot_index(g);
   if (rc != BLP_OK) return rc;
+  stage("hot");
   if ((rc = build_node2(g)) != BLP_OK) return rc;
-  return build_wedge_index(g);
+  stage("node2");
+  rc = build_wedge_index(g);
+  stage("wedge");
+  return rc;
 }
 
 }  // namespace blp

@@ -1702,6 +1702,14 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
   const bool packed = RC && want_a && nchunks == 1 && !(a.short_rows & 2) && CAP_BITS < (1 << PK_CN_BITS);
   uint4* bm4 = reinterpret_cast<uint4*>(bm);
   const int n_active = a.misc->n_active;
+  // Short-row scorer on a one-chunk universe: the bitmap is zeroed once here, and afterwards by
+  // each source right after its last scan, interleaved with its output stores and ordered by the
+  // barrier that ends them -- so a source starts its build on a clean bitmap with no zeroing pass
+  // and no barrier of its own in front of it.
+  const bool clean_after = SHORT && nchunks == 1;
+  const int nw4_u = (int)((((span + 31) >> 5) + 3) >> 2);
+  if (clean_after)
+    for (int i = threadIdx.x; i < nw4_u; i += BLOCK) bm4[i] = make_uint4(0, 0, 0, 0);  // before the first barrier
 
   PROF_INIT
   // dequeue one ahead: the next source's atomic is in flight while this one is scored
@@ -1826,7 +1834,7 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
               const int q = threadIdx.x + j * BLOCK;
               if (q < nw4) bm4[q] = acc[j];
             }
-          } else {
+          } else if (!clean_after) {
             for (int q = threadIdx.x; q < nw4; q += BLOCK) {
               uint4 v = make_uint4(0, 0, 0, 0);
               for (int r = 0; r < nhot; ++r) {
@@ -1842,7 +1850,7 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
               bm4[q] = v;
             }
           }
-          __syncthreads();
+          if (!clean_after) __syncthreads();  // (uniform)
           PROF(2)
           if (SHORT && a.wp) {
             // N(N(x)) from x's wedge row: one contiguous range, two 16-byte vectors per thread
@@ -1985,6 +1993,8 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
           }
           __syncthreads();
           PROF(7)
+          if (clean_after && sb + SEG >= pcnt)  // the last scan is done: clean for the next source
+            for (int i = threadIdx.x; i < nw4; i += BLOCK) bm4[i] = make_uint4(0, 0, 0, 0);
           for (int t = threadIdx.x; t < ns; t += BLOCK) {  // ns <= SEG <= BLOCK: t == threadIdx.x
             const int p = pout;
             if (!PS_OK(a.misc, p >= 0 && p < a.np, 4, p, a.np)) continue;
@@ -2018,6 +2028,10 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
           }
           __syncthreads();
           PROF(8)
+        }
+        if (clean_after && pcnt == 0) {  // (uniform) no scan to clean after
+          for (int i = threadIdx.x; i < nw4; i += BLOCK) bm4[i] = make_uint4(0, 0, 0, 0);
+          __syncthreads();
         }
       }
     }

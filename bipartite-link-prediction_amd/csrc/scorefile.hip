@@ -29,15 +29,46 @@
 
 #include "blp_internal.h"
 
+namespace {
+// vector storage that resize() leaves uninitialised (every element is written right after)
+template <class T>
+struct NoInit : std::allocator<T> {
+  template <class U>
+  struct rebind {
+    using other = NoInit<U>;
+  };
+  NoInit() = default;
+  template <class U>
+  NoInit(const NoInit<U>&) noexcept {}
+  template <class U>
+  void construct(U* p) noexcept {
+    ::new ((void*)p) U;
+  }
+  template <class U, class... A>
+  void construct(U* p, A&&... a) {
+    ::new ((void*)p) U(std::forward<A>(a)...);
+  }
+};
+template <class T>
+using Vec = std::vector<T, NoInit<T>>;
+
+struct Text {  // the file's bytes, read once (not zero-filled first)
+  std::unique_ptr<char[]> p;
+  size_t n = 0;
+  const char* data() const { return p.get(); }
+  size_t size() const { return n; }
+};
+}  // namespace
+
 struct blp_examples {
-  std::string text;               // the file
-  std::vector<int64_t> u_off;     // [n_users + 1] first pair of each user
-  std::vector<int64_t> u_key;     // [n_users] byte offset of the user key (inside its quotes)
-  std::vector<int32_t> u_len;     // [n_users] its length
-  std::vector<int64_t> u_id;      // [n_users] int(user key)
-  std::vector<int64_t> v_key;     // [n_pairs] byte offset of the business key
-  std::vector<int32_t> v_len;     // [n_pairs]
-  std::vector<int64_t> v_id;      // [n_pairs] int(business key)
+  Text text;               // the file
+  Vec<int64_t> u_off;      // [n_users + 1] first pair of each user
+  Vec<int64_t> u_key;      // [n_users] byte offset of the user key (inside its quotes)
+  Vec<int32_t> u_len;      // [n_users] its length
+  Vec<int64_t> u_id;       // [n_users] int(user key)
+  Vec<int64_t> v_key;      // [n_pairs] byte offset of the business key
+  Vec<int32_t> v_len;      // [n_pairs]
+  Vec<int64_t> v_id;       // [n_pairs] int(business key)
 };
 
 namespace {
@@ -124,64 +155,163 @@ bool skip_scalar(Cursor& c) {
   return true;
 }
 
+// The users of one byte range of the outer object: [p, e) starts at a user key and ends right
+// after the ',' that follows its last user -- or, for the last range, at the end of the text
+// (the outer '}' and trailing whitespace).
+struct Part {
+  std::vector<int64_t> u_key, u_id, v_key, v_id, u_cnt;
+  std::vector<int32_t> u_len, v_len;
+  int rc = BLP_OK;
+  const char* err = nullptr;
+};
+
+void parse_part(const char* base, const char* p, const char* e, bool last, Part* o) {
+  Cursor c{p, e};
+  const size_t est = (size_t)(e - p) / 8 + 16;  // a pair takes >= 8 bytes ("1": 0, ): no regrowth
+  o->v_key.reserve(est), o->v_len.reserve(est), o->v_id.reserve(est);
+  auto bad = [&](const char* m) {
+    o->rc = BLP_E_UNSUP;
+    o->err = m;
+  };
+  for (;;) {
+    int64_t off, id;
+    int32_t len;
+    if (!int_key(c, &off, &len, &id, base) || !c.eat(':') || !c.eat('{'))
+      return bad("blp_examples_parse: outer key / inner object not of the simple shape");
+    o->u_key.push_back(off);
+    o->u_len.push_back(len);
+    o->u_id.push_back(id);
+    const size_t v0 = o->v_key.size();
+    if (!c.eat('}')) {
+      for (;;) {
+        if (!int_key(c, &off, &len, &id, base) || !c.eat(':') || !skip_scalar(c))
+          return bad("blp_examples_parse: inner key / value not of the simple shape");
+        o->v_key.push_back(off);
+        o->v_len.push_back(len);
+        o->v_id.push_back(id);
+        if (c.eat(',')) continue;
+        if (c.eat('}')) break;
+        return bad("blp_examples_parse: malformed inner object");
+      }
+    }
+    o->u_cnt.push_back((int64_t)(o->v_key.size() - v0));
+    if (c.eat(',')) {
+      c.ws();
+      if (!last && c.p == e) return;  // this range ends after the separator
+      continue;
+    }
+    if (last && c.eat('}')) {
+      c.ws();
+      if (c.p != c.e) return bad("blp_examples_parse: trailing data");
+      return;
+    }
+    return bad("blp_examples_parse: malformed outer object");
+  }
+}
+
+// Duplicate business keys of users [u0, u1) (json.loads would keep the first position and the
+// last value: not handled here, so refused). Equal keys have equal ids: the ids are sorted
+// first, and key bytes compared only where two ids are equal ("5" and "05" differ).
+bool unique_business_keys(const blp_examples* x, size_t u0, size_t u1) {
+  const char* base = x->text.data();
+  auto view = [&](int64_t k) { return std::string_view(base + x->v_key[k], (size_t)x->v_len[k]); };
+  std::vector<int64_t> ids, ord;
+  for (size_t u = u0; u < u1; ++u) {
+    const int64_t b = x->u_off[u], e = x->u_off[u + 1];
+    ids.assign(x->v_id.begin() + b, x->v_id.begin() + e);
+    std::sort(ids.begin(), ids.end());
+    if (std::adjacent_find(ids.begin(), ids.end()) == ids.end()) continue;
+    ord.resize(e - b);
+    for (int64_t k = b; k < e; ++k) ord[k - b] = k;
+    std::sort(ord.begin(), ord.end(), [&](int64_t i, int64_t j) {
+      if (x->v_id[i] != x->v_id[j]) return x->v_id[i] < x->v_id[j];
+      return view(i) < view(j);
+    });
+    for (size_t k = 1; k < ord.size(); ++k)
+      if (x->v_id[ord[k]] == x->v_id[ord[k - 1]] && view(ord[k]) == view(ord[k - 1])) return false;
+  }
+  return true;
+}
+
+// examples.json of the reference's shape, {"user": {"business": label, ...}, ...}, parsed on up
+// to 16 threads: the text is cut at user boundaries (in this shape every '}' outside the outer
+// braces closes a user's object: keys are digit strings and values scalars -- a '}' anywhere
+// else fails the range that holds it, and the whole parse with it), each range parsed on its
+// own, the parts concatenated in file order.
 int parse(blp_examples* x) {
   const char* base = x->text.data();
-  Cursor c{base, base + x->text.size()};
+  const char* const end = base + x->text.size();
+  Cursor c{base, end};
   if (!c.eat('{')) return fail(BLP_E_UNSUP, "blp_examples_parse: not a JSON object");
-  x->u_off.push_back(0);
-  if (!c.eat('}')) {
-    for (;;) {
-      int64_t off, id;
-      int32_t len;
-      if (!int_key(c, &off, &len, &id, base) || !c.eat(':') || !c.eat('{'))
-        return fail(BLP_E_UNSUP, "blp_examples_parse: outer key / inner object not of the simple shape");
-      x->u_key.push_back(off);
-      x->u_len.push_back(len);
-      x->u_id.push_back(id);
-      if (!c.eat('}')) {
-        for (;;) {
-          if (!int_key(c, &off, &len, &id, base) || !c.eat(':') || !skip_scalar(c))
-            return fail(BLP_E_UNSUP, "blp_examples_parse: inner key / value not of the simple shape");
-          x->v_key.push_back(off);
-          x->v_len.push_back(len);
-          x->v_id.push_back(id);
-          if (c.eat(',')) continue;
-          if (c.eat('}')) break;
-          return fail(BLP_E_UNSUP, "blp_examples_parse: malformed inner object");
-        }
-      }
-      x->u_off.push_back((int64_t)x->v_key.size());
-      if (c.eat(',')) continue;
-      if (c.eat('}')) break;
-      return fail(BLP_E_UNSUP, "blp_examples_parse: malformed outer object");
-    }
+  x->u_off.assign(1, 0);
+  if (c.eat('}')) {
+    c.ws();
+    return c.p == c.e ? BLP_OK : fail(BLP_E_UNSUP, "blp_examples_parse: trailing data");
   }
-  c.ws();
-  if (c.p != c.e) return fail(BLP_E_UNSUP, "blp_examples_parse: trailing data");
-  // duplicate keys (json.loads keeps the first position and the last value): not handled here
-  auto view = [&](int64_t off, int32_t len) { return std::string_view(base + off, (size_t)len); };
+  const char* body = c.p;
+  const size_t n = (size_t)(end - body);
+  const unsigned nt = (unsigned)std::max<size_t>(1, std::min<size_t>({16, std::thread::hardware_concurrency(), n >> 20}));
+  std::vector<const char*> cut{body};
+  for (unsigned t = 1; t < nt; ++t) {
+    const char* q = std::max(body + n * t / nt, cut.back());
+    q = static_cast<const char*>(memchr(q, '}', (size_t)(end - q)));
+    if (!q) break;
+    Cursor k{q + 1, end};
+    if (!k.eat(',')) continue;  // the outer object's own '}' (or not this shape: the range fails)
+    k.ws();
+    if (k.p > cut.back() && k.p < end) cut.push_back(k.p);
+  }
+  cut.push_back(end);
+  const size_t np = cut.size() - 1;
+  std::vector<Part> part(np);
+  std::vector<std::thread> th;
+  for (size_t i = 1; i < np; ++i) th.emplace_back(parse_part, base, cut[i], cut[i + 1], i + 1 == np, &part[i]);
+  parse_part(base, cut[0], cut[1], np == 1, &part[0]);
+  for (auto& h : th) h.join();
+  // the parts back to back, each copied by its own thread into its place
+  std::vector<size_t> ub(np + 1, 0), vb(np + 1, 0);
+  for (size_t i = 0; i < np; ++i) {
+    if (part[i].rc) return fail(part[i].rc, part[i].err);
+    ub[i + 1] = ub[i] + part[i].u_key.size();
+    vb[i + 1] = vb[i] + part[i].v_key.size();
+  }
+  const size_t nu = ub[np], nv = vb[np];
+  x->u_key.resize(nu), x->u_len.resize(nu), x->u_id.resize(nu), x->u_off.resize(nu + 1);
+  x->v_key.resize(nv), x->v_len.resize(nv), x->v_id.resize(nv);
+  x->u_off[0] = 0;
+  auto place = [&](size_t i) {
+    Part& pt = part[i];
+    std::copy(pt.u_key.begin(), pt.u_key.end(), x->u_key.begin() + ub[i]);
+    std::copy(pt.u_len.begin(), pt.u_len.end(), x->u_len.begin() + ub[i]);
+    std::copy(pt.u_id.begin(), pt.u_id.end(), x->u_id.begin() + ub[i]);
+    int64_t o = (int64_t)vb[i];
+    for (size_t j = 0; j < pt.u_cnt.size(); ++j) x->u_off[ub[i] + j + 1] = (o += pt.u_cnt[j]);
+    std::copy(pt.v_key.begin(), pt.v_key.end(), x->v_key.begin() + vb[i]);
+    std::copy(pt.v_len.begin(), pt.v_len.end(), x->v_len.begin() + vb[i]);
+    std::copy(pt.v_id.begin(), pt.v_id.end(), x->v_id.begin() + vb[i]);
+    pt = Part();
+  };
+  th.clear();
+  for (size_t i = 1; i < np; ++i) th.emplace_back(place, i);
+  place(0);
+  for (auto& h : th) h.join();
   {
     std::unordered_set<std::string_view> seen;
     seen.reserve(x->u_key.size() * 2);
     for (size_t i = 0; i < x->u_key.size(); ++i)
-      if (!seen.insert(view(x->u_key[i], x->u_len[i])).second)
+      if (!seen.insert(std::string_view(base + x->u_key[i], (size_t)x->u_len[i])).second)
         return fail(BLP_E_UNSUP, "blp_examples_parse: duplicate user key");
   }
-  std::vector<int64_t> ord;
-  for (size_t u = 0; u + 1 < x->u_off.size(); ++u) {
-    const int64_t b = x->u_off[u], e = x->u_off[u + 1];
-    ord.resize(e - b);
-    for (int64_t k = b; k < e; ++k) ord[k - b] = k;
-    // by (id, key bytes): equal keys are then adjacent even where keys of one id differ ("5", "05")
-    std::sort(ord.begin(), ord.end(), [&](int64_t i, int64_t j) {
-      if (x->v_id[i] != x->v_id[j]) return x->v_id[i] < x->v_id[j];
-      return view(x->v_key[i], x->v_len[i]) < view(x->v_key[j], x->v_len[j]);
-    });
-    for (size_t k = 1; k < ord.size(); ++k)
-      if (x->v_id[ord[k]] == x->v_id[ord[k - 1]] &&
-          view(x->v_key[ord[k]], x->v_len[ord[k]]) == view(x->v_key[ord[k - 1]], x->v_len[ord[k - 1]]))
-        return fail(BLP_E_UNSUP, "blp_examples_parse: duplicate business key");
-  }
+  const size_t nusers = x->u_key.size();
+  const unsigned nd = (unsigned)std::max<size_t>(1, std::min<size_t>(nt, nusers / 64));
+  std::vector<uint8_t> ok(nd, 1);
+  th.clear();
+  for (unsigned t = 1; t < nd; ++t)
+    th.emplace_back([&, t]() { ok[t] = unique_business_keys(x, nusers * t / nd, nusers * (t + 1) / nd); });
+  ok[0] = unique_business_keys(x, 0, nusers / nd);
+  for (auto& h : th) h.join();
+  for (unsigned t = 0; t < nd; ++t)
+    if (!ok[t]) return fail(BLP_E_UNSUP, "blp_examples_parse: duplicate business key");
   return BLP_OK;
 }
 
@@ -263,15 +393,30 @@ int blp_examples_parse(const char* path, blp_examples** out) {
     return fail(BLP_E_ARG, "blp_examples_parse: stat failed");
   }
   auto* x = new blp_examples();
-  x->text.resize((size_t)st.st_size);
-  size_t got = 0;
-  while (got < x->text.size()) {
-    const ssize_t r = read(fd, &x->text[got], x->text.size() - got);
-    if (r <= 0) break;
-    got += (size_t)r;
+  const size_t n = (size_t)st.st_size;
+  x->text.p.reset(new char[std::max<size_t>(n, 1)]);
+  x->text.n = n;
+  // read in slices of >= 8 MiB on up to 16 threads (a 100 MB examples.json: ~4x one read())
+  const size_t nt = std::max<size_t>(1, std::min<size_t>({16, std::thread::hardware_concurrency(), n >> 23}));
+  std::vector<uint8_t> rok(nt, 0);
+  auto slice = [&](size_t t) {
+    size_t at = n * t / nt;
+    const size_t to = n * (t + 1) / nt;
+    while (at < to) {
+      const ssize_t r = pread(fd, x->text.p.get() + at, to - at, (off_t)at);
+      if (r <= 0) return;
+      at += (size_t)r;
+    }
+    rok[t] = 1;
+  };
+  {
+    std::vector<std::thread> th;
+    for (size_t t = 1; t < nt; ++t) th.emplace_back(slice, t);
+    slice(0);
+    for (auto& h : th) h.join();
   }
   close(fd);
-  if (got != x->text.size()) {
+  if (std::count(rok.begin(), rok.end(), 1) != (long)nt) {
     delete x;
     return fail(BLP_E_ARG, "blp_examples_parse: short read");
   }
