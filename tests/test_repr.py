@@ -65,4 +65,5 @@ def test_device_repr_equals_host(gpu):
         got = dout.cpu().numpy().reshape(-1, 24)
         want = scorefile.format_repr(v, zero_int=bool(zero_int))
         assert np.array_equal(got, want)
-    assert scorefile.slot_strings(got[:3]) == [repr(x) for x in v[:3].tolist()]
+        if not zero_int:
+            assert scorefile.slot_strings(got[:1000]) == [repr(x) for x in v[:1000].tolist()]
