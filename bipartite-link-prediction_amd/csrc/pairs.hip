@@ -1706,7 +1706,11 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
   // each source right after its last scan, interleaved with its output stores and ordered by the
   // barrier that ends them -- so a source starts its build on a clean bitmap with no zeroing pass
   // and no barrier of its own in front of it.
+#ifdef BLP_EXP_NOCLEAN  // experiment build: the round-3 order (zero before each build)
+  const bool clean_after = false;
+#else
   const bool clean_after = SHORT && nchunks == 1;
+#endif
   const int nw4_u = (int)((((span + 31) >> 5) + 3) >> 2);
   if (clean_after)
     for (int i = threadIdx.x; i < nw4_u; i += BLOCK) bm4[i] = make_uint4(0, 0, 0, 0);  // before the first barrier
@@ -3517,6 +3521,9 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   a.all_coded = coded && std::lower_bound(g->h_uncoded.begin(), g->h_uncoded.end(), (int32_t)b->lo) ==
                              std::lower_bound(g->h_uncoded.begin(), g->h_uncoded.end(),
                                               (int32_t)std::min<int64_t>(b->hi, INT32_MAX));
+#ifdef BLP_EXP_ESC  // experiment build: always the escape-testing scan
+  a.all_coded = 0;
+#endif
 
   a.off = b->off.as<int32_t>();
   a.cnt = b->cnt.as<int32_t>();

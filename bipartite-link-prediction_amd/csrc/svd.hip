@@ -756,7 +756,11 @@ static int svd_topk_enqueue(blp_svd* h, const int32_t* d_users, int64_t n_users,
   }
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, waves * 64, 0) != hipSuccess || per_cu < 1) per_cu = 1;
-  int n_chunks = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)h->n_cu * per_cu / ublocks, h->ncol_pad / 256));
+  // (capped so the merge ranks at most TK_MERGE_CAP partial entries per user in LDS: a 64-user
+  // call would otherwise cut 200K columns into ~780 chunks and the merge rank 15.6K entries per
+  // user in place, O(n^2): 100 ms for a 4 us top-k)
+  int n_chunks = (int)std::max<int64_t>(
+      1, std::min<int64_t>({(int64_t)h->n_cu * per_cu / ublocks, h->ncol_pad / 256, (int64_t)(TK_MERGE_CAP / topk)}));
   const int64_t chunk = ((h->n_cols + n_chunks - 1) / n_chunks + 15) / 16 * 16;
   n_chunks = (int)((h->n_cols + chunk - 1) / chunk);
   {
