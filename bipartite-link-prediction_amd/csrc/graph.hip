@@ -8,6 +8,7 @@
 #include <cmath>
 #include <cstring>
 #include <mutex>
+#include <thread>
 #include <unordered_map>
 
 #include <chrono>
@@ -149,8 +150,23 @@ int build_weight_codes(blp_graph* g, const int64_t* row_ptr, const std::vector<l
   BLP_HIP(hipMalloc(&g->d_wtab, sizeof(long long) * 256));  // always: code 0 reads wtab[0]
   BLP_HIP(hipMemcpy(g->d_wtab, wtab.data(), sizeof(long long) * 256, hipMemcpyHostToDevice));
   if (max_codes <= 0 || nnz == 0) return BLP_OK;
+  // occurrences per distinct weight, node slices on up to 16 threads (a handful of distinct
+  // weights: each thread's table stays small), then merged
+  const int nt = (int)std::max<int64_t>(1, std::min<int64_t>({16, (int64_t)std::thread::hardware_concurrency(), n >> 16}));
+  std::vector<std::unordered_map<long long, int64_t>> part_uses((size_t)nt);
+  auto par = [&](auto fn) {
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) th.emplace_back(fn, t);
+    fn(0);
+    for (auto& h : th) h.join();
+  };
+  par([&](int t) {
+    auto& m = part_uses[t];
+    for (int64_t i = n * t / nt, e = n * (t + 1) / nt; i < e; ++i) m[fx[i]] += row_ptr[i + 1] - row_ptr[i];
+  });
   std::unordered_map<long long, int64_t> uses;
-  for (int64_t i = 0; i < n; ++i) uses[fx[i]] += row_ptr[i + 1] - row_ptr[i];
+  for (const auto& m : part_uses)
+    for (const auto& kv : m) uses[kv.first] += kv.second;
   std::vector<std::pair<int64_t, long long>> order;
   order.reserve(uses.size());
   for (const auto& kv : uses)
@@ -162,14 +178,18 @@ int build_weight_codes(blp_graph* g, const int64_t* row_ptr, const std::vector<l
     code[order[j].second] = (int)j + 1;
   }
   std::vector<uint8_t> ncode((size_t)n, 0);
+  std::vector<std::vector<int32_t>> part_unc((size_t)nt);
+  par([&](int t) {
+    for (int64_t i = n * t / nt, e = n * (t + 1) / nt; i < e; ++i) {
+      const auto it = code.find(fx[i]);
+      if (it != code.end())
+        ncode[i] = (uint8_t)it->second;
+      else if (row_ptr[i + 1] > row_ptr[i])
+        part_unc[t].push_back((int32_t)i);  // its weight is gathered (code 0): scans over it test for escapes
+    }
+  });
   g->h_uncoded.clear();
-  for (int64_t i = 0; i < n; ++i) {
-    const auto it = code.find(fx[i]);
-    if (it != code.end())
-      ncode[i] = (uint8_t)it->second;
-    else if (row_ptr[i + 1] > row_ptr[i])
-      g->h_uncoded.push_back((int32_t)i);  // its weight is gathered (code 0): scans over it test for escapes
-  }
+  for (const auto& v : part_unc) g->h_uncoded.insert(g->h_uncoded.end(), v.begin(), v.end());
   uint8_t* d_ncode = nullptr;
   BLP_HIP(hipMemcpy(g->d_wtab, wtab.data(), sizeof(long long) * 256, hipMemcpyHostToDevice));
   BLP_HIP(hipMalloc(&g->d_ci_w, sizeof(int32_t) * (nnz + 2 * CI_PAD)));
