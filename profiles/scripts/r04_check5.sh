@@ -8,6 +8,11 @@ set -o pipefail
 R=$GRAFT_REPO_ROOT
 cd $R || exit 1
 mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests/test_gpu_similarity.py tests/test_gpu_headline.py tests/test_gpu_svd.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r04c5_gputest.log 2>&1 || { tail -40 gpurun_out/r04c5_gputest.log; exit 1; }
+tail -1 gpurun_out/r04c5_gputest.log
+BLP_GRAPH_PROF=1 timeout -k 10 300 python bench.py --mode e2e --config c2 > gpurun_out/r04c5_e2e.json 2> gpurun_out/r04c5_e2e.err || { tail -20 gpurun_out/r04c5_e2e.err; exit 1; }
+python -c "import json;d=json.loads(open('gpurun_out/r04c5_e2e.json').read().strip().splitlines()[-1]);print('e2e', d['e2e_s'], d['phases_s'], d['graph_phase_detail_s'], d['ok'])"
+grep -E "graph_finish" gpurun_out/r04c5_e2e.err | tail -8
 bash profiles/scripts/r04_prof.sh r04_svd_c4 --mode svd || { echo "svd profile failed"; exit 1; }
 head -8 gpurun_out/r04_svd_c4.md
 timeout -k 10 300 python bench.py --mode svd > gpurun_out/r04c5_svd.json 2> gpurun_out/r04c5_svd.err || { tail -20 gpurun_out/r04c5_svd.err; exit 1; }
