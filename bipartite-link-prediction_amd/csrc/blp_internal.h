@@ -150,7 +150,6 @@ struct blp_graph {
   std::vector<unsigned long long> h_w2;
   std::vector<int32_t> h_lo2, h_hi2, h_maxd;
   std::vector<uint8_t> h_flag2;
-  std::vector<int32_t> h_uncoded;  // nodes of nonzero degree without a weight code (ascending; graph.hip)
   // wedge-row bitmaps (hop3.hip, blp::wedge_bitmaps): the SET of ids of each long wedge row over
   // an id range [lo, hi), built on first use per range (the hop-3 mark range; the business
   // batch's universe) and kept with the graph (at most 4 ranges)

@@ -178,18 +178,12 @@ int build_weight_codes(blp_graph* g, const int64_t* row_ptr, const std::vector<l
     code[order[j].second] = (int)j + 1;
   }
   std::vector<uint8_t> ncode((size_t)n, 0);
-  std::vector<std::vector<int32_t>> part_unc((size_t)nt);
   par([&](int t) {
     for (int64_t i = n * t / nt, e = n * (t + 1) / nt; i < e; ++i) {
       const auto it = code.find(fx[i]);
-      if (it != code.end())
-        ncode[i] = (uint8_t)it->second;
-      else if (row_ptr[i + 1] > row_ptr[i])
-        part_unc[t].push_back((int32_t)i);  // its weight is gathered (code 0): scans over it test for escapes
+      if (it != code.end()) ncode[i] = (uint8_t)it->second;
     }
   });
-  g->h_uncoded.clear();
-  for (const auto& v : part_unc) g->h_uncoded.insert(g->h_uncoded.end(), v.begin(), v.end());
   uint8_t* d_ncode = nullptr;
   BLP_HIP(hipMemcpy(g->d_wtab, wtab.data(), sizeof(long long) * 256, hipMemcpyHostToDevice));
   BLP_HIP(hipMalloc(&g->d_ci_w, sizeof(int32_t) * (nnz + 2 * CI_PAD)));

@@ -1256,7 +1256,7 @@ __device__ __attribute__((always_inline)) inline void rc_build(const int32_t* __
 // 64-bit sum. Valid while cn < 2^PK_CN_BITS (a chunk holds < 2^21 nodes) : each step's high part
 // undercounts S by < 2^40 + K * 2^32, so S - hi * 2^40 < cn * 2^41 < 2^64 (blp::aa_exact, hs = 40).
 
-template <int NT, int K, bool AA, bool ESC = true>
+template <int NT, int K, bool AA>
 __device__ __attribute__((always_inline)) inline void rc_scan(const int32_t* __restrict__ ci, uint32_t idmask, int idbits,
                                const long long* __restrict__ aaw, const long long* wtab, const int64_t* s_start,
                                const int32_t* s_off, const int32_t* s_coff, int ns, int64_t c0, int64_t width,
@@ -1286,19 +1286,8 @@ __device__ __attribute__((always_inline)) inline void rc_scan(const int32_t* __r
     for (int k = 0; k < K; ++k) hm |= ((wd[k] >> (rr[k] & 31)) & 1u) << k;
     if (hm) {
       if (AA) {
-        unsigned long long acc = 0;
-        if (!ESC && packed) {
-          // every id of the scan universe carries its weight's code (ESC false: the batch's
-          // range holds no code-0 node): no escape test, and the high field is the step sum's
-          // own >> PK_HS -- K <= 16 terms of W < 2^59 sum below 2^63, and each step undercounts
-          // S by < 2^PK_HS, so S - hi * 2^PK_HS < cn * 2^PK_HS (blp::aa_exact)
-#pragma unroll
-          for (int k = 0; k < K; ++k) acc += ((hm >> k) & 1u) ? (unsigned long long)wt[k] : 0ull;
-          atomicAdd(&s_aa[2 * st.s], acc);
-          atomicAdd(&s_aa[2 * st.s + 1], ((acc >> PK_HS) << PK_CN_BITS) | (unsigned)__popc(hm));
-          return;
-        }
         // the step's high words fit 32 bits: K <= 16 terms of W >> 32 < 2^27 (W < 2^59)
+        unsigned long long acc = 0;
         uint32_t esc = 0, acch = 0;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
@@ -1620,7 +1609,6 @@ struct ScoreArgs {
   int64_t nnz, wedge_vecs;      // CSR entries, wedge-row vectors (BLP_DEBUG bounds)
   int64_t n_hot, hot_vecs;      // dense rows, their pool's vectors (BLP_DEBUG bounds)
   int lq_wgs;                   // workgroups d_lq was sized for (BLP_DEBUG bound)
-  int all_coded;                // 1: every node of [lo, hi) carries a weight code (no code-0 gathers); 0: unknown
 };
 
 template <int BLOCK>
@@ -1702,18 +1690,6 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
   const bool packed = RC && want_a && nchunks == 1 && !(a.short_rows & 2) && CAP_BITS < (1 << PK_CN_BITS);
   uint4* bm4 = reinterpret_cast<uint4*>(bm);
   const int n_active = a.misc->n_active;
-  // Short-row scorer on a one-chunk universe: the bitmap is zeroed once here, and afterwards by
-  // each source right after its last scan, interleaved with its output stores and ordered by the
-  // barrier that ends them -- so a source starts its build on a clean bitmap with no zeroing pass
-  // and no barrier of its own in front of it.
-#ifdef BLP_EXP_NOCLEAN  // experiment build: the round-3 order (zero before each build)
-  const bool clean_after = false;
-#else
-  const bool clean_after = SHORT && nchunks == 1;
-#endif
-  const int nw4_u = (int)((((span + 31) >> 5) + 3) >> 2);
-  if (clean_after)
-    for (int i = threadIdx.x; i < nw4_u; i += BLOCK) bm4[i] = make_uint4(0, 0, 0, 0);  // before the first barrier
 
   PROF_INIT
   // dequeue one ahead: the next source's atomic is in flight while this one is scored
@@ -1838,7 +1814,7 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
               const int q = threadIdx.x + j * BLOCK;
               if (q < nw4) bm4[q] = acc[j];
             }
-          } else if (!clean_after) {
+          } else {
             for (int q = threadIdx.x; q < nw4; q += BLOCK) {
               uint4 v = make_uint4(0, 0, 0, 0);
               for (int r = 0; r < nhot; ++r) {
@@ -1854,7 +1830,7 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
               bm4[q] = v;
             }
           }
-          if (!clean_after) __syncthreads();  // (uniform)
+          __syncthreads();
           PROF(2)
           if (SHORT && a.wp) {
             // N(N(x)) from x's wedge row: one contiguous range, two 16-byte vectors per thread
@@ -1968,10 +1944,7 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
           } else if (RC) {
             rc_chunk_offsets<BLOCK, K>(s_off, ns, s_coff, red);
             const int shift = build_hint<BLOCK, HC>(s_coff, ns, BLOCK, s_hint);
-            if (want_a && packed && a.all_coded)
-              rc_scan<BLOCK, K, true, false>(a.cw, a.idmask, a.idbits, a.aaw, s_wtab, s_start, s_off, s_coff, ns, c0,
-                                             width, bm, CAP_WORDS, s_cn, s_aa, threadIdx.x, s_hint, shift, true);
-            else if (want_a)
+            if (want_a)
               rc_scan<BLOCK, K, true>(a.cw, a.idmask, a.idbits, a.aaw, s_wtab, s_start, s_off, s_coff, ns, c0, width,
                                       bm, CAP_WORDS, s_cn, s_aa, threadIdx.x, s_hint, shift, packed);
             else
@@ -1997,8 +1970,6 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
           }
           __syncthreads();
           PROF(7)
-          if (clean_after && sb + SEG >= pcnt)  // the last scan is done: clean for the next source
-            for (int i = threadIdx.x; i < nw4; i += BLOCK) bm4[i] = make_uint4(0, 0, 0, 0);
           for (int t = threadIdx.x; t < ns; t += BLOCK) {  // ns <= SEG <= BLOCK: t == threadIdx.x
             const int p = pout;
             if (!PS_OK(a.misc, p >= 0 && p < a.np, 4, p, a.np)) continue;
@@ -2032,10 +2003,6 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
           }
           __syncthreads();
           PROF(8)
-        }
-        if (clean_after && pcnt == 0) {  // (uniform) no scan to clean after
-          for (int i = threadIdx.x; i < nw4; i += BLOCK) bm4[i] = make_uint4(0, 0, 0, 0);
-          __syncthreads();
         }
       }
     }
@@ -2389,14 +2356,6 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
       if (want_a) {
         unsigned long long sh, sl;
         blp::aa_exact(w0, w1 >> PK_CN_BITS, &sh, &sl, PK_HS);
-#ifdef BLP_EXP_L2ATOM  // experiment only (wrong when a source's chunks span XCDs): atomics in L2
-        if (pk24) {
-          __hip_atomic_fetch_add(&paa[2 * gp], sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          __hip_atomic_fetch_add(&paa[2 * gp + 1], (((sh << 12) | (sl >> 52)) << SPLIT_CN_BITS) | c_t,
-                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          return;
-        }
-#endif
         atomicAdd(&paa[2 * gp], sl);
         if (pk24) {
           atomicAdd(&paa[2 * gp + 1], (((sh << 12) | (sl >> 52)) << SPLIT_CN_BITS) | c_t);
@@ -3517,13 +3476,6 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   a.idbits = coded ? g->id_bits : 31;
   a.idmask = (uint32_t)((1ull << a.idbits) - 1);
   a.wtab = g->d_wtab;
-  // no code-0 node in the universe: the escape-free packed scan (rc_scan ESC = false)
-  a.all_coded = coded && std::lower_bound(g->h_uncoded.begin(), g->h_uncoded.end(), (int32_t)b->lo) ==
-                             std::lower_bound(g->h_uncoded.begin(), g->h_uncoded.end(),
-                                              (int32_t)std::min<int64_t>(b->hi, INT32_MAX));
-#ifdef BLP_EXP_ESC  // experiment build: always the escape-testing scan
-  a.all_coded = 0;
-#endif
 
   a.off = b->off.as<int32_t>();
   a.cnt = b->cnt.as<int32_t>();

@@ -125,14 +125,12 @@ def score_both_sides(examples, G, u_mask, b_mask):
     return _score_both_ids(G, u_ids, v_ids, u_mask, b_mask)
 
 
-def _score_both_ids(G, u_ids, v_ids, u_mask, b_mask, timings=None, text=False, keep=False):
+def _score_both_ids(G, u_ids, v_ids, u_mask, b_mask, timings=None, text=False):
     """Id lookup, the two batches (created concurrently: blp_batch_create's host planning
     releases the GIL), one concurrent device step, and the results; phase times into
     ``timings`` (score_lookup, score_create, score_device, score_fetch) when given. ``text``:
     the Jaccard / Adamic-Adar scores come back as their json.dumps text, formatted on the
-    device (PairBatch.fetch_repr: "jaccard_repr" / "adamic_repr" slots), not as doubles.
-    ``keep``: return (present, user batch, business batch) right after the device step, unfetched;
-    the caller fetches and closes them."""
+    device (PairBatch.fetch_repr: "jaccard_repr" / "adamic_repr" slots), not as doubles."""
     import time
     from concurrent.futures import ThreadPoolExecutor
 
@@ -151,11 +149,6 @@ def _score_both_ids(G, u_ids, v_ids, u_mask, b_mask, timings=None, text=False, k
         G.score_batches([(ub, u_mask), (bb, b_mask)])
         blp.device_sync(G.device)  # the batches run on their own streams
         t3 = time.perf_counter()
-        if keep:
-            if timings is not None:
-                timings.update({"score_lookup": t1 - t0, "score_create": t2 - t1, "score_device": t3 - t2})
-            ub_, bb_, ub, bb = ub, bb, None, None  # handed over: not closed here
-            return present, ub_, bb_
         if text:
             res = present, _fetch_text(ub, u_mask), _fetch_text(bb, b_mask)
         else:
@@ -165,10 +158,8 @@ def _score_both_ids(G, u_ids, v_ids, u_mask, b_mask, timings=None, text=False, k
                             "score_fetch": time.perf_counter() - t3})
         return res
     finally:
-        if ub is not None:
-            ub.close()
-        if bb is not None:
-            bb.close()
+        ub.close()
+        bb.close()
 
 
 def _fetch_text(batch, mask):
@@ -179,16 +170,6 @@ def _fetch_text(batch, mask):
         res["jaccard_repr"] = batch.fetch_repr(blp.JACCARD)
     if mask & blp.ADAMIC:
         res["adamic_repr"] = batch.fetch_repr(blp.ADAMIC, zero_int=True)
-    return res
-
-
-def _fetch_text_async(pool, batch, mask):
-    """_fetch_text as one future per result: a file waits only for its own array."""
-    res = {"cn": pool.submit(lambda: batch.fetch(blp.CN)["cn"])}
-    if mask & blp.JACCARD:
-        res["jaccard_repr"] = pool.submit(batch.fetch_repr, blp.JACCARD)
-    if mask & blp.ADAMIC:
-        res["adamic_repr"] = pool.submit(batch.fetch_repr, blp.ADAMIC, True)
     return res
 
 
@@ -208,8 +189,7 @@ def _run_side(examples, G, methods, outfiles, table, side, sidecar=False, scored
 
 def _write_jobs(ex, methods, outfiles, table, present, scores):
     """The score files of one side straight from the device arrays (util.write_json's text):
-    one callable per file. ``scores``: the side's results; an entry may be a future
-    (similarity.main fetches while the first files are written)."""
+    one callable per file."""
     import os
 
     pres = None if present.all() else present
@@ -218,24 +198,18 @@ def _write_jobs(ex, methods, outfiles, table, present, scores):
         if f is None:
             continue
         bit = table.get(m, 0)
+        if bit == blp.CN:
+            args = (scorefile.U32, pres, scores["cn"])
+        elif bit == blp.JACCARD:
+            args = ((scorefile.REPR24, pres, scores["jaccard_repr"]) if "jaccard_repr" in scores
+                    else (scorefile.F64, pres, scores["jaccard"]))
+        elif bit == blp.ADAMIC:
+            args = ((scorefile.REPR24, pres, scores["adamic_repr"]) if "adamic_repr" in scores
+                    else (scorefile.F64_INT0, pres, scores["adamic"]))
+        else:  # a method the reference does not match: only missing-node zeros
+            args = (scorefile.NONE, pres)
 
-        def job(f=f, bit=bit):
-            class _Resolved(dict):  # entries may be futures (similarity.main): wait for the one used
-                def __getitem__(self, k):
-                    v = dict.__getitem__(self, k)
-                    return v.result() if hasattr(v, "result") else v
-
-            sc = _Resolved(scores)
-            if bit == blp.CN:
-                args = (scorefile.U32, pres, sc["cn"])
-            elif bit == blp.JACCARD:
-                args = ((scorefile.REPR24, pres, sc["jaccard_repr"]) if "jaccard_repr" in sc
-                        else (scorefile.F64, pres, sc["jaccard"]))
-            elif bit == blp.ADAMIC:
-                args = ((scorefile.REPR24, pres, sc["adamic_repr"]) if "adamic_repr" in sc
-                        else (scorefile.F64_INT0, pres, sc["adamic"]))
-            else:  # a method the reference does not match: only missing-node zeros
-                args = (scorefile.NONE, pres)
+        def job(f=f, args=args):
             ex.write(f, *args)
             if os.path.exists(f + ".npz"):  # as util.write_json: a stale sidecar goes
                 os.unlink(f + ".npz")
@@ -306,22 +280,15 @@ def main(example_file, graph_file, u_methods, u_outfiles, b_methods, b_outfiles,
         if ex is None:
             present, u_scores, b_scores = score_both_sides(examples, G, *masks)
         else:
-            present, ub, bb = _score_both_ids(G, ex.pair_user, ex.pair_business, *masks, timings=timings, keep=True)
+            present, u_scores, b_scores = _score_both_ids(G, ex.pair_user, ex.pair_business, *masks, timings=timings,
+                                                          text=True)
         t_s = clock()
         if ex is None:
             _run_side(examples, G, u_methods, u_outfiles, _U_BITS, 0, sidecar, scored=(present, u_scores))
             _run_side(examples, G, b_methods, b_outfiles, dict(_B_BITS), 1, sidecar, scored=(present, b_scores))
         else:
-            # both sides' results come back (counts, device-formatted text) on two threads while
-            # the files that are ready are written; a file job waits only for its own side
-            try:
-                with ThreadPoolExecutor(4) as fp:
-                    fu, fb = _fetch_text_async(fp, ub, masks[0]), _fetch_text_async(fp, bb, masks[1])
-                    _write_files(_write_jobs(ex, u_methods, u_outfiles, _U_BITS, present, fu) +
-                                 _write_jobs(ex, b_methods, b_outfiles, _B_BITS, present, fb))
-            finally:
-                ub.close()
-                bb.close()
+            _write_files(_write_jobs(ex, u_methods, u_outfiles, _U_BITS, present, u_scores) +
+                         _write_jobs(ex, b_methods, b_outfiles, _B_BITS, present, b_scores))
     finally:
         pool.shutdown(wait=True)
         if ex is None and fut_ex.done() and fut_ex.exception() is None:
