@@ -2714,7 +2714,10 @@ enum Variant { V_SMALL = 0, V_MED = 1, V_LARGE = 2 };
 constexpr int CAP_SMALL = 4096, CAP_MED = 16384, CAP_LARGE = 33792;  // 1.08M bits: fits 160 KiB with the exact AA words
 constexpr int BLOCK_SMALL = 256, BLOCK_MED = 512, BLOCK_LARGE = 1024;
 constexpr int HS_BLOCK = 512, HS_HT = 16384;  // hash-set scorer: 64 KiB table, two workgroups per CU
-constexpr int SEG_SMALL = 256, SEG_MED = 384, SEG_LARGE = 512;  // MED: two 512-thread workgroups per CU (<= 80 KiB LDS)
+#ifndef BLP_SEG_LARGE
+#define BLP_SEG_LARGE 512  // (experiment builds override it: pairs per scan segment of the large scorer)
+#endif
+constexpr int SEG_SMALL = 256, SEG_MED = 384, SEG_LARGE = BLP_SEG_LARGE;  // MED: two 512-thread workgroups per CU (<= 80 KiB LDS)
 constexpr int SEG_MED_NOAA = 512;  // MED without Adamic-Adar (no AA words, no weight table in LDS)
 constexpr int G_BLOCK = 1024, G_SEG = 512;  // HBM-bitmap scorer
 constexpr int S_BLOCK = 1024, S_CAP = 16384, S_SEG = 512;  // chunk-parallel scorer: 64 KiB chunks, 2 blocks / CU (<= 80 KiB LDS each)

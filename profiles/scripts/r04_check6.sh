@@ -16,3 +16,4 @@ for w in 3 6 3 6; do
 done
 bash profiles/scripts/r04_prof.sh r04_c2 || { echo "c2 profile failed"; exit 1; }
 head -10 gpurun_out/r04_c2.md
+bash profiles/scripts/r04_exp3.sh
