@@ -223,7 +223,7 @@ def _write_files(jobs):
     contents are what the reference's sequential writes give; a failure raises as there."""
     from concurrent.futures import ThreadPoolExecutor
 
-    workers = max(1, int(os.environ.get("BLP_FILE_WRITERS", "3")))
+    workers = max(1, int(os.environ.get("BLP_FILE_WRITERS", "6")))  # config 2: 6 -> 0.061-0.068 s, 3 -> 0.093-0.100 s
     if workers == 1 or len(jobs) < 2:
         for j in jobs:
             j()
