@@ -1654,7 +1654,12 @@ __device__ unsigned long long g_prof[16];
 // LDS, bound the residency (BLP_SHORT_MINB workgroups per CU).
 extern __shared__ uint4 blp_dyn_lds[];
 
-template <int BLOCK, int CAP_WORDS, int SEG, int K, bool SHORT = false, bool SAA = true>
+// PKO: the large scorer for universes of <= 32 * CAP_WORDS < 2^21 nodes in one chunk whose scan
+// rows are not all short -- counts always in the packed word, so no per-pair count array, and the
+// LDS that frees holds longer scan segments (SEG_PKO pairs: one segment for a typical config-2
+// source of ~750 pairs instead of two; each segment costs its offset scans, hint table, barriers
+// and a refill of the two-step load pipeline).
+template <int BLOCK, int CAP_WORDS, int SEG, int K, bool SHORT = false, bool SAA = true, bool PKO = false>
 __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(ScoreArgs a) {
   static_assert(SEG <= BLOCK, "one pair segment per thread in the output loop");
   constexpr int NW = BLOCK / 64;
@@ -1665,7 +1670,7 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
   __shared__ int32_t s_coff[RC ? SEG + 1 : 1];
   __shared__ int64_t s_start[SEG];
   __shared__ int32_t s_off[SEG + 1];
-  __shared__ uint32_t s_cn[SEG];
+  __shared__ uint32_t s_cn[PKO ? 1 : SEG];
   __shared__ unsigned long long s_aa[SAA ? 2 * SEG : 1];  // exact AA words, interleaved (aa_push)
   __shared__ unsigned long long red64[NW];
   __shared__ int red[NW];
@@ -1674,7 +1679,7 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
   __shared__ blp::HotRow s_hot[SHORT ? 1 : HOT_LIST];
   __shared__ long long s_wtab[SAA ? 256 : 1];
   // hint table where the LDS allows it (the 64 KiB-bitmap variant keeps 2 workgroups per CU)
-  constexpr int HC = SHORT ? 1 : CAP_WORDS > 16384 ? (RC ? 1536 : 2048) : CAP_WORDS >= 16384 ? 1 : 512;
+  constexpr int HC = PKO ? 1024 : SHORT ? 1 : CAP_WORDS > 16384 ? (RC ? 1536 : 2048) : CAP_WORDS >= 16384 ? 1 : 512;
   __shared__ int32_t s_hint[HC];
 
   if (SAA && a.wtab)  // visible after the first barrier
@@ -1687,7 +1692,8 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
   const bool want_j = (a.mask & BLP_JACCARD) != 0;
   const bool want_a = SAA && (a.mask & BLP_ADAMIC) != 0;
   // packed count + high word (rc_scan): row-chunk scans of a one-chunk universe (< 2^21 nodes)
-  const bool packed = RC && want_a && nchunks == 1 && !(a.short_rows & 2) && CAP_BITS < (1 << PK_CN_BITS);
+  const bool packed = PKO || (RC && want_a && nchunks == 1 && !(a.short_rows & 2) && CAP_BITS < (1 << PK_CN_BITS));
+  static_assert(!PKO || (RC && 32ll * CAP_WORDS < (1ll << PK_CN_BITS)), "PKO: one packed chunk");
   uint4* bm4 = reinterpret_cast<uint4*>(bm);
   const int n_active = a.misc->n_active;
 
@@ -1902,7 +1908,7 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
               s_start[threadIdx.x] = pf_start;
               len = pf_len;
               pout = pf_out;
-              s_cn[threadIdx.x] = 0;
+              if (!PKO) s_cn[threadIdx.x] = 0;
               if (SAA) {
                 s_aa[2 * threadIdx.x] = 0;
                 s_aa[2 * threadIdx.x + 1] = 0;
@@ -1913,7 +1919,7 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
             s_start[threadIdx.x] = a.g_yb[gp];
             len = a.g_yl[gp];
             pout = a.g_out[gp];  // used after the scan: its latency hides behind it
-            s_cn[threadIdx.x] = 0;
+            if (!PKO) s_cn[threadIdx.x] = 0;
             if (SAA) {
               s_aa[2 * threadIdx.x] = 0;
               s_aa[2 * threadIdx.x + 1] = 0;
@@ -1949,7 +1955,7 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
                                       bm, CAP_WORDS, s_cn, s_aa, threadIdx.x, s_hint, shift, packed);
             else
               rc_scan<BLOCK, K, false>(a.cw, a.idmask, a.idbits, a.aaw, s_wtab, s_start, s_off, s_coff, ns, c0, width,
-                                       bm, CAP_WORDS, s_cn, s_aa, threadIdx.x, s_hint, shift);
+                                       bm, CAP_WORDS, s_cn, s_aa, threadIdx.x, s_hint, shift, packed);
           } else {
             const int shift = build_hint<BLOCK, HC>(s_off, ns, BLOCK * K, s_hint);
 #if BLP_PP
@@ -1973,7 +1979,7 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
           for (int t = threadIdx.x; t < ns; t += BLOCK) {  // ns <= SEG <= BLOCK: t == threadIdx.x
             const int p = pout;
             if (!PS_OK(a.misc, p >= 0 && p < a.np, 4, p, a.np)) continue;
-            unsigned c = packed ? (unsigned)(s_aa[2 * t + 1] & ((1u << PK_CN_BITS) - 1)) : s_cn[t];
+            unsigned c = packed ? (unsigned)(s_aa[2 * t + 1] & ((1u << PK_CN_BITS) - 1)) : s_cn[PKO ? 0 : t];
             if (ch > 0) c += a.cn[p];
             a.cn[p] = c;
             if (SAA && want_a && packed) {
@@ -2717,6 +2723,7 @@ constexpr int HS_BLOCK = 512, HS_HT = 16384;  // hash-set scorer: 64 KiB table, 
 #ifndef BLP_SEG_LARGE
 #define BLP_SEG_LARGE 512  // (experiment builds override it: pairs per scan segment of the large scorer)
 #endif
+constexpr int CAP_PKO = 31744, SEG_PKO = 896;  // k_score PKO: <= 1,015,808-node universes (config 2: 1M users)
 constexpr int SEG_SMALL = 256, SEG_MED = 384, SEG_LARGE = BLP_SEG_LARGE;  // MED: two 512-thread workgroups per CU (<= 80 KiB LDS)
 constexpr int SEG_MED_NOAA = 512;  // MED without Adamic-Adar (no AA words, no weight table in LDS)
 constexpr int G_BLOCK = 1024, G_SEG = 512;  // HBM-bitmap scorer
@@ -2754,6 +2761,7 @@ struct Knobs {
   bool split_nopk = false;       // BLP_SPLIT_NOPK: unpacked split partials
   int split_short = -1;          // BLP_SPLIT_SHORT: register-scanned slice bound (0: off)
   int cosched_cus = -1;          // BLP_COSCHED_CUS: tuning override of the co-scheduled CU share
+  bool no_pko = false;           // BLP_NO_PKO: the large scorer's general variant instead of PKO
 };
 
 Knobs read_knobs() {
@@ -2783,6 +2791,7 @@ Knobs read_knobs() {
   k.split_nopk = on("BLP_SPLIT_NOPK");
   k.split_short = (int)num("BLP_SPLIT_SHORT", -1);
   k.cosched_cus = (int)num("BLP_COSCHED_CUS", -1);
+  k.no_pko = on("BLP_NO_PKO");
   return k;
 }
 }  // namespace
@@ -2813,6 +2822,7 @@ struct blp_batch {
   bool use_hot = false;  // some source has a dense row in N(x)
   int short_rows = 0;    // ScoreArgs::short_rows
   bool global = false;   // HBM-bitmap scorer (universe wider than LDS)
+  bool pko = false;      // the large scorer's packed-count variant (k_score PKO) takes this batch
   int split = 0;         // chunk-parallel scorer: universe cut into `split` LDS chunks, 2 workgroups / CU
   bool split_big = false;  // ... 128 KiB chunks, one workgroup per CU
   int64_t rs_lo = 0;     // first node of the split table
@@ -2869,11 +2879,11 @@ static int variant_occupancy(int v, int* per_cu) {
   return score_occupancy<BLOCK_LARGE, CAP_LARGE, SEG_LARGE>(per_cu);
 }
 
-template <int BLOCK, int CAP, int SEG, bool SAA = true>
+template <int BLOCK, int CAP, int SEG, bool SAA = true, bool PKO = false>
 static int launch_score(blp_graph* g, hipStream_t st, const ScoreArgs& a, int per_cu, int cus) {
   if (cus <= 0 || cus > g->n_cu) cus = g->n_cu;
   const dim3 grid(cus * per_cu), block(BLOCK);
-  hipLaunchKernelGGL((k_score<BLOCK, CAP, SEG, 8, false, SAA>), grid, block, 0, st, a);
+  hipLaunchKernelGGL((k_score<BLOCK, CAP, SEG, 8, false, SAA, PKO>), grid, block, 0, st, a);
   BLP_HIP(hipGetLastError());
   return BLP_OK;
 }
@@ -3069,6 +3079,10 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   // (BLP_NO_GLOBAL keeps the chunked path, BLP_FORCE_GLOBAL selects HBM on any universe)
   b->global = !b->split && ((b->chunks > 1 && !kn.no_global) || kn.force_global);
   if (b->global) b->chunks = 1;
+  // the large scorer's packed-count variant: one chunk of <= 32 * CAP_PKO nodes, and scan rows not
+  // all short (those take row_scan, which counts per pair)
+  b->pko = b->variant == V_LARGE && !b->split && !b->global && b->chunks == 1 && span <= 32ll * CAP_PKO &&
+           !(b->short_rows & 2) && !kn.no_pko;
   auto bail = [&](int rc) {
     blp_batch_destroy(b);
     return rc;
@@ -3579,7 +3593,10 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
     else if (b->variant == V_MED)
       rc = (mask & BLP_ADAMIC) ? launch_score<BLOCK_MED, CAP_MED, SEG_MED>(g, b->stream, a, per_cu, b->cus)
                                : launch_score<BLOCK_MED, CAP_MED, SEG_MED_NOAA, false>(g, b->stream, a, per_cu, b->cus);
-    else
+    else if (b->pko) {
+      a.cap_bits = std::min<int64_t>(a.cap_bits, 32ll * CAP_PKO);
+      rc = launch_score<BLOCK_LARGE, CAP_PKO, SEG_PKO, true, true>(g, b->stream, a, per_cu, b->cus);
+    } else
       rc = launch_score<BLOCK_LARGE, CAP_LARGE, SEG_LARGE>(g, b->stream, a, per_cu, b->cus);
     if (rc) return rc;
   }
