@@ -1182,7 +1182,7 @@ def main():
     xs, ys = (ex_x, ex_y) if name0 == "user" else (ex_y, ex_x)
     byts = alg_bytes(G, xs, ys, mask0, cn0)
     sec = ktimes[name0]["score_ms"] / 1e3
-    kname = "k_score<1024, 33792, 512, 8, false, true>" if bt0.plan()["block"] == 1024 else "k_score_wave<2, 3328, 8>"
+    kname = bt0.kernel(mask0)
     out["roofline"] = {"bound": "hbm", "achieved": byts / sec / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                        "frac": byts / sec / 1e9 / HBM_PEAK_GBS,
                        # the counters' HBM-side bytes over the same kernel time: what DRAM actually moved

@@ -72,6 +72,7 @@ SIGNATURES = {
     "blp_batches_score": [_P, _I32, _P, _P],
     "blp_batch_fetch": [_P, _P, _P, _P, _P],
     "blp_batch_fetch_repr": [_P, _P, _I32, _I32, _P],
+    "blp_batch_kernel": [_P, _U32, _P, _I32],
     "blp_repr_format": [_P, _I64, _I32, _P],
     "blp_repr_format_device": [_I32, _P, _I64, _I32, _P],
     "blp_batch_destroy": [_P],

@@ -474,6 +474,12 @@ class PairBatch:
     def score(self, mask=7):
         check(lib().blp_batch_score(self.graph.handle, self.handle, mask))
 
+    def kernel(self, mask=7):
+        """The scorer kernel's template instance, as rocprofv3 names it (blp_batch_kernel)."""
+        buf = ctypes.create_string_buffer(128)
+        check(lib().blp_batch_kernel(self.handle, mask, buf, len(buf)))
+        return buf.value.decode()
+
     def stats(self, which=0):
         """(total ms, launches) of this batch's scorer (0) or grouping (1) kernels."""
         ms = ctypes.c_double(0)

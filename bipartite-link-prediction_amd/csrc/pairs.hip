@@ -3311,6 +3311,29 @@ int blp_batch_plan(const blp_batch* b, int64_t* lo, int64_t* hi, int* chunks, in
   return BLP_OK;
 }
 
+int blp_batch_kernel(const blp_batch* b, uint32_t mask, char* name, int cap) {
+  BLP_CHECK(b && name && cap > 0, BLP_E_ARG, "blp_batch_kernel: bad arguments");
+  const bool aa = (mask & BLP_ADAMIC) != 0;
+  char buf[96];
+  if (b->global)
+    snprintf(buf, sizeof buf, "k_score_global<%d, %d, 8>", G_BLOCK, G_SEG);
+  else if (b->split)
+    snprintf(buf, sizeof buf, "k_score_split<%d, %d, %d, 8>", S_BLOCK, b->split_big ? S_CAP_BIG : S_CAP, S_SEG);
+  else if (b->use_short)
+    snprintf(buf, sizeof buf, "k_score<%d, %d, %d, 8, true, %s>", BLOCK_SMALL, CAP_SMALL, SEG_SMALL, aa ? "true" : "false");
+  else if (b->variant == V_SMALL)
+    snprintf(buf, sizeof buf, "k_score<%d, %d, %d, 8, false, true>", BLOCK_SMALL, CAP_SMALL, SEG_SMALL);
+  else if (b->variant == V_MED)
+    snprintf(buf, sizeof buf, "k_score<%d, %d, %d, 8, false, %s>", BLOCK_MED, CAP_MED, aa ? SEG_MED : SEG_MED_NOAA,
+             aa ? "true" : "false");
+  else if (b->pko)
+    snprintf(buf, sizeof buf, "k_score<%d, %d, %d, 8, false, true, true>", BLOCK_LARGE, CAP_PKO, SEG_PKO);
+  else
+    snprintf(buf, sizeof buf, "k_score<%d, %d, %d, 8, false, true>", BLOCK_LARGE, CAP_LARGE, SEG_LARGE);
+  snprintf(name, (size_t)cap, "%s", buf);
+  return BLP_OK;
+}
+
 int blp_batch_routes(const blp_batch* b, int64_t* n_sources, int64_t* n_hash, int* runs, int* wedge_bitmaps) {
   BLP_CHECK(b, BLP_E_ARG, "blp_batch_routes: null batch");
   if (n_sources) *n_sources = b->n_sources;

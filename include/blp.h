@@ -259,6 +259,10 @@ int blp_batch_plan(const blp_batch* b, int64_t* lo, int64_t* hi, int* chunks, in
  * batches; else 0), 1 if the pairs arrive grouped by source (run-head grouping), and 1 if long
  * sources copy the graph's wedge-row bitmaps as pre-built H2 sets (short-row batches).      */
 int blp_batch_routes(const blp_batch* b, int64_t* n_sources, int64_t* n_hash, int* runs, int* wedge_bitmaps);
+/* The scorer kernel blp_batch_score launches for this batch under `mask`, as its template
+ * instance reads in a rocprofv3 trace (e.g. "k_score<1024, 31744, 896, 8, false, true, true>"),
+ * NUL-terminated into name[cap]: what bench.py prices and looks up in the committed profiles. */
+int blp_batch_kernel(const blp_batch* b, uint32_t mask, char* name, int cap);
 
 /* Per-batch device time of the last/accumulated blp_batch_score calls (HIP events on the
  * batch stream): which 0 = scorer kernel, 1 = grouping kernels. Reset with blp_batch_stats_reset. */

@@ -16,3 +16,6 @@ ab() {  # name, env...
 ab pko1 BLP_X=0 && ab gen1 BLP_NO_PKO=1 && ab pko2 BLP_X=0 && ab gen2 BLP_NO_PKO=1 && ab pko3 BLP_X=0 && ab gen3 BLP_NO_PKO=1 || exit 1
 timeout -k 10 300 python bench.py > gpurun_out/r04c7_bench.json 2> gpurun_out/r04c7_bench.err || { tail -20 gpurun_out/r04c7_bench.err; exit 1; }
 python -c "import json;d=json.load(open('gpurun_out/r04c7_bench.json'));print('bench', round(d['ms_per_step'],3), d['value'], d['kernels_ms'], d['parity']['ok'], d['roofline']['kernel'])"
+bash profiles/scripts/r04_prof.sh r04_v7_bench || { echo "c2 profile failed"; exit 1; }
+head -8 gpurun_out/r04_v7_bench.md
+grep -A18 "31744" gpurun_out/r04_v7_bench_pmc.txt | head -20
