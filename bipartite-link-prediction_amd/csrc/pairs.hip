@@ -671,8 +671,10 @@ __global__ __launch_bounds__(GB_BLOCK) void k_active_write(const int32_t* __rest
 }
 
 // ------------------------------------------------------------------ segment machinery
-// Exclusive scan of one int per thread over the block (values of threads >= n are 0).
-template <int BLOCK>
+// Exclusive scan of one int per thread over the block (values of threads >= n are 0). TAIL = false
+// drops the closing barrier (it only keeps red from being rewritten while other waves still read
+// it): for callers that write their results and reach a barrier before red's next use.
+template <int BLOCK, bool TAIL = true>
 __device__ inline int block_exscan(int v, int* red, int* total) {
   constexpr int NW = BLOCK / 64;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -691,7 +693,7 @@ __device__ inline int block_exscan(int v, int* red, int* total) {
     base += w < wid ? t : 0;
     tot += t;
   }
-  __syncthreads();
+  if (TAIL) __syncthreads();
   *total = tot;
   return base + inc - v;
 }
@@ -1329,7 +1331,7 @@ template <int BLOCK, int K>
 __device__ __attribute__((always_inline)) inline void rc_chunk_offsets(const int32_t* s_off, int ns, int32_t* s_coff, int* red) {
   const int nc = (int)threadIdx.x < ns ? (s_off[threadIdx.x + 1] - s_off[threadIdx.x] + K - 1) / K : 0;
   int tot;
-  const int ex = block_exscan<BLOCK>(nc, red, &tot);
+  const int ex = block_exscan<BLOCK, false>(nc, red, &tot);  // (the barrier below ends red's use)
   if ((int)threadIdx.x < ns) s_coff[threadIdx.x] = ex;
   if (threadIdx.x == 0) s_coff[ns] = tot;
   __syncthreads();
@@ -1470,7 +1472,7 @@ __device__ __attribute__((always_inline)) inline void load_row_segments(const in
     len = (skip && skip[z] >= 0) ? 0 : (int)(rp[z + 1] - st);  // dense rows were OR-ed in already
   }
   int tot;
-  const int ex = block_exscan<BLOCK>(len, red, &tot);
+  const int ex = block_exscan<BLOCK, false>(len, red, &tot);  // (the barrier below ends red's use)
   if ((int)threadIdx.x < ns) s_off[threadIdx.x] = ex;
   if (threadIdx.x == 0) s_off[ns] = tot;
   __syncthreads();
@@ -1611,7 +1613,7 @@ struct ScoreArgs {
   int lq_wgs;                   // workgroups d_lq was sized for (BLP_DEBUG bound)
 };
 
-template <int BLOCK>
+template <int BLOCK, bool TAIL = true>  // TAIL: see block_exscan
 __device__ inline unsigned long long block_sum_u64(unsigned long long v, unsigned long long* red) {
   constexpr int NW = BLOCK / 64;
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -1621,7 +1623,7 @@ __device__ inline unsigned long long block_sum_u64(unsigned long long v, unsigne
   unsigned long long t = 0;
 #pragma unroll
   for (int w = 0; w < NW; ++w) t += red[w];
-  __syncthreads();
+  if (TAIL) __syncthreads();
   return t;
 }
 
@@ -1674,7 +1676,7 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
   __shared__ unsigned long long s_aa[SAA ? 2 * SEG : 1];  // exact AA words, interleaved (aa_push)
   __shared__ unsigned long long red64[NW];
   __shared__ int red[NW];
-  __shared__ int s_src;
+  __shared__ int s_src[2];  // the claimed source, alternating slots (no barrier guards its rewrite)
   __shared__ int s_nhot;
   __shared__ blp::HotRow s_hot[SHORT ? 1 : HOT_LIST];
   __shared__ long long s_wtab[SAA ? 256 : 1];
@@ -1700,15 +1702,16 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
   PROF_INIT
   // dequeue one ahead: the next source's atomic is in flight while this one is scored
   int nxt = threadIdx.x == 0 ? atomicAdd(&a.misc->queue, a.dq) : 0;
-  for (;;) {
+  if (!SHORT && threadIdx.x == 0) s_nhot = 0;  // (reset again after each use, before a barrier)
+  for (int it = 0;; ++it) {
     int s_first;
+    // slot it & 1 is rewritten two claims later, after this claim's barriers: one barrier here
     if (threadIdx.x == 0) {
-      s_src = nxt;
+      s_src[it & 1] = nxt;
       if (nxt < n_active) nxt = atomicAdd(&a.misc->queue, a.dq);
     }
     __syncthreads();
-    s_first = s_src;
-    __syncthreads();
+    s_first = s_src[it & 1];
     if (s_first >= n_active) break;
     PROF(0)
     const int s_last = min(n_active, s_first + a.dq);
@@ -1775,8 +1778,7 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
           // 1. the dense rows of N(x) initialise the bitmap (their OR, 16-byte vectors), then
           // 2. the sparse rows mark N(N(x)) ∩ [c0, c1) through merge-path row segments
           if constexpr (!SHORT) {  // short rows are never dense: the bitmap is only zeroed
-            if (threadIdx.x == 0) s_nhot = 0;
-            __syncthreads();
+            // (s_nhot is 0 here: set before the loop and after each use below)
             if (a.hot_idx) {
               for (int64_t k = xb + threadIdx.x; k < xe; k += BLOCK) {
                 const int hi = a.hot_idx[a.ci[k]];
@@ -1837,6 +1839,7 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
             }
           }
           __syncthreads();
+          if (!SHORT && threadIdx.x == 0) s_nhot = 0;  // s_hot / s_nhot are read: ready for the next detection
           PROF(2)
           if (SHORT && a.wp) {
             // N(N(x)) from x's wedge row: one contiguous range, two 16-byte vectors per thread
@@ -1895,7 +1898,7 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
             const uint4 q = bm4[i];
             pc += __popc(q.x) + __popc(q.y) + __popc(q.z) + __popc(q.w);
           }
-          h2 += block_sum_u64<BLOCK>(pc, red64);
+          h2 += block_sum_u64<BLOCK, false>(pc, red64);  // red64's next use is past the scan's barriers
         }
         PROF(5)
         // 5. scan N(y) of every pair of x, SEG pairs at a time
@@ -1926,7 +1929,7 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
             }
           }
           int tot;
-          const int ex = block_exscan<BLOCK>(len, red, &tot);
+          const int ex = block_exscan<BLOCK, false>(len, red, &tot);  // (the barrier below ends red's use)
           if ((int)threadIdx.x < ns) s_off[threadIdx.x] = ex;
           if (threadIdx.x == 0) s_off[ns] = tot;
           __syncthreads();
