@@ -1777,11 +1777,25 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
         } else {
           // 1. the dense rows of N(x) initialise the bitmap (their OR, 16-byte vectors), then
           // 2. the sparse rows mark N(N(x)) ∩ [c0, c1) through merge-path row segments
+          // Row-chunk builds of one segment (deg(x) <= SEG): each thread's row N(z) of N(x) -- its
+          // start and length -- is read here, in the round trip of its dense-row test, and held in
+          // registers over the bitmap init, instead of N(x) and the row pointers being read again
+          // after it (two dependent round trips off every source's critical path).
+          const bool pre = !SHORT && RC && xe - xb <= SEG && !(a.short_rows & 1);  // (uniform)
+          int64_t pre_st = 0;
+          int pre_len = 0;
+          bool pre_hot = false;
           if constexpr (!SHORT) {  // short rows are never dense: the bitmap is only zeroed
             // (s_nhot is 0 here: set before the loop and after each use below)
-            if (a.hot_idx) {
-              for (int64_t k = xb + threadIdx.x; k < xe; k += BLOCK) {
-                const int hi = a.hot_idx[a.ci[k]];
+            if (a.hot_idx || pre) {
+              for (int64_t k = xb + threadIdx.x; k < xe; k += BLOCK) {  // (pre: one row per thread)
+                const int z = a.ci[k];
+                const int hi = a.hot_idx ? a.hot_idx[z] : -1;
+                if (pre) {
+                  pre_st = a.rp[z];
+                  pre_len = (int)(a.rp[z + 1] - pre_st);
+                  pre_hot = hi >= 0;
+                }
                 if (hi >= 0 && PS_OK(a.misc, hi < a.n_hot, 12, hi, a.n_hot)) {
                   const int slot = atomicAdd(&s_nhot, 1);
                   if (slot < HOT_LIST) s_hot[slot] = a.hot_tab[hi];
@@ -1859,7 +1873,17 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
           } else
           for (int64_t k0 = xb; k0 < xe; k0 += SEG) {
             const int ns = (int)min<int64_t>(SEG, xe - k0);
-            load_row_segments<BLOCK>(a.rp, a.ci, k0, ns, s_start, s_off, red, nhot ? a.hot_idx : nullptr);
+            if (pre) {  // the one segment's rows, from registers (dense rows were OR-ed in: length 0)
+              const bool mine = (int)threadIdx.x < ns;
+              if (mine) s_start[threadIdx.x] = pre_st;
+              int tot;
+              const int ex = block_exscan<BLOCK, false>(mine && !(nhot && pre_hot) ? pre_len : 0, red, &tot);
+              if (mine) s_off[threadIdx.x] = ex;
+              if (threadIdx.x == 0) s_off[ns] = tot;
+              __syncthreads();
+            } else {
+              load_row_segments<BLOCK>(a.rp, a.ci, k0, ns, s_start, s_off, red, nhot ? a.hot_idx : nullptr);
+            }
             if (SHORT || (a.short_rows & 1)) {
               row_build<BLOCK>(a.cw, a.idmask, s_start, s_off, ns, c0, width, bm, threadIdx.x);
             } else if constexpr (!SHORT) {
