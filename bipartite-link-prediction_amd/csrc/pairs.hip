@@ -1718,7 +1718,7 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
     for (int s = s_first; s < s_last; ++s) {
       int x, pbeg, pcnt, hslot;
       int64_t xb, xe, wb = 0, we = 0, nx_lo, nx_hi;
-      if constexpr (SHORT) {  // one record per source (s is uniform)
+      if (SHORT || (RC && a.rec)) {  // one record per source (s is uniform): one round trip, not two
         // uniform: kept in scalar registers (the VGPR budget of 7 workgroups per CU is tight)
         const SrcRec& r = a.rec[__builtin_amdgcn_readfirstlane(s)];
         auto u32 = [](int32_t v) { return (int32_t)__builtin_amdgcn_readfirstlane(v); };
@@ -1777,25 +1777,11 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
         } else {
           // 1. the dense rows of N(x) initialise the bitmap (their OR, 16-byte vectors), then
           // 2. the sparse rows mark N(N(x)) ∩ [c0, c1) through merge-path row segments
-          // Row-chunk builds of one segment (deg(x) <= SEG): each thread's row N(z) of N(x) -- its
-          // start and length -- is read here, in the round trip of its dense-row test, and held in
-          // registers over the bitmap init, instead of N(x) and the row pointers being read again
-          // after it (two dependent round trips off every source's critical path).
-          const bool pre = !SHORT && RC && xe - xb <= SEG && !(a.short_rows & 1);  // (uniform)
-          int64_t pre_st = 0;
-          int pre_len = 0;
-          bool pre_hot = false;
           if constexpr (!SHORT) {  // short rows are never dense: the bitmap is only zeroed
             // (s_nhot is 0 here: set before the loop and after each use below)
-            if (a.hot_idx || pre) {
-              for (int64_t k = xb + threadIdx.x; k < xe; k += BLOCK) {  // (pre: one row per thread)
-                const int z = a.ci[k];
-                const int hi = a.hot_idx ? a.hot_idx[z] : -1;
-                if (pre) {
-                  pre_st = a.rp[z];
-                  pre_len = (int)(a.rp[z + 1] - pre_st);
-                  pre_hot = hi >= 0;
-                }
+            if (a.hot_idx) {
+              for (int64_t k = xb + threadIdx.x; k < xe; k += BLOCK) {
+                const int hi = a.hot_idx[a.ci[k]];
                 if (hi >= 0 && PS_OK(a.misc, hi < a.n_hot, 12, hi, a.n_hot)) {
                   const int slot = atomicAdd(&s_nhot, 1);
                   if (slot < HOT_LIST) s_hot[slot] = a.hot_tab[hi];
@@ -1873,17 +1859,7 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
           } else
           for (int64_t k0 = xb; k0 < xe; k0 += SEG) {
             const int ns = (int)min<int64_t>(SEG, xe - k0);
-            if (pre) {  // the one segment's rows, from registers (dense rows were OR-ed in: length 0)
-              const bool mine = (int)threadIdx.x < ns;
-              if (mine) s_start[threadIdx.x] = pre_st;
-              int tot;
-              const int ex = block_exscan<BLOCK, false>(mine && !(nhot && pre_hot) ? pre_len : 0, red, &tot);
-              if (mine) s_off[threadIdx.x] = ex;
-              if (threadIdx.x == 0) s_off[ns] = tot;
-              __syncthreads();
-            } else {
-              load_row_segments<BLOCK>(a.rp, a.ci, k0, ns, s_start, s_off, red, nhot ? a.hot_idx : nullptr);
-            }
+            load_row_segments<BLOCK>(a.rp, a.ci, k0, ns, s_start, s_off, red, nhot ? a.hot_idx : nullptr);
             if (SHORT || (a.short_rows & 1)) {
               row_build<BLOCK>(a.cw, a.idmask, s_start, s_off, ns, c0, width, bm, threadIdx.x);
             } else if constexpr (!SHORT) {
@@ -3283,7 +3259,9 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   if (b->chunks > 1 && hipMalloc(&b->d_aa_part, 16 * np) != hipSuccess)
     return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: hipMalloc failed"));
   b->use_short = short_kernel(b);  // fixed here: d_rec's allocation and the launch must agree
-  if (b->use_short &&
+  // source records: the short-row scorer, and the large scorer (its header in one round trip)
+  const bool want_rec = b->use_short || (b->variant == V_LARGE && !b->split && !b->global);
+  if (want_rec &&
       hipMalloc(&b->d_rec, sizeof(SrcRec) * (size_t)std::max<int64_t>(b->n_sources, 1)) != hipSuccess)
     return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: hipMalloc failed"));
   if (hipMemset(b->d_misc, 0, sizeof(Misc)) != hipSuccess)  // dbg[] is zeroed here, not per score
@@ -3638,6 +3616,13 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   } else if (np) {
     int per_cu = 1;
     if ((rc = variant_occupancy(b->variant, &per_cu))) return rc;
+    if (b->d_rec && b->variant == V_LARGE) {  // the large scorer's source headers (after grouping)
+      hipLaunchKernelGGL(k_source_records, dim3((unsigned)std::min<int64_t>((b->n_sources + 255) / 256, 2048)),
+                         dim3(256), 0, b->stream, a.active, b->d_misc, a.off, a.cnt, g->d_rp, g->d_ci, a.heavy_slot,
+                         nullptr, b->d_rec);
+      BLP_HIP(hipGetLastError());
+      a.rec = b->d_rec;
+    }
     if (b->variant == V_SMALL)
       rc = launch_score<BLOCK_SMALL, CAP_SMALL, SEG_SMALL>(g, b->stream, a, per_cu, b->cus);
     else if (b->variant == V_MED)
