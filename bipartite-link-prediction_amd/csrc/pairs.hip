@@ -1677,7 +1677,6 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
   __shared__ unsigned long long red64[NW];
   __shared__ int red[NW];
   __shared__ int s_src[2];  // the claimed source, alternating slots (no barrier guards its rewrite)
-  __shared__ unsigned s_xcorr;  // x's own bit, counted in |H2| before it was dropped (0 / 1)
   __shared__ int s_nhot;
   __shared__ blp::HotRow s_hot[SHORT ? 1 : HOT_LIST];
   __shared__ long long s_wtab[SAA ? 256 : 1];
@@ -1883,16 +1882,14 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
         }
         PROF(3)
         // 3. exact distance 2: drop x (distance 0) and N(x) (distance 1)
-        const bool nx_in = nx_hi >= c0 && nx_lo < c1;  // (uniform)
-        const bool x_in = x >= c0 && x < c1;
-        if (nx_in) {
+        if (nx_hi >= c0 && nx_lo < c1) {
           for (int64_t k = xb + threadIdx.x; k < xe; k += BLOCK) {
             const int64_t r = (int64_t)a.ci[k] - c0;
             if (r >= 0 && r < width) atomicAnd(&bm[r >> 5], ~(1u << (r & 31)));
           }
-          if (threadIdx.x == 0 && x_in) atomicAnd(&bm[(x - c0) >> 5], ~(1u << ((x - c0) & 31)));
-          __syncthreads();
         }
+        if (threadIdx.x == 0 && x >= c0 && x < c1) atomicAnd(&bm[(x - c0) >> 5], ~(1u << ((x - c0) & 31)));
+        __syncthreads();
         PROF(4)
         // 4. |H2(x) ∩ chunk|
         if (want_j) {
@@ -1902,18 +1899,6 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
             pc += __popc(q.x) + __popc(q.y) + __popc(q.z) + __popc(q.w);
           }
           h2 += block_sum_u64<BLOCK, false>(pc, red64);  // red64's next use is past the scan's barriers
-        }
-        // N(x) outside this chunk (the other side of a bipartite graph): x alone is dropped, after
-        // the count -- the sum's barrier has ordered every popcount read -- and the count corrected
-        // by what it held; the scan reads the bitmap only behind the segment offsets' barrier, which
-        // also publishes the correction. One barrier per source fewer.
-        if (threadIdx.x == 0) {
-          unsigned corr = 0;
-          if (!nx_in && x_in) {
-            const uint32_t bit = 1u << ((x - c0) & 31);
-            corr = (atomicAnd(&bm[(x - c0) >> 5], ~bit) & bit) ? 1u : 0u;
-          }
-          s_xcorr = corr;
         }
         PROF(5)
         // 5. scan N(y) of every pair of x, SEG pairs at a time
@@ -1948,7 +1933,6 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
           if ((int)threadIdx.x < ns) s_off[threadIdx.x] = ex;
           if (threadIdx.x == 0) s_off[ns] = tot;
           __syncthreads();
-          if (sb == 0) h2 -= s_xcorr;  // (published by the barrier above)
           // the next segment's metadata, in flight during this segment's scan (BLP_PFN)
           have_pf = PF && !SHORT && BLP_PFN && nchunks == 1 && sb + SEG < pcnt;
           if (have_pf && (int)threadIdx.x < min(SEG, pcnt - sb - SEG)) {
