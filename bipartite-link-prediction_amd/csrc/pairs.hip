@@ -589,13 +589,11 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_run_write(const int32_t* __restr
                                                           const int32_t* __restrict__ tile_off, int32_t* __restrict__ active,
                                                           int32_t* __restrict__ off, int32_t* __restrict__ g_out,
                                                           int64_t* __restrict__ g_yb, int32_t* __restrict__ g_yl,
-                                                          int32_t* __restrict__ g_y, int meta) {
+                                                          int32_t* __restrict__ g_y) {
   __shared__ int red[SCAN_BLOCK / 64];
   const int64_t t0 = (int64_t)blockIdx.x * SCAN_TILE;
-  // per-pair metadata (meta = 0: the scorer reads y and its row itself -- ScoreArgs::ry), coalesced;
-  // the tile's y loads, then its row_ptr gathers, all in flight
+  // per-pair metadata, coalesced; the tile's y loads, then its row_ptr gathers, all in flight
   constexpr int PT = SCAN_TILE / SCAN_BLOCK;
-  if (meta) {
   int yv[PT];
 #pragma unroll
   for (int q = 0; q < PT; ++q) {
@@ -617,7 +615,6 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_run_write(const int32_t* __restr
       g_yl[i] = (int32_t)(en[q] - st[q]);
       if (g_y) g_y[i] = yv[q];
     }
-  }
   }
   const int64_t base = t0 + (int64_t)threadIdx.x * SCAN_ITEMS;
   bool h[SCAN_ITEMS];
@@ -1614,7 +1611,6 @@ struct ScoreArgs {
   int64_t nnz, wedge_vecs;      // CSR entries, wedge-row vectors (BLP_DEBUG bounds)
   int64_t n_hot, hot_vecs;      // dense rows, their pool's vectors (BLP_DEBUG bounds)
   int lq_wgs;                   // workgroups d_lq was sized for (BLP_DEBUG bound)
-  const int32_t* ry;            // run-grouped batches (k_score): y in caller = grouped order; null: g_yb / g_yl / g_out
 };
 
 template <int BLOCK, bool TAIL = true>  // TAIL: see block_exscan
@@ -1759,21 +1755,12 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
       int64_t pf_start = 0;
       int pf_len = 0, pf_out = 0;
       constexpr bool PF = SHORT ? BLP_PF : (RC && BLP_PFL);
-      // a pair's N(y) bounds and caller index: from the grouped metadata, or (ry: run-grouped
-      // batches, grouped order = caller order) from y and the row pointers
-      auto pair_meta = [&](int gp, int64_t& st, int& len, int& out) {
-        if (a.ry) {
-          const int yv = a.ry[gp];
-          st = a.rp[yv];
-          len = (int)(a.rp[yv + 1] - st);
-          out = gp;
-        } else {
-          st = a.g_yb[gp];
-          len = a.g_yl[gp];
-          out = a.g_out[gp];
-        }
-      };
-      if (PF && nchunks == 1 && (int)threadIdx.x < min(SEG, pcnt)) pair_meta(pbeg + threadIdx.x, pf_start, pf_len, pf_out);
+      if (PF && nchunks == 1 && (int)threadIdx.x < min(SEG, pcnt)) {
+        const int gp = pbeg + threadIdx.x;
+        pf_start = a.g_yb[gp];
+        pf_len = a.g_yl[gp];
+        pf_out = a.g_out[gp];
+      }
       PROF(1)
 
       for (int ch = 0; ch < nchunks; ++ch) {
@@ -1931,9 +1918,10 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
               }
             }
           } else if ((int)threadIdx.x < ns) {
-            int64_t st;
-            pair_meta(pbeg + sb + threadIdx.x, st, len, pout);  // pout is used after the scan: its latency hides
-            s_start[threadIdx.x] = st;
+            const int gp = pbeg + sb + threadIdx.x;
+            s_start[threadIdx.x] = a.g_yb[gp];
+            len = a.g_yl[gp];
+            pout = a.g_out[gp];  // used after the scan: its latency hides behind it
             if (!PKO) s_cn[threadIdx.x] = 0;
             if (SAA) {
               s_aa[2 * threadIdx.x] = 0;
@@ -1947,8 +1935,12 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
           __syncthreads();
           // the next segment's metadata, in flight during this segment's scan (BLP_PFN)
           have_pf = PF && !SHORT && BLP_PFN && nchunks == 1 && sb + SEG < pcnt;
-          if (have_pf && (int)threadIdx.x < min(SEG, pcnt - sb - SEG))
-            pair_meta(pbeg + sb + SEG + threadIdx.x, pf_start, pf_len, pf_out);
+          if (have_pf && (int)threadIdx.x < min(SEG, pcnt - sb - SEG)) {
+            const int gp = pbeg + sb + SEG + threadIdx.x;
+            pf_start = a.g_yb[gp];
+            pf_len = a.g_yl[gp];
+            pf_out = a.g_out[gp];
+          }
           PROF(6)
           if (SHORT || (a.short_rows & 2)) {
             if (SAA && want_a)
@@ -2773,7 +2765,6 @@ struct Knobs {
   int split_short = -1;          // BLP_SPLIT_SHORT: register-scanned slice bound (0: off)
   int cosched_cus = -1;          // BLP_COSCHED_CUS: tuning override of the co-scheduled CU share
   bool no_pko = false;           // BLP_NO_PKO: the large scorer's general variant instead of PKO
-  bool no_direct_meta = false;   // BLP_NO_DIRECT_META: run-grouped pairs get the grouped metadata arrays
 };
 
 Knobs read_knobs() {
@@ -2804,7 +2795,6 @@ Knobs read_knobs() {
   k.split_short = (int)num("BLP_SPLIT_SHORT", -1);
   k.cosched_cus = (int)num("BLP_COSCHED_CUS", -1);
   k.no_pko = on("BLP_NO_PKO");
-  k.no_direct_meta = on("BLP_NO_DIRECT_META");
   return k;
 }
 }  // namespace
@@ -2836,7 +2826,6 @@ struct blp_batch {
   int short_rows = 0;    // ScoreArgs::short_rows
   bool global = false;   // HBM-bitmap scorer (universe wider than LDS)
   bool pko = false;      // the large scorer's packed-count variant (k_score PKO) takes this batch
-  bool direct_meta = false;  // run-grouped pairs scored by k_score: it reads y and N(y)'s bounds itself
   int split = 0;         // chunk-parallel scorer: universe cut into `split` LDS chunks, 2 workgroups / CU
   bool split_big = false;  // ... 128 KiB chunks, one workgroup per CU
   int64_t rs_lo = 0;     // first node of the split table
@@ -3097,9 +3086,6 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   // all short (those take row_scan, which counts per pair)
   b->pko = b->variant == V_LARGE && !b->split && !b->global && b->chunks == 1 && span <= 32ll * CAP_PKO &&
            !(b->short_rows & 2) && !kn.no_pko;
-  // a run-grouped list's grouped order IS the caller's: k_score reads y[p] and N(y)'s bounds
-  // itself instead of a grouping pass writing 16 B of metadata per pair for it to read back
-  b->direct_meta = b->runs && !b->split && !b->global && !kn.no_direct_meta;
   auto bail = [&](int rc) {
     blp_batch_destroy(b);
     return rc;
@@ -3410,7 +3396,7 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
     hipLaunchKernelGGL(k_scan_mid, dim3(1), dim3(SCAN_BLOCK), 0, b->stream, rtile, tiles, &b->d_misc->n_active);
     hipLaunchKernelGGL(k_run_write, dim3((unsigned)tiles), dim3(SCAN_BLOCK), 0, b->stream, b->d_x, b->d_y, np, g->d_rp,
                        rtile, b->active.as<int32_t>(), b->off.as<int32_t>(), b->d_gout, b->d_gyb, b->d_gyl,
-                       b->d_gy, b->direct_meta ? 0 : 1);
+                       b->d_gy);
     hipLaunchKernelGGL(k_run_cnt, dim3(1024), dim3(256), 0, b->stream, b->active.as<int32_t>(), &b->d_misc->n_active,
                        np, b->off.as<int32_t>(), b->cnt.as<int32_t>());
   } else if (np) {
@@ -3542,7 +3528,6 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   a.g_out = b->d_gout;
   a.g_yb = b->d_gyb;
   a.g_yl = b->d_gyl;
-  a.ry = b->direct_meta ? b->d_y : nullptr;
   a.hot_idx = b->use_hot ? g->d_hot_idx : nullptr;
   a.hot_tab = (const HotRow*)g->d_hot_tab;
   a.hot_pool = (const uint4*)g->d_hot_pool;

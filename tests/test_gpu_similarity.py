@@ -131,8 +131,6 @@ def test_general_graph_exact_distance(gpu):
     {"BLP_VARIANT": "2", "BLP_HOT_MIN": "8"},           # ... dense rows skipped: empty build rows
     {"BLP_VARIANT": "2", "BLP_CHUNK_BITS": "1024", "BLP_NO_GLOBAL": "1"},  # ... several LDS chunks
     {"BLP_VARIANT": "2", "BLP_NO_PKO": "1"},            # ... the general large scorer (per-pair counts, 512-pair segments)
-    {"BLP_VARIANT": "2", "BLP_NO_DIRECT_META": "1"},    # ... run-grouped pairs through the grouped metadata arrays
-    {"BLP_NO_DIRECT_META": "1"},
     {"BLP_VARIANT": "2", "BLP_NO_PKO": "1", "BLP_NO_SHORT": "1"},
     {"BLP_NO_SHORT_KERNEL": "1"},                       # short rows through the general block scorer
     {"BLP_WCODES": "0"},                                # every AA weight gathered per node
