@@ -2171,7 +2171,7 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
   __shared__ unsigned long long s_aa[2 * SEG];  // packed: [2t] Σ W, [2t + 1] high word << 21 | count
   __shared__ unsigned long long red64[NW];
   __shared__ int red[NW];
-  __shared__ int64_t s_item;
+  __shared__ int64_t s_item[2];  // the claimed item, alternating slots (no barrier guards its rewrite)
   __shared__ int s_nhot;
   __shared__ int s_nl;  // long slices queued in this round
   __shared__ blp::HotRow s_hot[HOT_LIST];
@@ -2199,23 +2199,23 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
   constexpr int ngrp = 8;
   int gq = 0;  // thread 0: groups found empty so far
   PROF_INIT  // -DBLP_PROF phase clocks: 0 claim, 1 build, 2 popcount, 3 batch to short scan, 4 long scan, 5 partials
-  for (;;) {
+  for (int it = 0;; ++it) {
     if (threadIdx.x == 0) {
-      s_item = -1;
+      int64_t claimed = -1;
       while (gq < ngrp) {
         const int g = (grp + gq) % ngrp;
         const int64_t n_g = n_src > g ? (n_src - g + ngrp - 1) / ngrp : 0;
         const int k = atomicAdd(&a.misc->qh[g], 1);
         if ((int64_t)k < n_g * C) {
-          s_item = (int64_t)(g + (int64_t)ngrp * (k / C)) * C + k % C;
+          claimed = (int64_t)(g + (int64_t)ngrp * (k / C)) * C + k % C;
           break;
         }
         ++gq;
       }
+      s_item[it & 1] = claimed;  // slot it & 1 is rewritten two claims later, past this one's barriers
     }
     __syncthreads();
-    const int64_t item = s_item;
-    __syncthreads();
+    const int64_t item = s_item[it & 1];
     if (item < 0) break;
     PROF(0)
     const int s = s_base + (int)(item / C), c = (int)(item % C);
@@ -2334,7 +2334,7 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
         const uint4 q = bm4[i];
         pc += __popc(q.x) + __popc(q.y) + __popc(q.z) + __popc(q.w);
       }
-      const unsigned long long h2 = block_sum_u64<BLOCK>(pc, red64);
+      const unsigned long long h2 = block_sum_u64<BLOCK, false>(pc, red64);  // red64's next use is past a round's barrier
       if (threadIdx.x == 0) ph2[(int64_t)s * C + c] = (uint32_t)h2;
     }
     PROF(2)
@@ -2561,7 +2561,7 @@ __global__ __launch_bounds__(BLOCK) void k_score_hash(ScoreArgs a) {
   static_assert((HT & (HT - 1)) == 0, "HT: a power of two");
   __shared__ uint32_t tab[HT];
   __shared__ unsigned long long red64[NW];
-  __shared__ int s_src;
+  __shared__ int s_src[2];  // claimed sources, alternating slots
   const int n_hash = a.misc->n_hash_front;  // the partitioned active list's hash sources come first
   const bool want_j = (a.mask & BLP_JACCARD) != 0;
   const bool want_a = (a.mask & BLP_ADAMIC) != 0;
@@ -2580,14 +2580,15 @@ __global__ __launch_bounds__(BLOCK) void k_score_hash(ScoreArgs a) {
   // Sources are claimed HS_DQ at a time (one device-scope atomic per HS_DQ sources), and a
   // source's header -- its rows, its pair range and this thread's first pair -- is loaded before
   // the table is cleared, so those round trips overlap the clear instead of following the build.
-  int si_next = 0, left = 0;  // uniform over the workgroup
+  int si_next = 0, left = 0, claims = 0;  // uniform over the workgroup
   for (;;) {
     if (left == 0) {
-      if (threadIdx.x == 0) s_src = atomicAdd(&a.misc->hq, HS_DQ);
+      // slot claims & 1 is rewritten two claims later, past this claim's barriers
+      if (threadIdx.x == 0) s_src[claims & 1] = atomicAdd(&a.misc->hq, HS_DQ);
       __syncthreads();
-      si_next = s_src;
+      si_next = s_src[claims & 1];
+      ++claims;
       left = HS_DQ;
-      __syncthreads();
     }
     const int si = si_next++;
     --left;
@@ -2671,7 +2672,7 @@ __global__ __launch_bounds__(BLOCK) void k_score_hash(ScoreArgs a) {
         }
       }
     }
-    const unsigned long long h2 = want_j ? block_sum_u64<BLOCK>(added - removed, red64) : 0ull;
+    const unsigned long long h2 = want_j ? block_sum_u64<BLOCK, false>(added - removed, red64) : 0ull;  // (next use: past the source's closing barrier)
     if (!want_j) __syncthreads();  // tombstones written before any probe
     // scan: one pair per thread (the first one's metadata came with the header)
     for (int t = threadIdx.x; t < pcnt; t += BLOCK) {
