@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 4, final check at HEAD: the whole GPU suite, smoke(), the default bench line, the config-2
+# Round 4, final check at HEAD (run again after the last code change): the whole GPU suite, smoke(), the default bench line, the config-2
 # profile the line cites (r04_v8_bench), and config 2 end to end twice.
 set -o pipefail
 R=$GRAFT_REPO_ROOT
