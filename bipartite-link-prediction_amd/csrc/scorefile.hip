@@ -234,7 +234,7 @@ bool unique_business_keys(const blp_examples* x, size_t u0, size_t u1) {
 }
 
 // examples.json of the reference's shape, {"user": {"business": label, ...}, ...}, parsed on up
-// to 8 threads: the text is cut at user boundaries (in this shape every '}' outside the outer
+// to 16 threads: the text is cut at user boundaries (in this shape every '}' outside the outer
 // braces closes a user's object: keys are digit strings and values scalars -- a '}' anywhere
 // else fails the range that holds it, and the whole parse with it), each range parsed on its
 // own, the parts concatenated in file order.
@@ -250,9 +250,7 @@ int parse(blp_examples* x) {
   }
   const char* body = c.p;
   const size_t n = (size_t)(end - body);
-  // 8 threads: similarity.main parses examples.json while graph.txt loads on 16 more; this parse
-  // finishes first either way, and fewer threads leave the graph load its cores
-  const unsigned nt = (unsigned)std::max<size_t>(1, std::min<size_t>({8, std::thread::hardware_concurrency(), n >> 20}));
+  const unsigned nt = (unsigned)std::max<size_t>(1, std::min<size_t>({16, std::thread::hardware_concurrency(), n >> 20}));
   std::vector<const char*> cut{body};
   for (unsigned t = 1; t < nt; ++t) {
     const char* q = std::max(body + n * t / nt, cut.back());
@@ -398,8 +396,8 @@ int blp_examples_parse(const char* path, blp_examples** out) {
   const size_t n = (size_t)st.st_size;
   x->text.p.reset(new char[std::max<size_t>(n, 1)]);
   x->text.n = n;
-  // read in slices of >= 8 MiB on up to 8 threads (a 100 MB examples.json: ~4x one read())
-  const size_t nt = std::max<size_t>(1, std::min<size_t>({8, std::thread::hardware_concurrency(), n >> 23}));
+  // read in slices of >= 8 MiB on up to 16 threads (a 100 MB examples.json: ~4x one read())
+  const size_t nt = std::max<size_t>(1, std::min<size_t>({16, std::thread::hardware_concurrency(), n >> 23}));
   std::vector<uint8_t> rok(nt, 0);
   auto slice = [&](size_t t) {
     size_t at = n * t / nt;
@@ -441,8 +439,8 @@ int blp_examples_info(const blp_examples* x, int64_t* n_users, int64_t* n_pairs)
 int blp_examples_ids(const blp_examples* x, int64_t* pair_u, int64_t* pair_v, int64_t* user_off) {
   BLP_CHECK(x, BLP_E_ARG, "blp_examples_ids: null handle");
   const int64_t nu = (int64_t)x->u_key.size(), np = (int64_t)x->v_key.size();
-  // users in slices of about equal pair counts, on up to 8 threads (7.5M pairs at config 2)
-  const unsigned nt = (unsigned)std::max<int64_t>(1, std::min<int64_t>({8, (int64_t)std::thread::hardware_concurrency(), np >> 18}));
+  // users in slices of about equal pair counts, on up to 16 threads (7.5M pairs at config 2)
+  const unsigned nt = (unsigned)std::max<int64_t>(1, std::min<int64_t>({16, (int64_t)std::thread::hardware_concurrency(), np >> 18}));
   auto work = [&](unsigned t) {
     const int64_t u0 = std::lower_bound(x->u_off.begin(), x->u_off.end() - 1, np * (int64_t)t / nt) - x->u_off.begin();
     const int64_t u1 = t + 1 == nt ? nu : std::lower_bound(x->u_off.begin(), x->u_off.end() - 1, np * (int64_t)(t + 1) / nt) - x->u_off.begin();
