@@ -45,6 +45,34 @@ inline bool fast_line(const char*& p, const char* end, int64_t* va, int64_t* vb)
   return true;
 }
 
+// fast_line without bounds checks, for text the caller knows holds a '\n' at or after p: every
+// scan below stops at the first byte outside its class, and '\n' is outside all of them.
+inline bool fast_line_nl(const char*& p, int64_t* va, int64_t* vb) {
+  const char* q = p;
+  unsigned d = (unsigned char)*q - '0';
+  if (d > 9) return false;
+  uint64_t x = 0;
+  const char* s = q;
+  do x = x * 10 + d, d = (unsigned char)*++q - '0';
+  while (d <= 9);
+  if (q - s > 18 || (*q != ' ' && *q != '\t')) return false;
+  do ++q;
+  while (*q == ' ' || *q == '\t');
+  d = (unsigned char)*q - '0';
+  if (d > 9) return false;
+  uint64_t y = 0;
+  s = q;
+  do y = y * 10 + d, d = (unsigned char)*++q - '0';
+  while (d <= 9);
+  if (q - s > 18) return false;
+  while (*q == ' ' || *q == '\t' || *q == '\r') ++q;
+  if (*q != '\n') return false;
+  *va = (int64_t)x;
+  *vb = (int64_t)y;
+  p = q + 1;
+  return true;
+}
+
 inline bool is_ws(char c) { return c == ' ' || c == '\t' || c == '\r' || c == '\v' || c == '\f'; }
 
 // parse one line [p, e) -> columns c0/c1 as int64; false when the line has too few columns
@@ -127,9 +155,12 @@ int parse_slices(const char* path, int c0, int c1, std::vector<Slice>& sl) {
     S.b.reserve((cut[t + 1] - cut[t]) / 12 + 16);
     int64_t mn = INT64_MAX, mx = INT64_MIN;
     const bool fast = c0 == 0 && c1 == 1;
+    // [p, nl_end): whole lines, each ending in '\n', parsed without bounds checks
+    const char* nl_end = end;
+    while (nl_end > p && nl_end[-1] != '\n') --nl_end;
     while (p < end) {
       int64_t va, vb;
-      if (fast && fast_line(p, end, &va, &vb)) {
+      if (fast && (p < nl_end ? fast_line_nl(p, &va, &vb) : fast_line(p, end, &va, &vb))) {
         S.a.push_back(va);
         S.b.push_back(vb);
         mn = std::min(mn, std::min(va, vb));

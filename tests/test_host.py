@@ -39,9 +39,11 @@ def test_edge_list_parser_matches_snap_text_rules(tmp_path):
         ra, rb = read_edges(os.path.join(GOLDEN, case, "graph.txt"))
         assert a.tolist() == ra.tolist() and b.tolist() == rb.tolist()
     # > 1 MiB (threaded slices): the one-pass "digits ws digits" lines mixed with every other
-    # shape the SNAP rules accept or skip (CRLF, tabs, extra columns, signs, comments, blanks)
+    # shape the SNAP rules accept or skip (CRLF, tabs, extra columns, signs, comments, blanks,
+    # 18- and 19-digit ids)
     rng = np.random.default_rng(9)
-    shapes = ["%d %d\n", "%d\t%d\r\n", "%d  %d extra\n", "-%d +%d\n", "  %d %d\n", "%d\t%d \t\n", "# %d %d\n", "%d\n\n"]
+    shapes = ["%d %d\n", "%d\t%d\r\n", "%d  %d extra\n", "-%d +%d\n", "  %d %d\n", "%d\t%d \t\n", "# %d %d\n", "%d\n\n",
+              "%d000000000 %d\n", "%d 1%018d\n"]
     lines = []
     for k in rng.integers(0, len(shapes), 200000):
         x, y = rng.integers(0, 10**9, 2)
