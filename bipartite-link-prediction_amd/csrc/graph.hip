@@ -150,6 +150,14 @@ int build_weight_codes(blp_graph* g, const int64_t* row_ptr, const std::vector<l
   BLP_HIP(hipMalloc(&g->d_wtab, sizeof(long long) * 256));  // always: code 0 reads wtab[0]
   BLP_HIP(hipMemcpy(g->d_wtab, wtab.data(), sizeof(long long) * 256, hipMemcpyHostToDevice));
   if (max_codes <= 0 || nnz == 0) return BLP_OK;
+  const bool gprof = getenv("BLP_GRAPH_PROF") != nullptr;
+  auto t_prev = std::chrono::steady_clock::now();
+  auto stage = [&](const char* what) {
+    if (!gprof) return;
+    const auto t = std::chrono::steady_clock::now();
+    fprintf(stderr, "  codes %-8s %.3f ms\n", what, std::chrono::duration<double, std::milli>(t - t_prev).count());
+    t_prev = t;
+  };
   // occurrences per distinct weight, node slices on up to 16 threads (a handful of distinct
   // weights: each thread's table stays small), then merged
   const int nt = (int)std::max<int64_t>(1, std::min<int64_t>({16, (int64_t)std::thread::hardware_concurrency(), n >> 16}));
@@ -177,6 +185,7 @@ int build_weight_codes(blp_graph* g, const int64_t* row_ptr, const std::vector<l
     wtab[j + 1] = order[j].second;
     code[order[j].second] = (int)j + 1;
   }
+  stage("uses");
   std::vector<uint8_t> ncode((size_t)n, 0);
   par([&](int t) {
     for (int64_t i = n * t / nt, e = n * (t + 1) / nt; i < e; ++i) {
@@ -184,11 +193,13 @@ int build_weight_codes(blp_graph* g, const int64_t* row_ptr, const std::vector<l
       if (it != code.end()) ncode[i] = (uint8_t)it->second;
     }
   });
+  stage("ncode");
   uint8_t* d_ncode = nullptr;
   BLP_HIP(hipMemcpy(g->d_wtab, wtab.data(), sizeof(long long) * 256, hipMemcpyHostToDevice));
   BLP_HIP(hipMalloc(&g->d_ci_w, sizeof(int32_t) * (nnz + 2 * CI_PAD)));
   BLP_HIP(hipMemset(g->d_ci_w, 0, sizeof(int32_t) * (nnz + 2 * CI_PAD)));
   g->d_ci_w += CI_PAD;
+  stage("alloc");
   BLP_HIP(hipMalloc(&d_ncode, (size_t)n));
   BLP_HIP(hipMemcpy(d_ncode, ncode.data(), (size_t)n, hipMemcpyHostToDevice));
   hipLaunchKernelGGL(k_code_ids, dim3((unsigned)std::min<int64_t>((nnz + 255) / 256, 1 << 20)), dim3(256), 0, g->stream,
@@ -196,6 +207,7 @@ int build_weight_codes(blp_graph* g, const int64_t* row_ptr, const std::vector<l
   BLP_HIP(hipGetLastError());
   BLP_HIP(hipStreamSynchronize(g->stream));
   BLP_HIP(hipFree(d_ncode));
+  stage("kernel");
   g->id_bits = bits;
   return BLP_OK;
 }

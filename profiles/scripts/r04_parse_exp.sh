@@ -24,3 +24,8 @@ from blp._lib import lib, check
 h=ctypes.c_void_p(); t=time.perf_counter(); check(lib().blp_edges_load(b'/tmp/graph_c2.txt',0,1,ctypes.byref(h))); print('load %.4f'%(time.perf_counter()-t))
 "; done > ../gpurun_out/pt/load.txt 2>&1
 echo done
+cd ..
+for i in 1 2; do
+  BLP_GRAPH_PROF=1 BLP_INGEST_PROF=1 timeout -k 10 300 python bench.py --mode e2e --config c2 > gpurun_out/pt/e2e_$i.json 2> gpurun_out/pt/e2e_$i.err || { tail -20 gpurun_out/pt/e2e_$i.err; exit 1; }
+done
+echo e2e done
