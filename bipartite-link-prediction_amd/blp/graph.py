@@ -29,6 +29,10 @@ _lib.register("blp_edges_load", [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ct
 _lib.register("blp_edges_info", [ctypes.c_void_p, _I64P, _I64P, _I64P, _I64P, _I64P])
 _lib.register("blp_edges_fetch", [ctypes.c_void_p] * 7)
 _lib.register("blp_edges_destroy", [ctypes.c_void_p])
+_lib.register("blp_edges_load_device", [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                        ctypes.POINTER(ctypes.c_void_p)])
+_lib.register("blp_edges_device", [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)])
+_lib.register("blp_edges_csr", [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)])
 _lib.register("blp_ids_lookup", [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64,
                                  ctypes.c_void_p])
 
@@ -263,6 +267,22 @@ class DeviceGraph(HostGraph):
         g = cls.__new__(cls)
         g._set_ids(node_ids, n_col0, id_lo, id_map, len(da))
         g._build(da, db, device, aa)
+        return g
+
+    @classmethod
+    def from_edges_handle(cls, h, node_ids, n_col0, id_lo, id_map, m, device=0, aa=True):
+        """A graph from a blp_edges handle whose dense endpoints are already in HBM
+        (blp_edges_load_device): blp_edges_csr builds the CSR from them, no upload."""
+        import time
+
+        g = cls.__new__(cls)
+        g._set_ids(node_ids, n_col0, id_lo, id_map, m)
+        t0 = time.perf_counter()
+        c = ctypes.c_void_p()
+        check(lib().blp_edges_csr(h, device, ctypes.byref(c)))
+        t1 = time.perf_counter()
+        g._adopt_csr(c, device, aa)
+        g.build_times.update({"device_csr_s": t1 - t0, "total_s": time.perf_counter() - t0})
         return g
 
     @classmethod
@@ -519,19 +539,29 @@ class PairBatch:
 def load_edge_list(path, c0=0, c1=1, device=0):
     """snap.LoadEdgeList(snap.PUNGraph, path, c0, c1) -> DeviceGraph (similarity.py:16).
 
-    The file is parsed once (multi-threaded) and, for a compact id space, mapped to dense ids
-    natively (blp_edges_load); otherwise the raw endpoints go through HostGraph._ids."""
+    The file is parsed once and, for a compact id space, mapped to dense ids natively: on the
+    device when it has the reference's own line shape (blp_edges_load_device, the dense
+    endpoints stay in HBM for the CSR build), else on the host (multi-threaded); a sparse id
+    space goes through HostGraph._ids."""
     import time
 
     t0 = time.perf_counter()
     L = lib()
     h = ctypes.c_void_p()
     bpath = path.encode() if isinstance(path, str) else path
-    check(L.blp_edges_load(bpath, c0, c1, ctypes.byref(h)))
+    check(L.blp_edges_load_device(bpath, c0, c1, device, ctypes.byref(h)))
     try:
         m, n, n0, lo, span = (ctypes.c_int64() for _ in range(5))
         check(L.blp_edges_info(h, *(ctypes.byref(v) for v in (m, n, n0, lo, span))))
-        if span.value > 0:
+        on = ctypes.c_int(-1)
+        check(L.blp_edges_device(h, ctypes.byref(on)))
+        if span.value > 0 and on.value >= 0:
+            node_ids = np.empty(n.value, np.int64)
+            id_map = np.empty(span.value, np.int32)
+            check(L.blp_edges_fetch(h, None, None, None, None, ptr(node_ids), ptr(id_map)))
+            t1 = time.perf_counter()
+            G = DeviceGraph.from_edges_handle(h, node_ids, n0.value, lo.value, id_map, m.value, device=device)
+        elif span.value > 0:
             da = np.empty(m.value, np.int32)
             db = np.empty(m.value, np.int32)
             node_ids = np.empty(n.value, np.int64)

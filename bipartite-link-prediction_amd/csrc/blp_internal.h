@@ -198,4 +198,8 @@ int timer_end(KernelTimer& t, hipStream_t s, hipEvent_t start);
 int timer_collect(KernelTimer& t);
 void timer_release(KernelTimer& t);
 int set_device(const blp_graph* g);
+// the device CSR of m dense endpoint pairs already in HBM on `device` (csr.hip; blp_csr_build_device
+// with sync_device, which first waits for all work queued on the device)
+int csr_build(int device, const int32_t* d_a, const int32_t* d_b, int64_t m, int64_t n, blp_csr** out,
+              bool sync_device);
 }  // namespace blp

@@ -81,8 +81,8 @@ extern "C" int blp_csr_destroy(blp_csr* c) {
 // wait for everything queued on the device first (a one-off ingest step). blp_csr_build_host's
 // uploads are synchronous already and skip it, so a graph load never waits for other graphs'
 // batches still running on the device.
-static int csr_build(int device, const int32_t* d_a, const int32_t* d_b, int64_t m, int64_t n, blp_csr** out,
-                     bool sync_device) {
+int blp::csr_build(int device, const int32_t* d_a, const int32_t* d_b, int64_t m, int64_t n, blp_csr** out,
+                   bool sync_device) {
   BLP_CHECK(out && n >= 0 && m >= 0 && (m == 0 || (d_a && d_b)), BLP_E_ARG, "blp_csr_build_device: bad arguments");
   BLP_CHECK(n < (int64_t(1) << 31), BLP_E_ARG, "blp_csr_build_device: n_nodes must fit int32");
   int ndev = 0;

@@ -14,6 +14,8 @@
 #include <thread>
 #include <vector>
 
+#include <hipcub/hipcub.hpp>
+
 #include "blp_internal.h"
 
 namespace {
@@ -206,13 +208,319 @@ unsigned n_threads() { return std::max(1u, std::min(16u, std::thread::hardware_c
 // A parsed edge list and, when the id space is compact, its dense id map: ids seen in column
 // 0 ascending, then the ids seen only in column 1 ascending (blp/graph.py HostGraph._ids; a
 // reference bipartite graph.txt puts users in one dense range and businesses in another).
+// blp_edges_load_device keeps the dense endpoints in HBM instead (sl empty, d_da / d_db set).
 struct blp_edges {
   std::vector<Slice> sl;
   int64_t m = 0;
   int64_t n = 0, n_col0 = 0, lo = 0, span = 0;  // span == 0: no dense map (sparse id space)
   std::vector<int32_t> map;                       // [span] dense id of id lo + i, or -1
   std::vector<int64_t> node_ids;                  // [n] dense id -> original id
+  int device = -1;                                // device of d_da / d_db, -1: host slices
+  int32_t* d_da = nullptr;                        // [m] dense endpoints, file order
+  int32_t* d_db = nullptr;
+  ~blp_edges() {
+    if (device >= 0) {
+      (void)hipSetDevice(device);
+      if (d_da) (void)hipFree(d_da);
+      if (d_db) (void)hipFree(d_db);
+    }
+  }
 };
+
+// ------------------------------------------------------------ device parse (blp_edges_load_device)
+// The reference's graph.txt is dataset_maker.py:197's "user business\n" lines. When EVERY line
+// has that shape -- digits, spaces/tabs, digits, optional trailing spaces/tabs/'\r' -- the file
+// is parsed and mapped to dense ids on the device: the text is copied to HBM once, newlines are
+// counted and located per 16 KB chunk, one thread parses one line, and the id map is built from
+// two presence bitmaps (column 0; column 1) by popcount ranks -- the same map as the host path
+// (ids seen in column 0 ascending, then ids only in column 1 ascending). Any other line (a
+// comment, a blank line, a sign, an extra column, a 19-digit id), a non-compact id space or a
+// file under 1 MiB leaves the work to the host parser, whose rules cover them all.
+namespace {
+
+using namespace blp;
+
+constexpr int NL_BLOCK = 256;
+constexpr int NL_BYTES = 64;                       // text bytes per thread
+constexpr int64_t NL_CHUNK = NL_BLOCK * NL_BYTES;  // text bytes per workgroup
+constexpr int64_t DEVICE_PARSE_MIN = 1 << 20;
+
+// bit 7 of each byte lane set where that byte is '\n' (exact: no carry crosses a lane)
+__device__ inline uint32_t nl_bits(uint32_t w) {
+  const uint32_t x = w ^ 0x0A0A0A0Au;
+  const uint32_t t = ((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x;
+  return ~t & 0x80808080u;
+}
+
+__device__ inline void load_chunk(const uint8_t* txt, uint32_t (&w)[16]) {
+  const uint4* p = reinterpret_cast<const uint4*>(txt + (int64_t)blockIdx.x * NL_CHUNK + threadIdx.x * NL_BYTES);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint4 v = p[j];
+    w[4 * j] = v.x;
+    w[4 * j + 1] = v.y;
+    w[4 * j + 2] = v.z;
+    w[4 * j + 3] = v.w;
+  }
+}
+
+// newlines per workgroup chunk (the text is zero-padded to whole chunks)
+__global__ __launch_bounds__(NL_BLOCK) void k_nl_count(const uint8_t* txt, uint64_t* blk) {
+  uint32_t w[16];
+  load_chunk(txt, w);
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) c += __popc(nl_bits(w[i]));
+  using R = hipcub::BlockReduce<uint32_t, NL_BLOCK>;
+  __shared__ typename R::TempStorage tmp;
+  const uint32_t s = R(tmp).Sum(c);
+  if (threadIdx.x == 0) blk[blockIdx.x] = s;
+}
+
+// nl[k] = byte offset of the k-th newline
+__global__ __launch_bounds__(NL_BLOCK) void k_nl_pos(const uint8_t* txt, const uint64_t* blk_off, int64_t* nl) {
+  uint32_t w[16];
+  load_chunk(txt, w);
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) c += __popc(nl_bits(w[i]));
+  using S = hipcub::BlockScan<uint32_t, NL_BLOCK>;
+  __shared__ typename S::TempStorage tmp;
+  uint32_t off;
+  S(tmp).ExclusiveSum(c, off);
+  int64_t o = (int64_t)blk_off[blockIdx.x] + off;
+  const int64_t base = (int64_t)blockIdx.x * NL_CHUNK + threadIdx.x * NL_BYTES;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    uint32_t m = nl_bits(w[i]);
+    while (m) {
+      nl[o++] = base + 4 * i + (__builtin_ctz(m) >> 3);
+      m &= m - 1;
+    }
+  }
+}
+
+struct ParseStats {
+  unsigned long long mn, mx;  // over both columns
+  unsigned int bad;           // some line is not "digits ws digits [ws]"
+};
+
+__device__ inline bool is_digit(uint8_t c) { return (unsigned)(c - '0') <= 9u; }
+
+// one thread per line [nl[k-1] + 1, nl[k])
+__global__ __launch_bounds__(256) void k_parse_lines(const uint8_t* txt, const int64_t* nl, int64_t L, int64_t* a,
+                                                     int64_t* b, ParseStats* st) {
+  unsigned long long mn = ~0ull, mx = 0;
+  unsigned int bad = 0;
+  for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < L; k += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = nl[k];
+    int64_t i = k ? nl[k - 1] + 1 : 0;
+    uint64_t x = 0, y = 0;
+    int nd = 0;
+    for (; i < e && nd <= 18 && is_digit(txt[i]); ++i, ++nd) x = x * 10 + (txt[i] - '0');
+    bool ok = nd >= 1 && nd <= 18;
+    int ws = 0;
+    for (; i < e && (txt[i] == ' ' || txt[i] == '\t'); ++i) ++ws;
+    ok = ok && ws > 0;
+    nd = 0;
+    for (; i < e && nd <= 18 && is_digit(txt[i]); ++i, ++nd) y = y * 10 + (txt[i] - '0');
+    ok = ok && nd >= 1 && nd <= 18;
+    for (; i < e && (txt[i] == ' ' || txt[i] == '\t' || txt[i] == '\r'); ++i) {
+    }
+    ok = ok && i == e;
+    a[k] = (int64_t)x;
+    b[k] = (int64_t)y;
+    if (ok) {
+      mn = min(mn, (unsigned long long)min(x, y));
+      mx = max(mx, (unsigned long long)max(x, y));
+    } else {
+      bad = 1;
+    }
+  }
+  for (int s = 32; s > 0; s >>= 1) {
+    mn = min(mn, (unsigned long long)__shfl_xor(mn, s));
+    mx = max(mx, (unsigned long long)__shfl_xor(mx, s));
+    bad |= __shfl_xor(bad, s);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMin(&st->mn, mn);
+    atomicMax(&st->mx, mx);
+    if (bad) atomicOr(&st->bad, 1u);
+  }
+}
+
+// presence bitmaps over [lo, lo + span): column 0 and column 1 (a set bit is read before the
+// atomic: most ids recur, and the business column is a few thousand hot words)
+__global__ void k_mark(const int64_t* a, const int64_t* b, int64_t L, int64_t lo, uint32_t* in0, uint32_t* in1) {
+  for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < L; k += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t u = (uint64_t)(a[k] - lo), v = (uint64_t)(b[k] - lo);
+    const uint32_t bu = 1u << (u & 31), bv = 1u << (v & 31);
+    if (!(in0[u >> 5] & bu)) atomicOr(&in0[u >> 5], bu);
+    if (!(in1[v >> 5] & bv)) atomicOr(&in1[v >> 5], bv);
+  }
+}
+
+// per bitmap word: ids seen in column 0 (low half), ids seen only in column 1 (high half)
+__global__ void k_word_counts(const uint32_t* in0, const uint32_t* in1, int64_t W, uint64_t* cnt) {
+  for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < W; w += (int64_t)gridDim.x * blockDim.x)
+    cnt[w] = (uint64_t)__popc(in0[w]) | (uint64_t)__popc(in1[w] & ~in0[w]) << 32;
+}
+
+__global__ void k_map(const uint32_t* in0, const uint32_t* in1, const uint64_t* base, int64_t span, int64_t lo,
+                      int64_t n_col0, int32_t* map, int64_t* node_ids) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < span; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t w = i >> 5;
+    const int bit = (int)(i & 31);
+    const uint32_t below = (1u << bit) - 1u;
+    const uint32_t u0 = in0[w], u1 = in1[w] & ~u0;
+    int64_t r = -1;
+    if ((u0 >> bit) & 1u)
+      r = (int64_t)(uint32_t)base[w] + __popc(u0 & below);
+    else if ((u1 >> bit) & 1u)
+      r = n_col0 + (int64_t)(base[w] >> 32) + __popc(u1 & below);
+    map[i] = (int32_t)r;
+    if (r >= 0) node_ids[r] = lo + i;
+  }
+}
+
+__global__ void k_dense(const int64_t* a, const int64_t* b, int64_t L, int64_t lo, const int32_t* map, int32_t* da,
+                        int32_t* db) {
+  for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < L; k += (int64_t)gridDim.x * blockDim.x) {
+    da[k] = map[a[k] - lo];
+    db[k] = map[b[k] - lo];
+  }
+}
+
+unsigned grid_for(int64_t n, int n_cu) {
+  return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, (int64_t)n_cu * 16));
+}
+
+// *out = a device-resident handle, or null (with BLP_OK) when the host parser must take the file
+int device_load(const char* path, int device, blp_edges** out) {
+  *out = nullptr;
+  int fd = open(path, O_RDONLY);
+  if (fd < 0) return fail(BLP_E_ARG, std::string("blp_edges_load_device: cannot open ") + path);
+  struct stat st_;
+  if (fstat(fd, &st_) != 0 || (int64_t)st_.st_size < DEVICE_PARSE_MIN) {
+    close(fd);
+    return BLP_OK;
+  }
+  const int64_t S = (int64_t)st_.st_size;
+  const uint8_t* data = (const uint8_t*)mmap(nullptr, (size_t)S, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
+  close(fd);
+  if (data == MAP_FAILED) return BLP_OK;  // the host parser reports it
+  hipStream_t st = nullptr;
+  ScopedBuf txt, blk, blk_off, tmp, nl, a, b, stats, in0, in1, cnt, base, map, ids;
+  blp_edges* e = nullptr;
+  auto run = [&]() -> int {
+    int ndev = 0;
+    BLP_HIP(hipGetDeviceCount(&ndev));
+    BLP_CHECK(device >= 0 && device < ndev, BLP_E_ARG, "blp_edges_load_device: no such device");
+    BLP_HIP(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    int n_cu = 256;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess) n_cu = prop.multiProcessorCount;
+    BLP_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    const bool tail_nl = data[S - 1] == '\n';
+    const int64_t T = S + (tail_nl ? 0 : 1);  // a missing final newline is supplied
+    const int64_t nb = (T + NL_CHUNK - 1) / NL_CHUNK;
+    int rc;
+    if ((rc = txt.reserve((size_t)(nb * NL_CHUNK))) || (rc = blk.reserve(8 * nb)) || (rc = blk_off.reserve(8 * nb)))
+      return rc;
+    uint8_t* d_txt = txt.as<uint8_t>();
+    BLP_HIP(hipMemsetAsync(d_txt + S, 0, (size_t)(nb * NL_CHUNK - S), st));
+    if (!tail_nl) BLP_HIP(hipMemsetAsync(d_txt + S, '\n', 1, st));
+    BLP_HIP(hipMemcpyAsync(d_txt, data, (size_t)S, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_nl_count, dim3((unsigned)nb), dim3(NL_BLOCK), 0, st, d_txt, blk.as<uint64_t>());
+    BLP_HIP(hipGetLastError());
+    size_t tb = 0;
+    BLP_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, blk.as<uint64_t>(), blk_off.as<uint64_t>(), (int)nb, st));
+    if ((rc = tmp.reserve(tb))) return rc;
+    tb = tmp.bytes;
+    BLP_HIP(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, blk.as<uint64_t>(), blk_off.as<uint64_t>(), (int)nb, st));
+    uint64_t last[2] = {0, 0};
+    BLP_HIP(hipMemcpyAsync(&last[0], blk_off.as<uint64_t>() + nb - 1, 8, hipMemcpyDeviceToHost, st));
+    BLP_HIP(hipMemcpyAsync(&last[1], blk.as<uint64_t>() + nb - 1, 8, hipMemcpyDeviceToHost, st));
+    BLP_HIP(hipStreamSynchronize(st));
+    const int64_t L = (int64_t)(last[0] + last[1]);
+    if (L < 1 || L >= (int64_t(1) << 31)) return BLP_OK;
+    if ((rc = nl.reserve(8 * L)) || (rc = a.reserve(8 * L)) || (rc = b.reserve(8 * L)) ||
+        (rc = stats.reserve(sizeof(ParseStats))))
+      return rc;
+    hipLaunchKernelGGL(k_nl_pos, dim3((unsigned)nb), dim3(NL_BLOCK), 0, st, d_txt, blk_off.as<uint64_t>(),
+                       nl.as<int64_t>());
+    BLP_HIP(hipGetLastError());
+    ParseStats ps{~0ull, 0ull, 0u};
+    BLP_HIP(hipMemcpyAsync(stats.p, &ps, sizeof ps, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_parse_lines, dim3(grid_for(L, n_cu)), dim3(256), 0, st, d_txt, nl.as<int64_t>(), L,
+                       a.as<int64_t>(), b.as<int64_t>(), stats.as<ParseStats>());
+    BLP_HIP(hipGetLastError());
+    BLP_HIP(hipMemcpyAsync(&ps, stats.p, sizeof ps, hipMemcpyDeviceToHost, st));
+    BLP_HIP(hipStreamSynchronize(st));
+    if (ps.bad) return BLP_OK;
+    const int64_t lo = (int64_t)ps.mn, span = (int64_t)(ps.mx - ps.mn) + 1;
+    // the host path's compactness rule (blp_edges_load)
+    if (!(span > 0 && span <= std::max<int64_t>(4 * L, 1 << 20) && span < (int64_t(1) << 31))) return BLP_OK;
+    txt.release();
+    nl.release();
+    const int64_t W = (span + 31) / 32;
+    if ((rc = in0.reserve(4 * W)) || (rc = in1.reserve(4 * W)) || (rc = cnt.reserve(8 * W)) ||
+        (rc = base.reserve(8 * W)) || (rc = map.reserve(4 * span)))
+      return rc;
+    BLP_HIP(hipMemsetAsync(in0.p, 0, 4 * W, st));
+    BLP_HIP(hipMemsetAsync(in1.p, 0, 4 * W, st));
+    hipLaunchKernelGGL(k_mark, dim3(grid_for(L, n_cu)), dim3(256), 0, st, a.as<int64_t>(), b.as<int64_t>(), L, lo,
+                       in0.as<uint32_t>(), in1.as<uint32_t>());
+    BLP_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_word_counts, dim3(grid_for(W, n_cu)), dim3(256), 0, st, in0.as<uint32_t>(),
+                       in1.as<uint32_t>(), W, cnt.as<uint64_t>());
+    BLP_HIP(hipGetLastError());
+    tb = 0;
+    BLP_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt.as<uint64_t>(), base.as<uint64_t>(), (int)W, st));
+    if ((rc = tmp.reserve(tb))) return rc;
+    tb = tmp.bytes;
+    BLP_HIP(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, cnt.as<uint64_t>(), base.as<uint64_t>(), (int)W, st));
+    BLP_HIP(hipMemcpyAsync(&last[0], base.as<uint64_t>() + W - 1, 8, hipMemcpyDeviceToHost, st));
+    BLP_HIP(hipMemcpyAsync(&last[1], cnt.as<uint64_t>() + W - 1, 8, hipMemcpyDeviceToHost, st));
+    BLP_HIP(hipStreamSynchronize(st));
+    const uint64_t tot = last[0] + last[1];
+    const int64_t n_col0 = (int64_t)(uint32_t)tot, n = n_col0 + (int64_t)(tot >> 32);
+    if ((rc = ids.reserve(8 * std::max<int64_t>(n, 1)))) return rc;
+    hipLaunchKernelGGL(k_map, dim3(grid_for(span, n_cu)), dim3(256), 0, st, in0.as<uint32_t>(), in1.as<uint32_t>(),
+                       base.as<uint64_t>(), span, lo, n_col0, map.as<int32_t>(), ids.as<int64_t>());
+    BLP_HIP(hipGetLastError());
+    e = new blp_edges();
+    e->device = device;
+    BLP_HIP(hipMalloc(&e->d_da, 4 * L));
+    BLP_HIP(hipMalloc(&e->d_db, 4 * L));
+    hipLaunchKernelGGL(k_dense, dim3(grid_for(L, n_cu)), dim3(256), 0, st, a.as<int64_t>(), b.as<int64_t>(), L, lo,
+                       map.as<int32_t>(), e->d_da, e->d_db);
+    BLP_HIP(hipGetLastError());
+    e->node_ids.resize((size_t)n);
+    e->map.resize((size_t)span);
+    BLP_HIP(hipMemcpyAsync(e->node_ids.data(), ids.p, 8 * n, hipMemcpyDeviceToHost, st));
+    BLP_HIP(hipMemcpyAsync(e->map.data(), map.p, 4 * span, hipMemcpyDeviceToHost, st));
+    BLP_HIP(hipStreamSynchronize(st));
+    e->m = L;
+    e->n = n;
+    e->n_col0 = n_col0;
+    e->lo = lo;
+    e->span = span;
+    *out = e;
+    e = nullptr;
+    return BLP_OK;
+  };
+  const int rc = run();
+  if (st) {
+    (void)hipStreamSynchronize(st);  // nothing of this call left in flight before its buffers go
+    (void)hipStreamDestroy(st);
+  }
+  delete e;  // a handle abandoned on an error path
+  munmap((void*)data, (size_t)S);
+  return rc;
+}
+
+}  // namespace
 
 using namespace blp;
 
@@ -372,6 +680,25 @@ extern "C" int blp_edges_fetch(const blp_edges* e, int64_t* a, int64_t* b, int32
   BLP_CHECK(e, BLP_E_ARG, "blp_edges_fetch: null handle");
   BLP_CHECK(e->span > 0 || !(da || db || node_ids || id_map), BLP_E_STATE,
             "blp_edges_fetch: no dense id map (sparse id space): fetch a / b only");
+  if (e->d_da) {  // device-resident: dense endpoints copied back, raw ids through node_ids
+    std::vector<int32_t> ta, tb;
+    int32_t* ha = da;
+    int32_t* hb = db;
+    if (a && !ha) ta.resize((size_t)e->m), ha = ta.data();
+    if (b && !hb) tb.resize((size_t)e->m), hb = tb.data();
+    BLP_HIP(hipSetDevice(e->device));
+    if (ha && e->m) BLP_HIP(hipMemcpy(ha, e->d_da, 4 * e->m, hipMemcpyDeviceToHost));
+    if (hb && e->m) BLP_HIP(hipMemcpy(hb, e->d_db, 4 * e->m, hipMemcpyDeviceToHost));
+    par_for(e->m, n_threads(), [&](unsigned, int64_t k0, int64_t k1) {
+      for (int64_t k = k0; k < k1; ++k) {
+        if (a) a[k] = e->node_ids[ha[k]];
+        if (b) b[k] = e->node_ids[hb[k]];
+      }
+    });
+    if (node_ids) std::copy(e->node_ids.begin(), e->node_ids.end(), node_ids);
+    if (id_map) std::copy(e->map.begin(), e->map.end(), id_map);
+    return BLP_OK;
+  }
   const unsigned nt = (unsigned)e->sl.size();
   std::vector<int64_t> base(nt + 1, 0);
   for (unsigned t = 0; t < nt; ++t) base[t + 1] = base[t] + (int64_t)e->sl[t].a.size();
@@ -392,6 +719,34 @@ extern "C" int blp_edges_fetch(const blp_edges* e, int64_t* a, int64_t* b, int32
   if (node_ids) std::copy(e->node_ids.begin(), e->node_ids.end(), node_ids);
   if (id_map) std::copy(e->map.begin(), e->map.end(), id_map);
   return BLP_OK;
+}
+
+extern "C" int blp_edges_load_device(const char* path, int c0, int c1, int device, blp_edges** out) {
+  BLP_CHECK(path && out, BLP_E_ARG, "blp_edges_load_device: bad arguments");
+  *out = nullptr;
+  if (c0 == 0 && c1 == 1) {
+    if (int rc = device_load(path, device, out)) return rc;
+    if (*out) return BLP_OK;
+  }
+  return blp_edges_load(path, c0, c1, out);
+}
+
+extern "C" int blp_edges_device(const blp_edges* e, int* device) {
+  BLP_CHECK(e && device, BLP_E_ARG, "blp_edges_device: bad arguments");
+  *device = e->d_da ? e->device : -1;
+  return BLP_OK;
+}
+
+extern "C" int blp_edges_csr(const blp_edges* e, int device, blp_csr** out) {
+  BLP_CHECK(e && out, BLP_E_ARG, "blp_edges_csr: bad arguments");
+  BLP_CHECK(e->span > 0, BLP_E_STATE, "blp_edges_csr: no dense id map (sparse id space)");
+  if (e->d_da) {
+    BLP_CHECK(device == e->device, BLP_E_ARG, "blp_edges_csr: the endpoints live on another device");
+    return csr_build(e->device, e->d_da, e->d_db, e->m, e->n, out, false);  // the load synchronised its stream
+  }
+  std::vector<int32_t> da((size_t)std::max<int64_t>(e->m, 1)), db((size_t)std::max<int64_t>(e->m, 1));
+  if (int rc = blp_edges_fetch(e, nullptr, nullptr, da.data(), db.data(), nullptr, nullptr)) return rc;
+  return blp_csr_build_host(device, da.data(), db.data(), e->m, e->n, out);
 }
 
 extern "C" int blp_edges_destroy(blp_edges* e) {

@@ -152,6 +152,17 @@ int blp_edges_info(const blp_edges* e, int64_t* m, int64_t* n_nodes, int64_t* n_
 int blp_edges_fetch(const blp_edges* e, int64_t* a, int64_t* b, int32_t* da, int32_t* db, int64_t* node_ids,
                     int32_t* id_map);
 int blp_edges_destroy(blp_edges* e);
+/* blp_edges_load_device: blp_edges_load with the parse and the id map on `device` when the file
+ * is the reference's own graph.txt shape (dataset_maker.py:197: every line "digits ws digits",
+ * optional trailing blanks / '\r', c0 = 0, c1 = 1, >= 1 MiB, compact id space): the text is
+ * copied to HBM once and the dense endpoints stay there. Anything else is parsed on the host
+ * exactly as blp_edges_load does. Same info / fetch / ids results either way.
+ * blp_edges_device: *device = the device holding the dense endpoints, or -1 (host slices).
+ * blp_edges_csr: the device CSR of the dense endpoints (as blp_csr_build_device; no upload when
+ *   they are device-resident, which must then be on `device`).                              */
+int blp_edges_load_device(const char* path, int c0, int c1, int device, blp_edges** out);
+int blp_edges_device(const blp_edges* e, int* device);
+int blp_edges_csr(const blp_edges* e, int device, blp_csr** out);
 int blp_ids_lookup(const int32_t* id_map, int64_t id_lo, int64_t id_span, const int64_t* ids, int64_t n, int32_t* dense);
 
 /* Upload a CSR (from blp_csr_from_edges or equivalent) to device `device`.

@@ -526,3 +526,134 @@ def test_multi_compact_rejects_bad_counts(gpu):
 
     with pytest.raises(RuntimeError):
         Multi.compact_csr(np.zeros(8, np.int32), np.array([2, -1], np.int64), 10, device=gpu)
+
+
+def _edges_load(path, device=None, csr_device=None):
+    """Everything a blp_edges handle reports: through blp_edges_load_device (device given) or
+    the host loader blp_edges_load; plus the CSR of blp_edges_csr when there is an id map."""
+    L, P, check = blp.lib(), blp._lib.ptr, blp._lib.check
+    h = ctypes.c_void_p()
+    if device is None:
+        check(L.blp_edges_load(str(path).encode(), 0, 1, ctypes.byref(h)))
+    else:
+        check(L.blp_edges_load_device(str(path).encode(), 0, 1, device, ctypes.byref(h)))
+    try:
+        v = [ctypes.c_int64() for _ in range(5)]
+        check(L.blp_edges_info(h, *(ctypes.byref(x) for x in v)))
+        m, n, n0, lo, span = (x.value for x in v)
+        on = ctypes.c_int(7)
+        check(L.blp_edges_device(h, ctypes.byref(on)))
+        out = {"info": (m, n, n0, lo, span), "on": on.value}
+        a, b = np.empty(m, np.int64), np.empty(m, np.int64)
+        if span == 0:
+            check(L.blp_edges_fetch(h, P(a), P(b), None, None, None, None))
+            out.update(a=a, b=b)
+            return out
+        da, db = np.empty(m, np.int32), np.empty(m, np.int32)
+        ids, idm = np.empty(n, np.int64), np.empty(span, np.int32)
+        check(L.blp_edges_fetch(h, P(a), P(b), P(da), P(db), P(ids), P(idm)))
+        out.update(a=a, b=b, da=da, db=db, node_ids=ids, id_map=idm)
+        c = ctypes.c_void_p()
+        check(L.blp_edges_csr(h, csr_device if csr_device is not None else 0, ctypes.byref(c)))
+        try:
+            nn, nnz = ctypes.c_int64(), ctypes.c_int64()
+            check(L.blp_csr_info(c, ctypes.byref(nn), ctypes.byref(nnz)))
+            rp = np.empty(n + 1, np.int64)
+            ci = np.empty(max(nnz.value, 1), np.int32)
+            sl = np.empty(max(n, 1), np.uint8)
+            check(L.blp_csr_fetch(c, P(rp), P(ci), P(sl)))
+            out["csr"] = (rp, ci[: nnz.value], sl[:n])
+        finally:
+            L.blp_csr_destroy(c)
+        return out
+    finally:
+        L.blp_edges_destroy(h)
+
+
+def _graph_txt(path, a, c, rng, shapes=("%d %d\n", "%d\t%d\r\n", "%d  %d \n", "%d\t \t%d\t\r\n", "%07d %d\n"),
+               final_newline=False, extra=()):
+    """graph.txt text of edges (a, c) with the line shapes the device parser takes; `extra`
+    lines (index, text) spliced in."""
+    pick = rng.integers(0, len(shapes), len(a))
+    lines = [shapes[k] % (x, y) for k, x, y in zip(pick.tolist(), a.tolist(), c.tolist())]
+    for i, t in extra:
+        lines.insert(i, t)
+    text = "".join(lines)
+    if not final_newline:
+        text = text.rstrip("\n").rstrip("\r")
+    path.write_text(text)
+    return path
+
+
+def _same_load(d, h):
+    assert d["info"] == h["info"]
+    for k in ("a", "b", "da", "db", "node_ids", "id_map"):
+        if k in h:
+            assert np.array_equal(d[k], h[k]), k
+    if "csr" in h:
+        for x, y in zip(d["csr"], h["csr"]):
+            assert np.array_equal(x, y)
+
+
+@pytest.mark.parametrize("final_newline", [False, True])
+def test_device_parse_equals_host_parse(gpu, tmp_path, final_newline):
+    """blp_edges_load_device on a graph.txt of the reference's line shape (dataset_maker.py:197;
+    tabs, CRLF, trailing blanks, leading zeros, duplicates, reversed duplicates, self-loops): the
+    parse, id map and CSR run on the device and equal the host loader's, and the CSR equals the
+    host CSR builder's on the dense endpoints."""
+    rng = np.random.default_rng(21)
+    a, c = _messy_edges(rng, 60000, 2500, 150000)
+    p = _graph_txt(tmp_path / "graph.txt", a + 5, c + 5, rng, final_newline=final_newline)
+    assert p.stat().st_size >= 1 << 20
+    d = _edges_load(p, device=gpu, csr_device=gpu)
+    h = _edges_load(p, csr_device=gpu)
+    assert d["on"] == gpu and h["on"] == -1
+    _same_load(d, h)
+    m, n, n0, lo, span = d["info"]
+    assert m == len(a) and lo == 5 and span > 0
+    rp, ci, sl = _host_csr(n, d["da"], d["db"])
+    for x, y in zip(d["csr"], (rp, ci, sl)):
+        assert np.array_equal(x, y)
+
+
+@pytest.mark.parametrize("case", ["comment", "blank_line", "sign", "extra_column", "long_id", "sparse_ids", "small"])
+def test_device_parse_falls_back_to_host(gpu, tmp_path, case):
+    """Text outside the device parser's shape is parsed on the host, with the host loader's
+    results: comments, blank lines, signs, extra columns, 19-digit ids, a non-compact id space,
+    files under 1 MiB."""
+    rng = np.random.default_rng(22)
+    a, c = _messy_edges(rng, 60000, 2500, 150000)
+    extra = {"comment": [(777, "# a comment\n")], "blank_line": [(5000, "\n")], "sign": [(9000, "+12 40\n")],
+             "extra_column": [(100, "12 40 3\n")], "long_id": [(123, "1000000000000000000 7\n")]}.get(case, ())
+    if case == "sparse_ids":
+        a, c = a * 7919, c * 7919
+    if case == "small":
+        a, c = a[:1000], c[:1000]
+    p = _graph_txt(tmp_path / "graph.txt", a, c, rng, extra=extra)
+    d = _edges_load(p, device=gpu, csr_device=gpu)
+    h = _edges_load(p, csr_device=gpu)
+    assert d["on"] == -1
+    _same_load(d, h)
+    if case in ("sparse_ids", "long_id"):
+        assert d["info"][4] == 0
+
+
+def test_load_edge_list_device_parse(gpu, tmp_path):
+    """blp.load_edge_list (similarity.py:16's snap.LoadEdgeList) on a device-parsed file gives
+    the graph DeviceGraph builds from the host-parsed ids: ids, CSR, weights and scores."""
+    rng = np.random.default_rng(23)
+    a, c = _messy_edges(rng, 50000, 2000, 140000)
+    p = _graph_txt(tmp_path / "graph.txt", a + 3, c + 3, rng)
+    G = blp.load_edge_list(str(p), device=gpu)
+    ra, rb = blp.parse_edge_list(str(p))
+    H = blp.DeviceGraph(ra, rb, device=gpu)
+    assert "device_csr_s" in G.build_times
+    for k in ("node_ids", "row_ptr", "col_idx", "self_loop", "degree", "aa_weight"):
+        assert np.array_equal(getattr(G, k), getattr(H, k)), k
+    assert G.n_col0 == H.n_col0
+    assert np.array_equal(G.dense(H.node_ids[:100]), np.arange(100))
+    users = rng.choice(np.flatnonzero(G.hop1_size[: G.n_col0] > 0), 50, replace=False)
+    x = np.repeat(users, 20).astype(np.int32)
+    y = rng.integers(G.n_col0, G.n, len(x)).astype(np.int32)
+    for k, v in G.score_pairs(x, y, 7).items():
+        np.testing.assert_array_equal(v, H.score_pairs(x, y, 7)[k])

@@ -188,12 +188,18 @@ def test_main_missing_examples_raises_like_reference(tmp_path):
                         [None] * 3, METHODS, [None] * 3)
 
 
-def _native_edges(path):
+def _native_edges(path, device_entry=False):
     L = blp.lib()
     from blp import graph as bg  # noqa: F401  (registers the blp_edges_* signatures)
 
     h = ctypes.c_void_p()
-    blp._lib.check(L.blp_edges_load(str(path).encode(), 0, 1, ctypes.byref(h)))
+    if device_entry:
+        blp._lib.check(L.blp_edges_load_device(str(path).encode(), 0, 1, 0, ctypes.byref(h)))
+        on = ctypes.c_int(7)
+        blp._lib.check(L.blp_edges_device(h, ctypes.byref(on)))
+        assert on.value == -1  # parsed on the host
+    else:
+        blp._lib.check(L.blp_edges_load(str(path).encode(), 0, 1, ctypes.byref(h)))
     try:
         m, n, n0, lo, span = (ctypes.c_int64() for _ in range(5))
         blp._lib.check(L.blp_edges_info(h, *(ctypes.byref(v) for v in (m, n, n0, lo, span))))
@@ -255,3 +261,18 @@ def test_native_edge_load_equals_host_id_map(tmp_path, kind):
                                             blp._lib.ptr(probe), len(probe), blp._lib.ptr(dense)))
     exp, _ = H.lookup(probe)
     np.testing.assert_array_equal(dense, exp)
+
+
+def test_device_edge_load_small_files_stay_on_host(tmp_path):
+    """blp_edges_load_device leaves files under 1 MiB (and text outside graph.txt's line shape)
+    to the host loader -- no device is touched, so this runs without one -- with the host
+    loader's results."""
+    rng = np.random.default_rng(4)
+    a = rng.integers(0, 5000, 20000)
+    b = rng.integers(5000, 5600, 20000)
+    path = tmp_path / "graph.txt"
+    path.write_text("".join("%d %d\n" % (x, y) for x, y in zip(a, b)))
+    got, exp = _native_edges(path, device_entry=True), _native_edges(path)
+    assert got.keys() == exp.keys()
+    for k in got:
+        np.testing.assert_array_equal(got[k], exp[k])
