@@ -198,6 +198,9 @@ int timer_end(KernelTimer& t, hipStream_t s, hipEvent_t start);
 int timer_collect(KernelTimer& t);
 void timer_release(KernelTimer& t);
 int set_device(const blp_graph* g);
+// touch every page of a fresh host buffer (>= 8 MB) from up to 16 threads before a pageable
+// device-to-host copy into it (graph.hip)
+void prefault_host(void* p, size_t bytes);
 // the device CSR of m dense endpoint pairs already in HBM on `device` (csr.hip; blp_csr_build_device
 // with sync_device, which first waits for all work queued on the device)
 int csr_build(int device, const int32_t* d_a, const int32_t* d_b, int64_t m, int64_t n, blp_csr** out,

@@ -9,8 +9,6 @@
 // 32 GB of keys + sort scratch on a 288 GB part.
 #include <hipcub/hipcub.hpp>
 
-#include <thread>
-
 #include "blp_internal.h"
 
 namespace {
@@ -203,26 +201,11 @@ extern "C" int blp_csr_info(const blp_csr* c, int64_t* n_nodes, int64_t* nnz) {
   return BLP_OK;
 }
 
-// Touch every page of a fresh host buffer from up to 16 threads: a pageable device-to-host copy
-// into never-touched memory takes its page faults one by one on the copying thread (80 MB of
-// col_idx at config 2: ~20 ms serial, a few ms spread over the threads).
-static void prefault(void* p, size_t bytes) {
-  if (!p || bytes < (size_t(8) << 20)) return;
-  const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-  std::vector<std::thread> th;
-  for (unsigned t = 0; t < nt; ++t)
-    th.emplace_back([=]() {
-      volatile char* q = static_cast<volatile char*>(p);
-      for (size_t o = bytes * t / nt / 4096 * 4096; o < bytes * (t + 1) / nt; o += 4096) q[o] = 0;
-    });
-  for (auto& x : th) x.join();
-}
-
 extern "C" int blp_csr_fetch(const blp_csr* c, int64_t* row_ptr, int32_t* col_idx, uint8_t* self_loop) {
   BLP_CHECK(c, BLP_E_ARG, "blp_csr_fetch: null csr");
   BLP_HIP(hipSetDevice(c->device));
-  prefault(row_ptr, 8 * (size_t)(c->n + 1));
-  if (c->nnz) prefault(col_idx, 4 * (size_t)c->nnz);
+  prefault_host(row_ptr, 8 * (size_t)(c->n + 1));
+  if (c->nnz) prefault_host(col_idx, 4 * (size_t)c->nnz);
   if (row_ptr) BLP_HIP(hipMemcpy(row_ptr, c->d_rp, 8 * (c->n + 1), hipMemcpyDeviceToHost));
   if (col_idx && c->nnz) BLP_HIP(hipMemcpy(col_idx, c->d_ci, 4 * c->nnz, hipMemcpyDeviceToHost));
   if (self_loop && c->n) BLP_HIP(hipMemcpy(self_loop, c->d_self, c->n, hipMemcpyDeviceToHost));

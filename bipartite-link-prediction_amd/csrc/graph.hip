@@ -69,6 +69,22 @@ int set_device(const blp_graph* g) {
   return BLP_OK;
 }
 
+// Touch every page of a fresh host buffer from up to 16 threads: a pageable device-to-host copy
+// into never-touched memory takes its page faults one by one on the copying thread (80 MB of
+// col_idx at config 2: ~20 ms serial, a few ms spread over the threads). Buffers under 8 MB are
+// left alone.
+void prefault_host(void* p, size_t bytes) {
+  if (!p || bytes < (size_t(8) << 20)) return;
+  const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < nt; ++t)
+    th.emplace_back([=]() {
+      volatile char* q = static_cast<volatile char*>(p);
+      for (size_t o = bytes * t / nt / 4096 * 4096; o < bytes * (t + 1) / nt; o += 4096) q[o] = 0;
+    });
+  for (auto& x : th) x.join();
+}
+
 int timer_begin(KernelTimer& t, hipStream_t s, hipEvent_t* start) {
   if (t.free_events.empty()) {
     hipEvent_t e;

@@ -3716,6 +3716,9 @@ int blp_batch_fetch(blp_graph* g, blp_batch* b, uint32_t* cn, double* jac, doubl
   Misc m;
   BLP_HIP(hipMemcpy(&m, b->d_misc, sizeof(Misc), hipMemcpyDeviceToHost));
   if (np) {
+    if (cn) prefault_host(cn, 4 * (size_t)np);
+    if (jac) prefault_host(jac, 8 * (size_t)np);
+    if (aa) prefault_host(aa, 8 * (size_t)np);
     if (cn) BLP_HIP(hipMemcpy(cn, b->d_cn, 4 * np, hipMemcpyDeviceToHost));
     if (jac) BLP_HIP(hipMemcpy(jac, b->d_jac, 8 * np, hipMemcpyDeviceToHost));
     if (aa) BLP_HIP(hipMemcpy(aa, b->d_aa, 8 * np, hipMemcpyDeviceToHost));
@@ -3750,6 +3753,7 @@ int blp_batch_fetch_repr(blp_graph* g, blp_batch* b, int which, int zero_int, ch
   if ((rc = slots.reserve((size_t)blp::REPR_SLOT_BYTES * np))) return rc;
   rc = repr_launch(which == BLP_JACCARD ? b->d_jac : b->d_aa, np, zero_int != 0, slots.as<char>(), g->n_cu, b->stream);
   if (rc) return rc;
+  prefault_host(out, (size_t)blp::REPR_SLOT_BYTES * np);  // while the formatter runs
   BLP_HIP(hipMemcpyAsync(out, slots.p, (size_t)blp::REPR_SLOT_BYTES * np, hipMemcpyDeviceToHost, b->stream));
   BLP_HIP(hipStreamSynchronize(b->stream));
   return BLP_OK;
