@@ -958,7 +958,7 @@ def exchange_check(dist, dev, a, b, U, B, G, timeout_s=120.0):
     union's CSR is built in HBM. The union is the whole graph, so its CSR must equal the
     replica's (checked). Reported beside the headline, never part of it. A watchdog bounds the
     collective: if it has not returned in timeout_s, rank 0 still prints its line (exchange
-    marked as timed out) and every rank exits."""
+    marked as timed out) and every rank exits with status 3 (main)."""
     import threading
 
     from blp import dist as bd
@@ -1203,9 +1203,13 @@ def main():
             out["cpu_baseline"]["multicore"] = multi
     if dist.rank == 0:
         print(json.dumps(out), flush=True)
-    if exchange and exchange.get("timed_out"):  # a collective still blocked in RCCL: do not wait for it
+    if exchange and exchange.get("timed_out"):
+        # a collective still blocked in RCCL: do not wait for it, and do not report success -- the
+        # line above stands, but a hung exchange on an N-GPU run must read as a failed job
+        log("exchange watchdog fired: exiting with status 3")
         sys.stdout.flush()
-        os._exit(0)
+        sys.stderr.flush()
+        os._exit(3)
 
 
 if __name__ == "__main__":

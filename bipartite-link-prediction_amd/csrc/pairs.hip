@@ -2766,6 +2766,8 @@ struct Knobs {
   int split_short = -1;          // BLP_SPLIT_SHORT: register-scanned slice bound (0: off)
   int cosched_cus = -1;          // BLP_COSCHED_CUS: tuning override of the co-scheduled CU share
   bool no_pko = false;           // BLP_NO_PKO: the large scorer's general variant instead of PKO
+  std::string debug_null;        // BLP_DEBUG_NULL (BLP_DEBUG builds only): null this launch pointer, to
+                                 // show the pre-launch pointer check (launch_pointers) refusing it
 };
 
 Knobs read_knobs() {
@@ -2796,6 +2798,9 @@ Knobs read_knobs() {
   k.split_short = (int)num("BLP_SPLIT_SHORT", -1);
   k.cosched_cus = (int)num("BLP_COSCHED_CUS", -1);
   k.no_pko = on("BLP_NO_PKO");
+#ifdef BLP_DEBUG
+  if (const char* e = getenv("BLP_DEBUG_NULL")) k.debug_null = e;
+#endif
   return k;
 }
 }  // namespace
@@ -2913,6 +2918,67 @@ static int launch_heavy(hipStream_t st, const HeavyArgs& h, int64_t n_items) {
   hipLaunchKernelGGL((k_heavy<BLOCK, CAP, SEG>), dim3((unsigned)n_items), dim3(BLOCK), 0, st, h);
   BLP_HIP(hipGetLastError());
   return BLP_OK;
+}
+
+// Every device pointer the chosen launch path dereferences, checked on the host before anything is
+// enqueued: a null base pointer is not an index, so the kernels' PS_OK bound checks cannot see it,
+// and a kernel writing through one faults the GPU (round 4: k_score_split's long-slice queue). The
+// scorer arguments are gathered into `a` first, so this sees exactly what the kernels will read.
+static int launch_pointers(const blp_graph* g, const blp_batch* b, ScoreArgs& a, uint32_t mask) {
+#ifdef BLP_DEBUG
+  if (!b->kn.debug_null.empty()) {  // test knob: null one pointer to show the check refusing it
+    const std::string& f = b->kn.debug_null;
+    if (f == "g_yb") a.g_yb = nullptr;
+    if (f == "cn") a.cn = nullptr;
+    if (f == "lq") a.lq = nullptr;
+    if (f == "wedge") a.wedge = nullptr;
+  }
+#endif
+  const char* missing = nullptr;
+  auto need = [&](const void* p, const char* what) {
+    if (!p && !missing) missing = what;
+  };
+  need(a.rp, "row_ptr");
+  need(a.ci, "col_idx");
+  need(a.cw, "coded col_idx");
+  need(a.off, "source offsets");
+  need(a.cnt, "source counts");
+  need(a.active, "active sources");
+  need(a.g_out, "grouped caller index");
+  need(a.g_yb, "grouped row starts");
+  need(a.g_yl, "grouped row lengths");
+  need(a.misc, "batch counters");
+  need(a.cn, "cn output");
+  need(a.jac, "jaccard output");
+  need(a.aa, "adamic output");
+  if (mask & BLP_ADAMIC) need(a.aaw, "aa weights");
+  if (a.hot_idx) {
+    need(a.hot_tab, "dense-row table");
+    need(a.hot_pool, "dense-row pool");
+  }
+  if (a.heavy_slot) need(a.heavy_bm, "pre-built bitmaps");
+  if ((a.wp != nullptr) != (a.wedge != nullptr)) missing = missing ? missing : "wedge rows (offsets without ids)";
+  if (b->chunks > 1 && (mask & BLP_ADAMIC)) need(a.aa_part, "chunk AA partials");
+  if (b->n_heavy) {
+    need(b->d_heavy_bm, "heavy bitmaps");
+    need(b->d_heavy_items, "heavy items");
+  }
+  if (b->split) {
+    need(a.lq, "long-slice queues");
+    need(b->d_gy, "grouped y");
+    need(b->d_rsplit, "row split table");
+    need(b->d_pcn, "chunk counts");
+    need(b->d_ph2, "chunk |H2| partials");
+    if (mask & BLP_ADAMIC) need(b->d_paa, "chunk AA words");
+    if (b->d_hflag) need(b->d_active2, "partitioned active list");
+  }
+  if (b->global) need(b->d_gbm, "HBM bitmap slots");
+  if ((b->use_short || (b->variant == V_LARGE && !b->split && !b->global)) && b->n_sources) need(b->d_rec, "source records");
+  if (!missing) return BLP_OK;
+  char msg[160];
+  snprintf(msg, sizeof msg, "blp_batch_score: the launch path reads a null device pointer (%s)", missing);
+  (void)g;
+  return fail(BLP_E_STATE, msg);
 }
 
 extern "C" {
@@ -3554,16 +3620,21 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   a.hot_vecs = g->hot_pool_words / 4;
   a.lq_wgs = b->d_lq ? 2 * g->n_cu : 0;
   if (np && b->split) {
-    // AA counts ride in the packed per-pair word while every row (hence every count) < 2^24
-    const int pk24 = (mask & BLP_ADAMIC) && g->max_row < (int64_t(1) << SPLIT_CN_BITS) && !b->kn.split_nopk;
-    // slices of <= short_max ids scanned by their pair's thread (128 KiB chunks; BLP_SPLIT_SHORT=0: off)
-    const int short_max = std::min(SHORT_PART, b->kn.split_short >= 0 ? b->kn.split_short : SHORT_PART);
-    a.lq = b->d_lq;  // k_score_split's long-slice queues (SPLIT_LQ entries per resident workgroup)
-    BLP_CHECK(a.lq, BLP_E_STATE, "blp_batch_score: split batch without its long-slice queues");
+    a.lq = b->d_lq;
     if (g->d_wp && !b->kn.no_wedge) {  // sources with wedge rows build from them (split and hash kernels)
       a.wp = g->d_wp;
       a.wedge = reinterpret_cast<const uint4*>(g->d_wedge);
     }
+  } else if (np && b->use_short && g->d_wp && !b->kn.no_wedge) {  // test knob: BLP_NO_WEDGE builds from CSR
+    a.wp = g->d_wp;
+    a.wedge = reinterpret_cast<const uint4*>(g->d_wedge);
+  }
+  if (np && (rc = launch_pointers(g, b, a, mask))) return rc;
+  if (np && b->split) {
+    // AA counts ride in the packed per-pair word while every row (hence every count) < 2^24
+    const int pk24 = (mask & BLP_ADAMIC) && g->max_row < (int64_t(1) << SPLIT_CN_BITS) && !b->kn.split_nopk;
+    // slices of <= short_max ids scanned by their pair's thread (128 KiB chunks; BLP_SPLIT_SHORT=0: off)
+    const int short_max = std::min(SHORT_PART, b->kn.split_short >= 0 ? b->kn.split_short : SHORT_PART);
     // CUs the persistent grids may fill (blp_batches_score), within [1, n_cu]: d_lq holds 2 workgroups per CU
     const int scu = std::max(1, std::min(b->cus > 0 ? b->cus : g->n_cu, g->n_cu));
     if (b->d_hflag) {  // small-H2 sources first, on their own hash-set kernel
@@ -3602,10 +3673,6 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   } else if (np && b->use_short) {
     // bitmap in dynamic LDS, sized to the universe (whole 16-byte vectors)
     const size_t dyn = 4 * (size_t)std::max<int64_t>(4, ((b->hi - b->lo + 31) / 32 + 3) / 4 * 4);
-    if (g->d_wp && !b->kn.no_wedge) {  // test knob: BLP_NO_WEDGE builds from CSR
-      a.wp = g->d_wp;
-      a.wedge = reinterpret_cast<const uint4*>(g->d_wedge);
-    }
     if (b->d_rec) {  // one record per active source (after grouping, on the batch stream)
       hipLaunchKernelGGL(k_source_records, dim3((unsigned)std::min<int64_t>((b->n_sources + 255) / 256, 2048)),
                          dim3(256), 0, b->stream, a.active, b->d_misc, a.off, a.cnt, g->d_rp, g->d_ci, a.heavy_slot,
@@ -3747,6 +3814,17 @@ int blp_batch_fetch_repr(blp_graph* g, blp_batch* b, int which, int zero_int, ch
   BLP_HIP(hipStreamSynchronize(b->stream));
   Misc m;
   BLP_HIP(hipMemcpy(&m, b->d_misc, sizeof(Misc), hipMemcpyDeviceToHost));
+#ifdef BLP_DEBUG
+  if (m.dbg[0]) {  // the same bound-check report as blp_batch_fetch: no slots from a violating batch
+    const long long z[4] = {0, 0, 0, 0};
+    BLP_HIP(hipMemcpy(b->d_misc->dbg, z, sizeof(z), hipMemcpyHostToDevice));
+    char msg[160];
+    snprintf(msg, sizeof msg,
+             "blp_batch_fetch_repr [BLP_DEBUG]: %lld bound violations; first at site %lld: %lld vs bound %lld",
+             m.dbg[0], m.dbg[1], m.dbg[2], m.dbg[3]);
+    return fail(BLP_E_STATE, msg);
+  }
+#endif
   if (which == BLP_JACCARD && m.zero_div) return fail(BLP_E_ZERODIV, "float division by zero (Jaccard union is empty)");
   if (np == 0) return BLP_OK;
   ScopedBuf slots;

@@ -1597,7 +1597,8 @@ extern "C" int blp_topk_stats(blp_topk* t, int which, double* total_ms, int64_t*
   // 3: sum of |H2(x)|; 4: sum over x and w in H2(x) of |N(w)| (the push volume of one pass);
   // 5: sources whose AA top-k came straight from the fused sums; 6: row entries actually pushed by
   // the count pass (walk + dense corrections); 7: dense target counts added; 8 (above): bytes read
-  // per dense add  BLP_HIP(hipStreamSynchronize(t->g->stream));
+  // per dense add
+  BLP_HIP(hipStreamSynchronize(t->g->stream));  // blp_topk_run is asynchronous on g->stream
   unsigned long long c[8];
   BLP_HIP(hipMemcpy(c, t->counters.p, 64, hipMemcpyDeviceToHost));
   if (total_ms) *total_ms = 0.0;

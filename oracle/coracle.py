@@ -30,6 +30,7 @@ def lib():
         L.og_nnz.argtypes = [P]
         L.og_score_pairs.restype = ctypes.c_int
         L.og_score_pairs.argtypes = [P, ctypes.c_int64, P, P, ctypes.c_uint32, P, P, P, P, ctypes.c_int]
+        L.og_csr.argtypes = [P, P, P]
         L.og_hop3.restype = ctypes.c_int64
         L.og_hop3.argtypes = [P, ctypes.c_int64, P, P, P, ctypes.c_int64]
         _LIB = L
@@ -53,6 +54,20 @@ class OracleGraph:
         if getattr(self, "h", None):
             lib().og_destroy(self.h)
             self.h = None
+
+    def csr(self):
+        """(row_ptr int64[n + 1], col_idx int32[nnz]): read-only views of the oracle's own CSR,
+        valid while this graph lives."""
+        L = lib()
+        rp = ctypes.POINTER(ctypes.c_int64)()
+        ci = ctypes.POINTER(ctypes.c_int32)()
+        L.og_csr(self.h, ctypes.byref(rp), ctypes.byref(ci))
+        nnz = int(L.og_nnz(self.h))
+        r = np.ctypeslib.as_array(rp, (self.n + 1,))
+        c = np.ctypeslib.as_array(ci, (max(nnz, 1),))[:nnz]
+        r.flags.writeable = False
+        c.flags.writeable = False
+        return r, c
 
     def score_pairs(self, x, y, mask=7, nthreads=1):
         """-> (cn uint32, jaccard f64, adamic f64, |H2(x)| uint32) per pair."""

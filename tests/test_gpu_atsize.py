@@ -8,7 +8,8 @@ factors (svd.py:28-30). Marked `gpu`.
   config 3  full-candidate top-k on the 10M-edge graph (hop-3 set, dataset_maker.py:139)
   config 4  rank-64 SVD top-k on the 2M x 200K, 50M-draw matrix: dense MFMA and norm-pruned
   config 5  the 50M-user x 2M-business universe: 48 chunk-parallel 128 KiB chunks on the user
-            side, the hash-set partition on the business side (100M of the 1B draws)
+            side, the hash-set partition on the business side -- a fast geometry check on 100M
+            of the draws, and the full 1B draws through the RCCL exchange (blp_multi_gather_csr)
 """
 import os
 
@@ -254,6 +255,77 @@ def test_config5_geometry_at_size(gpu):
     cn, jac, _, _ = og.score_pairs(ex_y, ex_x, 3, nthreads=NT)  # every business source's pairs
     np.testing.assert_array_equal(gb["cn"], cn)
     np.testing.assert_array_equal(gb["jaccard"], jac)
+    for bt in (ub, bb):
+        bt.close()
+    G.close()
+
+
+def test_config5_full_1b_draws_through_rccl_exchange(gpu):
+    """Config 5's own workload (BASELINE.json configs[4]): the 50M-user x 2M-business universe
+    with ALL 1B draws (dataset_maker.py:139 / similarity.py:20-106 at that scale). The row-block
+    generator (dist.block_review_edges) makes the partial of the whole user range -- world 1 --
+    and it goes through the exchange the N-GPU bench runs: libblp's own RCCL communicator
+    (blp_multi_gather_csr: counts, then the padded partials in one ncclAllGather, the CSR built
+    in HBM), then the graph handle over that device CSR. Checked:
+      - the gathered union CSR equals the C oracle's CSR of the same 1B edges (built on the host,
+        independently: row pointers and every column id), so every duplicate was merged once;
+      - the plan: 48 chunk-parallel 128 KiB chunks on the user side, the hash-set partition on
+        the business side;
+      - 24 user sources (every candidate pair: CN, Jaccard, AA) and the >100K business sources
+        of the transposed list (CN, Jaccard) bit-exact against the oracle on that graph.
+    Runtime on one MI355X box: see DESIGN.md §6 (config 5 parity in the suite)."""
+    import time
+
+    from blp import dist as bd
+    from blp.multi import Multi
+
+    U, B, D = synth.CONFIGS["c5"]
+    t0 = time.time()
+    u, b = bd.block_review_edges(U, B, D, 0, U, seed=0)
+    u = u.astype(np.int32)
+    b = b.astype(np.int32)
+    assert len(u) == D
+    t_gen = time.time() - t0
+    with bd.stdout_to_stderr():  # RCCL's banner
+        m = Multi(Multi.unique_id(), 1, 0, gpu)
+    t0 = time.time()
+    c = m.gather_csr(u, b, U + B)
+    t_x = time.time() - t0
+    assert m.bytes_in == 0  # world 1: nothing arrives from another rank
+    m.close()
+    G = blp.DeviceGraph.from_csr_handle(c, U + B, U, device=gpu)
+    t0 = time.time()
+    og = coracle.OracleGraph(U + B, u, b)
+    t_og = time.time() - t0
+    del u, b
+    orp, oci = og.csr()
+    assert G.nnz == len(oci) and G.nnz > 1_990_000_000
+    np.testing.assert_array_equal(G.row_ptr, orp)
+    assert np.array_equal(G.col_idx, oci)  # 2G column ids: the union CSR is the oracle's
+    rng = np.random.default_rng(77)
+    cand = np.flatnonzero(G.hop1_size[:U] >= 4)
+    src = np.sort(rng.choice(cand, 24, replace=False)).astype(np.int32)
+    ex_x, ex_y = synth.uniform_examples(G, src, rate=0.01, seed=11)
+    assert len(ex_x) > 24 * 15_000
+    ub, bb = G.batch(ex_x, ex_y), G.batch(ex_y, ex_x)
+    pu, pb = ub.plan(), bb.plan()
+    assert pu["chunks"] == -48 and pu["hi"] - pu["lo"] > 45_000_000, pu
+    assert pb["chunks"] < 0 and pb["hash_sources"] > 0 and pb["sources"] > 100_000, pb
+    t0 = time.time()
+    G.score_batches([(ub, 7), (bb, 3)])
+    gu, gb = ub.fetch(7), bb.fetch(3)
+    t_sc = time.time() - t0
+    t0 = time.time()
+    cn, jac, aa, _ = og.score_pairs(ex_x, ex_y, 7, nthreads=NT)
+    np.testing.assert_array_equal(gu["cn"], cn)
+    np.testing.assert_array_equal(gu["jaccard"], jac)
+    np.testing.assert_array_equal(gu["adamic"], aa)
+    cn, jac, _, _ = og.score_pairs(ex_y, ex_x, 3, nthreads=NT)
+    np.testing.assert_array_equal(gb["cn"], cn)
+    np.testing.assert_array_equal(gb["jaccard"], jac)
+    t_or = time.time() - t0
+    print("config5 1B: generate %.1fs, exchange+CSR %.1fs, oracle graph %.1fs, score %.2fs, oracle score %.1fs, "
+          "%d + %d pairs" % (t_gen, t_x, t_og, t_sc, t_or, len(ex_x), len(ex_y)))
     for bt in (ub, bb):
         bt.close()
     G.close()

@@ -73,3 +73,19 @@ def test_debug_build_reports_overfilled_hash_table(gpu):
     r = _run("overfill", {"BLP_SPLIT": "3", "BLP_HASH_WORK": "1000000000"})
     assert r.returncode == 3, (r.stdout[-2000:], r.stderr[-2000:])
     assert "BLP_DEBUG" in r.stdout and "site 8" in r.stdout, r.stdout[-2000:]
+
+
+@pytest.mark.parametrize("field,extra", [
+    ("g_yb", {}),
+    ("cn", {}),
+    ("lq", {"BLP_SPLIT": "3"}),
+    ("wedge", {}),
+])
+def test_null_launch_pointer_is_refused(gpu, field, extra):
+    """A launch path's device pointer nulled (BLP_DEBUG_NULL, debug build only) is refused on the
+    host by blp_batch_score's pre-launch check (pairs.hip launch_pointers) with the pointer's
+    name, before any kernel runs: the class of bug behind round 4's k_score_split fault (a
+    dropped queue pointer) fails the call instead of the GPU."""
+    r = _run("null " + field, dict(extra, BLP_DEBUG_NULL=field))
+    assert r.returncode == 3, (r.stdout[-2000:], r.stderr[-2000:])
+    assert "null device pointer" in r.stdout, r.stdout[-2000:]

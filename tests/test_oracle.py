@@ -189,6 +189,30 @@ def test_c_oracle_matches_scipy_formulation(seed):
     np.testing.assert_array_equal(jac, scn / uni)
 
 
+@pytest.mark.parametrize("threads", [2, 7])
+def test_c_oracle_partitioned_build_equals_serial(threads, monkeypatch):
+    """og_create's many-thread path (edges partitioned by row range, each range counting-sorted
+    on its own: what builds the 1B-edge config-5 oracle) gives the serial path's CSR, self-loops,
+    duplicates and reversed duplicates included, and the same scores."""
+    rng = np.random.default_rng(threads)
+    a = rng.integers(0, 3000, 60000)
+    b = 3000 + np.minimum((rng.pareto(1.0, 60000) * 20).astype(np.int64), 999)
+    a[:50] = b[:50]  # self-loops
+    a = np.concatenate([a, b[:500]])  # reversed duplicates
+    b = np.concatenate([b, a[:500]])
+    monkeypatch.setenv("OG_THREADS", "1")
+    g1 = coracle.OracleGraph(4000, a, b)
+    monkeypatch.setenv("OG_THREADS", str(threads))
+    g2 = coracle.OracleGraph(4000, a, b)
+    (r1, c1), (r2, c2) = g1.csr(), g2.csr()
+    np.testing.assert_array_equal(r1, r2)
+    np.testing.assert_array_equal(c1, c2)
+    x = rng.integers(0, 4000, 2000).astype(np.int32)
+    y = rng.integers(0, 4000, 2000).astype(np.int32)
+    for p, q in zip(g1.score_pairs(x, y, 5), g2.score_pairs(x, y, 5)):  # (isolated ids: no Jaccard)
+        np.testing.assert_array_equal(p, q)
+
+
 @settings(max_examples=40, deadline=None)
 @given(st.lists(st.tuples(st.integers(0, 25), st.integers(0, 25)), min_size=1, max_size=80),
        st.integers(0, 10 ** 6))
