@@ -534,6 +534,83 @@ __global__ __launch_bounds__(GB_BLOCK) void k_item_write_runs(const int64_t* __r
   }
 }
 
+// The short-row scorer's variant of k_item_write_runs (round 5): it writes each grouped pair's
+// caller index and y only (g_out, g_y: 8 B per pair, in whole runs) and leaves N(y)'s row bounds
+// to the scorer (pair_row: rp[y], rp[y + 1] in one 16-byte load, issued with the pair's other
+// metadata before the H2 build). No random row-pointer gathers here, and the stage holds 8-byte
+// records (32 KiB): twice the resident workgroups of the 16-byte version.
+template <int KEYS>
+__global__ __launch_bounds__(GB_BLOCK) void k_item_write_ids(const int4* __restrict__ tmp, const int32_t* __restrict__ item_b,
+                                                             const int32_t* __restrict__ item_s,
+                                                             const int32_t* __restrict__ item_e,
+                                                             const int32_t* __restrict__ n_items, int32_t xlo, int lognb,
+                                                             const int32_t* __restrict__ ih,
+                                                             const int32_t* __restrict__ off, int32_t* __restrict__ fill,
+                                                             int32_t* __restrict__ g_out, int32_t* __restrict__ g_y) {
+  static_assert(KEYS <= 1024, "key tables in LDS");
+  constexpr int PER = KEYS >= GB_BLOCK ? KEYS / GB_BLOCK : 1;
+  __shared__ int h[KEYS];      // local cursors
+  __shared__ int lofs[KEYS];   // the key's first local position
+  __shared__ int gbase[KEYS];  // ... and its first global position
+  __shared__ int2 stage[GI_PAIRS];
+  __shared__ int red[GB_BLOCK / 64];
+  const int i = blockIdx.x;
+  if (i >= *n_items) return;
+  const int b = item_b[i], s = item_s[i], e = item_e[i];
+  int c[PER];
+  int v = 0;
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const int j = (int)threadIdx.x * PER + q;
+    c[q] = j < KEYS ? ih[(int64_t)i * KEYS + j] : 0;
+    v += c[q];
+  }
+  int tot;
+  int o = block_exscan_i<GB_BLOCK>(v, red, &tot);
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const int j = (int)threadIdx.x * PER + q;
+    if (j < KEYS) {
+      const int vv = b + (j << lognb);
+      lofs[j] = o;
+      gbase[j] = c[q] ? off[xlo + vv] + atomicAdd(&fill[vv], c[q]) : 0;
+      h[j] = o;
+      o += c[q];
+    }
+  }
+  __syncthreads();
+  constexpr int U = 4;
+  for (int kr = s; kr < e; kr += U * GB_BLOCK) {  // the item's records, staged in key order
+    int4 t[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = kr + u * GB_BLOCK + (int)threadIdx.x;
+      t[u] = k < e ? tmp[k] : make_int4(-1, xlo, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (t[u].x >= 0) stage[atomicAdd(&h[(t[u].y - xlo) >> lognb], 1)] = make_int2(t[u].x, t[u].z);
+  }
+  __syncthreads();
+  const int n = e - s;
+  for (int p = (int)threadIdx.x; p < n; p += GB_BLOCK) {  // consecutive local slots -> consecutive positions
+    // the slot's key: the LAST j with lofs[j] <= p (lofs[0] = 0 <= p). Empty keys share their start
+    // with the next key, so the last such j is the non-empty key whose run holds p.
+    int lo = 0, hi = KEYS;
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (lofs[mid] <= p)
+        lo = mid;
+      else
+        hi = mid;
+    }
+    const int2 r = stage[p];
+    const int pos = gbase[lo] + (p - lofs[lo]);
+    g_out[pos] = r.x;
+    g_y[pos] = r.y;
+  }
+}
+
 // active sources = ids with cnt > 0, ascending (tile counts -> scan -> writes)
 __global__ __launch_bounds__(SCAN_BLOCK) void k_nz_count(const int32_t* __restrict__ cnt, int64_t n,
                                                          int32_t* __restrict__ tile_cnt) {
@@ -1586,6 +1663,7 @@ struct ScoreArgs {
   const int32_t* g_out;    // grouped position -> caller index
   const int64_t* g_yb;     // grouped position -> start of N(y) in ci
   const int32_t* g_yl;     // grouped position -> |N(y)|
+  const int32_t* g_yn;     // grouped position -> y (short-row scorer: N(y)'s bounds from rp; null: g_yb / g_yl)
   const int32_t* hot_idx;     // per node: dense-row number or -1 (null: no dense rows)
   const blp::HotRow* hot_tab;
   const uint4* hot_pool;
@@ -1612,6 +1690,27 @@ struct ScoreArgs {
   int64_t n_hot, hot_vecs;      // dense rows, their pool's vectors (BLP_DEBUG bounds)
   int lq_wgs;                   // workgroups d_lq was sized for (BLP_DEBUG bound)
 };
+
+// N(y)'s row [st, st + len) of grouped pair gp. YN (the short-row scorer) with a.g_yn set: from
+// y's row pointers, rp[y] and rp[y + 1] in one 16-byte load (k_item_write_ids groups only y);
+// otherwise from the grouped metadata g_yb / g_yl.
+template <bool YN>
+__device__ __attribute__((always_inline)) inline void pair_row(const ScoreArgs& a, int gp, int64_t& st, int& len) {
+  if (YN && a.g_yn) {
+    const int y = a.g_yn[gp];
+    if (!PS_OK(a.misc, y >= 0 && y < a.n_nodes, 2, y, a.n_nodes)) {
+      st = 0;
+      len = 0;
+      return;
+    }
+    const blp::U4a r = *reinterpret_cast<const blp::U4a*>(a.rp + y);
+    st = (int64_t)(((uint64_t)(uint32_t)r.y << 32) | (uint32_t)r.x);
+    len = (int)((int64_t)(((uint64_t)(uint32_t)r.w << 32) | (uint32_t)r.z) - st);
+  } else {
+    st = a.g_yb[gp];
+    len = a.g_yl[gp];
+  }
+}
 
 template <int BLOCK, bool TAIL = true>  // TAIL: see block_exscan
 __device__ inline unsigned long long block_sum_u64(unsigned long long v, unsigned long long* red) {
@@ -1757,8 +1856,7 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
       constexpr bool PF = SHORT ? BLP_PF : (RC && BLP_PFL);
       if (PF && nchunks == 1 && (int)threadIdx.x < min(SEG, pcnt)) {
         const int gp = pbeg + threadIdx.x;
-        pf_start = a.g_yb[gp];
-        pf_len = a.g_yl[gp];
+        pair_row<SHORT>(a, gp, pf_start, pf_len);
         pf_out = a.g_out[gp];
       }
       PROF(1)
@@ -1919,8 +2017,9 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
             }
           } else if ((int)threadIdx.x < ns) {
             const int gp = pbeg + sb + threadIdx.x;
-            s_start[threadIdx.x] = a.g_yb[gp];
-            len = a.g_yl[gp];
+            int64_t st;
+            pair_row<SHORT>(a, gp, st, len);
+            s_start[threadIdx.x] = st;
             pout = a.g_out[gp];  // used after the scan: its latency hides behind it
             if (!PKO) s_cn[threadIdx.x] = 0;
             if (SAA) {
@@ -2766,6 +2865,7 @@ struct Knobs {
   int split_short = -1;          // BLP_SPLIT_SHORT: register-scanned slice bound (0: off)
   int cosched_cus = -1;          // BLP_COSCHED_CUS: tuning override of the co-scheduled CU share
   bool no_pko = false;           // BLP_NO_PKO: the large scorer's general variant instead of PKO
+  bool group_rows = false;       // BLP_GROUP_ROWS: short-row batches group N(y)'s bounds too (k_item_write_runs)
   std::string debug_null;        // BLP_DEBUG_NULL (BLP_DEBUG builds only): null this launch pointer, to
                                  // show the pre-launch pointer check (launch_pointers) refusing it
 };
@@ -2798,6 +2898,7 @@ Knobs read_knobs() {
   k.split_short = (int)num("BLP_SPLIT_SHORT", -1);
   k.cosched_cus = (int)num("BLP_COSCHED_CUS", -1);
   k.no_pko = on("BLP_NO_PKO");
+  k.group_rows = on("BLP_GROUP_ROWS");
 #ifdef BLP_DEBUG
   if (const char* e = getenv("BLP_DEBUG_NULL")) k.debug_null = e;
 #endif
@@ -2864,6 +2965,7 @@ struct blp_batch {
   int32_t* d_active2 = nullptr;  // the active list partitioned by k_hash_partition (with d_hflag)
   int64_t n_hash = 0;          // such sources
   bool use_short = false;   // the short-row scorer takes this batch (decided once, at create)
+  bool yn_grouped = false;  // short-row batch grouped by k_item_write_ids: the scorer reads g_yn = d_gy
   int64_t work_elems = 0;  // planned build + scan elements (co-scheduling estimate)
   Knobs kn;               // environment switches, read once at create
 };
@@ -2945,8 +3047,10 @@ static int launch_pointers(const blp_graph* g, const blp_batch* b, ScoreArgs& a,
   need(a.cnt, "source counts");
   need(a.active, "active sources");
   need(a.g_out, "grouped caller index");
-  need(a.g_yb, "grouped row starts");
-  need(a.g_yl, "grouped row lengths");
+  if (!a.g_yn) {
+    need(a.g_yb, "grouped row starts");
+    need(a.g_yl, "grouped row lengths");
+  }
   need(a.misc, "batch counters");
   need(a.cn, "cn output");
   need(a.jac, "jaccard output");
@@ -3326,6 +3430,9 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   if (b->chunks > 1 && hipMalloc(&b->d_aa_part, 16 * np) != hipSuccess)
     return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: hipMalloc failed"));
   b->use_short = short_kernel(b);  // fixed here: d_rec's allocation and the launch must agree
+  // short-row batches grouped by items carry y per grouped pair (k_item_write_ids), not N(y)'s bounds
+  if (b->use_short && !b->runs && b->items && !kn.group_rows && !b->d_gy && hipMalloc(&b->d_gy, 4 * np) != hipSuccess)
+    return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: hipMalloc failed"));
   // source records: the short-row scorer, and the large scorer (its header in one round trip)
   const bool want_rec = b->use_short || (b->variant == V_LARGE && !b->split && !b->global);
   if (want_rec &&
@@ -3487,6 +3594,8 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
                          &b->d_misc->n_items);
       const int64_t keys = (b->xspan + b->nb - 1) >> b->shift;
       const bool runs_w = keys <= 1024;
+      const bool ids_w = b->use_short && b->d_gy && !b->kn.group_rows;  // k_item_write_ids (short-row scorer)
+      b->yn_grouped = runs_w && ids_w;
       int32_t* ih = tx2 + tx + 1;  // [ub][K] item histograms (runs_w)
 #define BLP_ITEM_LAUNCH(K)                                                                                         \
   hipLaunchKernelGGL(k_item_count<K>, dim3((unsigned)ub), dim3(GB_BLOCK), 0, b->stream, tmp, it_b, it_s, it_e,     \
@@ -3499,7 +3608,11 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   hipLaunchKernelGGL(k_scan_mid, dim3(1), dim3(SCAN_BLOCK), 0, b->stream, tx2, tx, &b->d_misc->n_active);          \
   hipLaunchKernelGGL(k_nz_write, dim3((unsigned)tx), dim3(SCAN_BLOCK), 0, b->stream, cnt + b->xlo, b->xspan, tx2,  \
                      b->xlo, b->active.as<int32_t>());                                                              \
-  if (runs_w)                                                                                                         \
+  if (runs_w && ids_w)                                                                                                \
+    hipLaunchKernelGGL(k_item_write_ids<(K <= 1024 ? K : 1024)>, dim3((unsigned)ub), dim3(GB_BLOCK), 0, b->stream,   \
+                       tmp, it_b, it_s, it_e, &b->d_misc->n_items, b->xlo, b->shift, ih, off, fill, b->d_gout,        \
+                       b->d_gy);                                                                                      \
+  else if (runs_w)                                                                                                    \
     hipLaunchKernelGGL(k_item_write_runs<(K <= 1024 ? K : 1024)>, dim3((unsigned)ub), dim3(GB_BLOCK), 0, b->stream,  \
                        g->d_rp, tmp, it_b, it_s, it_e, &b->d_misc->n_items, b->xlo, b->shift, ih, off, fill,         \
                        b->d_gout, b->d_gyb, b->d_gyl, b->d_gy);                                                       \
@@ -3595,6 +3708,7 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   a.g_out = b->d_gout;
   a.g_yb = b->d_gyb;
   a.g_yl = b->d_gyl;
+  a.g_yn = b->use_short && b->yn_grouped ? b->d_gy : nullptr;
   a.hot_idx = b->use_hot ? g->d_hot_idx : nullptr;
   a.hot_tab = (const HotRow*)g->d_hot_tab;
   a.hot_pool = (const uint4*)g->d_hot_pool;
