@@ -1167,6 +1167,11 @@ def main():
             "parallelism": "replicas x%d (graph replicated, users split, no collective)" % dist.world,
         },
         "kernels_ms": ktimes,
+        # a NEW pair list's rate: planning both batches (blp_batch_create: upload + device planning
+        # pass) plus one step, as similarity.main pays it once per call (never `value`)
+        "including_batch_create": {"batch_create_s": round(t_batch, 4),
+                                   "seconds": t_batch + t_max / args.steps,
+                                   "pairs_per_s": len(ex_x) / (t_batch + t_max / args.steps)},
         "exchange": exchange,
         # outside the timed step (once per graph / per example set), reported for completeness
         "setup_s": {"edge_generation": round(t_gen, 3), "graph_build": round(t_graph, 3),

@@ -150,6 +150,14 @@ struct blp_graph {
   std::vector<unsigned long long> h_w2;
   std::vector<int32_t> h_lo2, h_hi2, h_maxd;
   std::vector<uint8_t> h_flag2;
+  // ... and their device arrays, kept for blp_batch_create's device planning pass (k_plan_pairs)
+  unsigned long long* d_w2 = nullptr;
+  int32_t *d_lo2 = nullptr, *d_hi2 = nullptr, *d_maxd = nullptr;
+  uint8_t* d_flag2 = nullptr;
+  // batch streams returned by destroyed batches, handed to the next ones (blp_batch_create):
+  // a stream per batch keeps the passes of a step concurrent without a hipStreamCreate per batch
+  std::vector<hipStream_t> stream_pool;
+  std::mutex stream_mu;
   // wedge-row bitmaps (hop3.hip, blp::wedge_bitmaps): the SET of ids of each long wedge row over
   // an id range [lo, hi), built on first use per range (the hop-3 mark range; the business
   // batch's universe) and kept with the graph (at most 4 ranges)
@@ -182,6 +190,7 @@ int build_hot_index(blp_graph* g);
 int graph_finish(blp_graph* g, const double* aaw);
 int build_wedge_index(blp_graph* g);
 int build_node2(blp_graph* g);  // after build_hot_index (the dense-row flag)
+void free_node2(blp_graph* g);
 constexpr int REPR_SLOT_BYTES = 24;  // repr.h REPR_SLOT
 // repr(v) of n device doubles into 24-byte slots at d_out (repr.hip); enqueued on s
 int repr_launch(const double* d_v, int64_t n, bool zero_int, char* d_out, int n_cu, hipStream_t s);

@@ -398,6 +398,9 @@ int blp_graph_destroy(blp_graph* g) {
   for (auto& t : g->timers) timer_release(t);
   free_hot_index(g);
   free_wedge_index(g);
+  free_node2(g);
+  for (hipStream_t st : g->stream_pool) (void)hipStreamDestroy(st);
+  g->stream_pool.clear();
   if (g->d_rp) (void)hipFree(g->d_rp);
   if (g->d_ci) (void)hipFree(g->d_ci - CI_PAD);
   if (g->d_aaw_fx) (void)hipFree(g->d_aaw_fx);

@@ -127,30 +127,39 @@ int build_node2(blp_graph* g) {
   g->h_hi2.assign((size_t)n, 0);
   g->h_maxd.assign((size_t)n, 0);
   g->h_flag2.assign((size_t)n, 0);
+  free_node2(g);
   if (n == 0 || nnz == 0) return BLP_OK;
-  ScopedBuf w2, lo2, hi2, md, fl;
-  int rc;
-  if ((rc = w2.reserve(8 * (size_t)n)) || (rc = lo2.reserve(4 * (size_t)n)) || (rc = hi2.reserve(4 * (size_t)n)) ||
-      (rc = md.reserve(4 * (size_t)n)) || (rc = fl.reserve(((size_t)n + 3) / 4 * 4)))
-    return rc;
-  BLP_HIP(hipMemsetAsync(w2.p, 0, 8 * (size_t)n, g->stream));
-  BLP_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(lo2.p), INT32_MAX, (size_t)n, g->stream));
-  BLP_HIP(hipMemsetAsync(hi2.p, 0, 4 * (size_t)n, g->stream));
-  BLP_HIP(hipMemsetAsync(md.p, 0, 4 * (size_t)n, g->stream));
-  BLP_HIP(hipMemsetAsync(fl.p, 0, ((size_t)n + 3) / 4 * 4, g->stream));
+  BLP_HIP(hipMalloc(&g->d_w2, 8 * (size_t)n));
+  BLP_HIP(hipMalloc(&g->d_lo2, 4 * (size_t)n));
+  BLP_HIP(hipMalloc(&g->d_hi2, 4 * (size_t)n));
+  BLP_HIP(hipMalloc(&g->d_maxd, 4 * (size_t)n));
+  BLP_HIP(hipMalloc(&g->d_flag2, ((size_t)n + 3) / 4 * 4));
+  BLP_HIP(hipMemsetAsync(g->d_w2, 0, 8 * (size_t)n, g->stream));
+  BLP_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(g->d_lo2), INT32_MAX, (size_t)n, g->stream));
+  BLP_HIP(hipMemsetAsync(g->d_hi2, 0, 4 * (size_t)n, g->stream));
+  BLP_HIP(hipMemsetAsync(g->d_maxd, 0, 4 * (size_t)n, g->stream));
+  BLP_HIP(hipMemsetAsync(g->d_flag2, 0, ((size_t)n + 3) / 4 * 4, g->stream));
   const int64_t tiles = (nnz + N2_T - 1) / N2_T;
   hipLaunchKernelGGL(k_node2, dim3((unsigned)std::min<int64_t>(tiles, (int64_t)g->n_cu * 16)), dim3(N2_BLOCK), 0,
                      g->stream, (const int64_t*)g->d_rp, (const int32_t*)g->d_ci, (const int32_t*)g->d_hot_idx, n, nnz,
-                     w2.as<unsigned long long>(), lo2.as<int32_t>(), hi2.as<int32_t>(), md.as<int32_t>(),
-                     fl.as<uint8_t>());
+                     g->d_w2, g->d_lo2, g->d_hi2, g->d_maxd, g->d_flag2);
   BLP_HIP(hipGetLastError());
-  BLP_HIP(hipMemcpyAsync(g->h_w2.data(), w2.p, 8 * (size_t)n, hipMemcpyDeviceToHost, g->stream));
-  BLP_HIP(hipMemcpyAsync(g->h_lo2.data(), lo2.p, 4 * (size_t)n, hipMemcpyDeviceToHost, g->stream));
-  BLP_HIP(hipMemcpyAsync(g->h_hi2.data(), hi2.p, 4 * (size_t)n, hipMemcpyDeviceToHost, g->stream));
-  BLP_HIP(hipMemcpyAsync(g->h_maxd.data(), md.p, 4 * (size_t)n, hipMemcpyDeviceToHost, g->stream));
-  BLP_HIP(hipMemcpyAsync(g->h_flag2.data(), fl.p, (size_t)n, hipMemcpyDeviceToHost, g->stream));
+  BLP_HIP(hipMemcpyAsync(g->h_w2.data(), g->d_w2, 8 * (size_t)n, hipMemcpyDeviceToHost, g->stream));
+  BLP_HIP(hipMemcpyAsync(g->h_lo2.data(), g->d_lo2, 4 * (size_t)n, hipMemcpyDeviceToHost, g->stream));
+  BLP_HIP(hipMemcpyAsync(g->h_hi2.data(), g->d_hi2, 4 * (size_t)n, hipMemcpyDeviceToHost, g->stream));
+  BLP_HIP(hipMemcpyAsync(g->h_maxd.data(), g->d_maxd, 4 * (size_t)n, hipMemcpyDeviceToHost, g->stream));
+  BLP_HIP(hipMemcpyAsync(g->h_flag2.data(), g->d_flag2, (size_t)n, hipMemcpyDeviceToHost, g->stream));
   BLP_HIP(hipStreamSynchronize(g->stream));
   return BLP_OK;
+}
+
+void free_node2(blp_graph* g) {
+  void* ps[] = {g->d_w2, g->d_lo2, g->d_hi2, g->d_maxd, g->d_flag2};
+  for (void* p : ps)
+    if (p) (void)hipFree(p);
+  g->d_w2 = nullptr;
+  g->d_lo2 = g->d_hi2 = g->d_maxd = nullptr;
+  g->d_flag2 = nullptr;
 }
 
 }  // namespace blp

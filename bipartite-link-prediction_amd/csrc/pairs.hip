@@ -534,19 +534,21 @@ __global__ __launch_bounds__(GB_BLOCK) void k_item_write_runs(const int64_t* __r
   }
 }
 
-// The short-row scorer's variant of k_item_write_runs (round 5): it writes each grouped pair's
-// caller index and y only (g_out, g_y: 8 B per pair, in whole runs) and leaves N(y)'s row bounds
-// to the scorer (pair_row: rp[y], rp[y + 1] in one 16-byte load, issued with the pair's other
-// metadata before the H2 build). No random row-pointer gathers here, and the stage holds 8-byte
-// records (32 KiB): twice the resident workgroups of the 16-byte version.
-template <int KEYS>
-__global__ __launch_bounds__(GB_BLOCK) void k_item_write_ids(const int4* __restrict__ tmp, const int32_t* __restrict__ item_b,
+// k_item_write_runs with 8-byte stage records (round 5): the item's (caller index, y) pairs are
+// staged in key order (32 KiB of LDS instead of 64: twice the resident workgroups), and the write
+// loop finds each slot's key by a binary search of the key starts. ROWS: N(y)'s bounds gathered
+// from rp and written as g_yb / g_yl (what the scorers read), U slots per thread with their
+// gathers in flight together; otherwise y itself (g_y) and the scorer gathers them (pair_row).
+template <int KEYS, bool ROWS>
+__global__ __launch_bounds__(GB_BLOCK) void k_item_write_ids(const int64_t* __restrict__ rp, const int4* __restrict__ tmp,
+                                                             const int32_t* __restrict__ item_b,
                                                              const int32_t* __restrict__ item_s,
                                                              const int32_t* __restrict__ item_e,
                                                              const int32_t* __restrict__ n_items, int32_t xlo, int lognb,
                                                              const int32_t* __restrict__ ih,
                                                              const int32_t* __restrict__ off, int32_t* __restrict__ fill,
-                                                             int32_t* __restrict__ g_out, int32_t* __restrict__ g_y) {
+                                                             int32_t* __restrict__ g_out, int64_t* __restrict__ g_yb,
+                                                             int32_t* __restrict__ g_yl, int32_t* __restrict__ g_y) {
   static_assert(KEYS <= 1024, "key tables in LDS");
   constexpr int PER = KEYS >= GB_BLOCK ? KEYS / GB_BLOCK : 1;
   __shared__ int h[KEYS];      // local cursors
@@ -593,21 +595,52 @@ __global__ __launch_bounds__(GB_BLOCK) void k_item_write_ids(const int4* __restr
   }
   __syncthreads();
   const int n = e - s;
-  for (int p = (int)threadIdx.x; p < n; p += GB_BLOCK) {  // consecutive local slots -> consecutive positions
-    // the slot's key: the LAST j with lofs[j] <= p (lofs[0] = 0 <= p). Empty keys share their start
-    // with the next key, so the last such j is the non-empty key whose run holds p.
-    int lo = 0, hi = KEYS;
-    while (hi - lo > 1) {
-      const int mid = (lo + hi) >> 1;
-      if (lofs[mid] <= p)
-        lo = mid;
-      else
-        hi = mid;
+  for (int pr = 0; pr < n; pr += U * GB_BLOCK) {  // consecutive local slots -> consecutive positions
+    int pos[U];
+    int2 r[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int p = pr + u * GB_BLOCK + (int)threadIdx.x;
+      pos[u] = -1;
+      if (p < n) {
+        // the slot's key: the LAST j with lofs[j] <= p (lofs[0] = 0 <= p). Empty keys share their
+        // start with the next key, so the last such j is the non-empty key whose run holds p.
+        int lo = 0, hi = KEYS;
+        while (hi - lo > 1) {
+          const int mid = (lo + hi) >> 1;
+          if (lofs[mid] <= p)
+            lo = mid;
+          else
+            hi = mid;
+        }
+        r[u] = stage[p];
+        pos[u] = gbase[lo] + (p - lofs[lo]);
+      }
     }
-    const int2 r = stage[p];
-    const int pos = gbase[lo] + (p - lofs[lo]);
-    g_out[pos] = r.x;
-    g_y[pos] = r.y;
+    if (ROWS) {
+      int64_t st[U], en[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int yy = pos[u] >= 0 ? r[u].y : 0;
+        st[u] = rp[yy];
+        en[u] = rp[yy + 1];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (pos[u] >= 0) {
+          g_out[pos[u]] = r[u].x;
+          g_yb[pos[u]] = st[u];
+          g_yl[pos[u]] = (int32_t)(en[u] - st[u]);
+          if (g_y) g_y[pos[u]] = r[u].y;
+        }
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (pos[u] >= 0) {
+          g_out[pos[u]] = r[u].x;
+          g_y[pos[u]] = r[u].y;
+        }
+    }
   }
 }
 
@@ -641,6 +674,144 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_nz_write(const int32_t* __restri
 #pragma unroll
   for (int k = 0; k < SCAN_ITEMS; ++k)
     if (h[k]) active[o++] = xlo + (int32_t)(base + k);
+}
+
+// ------------------------------------------------------------------ batch planning (device)
+// blp_batch_create's statistics of a pair list, in one pass over its pairs on the device (round 5:
+// the host walked every pair's row and built a first-appearance source list, 8-30 ms at config
+// 2). Per pair: the id bounds, whether x is non-decreasing (source-grouped), |N(y)| (scan work),
+// the id range of N(y) (the bitmap universe) and y (rows read). Per distinct source -- the thread
+// that sets its bit in `seen` -- the graph's two-hop statistics (node2.hip): its H2 build work,
+// the id range of N(N(x)), its longest member row, whether a member row is dense, and N(x)'s own
+// id range (rows read); the source is appended to `srcs` (order not meaningful). Per-thread
+// partials reduce through the wave, then one atomic per block and field.
+struct PlanStats {
+  unsigned long long lo, hi;            // universe: min / max + 1 over N(y) rows and N(N(x))
+  unsigned long long rows_lo, rows_hi;  // rows read: the y, and the ids of N(x)
+  unsigned long long xlo, xhi;          // sources' id range
+  unsigned long long scan, max_scan;    // sum / max of |N(y)|
+  unsigned long long work, max_build;   // sum of the sources' w2 / max member row
+  unsigned long long n_sources;
+  unsigned int bad, not_runs, any_hot;
+};
+
+constexpr int PLAN_BLOCK = 256;
+
+__device__ inline unsigned long long wave_min_u64(unsigned long long v) {
+  for (int o = 32; o > 0; o >>= 1) v = min(v, (unsigned long long)__shfl_xor(v, o, 64));
+  return v;
+}
+__device__ inline unsigned long long wave_max_u64(unsigned long long v) {
+  for (int o = 32; o > 0; o >>= 1) v = max(v, (unsigned long long)__shfl_xor(v, o, 64));
+  return v;
+}
+__device__ inline unsigned long long wave_sum_u64(unsigned long long v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__global__ __launch_bounds__(PLAN_BLOCK) void k_plan_pairs(const int32_t* __restrict__ x, const int32_t* __restrict__ y,
+                                                           int64_t np, int64_t n, const int64_t* __restrict__ rp,
+                                                           const int32_t* __restrict__ ci,
+                                                           const unsigned long long* __restrict__ w2,
+                                                           const int32_t* __restrict__ lo2, const int32_t* __restrict__ hi2,
+                                                           const int32_t* __restrict__ maxd, const uint8_t* __restrict__ flag2,
+                                                           uint32_t* __restrict__ seen, int32_t* __restrict__ srcs,
+                                                           PlanStats* __restrict__ st) {
+  unsigned long long lo = ~0ull, hi = 0, rlo = ~0ull, rhi = 0, xl = ~0ull, xh = 0, scan = 0, mscan = 0, work = 0,
+                     mbuild = 0, nsrc = 0;
+  unsigned bad = 0, nruns = 0, hot = 0;
+  for (int64_t i = (int64_t)blockIdx.x * PLAN_BLOCK + threadIdx.x; i < np; i += (int64_t)gridDim.x * PLAN_BLOCK) {
+    const int32_t xi = x[i], yi = y[i];
+    const int32_t xp = i > 0 ? x[i - 1] : INT32_MIN;
+    if (xi < 0 || xi >= n || yi < 0 || yi >= n) {
+      bad = 1;
+      continue;
+    }
+    nruns |= xp > xi ? 1u : 0u;
+    const int64_t yb = rp[yi], ye = rp[yi + 1];
+    scan += (unsigned long long)(ye - yb);
+    mscan = max(mscan, (unsigned long long)(ye - yb));
+    if (ye > yb) {
+      lo = min(lo, (unsigned long long)ci[yb]);
+      hi = max(hi, (unsigned long long)ci[ye - 1] + 1);
+    }
+    rlo = min(rlo, (unsigned long long)yi);
+    rhi = max(rhi, (unsigned long long)yi + 1);
+    if (xp == xi) continue;  // a run of one source (similarity.users' order): counted at its head
+    const uint32_t bit = 1u << (xi & 31);
+    if (seen[xi >> 5] & bit) continue;  // most repeats of a popular source stop at this read
+    if (atomicOr(&seen[xi >> 5], bit) & bit) continue;
+    srcs[atomicAdd(reinterpret_cast<unsigned long long*>(&st->n_sources), 1ull)] = xi;
+    ++nsrc;
+    xl = min(xl, (unsigned long long)xi);
+    xh = max(xh, (unsigned long long)xi + 1);
+    const int64_t xb = rp[xi], xe = rp[xi + 1];
+    if (xe > xb) {
+      work += w2[xi];
+      mbuild = max(mbuild, (unsigned long long)maxd[xi]);
+      hot |= flag2[xi] & 1u;
+      if (lo2[xi] != INT32_MAX) {
+        lo = min(lo, (unsigned long long)lo2[xi]);
+        hi = max(hi, (unsigned long long)hi2[xi]);
+      }
+      rlo = min(rlo, (unsigned long long)ci[xb]);  // rows are sorted: N(x)'s first and last
+      rhi = max(rhi, (unsigned long long)ci[xe - 1] + 1);
+    }
+  }
+  (void)nsrc;
+  lo = wave_min_u64(lo);
+  rlo = wave_min_u64(rlo);
+  xl = wave_min_u64(xl);
+  hi = wave_max_u64(hi);
+  rhi = wave_max_u64(rhi);
+  xh = wave_max_u64(xh);
+  mscan = wave_max_u64(mscan);
+  mbuild = wave_max_u64(mbuild);
+  scan = wave_sum_u64(scan);
+  work = wave_sum_u64(work);
+  const unsigned long long flags = wave_max_u64((unsigned long long)(bad | nruns << 1 | hot << 2));
+  if ((threadIdx.x & 63) == 0) {
+    atomicMin(&st->lo, lo);
+    atomicMax(&st->hi, hi);
+    atomicMin(&st->rows_lo, rlo);
+    atomicMax(&st->rows_hi, rhi);
+    atomicMin(&st->xlo, xl);
+    atomicMax(&st->xhi, xh);
+    atomicAdd(&st->scan, scan);
+    atomicMax(&st->max_scan, mscan);
+    atomicAdd(&st->work, work);
+    atomicMax(&st->max_build, mbuild);
+    if (flags & 1) atomicOr(&st->bad, 1u);
+    if (flags & 2) atomicOr(&st->not_runs, 1u);
+    if (flags & 4) atomicOr(&st->any_hot, 1u);
+  }
+}
+
+// Planning outputs that need the whole list's statistics first: the sources above the heavy
+// candidate bound (their ids, for the host's heavy-source plan) and, for chunk-parallel batches,
+// the hash-set routing flag of every source (flag indexed by node id: hflag[x - base]).
+__global__ void k_plan_sources(const int32_t* __restrict__ srcs, int64_t ns, const unsigned long long* __restrict__ w2,
+                               const int64_t* __restrict__ rp, unsigned long long heavy_min, int32_t* __restrict__ heavy,
+                               unsigned int* __restrict__ n_heavy, unsigned int heavy_cap, uint8_t* __restrict__ hflag,
+                               int64_t hbase, unsigned long long hash_cap, unsigned int* __restrict__ n_hash) {
+  unsigned nh = 0;
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < ns; s += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t xs = srcs[s];
+    const unsigned long long w = rp[xs + 1] > rp[xs] ? w2[xs] : 0ull;
+    if (heavy && w > heavy_min) {
+      const unsigned k = atomicAdd(n_heavy, 1u);
+      if (k < heavy_cap) heavy[k] = xs;
+    }
+    if (hflag && w <= hash_cap) {
+      hflag[xs - hbase] = 1;
+      ++nh;
+    }
+  }
+  if (hflag) {
+    for (int o = 32; o > 0; o >>= 1) nh += __shfl_xor(nh, o, 64);
+    if ((threadIdx.x & 63) == 0 && nh) atomicAdd(n_hash, nh);
+  }
 }
 
 // ---- grouping of a pair list that arrives already grouped by source (x non-decreasing, as
@@ -2865,7 +3036,10 @@ struct Knobs {
   int split_short = -1;          // BLP_SPLIT_SHORT: register-scanned slice bound (0: off)
   int cosched_cus = -1;          // BLP_COSCHED_CUS: tuning override of the co-scheduled CU share
   bool no_pko = false;           // BLP_NO_PKO: the large scorer's general variant instead of PKO
-  bool group_rows = false;       // BLP_GROUP_ROWS: short-row batches group N(y)'s bounds too (k_item_write_runs)
+  bool host_plan = false;        // BLP_HOST_PLAN: blp_batch_create plans on the host (mirror loops)
+  bool group_rows = true;        // BLP_GROUP_YN=1 clears it: short-row batches then group y only and the
+                                 // scorer gathers N(y)'s bounds (k_item_write_ids<K, false>; measured slower)
+  bool group_rows16 = false;     // BLP_GROUP_ROWS16: the 16-byte-stage grouping write (k_item_write_runs)
   std::string debug_null;        // BLP_DEBUG_NULL (BLP_DEBUG builds only): null this launch pointer, to
                                  // show the pre-launch pointer check (launch_pointers) refusing it
 };
@@ -2898,7 +3072,9 @@ Knobs read_knobs() {
   k.split_short = (int)num("BLP_SPLIT_SHORT", -1);
   k.cosched_cus = (int)num("BLP_COSCHED_CUS", -1);
   k.no_pko = on("BLP_NO_PKO");
-  k.group_rows = on("BLP_GROUP_ROWS");
+  k.group_rows = !on("BLP_GROUP_YN");
+  k.group_rows16 = on("BLP_GROUP_ROWS16");
+  k.host_plan = on("BLP_HOST_PLAN");
 #ifdef BLP_DEBUG
   if (const char* e = getenv("BLP_DEBUG_NULL")) k.debug_null = e;
 #endif
@@ -3091,41 +3267,6 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   BLP_CHECK(g && out && n_pairs >= 0 && (n_pairs == 0 || (x && y)), BLP_E_ARG, "blp_batch_create: bad arguments");
   BLP_CHECK(n_pairs < (int64_t(1) << 31) - 1, BLP_E_ARG, "blp_batch_create: at most 2^31-2 pairs per batch");
   const int64_t n = g->n;
-  const int64_t* rp = g->hrp;
-  const int32_t* ci = g->hci;
-  // ---- plan: node universe touched by H2(x) and N(y); per-source build work. The pair and
-  // source loops gather rows at random (row_ptr / col_idx of the host mirror): several threads
-  // for large batches (the business side of config 2: 0.26 s on one thread).
-  struct Acc {
-    int64_t lo = INT64_MAX, hi = INT64_MIN, scan = 0, max_scan = 0, max_build = 0;
-    int64_t rows_lo = INT64_MAX, rows_hi = INT64_MIN;  // nodes whose rows are read (the y and the z in N(x))
-    bool bad = false, runs = true, any_hot = false;
-    void row(const int64_t* rp, const int32_t* ci, int64_t v) {
-      if (rp[v + 1] > rp[v]) {
-        lo = std::min<int64_t>(lo, ci[rp[v]]);
-        hi = std::max<int64_t>(hi, (int64_t)ci[rp[v + 1] - 1] + 1);
-      }
-      rows_lo = std::min<int64_t>(rows_lo, v);
-      rows_hi = std::max<int64_t>(rows_hi, v + 1);
-    }
-    void merge(const Acc& o) {
-      lo = std::min(lo, o.lo), hi = std::max(hi, o.hi), scan += o.scan, max_scan = std::max(max_scan, o.max_scan);
-      max_build = std::max(max_build, o.max_build), rows_lo = std::min(rows_lo, o.rows_lo);
-      rows_hi = std::max(rows_hi, o.rows_hi), bad |= o.bad, runs &= o.runs, any_hot |= o.any_hot;
-    }
-  };
-  const int32_t* hot = g->h_hot_idx.empty() ? nullptr : g->h_hot_idx.data();
-  auto parallel = [](int64_t count, int64_t min_per_thread, auto body) {  // body(acc, begin, end)
-    const int nt = (int)std::max<int64_t>(1, std::min<int64_t>({16, (int64_t)std::thread::hardware_concurrency(),
-                                                                  count / std::max<int64_t>(min_per_thread, 1)}));
-    std::vector<Acc> acc(nt);
-    std::vector<std::thread> th;
-    for (int t = 1; t < nt; ++t) th.emplace_back(body, std::ref(acc[t]), count * t / nt, count * (t + 1) / nt);
-    body(acc[0], 0, count / nt);
-    for (auto& h : th) h.join();
-    for (int t = 1; t < nt; ++t) acc[0].merge(acc[t]);
-    return acc[0];
-  };
   // BLP_CREATE_PROF=1: the planning stages' wall times on stderr (the e2e score phase)
   const bool cprof = getenv("BLP_CREATE_PROF") != nullptr;
   auto ct0 = std::chrono::steady_clock::now();
@@ -3136,81 +3277,209 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
             std::chrono::duration<double, std::milli>(t - ct0).count());
     ct0 = t;
   };
-  Acc A = parallel(n_pairs, 1 << 18, [&](Acc& a, int64_t i0, int64_t i1) {
-    for (int64_t i = i0; i < i1; ++i) {
-      const int32_t xi = x[i], yi = y[i];
-      if (xi < 0 || xi >= n || yi < 0 || yi >= n) {
-        a.bad = true;
-        return;
-      }
-      a.runs = a.runs && (i == 0 || x[i - 1] <= xi);
-      a.scan += rp[yi + 1] - rp[yi];
-      a.max_scan = std::max<int64_t>(a.max_scan, rp[yi + 1] - rp[yi]);
-      a.row(rp, ci, yi);
-    }
-  });
-  if (A.bad) return fail(BLP_E_ARG, "blp_batch_create: node id out of range");
-  stage("pairs");
-  std::vector<uint8_t> seen((size_t)n, 0);
-  std::vector<int32_t> srcs;  // in order of first appearance
-  for (int64_t i = 0; i < n_pairs; ++i)
-    if (!seen[x[i]]) {
-      seen[x[i]] = 1;
-      srcs.push_back(x[i]);
-    }
-  stage("sources");
-  std::vector<int64_t> work(srcs.size());
-  // per source: the graph's two-hop statistics (node2.hip, computed on the device at graph
-  // creation) instead of a walk over N(x) -- the rows N(z) it reads, their id range, the longest
-  const bool have2 = (int64_t)g->h_w2.size() == n;
-  A.merge(parallel((int64_t)srcs.size(), 1 << 14, [&](Acc& a, int64_t s0, int64_t s1) {
-    for (int64_t s = s0; s < s1; ++s) {
-      const int32_t xi = srcs[s];
-      if (rp[xi + 1] == rp[xi]) {
-        work[s] = 0;
-        continue;
-      }
-      if (have2) {
-        work[s] = (int64_t)g->h_w2[xi];
-        a.max_build = std::max<int64_t>(a.max_build, g->h_maxd[xi]);
-        a.any_hot |= (g->h_flag2[xi] & 1) != 0;
-        if (g->h_lo2[xi] != INT32_MAX) {
-          a.lo = std::min<int64_t>(a.lo, g->h_lo2[xi]);
-          a.hi = std::max<int64_t>(a.hi, g->h_hi2[xi]);
-        }
-        a.rows_lo = std::min<int64_t>(a.rows_lo, ci[rp[xi]]);  // rows are sorted: N(x)'s first and last
-        a.rows_hi = std::max<int64_t>(a.rows_hi, (int64_t)ci[rp[xi + 1] - 1] + 1);
-        continue;
-      }
-      int64_t wsum = 0;
-      for (int64_t k = rp[xi]; k < rp[xi + 1]; ++k) {
-        const int32_t z = ci[k];
-        wsum += rp[z + 1] - rp[z];
-        a.max_build = std::max<int64_t>(a.max_build, rp[z + 1] - rp[z]);
-        a.any_hot |= hot && hot[z] >= 0;
-        a.row(rp, ci, z);
-      }
-      work[s] = wsum;
-    }
-  }));
-  stage("work");
-  int64_t lo = A.lo, hi = A.hi;
-  const int64_t scan_work = A.scan, max_scan_row = A.max_scan, max_build_row = A.max_build;
-  const bool any_hot = A.any_hot;
   const Knobs kn = read_knobs();
-  bool runs = A.runs && !kn.no_runs;  // x non-decreasing: grouped by run heads (BLP_NO_RUNS: bucket sort)
-  const int64_t rows_lo = A.rows_lo, rows_hi = A.rows_hi;
-  if (lo > hi) lo = hi = 0;
-  lo &= ~int64_t(127);  // 128-bit aligned so dense rows map onto whole 16-byte LDS vectors
   blp_batch* b = new blp_batch();
   b->g = g;
   b->n_pairs = n_pairs;
+  b->kn = kn;
+  auto bail = [&](int rc) {
+    blp_batch_destroy(b);
+    return rc;
+  };
+  int rc = set_device(g);
+  if (rc) return bail(rc);
+  {  // the batch's stream: one a destroyed batch returned to the graph, else a new one
+    std::lock_guard<std::mutex> lk(g->stream_mu);
+    if (!g->stream_pool.empty()) {
+      b->stream = g->stream_pool.back();
+      g->stream_pool.pop_back();
+    }
+  }
+  if (!b->stream) BLP_HIP_OR(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking), bail);
+  {  // the graph's own uploads complete before this stream reads them (an event, not a host wait)
+    hipEvent_t ev;
+    BLP_HIP_OR(hipEventCreateWithFlags(&ev, hipEventDisableTiming), bail);
+    hipError_t e = hipEventRecord(ev, g->stream);
+    if (e == hipSuccess) e = hipStreamWaitEvent(b->stream, ev, 0);
+    (void)hipEventDestroy(ev);
+    BLP_HIP_OR(e, bail);
+  }
+  // ---- the pairs go to HBM first: the device planning pass reads them there
+  const size_t np = (size_t)std::max<int64_t>(n_pairs, 1);
+  if (hipMalloc(&b->d_x, 4 * np) != hipSuccess || hipMalloc(&b->d_y, 4 * np) != hipSuccess ||
+      hipMalloc(&b->d_misc, sizeof(Misc)) != hipSuccess)
+    return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: hipMalloc failed"));
+  if (n_pairs) {
+    BLP_HIP_OR(hipMemcpyAsync(b->d_x, x, 4 * n_pairs, hipMemcpyHostToDevice, b->stream), bail);
+    BLP_HIP_OR(hipMemcpyAsync(b->d_y, y, 4 * n_pairs, hipMemcpyHostToDevice, b->stream), bail);
+  }
+  BLP_HIP_OR(hipMemsetAsync(b->d_misc, 0, sizeof(Misc), b->stream), bail);  // dbg[] is zeroed here, not per score
+  stage("upload");
+  // ---- plan: node universe touched by H2(x) and N(y); per-source build work
+  int64_t lo = INT64_MAX, hi = INT64_MIN, scan_work = 0, max_scan_row = 0, max_build_row = 0;
+  int64_t rows_lo = INT64_MAX, rows_hi = INT64_MIN, build_work = 0, n_sources = 0;
+  int32_t xlo = INT32_MAX, xhi = 0;
+  bool bad = false, in_runs = true, any_hot = false;
+  std::vector<std::pair<int32_t, int64_t>> heavy_cand;  // sources whose build work may make them heavy
+  constexpr int64_t HEAVY_MIN = 2 * 16384;              // 2 * the smallest item_work below
+  std::vector<int32_t> srcs;                            // host planning: sources, first appearance
+  std::vector<int64_t> work;                            // ... and their build work
+  ScopedBuf d_seen, d_srcs, d_stats, d_heavy;
+  const bool dev_plan = n_pairs > 0 && g->d_w2 && !kn.host_plan;
+  if (dev_plan) {
+    // one pass over the pairs on the device (k_plan_pairs); the host only reads the totals
+    const int64_t seen_words = (n + 31) / 32;
+    if ((rc = d_seen.reserve(4 * (size_t)seen_words)) || (rc = d_srcs.reserve(4 * (size_t)std::min<int64_t>(n, n_pairs))) ||
+        (rc = d_stats.reserve(sizeof(PlanStats) + 64)))
+      return bail(rc);
+    PlanStats init{};
+    init.lo = init.rows_lo = init.xlo = ~0ull;
+    BLP_HIP_OR(hipMemsetAsync(d_seen.p, 0, 4 * (size_t)seen_words, b->stream), bail);
+    BLP_HIP_OR(hipMemcpyAsync(d_stats.p, &init, sizeof init, hipMemcpyHostToDevice, b->stream), bail);
+    const int64_t grid = std::max<int64_t>(1, std::min<int64_t>((int64_t)g->n_cu * 8, (n_pairs + PLAN_BLOCK - 1) / PLAN_BLOCK));
+    hipLaunchKernelGGL(k_plan_pairs, dim3((unsigned)grid), dim3(PLAN_BLOCK), 0, b->stream, b->d_x, b->d_y, n_pairs, n,
+                       g->d_rp, g->d_ci, g->d_w2, g->d_lo2, g->d_hi2, g->d_maxd, g->d_flag2, d_seen.as<uint32_t>(),
+                       d_srcs.as<int32_t>(), d_stats.as<PlanStats>());
+    BLP_HIP_OR(hipGetLastError(), bail);
+    PlanStats ps;
+    BLP_HIP_OR(hipMemcpyAsync(&ps, d_stats.p, sizeof ps, hipMemcpyDeviceToHost, b->stream), bail);
+    BLP_HIP_OR(hipStreamSynchronize(b->stream), bail);
+    bad = ps.bad != 0;
+    if (bad) return bail(fail(BLP_E_ARG, "blp_batch_create: node id out of range"));
+    in_runs = ps.not_runs == 0;
+    any_hot = ps.any_hot != 0;
+    scan_work = (int64_t)ps.scan;
+    max_scan_row = (int64_t)ps.max_scan;
+    max_build_row = (int64_t)ps.max_build;
+    build_work = (int64_t)ps.work;
+    n_sources = (int64_t)ps.n_sources;
+    if (ps.hi > 0) {
+      lo = (int64_t)ps.lo;
+      hi = (int64_t)ps.hi;
+    }
+    if (ps.rows_hi > 0) {
+      rows_lo = (int64_t)ps.rows_lo;
+      rows_hi = (int64_t)ps.rows_hi;
+    }
+    if (ps.xhi > 0) {
+      xlo = (int32_t)ps.xlo;
+      xhi = (int32_t)ps.xhi;
+    }
+  } else {
+    // host planning (a graph without device two-hop statistics, or BLP_HOST_PLAN): the pair and
+    // source loops gather rows at random from the host mirror, on up to 16 threads
+    const int64_t* rp = g->hrp;
+    const int32_t* ci = g->hci;
+    struct Acc {
+      int64_t lo = INT64_MAX, hi = INT64_MIN, scan = 0, max_scan = 0, max_build = 0;
+      int64_t rows_lo = INT64_MAX, rows_hi = INT64_MIN;  // nodes whose rows are read (the y and the z in N(x))
+      bool bad = false, runs = true, any_hot = false;
+      void row(const int64_t* rp, const int32_t* ci, int64_t v) {
+        if (rp[v + 1] > rp[v]) {
+          lo = std::min<int64_t>(lo, ci[rp[v]]);
+          hi = std::max<int64_t>(hi, (int64_t)ci[rp[v + 1] - 1] + 1);
+        }
+        rows_lo = std::min<int64_t>(rows_lo, v);
+        rows_hi = std::max<int64_t>(rows_hi, v + 1);
+      }
+      void merge(const Acc& o) {
+        lo = std::min(lo, o.lo), hi = std::max(hi, o.hi), scan += o.scan, max_scan = std::max(max_scan, o.max_scan);
+        max_build = std::max(max_build, o.max_build), rows_lo = std::min(rows_lo, o.rows_lo);
+        rows_hi = std::max(rows_hi, o.rows_hi), bad |= o.bad, runs &= o.runs, any_hot |= o.any_hot;
+      }
+    };
+    const int32_t* hot = g->h_hot_idx.empty() ? nullptr : g->h_hot_idx.data();
+    auto parallel = [](int64_t count, int64_t min_per_thread, auto body) {  // body(acc, begin, end)
+      const int nt = (int)std::max<int64_t>(1, std::min<int64_t>({16, (int64_t)std::thread::hardware_concurrency(),
+                                                                    count / std::max<int64_t>(min_per_thread, 1)}));
+      std::vector<Acc> acc(nt);
+      std::vector<std::thread> th;
+      for (int t = 1; t < nt; ++t) th.emplace_back(body, std::ref(acc[t]), count * t / nt, count * (t + 1) / nt);
+      body(acc[0], 0, count / nt);
+      for (auto& h : th) h.join();
+      for (int t = 1; t < nt; ++t) acc[0].merge(acc[t]);
+      return acc[0];
+    };
+    Acc A = parallel(n_pairs, 1 << 18, [&](Acc& a, int64_t i0, int64_t i1) {
+      for (int64_t i = i0; i < i1; ++i) {
+        const int32_t xi = x[i], yi = y[i];
+        if (xi < 0 || xi >= n || yi < 0 || yi >= n) {
+          a.bad = true;
+          return;
+        }
+        a.runs = a.runs && (i == 0 || x[i - 1] <= xi);
+        a.scan += rp[yi + 1] - rp[yi];
+        a.max_scan = std::max<int64_t>(a.max_scan, rp[yi + 1] - rp[yi]);
+        a.row(rp, ci, yi);
+      }
+    });
+    if (A.bad) return bail(fail(BLP_E_ARG, "blp_batch_create: node id out of range"));
+    stage("pairs");
+    std::vector<uint8_t> seen((size_t)n, 0);
+    for (int64_t i = 0; i < n_pairs; ++i)
+      if (!seen[x[i]]) {
+        seen[x[i]] = 1;
+        srcs.push_back(x[i]);
+      }
+    work.resize(srcs.size());
+    const bool have2 = (int64_t)g->h_w2.size() == n;
+    A.merge(parallel((int64_t)srcs.size(), 1 << 14, [&](Acc& a, int64_t s0, int64_t s1) {
+      for (int64_t s = s0; s < s1; ++s) {
+        const int32_t xi = srcs[s];
+        if (rp[xi + 1] == rp[xi]) {
+          work[s] = 0;
+          continue;
+        }
+        if (have2) {
+          work[s] = (int64_t)g->h_w2[xi];
+          a.max_build = std::max<int64_t>(a.max_build, g->h_maxd[xi]);
+          a.any_hot |= (g->h_flag2[xi] & 1) != 0;
+          if (g->h_lo2[xi] != INT32_MAX) {
+            a.lo = std::min<int64_t>(a.lo, g->h_lo2[xi]);
+            a.hi = std::max<int64_t>(a.hi, g->h_hi2[xi]);
+          }
+          a.rows_lo = std::min<int64_t>(a.rows_lo, ci[rp[xi]]);  // rows are sorted: N(x)'s first and last
+          a.rows_hi = std::max<int64_t>(a.rows_hi, (int64_t)ci[rp[xi + 1] - 1] + 1);
+          continue;
+        }
+        int64_t wsum = 0;
+        for (int64_t k = rp[xi]; k < rp[xi + 1]; ++k) {
+          const int32_t z = ci[k];
+          wsum += rp[z + 1] - rp[z];
+          a.max_build = std::max<int64_t>(a.max_build, rp[z + 1] - rp[z]);
+          a.any_hot |= hot && hot[z] >= 0;
+          a.row(rp, ci, z);
+        }
+        work[s] = wsum;
+      }
+    }));
+    lo = A.lo;
+    hi = A.hi;
+    scan_work = A.scan;
+    max_scan_row = A.max_scan;
+    max_build_row = A.max_build;
+    any_hot = A.any_hot;
+    in_runs = A.runs;
+    rows_lo = A.rows_lo;
+    rows_hi = A.rows_hi;
+    n_sources = (int64_t)srcs.size();
+    build_work = std::accumulate(work.begin(), work.end(), (int64_t)0);
+    for (size_t i = 0; i < srcs.size(); ++i) {
+      xlo = std::min(xlo, srcs[i]);
+      xhi = std::max(xhi, srcs[i] + 1);
+      if (work[i] > HEAVY_MIN) heavy_cand.emplace_back(srcs[i], work[i]);
+    }
+  }
+  stage("plan");
+  if (n_sources == 0) xlo = xhi = 0;
+  bool runs = in_runs && !kn.no_runs;  // x non-decreasing: grouped by run heads (BLP_NO_RUNS: bucket sort)
+  if (lo > hi) lo = hi = 0;
+  lo &= ~int64_t(127);  // 128-bit aligned so dense rows map onto whole 16-byte LDS vectors
   b->runs = runs;
   b->lo = lo;
   b->hi = hi;
-  b->n_sources = (int64_t)srcs.size();
+  b->n_sources = n_sources;
   b->use_hot = any_hot;
-  b->kn = kn;
   if (!kn.no_short)  // test knob
     b->short_rows = (max_build_row <= SHORT_MAX ? 1 : 0) | (max_scan_row <= SHORT_MAX ? 2 : 0);
   const int64_t span = hi - lo;
@@ -3257,14 +3526,6 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   // all short (those take row_scan, which counts per pair)
   b->pko = b->variant == V_LARGE && !b->split && !b->global && b->chunks == 1 && span <= 32ll * CAP_PKO &&
            !(b->short_rows & 2) && !kn.no_pko;
-  auto bail = [&](int rc) {
-    blp_batch_destroy(b);
-    return rc;
-  };
-  int rc = set_device(g);
-  if (rc) return bail(rc);
-  BLP_HIP_OR(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking), bail);
-  BLP_HIP_OR(hipStreamSynchronize(g->stream), bail);  // the graph's own uploads are complete
   int per_cu = 1;
   if (b->split) {
     BLP_HIP_OR(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_score_split<S_BLOCK, S_CAP, S_SEG, 8>,
@@ -3277,24 +3538,98 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   // unless there are very many light sources per worker
   // (two once a worker has ~64+ sources: the business side of config 2, 1.44 -> 1.30 ms)
   b->dq = b->n_sources >= n_wg * 64 ? (int)std::max<int64_t>(2, std::min<int64_t>(DQ_MAX, b->n_sources / (n_wg * 64))) : 1;
-  stage("stream");
+  // ---- hash-set scorer (split batches): sources whose build work fits half the hash table
+  // work bounds the distinct ids inserted; at most HT - 1 keeps an empty slot, so every insert
+  // and probe chain ends (the knob is clamped: a fuller table is slower, never unbounded)
+  const bool want_hash = b->split && n_pairs && !kn.no_hash;
+  const int64_t hash_want = kn.hash_work >= 0 ? kn.hash_work : HS_HT / 2;
+#ifdef BLP_DEBUG
+  // debug builds take the knob unclamped, so a test can overfill the table and see the probe
+  // bound (PS_OK site 8) report it instead of a spin
+  const int64_t hash_cap = kn.hash_work >= 0 ? kn.hash_work : std::min<int64_t>(std::max<int64_t>(1, hash_want), HS_HT - 1);
+#else
+  const int64_t hash_cap = std::min<int64_t>(std::max<int64_t>(1, hash_want), HS_HT - 1);
+#endif
+  b->xlo = xlo;
+  b->xspan = (int64_t)xhi - xlo;
+  if (dev_plan) {
+    // the heavy candidates' ids, and (split batches) the hash-set flags, from the device source list
+    const int64_t cap_heavy = std::max<int64_t>(1, std::min<int64_t>(n_sources, build_work / HEAVY_MIN + 1));
+    if ((rc = d_heavy.reserve(4 * (size_t)cap_heavy + 64))) return bail(rc);
+    uint32_t* counts = reinterpret_cast<uint32_t*>(d_heavy.as<int32_t>() + cap_heavy);  // [n_heavy, n_hash]
+    BLP_HIP_OR(hipMemsetAsync(counts, 0, 8, b->stream), bail);
+    if (want_hash) {
+      if (hipMalloc(&b->d_hflag, (size_t)std::max<int64_t>(b->xspan, 1)) != hipSuccess)
+        return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: hash flags"));
+      BLP_HIP_OR(hipMemsetAsync(b->d_hflag, 0, (size_t)std::max<int64_t>(b->xspan, 1), b->stream), bail);
+    }
+    hipLaunchKernelGGL(k_plan_sources, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((int64_t)g->n_cu * 4, (n_sources + 255) / 256))),
+                       dim3(256), 0, b->stream, d_srcs.as<int32_t>(), n_sources, g->d_w2, g->d_rp,
+                       (unsigned long long)HEAVY_MIN, d_heavy.as<int32_t>(), counts, (unsigned)cap_heavy, b->d_hflag,
+                       (int64_t)xlo, (unsigned long long)hash_cap, counts + 1);
+    BLP_HIP_OR(hipGetLastError(), bail);
+    uint32_t hc[2];
+    BLP_HIP_OR(hipMemcpyAsync(hc, counts, 8, hipMemcpyDeviceToHost, b->stream), bail);
+    BLP_HIP_OR(hipStreamSynchronize(b->stream), bail);
+    if ((int64_t)hc[0] > cap_heavy) return bail(fail(BLP_E_STATE, "blp_batch_create: heavy candidate list overflow"));
+    std::vector<int32_t> hv(hc[0]);
+    if (hc[0]) BLP_HIP_OR(hipMemcpy(hv.data(), d_heavy.p, 4 * (size_t)hc[0], hipMemcpyDeviceToHost), bail);
+    std::sort(hv.begin(), hv.end());  // id order: the slots do not depend on the atomics' order
+    for (int32_t v : hv) heavy_cand.emplace_back(v, (int64_t)g->h_w2[v]);
+    b->n_hash = want_hash ? (int64_t)hc[1] : 0;
+    if (want_hash && !b->n_hash) {
+      (void)hipFree(b->d_hflag);
+      b->d_hflag = nullptr;
+    }
+  } else if (want_hash) {
+    std::vector<uint8_t> hf((size_t)std::max<int64_t>(b->xspan, 1), 0);
+    for (size_t i = 0; i < srcs.size(); ++i)
+      if (work[i] <= hash_cap) {
+        hf[srcs[i] - b->xlo] = 1;
+        ++b->n_hash;
+      }
+    if (b->n_hash) {
+      if (hipMalloc(&b->d_hflag, hf.size()) != hipSuccess)
+        return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: hash flags"));
+      BLP_HIP_OR(hipMemcpy(b->d_hflag, hf.data(), hf.size(), hipMemcpyHostToDevice), bail);
+    }
+  }
+  if (b->n_hash && hipMalloc(&b->d_active2, 4 * ((size_t)std::max<int64_t>(b->xspan, 1) + 1)) != hipSuccess)
+    return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: hash flags"));
+  stage("sources");
   // ---- heavy sources: build work far above the per-workgroup share goes to k_heavy
-  const int64_t total_work = std::accumulate(work.begin(), work.end(), (int64_t)0) + scan_work;
+  const int64_t total_work = build_work + scan_work;
   b->work_elems = total_work;
   int64_t item_work = std::max<int64_t>(16384, total_work / std::max<int64_t>(4 * n_wg, 1));
   if (kn.heavy_work >= 0) item_work = std::max<int64_t>(1, kn.heavy_work);  // test knob
+  if (kn.heavy_work >= 0 && 2 * item_work < HEAVY_MIN) {
+    // test knob below the candidate bound: every source is a candidate (host planning's lists)
+    heavy_cand.clear();
+    if (dev_plan) {
+      std::vector<int32_t> all((size_t)n_sources);
+      if (n_sources) BLP_HIP_OR(hipMemcpy(all.data(), d_srcs.p, 4 * (size_t)n_sources, hipMemcpyDeviceToHost), bail);
+      std::sort(all.begin(), all.end());
+      for (int32_t v : all) heavy_cand.emplace_back(v, g->hrp[v + 1] > g->hrp[v] ? (int64_t)g->h_w2[v] : 0);
+    } else {
+      for (size_t i = 0; i < srcs.size(); ++i) heavy_cand.emplace_back(srcs[i], work[i]);
+    }
+  }
   std::vector<int32_t> heavy_slot;
+  std::vector<int32_t> heavy_src;  // sources given a slot
   std::vector<HeavyItem> items;
   // every source's rows are short and the graph holds wedge rows: heavy sources are split into
   // slices of their wedge rows (the short-row scorer's layout)
   const bool wedge_items = (b->short_rows & 1) && g->d_wp && !kn.no_wedge;
   if (b->chunks == 1 && span > 0 && !b->global && (!b->split || span <= variant_cap_bits(V_LARGE))) {
-    for (size_t i = 0; i < srcs.size(); ++i) {
-      if (work[i] <= 2 * item_work) continue;
+    const int64_t* rp = g->hrp;
+    const int32_t* ci = g->hci;
+    for (const auto& hc : heavy_cand) {
+      if (hc.second <= 2 * item_work) continue;
       if (heavy_slot.empty()) heavy_slot.assign((size_t)n, -1);
-      const int32_t xs = srcs[i];
+      const int32_t xs = hc.first;
       const int32_t slot = (int32_t)b->n_heavy++;
       heavy_slot[xs] = slot;
+      heavy_src.push_back(xs);
       if (wedge_items) {  // slices of x's wedge row, item_work ids each
         const int64_t wb = g->h_wp[xs], we = g->h_wp[xs + 1], step = std::max<int64_t>(1, item_work / 4);
         for (int64_t q = wb; q < we; q += step) items.push_back(HeavyItem{slot, 1, q, std::min(we, q + step)});
@@ -3324,8 +3659,7 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
     if (rcw) return bail(rcw);
     if (w && w->slots && w->words == b->hb_words) {
       bool covered = true;  // every planned heavy source has a bitmap (the longest rows do)
-      for (size_t i = 0; i < srcs.size() && covered; ++i)
-        covered = heavy_slot.empty() || heavy_slot[srcs[i]] < 0 || w->h_slot[srcs[i]] >= 0;
+      for (size_t i = 0; i < heavy_src.size() && covered; ++i) covered = w->h_slot[heavy_src[i]] >= 0;
       if (covered) {
         b->wbm_slot = w->d_slot;
         b->wbm_pool = w->d_pool;
@@ -3340,14 +3674,6 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   // ---- grouping geometry: buckets of 2^shift node ids, at most NB_MAX buckets
   {
     // buckets cover the sources' id range [xlo, xhi): ~2K buckets of 2^shift ids each
-    int32_t xlo = INT32_MAX, xhi = 0;
-    for (int32_t v : srcs) {
-      xlo = std::min(xlo, v);
-      xhi = std::max(xhi, v + 1);
-    }
-    if (srcs.empty()) xlo = xhi = 0;
-    b->xlo = xlo;
-    b->xspan = (int64_t)xhi - xlo;
     b->items = !kn.group_buckets;  // test knob: one workgroup per contiguous bucket
     if (b->items) {
       // nb = 2^shift interleaved buckets (<= 2048), each with ceil(xspan / nb) keys
@@ -3378,35 +3704,10 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
         hipMalloc(&b->d_ph2, 4 * (size_t)std::max<int64_t>(b->n_sources, 1) * C) != hipSuccess ||
         hipMalloc(&b->d_lq, sizeof(int4) * SPLIT_LQ * (size_t)g->n_cu * 2) != hipSuccess)
       return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: split buffers"));
-    hipLaunchKernelGGL(k_row_splits, dim3(2048), dim3(256), 0, g->stream, g->d_rp, g->d_ci, rows_lo, nrows, b->lo,
+    // on the batch's stream: ordered before its scoring, no host wait
+    hipLaunchKernelGGL(k_row_splits, dim3(2048), dim3(256), 0, b->stream, g->d_rp, g->d_ci, rows_lo, nrows, b->lo,
                        b->cap_bits, C, b->d_rsplit);
     BLP_HIP_OR(hipGetLastError(), bail);
-    BLP_HIP_OR(hipStreamSynchronize(g->stream), bail);
-  }
-  // ---- hash-set scorer (split batches): sources whose build work fits half the hash table
-  if (b->split && n_pairs && !kn.no_hash) {
-    // work bounds the distinct ids inserted; at most HT - 1 keeps an empty slot, so every insert
-    // and probe chain ends (the knob is clamped: a fuller table is slower, never unbounded)
-    const int64_t want = kn.hash_work >= 0 ? kn.hash_work : HS_HT / 2;
-#ifdef BLP_DEBUG
-    // debug builds take the knob unclamped, so a test can overfill the table and see the probe
-    // bound (PS_OK site 8) report it instead of a spin
-    const int64_t cap = kn.hash_work >= 0 ? kn.hash_work : std::min<int64_t>(std::max<int64_t>(1, want), HS_HT - 1);
-#else
-    const int64_t cap = std::min<int64_t>(std::max<int64_t>(1, want), HS_HT - 1);
-#endif
-    std::vector<uint8_t> hf((size_t)std::max<int64_t>(b->xspan, 1), 0);
-    for (size_t i = 0; i < srcs.size(); ++i)
-      if (work[i] <= cap) {
-        hf[srcs[i] - b->xlo] = 1;
-        ++b->n_hash;
-      }
-    if (b->n_hash) {
-      if (hipMalloc(&b->d_hflag, hf.size()) != hipSuccess ||
-          hipMalloc(&b->d_active2, 4 * (hf.size() + 1)) != hipSuccess)
-        return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: hash flags"));
-      BLP_HIP_OR(hipMemcpy(b->d_hflag, hf.data(), hf.size(), hipMemcpyHostToDevice), bail);
-    }
   }
   // ---- HBM bitmap slots: one per resident workgroup of k_score_global
   if (b->global && n_pairs) {
@@ -3420,12 +3721,9 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   }
   stage("split");
   // ---- device buffers
-  const size_t np = (size_t)std::max<int64_t>(n_pairs, 1);
-  if (hipMalloc(&b->d_x, 4 * np) != hipSuccess || hipMalloc(&b->d_y, 4 * np) != hipSuccess ||
-      hipMalloc(&b->d_cn, 4 * np) != hipSuccess || hipMalloc(&b->d_jac, 8 * np) != hipSuccess ||
+  if (hipMalloc(&b->d_cn, 4 * np) != hipSuccess || hipMalloc(&b->d_jac, 8 * np) != hipSuccess ||
       hipMalloc(&b->d_aa, 8 * np) != hipSuccess || hipMalloc(&b->d_gout, 4 * np) != hipSuccess ||
-      hipMalloc(&b->d_gyb, 8 * np) != hipSuccess || hipMalloc(&b->d_gyl, 4 * np) != hipSuccess ||
-      hipMalloc(&b->d_misc, sizeof(Misc)) != hipSuccess)
+      hipMalloc(&b->d_gyb, 8 * np) != hipSuccess || hipMalloc(&b->d_gyl, 4 * np) != hipSuccess)
     return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: hipMalloc failed"));
   if (b->chunks > 1 && hipMalloc(&b->d_aa_part, 16 * np) != hipSuccess)
     return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: hipMalloc failed"));
@@ -3438,13 +3736,6 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   if (want_rec &&
       hipMalloc(&b->d_rec, sizeof(SrcRec) * (size_t)std::max<int64_t>(b->n_sources, 1)) != hipSuccess)
     return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: hipMalloc failed"));
-  if (hipMemset(b->d_misc, 0, sizeof(Misc)) != hipSuccess)  // dbg[] is zeroed here, not per score
-    return bail(fail(BLP_E_HIP_BASE, "blp_batch_create: hipMemset failed"));
-  if (n_pairs) {
-    if (hipMemcpy(b->d_x, x, 4 * n_pairs, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(b->d_y, y, 4 * n_pairs, hipMemcpyHostToDevice) != hipSuccess)
-      return bail(fail(BLP_E_HIP_BASE, "blp_batch_create: upload failed"));
-  }
   if (b->n_heavy) {
     if (hipMalloc(&b->d_heavy_slot, 4 * n) != hipSuccess ||
         hipMalloc(&b->d_heavy_bm, 4 * b->hb_words * b->n_heavy) != hipSuccess ||
@@ -3471,7 +3762,17 @@ int blp_batch_destroy(blp_batch* b) {
   b->off.release();
   b->active.release();
   b->scratch.release();
-  if (b->stream) (void)hipStreamDestroy(b->stream);
+  if (b->stream) {  // back to the graph's pool for the next batch (a few at most)
+    bool kept = false;
+    if (b->g) {
+      std::lock_guard<std::mutex> lk(b->g->stream_mu);
+      if (b->g->stream_pool.size() < 8) {
+        b->g->stream_pool.push_back(b->stream);
+        kept = true;
+      }
+    }
+    if (!kept) (void)hipStreamDestroy(b->stream);
+  }
   void* ps[] = {b->d_x,    b->d_y,    b->d_cn,   b->d_jac,  b->d_aa,          b->d_gout,        b->d_gyb,
                 b->d_gyl,  b->d_misc, b->d_heavy_slot, b->d_heavy_bm, b->d_heavy_items, b->d_gbm, b->d_gy, b->d_rsplit, b->d_pcn, b->d_paa, b->d_ph2, b->d_aa_part, b->d_rec, b->d_hflag, b->d_lq, b->d_active2};
   for (void* p : ps)
@@ -3609,9 +3910,13 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   hipLaunchKernelGGL(k_nz_write, dim3((unsigned)tx), dim3(SCAN_BLOCK), 0, b->stream, cnt + b->xlo, b->xspan, tx2,  \
                      b->xlo, b->active.as<int32_t>());                                                              \
   if (runs_w && ids_w)                                                                                                \
-    hipLaunchKernelGGL(k_item_write_ids<(K <= 1024 ? K : 1024)>, dim3((unsigned)ub), dim3(GB_BLOCK), 0, b->stream,   \
-                       tmp, it_b, it_s, it_e, &b->d_misc->n_items, b->xlo, b->shift, ih, off, fill, b->d_gout,        \
-                       b->d_gy);                                                                                      \
+    hipLaunchKernelGGL((k_item_write_ids<(K <= 1024 ? K : 1024), false>), dim3((unsigned)ub), dim3(GB_BLOCK), 0,     \
+                       b->stream, g->d_rp, tmp, it_b, it_s, it_e, &b->d_misc->n_items, b->xlo, b->shift, ih, off,     \
+                       fill, b->d_gout, b->d_gyb, b->d_gyl, b->d_gy);                                                 \
+  else if (runs_w && !b->kn.group_rows16)                                                                             \
+    hipLaunchKernelGGL((k_item_write_ids<(K <= 1024 ? K : 1024), true>), dim3((unsigned)ub), dim3(GB_BLOCK), 0,      \
+                       b->stream, g->d_rp, tmp, it_b, it_s, it_e, &b->d_misc->n_items, b->xlo, b->shift, ih, off,     \
+                       fill, b->d_gout, b->d_gyb, b->d_gyl, b->d_gy);                                                 \
   else if (runs_w)                                                                                                    \
     hipLaunchKernelGGL(k_item_write_runs<(K <= 1024 ? K : 1024)>, dim3((unsigned)ub), dim3(GB_BLOCK), 0, b->stream,  \
                        g->d_rp, tmp, it_b, it_s, it_e, &b->d_misc->n_items, b->xlo, b->shift, ih, off, fill,         \

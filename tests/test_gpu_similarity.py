@@ -150,6 +150,10 @@ def test_general_graph_exact_distance(gpu):
     {"BLP_SPLIT": "3", "BLP_SPLIT_BIG": "1", "BLP_HASH_WORK": "600"},  # hash-set scorer for light sources, split for the rest
     {"BLP_SPLIT": "2", "BLP_SPLIT_BIG": "1", "BLP_HASH_WORK": "100000"},  # every source on the hash-set scorer (knob clamped to HT - 1)
     {"BLP_SPLIT": "4", "BLP_HASH_WORK": "400"},          # ... beside the 64 KiB chunk scorer
+    {"BLP_GROUP_YN": "1"},                              # short-row batches grouped by y only: the scorer reads N(y)'s bounds
+    {"BLP_GROUP_ROWS16": "1"},                          # the 16-byte-stage grouping write (k_item_write_runs)
+    {"BLP_HOST_PLAN": "1"},                             # blp_batch_create's planning on the host mirror
+    {"BLP_HOST_PLAN": "1", "BLP_SPLIT": "3", "BLP_SPLIT_BIG": "1", "BLP_HASH_WORK": "600"},
 ])
 def test_kernel_paths_vs_oracle(gpu, knobs, monkeypatch):
     for k, v in knobs.items():
@@ -475,3 +479,42 @@ def test_node2_planning_with_empty_row_runs(gpu):
                 np.testing.assert_array_equal(np.unique(got_w), np.unique(want))
                 assert len(got_w) == (len(want) + 3) // 4 * 4
     G.close()
+
+
+@pytest.mark.parametrize("knobs", [
+    {},
+    {"BLP_HEAVY_WORK": "50"},
+    {"BLP_HEAVY_WORK": "50", "BLP_NO_WEDGE": "1"},
+    {"BLP_HEAVY_WORK": "50000", "BLP_NO_WBM_BATCH": "1"},
+    {"BLP_SPLIT": "3", "BLP_SPLIT_BIG": "1", "BLP_HASH_WORK": "600"},
+    {"BLP_FORCE_GLOBAL": "1"},
+])
+def test_device_plan_equals_host_plan(gpu, knobs, monkeypatch):
+    """blp_batch_create's planning pass on the device (k_plan_pairs / k_plan_sources: bounds, the
+    universe, runs, the sources, build work, heavy and hash-set routing) gives the host loops'
+    plan (BLP_HOST_PLAN=1) on both sides, for source-grouped and shuffled pair lists, and the
+    same scores (similarity.py:20-106)."""
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    rng = np.random.default_rng(21)
+    a, b = bipartite_edges(rng, 30000, 1500, 300000)
+    G = blp.DeviceGraph(a, b)
+    nu = G.n - len(np.unique(b))
+    x = np.repeat(np.sort(rng.choice(nu, 120, replace=False)), 40).astype(np.int32)
+    y = rng.integers(nu, G.n, len(x)).astype(np.int32)
+    perm = rng.permutation(len(x))
+    for xs, ys in ((x, y), (y, x), (x[perm], y[perm])):
+        dev = G.batch(xs, ys)
+        monkeypatch.setenv("BLP_HOST_PLAN", "1")
+        host = G.batch(xs, ys)
+        monkeypatch.delenv("BLP_HOST_PLAN")
+        assert dev.plan() == host.plan(), (dev.plan(), host.plan())
+        assert dev.kernel(7) == host.kernel(7)
+        dev.score(7)
+        host.score(7)
+        rd, rh = dev.fetch(7), host.fetch(7)
+        for k in ("cn", "jaccard", "adamic"):
+            np.testing.assert_array_equal(rd[k], rh[k])
+        dev.close()
+        host.close()
+    _check_against_oracle(a, b, y[perm], x[perm])
