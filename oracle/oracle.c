@@ -69,60 +69,65 @@ static void og_rows_pass(int64_t m, const int32_t* a, const int32_t* b, int32_t 
 static int32_t* og_raw_partitioned(int64_t n, int64_t m, const int32_t* a, const int32_t* b, int nt,
                                    int64_t* pos) {
     const int64_t R = 64 * (int64_t)nt, rb = (n + R - 1) / R;
-    int64_t* cnt = (int64_t*)calloc((size_t)(R * nt + 1), sizeof(int64_t)); /* [range][thread] */
+    /* per-thread cursors, thread-major ([thread][range]): no two threads share a cache line */
+    int64_t* cnt = (int64_t*)calloc((size_t)(R * nt), sizeof(int64_t));
+    int64_t* rstart = (int64_t*)calloc((size_t)(R + 1), sizeof(int64_t));
 #ifdef _OPENMP
 #pragma omp parallel for num_threads(nt) schedule(static, 1)
 #endif
     for (int t = 0; t < nt; ++t) {
+        int64_t* c = cnt + (int64_t)t * R;
         const int64_t e0 = m * t / nt, e1 = m * (t + 1) / nt;
         for (int64_t i = e0; i < e1; ++i) {
-            cnt[(a[i] / rb) * nt + t]++;
-            if (a[i] != b[i]) cnt[(b[i] / rb) * nt + t]++;
+            c[a[i] / rb]++;
+            if (a[i] != b[i]) c[b[i] / rb]++;
         }
     }
     int64_t tot = 0;
-    for (int64_t j = 0; j < R * nt; ++j) {
-        const int64_t c = cnt[j];
-        cnt[j] = tot;
-        tot += c;
+    for (int64_t r = 0; r < R; ++r) {
+        rstart[r] = tot;
+        for (int t = 0; t < nt; ++t) {
+            const int64_t c = cnt[(int64_t)t * R + r];
+            cnt[(int64_t)t * R + r] = tot;
+            tot += c;
+        }
     }
-    cnt[R * nt] = tot;
+    rstart[R] = tot;
     uint64_t* buf = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)(tot + 1));
 #ifdef _OPENMP
 #pragma omp parallel for num_threads(nt) schedule(static, 1)
 #endif
     for (int t = 0; t < nt; ++t) {
+        int64_t* c = cnt + (int64_t)t * R;
         const int64_t e0 = m * t / nt, e1 = m * (t + 1) / nt;
         for (int64_t i = e0; i < e1; ++i) {
             const uint32_t x = (uint32_t)a[i], y = (uint32_t)b[i];
-            buf[cnt[(x / rb) * nt + t]++] = (uint64_t)x << 32 | y;
-            if (x != y) buf[cnt[(y / rb) * nt + t]++] = (uint64_t)y << 32 | x;
+            buf[c[x / rb]++] = (uint64_t)x << 32 | y;
+            if (x != y) buf[c[y / rb]++] = (uint64_t)y << 32 | x;
         }
     }
-    /* after the scatter cnt[r * nt + nt - 1] is the end of range r; its start is the previous end */
     int32_t* raw = (int32_t*)malloc(sizeof(int32_t) * (size_t)(tot + 1));
 #ifdef _OPENMP
 #pragma omp parallel for num_threads(nt) schedule(dynamic, 1)
 #endif
-    for (int64_t r = 0; r < R; ++r) { /* row counts of the range */
-        const int64_t s = r ? cnt[(r - 1) * nt + nt - 1] : 0, e = cnt[r * nt + nt - 1];
-        for (int64_t i = s; i < e; ++i) pos[(buf[i] >> 32) + 1]++;
+    for (int64_t r = 0; r < R; ++r) { /* row counts of the range (its rows are its own) */
+        for (int64_t i = rstart[r]; i < rstart[r + 1]; ++i) pos[(buf[i] >> 32) + 1]++;
     }
     for (int64_t i = 0; i < n; ++i) pos[i + 1] += pos[i];
 #ifdef _OPENMP
 #pragma omp parallel for num_threads(nt) schedule(dynamic, 1)
 #endif
     for (int64_t r = 0; r < R; ++r) { /* rows of the range: a cursor per row, from pos */
-        const int64_t s = r ? cnt[(r - 1) * nt + nt - 1] : 0, e = cnt[r * nt + nt - 1];
         const int64_t v0 = r * rb, v1 = v0 + rb < n ? v0 + rb : n;
         if (v0 >= v1) continue;
         int64_t* cur = (int64_t*)malloc(sizeof(int64_t) * (size_t)(v1 - v0));
         for (int64_t v = v0; v < v1; ++v) cur[v - v0] = pos[v];
-        for (int64_t i = s; i < e; ++i) raw[cur[(int64_t)(buf[i] >> 32) - v0]++] = (int32_t)(uint32_t)buf[i];
+        for (int64_t i = rstart[r]; i < rstart[r + 1]; ++i) raw[cur[(int64_t)(buf[i] >> 32) - v0]++] = (int32_t)(uint32_t)buf[i];
         free(cur);
     }
     free(buf);
     free(cnt);
+    free(rstart);
     return raw;
 }
 
