@@ -2289,6 +2289,178 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
   PROF_FLUSH
 }
 
+// ------------------------------------------------------------------ short-row scorer, 3 barriers
+// The short-row scorer (the business side of a review graph: 100K light sources, ~75 pairs each,
+// rows of <= SHORT_MAX ids) restated around its dependent chain (round 5). k_score<..., SHORT>
+// passes every pair's row bounds through LDS segments (an offset scan, a segment table, a
+// per-segment count array) and popcounts the bitmap: ~9 block barriers per source, each one a
+// point where the 4 waves of a workgroup wait for the slowest's round trip. Here:
+//   P1  copy the source's pre-built set (wedge-row bitmap / k_heavy slot), counting its bits on
+//       the way, or zero the bitmap                                              -- barrier
+//   P2  OR in the wedge row, counting the bits an atomicOr newly sets (its return value), so
+//       |N(N(x)) ∩ universe| is known without a popcount pass                     -- barrier
+//   (general graphs only, N(x) inside the universe: drop distance 1, counting the cleared bits -- barrier)
+//   P3  every thread scores its own pairs t, t + 256, ... straight from registers (the first one's
+//       metadata was loaded before P1): N(y) tested against the bitmap, x itself skipped (distance
+//       0; |H2| = count - x's bit), outputs written                               -- barrier
+// Three barriers per source instead of ~9, the same bitmap and the same exact arithmetic.
+template <bool SAA>
+__global__ __launch_bounds__(256, BLP_SHORT_MINB) void k_score_short(ScoreArgs a) {
+  constexpr int BLOCK = 256;
+  constexpr int NW = BLOCK / 64;
+  uint32_t* bm = reinterpret_cast<uint32_t*>(blp_dyn_lds);
+  uint4* bm4 = reinterpret_cast<uint4*>(bm);
+  __shared__ long long s_wtab[SAA ? 256 : 1];
+  __shared__ int s_src[2];
+  __shared__ unsigned s_h2[2];
+  (void)NW;
+  if (SAA && a.wtab)
+    for (int i = threadIdx.x; i < 256; i += BLOCK) s_wtab[i] = a.wtab[i];
+  if (threadIdx.x == 0) s_h2[0] = s_h2[1] = 0;
+  const int64_t c0 = a.lo, width = max<int64_t>(a.hi - a.lo, 0);
+  const int nw4 = (int)((((width + 31) >> 5) + 3) >> 2);
+  const uint32_t c0u = (uint32_t)c0, wu = (uint32_t)width, keep = a.idmask | 0x80000000u;
+  const bool want_j = (a.mask & BLP_JACCARD) != 0;
+  const bool want_a = SAA && (a.mask & BLP_ADAMIC) != 0;
+  const int n_active = a.misc->n_active;
+  const int lane = threadIdx.x & 63;
+  // wave-sum an unsigned count into an LDS counter: one atomic per wave
+  auto add_count = [&](unsigned c, unsigned* dst) {
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    if (lane == 0 && c) atomicAdd(dst, c);
+  };
+  int nxt = threadIdx.x == 0 ? atomicAdd(&a.misc->queue, a.dq) : 0;  // dequeue one ahead
+  int k = 0;  // sources scored by this workgroup: s_h2 slot k & 1
+  for (int it = 0;; ++it) {
+    if (threadIdx.x == 0) {
+      s_src[it & 1] = nxt;
+      if (nxt < n_active) nxt = atomicAdd(&a.misc->queue, a.dq);
+    }
+    __syncthreads();
+    const int s_first = s_src[it & 1];
+    if (s_first >= n_active) break;
+    const int s_last = min(n_active, s_first + a.dq);
+    for (int s = s_first; s < s_last; ++s, ++k) {
+      const SrcRec& r = a.rec[__builtin_amdgcn_readfirstlane(s)];
+      auto u32 = [](int32_t v) { return (int32_t)__builtin_amdgcn_readfirstlane(v); };
+      auto u64 = [](int64_t v) {
+        return (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(v >> 32)) << 32) |
+                         (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)v));
+      };
+      const int x = u32(r.x), pbeg = u32(r.pbeg), pcnt = u32(r.pcnt), hslot = u32(r.hslot);
+      const int64_t xb = u64(r.xb), xe = u64(r.xe), wb = u64(r.wb), we = u64(r.we);
+      const int64_t nx_lo = u32(r.nx_lo), nx_hi = u32(r.nx_hi);
+      const int slot = k & 1;
+      // the first pair's metadata, in flight during P1 / P2
+      int64_t pf_start = 0;
+      int pf_len = 0, pf_out = 0;
+      const bool pairs_ok = PS_OK(a.misc, pbeg >= 0 && (int64_t)pbeg + pcnt <= a.np, 3, (int64_t)pbeg + pcnt, a.np);
+      if (pairs_ok && (int)threadIdx.x < pcnt) {
+        pair_row<true>(a, pbeg + threadIdx.x, pf_start, pf_len);
+        pf_out = a.g_out[pbeg + threadIdx.x];
+      }
+      // P1: the pre-built set, counted while copied, or a zeroed bitmap
+      unsigned cnt = 0;
+      if (hslot >= 0) {
+        const uint4* src4 = reinterpret_cast<const uint4*>(a.heavy_bm + (int64_t)hslot * a.hb_words);
+        for (int i = threadIdx.x; i < nw4; i += BLOCK) {
+          const uint4 q = src4[i];
+          bm4[i] = q;
+          cnt += __popc(q.x) + __popc(q.y) + __popc(q.z) + __popc(q.w);
+        }
+      } else {
+        for (int i = threadIdx.x; i < nw4; i += BLOCK) bm4[i] = make_uint4(0, 0, 0, 0);
+      }
+      if (threadIdx.x == 0) s_h2[slot ^ 1] = 0;  // the next source's counter (its last reader is past a barrier)
+      add_count(cnt, &s_h2[slot]);
+      __syncthreads();
+      // P2: N(N(x)) from x's wedge row, counting newly set bits
+      if (hslot < 0) {
+        cnt = 0;
+        if (PS_OK(a.misc, wb >= 0 && we <= a.wedge_vecs, 11, we, a.wedge_vecs)) {
+          for (int64_t q = wb + threadIdx.x; q < we; q += 2 * BLOCK) {
+            const uint4 v0 = a.wedge[q];
+            const uint4 v1 = q + BLOCK < we ? a.wedge[q + BLOCK] : v0;  // (a repeat sets nothing new)
+            const uint32_t ids[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const uint32_t rr = in_chunk((int)ids[j], keep, c0u);
+              if (rr < wu) {
+                const uint32_t bit = 1u << (rr & 31);
+                cnt += (atomicOr(&bm[rr >> 5], bit) & bit) ? 0u : 1u;
+              }
+            }
+          }
+        }
+        add_count(cnt, &s_h2[slot]);
+        __syncthreads();
+      }
+      // distance 1 (general graphs: N(x) meets the universe): drop it, counting the cleared bits
+      if (nx_hi >= c0 && nx_lo < c0 + width) {
+        cnt = 0;
+        for (int64_t q = xb + threadIdx.x; q < xe; q += BLOCK) {
+          const int64_t rr = (int64_t)a.ci[q] - c0;
+          if (rr >= 0 && rr < width) {
+            const uint32_t bit = 1u << (rr & 31);
+            cnt += (atomicAnd(&bm[rr >> 5], ~bit) & bit) ? 1u : 0u;
+          }
+        }
+        for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+        if (lane == 0 && cnt) atomicSub(&s_h2[slot], cnt);
+        __syncthreads();
+      }
+      // P3: |H2(x)| = the count minus x itself (distance 0); each thread scores its own pairs
+      const int64_t xr = (int64_t)x - c0;
+      const unsigned xbit = (xr >= 0 && xr < width) ? (bm[xr >> 5] >> (xr & 31)) & 1u : 0u;
+      const long long h2 = (long long)s_h2[slot] - xbit;
+      for (int p = threadIdx.x; pairs_ok && p < pcnt; p += BLOCK) {
+        int64_t st = pf_start;
+        int len = pf_len, pout = pf_out;
+        if (p != (int)threadIdx.x) {
+          pair_row<true>(a, pbeg + p, st, len);
+          pout = a.g_out[pbeg + p];
+        }
+        if (!PS_OK(a.misc, pout >= 0 && pout < a.np, 4, pout, a.np)) continue;
+        if (!PS_OK(a.misc, st >= 0 && st + len <= a.nnz + CI_PAD, 10, st + len, a.nnz)) continue;
+        unsigned c = 0;
+        unsigned long long acc = 0;
+        uint32_t acch = 0;  // <= SHORT_MAX terms of W >> 32 < 2^27
+        for (int h = 0; h < len; h += SHORT_PART) {
+          int e[SHORT_PART];
+          row_part(a.cw, st, len, h, e);
+#pragma unroll
+          for (int j = 0; j < SHORT_PART; ++j) {
+            if (h + j < len) {
+              const uint32_t rr = in_chunk(e[j], keep, c0u);
+              const uint32_t word = bm[(rr < wu ? rr : 0u) >> 5];
+              const bool hit = rr < wu && ((word >> (rr & 31)) & 1u) && (int)((uint32_t)e[j] & a.idmask) != x;
+              c += hit ? 1u : 0u;
+              if (SAA && want_a && hit) {
+                const uint32_t code = ((uint32_t)e[j] >> a.idbits) & 255u;
+                const unsigned long long w = (unsigned long long)(code ? s_wtab[code] : a.aaw[e[j] & a.idmask]);
+                acc += w;
+                acch += (uint32_t)(w >> 32);
+              }
+            }
+          }
+        }
+        a.cn[pout] = c;
+        if (SAA && want_a) a.aa[pout] = blp::aa_value(acc, acch);
+        if (want_j) {
+          const long long uni = h2 + len - (long long)c;
+          if (uni <= 0) {
+            a.jac[pout] = __builtin_nan("");
+            atomicOr(&a.misc->zero_div, 1);
+          } else {
+            a.jac[pout] = (double)c / (double)uni;  // correctly rounded, as Python's float division
+          }
+        }
+      }
+      __syncthreads();  // the bitmap and this source's counter are free for the next source
+    }
+  }
+}
+
 // ------------------------------------------------------------------ HBM-bitmap scorer
 // Universes wider than one workgroup's LDS (config 5: H2(u) over 50M users = 6.25 MB) would
 // need one full H2 rebuild per LDS chunk. Here every workgroup owns a private bitmap slot in
@@ -3036,6 +3208,7 @@ struct Knobs {
   int split_short = -1;          // BLP_SPLIT_SHORT: register-scanned slice bound (0: off)
   int cosched_cus = -1;          // BLP_COSCHED_CUS: tuning override of the co-scheduled CU share
   bool no_pko = false;           // BLP_NO_PKO: the large scorer's general variant instead of PKO
+  bool short_seg = false;        // BLP_SHORT_SEG: short-row batches on the segment scorer (k_score SHORT)
   bool host_plan = false;        // BLP_HOST_PLAN: blp_batch_create plans on the host (mirror loops)
   bool group_rows = true;        // BLP_GROUP_YN=1 clears it: short-row batches then group y only and the
                                  // scorer gathers N(y)'s bounds (k_item_write_ids<K, false>; measured slower)
@@ -3075,6 +3248,7 @@ Knobs read_knobs() {
   k.group_rows = !on("BLP_GROUP_YN");
   k.group_rows16 = on("BLP_GROUP_ROWS16");
   k.host_plan = on("BLP_HOST_PLAN");
+  k.short_seg = on("BLP_SHORT_SEG");
 #ifdef BLP_DEBUG
   if (const char* e = getenv("BLP_DEBUG_NULL")) k.debug_null = e;
 #endif
@@ -3180,13 +3354,15 @@ static int launch_score(blp_graph* g, hipStream_t st, const ScoreArgs& a, int pe
 // limit (one device-scope atomic word saturates near 90 dequeues per microsecond).
 template <bool SAA>
 static int launch_short(blp_graph* g, const blp_batch* b, ScoreArgs a, size_t dyn) {
-  auto kern = k_score<BLOCK_SMALL, CAP_SMALL, SEG_SMALL, 8, true, SAA>;
+  // the three-barrier scorer takes batches with wedge rows (every review-graph business pass);
+  // the segment scorer builds from the CSR otherwise (BLP_SHORT_SEG: it takes every batch)
+  const bool three = a.wp && !b->kn.short_seg;
+  auto kern = three ? k_score_short<SAA> : k_score<BLOCK_SMALL, CAP_SMALL, SEG_SMALL, 8, true, SAA>;
   int per_cu = 1;
   BLP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, BLOCK_SMALL, dyn));
   const int64_t n_wg = (int64_t)g->n_cu * std::max(per_cu, 1);
   if (b->n_sources >= n_wg * 16) a.dq = std::max(a.dq, 2);
-  hipLaunchKernelGGL((k_score<BLOCK_SMALL, CAP_SMALL, SEG_SMALL, 8, true, SAA>), dim3((unsigned)n_wg),
-                     dim3(BLOCK_SMALL), dyn, b->stream, a);
+  hipLaunchKernelGGL(kern, dim3((unsigned)n_wg), dim3(BLOCK_SMALL), dyn, b->stream, a);
   BLP_HIP(hipGetLastError());
   return BLP_OK;
 }
@@ -3799,6 +3975,8 @@ int blp_batch_kernel(const blp_batch* b, uint32_t mask, char* name, int cap) {
     snprintf(buf, sizeof buf, "k_score_global<%d, %d, 8>", G_BLOCK, G_SEG);
   else if (b->split)
     snprintf(buf, sizeof buf, "k_score_split<%d, %d, %d, 8>", S_BLOCK, b->split_big ? S_CAP_BIG : S_CAP, S_SEG);
+  else if (b->use_short && b->g->d_wp && !b->kn.no_wedge && !b->kn.short_seg)
+    snprintf(buf, sizeof buf, "k_score_short<%s>", aa ? "true" : "false");
   else if (b->use_short)
     snprintf(buf, sizeof buf, "k_score<%d, %d, %d, 8, true, %s>", BLOCK_SMALL, CAP_SMALL, SEG_SMALL, aa ? "true" : "false");
   else if (b->variant == V_SMALL)
