@@ -45,6 +45,10 @@
 #ifndef BLP_PFN
 #define BLP_PFN 1  // ... and every later segment's metadata during the previous segment's scan
 #endif
+#ifndef BLP_EXP_PHASE
+#define BLP_EXP_PHASE 0  // experiment builds only (LDS bank-conflict attribution of the large scorer):
+                         // 1 = no pair scan, 2 = no H2 build (dense OR and sparse rows; the scan finds no hits)
+#endif
 #ifndef BLP_PP
 #define BLP_PP 1  // ping-pong merge-path loops in k_score (0: the single-buffer mp_build / mp_scan)
 #endif
@@ -2070,7 +2074,7 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
             uint4 acc[QPT];
 #pragma unroll
             for (int j = 0; j < QPT; ++j) acc[j] = make_uint4(0, 0, 0, 0);
-            for (int r = 0; r < nhot; ++r) {
+            for (int r = 0; r < (BLP_EXP_PHASE == 2 ? 0 : nhot); ++r) {
               const blp::HotRow h = s_hot[r];
               const uint4* row = a.hot_pool + h.vec_off;
 #pragma unroll
@@ -2135,8 +2139,9 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
               if (RC) {
                 rc_chunk_offsets<BLOCK, K>(s_off, ns, s_coff, red);
                 const int shift = build_hint<BLOCK, HC>(s_coff, ns, BLOCK, s_hint);
-                rc_build<BLOCK, K>(a.cw, a.idmask, s_start, s_off, s_coff, ns, c0, width, bm, CAP_WORDS, threadIdx.x,
-                                   s_hint, shift);
+                if (BLP_EXP_PHASE != 2)
+                  rc_build<BLOCK, K>(a.cw, a.idmask, s_start, s_off, s_coff, ns, c0, width, bm, CAP_WORDS, threadIdx.x,
+                                     s_hint, shift);
               } else {
                 const int shift = build_hint<BLOCK, HC>(s_off, ns, BLOCK * K, s_hint);
 #if BLP_PP
@@ -2223,7 +2228,8 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
           } else if (RC) {
             rc_chunk_offsets<BLOCK, K>(s_off, ns, s_coff, red);
             const int shift = build_hint<BLOCK, HC>(s_coff, ns, BLOCK, s_hint);
-            if (want_a)
+            if (BLP_EXP_PHASE == 1) {
+            } else if (want_a)
               rc_scan<BLOCK, K, true>(a.cw, a.idmask, a.idbits, a.aaw, s_wtab, s_start, s_off, s_coff, ns, c0, width,
                                       bm, CAP_WORDS, s_cn, s_aa, threadIdx.x, s_hint, shift, packed);
             else
@@ -2421,7 +2427,7 @@ __global__ __launch_bounds__(256, BLP_SHORT_MINB) void k_score_short(ScoreArgs a
           pout = a.g_out[pbeg + p];
         }
         if (!PS_OK(a.misc, pout >= 0 && pout < a.np, 4, pout, a.np)) continue;
-        if (!PS_OK(a.misc, st >= 0 && st + len <= a.nnz + CI_PAD, 10, st + len, a.nnz)) continue;
+        if (!PS_OK(a.misc, st >= 0 && st + len <= a.nnz + blp::CI_PAD, 10, st + len, a.nnz)) continue;
         unsigned c = 0;
         unsigned long long acc = 0;
         uint32_t acch = 0;  // <= SHORT_MAX terms of W >> 32 < 2^27
