@@ -62,6 +62,7 @@ SIGNATURES = {
     "blp_multi_destroy": [_P],
     "blp_multi_compact_csr": [_I32, _P, _P, _I32, _I64, _PP, ctypes.POINTER(ctypes.c_int64)],
     "blp_graph_wedge": [_P, ctypes.POINTER(ctypes.c_int64), _P, _P],
+    "blp_graph_col_idx": [_P, _P],
     "blp_graph_info": [_P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
                        ctypes.POINTER(ctypes.c_int)],
     "blp_graph_sync": [_P],

@@ -173,7 +173,23 @@ class HostGraph:
 
     @property
     def nnz(self):
-        return len(self.col_idx)
+        return int(self.row_ptr[-1])
+
+    @property
+    def col_idx(self):
+        """Column ids of the CSR (int32, nnz). A graph adopted from a device CSR fetches them on
+        first access (similarity.main never does: its scoring plans on the device)."""
+        ci = self.__dict__.get("_col_idx")
+        if ci is None:
+            ci = self._col_idx = self._fetch_col_idx()
+        return ci
+
+    @col_idx.setter
+    def col_idx(self, v):
+        self._col_idx = v
+
+    def _fetch_col_idx(self):
+        raise AttributeError("col_idx")
 
     # ------------------------------------------------------------------ ids
     def lookup(self, ids):
@@ -335,28 +351,33 @@ class DeviceGraph(HostGraph):
             check(L.blp_csr_info(c, ctypes.byref(nn), ctypes.byref(nnz)))
             n = nn.value
             t0 = time.perf_counter()
+            # row offsets and self-loop flags only: the column ids stay in HBM (col_idx fetches
+            # them on first access; the handle's own planning runs on the device)
             rp = np.empty(n + 1, np.int64)
-            ci = np.empty(max(nnz.value, 1), np.int32)
             sl = np.empty(max(n, 1), np.uint8)
-            check(L.blp_csr_fetch(c, ptr(rp), ptr(ci), ptr(sl)))
+            check(L.blp_csr_fetch(c, ptr(rp), None, ptr(sl)))
             t["fetch_s"] = time.perf_counter() - t0
             t0 = time.perf_counter()
             self.n = n
-            self._set_csr(rp, ci[: nnz.value], sl[:n], aa)
+            self._set_csr(rp, None, sl[:n], aa)
             t["host_half_s"] = time.perf_counter() - t0
             t0 = time.perf_counter()
             h = ctypes.c_void_p()
-            check(L.blp_graph_create_from_csr(c, ptr(self.row_ptr), ptr(ci), ptr(self.aa_weight) if aa else None,
+            check(L.blp_graph_create_from_csr(c, ptr(self.row_ptr), None, ptr(self.aa_weight) if aa else None,
                                               ctypes.byref(h)))
             c = None  # consumed
             t["graph_create_s"] = time.perf_counter() - t0
         finally:
             if c is not None:
                 L.blp_csr_destroy(c)
-        self._mirror = ci  # the handle borrows row_ptr / col_idx (their full allocations)
         self.device = device
         self.handle = h
         self.build_times = t
+
+    def _fetch_col_idx(self):
+        ci = np.empty(max(self.nnz, 1), np.int32)
+        check(lib().blp_graph_col_idx(self.handle, ptr(ci)))
+        return ci[: self.nnz]
 
     def _upload(self, device, aa):
         self.device = device

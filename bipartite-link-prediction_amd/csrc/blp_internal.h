@@ -169,7 +169,8 @@ struct blp_graph {
   std::vector<int64_t> h_rp;
   std::vector<int32_t> h_ci;
   const int64_t* hrp = nullptr;
-  const int32_t* hci = nullptr;
+  const int32_t* hci = nullptr;  // null until first needed when the graph was created without it (host_col_idx)
+  std::mutex mirror_mu;          // held while host_col_idx fetches the column mirror
   blp::KernelTimer timers[blp::K_COUNT];
 };
 
@@ -190,6 +191,10 @@ int build_hot_index(blp_graph* g);
 int graph_finish(blp_graph* g, const double* aaw);
 int build_wedge_index(blp_graph* g);
 int build_node2(blp_graph* g);  // after build_hot_index (the dense-row flag)
+// The host column-id mirror, fetched from the device on first use when the graph was created
+// without one (blp_graph_create_from_csr with col_idx = NULL: similarity.main's path, whose
+// scoring plans on the device and never reads it). Null + error set on failure.
+const int32_t* host_col_idx(blp_graph* g);
 void free_node2(blp_graph* g);
 constexpr int REPR_SLOT_BYTES = 24;  // repr.h REPR_SLOT
 // repr(v) of n device doubles into 24-byte slots at d_out (repr.hip); enqueued on s

@@ -205,7 +205,7 @@ extern "C" int blp_csr_fetch(const blp_csr* c, int64_t* row_ptr, int32_t* col_id
   BLP_CHECK(c, BLP_E_ARG, "blp_csr_fetch: null csr");
   BLP_HIP(hipSetDevice(c->device));
   prefault_host(row_ptr, 8 * (size_t)(c->n + 1));
-  if (c->nnz) prefault_host(col_idx, 4 * (size_t)c->nnz);
+  if (c->nnz && col_idx) prefault_host(col_idx, 4 * (size_t)c->nnz);
   if (row_ptr) BLP_HIP(hipMemcpy(row_ptr, c->d_rp, 8 * (c->n + 1), hipMemcpyDeviceToHost));
   if (col_idx && c->nnz) BLP_HIP(hipMemcpy(col_idx, c->d_ci, 4 * c->nnz, hipMemcpyDeviceToHost));
   if (self_loop && c->n) BLP_HIP(hipMemcpy(self_loop, c->d_self, c->n, hipMemcpyDeviceToHost));
@@ -214,7 +214,7 @@ extern "C" int blp_csr_fetch(const blp_csr* c, int64_t* row_ptr, int32_t* col_id
 
 extern "C" int blp_graph_create_from_csr(blp_csr* c, const int64_t* row_ptr, const int32_t* col_idx,
                                          const double* aaw, blp_graph** out) {
-  BLP_CHECK(c && out && row_ptr && (c->nnz == 0 || col_idx), BLP_E_ARG, "blp_graph_create_from_csr: bad arguments");
+  BLP_CHECK(c && out && row_ptr, BLP_E_ARG, "blp_graph_create_from_csr: bad arguments");  // col_idx may be NULL (fetched on demand)
   BLP_CHECK(row_ptr[c->n] == c->nnz, BLP_E_ARG, "blp_graph_create_from_csr: host mirror does not match the csr");
   BLP_HIP(hipSetDevice(c->device));
   blp_graph* g = new blp_graph();

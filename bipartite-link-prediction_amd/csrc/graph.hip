@@ -285,6 +285,28 @@ int graph_finish(blp_graph* g, const double* aaw) {
 
 }  // namespace blp
 
+namespace blp {
+const int32_t* host_col_idx(blp_graph* g) {
+  std::lock_guard<std::mutex> lk(g->mirror_mu);
+  static const int32_t none = 0;  // an empty graph's mirror: nothing to read
+  if (g->hci || g->nnz == 0) return g->hci ? g->hci : &none;
+  try {
+    g->h_ci.resize((size_t)g->nnz);
+  } catch (...) {
+    fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "host_col_idx: host mirror allocation");
+    return nullptr;
+  }
+  prefault_host(g->h_ci.data(), 4 * (size_t)g->nnz);
+  if (hipSetDevice(g->device) != hipSuccess ||
+      hipMemcpy(g->h_ci.data(), g->d_ci, 4 * (size_t)g->nnz, hipMemcpyDeviceToHost) != hipSuccess) {
+    fail(BLP_E_HIP_BASE, "host_col_idx: fetch of the column ids failed");
+    return nullptr;
+  }
+  g->hci = g->h_ci.data();
+  return g->hci;
+}
+}  // namespace blp
+
 using namespace blp;
 
 extern "C" {
@@ -414,6 +436,15 @@ int blp_graph_destroy(blp_graph* g) {
 int blp_graph_aa_shift(const blp_graph* g, int* shift) {
   BLP_CHECK(g && shift, BLP_E_ARG, "blp_graph_aa_shift: bad arguments");
   *shift = AA_SHIFT;  // fixed: W = w * 2^58 (exact sums, blp_internal.h)
+  return BLP_OK;
+}
+
+int blp_graph_col_idx(const blp_graph* g, int32_t* out) {
+  BLP_CHECK(g && (g->nnz == 0 || out), BLP_E_ARG, "blp_graph_col_idx: bad arguments");
+  if (g->nnz == 0) return BLP_OK;
+  BLP_HIP(hipSetDevice(g->device));
+  prefault_host(out, 4 * (size_t)g->nnz);
+  BLP_HIP(hipMemcpy(out, g->d_ci, 4 * (size_t)g->nnz, hipMemcpyDeviceToHost));
   return BLP_OK;
 }
 

@@ -492,7 +492,8 @@ extern "C" int blp_hop3_sample(blp_graph* g, const int32_t* src, int64_t n_src, 
   BLP_CHECK(n_src < (int64_t(1) << 31), BLP_E_ARG, "blp_hop3_sample: too many sources");
   BLP_CHECK(cap == 0 || (out_x && out_y && out_label), BLP_E_ARG, "blp_hop3_sample: null outputs");
   const int64_t* rp = g->hrp;
-  const int32_t* ci = g->hci;
+  const int32_t* ci = host_col_idx(g);
+  if (!ci) return BLP_E_STATE;
   const int64_t n = g->n;
   // plan the two universes: H2 ⊂ N(N(x)), distance-3 marks ⊂ N(H2) ⊂ the rows' neighbour ranges
   int64_t lo2 = INT64_MAX, hi2 = INT64_MIN;

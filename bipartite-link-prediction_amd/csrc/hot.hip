@@ -25,6 +25,16 @@ __global__ void k_hot_fill(const int64_t* __restrict__ rp, const int32_t* __rest
   }
 }
 
+// first and last id of each listed row (rows of >= hot_min ids: never empty)
+__global__ void k_row_ends(const int64_t* __restrict__ rp, const int32_t* __restrict__ ci, const int32_t* __restrict__ rows,
+                           int64_t nrows, int32_t* __restrict__ ends) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nrows; i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t v = rows[i];
+    ends[2 * i] = ci[rp[v]];
+    ends[2 * i + 1] = ci[rp[v + 1] - 1];
+  }
+}
+
 }  // namespace
 
 namespace blp {
@@ -34,19 +44,42 @@ int build_hot_index(blp_graph* g) {
   if (const char* e = getenv("BLP_HOT_MIN")) hot_min = std::max<int64_t>(1, atoll(e));
   if (const char* e = getenv("BLP_HOT_DENSITY")) density = std::max<int64_t>(1, atoll(e));
   const int64_t* rp = g->hrp;
-  const int32_t* ci = g->hci;
+  std::vector<int32_t> cand;  // rows long enough to be dense
+  for (int64_t v = 0; v < g->n; ++v)
+    if (rp[v + 1] - rp[v] >= hot_min) cand.push_back((int32_t)v);
+  // each candidate's first and last id: from the host mirror, or gathered on the device when the
+  // graph was created without one (only these 2 ids per long row are read)
+  std::vector<int32_t> ends(2 * cand.size());
+  if (g->hci) {
+    for (size_t i = 0; i < cand.size(); ++i) {
+      ends[2 * i] = g->hci[rp[cand[i]]];
+      ends[2 * i + 1] = g->hci[rp[cand[i] + 1] - 1];
+    }
+  } else if (!cand.empty()) {
+    ScopedBuf d;
+    int rc;
+    if ((rc = d.reserve(12 * cand.size()))) return rc;
+    int32_t* d_rows = d.as<int32_t>();
+    int32_t* d_ends = d_rows + cand.size();
+    BLP_HIP(hipMemcpy(d_rows, cand.data(), 4 * cand.size(), hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_row_ends, dim3((unsigned)std::min<size_t>((cand.size() + 255) / 256, 1024)), dim3(256), 0,
+                       g->stream, g->d_rp, g->d_ci, d_rows, (int64_t)cand.size(), d_ends);
+    BLP_HIP(hipGetLastError());
+    BLP_HIP(hipMemcpyAsync(ends.data(), d_ends, 8 * cand.size(), hipMemcpyDeviceToHost, g->stream));
+    BLP_HIP(hipStreamSynchronize(g->stream));
+  }
   std::vector<int32_t> idx((size_t)g->n, -1), rows;
   std::vector<HotRow> tab;
   int64_t vecs = 0;
-  for (int64_t v = 0; v < g->n; ++v) {
+  for (size_t i = 0; i < cand.size(); ++i) {
+    const int32_t v = cand[i];
     const int64_t d = rp[v + 1] - rp[v];
-    if (d < hot_min) continue;
-    const int64_t lo = ci[rp[v]], hi = (int64_t)ci[rp[v + 1] - 1] + 1;
+    const int64_t lo = ends[2 * i], hi = (int64_t)ends[2 * i + 1] + 1;
     if (d * density < hi - lo) continue;
     const int32_t vlo = (int32_t)(lo >> 7);
     const int32_t nvec = (int32_t)(((hi + 127) >> 7) - vlo);
     idx[v] = (int32_t)rows.size();
-    rows.push_back((int32_t)v);
+    rows.push_back(v);
     tab.push_back(HotRow{vecs, vlo, nvec});
     vecs += nvec;
   }

@@ -3551,7 +3551,8 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
     // host planning (a graph without device two-hop statistics, or BLP_HOST_PLAN): the pair and
     // source loops gather rows at random from the host mirror, on up to 16 threads
     const int64_t* rp = g->hrp;
-    const int32_t* ci = g->hci;
+    const int32_t* ci = host_col_idx(g);
+    if (!ci) return bail(BLP_E_STATE);
     struct Acc {
       int64_t lo = INT64_MAX, hi = INT64_MIN, scan = 0, max_scan = 0, max_build = 0;
       int64_t rows_lo = INT64_MAX, rows_hi = INT64_MIN;  // nodes whose rows are read (the y and the z in N(x))
@@ -3804,7 +3805,8 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   const bool wedge_items = (b->short_rows & 1) && g->d_wp && !kn.no_wedge;
   if (b->chunks == 1 && span > 0 && !b->global && (!b->split || span <= variant_cap_bits(V_LARGE))) {
     const int64_t* rp = g->hrp;
-    const int32_t* ci = g->hci;
+    const int32_t* ci = (!heavy_cand.empty() && !wedge_items) ? host_col_idx(g) : g->hci;  // CSR items only
+    if (!heavy_cand.empty() && !wedge_items && !ci) return bail(BLP_E_STATE);
     for (const auto& hc : heavy_cand) {
       if (hc.second <= 2 * item_work) continue;
       if (heavy_slot.empty()) heavy_slot.assign((size_t)n, -1);

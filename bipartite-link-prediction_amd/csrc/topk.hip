@@ -1269,7 +1269,8 @@ extern "C" int blp_topk_create(blp_graph* g, int64_t src_lo, int64_t src_hi, int
             BLP_E_ARG, "blp_topk_create: bad id ranges");
   BLP_CHECK(src_hi <= tgt_lo || tgt_hi <= src_lo, BLP_E_ARG, "blp_topk_create: source and target ranges overlap");
   const int64_t* rp = g->hrp;
-  const int32_t* ci = g->hci;
+  const int32_t* ci = host_col_idx(g);
+  if (!ci) return BLP_E_STATE;
   // bipartite check: every source row points into the targets and every target row into the sources
   for (int64_t v = src_lo; v < src_hi; ++v)
     for (int64_t e = rp[v]; e < rp[v + 1]; ++e)

@@ -80,7 +80,9 @@ int blp_csr_from_edges_device(int device, const int32_t* d_a, const int32_t* d_b
  * blp_graph_create_from_csr: a graph handle over that device CSR (no upload). row_ptr /
  *   col_idx are the host mirror of the same CSR (from blp_csr_fetch); unlike
  *   blp_graph_create, the handle BORROWS them: the caller keeps them alive and unchanged
- *   until blp_graph_destroy. On success the csr is consumed (do not destroy it); on failure
+ *   until blp_graph_destroy. col_idx may be NULL: pair scoring plans on the device and never
+ *   reads it, and the calls that do (hop-3 sampling, top-k create, host-planned batches) fetch
+ *   their own copy from HBM on first use. On success the csr is consumed (do not destroy it); on failure
  *   it is left intact. aaw as for blp_graph_create.                                       */
 typedef struct blp_csr blp_csr;
 int blp_csr_build_device(int device, const int32_t* d_a, const int32_t* d_b, int64_t m, int64_t n_nodes,
@@ -210,6 +212,9 @@ int blp_graph_destroy(blp_graph* g);
  * (-1: not built); wp [n + 1] (vector offsets) and wedge [4 * n_vecs] may be NULL.         */
 int blp_graph_wedge(const blp_graph* g, int64_t* n_vecs, int64_t* wp, int32_t* wedge);
 int blp_graph_info(const blp_graph* g, int64_t* n_nodes, int64_t* nnz, int* device);
+/* blp_graph_col_idx: the graph's column ids (nnz int32, the device CSR's) copied to `out`: the
+ * host copy of a graph created from a device CSR without one (blp_graph_create_from_csr).   */
+int blp_graph_col_idx(const blp_graph* g, int32_t* out);
 int blp_graph_sync(blp_graph* g); /* wait for all work queued on the handle's stream */
 /* Fixed-point scale of the Adamic-Adar terms: W = w * 2^shift with shift = 58, exact for every
  * weight the reference produces ((log d)^-1 in [2^-5, 2)); a pair's sum is carried exactly in
