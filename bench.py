@@ -1102,10 +1102,14 @@ def main():
 
     passes = []
     t0 = time.time()
-    if args.sides in ("both", "user"):
+    b_mask = 7 if getattr(args, "fix_adamic", False) else 3
+    if args.sides == "both":  # one upload of the pairs for both passes (blp_batch_create_pair)
+        ub_, bb_ = G.batch_pair(ex_x, ex_y)
+        passes += [("user", ub_, args.user_mask), ("business", bb_, b_mask)]
+    elif args.sides == "user":
         passes.append(("user", G.batch(ex_x, ex_y), args.user_mask))
-    if args.sides in ("both", "business"):
-        passes.append(("business", G.batch(ex_y, ex_x), 7 if getattr(args, "fix_adamic", False) else 3))
+    else:
+        passes.append(("business", G.batch(ex_y, ex_x), b_mask))
     t_batch = time.time() - t0
     if args.business_first:  # enqueue order of the two concurrent passes
         passes.reverse()

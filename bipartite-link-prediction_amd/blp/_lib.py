@@ -69,6 +69,7 @@ SIGNATURES = {
     "blp_graph_aa_shift": [_P, ctypes.POINTER(ctypes.c_int)],
     "blp_score_pairs": [_P, _I32, _U32, _P, _P, _I64, _P, _P, _P],
     "blp_batch_create": [_P, _P, _P, _I64, _PP],
+    "blp_batch_create_pair": [_P, _P, _P, _I64, _PP, _PP],
     "blp_batch_score": [_P, _P, _U32],
     "blp_batches_score": [_P, _I32, _P, _P],
     "blp_batch_fetch": [_P, _P, _P, _P, _P],

@@ -433,6 +433,11 @@ class DeviceGraph(HostGraph):
     def batch(self, x, y):
         return PairBatch(self, x, y)
 
+    def batch_pair(self, x, y):
+        """(PairBatch(x, y), PairBatch(y, x)): similarity.main's two passes over one pair list
+        with ONE upload of the pairs (blp_batch_create_pair)."""
+        return PairBatch.pair(self, x, y)
+
     def score_batches(self, items):
         """Enqueue several batches of this graph as one concurrent step (blp_batches_score).
         items: [(PairBatch, mask), ...]; returns at once, fetch() waits."""
@@ -499,6 +504,21 @@ class PairBatch:
         check(lib().blp_batch_create(graph.handle, ptr(self.x), ptr(self.y), self.n, ctypes.byref(h)))
         self.handle = h
         graph._adopt(self)
+
+    @classmethod
+    def pair(cls, graph, x, y):
+        xs, ys = _lib.as_i32(x), _lib.as_i32(y)
+        if len(xs) != len(ys):
+            raise ValueError("pair arrays differ in length")
+        h1, h2 = ctypes.c_void_p(), ctypes.c_void_p()
+        check(lib().blp_batch_create_pair(graph.handle, ptr(xs), ptr(ys), len(xs), ctypes.byref(h1), ctypes.byref(h2)))
+        out = []
+        for h, (a, b) in ((h1, (xs, ys)), (h2, (ys, xs))):
+            bt = cls.__new__(cls)
+            bt.graph, bt.x, bt.y, bt.n, bt.handle = graph, a, b, len(a), h
+            graph._adopt(bt)
+            out.append(bt)
+        return tuple(out)
 
     def plan(self):
         lo, hi = ctypes.c_int64(), ctypes.c_int64()

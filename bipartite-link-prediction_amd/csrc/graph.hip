@@ -256,8 +256,9 @@ int graph_finish(blp_graph* g, const double* aaw) {
     fprintf(stderr, "graph_finish %-8s %.3f ms\n", what, std::chrono::duration<double, std::milli>(t - t_prev).count());
     t_prev = t;
   };
-  hipDeviceProp_t prop;
-  if (hipGetDeviceProperties(&prop, g->device) == hipSuccess) g->n_cu = prop.multiProcessorCount;
+  int n_cu = 0;  // one attribute, not hipGetDeviceProperties' full query (~5 ms)
+  if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, g->device) == hipSuccess && n_cu > 0)
+    g->n_cu = n_cu;
   if (!g->stream) BLP_HIP(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
   const int64_t n = g->n;
   g->max_row = 0;

@@ -3445,7 +3445,13 @@ static int launch_pointers(const blp_graph* g, const blp_batch* b, ScoreArgs& a,
 
 extern "C" {
 
-int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n_pairs, blp_batch** out) {
+}  // extern "C"
+
+// blp_batch_create, and blp_batch_create_pair's second batch: `twin` (or null) is a batch of the
+// same pairs with x and y swapped whose device copies are taken (a device-to-device copy after the
+// twin's upload, on this batch's stream) instead of a second host-to-device upload.
+static int batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n_pairs, const blp_batch* twin,
+                        blp_batch** out) {
   BLP_CHECK(g && out && n_pairs >= 0 && (n_pairs == 0 || (x && y)), BLP_E_ARG, "blp_batch_create: bad arguments");
   BLP_CHECK(n_pairs < (int64_t(1) << 31) - 1, BLP_E_ARG, "blp_batch_create: at most 2^31-2 pairs per batch");
   const int64_t n = g->n;
@@ -3491,7 +3497,16 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   if (hipMalloc(&b->d_x, 4 * np) != hipSuccess || hipMalloc(&b->d_y, 4 * np) != hipSuccess ||
       hipMalloc(&b->d_misc, sizeof(Misc)) != hipSuccess)
     return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: hipMalloc failed"));
-  if (n_pairs) {
+  if (n_pairs && twin) {  // the twin's device copies, swapped, once its upload is done
+    hipEvent_t ev;
+    BLP_HIP_OR(hipEventCreateWithFlags(&ev, hipEventDisableTiming), bail);
+    hipError_t e = hipEventRecord(ev, twin->stream);
+    if (e == hipSuccess) e = hipStreamWaitEvent(b->stream, ev, 0);
+    (void)hipEventDestroy(ev);
+    BLP_HIP_OR(e, bail);
+    BLP_HIP_OR(hipMemcpyAsync(b->d_x, twin->d_y, 4 * n_pairs, hipMemcpyDeviceToDevice, b->stream), bail);
+    BLP_HIP_OR(hipMemcpyAsync(b->d_y, twin->d_x, 4 * n_pairs, hipMemcpyDeviceToDevice, b->stream), bail);
+  } else if (n_pairs) {
     BLP_HIP_OR(hipMemcpyAsync(b->d_x, x, 4 * n_pairs, hipMemcpyHostToDevice, b->stream), bail);
     BLP_HIP_OR(hipMemcpyAsync(b->d_y, y, 4 * n_pairs, hipMemcpyHostToDevice, b->stream), bail);
   }
@@ -3932,6 +3947,29 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   }
   stage("buffers");
   *out = b;
+  return BLP_OK;
+}
+
+extern "C" {
+
+int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n_pairs, blp_batch** out) {
+  return batch_create(g, x, y, n_pairs, nullptr, out);
+}
+
+int blp_batch_create_pair(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n_pairs, blp_batch** out_xy,
+                          blp_batch** out_yx) {
+  BLP_CHECK(out_xy && out_yx, BLP_E_ARG, "blp_batch_create_pair: null outputs");
+  blp_batch* a = nullptr;
+  int rc = batch_create(g, x, y, n_pairs, nullptr, &a);
+  if (rc) return rc;
+  blp_batch* b = nullptr;
+  rc = batch_create(g, y, x, n_pairs, a, &b);
+  if (rc) {
+    blp_batch_destroy(a);
+    return rc;
+  }
+  *out_xy = a;
+  *out_yx = b;
   return BLP_OK;
 }
 

@@ -126,13 +126,12 @@ def score_both_sides(examples, G, u_mask, b_mask):
 
 
 def _score_both_ids(G, u_ids, v_ids, u_mask, b_mask, timings=None, text=False):
-    """Id lookup, the two batches (created concurrently: blp_batch_create's host planning
-    releases the GIL), one concurrent device step, and the results; phase times into
+    """Id lookup, the two batches (blp_batch_create_pair: one upload, planned on the device),
+    one concurrent device step, and the results; phase times into
     ``timings`` (score_lookup, score_create, score_device, score_fetch) when given. ``text``:
     the Jaccard / Adamic-Adar scores come back as their json.dumps text, formatted on the
     device (PairBatch.fetch_repr: "jaccard_repr" / "adamic_repr" slots), not as doubles."""
     import time
-    from concurrent.futures import ThreadPoolExecutor
 
     t0 = time.perf_counter()
     du, pu = G.lookup(u_ids)
@@ -140,10 +139,7 @@ def _score_both_ids(G, u_ids, v_ids, u_mask, b_mask, timings=None, text=False):
     present = pu & pv
     xs, ys = (du, dv) if present.all() else (du[present], dv[present])
     t1 = time.perf_counter()
-    with ThreadPoolExecutor(1) as pool:
-        fb = pool.submit(G.batch, ys, xs)
-        ub = G.batch(xs, ys)
-        bb = fb.result()
+    ub, bb = G.batch_pair(xs, ys)  # one upload of the pairs for both passes
     try:
         t2 = time.perf_counter()
         G.score_batches([(ub, u_mask), (bb, b_mask)])
@@ -290,16 +286,21 @@ def main(example_file, graph_file, u_methods, u_outfiles, b_methods, b_outfiles,
             _write_files(_write_jobs(ex, u_methods, u_outfiles, _U_BITS, present, u_scores) +
                          _write_jobs(ex, b_methods, b_outfiles, _B_BITS, present, b_scores))
     finally:
+        t_f = clock()
         pool.shutdown(wait=True)
         if ex is None and fut_ex.done() and fut_ex.exception() is None:
             ex = fut_ex.result()[0]
         if ex is not None:
             ex.close()
+        t_c = clock()
+        G = locals().get("G")
+        if G is not None:  # the reference's graph goes when main returns; so does this one (HBM freed here)
+            G.close()
     if timings is not None:
         # examples and graph load concurrently: "graph" is the graph load, "examples" the extra
         # wait for examples.json after it
-        timings.update({"graph": t_g - t, "examples": t_ex - t_g, "score": t_s - t_ex, "files": clock() - t_s,
-                        "pairs": int(present.sum())})
+        timings.update({"graph": t_g - t, "examples": t_ex - t_g, "score": t_s - t_ex, "files": t_f - t_s,
+                        "teardown": t_c - t_f, "graph_release": clock() - t_c, "pairs": int(present.sum())})
         timings["graph_detail"] = dict(getattr(G, "build_times", None) or {})
 
 

@@ -249,6 +249,12 @@ int blp_score_pairs(blp_graph* g, int side, uint32_t mask, const int32_t* pair_u
  * for every batch of the device. */
 int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n_pairs,
                      blp_batch** out);
+/* blp_batch_create_pair: both passes of similarity.main over one pair list -- *out_xy the
+ * batch (x, y) (the user side), *out_yx the batch (y, x) (the business side) -- with ONE
+ * host-to-device upload: the second batch copies the first's device arrays, swapped. Each
+ * batch is then destroyed on its own (blp_batch_destroy).                                    */
+int blp_batch_create_pair(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n_pairs,
+                          blp_batch** out_xy, blp_batch** out_yx);
 int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask);
 int blp_batch_fetch(blp_graph* g, blp_batch* b, uint32_t* cn, double* jac, double* aa);
 /* blp_batch_fetch_repr: the batch's Jaccard (which = BLP_JACCARD) or Adamic-Adar (BLP_ADAMIC)

@@ -520,3 +520,29 @@ def test_device_plan_equals_host_plan(gpu, knobs, monkeypatch):
         dev.close()
         host.close()
     _check_against_oracle(a, b, y[perm], x[perm])
+
+
+def test_batch_pair_equals_two_batches(gpu):
+    """blp_batch_create_pair (one upload, the business batch copies the user batch's device
+    arrays swapped) gives the two batches blp_batch_create gives, scores and plans alike, for a
+    source-grouped list and a shuffled one (similarity.main's two passes, similarity.py:20-106)."""
+    rng = np.random.default_rng(23)
+    a, b = bipartite_edges(rng, 30000, 1500, 300000)
+    G = blp.DeviceGraph(a, b)
+    nu = G.n - len(np.unique(b))
+    x = np.repeat(np.sort(rng.choice(nu, 150, replace=False)), 30).astype(np.int32)
+    y = rng.integers(nu, G.n, len(x)).astype(np.int32)
+    perm = rng.permutation(len(x))
+    for xs, ys in ((x, y), (x[perm], y[perm]), (x[:0], y[:0])):
+        ub, bb = G.batch_pair(xs, ys)
+        u1, b1 = G.batch(xs, ys), G.batch(ys, xs)
+        assert ub.plan() == u1.plan() and bb.plan() == b1.plan()
+        G.score_batches([(ub, 7), (bb, 3)])
+        G.score_batches([(u1, 7), (b1, 3)])
+        for p, q, m in ((ub, u1, 7), (bb, b1, 3)):
+            rp, rq = p.fetch(m), q.fetch(m)
+            for k in rp:
+                np.testing.assert_array_equal(rp[k], rq[k])
+        for bt in (ub, bb, u1, b1):
+            bt.close()
+    _check_against_oracle(a, b, x[perm], y[perm])
