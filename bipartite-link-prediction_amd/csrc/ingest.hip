@@ -417,8 +417,8 @@ int device_load(const char* path, int device, blp_edges** out) {
     BLP_HIP(hipGetDeviceCount(&ndev));
     BLP_CHECK(device >= 0 && device < ndev, BLP_E_ARG, "blp_edges_load_device: no such device");
     BLP_HIP(hipSetDevice(device));
-    int n_cu = 256, a = 0;
-    if (hipDeviceGetAttribute(&a, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && a > 0) n_cu = a;
+    int n_cu = 256, cu_attr = 0;
+    if (hipDeviceGetAttribute(&cu_attr, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cu_attr > 0) n_cu = cu_attr;
     BLP_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     const bool tail_nl = data[S - 1] == '\n';
     const int64_t T = S + (tail_nl ? 0 : 1);  // a missing final newline is supplied
