@@ -211,10 +211,17 @@ __global__ __launch_bounds__(GP_BLOCK) void k_bucket_hist(const int32_t* __restr
 
 // The pair itself (caller index, x, y) moves into bucket order, so the group kernel reads
 // its bucket contiguously instead of gathering x[i] / y[i] at random caller positions.
+// ROWS (round 5): the record carries N(y)'s row instead of y -- (caller index, x, rp[y] as int32,
+// |N(y)|) -- gathered HERE, in caller order: similarity.users' order keeps a user's ~750 pairs
+// together, so on the business side (y = user) a wave's gathers hit one or two rows and cost
+// nothing, where the grouped order of the later write kernel scatters them over the whole
+// row_ptr array. keys (or null): x again, 4 bytes per pair, for k_item_count.
+template <bool ROWS = false>
 __global__ __launch_bounds__(GP_BLOCK) void k_bucket_scatter(const int32_t* __restrict__ x, const int32_t* __restrict__ y,
                                                              int64_t np, int32_t xlo, int shift, int bmask, int nb, int nblk,
                                                              int64_t per_blk, const int32_t* __restrict__ hoff,
-                                                             int4* __restrict__ tmp) {
+                                                             int4* __restrict__ tmp, const int64_t* __restrict__ rp = nullptr,
+                                                             int32_t* __restrict__ keys = nullptr) {
   __shared__ int cur[NB_MAX];
   for (int i = threadIdx.x; i < nb; i += GP_BLOCK) cur[i] = hoff[(int64_t)i * nblk + blockIdx.x];
   __syncthreads();
@@ -229,11 +236,24 @@ __global__ __launch_bounds__(GP_BLOCK) void k_bucket_scatter(const int32_t* __re
       yv[u] = i < b1 ? y[i] : 0;
     }
     int pos[U];
+    int sv[U], lv[U];
+    if (ROWS) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t b0 = rp[yv[u]], b1 = rp[yv[u] + 1];
+        sv[u] = (int)b0;
+        lv[u] = (int)(b1 - b0);
+      }
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u) pos[u] = xv[u] != INT32_MIN ? atomicAdd(&cur[((xv[u] - xlo) >> shift) & bmask], 1) : -1;
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      if (pos[u] >= 0) tmp[pos[u]] = make_int4((int32_t)(r + u * GP_BLOCK + threadIdx.x), xv[u], yv[u], 0);
+      if (pos[u] >= 0) {
+        const int32_t ci = (int32_t)(r + u * GP_BLOCK + threadIdx.x);
+        tmp[pos[u]] = ROWS ? make_int4(ci, xv[u], sv[u], lv[u]) : make_int4(ci, xv[u], yv[u], 0);
+        if (keys) keys[pos[u]] = xv[u];
+      }
   }
 }
 
@@ -365,7 +385,8 @@ __global__ __launch_bounds__(1024) void k_item_plan(const int32_t* __restrict__ 
 }
 
 template <int KEYS>
-__device__ inline void item_hist(const int4* __restrict__ tmp, int s, int e, int32_t xlo, int lognb, int* h) {
+__device__ inline void item_hist(const int4* __restrict__ tmp, int s, int e, int32_t xlo, int lognb, int* h,
+                                 const int32_t* __restrict__ keys = nullptr) {
   for (int i = threadIdx.x; i < KEYS; i += GB_BLOCK) h[i] = 0;
   __syncthreads();
   constexpr int UC = 4;  // GI_PAIRS / GB_BLOCK = 16 pairs per thread: UC loads in flight
@@ -374,7 +395,7 @@ __device__ inline void item_hist(const int4* __restrict__ tmp, int s, int e, int
 #pragma unroll
     for (int u = 0; u < UC; ++u) {
       const int k = kr + u * GB_BLOCK + (int)threadIdx.x;
-      xv[u] = k < e ? tmp[k].y : INT32_MIN;
+      xv[u] = k < e ? (keys ? keys[k] : tmp[k].y) : INT32_MIN;  // keys: 4 bytes per pair, not a 16-byte record's line
     }
 #pragma unroll
     for (int u = 0; u < UC; ++u)
@@ -388,12 +409,13 @@ __global__ __launch_bounds__(GB_BLOCK) void k_item_count(const int4* __restrict_
                                                          const int32_t* __restrict__ item_s,
                                                          const int32_t* __restrict__ item_e,
                                                          const int32_t* __restrict__ n_items, int32_t xlo, int lognb,
-                                                         int32_t* __restrict__ cnt, int32_t* __restrict__ ih) {
+                                                         int32_t* __restrict__ cnt, int32_t* __restrict__ ih,
+                                                         const int32_t* __restrict__ keys = nullptr) {
   __shared__ int h[KEYS];
   const int i = blockIdx.x;
   if (i >= *n_items) return;  // uniform: the grid is the host's upper bound on items
   const int b = item_b[i];
-  item_hist<KEYS>(tmp, item_s[i], item_e[i], xlo, lognb, h);
+  item_hist<KEYS>(tmp, item_s[i], item_e[i], xlo, lognb, h, keys);
   for (int j = threadIdx.x; j < KEYS; j += GB_BLOCK) {
     if (h[j]) atomicAdd(&cnt[xlo + b + (j << lognb)], h[j]);
     if (ih) ih[(int64_t)i * KEYS + j] = h[j];  // the item's histogram, for k_item_write_runs
@@ -538,12 +560,14 @@ __global__ __launch_bounds__(GB_BLOCK) void k_item_write_runs(const int64_t* __r
   }
 }
 
-// k_item_write_runs with 8-byte stage records (round 5): the item's (caller index, y) pairs are
-// staged in key order (32 KiB of LDS instead of 64: twice the resident workgroups), and the write
-// loop finds each slot's key by a binary search of the key starts. ROWS: N(y)'s bounds gathered
-// from rp and written as g_yb / g_yl (what the scorers read), U slots per thread with their
-// gathers in flight together; otherwise y itself (g_y) and the scorer gathers them (pair_row).
-template <int KEYS, bool ROWS>
+// k_item_write_runs with 8-byte stage records (round 5): the item's pairs are staged in key
+// order in 32 KiB of LDS instead of 64 (twice the resident workgroups), and the write loop finds
+// each slot's key by a binary search of the key starts. MODE 2: the records already carry N(y)'s
+// row (k_bucket_scatter<true>): (caller index, row start) staged, row lengths beside them (48 KiB),
+// no gathers at all. MODE 1: (caller index, y) staged, the row gathered from rp here, U slots per
+// thread in flight together. MODE 0: y itself goes out (g_y) and the scorer gathers the row
+// (pair_row).
+template <int KEYS, int MODE>
 __global__ __launch_bounds__(GB_BLOCK) void k_item_write_ids(const int64_t* __restrict__ rp, const int4* __restrict__ tmp,
                                                              const int32_t* __restrict__ item_b,
                                                              const int32_t* __restrict__ item_s,
@@ -559,6 +583,7 @@ __global__ __launch_bounds__(GB_BLOCK) void k_item_write_ids(const int64_t* __re
   __shared__ int lofs[KEYS];   // the key's first local position
   __shared__ int gbase[KEYS];  // ... and its first global position
   __shared__ int2 stage[GI_PAIRS];
+  __shared__ int stage_len[MODE == 2 ? GI_PAIRS : 1];
   __shared__ int red[GB_BLOCK / 64];
   const int i = blockIdx.x;
   if (i >= *n_items) return;
@@ -595,7 +620,11 @@ __global__ __launch_bounds__(GB_BLOCK) void k_item_write_ids(const int64_t* __re
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      if (t[u].x >= 0) stage[atomicAdd(&h[(t[u].y - xlo) >> lognb], 1)] = make_int2(t[u].x, t[u].z);
+      if (t[u].x >= 0) {
+        const int slot = atomicAdd(&h[(t[u].y - xlo) >> lognb], 1);
+        stage[slot] = make_int2(t[u].x, t[u].z);
+        if (MODE == 2) stage_len[slot] = t[u].w;
+      }
   }
   __syncthreads();
   const int n = e - s;
@@ -621,7 +650,15 @@ __global__ __launch_bounds__(GB_BLOCK) void k_item_write_ids(const int64_t* __re
         pos[u] = gbase[lo] + (p - lofs[lo]);
       }
     }
-    if (ROWS) {
+    if (MODE == 2) {
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (pos[u] >= 0) {
+          g_out[pos[u]] = r[u].x;
+          g_yb[pos[u]] = (int64_t)(uint32_t)r[u].y;
+          g_yl[pos[u]] = stage_len[pr + u * GB_BLOCK + (int)threadIdx.x];
+        }
+    } else if (MODE == 1) {
       int64_t st[U], en[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -3219,6 +3256,7 @@ struct Knobs {
   bool group_rows = true;        // BLP_GROUP_YN=1 clears it: short-row batches then group y only and the
                                  // scorer gathers N(y)'s bounds (k_item_write_ids<K, false>; measured slower)
   bool group_rows16 = false;     // BLP_GROUP_ROWS16: the 16-byte-stage grouping write (k_item_write_runs)
+  bool group_gather = false;     // BLP_GROUP_GATHER: rows gathered by the write kernel, not carried by the scatter
   std::string debug_null;        // BLP_DEBUG_NULL (BLP_DEBUG builds only): null this launch pointer, to
                                  // show the pre-launch pointer check (launch_pointers) refusing it
 };
@@ -3253,6 +3291,7 @@ Knobs read_knobs() {
   k.no_pko = on("BLP_NO_PKO");
   k.group_rows = !on("BLP_GROUP_YN");
   k.group_rows16 = on("BLP_GROUP_ROWS16");
+  k.group_gather = on("BLP_GROUP_GATHER");
   k.host_plan = on("BLP_HOST_PLAN");
   k.short_seg = on("BLP_SHORT_SEG");
 #ifdef BLP_DEBUG
@@ -4074,7 +4113,7 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   // scratch: hist | hoff | tiles | bucket_active | abase | tmp [| fill | item table | id-range tiles]
   const int64_t items_ub = (np + GI_PAIRS - 1) / GI_PAIRS + b->nb;
   const int64_t items_ints = b->items ? b->xspan + 3 * items_ub + 2 * ((b->xspan + SCAN_TILE - 1) / SCAN_TILE + 1) +
-                                            1024 * items_ub
+                                            1024 * items_ub + np  // ... + the scatter's key array
                                       : 0;
   const int64_t sc_ints = 2 * nh + std::max(tiles_h, tiles_b) + 1 + 2 * (int64_t)b->nb + 4 * np + items_ints;
   if ((rc = b->scratch.reserve(4 * (sc_ints + 16)))) return rc;
@@ -4106,10 +4145,22 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
     hipLaunchKernelGGL(k_scan_sum, dim3((unsigned)tiles_h), dim3(SCAN_BLOCK), 0, b->stream, hist, nh, tiles);
     hipLaunchKernelGGL(k_scan_mid, dim3(1), dim3(SCAN_BLOCK), 0, b->stream, tiles, tiles_h, (int32_t*)nullptr);
     hipLaunchKernelGGL(k_scan_out, dim3((unsigned)tiles_h), dim3(SCAN_BLOCK), 0, b->stream, hist, nh, tiles, hoff);
-    hipLaunchKernelGGL(k_bucket_scatter, dim3(b->nblk), dim3(GP_BLOCK), 0, b->stream, b->d_x, b->d_y, np, b->xlo,
-                       hshift, bmask, b->nb, b->nblk, b->per_blk, hoff, tmp);
+    // item grouping whose write kernel stages runs (<= 1024 keys per bucket) and whose scorer reads
+    // grouped row bounds (no g_y): the scatter gathers N(y)'s row in caller order (rec_rows) and
+    // writes a compact key array for the item histograms
+    const int64_t ub = (np + GI_PAIRS - 1) / GI_PAIRS + b->nb, tx = (b->xspan + SCAN_TILE - 1) / SCAN_TILE;
+    const int64_t ikeys = b->items ? (b->xspan + b->nb - 1) >> b->shift : 0;
+    const bool rec_rows = b->items && ikeys <= 1024 && !b->d_gy && g->nnz < (int64_t(1) << 31) &&
+                          !b->kn.group_gather && !b->kn.group_rows16;
+    int32_t* keyarr = b->items ? reinterpret_cast<int32_t*>(tmp + np) + b->xspan + 3 * ub + 2 * (tx + 1) + 1024 * ub
+                               : nullptr;
+    if (rec_rows)
+      hipLaunchKernelGGL((k_bucket_scatter<true>), dim3(b->nblk), dim3(GP_BLOCK), 0, b->stream, b->d_x, b->d_y, np,
+                         b->xlo, hshift, bmask, b->nb, b->nblk, b->per_blk, hoff, tmp, g->d_rp, keyarr);
+    else
+      hipLaunchKernelGGL((k_bucket_scatter<false>), dim3(b->nblk), dim3(GP_BLOCK), 0, b->stream, b->d_x, b->d_y, np,
+                         b->xlo, hshift, bmask, b->nb, b->nblk, b->per_blk, hoff, tmp, (const int64_t*)nullptr, keyarr);
     if (b->items) {
-      const int64_t ub = (np + GI_PAIRS - 1) / GI_PAIRS + b->nb, tx = (b->xspan + SCAN_TILE - 1) / SCAN_TILE;
       int32_t* fill = reinterpret_cast<int32_t*>(tmp + np);
       int32_t *it_b = fill + b->xspan, *it_s = it_b + ub, *it_e = it_s + ub, *tx1 = it_e + ub, *tx2 = tx1 + tx + 1;
       int32_t *cnt = b->cnt.as<int32_t>(), *off = b->off.as<int32_t>();
@@ -4117,14 +4168,14 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
       BLP_HIP(hipMemsetAsync(fill, 0, 4 * (size_t)b->xspan, b->stream));
       hipLaunchKernelGGL(k_item_plan, dim3(1), dim3(1024), 0, b->stream, hoff, b->nblk, b->nb, np, it_b, it_s, it_e,
                          &b->d_misc->n_items);
-      const int64_t keys = (b->xspan + b->nb - 1) >> b->shift;
+      const int64_t keys = ikeys;
       const bool runs_w = keys <= 1024;
       const bool ids_w = b->use_short && b->d_gy && !b->kn.group_rows;  // k_item_write_ids (short-row scorer)
       b->yn_grouped = runs_w && ids_w;
       int32_t* ih = tx2 + tx + 1;  // [ub][K] item histograms (runs_w)
 #define BLP_ITEM_LAUNCH(K)                                                                                         \
   hipLaunchKernelGGL(k_item_count<K>, dim3((unsigned)ub), dim3(GB_BLOCK), 0, b->stream, tmp, it_b, it_s, it_e,     \
-                     &b->d_misc->n_items, b->xlo, b->shift, cnt, runs_w ? ih : nullptr);                           \
+                     &b->d_misc->n_items, b->xlo, b->shift, cnt, runs_w ? ih : nullptr, keyarr);                   \
   hipLaunchKernelGGL(k_scan_sum, dim3((unsigned)tx), dim3(SCAN_BLOCK), 0, b->stream, cnt + b->xlo, b->xspan, tx1); \
   hipLaunchKernelGGL(k_scan_mid, dim3(1), dim3(SCAN_BLOCK), 0, b->stream, tx1, tx, (int32_t*)nullptr);             \
   hipLaunchKernelGGL(k_scan_out, dim3((unsigned)tx), dim3(SCAN_BLOCK), 0, b->stream, cnt + b->xlo, b->xspan, tx1,  \
@@ -4134,11 +4185,15 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   hipLaunchKernelGGL(k_nz_write, dim3((unsigned)tx), dim3(SCAN_BLOCK), 0, b->stream, cnt + b->xlo, b->xspan, tx2,  \
                      b->xlo, b->active.as<int32_t>());                                                              \
   if (runs_w && ids_w)                                                                                                \
-    hipLaunchKernelGGL((k_item_write_ids<(K <= 1024 ? K : 1024), false>), dim3((unsigned)ub), dim3(GB_BLOCK), 0,     \
+    hipLaunchKernelGGL((k_item_write_ids<(K <= 1024 ? K : 1024), 0>), dim3((unsigned)ub), dim3(GB_BLOCK), 0,         \
+                       b->stream, g->d_rp, tmp, it_b, it_s, it_e, &b->d_misc->n_items, b->xlo, b->shift, ih, off,     \
+                       fill, b->d_gout, b->d_gyb, b->d_gyl, b->d_gy);                                                 \
+  else if (runs_w && rec_rows)                                                                                        \
+    hipLaunchKernelGGL((k_item_write_ids<(K <= 1024 ? K : 1024), 2>), dim3((unsigned)ub), dim3(GB_BLOCK), 0,         \
                        b->stream, g->d_rp, tmp, it_b, it_s, it_e, &b->d_misc->n_items, b->xlo, b->shift, ih, off,     \
                        fill, b->d_gout, b->d_gyb, b->d_gyl, b->d_gy);                                                 \
   else if (runs_w && !b->kn.group_rows16)                                                                             \
-    hipLaunchKernelGGL((k_item_write_ids<(K <= 1024 ? K : 1024), true>), dim3((unsigned)ub), dim3(GB_BLOCK), 0,      \
+    hipLaunchKernelGGL((k_item_write_ids<(K <= 1024 ? K : 1024), 1>), dim3((unsigned)ub), dim3(GB_BLOCK), 0,         \
                        b->stream, g->d_rp, tmp, it_b, it_s, it_e, &b->d_misc->n_items, b->xlo, b->shift, ih, off,     \
                        fill, b->d_gout, b->d_gyb, b->d_gyl, b->d_gy);                                                 \
   else if (runs_w)                                                                                                    \

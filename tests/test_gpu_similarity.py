@@ -154,6 +154,7 @@ def test_general_graph_exact_distance(gpu):
     {"BLP_SHORT_SEG": "1", "BLP_HEAVY_WORK": "7"},
     {"BLP_GROUP_YN": "1"},                              # short-row batches grouped by y only: the scorer reads N(y)'s bounds
     {"BLP_GROUP_ROWS16": "1"},                          # the 16-byte-stage grouping write (k_item_write_runs)
+    {"BLP_GROUP_GATHER": "1"},                          # rows gathered by the grouping write, not carried by the scatter
     {"BLP_HOST_PLAN": "1"},                             # blp_batch_create's planning on the host mirror
     {"BLP_HOST_PLAN": "1", "BLP_SPLIT": "3", "BLP_SPLIT_BIG": "1", "BLP_HASH_WORK": "600"},
 ])
