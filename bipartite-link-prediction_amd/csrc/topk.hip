@@ -154,6 +154,7 @@ struct TkShared {
   long long red[TK_NT / 64];
   unsigned long long thr_key;
   int thr_col, have_thr, n, item;
+  int need[2];  // a selection round (by parity) left the buffer past TK_SEL - TK_NT: compact (sel_round_end)
   int nv[3];
   int nd;  // hot targets of this source handled by dense_pass
 };
@@ -598,6 +599,7 @@ __device__ __attribute__((always_inline)) void compact(const TkArgs& a, TkShared
   if (tid == 0) {
     const int keep = min(n, a.k);
     s.n = keep;
+    s.need[0] = s.need[1] = 0;
     if (keep == a.k) {
       s.thr_key = s.key[keep - 1];
       s.thr_col = s.col[keep - 1];
@@ -616,6 +618,7 @@ __device__ __attribute__((always_inline)) void sel_begin(const TkArgs& a, TkShar
   }
   if (threadIdx.x == 0) {
     s.n = nv;
+    s.need[0] = s.need[1] = 0;
     s.have_thr = nv == a.k;
     if (nv == a.k) {
       s.thr_key = a.keys[base + nv - 1];
@@ -637,21 +640,35 @@ __device__ __attribute__((always_inline)) void sel_end(const TkArgs& a, TkShared
   __syncthreads();
 }
 
-__device__ inline void sel_offer(TkShared& s, bool ok, unsigned long long key, int col) {
+// A round of offers, then ONE barrier (round 5; two before). The buffer passes TK_SEL - TK_NT in a
+// round exactly when one offer of that round takes slot TK_SEL - TK_NT (slots are consecutive), and
+// that offer raises the round's flag need[parity]. After the barrier every thread reads the flag of
+// ITS round: the next round's offers raise the other parity's flag, so a thread that runs ahead
+// into round r + 1 cannot change what a slow one reads for round r (reading s.n instead would need
+// a second barrier to stop exactly that). compact() clears both flags.
+__device__ inline void sel_offer(TkShared& s, bool ok, unsigned long long key, int col, int par) {
   if (ok && (!s.have_thr || better(key, col, s.thr_key, s.thr_col))) {
     const int slot = atomicAdd(&s.n, 1);
     if (TK_OK(slot < TK_SEL, 10, slot, TK_SEL)) {
       s.key[slot] = key;
       s.col[slot] = col;
     }
+    if (slot == TK_SEL - TK_NT) s.need[par] = 1;
   }
 }
 
-__device__ inline void sel_round_end(const TkArgs& a, TkShared& s) {
+#ifndef BLP_TK_ONEBAR
+#define BLP_TK_ONEBAR 1  // 0 (experiment builds): the two-barrier round end, for A/B
+#endif
+__device__ inline void sel_round_end(const TkArgs& a, TkShared& s, int par) {
   __syncthreads();
-  const int n = s.n;
-  __syncthreads();
-  if (n > TK_SEL - TK_NT) compact(a, s, n);
+  if (!BLP_TK_ONEBAR) {
+    const int n = s.n;
+    __syncthreads();
+    if (n > TK_SEL - TK_NT) compact(a, s, n);
+    return;
+  }
+  if (s.need[par]) compact(a, s, s.n);  // uniform: no offer runs until compact's own barriers are passed
 }
 
 // METHOD 0: CN key; 1: Jaccard key (fp64 bits); the counters of chunk c
@@ -687,8 +704,9 @@ __device__ __attribute__((always_inline)) long long sel_counts(const TkArgs& a, 
         col = inv_c;
       }
     }
-    sel_offer(s, ok, key, col);
-    sel_round_end(a, s);
+    const int par = (int)(((base - c.c0) / TK_NT) & 1);
+    sel_offer(s, ok, key, col, par);
+    sel_round_end(a, s, par);
     inv_c = inv_n;
     deg_c = deg_n;
     // Pruning: targets are in degree order (descending), and a target of degree d scores at
@@ -1020,8 +1038,9 @@ __global__ __launch_bounds__(TK_NT) void k_topk(TkArgs a) {
           for (int64_t base = 0; base < a.H; base += TK_NT) {
             const int64_t p = base + tid;
             const bool ok = p < a.H && acc_get(a, s.acc, c, addr_of(a, p)) > 0;
-            sel_offer(s, ok, ok ? aa_key(aah, p) : 0ull, ok ? a.inv[p] : 0);
-            sel_round_end(a, s);
+            const int par = (int)((base / TK_NT) & 1);
+            sel_offer(s, ok, ok ? aa_key(aah, p) : 0ull, ok ? a.inv[p] : 0, par);
+            sel_round_end(a, s, par);
           }
           sel_end(a, s, 2, it);
           if (tid == 0) atomicAdd(&a.counters[5], 1ull);
@@ -1100,8 +1119,9 @@ __global__ __launch_bounds__(TK_NT) void k_topk(TkArgs a) {
           for (int64_t base = d0; base < d1; base += TK_NT) {
             const int64_t p = base + tid;
             const unsigned long long v = p < d1 ? aa_key(acc64, p - d0) : 0ull;
-            sel_offer(s, v > 0, v, v > 0 ? a.inv[p] : 0);
-            sel_round_end(a, s);
+            const int par = (int)(((base - d0) / TK_NT) & 1);
+            sel_offer(s, v > 0, v, v > 0 ? a.inv[p] : 0, par);
+            sel_round_end(a, s, par);
           }
           sel_end(a, s, 2, it);
         }
