@@ -2617,11 +2617,19 @@ __global__ __launch_bounds__(BLOCK) void k_score_global(ScoreArgs a, uint32_t* g
 // count and exact AA words to the pair's accumulators in HBM (device-scope atomics; slices
 // without hits add nothing); |H2| partials go to [sources][chunks]; k_split_combine computes
 // the final values and Jaccard.
+// The split table rsplit[row][c] (int32 offsets into the row), and its 16-bit twin rsplit16 (or
+// null): the same offsets for rows shorter than 65535 ids, 0xFFFF in every entry of a longer row
+// (whose scans then read the int32 table). The twin is what the scorer reads: at config 5 the
+// 2M business rows x 49 offsets are 196 MB instead of 392 MB, within the 256 MB Infinity Cache.
+constexpr uint16_t SPLIT16_LONG = 0xFFFF;
+
 __global__ void k_row_splits(const int64_t* __restrict__ rp, const int32_t* __restrict__ ci, int64_t v0, int64_t n,
-                             int64_t lo, int64_t cap_bits, int C, int32_t* __restrict__ rsplit) {
+                             int64_t lo, int64_t cap_bits, int C, int32_t* __restrict__ rsplit,
+                             uint16_t* __restrict__ rsplit16) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t v = v0 + i;
     const int64_t b = rp[v], e = rp[v + 1];
+    const bool short16 = e - b < SPLIT16_LONG;
     for (int c = 0; c <= C; ++c) {
       const int64_t bound = c == C ? INT64_MAX : lo + c * cap_bits;
       int64_t l = b, h = e;
@@ -2630,8 +2638,28 @@ __global__ void k_row_splits(const int64_t* __restrict__ rp, const int32_t* __re
         if (ci[m] < bound) l = m + 1; else h = m;
       }
       rsplit[i * (C + 1) + c] = (int32_t)(l - b);
+      if (rsplit16) rsplit16[i * (C + 1) + c] = short16 ? (uint16_t)(l - b) : SPLIT16_LONG;
     }
   }
+}
+
+// Row offsets [s0, s1) of chunk c of split-table row `row`: the 16-bit table when present and the
+// row is short, else the int32 table.
+__device__ __attribute__((always_inline)) inline void split_bounds(const int32_t* __restrict__ rsplit,
+                                                                   const uint16_t* __restrict__ rsplit16, int64_t row,
+                                                                   int C, int c, int& s0, int& s1) {
+  if (rsplit16) {
+    const uint16_t* q = rsplit16 + row * (C + 1) + c;
+    const uint32_t a = q[0], b = q[1];
+    if (a != SPLIT16_LONG) {
+      s0 = (int)a;
+      s1 = (int)b;
+      return;
+    }
+  }
+  const int32_t* sp = rsplit + row * (C + 1) + c;
+  s0 = sp[0];
+  s1 = sp[1];
 }
 
 constexpr int SPLIT_CN_BITS = 24;  // k_score_split pk24: count field of the packed per-pair word
@@ -2640,7 +2668,8 @@ constexpr int SPLIT_LQ = 16 * SPLIT_ROUND * 64;  // long-slice queue entries per
 
 template <int BLOCK, int CAP_WORDS, int SEG, int K>
 __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_split(ScoreArgs a, const int32_t* __restrict__ g_y,
-                                                       const int32_t* __restrict__ rsplit, int64_t rs_lo, int C,
+                                                       const int32_t* __restrict__ rsplit,
+                                                       const uint16_t* __restrict__ rsplit16, int64_t rs_lo, int C,
                                                        uint32_t* __restrict__ pcn, unsigned long long* __restrict__ paa,
                                                        uint32_t* __restrict__ ph2, int64_t np, int pk24, int short_max) {
   constexpr int NW = BLOCK / 64;
@@ -2776,10 +2805,11 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
         if ((int)threadIdx.x < ns) {
           const int z = a.ci[k0 + threadIdx.x];
           if (PS_OK(a.misc, (int64_t)z - rs_lo >= 0 && (int64_t)z - rs_lo < a.rs_rows, 7, (int64_t)z - rs_lo, a.rs_rows)) {
-            const int32_t* sp = rsplit + ((int64_t)z - rs_lo) * (C + 1) + c;
-            s_start[threadIdx.x] = a.rp[z] + sp[0];
-            len = (nhot && a.hot_idx[z] >= 0) ? 0 : sp[1] - sp[0];  // dense rows were OR-ed in
-            if (!PS_OK(a.misc, sp[0] >= 0 && len >= 0 && s_start[threadIdx.x] + len <= a.nnz, 10,
+            int sp0, sp1;
+            split_bounds(rsplit, rsplit16, (int64_t)z - rs_lo, C, c, sp0, sp1);
+            s_start[threadIdx.x] = a.rp[z] + sp0;
+            len = (nhot && a.hot_idx[z] >= 0) ? 0 : sp1 - sp0;  // dense rows were OR-ed in
+            if (!PS_OK(a.misc, sp0 >= 0 && len >= 0 && s_start[threadIdx.x] + len <= a.nnz, 10,
                        s_start[threadIdx.x] + len, a.nnz))
               len = 0;
           } else {
@@ -2873,9 +2903,9 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
           const int gp = pbeg + q;
           const int64_t row = (int64_t)g_y[gp] - rs_lo;
           if (PS_OK(a.misc, row >= 0 && row < a.rs_rows, 7, row, a.rs_rows)) {
-            const int32_t* sp = rsplit + row * (C + 1) + c;
-            const int s0 = sp[0];
-            len = sp[1] - s0;
+            int s0, s1;
+            split_bounds(rsplit, rsplit16, row, C, c, s0, s1);
+            len = s1 - s0;
             st = a.g_yb[gp] + s0;
             if (!PS_OK(a.misc, s0 >= 0 && len >= 0 && st + len <= a.nnz, 10, st + len, a.nnz)) len = 0;
           }
@@ -3256,6 +3286,7 @@ struct Knobs {
   bool group_rows = true;        // BLP_GROUP_YN=1 clears it: short-row batches then group y only and the
                                  // scorer gathers N(y)'s bounds (k_item_write_ids<K, false>; measured slower)
   bool group_rows16 = false;     // BLP_GROUP_ROWS16: the 16-byte-stage grouping write (k_item_write_runs)
+  bool split32 = false;          // BLP_SPLIT32: the chunk-parallel scorer reads the int32 split table only
   bool group_gather = false;     // BLP_GROUP_GATHER: rows gathered by the write kernel, not carried by the scatter
   std::string debug_null;        // BLP_DEBUG_NULL (BLP_DEBUG builds only): null this launch pointer, to
                                  // show the pre-launch pointer check (launch_pointers) refusing it
@@ -3292,6 +3323,7 @@ Knobs read_knobs() {
   k.group_rows = !on("BLP_GROUP_YN");
   k.group_rows16 = on("BLP_GROUP_ROWS16");
   k.group_gather = on("BLP_GROUP_GATHER");
+  k.split32 = on("BLP_SPLIT32");
   k.host_plan = on("BLP_HOST_PLAN");
   k.short_seg = on("BLP_SHORT_SEG");
 #ifdef BLP_DEBUG
@@ -3334,6 +3366,7 @@ struct blp_batch {
   int64_t rs_rows = 0;   // its rows
   int32_t* d_gy = nullptr;     // grouped position -> y (split mode)
   int32_t* d_rsplit = nullptr; // [n][split + 1] row offsets where neighbour ids cross chunk boundaries
+  uint16_t* d_rsplit16 = nullptr;  // ... the same, 16-bit (0xFFFF: a long row, read d_rsplit; null: BLP_SPLIT32)
   int4* d_lq = nullptr;        // k_score_split's long-slice queues (SPLIT_LQ per resident workgroup)
   uint32_t* d_pcn = nullptr;   // [n_pairs] counts, summed over chunks (zeroed per score)
   unsigned long long* d_paa = nullptr;  // [n_pairs][2] exact AA words, summed over chunks
@@ -3943,8 +3976,10 @@ static int batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_
         hipMalloc(&b->d_lq, sizeof(int4) * SPLIT_LQ * (size_t)g->n_cu * 2) != hipSuccess)
       return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: split buffers"));
     // on the batch's stream: ordered before its scoring, no host wait
+    if (!kn.split32 && hipMalloc(&b->d_rsplit16, 2 * (size_t)nrows * (C + 1)) != hipSuccess)
+      return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: split buffers"));
     hipLaunchKernelGGL(k_row_splits, dim3(2048), dim3(256), 0, b->stream, g->d_rp, g->d_ci, rows_lo, nrows, b->lo,
-                       b->cap_bits, C, b->d_rsplit);
+                       b->cap_bits, C, b->d_rsplit, b->d_rsplit16);
     BLP_HIP_OR(hipGetLastError(), bail);
   }
   // ---- HBM bitmap slots: one per resident workgroup of k_score_global
@@ -4035,7 +4070,7 @@ int blp_batch_destroy(blp_batch* b) {
     if (!kept) (void)hipStreamDestroy(b->stream);
   }
   void* ps[] = {b->d_x,    b->d_y,    b->d_cn,   b->d_jac,  b->d_aa,          b->d_gout,        b->d_gyb,
-                b->d_gyl,  b->d_misc, b->d_heavy_slot, b->d_heavy_bm, b->d_heavy_items, b->d_gbm, b->d_gy, b->d_rsplit, b->d_pcn, b->d_paa, b->d_ph2, b->d_aa_part, b->d_rec, b->d_hflag, b->d_lq, b->d_active2};
+                b->d_gyl,  b->d_misc, b->d_heavy_slot, b->d_heavy_bm, b->d_heavy_items, b->d_gbm, b->d_gy, b->d_rsplit, b->d_rsplit16, b->d_pcn, b->d_paa, b->d_ph2, b->d_aa_part, b->d_rec, b->d_hflag, b->d_lq, b->d_active2};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   delete b;
@@ -4351,12 +4386,12 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
     if (b->split_big) {
       BLP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_score_split<S_BLOCK, S_CAP_BIG, S_SEG, 8>, S_BLOCK, 0));
       hipLaunchKernelGGL((k_score_split<S_BLOCK, S_CAP_BIG, S_SEG, 8>), dim3(scu * std::min(std::max(per_cu, 1), 2)), dim3(S_BLOCK),
-                         0, b->stream, a, b->d_gy, b->d_rsplit, b->rs_lo, b->split, b->d_pcn, b->d_paa, b->d_ph2, np, pk24,
+                         0, b->stream, a, b->d_gy, b->d_rsplit, b->d_rsplit16, b->rs_lo, b->split, b->d_pcn, b->d_paa, b->d_ph2, np, pk24,
                          short_max);
     } else {
       BLP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_score_split<S_BLOCK, S_CAP, S_SEG, 8>, S_BLOCK, 0));
       hipLaunchKernelGGL((k_score_split<S_BLOCK, S_CAP, S_SEG, 8>), dim3(scu * std::min(std::max(per_cu, 1), 2)), dim3(S_BLOCK), 0,
-                         b->stream, a, b->d_gy, b->d_rsplit, b->rs_lo, b->split, b->d_pcn, b->d_paa, b->d_ph2, np, pk24,
+                         b->stream, a, b->d_gy, b->d_rsplit, b->d_rsplit16, b->rs_lo, b->split, b->d_pcn, b->d_paa, b->d_ph2, np, pk24,
                          short_max);
     }
     BLP_HIP(hipGetLastError());
