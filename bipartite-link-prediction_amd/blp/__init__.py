@@ -5,11 +5,11 @@ This package binds it with ctypes and keeps the data contract of the reference's
 scripts; the reference-named modules (similarity, svd, random_walks, util, eval,
 dataset_maker) one directory up are the drop-in call surface.
 """
-from ._lib import ADAMIC, CN, JACCARD, BLPError, BLPUnavailable, device_count, device_sync, lib, version
+from ._lib import ADAMIC, CN, JACCARD, BLPError, BLPUnavailable, device_count, device_sync, lib, prewarm, version
 from .topk import TopK
 from .graph import DeviceGraph, HostGraph, LoadEdgeList, PairBatch, load_edge_list, parse_edge_list
 
 __all__ = [
     "ADAMIC", "CN", "JACCARD", "BLPError", "BLPUnavailable", "DeviceGraph", "HostGraph", "LoadEdgeList",
-    "PairBatch", "TopK", "device_count", "device_sync", "lib", "load_edge_list", "parse_edge_list", "version",
+    "PairBatch", "TopK", "device_count", "device_sync", "lib", "load_edge_list", "parse_edge_list", "prewarm", "version",
 ]

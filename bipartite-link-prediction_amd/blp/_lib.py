@@ -43,6 +43,7 @@ SIGNATURES = {
     "blp_version": [],
     "blp_device_count": [ctypes.POINTER(ctypes.c_int)],
     "blp_device_sync": [_I32],
+    "blp_stream_prewarm": [_I32, _I32],
     "blp_edges_parse": [ctypes.c_char_p, _I32, _I32, _P, _P, ctypes.POINTER(ctypes.c_int64)],
     "blp_csr_from_edges": [_I64, _I64, _P, _P, _P, _P, _P, ctypes.POINTER(ctypes.c_int64)],
     "blp_csr_from_edges_device": [_I32, _P, _P, _I64, _I64, _P, _P, _P, ctypes.POINTER(ctypes.c_int64)],
@@ -152,6 +153,13 @@ def device_count():
 
 def device_sync(device=0):
     check(lib().blp_device_sync(device))
+
+
+def prewarm(device=0, streams=4):
+    """Start the HIP runtime on `device` and fill the library's stream pool (blp_stream_prewarm):
+    run on a spare thread while inputs load, so neither lands on the critical path."""
+    check(lib().blp_device_sync(device))
+    check(lib().blp_stream_prewarm(device, streams))
 
 
 def version():

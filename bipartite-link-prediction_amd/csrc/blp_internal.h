@@ -154,10 +154,7 @@ struct blp_graph {
   unsigned long long* d_w2 = nullptr;
   int32_t *d_lo2 = nullptr, *d_hi2 = nullptr, *d_maxd = nullptr;
   uint8_t* d_flag2 = nullptr;
-  // batch streams returned by destroyed batches, handed to the next ones (blp_batch_create):
-  // a stream per batch keeps the passes of a step concurrent without a hipStreamCreate per batch
-  std::vector<hipStream_t> stream_pool;
-  std::mutex stream_mu;
+
   // wedge-row bitmaps (hop3.hip, blp::wedge_bitmaps): the SET of ids of each long wedge row over
   // an id range [lo, hi), built on first use per range (the hop-3 mark range; the business
   // batch's universe) and kept with the graph (at most 4 ranges)
@@ -191,6 +188,14 @@ int build_hot_index(blp_graph* g);
 int graph_finish(blp_graph* g, const double* aaw);
 int build_wedge_index(blp_graph* g);
 int build_node2(blp_graph* g);  // after build_hot_index (the dense-row flag)
+// Non-blocking streams kept across handles, per device. hipStreamCreate costs milliseconds (it
+// sets up a hardware queue); similarity.main would pay it for the parse, the CSR build, the graph
+// and each batch. stream_take returns a pooled stream of `device` (the current device) or a new
+// one (null on failure, the HIP error recorded); stream_give synchronizes it and pools it (a few
+// per device; the rest are destroyed). blp_stream_prewarm fills the pool ahead of time.
+hipStream_t stream_take(int device);
+void stream_give(int device, hipStream_t s);
+
 // The host column-id mirror, fetched from the device on first use when the graph was created
 // without one (blp_graph_create_from_csr with col_idx = NULL: similarity.main's path, whose
 // scoring plans on the device and never reads it). Null + error set on failure.

@@ -90,16 +90,15 @@ int blp::csr_build(int device, const int32_t* d_a, const int32_t* d_b, int64_t m
   BLP_CHECK(device >= 0 && device < ndev, BLP_E_ARG, "blp_csr_build_device: no such device");
   BLP_HIP(hipSetDevice(device));
   if (sync_device) BLP_HIP(hipDeviceSynchronize());
-  hipStream_t st = nullptr;
-  BLP_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  hipStream_t st = stream_take(device);  // pooled (blp_stream_prewarm)
+  if (!st) return BLP_E_HIP_BASE;
   blp_csr* c = new blp_csr();
   c->device = device;
   c->n = n;
   DevBuf keys, sorted, temp, flag, nsel;
   auto done = [&](int rc) {
     for (DevBuf* b : {&keys, &sorted, &temp, &flag, &nsel}) b->release();
-    (void)hipStreamSynchronize(st);
-    (void)hipStreamDestroy(st);
+    stream_give(device, st);  // synchronized first
     if (rc != BLP_OK) blp_csr_destroy(c);
     return rc;
   };

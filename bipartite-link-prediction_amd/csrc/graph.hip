@@ -259,7 +259,7 @@ int graph_finish(blp_graph* g, const double* aaw) {
   int n_cu = 0;  // one attribute, not hipGetDeviceProperties' full query (~5 ms)
   if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, g->device) == hipSuccess && n_cu > 0)
     g->n_cu = n_cu;
-  if (!g->stream) BLP_HIP(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
+  if (!g->stream && !(g->stream = stream_take(g->device))) return BLP_E_HIP_BASE;
   const int64_t n = g->n;
   g->max_row = 0;
   for (int64_t v = 0; v < n; ++v) g->max_row = std::max<int64_t>(g->max_row, g->hrp[v + 1] - g->hrp[v]);
@@ -287,6 +287,44 @@ int graph_finish(blp_graph* g, const double* aaw) {
 }  // namespace blp
 
 namespace blp {
+namespace {
+std::mutex g_stream_mu;
+std::vector<std::vector<hipStream_t>> g_stream_pool;  // [device]
+constexpr size_t STREAM_POOL_CAP = 16;
+}  // namespace
+
+hipStream_t stream_take(int device) {
+  {
+    std::lock_guard<std::mutex> lk(g_stream_mu);
+    if ((size_t)device < g_stream_pool.size() && !g_stream_pool[device].empty()) {
+      hipStream_t s = g_stream_pool[device].back();
+      g_stream_pool[device].pop_back();
+      return s;
+    }
+  }
+  hipStream_t s = nullptr;
+  const hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    hip_fail(e, "hipStreamCreateWithFlags", __FILE__, __LINE__);
+    return nullptr;
+  }
+  return s;
+}
+
+void stream_give(int device, hipStream_t s) {
+  if (!s) return;
+  (void)hipStreamSynchronize(s);
+  {
+    std::lock_guard<std::mutex> lk(g_stream_mu);
+    if ((size_t)device >= g_stream_pool.size()) g_stream_pool.resize((size_t)device + 1);
+    if (g_stream_pool[device].size() < STREAM_POOL_CAP) {
+      g_stream_pool[device].push_back(s);
+      return;
+    }
+  }
+  (void)hipStreamDestroy(s);
+}
+
 const int32_t* host_col_idx(blp_graph* g) {
   std::lock_guard<std::mutex> lk(g->mirror_mu);
   static const int32_t none = 0;  // an empty graph's mirror: nothing to read
@@ -319,6 +357,19 @@ const char* blp_version(void) { return "libblp 0.1 (gfx950)"; }
 int blp_device_count(int* n) {
   BLP_CHECK(n, BLP_E_ARG, "blp_device_count: null out");
   BLP_HIP(hipGetDeviceCount(n));
+  return BLP_OK;
+}
+
+int blp_stream_prewarm(int device, int n) {
+  BLP_CHECK(n >= 0 && n <= 16, BLP_E_ARG, "blp_stream_prewarm: 0 <= n <= 16");
+  BLP_HIP(hipSetDevice(device));
+  std::vector<hipStream_t> made;
+  for (int i = 0; i < n; ++i) {
+    hipStream_t s = nullptr;
+    BLP_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    made.push_back(s);
+  }
+  for (hipStream_t s : made) stream_give(device, s);
   return BLP_OK;
 }
 
@@ -422,14 +473,12 @@ int blp_graph_destroy(blp_graph* g) {
   free_hot_index(g);
   free_wedge_index(g);
   free_node2(g);
-  for (hipStream_t st : g->stream_pool) (void)hipStreamDestroy(st);
-  g->stream_pool.clear();
   if (g->d_rp) (void)hipFree(g->d_rp);
   if (g->d_ci) (void)hipFree(g->d_ci - CI_PAD);
   if (g->d_aaw_fx) (void)hipFree(g->d_aaw_fx);
   if (g->d_ci_w) (void)hipFree(g->d_ci_w - CI_PAD);
   if (g->d_wtab) (void)hipFree(g->d_wtab);
-  if (g->stream) (void)hipStreamDestroy(g->stream);
+  stream_give(g->device, g->stream);
   delete g;
   return BLP_OK;
 }

@@ -419,7 +419,7 @@ int device_load(const char* path, int device, blp_edges** out) {
     BLP_HIP(hipSetDevice(device));
     int n_cu = 256, cu_attr = 0;
     if (hipDeviceGetAttribute(&cu_attr, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cu_attr > 0) n_cu = cu_attr;
-    BLP_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    if (!(st = stream_take(device))) return BLP_E_HIP_BASE;
     const bool tail_nl = data[S - 1] == '\n';
     const int64_t T = S + (tail_nl ? 0 : 1);  // a missing final newline is supplied
     const int64_t nb = (T + NL_CHUNK - 1) / NL_CHUNK;
@@ -510,10 +510,7 @@ int device_load(const char* path, int device, blp_edges** out) {
     return BLP_OK;
   };
   const int rc = run();
-  if (st) {
-    (void)hipStreamSynchronize(st);  // nothing of this call left in flight before its buffers go
-    (void)hipStreamDestroy(st);
-  }
+  if (st) stream_give(device, st);  // synchronized: nothing of this call left in flight before its buffers go
   delete e;  // a handle abandoned on an error path
   munmap((void*)data, (size_t)S);
   return rc;

@@ -3548,14 +3548,7 @@ static int batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_
   };
   int rc = set_device(g);
   if (rc) return bail(rc);
-  {  // the batch's stream: one a destroyed batch returned to the graph, else a new one
-    std::lock_guard<std::mutex> lk(g->stream_mu);
-    if (!g->stream_pool.empty()) {
-      b->stream = g->stream_pool.back();
-      g->stream_pool.pop_back();
-    }
-  }
-  if (!b->stream) BLP_HIP_OR(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking), bail);
+  if (!(b->stream = stream_take(g->device))) return bail(BLP_E_HIP_BASE);  // pooled (blp_stream_prewarm)
   {  // the graph's own uploads complete before this stream reads them (an event, not a host wait)
     hipEvent_t ev;
     BLP_HIP_OR(hipEventCreateWithFlags(&ev, hipEventDisableTiming), bail);
@@ -4058,17 +4051,7 @@ int blp_batch_destroy(blp_batch* b) {
   b->off.release();
   b->active.release();
   b->scratch.release();
-  if (b->stream) {  // back to the graph's pool for the next batch (a few at most)
-    bool kept = false;
-    if (b->g) {
-      std::lock_guard<std::mutex> lk(b->g->stream_mu);
-      if (b->g->stream_pool.size() < 8) {
-        b->g->stream_pool.push_back(b->stream);
-        kept = true;
-      }
-    }
-    if (!kept) (void)hipStreamDestroy(b->stream);
-  }
+  if (b->stream) stream_give(b->g ? b->g->device : 0, b->stream);  // back to the pool for the next batch
   void* ps[] = {b->d_x,    b->d_y,    b->d_cn,   b->d_jac,  b->d_aa,          b->d_gout,        b->d_gyb,
                 b->d_gyl,  b->d_misc, b->d_heavy_slot, b->d_heavy_bm, b->d_heavy_items, b->d_gbm, b->d_gy, b->d_rsplit, b->d_rsplit16, b->d_pcn, b->d_paa, b->d_ph2, b->d_aa_part, b->d_rec, b->d_hflag, b->d_lq, b->d_active2};
   for (void* p : ps)

@@ -257,7 +257,7 @@ def main(example_file, graph_file, u_methods, u_outfiles, b_methods, b_outfiles,
     # the GIL); a third starts the HIP runtime, whose first call costs a few tenths of a second
     pool = ThreadPoolExecutor(2)
     fut_ex = pool.submit(load_examples)
-    pool.submit(blp.device_sync, 0)
+    pool.submit(blp.prewarm, 0, 4)  # the HIP runtime and the pooled streams (graph, parse, CSR, batches)
     ex = None
     try:
         print("Loading graph...")

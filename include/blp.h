@@ -52,6 +52,11 @@ const char* blp_last_error(void);
 const char* blp_version(void);
 int blp_device_count(int* n);
 int blp_device_sync(int device); /* hipDeviceSynchronize on `device` */
+/* blp_stream_prewarm: create n (<= 16) non-blocking streams of `device` into the library's
+ * stream pool, which the CSR build, the graph.txt parse, graph handles and pair batches draw
+ * from instead of creating their own (a stream costs milliseconds to create): call it on a
+ * spare thread while the inputs load (similarity.main does).                                  */
+int blp_stream_prewarm(int device, int n);
 
 /* ---------------------------------------------------------------- graph
  * Replaces snap.LoadEdgeList(snap.PUNGraph, graph_file, 0, 1) (similarity.py:16) and the
