@@ -49,6 +49,9 @@
 #define BLP_EXP_PHASE 0  // experiment builds only (LDS bank-conflict attribution of the large scorer):
                          // 1 = no pair scan, 2 = no H2 build (dense OR and sparse rows; the scan finds no hits)
 #endif
+#ifndef BLP_SEGOFF
+#define BLP_SEGOFF 0  // large scorer: element and chunk offsets of a segment batch in ONE scan (seg_offsets)
+#endif
 #ifndef BLP_PP
 #define BLP_PP 1  // ping-pong merge-path loops in k_score (0: the single-buffer mp_build / mp_scan)
 #endif
@@ -1767,6 +1770,25 @@ __device__ __attribute__((always_inline)) inline void load_row_segments(const in
   __syncthreads();
 }
 
+// load_row_segments for the row-chunk loops: element and chunk offsets together (seg_offsets: one
+// scan and two barriers, instead of the offset scan and rc_chunk_offsets' second one). Ends with a
+// barrier.
+template <int BLOCK, int K>
+__device__ __attribute__((always_inline)) inline void load_row_segments_rc(const int64_t* __restrict__ rp,
+                                                                           const int32_t* __restrict__ ci, int64_t k0,
+                                                                           int ns, int64_t* s_start, int32_t* s_off,
+                                                                           int32_t* s_coff, unsigned long long* red64,
+                                                                           const int32_t* __restrict__ skip) {
+  int len = 0;
+  if ((int)threadIdx.x < ns) {
+    const int z = ci[k0 + threadIdx.x];
+    const int64_t st = rp[z];
+    s_start[threadIdx.x] = st;
+    len = (skip && skip[z] >= 0) ? 0 : (int)(rp[z + 1] - st);  // dense rows were OR-ed in already
+  }
+  seg_offsets<BLOCK, K>(len, ns, s_off, s_coff, red64);
+}
+
 // ------------------------------------------------------------------ heavy-source pre-build
 struct HeavyItem {
   int32_t slot;
@@ -1986,6 +2008,7 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
   __shared__ uint32_t s_cn[PKO ? 1 : SEG];
   __shared__ unsigned long long s_aa[SAA ? 2 * SEG : 1];  // exact AA words, interleaved (aa_push)
   __shared__ unsigned long long red64[NW];
+  __shared__ unsigned long long red64s[RC && BLP_SEGOFF ? NW : 1];  // seg_offsets' own (the popcount's red64 is read late)
   __shared__ int red[NW];
   __shared__ int s_src[2];  // the claimed source, alternating slots (no barrier guards its rewrite)
   __shared__ int s_nhot;
@@ -2169,12 +2192,17 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
           } else
           for (int64_t k0 = xb; k0 < xe; k0 += SEG) {
             const int ns = (int)min<int64_t>(SEG, xe - k0);
-            load_row_segments<BLOCK>(a.rp, a.ci, k0, ns, s_start, s_off, red, nhot ? a.hot_idx : nullptr);
+            // the row-chunk build: its offsets in one scan (BLP_SEGOFF)
+            const bool seg1 = RC && BLP_SEGOFF && !(a.short_rows & 1);
+            if (seg1)
+              load_row_segments_rc<BLOCK, K>(a.rp, a.ci, k0, ns, s_start, s_off, s_coff, red64s, nhot ? a.hot_idx : nullptr);
+            else
+              load_row_segments<BLOCK>(a.rp, a.ci, k0, ns, s_start, s_off, red, nhot ? a.hot_idx : nullptr);
             if (SHORT || (a.short_rows & 1)) {
               row_build<BLOCK>(a.cw, a.idmask, s_start, s_off, ns, c0, width, bm, threadIdx.x);
             } else if constexpr (!SHORT) {
               if (RC) {
-                rc_chunk_offsets<BLOCK, K>(s_off, ns, s_coff, red);
+                if (!seg1) rc_chunk_offsets<BLOCK, K>(s_off, ns, s_coff, red);
                 const int shift = build_hint<BLOCK, HC>(s_coff, ns, BLOCK, s_hint);
                 if (BLP_EXP_PHASE != 2)
                   rc_build<BLOCK, K>(a.cw, a.idmask, s_start, s_off, s_coff, ns, c0, width, bm, CAP_WORDS, threadIdx.x,
@@ -2240,11 +2268,17 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
               s_aa[2 * threadIdx.x + 1] = 0;
             }
           }
-          int tot;
-          const int ex = block_exscan<BLOCK, false>(len, red, &tot);  // (the barrier below ends red's use)
-          if ((int)threadIdx.x < ns) s_off[threadIdx.x] = ex;
-          if (threadIdx.x == 0) s_off[ns] = tot;
-          __syncthreads();
+          // the row-chunk scan's element and chunk offsets in one scan (BLP_SEGOFF), else the offsets
+          const bool seg2 = RC && BLP_SEGOFF && !SHORT && !(a.short_rows & 2);
+          if (seg2) {
+            seg_offsets<BLOCK, K>(len, ns, s_off, s_coff, red64s);
+          } else {
+            int tot;
+            const int ex = block_exscan<BLOCK, false>(len, red, &tot);  // (the barrier below ends red's use)
+            if ((int)threadIdx.x < ns) s_off[threadIdx.x] = ex;
+            if (threadIdx.x == 0) s_off[ns] = tot;
+            __syncthreads();
+          }
           // the next segment's metadata, in flight during this segment's scan (BLP_PFN)
           have_pf = PF && !SHORT && BLP_PFN && nchunks == 1 && sb + SEG < pcnt;
           if (have_pf && (int)threadIdx.x < min(SEG, pcnt - sb - SEG)) {
@@ -2263,7 +2297,7 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
                                      s_aa, threadIdx.x);
           } else if constexpr (SHORT) {
           } else if (RC) {
-            rc_chunk_offsets<BLOCK, K>(s_off, ns, s_coff, red);
+            if (!seg2) rc_chunk_offsets<BLOCK, K>(s_off, ns, s_coff, red);
             const int shift = build_hint<BLOCK, HC>(s_coff, ns, BLOCK, s_hint);
             if (BLP_EXP_PHASE == 1) {
             } else if (want_a)
