@@ -159,6 +159,7 @@ struct blp_graph {
   // an id range [lo, hi), built on first use per range (the hop-3 mark range; the business
   // batch's universe) and kept with the graph (at most 4 ranges)
   std::vector<blp::WedgeBitmaps> wbm;
+  int wedge_users = 0;  // live batches whose plan reads the wedge index or its bitmaps (under wbm_mu)
   std::mutex wbm_mu;  // held across wedge_bitmaps' lookup-or-build (batches are created concurrently)
   // host mirrors used for launch planning (bitmap universe bounds) and the host-built indexes:
   // owned copies (blp_graph_create), or the caller's buffers (blp_graph_create_from_csr, which

@@ -3320,6 +3320,7 @@ struct Knobs {
   bool group_rows = true;        // BLP_GROUP_YN=1 clears it: short-row batches then group y only and the
                                  // scorer gathers N(y)'s bounds (k_item_write_ids<K, false>; measured slower)
   bool group_rows16 = false;     // BLP_GROUP_ROWS16: the 16-byte-stage grouping write (k_item_write_runs)
+  bool debug_oom = false;        // BLP_DEBUG_OOM (BLP_DEBUG builds): the first create fails out of memory
   bool split32 = false;          // BLP_SPLIT32: the chunk-parallel scorer reads the int32 split table only
   bool group_gather = false;     // BLP_GROUP_GATHER: rows gathered by the write kernel, not carried by the scatter
   std::string debug_null;        // BLP_DEBUG_NULL (BLP_DEBUG builds only): null this launch pointer, to
@@ -3362,6 +3363,7 @@ Knobs read_knobs() {
   k.short_seg = on("BLP_SHORT_SEG");
 #ifdef BLP_DEBUG
   if (const char* e = getenv("BLP_DEBUG_NULL")) k.debug_null = e;
+  k.debug_oom = on("BLP_DEBUG_OOM");
 #endif
   return k;
 }
@@ -3428,6 +3430,7 @@ struct blp_batch {
   int64_t n_hash = 0;          // such sources
   bool use_short = false;   // the short-row scorer takes this batch (decided once, at create)
   bool yn_grouped = false;  // short-row batch grouped by k_item_write_ids: the scorer reads g_yn = d_gy
+  bool wedge_user = false;  // its plan reads the graph's wedge index (counted in g->wedge_users)
   int64_t work_elems = 0;  // planned build + scan elements (co-scheduling estimate)
   Knobs kn;               // environment switches, read once at create
 };
@@ -3557,7 +3560,7 @@ extern "C" {
 // same pairs with x and y swapped whose device copies are taken (a device-to-device copy after the
 // twin's upload, on this batch's stream) instead of a second host-to-device upload.
 static int batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n_pairs, const blp_batch* twin,
-                        blp_batch** out) {
+                        blp_batch** out, bool retry = false) {
   BLP_CHECK(g && out && n_pairs >= 0 && (n_pairs == 0 || (x && y)), BLP_E_ARG, "blp_batch_create: bad arguments");
   BLP_CHECK(n_pairs < (int64_t(1) << 31) - 1, BLP_E_ARG, "blp_batch_create: at most 2^31-2 pairs per batch");
   const int64_t n = g->n;
@@ -4047,24 +4050,55 @@ static int batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_
       return bail(fail(BLP_E_HIP_BASE, "blp_batch_create: upload failed"));
   }
   stage("buffers");
+#ifdef BLP_DEBUG
+  if (kn.debug_oom && g->d_wp && !retry)  // test knob: this create runs out of memory once
+    return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create [BLP_DEBUG_OOM]: out of memory"));
+#endif
+  // the plan reads the wedge index (wedge rows, wedge slices of heavy sources, wedge-row bitmaps):
+  // counted, so an out-of-memory retry releases the index only when no live batch reads it
+  b->wedge_user = g->d_wp && !kn.no_wedge && (b->use_short || b->split || wedge_items || b->wbm_slot);
+  if (b->wedge_user) {
+    std::lock_guard<std::mutex> lk(g->wbm_mu);
+    ++g->wedge_users;
+  }
   *out = b;
   return BLP_OK;
 }
 
 extern "C" {
 
+// Out of HBM while creating a batch: the graph's wedge index (up to 35 % of the HBM that was free
+// at graph creation, wedge.hip) is an accelerator every scorer can do without, so it is released
+// -- when no live batch's plan reads it -- and the batch is planned again without it.
+static bool is_oom(int rc) { return rc == BLP_E_HIP_BASE - (int)hipErrorOutOfMemory; }
+
+static int create_or_release(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n, const blp_batch* twin,
+                             blp_batch** out) {
+  int rc = batch_create(g, x, y, n, twin, out);
+  if (!is_oom(rc) || !g || !g->d_wp) return rc;
+  {
+    std::lock_guard<std::mutex> lk(g->wbm_mu);
+    if (g->wedge_users > 0) return rc;  // a live batch reads it: the failure stands
+    (void)hipGetLastError();
+    (void)hipSetDevice(g->device);
+    (void)hipStreamSynchronize(g->stream);
+    free_wedge_index(g);
+  }
+  return batch_create(g, x, y, n, twin, out, true);
+}
+
 int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n_pairs, blp_batch** out) {
-  return batch_create(g, x, y, n_pairs, nullptr, out);
+  return create_or_release(g, x, y, n_pairs, nullptr, out);
 }
 
 int blp_batch_create_pair(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n_pairs, blp_batch** out_xy,
                           blp_batch** out_yx) {
   BLP_CHECK(out_xy && out_yx, BLP_E_ARG, "blp_batch_create_pair: null outputs");
   blp_batch* a = nullptr;
-  int rc = batch_create(g, x, y, n_pairs, nullptr, &a);
+  int rc = create_or_release(g, x, y, n_pairs, nullptr, &a);
   if (rc) return rc;
   blp_batch* b = nullptr;
-  rc = batch_create(g, y, x, n_pairs, a, &b);
+  rc = create_or_release(g, y, x, n_pairs, a, &b);
   if (rc) {
     blp_batch_destroy(a);
     return rc;
@@ -4086,6 +4120,10 @@ int blp_batch_destroy(blp_batch* b) {
   b->active.release();
   b->scratch.release();
   if (b->stream) stream_give(b->g ? b->g->device : 0, b->stream);  // back to the pool for the next batch
+  if (b->wedge_user && b->g) {
+    std::lock_guard<std::mutex> lk(b->g->wbm_mu);
+    --b->g->wedge_users;
+  }
   void* ps[] = {b->d_x,    b->d_y,    b->d_cn,   b->d_jac,  b->d_aa,          b->d_gout,        b->d_gyb,
                 b->d_gyl,  b->d_misc, b->d_heavy_slot, b->d_heavy_bm, b->d_heavy_items, b->d_gbm, b->d_gy, b->d_rsplit, b->d_rsplit16, b->d_pcn, b->d_paa, b->d_ph2, b->d_aa_part, b->d_rec, b->d_hflag, b->d_lq, b->d_active2};
   for (void* p : ps)

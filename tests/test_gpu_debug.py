@@ -41,6 +41,11 @@ for xs, ys in ((x, y), (y, x)):
         sys.exit(3)
     cn, jac, aa, _ = og.score_pairs(np.searchsorted(ids, G.node_ids[xs]), np.searchsorted(ids, G.node_ids[ys]), 7)
     assert np.array_equal(got["cn"], cn) and np.array_equal(got["jaccard"], jac) and np.array_equal(got["adamic"], aa)
+if mode == "oom":  # the create that ran out of memory released the wedge index and planned again
+    import ctypes
+    nv = ctypes.c_int64(0)
+    blp.lib().blp_graph_wedge(G.handle, ctypes.byref(nv), None, None)
+    assert nv.value == -1, nv.value
 print("OK", mode)
 '''
 
@@ -89,3 +94,11 @@ def test_null_launch_pointer_is_refused(gpu, field, extra):
     r = _run("null " + field, dict(extra, BLP_DEBUG_NULL=field))
     assert r.returncode == 3, (r.stdout[-2000:], r.stderr[-2000:])
     assert "null device pointer" in r.stdout, r.stdout[-2000:]
+
+
+def test_batch_oom_releases_wedge_index(gpu):
+    """A batch create that runs out of HBM (BLP_DEBUG_OOM, debug build: the first create fails as
+    hipMalloc would) releases the graph's wedge index -- no live batch reads it -- and plans the
+    batch again without it; both sides still score bit-exact against the oracle."""
+    r = _run("oom", {"BLP_DEBUG_OOM": "1"})
+    assert r.returncode == 0 and "OK oom" in r.stdout, (r.stdout[-2000:], r.stderr[-2000:])
