@@ -2652,9 +2652,10 @@ __global__ __launch_bounds__(BLOCK) void k_score_global(ScoreArgs a, uint32_t* g
 // without hits add nothing); |H2| partials go to [sources][chunks]; k_split_combine computes
 // the final values and Jaccard.
 // The split table rsplit[row][c] (int32 offsets into the row), and its 16-bit twin rsplit16 (or
-// null): the same offsets for rows shorter than 65535 ids, 0xFFFF in every entry of a longer row
-// (whose scans then read the int32 table). The twin is what the scorer reads: at config 5 the
-// 2M business rows x 49 offsets are 196 MB instead of 392 MB, within the 256 MB Infinity Cache.
+// null; BLP_SPLIT16): the same offsets for rows shorter than 65535 ids, 0xFFFF in every entry of a
+// longer row (whose scans then read the int32 table). At config 5 the 2M business rows x 49
+// offsets are 196 MB instead of 392 MB, within the 256 MB Infinity Cache -- yet the step measured
+// 514 ms against 482 with the int32 table alone (r05ab6), so the twin is off by default.
 constexpr uint16_t SPLIT16_LONG = 0xFFFF;
 
 __global__ void k_row_splits(const int64_t* __restrict__ rp, const int32_t* __restrict__ ci, int64_t v0, int64_t n,
@@ -3321,7 +3322,8 @@ struct Knobs {
                                  // scorer gathers N(y)'s bounds (k_item_write_ids<K, false>; measured slower)
   bool group_rows16 = false;     // BLP_GROUP_ROWS16: the 16-byte-stage grouping write (k_item_write_runs)
   bool debug_oom = false;        // BLP_DEBUG_OOM (BLP_DEBUG builds): the first create fails out of memory
-  bool split32 = false;          // BLP_SPLIT32: the chunk-parallel scorer reads the int32 split table only
+  bool split16 = false;          // BLP_SPLIT16: the chunk-parallel scorer reads a 16-bit split table (measured
+                                 // slower at config 5: 514 against 482 ms per step)
   bool group_gather = false;     // BLP_GROUP_GATHER: rows gathered by the write kernel, not carried by the scatter
   std::string debug_null;        // BLP_DEBUG_NULL (BLP_DEBUG builds only): null this launch pointer, to
                                  // show the pre-launch pointer check (launch_pointers) refusing it
@@ -3358,7 +3360,7 @@ Knobs read_knobs() {
   k.group_rows = !on("BLP_GROUP_YN");
   k.group_rows16 = on("BLP_GROUP_ROWS16");
   k.group_gather = on("BLP_GROUP_GATHER");
-  k.split32 = on("BLP_SPLIT32");
+  k.split16 = on("BLP_SPLIT16");
   k.host_plan = on("BLP_HOST_PLAN");
   k.short_seg = on("BLP_SHORT_SEG");
 #ifdef BLP_DEBUG
@@ -3402,7 +3404,7 @@ struct blp_batch {
   int64_t rs_rows = 0;   // its rows
   int32_t* d_gy = nullptr;     // grouped position -> y (split mode)
   int32_t* d_rsplit = nullptr; // [n][split + 1] row offsets where neighbour ids cross chunk boundaries
-  uint16_t* d_rsplit16 = nullptr;  // ... the same, 16-bit (0xFFFF: a long row, read d_rsplit; null: BLP_SPLIT32)
+  uint16_t* d_rsplit16 = nullptr;  // ... the same, 16-bit (0xFFFF: a long row, read d_rsplit; BLP_SPLIT16 only)
   int4* d_lq = nullptr;        // k_score_split's long-slice queues (SPLIT_LQ per resident workgroup)
   uint32_t* d_pcn = nullptr;   // [n_pairs] counts, summed over chunks (zeroed per score)
   unsigned long long* d_paa = nullptr;  // [n_pairs][2] exact AA words, summed over chunks
@@ -4006,7 +4008,7 @@ static int batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_
         hipMalloc(&b->d_lq, sizeof(int4) * SPLIT_LQ * (size_t)g->n_cu * 2) != hipSuccess)
       return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: split buffers"));
     // on the batch's stream: ordered before its scoring, no host wait
-    if (!kn.split32 && hipMalloc(&b->d_rsplit16, 2 * (size_t)nrows * (C + 1)) != hipSuccess)
+    if (kn.split16 && hipMalloc(&b->d_rsplit16, 2 * (size_t)nrows * (C + 1)) != hipSuccess)
       return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: split buffers"));
     hipLaunchKernelGGL(k_row_splits, dim3(2048), dim3(256), 0, b->stream, g->d_rp, g->d_ci, rows_lo, nrows, b->lo,
                        b->cap_bits, C, b->d_rsplit, b->d_rsplit16);

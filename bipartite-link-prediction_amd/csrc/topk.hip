@@ -640,7 +640,8 @@ __device__ __attribute__((always_inline)) void sel_end(const TkArgs& a, TkShared
   __syncthreads();
 }
 
-// A round of offers, then ONE barrier (round 5; two before). The buffer passes TK_SEL - TK_NT in a
+// A round of offers, then ONE barrier (round 5, BLP_TK_ONEBAR=1; measured no faster, so the default
+// keeps two). The buffer passes TK_SEL - TK_NT in a
 // round exactly when one offer of that round takes slot TK_SEL - TK_NT (slots are consecutive), and
 // that offer raises the round's flag need[parity]. After the barrier every thread reads the flag of
 // ITS round: the next round's offers raise the other parity's flag, so a thread that runs ahead
@@ -658,7 +659,7 @@ __device__ inline void sel_offer(TkShared& s, bool ok, unsigned long long key, i
 }
 
 #ifndef BLP_TK_ONEBAR
-#define BLP_TK_ONEBAR 1  // 0 (experiment builds): the two-barrier round end, for A/B
+#define BLP_TK_ONEBAR 0  // 1: one barrier per round (parity flags); measured 17.09 / 17.10 against 16.99 / 17.02 ms
 #endif
 __device__ inline void sel_round_end(const TkArgs& a, TkShared& s, int par) {
   __syncthreads();

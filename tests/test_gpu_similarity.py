@@ -150,7 +150,7 @@ def test_general_graph_exact_distance(gpu):
     {"BLP_SPLIT": "3", "BLP_SPLIT_BIG": "1", "BLP_HASH_WORK": "600"},  # hash-set scorer for light sources, split for the rest
     {"BLP_SPLIT": "2", "BLP_SPLIT_BIG": "1", "BLP_HASH_WORK": "100000"},  # every source on the hash-set scorer (knob clamped to HT - 1)
     {"BLP_SPLIT": "4", "BLP_HASH_WORK": "400"},          # ... beside the 64 KiB chunk scorer
-    {"BLP_SPLIT": "3", "BLP_SPLIT32": "1"},             # chunk-parallel scorer on the int32 split table only
+    {"BLP_SPLIT": "3", "BLP_SPLIT16": "1"},             # chunk-parallel scorer on the 16-bit split table
     {"BLP_SHORT_SEG": "1"},                             # short-row batches on the segment scorer (k_score SHORT)
     {"BLP_SHORT_SEG": "1", "BLP_HEAVY_WORK": "7"},
     {"BLP_GROUP_YN": "1"},                              # short-row batches grouped by y only: the scorer reads N(y)'s bounds
