@@ -412,7 +412,14 @@ int device_load(const char* path, int device, blp_edges** out) {
   hipStream_t st = nullptr;
   ScopedBuf txt, blk, blk_off, tmp, nl, a, b, stats, in0, in1, cnt, base, map, ids;
   blp_edges* e = nullptr;
+  // BLP_PARSE_MEM_CAP (test knob): device memory the parse may take, in bytes; past it a
+  // reservation fails as out of memory would, and the host parser takes the file
+  const char* cap_env = getenv("BLP_PARSE_MEM_CAP");
+  const int64_t mem_cap = cap_env ? atoll(cap_env) : -1;
+  const int64_t peak = S + 24 * (S / 8 + 1);  // the text plus ~24 B per line (a line is >= 4 bytes)
   auto run = [&]() -> int {
+    if (mem_cap >= 0 && peak > mem_cap)
+      return fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_edges_load_device [BLP_PARSE_MEM_CAP]: out of memory");
     int ndev = 0;
     BLP_HIP(hipGetDeviceCount(&ndev));
     BLP_CHECK(device >= 0 && device < ndev, BLP_E_ARG, "blp_edges_load_device: no such device");
@@ -509,10 +516,15 @@ int device_load(const char* path, int device, blp_edges** out) {
     e = nullptr;
     return BLP_OK;
   };
-  const int rc = run();
+  int rc = run();
   if (st) stream_give(device, st);  // synchronized: nothing of this call left in flight before its buffers go
   delete e;  // a handle abandoned on an error path
   munmap((void*)data, (size_t)S);
+  if (rc == BLP_E_HIP_BASE - (int)hipErrorOutOfMemory) {  // no room on the device: the host parser takes the file
+    (void)hipGetLastError();
+    *out = nullptr;
+    rc = BLP_OK;
+  }
   return rc;
 }
 

@@ -638,6 +638,21 @@ def test_device_parse_falls_back_to_host(gpu, tmp_path, case):
         assert d["info"][4] == 0
 
 
+def test_device_parse_out_of_memory_falls_back_to_host(gpu, tmp_path, monkeypatch):
+    """A device parse that cannot get its HBM (BLP_PARSE_MEM_CAP: the reservations fail as out
+    of memory) is not an error: the host parser takes the file, with the host loader's results
+    (similarity.py:16, blp_edges_load_device)."""
+    rng = np.random.default_rng(24)
+    a, c = _messy_edges(rng, 60000, 2500, 150000)
+    p = _graph_txt(tmp_path / "graph.txt", a, c, rng)
+    monkeypatch.setenv("BLP_PARSE_MEM_CAP", "4096")
+    d = _edges_load(p, device=gpu, csr_device=gpu)
+    monkeypatch.delenv("BLP_PARSE_MEM_CAP")
+    h = _edges_load(p, csr_device=gpu)
+    assert d["on"] == -1
+    _same_load(d, h)
+
+
 def test_load_edge_list_device_parse(gpu, tmp_path):
     """blp.load_edge_list (similarity.py:16's snap.LoadEdgeList) on a device-parsed file gives
     the graph DeviceGraph builds from the host-parsed ids: ids, CSR, weights and scores."""
