@@ -3924,8 +3924,12 @@ static int batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_
   const bool wedge_items = (b->short_rows & 1) && g->d_wp && !kn.no_wedge;
   if (b->chunks == 1 && span > 0 && !b->global && (!b->split || span <= variant_cap_bits(V_LARGE))) {
     const int64_t* rp = g->hrp;
-    const int32_t* ci = (!heavy_cand.empty() && !wedge_items) ? host_col_idx(g) : g->hci;  // CSR items only
-    if (!heavy_cand.empty() && !wedge_items && !ci) return bail(BLP_E_STATE);
+    // CSR items walk N(x) on the host: the column mirror only when some candidate IS heavy (its
+    // fetch is ~80 MB at config 2, where the user side's candidates stay below the bound)
+    bool csr_items = false;
+    for (const auto& hc : heavy_cand) csr_items |= !wedge_items && hc.second > 2 * item_work;
+    const int32_t* ci = csr_items ? host_col_idx(g) : g->hci;
+    if (csr_items && !ci) return bail(BLP_E_STATE);
     for (const auto& hc : heavy_cand) {
       if (hc.second <= 2 * item_work) continue;
       if (heavy_slot.empty()) heavy_slot.assign((size_t)n, -1);
