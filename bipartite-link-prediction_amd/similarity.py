@@ -146,12 +146,16 @@ def _score_both_ids(G, u_ids, v_ids, u_mask, b_mask, timings=None, text=False):
         blp.device_sync(G.device)  # the batches run on their own streams
         t3 = time.perf_counter()
         if text:
-            res = present, _fetch_text(ub, u_mask), _fetch_text(bb, b_mask)
+            ru = _fetch_text(ub, u_mask)
+            t4 = time.perf_counter()
+            res = present, ru, _fetch_text(bb, b_mask)
         else:
-            res = present, ub.fetch(u_mask), bb.fetch(b_mask)
+            ru = ub.fetch(u_mask)
+            t4 = time.perf_counter()
+            res = present, ru, bb.fetch(b_mask)
         if timings is not None:
             timings.update({"score_lookup": t1 - t0, "score_create": t2 - t1, "score_device": t3 - t2,
-                            "score_fetch": time.perf_counter() - t3})
+                            "score_fetch": time.perf_counter() - t3, "score_fetch_user": t4 - t3})
         return res
     finally:
         ub.close()
@@ -257,7 +261,10 @@ def main(example_file, graph_file, u_methods, u_outfiles, b_methods, b_outfiles,
     # the GIL); a third starts the HIP runtime, whose first call costs a few tenths of a second
     pool = ThreadPoolExecutor(2)
     fut_ex = pool.submit(load_examples)
-    pool.submit(blp.prewarm, 0, 4)  # the HIP runtime and the pooled streams (graph, parse, CSR, batches)
+    if os.environ.get("BLP_NO_PREWARM"):  # A/B knob: the HIP runtime only
+        pool.submit(blp.device_sync, 0)
+    else:
+        pool.submit(blp.prewarm, 0, 4)  # the HIP runtime and the pooled streams (graph, parse, CSR, batches)
     ex = None
     try:
         print("Loading graph...")
