@@ -19,15 +19,25 @@ void set_error(const std::string& msg);
 int fail(int code, const std::string& msg);
 int hip_fail(hipError_t e, const char* what, const char* file, int line);
 
+// BLP_SLOW_HIP_MS=t (profiling): every HIP call made through BLP_HIP / BLP_HIP_OR that takes
+// longer than t ms is reported on stderr (call, file:line, thread, start time); 0 / unset = off,
+// one relaxed load per call.
+int64_t slow_clock();  // ns since the first traced call, or 0 when tracing is off
+void slow_check(int64_t t0, const char* what, const char* file, int line);
+
 #define BLP_HIP(call)                                                         \
   do {                                                                        \
+    const int64_t _t0 = ::blp::slow_clock();                                  \
     hipError_t _e = (call);                                                   \
+    if (_t0) ::blp::slow_check(_t0, #call, __FILE__, __LINE__);               \
     if (_e != hipSuccess) return ::blp::hip_fail(_e, #call, __FILE__, __LINE__); \
   } while (0)
 
 #define BLP_HIP_OR(call, handler)                                              \
   do {                                                                          \
+    const int64_t _t0 = ::blp::slow_clock();                                    \
     hipError_t _e = (call);                                                     \
+    if (_t0) ::blp::slow_check(_t0, #call, __FILE__, __LINE__);                 \
     if (_e != hipSuccess) return handler(::blp::hip_fail(_e, #call, __FILE__, __LINE__)); \
   } while (0)
 

@@ -5,6 +5,7 @@
 // dense node ids, both directions stored, rows sorted ascending, int64 row offsets and
 // int32 column ids.
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstring>
 #include <mutex>
@@ -45,6 +46,40 @@ int hip_fail(hipError_t e, const char* what, const char* file, int line) {
   return BLP_E_HIP_BASE - (int)e;
 }
 
+namespace {
+std::atomic<int> g_slow_state{-1};  // -1 unread, 0 off, else the threshold in microseconds
+std::chrono::steady_clock::time_point g_slow_t0;
+std::mutex g_slow_mu;
+}  // namespace
+
+int64_t slow_clock() {
+  int st = g_slow_state.load(std::memory_order_relaxed);
+  if (st == 0) return 0;
+  if (st < 0) {
+    std::lock_guard<std::mutex> lk(g_slow_mu);
+    st = g_slow_state.load();
+    if (st < 0) {
+      const char* e = getenv("BLP_SLOW_HIP_MS");
+      const double ms = e ? atof(e) : 0.0;
+      g_slow_t0 = std::chrono::steady_clock::now();
+      st = ms > 0 ? std::max(1, (int)(ms * 1000)) : 0;
+      g_slow_state.store(st);
+    }
+    if (st == 0) return 0;
+  }
+  return std::max<int64_t>(1, std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() -
+                                                                                     g_slow_t0).count());
+}
+
+void slow_check(int64_t t0, const char* what, const char* file, int line) {
+  const int64_t t1 = slow_clock();
+  if (t1 && (t1 - t0) / 1000 >= g_slow_state.load(std::memory_order_relaxed)) {
+    const char* f = strrchr(file, '/');
+    fprintf(stderr, "[blp slow hip] %8.3f ms at t=%9.3f ms tid %zx %s:%d %s\n", (t1 - t0) * 1e-6, t0 * 1e-6,
+            (size_t)std::hash<std::thread::id>()(std::this_thread::get_id()) & 0xffff, f ? f + 1 : file, line, what);
+  }
+}
+
 int DevBuf::reserve(size_t want) {
   if (want <= bytes && p) return BLP_OK;
   if (p) {
@@ -59,7 +94,11 @@ int DevBuf::reserve(size_t want) {
 }
 
 void DevBuf::release() {
-  if (p) (void)hipFree(p);
+  if (p) {
+    const int64_t t0 = slow_clock();
+    (void)hipFree(p);
+    if (t0) slow_check(t0, "hipFree (DevBuf::release)", __FILE__, __LINE__);
+  }
   p = nullptr;
   bytes = 0;
 }
