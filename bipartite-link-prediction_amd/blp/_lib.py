@@ -44,6 +44,8 @@ SIGNATURES = {
     "blp_device_count": [ctypes.POINTER(ctypes.c_int)],
     "blp_device_sync": [_I32],
     "blp_stream_prewarm": [_I32, _I32],
+    "blp_host_alloc": [ctypes.c_size_t, _PP],
+    "blp_host_free": [_P, ctypes.c_size_t],
     "blp_edges_parse": [ctypes.c_char_p, _I32, _I32, _P, _P, ctypes.POINTER(ctypes.c_int64)],
     "blp_csr_from_edges": [_I64, _I64, _P, _P, _P, _P, _P, ctypes.POINTER(ctypes.c_int64)],
     "blp_csr_from_edges_device": [_I32, _P, _P, _I64, _I64, _P, _P, _P, ctypes.POINTER(ctypes.c_int64)],
@@ -160,6 +162,23 @@ def prewarm(device=0, streams=4):
     run on a spare thread while inputs load, so neither lands on the critical path."""
     check(lib().blp_device_sync(device))
     check(lib().blp_stream_prewarm(device, streams))
+
+
+def host_empty(shape, dtype):
+    """numpy.empty over blp_host_alloc: from 4 MiB on the memory is advised as transparent huge
+    pages, so filling a fresh result array (a device-to-host fetch) and releasing it take a fault
+    and an unmap per 2 MiB instead of per 4 KiB. Released with the last view of the array."""
+    import weakref
+
+    dt = np.dtype(dtype)
+    shape = (int(shape),) if np.isscalar(shape) else tuple(int(s) for s in shape)
+    nbytes = max(int(np.prod(shape, dtype=np.int64)) * dt.itemsize, 1)
+    p = ctypes.c_void_p()
+    check(lib().blp_host_alloc(nbytes, ctypes.byref(p)))
+    buf = (ctypes.c_uint8 * nbytes).from_address(p.value)
+    weakref.finalize(buf, lib().blp_host_free, ctypes.c_void_p(p.value), nbytes)
+    n = int(np.prod(shape, dtype=np.int64))
+    return np.frombuffer(buf, dtype=dt, count=n).reshape(shape)
 
 
 def version():

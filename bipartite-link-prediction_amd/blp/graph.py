@@ -552,16 +552,17 @@ class PairBatch:
         check(lib().blp_batch_stats_reset(self.handle))
 
     def fetch(self, mask=7):
-        cn = np.zeros(self.n, np.uint32)
-        jac = np.zeros(self.n, np.float64) if mask & _lib.JACCARD else None
-        aa = np.zeros(self.n, np.float64) if mask & _lib.ADAMIC else None
+        # every entry is written by the copy (huge-page host memory: _lib.host_empty)
+        cn = _lib.host_empty(self.n, np.uint32)
+        jac = _lib.host_empty(self.n, np.float64) if mask & _lib.JACCARD else None
+        aa = _lib.host_empty(self.n, np.float64) if mask & _lib.ADAMIC else None
         check(lib().blp_batch_fetch(self.graph.handle, self.handle, ptr(cn), ptr(jac), ptr(aa)))
         return {"cn": cn, "jaccard": jac, "adamic": aa}
 
     def fetch_repr(self, which, zero_int=False):
         """The Jaccard (which = JACCARD) or Adamic-Adar (ADAMIC) scores as json.dumps text,
         formatted on the device: uint8[n, 24], NUL-padded slots (blp_batch_fetch_repr)."""
-        out = np.empty((self.n, 24), np.uint8)
+        out = _lib.host_empty((self.n, 24), np.uint8)
         check(lib().blp_batch_fetch_repr(self.graph.handle, self.handle, which, int(bool(zero_int)), ptr(out)))
         return out
 

@@ -9,7 +9,7 @@ import ctypes
 import numpy as np
 
 from . import _lib
-from ._lib import check, lib, ptr
+from ._lib import check, host_empty, lib, ptr
 
 _P = ctypes.c_void_p
 _I64P = ctypes.POINTER(ctypes.c_int64)
@@ -32,8 +32,8 @@ class Examples:
         nu, npairs = ctypes.c_int64(0), ctypes.c_int64(0)
         check(lib().blp_examples_info(handle, ctypes.byref(nu), ctypes.byref(npairs)))
         self.n_users, self.n_pairs = nu.value, npairs.value
-        self.pair_user = np.empty(self.n_pairs, np.int64)
-        self.pair_business = np.empty(self.n_pairs, np.int64)
+        self.pair_user = host_empty(self.n_pairs, np.int64)
+        self.pair_business = host_empty(self.n_pairs, np.int64)
         self.user_off = np.empty(self.n_users + 1, np.int64)
         check(lib().blp_examples_ids(handle, ptr(self.pair_user), ptr(self.pair_business), ptr(self.user_off)))
 

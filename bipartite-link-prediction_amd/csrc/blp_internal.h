@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstring>
 #include <mutex>
+#include <new>
 #include <string>
 #include <vector>
 
@@ -231,6 +232,40 @@ int set_device(const blp_graph* g);
 // touch every page of a fresh host buffer (>= 8 MB) from up to 16 threads before a pageable
 // device-to-host copy into it (graph.hip)
 void prefault_host(void* p, size_t bytes);
+// Large host buffers (score files, examples, fetched scores): at >= 4 MiB an anonymous mapping,
+// 2 MiB aligned, advised as transparent huge pages (the GPU boxes run THP in madvise mode), so
+// first touch takes one fault per 2 MiB instead of per 4 KiB and the release is one munmap of a
+// few hundred pages. Smaller sizes (and BLP_NO_THP=1) use malloc. Null on failure.
+void* host_alloc(size_t bytes);
+void host_free(void* p, size_t bytes);
+// std allocator over host_alloc that leaves elements uninitialised on resize()
+template <class T>
+struct HostAlloc {
+  using value_type = T;
+  HostAlloc() = default;
+  template <class U>
+  HostAlloc(const HostAlloc<U>&) noexcept {}
+  T* allocate(size_t n) {
+    void* p = host_alloc(n * sizeof(T));
+    if (!p) throw std::bad_alloc();
+    return static_cast<T*>(p);
+  }
+  void deallocate(T* p, size_t n) noexcept { host_free(p, n * sizeof(T)); }
+  template <class U>
+  void construct(U* p) noexcept {
+    ::new ((void*)p) U;
+  }
+  template <class U, class... A>
+  void construct(U* p, A&&... a) {
+    ::new ((void*)p) U(std::forward<A>(a)...);
+  }
+  template <class U>
+  bool operator==(const HostAlloc<U>&) const noexcept { return true; }
+  template <class U>
+  bool operator!=(const HostAlloc<U>&) const noexcept { return false; }
+};
+template <class T>
+using HostVec = std::vector<T, HostAlloc<T>>;
 // the device CSR of m dense endpoint pairs already in HBM on `device` (csr.hip; blp_csr_build_device
 // with sync_device, which first waits for all work queued on the device)
 int csr_build(int device, const int32_t* d_a, const int32_t* d_b, int64_t m, int64_t n, blp_csr** out,

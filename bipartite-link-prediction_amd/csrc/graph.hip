@@ -12,6 +12,8 @@
 #include <thread>
 #include <unordered_map>
 
+#include <sys/mman.h>
+
 #include <chrono>
 
 #include "blp_internal.h"
@@ -122,6 +124,37 @@ void prefault_host(void* p, size_t bytes) {
       for (size_t o = bytes * t / nt / 4096 * 4096; o < bytes * (t + 1) / nt; o += 4096) q[o] = 0;
     });
   for (auto& x : th) x.join();
+}
+
+namespace {
+constexpr size_t HUGE_MIN = size_t(4) << 20, HUGE_PAGE = size_t(2) << 20;
+bool thp_on() {
+  static const bool on = !getenv("BLP_NO_THP");
+  return on;
+}
+}  // namespace
+
+void* host_alloc(size_t bytes) {
+  if (bytes < HUGE_MIN || !thp_on()) return malloc(std::max<size_t>(bytes, 1));
+  // over-map by one huge page, then trim to a 2 MiB aligned span (the kernel backs only aligned
+  // 2 MiB ranges with huge pages)
+  const size_t len = (bytes + HUGE_PAGE - 1) / HUGE_PAGE * HUGE_PAGE;
+  void* m = mmap(nullptr, len + HUGE_PAGE, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+  if (m == MAP_FAILED) return nullptr;
+  const uintptr_t b = (uintptr_t)m, a = (b + HUGE_PAGE - 1) / HUGE_PAGE * HUGE_PAGE;
+  if (a > b) munmap(m, a - b);
+  if (b + HUGE_PAGE > a) munmap((void*)(a + len), b + HUGE_PAGE - a);
+  madvise((void*)a, len, MADV_HUGEPAGE);
+  return (void*)a;
+}
+
+void host_free(void* p, size_t bytes) {
+  if (!p) return;
+  if (bytes < HUGE_MIN || !thp_on()) {
+    free(p);
+    return;
+  }
+  munmap(p, (bytes + HUGE_PAGE - 1) / HUGE_PAGE * HUGE_PAGE);
 }
 
 int timer_begin(KernelTimer& t, hipStream_t s, hipEvent_t* start) {
@@ -392,6 +425,18 @@ extern "C" {
 const char* blp_last_error(void) { return g_last_error.c_str(); }
 
 const char* blp_version(void) { return "libblp 0.1 (gfx950)"; }
+
+int blp_host_alloc(size_t bytes, void** out) {
+  BLP_CHECK(out, BLP_E_ARG, "blp_host_alloc: null out");
+  *out = host_alloc(bytes);
+  BLP_CHECK(*out, BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_host_alloc: out of host memory");
+  return BLP_OK;
+}
+
+int blp_host_free(void* p, size_t bytes) {
+  host_free(p, bytes);
+  return BLP_OK;
+}
 
 int blp_device_count(int* n) {
   BLP_CHECK(n, BLP_E_ARG, "blp_device_count: null out");

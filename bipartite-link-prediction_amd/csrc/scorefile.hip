@@ -30,30 +30,18 @@
 #include "blp_internal.h"
 
 namespace {
-// vector storage that resize() leaves uninitialised (every element is written right after)
 template <class T>
-struct NoInit : std::allocator<T> {
-  template <class U>
-  struct rebind {
-    using other = NoInit<U>;
-  };
-  NoInit() = default;
-  template <class U>
-  NoInit(const NoInit<U>&) noexcept {}
-  template <class U>
-  void construct(U* p) noexcept {
-    ::new ((void*)p) U;
-  }
-  template <class U, class... A>
-  void construct(U* p, A&&... a) {
-    ::new ((void*)p) U(std::forward<A>(a)...);
-  }
+using Vec = blp::HostVec<T>;  // uninitialised on resize(); huge pages from 4 MiB (blp_internal.h)
+
+struct HostFree {
+  size_t n = 0;
+  void operator()(char* p) const { blp::host_free(p, n); }
 };
-template <class T>
-using Vec = std::vector<T, NoInit<T>>;
+using HostBytes = std::unique_ptr<char[], HostFree>;
+HostBytes host_bytes(size_t n) { return HostBytes(static_cast<char*>(blp::host_alloc(n)), HostFree{n}); }
 
 struct Text {  // the file's bytes, read once (not zero-filled first)
-  std::unique_ptr<char[]> p;
+  HostBytes p;
   size_t n = 0;
   const char* data() const { return p.get(); }
   size_t size() const { return n; }
@@ -394,8 +382,13 @@ int blp_examples_parse(const char* path, blp_examples** out) {
   }
   auto* x = new blp_examples();
   const size_t n = (size_t)st.st_size;
-  x->text.p.reset(new char[std::max<size_t>(n, 1)]);
+  x->text.p = host_bytes(std::max<size_t>(n, 1));
   x->text.n = n;
+  if (!x->text.p) {
+    close(fd);
+    delete x;
+    return fail(BLP_E_ARG, "blp_examples_parse: out of host memory");
+  }
   // read in slices of >= 8 MiB on up to 16 threads (a 100 MB examples.json: ~4x one read())
   const size_t nt = std::max<size_t>(1, std::min<size_t>({16, std::thread::hardware_concurrency(), n >> 23}));
   std::vector<uint8_t> rok(nt, 0);
@@ -488,15 +481,19 @@ int blp_scores_write(const blp_examples* x, const char* path, int kind, const ui
   for (unsigned t = 1; t <= nt; ++t) cut[t] = std::max(cut[t], cut[t - 1]);
   // each slice formats into its own buffer, sized by a bound: per user its key + 8 bytes,
   // per pair its key + 6 + a value of at most 24 bytes (repr of a double; 10 digits of a u32)
-  std::vector<std::unique_ptr<char[]>> part(nt);
+  std::vector<HostBytes> part(nt);
   std::vector<int64_t> part_len(nt, 0);
   std::vector<uint8_t> nonempty(nt, 0);
   auto work = [&](unsigned t) {
     int64_t bound = 16;
     for (int64_t u = cut[t]; u < cut[t + 1]; ++u) bound += x->u_len[u] + 8;
     for (int64_t k = x->u_off[cut[t]]; k < x->u_off[cut[t + 1]]; ++k) bound += x->v_len[k] + 30;
-    part[t].reset(new char[(size_t)bound]);
+    part[t] = host_bytes((size_t)bound);
     char* const o0 = part[t].get();
+    if (!o0) {
+      part_len[t] = -1;  // reported after the join
+      return;
+    }
     char* o = o0;
     bool first_user = true;
     for (int64_t u = cut[t]; u < cut[t + 1]; ++u) {
@@ -547,6 +544,8 @@ int blp_scores_write(const blp_examples* x, const char* path, int kind, const ui
   for (unsigned t = 1; t < nt; ++t) th.emplace_back(work, t);
   work(0);
   for (auto& h : th) h.join();
+  BLP_CHECK(std::find(part_len.begin(), part_len.end(), int64_t(-1)) == part_len.end(), BLP_E_ARG,
+            "blp_scores_write: out of host memory");
   // "{" part ", " part ... "}": every slice written at its own offset, concurrently (one
   // sequential fwrite of ~200 MB per file at config 2 dominated the file phase)
   const int fd = open(path, O_WRONLY | O_CREAT | O_TRUNC, 0666);

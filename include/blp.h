@@ -57,6 +57,13 @@ int blp_device_sync(int device); /* hipDeviceSynchronize on `device` */
  * from instead of creating their own (a stream costs milliseconds to create): call it on a
  * spare thread while the inputs load (similarity.main does).                                  */
 int blp_stream_prewarm(int device, int n);
+/* blp_host_alloc / blp_host_free: host memory for large result arrays (fetched scores): from
+ * 4 MiB on, an anonymous mapping advised as transparent huge pages (first touch and release
+ * cost a fault / an unmap per 2 MiB, not per 4 KiB); malloc below that, or with BLP_NO_THP=1.
+ * blp_host_free takes the size given to blp_host_alloc. Not pinned: any host pointer works with
+ * the fetch entry points.                                                                   */
+int blp_host_alloc(size_t bytes, void** out);
+int blp_host_free(void* p, size_t bytes);
 
 /* ---------------------------------------------------------------- graph
  * Replaces snap.LoadEdgeList(snap.PUNGraph, graph_file, 0, 1) (similarity.py:16) and the
