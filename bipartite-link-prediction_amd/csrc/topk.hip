@@ -567,9 +567,37 @@ __device__ __attribute__((always_inline)) long long push_pass(const TkArgs& a, T
   return h2;
 }
 
+#ifdef BLP_PROF  // experiment builds only: per-phase clock sums of thread 0 (blp_topk_prof_read)
+__device__ unsigned long long g_tkprof[16];
+#define TKP_INIT                          \
+  unsigned long long tkp_t0 = clock64();  \
+  unsigned long long tkp_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#define TKP(i)                                 \
+  {                                            \
+    const unsigned long long t1_ = clock64();  \
+    tkp_acc[i] += t1_ - tkp_t0;                \
+    tkp_t0 = t1_;                              \
+  }
+#define TKP_FLUSH \
+  if (tid == 0)   \
+    for (int i_ = 0; i_ < 10; ++i_) atomicAdd(&g_tkprof[i_], tkp_acc[i_]);
+// selection rounds walked per method (g_tkprof[10 + METHOD]) and compactions ([12])
+#define TKP_ROUND(m) \
+  if (threadIdx.x == 0) atomicAdd(&g_tkprof[10 + (m)], 1ull);
+#define TKP_COMPACT \
+  if (threadIdx.x == 0) atomicAdd(&g_tkprof[12], 1ull);
+#else
+#define TKP_ROUND(m)
+#define TKP_COMPACT
+#define TKP_INIT
+#define TKP(i)
+#define TKP_FLUSH
+#endif
+
 // Sort s.key/s.col[0, TK_SEL) best-first (bitonic), keep min(n, k); update the threshold.
 __device__ __attribute__((always_inline)) void compact(const TkArgs& a, TkShared& s, int n) {
   const int tid = threadIdx.x;
+  TKP_COMPACT
   for (int i = n + tid; i < TK_SEL; i += TK_NT) {
     s.key[i] = 0;
     s.col[i] = 0x7FFFFFFF;
@@ -706,6 +734,7 @@ __device__ __attribute__((always_inline)) long long sel_counts(const TkArgs& a, 
       }
     }
     const int par = (int)(((base - c.c0) / TK_NT) & 1);
+    TKP_ROUND(METHOD)
     sel_offer(s, ok, key, col, par);
     sel_round_end(a, s, par);
     inv_c = inv_n;
@@ -728,25 +757,6 @@ __device__ __attribute__((always_inline)) long long sel_counts(const TkArgs& a, 
   return nc;
 }
 
-#ifdef BLP_PROF  // experiment builds only: per-phase clock sums of thread 0 (blp_topk_prof_read)
-__device__ unsigned long long g_tkprof[16];
-#define TKP_INIT                          \
-  unsigned long long tkp_t0 = clock64();  \
-  unsigned long long tkp_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#define TKP(i)                                 \
-  {                                            \
-    const unsigned long long t1_ = clock64();  \
-    tkp_acc[i] += t1_ - tkp_t0;                \
-    tkp_t0 = t1_;                              \
-  }
-#define TKP_FLUSH \
-  if (tid == 0)   \
-    for (int i_ = 0; i_ < 8; ++i_) atomicAdd(&g_tkprof[i_], tkp_acc[i_]);
-#else
-#define TKP_INIT
-#define TKP(i)
-#define TKP_FLUSH
-#endif
 
 // Dense counts of the hot prefix of N'(x) (single counter chunk, a0 = 0; header comment). h2 /
 // np / fix receive this thread's share of |H2(x)|, of sum_{w in H2(x)} |N(w)| and of the rows
@@ -1008,8 +1018,9 @@ __global__ __launch_bounds__(TK_NT) void k_topk(TkArgs a) {
       }
       __syncthreads();
       if (want_cn) ncand += sel_counts<0>(a, s, it, c, h2, true);
-      if (want_j) ncand += sel_counts<1>(a, s, it, c, h2, !want_cn);
       TKP(3)
+      if (want_j) ncand += sel_counts<1>(a, s, it, c, h2, !want_cn);
+      TKP(8)
     }
     ncand = block_sum(s, ncand);
     if (want_aa && ncand > 0) {

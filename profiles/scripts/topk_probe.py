@@ -1,7 +1,9 @@
 """Config-3 top-k phase clocks (experiment library built with -DBLP_PROF: BLP_LIB=...libblp_tkprof.so).
 Sums of thread 0's clock64 deltas over all workgroups, per phase of k_topk:
 0 dequeue/setup+filter, 1 counter zeroing, 2 count push (fused AA), 3 clear + CN/J selection,
-4 AA from the fused sums, 5 AA hash path, 6 AA direct path, 7 list padding."""
+4 AA from the fused sums, 5 AA hash path, 6 AA direct path, 7 list padding, 8 Jaccard selection
+(3 is then the clear + CN selection); then the selection rounds walked per method and the
+compactions (round 5)."""
 import ctypes
 import os
 import sys
@@ -28,6 +30,8 @@ blp.lib().blp_topk_prof_read(buf)
 T.run(20, mask)
 blp.device_sync(0)
 blp.lib().blp_topk_prof_read(buf)
-v = np.array(buf[:8], np.float64)
-names = ["setup", "zero", "push", "sel_cn_j", "aa_fused", "aa_hash", "aa_direct", "pad"]
+v = np.array(buf[:10], np.float64)
+names = ["setup", "zero", "push", "sel_cn", "aa_fused", "aa_hash", "aa_direct", "pad", "sel_j", "-"]
 print({n: "%.1f%%" % (100 * x / v.sum()) for n, x in zip(names, v)}, "info", T.info(), flush=True)
+print("rounds per source: CN %.1f, Jaccard %.1f; compactions per source %.2f" %
+      (buf[10] / len(src), buf[11] / len(src), buf[12] / len(src)), flush=True)
