@@ -6,6 +6,8 @@ set -o pipefail
 R=$GRAFT_REPO_ROOT
 cd $R || exit 1
 mkdir -p gpurun_out
+timeout -k 10 180 python profiles/scripts/r05_evict.py > gpurun_out/r05_evict.json || exit 1
+cat gpurun_out/r05_evict.json
 bash profiles/scripts/r05_thp_ab.sh || exit 1
 BLP_LIB=$R/bipartite-link-prediction_amd/blp/libblp_tkprof.so timeout -k 10 300 python profiles/scripts/topk_probe.py > gpurun_out/r05_topk_phases.txt 2>&1 || { tail gpurun_out/r05_topk_phases.txt; exit 1; }
 cat gpurun_out/r05_topk_phases.txt
