@@ -213,6 +213,16 @@ void stream_give(int device, hipStream_t s);
 // scoring plans on the device and never reads it). Null + error set on failure.
 const int32_t* host_col_idx(blp_graph* g);
 void free_node2(blp_graph* g);
+// per translation unit: load its GPU code object now (hipFuncGetAttributes on one of its kernels)
+int preload_ingest();
+int preload_csr();
+int preload_graph();
+int preload_hot();
+int preload_node2();
+int preload_wedge();
+int preload_pairs();
+int preload_hop3();
+int preload_repr();
 constexpr int REPR_SLOT_BYTES = 24;  // repr.h REPR_SLOT
 // repr(v) of n device doubles into 24-byte slots at d_out (repr.hip); enqueued on s
 int repr_launch(const double* d_v, int64_t n, bool zero_int, char* d_out, int n_cu, hipStream_t s);

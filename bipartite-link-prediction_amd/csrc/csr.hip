@@ -250,3 +250,12 @@ extern "C" int blp_csr_from_edges_device(int device, const int32_t* d_a, const i
   blp_csr_destroy(c);
   return rc;
 }
+
+// Loads this file's GPU code object (blp_stream_prewarm): the HIP runtime loads a translation
+// unit's code object on the first launch of any of its kernels, 10-30 ms on the caller's thread.
+namespace blp {
+int preload_csr() {
+  hipFuncAttributes fa;
+  return hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&k_edge_keys)) == hipSuccess ? 0 : -1;
+}
+}  // namespace blp

@@ -447,6 +447,12 @@ int blp_device_count(int* n) {
 int blp_stream_prewarm(int device, int n) {
   BLP_CHECK(n >= 0 && n <= 16, BLP_E_ARG, "blp_stream_prewarm: 0 <= n <= 16");
   BLP_HIP(hipSetDevice(device));
+  // the code objects of similarity.main's kernels, in the order it first launches them
+  // (BLP_NO_PRELOAD=1: A/B knob, each loads on its first launch instead)
+  if (!getenv("BLP_NO_PRELOAD"))
+    for (int (*f)() : {preload_ingest, preload_csr, preload_graph, preload_hot, preload_node2, preload_wedge,
+                       preload_pairs, preload_hop3, preload_repr})
+      if (f()) return fail(BLP_E_HIP_BASE, "blp_stream_prewarm: kernel code object load failed");
   std::vector<hipStream_t> made;
   for (int i = 0; i < n; ++i) {
     hipStream_t s = nullptr;
@@ -618,3 +624,12 @@ int blp_stats_get(blp_graph* g, int kernel, double* total_ms, int64_t* launches)
 }
 
 }  // extern "C"
+
+// Loads this file's GPU code object (blp_stream_prewarm): the HIP runtime loads a translation
+// unit's code object on the first launch of any of its kernels, 10-30 ms on the caller's thread.
+namespace blp {
+int preload_graph() {
+  hipFuncAttributes fa;
+  return hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&k_code_ids)) == hipSuccess ? 0 : -1;
+}
+}  // namespace blp

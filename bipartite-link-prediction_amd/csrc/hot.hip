@@ -114,3 +114,12 @@ void free_hot_index(blp_graph* g) {
 }
 
 }  // namespace blp
+
+// Loads this file's GPU code object (blp_stream_prewarm): the HIP runtime loads a translation
+// unit's code object on the first launch of any of its kernels, 10-30 ms on the caller's thread.
+namespace blp {
+int preload_hot() {
+  hipFuncAttributes fa;
+  return hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&k_hot_fill)) == hipSuccess ? 0 : -1;
+}
+}  // namespace blp

@@ -774,3 +774,12 @@ extern "C" int blp_ids_lookup(const int32_t* id_map, int64_t id_lo, int64_t id_s
   });
   return BLP_OK;
 }
+
+// Loads this file's GPU code object (blp_stream_prewarm): the HIP runtime loads a translation
+// unit's code object on the first launch of any of its kernels, 10-30 ms on the caller's thread.
+namespace blp {
+int preload_ingest() {
+  hipFuncAttributes fa;
+  return hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&k_nl_count)) == hipSuccess ? 0 : -1;
+}
+}  // namespace blp

@@ -163,3 +163,12 @@ void free_node2(blp_graph* g) {
 }
 
 }  // namespace blp
+
+// Loads this file's GPU code object (blp_stream_prewarm): the HIP runtime loads a translation
+// unit's code object on the first launch of any of its kernels, 10-30 ms on the caller's thread.
+namespace blp {
+int preload_node2() {
+  hipFuncAttributes fa;
+  return hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&k_node2)) == hipSuccess ? 0 : -1;
+}
+}  // namespace blp

@@ -4649,3 +4649,12 @@ int blp_score_pairs(blp_graph* g, int side, uint32_t mask, const int32_t* pu, co
 }
 
 }  // extern "C"
+
+// Loads this file's GPU code object (blp_stream_prewarm): the HIP runtime loads a translation
+// unit's code object on the first launch of any of its kernels, 10-30 ms on the caller's thread.
+namespace blp {
+int preload_pairs() {
+  hipFuncAttributes fa;
+  return hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&k_scan_sum)) == hipSuccess ? 0 : -1;
+}
+}  // namespace blp

@@ -71,3 +71,12 @@ int blp_repr_format_device(int device, const double* d_values, int64_t n, int ze
 }
 
 }  // extern "C"
+
+// Loads this file's GPU code object (blp_stream_prewarm): the HIP runtime loads a translation
+// unit's code object on the first launch of any of its kernels, 10-30 ms on the caller's thread.
+namespace blp {
+int preload_repr() {
+  hipFuncAttributes fa;
+  return hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&k_repr)) == hipSuccess ? 0 : -1;
+}
+}  // namespace blp

@@ -230,3 +230,11 @@ extern "C" int blp_graph_wedge(const blp_graph* g, int64_t* n_vecs, int64_t* wp,
   return BLP_OK;
 }
 
+// Loads this file's GPU code object (blp_stream_prewarm): the HIP runtime loads a translation
+// unit's code object on the first launch of any of its kernels, 10-30 ms on the caller's thread.
+namespace blp {
+int preload_wedge() {
+  hipFuncAttributes fa;
+  return hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&k_wedge_fill)) == hipSuccess ? 0 : -1;
+}
+}  // namespace blp
