@@ -55,6 +55,8 @@ constexpr int TK_SEG = 256;           // N(x) entries staged per batch
 constexpr int TK_FILT = 128;          // words of the N'(x) membership filter (4096 bits)
 constexpr int TK_ACC_WORDS = 32768;   // counter space: 128 KiB
 constexpr int TK_KMAX = 256;
+constexpr int TK_WB = TK_SEL / (TK_NT / 64);  // sel_counts_wave: selection entries per wave (128)
+constexpr int TK_WK = 64;                     // ... for lists of at most 64 (one per lane after a sort)
 #ifndef BLP_TK_RB
 #define BLP_TK_RB 8
 #endif
@@ -118,6 +120,7 @@ struct TkArgs {
                                     // hash / direct AA passes; or null: those passes walk every target)
   int dw_n, dw_max;                 // hot targets; at most dw_max of them per source
   int64_t dw_words, dw_bmw, slo;
+  int wavesel;  // CN / Jaccard selection per wave (sel_counts_wave; k <= TK_WK), else block rounds
 };
 
 // BLP_DEBUG builds (make debug -> libblp_debug.so): every LDS index and every row read of the
@@ -157,6 +160,8 @@ struct TkShared {
   int need[2];  // a selection round (by parity) left the buffer past TK_SEL - TK_NT: compact (sel_round_end)
   int nv[3];
   int nd;  // hot targets of this source handled by dense_pass
+  unsigned long long sthr;  // sel_counts_wave: the best of the waves' k-th keys (a shared pruning bound)
+  int wcnt[TK_NT / 64];     // sel_counts_wave: entries each wave hands to the final merge
 };
 
 __device__ inline uint32_t filt_bit(int32_t e) { return ((uint32_t)e * 2654435761u) >> 20; }
@@ -586,9 +591,13 @@ __device__ unsigned long long g_tkprof[16];
   if (threadIdx.x == 0) atomicAdd(&g_tkprof[10 + (m)], 1ull);
 #define TKP_COMPACT \
   if (threadIdx.x == 0) atomicAdd(&g_tkprof[12], 1ull);
+// sel_counts_wave: 64-target blocks walked, per method, over all waves ([13 + METHOD])
+#define TKP_WROUND(m) \
+  if ((threadIdx.x & 63) == 0) atomicAdd(&g_tkprof[13 + (m)], 1ull);
 #else
 #define TKP_ROUND(m)
 #define TKP_COMPACT
+#define TKP_WROUND(m)
 #define TKP_INIT
 #define TKP(i)
 #define TKP_FLUSH
@@ -756,6 +765,166 @@ __device__ __attribute__((always_inline)) long long sel_counts(const TkArgs& a, 
   sel_end(a, s, METHOD, it);
   return nc;
 }
+
+// ---- per-wave selection (round 5, BLP_TK_WAVESEL): each wave walks its own blocks of 64 targets
+// (wave w takes blocks w, w + 16, ... of the degree order) with NO block barrier: offers are
+// appended to the wave's 128-entry region of s.key / s.col by ballot, and when it passes 64 the
+// wave sorts its region in registers (two entries per lane, bitonic over lane shuffles) and keeps
+// the best k. A wave stops when the degree bound of its next block falls below max(its own k-th
+// key, s.sthr), s.sthr being the best of every wave's k-th key (each wave's k-th best is a lower
+// bound of the list's: the list's k-th is the best k-th over any k candidates). At the end the
+// waves' lists (<= k each) are packed and sel_end merges them.
+__device__ inline void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// sort the wave's region [0, n) (n <= TK_WB) best-first; lane i ends holding entry i in (ka, ca)
+// (entries past n are padding: key 0, col INT_MAX)
+__device__ __attribute__((always_inline)) void wave_sort(const unsigned long long* wk, const int32_t* wc, int n,
+                                                         unsigned long long& ka, int& ca) {
+  const int lane = threadIdx.x & 63;
+  ka = lane < n ? wk[lane] : 0ull;
+  ca = lane < n ? wc[lane] : 0x7FFFFFFF;
+  unsigned long long kb = lane + 64 < n ? wk[lane + 64] : 0ull;
+  int cb = lane + 64 < n ? wc[lane + 64] : 0x7FFFFFFF;
+#pragma unroll
+  for (int size = 2; size <= TK_WB; size <<= 1) {
+#pragma unroll
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      if (stride == 64) {  // the two entries of this lane: indexes lane (lower) and lane + 64
+        const bool desc = true;  // size == TK_WB
+        const bool sw = desc ? better(kb, cb, ka, ca) : better(ka, ca, kb, cb);
+        if (sw) {
+          const unsigned long long tk = ka;
+          const int tc = ca;
+          ka = kb, ca = cb, kb = tk, cb = tc;
+        }
+        continue;
+      }
+      const unsigned long long oka = __shfl_xor(ka, stride, 64), okb = __shfl_xor(kb, stride, 64);
+      const int oca = __shfl_xor(ca, stride, 64), ocb = __shfl_xor(cb, stride, 64);
+      const bool lower = (lane & stride) == 0;
+      // entry A has index lane, entry B index lane + 64; the pair's lower index decides the direction
+      const bool desc_a = ((((lane & ~stride)) & size) == 0) || size == TK_WB;
+      const bool desc_b = ((((lane + 64) & ~stride) & size) == 0) || size == TK_WB;
+      // the lower entry of a descending pair keeps the better one
+      const bool keep_better_a = lower == desc_a, keep_better_b = lower == desc_b;
+      const bool a_better = better(ka, ca, oka, oca), b_better = better(kb, cb, okb, ocb);
+      if (keep_better_a != a_better) ka = oka, ca = oca;
+      if (keep_better_b != b_better) kb = okb, cb = ocb;
+    }
+  }
+}
+
+// METHOD 0: CN key; 1: Jaccard key; the same list as sel_counts for k <= TK_WK
+template <int METHOD>
+__device__ __attribute__((always_inline)) long long sel_counts_wave(const TkArgs& a, TkShared& s, int it, const TkChunk& c,
+                                                                    long long h2, bool count) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  constexpr int NWV = TK_NT / 64;
+  unsigned long long* wk = s.key + w * TK_WB;
+  int32_t* wc = s.col + w * TK_WB;
+  const int k = a.k;
+  const int nv = s.nv[METHOD];
+  const size_t gbase = ((size_t)METHOD * a.n_src + it) * a.k;
+  if (tid == 0) s.sthr = 0;
+  // wave 0 starts from the list of the earlier chunks (best-first, nv <= k <= 64 entries)
+  int n = w == 0 ? nv : 0;
+  if (w == 0 && lane < nv) {
+    wk[lane] = a.keys[gbase + lane];
+    wc[lane] = a.cols[gbase + lane];
+  }
+  bool have = w == 0 && nv == k;
+  unsigned long long tkey = have ? a.keys[gbase + k - 1] : 0ull;
+  int tcol = have ? a.cols[gbase + k - 1] : 0;
+  __syncthreads();  // s.sthr reset, the old list in place, s.nv read by all
+  if (have) atomicMax(&s.sthr, tkey);
+  long long nc = 0;
+  if (count)
+    for (int64_t q = c.c0 + tid; q < c.c1; q += TK_NT) nc += acc_get(a, s.acc, c, addr_of(a, q)) > 0;
+  for (int64_t base = c.c0 + (int64_t)w * 64; base < c.c1; base += (int64_t)NWV * 64) {
+    // prune: the block's first target has its largest degree
+    const unsigned long long sthr = s.sthr;
+    const unsigned long long thr = have && tkey > sthr ? tkey : sthr;
+    if (thr > 0) {
+      const long long d = a.tdeg[base];
+      const bool stop = METHOD == 0 ? (unsigned long long)d < thr
+                                    : h2 > 0 && d <= h2 && (unsigned long long)__double_as_longlong((double)d / (double)h2) < thr;
+      if (stop) break;  // uniform in the wave
+    }
+    TKP_WROUND(METHOD)
+    const int64_t p = base + lane;
+    bool ok = false;
+    unsigned long long key = 0;
+    int col = 0;
+    if (p < c.c1) {
+      const uint32_t cnt = acc_get(a, s.acc, c, addr_of(a, p));
+      if (cnt > 0) {
+        if (METHOD == 0) {
+          key = cnt;
+        } else {
+          const double jac = (double)cnt / (double)(h2 + (long long)a.tdeg[p] - (long long)cnt);
+          key = (unsigned long long)__double_as_longlong(jac);
+        }
+        col = a.inv[p];
+        ok = key >= sthr && (!have || better(key, col, tkey, tcol));
+      }
+    }
+    if (n > TK_WB - 64) {  // room for a full block of offers: keep the best k first
+      wave_sync();
+      unsigned long long ka;
+      int ca;
+      wave_sort(wk, wc, n, ka, ca);
+      n = min(n, k);
+      wave_sync();
+      if (lane < n) {
+        wk[lane] = ka;
+        wc[lane] = ca;
+      }
+      if (n == k) {
+        tkey = __shfl(ka, k - 1, 64);
+        tcol = __shfl(ca, k - 1, 64);
+        have = true;
+        if (lane == 0) atomicMax(&s.sthr, tkey);
+        ok = ok && better(key, col, tkey, tcol);
+      }
+    }
+    const unsigned long long bal = __ballot(ok);
+    if (ok) {
+      const int slot = n + (int)__popcll(bal & ((1ull << lane) - 1ull));
+      if (TK_OK(slot < TK_WB, 10, slot, TK_WB)) {
+        wk[slot] = key;
+        wc[slot] = col;
+      }
+    }
+    n += (int)__popcll(bal);
+  }
+  // each wave's best k, packed in wave order, then one merge (sel_end)
+  wave_sync();
+  unsigned long long ka;
+  int ca;
+  wave_sort(wk, wc, n, ka, ca);
+  const int m = min(n, k);
+  if (lane == 0) s.wcnt[w] = m;
+  __syncthreads();  // every wave holds its entries in registers before any region is overwritten
+  int off = 0;
+  for (int v = 0; v < w; ++v) off += s.wcnt[v];
+  if (lane < m && TK_OK(off + lane < TK_SEL, 10, off + lane, TK_SEL)) {
+    s.key[off + lane] = ka;
+    s.col[off + lane] = ca;
+  }
+  if (tid == 0) {
+    int tot = 0;
+    for (int v = 0; v < NWV; ++v) tot += s.wcnt[v];
+    s.n = tot;
+  }
+  __syncthreads();
+  sel_end(a, s, METHOD, it);
+  return nc;
+}
+
 
 
 // Dense counts of the hot prefix of N'(x) (single counter chunk, a0 = 0; header comment). h2 /
@@ -1017,9 +1186,11 @@ __global__ __launch_bounds__(TK_NT) void k_topk(TkArgs a) {
         if (e >= c.a0 && e < c.a1) acc_clear(a, s.acc, c, e);
       }
       __syncthreads();
-      if (want_cn) ncand += sel_counts<0>(a, s, it, c, h2, true);
+      const bool wsel = a.wavesel && a.k <= TK_WK;
+      if (want_cn) ncand += wsel ? sel_counts_wave<0>(a, s, it, c, h2, true) : sel_counts<0>(a, s, it, c, h2, true);
       TKP(3)
-      if (want_j) ncand += sel_counts<1>(a, s, it, c, h2, !want_cn);
+      if (want_j)
+        ncand += wsel ? sel_counts_wave<1>(a, s, it, c, h2, !want_cn) : sel_counts<1>(a, s, it, c, h2, !want_cn);
       TKP(8)
     }
     ncand = block_sum(s, ncand);
@@ -1291,6 +1462,7 @@ static TkArgs topk_args(blp_topk* t, int k, uint32_t mask) {
   a.dw_words = t->dw_words;
   a.dw_bmw = t->dw_bmw;
   a.slo = t->slo;
+  a.wavesel = (int)env_i64("BLP_TK_WAVESEL", 0);
   return a;
 }
 

@@ -9,6 +9,18 @@ mkdir -p gpurun_out
 timeout -k 10 180 python profiles/scripts/r05_evict.py > gpurun_out/r05_evict.json || exit 1
 cat gpurun_out/r05_evict.json
 bash profiles/scripts/r05_thp_ab.sh || exit 1
-BLP_LIB=$R/bipartite-link-prediction_amd/blp/libblp_tkprof.so timeout -k 10 300 python profiles/scripts/topk_probe.py > gpurun_out/r05_topk_phases.txt 2>&1 || { tail gpurun_out/r05_topk_phases.txt; exit 1; }
+BLP_LIB=$R/bipartite-link-prediction_amd/blp/libblp_debug.so timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_topk.py -k "wavesel or pruning" > gpurun_out/r05_topk_tests_debug.log 2>&1 || { tail -30 gpurun_out/r05_topk_tests_debug.log; exit 1; }
+tail -3 gpurun_out/r05_topk_tests_debug.log
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_topk.py > gpurun_out/r05_topk_tests.log 2>&1 || { tail -30 gpurun_out/r05_topk_tests.log; exit 1; }
+tail -3 gpurun_out/r05_topk_tests.log
+for w in 0 1; do
+  BLP_TK_WAVESEL=$w BLP_LIB=$R/bipartite-link-prediction_amd/blp/libblp_tkprof.so timeout -k 10 300 python profiles/scripts/topk_probe.py >> gpurun_out/r05_topk_phases.txt 2>&1 || { tail gpurun_out/r05_topk_phases.txt; exit 1; }
+done
 cat gpurun_out/r05_topk_phases.txt
+for i in 1 2; do
+  for w in 0 1; do
+    BLP_TK_WAVESEL=$w timeout -k 10 300 python bench.py --mode topk --steps 10 > gpurun_out/r05tk_w${w}_$i.json 2> gpurun_out/r05tk_w${w}_$i.err || { tail gpurun_out/r05tk_w${w}_$i.err; exit 1; }
+    python -c "import json;d=json.loads(open('gpurun_out/r05tk_w${w}_$i.json').read().strip().splitlines()[-1]);print('wavesel $w', d['ms_per_step'], d.get('parity'))"
+  done
+done
 bash profiles/scripts/r05_profB.sh

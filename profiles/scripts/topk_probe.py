@@ -33,5 +33,7 @@ blp.lib().blp_topk_prof_read(buf)
 v = np.array(buf[:10], np.float64)
 names = ["setup", "zero", "push", "sel_cn", "aa_fused", "aa_hash", "aa_direct", "pad", "sel_j", "-"]
 print({n: "%.1f%%" % (100 * x / v.sum()) for n, x in zip(names, v)}, "info", T.info(), flush=True)
-print("rounds per source: CN %.1f, Jaccard %.1f; compactions per source %.2f" %
-      (buf[10] / len(src), buf[11] / len(src), buf[12] / len(src)), flush=True)
+print("wavesel=%s rounds per source: CN %.1f, Jaccard %.1f; compactions per source %.2f; per-wave 64-target "
+      "blocks per source: CN %.1f, Jaccard %.1f" % (os.environ.get("BLP_TK_WAVESEL", "0"), buf[10] / len(src),
+                                                    buf[11] / len(src), buf[12] / len(src), buf[13] / len(src),
+                                                    buf[14] / len(src)), flush=True)

@@ -160,6 +160,19 @@ def test_config3_topk_at_size(gpu, c2_graph):
         np.testing.assert_array_equal(sa[i], aa[s:e][o])
     pair = G.score_pairs(np.repeat(src, 20).astype(np.int32), ca.reshape(-1).astype(np.int32), 7)["adamic"]
     np.testing.assert_array_equal(pair, sa.reshape(-1))
+    # the per-wave CN / Jaccard selection (BLP_TK_WAVESEL) gives the same lists at size
+    import os
+
+    os.environ["BLP_TK_WAVESEL"] = "1"
+    try:
+        T.run(20, blp.JACCARD | blp.ADAMIC)
+        for m, (c0, s0) in (("jaccard", (cj, sj)), ("adamic_adar", (ca, sa))):
+            c1, s1, n1 = T.fetch(m)
+            np.testing.assert_array_equal(c1, c0)
+            np.testing.assert_array_equal(s1, s0)
+            np.testing.assert_array_equal(n1, ncand)
+    finally:
+        del os.environ["BLP_TK_WAVESEL"]
     T.close()
 
 

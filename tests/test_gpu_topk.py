@@ -54,11 +54,14 @@ def small(gpu):
     return G, adj_of(a, b), rng
 
 
+@pytest.mark.parametrize("wavesel", ["0", "1"])
 @pytest.mark.parametrize("expand", ["1", "0"])
-def test_topk_all_methods_match_oracle(small, monkeypatch, expand):
-    """Both row layouts: expanded wedge rows (default) and the rp[w] -> N(w) walk."""
+def test_topk_all_methods_match_oracle(small, monkeypatch, expand, wavesel):
+    """Both row layouts: expanded wedge rows (default) and the rp[w] -> N(w) walk; block-round
+    and per-wave CN / Jaccard selection (BLP_TK_WAVESEL)."""
     G, adj, rng = small
     monkeypatch.setenv("BLP_TOPK_EXPAND", expand)
+    monkeypatch.setenv("BLP_TK_WAVESEL", wavesel)
     T = blp.TopK(G, "user")
     assert (T.info()["wedge_entries"] > 0) == (expand == "1")
     src = rng.choice(G.n_col0, 40, replace=False)
@@ -83,11 +86,15 @@ def test_topk_u32_tier_and_multi_chunk(small, monkeypatch):
     assert T2.stats(2)[1] == len(src)  # every source took the direct Adamic-Adar path
 
 
+@pytest.mark.parametrize("wavesel", ["0", "1"])
 @pytest.mark.parametrize("acc_words", [None, "600"])
-def test_topk_selection_pruning_many_targets(gpu, monkeypatch, acc_words):
+def test_topk_selection_pruning_many_targets(gpu, monkeypatch, acc_words, wavesel):
     """More targets than one selection round (1,024): the CN and Jaccard walks stop once the
     degree bound falls below the k-th key. Many equal degrees and equal counts (ties broken by
-    id), k = 1, 5 and 20; with a small counter space the bound is applied per chunk."""
+    id), k = 1, 5, 20 and 64 (the per-wave selection's largest list) and 65 (its fallback to
+    block rounds); with a small counter space the bound is applied per chunk and the per-wave
+    selection starts from the earlier chunks' list."""
+    monkeypatch.setenv("BLP_TK_WAVESEL", wavesel)
     rng = np.random.default_rng(21)
     a, b = bipartite_edges(rng, 20000, 5000, 120000, zipf=0.5)
     G = blp.DeviceGraph(a, b, device=gpu)
@@ -97,7 +104,7 @@ def test_topk_selection_pruning_many_targets(gpu, monkeypatch, acc_words):
     T = blp.TopK(G, "user")
     assert (T.info()["chunks"] > 1) == (acc_words is not None)
     src = rng.choice(np.flatnonzero(G.hop1_size[: G.n_col0] > 1), 12, replace=False)
-    for k in (1, 5, 20):
+    for k in (1, 5, 20, 64, 65):
         check_against_oracle(G, T, adj, src, k, mask=blp.CN | blp.JACCARD, methods=METHODS[:2])
 
 
