@@ -247,6 +247,13 @@ void prefault_host(void* p, size_t bytes);
 // first touch takes one fault per 2 MiB instead of per 4 KiB and the release is one munmap of a
 // few hundred pages. Smaller sizes (and BLP_NO_THP=1) use malloc. Null on failure.
 void* host_alloc(size_t bytes);
+// A host<->device copy of `bytes` on stream st, complete on return. BLP_PIN_COPY=1 (round-5 A/B):
+// a host range of >= 1 MiB is registered with the HIP runtime for the copy and unregistered right
+// after, so the runtime does not pin the caller's pages implicitly (an implicit pinning that
+// outlives the copy is invalidated when the memory is unmapped later, and the driver then stalls
+// the process's GPU queues until it restores them). Otherwise, or if registration fails, a plain
+// pageable copy.
+int copy_sync(void* dst, const void* src, size_t bytes, hipMemcpyKind kind, hipStream_t st);
 void host_free(void* p, size_t bytes);
 // std allocator over host_alloc that leaves elements uninitialised on resize()
 template <class T>

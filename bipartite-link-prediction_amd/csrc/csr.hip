@@ -205,9 +205,14 @@ extern "C" int blp_csr_fetch(const blp_csr* c, int64_t* row_ptr, int32_t* col_id
   BLP_HIP(hipSetDevice(c->device));
   prefault_host(row_ptr, 8 * (size_t)(c->n + 1));
   if (c->nnz && col_idx) prefault_host(col_idx, 4 * (size_t)c->nnz);
-  if (row_ptr) BLP_HIP(hipMemcpy(row_ptr, c->d_rp, 8 * (c->n + 1), hipMemcpyDeviceToHost));
-  if (col_idx && c->nnz) BLP_HIP(hipMemcpy(col_idx, c->d_ci, 4 * c->nnz, hipMemcpyDeviceToHost));
-  if (self_loop && c->n) BLP_HIP(hipMemcpy(self_loop, c->d_self, c->n, hipMemcpyDeviceToHost));
+  hipStream_t st = stream_take(c->device);
+  if (!st) return BLP_E_HIP_BASE;
+  int rc = BLP_OK;
+  if (row_ptr) rc = copy_sync(row_ptr, c->d_rp, 8 * (c->n + 1), hipMemcpyDeviceToHost, st);
+  if (!rc && col_idx && c->nnz) rc = copy_sync(col_idx, c->d_ci, 4 * c->nnz, hipMemcpyDeviceToHost, st);
+  if (!rc && self_loop && c->n) rc = copy_sync(self_loop, c->d_self, c->n, hipMemcpyDeviceToHost, st);
+  stream_give(c->device, st);
+  if (rc) return rc;
   return BLP_OK;
 }
 

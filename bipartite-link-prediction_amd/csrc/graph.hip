@@ -148,6 +148,26 @@ void* host_alloc(size_t bytes) {
   return (void*)a;
 }
 
+int copy_sync(void* dst, const void* src, size_t bytes, hipMemcpyKind kind, hipStream_t st) {
+  if (!bytes) return BLP_OK;
+  static const bool pin = getenv("BLP_PIN_COPY") && atoi(getenv("BLP_PIN_COPY")) > 0;
+  void* reg = nullptr;
+  if (pin && bytes >= (size_t(1) << 20) && (kind == hipMemcpyHostToDevice || kind == hipMemcpyDeviceToHost)) {
+    const uintptr_t h = (uintptr_t)(kind == hipMemcpyHostToDevice ? src : dst);
+    const uintptr_t b = h & ~uintptr_t(4095), e = (h + bytes + 4095) & ~uintptr_t(4095);
+    if (hipHostRegister((void*)b, e - b, hipHostRegisterDefault) == hipSuccess ||
+        (kind == hipMemcpyHostToDevice && hipHostRegister((void*)b, e - b, hipHostRegisterReadOnly) == hipSuccess))
+      reg = (void*)b;
+    else
+      (void)hipGetLastError();  // not registrable (already registered, ...): a pageable copy
+  }
+  hipError_t err = hipMemcpyAsync(dst, src, bytes, kind, st);
+  if (err == hipSuccess) err = hipStreamSynchronize(st);
+  if (reg) (void)hipHostUnregister(reg);
+  if (err != hipSuccess) return hip_fail(err, "copy_sync", __FILE__, __LINE__);
+  return BLP_OK;
+}
+
 void host_free(void* p, size_t bytes) {
   if (!p) return;
   if (bytes < HUGE_MIN || !thp_on()) {
@@ -340,7 +360,9 @@ int graph_finish(blp_graph* g, const double* aaw) {
     std::vector<long long> fx;
     if (int rc = aa_weights_fixed(aaw, n, fx)) return rc;
     BLP_HIP(hipMalloc(&g->d_aaw_fx, sizeof(long long) * std::max<int64_t>(n, 1)));
-    if (n) BLP_HIP(hipMemcpy(g->d_aaw_fx, fx.data(), sizeof(long long) * n, hipMemcpyHostToDevice));
+    if (n) {
+      if (int rc = copy_sync(g->d_aaw_fx, fx.data(), sizeof(long long) * n, hipMemcpyHostToDevice, g->stream)) return rc;
+    }
     stage("weights");
     int rc = build_weight_codes(g, g->hrp, fx);
     if (rc != BLP_OK) return rc;

@@ -436,7 +436,7 @@ int device_load(const char* path, int device, blp_edges** out) {
     uint8_t* d_txt = txt.as<uint8_t>();
     BLP_HIP(hipMemsetAsync(d_txt + S, 0, (size_t)(nb * NL_CHUNK - S), st));
     if (!tail_nl) BLP_HIP(hipMemsetAsync(d_txt + S, '\n', 1, st));
-    BLP_HIP(hipMemcpyAsync(d_txt, data, (size_t)S, hipMemcpyHostToDevice, st));
+    if ((rc = copy_sync(d_txt, data, (size_t)S, hipMemcpyHostToDevice, st))) return rc;
     hipLaunchKernelGGL(k_nl_count, dim3((unsigned)nb), dim3(NL_BLOCK), 0, st, d_txt, blk.as<uint64_t>());
     BLP_HIP(hipGetLastError());
     size_t tb = 0;
@@ -504,9 +504,9 @@ int device_load(const char* path, int device, blp_edges** out) {
     BLP_HIP(hipGetLastError());
     e->node_ids.resize((size_t)n);
     e->map.resize((size_t)span);
-    BLP_HIP(hipMemcpyAsync(e->node_ids.data(), ids.p, 8 * n, hipMemcpyDeviceToHost, st));
-    BLP_HIP(hipMemcpyAsync(e->map.data(), map.p, 4 * span, hipMemcpyDeviceToHost, st));
-    BLP_HIP(hipStreamSynchronize(st));
+    if ((rc = copy_sync(e->node_ids.data(), ids.p, 8 * n, hipMemcpyDeviceToHost, st)) ||
+        (rc = copy_sync(e->map.data(), map.p, 4 * span, hipMemcpyDeviceToHost, st)))
+      return rc;
     e->m = L;
     e->n = n;
     e->n_col0 = n_col0;

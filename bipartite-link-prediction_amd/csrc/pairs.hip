@@ -3611,8 +3611,9 @@ static int batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_
     BLP_HIP_OR(hipMemcpyAsync(b->d_x, twin->d_y, 4 * n_pairs, hipMemcpyDeviceToDevice, b->stream), bail);
     BLP_HIP_OR(hipMemcpyAsync(b->d_y, twin->d_x, 4 * n_pairs, hipMemcpyDeviceToDevice, b->stream), bail);
   } else if (n_pairs) {
-    BLP_HIP_OR(hipMemcpyAsync(b->d_x, x, 4 * n_pairs, hipMemcpyHostToDevice, b->stream), bail);
-    BLP_HIP_OR(hipMemcpyAsync(b->d_y, y, 4 * n_pairs, hipMemcpyHostToDevice, b->stream), bail);
+    if ((rc = copy_sync(b->d_x, x, 4 * n_pairs, hipMemcpyHostToDevice, b->stream)) ||
+        (rc = copy_sync(b->d_y, y, 4 * n_pairs, hipMemcpyHostToDevice, b->stream)))
+      return bail(rc);
   }
   BLP_HIP_OR(hipMemsetAsync(b->d_misc, 0, sizeof(Misc), b->stream), bail);  // dbg[] is zeroed here, not per score
   stage("upload");
@@ -4580,9 +4581,9 @@ int blp_batch_fetch(blp_graph* g, blp_batch* b, uint32_t* cn, double* jac, doubl
     if (cn) prefault_host(cn, 4 * (size_t)np);
     if (jac) prefault_host(jac, 8 * (size_t)np);
     if (aa) prefault_host(aa, 8 * (size_t)np);
-    if (cn) BLP_HIP(hipMemcpy(cn, b->d_cn, 4 * np, hipMemcpyDeviceToHost));
-    if (jac) BLP_HIP(hipMemcpy(jac, b->d_jac, 8 * np, hipMemcpyDeviceToHost));
-    if (aa) BLP_HIP(hipMemcpy(aa, b->d_aa, 8 * np, hipMemcpyDeviceToHost));
+    if (cn && (rc = copy_sync(cn, b->d_cn, 4 * np, hipMemcpyDeviceToHost, b->stream))) return rc;
+    if (jac && (rc = copy_sync(jac, b->d_jac, 8 * np, hipMemcpyDeviceToHost, b->stream))) return rc;
+    if (aa && (rc = copy_sync(aa, b->d_aa, 8 * np, hipMemcpyDeviceToHost, b->stream))) return rc;
   }
 #ifdef BLP_DEBUG
   if (m.dbg[0]) {  // the scorers' bound checks (PS_OK): any violation fails the batch
@@ -4626,9 +4627,7 @@ int blp_batch_fetch_repr(blp_graph* g, blp_batch* b, int which, int zero_int, ch
   rc = repr_launch(which == BLP_JACCARD ? b->d_jac : b->d_aa, np, zero_int != 0, slots.as<char>(), g->n_cu, b->stream);
   if (rc) return rc;
   prefault_host(out, (size_t)blp::REPR_SLOT_BYTES * np);  // while the formatter runs
-  BLP_HIP(hipMemcpyAsync(out, slots.p, (size_t)blp::REPR_SLOT_BYTES * np, hipMemcpyDeviceToHost, b->stream));
-  BLP_HIP(hipStreamSynchronize(b->stream));
-  return BLP_OK;
+  return copy_sync(out, slots.p, (size_t)blp::REPR_SLOT_BYTES * np, hipMemcpyDeviceToHost, b->stream);
 }
 
 int blp_score_pairs(blp_graph* g, int side, uint32_t mask, const int32_t* pu, const int32_t* pb, int64_t n_pairs,
