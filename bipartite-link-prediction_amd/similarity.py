@@ -309,6 +309,14 @@ def main(example_file, graph_file, u_methods, u_outfiles, b_methods, b_outfiles,
         timings.update({"graph": t_g - t, "examples": t_ex - t_g, "score": t_s - t_ex, "files": t_f - t_s,
                         "teardown": t_c - t_f, "graph_release": clock() - t_c, "pairs": int(present.sum())})
         timings["graph_detail"] = dict(getattr(G, "build_times", None) or {})
+        # what returning releases, timed: the score arrays, the examples, the host half of the graph
+        t_r = clock()
+        del present, u_scores, b_scores
+        t_r1 = clock()
+        del ex, fut_ex
+        t_r2 = clock()
+        del G
+        timings.update({"release_scores": t_r1 - t_r, "release_examples": t_r2 - t_r1, "release_graph": clock() - t_r2})
 
 
 def users(examples, G, methods, outfiles, *, sidecar=False):
