@@ -23,4 +23,4 @@ for i in 1 2; do
     python -c "import json;d=json.loads(open('gpurun_out/r05tk_w${w}_$i.json').read().strip().splitlines()[-1]);print('wavesel $w', d['ms_per_step'], d.get('parity'))"
   done
 done
-bash profiles/scripts/r05_profB.sh
+echo "call D done"
