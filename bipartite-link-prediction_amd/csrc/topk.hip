@@ -47,7 +47,10 @@
 
 namespace {
 
-constexpr int TK_NT = 1024;
+#ifndef BLP_TK_NT
+#define BLP_TK_NT 1024  // workgroup size (experiment builds: 512 halves the waves and lifts the 128-register cap)
+#endif
+constexpr int TK_NT = BLP_TK_NT;
 constexpr int TK_SEL = 2048;          // selection buffer entries (also the AA hash table)
 constexpr int TK_AH = TK_SEL / 2;     // AA hash slots: two u64 words each in s.key (exact sums)
 constexpr int TK_HCAP = TK_AH / 2;    // AA candidates handled by the hash (load <= 1/2)
@@ -1186,7 +1189,7 @@ __global__ __launch_bounds__(TK_NT) void k_topk(TkArgs a) {
         if (e >= c.a0 && e < c.a1) acc_clear(a, s.acc, c, e);
       }
       __syncthreads();
-      const bool wsel = a.wavesel && a.k <= TK_WK;
+      const bool wsel = TK_WB == 128 && a.wavesel && a.k <= TK_WK;  // wave_sort: two entries per lane
       if (want_cn) ncand += wsel ? sel_counts_wave<0>(a, s, it, c, h2, true) : sel_counts<0>(a, s, it, c, h2, true);
       TKP(3)
       if (want_j)

@@ -17,10 +17,18 @@ for w in 0 1; do
   BLP_TK_WAVESEL=$w BLP_LIB=$R/bipartite-link-prediction_amd/blp/libblp_tkprof.so timeout -k 10 300 python profiles/scripts/topk_probe.py >> gpurun_out/r05_topk_phases.txt 2>&1 || { tail gpurun_out/r05_topk_phases.txt; exit 1; }
 done
 cat gpurun_out/r05_topk_phases.txt
+BLP_LIB=$R/bipartite-link-prediction_amd/blp/libblp_tk512.so timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_topk.py tests/test_gpu_atsize.py -k "topk" > gpurun_out/r05_topk_tests_512.log 2>&1 || { tail -30 gpurun_out/r05_topk_tests_512.log; exit 1; }
+tail -2 gpurun_out/r05_topk_tests_512.log
+tk() {  # name, env...
+  local n=$1
+  shift
+  env "$@" timeout -k 10 300 python bench.py --mode topk --steps 10 > gpurun_out/r05tk_$n.json 2> gpurun_out/r05tk_$n.err || { tail gpurun_out/r05tk_$n.err; exit 1; }
+  python -c "import json;d=json.loads(open('gpurun_out/r05tk_$n.json').read().strip().splitlines()[-1]);print('$n', d['ms_per_step'], d.get('parity'))"
+}
 for i in 1 2; do
-  for w in 0 1; do
-    BLP_TK_WAVESEL=$w timeout -k 10 300 python bench.py --mode topk --steps 10 > gpurun_out/r05tk_w${w}_$i.json 2> gpurun_out/r05tk_w${w}_$i.err || { tail gpurun_out/r05tk_w${w}_$i.err; exit 1; }
-    python -c "import json;d=json.loads(open('gpurun_out/r05tk_w${w}_$i.json').read().strip().splitlines()[-1]);print('wavesel $w', d['ms_per_step'], d.get('parity'))"
-  done
+  tk def_$i
+  tk wave_$i BLP_TK_WAVESEL=1
+  tk nt512_$i BLP_LIB=$R/bipartite-link-prediction_amd/blp/libblp_tk512.so
+  tk nt512w_$i BLP_LIB=$R/bipartite-link-prediction_amd/blp/libblp_tk512.so BLP_TK_WAVESEL=1
 done
 echo "call D done"
