@@ -13,7 +13,7 @@ e2e() {  # name, env...
   env BLP_SLOW_HIP_MS=3 "$@" timeout -k 10 300 python bench.py --mode e2e --config c2 > gpurun_out/r05thp_$n.json 2> gpurun_out/r05thp_$n.err || { tail -20 gpurun_out/r05thp_$n.err; exit 1; }
   python -c "import json;d=json.loads(open('gpurun_out/r05thp_$n.json').read().strip().splitlines()[-1]);print('$n', round(d['e2e_s'],4), {k: round(v,4) for k,v in d['phases_s'].items()}, d['ok'])"
 }
-for i in 1 2 3; do
+for i in 1 2; do
   e2e thp_$i
   e2e pin_$i BLP_PIN_COPY=1
   e2e nothp_$i BLP_NO_THP=1
