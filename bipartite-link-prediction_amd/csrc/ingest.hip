@@ -406,9 +406,45 @@ int device_load(const char* path, int device, blp_edges** out) {
     return BLP_OK;
   }
   const int64_t S = (int64_t)st_.st_size;
-  const uint8_t* data = (const uint8_t*)mmap(nullptr, (size_t)S, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
-  close(fd);
-  if (data == MAP_FAILED) return BLP_OK;  // the host parser reports it
+  // The text: read on up to 16 threads into huge-page host memory that is registered for the one
+  // upload and released right after (default), or (BLP_PARSE_MMAP=1, the round-4 path) a populated
+  // file mapping uploaded as pageable memory and unmapped afterwards.
+  const bool use_mmap = getenv("BLP_PARSE_MMAP") && atoi(getenv("BLP_PARSE_MMAP")) > 0;
+  const uint8_t* data = nullptr;
+  uint8_t* rbuf = nullptr;
+  if (use_mmap) {
+    data = (const uint8_t*)mmap(nullptr, (size_t)S, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
+    close(fd);
+    if (data == MAP_FAILED) return BLP_OK;  // the host parser reports it
+  } else {
+    rbuf = static_cast<uint8_t*>(host_alloc((size_t)S));
+    bool ok = rbuf != nullptr;
+    if (ok) {
+      const int64_t nt = std::max<int64_t>(1, std::min<int64_t>(16, S >> 23));
+      std::vector<uint8_t> rok((size_t)nt, 0);
+      auto slice = [&](int64_t t) {
+        int64_t at = S * t / nt;
+        const int64_t to = S * (t + 1) / nt;
+        while (at < to) {
+          const ssize_t r = pread(fd, rbuf + at, (size_t)(to - at), (off_t)at);
+          if (r <= 0) return;
+          at += r;
+        }
+        rok[(size_t)t] = 1;
+      };
+      std::vector<std::thread> th;
+      for (int64_t t = 1; t < nt; ++t) th.emplace_back(slice, t);
+      slice(0);
+      for (auto& h : th) h.join();
+      ok = std::count(rok.begin(), rok.end(), 1) == nt;
+    }
+    close(fd);
+    if (!ok) {
+      host_free(rbuf, (size_t)S);
+      return BLP_OK;  // the host parser reports it
+    }
+    data = rbuf;
+  }
   hipStream_t st = nullptr;
   ScopedBuf txt, blk, blk_off, tmp, nl, a, b, stats, in0, in1, cnt, base, map, ids;
   blp_edges* e = nullptr;
@@ -436,7 +472,18 @@ int device_load(const char* path, int device, blp_edges** out) {
     uint8_t* d_txt = txt.as<uint8_t>();
     BLP_HIP(hipMemsetAsync(d_txt + S, 0, (size_t)(nb * NL_CHUNK - S), st));
     if (!tail_nl) BLP_HIP(hipMemsetAsync(d_txt + S, '\n', 1, st));
-    if ((rc = copy_sync(d_txt, data, (size_t)S, hipMemcpyHostToDevice, st))) return rc;
+    if (use_mmap) {
+      if ((rc = copy_sync(d_txt, data, (size_t)S, hipMemcpyHostToDevice, st))) return rc;
+    } else {  // registered for this copy only: the runtime holds no pinning of it afterwards
+      const bool reg = hipHostRegister(rbuf, (size_t)S, hipHostRegisterDefault) == hipSuccess;
+      if (!reg) (void)hipGetLastError();
+      hipError_t ce = hipMemcpyAsync(d_txt, data, (size_t)S, hipMemcpyHostToDevice, st);
+      if (ce == hipSuccess) ce = hipStreamSynchronize(st);
+      if (reg) (void)hipHostUnregister(rbuf);
+      host_free(rbuf, (size_t)S);
+      rbuf = nullptr;
+      if (ce != hipSuccess) return hip_fail(ce, "hipMemcpyAsync (graph.txt upload)", __FILE__, __LINE__);
+    }
     hipLaunchKernelGGL(k_nl_count, dim3((unsigned)nb), dim3(NL_BLOCK), 0, st, d_txt, blk.as<uint64_t>());
     BLP_HIP(hipGetLastError());
     size_t tb = 0;
@@ -519,7 +566,10 @@ int device_load(const char* path, int device, blp_edges** out) {
   int rc = run();
   if (st) stream_give(device, st);  // synchronized: nothing of this call left in flight before its buffers go
   delete e;  // a handle abandoned on an error path
-  munmap((void*)data, (size_t)S);
+  if (use_mmap)
+    munmap((void*)data, (size_t)S);
+  else if (rbuf)
+    host_free(rbuf, (size_t)S);  // an error before the upload
   if (rc == BLP_E_HIP_BASE - (int)hipErrorOutOfMemory) {  // no room on the device: the host parser takes the file
     (void)hipGetLastError();
     *out = nullptr;

@@ -595,12 +595,16 @@ def _same_load(d, h):
             assert np.array_equal(x, y)
 
 
+@pytest.mark.parametrize("text_path", ["read", "mmap"])
 @pytest.mark.parametrize("final_newline", [False, True])
-def test_device_parse_equals_host_parse(gpu, tmp_path, final_newline):
+def test_device_parse_equals_host_parse(gpu, tmp_path, final_newline, text_path, monkeypatch):
     """blp_edges_load_device on a graph.txt of the reference's line shape (dataset_maker.py:197;
     tabs, CRLF, trailing blanks, leading zeros, duplicates, reversed duplicates, self-loops): the
     parse, id map and CSR run on the device and equal the host loader's, and the CSR equals the
-    host CSR builder's on the dense endpoints."""
+    host CSR builder's on the dense endpoints. The text reaches HBM from a threaded read into
+    registered huge-page memory (default) or from a file mapping (BLP_PARSE_MMAP=1)."""
+    if text_path == "mmap":
+        monkeypatch.setenv("BLP_PARSE_MMAP", "1")
     rng = np.random.default_rng(21)
     a, c = _messy_edges(rng, 60000, 2500, 150000)
     p = _graph_txt(tmp_path / "graph.txt", a + 5, c + 5, rng, final_newline=final_newline)
