@@ -1,7 +1,8 @@
 #!/bin/bash
 # Round 5: large host buffers on transparent huge pages (default) against plain malloc / numpy
 # (BLP_NO_THP=1) in config-2 similarity.main, and with the large copies explicitly registered
-# (BLP_PIN_COPY=1), alternating, three runs each; then the THP
+# (BLP_PIN_COPY=1), and with graph.txt uploaded from a file mapping (BLP_PARSE_MMAP=1, the
+# round-4 path), alternating, two runs each; then the THP
 # microbenchmark (first touch, fetch, unmap of 600 MB).
 set -o pipefail
 R=$GRAFT_REPO_ROOT
@@ -16,6 +17,7 @@ e2e() {  # name, env...
 for i in 1 2; do
   e2e thp_$i
   e2e pin_$i BLP_PIN_COPY=1
+  e2e mmap_$i BLP_PARSE_MMAP=1
   e2e nothp_$i BLP_NO_THP=1
 done
 timeout -k 10 120 python profiles/scripts/r05_hostmem2.py 600 > gpurun_out/r05_hostmem2.json || exit 1
