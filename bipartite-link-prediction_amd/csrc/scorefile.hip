@@ -479,22 +479,40 @@ int blp_scores_write(const blp_examples* x, const char* path, int kind, const ui
   for (unsigned t = 1; t < nt; ++t)
     cut[t] = std::lower_bound(x->u_off.begin(), x->u_off.end(), np * (int64_t)t / nt) - x->u_off.begin();
   for (unsigned t = 1; t <= nt; ++t) cut[t] = std::max(cut[t], cut[t - 1]);
-  // each slice formats into its own buffer, sized by a bound: per user its key + 8 bytes,
-  // per pair its key + 6 + a value of at most 24 bytes (repr of a double; 10 digits of a u32)
-  std::vector<HostBytes> part(nt);
+  // Two passes per slice: the exact byte length of its text (so every slice knows its file offset
+  // up front), then the text itself, formatted through a small reusable buffer and written at its
+  // offset as the buffer fills (no slice-sized buffers: their first-touch faults and zeroing were
+  // most of this call's cost at config 2's ~1.2 GB of text per six files).
+  // value text of present pair k (vi = its values index); returns its length, writing at o
+  auto value = [&](char* o, int64_t vi) -> char* {
+    if (kind == BLP_SCORE_U32) return std::to_chars(o, o + 12, ((const uint32_t*)values)[vi]).ptr;
+    if (kind == BLP_SCORE_REPR24) {  // formatted on the device: copy the slot
+      const char* sl = (const char*)values + 24 * vi;
+      std::memcpy(o, sl, 24);  // within the pair's bound (key + 30)
+      return o + strnlen(sl, 24);
+    }
+    const double v = ((const double*)values)[vi];
+    if (kind == BLP_SCORE_F64_INT0 && v == 0.0) {
+      *o++ = '0';  // similarity.py:118: nothing added -> the int 0
+      return o;
+    }
+    return put_repr(o, v);
+  };
+  auto value_len = [&](int64_t vi) -> int64_t {
+    if (kind == BLP_SCORE_U32) {
+      uint32_t v = ((const uint32_t*)values)[vi];
+      int64_t d = 1;
+      while (v >= 10) v /= 10, ++d;
+      return d;
+    }
+    if (kind == BLP_SCORE_REPR24) return (int64_t)strnlen((const char*)values + 24 * vi, 24);
+    char tmp[40];
+    return value(tmp, vi) - tmp;
+  };
   std::vector<int64_t> part_len(nt, 0);
   std::vector<uint8_t> nonempty(nt, 0);
-  auto work = [&](unsigned t) {
-    int64_t bound = 16;
-    for (int64_t u = cut[t]; u < cut[t + 1]; ++u) bound += x->u_len[u] + 8;
-    for (int64_t k = x->u_off[cut[t]]; k < x->u_off[cut[t + 1]]; ++k) bound += x->v_len[k] + 30;
-    part[t] = host_bytes((size_t)bound);
-    char* const o0 = part[t].get();
-    if (!o0) {
-      part_len[t] = -1;  // reported after the join
-      return;
-    }
-    char* o = o0;
+  // the walk shared by both passes: emit(bytes) for the structure, val(k, vi) for a value
+  auto walk = [&](unsigned t, auto&& put, auto&& put_value, auto&& put_zero) {
     bool first_user = true;
     for (int64_t u = cut[t]; u < cut[t + 1]; ++u) {
       bool opened = false;
@@ -504,52 +522,47 @@ int blp_scores_write(const blp_examples* x, const char* path, int kind, const ui
         // for a present pair under an unmatched method (defaultdict: no empty user dicts)
         if (kind == BLP_SCORE_NONE && pres) continue;
         if (!opened) {
-          if (!first_user) o = put_bytes(o, ", ", 2);
+          if (!first_user) put(", ", 2);
           first_user = false;
-          *o++ = '"';
-          o = put_bytes(o, base + x->u_key[u], x->u_len[u]);
-          o = put_bytes(o, "\": {", 4);
+          put("\"", 1);
+          put(base + x->u_key[u], x->u_len[u]);
+          put("\": {", 4);
           opened = true;
         } else {
-          o = put_bytes(o, ", ", 2);
+          put(", ", 2);
         }
-        *o++ = '"';
-        o = put_bytes(o, base + x->v_key[k], x->v_len[k]);
-        o = put_bytes(o, "\": ", 3);
-        if (!pres) {
-          *o++ = '0';
-          continue;
-        }
-        const int64_t vi = present ? vidx[k] : k;
-        if (kind == BLP_SCORE_U32) {
-          o = std::to_chars(o, o + 12, ((const uint32_t*)values)[vi]).ptr;
-        } else if (kind == BLP_SCORE_REPR24) {  // formatted on the device: copy the slot
-          const char* sl = (const char*)values + 24 * vi;
-          std::memcpy(o, sl, 24);  // within the pair's bound (key + 30)
-          o += strnlen(sl, 24);
-        } else {
-          const double v = ((const double*)values)[vi];
-          if (kind == BLP_SCORE_F64_INT0 && v == 0.0)
-            *o++ = '0';  // similarity.py:118: nothing added -> the int 0
-          else
-            o = put_repr(o, v);
-        }
+        put("\"", 1);
+        put(base + x->v_key[k], x->v_len[k]);
+        put("\": ", 3);
+        if (!pres)
+          put_zero();
+        else
+          put_value(present ? vidx[k] : k);
       }
-      if (opened) *o++ = '}';
+      if (opened) put("}", 1);
     }
-    part_len[t] = o - o0;
-    nonempty[t] = !first_user;
+    return !first_user;
   };
-  std::vector<std::thread> th;
-  for (unsigned t = 1; t < nt; ++t) th.emplace_back(work, t);
-  work(0);
-  for (auto& h : th) h.join();
-  BLP_CHECK(std::find(part_len.begin(), part_len.end(), int64_t(-1)) == part_len.end(), BLP_E_ARG,
-            "blp_scores_write: out of host memory");
-  // "{" part ", " part ... "}": every slice written at its own offset, concurrently (one
-  // sequential fwrite of ~200 MB per file at config 2 dominated the file phase)
-  const int fd = open(path, O_WRONLY | O_CREAT | O_TRUNC, 0666);
-  if (fd < 0) return fail(BLP_E_ARG, std::string("blp_scores_write: cannot open ") + path);
+  std::vector<int64_t> piece_max(nt, 0);  // the longest single piece of a slice's text
+  auto count_slice = [&](unsigned t) {
+    int64_t len = 0, mx = 0;
+    nonempty[t] = walk(
+        t,
+        [&](const char*, size_t n) {
+          len += (int64_t)n;
+          mx = std::max<int64_t>(mx, (int64_t)n);
+        },
+        [&](int64_t vi) { len += value_len(vi); }, [&]() { len += 1; });
+    part_len[t] = len;
+    piece_max[t] = mx;
+  };
+  {
+    std::vector<std::thread> th;
+    for (unsigned t = 1; t < nt; ++t) th.emplace_back(count_slice, t);
+    count_slice(0);
+    for (auto& h : th) h.join();
+  }
+  // "{" part ", " part ... "}": every slice at its own offset
   std::vector<int64_t> at(nt, 0);
   int64_t pos = 1;
   bool any = false;
@@ -560,7 +573,9 @@ int blp_scores_write(const blp_examples* x, const char* path, int kind, const ui
     pos += part_len[t];
     any = true;
   }
-  auto put = [fd](const char* p, int64_t len, int64_t off) {
+  const int fd = open(path, O_WRONLY | O_CREAT | O_TRUNC, 0666);
+  if (fd < 0) return fail(BLP_E_ARG, std::string("blp_scores_write: cannot open ") + path);
+  auto put_at = [fd](const char* p, int64_t len, int64_t off) {
     while (len > 0) {
       const ssize_t w = pwrite(fd, p, (size_t)std::min<int64_t>(len, int64_t(1) << 30), (off_t)off);
       if (w <= 0) return false;
@@ -569,17 +584,50 @@ int blp_scores_write(const blp_examples* x, const char* path, int kind, const ui
     return true;
   };
   std::vector<uint8_t> wok(nt, 1);
-  th.clear();
-  bool sep = false;
-  for (unsigned t = 0; t < nt; ++t) {
-    if (!nonempty[t]) continue;
-    const bool with_sep = sep;
-    sep = true;
-    th.emplace_back([&, t, with_sep]() {
-      wok[t] = (!with_sep || put(", ", 2, at[t] - 2)) && put(part[t].get(), part_len[t], at[t]);
-    });
-  }
-  bool ok = put("{", 1, 0) && put("}", 1, pos);
+  auto write_slice = [&](unsigned t) {
+    if (!nonempty[t]) return;
+    // 1 MiB, or room for the slice's longest key (a piece) with the value after it
+    const int64_t buf_bytes = std::max<int64_t>(int64_t(1) << 20, 2 * (piece_max[t] + 48));
+    std::unique_ptr<char[]> buf(new (std::nothrow) char[(size_t)buf_bytes]);
+    if (!buf) {
+      wok[t] = 0;
+      return;
+    }
+    char* const b0 = buf.get();
+    char* o = b0;
+    int64_t off = at[t];
+    bool ok = true;
+    if (any && at[t] > 1) {  // the ", " before this slice (not before the first non-empty one)
+      ok = put_at(", ", 2, off - 2);
+    }
+    auto flush_if = [&](int64_t need) {
+      if ((o - b0) + need <= buf_bytes) return;
+      ok = ok && put_at(b0, o - b0, off);
+      off += o - b0;
+      o = b0;
+    };
+    walk(
+        t,
+        [&](const char* p, size_t n) {
+          flush_if((int64_t)n);
+          o = put_bytes(o, p, n);
+        },
+        [&](int64_t vi) {
+          flush_if(40);
+          o = value(o, vi);
+        },
+        [&]() {
+          flush_if(1);
+          *o++ = '0';
+        });
+    ok = ok && put_at(b0, o - b0, off);
+    off += o - b0;
+    wok[t] = ok && off == at[t] + part_len[t];
+  };
+  std::vector<std::thread> th;
+  for (unsigned t = 1; t < nt; ++t) th.emplace_back(write_slice, t);
+  write_slice(0);
+  bool ok = put_at("{", 1, 0) && put_at("}", 1, pos);
   for (auto& h : th) h.join();
   for (unsigned t = 0; t < nt; ++t) ok = ok && wok[t];
   ok = (close(fd) == 0) && ok;
