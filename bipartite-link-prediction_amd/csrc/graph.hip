@@ -28,6 +28,8 @@ __global__ void k_code_ids(const int32_t* __restrict__ ci, int64_t nnz, const ui
   }
 }
 
+__global__ void k_noop() {}  // blp_stream_prewarm: the first work of a new stream
+
 }  // namespace
 
 namespace blp {
@@ -475,13 +477,25 @@ int blp_stream_prewarm(int device, int n) {
     for (int (*f)() : {preload_ingest, preload_csr, preload_graph, preload_hot, preload_node2, preload_wedge,
                        preload_pairs, preload_hop3, preload_repr})
       if (f()) return fail(BLP_E_HIP_BASE, "blp_stream_prewarm: kernel code object load failed");
+  // Top the pool up to n streams, and run one empty kernel on each new stream: the first work on
+  // a fresh stream waited 16-26 ms to start in similarity.main (the CSR build's first sync,
+  // profiles/r05_e2e_slow_calls.txt), so the prewarm thread pays that instead. Streams the pool
+  // already holds were used before (BLP_PREWARM_ALWAYS=1: always create n, the round-4 behaviour).
+  size_t have = 0;
+  {
+    std::lock_guard<std::mutex> lk(g_stream_mu);
+    if ((size_t)device < g_stream_pool.size()) have = g_stream_pool[device].size();
+  }
+  if (getenv("BLP_PREWARM_ALWAYS")) have = 0;
   std::vector<hipStream_t> made;
-  for (int i = 0; i < n; ++i) {
+  for (int i = (int)std::min<size_t>(have, (size_t)n); i < n; ++i) {
     hipStream_t s = nullptr;
     BLP_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     made.push_back(s);
+    hipLaunchKernelGGL(k_noop, dim3(1), dim3(64), 0, s);
+    BLP_HIP(hipGetLastError());
   }
-  for (hipStream_t s : made) stream_give(device, s);
+  for (hipStream_t s : made) stream_give(device, s);  // synchronizes each
   return BLP_OK;
 }
 

@@ -123,7 +123,7 @@ struct TkArgs {
                                     // hash / direct AA passes; or null: those passes walk every target)
   int dw_n, dw_max;                 // hot targets; at most dw_max of them per source
   int64_t dw_words, dw_bmw, slo;
-  int wavesel;  // CN / Jaccard selection per wave (sel_counts_wave; k <= TK_WK), else block rounds
+  int wavesel;  // CN / Jaccard selection per wave (sel_counts_wave; k <= TK_WK; default), else block rounds (BLP_TK_WAVESEL=0)
 };
 
 // BLP_DEBUG builds (make debug -> libblp_debug.so): every LDS index and every row read of the
@@ -769,7 +769,7 @@ __device__ __attribute__((always_inline)) long long sel_counts(const TkArgs& a, 
   return nc;
 }
 
-// ---- per-wave selection (round 5, BLP_TK_WAVESEL): each wave walks its own blocks of 64 targets
+// ---- per-wave selection (round 5, the default; BLP_TK_WAVESEL=0 for block rounds): each wave walks its own blocks of 64 targets
 // (wave w takes blocks w, w + 16, ... of the degree order) with NO block barrier: offers are
 // appended to the wave's 128-entry region of s.key / s.col by ballot, and when it passes 64 the
 // wave sorts its region in registers (two entries per lane, bitonic over lane shuffles) and keeps
@@ -1465,7 +1465,7 @@ static TkArgs topk_args(blp_topk* t, int k, uint32_t mask) {
   a.dw_words = t->dw_words;
   a.dw_bmw = t->dw_bmw;
   a.slo = t->slo;
-  a.wavesel = (int)env_i64("BLP_TK_WAVESEL", 0);
+  a.wavesel = (int)env_i64("BLP_TK_WAVESEL", 1);  // r05_tk: 16.99 / 17.05 -> 16.53 / 16.48 ms at config 3
   return a;
 }
 

@@ -160,10 +160,11 @@ def test_config3_topk_at_size(gpu, c2_graph):
         np.testing.assert_array_equal(sa[i], aa[s:e][o])
     pair = G.score_pairs(np.repeat(src, 20).astype(np.int32), ca.reshape(-1).astype(np.int32), 7)["adamic"]
     np.testing.assert_array_equal(pair, sa.reshape(-1))
-    # the per-wave CN / Jaccard selection (BLP_TK_WAVESEL) gives the same lists at size
+    # the block-round CN / Jaccard selection (BLP_TK_WAVESEL=0; the per-wave one is the default)
+    # gives the same lists at size
     import os
 
-    os.environ["BLP_TK_WAVESEL"] = "1"
+    os.environ["BLP_TK_WAVESEL"] = "0"
     try:
         T.run(20, blp.JACCARD | blp.ADAMIC)
         for m, (c0, s0) in (("jaccard", (cj, sj)), ("adamic_adar", (ca, sa))):
