@@ -48,7 +48,7 @@
 namespace {
 
 #ifndef BLP_TK_NT
-#define BLP_TK_NT 1024  // workgroup size (experiment builds: 512 halves the waves and lifts the 128-register cap)
+#define BLP_TK_NT 1024  // workgroup size (512: no VGPR spills, but 25.2 against 17.0 ms at config 3, r05_tk_ab)
 #endif
 constexpr int TK_NT = BLP_TK_NT;
 constexpr int TK_SEL = 2048;          // selection buffer entries (also the AA hash table)
