@@ -914,7 +914,10 @@ def run_e2e(args):
         ph = {}
         t = time.perf_counter()
         sim.main(epath, gpath, methods, uf, methods, bf, timings=ph)
-        e2e = time.perf_counter() - t
+        t_back = time.perf_counter()
+        e2e = t_back - t
+        ph["call_overhead"] = ph.pop("_clock_entry") - t
+        ph["return_overhead"] = t_back - ph.pop("_clock_exit")
         n = ph["pairs"]
         # the C oracle (reference algorithm) on every pair of both sides
         cpu = {}
