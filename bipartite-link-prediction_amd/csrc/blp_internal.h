@@ -55,6 +55,8 @@ struct DevBuf {
   void release();
   template <class T> T* as() const { return reinterpret_cast<T*>(p); }
 };
+// empty the device scratch cache of `device` (DevBuf blocks kept for reuse; graph.hip)
+void dev_cache_flush(int device);
 // A DevBuf freed when it leaves scope (temporaries on paths with early returns).
 struct ScopedBuf : DevBuf {
   ScopedBuf() = default;

@@ -10,6 +10,7 @@
 #include <cstring>
 #include <mutex>
 #include <thread>
+#include <map>
 #include <unordered_map>
 
 #include <sys/mman.h>
@@ -84,15 +85,71 @@ void slow_check(int64_t t0, const char* what, const char* file, int line) {
   }
 }
 
+// Device scratch cache (round 5). Freeing a large device buffer and allocating a new one made the
+// next kernels wait 16-26 ms in similarity.main (the driver clears released VRAM before it is
+// handed out again; profiles/r05_e2e_*slow_calls.txt). Released DevBuf blocks are kept per device
+// (after a device sync, which hipFree implied) up to a budget (BLP_DEV_CACHE_MB, default 8192; 0
+// disables) and handed back to a later reservation of at most the same size and at least half;
+// an allocation that runs out of memory empties the cache and tries again.
+namespace {
+struct DevCache {
+  std::multimap<size_t, void*> blocks;
+  size_t bytes = 0;
+};
+std::mutex g_dc_mu;
+std::vector<DevCache> g_dc;  // [device]
+size_t dc_budget() {
+  static const size_t b = getenv("BLP_DEV_CACHE_MB") ? (size_t)std::max(0ll, atoll(getenv("BLP_DEV_CACHE_MB"))) << 20
+                                                       : size_t(8192) << 20;
+  return b;
+}
+int current_device() {
+  int d = 0;
+  return hipGetDevice(&d) == hipSuccess ? d : 0;
+}
+}  // namespace
+
+void dev_cache_flush(int device) {
+  std::vector<void*> drop;
+  {
+    std::lock_guard<std::mutex> lk(g_dc_mu);
+    if ((size_t)device >= g_dc.size()) return;
+    for (auto& kv : g_dc[device].blocks) drop.push_back(kv.second);
+    g_dc[device].blocks.clear();
+    g_dc[device].bytes = 0;
+  }
+  for (void* q : drop) (void)hipFree(q);
+}
+
 int DevBuf::reserve(size_t want) {
   if (want <= bytes && p) return BLP_OK;
-  if (p) {
-    BLP_HIP(hipFree(p));
-    p = nullptr;
-    bytes = 0;
+  if (p) release();
+  const size_t sz = std::max<size_t>(want, 256);
+  const int dev = current_device();
+  if (dc_budget()) {
+    std::lock_guard<std::mutex> lk(g_dc_mu);
+    if ((size_t)dev < g_dc.size()) {
+      DevCache& c = g_dc[dev];
+      auto it = c.blocks.lower_bound(sz);
+      if (it != c.blocks.end() && it->first <= 2 * sz) {
+        p = it->second;
+        bytes = it->first;
+        c.bytes -= it->first;
+        c.blocks.erase(it);
+        return BLP_OK;
+      }
+    }
   }
-  size_t sz = std::max<size_t>(want, 256);
-  BLP_HIP(hipMalloc(&p, sz));
+  hipError_t e = hipMalloc(&p, sz);
+  if (e == hipErrorOutOfMemory && dc_budget()) {
+    (void)hipGetLastError();
+    dev_cache_flush(dev);
+    e = hipMalloc(&p, sz);
+  }
+  if (e != hipSuccess) {
+    p = nullptr;
+    return hip_fail(e, "hipMalloc (DevBuf)", __FILE__, __LINE__);
+  }
   bytes = sz;
   return BLP_OK;
 }
@@ -100,8 +157,24 @@ int DevBuf::reserve(size_t want) {
 void DevBuf::release() {
   if (p) {
     const int64_t t0 = slow_clock();
-    (void)hipFree(p);
-    if (t0) slow_check(t0, "hipFree (DevBuf::release)", __FILE__, __LINE__);
+    bool kept = false;
+    const size_t budget = dc_budget();
+    if (budget && bytes <= budget) {
+      const int dev = current_device();
+      // what hipFree implied: nothing queued on the device still reads the block
+      if (hipDeviceSynchronize() == hipSuccess) {
+        std::lock_guard<std::mutex> lk(g_dc_mu);
+        if ((size_t)dev >= g_dc.size()) g_dc.resize((size_t)dev + 1);
+        DevCache& c = g_dc[dev];
+        if (c.bytes + bytes <= budget) {
+          c.blocks.emplace(bytes, p);
+          c.bytes += bytes;
+          kept = true;
+        }
+      }
+    }
+    if (!kept) (void)hipFree(p);
+    if (t0) slow_check(t0, "DevBuf::release", __FILE__, __LINE__);
   }
   p = nullptr;
   bytes = 0;

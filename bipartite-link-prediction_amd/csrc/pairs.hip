@@ -4082,6 +4082,11 @@ static bool is_oom(int rc) { return rc == BLP_E_HIP_BASE - (int)hipErrorOutOfMem
 static int create_or_release(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n, const blp_batch* twin,
                              blp_batch** out) {
   int rc = batch_create(g, x, y, n, twin, out);
+  if (is_oom(rc) && g) {  // the device scratch cache first (DevBuf blocks kept for reuse)
+    (void)hipGetLastError();
+    dev_cache_flush(g->device);
+    rc = batch_create(g, x, y, n, twin, out);
+  }
   if (!is_oom(rc) || !g || !g->d_wp) return rc;
   {
     std::lock_guard<std::mutex> lk(g->wbm_mu);
