@@ -398,6 +398,15 @@ unsigned grid_for(int64_t n, int n_cu) {
 // *out = a device-resident handle, or null (with BLP_OK) when the host parser must take the file
 int device_load(const char* path, int device, blp_edges** out) {
   *out = nullptr;
+  // BLP_GRAPH_PROF: stage wall times on stderr (as graph_finish's)
+  const bool gprof = getenv("BLP_GRAPH_PROF") != nullptr;
+  auto t_prev = std::chrono::steady_clock::now();
+  auto stage = [&](const char* what) {
+    if (!gprof) return;
+    const auto t = std::chrono::steady_clock::now();
+    fprintf(stderr, "device_parse %-8s %.3f ms\n", what, std::chrono::duration<double, std::milli>(t - t_prev).count());
+    t_prev = t;
+  };
   int fd = open(path, O_RDONLY);
   if (fd < 0) return fail(BLP_E_ARG, std::string("blp_edges_load_device: cannot open ") + path);
   struct stat st_;
@@ -445,6 +454,7 @@ int device_load(const char* path, int device, blp_edges** out) {
     }
     data = rbuf;
   }
+  stage("read");
   hipStream_t st = nullptr;
   ScopedBuf txt, blk, blk_off, tmp, nl, a, b, stats, in0, in1, cnt, base, map, ids;
   blp_edges* e = nullptr;
@@ -484,6 +494,7 @@ int device_load(const char* path, int device, blp_edges** out) {
       rbuf = nullptr;
       if (ce != hipSuccess) return hip_fail(ce, "hipMemcpyAsync (graph.txt upload)", __FILE__, __LINE__);
     }
+    stage("upload");
     hipLaunchKernelGGL(k_nl_count, dim3((unsigned)nb), dim3(NL_BLOCK), 0, st, d_txt, blk.as<uint64_t>());
     BLP_HIP(hipGetLastError());
     size_t tb = 0;
@@ -510,6 +521,7 @@ int device_load(const char* path, int device, blp_edges** out) {
     BLP_HIP(hipGetLastError());
     BLP_HIP(hipMemcpyAsync(&ps, stats.p, sizeof ps, hipMemcpyDeviceToHost, st));
     BLP_HIP(hipStreamSynchronize(st));
+    stage("lines");
     if (ps.bad) return BLP_OK;
     const int64_t lo = (int64_t)ps.mn, span = (int64_t)(ps.mx - ps.mn) + 1;
     // the host path's compactness rule (blp_edges_load)
@@ -554,6 +566,7 @@ int device_load(const char* path, int device, blp_edges** out) {
     if ((rc = copy_sync(e->node_ids.data(), ids.p, 8 * n, hipMemcpyDeviceToHost, st)) ||
         (rc = copy_sync(e->map.data(), map.p, 4 * span, hipMemcpyDeviceToHost, st)))
       return rc;
+    stage("idmap");
     e->m = L;
     e->n = n;
     e->n_col0 = n_col0;
@@ -570,6 +583,7 @@ int device_load(const char* path, int device, blp_edges** out) {
     munmap((void*)data, (size_t)S);
   else if (rbuf)
     host_free(rbuf, (size_t)S);  // an error before the upload
+  stage("release");
   if (rc == BLP_E_HIP_BASE - (int)hipErrorOutOfMemory) {  // no room on the device: the host parser takes the file
     (void)hipGetLastError();
     *out = nullptr;
