@@ -310,6 +310,16 @@ def main(example_file, graph_file, u_methods, u_outfiles, b_methods, b_outfiles,
                         "teardown": t_c - t_f, "graph_release": clock() - t_c, "pairs": int(present.sum())})
         timings["graph_detail"] = dict(getattr(G, "build_times", None) or {})
         # what returning releases, timed: the score arrays, the examples, the host half of the graph
+        if os.environ.get("BLP_E2E_REFDEBUG"):  # diagnostics: who else holds them at this point
+            import gc
+            import sys
+
+            for name, obj in (("u_scores", u_scores), ("u_jaccard_repr", u_scores.get("jaccard_repr")), ("ex", ex),
+                              ("G", G), ("present", present)):
+                if obj is None:
+                    continue
+                refs = [type(r).__name__ for r in gc.get_referrers(obj)]
+                print("[refdebug] %s refcount %d referrers %s" % (name, sys.getrefcount(obj), refs[:8]), file=sys.stderr)
         t_r = clock()
         del present, u_scores, b_scores
         t_r1 = clock()

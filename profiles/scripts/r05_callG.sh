@@ -6,6 +6,11 @@ set -o pipefail
 R=$GRAFT_REPO_ROOT
 cd $R || exit 1
 mkdir -p gpurun_out
+for i in 1 2; do
+  BLP_E2E_REFDEBUG=1 BLP_GRAPH_PROF=1 BLP_SLOW_HIP_MS=3 timeout -k 10 300 python bench.py --mode e2e --config c2 > gpurun_out/r05g_e2e_$i.json 2> gpurun_out/r05g_e2e_$i.err || { tail -20 gpurun_out/r05g_e2e_$i.err; exit 1; }
+  python -c "import json;d=json.loads(open('gpurun_out/r05g_e2e_$i.json').read().strip().splitlines()[-1]);print('e2e', round(d['e2e_s'],4), {k: round(v,4) for k,v in d['phases_s'].items()}, d['ok'])"
+  grep refdebug gpurun_out/r05g_e2e_$i.err
+done
 bash profiles/scripts/r05_profB.sh || exit 1
 head -8 gpurun_out/r05_topk_v1.md
 timeout -k 10 600 python bench.py --mode topk > gpurun_out/r05g_topk.json 2> gpurun_out/r05g_topk.err || { tail -20 gpurun_out/r05g_topk.err; exit 1; }
