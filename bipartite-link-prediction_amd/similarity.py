@@ -265,7 +265,7 @@ def main(example_file, graph_file, u_methods, u_outfiles, b_methods, b_outfiles,
         pool.submit(blp.device_sync, 0)
     else:
         pool.submit(blp.prewarm, 0, 4)  # the HIP runtime and the pooled streams (graph, parse, CSR, batches)
-    ex = None
+    ex = G = None
     try:
         print("Loading graph...")
         try:
@@ -300,7 +300,7 @@ def main(example_file, graph_file, u_methods, u_outfiles, b_methods, b_outfiles,
         if ex is not None:
             ex.close()
         t_c = clock()
-        G = locals().get("G")
+        # (no locals(): its snapshot dict would hold every array of this frame until main returns)
         if G is not None:  # the reference's graph goes when main returns; so does this one (HBM freed here)
             G.close()
     if timings is not None:
