@@ -1,0 +1,20 @@
+#!/bin/bash
+# Round 5, final check at HEAD (run again after the last code change): the whole GPU suite,
+# smoke(), the config-2 profile the line cites (r05_v2_bench), the default bench line, and config-2
+# similarity.main three times.
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+cd $R || exit 1
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -rs > gpurun_out/r05fin_gputest.log 2>&1 || { tail -60 gpurun_out/r05fin_gputest.log; exit 1; }
+tail -3 gpurun_out/r05fin_gputest.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/r05fin_smoke.log 2>&1 || { tail -20 gpurun_out/r05fin_smoke.log; exit 1; }
+tail -1 gpurun_out/r05fin_smoke.log
+bash profiles/scripts/r05_prof.sh r05_v2_bench 300 --steps 5 || { echo "c2 profile failed"; exit 1; }
+head -6 gpurun_out/r05_v2_bench.md
+timeout -k 10 300 python bench.py > gpurun_out/r05fin_bench.json 2> gpurun_out/r05fin_bench.err || { tail -20 gpurun_out/r05fin_bench.err; exit 1; }
+python -c "import json;d=json.load(open('gpurun_out/r05fin_bench.json'));print('bench', round(d['ms_per_step'],3), d['value'], d['kernels_ms'], d['parity']['ok'], d['roofline'], d.get('including_batch_create'))"
+for i in 1 2 3; do
+  timeout -k 10 300 python bench.py --mode e2e --config c2 > gpurun_out/r05fin_e2e_$i.json 2> gpurun_out/r05fin_e2e_$i.err || { tail -20 gpurun_out/r05fin_e2e_$i.err; exit 1; }
+  python -c "import json;d=json.loads(open('gpurun_out/r05fin_e2e_$i.json').read().strip().splitlines()[-1]);print('e2e', round(d['e2e_s'],4), {k: round(v,4) for k,v in d['phases_s'].items()}, d['ok'])"
+done
