@@ -6,6 +6,7 @@
 // int32 column ids.
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
 #include <cmath>
 #include <cstring>
 #include <mutex>
@@ -458,13 +459,18 @@ int graph_finish(blp_graph* g, const double* aaw) {
 namespace blp {
 namespace {
 std::mutex g_stream_mu;
+std::condition_variable g_stream_cv;
+int g_prewarming = 0;  // blp_stream_prewarm calls creating streams (under g_stream_mu)
 std::vector<std::vector<hipStream_t>> g_stream_pool;  // [device]
 constexpr size_t STREAM_POOL_CAP = 16;
 }  // namespace
 
 hipStream_t stream_take(int device) {
   {
-    std::lock_guard<std::mutex> lk(g_stream_mu);
+    std::unique_lock<std::mutex> lk(g_stream_mu);
+    // a prewarm creating streams: wait for them rather than overlap this caller's first GPU work
+    // with the stream creation (that overlap preceded 27-39 ms stalls, r05_e2e_final_ab)
+    g_stream_cv.wait(lk, [] { return g_prewarming == 0; });
     if ((size_t)device < g_stream_pool.size() && !g_stream_pool[device].empty()) {
       hipStream_t s = g_stream_pool[device].back();
       g_stream_pool[device].pop_back();
@@ -544,31 +550,42 @@ int blp_device_count(int* n) {
 int blp_stream_prewarm(int device, int n) {
   BLP_CHECK(n >= 0 && n <= 16, BLP_E_ARG, "blp_stream_prewarm: 0 <= n <= 16");
   BLP_HIP(hipSetDevice(device));
-  // the code objects of similarity.main's kernels, in the order it first launches them
+  // Top the pool up to n streams (BLP_PREWARM_ALWAYS=1: always create n, the round-4 behaviour),
+  // run one empty kernel on each new one, and hold stream_take until they are in the pool: the
+  // caller's first GPU work then neither creates a stream nor overlaps this thread's creation (an
+  // overlap that preceded 27-39 ms stalls in similarity.main, profiles/r05_e2e_final_ab_slow_calls.txt).
+  size_t have = 0;
+  {
+    std::lock_guard<std::mutex> lk(g_stream_mu);
+    if ((size_t)device < g_stream_pool.size()) have = g_stream_pool[device].size();
+    if (getenv("BLP_PREWARM_ALWAYS")) have = 0;
+    if ((size_t)n > have) ++g_prewarming;  // stream_take waits until these are in the pool
+  }
+  std::vector<hipStream_t> made;
+  hipError_t err = hipSuccess;
+  for (int i = (int)std::min<size_t>(have, (size_t)n); i < n && err == hipSuccess; ++i) {
+    hipStream_t s = nullptr;
+    err = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    if (err != hipSuccess) break;
+    made.push_back(s);
+    hipLaunchKernelGGL(k_noop, dim3(1), dim3(64), 0, s);
+    err = hipGetLastError();
+  }
+  for (hipStream_t s : made) (void)hipStreamSynchronize(s);
+  if ((size_t)n > have) {
+    std::lock_guard<std::mutex> lk(g_stream_mu);
+    if ((size_t)device >= g_stream_pool.size()) g_stream_pool.resize((size_t)device + 1);
+    for (hipStream_t s : made) g_stream_pool[device].push_back(s);  // (at most 16: n <= 16)
+    --g_prewarming;
+  }
+  g_stream_cv.notify_all();
+  if (err != hipSuccess) return hip_fail(err, "blp_stream_prewarm", __FILE__, __LINE__);
+  // then the code objects of similarity.main's kernels, in the order it first launches them
   // (BLP_NO_PRELOAD=1: A/B knob, each loads on its first launch instead)
   if (!getenv("BLP_NO_PRELOAD"))
     for (int (*f)() : {preload_ingest, preload_csr, preload_graph, preload_hot, preload_node2, preload_wedge,
                        preload_pairs, preload_hop3, preload_repr})
       if (f()) return fail(BLP_E_HIP_BASE, "blp_stream_prewarm: kernel code object load failed");
-  // Top the pool up to n streams, and run one empty kernel on each new stream: the first work on
-  // a fresh stream waited 16-26 ms to start in similarity.main (the CSR build's first sync,
-  // profiles/r05_e2e_slow_calls.txt), so the prewarm thread pays that instead. Streams the pool
-  // already holds were used before (BLP_PREWARM_ALWAYS=1: always create n, the round-4 behaviour).
-  size_t have = 0;
-  {
-    std::lock_guard<std::mutex> lk(g_stream_mu);
-    if ((size_t)device < g_stream_pool.size()) have = g_stream_pool[device].size();
-  }
-  if (getenv("BLP_PREWARM_ALWAYS")) have = 0;
-  std::vector<hipStream_t> made;
-  for (int i = (int)std::min<size_t>(have, (size_t)n); i < n; ++i) {
-    hipStream_t s = nullptr;
-    BLP_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-    made.push_back(s);
-    hipLaunchKernelGGL(k_noop, dim3(1), dim3(64), 0, s);
-    BLP_HIP(hipGetLastError());
-  }
-  for (hipStream_t s : made) stream_give(device, s);  // synchronizes each
   return BLP_OK;
 }
 

@@ -264,7 +264,7 @@ def main(example_file, graph_file, u_methods, u_outfiles, b_methods, b_outfiles,
     if os.environ.get("BLP_NO_PREWARM"):  # A/B knob: the HIP runtime only
         pool.submit(blp.device_sync, 0)
     else:
-        pool.submit(blp.prewarm, 0, 4)  # the HIP runtime and the pooled streams (graph, parse, CSR, batches)
+        pool.submit(blp.prewarm, 0, 3)  # the HIP runtime, the pooled streams (parse / CSR / fetch in turn, the graph, two batches at most 3 at once) and the kernels' code objects
     ex = G = None
     try:
         print("Loading graph...")
