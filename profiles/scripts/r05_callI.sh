@@ -1,0 +1,16 @@
+#!/bin/bash
+# Round 5 call I: config-2 similarity.main with the prewarm latch (stream_take waits while the prewarm
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+cd $R || exit 1
+mkdir -p gpurun_out
+e2e() {  # name, env...
+  local n=$1
+  shift
+  env BLP_SLOW_HIP_MS=3 BLP_GRAPH_PROF=1 "$@" timeout -k 10 300 python bench.py --mode e2e --config c2 > gpurun_out/r05i_$n.json 2> gpurun_out/r05i_$n.err || { tail -20 gpurun_out/r05i_$n.err; exit 1; }
+  python -c "import json;d=json.loads(open('gpurun_out/r05i_$n.json').read().strip().splitlines()[-1]);print('$n', round(d['e2e_s'],4), {k: round(v,4) for k,v in d['phases_s'].items()}, d['ok'])"
+}
+for i in 1 2 3; do
+  e2e def_$i
+  e2e nopre_$i BLP_NO_PREWARM=1
+done
