@@ -548,3 +548,41 @@ def test_batch_pair_equals_two_batches(gpu):
         for bt in (ub, bb, u1, b1):
             bt.close()
     _check_against_oracle(a, b, x[perm], y[perm])
+
+
+@pytest.mark.parametrize("cache_mb", ["0", "1", "8192"])
+def test_device_scratch_cache_budgets(gpu, cache_mb):
+    """The device scratch cache (released DevBuf blocks kept for reuse, graph.hip): no cache (0),
+    a budget too small for most blocks (1 MiB: freed as before), and the default. In a child
+    process (the budget is read once): both passes scored repeatedly through create / score /
+    destroy cycles that reuse the cached blocks, every score equal to the C oracle's."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = r'''
+import os, sys
+import numpy as np
+sys.path[:0] = [os.path.join(ROOT, "bipartite-link-prediction_amd"), os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")]
+import blp, coracle
+from helpers import bipartite_edges, dense_edges
+rng = np.random.default_rng(7)
+a, b = bipartite_edges(rng, 40000, 2000, 300000)
+G = blp.DeviceGraph(a, b)
+ids, oa, ob = dense_edges(a, b)
+og = coracle.OracleGraph(len(ids), oa, ob)
+nu = G.n_col0
+for rep in range(3):
+    x = np.repeat(rng.choice(nu, 100 + 50 * rep, replace=False), 25).astype(np.int32)
+    y = rng.integers(nu, G.n, len(x)).astype(np.int32)
+    for xs, ys in ((x, y), (y, x)):
+        got = G.score_pairs(xs, ys, 7)
+        cn, jac, aa, _ = og.score_pairs(np.searchsorted(ids, G.node_ids[xs]), np.searchsorted(ids, G.node_ids[ys]), 7)
+        assert np.array_equal(got["cn"], cn) and np.array_equal(got["jaccard"], jac) and np.array_equal(got["adamic"], aa)
+G.close()
+print("OK")
+'''
+    env = dict(os.environ, BLP_DEV_CACHE_MB=cache_mb)
+    r = subprocess.run([sys.executable, "-c", "ROOT = %r\n" % root + code], env=env, cwd=root, capture_output=True,
+                       text=True, timeout=240)
+    assert r.returncode == 0 and "OK" in r.stdout, (r.stdout[-2000:], r.stderr[-2000:])

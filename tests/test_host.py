@@ -276,3 +276,36 @@ def test_device_edge_load_small_files_stay_on_host(tmp_path):
     assert got.keys() == exp.keys()
     for k in got:
         np.testing.assert_array_equal(got[k], exp[k])
+
+
+@pytest.mark.parametrize("thp", ["1", "0"])
+def test_host_alloc_arrays(thp, monkeypatch):
+    """blp_host_alloc / blp_host_free (huge-page host memory for result arrays; BLP_NO_THP=1:
+    malloc) behind blp._lib.host_empty: shapes, dtypes, writable, independent, released with the
+    last view; sizes below and above the 4 MiB huge-page threshold, and zero."""
+    import subprocess
+    import sys
+
+    code = r'''
+import gc, numpy as np
+from blp import _lib
+for shape, dt in [(0, np.uint8), (10, np.uint32), ((1 << 20, 24), np.uint8), (3_000_001, np.float64)]:
+    a = _lib.host_empty(shape, dt)
+    b = _lib.host_empty(shape, dt)
+    assert a.shape == ((shape,) if np.isscalar(shape) else shape) and a.dtype == dt and a.flags["C_CONTIGUOUS"]
+    a[...] = 1
+    b[...] = 2
+    assert (a == 1).all() and (b == 2).all()
+    v = a.reshape(-1)[: max(a.size // 2, 0)]
+    del a
+    gc.collect()
+    assert (v == 1).all()  # a view keeps the block alive
+    del v, b
+print("ok")
+'''
+    env = dict(os.environ, PYTHONPATH=os.pathsep.join([os.path.join(os.path.dirname(__file__), "..",
+                                                                   "bipartite-link-prediction_amd")]))
+    if thp == "0":
+        env["BLP_NO_THP"] = "1"
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
