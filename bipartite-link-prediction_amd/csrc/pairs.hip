@@ -3274,6 +3274,7 @@ enum Variant { V_SMALL = 0, V_MED = 1, V_LARGE = 2 };
 constexpr int CAP_SMALL = 4096, CAP_MED = 16384, CAP_LARGE = 33792;  // 1.08M bits: fits 160 KiB with the exact AA words
 constexpr int BLOCK_SMALL = 256, BLOCK_MED = 512, BLOCK_LARGE = 1024;
 constexpr int HS_BLOCK = 512, HS_HT = 16384;  // hash-set scorer: 64 KiB table, two workgroups per CU
+constexpr int HS_BLOCK_BIG = 1024, HS_HT_BIG = 32768;  // ... 128 KiB table, one per CU (BLP_HASH_BIG)
 #ifndef BLP_SEG_LARGE
 #define BLP_SEG_LARGE 512  // (experiment builds override it: pairs per scan segment of the large scorer)
 #endif
@@ -3310,6 +3311,7 @@ struct Knobs {
   bool no_wbm_batch = false;     // BLP_NO_WBM_BATCH: no wedge-row bitmaps as pre-built H2 sets
   bool group_buckets = false;    // BLP_GROUP_BUCKETS: one workgroup per contiguous bucket
   bool no_hash = false;          // BLP_NO_HASH: no hash-set scorer in split batches
+  bool hash_big = false;         // BLP_HASH_BIG: the 128 KiB-table hash-set scorer (1024 threads, build <= 16K ids)
   int64_t hash_work = -1;        // BLP_HASH_WORK: hash-set routing bound (build ids)
   bool no_wcodes = false;        // BLP_NO_WCODES: plain ids (per-hit weight gathers)
   bool split_nopk = false;       // BLP_SPLIT_NOPK: unpacked split partials
@@ -3351,6 +3353,7 @@ Knobs read_knobs() {
   k.no_wbm_batch = on("BLP_NO_WBM_BATCH");
   k.group_buckets = on("BLP_GROUP_BUCKETS");
   k.no_hash = on("BLP_NO_HASH");
+  k.hash_big = on("BLP_HASH_BIG");
   k.hash_work = num("BLP_HASH_WORK", -1);
   k.no_wcodes = on("BLP_NO_WCODES");
   k.split_nopk = on("BLP_SPLIT_NOPK");
@@ -3845,13 +3848,14 @@ static int batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_
   // work bounds the distinct ids inserted; at most HT - 1 keeps an empty slot, so every insert
   // and probe chain ends (the knob is clamped: a fuller table is slower, never unbounded)
   const bool want_hash = b->split && n_pairs && !kn.no_hash;
-  const int64_t hash_want = kn.hash_work >= 0 ? kn.hash_work : HS_HT / 2;
+  const int64_t hs_ht = kn.hash_big ? HS_HT_BIG : HS_HT;
+  const int64_t hash_want = kn.hash_work >= 0 ? kn.hash_work : hs_ht / 2;
 #ifdef BLP_DEBUG
   // debug builds take the knob unclamped, so a test can overfill the table and see the probe
   // bound (PS_OK site 8) report it instead of a spin
-  const int64_t hash_cap = kn.hash_work >= 0 ? kn.hash_work : std::min<int64_t>(std::max<int64_t>(1, hash_want), HS_HT - 1);
+  const int64_t hash_cap = kn.hash_work >= 0 ? kn.hash_work : std::min<int64_t>(std::max<int64_t>(1, hash_want), hs_ht - 1);
 #else
-  const int64_t hash_cap = std::min<int64_t>(std::max<int64_t>(1, hash_want), HS_HT - 1);
+  const int64_t hash_cap = std::min<int64_t>(std::max<int64_t>(1, hash_want), hs_ht - 1);
 #endif
   b->xlo = xlo;
   b->xspan = (int64_t)xhi - xlo;
@@ -4443,8 +4447,14 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
       BLP_HIP(hipGetLastError());
       a.active = b->d_active2;
       int hcu = 1;
-      BLP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&hcu, k_score_hash<HS_BLOCK, HS_HT>, HS_BLOCK, 0));
-      hipLaunchKernelGGL((k_score_hash<HS_BLOCK, HS_HT>), dim3(scu * std::max(hcu, 1)), dim3(HS_BLOCK), 0, b->stream, a);
+      if (b->kn.hash_big) {
+        BLP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&hcu, k_score_hash<HS_BLOCK_BIG, HS_HT_BIG>, HS_BLOCK_BIG, 0));
+        hipLaunchKernelGGL((k_score_hash<HS_BLOCK_BIG, HS_HT_BIG>), dim3(scu * std::max(hcu, 1)), dim3(HS_BLOCK_BIG), 0,
+                           b->stream, a);
+      } else {
+        BLP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&hcu, k_score_hash<HS_BLOCK, HS_HT>, HS_BLOCK, 0));
+        hipLaunchKernelGGL((k_score_hash<HS_BLOCK, HS_HT>), dim3(scu * std::max(hcu, 1)), dim3(HS_BLOCK), 0, b->stream, a);
+      }
       BLP_HIP(hipGetLastError());
     }
     if (!pk24) BLP_HIP(hipMemsetAsync(b->d_pcn, 0, 4 * (size_t)np, b->stream));

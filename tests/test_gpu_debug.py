@@ -61,6 +61,7 @@ def _run(mode, extra):
 @pytest.mark.parametrize("mode,extra", [
     ("default", {}),
     ("split+hash", {"BLP_SPLIT": "3"}),
+    ("split+hash big", {"BLP_SPLIT": "3", "BLP_HASH_BIG": "1"}),
     ("split big", {"BLP_SPLIT": "3", "BLP_SPLIT_BIG": "1", "BLP_NO_HASH": "1"}),
     ("split heavy", {"BLP_SPLIT": "8", "BLP_HEAVY_WORK": "50", "BLP_NO_HASH": "1"}),
     ("large", {"BLP_VARIANT": "2"}),

@@ -115,6 +115,8 @@ def test_general_graph_exact_distance(gpu):
     {"BLP_SPLIT": "24", "BLP_SPLIT_BIG": "1", "BLP_NO_HASH": "1"},          # ... same, many chunks
     {"BLP_SPLIT": "3", "BLP_SPLIT_BIG": "1", "BLP_NO_HASH": "1", "BLP_NO_WEDGE": "1"},  # ... members' rows from the CSR, not wedge rows
     {"BLP_SPLIT": "3", "BLP_SPLIT_BIG": "1", "BLP_HASH_WORK": "600", "BLP_NO_WEDGE": "1"},  # hash-set build from the CSR
+    {"BLP_SPLIT": "3", "BLP_HASH_BIG": "1"},                                # 128 KiB hash tables (1024 threads)
+    {"BLP_SPLIT": "3", "BLP_HASH_BIG": "1", "BLP_NO_WEDGE": "1"},           # ... built from the CSR
     {"BLP_HEAVY_WORK": "50"},                           # heavy sources pre-built by k_heavy
     {"BLP_HEAVY_WORK": "1"},                            # one row per heavy item
     {"BLP_CHUNK_BITS": "2048", "BLP_HEAVY_WORK": "50", "BLP_NO_GLOBAL": "1"},  # multi-chunk: no heavy path
