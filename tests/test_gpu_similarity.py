@@ -588,3 +588,41 @@ print("OK")
     r = subprocess.run([sys.executable, "-c", "ROOT = %r\n" % root + code], env=env, cwd=root, capture_output=True,
                        text=True, timeout=240)
     assert r.returncode == 0 and "OK" in r.stdout, (r.stdout[-2000:], r.stderr[-2000:])
+
+
+def test_prewarm_concurrent_with_batches(gpu):
+    """blp_stream_prewarm on other threads while batches are created, scored and destroyed (the
+    pool's latch: stream_take waits while a prewarm creates streams; similarity.main prewarms on
+    a spare thread): no deadlock, and every score equal to the single-threaded ones."""
+    import threading
+
+    rng = np.random.default_rng(29)
+    a, b = bipartite_edges(rng, 20000, 1000, 150000)
+    G = blp.DeviceGraph(a, b)
+    nu = G.n_col0
+    x = np.repeat(np.sort(rng.choice(nu, 80, replace=False)), 20).astype(np.int32)
+    y = rng.integers(nu, G.n, len(x)).astype(np.int32)
+    ref = G.score_pairs(x, y, 7)
+    errs = []
+
+    def warm():
+        try:
+            for _ in range(3):
+                blp.prewarm(gpu, 16)
+        except Exception as e:  # pragma: no cover - reported below
+            errs.append(e)
+
+    th = [threading.Thread(target=warm) for _ in range(2)]
+    for t in th:
+        t.start()
+    for _ in range(4):
+        ub, bb = G.batch_pair(x, y)
+        G.score_batches([(ub, 7), (bb, 3)])
+        got = ub.fetch(7)
+        for k in ref:
+            np.testing.assert_array_equal(got[k], ref[k])
+        ub.close()
+        bb.close()
+    for t in th:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in th) and not errs, errs
