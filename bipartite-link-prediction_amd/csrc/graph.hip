@@ -572,12 +572,19 @@ int blp_stream_prewarm(int device, int n) {
     err = hipGetLastError();
   }
   for (hipStream_t s : made) (void)hipStreamSynchronize(s);
+  std::vector<hipStream_t> extra;  // past the pool's cap (concurrent prewarms): destroyed
   if ((size_t)n > have) {
     std::lock_guard<std::mutex> lk(g_stream_mu);
     if ((size_t)device >= g_stream_pool.size()) g_stream_pool.resize((size_t)device + 1);
-    for (hipStream_t s : made) g_stream_pool[device].push_back(s);  // (at most 16: n <= 16)
+    for (hipStream_t s : made) {
+      if (g_stream_pool[device].size() < STREAM_POOL_CAP)
+        g_stream_pool[device].push_back(s);
+      else
+        extra.push_back(s);
+    }
     --g_prewarming;
   }
+  for (hipStream_t s : extra) (void)hipStreamDestroy(s);
   g_stream_cv.notify_all();
   if (err != hipSuccess) return hip_fail(err, "blp_stream_prewarm", __FILE__, __LINE__);
   // then the code objects of similarity.main's kernels, in the order it first launches them
