@@ -18,3 +18,5 @@ for i in 1 2 3; do
   timeout -k 10 300 python bench.py --mode e2e --config c2 > gpurun_out/r05fin_e2e_$i.json 2> gpurun_out/r05fin_e2e_$i.err || { tail -20 gpurun_out/r05fin_e2e_$i.err; exit 1; }
   python -c "import json;d=json.loads(open('gpurun_out/r05fin_e2e_$i.json').read().strip().splitlines()[-1]);print('e2e', round(d['e2e_s'],4), {k: round(v,4) for k,v in d['phases_s'].items()}, d['ok'])"
 done
+timeout -k 10 300 python bench.py --mode e2e --config yelp > gpurun_out/r05fin_e2e_yelp.json 2> gpurun_out/r05fin_e2e_yelp.err || { tail -20 gpurun_out/r05fin_e2e_yelp.err; exit 1; }
+python -c "import json;d=json.loads(open('gpurun_out/r05fin_e2e_yelp.json').read().strip().splitlines()[-1]);print('e2e yelp', round(d['e2e_s'],4), d['ok'])"
