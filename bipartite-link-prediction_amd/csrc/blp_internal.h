@@ -51,6 +51,7 @@ void slow_check(int64_t t0, const char* what, const char* file, int line);
 struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
+  int dev = -1;  // the device the block belongs to (release returns it to that device's cache)
   int reserve(size_t want);
   void release();
   template <class T> T* as() const { return reinterpret_cast<T*>(p); }

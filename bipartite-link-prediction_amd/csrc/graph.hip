@@ -135,6 +135,7 @@ int DevBuf::reserve(size_t want) {
       if (it != c.blocks.end() && it->first <= 2 * sz) {
         p = it->second;
         bytes = it->first;
+        this->dev = dev;
         c.bytes -= it->first;
         c.blocks.erase(it);
         return BLP_OK;
@@ -149,9 +150,11 @@ int DevBuf::reserve(size_t want) {
   }
   if (e != hipSuccess) {
     p = nullptr;
+    this->dev = -1;
     return hip_fail(e, "hipMalloc (DevBuf)", __FILE__, __LINE__);
   }
   bytes = sz;
+  this->dev = dev;
   return BLP_OK;
 }
 
@@ -160,10 +163,15 @@ void DevBuf::release() {
     const int64_t t0 = slow_clock();
     bool kept = false;
     const size_t budget = dc_budget();
-    if (budget && bytes <= budget) {
-      const int dev = current_device();
-      // what hipFree implied: nothing queued on the device still reads the block
-      if (hipDeviceSynchronize() == hipSuccess) {
+    if (budget && bytes <= budget && dev >= 0) {
+      // what hipFree implied: nothing queued on the device still reads the block (the block's
+      // own device: the caller may have another one current)
+      int cur = -1;
+      (void)hipGetDevice(&cur);
+      if (cur != dev) (void)hipSetDevice(dev);
+      const bool synced = hipDeviceSynchronize() == hipSuccess;
+      if (cur != dev && cur >= 0) (void)hipSetDevice(cur);
+      if (synced) {
         std::lock_guard<std::mutex> lk(g_dc_mu);
         if ((size_t)dev >= g_dc.size()) g_dc.resize((size_t)dev + 1);
         DevCache& c = g_dc[dev];
@@ -179,6 +187,7 @@ void DevBuf::release() {
   }
   p = nullptr;
   bytes = 0;
+  dev = -1;
 }
 
 int set_device(const blp_graph* g) {
