@@ -111,6 +111,7 @@ int blp::csr_build(int device, const int32_t* d_a, const int32_t* d_b, int64_t m
   BLP_HIP_OR(hipMemsetAsync(flag.p, 0, 4, st), done);
   BLP_HIP_OR(hipMemsetAsync(c->d_rp, 0, 8 * (n + 1), st), done);
   int64_t nnz = 0;
+  const uint64_t* uq = nullptr;  // the unique sorted keys (in keys or sorted)
   if (m) {
     if ((rc = keys.reserve(8 * mk)) || (rc = sorted.reserve(8 * mk))) return done(rc);
     hipLaunchKernelGGL(k_edge_keys, dim3(4096), dim3(256), 0, st, d_a, d_b, m, n, keys.as<uint64_t>(), c->d_self,
@@ -121,17 +122,19 @@ int blp::csr_build(int device, const int32_t* d_a, const int32_t* d_b, int64_t m
     while ((int64_t(1) << idbits) < n) ++idbits;
     const int end_bit = std::min(64, 32 + idbits + 1);
     size_t tb = 0, tb2 = 0;
-    BLP_HIP_OR(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, keys.as<uint64_t>(), sorted.as<uint64_t>(), mk, 0,
-                                                 end_bit, st), done);
-    BLP_HIP_OR(hipcub::DeviceSelect::Unique(nullptr, tb2, sorted.as<uint64_t>(), keys.as<uint64_t>(),
-                                            nsel.as<int64_t>(), mk, st), done);
+    // the sort ping-pongs between the two key buffers (no third one of the same size inside the
+    // temporary storage), then the unique keys go to whichever buffer the sorted ones are not in
+    hipcub::DoubleBuffer<uint64_t> kb(keys.as<uint64_t>(), sorted.as<uint64_t>());
+    BLP_HIP_OR(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, kb, mk, 0, end_bit, st), done);
+    BLP_HIP_OR(hipcub::DeviceSelect::Unique(nullptr, tb2, kb.Current(), kb.Alternate(), nsel.as<int64_t>(), mk, st),
+               done);
     if ((rc = temp.reserve(std::max(tb, tb2)))) return done(rc);
     tb = temp.bytes;
-    BLP_HIP_OR(hipcub::DeviceRadixSort::SortKeys(temp.p, tb, keys.as<uint64_t>(), sorted.as<uint64_t>(), mk, 0,
-                                                 end_bit, st), done);
+    BLP_HIP_OR(hipcub::DeviceRadixSort::SortKeys(temp.p, tb, kb, mk, 0, end_bit, st), done);
     tb2 = temp.bytes;
-    BLP_HIP_OR(hipcub::DeviceSelect::Unique(temp.p, tb2, sorted.as<uint64_t>(), keys.as<uint64_t>(),
-                                            nsel.as<int64_t>(), mk, st), done);
+    BLP_HIP_OR(hipcub::DeviceSelect::Unique(temp.p, tb2, kb.Current(), kb.Alternate(), nsel.as<int64_t>(), mk, st),
+               done);
+    uq = kb.Alternate();
     int64_t nu = 0;
     int bad = 0;
     BLP_HIP_OR(hipMemcpyAsync(&nu, nsel.p, 8, hipMemcpyDeviceToHost, st), done);
@@ -141,20 +144,20 @@ int blp::csr_build(int device, const int32_t* d_a, const int32_t* d_b, int64_t m
     nnz = nu;
     if (nnz > 0) {  // a trailing KEY_NONE (self-loops present) is not an entry
       uint64_t last = 0;
-      BLP_HIP_OR(hipMemcpyAsync(&last, keys.as<uint64_t>() + nnz - 1, 8, hipMemcpyDeviceToHost, st), done);
+      BLP_HIP_OR(hipMemcpyAsync(&last, uq + nnz - 1, 8, hipMemcpyDeviceToHost, st), done);
       BLP_HIP_OR(hipStreamSynchronize(st), done);
       if (last == KEY_NONE) --nnz;
     }
-    sorted.release();
+    (uq == keys.as<uint64_t>() ? sorted : keys).release();  // the buffer not holding the unique keys
     temp.release();
-    hipLaunchKernelGGL(k_row_ptr, dim3(2048), dim3(256), 0, st, keys.as<uint64_t>(), nnz, n, c->d_rp);
+    hipLaunchKernelGGL(k_row_ptr, dim3(2048), dim3(256), 0, st, uq, nnz, n, c->d_rp);
     BLP_HIP_OR(hipGetLastError(), done);
   }
   BLP_HIP_OR(hipMalloc(&c->d_ci, sizeof(int32_t) * (nnz + 2 * CI_PAD)), done);
   c->d_ci += CI_PAD;
   BLP_HIP_OR(hipMemsetAsync(c->d_ci - CI_PAD, 0, sizeof(int32_t) * (nnz + 2 * CI_PAD), st), done);
   if (nnz) {
-    hipLaunchKernelGGL(k_low_halves, dim3(4096), dim3(256), 0, st, keys.as<uint64_t>(), nnz, c->d_ci);
+    hipLaunchKernelGGL(k_low_halves, dim3(4096), dim3(256), 0, st, uq, nnz, c->d_ci);
     BLP_HIP_OR(hipGetLastError(), done);
   }
   BLP_HIP_OR(hipStreamSynchronize(st), done);

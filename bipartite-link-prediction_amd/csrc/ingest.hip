@@ -456,7 +456,7 @@ int device_load(const char* path, int device, blp_edges** out) {
   }
   stage("read");
   hipStream_t st = nullptr;
-  ScopedBuf txt, blk, blk_off, tmp, nl, a, b, stats, in0, in1, cnt, base, map, ids;
+  ScopedBuf txt, blk, blk_off, tmp, nl, ab, stats, in0, in1, cnt, base, map, ids;
   blp_edges* e = nullptr;
   // BLP_PARSE_MEM_CAP (test knob): device memory the parse may take, in bytes; past it a
   // reservation fails as out of memory would, and the host parser takes the file
@@ -508,7 +508,11 @@ int device_load(const char* path, int device, blp_edges** out) {
     BLP_HIP(hipStreamSynchronize(st));
     const int64_t L = (int64_t)(last[0] + last[1]);
     if (L < 1 || L >= (int64_t(1) << 31)) return BLP_OK;
-    if ((rc = nl.reserve(8 * L)) || (rc = a.reserve(8 * L)) || (rc = b.reserve(8 * L)) ||
+    // the raw endpoint ids as one block (a, then b) and the line offsets, each 16 B per line: the
+    // CSR build's two sort buffers (2 x 8 B keys per edge, csr.hip) reuse exactly these blocks
+    // from the device scratch cache instead of fresh VRAM (whose first use can wait for the
+    // driver's clear)
+    if ((rc = nl.reserve(16 * L)) || (rc = ab.reserve(16 * L)) ||
         (rc = stats.reserve(sizeof(ParseStats))))
       return rc;
     hipLaunchKernelGGL(k_nl_pos, dim3((unsigned)nb), dim3(NL_BLOCK), 0, st, d_txt, blk_off.as<uint64_t>(),
@@ -517,7 +521,7 @@ int device_load(const char* path, int device, blp_edges** out) {
     ParseStats ps{~0ull, 0ull, 0u};
     BLP_HIP(hipMemcpyAsync(stats.p, &ps, sizeof ps, hipMemcpyHostToDevice, st));
     hipLaunchKernelGGL(k_parse_lines, dim3(grid_for(L, n_cu)), dim3(256), 0, st, d_txt, nl.as<int64_t>(), L,
-                       a.as<int64_t>(), b.as<int64_t>(), stats.as<ParseStats>());
+                       ab.as<int64_t>(), ab.as<int64_t>() + L, stats.as<ParseStats>());
     BLP_HIP(hipGetLastError());
     BLP_HIP(hipMemcpyAsync(&ps, stats.p, sizeof ps, hipMemcpyDeviceToHost, st));
     BLP_HIP(hipStreamSynchronize(st));
@@ -534,7 +538,7 @@ int device_load(const char* path, int device, blp_edges** out) {
       return rc;
     BLP_HIP(hipMemsetAsync(in0.p, 0, 4 * W, st));
     BLP_HIP(hipMemsetAsync(in1.p, 0, 4 * W, st));
-    hipLaunchKernelGGL(k_mark, dim3(grid_for(L, n_cu)), dim3(256), 0, st, a.as<int64_t>(), b.as<int64_t>(), L, lo,
+    hipLaunchKernelGGL(k_mark, dim3(grid_for(L, n_cu)), dim3(256), 0, st, ab.as<int64_t>(), ab.as<int64_t>() + L, L, lo,
                        in0.as<uint32_t>(), in1.as<uint32_t>());
     BLP_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_word_counts, dim3(grid_for(W, n_cu)), dim3(256), 0, st, in0.as<uint32_t>(),
@@ -558,7 +562,7 @@ int device_load(const char* path, int device, blp_edges** out) {
     e->device = device;
     BLP_HIP(hipMalloc(&e->d_da, 4 * L));
     BLP_HIP(hipMalloc(&e->d_db, 4 * L));
-    hipLaunchKernelGGL(k_dense, dim3(grid_for(L, n_cu)), dim3(256), 0, st, a.as<int64_t>(), b.as<int64_t>(), L, lo,
+    hipLaunchKernelGGL(k_dense, dim3(grid_for(L, n_cu)), dim3(256), 0, st, ab.as<int64_t>(), ab.as<int64_t>() + L, L, lo,
                        map.as<int32_t>(), e->d_da, e->d_db);
     BLP_HIP(hipGetLastError());
     e->node_ids.resize((size_t)n);
