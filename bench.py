@@ -1109,6 +1109,9 @@ def main():
         (len(ex_x), len(np.unique(ex_x)), int(ex_l.sum()), t_ex, hop3_ms / max(hop3_n, 1)))
 
     passes = []
+    # the kernels' code objects and the pooled streams, as similarity.main's prewarm thread loads
+    # them: a one-off cost of the process, not of a pair list
+    blp.prewarm(dev, 3)
     t0 = time.time()
     b_mask = 7 if getattr(args, "fix_adamic", False) else 3
     if args.sides == "both":  # one upload of the pairs for both passes (blp_batch_create_pair)
