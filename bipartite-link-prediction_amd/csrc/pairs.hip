@@ -3561,18 +3561,10 @@ extern "C" {
 
 }  // extern "C"
 
-// The pair arrays already in HBM (blp_batch_create_pair: one upload for both batches): device
-// copies d_x / d_y, ready once `ready` (recorded on the uploading stream) has completed.
-struct DevPairs {
-  const int32_t* d_x;
-  const int32_t* d_y;
-  hipEvent_t ready;
-};
-
-// blp_batch_create, and each batch of blp_batch_create_pair: with `src` (or null) the pairs are
-// taken from device arrays (a device-to-device copy on this batch's stream once src->ready has
-// completed) instead of a host-to-device upload.
-static int batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n_pairs, const DevPairs* src,
+// blp_batch_create, and blp_batch_create_pair's second batch: `twin` (or null) is a batch of the
+// same pairs with x and y swapped whose device copies are taken (a device-to-device copy after the
+// twin's upload, on this batch's stream) instead of a second host-to-device upload.
+static int batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n_pairs, const blp_batch* twin,
                         blp_batch** out, bool retry = false) {
   BLP_CHECK(g && out && n_pairs >= 0 && (n_pairs == 0 || (x && y)), BLP_E_ARG, "blp_batch_create: bad arguments");
   BLP_CHECK(n_pairs < (int64_t(1) << 31) - 1, BLP_E_ARG, "blp_batch_create: at most 2^31-2 pairs per batch");
@@ -3612,10 +3604,15 @@ static int batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_
   if (hipMalloc(&b->d_x, 4 * np) != hipSuccess || hipMalloc(&b->d_y, 4 * np) != hipSuccess ||
       hipMalloc(&b->d_misc, sizeof(Misc)) != hipSuccess)
     return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: hipMalloc failed"));
-  if (n_pairs && src) {  // the shared upload's device copies, once it is done
-    BLP_HIP_OR(hipStreamWaitEvent(b->stream, src->ready, 0), bail);
-    BLP_HIP_OR(hipMemcpyAsync(b->d_x, src->d_x, 4 * n_pairs, hipMemcpyDeviceToDevice, b->stream), bail);
-    BLP_HIP_OR(hipMemcpyAsync(b->d_y, src->d_y, 4 * n_pairs, hipMemcpyDeviceToDevice, b->stream), bail);
+  if (n_pairs && twin) {  // the twin's device copies, swapped, once its upload is done
+    hipEvent_t ev;
+    BLP_HIP_OR(hipEventCreateWithFlags(&ev, hipEventDisableTiming), bail);
+    hipError_t e = hipEventRecord(ev, twin->stream);
+    if (e == hipSuccess) e = hipStreamWaitEvent(b->stream, ev, 0);
+    (void)hipEventDestroy(ev);
+    BLP_HIP_OR(e, bail);
+    BLP_HIP_OR(hipMemcpyAsync(b->d_x, twin->d_y, 4 * n_pairs, hipMemcpyDeviceToDevice, b->stream), bail);
+    BLP_HIP_OR(hipMemcpyAsync(b->d_y, twin->d_x, 4 * n_pairs, hipMemcpyDeviceToDevice, b->stream), bail);
   } else if (n_pairs) {
     if ((rc = copy_sync(b->d_x, x, 4 * n_pairs, hipMemcpyHostToDevice, b->stream)) ||
         (rc = copy_sync(b->d_y, y, 4 * n_pairs, hipMemcpyHostToDevice, b->stream)))
@@ -4086,18 +4083,15 @@ extern "C" {
 // -- when no live batch's plan reads it -- and the batch is planned again without it.
 static bool is_oom(int rc) { return rc == BLP_E_HIP_BASE - (int)hipErrorOutOfMemory; }
 
-// allow_release = false (the concurrent creates of blp_batch_create_pair): an out-of-memory failure
-// stands here, and the caller retries both creates one after the other, where releasing the
-// wedge index cannot race the other create's reads of it
-static int create_or_release(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n, const DevPairs* twin,
-                             blp_batch** out, bool allow_release = true) {
+static int create_or_release(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n, const blp_batch* twin,
+                             blp_batch** out) {
   int rc = batch_create(g, x, y, n, twin, out);
   if (is_oom(rc) && g) {  // the device scratch cache first (DevBuf blocks kept for reuse)
     (void)hipGetLastError();
     dev_cache_flush(g->device);
     rc = batch_create(g, x, y, n, twin, out);
   }
-  if (!is_oom(rc) || !g || !g->d_wp || !allow_release) return rc;
+  if (!is_oom(rc) || !g || !g->d_wp) return rc;
   {
     std::lock_guard<std::mutex> lk(g->wbm_mu);
     if (g->wedge_users > 0) return rc;  // a live batch reads it: the failure stands
@@ -4113,80 +4107,16 @@ int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n
   return create_or_release(g, x, y, n_pairs, nullptr, out);
 }
 
-// One upload of the pairs into shared device arrays, then both batches planned at once on two host
-// threads, each copying the shared arrays on its own stream (x, y for the first; swapped for the
-// second): the planning passes' device work and host round trips overlap (BLP_PAIR_SERIAL=1: one
-// after the other).
 int blp_batch_create_pair(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n_pairs, blp_batch** out_xy,
                           blp_batch** out_yx) {
-  BLP_CHECK(g && out_xy && out_yx && n_pairs >= 0 && (n_pairs == 0 || (x && y)), BLP_E_ARG,
-            "blp_batch_create_pair: bad arguments");
-  int rc = set_device(g);
+  BLP_CHECK(out_xy && out_yx, BLP_E_ARG, "blp_batch_create_pair: null outputs");
+  blp_batch* a = nullptr;
+  int rc = create_or_release(g, x, y, n_pairs, nullptr, &a);
   if (rc) return rc;
-  if (n_pairs == 0) {
-    blp_batch *a = nullptr, *b = nullptr;
-    if ((rc = create_or_release(g, x, y, 0, nullptr, &a))) return rc;
-    if ((rc = create_or_release(g, y, x, 0, nullptr, &b))) {
-      blp_batch_destroy(a);
-      return rc;
-    }
-    *out_xy = a;
-    *out_yx = b;
-    return BLP_OK;
-  }
-  ScopedBuf dx, dy;
-  if ((rc = dx.reserve(4 * (size_t)n_pairs)) || (rc = dy.reserve(4 * (size_t)n_pairs))) return rc;
-  hipStream_t st = stream_take(g->device);
-  if (!st) return BLP_E_HIP_BASE;
-  hipEvent_t ev = nullptr;
-  rc = copy_sync(dx.p, x, 4 * (size_t)n_pairs, hipMemcpyHostToDevice, st);
-  if (!rc) rc = copy_sync(dy.p, y, 4 * (size_t)n_pairs, hipMemcpyHostToDevice, st);
-  if (!rc && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) rc = fail(BLP_E_HIP_BASE, "hipEventCreate");
-  if (!rc && hipEventRecord(ev, st) != hipSuccess) rc = fail(BLP_E_HIP_BASE, "hipEventRecord");
+  blp_batch* b = nullptr;
+  rc = create_or_release(g, y, x, n_pairs, a, &b);
   if (rc) {
-    if (ev) (void)hipEventDestroy(ev);
-    stream_give(g->device, st);
-    return rc;
-  }
-  const DevPairs pxy{dx.as<int32_t>(), dy.as<int32_t>(), ev}, pyx{dy.as<int32_t>(), dx.as<int32_t>(), ev};
-  blp_batch *a = nullptr, *b = nullptr;
-  int rc_b = BLP_OK;
-  std::string err_b;
-  bool serial = getenv("BLP_PAIR_SERIAL") != nullptr;
-  if (!serial) {
-    std::thread t([&]() {
-      if (hipSetDevice(g->device) != hipSuccess) {
-        rc_b = fail(BLP_E_HIP_BASE, "blp_batch_create_pair: hipSetDevice");
-      } else {
-        rc_b = create_or_release(g, y, x, n_pairs, &pyx, &b, false);
-      }
-      if (rc_b) err_b = blp_last_error();
-    });
-    rc = create_or_release(g, x, y, n_pairs, &pxy, &a, false);
-    t.join();
-    if (is_oom(rc) || is_oom(rc_b)) {  // out of memory: both again, one after the other (wedge release allowed)
-      blp_batch_destroy(a);
-      blp_batch_destroy(b);
-      a = b = nullptr;
-      rc = rc_b = BLP_OK;
-      err_b.clear();
-      serial = true;
-    }
-  }
-  if (serial) {
-    rc = create_or_release(g, x, y, n_pairs, &pxy, &a);
-    if (!rc) rc_b = create_or_release(g, y, x, n_pairs, &pyx, &b);
-    if (rc_b) err_b = blp_last_error();
-  }
-  stream_give(g->device, st);
-  (void)hipEventDestroy(ev);  // both batches' copies were enqueued behind it (and their creates synchronized)
-  if (rc || rc_b) {
     blp_batch_destroy(a);
-    blp_batch_destroy(b);
-    if (!rc) {
-      set_error(err_b);
-      rc = rc_b;
-    }
     return rc;
   }
   *out_xy = a;

@@ -526,14 +526,10 @@ def test_device_plan_equals_host_plan(gpu, knobs, monkeypatch):
     _check_against_oracle(a, b, y[perm], x[perm])
 
 
-@pytest.mark.parametrize("serial", ["0", "1"])
-def test_batch_pair_equals_two_batches(gpu, serial, monkeypatch):
-    """blp_batch_create_pair (one upload into shared device arrays, both batches planned at once
-    on two host threads, or one after the other with BLP_PAIR_SERIAL=1) gives the two batches
-    blp_batch_create gives, scores and plans alike, for a source-grouped list and a shuffled one
-    (similarity.main's two passes, similarity.py:20-106)."""
-    if serial == "1":
-        monkeypatch.setenv("BLP_PAIR_SERIAL", "1")
+def test_batch_pair_equals_two_batches(gpu):
+    """blp_batch_create_pair (one upload, the business batch copies the user batch's device
+    arrays swapped) gives the two batches blp_batch_create gives, scores and plans alike, for a
+    source-grouped list and a shuffled one (similarity.main's two passes, similarity.py:20-106)."""
     rng = np.random.default_rng(23)
     a, b = bipartite_edges(rng, 30000, 1500, 300000)
     G = blp.DeviceGraph(a, b)
