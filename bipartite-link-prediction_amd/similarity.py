@@ -189,7 +189,9 @@ def _run_side(examples, G, methods, outfiles, table, side, sidecar=False, scored
 
 def _write_jobs(ex, methods, outfiles, table, present, scores):
     """The score files of one side straight from the device arrays (util.write_json's text):
-    one callable per file."""
+    one callable per file. The jobs take over the score arrays (``scores`` is emptied): each job
+    drops its array when its file is written, so the array is released on that writer thread while
+    the other files are still being written, not all at once after the last one."""
     import os
 
     pres = None if present.all() else present
@@ -209,11 +211,14 @@ def _write_jobs(ex, methods, outfiles, table, present, scores):
         else:  # a method the reference does not match: only missing-node zeros
             args = (scorefile.NONE, pres)
 
-        def job(f=f, args=args):
+        def job(f=f, held=[args]):
+            args = held.pop()  # from here on the only reference this job keeps
             ex.write(f, *args)
+            del args
             if os.path.exists(f + ".npz"):  # as util.write_json: a stale sidecar goes
                 os.unlink(f + ".npz")
         jobs.append(job)
+    scores.clear()
     return jobs
 
 
@@ -225,11 +230,13 @@ def _write_files(jobs):
 
     workers = max(1, int(os.environ.get("BLP_FILE_WRITERS", "6")))  # config 2: 6 -> 0.061-0.068 s, 3 -> 0.093-0.100 s
     if workers == 1 or len(jobs) < 2:
-        for j in jobs:
-            j()
+        while jobs:
+            jobs.pop(0)()
         return
     with ThreadPoolExecutor(min(workers, len(jobs))) as pool:
-        for fut in [pool.submit(j) for j in jobs]:
+        futs = [pool.submit(j) for j in jobs]
+        jobs.clear()  # the executor holds the jobs now: each is released once it has run
+        for fut in futs:
             fut.result()
 
 
