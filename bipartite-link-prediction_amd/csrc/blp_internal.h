@@ -183,11 +183,6 @@ struct blp_graph {
   const int64_t* hrp = nullptr;
   const int32_t* hci = nullptr;  // null until first needed when the graph was created without it (host_col_idx)
   std::mutex mirror_mu;          // held while host_col_idx fetches the column mirror
-  // blp_batches_score's co-scheduled passes each run on a stream with a dedicated hardware queue
-  // (created on first use, full CU mask): pooled streams share the process's few hardware queues,
-  // and two passes whose streams share one run one after the other
-  hipStream_t co_stream[2] = {nullptr, nullptr};
-  std::mutex co_mu;
   blp::KernelTimer timers[blp::K_COUNT];
 };
 

@@ -701,12 +701,6 @@ int blp_graph_destroy(blp_graph* g) {
   if (!g) return BLP_OK;
   (void)hipSetDevice(g->device);
   if (g->stream) (void)hipStreamSynchronize(g->stream);
-  for (hipStream_t& s : g->co_stream)
-    if (s) {
-      (void)hipStreamSynchronize(s);
-      (void)hipStreamDestroy(s);
-      s = nullptr;
-    }
   for (auto& t : g->timers) timer_release(t);
   free_hot_index(g);
   free_wedge_index(g);

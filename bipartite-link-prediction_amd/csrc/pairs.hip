@@ -28,8 +28,6 @@
 #include <numeric>
 #include <thread>
 
-#include <hip/hip_ext.h>
-
 #include "blp_internal.h"
 
 #ifndef BLP_RC
@@ -4553,45 +4551,10 @@ int blp_batches_score(blp_graph* g, int n, blp_batch* const* bs, const uint32_t*
   // chunk-parallel batches (config 5's two passes) each take the whole chip: holding each
   // persistent grid to a CU share was slower at every share tried (1951 ms per config-5 step in
   // proportion to planned work, 864 / 903 ms at 176 / 128 user CUs, against 743 ms)
-  // Two or more passes: the first two run on the graph's co-scheduling streams, each with a
-  // hardware queue of its own (a CU-masked stream is never mapped onto a shared queue), ordered
-  // after the batch's own stream and before its next work by events (BLP_CO_STREAMS=0: each on its
-  // own pooled stream, which may share a queue with the other and then run after it: 3.4 ms
-  // instead of 2.27 at config 2, r05 final check 2).
-  const bool co = n >= 2 && !getenv("BLP_CO_STREAMS_OFF") && !(getenv("BLP_CO_STREAMS") && atoi(getenv("BLP_CO_STREAMS")) == 0);
-  if (co) {
-    int rc = set_device(g);
-    if (rc) return rc;
-    std::lock_guard<std::mutex> lk(g->co_mu);
-    for (int i = 0; i < 2; ++i)
-      if (!g->co_stream[i]) {
-        std::vector<uint32_t> mask((size_t)(g->n_cu + 31) / 32, 0u);
-        for (int c = 0; c < g->n_cu; ++c) mask[(size_t)c / 32] |= 1u << (c % 32);
-        BLP_HIP(hipExtStreamCreateWithCUMask(&g->co_stream[i], (uint32_t)mask.size(), mask.data()));
-      }
-  }
   for (int i = 0; i < n; ++i) {
     blp_batch* b = bs[i];
     b->cus = is_large(b) && t_other > 0.0 ? share : 0;
-    hipStream_t own = b->stream;
-    hipEvent_t ev_in = nullptr, ev_out = nullptr;
-    const bool on_co = co && i < 2;
-    if (on_co) {  // the co stream waits for the batch's own stream, then takes its work
-      BLP_HIP(hipEventCreateWithFlags(&ev_in, hipEventDisableTiming));
-      BLP_HIP(hipEventRecord(ev_in, own));
-      BLP_HIP(hipStreamWaitEvent(g->co_stream[i], ev_in, 0));
-      b->stream = g->co_stream[i];
-    }
-    int rc = blp_batch_score(g, b, masks[i]);
-    if (on_co) {  // ... and the batch's own stream (fetch, the next step) waits for it
-      b->stream = own;
-      hipError_t e = hipEventCreateWithFlags(&ev_out, hipEventDisableTiming);
-      if (e == hipSuccess) e = hipEventRecord(ev_out, g->co_stream[i]);
-      if (e == hipSuccess) e = hipStreamWaitEvent(own, ev_out, 0);
-      (void)hipEventDestroy(ev_in);
-      if (ev_out) (void)hipEventDestroy(ev_out);
-      if (!rc && e != hipSuccess) rc = hip_fail(e, "blp_batches_score: co-stream event", __FILE__, __LINE__);
-    }
+    const int rc = blp_batch_score(g, b, masks[i]);
     b->cus = 0;
     if (rc) return rc;
   }
