@@ -1111,7 +1111,8 @@ def main():
     passes = []
     # the kernels' code objects and the pooled streams, as similarity.main's prewarm thread loads
     # them: a one-off cost of the process, not of a pair list
-    blp.prewarm(dev, 3)
+    if not os.environ.get("BLP_BENCH_NO_PREWARM"):  # (A/B knob)
+        blp.prewarm(dev, 3)
     t0 = time.time()
     b_mask = 7 if getattr(args, "fix_adamic", False) else 3
     if args.sides == "both":  # one upload of the pairs for both passes (blp_batch_create_pair)
