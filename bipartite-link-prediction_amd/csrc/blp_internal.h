@@ -208,8 +208,13 @@ int build_node2(blp_graph* g);  // after build_hot_index (the dense-row flag)
 // and each batch. stream_take returns a pooled stream of `device` (the current device) or a new
 // one (null on failure, the HIP error recorded); stream_give synchronizes it and pools it (a few
 // per device; the rest are destroyed). blp_stream_prewarm fills the pool ahead of time.
-hipStream_t stream_take(int device);
-void stream_give(int device, hipStream_t s);
+// hi: the highest-priority pool -- a stream of the highest priority is never placed on a
+// hardware queue of normal-priority streams (blp_batch_create_pair's first batch, so the two
+// co-scheduled passes cannot serialize on one queue; with 4 queues per process two pooled
+// streams did, config-2 step 3.4 instead of 2.27 ms, r05 call O)
+hipStream_t stream_take(int device, bool hi = false);
+void stream_give(int device, hipStream_t s, bool hi = false);
+hipStream_t stream_new(bool hi);  // a new non-blocking stream (null + error recorded on failure)
 
 // The host column-id mirror, fetched from the device on first use when the graph was created
 // without one (blp_graph_create_from_csr with col_idx = NULL: similarity.main's path, whose

@@ -470,39 +470,53 @@ namespace {
 std::mutex g_stream_mu;
 std::condition_variable g_stream_cv;
 int g_prewarming = 0;  // blp_stream_prewarm calls creating streams (under g_stream_mu)
-std::vector<std::vector<hipStream_t>> g_stream_pool;  // [device]
+std::vector<std::vector<hipStream_t>> g_stream_pool;     // [device]
+std::vector<std::vector<hipStream_t>> g_stream_pool_hi;  // [device] highest-priority streams
 constexpr size_t STREAM_POOL_CAP = 16;
 }  // namespace
 
-hipStream_t stream_take(int device) {
+hipStream_t stream_take(int device, bool hi) {
   {
     std::unique_lock<std::mutex> lk(g_stream_mu);
     // a prewarm creating streams: wait for them rather than overlap this caller's first GPU work
     // with the stream creation (that overlap preceded 27-39 ms stalls, r05_e2e_final_ab)
     g_stream_cv.wait(lk, [] { return g_prewarming == 0; });
-    if ((size_t)device < g_stream_pool.size() && !g_stream_pool[device].empty()) {
-      hipStream_t s = g_stream_pool[device].back();
-      g_stream_pool[device].pop_back();
+    auto& pool = hi ? g_stream_pool_hi : g_stream_pool;
+    if ((size_t)device < pool.size() && !pool[device].empty()) {
+      hipStream_t s = pool[device].back();
+      pool[device].pop_back();
       return s;
     }
   }
+  return stream_new(hi);
+}
+
+hipStream_t stream_new(bool hi) {
   hipStream_t s = nullptr;
-  const hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+  hipError_t e;
+  if (hi) {
+    int least = 0, greatest = 0;
+    e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+    if (e == hipSuccess) e = hipStreamCreateWithPriority(&s, hipStreamNonBlocking, greatest);
+  } else {
+    e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+  }
   if (e != hipSuccess) {
-    hip_fail(e, "hipStreamCreateWithFlags", __FILE__, __LINE__);
+    hip_fail(e, "hipStreamCreate", __FILE__, __LINE__);
     return nullptr;
   }
   return s;
 }
 
-void stream_give(int device, hipStream_t s) {
+void stream_give(int device, hipStream_t s, bool hi) {
   if (!s) return;
   (void)hipStreamSynchronize(s);
   {
     std::lock_guard<std::mutex> lk(g_stream_mu);
-    if ((size_t)device >= g_stream_pool.size()) g_stream_pool.resize((size_t)device + 1);
-    if (g_stream_pool[device].size() < STREAM_POOL_CAP) {
-      g_stream_pool[device].push_back(s);
+    auto& pool = hi ? g_stream_pool_hi : g_stream_pool;
+    if ((size_t)device >= pool.size()) pool.resize((size_t)device + 1);
+    if (pool[device].size() < STREAM_POOL_CAP) {
+      pool[device].push_back(s);
       return;
     }
   }
@@ -563,13 +577,15 @@ int blp_stream_prewarm(int device, int n) {
   // run one empty kernel on each new one, and hold stream_take until they are in the pool: the
   // caller's first GPU work then neither creates a stream nor overlaps this thread's creation (an
   // overlap that preceded 27-39 ms stalls in similarity.main, profiles/r05_e2e_final_ab_slow_calls.txt).
-  size_t have = 0;
+  size_t have = 0, hi_have = 0;
   {
     std::lock_guard<std::mutex> lk(g_stream_mu);
     if ((size_t)device < g_stream_pool.size()) have = g_stream_pool[device].size();
+    if ((size_t)device < g_stream_pool_hi.size()) hi_have = g_stream_pool_hi[device].size();
     if (getenv("BLP_PREWARM_ALWAYS")) have = 0;
-    if ((size_t)n > have) ++g_prewarming;  // stream_take waits until these are in the pool
+    if ((size_t)n > have || (n > 0 && hi_have == 0)) ++g_prewarming;  // stream_take waits until these are in the pool
   }
+  const bool latched = (size_t)n > have || (n > 0 && hi_have == 0);
   std::vector<hipStream_t> made;
   hipError_t err = hipSuccess;
   for (int i = (int)std::min<size_t>(have, (size_t)n); i < n && err == hipSuccess; ++i) {
@@ -580,16 +596,34 @@ int blp_stream_prewarm(int device, int n) {
     hipLaunchKernelGGL(k_noop, dim3(1), dim3(64), 0, s);
     err = hipGetLastError();
   }
+  // and one highest-priority stream (blp_batch_create_pair's first batch: its own hardware queue)
+  hipStream_t made_hi = nullptr;
+  if (err == hipSuccess && n > 0 && hi_have == 0) {
+    if (!(made_hi = stream_new(true))) {
+      err = hipErrorOutOfMemory;
+    } else {
+      hipLaunchKernelGGL(k_noop, dim3(1), dim3(64), 0, made_hi);
+      err = hipGetLastError();
+    }
+  }
   for (hipStream_t s : made) (void)hipStreamSynchronize(s);
+  if (made_hi) (void)hipStreamSynchronize(made_hi);
   std::vector<hipStream_t> extra;  // past the pool's cap (concurrent prewarms): destroyed
-  if ((size_t)n > have) {
+  if (latched) {
     std::lock_guard<std::mutex> lk(g_stream_mu);
     if ((size_t)device >= g_stream_pool.size()) g_stream_pool.resize((size_t)device + 1);
+    if ((size_t)device >= g_stream_pool_hi.size()) g_stream_pool_hi.resize((size_t)device + 1);
     for (hipStream_t s : made) {
       if (g_stream_pool[device].size() < STREAM_POOL_CAP)
         g_stream_pool[device].push_back(s);
       else
         extra.push_back(s);
+    }
+    if (made_hi) {
+      if (g_stream_pool_hi[device].size() < STREAM_POOL_CAP)
+        g_stream_pool_hi[device].push_back(made_hi);
+      else
+        extra.push_back(made_hi);
     }
     --g_prewarming;
   }

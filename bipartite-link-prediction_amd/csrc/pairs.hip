@@ -3375,6 +3375,7 @@ Knobs read_knobs() {
 }  // namespace
 
 struct blp_batch {
+  bool hi_prio = false;  // its stream came from the highest-priority pool (stream_give returns it there)
   blp_graph* g = nullptr;
   int64_t n_pairs = 0;
   int32_t* d_x = nullptr;
@@ -3565,7 +3566,7 @@ extern "C" {
 // same pairs with x and y swapped whose device copies are taken (a device-to-device copy after the
 // twin's upload, on this batch's stream) instead of a second host-to-device upload.
 static int batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n_pairs, const blp_batch* twin,
-                        blp_batch** out, bool retry = false) {
+                        blp_batch** out, bool retry = false, bool hi_prio = false) {
   BLP_CHECK(g && out && n_pairs >= 0 && (n_pairs == 0 || (x && y)), BLP_E_ARG, "blp_batch_create: bad arguments");
   BLP_CHECK(n_pairs < (int64_t(1) << 31) - 1, BLP_E_ARG, "blp_batch_create: at most 2^31-2 pairs per batch");
   const int64_t n = g->n;
@@ -3590,7 +3591,8 @@ static int batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_
   };
   int rc = set_device(g);
   if (rc) return bail(rc);
-  if (!(b->stream = stream_take(g->device))) return bail(BLP_E_HIP_BASE);  // pooled (blp_stream_prewarm)
+  b->hi_prio = hi_prio;
+  if (!(b->stream = stream_take(g->device, hi_prio))) return bail(BLP_E_HIP_BASE);  // pooled (blp_stream_prewarm)
   {  // the graph's own uploads complete before this stream reads them (an event, not a host wait)
     hipEvent_t ev;
     BLP_HIP_OR(hipEventCreateWithFlags(&ev, hipEventDisableTiming), bail);
@@ -4084,12 +4086,12 @@ extern "C" {
 static bool is_oom(int rc) { return rc == BLP_E_HIP_BASE - (int)hipErrorOutOfMemory; }
 
 static int create_or_release(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n, const blp_batch* twin,
-                             blp_batch** out) {
-  int rc = batch_create(g, x, y, n, twin, out);
+                             blp_batch** out, bool hi = false) {
+  int rc = batch_create(g, x, y, n, twin, out, false, hi);
   if (is_oom(rc) && g) {  // the device scratch cache first (DevBuf blocks kept for reuse)
     (void)hipGetLastError();
     dev_cache_flush(g->device);
-    rc = batch_create(g, x, y, n, twin, out);
+    rc = batch_create(g, x, y, n, twin, out, false, hi);
   }
   if (!is_oom(rc) || !g || !g->d_wp) return rc;
   {
@@ -4100,7 +4102,7 @@ static int create_or_release(blp_graph* g, const int32_t* x, const int32_t* y, i
     (void)hipStreamSynchronize(g->stream);
     free_wedge_index(g);
   }
-  return batch_create(g, x, y, n, twin, out, true);
+  return batch_create(g, x, y, n, twin, out, true, hi);
 }
 
 int blp_batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_t n_pairs, blp_batch** out) {
@@ -4111,7 +4113,9 @@ int blp_batch_create_pair(blp_graph* g, const int32_t* x, const int32_t* y, int6
                           blp_batch** out_yx) {
   BLP_CHECK(out_xy && out_yx, BLP_E_ARG, "blp_batch_create_pair: null outputs");
   blp_batch* a = nullptr;
-  int rc = create_or_release(g, x, y, n_pairs, nullptr, &a);
+  // the first batch (similarity.main's user pass) on a highest-priority stream: the two passes
+  // then run on different hardware queues (BLP_PAIR_SAME_PRIO=1: both from the normal pool)
+  int rc = create_or_release(g, x, y, n_pairs, nullptr, &a, !getenv("BLP_PAIR_SAME_PRIO"));
   if (rc) return rc;
   blp_batch* b = nullptr;
   rc = create_or_release(g, y, x, n_pairs, a, &b);
@@ -4135,7 +4139,7 @@ int blp_batch_destroy(blp_batch* b) {
   b->off.release();
   b->active.release();
   b->scratch.release();
-  if (b->stream) stream_give(b->g ? b->g->device : 0, b->stream);  // back to the pool for the next batch
+  if (b->stream) stream_give(b->g ? b->g->device : 0, b->stream, b->hi_prio);  // back to the pool for the next batch
   if (b->wedge_user && b->g) {
     std::lock_guard<std::mutex> lk(b->g->wbm_mu);
     --b->g->wedge_users;
