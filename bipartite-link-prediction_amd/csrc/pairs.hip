@@ -3327,6 +3327,10 @@ struct Knobs {
   bool split16 = false;          // BLP_SPLIT16: the chunk-parallel scorer reads a 16-bit split table (measured
                                  // slower at config 5: 514 against 482 ms per step)
   bool group_gather = false;     // BLP_GROUP_GATHER: rows gathered by the write kernel, not carried by the scatter
+  int item_nb = 2048;            // BLP_ITEM_NB: at most this many interleaved buckets (a power of two)
+  int group_nblk = -1;           // BLP_GROUP_NBLK: hist / scatter workgroups (default 2 per CU)
+  bool pair_gate = false;        // BLP_PAIR_GATE: blp_batches_score holds the other passes' grouping until the
+                                 // large-universe pass's grouping is done
   std::string debug_null;        // BLP_DEBUG_NULL (BLP_DEBUG builds only): null this launch pointer, to
                                  // show the pre-launch pointer check (launch_pointers) refusing it
 };
@@ -3363,6 +3367,9 @@ Knobs read_knobs() {
   k.group_rows = !on("BLP_GROUP_YN");
   k.group_rows16 = on("BLP_GROUP_ROWS16");
   k.group_gather = on("BLP_GROUP_GATHER");
+  k.item_nb = (int)num("BLP_ITEM_NB", 2048);
+  k.group_nblk = (int)num("BLP_GROUP_NBLK", -1);
+  k.pair_gate = on("BLP_PAIR_GATE");
   k.split16 = on("BLP_SPLIT16");
   k.host_plan = on("BLP_HOST_PLAN");
   k.short_seg = on("BLP_SHORT_SEG");
@@ -3376,6 +3383,7 @@ Knobs read_knobs() {
 
 struct blp_batch {
   bool hi_prio = false;  // its stream came from the highest-priority pool (stream_give returns it there)
+  hipEvent_t gate_wait = nullptr, gate_rec = nullptr;  // blp_batches_score's grouping gate (BLP_PAIR_GATE), per call
   blp_graph* g = nullptr;
   int64_t n_pairs = 0;
   int32_t* d_x = nullptr;
@@ -3992,7 +4000,8 @@ static int batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_
     if (b->items) {
       // nb = 2^shift interleaved buckets (<= 2048), each with ceil(xspan / nb) keys
       b->shift = 0;
-      while ((int64_t(1) << b->shift) < std::min<int64_t>(b->xspan, 2048)) ++b->shift;
+      const int64_t nb_cap = std::max(1, std::min(kn.item_nb, 4096));
+      while ((int64_t(1) << b->shift) < std::min<int64_t>(b->xspan, nb_cap)) ++b->shift;
       b->nb = 1 << b->shift;
       if (((b->xspan + b->nb - 1) >> b->shift) > 32768)
         return bail(fail(BLP_E_UNSUP, "blp_batch_create: source id range too wide"));
@@ -4002,7 +4011,8 @@ static int batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_
       b->nb = (int)std::max<int64_t>(1, (b->xspan + (int64_t(1) << b->shift) - 1) >> b->shift);
       if (b->shift > 15 || b->nb > NB_MAX) return bail(fail(BLP_E_UNSUP, "blp_batch_create: source id range too wide"));
     }
-    b->nblk = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)g->n_cu * 2, (n_pairs + 4095) / 4096));
+    b->nblk = (int)std::max<int64_t>(1, std::min<int64_t>(kn.group_nblk > 0 ? kn.group_nblk : (int64_t)g->n_cu * 2,
+                                                          (n_pairs + 4095) / 4096));
     b->per_blk = (n_pairs + b->nblk - 1) / b->nblk;
   }
   // ---- chunk-parallel scorer: per-row chunk offsets and partial-result buffers
@@ -4233,6 +4243,7 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   int32_t* bact = tiles + std::max(tiles_h, tiles_b) + 1;
   int32_t* abase = bact + b->nb;
   int4* tmp = reinterpret_cast<int4*>((reinterpret_cast<uintptr_t>(abase + b->nb) + 15) & ~uintptr_t(15));
+  if (b->gate_wait) BLP_HIP(hipStreamWaitEvent(b->stream, b->gate_wait, 0));
   hipEvent_t t0, bt0;
   if ((rc = timer_begin(g->timers[K_GROUP], b->stream, &t0))) return rc;
   if ((rc = timer_begin(b->t_group, b->stream, &bt0))) return rc;
@@ -4367,6 +4378,7 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   if ((rc = timer_end(b->t_group, b->stream, bt0))) return rc;
   if ((rc = timer_end(g->timers[K_GROUP], b->stream, t0))) return rc;
 
+  if (b->gate_rec) BLP_HIP(hipEventRecord(b->gate_rec, b->stream));
   hipEvent_t t1, bt1;
   if ((rc = timer_begin(g->timers[K_SCORE], b->stream, &t1))) return rc;
   if ((rc = timer_begin(b->t_score, b->stream, &bt1))) return rc;
@@ -4555,14 +4567,30 @@ int blp_batches_score(blp_graph* g, int n, blp_batch* const* bs, const uint32_t*
   // chunk-parallel batches (config 5's two passes) each take the whole chip: holding each
   // persistent grid to a CU share was slower at every share tried (1951 ms per config-5 step in
   // proportion to planned work, 864 / 903 ms at 176 / 128 user CUs, against 743 ms)
-  for (int i = 0; i < n; ++i) {
+  // BLP_PAIR_GATE (measurement knob): the large pass is enqueued first and records an event after
+  // its grouping; the other passes' grouping waits on it, so their sorts cannot hold the CUs the
+  // large pass's grouping needs
+  hipEvent_t gate = nullptr;
+  int first = -1;
+  if (n > 1 && bs[0]->kn.pair_gate && t_large > 0.0 && t_other > 0.0) {
+    for (int i = 0; i < n && first < 0; ++i)
+      if (is_large(bs[i])) first = i;
+    int rc = set_device(g);
+    if (rc) return rc;
+    BLP_HIP(hipEventCreateWithFlags(&gate, hipEventDisableTiming));
+  }
+  int rc = BLP_OK;
+  for (int k = 0; k < n && !rc; ++k) {
+    const int i = first < 0 ? k : (k == 0 ? first : (k <= first ? k - 1 : k));
     blp_batch* b = bs[i];
     b->cus = is_large(b) && t_other > 0.0 ? share : 0;
-    const int rc = blp_batch_score(g, b, masks[i]);
+    if (gate) (i == first ? b->gate_rec : b->gate_wait) = gate;
+    rc = blp_batch_score(g, b, masks[i]);
     b->cus = 0;
-    if (rc) return rc;
+    b->gate_rec = b->gate_wait = nullptr;
   }
-  return BLP_OK;
+  if (gate) (void)hipEventDestroy(gate);
+  return rc;
 }
 
 int blp_batch_stats(blp_batch* b, int which, double* total_ms, int64_t* launches) {
