@@ -3327,7 +3327,8 @@ struct Knobs {
   bool split16 = false;          // BLP_SPLIT16: the chunk-parallel scorer reads a 16-bit split table (measured
                                  // slower at config 5: 514 against 482 ms per step)
   bool group_gather = false;     // BLP_GROUP_GATHER: rows gathered by the write kernel, not carried by the scatter
-  int item_nb = 2048;            // BLP_ITEM_NB: at most this many interleaved buckets (a power of two)
+  int item_nb = 512;             // BLP_ITEM_NB: at most this many interleaved buckets (a power of two; 512:
+                                 // 2.271 / 2.261 against 2.317 / 2.315 ms with 2048, r05_group_geometry)
   int group_nblk = -1;           // BLP_GROUP_NBLK: hist / scatter workgroups (default 2 per CU)
   bool pair_gate = false;        // BLP_PAIR_GATE: blp_batches_score holds the other passes' grouping until the
                                  // large-universe pass's grouping is done
@@ -3367,7 +3368,7 @@ Knobs read_knobs() {
   k.group_rows = !on("BLP_GROUP_YN");
   k.group_rows16 = on("BLP_GROUP_ROWS16");
   k.group_gather = on("BLP_GROUP_GATHER");
-  k.item_nb = (int)num("BLP_ITEM_NB", 2048);
+  k.item_nb = (int)num("BLP_ITEM_NB", 512);
   k.group_nblk = (int)num("BLP_GROUP_NBLK", -1);
   k.pair_gate = on("BLP_PAIR_GATE");
   k.split16 = on("BLP_SPLIT16");
@@ -3998,9 +3999,11 @@ static int batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_
     // buckets cover the sources' id range [xlo, xhi): ~2K buckets of 2^shift ids each
     b->items = !kn.group_buckets;  // test knob: one workgroup per contiguous bucket
     if (b->items) {
-      // nb = 2^shift interleaved buckets (<= 2048), each with ceil(xspan / nb) keys
+      // nb = 2^shift interleaved buckets, each with ceil(xspan / nb) keys: kn.item_nb of them, or
+      // more (<= 2048) when that keeps a bucket's keys <= 1024 (the staged write, k_item_write_ids)
       b->shift = 0;
-      const int64_t nb_cap = std::max(1, std::min(kn.item_nb, 4096));
+      int64_t nb_cap = std::max(1, std::min(kn.item_nb, 2048));
+      while (nb_cap < 2048 && (b->xspan + nb_cap - 1) / nb_cap > 1024) nb_cap *= 2;
       while ((int64_t(1) << b->shift) < std::min<int64_t>(b->xspan, nb_cap)) ++b->shift;
       b->nb = 1 << b->shift;
       if (((b->xspan + b->nb - 1) >> b->shift) > 32768)
