@@ -158,6 +158,8 @@ def test_general_graph_exact_distance(gpu):
     {"BLP_GROUP_YN": "1"},                              # short-row batches grouped by y only: the scorer reads N(y)'s bounds
     {"BLP_GROUP_ROWS16": "1"},                          # the 16-byte-stage grouping write (k_item_write_runs)
     {"BLP_GROUP_GATHER": "1"},                          # rows gathered by the grouping write, not carried by the scatter
+    {"BLP_ITEM_NB": "1"},                               # one interleaved bucket (or the fewest that keep <= 1024 keys)
+    {"BLP_ITEM_NB": "4", "BLP_GROUP_NBLK": "3"},        # few buckets, few scatter workgroups
     {"BLP_HOST_PLAN": "1"},                             # blp_batch_create's planning on the host mirror
     {"BLP_HOST_PLAN": "1", "BLP_SPLIT": "3", "BLP_SPLIT_BIG": "1", "BLP_HASH_WORK": "600"},
 ])
@@ -299,13 +301,15 @@ def test_business_fix_adamic_matches_oracle(gpu):
     assert_same_scores(got, exp, "adamic_adar")
 
 
-@pytest.mark.parametrize("variant", [None, "2"])
+@pytest.mark.parametrize("variant", [None, "2", "2+gate"])
 def test_coscheduled_passes_match_single_passes(gpu, variant, monkeypatch):
     # blp_batches_score: the user and business passes of one step run concurrently on their
     # own streams (the large-universe scorer held to a share of the CUs); results must equal
     # each pass scored alone, repeated steps included
     if variant:
-        monkeypatch.setenv("BLP_VARIANT", variant)  # the large-universe block scorer on this graph
+        monkeypatch.setenv("BLP_VARIANT", variant[0])  # the large-universe block scorer on this graph
+    if variant and variant.endswith("gate"):
+        monkeypatch.setenv("BLP_PAIR_GATE", "1")  # the business grouping waits for the user grouping
     rng = np.random.default_rng(21)
     a, b = bipartite_edges(rng, 20000, 1500, 200000)
     G = blp.DeviceGraph(a, b)
