@@ -3330,6 +3330,7 @@ struct Knobs {
   int item_nb = 512;             // BLP_ITEM_NB: at most this many interleaved buckets (a power of two; 512:
                                  // 2.271 / 2.261 against 2.317 / 2.315 ms with 2048, r05_group_geometry)
   int group_nblk = -1;           // BLP_GROUP_NBLK: hist / scatter workgroups (default 2 per CU)
+  int short_cus = -1;            // BLP_SHORT_CUS: CUs' worth of short-row scorer workgroups (default all)
   bool pair_gate = false;        // BLP_PAIR_GATE: blp_batches_score holds the other passes' grouping until the
                                  // large-universe pass's grouping is done
   std::string debug_null;        // BLP_DEBUG_NULL (BLP_DEBUG builds only): null this launch pointer, to
@@ -3371,6 +3372,7 @@ Knobs read_knobs() {
   k.item_nb = (int)num("BLP_ITEM_NB", 512);
   k.group_nblk = (int)num("BLP_GROUP_NBLK", -1);
   k.pair_gate = on("BLP_PAIR_GATE");
+  k.short_cus = (int)num("BLP_SHORT_CUS", -1);
   k.split16 = on("BLP_SPLIT16");
   k.host_plan = on("BLP_HOST_PLAN");
   k.short_seg = on("BLP_SHORT_SEG");
@@ -3490,7 +3492,8 @@ static int launch_short(blp_graph* g, const blp_batch* b, ScoreArgs a, size_t dy
   auto kern = three ? k_score_short<SAA> : k_score<BLOCK_SMALL, CAP_SMALL, SEG_SMALL, 8, true, SAA>;
   int per_cu = 1;
   BLP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, BLOCK_SMALL, dyn));
-  const int64_t n_wg = (int64_t)g->n_cu * std::max(per_cu, 1);
+  const int cus = b->kn.short_cus > 0 ? std::min(b->kn.short_cus, g->n_cu) : g->n_cu;  // tuning knob
+  const int64_t n_wg = (int64_t)cus * std::max(per_cu, 1);
   if (b->n_sources >= n_wg * 16) a.dq = std::max(a.dq, 2);
   hipLaunchKernelGGL(kern, dim3((unsigned)n_wg), dim3(BLOCK_SMALL), dyn, b->stream, a);
   BLP_HIP(hipGetLastError());
