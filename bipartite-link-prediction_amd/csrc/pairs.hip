@@ -229,7 +229,10 @@ __global__ __launch_bounds__(GP_BLOCK) void k_bucket_scatter(const int32_t* __re
   for (int i = threadIdx.x; i < nb; i += GP_BLOCK) cur[i] = hoff[(int64_t)i * nblk + blockIdx.x];
   __syncthreads();
   const int64_t b0 = (int64_t)blockIdx.x * per_blk, b1 = min(np, b0 + per_blk);
-  constexpr int U = 4;  // U pairs per thread per round: loads and LDS atomics overlap
+#ifndef BLP_SCATTER_U
+#define BLP_SCATTER_U 4
+#endif
+  constexpr int U = BLP_SCATTER_U;  // U pairs per thread per round: loads and LDS atomics overlap
   for (int64_t r = b0; r < b1; r += U * GP_BLOCK) {
     int xv[U], yv[U];
 #pragma unroll
