@@ -230,7 +230,7 @@ __global__ __launch_bounds__(GP_BLOCK) void k_bucket_scatter(const int32_t* __re
   __syncthreads();
   const int64_t b0 = (int64_t)blockIdx.x * per_blk, b1 = min(np, b0 + per_blk);
 #ifndef BLP_SCATTER_U
-#define BLP_SCATTER_U 4
+#define BLP_SCATTER_U 8  // 8: 2.230 / 2.231 / 2.230 against 2.261 / 2.272 / 2.261 ms with 4 (r05_scatter_u)
 #endif
   constexpr int U = BLP_SCATTER_U;  // U pairs per thread per round: loads and LDS atomics overlap
   for (int64_t r = b0; r < b1; r += U * GP_BLOCK) {
@@ -616,7 +616,10 @@ __global__ __launch_bounds__(GB_BLOCK) void k_item_write_ids(const int64_t* __re
     }
   }
   __syncthreads();
-  constexpr int U = 4;
+#ifndef BLP_ITEMW_U
+#define BLP_ITEMW_U 4
+#endif
+  constexpr int U = BLP_ITEMW_U;
   for (int kr = s; kr < e; kr += U * GB_BLOCK) {  // the item's records, staged in key order
     int4 t[U];
 #pragma unroll
