@@ -416,36 +416,15 @@ __global__ __launch_bounds__(GB_BLOCK) void k_item_count(const int4* __restrict_
                                                          const int32_t* __restrict__ item_e,
                                                          const int32_t* __restrict__ n_items, int32_t xlo, int lognb,
                                                          int32_t* __restrict__ cnt, int32_t* __restrict__ ih,
-                                                         const int32_t* __restrict__ keys = nullptr,
-                                                         int32_t* __restrict__ n_active = nullptr,
-                                                         int32_t* __restrict__ active = nullptr) {
+                                                         const int32_t* __restrict__ keys = nullptr) {
   __shared__ int h[KEYS];
   const int i = blockIdx.x;
   if (i >= *n_items) return;  // uniform: the grid is the host's upper bound on items
   const int b = item_b[i];
   item_hist<KEYS>(tmp, item_s[i], item_e[i], xlo, lognb, h, keys);
-  // active (round 5, the default): the item whose add finds a source's count still 0 appends the
-  // source (one wave-aggregated atomic), so no nonzero-count pass over the id range is needed;
-  // the list's order is arbitrary, which no scorer depends on (BLP_ITEM_NZ_SCAN: the ordered pass)
-  const int lane = (int)threadIdx.x & 63;
-  for (int j0 = 0; j0 < KEYS; j0 += GB_BLOCK) {  // uniform trip count: the ballot below sees every lane
-    const int j = j0 + (int)threadIdx.x;
-    bool first = false;
-    if (j < KEYS) {
-      const int c = h[j];
-      if (c) first = atomicAdd(&cnt[xlo + b + (j << lognb)], c) == 0;
-      if (ih) ih[(int64_t)i * KEYS + j] = c;  // the item's histogram, for k_item_write_runs
-    }
-    if (active) {
-      const unsigned long long m = __ballot(first);
-      if (m) {
-        const int leader = __ffsll((long long)m) - 1;
-        int base = 0;
-        if (lane == leader) base = atomicAdd(n_active, __popcll(m));
-        base = __shfl(base, leader, 64);
-        if (first) active[base + __popcll(m & ((1ull << lane) - 1ull))] = xlo + b + (j << lognb);
-      }
-    }
+  for (int j = threadIdx.x; j < KEYS; j += GB_BLOCK) {
+    if (h[j]) atomicAdd(&cnt[xlo + b + (j << lognb)], h[j]);
+    if (ih) ih[(int64_t)i * KEYS + j] = h[j];  // the item's histogram, for k_item_write_runs
   }
 }
 
@@ -962,73 +941,6 @@ __global__ void k_run_cnt(const int32_t* __restrict__ active, const int32_t* __r
     const int xa = active[a];
     const int nxt = a + 1 < na ? off[active[a + 1]] : (int)np;
     cnt[xa] = nxt - off[xa];
-  }
-}
-
-// One-pass run grouping (round 5, the default): the active list needs no order -- every pair
-// carries its caller index and the persistent scorers dequeue sources in any order -- so run heads
-// append themselves with one wave-aggregated atomic on n_active (zeroed with Misc at the step's
-// start) instead of k_run_count + a scan + k_run_write. Head lanes write off[x], tail lanes the
-// run's end into cnt[x]; k_run_len turns the end into the length. (BLP_RUNS_SCAN: the scan path.)
-__global__ __launch_bounds__(SCAN_BLOCK) void k_run_heads(const int32_t* __restrict__ x, const int32_t* __restrict__ y,
-                                                          int64_t np, const int64_t* __restrict__ rp,
-                                                          int32_t* __restrict__ n_active, int32_t* __restrict__ active,
-                                                          int32_t* __restrict__ off, int32_t* __restrict__ cnt_end,
-                                                          int32_t* __restrict__ g_out, int64_t* __restrict__ g_yb,
-                                                          int32_t* __restrict__ g_yl, int32_t* __restrict__ g_y) {
-  const int64_t t0 = (int64_t)blockIdx.x * SCAN_TILE;
-  constexpr int PT = SCAN_TILE / SCAN_BLOCK;
-  const int lane = (int)threadIdx.x & 63;
-  int yv[PT], xv[PT], xp[PT], xn[PT];
-#pragma unroll
-  for (int q = 0; q < PT; ++q) {
-    const int64_t i = t0 + q * SCAN_BLOCK + threadIdx.x;
-    yv[q] = i < np ? y[i] : 0;
-    xv[q] = i < np ? x[i] : 0;
-    xp[q] = i > 0 && i < np ? x[i - 1] : INT32_MIN;   // (the neighbours' lines are the same lines)
-    xn[q] = i + 1 < np ? x[i + 1] : INT32_MIN;
-  }
-  int64_t st[PT], en[PT];
-#pragma unroll
-  for (int q = 0; q < PT; ++q) {
-    st[q] = rp[yv[q]];
-    en[q] = rp[yv[q] + 1];
-  }
-#pragma unroll
-  for (int q = 0; q < PT; ++q) {
-    const int64_t i = t0 + q * SCAN_BLOCK + threadIdx.x;
-    if (i < np) {
-      g_out[i] = (int32_t)i;
-      g_yb[i] = st[q];
-      g_yl[i] = (int32_t)(en[q] - st[q]);
-      if (g_y) g_y[i] = yv[q];
-    }
-  }
-#pragma unroll
-  for (int q = 0; q < PT; ++q) {
-    const int64_t i = t0 + q * SCAN_BLOCK + threadIdx.x;
-    const bool in = i < np;
-    const bool head = in && xp[q] != xv[q];
-    if (head) off[xv[q]] = (int32_t)i;
-    if (in && xn[q] != xv[q]) cnt_end[xv[q]] = (int32_t)(i + 1);
-    const unsigned long long m = __ballot(head);  // every lane of the wave executes it
-    if (m) {
-      const int leader = __ffsll((long long)m) - 1;
-      int base = 0;
-      if (lane == leader) base = atomicAdd(n_active, __popcll(m));
-      base = __shfl(base, leader, 64);
-      if (head) active[base + __popcll(m & ((1ull << lane) - 1ull))] = xv[q];
-    }
-  }
-}
-
-// cnt[x] = run end - off[x] for every active source (after k_run_heads)
-__global__ void k_run_len(const int32_t* __restrict__ active, const int32_t* __restrict__ n_active,
-                          const int32_t* __restrict__ off, int32_t* __restrict__ cnt) {
-  const int na = *n_active;
-  for (int a = blockIdx.x * blockDim.x + threadIdx.x; a < na; a += gridDim.x * blockDim.x) {
-    const int xa = active[a];
-    cnt[xa] -= off[xa];
   }
 }
 
@@ -3425,8 +3337,6 @@ struct Knobs {
                                  // 2.271 / 2.261 against 2.317 / 2.315 ms with 2048, r05_group_geometry)
   int group_nblk = -1;           // BLP_GROUP_NBLK: hist / scatter workgroups (default 2 per CU)
   int short_cus = -1;            // BLP_SHORT_CUS: CUs' worth of short-row scorer workgroups (default all)
-  bool item_nz_scan = false;     // BLP_ITEM_NZ_SCAN: item grouping's active list by a nonzero-count pass (ordered)
-  bool runs_scan = false;        // BLP_RUNS_SCAN: run grouping by tile counts and a scan (ordered active list)
   bool pair_gate = false;        // BLP_PAIR_GATE: blp_batches_score holds the other passes' grouping until the
                                  // large-universe pass's grouping is done
   std::string debug_null;        // BLP_DEBUG_NULL (BLP_DEBUG builds only): null this launch pointer, to
@@ -3468,8 +3378,6 @@ Knobs read_knobs() {
   k.item_nb = (int)num("BLP_ITEM_NB", 512);
   k.group_nblk = (int)num("BLP_GROUP_NBLK", -1);
   k.pair_gate = on("BLP_PAIR_GATE");
-  k.runs_scan = on("BLP_RUNS_SCAN");
-  k.item_nz_scan = on("BLP_ITEM_NZ_SCAN");
   k.short_cus = (int)num("BLP_SHORT_CUS", -1);
   k.split16 = on("BLP_SPLIT16");
   k.host_plan = on("BLP_HOST_PLAN");
@@ -4352,14 +4260,7 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   if ((rc = timer_begin(g->timers[K_GROUP], b->stream, &t0))) return rc;
   if ((rc = timer_begin(b->t_group, b->stream, &bt0))) return rc;
   BLP_HIP(hipMemsetAsync(b->d_misc, 0, offsetof(Misc, dbg), b->stream));  // the debug record persists to fetch
-  if (np && b->runs && !b->kn.runs_scan) {
-    const int64_t tiles = (np + SCAN_TILE - 1) / SCAN_TILE;
-    hipLaunchKernelGGL(k_run_heads, dim3((unsigned)tiles), dim3(SCAN_BLOCK), 0, b->stream, b->d_x, b->d_y, np, g->d_rp,
-                       &b->d_misc->n_active, b->active.as<int32_t>(), b->off.as<int32_t>(), b->cnt.as<int32_t>(),
-                       b->d_gout, b->d_gyb, b->d_gyl, b->d_gy);
-    hipLaunchKernelGGL(k_run_len, dim3(1024), dim3(256), 0, b->stream, b->active.as<int32_t>(), &b->d_misc->n_active,
-                       b->off.as<int32_t>(), b->cnt.as<int32_t>());
-  } else if (np && b->runs) {
+  if (np && b->runs) {
     const int64_t tiles = (np + SCAN_TILE - 1) / SCAN_TILE;
     int32_t* rtile = reinterpret_cast<int32_t*>(tmp);  // the bucket sort's pair buffer is free here
     hipLaunchKernelGGL(k_run_count, dim3((unsigned)tiles), dim3(SCAN_BLOCK), 0, b->stream, b->d_x, np, rtile);
@@ -4403,23 +4304,19 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
       const int64_t keys = ikeys;
       const bool runs_w = keys <= 1024;
       const bool ids_w = b->use_short && b->d_gy && !b->kn.group_rows;  // k_item_write_ids (short-row scorer)
-      const bool nz_scan = b->kn.item_nz_scan;  // test knob: the ordered active list
       b->yn_grouped = runs_w && ids_w;
       int32_t* ih = tx2 + tx + 1;  // [ub][K] item histograms (runs_w)
 #define BLP_ITEM_LAUNCH(K)                                                                                         \
   hipLaunchKernelGGL(k_item_count<K>, dim3((unsigned)ub), dim3(GB_BLOCK), 0, b->stream, tmp, it_b, it_s, it_e,     \
-                     &b->d_misc->n_items, b->xlo, b->shift, cnt, runs_w ? ih : nullptr, keyarr,                     \
-                     nz_scan ? nullptr : &b->d_misc->n_active, nz_scan ? nullptr : b->active.as<int32_t>());        \
+                     &b->d_misc->n_items, b->xlo, b->shift, cnt, runs_w ? ih : nullptr, keyarr);                   \
   hipLaunchKernelGGL(k_scan_sum, dim3((unsigned)tx), dim3(SCAN_BLOCK), 0, b->stream, cnt + b->xlo, b->xspan, tx1); \
   hipLaunchKernelGGL(k_scan_mid, dim3(1), dim3(SCAN_BLOCK), 0, b->stream, tx1, tx, (int32_t*)nullptr);             \
   hipLaunchKernelGGL(k_scan_out, dim3((unsigned)tx), dim3(SCAN_BLOCK), 0, b->stream, cnt + b->xlo, b->xspan, tx1,  \
                      off + b->xlo);                                                                                 \
-  if (nz_scan) {                                                                                                    \
-    hipLaunchKernelGGL(k_nz_count, dim3((unsigned)tx), dim3(SCAN_BLOCK), 0, b->stream, cnt + b->xlo, b->xspan, tx2); \
-    hipLaunchKernelGGL(k_scan_mid, dim3(1), dim3(SCAN_BLOCK), 0, b->stream, tx2, tx, &b->d_misc->n_active);        \
-    hipLaunchKernelGGL(k_nz_write, dim3((unsigned)tx), dim3(SCAN_BLOCK), 0, b->stream, cnt + b->xlo, b->xspan, tx2, \
-                       b->xlo, b->active.as<int32_t>());                                                            \
-  }                                                                                                                 \
+  hipLaunchKernelGGL(k_nz_count, dim3((unsigned)tx), dim3(SCAN_BLOCK), 0, b->stream, cnt + b->xlo, b->xspan, tx2); \
+  hipLaunchKernelGGL(k_scan_mid, dim3(1), dim3(SCAN_BLOCK), 0, b->stream, tx2, tx, &b->d_misc->n_active);          \
+  hipLaunchKernelGGL(k_nz_write, dim3((unsigned)tx), dim3(SCAN_BLOCK), 0, b->stream, cnt + b->xlo, b->xspan, tx2,  \
+                     b->xlo, b->active.as<int32_t>());                                                              \
   if (runs_w && ids_w)                                                                                                \
     hipLaunchKernelGGL((k_item_write_ids<(K <= 1024 ? K : 1024), 0>), dim3((unsigned)ub), dim3(GB_BLOCK), 0,         \
                        b->stream, g->d_rp, tmp, it_b, it_s, it_e, &b->d_misc->n_items, b->xlo, b->shift, ih, off,     \

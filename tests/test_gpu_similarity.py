@@ -67,16 +67,14 @@ def _check_against_oracle(ga, gb, x, y, mask=7):
     return G
 
 
-@pytest.mark.parametrize("no_runs", [False, True, "scan"])
+@pytest.mark.parametrize("no_runs", [False, True])
 @pytest.mark.parametrize("n_users,n_bus,n_draws,seed", [
     (2000, 300, 20000, 0),     # small universe: SMALL block variant / short-row scorer
     (30000, 2000, 150000, 1),  # MED block variant
     (300000, 5000, 600000, 2), # LARGE block variant, long rows (popular businesses)
 ])
 def test_user_and_business_side_vs_oracle(gpu, n_users, n_bus, n_draws, seed, no_runs, monkeypatch):
-    if no_runs == "scan":
-        monkeypatch.setenv("BLP_RUNS_SCAN", "1")  # run grouping by tile counts and a scan, not run-head atomics
-    elif no_runs:
+    if no_runs:
         monkeypatch.setenv("BLP_NO_RUNS", "1")  # bucket-sort grouping even for source-grouped lists
     rng = np.random.default_rng(seed)
     a, b = bipartite_edges(rng, n_users, n_bus, n_draws)
@@ -162,8 +160,6 @@ def test_general_graph_exact_distance(gpu):
     {"BLP_GROUP_GATHER": "1"},                          # rows gathered by the grouping write, not carried by the scatter
     {"BLP_ITEM_NB": "1"},                               # one interleaved bucket (or the fewest that keep <= 1024 keys)
     {"BLP_ITEM_NB": "4", "BLP_GROUP_NBLK": "3"},        # few buckets, few scatter workgroups
-    {"BLP_ITEM_NZ_SCAN": "1"},                          # item grouping's active list by the ordered nonzero-count pass
-    {"BLP_RUNS_SCAN": "1"},                             # run grouping by tile counts and a scan, not run-head atomics
     {"BLP_HOST_PLAN": "1"},                             # blp_batch_create's planning on the host mirror
     {"BLP_HOST_PLAN": "1", "BLP_SPLIT": "3", "BLP_SPLIT_BIG": "1", "BLP_HASH_WORK": "600"},
 ])
