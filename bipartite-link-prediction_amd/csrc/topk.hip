@@ -97,6 +97,7 @@ struct TkArgs {
   const int32_t* x2;      // wedge rows: for each target b' and member w of N(b'), N'(w)
   int64_t kbase;          // rp[tlo]
   const int32_t* src;
+  const int32_t* order;  // [n_src] dequeue order: list index of the q-th source claimed (or null: q itself)
   int n_src;
   int64_t tlo, T;
   const TkChunk* chunks;
@@ -1138,9 +1139,9 @@ __global__ __launch_bounds__(TK_NT) void k_topk(TkArgs a) {
     __syncthreads();
     if (tid == 0) s.item = (int)atomicAdd(&a.counters[0], 1ull);
     __syncthreads();
-    const int it = s.item;
+    if (s.item >= a.n_src) break;
+    const int it = a.order ? a.order[s.item] : s.item;
     TKP(0)
-    if (it >= a.n_src) break;
     const int x = a.src[it];
     const int64_t xb = a.rp[x];
     const int du = (int)(a.rp[x + 1] - xb);
@@ -1355,7 +1356,8 @@ struct blp_topk {
   bool have_aa = false;
   std::vector<TkChunk> chunks;
   int64_t aa_chunk = 0;
-  DevBuf perm, inv, tdeg, ge, pci, d_chunks, src, keys, cols, ncand, counters, wtab, x2_off, x2;
+  DevBuf perm, inv, tdeg, ge, pci, d_chunks, src, order, keys, cols, ncand, counters, wtab, x2_off, x2;
+  bool ordered = false;  // t->order holds a largest-first dequeue order of the sources
   DevBuf dw_cv, dw_ca, dw_bm, dw_info, dw_caf;  // dense counts of the hot targets (see the header comment)
   int64_t dw_n = 0, dw_words = 0, dw_bmw = 0;
   int64_t kbase = 0, x2_entries = -1;
@@ -1437,6 +1439,7 @@ static TkArgs topk_args(blp_topk* t, int k, uint32_t mask) {
   a.x2 = t->x2_entries >= 0 ? t->x2.as<int32_t>() : nullptr;
   a.kbase = t->kbase;
   a.src = t->src.as<int32_t>();
+  a.order = t->ordered ? t->order.as<int32_t>() : nullptr;
   a.n_src = (int)t->n_src;
   a.tlo = t->tlo;
   a.T = t->T;
@@ -1679,7 +1682,7 @@ extern "C" int blp_topk_create(blp_graph* g, int64_t src_lo, int64_t src_hi, int
 extern "C" int blp_topk_destroy(blp_topk* t) {
   if (!t) return BLP_OK;
   (void)set_device(t->g);
-  for (DevBuf* b : {&t->perm, &t->inv, &t->tdeg, &t->ge, &t->pci, &t->d_chunks, &t->src, &t->keys, &t->cols, &t->ncand,
+  for (DevBuf* b : {&t->perm, &t->inv, &t->tdeg, &t->ge, &t->pci, &t->d_chunks, &t->src, &t->order, &t->keys, &t->cols, &t->ncand,
                     &t->counters, &t->wtab, &t->x2_off, &t->x2, &t->dw_cv, &t->dw_ca, &t->dw_bm, &t->dw_info,
                     &t->dw_caf})
     b->release();
@@ -1708,6 +1711,26 @@ extern "C" int blp_topk_set_sources(blp_topk* t, const int32_t* src, int64_t n_s
   if ((rc = t->src.reserve(4 * std::max<int64_t>(n_src, 1)))) return rc;
   if (n_src) BLP_HIP(hipMemcpy(t->src.p, src, 4 * n_src, hipMemcpyHostToDevice));
   t->n_src = n_src;
+  // Largest first: the one-workgroup-per-source kernel claims sources in descending order of their
+  // two-hop walk, sum over b in N(x) of |N(b)|, so the long sources start early instead of
+  // finishing last on a few CUs (BLP_TK_ORDER=0: list order). Results land by list index.
+  t->ordered = false;
+  const int32_t* ci = host_col_idx(t->g);
+  if (n_src > 1 && ci && env_i64("BLP_TK_ORDER", 1) != 0) {
+    const int64_t* rp = t->g->hrp;
+    std::vector<int64_t> est((size_t)n_src);
+    for (int64_t i = 0; i < n_src; ++i) {
+      int64_t w = 0;
+      for (int64_t e = rp[src[i]]; e < rp[src[i] + 1]; ++e) w += rp[ci[e] + 1] - rp[ci[e]];
+      est[i] = w;
+    }
+    std::vector<int32_t> ord((size_t)n_src);
+    for (int64_t i = 0; i < n_src; ++i) ord[i] = (int32_t)i;
+    std::stable_sort(ord.begin(), ord.end(), [&](int32_t a, int32_t b) { return est[a] > est[b]; });
+    if ((rc = t->order.reserve(4 * n_src))) return rc;
+    BLP_HIP(hipMemcpy(t->order.p, ord.data(), 4 * n_src, hipMemcpyHostToDevice));
+    t->ordered = true;
+  }
   t->ran = false;
   return BLP_OK;
 }

@@ -248,3 +248,21 @@ def test_topk_repeat_is_deterministic(small):
     for r1, r2 in zip(*outs):
         for x, y in zip(r1, r2):
             assert np.array_equal(x, y)
+
+
+def test_topk_largest_first_order_matches_list_order(small, monkeypatch):
+    """Sources are claimed largest two-hop walk first (blp_topk_set_sources), results land by
+    list index: the lists equal those of the plain list order (BLP_TK_ORDER=0) and the oracle's."""
+    G, adj, rng = small
+    src = rng.choice(G.n_col0, 48, replace=False)
+    got = {}
+    for order in ("0", "1"):
+        monkeypatch.setenv("BLP_TK_ORDER", order)
+        T = blp.TopK(G, "user")
+        T.set_sources(src)
+        T.run(15, ALL)
+        got[order] = [T.fetch(m) for m in METHODS]
+    for r0, r1 in zip(got["0"], got["1"]):
+        for x, y in zip(r0, r1):
+            assert np.array_equal(x, y)
+    check_against_oracle(G, blp.TopK(G, "user"), adj, src, 15)
