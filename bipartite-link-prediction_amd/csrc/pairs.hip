@@ -933,15 +933,54 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_run_write(const int32_t* __restr
     }
 }
 
-// cnt of every run from the next run's head (after k_run_write: off[] of all heads)
+// cnt of every run from the next run's head (after k_run_write: off[] of all heads). rank (or
+// null): the batch's largest-first order (BLP_LPT, planned at create), the sources copied into
+// lpt in that order for the scorer's queue.
 __global__ void k_run_cnt(const int32_t* __restrict__ active, const int32_t* __restrict__ n_active, int64_t np,
-                          const int32_t* __restrict__ off, int32_t* __restrict__ cnt) {
+                          const int32_t* __restrict__ off, int32_t* __restrict__ cnt,
+                          const int32_t* __restrict__ rank = nullptr, int32_t xlo = 0, int32_t* __restrict__ lpt = nullptr) {
   const int na = *n_active;
   for (int a = blockIdx.x * blockDim.x + threadIdx.x; a < na; a += gridDim.x * blockDim.x) {
     const int xa = active[a];
     const int nxt = a + 1 < na ? off[active[a + 1]] : (int)np;
     cnt[xa] = nxt - off[xa];
+    if (rank) lpt[rank[xa - xlo]] = xa;
   }
+}
+
+// BLP_LPT planning: each source's scan work, sum of |N(y)| over its pairs (wave-aggregated when
+// the wave's pairs share their source, as run-grouped lists do), into est[x - xlo]
+__global__ void k_src_scan_work(const int32_t* __restrict__ x, const int32_t* __restrict__ y, int64_t np,
+                                const int64_t* __restrict__ rp, int32_t xlo, unsigned long long* __restrict__ est) {
+  const int lane = (int)threadIdx.x & 63;
+  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x; i0 < np; i0 += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = i0 + threadIdx.x;
+    const bool in = i < np;
+    const int xi = in ? x[i] : INT32_MIN;
+    const unsigned long long w = in ? (unsigned long long)(rp[y[i] + 1] - rp[y[i]]) : 0ull;
+    const int x0 = __shfl(xi, 0, 64);
+    const bool same = __all(!in || xi == x0);
+    if (same) {
+      unsigned long long t = w;
+      for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+      if (lane == 0 && x0 != INT32_MIN) atomicAdd(&est[x0 - xlo], t);
+    } else if (in) {
+      atomicAdd(&est[xi - xlo], w);
+    }
+  }
+}
+
+// est of source i = its scan work + its build work w2[x]
+__global__ void k_src_est(const int32_t* __restrict__ srcs, int64_t n, const unsigned long long* __restrict__ est,
+                          const unsigned long long* __restrict__ w2, int32_t xlo, unsigned long long* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = est[srcs[i] - xlo] + w2[srcs[i]];
+}
+
+__global__ void k_src_rank(const int32_t* __restrict__ srcs, int64_t n, const int32_t* __restrict__ r, int32_t xlo,
+                           int32_t* __restrict__ rank) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    rank[srcs[i] - xlo] = r[i];
 }
 
 constexpr int DQ_MAX = 8;  // sources per dequeue (blp_batch::dq)
@@ -3337,6 +3376,7 @@ struct Knobs {
                                  // 2.271 / 2.261 against 2.317 / 2.315 ms with 2048, r05_group_geometry)
   int group_nblk = -1;           // BLP_GROUP_NBLK: hist / scatter workgroups (default 2 per CU)
   int short_cus = -1;            // BLP_SHORT_CUS: CUs' worth of short-row scorer workgroups (default all)
+  bool lpt = false;              // BLP_LPT: run-grouped batches queue their sources largest (build + scan work) first
   bool pair_gate = false;        // BLP_PAIR_GATE: blp_batches_score holds the other passes' grouping until the
                                  // large-universe pass's grouping is done
   std::string debug_null;        // BLP_DEBUG_NULL (BLP_DEBUG builds only): null this launch pointer, to
@@ -3378,6 +3418,7 @@ Knobs read_knobs() {
   k.item_nb = (int)num("BLP_ITEM_NB", 512);
   k.group_nblk = (int)num("BLP_GROUP_NBLK", -1);
   k.pair_gate = on("BLP_PAIR_GATE");
+  k.lpt = num("BLP_LPT", 0) != 0;
   k.short_cus = (int)num("BLP_SHORT_CUS", -1);
   k.split16 = on("BLP_SPLIT16");
   k.host_plan = on("BLP_HOST_PLAN");
@@ -3450,6 +3491,8 @@ struct blp_batch {
   SrcRec* d_rec = nullptr;  // [n_sources] source records of the short-row scorer (or null)
   uint8_t* d_hflag = nullptr;  // [xspan] 1: source scored by k_score_hash (split batches; or null)
   int32_t* d_active2 = nullptr;  // the active list partitioned by k_hash_partition (with d_hflag)
+  int32_t* d_rank = nullptr;     // [xspan] BLP_LPT: the source's place in the largest-first order (or null)
+  int32_t* d_lpt = nullptr;      // [n_sources] the active list in that order, written by k_run_cnt
   int64_t n_hash = 0;          // such sources
   bool use_short = false;   // the short-row scorer takes this batch (decided once, at create)
   bool yn_grouped = false;  // short-row batch grouped by k_item_write_ids: the scorer reads g_yn = d_gy
@@ -3923,6 +3966,37 @@ static int batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_
   }
   if (b->n_hash && hipMalloc(&b->d_active2, 4 * ((size_t)std::max<int64_t>(b->xspan, 1) + 1)) != hipSuccess)
     return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: hash flags"));
+  if (dev_plan && runs && kn.lpt && n_sources > 1) {
+    // BLP_LPT: the sources' queue order, largest estimated work (build w2[x] + scan sum |N(y)|) first
+    ScopedBuf d_est, d_out, d_r;
+    if ((rc = d_est.reserve(8 * (size_t)std::max<int64_t>(b->xspan, 1))) || (rc = d_out.reserve(8 * (size_t)n_sources)) ||
+        (rc = d_r.reserve(4 * (size_t)n_sources)))
+      return bail(rc);
+    if (hipMalloc(&b->d_rank, 4 * (size_t)std::max<int64_t>(b->xspan, 1)) != hipSuccess ||
+        hipMalloc(&b->d_lpt, 4 * (size_t)n_sources + 4) != hipSuccess)
+      return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: source order"));
+    BLP_HIP_OR(hipMemsetAsync(d_est.p, 0, 8 * (size_t)std::max<int64_t>(b->xspan, 1), b->stream), bail);
+    const unsigned gp = (unsigned)std::max<int64_t>(1, std::min<int64_t>((int64_t)g->n_cu * 8, (n_pairs + 255) / 256));
+    hipLaunchKernelGGL(k_src_scan_work, dim3(gp), dim3(256), 0, b->stream, b->d_x, b->d_y, n_pairs, g->d_rp, (int32_t)xlo,
+                       d_est.as<unsigned long long>());
+    const unsigned gs = (unsigned)std::max<int64_t>(1, std::min<int64_t>((int64_t)g->n_cu * 4, (n_sources + 255) / 256));
+    hipLaunchKernelGGL(k_src_est, dim3(gs), dim3(256), 0, b->stream, d_srcs.as<int32_t>(), n_sources,
+                       d_est.as<unsigned long long>(), reinterpret_cast<const unsigned long long*>(g->d_w2), (int32_t)xlo,
+                       d_out.as<unsigned long long>());
+    BLP_HIP_OR(hipGetLastError(), bail);
+    std::vector<unsigned long long> est((size_t)n_sources);
+    BLP_HIP_OR(hipMemcpyAsync(est.data(), d_out.p, 8 * (size_t)n_sources, hipMemcpyDeviceToHost, b->stream), bail);
+    BLP_HIP_OR(hipStreamSynchronize(b->stream), bail);
+    std::vector<int32_t> ord((size_t)n_sources), r((size_t)n_sources);
+    for (int64_t i = 0; i < n_sources; ++i) ord[i] = (int32_t)i;
+    std::stable_sort(ord.begin(), ord.end(), [&](int32_t p, int32_t q) { return est[p] > est[q]; });
+    for (int64_t j = 0; j < n_sources; ++j) r[ord[j]] = (int32_t)j;
+    BLP_HIP_OR(hipMemcpyAsync(d_r.p, r.data(), 4 * (size_t)n_sources, hipMemcpyHostToDevice, b->stream), bail);
+    hipLaunchKernelGGL(k_src_rank, dim3(gs), dim3(256), 0, b->stream, d_srcs.as<int32_t>(), n_sources, d_r.as<int32_t>(),
+                       (int32_t)xlo, b->d_rank);
+    BLP_HIP_OR(hipGetLastError(), bail);
+    BLP_HIP_OR(hipStreamSynchronize(b->stream), bail);  // the scoped buffers go after this
+  }
   stage("sources");
   // ---- heavy sources: build work far above the per-workgroup share goes to k_heavy
   const int64_t total_work = build_work + scan_work;
@@ -4167,7 +4241,7 @@ int blp_batch_destroy(blp_batch* b) {
     --b->g->wedge_users;
   }
   void* ps[] = {b->d_x,    b->d_y,    b->d_cn,   b->d_jac,  b->d_aa,          b->d_gout,        b->d_gyb,
-                b->d_gyl,  b->d_misc, b->d_heavy_slot, b->d_heavy_bm, b->d_heavy_items, b->d_gbm, b->d_gy, b->d_rsplit, b->d_rsplit16, b->d_pcn, b->d_paa, b->d_ph2, b->d_aa_part, b->d_rec, b->d_hflag, b->d_lq, b->d_active2};
+                b->d_gyl,  b->d_misc, b->d_heavy_slot, b->d_heavy_bm, b->d_heavy_items, b->d_gbm, b->d_gy, b->d_rsplit, b->d_rsplit16, b->d_pcn, b->d_paa, b->d_ph2, b->d_aa_part, b->d_rec, b->d_hflag, b->d_lq, b->d_active2, b->d_rank, b->d_lpt};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   delete b;
@@ -4269,7 +4343,7 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
                        rtile, b->active.as<int32_t>(), b->off.as<int32_t>(), b->d_gout, b->d_gyb, b->d_gyl,
                        b->d_gy);
     hipLaunchKernelGGL(k_run_cnt, dim3(1024), dim3(256), 0, b->stream, b->active.as<int32_t>(), &b->d_misc->n_active,
-                       np, b->off.as<int32_t>(), b->cnt.as<int32_t>());
+                       np, b->off.as<int32_t>(), b->cnt.as<int32_t>(), b->d_rank, (int32_t)b->xlo, b->d_lpt);
   } else if (np) {
     // items mode: interleaved buckets (v & (nb - 1)); bucket mode: contiguous (v >> shift)
     const int hshift = b->items ? 0 : b->shift, bmask = b->items ? b->nb - 1 : -1;
@@ -4422,7 +4496,7 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
 
   a.off = b->off.as<int32_t>();
   a.cnt = b->cnt.as<int32_t>();
-  a.active = b->active.as<int32_t>();
+  a.active = b->runs && b->d_lpt ? b->d_lpt : b->active.as<int32_t>();  // BLP_LPT: the largest-first queue
   a.g_out = b->d_gout;
   a.g_yb = b->d_gyb;
   a.g_yl = b->d_gyl;
