@@ -709,7 +709,9 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_nz_count(const int32_t* __restri
 
 __global__ __launch_bounds__(SCAN_BLOCK) void k_nz_write(const int32_t* __restrict__ cnt, int64_t n,
                                                          const int32_t* __restrict__ tile_off, int32_t xlo,
-                                                         int32_t* __restrict__ active) {
+                                                         int32_t* __restrict__ active,
+                                                         const int32_t* __restrict__ rank = nullptr,
+                                                         int32_t* __restrict__ lpt = nullptr) {
   __shared__ int red[SCAN_BLOCK / 64];
   const int64_t base = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)threadIdx.x * SCAN_ITEMS;
   bool h[SCAN_ITEMS];
@@ -723,7 +725,10 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_nz_write(const int32_t* __restri
   int o = block_exscan_i<SCAN_BLOCK>(v, red, &tot) + tile_off[blockIdx.x];
 #pragma unroll
   for (int k = 0; k < SCAN_ITEMS; ++k)
-    if (h[k]) active[o++] = xlo + (int32_t)(base + k);
+    if (h[k]) {
+      active[o++] = xlo + (int32_t)(base + k);
+      if (rank) lpt[rank[base + k]] = xlo + (int32_t)(base + k);  // BLP_LPT: the largest-first queue
+    }
 }
 
 // ------------------------------------------------------------------ batch planning (device)
@@ -3376,7 +3381,8 @@ struct Knobs {
                                  // 2.271 / 2.261 against 2.317 / 2.315 ms with 2048, r05_group_geometry)
   int group_nblk = -1;           // BLP_GROUP_NBLK: hist / scatter workgroups (default 2 per CU)
   int short_cus = -1;            // BLP_SHORT_CUS: CUs' worth of short-row scorer workgroups (default all)
-  bool lpt = false;              // BLP_LPT: run-grouped batches queue their sources largest (build + scan work) first
+  int lpt = 0;                   // BLP_LPT: sources queued largest (build + scan work) first -- bit 1: run-grouped
+                                 // batches, bit 2: item-grouped batches
   bool pair_gate = false;        // BLP_PAIR_GATE: blp_batches_score holds the other passes' grouping until the
                                  // large-universe pass's grouping is done
   std::string debug_null;        // BLP_DEBUG_NULL (BLP_DEBUG builds only): null this launch pointer, to
@@ -3418,7 +3424,7 @@ Knobs read_knobs() {
   k.item_nb = (int)num("BLP_ITEM_NB", 512);
   k.group_nblk = (int)num("BLP_GROUP_NBLK", -1);
   k.pair_gate = on("BLP_PAIR_GATE");
-  k.lpt = num("BLP_LPT", 0) != 0;
+  k.lpt = (int)num("BLP_LPT", 0);
   k.short_cus = (int)num("BLP_SHORT_CUS", -1);
   k.split16 = on("BLP_SPLIT16");
   k.host_plan = on("BLP_HOST_PLAN");
@@ -3966,7 +3972,7 @@ static int batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_
   }
   if (b->n_hash && hipMalloc(&b->d_active2, 4 * ((size_t)std::max<int64_t>(b->xspan, 1) + 1)) != hipSuccess)
     return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: hash flags"));
-  if (dev_plan && runs && kn.lpt && n_sources > 1) {
+  if (dev_plan && n_sources > 1 && ((runs && (kn.lpt & 1)) || (!runs && !kn.group_buckets && (kn.lpt & 2)))) {
     // BLP_LPT: the sources' queue order, largest estimated work (build w2[x] + scan sum |N(y)|) first
     ScopedBuf d_est, d_out, d_r;
     if ((rc = d_est.reserve(8 * (size_t)std::max<int64_t>(b->xspan, 1))) || (rc = d_out.reserve(8 * (size_t)n_sources)) ||
@@ -4390,7 +4396,7 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   hipLaunchKernelGGL(k_nz_count, dim3((unsigned)tx), dim3(SCAN_BLOCK), 0, b->stream, cnt + b->xlo, b->xspan, tx2); \
   hipLaunchKernelGGL(k_scan_mid, dim3(1), dim3(SCAN_BLOCK), 0, b->stream, tx2, tx, &b->d_misc->n_active);          \
   hipLaunchKernelGGL(k_nz_write, dim3((unsigned)tx), dim3(SCAN_BLOCK), 0, b->stream, cnt + b->xlo, b->xspan, tx2,  \
-                     b->xlo, b->active.as<int32_t>());                                                              \
+                     b->xlo, b->active.as<int32_t>(), b->d_rank, b->d_lpt);                                         \
   if (runs_w && ids_w)                                                                                                \
     hipLaunchKernelGGL((k_item_write_ids<(K <= 1024 ? K : 1024), 0>), dim3((unsigned)ub), dim3(GB_BLOCK), 0,         \
                        b->stream, g->d_rp, tmp, it_b, it_s, it_e, &b->d_misc->n_items, b->xlo, b->shift, ih, off,     \
@@ -4496,7 +4502,7 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
 
   a.off = b->off.as<int32_t>();
   a.cnt = b->cnt.as<int32_t>();
-  a.active = b->runs && b->d_lpt ? b->d_lpt : b->active.as<int32_t>();  // BLP_LPT: the largest-first queue
+  a.active = b->d_lpt ? b->d_lpt : b->active.as<int32_t>();  // BLP_LPT: the largest-first queue
   a.g_out = b->d_gout;
   a.g_yb = b->d_gyb;
   a.g_yl = b->d_gyl;
