@@ -295,4 +295,6 @@ using HostVec = std::vector<T, HostAlloc<T>>;
 // with sync_device, which first waits for all work queued on the device)
 int csr_build(int device, const int32_t* d_a, const int32_t* d_b, int64_t m, int64_t n, blp_csr** out,
               bool sync_device);
+// d_idx = 0..n-1 ordered by d_keys descending, ties by index (csr.hip; enqueued on st, then synced)
+int order_desc_u64(const uint64_t* d_keys, int64_t n, int32_t* d_idx, hipStream_t st);
 }  // namespace blp

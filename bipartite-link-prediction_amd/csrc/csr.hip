@@ -52,6 +52,11 @@ __global__ void k_low_halves(const uint64_t* keys, int64_t nnz, int32_t* ci) {
     ci[i] = (int32_t)(uint32_t)keys[i];
 }
 
+__global__ void k_iota(int32_t* v, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    v[i] = (int32_t)i;
+}
+
 }  // namespace
 
 using namespace blp;
@@ -267,3 +272,27 @@ int preload_csr() {
   return hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&k_edge_keys)) == hipSuccess ? 0 : -1;
 }
 }  // namespace blp
+
+// Indices 0..n-1 ordered by key descending, ties by index (a stable radix sort of (key, index)
+// pairs): blp_batch_create's largest-first source order (BLP_LPT), on the batch's stream.
+int blp::order_desc_u64(const uint64_t* d_keys, int64_t n, int32_t* d_idx, hipStream_t st) {
+  if (n <= 0) return BLP_OK;
+  DevBuf kout, iin, temp;
+  auto done = [&](int rc) {
+    BLP_HIP(hipStreamSynchronize(st));  // the scratch goes back after the sort ran
+    for (DevBuf* b : {&kout, &iin, &temp}) b->release();
+    return rc;
+  };
+  int rc;
+  if ((rc = kout.reserve(8 * n)) || (rc = iin.reserve(4 * n))) return done(rc);
+  hipLaunchKernelGGL(k_iota, dim3((unsigned)std::min<int64_t>(1024, (n + 255) / 256)), dim3(256), 0, st, iin.as<int32_t>(), n);
+  BLP_HIP_OR(hipGetLastError(), done);
+  size_t tb = 0;
+  BLP_HIP_OR(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, tb, d_keys, kout.as<uint64_t>(), iin.as<int32_t>(), d_idx,
+                                                          (int)n, 0, 64, st), done);
+  if ((rc = temp.reserve(std::max<size_t>(tb, 16)))) return done(rc);
+  tb = temp.bytes;
+  BLP_HIP_OR(hipcub::DeviceRadixSort::SortPairsDescending(temp.p, tb, d_keys, kout.as<uint64_t>(), iin.as<int32_t>(), d_idx,
+                                                          (int)n, 0, 64, st), done);
+  return done(BLP_OK);
+}

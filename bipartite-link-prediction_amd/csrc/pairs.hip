@@ -982,10 +982,11 @@ __global__ void k_src_est(const int32_t* __restrict__ srcs, int64_t n, const uns
     out[i] = est[srcs[i] - xlo] + w2[srcs[i]];
 }
 
-__global__ void k_src_rank(const int32_t* __restrict__ srcs, int64_t n, const int32_t* __restrict__ r, int32_t xlo,
+// ord[j] = list index of the source placed j-th: rank[srcs[ord[j]] - xlo] = j
+__global__ void k_src_rank(const int32_t* __restrict__ srcs, int64_t n, const int32_t* __restrict__ ord, int32_t xlo,
                            int32_t* __restrict__ rank) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    rank[srcs[i] - xlo] = r[i];
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x)
+    rank[srcs[ord[j]] - xlo] = (int32_t)j;
 }
 
 constexpr int DQ_MAX = 8;  // sources per dequeue (blp_batch::dq)
@@ -3990,14 +3991,8 @@ static int batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_
                        d_est.as<unsigned long long>(), reinterpret_cast<const unsigned long long*>(g->d_w2), (int32_t)xlo,
                        d_out.as<unsigned long long>());
     BLP_HIP_OR(hipGetLastError(), bail);
-    std::vector<unsigned long long> est((size_t)n_sources);
-    BLP_HIP_OR(hipMemcpyAsync(est.data(), d_out.p, 8 * (size_t)n_sources, hipMemcpyDeviceToHost, b->stream), bail);
-    BLP_HIP_OR(hipStreamSynchronize(b->stream), bail);
-    std::vector<int32_t> ord((size_t)n_sources), r((size_t)n_sources);
-    for (int64_t i = 0; i < n_sources; ++i) ord[i] = (int32_t)i;
-    std::stable_sort(ord.begin(), ord.end(), [&](int32_t p, int32_t q) { return est[p] > est[q]; });
-    for (int64_t j = 0; j < n_sources; ++j) r[ord[j]] = (int32_t)j;
-    BLP_HIP_OR(hipMemcpyAsync(d_r.p, r.data(), 4 * (size_t)n_sources, hipMemcpyHostToDevice, b->stream), bail);
+    // the order on the device (a stable radix sort), then rank[x - xlo] = place of x in it
+    if ((rc = order_desc_u64(d_out.as<uint64_t>(), n_sources, d_r.as<int32_t>(), b->stream))) return bail(rc);
     hipLaunchKernelGGL(k_src_rank, dim3(gs), dim3(256), 0, b->stream, d_srcs.as<int32_t>(), n_sources, d_r.as<int32_t>(),
                        (int32_t)xlo, b->d_rank);
     BLP_HIP_OR(hipGetLastError(), bail);
