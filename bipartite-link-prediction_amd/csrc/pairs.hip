@@ -4211,11 +4211,13 @@ int blp_batch_create_pair(blp_graph* g, const int32_t* x, const int32_t* y, int6
   BLP_CHECK(out_xy && out_yx, BLP_E_ARG, "blp_batch_create_pair: null outputs");
   blp_batch* a = nullptr;
   // the first batch (similarity.main's user pass) on a highest-priority stream: the two passes
-  // then run on different hardware queues (BLP_PAIR_SAME_PRIO=1: both from the normal pool)
-  int rc = create_or_release(g, x, y, n_pairs, nullptr, &a, !getenv("BLP_PAIR_SAME_PRIO"));
+  // then run on different hardware queues (BLP_PAIR_SAME_PRIO=1: both from the normal pool;
+  // BLP_PAIR_HI_SECOND=1: the second batch takes the highest-priority stream instead)
+  const bool same = getenv("BLP_PAIR_SAME_PRIO") != nullptr, second = getenv("BLP_PAIR_HI_SECOND") != nullptr;
+  int rc = create_or_release(g, x, y, n_pairs, nullptr, &a, !same && !second);
   if (rc) return rc;
   blp_batch* b = nullptr;
-  rc = create_or_release(g, y, x, n_pairs, a, &b);
+  rc = create_or_release(g, y, x, n_pairs, a, &b, !same && second);
   if (rc) {
     blp_batch_destroy(a);
     return rc;
