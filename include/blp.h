@@ -329,7 +329,9 @@ int blp_hop3_sample(blp_graph* g, const int32_t* src, int64_t n_src, const int32
  *   blp_topk_create:      builds the degree-ordered target numbering, the permuted source rows
  *                         and (memory permitting) the expanded wedge rows; blp_topk_info
  *                         reports the counter chunks, tier sizes and wedge entries (-1: none).
- *   blp_topk_set_sources: uploads the sources (kept in HBM across runs).
+ *   blp_topk_set_sources: uploads the sources (kept in HBM across runs) and plans the order the
+ *     workgroups claim them in: largest two-hop walk first (BLP_TK_ORDER=0: list order). Results
+ *     are indexed by the sources' list positions either way.
  *   blp_topk_run:         k in [1, 256], mask of BLP_CN | BLP_JACCARD | BLP_ADAMIC; async.
  *   blp_topk_fetch:       one method's [n_src][k] lists (col -1 / score 0 past the end) and
  *                         n_cand[i] = |H3(src[i])|, the number of candidates scored.
