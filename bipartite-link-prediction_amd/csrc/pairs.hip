@@ -3382,8 +3382,9 @@ struct Knobs {
                                  // 2.271 / 2.261 against 2.317 / 2.315 ms with 2048, r05_group_geometry)
   int group_nblk = -1;           // BLP_GROUP_NBLK: hist / scatter workgroups (default 2 per CU)
   int short_cus = -1;            // BLP_SHORT_CUS: CUs' worth of short-row scorer workgroups (default all)
-  int lpt = 0;                   // BLP_LPT: sources queued largest (build + scan work) first -- bit 1: run-grouped
-                                 // batches, bit 2: item-grouped batches
+  int lpt = 1;                   // BLP_LPT: sources queued largest (build + scan work) first -- bit 1: run-grouped
+                                 // batches (the default: config-2 step 2.243 / 2.238 / 2.233 -> 2.214 / 2.211 /
+                                 // 2.213 ms, r05_pair_hi_second), bit 2: item-grouped batches (no gain); 0: id order
   bool pair_gate = false;        // BLP_PAIR_GATE: blp_batches_score holds the other passes' grouping until the
                                  // large-universe pass's grouping is done
   std::string debug_null;        // BLP_DEBUG_NULL (BLP_DEBUG builds only): null this launch pointer, to
@@ -3425,7 +3426,7 @@ Knobs read_knobs() {
   k.item_nb = (int)num("BLP_ITEM_NB", 512);
   k.group_nblk = (int)num("BLP_GROUP_NBLK", -1);
   k.pair_gate = on("BLP_PAIR_GATE");
-  k.lpt = (int)num("BLP_LPT", 0);
+  k.lpt = (int)num("BLP_LPT", 1);
   k.short_cus = (int)num("BLP_SHORT_CUS", -1);
   k.split16 = on("BLP_SPLIT16");
   k.host_plan = on("BLP_HOST_PLAN");
