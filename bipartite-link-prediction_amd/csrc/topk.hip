@@ -1358,6 +1358,7 @@ struct blp_topk {
   int64_t aa_chunk = 0;
   DevBuf perm, inv, tdeg, ge, pci, d_chunks, src, order, keys, cols, ncand, counters, wtab, x2_off, x2;
   bool ordered = false;  // t->order holds a largest-first dequeue order of the sources
+  std::vector<int32_t> h_perm;  // target offset -> permuted id (the hot targets are p < dw_n)
   DevBuf dw_cv, dw_ca, dw_bm, dw_info, dw_caf;  // dense counts of the hot targets (see the header comment)
   int64_t dw_n = 0, dw_words = 0, dw_bmw = 0;
   int64_t kbase = 0, x2_entries = -1;
@@ -1511,6 +1512,7 @@ extern "C" int blp_topk_create(blp_graph* g, int64_t src_lo, int64_t src_hi, int
     inv[j] = (int32_t)(tgt_lo + order[j]);
     tdeg[j] = (int32_t)(rp[tgt_lo + order[j] + 1] - rp[tgt_lo + order[j]]);
   }
+  t->h_perm = perm;
   // counter tiers: CN(x, b) <= |N(b)|, so |N(b)| <= 255 fits a u8 and <= 65535 a u16.
   // BLP_TOPK_T8 / BLP_TOPK_T16 lower the limits and BLP_TOPK_ACC_WORDS the counter space
   // (test knobs for the u32 tier and the multi-chunk path).
@@ -1716,12 +1718,23 @@ extern "C" int blp_topk_set_sources(blp_topk* t, const int32_t* src, int64_t n_s
   // finishing last on a few CUs (BLP_TK_ORDER=0: list order). Results land by list index.
   t->ordered = false;
   const int32_t* ci = host_col_idx(t->g);
-  if (n_src > 1 && ci && env_i64("BLP_TK_ORDER", 1) != 0) {
+  const int64_t how = env_i64("BLP_TK_ORDER", 1);
+  if (n_src > 1 && ci && how != 0) {
     const int64_t* rp = t->g->hrp;
+    // 1: the walk's wedges, sum |N(b)|; 2 (measurement): its pushes, sum w2[b] over the walked
+    // targets plus the counter words of each dense (hot) target's add
+    const bool pushes = how == 2 && (int64_t)t->g->h_w2.size() > t->thi - 1 && (int64_t)t->h_perm.size() == t->T;
     std::vector<int64_t> est((size_t)n_src);
     for (int64_t i = 0; i < n_src; ++i) {
       int64_t w = 0;
-      for (int64_t e = rp[src[i]]; e < rp[src[i] + 1]; ++e) w += rp[ci[e] + 1] - rp[ci[e]];
+      for (int64_t e = rp[src[i]]; e < rp[src[i] + 1]; ++e) {
+        if (!pushes)
+          w += rp[ci[e] + 1] - rp[ci[e]];
+        else if (t->h_perm[ci[e] - t->tlo] < t->dw_n)
+          w += t->dw_words;
+        else
+          w += (int64_t)t->g->h_w2[ci[e]];
+      }
       est[i] = w;
     }
     std::vector<int32_t> ord((size_t)n_src);

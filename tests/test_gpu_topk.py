@@ -256,13 +256,14 @@ def test_topk_largest_first_order_matches_list_order(small, monkeypatch):
     G, adj, rng = small
     src = rng.choice(G.n_col0, 48, replace=False)
     got = {}
-    for order in ("0", "1"):
+    for order in ("0", "1", "2"):
         monkeypatch.setenv("BLP_TK_ORDER", order)
         T = blp.TopK(G, "user")
         T.set_sources(src)
         T.run(15, ALL)
         got[order] = [T.fetch(m) for m in METHODS]
-    for r0, r1 in zip(got["0"], got["1"]):
-        for x, y in zip(r0, r1):
-            assert np.array_equal(x, y)
+    for o in ("1", "2"):
+        for r0, r1 in zip(got["0"], got[o]):
+            for x, y in zip(r0, r1):
+                assert np.array_equal(x, y)
     check_against_oracle(G, blp.TopK(G, "user"), adj, src, 15)
