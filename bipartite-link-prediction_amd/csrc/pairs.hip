@@ -366,7 +366,10 @@ __global__ __launch_bounds__(GB_BLOCK) void k_bucket_group(const int64_t* __rest
 //                 run inside [off, off + cnt) (fill), then LDS cursors place every pair
 // Order within one source's group follows item order (not caller order): every grouped pair
 // carries its caller index (g_out), so results do not depend on it.
-constexpr int GI_PAIRS = 4096;
+#ifndef BLP_GI_PAIRS
+#define BLP_GI_PAIRS 4096
+#endif
+constexpr int GI_PAIRS = BLP_GI_PAIRS;
 
 __global__ __launch_bounds__(1024) void k_item_plan(const int32_t* __restrict__ hoff, int nblk, int nb, int64_t np,
                                                     int32_t* __restrict__ item_b, int32_t* __restrict__ item_s,
