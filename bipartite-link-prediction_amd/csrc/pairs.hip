@@ -196,7 +196,10 @@ __global__ __launch_bounds__(GP_BLOCK) void k_bucket_hist(const int32_t* __restr
   for (int i = threadIdx.x; i < nb; i += GP_BLOCK) h[i] = 0;
   __syncthreads();
   const int64_t b0 = (int64_t)blockIdx.x * per_blk, b1 = min(np, b0 + per_blk);
-  constexpr int U = 4;
+#ifndef BLP_HIST_U
+#define BLP_HIST_U 4
+#endif
+  constexpr int U = BLP_HIST_U;
   for (int64_t r = b0; r < b1; r += U * GP_BLOCK) {
     int xv[U];
 #pragma unroll
@@ -398,7 +401,10 @@ __device__ inline void item_hist(const int4* __restrict__ tmp, int s, int e, int
                                  const int32_t* __restrict__ keys = nullptr) {
   for (int i = threadIdx.x; i < KEYS; i += GB_BLOCK) h[i] = 0;
   __syncthreads();
-  constexpr int UC = 4;  // GI_PAIRS / GB_BLOCK = 16 pairs per thread: UC loads in flight
+#ifndef BLP_ITEMC_U
+#define BLP_ITEMC_U 4
+#endif
+  constexpr int UC = BLP_ITEMC_U;  // GI_PAIRS / GB_BLOCK = 16 pairs per thread: UC loads in flight
   for (int kr = s; kr < e; kr += UC * GB_BLOCK) {
     int xv[UC];
 #pragma unroll
