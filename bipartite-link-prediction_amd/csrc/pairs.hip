@@ -197,7 +197,7 @@ __global__ __launch_bounds__(GP_BLOCK) void k_bucket_hist(const int32_t* __restr
   __syncthreads();
   const int64_t b0 = (int64_t)blockIdx.x * per_blk, b1 = min(np, b0 + per_blk);
 #ifndef BLP_HIST_U
-#define BLP_HIST_U 4
+#define BLP_HIST_U 8  // (with BLP_ITEMC_U 8 and BLP_SCATTER_U 12: r05_group_rounds)
 #endif
   constexpr int U = BLP_HIST_U;
   for (int64_t r = b0; r < b1; r += U * GP_BLOCK) {
@@ -233,7 +233,7 @@ __global__ __launch_bounds__(GP_BLOCK) void k_bucket_scatter(const int32_t* __re
   __syncthreads();
   const int64_t b0 = (int64_t)blockIdx.x * per_blk, b1 = min(np, b0 + per_blk);
 #ifndef BLP_SCATTER_U
-#define BLP_SCATTER_U 8  // 8: 2.230 / 2.231 / 2.230 against 2.261 / 2.272 / 2.261 ms with 4 (r05_scatter_u)
+#define BLP_SCATTER_U 12  // 8: 2.230 / 2.231 / 2.230 against 2.261 / 2.272 / 2.261 ms with 4 (r05_scatter_u); 12: r05_group_rounds
 #endif
   constexpr int U = BLP_SCATTER_U;  // U pairs per thread per round: loads and LDS atomics overlap
   for (int64_t r = b0; r < b1; r += U * GP_BLOCK) {
@@ -402,7 +402,7 @@ __device__ inline void item_hist(const int4* __restrict__ tmp, int s, int e, int
   for (int i = threadIdx.x; i < KEYS; i += GB_BLOCK) h[i] = 0;
   __syncthreads();
 #ifndef BLP_ITEMC_U
-#define BLP_ITEMC_U 4
+#define BLP_ITEMC_U 8
 #endif
   constexpr int UC = BLP_ITEMC_U;  // GI_PAIRS / GB_BLOCK = 16 pairs per thread: UC loads in flight
   for (int kr = s; kr < e; kr += UC * GB_BLOCK) {
