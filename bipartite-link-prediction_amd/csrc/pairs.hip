@@ -3394,7 +3394,8 @@ struct Knobs {
   int lpt = 1;                   // BLP_LPT: sources queued largest (build + scan work) first -- bit 1: run-grouped
                                  // batches (the default: config-2 step 2.243 / 2.238 / 2.233 -> 2.214 / 2.211 /
                                  // 2.213 ms, r05_pair_hi_second), bit 2: item-grouped batches (no gain); 0: id order
-  bool no_keys = false;          // BLP_NO_KEYS: the scatter writes no 4-byte key array (item counts read the records)
+  bool no_keys = true;           // the scatter writes no 4-byte key array (item counts read the records);
+                                 // BLP_SCATTER_KEYS=1 writes it
   bool pair_gate = false;        // BLP_PAIR_GATE: blp_batches_score holds the other passes' grouping until the
                                  // large-universe pass's grouping is done
   std::string debug_null;        // BLP_DEBUG_NULL (BLP_DEBUG builds only): null this launch pointer, to
@@ -3436,7 +3437,7 @@ Knobs read_knobs() {
   k.item_nb = (int)num("BLP_ITEM_NB", 512);
   k.group_nblk = (int)num("BLP_GROUP_NBLK", -1);
   k.pair_gate = on("BLP_PAIR_GATE");
-  k.no_keys = on("BLP_NO_KEYS");
+  k.no_keys = !on("BLP_SCATTER_KEYS");
   k.lpt = (int)num("BLP_LPT", 1);
   k.short_cus = (int)num("BLP_SHORT_CUS", -1);
   k.split16 = on("BLP_SPLIT16");
@@ -4374,7 +4375,9 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
     const int64_t ikeys = b->items ? (b->xspan + b->nb - 1) >> b->shift : 0;
     const bool rec_rows = b->items && ikeys <= 1024 && !b->d_gy && g->nnz < (int64_t(1) << 31) &&
                           !b->kn.group_gather && !b->kn.group_rows16;
-    // (BLP_NO_KEYS: no key array; the item counts read the records' x)
+    // no key array by default: its 512 scattered write streams per block, beside the records',
+    // overflowed the XCD's L2 (3x the written bytes, r05_group_pmc); the item counts read the
+    // records' x instead (2.13-2.15 against 2.18-2.20 ms, r05_scatter_nokeys; BLP_SCATTER_KEYS=1: the array)
     int32_t* keyarr = b->items && !b->kn.no_keys
                           ? reinterpret_cast<int32_t*>(tmp + np) + b->xspan + 3 * ub + 2 * (tx + 1) + 1024 * ub
                           : nullptr;

@@ -160,7 +160,7 @@ def test_general_graph_exact_distance(gpu):
     {"BLP_GROUP_GATHER": "1"},                          # rows gathered by the grouping write, not carried by the scatter
     {"BLP_ITEM_NB": "1"},                               # one interleaved bucket (or the fewest that keep <= 1024 keys)
     {"BLP_ITEM_NB": "4", "BLP_GROUP_NBLK": "3"},        # few buckets, few scatter workgroups
-    {"BLP_NO_KEYS": "1"},                               # item counts read the scattered records' x (no key array)
+    {"BLP_SCATTER_KEYS": "1"},                          # the scatter's key array for the item counts (default: the records' x)
     {"BLP_LPT": "0"},                                   # run-grouped sources queued in id order (default: largest work first)
     {"BLP_LPT": "3"},                                   # ... and item-grouped ones
     {"BLP_LPT": "3", "BLP_SPLIT": "3", "BLP_HASH_WORK": "600"},  # ... with the hash-set partition of the queue
