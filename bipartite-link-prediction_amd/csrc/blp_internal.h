@@ -53,11 +53,23 @@ struct DevBuf {
   size_t bytes = 0;
   int dev = -1;  // the device the block belongs to (release returns it to that device's cache)
   int reserve(size_t want);
-  void release();
+  // back to the device scratch cache after a device sync, or freed; a failed sync (a fault in
+  // work queued earlier) is recorded as the last error and returned, and the block is then freed,
+  // never cached
+  int release();
   template <class T> T* as() const { return reinterpret_cast<T*>(p); }
 };
 // empty the device scratch cache of `device` (DevBuf blocks kept for reuse; graph.hip)
 void dev_cache_flush(int device);
+// bytes the scratch cache of `device` holds (free for any allocation that flushes it)
+size_t dev_cache_bytes(int device);
+// hipMalloc on the current device; out of memory empties the device scratch cache and tries once
+// more (every raw device allocation goes through it: cached blocks must not starve them)
+hipError_t dev_malloc(void** p, size_t bytes);
+template <class T>
+hipError_t dev_malloc(T** p, size_t bytes) {
+  return dev_malloc(reinterpret_cast<void**>(p), bytes);
+}
 // A DevBuf freed when it leaves scope (temporaries on paths with early returns).
 struct ScopedBuf : DevBuf {
   ScopedBuf() = default;
@@ -255,12 +267,7 @@ void prefault_host(void* p, size_t bytes);
 // first touch takes one fault per 2 MiB instead of per 4 KiB and the release is one munmap of a
 // few hundred pages. Smaller sizes (and BLP_NO_THP=1) use malloc. Null on failure.
 void* host_alloc(size_t bytes);
-// A host<->device copy of `bytes` on stream st, complete on return. BLP_PIN_COPY=1 (round-5 A/B):
-// a host range of >= 1 MiB is registered with the HIP runtime for the copy and unregistered right
-// after, so the runtime does not pin the caller's pages implicitly (an implicit pinning that
-// outlives the copy is invalidated when the memory is unmapped later, and the driver then stalls
-// the process's GPU queues until it restores them). Otherwise, or if registration fails, a plain
-// pageable copy.
+// A host<->device copy of `bytes` on stream st, complete on return.
 int copy_sync(void* dst, const void* src, size_t bytes, hipMemcpyKind kind, hipStream_t st);
 void host_free(void* p, size_t bytes);
 // std allocator over host_alloc that leaves elements uninitialised on resize()

@@ -109,8 +109,8 @@ int blp::csr_build(int device, const int32_t* d_a, const int32_t* d_b, int64_t m
   };
   int rc;
   const int64_t mk = 2 * m;
-  BLP_HIP_OR(hipMalloc(&c->d_rp, 8 * (n + 1)), done);
-  BLP_HIP_OR(hipMalloc(&c->d_self, std::max<int64_t>(n, 1)), done);
+  BLP_HIP_OR(dev_malloc(&c->d_rp, 8 * (n + 1)), done);
+  BLP_HIP_OR(dev_malloc(&c->d_self, std::max<int64_t>(n, 1)), done);
   if ((rc = flag.reserve(4)) || (rc = nsel.reserve(8))) return done(rc);
   BLP_HIP_OR(hipMemsetAsync(c->d_self, 0, std::max<int64_t>(n, 1), st), done);
   BLP_HIP_OR(hipMemsetAsync(flag.p, 0, 4, st), done);
@@ -158,7 +158,7 @@ int blp::csr_build(int device, const int32_t* d_a, const int32_t* d_b, int64_t m
     hipLaunchKernelGGL(k_row_ptr, dim3(2048), dim3(256), 0, st, uq, nnz, n, c->d_rp);
     BLP_HIP_OR(hipGetLastError(), done);
   }
-  BLP_HIP_OR(hipMalloc(&c->d_ci, sizeof(int32_t) * (nnz + 2 * CI_PAD)), done);
+  BLP_HIP_OR(dev_malloc(&c->d_ci, sizeof(int32_t) * (nnz + 2 * CI_PAD)), done);
   c->d_ci += CI_PAD;
   BLP_HIP_OR(hipMemsetAsync(c->d_ci - CI_PAD, 0, sizeof(int32_t) * (nnz + 2 * CI_PAD), st), done);
   if (nnz) {
@@ -279,8 +279,12 @@ int blp::order_desc_u64(const uint64_t* d_keys, int64_t n, int32_t* d_idx, hipSt
   if (n <= 0) return BLP_OK;
   DevBuf kout, iin, temp;
   auto done = [&](int rc) {
-    BLP_HIP(hipStreamSynchronize(st));  // the scratch goes back after the sort ran
-    for (DevBuf* b : {&kout, &iin, &temp}) b->release();
+    const hipError_t se = hipStreamSynchronize(st);  // the scratch goes back after the sort ran
+    for (DevBuf* b : {&kout, &iin, &temp}) {
+      const int r = b->release();
+      if (!rc) rc = r;
+    }
+    if (se != hipSuccess && !rc) rc = hip_fail(se, "hipStreamSynchronize (order_desc_u64)", __FILE__, __LINE__);
     return rc;
   };
   int rc;

@@ -158,7 +158,8 @@ int DevBuf::reserve(size_t want) {
   return BLP_OK;
 }
 
-void DevBuf::release() {
+int DevBuf::release() {
+  int rc = BLP_OK;
   if (p) {
     const int64_t t0 = slow_clock();
     bool kept = false;
@@ -169,9 +170,12 @@ void DevBuf::release() {
       int cur = -1;
       (void)hipGetDevice(&cur);
       if (cur != dev) (void)hipSetDevice(dev);
-      const bool synced = hipDeviceSynchronize() == hipSuccess;
+      const hipError_t se = hipDeviceSynchronize();
       if (cur != dev && cur >= 0) (void)hipSetDevice(cur);
-      if (synced) {
+      if (se != hipSuccess) {
+        rc = hip_fail(se, "hipDeviceSynchronize (DevBuf::release: work queued before the release failed)", __FILE__,
+                      __LINE__);
+      } else {
         std::lock_guard<std::mutex> lk(g_dc_mu);
         if ((size_t)dev >= g_dc.size()) g_dc.resize((size_t)dev + 1);
         DevCache& c = g_dc[dev];
@@ -188,6 +192,26 @@ void DevBuf::release() {
   p = nullptr;
   bytes = 0;
   dev = -1;
+  return rc;
+}
+
+size_t dev_cache_bytes(int device) {
+  std::lock_guard<std::mutex> lk(g_dc_mu);
+  return (size_t)device < g_dc.size() ? g_dc[device].bytes : 0;
+}
+
+hipError_t dev_malloc(void** p, size_t bytes) {
+  hipError_t e = hipMalloc(p, bytes);
+  if (e == hipErrorOutOfMemory) {
+    (void)hipGetLastError();
+    const int dev = current_device();
+    if (dev_cache_bytes(dev)) {
+      dev_cache_flush(dev);
+      e = hipMalloc(p, bytes);
+    }
+  }
+  if (e != hipSuccess) *p = nullptr;
+  return e;
 }
 
 int set_device(const blp_graph* g) {
@@ -235,20 +259,8 @@ void* host_alloc(size_t bytes) {
 
 int copy_sync(void* dst, const void* src, size_t bytes, hipMemcpyKind kind, hipStream_t st) {
   if (!bytes) return BLP_OK;
-  static const bool pin = getenv("BLP_PIN_COPY") && atoi(getenv("BLP_PIN_COPY")) > 0;
-  void* reg = nullptr;
-  if (pin && bytes >= (size_t(1) << 20) && (kind == hipMemcpyHostToDevice || kind == hipMemcpyDeviceToHost)) {
-    const uintptr_t h = (uintptr_t)(kind == hipMemcpyHostToDevice ? src : dst);
-    const uintptr_t b = h & ~uintptr_t(4095), e = (h + bytes + 4095) & ~uintptr_t(4095);
-    if (hipHostRegister((void*)b, e - b, hipHostRegisterDefault) == hipSuccess ||
-        (kind == hipMemcpyHostToDevice && hipHostRegister((void*)b, e - b, hipHostRegisterReadOnly) == hipSuccess))
-      reg = (void*)b;
-    else
-      (void)hipGetLastError();  // not registrable (already registered, ...): a pageable copy
-  }
   hipError_t err = hipMemcpyAsync(dst, src, bytes, kind, st);
   if (err == hipSuccess) err = hipStreamSynchronize(st);
-  if (reg) (void)hipHostUnregister(reg);
   if (err != hipSuccess) return hip_fail(err, "copy_sync", __FILE__, __LINE__);
   return BLP_OK;
 }
@@ -340,7 +352,7 @@ int build_weight_codes(blp_graph* g, const int64_t* row_ptr, const std::vector<l
   int max_codes = (1 << cbits) - 1;
   if (const char* e = getenv("BLP_WCODES")) max_codes = std::min(max_codes, std::max(0, atoi(e)));  // test knob
   std::vector<long long> wtab(256, 0);
-  BLP_HIP(hipMalloc(&g->d_wtab, sizeof(long long) * 256));  // always: code 0 reads wtab[0]
+  BLP_HIP(dev_malloc(&g->d_wtab, sizeof(long long) * 256));  // always: code 0 reads wtab[0]
   BLP_HIP(hipMemcpy(g->d_wtab, wtab.data(), sizeof(long long) * 256, hipMemcpyHostToDevice));
   if (max_codes <= 0 || nnz == 0) return BLP_OK;
   const bool gprof = getenv("BLP_GRAPH_PROF") != nullptr;
@@ -389,11 +401,11 @@ int build_weight_codes(blp_graph* g, const int64_t* row_ptr, const std::vector<l
   stage("ncode");
   uint8_t* d_ncode = nullptr;
   BLP_HIP(hipMemcpy(g->d_wtab, wtab.data(), sizeof(long long) * 256, hipMemcpyHostToDevice));
-  BLP_HIP(hipMalloc(&g->d_ci_w, sizeof(int32_t) * (nnz + 2 * CI_PAD)));
+  BLP_HIP(dev_malloc(&g->d_ci_w, sizeof(int32_t) * (nnz + 2 * CI_PAD)));
   BLP_HIP(hipMemset(g->d_ci_w, 0, sizeof(int32_t) * (nnz + 2 * CI_PAD)));
   g->d_ci_w += CI_PAD;
   stage("alloc");
-  BLP_HIP(hipMalloc(&d_ncode, (size_t)n));
+  BLP_HIP(dev_malloc(&d_ncode, (size_t)n));
   BLP_HIP(hipMemcpy(d_ncode, ncode.data(), (size_t)n, hipMemcpyHostToDevice));
   hipLaunchKernelGGL(k_code_ids, dim3((unsigned)std::min<int64_t>((nnz + 255) / 256, 1 << 20)), dim3(256), 0, g->stream,
                      g->d_ci, nnz, d_ncode, bits, g->d_ci_w);
@@ -444,7 +456,7 @@ int graph_finish(blp_graph* g, const double* aaw) {
   if (aaw) {
     std::vector<long long> fx;
     if (int rc = aa_weights_fixed(aaw, n, fx)) return rc;
-    BLP_HIP(hipMalloc(&g->d_aaw_fx, sizeof(long long) * std::max<int64_t>(n, 1)));
+    BLP_HIP(dev_malloc(&g->d_aaw_fx, sizeof(long long) * std::max<int64_t>(n, 1)));
     if (n) {
       if (int rc = copy_sync(g->d_aaw_fx, fx.data(), sizeof(long long) * n, hipMemcpyHostToDevice, g->stream)) return rc;
     }
@@ -706,10 +718,10 @@ int blp_graph_create(const int64_t* row_ptr, const int32_t* col_idx, int64_t n, 
   g->nnz = nnz;
   int rc = BLP_OK;
   if ((rc = [&]() -> int {
-         BLP_HIP(hipMalloc(&g->d_rp, sizeof(int64_t) * (n + 1)));
+         BLP_HIP(dev_malloc(&g->d_rp, sizeof(int64_t) * (n + 1)));
          // padded on both sides (CI_PAD ids): the scorers read rows in 16-byte vectors, up to
          // 15 ids past a row end or before a row start
-         BLP_HIP(hipMalloc(&g->d_ci, sizeof(int32_t) * (nnz + 2 * CI_PAD)));
+         BLP_HIP(dev_malloc(&g->d_ci, sizeof(int32_t) * (nnz + 2 * CI_PAD)));
          BLP_HIP(hipMemset(g->d_ci, 0, sizeof(int32_t) * (nnz + 2 * CI_PAD)));
          g->d_ci += CI_PAD;
          BLP_HIP(hipMemcpy(g->d_rp, row_ptr, sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice));

@@ -461,8 +461,8 @@ const WedgeBitmaps* wedge_bitmaps(blp_graph* g, int64_t lo, int64_t hi, int* rc)
       if (e != hipSuccess) *rc = hip_fail(e, what, __FILE__, __LINE__);
       return e == hipSuccess;
     };
-    bool ok = hip(hipMalloc(&w.d_slot, 4 * (size_t)g->n), "hipMalloc") &&
-              hip(hipMalloc(&w.d_pool, 4 * (size_t)words * rows.size()), "hipMalloc (wedge bitmaps)");
+    bool ok = hip(dev_malloc(&w.d_slot, 4 * (size_t)g->n), "hipMalloc") &&
+              hip(dev_malloc(&w.d_pool, 4 * (size_t)words * rows.size()), "hipMalloc (wedge bitmaps)");
     if (ok && (*rc = d_rows.reserve(4 * rows.size())) != BLP_OK) ok = false;
     ok = ok && hip(hipMemcpy(w.d_slot, w.h_slot.data(), 4 * (size_t)g->n, hipMemcpyHostToDevice), "hipMemcpy") &&
          hip(hipMemcpy(d_rows.p, order.data(), 4 * order.size(), hipMemcpyHostToDevice), "hipMemcpy");
@@ -548,15 +548,15 @@ extern "C" int blp_hop3_sample(blp_graph* g, const int32_t* src, int64_t n_src, 
     }
     return 0;
   };
-  if ((rc = hip(hipMalloc(&d_src, 4 * std::max<int64_t>(n_src, 1)), "hipMalloc"))) return rc;
-  if ((rc = hip(hipMalloc(&d_off, 4 * (n_src + 1)), "hipMalloc"))) return rc;
-  if ((rc = hip(hipMalloc(&d_pos, 4 * std::max<int64_t>(npos, 1)), "hipMalloc"))) return rc;
-  if ((rc = hip(hipMalloc(&d_cnt, 16), "hipMalloc"))) return rc;
+  if ((rc = hip(dev_malloc(&d_src, 4 * std::max<int64_t>(n_src, 1)), "hipMalloc"))) return rc;
+  if ((rc = hip(dev_malloc(&d_off, 4 * (n_src + 1)), "hipMalloc"))) return rc;
+  if ((rc = hip(dev_malloc(&d_pos, 4 * std::max<int64_t>(npos, 1)), "hipMalloc"))) return rc;
+  if ((rc = hip(dev_malloc(&d_cnt, 16), "hipMalloc"))) return rc;
   const int64_t dcap = std::max<int64_t>(cap, 1);
-  if ((rc = hip(hipMalloc(&d_x, 4 * dcap), "hipMalloc"))) return rc;
-  if ((rc = hip(hipMalloc(&d_y, 4 * dcap), "hipMalloc"))) return rc;
-  if ((rc = hip(hipMalloc(&d_l, dcap), "hipMalloc"))) return rc;
-  if (global && !wedge && (rc = hip(hipMalloc(&d_gbm, 4 * (size_t)gwords * g->n_cu), "hipMalloc (HBM bitmaps)")))
+  if ((rc = hip(dev_malloc(&d_x, 4 * dcap), "hipMalloc"))) return rc;
+  if ((rc = hip(dev_malloc(&d_y, 4 * dcap), "hipMalloc"))) return rc;
+  if ((rc = hip(dev_malloc(&d_l, dcap), "hipMalloc"))) return rc;
+  if (global && !wedge && (rc = hip(dev_malloc(&d_gbm, 4 * (size_t)gwords * g->n_cu), "hipMalloc (HBM bitmaps)")))
     return rc;
   if (n_src) {
     if ((rc = hip(hipMemcpy(d_src, src, 4 * n_src, hipMemcpyHostToDevice), "hipMemcpy"))) return rc;

@@ -88,10 +88,10 @@ int build_hot_index(blp_graph* g) {
   if (!g->n_hot) return BLP_OK;
   g->h_hot_idx = idx;
   int32_t* d_rows = nullptr;
-  BLP_HIP(hipMalloc(&g->d_hot_idx, 4 * g->n));
-  BLP_HIP(hipMalloc(&g->d_hot_tab, sizeof(HotRow) * tab.size()));
-  BLP_HIP(hipMalloc(&g->d_hot_pool, 4 * g->hot_pool_words));
-  BLP_HIP(hipMalloc(&d_rows, 4 * rows.size()));
+  BLP_HIP(dev_malloc(&g->d_hot_idx, 4 * g->n));
+  BLP_HIP(dev_malloc(&g->d_hot_tab, sizeof(HotRow) * tab.size()));
+  BLP_HIP(dev_malloc(&g->d_hot_pool, 4 * g->hot_pool_words));
+  BLP_HIP(dev_malloc(&d_rows, 4 * rows.size()));
   BLP_HIP(hipMemcpy(g->d_hot_idx, idx.data(), 4 * g->n, hipMemcpyHostToDevice));
   BLP_HIP(hipMemcpy(g->d_hot_tab, tab.data(), sizeof(HotRow) * tab.size(), hipMemcpyHostToDevice));
   BLP_HIP(hipMemcpy(d_rows, rows.data(), 4 * rows.size(), hipMemcpyHostToDevice));

@@ -7,10 +7,12 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <climits>
 #include <cstdio>
 #include <cstdlib>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -395,6 +397,108 @@ unsigned grid_for(int64_t n, int n_cu) {
   return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, (int64_t)n_cu * 16));
 }
 
+// The graph.txt upload (round 6). Up to round 5 the text was read into a fresh host buffer that
+// was registered with the runtime for the one copy, unregistered and freed. Every call then
+// pinned, unpinned and unmapped host pages, and a range the runtime had pinned could come back at
+// the same virtual address in a later call (malloc memory under 4 MiB, mmap above); one such
+// call faulted in the driver's suite (GPUTEST_r05: hipErrorIllegalAddress at the upload). Now the
+// text only ever passes through a ring of pinned slots that belongs to the process: allocated once
+// per device (hipHostMalloc), never registered, unregistered or freed while the library is loaded.
+// Reader threads pread chunk i into slot i % SLOTS and queue its copy; before a slot is refilled
+// its previous copy's event is waited on. The reads and the DMA overlap.
+constexpr int UP_THREADS = 8;                 // reader threads
+constexpr int UP_SLOTS = 2 * UP_THREADS;      // each reader double-buffers its own slots
+constexpr size_t UP_SLOT = size_t(2) << 20;   // bytes per slot: 32 MiB pinned per device
+struct Staging {
+  std::mutex mu;  // one upload at a time uses the ring
+  uint8_t* host = nullptr;
+  hipEvent_t ev[UP_SLOTS] = {};
+  bool pending[UP_SLOTS] = {};  // ev[s] records a copy out of slot s
+};
+std::mutex g_staging_mu;
+std::vector<Staging*> g_staging;  // [device]; never freed (pinned memory the process keeps)
+
+// the ring of `device` (the current device), created on first use; null + error on failure
+Staging* staging_of(int device) {
+  std::lock_guard<std::mutex> lk(g_staging_mu);
+  if ((size_t)device >= g_staging.size()) g_staging.resize((size_t)device + 1, nullptr);
+  if (g_staging[device]) return g_staging[device];
+  auto* s = new Staging();
+  hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&s->host), UP_SLOT * UP_SLOTS, hipHostMallocDefault);
+  for (int k = 0; k < UP_SLOTS && e == hipSuccess; ++k) e = hipEventCreateWithFlags(&s->ev[k], hipEventDisableTiming);
+  if (e != hipSuccess) {
+    hip_fail(e, "graph.txt staging ring", __FILE__, __LINE__);
+    for (int k = 0; k < UP_SLOTS; ++k)
+      if (s->ev[k]) (void)hipEventDestroy(s->ev[k]);
+    if (s->host) (void)hipHostFree(s->host);
+    delete s;
+    return nullptr;
+  }
+  g_staging[device] = s;
+  return s;
+}
+
+// Reads bytes [0, S) of fd into d_txt on stream st through the ring; complete (the stream
+// synchronized) on return. *read_ok = false when a read failed (the host parser then reports it);
+// a HIP failure is returned. chunk: bytes per slot fill (<= UP_SLOT; BLP_PARSE_CHUNK_KB test knob).
+int staged_upload(Staging* sg, int fd, int64_t S, uint8_t* d_txt, hipStream_t st, size_t chunk, bool* read_ok) {
+  std::lock_guard<std::mutex> lk(sg->mu);
+  const int64_t nch = (S + (int64_t)chunk - 1) / (int64_t)chunk;
+  const int nt = (int)std::min<int64_t>(UP_THREADS, nch);
+  std::mutex q_mu;  // a copy and the event recorded behind it are queued together
+  std::atomic<int> bad_read{0};
+  std::atomic<int> hip_err{(int)hipSuccess};
+  std::atomic<int> err_line{0};
+  auto reader = [&](int t) {
+    for (int64_t i = t; i < nch; i += nt) {
+      if (bad_read.load(std::memory_order_relaxed) || hip_err.load(std::memory_order_relaxed) != hipSuccess) return;
+      const int s = (int)(i % UP_SLOTS);  // UP_SLOTS is a multiple of nt's bound: slot s is this reader's
+      uint8_t* buf = sg->host + (size_t)s * UP_SLOT;
+      if (sg->pending[s]) {  // the slot's previous copy must have left it
+        const hipError_t e = hipEventSynchronize(sg->ev[s]);
+        if (e != hipSuccess) {
+          err_line = __LINE__;
+          hip_err = (int)e;
+          return;
+        }
+        sg->pending[s] = false;
+      }
+      const int64_t at0 = i * (int64_t)chunk, len = std::min<int64_t>((int64_t)chunk, S - at0);
+      int64_t got = 0;
+      while (got < len) {
+        const ssize_t r = pread(fd, buf + got, (size_t)(len - got), (off_t)(at0 + got));
+        if (r <= 0) {
+          bad_read = 1;
+          return;
+        }
+        got += r;
+      }
+      std::lock_guard<std::mutex> q(q_mu);
+      hipError_t e = hipMemcpyAsync(d_txt + at0, buf, (size_t)len, hipMemcpyHostToDevice, st);
+      if (e == hipSuccess) e = hipEventRecord(sg->ev[s], st);
+      if (e != hipSuccess) {
+        err_line = __LINE__;
+        hip_err = (int)e;
+        return;
+      }
+      sg->pending[s] = true;
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < nt; ++t) th.emplace_back(reader, t);
+  reader(0);
+  for (auto& h : th) h.join();
+  // the ring is released only once nothing queued reads it (and a fault in the copies surfaces
+  // here, attributed to the upload)
+  const hipError_t se = hipStreamSynchronize(st);
+  for (bool& p : sg->pending) p = false;
+  if (hip_err.load() != hipSuccess)
+    return hip_fail((hipError_t)hip_err.load(), "graph.txt upload (copy queue)", __FILE__, err_line.load());
+  if (se != hipSuccess) return hip_fail(se, "graph.txt upload (hipStreamSynchronize)", __FILE__, __LINE__);
+  *read_ok = bad_read.load() == 0;
+  return BLP_OK;
+}
+
 // *out = a device-resident handle, or null (with BLP_OK) when the host parser must take the file
 int device_load(const char* path, int device, blp_edges** out) {
   *out = nullptr;
@@ -415,46 +519,15 @@ int device_load(const char* path, int device, blp_edges** out) {
     return BLP_OK;
   }
   const int64_t S = (int64_t)st_.st_size;
-  // The text: read on up to 16 threads into huge-page host memory that is registered for the one
-  // upload and released right after (default), or (BLP_PARSE_MMAP=1, the round-4 path) a populated
-  // file mapping uploaded as pageable memory and unmapped afterwards.
-  const bool use_mmap = getenv("BLP_PARSE_MMAP") && atoi(getenv("BLP_PARSE_MMAP")) > 0;
-  const uint8_t* data = nullptr;
-  uint8_t* rbuf = nullptr;
-  if (use_mmap) {
-    data = (const uint8_t*)mmap(nullptr, (size_t)S, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
+  uint8_t last_byte = 0;
+  if (pread(fd, &last_byte, 1, (off_t)(S - 1)) != 1) {
     close(fd);
-    if (data == MAP_FAILED) return BLP_OK;  // the host parser reports it
-  } else {
-    rbuf = static_cast<uint8_t*>(host_alloc((size_t)S));
-    bool ok = rbuf != nullptr;
-    if (ok) {
-      const int64_t nt = std::max<int64_t>(1, std::min<int64_t>(16, S >> 23));
-      std::vector<uint8_t> rok((size_t)nt, 0);
-      auto slice = [&](int64_t t) {
-        int64_t at = S * t / nt;
-        const int64_t to = S * (t + 1) / nt;
-        while (at < to) {
-          const ssize_t r = pread(fd, rbuf + at, (size_t)(to - at), (off_t)at);
-          if (r <= 0) return;
-          at += r;
-        }
-        rok[(size_t)t] = 1;
-      };
-      std::vector<std::thread> th;
-      for (int64_t t = 1; t < nt; ++t) th.emplace_back(slice, t);
-      slice(0);
-      for (auto& h : th) h.join();
-      ok = std::count(rok.begin(), rok.end(), 1) == nt;
-    }
-    close(fd);
-    if (!ok) {
-      host_free(rbuf, (size_t)S);
-      return BLP_OK;  // the host parser reports it
-    }
-    data = rbuf;
+    return BLP_OK;  // the host parser reports it
   }
-  stage("read");
+  // BLP_PARSE_CHUNK_KB (test knob): bytes per staging-slot fill, so small files wrap the ring
+  size_t chunk = UP_SLOT;
+  if (const char* ck = getenv("BLP_PARSE_CHUNK_KB"))
+    chunk = std::min(UP_SLOT, std::max<size_t>(4096, (size_t)std::max(0ll, atoll(ck)) << 10));
   hipStream_t st = nullptr;
   ScopedBuf txt, blk, blk_off, tmp, nl, ab, stats, in0, in1, cnt, base, map, ids;
   blp_edges* e = nullptr;
@@ -473,7 +546,9 @@ int device_load(const char* path, int device, blp_edges** out) {
     int n_cu = 256, cu_attr = 0;
     if (hipDeviceGetAttribute(&cu_attr, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cu_attr > 0) n_cu = cu_attr;
     if (!(st = stream_take(device))) return BLP_E_HIP_BASE;
-    const bool tail_nl = data[S - 1] == '\n';
+    Staging* sg = staging_of(device);
+    if (!sg) return BLP_E_HIP_BASE;
+    const bool tail_nl = last_byte == '\n';
     const int64_t T = S + (tail_nl ? 0 : 1);  // a missing final newline is supplied
     const int64_t nb = (T + NL_CHUNK - 1) / NL_CHUNK;
     int rc;
@@ -482,18 +557,9 @@ int device_load(const char* path, int device, blp_edges** out) {
     uint8_t* d_txt = txt.as<uint8_t>();
     BLP_HIP(hipMemsetAsync(d_txt + S, 0, (size_t)(nb * NL_CHUNK - S), st));
     if (!tail_nl) BLP_HIP(hipMemsetAsync(d_txt + S, '\n', 1, st));
-    if (use_mmap) {
-      if ((rc = copy_sync(d_txt, data, (size_t)S, hipMemcpyHostToDevice, st))) return rc;
-    } else {  // registered for this copy only: the runtime holds no pinning of it afterwards
-      const bool reg = hipHostRegister(rbuf, (size_t)S, hipHostRegisterDefault) == hipSuccess;
-      if (!reg) (void)hipGetLastError();
-      hipError_t ce = hipMemcpyAsync(d_txt, data, (size_t)S, hipMemcpyHostToDevice, st);
-      if (ce == hipSuccess) ce = hipStreamSynchronize(st);
-      if (reg) (void)hipHostUnregister(rbuf);
-      host_free(rbuf, (size_t)S);
-      rbuf = nullptr;
-      if (ce != hipSuccess) return hip_fail(ce, "hipMemcpyAsync (graph.txt upload)", __FILE__, __LINE__);
-    }
+    bool read_ok = false;
+    if ((rc = staged_upload(sg, fd, S, d_txt, st, chunk, &read_ok))) return rc;
+    if (!read_ok) return BLP_OK;  // the host parser reports it
     stage("upload");
     hipLaunchKernelGGL(k_nl_count, dim3((unsigned)nb), dim3(NL_BLOCK), 0, st, d_txt, blk.as<uint64_t>());
     BLP_HIP(hipGetLastError());
@@ -530,8 +596,7 @@ int device_load(const char* path, int device, blp_edges** out) {
     const int64_t lo = (int64_t)ps.mn, span = (int64_t)(ps.mx - ps.mn) + 1;
     // the host path's compactness rule (blp_edges_load)
     if (!(span > 0 && span <= std::max<int64_t>(4 * L, 1 << 20) && span < (int64_t(1) << 31))) return BLP_OK;
-    txt.release();
-    nl.release();
+    if ((rc = txt.release()) || (rc = nl.release())) return rc;
     const int64_t W = (span + 31) / 32;
     if ((rc = in0.reserve(4 * W)) || (rc = in1.reserve(4 * W)) || (rc = cnt.reserve(8 * W)) ||
         (rc = base.reserve(8 * W)) || (rc = map.reserve(4 * span)))
@@ -560,8 +625,8 @@ int device_load(const char* path, int device, blp_edges** out) {
     BLP_HIP(hipGetLastError());
     e = new blp_edges();
     e->device = device;
-    BLP_HIP(hipMalloc(&e->d_da, 4 * L));
-    BLP_HIP(hipMalloc(&e->d_db, 4 * L));
+    BLP_HIP(dev_malloc(&e->d_da, 4 * L));
+    BLP_HIP(dev_malloc(&e->d_db, 4 * L));
     hipLaunchKernelGGL(k_dense, dim3(grid_for(L, n_cu)), dim3(256), 0, st, ab.as<int64_t>(), ab.as<int64_t>() + L, L, lo,
                        map.as<int32_t>(), e->d_da, e->d_db);
     BLP_HIP(hipGetLastError());
@@ -581,12 +646,9 @@ int device_load(const char* path, int device, blp_edges** out) {
     return BLP_OK;
   };
   int rc = run();
+  close(fd);
   if (st) stream_give(device, st);  // synchronized: nothing of this call left in flight before its buffers go
   delete e;  // a handle abandoned on an error path
-  if (use_mmap)
-    munmap((void*)data, (size_t)S);
-  else if (rbuf)
-    host_free(rbuf, (size_t)S);  // an error before the upload
   stage("release");
   if (rc == BLP_E_HIP_BASE - (int)hipErrorOutOfMemory) {  // no room on the device: the host parser takes the file
     (void)hipGetLastError();
@@ -848,6 +910,8 @@ extern "C" int blp_ids_lookup(const int32_t* id_map, int64_t id_lo, int64_t id_s
 namespace blp {
 int preload_ingest() {
   hipFuncAttributes fa;
-  return hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&k_nl_count)) == hipSuccess ? 0 : -1;
+  if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&k_nl_count)) != hipSuccess) return -1;
+  int dev = 0;  // and the current device's graph.txt staging ring (32 MiB pinned, a few ms once)
+  return hipGetDevice(&dev) == hipSuccess && staging_of(dev) ? 0 : -1;
 }
 }  // namespace blp

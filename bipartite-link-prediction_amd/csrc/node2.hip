@@ -129,11 +129,11 @@ int build_node2(blp_graph* g) {
   g->h_flag2.assign((size_t)n, 0);
   free_node2(g);
   if (n == 0 || nnz == 0) return BLP_OK;
-  BLP_HIP(hipMalloc(&g->d_w2, 8 * (size_t)n));
-  BLP_HIP(hipMalloc(&g->d_lo2, 4 * (size_t)n));
-  BLP_HIP(hipMalloc(&g->d_hi2, 4 * (size_t)n));
-  BLP_HIP(hipMalloc(&g->d_maxd, 4 * (size_t)n));
-  BLP_HIP(hipMalloc(&g->d_flag2, ((size_t)n + 3) / 4 * 4));
+  BLP_HIP(dev_malloc(&g->d_w2, 8 * (size_t)n));
+  BLP_HIP(dev_malloc(&g->d_lo2, 4 * (size_t)n));
+  BLP_HIP(dev_malloc(&g->d_hi2, 4 * (size_t)n));
+  BLP_HIP(dev_malloc(&g->d_maxd, 4 * (size_t)n));
+  BLP_HIP(dev_malloc(&g->d_flag2, ((size_t)n + 3) / 4 * 4));
   BLP_HIP(hipMemsetAsync(g->d_w2, 0, 8 * (size_t)n, g->stream));
   BLP_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(g->d_lo2), INT32_MAX, (size_t)n, g->stream));
   BLP_HIP(hipMemsetAsync(g->d_hi2, 0, 4 * (size_t)n, g->stream));

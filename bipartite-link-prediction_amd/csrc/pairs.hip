@@ -221,13 +221,12 @@ __global__ __launch_bounds__(GP_BLOCK) void k_bucket_hist(const int32_t* __restr
 // |N(y)|) -- gathered HERE, in caller order: similarity.users' order keeps a user's ~750 pairs
 // together, so on the business side (y = user) a wave's gathers hit one or two rows and cost
 // nothing, where the grouped order of the later write kernel scatters them over the whole
-// row_ptr array. keys (or null): x again, 4 bytes per pair, for k_item_count.
+// row_ptr array.
 template <bool ROWS = false>
 __global__ __launch_bounds__(GP_BLOCK) void k_bucket_scatter(const int32_t* __restrict__ x, const int32_t* __restrict__ y,
                                                              int64_t np, int32_t xlo, int shift, int bmask, int nb, int nblk,
                                                              int64_t per_blk, const int32_t* __restrict__ hoff,
-                                                             int4* __restrict__ tmp, const int64_t* __restrict__ rp = nullptr,
-                                                             int32_t* __restrict__ keys = nullptr) {
+                                                             int4* __restrict__ tmp, const int64_t* __restrict__ rp = nullptr) {
   __shared__ int cur[NB_MAX];
   for (int i = threadIdx.x; i < nb; i += GP_BLOCK) cur[i] = hoff[(int64_t)i * nblk + blockIdx.x];
   __syncthreads();
@@ -261,7 +260,6 @@ __global__ __launch_bounds__(GP_BLOCK) void k_bucket_scatter(const int32_t* __re
       if (pos[u] >= 0) {
         const int32_t ci = (int32_t)(r + u * GP_BLOCK + threadIdx.x);
         tmp[pos[u]] = ROWS ? make_int4(ci, xv[u], sv[u], lv[u]) : make_int4(ci, xv[u], yv[u], 0);
-        if (keys) keys[pos[u]] = xv[u];
       }
   }
 }
@@ -397,8 +395,7 @@ __global__ __launch_bounds__(1024) void k_item_plan(const int32_t* __restrict__ 
 }
 
 template <int KEYS>
-__device__ inline void item_hist(const int4* __restrict__ tmp, int s, int e, int32_t xlo, int lognb, int* h,
-                                 const int32_t* __restrict__ keys = nullptr) {
+__device__ inline void item_hist(const int4* __restrict__ tmp, int s, int e, int32_t xlo, int lognb, int* h) {
   for (int i = threadIdx.x; i < KEYS; i += GB_BLOCK) h[i] = 0;
   __syncthreads();
 #ifndef BLP_ITEMC_U
@@ -410,7 +407,7 @@ __device__ inline void item_hist(const int4* __restrict__ tmp, int s, int e, int
 #pragma unroll
     for (int u = 0; u < UC; ++u) {
       const int k = kr + u * GB_BLOCK + (int)threadIdx.x;
-      xv[u] = k < e ? (keys ? keys[k] : tmp[k].y) : INT32_MIN;  // keys: 4 bytes per pair, not a 16-byte record's line
+      xv[u] = k < e ? tmp[k].y : INT32_MIN;
     }
 #pragma unroll
     for (int u = 0; u < UC; ++u)
@@ -424,16 +421,15 @@ __global__ __launch_bounds__(GB_BLOCK) void k_item_count(const int4* __restrict_
                                                          const int32_t* __restrict__ item_s,
                                                          const int32_t* __restrict__ item_e,
                                                          const int32_t* __restrict__ n_items, int32_t xlo, int lognb,
-                                                         int32_t* __restrict__ cnt, int32_t* __restrict__ ih,
-                                                         const int32_t* __restrict__ keys = nullptr) {
+                                                         int32_t* __restrict__ cnt, int32_t* __restrict__ ih) {
   __shared__ int h[KEYS];
   const int i = blockIdx.x;
   if (i >= *n_items) return;  // uniform: the grid is the host's upper bound on items
   const int b = item_b[i];
-  item_hist<KEYS>(tmp, item_s[i], item_e[i], xlo, lognb, h, keys);
+  item_hist<KEYS>(tmp, item_s[i], item_e[i], xlo, lognb, h);
   for (int j = threadIdx.x; j < KEYS; j += GB_BLOCK) {
     if (h[j]) atomicAdd(&cnt[xlo + b + (j << lognb)], h[j]);
-    if (ih) ih[(int64_t)i * KEYS + j] = h[j];  // the item's histogram, for k_item_write_runs
+    if (ih) ih[(int64_t)i * KEYS + j] = h[j];  // the item's histogram, for k_item_write_ids
   }
 }
 
@@ -485,104 +481,15 @@ __global__ __launch_bounds__(GB_BLOCK) void k_item_write(const int64_t* __restri
   }
 }
 
-// The same write with the item's pairs first ordered by key in LDS, so each key's run goes out
-// as consecutive positions: the grouped metadata (16-20 B per pair) leaves in whole runs instead
-// of one scattered 4-8 B store per array per pair (k_item_write<64>: 533 us in-step at config 2).
-// The item's histogram comes from k_item_count (ih) and its records are read ONCE into an LDS
-// stage in key order (k_item_write re-reads the item three times). KEYS <= 1024: 64 KiB of
-// stage + 12 KiB of key tables.
-template <int KEYS>
-__global__ __launch_bounds__(GB_BLOCK) void k_item_write_runs(const int64_t* __restrict__ rp, const int4* __restrict__ tmp,
-                                                              const int32_t* __restrict__ item_b,
-                                                              const int32_t* __restrict__ item_s,
-                                                              const int32_t* __restrict__ item_e,
-                                                              const int32_t* __restrict__ n_items, int32_t xlo, int lognb,
-                                                              const int32_t* __restrict__ ih,
-                                                              const int32_t* __restrict__ off, int32_t* __restrict__ fill,
-                                                              int32_t* __restrict__ g_out, int64_t* __restrict__ g_yb,
-                                                              int32_t* __restrict__ g_yl, int32_t* __restrict__ g_y) {
-  static_assert(KEYS <= 1024, "key tables in LDS");
-  constexpr int PER = KEYS >= GB_BLOCK ? KEYS / GB_BLOCK : 1;
-  __shared__ int h[KEYS];      // local cursors
-  __shared__ int lofs[KEYS];   // the key's first local position
-  __shared__ int gbase[KEYS];  // ... and its first global position
-  __shared__ int4 stage[GI_PAIRS];
-  __shared__ int red[GB_BLOCK / 64];
-  const int i = blockIdx.x;
-  if (i >= *n_items) return;
-  const int b = item_b[i], s = item_s[i], e = item_e[i];
-  int c[PER];
-  int v = 0;
-#pragma unroll
-  for (int q = 0; q < PER; ++q) {
-    const int j = (int)threadIdx.x * PER + q;
-    c[q] = j < KEYS ? ih[(int64_t)i * KEYS + j] : 0;
-    v += c[q];
-  }
-  int tot;
-  int o = block_exscan_i<GB_BLOCK>(v, red, &tot);
-#pragma unroll
-  for (int q = 0; q < PER; ++q) {
-    const int j = (int)threadIdx.x * PER + q;
-    if (j < KEYS) {
-      const int vv = b + (j << lognb);
-      lofs[j] = o;
-      gbase[j] = c[q] ? off[xlo + vv] + atomicAdd(&fill[vv], c[q]) : 0;
-      h[j] = o;
-      o += c[q];
-    }
-  }
-  __syncthreads();
-  constexpr int U = 4;
-  for (int kr = s; kr < e; kr += U * GB_BLOCK) {  // the item's records, staged in key order
-    int4 t[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int k = kr + u * GB_BLOCK + (int)threadIdx.x;
-      t[u] = k < e ? tmp[k] : make_int4(-1, xlo, 0, 0);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      if (t[u].x >= 0) stage[atomicAdd(&h[(t[u].y - xlo) >> lognb], 1)] = t[u];
-  }
-  __syncthreads();
-  const int n = e - s;
-  for (int pr = 0; pr < n; pr += U * GB_BLOCK) {  // consecutive local slots -> consecutive global positions
-    int4 t[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int p = pr + u * GB_BLOCK + (int)threadIdx.x;
-      t[u] = p < n ? stage[p] : make_int4(-1, xlo, 0, 0);
-    }
-    int64_t st[U], en[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      st[u] = rp[t[u].z];
-      en[u] = rp[t[u].z + 1];
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (t[u].x >= 0) {
-        const int p = pr + u * GB_BLOCK + (int)threadIdx.x;
-        const int j = (t[u].y - xlo) >> lognb;
-        const int pos = gbase[j] + (p - lofs[j]);
-        g_out[pos] = t[u].x;
-        g_yb[pos] = st[u];
-        g_yl[pos] = (int32_t)(en[u] - st[u]);
-        if (g_y) g_y[pos] = t[u].z;
-      }
-    }
-  }
-}
-
-// k_item_write_runs with 8-byte stage records (round 5): the item's pairs are staged in key
-// order in 32 KiB of LDS instead of 64 (twice the resident workgroups), and the write loop finds
-// each slot's key by a binary search of the key starts. MODE 2: the records already carry N(y)'s
-// row (k_bucket_scatter<true>): (caller index, row start) staged, row lengths beside them (48 KiB),
-// no gathers at all. MODE 1: (caller index, y) staged, the row gathered from rp here, U slots per
-// thread in flight together. MODE 0: y itself goes out (g_y) and the scorer gathers the row
-// (pair_row).
-template <int KEYS, int MODE>
+// The grouping write with the item's pairs first ordered by key in LDS, so each key's run goes
+// out as consecutive positions: the grouped metadata leaves in whole runs instead of one scattered
+// 4-8 B store per array per pair (k_item_write<64>: 533 us in-step at config 2). The item's
+// histogram comes from k_item_count (ih); its records are read ONCE into a 32 KiB LDS stage of
+// 8-byte records in key order, and the write loop finds each slot's key by a binary search of the
+// key starts. MODE 2: the records already carry N(y)'s row (k_bucket_scatter<true>): (caller
+// index, row start) staged, row lengths beside them (48 KiB), no gathers at all. MODE 1: (caller
+// index, y) staged, the row gathered from rp here, U slots per thread in flight together.
+template <int KEYS, int MODE>  // MODE 1 or 2
 __global__ __launch_bounds__(GB_BLOCK) void k_item_write_ids(const int64_t* __restrict__ rp, const int4* __restrict__ tmp,
                                                              const int32_t* __restrict__ item_b,
                                                              const int32_t* __restrict__ item_s,
@@ -676,7 +583,7 @@ __global__ __launch_bounds__(GB_BLOCK) void k_item_write_ids(const int64_t* __re
           g_yb[pos[u]] = (int64_t)(uint32_t)r[u].y;
           g_yl[pos[u]] = stage_len[pr + u * GB_BLOCK + (int)threadIdx.x];
         }
-    } else if (MODE == 1) {
+    } else {
       int64_t st[U], en[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -691,13 +598,6 @@ __global__ __launch_bounds__(GB_BLOCK) void k_item_write_ids(const int64_t* __re
           g_yb[pos[u]] = st[u];
           g_yl[pos[u]] = (int32_t)(en[u] - st[u]);
           if (g_y) g_y[pos[u]] = r[u].y;
-        }
-    } else {
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        if (pos[u] >= 0) {
-          g_out[pos[u]] = r[u].x;
-          g_y[pos[u]] = r[u].y;
         }
     }
   }
@@ -1957,7 +1857,6 @@ struct ScoreArgs {
   const int32_t* g_out;    // grouped position -> caller index
   const int64_t* g_yb;     // grouped position -> start of N(y) in ci
   const int32_t* g_yl;     // grouped position -> |N(y)|
-  const int32_t* g_yn;     // grouped position -> y (short-row scorer: N(y)'s bounds from rp; null: g_yb / g_yl)
   const int32_t* hot_idx;     // per node: dense-row number or -1 (null: no dense rows)
   const blp::HotRow* hot_tab;
   const uint4* hot_pool;
@@ -1985,25 +1884,10 @@ struct ScoreArgs {
   int lq_wgs;                   // workgroups d_lq was sized for (BLP_DEBUG bound)
 };
 
-// N(y)'s row [st, st + len) of grouped pair gp. YN (the short-row scorer) with a.g_yn set: from
-// y's row pointers, rp[y] and rp[y + 1] in one 16-byte load (k_item_write_ids groups only y);
-// otherwise from the grouped metadata g_yb / g_yl.
-template <bool YN>
+// N(y)'s row [st, st + len) of grouped pair gp, from the grouped metadata g_yb / g_yl.
 __device__ __attribute__((always_inline)) inline void pair_row(const ScoreArgs& a, int gp, int64_t& st, int& len) {
-  if (YN && a.g_yn) {
-    const int y = a.g_yn[gp];
-    if (!PS_OK(a.misc, y >= 0 && y < a.n_nodes, 2, y, a.n_nodes)) {
-      st = 0;
-      len = 0;
-      return;
-    }
-    const blp::U4a r = *reinterpret_cast<const blp::U4a*>(a.rp + y);
-    st = (int64_t)(((uint64_t)(uint32_t)r.y << 32) | (uint32_t)r.x);
-    len = (int)((int64_t)(((uint64_t)(uint32_t)r.w << 32) | (uint32_t)r.z) - st);
-  } else {
-    st = a.g_yb[gp];
-    len = a.g_yl[gp];
-  }
+  st = a.g_yb[gp];
+  len = a.g_yl[gp];
 }
 
 template <int BLOCK, bool TAIL = true>  // TAIL: see block_exscan
@@ -2151,7 +2035,7 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
       constexpr bool PF = SHORT ? BLP_PF : (RC && BLP_PFL);
       if (PF && nchunks == 1 && (int)threadIdx.x < min(SEG, pcnt)) {
         const int gp = pbeg + threadIdx.x;
-        pair_row<SHORT>(a, gp, pf_start, pf_len);
+        pair_row(a, gp, pf_start, pf_len);
         pf_out = a.g_out[gp];
       }
       PROF(1)
@@ -2319,7 +2203,7 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
           } else if ((int)threadIdx.x < ns) {
             const int gp = pbeg + sb + threadIdx.x;
             int64_t st;
-            pair_row<SHORT>(a, gp, st, len);
+            pair_row(a, gp, st, len);
             s_start[threadIdx.x] = st;
             pout = a.g_out[gp];  // used after the scan: its latency hides behind it
             if (!PKO) s_cn[threadIdx.x] = 0;
@@ -2493,7 +2377,7 @@ __global__ __launch_bounds__(256, BLP_SHORT_MINB) void k_score_short(ScoreArgs a
       int pf_len = 0, pf_out = 0;
       const bool pairs_ok = PS_OK(a.misc, pbeg >= 0 && (int64_t)pbeg + pcnt <= a.np, 3, (int64_t)pbeg + pcnt, a.np);
       if (pairs_ok && (int)threadIdx.x < pcnt) {
-        pair_row<true>(a, pbeg + threadIdx.x, pf_start, pf_len);
+        pair_row(a, pbeg + threadIdx.x, pf_start, pf_len);
         pf_out = a.g_out[pbeg + threadIdx.x];
       }
       // P1: the pre-built set, counted while copied, or a zeroed bitmap
@@ -2554,7 +2438,7 @@ __global__ __launch_bounds__(256, BLP_SHORT_MINB) void k_score_short(ScoreArgs a
         int64_t st = pf_start;
         int len = pf_len, pout = pf_out;
         if (p != (int)threadIdx.x) {
-          pair_row<true>(a, pbeg + p, st, len);
+          pair_row(a, pbeg + p, st, len);
           pout = a.g_out[pbeg + p];
         }
         if (!PS_OK(a.misc, pout >= 0 && pout < a.np, 4, pout, a.np)) continue;
@@ -2711,20 +2595,13 @@ __global__ __launch_bounds__(BLOCK) void k_score_global(ScoreArgs a, uint32_t* g
 // count and exact AA words to the pair's accumulators in HBM (device-scope atomics; slices
 // without hits add nothing); |H2| partials go to [sources][chunks]; k_split_combine computes
 // the final values and Jaccard.
-// The split table rsplit[row][c] (int32 offsets into the row), and its 16-bit twin rsplit16 (or
-// null; BLP_SPLIT16): the same offsets for rows shorter than 65535 ids, 0xFFFF in every entry of a
-// longer row (whose scans then read the int32 table). At config 5 the 2M business rows x 49
-// offsets are 196 MB instead of 392 MB, within the 256 MB Infinity Cache -- yet the step measured
-// 514 ms against 482 with the int32 table alone (r05ab6), so the twin is off by default.
-constexpr uint16_t SPLIT16_LONG = 0xFFFF;
-
+// The split table rsplit[row][c]: int32 offsets into the row. (A 16-bit twin for rows under
+// 65535 ids, 196 instead of 392 MB at config 5, measured 514 against 482 ms per step, r05_ab6.)
 __global__ void k_row_splits(const int64_t* __restrict__ rp, const int32_t* __restrict__ ci, int64_t v0, int64_t n,
-                             int64_t lo, int64_t cap_bits, int C, int32_t* __restrict__ rsplit,
-                             uint16_t* __restrict__ rsplit16) {
+                             int64_t lo, int64_t cap_bits, int C, int32_t* __restrict__ rsplit) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t v = v0 + i;
     const int64_t b = rp[v], e = rp[v + 1];
-    const bool short16 = e - b < SPLIT16_LONG;
     for (int c = 0; c <= C; ++c) {
       const int64_t bound = c == C ? INT64_MAX : lo + c * cap_bits;
       int64_t l = b, h = e;
@@ -2733,25 +2610,13 @@ __global__ void k_row_splits(const int64_t* __restrict__ rp, const int32_t* __re
         if (ci[m] < bound) l = m + 1; else h = m;
       }
       rsplit[i * (C + 1) + c] = (int32_t)(l - b);
-      if (rsplit16) rsplit16[i * (C + 1) + c] = short16 ? (uint16_t)(l - b) : SPLIT16_LONG;
     }
   }
 }
 
-// Row offsets [s0, s1) of chunk c of split-table row `row`: the 16-bit table when present and the
-// row is short, else the int32 table.
-__device__ __attribute__((always_inline)) inline void split_bounds(const int32_t* __restrict__ rsplit,
-                                                                   const uint16_t* __restrict__ rsplit16, int64_t row,
+// Row offsets [s0, s1) of chunk c of split-table row `row`.
+__device__ __attribute__((always_inline)) inline void split_bounds(const int32_t* __restrict__ rsplit, int64_t row,
                                                                    int C, int c, int& s0, int& s1) {
-  if (rsplit16) {
-    const uint16_t* q = rsplit16 + row * (C + 1) + c;
-    const uint32_t a = q[0], b = q[1];
-    if (a != SPLIT16_LONG) {
-      s0 = (int)a;
-      s1 = (int)b;
-      return;
-    }
-  }
   const int32_t* sp = rsplit + row * (C + 1) + c;
   s0 = sp[0];
   s1 = sp[1];
@@ -2764,7 +2629,7 @@ constexpr int SPLIT_LQ = 16 * SPLIT_ROUND * 64;  // long-slice queue entries per
 template <int BLOCK, int CAP_WORDS, int SEG, int K>
 __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_split(ScoreArgs a, const int32_t* __restrict__ g_y,
                                                        const int32_t* __restrict__ rsplit,
-                                                       const uint16_t* __restrict__ rsplit16, int64_t rs_lo, int C,
+                                                       int64_t rs_lo, int C,
                                                        uint32_t* __restrict__ pcn, unsigned long long* __restrict__ paa,
                                                        uint32_t* __restrict__ ph2, int64_t np, int pk24, int short_max) {
   constexpr int NW = BLOCK / 64;
@@ -2901,7 +2766,7 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
           const int z = a.ci[k0 + threadIdx.x];
           if (PS_OK(a.misc, (int64_t)z - rs_lo >= 0 && (int64_t)z - rs_lo < a.rs_rows, 7, (int64_t)z - rs_lo, a.rs_rows)) {
             int sp0, sp1;
-            split_bounds(rsplit, rsplit16, (int64_t)z - rs_lo, C, c, sp0, sp1);
+            split_bounds(rsplit, (int64_t)z - rs_lo, C, c, sp0, sp1);
             s_start[threadIdx.x] = a.rp[z] + sp0;
             len = (nhot && a.hot_idx[z] >= 0) ? 0 : sp1 - sp0;  // dense rows were OR-ed in
             if (!PS_OK(a.misc, sp0 >= 0 && len >= 0 && s_start[threadIdx.x] + len <= a.nnz, 10,
@@ -2999,7 +2864,7 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
           const int64_t row = (int64_t)g_y[gp] - rs_lo;
           if (PS_OK(a.misc, row >= 0 && row < a.rs_rows, 7, row, a.rs_rows)) {
             int s0, s1;
-            split_bounds(rsplit, rsplit16, row, C, c, s0, s1);
+            split_bounds(rsplit, row, C, c, s0, s1);
             len = s1 - s0;
             st = a.g_yb[gp] + s0;
             if (!PS_OK(a.misc, s0 >= 0 && len >= 0 && st + len <= a.nnz, 10, st + len, a.nnz)) len = 0;
@@ -3378,15 +3243,7 @@ struct Knobs {
   int split_short = -1;          // BLP_SPLIT_SHORT: register-scanned slice bound (0: off)
   int cosched_cus = -1;          // BLP_COSCHED_CUS: tuning override of the co-scheduled CU share
   bool no_pko = false;           // BLP_NO_PKO: the large scorer's general variant instead of PKO
-  bool short_seg = false;        // BLP_SHORT_SEG: short-row batches on the segment scorer (k_score SHORT)
-  bool host_plan = false;        // BLP_HOST_PLAN: blp_batch_create plans on the host (mirror loops)
-  bool group_rows = true;        // BLP_GROUP_YN=1 clears it: short-row batches then group y only and the
-                                 // scorer gathers N(y)'s bounds (k_item_write_ids<K, false>; measured slower)
-  bool group_rows16 = false;     // BLP_GROUP_ROWS16: the 16-byte-stage grouping write (k_item_write_runs)
   bool debug_oom = false;        // BLP_DEBUG_OOM (BLP_DEBUG builds): the first create fails out of memory
-  bool split16 = false;          // BLP_SPLIT16: the chunk-parallel scorer reads a 16-bit split table (measured
-                                 // slower at config 5: 514 against 482 ms per step)
-  bool group_gather = false;     // BLP_GROUP_GATHER: rows gathered by the write kernel, not carried by the scatter
   int item_nb = 512;             // BLP_ITEM_NB: at most this many interleaved buckets (a power of two; 512:
                                  // 2.271 / 2.261 against 2.317 / 2.315 ms with 2048, r05_group_geometry)
   int group_nblk = -1;           // BLP_GROUP_NBLK: hist / scatter workgroups (default 2 per CU)
@@ -3394,10 +3251,6 @@ struct Knobs {
   int lpt = 1;                   // BLP_LPT: sources queued largest (build + scan work) first -- bit 1: run-grouped
                                  // batches (the default: config-2 step 2.243 / 2.238 / 2.233 -> 2.214 / 2.211 /
                                  // 2.213 ms, r05_pair_hi_second), bit 2: item-grouped batches (no gain); 0: id order
-  bool no_keys = true;           // the scatter writes no 4-byte key array (item counts read the records);
-                                 // BLP_SCATTER_KEYS=1 writes it
-  bool pair_gate = false;        // BLP_PAIR_GATE: blp_batches_score holds the other passes' grouping until the
-                                 // large-universe pass's grouping is done
   std::string debug_null;        // BLP_DEBUG_NULL (BLP_DEBUG builds only): null this launch pointer, to
                                  // show the pre-launch pointer check (launch_pointers) refusing it
 };
@@ -3431,18 +3284,10 @@ Knobs read_knobs() {
   k.split_short = (int)num("BLP_SPLIT_SHORT", -1);
   k.cosched_cus = (int)num("BLP_COSCHED_CUS", -1);
   k.no_pko = on("BLP_NO_PKO");
-  k.group_rows = !on("BLP_GROUP_YN");
-  k.group_rows16 = on("BLP_GROUP_ROWS16");
-  k.group_gather = on("BLP_GROUP_GATHER");
   k.item_nb = (int)num("BLP_ITEM_NB", 512);
   k.group_nblk = (int)num("BLP_GROUP_NBLK", -1);
-  k.pair_gate = on("BLP_PAIR_GATE");
-  k.no_keys = !on("BLP_SCATTER_KEYS");
   k.lpt = (int)num("BLP_LPT", 1);
   k.short_cus = (int)num("BLP_SHORT_CUS", -1);
-  k.split16 = on("BLP_SPLIT16");
-  k.host_plan = on("BLP_HOST_PLAN");
-  k.short_seg = on("BLP_SHORT_SEG");
 #ifdef BLP_DEBUG
   if (const char* e = getenv("BLP_DEBUG_NULL")) k.debug_null = e;
   k.debug_oom = on("BLP_DEBUG_OOM");
@@ -3453,7 +3298,6 @@ Knobs read_knobs() {
 
 struct blp_batch {
   bool hi_prio = false;  // its stream came from the highest-priority pool (stream_give returns it there)
-  hipEvent_t gate_wait = nullptr, gate_rec = nullptr;  // blp_batches_score's grouping gate (BLP_PAIR_GATE), per call
   blp_graph* g = nullptr;
   int64_t n_pairs = 0;
   int32_t* d_x = nullptr;
@@ -3486,7 +3330,6 @@ struct blp_batch {
   int64_t rs_rows = 0;   // its rows
   int32_t* d_gy = nullptr;     // grouped position -> y (split mode)
   int32_t* d_rsplit = nullptr; // [n][split + 1] row offsets where neighbour ids cross chunk boundaries
-  uint16_t* d_rsplit16 = nullptr;  // ... the same, 16-bit (0xFFFF: a long row, read d_rsplit; BLP_SPLIT16 only)
   int4* d_lq = nullptr;        // k_score_split's long-slice queues (SPLIT_LQ per resident workgroup)
   uint32_t* d_pcn = nullptr;   // [n_pairs] counts, summed over chunks (zeroed per score)
   unsigned long long* d_paa = nullptr;  // [n_pairs][2] exact AA words, summed over chunks
@@ -3515,7 +3358,6 @@ struct blp_batch {
   int32_t* d_lpt = nullptr;      // [n_sources] the active list in that order, written by k_run_cnt
   int64_t n_hash = 0;          // such sources
   bool use_short = false;   // the short-row scorer takes this batch (decided once, at create)
-  bool yn_grouped = false;  // short-row batch grouped by k_item_write_ids: the scorer reads g_yn = d_gy
   bool wedge_user = false;  // its plan reads the graph's wedge index (counted in g->wedge_users)
   int64_t work_elems = 0;  // planned build + scan elements (co-scheduling estimate)
   Knobs kn;               // environment switches, read once at create
@@ -3556,8 +3398,8 @@ static int launch_score(blp_graph* g, hipStream_t st, const ScoreArgs& a, int pe
 template <bool SAA>
 static int launch_short(blp_graph* g, const blp_batch* b, ScoreArgs a, size_t dyn) {
   // the three-barrier scorer takes batches with wedge rows (every review-graph business pass);
-  // the segment scorer builds from the CSR otherwise (BLP_SHORT_SEG: it takes every batch)
-  const bool three = a.wp && !b->kn.short_seg;
+  // the segment scorer builds from the CSR otherwise
+  const bool three = a.wp != nullptr;
   auto kern = three ? k_score_short<SAA> : k_score<BLOCK_SMALL, CAP_SMALL, SEG_SMALL, 8, true, SAA>;
   int per_cu = 1;
   BLP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, BLOCK_SMALL, dyn));
@@ -3601,10 +3443,8 @@ static int launch_pointers(const blp_graph* g, const blp_batch* b, ScoreArgs& a,
   need(a.cnt, "source counts");
   need(a.active, "active sources");
   need(a.g_out, "grouped caller index");
-  if (!a.g_yn) {
-    need(a.g_yb, "grouped row starts");
-    need(a.g_yl, "grouped row lengths");
-  }
+  need(a.g_yb, "grouped row starts");
+  need(a.g_yl, "grouped row lengths");
   need(a.misc, "batch counters");
   need(a.cn, "cn output");
   need(a.jac, "jaccard output");
@@ -3670,6 +3510,14 @@ static int batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_
     blp_batch_destroy(b);
     return rc;
   };
+  {  // registered as a reader of the wedge index before planning reads it (d_wp, h_wp, the
+     // bitmaps): an out-of-memory retry of a concurrent create cannot free it under this plan
+    std::lock_guard<std::mutex> lk(g->wbm_mu);
+    if (g->d_wp) {
+      ++g->wedge_users;
+      b->wedge_user = true;
+    }
+  }
   int rc = set_device(g);
   if (rc) return bail(rc);
   b->hi_prio = hi_prio;
@@ -3684,8 +3532,8 @@ static int batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_
   }
   // ---- the pairs go to HBM first: the device planning pass reads them there
   const size_t np = (size_t)std::max<int64_t>(n_pairs, 1);
-  if (hipMalloc(&b->d_x, 4 * np) != hipSuccess || hipMalloc(&b->d_y, 4 * np) != hipSuccess ||
-      hipMalloc(&b->d_misc, sizeof(Misc)) != hipSuccess)
+  if (dev_malloc(&b->d_x, 4 * np) != hipSuccess || dev_malloc(&b->d_y, 4 * np) != hipSuccess ||
+      dev_malloc(&b->d_misc, sizeof(Misc)) != hipSuccess)
     return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: hipMalloc failed"));
   if (n_pairs && twin) {  // the twin's device copies, swapped, once its upload is done
     hipEvent_t ev;
@@ -3710,10 +3558,10 @@ static int batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_
   bool bad = false, in_runs = true, any_hot = false;
   std::vector<std::pair<int32_t, int64_t>> heavy_cand;  // sources whose build work may make them heavy
   constexpr int64_t HEAVY_MIN = 2 * 16384;              // 2 * the smallest item_work below
-  std::vector<int32_t> srcs;                            // host planning: sources, first appearance
-  std::vector<int64_t> work;                            // ... and their build work
   ScopedBuf d_seen, d_srcs, d_stats, d_heavy;
-  const bool dev_plan = n_pairs > 0 && g->d_w2 && !kn.host_plan;
+  // planned on the device from the graph's two-hop statistics (graph_finish always builds them)
+  if (n_pairs > 0 && !g->d_w2) return bail(fail(BLP_E_STATE, "blp_batch_create: the graph has no two-hop statistics"));
+  const bool dev_plan = n_pairs > 0;
   if (dev_plan) {
     // one pass over the pairs on the device (k_plan_pairs); the host only reads the totals
     const int64_t seen_words = (n + 31) / 32;
@@ -3752,111 +3600,6 @@ static int batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_
     if (ps.xhi > 0) {
       xlo = (int32_t)ps.xlo;
       xhi = (int32_t)ps.xhi;
-    }
-  } else {
-    // host planning (a graph without device two-hop statistics, or BLP_HOST_PLAN): the pair and
-    // source loops gather rows at random from the host mirror, on up to 16 threads
-    const int64_t* rp = g->hrp;
-    const int32_t* ci = host_col_idx(g);
-    if (!ci) return bail(BLP_E_STATE);
-    struct Acc {
-      int64_t lo = INT64_MAX, hi = INT64_MIN, scan = 0, max_scan = 0, max_build = 0;
-      int64_t rows_lo = INT64_MAX, rows_hi = INT64_MIN;  // nodes whose rows are read (the y and the z in N(x))
-      bool bad = false, runs = true, any_hot = false;
-      void row(const int64_t* rp, const int32_t* ci, int64_t v) {
-        if (rp[v + 1] > rp[v]) {
-          lo = std::min<int64_t>(lo, ci[rp[v]]);
-          hi = std::max<int64_t>(hi, (int64_t)ci[rp[v + 1] - 1] + 1);
-        }
-        rows_lo = std::min<int64_t>(rows_lo, v);
-        rows_hi = std::max<int64_t>(rows_hi, v + 1);
-      }
-      void merge(const Acc& o) {
-        lo = std::min(lo, o.lo), hi = std::max(hi, o.hi), scan += o.scan, max_scan = std::max(max_scan, o.max_scan);
-        max_build = std::max(max_build, o.max_build), rows_lo = std::min(rows_lo, o.rows_lo);
-        rows_hi = std::max(rows_hi, o.rows_hi), bad |= o.bad, runs &= o.runs, any_hot |= o.any_hot;
-      }
-    };
-    const int32_t* hot = g->h_hot_idx.empty() ? nullptr : g->h_hot_idx.data();
-    auto parallel = [](int64_t count, int64_t min_per_thread, auto body) {  // body(acc, begin, end)
-      const int nt = (int)std::max<int64_t>(1, std::min<int64_t>({16, (int64_t)std::thread::hardware_concurrency(),
-                                                                    count / std::max<int64_t>(min_per_thread, 1)}));
-      std::vector<Acc> acc(nt);
-      std::vector<std::thread> th;
-      for (int t = 1; t < nt; ++t) th.emplace_back(body, std::ref(acc[t]), count * t / nt, count * (t + 1) / nt);
-      body(acc[0], 0, count / nt);
-      for (auto& h : th) h.join();
-      for (int t = 1; t < nt; ++t) acc[0].merge(acc[t]);
-      return acc[0];
-    };
-    Acc A = parallel(n_pairs, 1 << 18, [&](Acc& a, int64_t i0, int64_t i1) {
-      for (int64_t i = i0; i < i1; ++i) {
-        const int32_t xi = x[i], yi = y[i];
-        if (xi < 0 || xi >= n || yi < 0 || yi >= n) {
-          a.bad = true;
-          return;
-        }
-        a.runs = a.runs && (i == 0 || x[i - 1] <= xi);
-        a.scan += rp[yi + 1] - rp[yi];
-        a.max_scan = std::max<int64_t>(a.max_scan, rp[yi + 1] - rp[yi]);
-        a.row(rp, ci, yi);
-      }
-    });
-    if (A.bad) return bail(fail(BLP_E_ARG, "blp_batch_create: node id out of range"));
-    stage("pairs");
-    std::vector<uint8_t> seen((size_t)n, 0);
-    for (int64_t i = 0; i < n_pairs; ++i)
-      if (!seen[x[i]]) {
-        seen[x[i]] = 1;
-        srcs.push_back(x[i]);
-      }
-    work.resize(srcs.size());
-    const bool have2 = (int64_t)g->h_w2.size() == n;
-    A.merge(parallel((int64_t)srcs.size(), 1 << 14, [&](Acc& a, int64_t s0, int64_t s1) {
-      for (int64_t s = s0; s < s1; ++s) {
-        const int32_t xi = srcs[s];
-        if (rp[xi + 1] == rp[xi]) {
-          work[s] = 0;
-          continue;
-        }
-        if (have2) {
-          work[s] = (int64_t)g->h_w2[xi];
-          a.max_build = std::max<int64_t>(a.max_build, g->h_maxd[xi]);
-          a.any_hot |= (g->h_flag2[xi] & 1) != 0;
-          if (g->h_lo2[xi] != INT32_MAX) {
-            a.lo = std::min<int64_t>(a.lo, g->h_lo2[xi]);
-            a.hi = std::max<int64_t>(a.hi, g->h_hi2[xi]);
-          }
-          a.rows_lo = std::min<int64_t>(a.rows_lo, ci[rp[xi]]);  // rows are sorted: N(x)'s first and last
-          a.rows_hi = std::max<int64_t>(a.rows_hi, (int64_t)ci[rp[xi + 1] - 1] + 1);
-          continue;
-        }
-        int64_t wsum = 0;
-        for (int64_t k = rp[xi]; k < rp[xi + 1]; ++k) {
-          const int32_t z = ci[k];
-          wsum += rp[z + 1] - rp[z];
-          a.max_build = std::max<int64_t>(a.max_build, rp[z + 1] - rp[z]);
-          a.any_hot |= hot && hot[z] >= 0;
-          a.row(rp, ci, z);
-        }
-        work[s] = wsum;
-      }
-    }));
-    lo = A.lo;
-    hi = A.hi;
-    scan_work = A.scan;
-    max_scan_row = A.max_scan;
-    max_build_row = A.max_build;
-    any_hot = A.any_hot;
-    in_runs = A.runs;
-    rows_lo = A.rows_lo;
-    rows_hi = A.rows_hi;
-    n_sources = (int64_t)srcs.size();
-    build_work = std::accumulate(work.begin(), work.end(), (int64_t)0);
-    for (size_t i = 0; i < srcs.size(); ++i) {
-      xlo = std::min(xlo, srcs[i]);
-      xhi = std::max(xhi, srcs[i] + 1);
-      if (work[i] > HEAVY_MIN) heavy_cand.emplace_back(srcs[i], work[i]);
     }
   }
   stage("plan");
@@ -3949,7 +3692,7 @@ static int batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_
     uint32_t* counts = reinterpret_cast<uint32_t*>(d_heavy.as<int32_t>() + cap_heavy);  // [n_heavy, n_hash]
     BLP_HIP_OR(hipMemsetAsync(counts, 0, 8, b->stream), bail);
     if (want_hash) {
-      if (hipMalloc(&b->d_hflag, (size_t)std::max<int64_t>(b->xspan, 1)) != hipSuccess)
+      if (dev_malloc(&b->d_hflag, (size_t)std::max<int64_t>(b->xspan, 1)) != hipSuccess)
         return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: hash flags"));
       BLP_HIP_OR(hipMemsetAsync(b->d_hflag, 0, (size_t)std::max<int64_t>(b->xspan, 1), b->stream), bail);
     }
@@ -3971,20 +3714,8 @@ static int batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_
       (void)hipFree(b->d_hflag);
       b->d_hflag = nullptr;
     }
-  } else if (want_hash) {
-    std::vector<uint8_t> hf((size_t)std::max<int64_t>(b->xspan, 1), 0);
-    for (size_t i = 0; i < srcs.size(); ++i)
-      if (work[i] <= hash_cap) {
-        hf[srcs[i] - b->xlo] = 1;
-        ++b->n_hash;
-      }
-    if (b->n_hash) {
-      if (hipMalloc(&b->d_hflag, hf.size()) != hipSuccess)
-        return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: hash flags"));
-      BLP_HIP_OR(hipMemcpy(b->d_hflag, hf.data(), hf.size(), hipMemcpyHostToDevice), bail);
-    }
   }
-  if (b->n_hash && hipMalloc(&b->d_active2, 4 * ((size_t)std::max<int64_t>(b->xspan, 1) + 1)) != hipSuccess)
+  if (b->n_hash && dev_malloc(&b->d_active2, 4 * ((size_t)std::max<int64_t>(b->xspan, 1) + 1)) != hipSuccess)
     return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: hash flags"));
   if (dev_plan && n_sources > 1 && ((runs && (kn.lpt & 1)) || (!runs && !kn.group_buckets && (kn.lpt & 2)))) {
     // BLP_LPT: the sources' queue order, largest estimated work (build w2[x] + scan sum |N(y)|) first
@@ -3992,8 +3723,8 @@ static int batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_
     if ((rc = d_est.reserve(8 * (size_t)std::max<int64_t>(b->xspan, 1))) || (rc = d_out.reserve(8 * (size_t)n_sources)) ||
         (rc = d_r.reserve(4 * (size_t)n_sources)))
       return bail(rc);
-    if (hipMalloc(&b->d_rank, 4 * (size_t)std::max<int64_t>(b->xspan, 1)) != hipSuccess ||
-        hipMalloc(&b->d_lpt, 4 * (size_t)n_sources + 4) != hipSuccess)
+    if (dev_malloc(&b->d_rank, 4 * (size_t)std::max<int64_t>(b->xspan, 1)) != hipSuccess ||
+        dev_malloc(&b->d_lpt, 4 * (size_t)n_sources + 4) != hipSuccess)
       return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: source order"));
     BLP_HIP_OR(hipMemsetAsync(d_est.p, 0, 8 * (size_t)std::max<int64_t>(b->xspan, 1), b->stream), bail);
     const unsigned gp = (unsigned)std::max<int64_t>(1, std::min<int64_t>((int64_t)g->n_cu * 8, (n_pairs + 255) / 256));
@@ -4025,8 +3756,6 @@ static int batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_
       if (n_sources) BLP_HIP_OR(hipMemcpy(all.data(), d_srcs.p, 4 * (size_t)n_sources, hipMemcpyDeviceToHost), bail);
       std::sort(all.begin(), all.end());
       for (int32_t v : all) heavy_cand.emplace_back(v, g->hrp[v + 1] > g->hrp[v] ? (int64_t)g->h_w2[v] : 0);
-    } else {
-      for (size_t i = 0; i < srcs.size(); ++i) heavy_cand.emplace_back(srcs[i], work[i]);
     }
   }
   std::vector<int32_t> heavy_slot;
@@ -4121,18 +3850,16 @@ static int batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_
     b->rs_lo = rows_lo;
     const int64_t nrows = std::max<int64_t>(rows_hi - rows_lo, 1);
     b->rs_rows = nrows;
-    if (hipMalloc(&b->d_gy, 4 * (size_t)n_pairs) != hipSuccess ||
-        hipMalloc(&b->d_rsplit, 4 * (size_t)nrows * (C + 1)) != hipSuccess ||
-        hipMalloc(&b->d_pcn, 4 * (size_t)n_pairs) != hipSuccess ||
-        hipMalloc(&b->d_paa, 16 * (size_t)n_pairs) != hipSuccess ||
-        hipMalloc(&b->d_ph2, 4 * (size_t)std::max<int64_t>(b->n_sources, 1) * C) != hipSuccess ||
-        hipMalloc(&b->d_lq, sizeof(int4) * SPLIT_LQ * (size_t)g->n_cu * 2) != hipSuccess)
+    if (dev_malloc(&b->d_gy, 4 * (size_t)n_pairs) != hipSuccess ||
+        dev_malloc(&b->d_rsplit, 4 * (size_t)nrows * (C + 1)) != hipSuccess ||
+        dev_malloc(&b->d_pcn, 4 * (size_t)n_pairs) != hipSuccess ||
+        dev_malloc(&b->d_paa, 16 * (size_t)n_pairs) != hipSuccess ||
+        dev_malloc(&b->d_ph2, 4 * (size_t)std::max<int64_t>(b->n_sources, 1) * C) != hipSuccess ||
+        dev_malloc(&b->d_lq, sizeof(int4) * SPLIT_LQ * (size_t)g->n_cu * 2) != hipSuccess)
       return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: split buffers"));
     // on the batch's stream: ordered before its scoring, no host wait
-    if (kn.split16 && hipMalloc(&b->d_rsplit16, 2 * (size_t)nrows * (C + 1)) != hipSuccess)
-      return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: split buffers"));
     hipLaunchKernelGGL(k_row_splits, dim3(2048), dim3(256), 0, b->stream, g->d_rp, g->d_ci, rows_lo, nrows, b->lo,
-                       b->cap_bits, C, b->d_rsplit, b->d_rsplit16);
+                       b->cap_bits, C, b->d_rsplit);
     BLP_HIP_OR(hipGetLastError(), bail);
   }
   // ---- HBM bitmap slots: one per resident workgroup of k_score_global
@@ -4142,30 +3869,27 @@ static int batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_
                bail);
     b->gslots = (int64_t)g->n_cu * std::max(per_cu_g, 1);
     b->gwords = ((span + 31) / 32 + 3) / 4 * 4;
-    if (hipMalloc(&b->d_gbm, 4 * (size_t)b->gwords * b->gslots) != hipSuccess)
+    if (dev_malloc(&b->d_gbm, 4 * (size_t)b->gwords * b->gslots) != hipSuccess)
       return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: HBM bitmap slots"));
   }
   stage("split");
   // ---- device buffers
-  if (hipMalloc(&b->d_cn, 4 * np) != hipSuccess || hipMalloc(&b->d_jac, 8 * np) != hipSuccess ||
-      hipMalloc(&b->d_aa, 8 * np) != hipSuccess || hipMalloc(&b->d_gout, 4 * np) != hipSuccess ||
-      hipMalloc(&b->d_gyb, 8 * np) != hipSuccess || hipMalloc(&b->d_gyl, 4 * np) != hipSuccess)
+  if (dev_malloc(&b->d_cn, 4 * np) != hipSuccess || dev_malloc(&b->d_jac, 8 * np) != hipSuccess ||
+      dev_malloc(&b->d_aa, 8 * np) != hipSuccess || dev_malloc(&b->d_gout, 4 * np) != hipSuccess ||
+      dev_malloc(&b->d_gyb, 8 * np) != hipSuccess || dev_malloc(&b->d_gyl, 4 * np) != hipSuccess)
     return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: hipMalloc failed"));
-  if (b->chunks > 1 && hipMalloc(&b->d_aa_part, 16 * np) != hipSuccess)
+  if (b->chunks > 1 && dev_malloc(&b->d_aa_part, 16 * np) != hipSuccess)
     return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: hipMalloc failed"));
   b->use_short = short_kernel(b);  // fixed here: d_rec's allocation and the launch must agree
-  // short-row batches grouped by items carry y per grouped pair (k_item_write_ids), not N(y)'s bounds
-  if (b->use_short && !b->runs && b->items && !kn.group_rows && !b->d_gy && hipMalloc(&b->d_gy, 4 * np) != hipSuccess)
-    return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: hipMalloc failed"));
   // source records: the short-row scorer, and the large scorer (its header in one round trip)
   const bool want_rec = b->use_short || (b->variant == V_LARGE && !b->split && !b->global);
   if (want_rec &&
-      hipMalloc(&b->d_rec, sizeof(SrcRec) * (size_t)std::max<int64_t>(b->n_sources, 1)) != hipSuccess)
+      dev_malloc(&b->d_rec, sizeof(SrcRec) * (size_t)std::max<int64_t>(b->n_sources, 1)) != hipSuccess)
     return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: hipMalloc failed"));
   if (b->n_heavy) {
-    if (hipMalloc(&b->d_heavy_slot, 4 * n) != hipSuccess ||
-        hipMalloc(&b->d_heavy_bm, 4 * b->hb_words * b->n_heavy) != hipSuccess ||
-        hipMalloc(&b->d_heavy_items, sizeof(HeavyItem) * items.size()) != hipSuccess)
+    if (dev_malloc(&b->d_heavy_slot, 4 * n) != hipSuccess ||
+        dev_malloc(&b->d_heavy_bm, 4 * b->hb_words * b->n_heavy) != hipSuccess ||
+        dev_malloc(&b->d_heavy_items, sizeof(HeavyItem) * items.size()) != hipSuccess)
       return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: hipMalloc failed"));
     if (hipMemcpy(b->d_heavy_slot, heavy_slot.data(), 4 * n, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(b->d_heavy_items, items.data(), sizeof(HeavyItem) * items.size(), hipMemcpyHostToDevice) !=
@@ -4178,11 +3902,13 @@ static int batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_
     return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create [BLP_DEBUG_OOM]: out of memory"));
 #endif
   // the plan reads the wedge index (wedge rows, wedge slices of heavy sources, wedge-row bitmaps):
-  // counted, so an out-of-memory retry releases the index only when no live batch reads it
-  b->wedge_user = g->d_wp && !kn.no_wedge && (b->use_short || b->split || wedge_items || b->wbm_slot);
-  if (b->wedge_user) {
+  // the create's registration stays, so an out-of-memory retry releases the index only when no
+  // live batch reads it; a plan that does not read it drops the registration
+  const bool reads_wedge = b->wedge_user && !kn.no_wedge && (b->use_short || b->split || wedge_items || b->wbm_slot);
+  if (b->wedge_user && !reads_wedge) {
     std::lock_guard<std::mutex> lk(g->wbm_mu);
-    ++g->wedge_users;
+    --g->wedge_users;
+    b->wedge_user = false;
   }
   *out = b;
   return BLP_OK;
@@ -4257,7 +3983,7 @@ int blp_batch_destroy(blp_batch* b) {
     --b->g->wedge_users;
   }
   void* ps[] = {b->d_x,    b->d_y,    b->d_cn,   b->d_jac,  b->d_aa,          b->d_gout,        b->d_gyb,
-                b->d_gyl,  b->d_misc, b->d_heavy_slot, b->d_heavy_bm, b->d_heavy_items, b->d_gbm, b->d_gy, b->d_rsplit, b->d_rsplit16, b->d_pcn, b->d_paa, b->d_ph2, b->d_aa_part, b->d_rec, b->d_hflag, b->d_lq, b->d_active2, b->d_rank, b->d_lpt};
+                b->d_gyl,  b->d_misc, b->d_heavy_slot, b->d_heavy_bm, b->d_heavy_items, b->d_gbm, b->d_gy, b->d_rsplit, b->d_pcn, b->d_paa, b->d_ph2, b->d_aa_part, b->d_rec, b->d_hflag, b->d_lq, b->d_active2, b->d_rank, b->d_lpt};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   delete b;
@@ -4282,7 +4008,7 @@ int blp_batch_kernel(const blp_batch* b, uint32_t mask, char* name, int cap) {
     snprintf(buf, sizeof buf, "k_score_global<%d, %d, 8>", G_BLOCK, G_SEG);
   else if (b->split)
     snprintf(buf, sizeof buf, "k_score_split<%d, %d, %d, 8>", S_BLOCK, b->split_big ? S_CAP_BIG : S_CAP, S_SEG);
-  else if (b->use_short && b->g->d_wp && !b->kn.no_wedge && !b->kn.short_seg)
+  else if (b->use_short && b->g->d_wp && !b->kn.no_wedge)
     snprintf(buf, sizeof buf, "k_score_short<%s>", aa ? "true" : "false");
   else if (b->use_short)
     snprintf(buf, sizeof buf, "k_score<%d, %d, %d, 8, true, %s>", BLOCK_SMALL, CAP_SMALL, SEG_SMALL, aa ? "true" : "false");
@@ -4335,7 +4061,7 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   // scratch: hist | hoff | tiles | bucket_active | abase | tmp [| fill | item table | id-range tiles]
   const int64_t items_ub = (np + GI_PAIRS - 1) / GI_PAIRS + b->nb;
   const int64_t items_ints = b->items ? b->xspan + 3 * items_ub + 2 * ((b->xspan + SCAN_TILE - 1) / SCAN_TILE + 1) +
-                                            1024 * items_ub + np  // ... + the scatter's key array
+                                            1024 * items_ub
                                       : 0;
   const int64_t sc_ints = 2 * nh + std::max(tiles_h, tiles_b) + 1 + 2 * (int64_t)b->nb + 4 * np + items_ints;
   if ((rc = b->scratch.reserve(4 * (sc_ints + 16)))) return rc;
@@ -4345,7 +4071,6 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   int32_t* bact = tiles + std::max(tiles_h, tiles_b) + 1;
   int32_t* abase = bact + b->nb;
   int4* tmp = reinterpret_cast<int4*>((reinterpret_cast<uintptr_t>(abase + b->nb) + 15) & ~uintptr_t(15));
-  if (b->gate_wait) BLP_HIP(hipStreamWaitEvent(b->stream, b->gate_wait, 0));
   hipEvent_t t0, bt0;
   if ((rc = timer_begin(g->timers[K_GROUP], b->stream, &t0))) return rc;
   if ((rc = timer_begin(b->t_group, b->stream, &bt0))) return rc;
@@ -4373,20 +4098,16 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
     // writes a compact key array for the item histograms
     const int64_t ub = (np + GI_PAIRS - 1) / GI_PAIRS + b->nb, tx = (b->xspan + SCAN_TILE - 1) / SCAN_TILE;
     const int64_t ikeys = b->items ? (b->xspan + b->nb - 1) >> b->shift : 0;
-    const bool rec_rows = b->items && ikeys <= 1024 && !b->d_gy && g->nnz < (int64_t(1) << 31) &&
-                          !b->kn.group_gather && !b->kn.group_rows16;
-    // no key array by default: its 512 scattered write streams per block, beside the records',
-    // overflowed the XCD's L2 (3x the written bytes, r05_group_pmc); the item counts read the
-    // records' x instead (2.13-2.15 against 2.18-2.20 ms, r05_scatter_nokeys; BLP_SCATTER_KEYS=1: the array)
-    int32_t* keyarr = b->items && !b->kn.no_keys
-                          ? reinterpret_cast<int32_t*>(tmp + np) + b->xspan + 3 * ub + 2 * (tx + 1) + 1024 * ub
-                          : nullptr;
+    const bool rec_rows = b->items && ikeys <= 1024 && !b->d_gy && g->nnz < (int64_t(1) << 31);
+    // no key array beside the records: 512 more scattered write streams per block overflowed the
+    // XCD's L2 (3x the written bytes, r05_group_pmc); the item counts read the records' x
+    // (2.13-2.15 against 2.18-2.20 ms with the array, r05_scatter_nokeys)
     if (rec_rows)
       hipLaunchKernelGGL((k_bucket_scatter<true>), dim3(b->nblk), dim3(GP_BLOCK), 0, b->stream, b->d_x, b->d_y, np,
-                         b->xlo, hshift, bmask, b->nb, b->nblk, b->per_blk, hoff, tmp, g->d_rp, keyarr);
+                         b->xlo, hshift, bmask, b->nb, b->nblk, b->per_blk, hoff, tmp, g->d_rp);
     else
       hipLaunchKernelGGL((k_bucket_scatter<false>), dim3(b->nblk), dim3(GP_BLOCK), 0, b->stream, b->d_x, b->d_y, np,
-                         b->xlo, hshift, bmask, b->nb, b->nblk, b->per_blk, hoff, tmp, (const int64_t*)nullptr, keyarr);
+                         b->xlo, hshift, bmask, b->nb, b->nblk, b->per_blk, hoff, tmp);
     if (b->items) {
       int32_t* fill = reinterpret_cast<int32_t*>(tmp + np);
       int32_t *it_b = fill + b->xspan, *it_s = it_b + ub, *it_e = it_s + ub, *tx1 = it_e + ub, *tx2 = tx1 + tx + 1;
@@ -4397,12 +4118,10 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
                          &b->d_misc->n_items);
       const int64_t keys = ikeys;
       const bool runs_w = keys <= 1024;
-      const bool ids_w = b->use_short && b->d_gy && !b->kn.group_rows;  // k_item_write_ids (short-row scorer)
-      b->yn_grouped = runs_w && ids_w;
       int32_t* ih = tx2 + tx + 1;  // [ub][K] item histograms (runs_w)
 #define BLP_ITEM_LAUNCH(K)                                                                                         \
   hipLaunchKernelGGL(k_item_count<K>, dim3((unsigned)ub), dim3(GB_BLOCK), 0, b->stream, tmp, it_b, it_s, it_e,     \
-                     &b->d_misc->n_items, b->xlo, b->shift, cnt, runs_w ? ih : nullptr, keyarr);                   \
+                     &b->d_misc->n_items, b->xlo, b->shift, cnt, runs_w ? ih : nullptr);                           \
   hipLaunchKernelGGL(k_scan_sum, dim3((unsigned)tx), dim3(SCAN_BLOCK), 0, b->stream, cnt + b->xlo, b->xspan, tx1); \
   hipLaunchKernelGGL(k_scan_mid, dim3(1), dim3(SCAN_BLOCK), 0, b->stream, tx1, tx, (int32_t*)nullptr);             \
   hipLaunchKernelGGL(k_scan_out, dim3((unsigned)tx), dim3(SCAN_BLOCK), 0, b->stream, cnt + b->xlo, b->xspan, tx1,  \
@@ -4411,22 +4130,14 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   hipLaunchKernelGGL(k_scan_mid, dim3(1), dim3(SCAN_BLOCK), 0, b->stream, tx2, tx, &b->d_misc->n_active);          \
   hipLaunchKernelGGL(k_nz_write, dim3((unsigned)tx), dim3(SCAN_BLOCK), 0, b->stream, cnt + b->xlo, b->xspan, tx2,  \
                      b->xlo, b->active.as<int32_t>(), b->d_rank, b->d_lpt);                                         \
-  if (runs_w && ids_w)                                                                                                \
-    hipLaunchKernelGGL((k_item_write_ids<(K <= 1024 ? K : 1024), 0>), dim3((unsigned)ub), dim3(GB_BLOCK), 0,         \
-                       b->stream, g->d_rp, tmp, it_b, it_s, it_e, &b->d_misc->n_items, b->xlo, b->shift, ih, off,     \
-                       fill, b->d_gout, b->d_gyb, b->d_gyl, b->d_gy);                                                 \
-  else if (runs_w && rec_rows)                                                                                        \
+  if (runs_w && rec_rows)                                                                                             \
     hipLaunchKernelGGL((k_item_write_ids<(K <= 1024 ? K : 1024), 2>), dim3((unsigned)ub), dim3(GB_BLOCK), 0,         \
                        b->stream, g->d_rp, tmp, it_b, it_s, it_e, &b->d_misc->n_items, b->xlo, b->shift, ih, off,     \
                        fill, b->d_gout, b->d_gyb, b->d_gyl, b->d_gy);                                                 \
-  else if (runs_w && !b->kn.group_rows16)                                                                             \
+  else if (runs_w)                                                                                                    \
     hipLaunchKernelGGL((k_item_write_ids<(K <= 1024 ? K : 1024), 1>), dim3((unsigned)ub), dim3(GB_BLOCK), 0,         \
                        b->stream, g->d_rp, tmp, it_b, it_s, it_e, &b->d_misc->n_items, b->xlo, b->shift, ih, off,     \
                        fill, b->d_gout, b->d_gyb, b->d_gyl, b->d_gy);                                                 \
-  else if (runs_w)                                                                                                    \
-    hipLaunchKernelGGL(k_item_write_runs<(K <= 1024 ? K : 1024)>, dim3((unsigned)ub), dim3(GB_BLOCK), 0, b->stream,  \
-                       g->d_rp, tmp, it_b, it_s, it_e, &b->d_misc->n_items, b->xlo, b->shift, ih, off, fill,         \
-                       b->d_gout, b->d_gyb, b->d_gyl, b->d_gy);                                                       \
   else                                                                                                                \
     hipLaunchKernelGGL(k_item_write<K>, dim3((unsigned)ub), dim3(GB_BLOCK), 0, b->stream, g->d_rp, tmp, it_b, it_s,  \
                        it_e, &b->d_misc->n_items, b->xlo, b->shift, off, fill, b->d_gout, b->d_gyb, b->d_gyl, b->d_gy)
@@ -4484,7 +4195,6 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   if ((rc = timer_end(b->t_group, b->stream, bt0))) return rc;
   if ((rc = timer_end(g->timers[K_GROUP], b->stream, t0))) return rc;
 
-  if (b->gate_rec) BLP_HIP(hipEventRecord(b->gate_rec, b->stream));
   hipEvent_t t1, bt1;
   if ((rc = timer_begin(g->timers[K_SCORE], b->stream, &t1))) return rc;
   if ((rc = timer_begin(b->t_score, b->stream, &bt1))) return rc;
@@ -4520,7 +4230,6 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   a.g_out = b->d_gout;
   a.g_yb = b->d_gyb;
   a.g_yl = b->d_gyl;
-  a.g_yn = b->use_short && b->yn_grouped ? b->d_gy : nullptr;
   a.hot_idx = b->use_hot ? g->d_hot_idx : nullptr;
   a.hot_tab = (const HotRow*)g->d_hot_tab;
   a.hot_pool = (const uint4*)g->d_hot_pool;
@@ -4585,12 +4294,12 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
     if (b->split_big) {
       BLP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_score_split<S_BLOCK, S_CAP_BIG, S_SEG, 8>, S_BLOCK, 0));
       hipLaunchKernelGGL((k_score_split<S_BLOCK, S_CAP_BIG, S_SEG, 8>), dim3(scu * std::min(std::max(per_cu, 1), 2)), dim3(S_BLOCK),
-                         0, b->stream, a, b->d_gy, b->d_rsplit, b->d_rsplit16, b->rs_lo, b->split, b->d_pcn, b->d_paa, b->d_ph2, np, pk24,
+                         0, b->stream, a, b->d_gy, b->d_rsplit, b->rs_lo, b->split, b->d_pcn, b->d_paa, b->d_ph2, np, pk24,
                          short_max);
     } else {
       BLP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_score_split<S_BLOCK, S_CAP, S_SEG, 8>, S_BLOCK, 0));
       hipLaunchKernelGGL((k_score_split<S_BLOCK, S_CAP, S_SEG, 8>), dim3(scu * std::min(std::max(per_cu, 1), 2)), dim3(S_BLOCK), 0,
-                         b->stream, a, b->d_gy, b->d_rsplit, b->d_rsplit16, b->rs_lo, b->split, b->d_pcn, b->d_paa, b->d_ph2, np, pk24,
+                         b->stream, a, b->d_gy, b->d_rsplit, b->rs_lo, b->split, b->d_pcn, b->d_paa, b->d_ph2, np, pk24,
                          short_max);
     }
     BLP_HIP(hipGetLastError());
@@ -4673,29 +4382,13 @@ int blp_batches_score(blp_graph* g, int n, blp_batch* const* bs, const uint32_t*
   // chunk-parallel batches (config 5's two passes) each take the whole chip: holding each
   // persistent grid to a CU share was slower at every share tried (1951 ms per config-5 step in
   // proportion to planned work, 864 / 903 ms at 176 / 128 user CUs, against 743 ms)
-  // BLP_PAIR_GATE (measurement knob): the large pass is enqueued first and records an event after
-  // its grouping; the other passes' grouping waits on it, so their sorts cannot hold the CUs the
-  // large pass's grouping needs
-  hipEvent_t gate = nullptr;
-  int first = -1;
-  if (n > 1 && bs[0]->kn.pair_gate && t_large > 0.0 && t_other > 0.0) {
-    for (int i = 0; i < n && first < 0; ++i)
-      if (is_large(bs[i])) first = i;
-    int rc = set_device(g);
-    if (rc) return rc;
-    BLP_HIP(hipEventCreateWithFlags(&gate, hipEventDisableTiming));
-  }
   int rc = BLP_OK;
-  for (int k = 0; k < n && !rc; ++k) {
-    const int i = first < 0 ? k : (k == 0 ? first : (k <= first ? k - 1 : k));
+  for (int i = 0; i < n && !rc; ++i) {
     blp_batch* b = bs[i];
     b->cus = is_large(b) && t_other > 0.0 ? share : 0;
-    if (gate) (i == first ? b->gate_rec : b->gate_wait) = gate;
     rc = blp_batch_score(g, b, masks[i]);
     b->cus = 0;
-    b->gate_rec = b->gate_wait = nullptr;
   }
-  if (gate) (void)hipEventDestroy(gate);
   return rc;
 }
 

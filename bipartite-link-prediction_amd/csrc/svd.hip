@@ -559,10 +559,10 @@ static int svd_prune_prepare(blp_svd* h) {
   BLP_HIP_OR(hipcub::DeviceRadixSort::SortPairsDescending(temp.p, tb, key.as<unsigned long long>(),
                                                           skey.as<unsigned long long>(), idx.as<int32_t>(),
                                                           sidx.as<int32_t>(), (int)n, 0, 64, h->stream), done);
-  BLP_HIP_OR(hipMalloc(&h->d_vtp, 8 * (size_t)h->kpad * np), done);
-  BLP_HIP_OR(hipMalloc(&h->d_vnp, 8 * (size_t)np), done);
-  BLP_HIP_OR(hipMalloc(&h->d_perm, 4 * (size_t)np), done);
-  BLP_HIP_OR(hipMalloc(&h->d_tiles, 8), done);
+  BLP_HIP_OR(dev_malloc(&h->d_vtp, 8 * (size_t)h->kpad * np), done);
+  BLP_HIP_OR(dev_malloc(&h->d_vnp, 8 * (size_t)np), done);
+  BLP_HIP_OR(dev_malloc(&h->d_perm, 4 * (size_t)np), done);
+  BLP_HIP_OR(dev_malloc(&h->d_tiles, 8), done);
   BLP_HIP_OR(hipMemsetAsync(h->d_tiles, 0, 8, h->stream), done);
   hipLaunchKernelGGL(k_vt_perm, dim3(1024), dim3(256), 0, h->stream, h->d_vt, np, n, h->kpad,
                      skey.as<unsigned long long>(), sidx.as<int32_t>(), h->d_vtp, h->d_vnp, h->d_perm);
@@ -608,16 +608,16 @@ int blp_svd_create(const double* us, int64_t n_rows, const double* v, int64_t n_
   const int kp = h->kpad;
   std::vector<double> buf((size_t)std::max(n_rows, n_cols) * kp, 0.0);
   for (int64_t r = 0; r < n_rows; ++r) std::copy(us + r * k, us + r * k + k, buf.begin() + r * kp);
-  if ((e = hipMalloc(&h->d_us, 8 * n_rows * kp)) != hipSuccess) return fail_hip(e, "hipMalloc");
+  if ((e = dev_malloc(&h->d_us, 8 * n_rows * kp)) != hipSuccess) return fail_hip(e, "hipMalloc");
   if ((e = hipMemcpy(h->d_us, buf.data(), 8 * n_rows * kp, hipMemcpyHostToDevice)) != hipSuccess) return fail_hip(e, "copy");
   std::fill(buf.begin(), buf.end(), 0.0);
   for (int64_t c = 0; c < n_cols; ++c) std::copy(v + c * k, v + c * k + k, buf.begin() + c * kp);
-  if ((e = hipMalloc(&h->d_v, 8 * n_cols * kp)) != hipSuccess) return fail_hip(e, "hipMalloc");
+  if ((e = dev_malloc(&h->d_v, 8 * n_cols * kp)) != hipSuccess) return fail_hip(e, "hipMalloc");
   if ((e = hipMemcpy(h->d_v, buf.data(), 8 * n_cols * kp, hipMemcpyHostToDevice)) != hipSuccess) return fail_hip(e, "copy");
   std::vector<double> vt((size_t)kp * h->ncol_pad, 0.0);
   for (int64_t c = 0; c < n_cols; ++c)
     for (int j = 0; j < k; ++j) vt[(size_t)j * h->ncol_pad + c] = v[c * k + j];
-  if ((e = hipMalloc(&h->d_vt, 8 * vt.size())) != hipSuccess) return fail_hip(e, "hipMalloc");
+  if ((e = dev_malloc(&h->d_vt, 8 * vt.size())) != hipSuccess) return fail_hip(e, "hipMalloc");
   if ((e = hipMemcpy(h->d_vt, vt.data(), 8 * vt.size(), hipMemcpyHostToDevice)) != hipSuccess) return fail_hip(e, "copy");
   *out = h;
   return BLP_OK;
@@ -664,7 +664,7 @@ int blp_svd_score_pairs(blp_svd* h, const int32_t* rows, const int32_t* cols, in
   int32_t *dr = nullptr, *dc = nullptr;
   double* dout = nullptr;
   int rc = BLP_OK;
-  if (hipMalloc(&dr, 4 * n) != hipSuccess || hipMalloc(&dc, 4 * n) != hipSuccess || hipMalloc(&dout, 8 * n) != hipSuccess) {
+  if (dev_malloc(&dr, 4 * n) != hipSuccess || dev_malloc(&dc, 4 * n) != hipSuccess || dev_malloc(&dout, 8 * n) != hipSuccess) {
     rc = fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_svd_score_pairs: hipMalloc failed");
   } else if (hipMemcpy(dr, rows, 4 * n, hipMemcpyHostToDevice) != hipSuccess ||
              hipMemcpy(dc, cols, 4 * n, hipMemcpyHostToDevice) != hipSuccess) {
@@ -685,7 +685,7 @@ static int part_reserve(blp_svd* h, int64_t np) {
   h->d_ps = nullptr;
   h->d_pc = nullptr;
   h->part_cap = 0;
-  if (hipMalloc(&h->d_ps, 8 * np) != hipSuccess || hipMalloc(&h->d_pc, 4 * np) != hipSuccess)
+  if (dev_malloc(&h->d_ps, 8 * np) != hipSuccess || dev_malloc(&h->d_pc, 4 * np) != hipSuccess)
     return fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_svd_topk: partial buffers");
   h->part_cap = np;
   return BLP_OK;
@@ -815,9 +815,9 @@ int blp_svd_topk(blp_svd* h, const int32_t* users, int64_t n_users, const int64_
     for (void* p : {d_users, d_exo, d_exc, d_os, d_oc})
       if (p) (void)hipFree(p);
   };
-  if (hipMalloc(&d_users, 4 * n_users) != hipSuccess || hipMalloc(&d_os, 8 * n_users * topk) != hipSuccess ||
-      hipMalloc(&d_oc, 4 * n_users * topk) != hipSuccess ||
-      (ex_off && (hipMalloc(&d_exo, 8 * (n_users + 1)) != hipSuccess || hipMalloc(&d_exc, 4 * std::max<int64_t>(nex, 1)) != hipSuccess))) {
+  if (dev_malloc(&d_users, 4 * n_users) != hipSuccess || dev_malloc(&d_os, 8 * n_users * topk) != hipSuccess ||
+      dev_malloc(&d_oc, 4 * n_users * topk) != hipSuccess ||
+      (ex_off && (dev_malloc(&d_exo, 8 * (n_users + 1)) != hipSuccess || dev_malloc(&d_exc, 4 * std::max<int64_t>(nex, 1)) != hipSuccess))) {
     cleanup();
     return fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_svd_topk: hipMalloc failed");
   }

@@ -1717,8 +1717,9 @@ extern "C" int blp_topk_set_sources(blp_topk* t, const int32_t* src, int64_t n_s
   // two-hop walk, sum over b in N(x) of |N(b)|, so the long sources start early instead of
   // finishing last on a few CUs (BLP_TK_ORDER=0: list order). Results land by list index.
   t->ordered = false;
-  const int32_t* ci = host_col_idx(t->g);
   const int64_t how = env_i64("BLP_TK_ORDER", 1);
+  const int32_t* ci = n_src > 1 && how != 0 ? host_col_idx(t->g) : nullptr;
+  if (n_src > 1 && how != 0 && !ci) return BLP_E_STATE;  // the column mirror fetch failed (its error is set)
   if (n_src > 1 && ci && how != 0) {
     const int64_t* rp = t->g->hrp;
     // 1: the walk's wedges, sum |N(b)|; 2 (measurement): its pushes, sum w2[b] over the walked

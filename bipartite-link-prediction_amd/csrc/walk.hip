@@ -119,12 +119,12 @@ int blp_walk_create(const int64_t* row_ptr, const int32_t* col, const double* va
   };
   hipError_t e;
   if ((e = hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking)) != hipSuccess) return bad(e);
-  if ((e = hipMalloc(&w->d_col, 4 * std::max<int64_t>(nnz, 1))) != hipSuccess) return bad(e);
-  if ((e = hipMalloc(&w->d_val, 8 * std::max<int64_t>(nnz, 1))) != hipSuccess) return bad(e);
-  if ((e = hipMalloc(&w->d_items, sizeof(WalkItem) * std::max<size_t>(items.size(), 1))) != hipSuccess) return bad(e);
-  if ((e = hipMalloc(&w->d_split_rows, 4 * std::max<size_t>(split_rows.size(), 1))) != hipSuccess) return bad(e);
-  if ((e = hipMalloc(&w->d_p, 8 * n * WB)) != hipSuccess) return bad(e);
-  if ((e = hipMalloc(&w->d_pn, 8 * n * WB)) != hipSuccess) return bad(e);
+  if ((e = dev_malloc(&w->d_col, 4 * std::max<int64_t>(nnz, 1))) != hipSuccess) return bad(e);
+  if ((e = dev_malloc(&w->d_val, 8 * std::max<int64_t>(nnz, 1))) != hipSuccess) return bad(e);
+  if ((e = dev_malloc(&w->d_items, sizeof(WalkItem) * std::max<size_t>(items.size(), 1))) != hipSuccess) return bad(e);
+  if ((e = dev_malloc(&w->d_split_rows, 4 * std::max<size_t>(split_rows.size(), 1))) != hipSuccess) return bad(e);
+  if ((e = dev_malloc(&w->d_p, 8 * n * WB)) != hipSuccess) return bad(e);
+  if ((e = dev_malloc(&w->d_pn, 8 * n * WB)) != hipSuccess) return bad(e);
   if (nnz && ((e = hipMemcpy(w->d_col, col, 4 * nnz, hipMemcpyHostToDevice)) != hipSuccess ||
               (e = hipMemcpy(w->d_val, val, 8 * nnz, hipMemcpyHostToDevice)) != hipSuccess))
     return bad(e);
@@ -168,10 +168,10 @@ int blp_walk_run(blp_walk* w, const int32_t* starts, int64_t n_starts, int itera
   int32_t *d_starts = nullptr, *d_qb = nullptr, *d_qn = nullptr;
   double* d_out = nullptr;
   const int64_t qcap = std::max<int64_t>(n_q, 1);
-  BLP_HIP(hipMalloc(&d_starts, 4 * std::max<int64_t>(n_starts, 1)));
-  BLP_HIP(hipMalloc(&d_qb, 4 * qcap));
-  BLP_HIP(hipMalloc(&d_qn, 4 * qcap));
-  BLP_HIP(hipMalloc(&d_out, 8 * qcap));
+  BLP_HIP(dev_malloc(&d_starts, 4 * std::max<int64_t>(n_starts, 1)));
+  BLP_HIP(dev_malloc(&d_qb, 4 * qcap));
+  BLP_HIP(dev_malloc(&d_qn, 4 * qcap));
+  BLP_HIP(dev_malloc(&d_out, 8 * qcap));
   if (n_starts) BLP_HIP(hipMemcpy(d_starts, starts, 4 * n_starts, hipMemcpyHostToDevice));
   std::vector<int32_t> qb(qcap);
   for (int64_t k = 0; k < n_q; ++k) qb[k] = q_start[k] % WB;

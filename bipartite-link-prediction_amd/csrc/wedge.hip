@@ -138,6 +138,7 @@ int build_wedge_index(blp_graph* g) {
   if (const char* e = getenv("BLP_WEDGE_MAX_X")) max_x = atof(e);
   size_t free_b = 0, total_b = 0;
   BLP_HIP(hipMemGetInfo(&free_b, &total_b));
+  free_b += dev_cache_bytes(g->device);  // cached scratch blocks are free to any allocation (dev_malloc)
   const double budget = std::min(max_x * (double)g->nnz, 0.35 * (double)free_b);
   // members' rows up to BLP_WEDGE_ROW_MAX (64) ids: the short-row scorer's sources (rows <=
   // SHORT_ROW_MAX) always qualify; the chunk-parallel and hash-set scorers use any wedge row
@@ -158,8 +159,8 @@ int build_wedge_index(blp_graph* g) {
   // the rows themselves are gathered on the device from the CSR already there (435 MB at
   // config 2: a host fill and upload took ~0.2 s)
   // an index that does not fit is skipped (every scorer also builds from the CSR)
-  if (hipMalloc(&g->d_wp, sizeof(int64_t) * (n + 1)) != hipSuccess ||
-      hipMalloc(&g->d_wedge, sizeof(int32_t) * 4 * total) != hipSuccess) {
+  if (dev_malloc(&g->d_wp, sizeof(int64_t) * (n + 1)) != hipSuccess ||
+      dev_malloc(&g->d_wedge, sizeof(int32_t) * 4 * total) != hipSuccess) {
     (void)hipGetLastError();
     if (g->d_wp) (void)hipFree(g->d_wp);
     g->d_wp = nullptr;

@@ -20,13 +20,17 @@ from helpers import dense_edges
 pytestmark = pytest.mark.gpu
 
 
-def test_config2_slice_both_sides_coscheduled(gpu):
+@pytest.mark.parametrize("create", ["pair", "two"])
+def test_config2_slice_both_sides_coscheduled(gpu, create):
+    """create="pair": the bench's own creation (bench.py: G.batch_pair, blp_batch_create_pair --
+    one upload of the pairs, the user pass on a highest-priority stream, the business pass's pairs
+    copied device to device); "two": two independent blp_batch_create calls."""
     U, B, D = synth.CONFIGS["c2"]
     a, b = synth.review_edges(U, B, D, seed=0)
     G = blp.DeviceGraph(a, b, device=gpu)
     ex_x, ex_y, ex_l = synth.make_examples(G, U, B, D, n_users=220, rate=0.01, seed=7)
     assert len(ex_x) >= 150_000 and len(np.unique(ex_x)) == 220
-    ub, bb = G.batch(ex_x, ex_y), G.batch(ex_y, ex_x)
+    ub, bb = G.batch_pair(ex_x, ex_y) if create == "pair" else (G.batch(ex_x, ex_y), G.batch(ex_y, ex_x))
     plan = ub.plan()
     assert plan["block"] == 1024 and plan["chunks"] == 1 and plan["hi"] - plan["lo"] > 31744 * 16, plan
     assert ub.kernel(7) == "k_score<1024, 31744, 896, 8, false, true, true>", ub.kernel(7)  # bench.py's roofline kernel

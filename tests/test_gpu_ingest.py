@@ -595,16 +595,17 @@ def _same_load(d, h):
             assert np.array_equal(x, y)
 
 
-@pytest.mark.parametrize("text_path", ["read", "mmap"])
+@pytest.mark.parametrize("chunk_kb", [None, "64", "12"])
 @pytest.mark.parametrize("final_newline", [False, True])
-def test_device_parse_equals_host_parse(gpu, tmp_path, final_newline, text_path, monkeypatch):
+def test_device_parse_equals_host_parse(gpu, tmp_path, final_newline, chunk_kb, monkeypatch):
     """blp_edges_load_device on a graph.txt of the reference's line shape (dataset_maker.py:197;
     tabs, CRLF, trailing blanks, leading zeros, duplicates, reversed duplicates, self-loops): the
     parse, id map and CSR run on the device and equal the host loader's, and the CSR equals the
-    host CSR builder's on the dense endpoints. The text reaches HBM from a threaded read into
-    registered huge-page memory (default) or from a file mapping (BLP_PARSE_MMAP=1)."""
-    if text_path == "mmap":
-        monkeypatch.setenv("BLP_PARSE_MMAP", "1")
+    host CSR builder's on the dense endpoints. The text reaches HBM through the process's pinned
+    staging ring (2 MiB slot fills by default; 64 KiB and 12 KiB fills wrap the ring many times,
+    BLP_PARSE_CHUNK_KB)."""
+    if chunk_kb:
+        monkeypatch.setenv("BLP_PARSE_CHUNK_KB", chunk_kb)
     rng = np.random.default_rng(21)
     a, c = _messy_edges(rng, 60000, 2500, 150000)
     p = _graph_txt(tmp_path / "graph.txt", a + 5, c + 5, rng, final_newline=final_newline)
@@ -618,6 +619,26 @@ def test_device_parse_equals_host_parse(gpu, tmp_path, final_newline, text_path,
     rp, ci, sl = _host_csr(n, d["da"], d["db"])
     for x, y in zip(d["csr"], (rp, ci, sl)):
         assert np.array_equal(x, y)
+
+
+@pytest.mark.parametrize("draws,lo_mib,hi_mib", [(100000, 1, 4), (230000, 1, 4), (700000, 4, 64)])
+@pytest.mark.parametrize("final_newline", [False, True])
+def test_device_parse_sizes_repeated(gpu, tmp_path, draws, lo_mib, hi_mib, final_newline):
+    """The round-5 driver fault (GPUTEST_r05: an illegal address at the graph.txt upload of a
+    ~2 MB file) came from the upload's host buffer: a fresh 1-4 MiB malloc block or >= 4 MiB
+    mapping, registered, copied, unregistered and freed on every call. The upload now goes through
+    the process's pinned staging ring only. Files in the 1-4 MiB band and above it, with and without
+    the final newline, each loaded three times in a row through the device parser (the ring and
+    the device scratch blocks reused), every load equal to the host loader's."""
+    rng = np.random.default_rng(draws + final_newline)
+    a, c = _messy_edges(rng, 90000, 3000, draws)
+    p = _graph_txt(tmp_path / "graph.txt", a + 1, c + 1, rng, final_newline=final_newline)
+    assert (lo_mib << 20) <= p.stat().st_size < (hi_mib << 20)
+    h = _edges_load(p, csr_device=gpu)
+    for _ in range(3):
+        d = _edges_load(p, device=gpu, csr_device=gpu)
+        assert d["on"] == gpu
+        _same_load(d, h)
 
 
 @pytest.mark.parametrize("case", ["comment", "blank_line", "sign", "extra_column", "long_id", "sparse_ids", "small"])

@@ -152,20 +152,12 @@ def test_general_graph_exact_distance(gpu):
     {"BLP_SPLIT": "3", "BLP_SPLIT_BIG": "1", "BLP_HASH_WORK": "600"},  # hash-set scorer for light sources, split for the rest
     {"BLP_SPLIT": "2", "BLP_SPLIT_BIG": "1", "BLP_HASH_WORK": "100000"},  # every source on the hash-set scorer (knob clamped to HT - 1)
     {"BLP_SPLIT": "4", "BLP_HASH_WORK": "400"},          # ... beside the 64 KiB chunk scorer
-    {"BLP_SPLIT": "3", "BLP_SPLIT16": "1"},             # chunk-parallel scorer on the 16-bit split table
-    {"BLP_SHORT_SEG": "1"},                             # short-row batches on the segment scorer (k_score SHORT)
-    {"BLP_SHORT_SEG": "1", "BLP_HEAVY_WORK": "7"},
-    {"BLP_GROUP_YN": "1"},                              # short-row batches grouped by y only: the scorer reads N(y)'s bounds
-    {"BLP_GROUP_ROWS16": "1"},                          # the 16-byte-stage grouping write (k_item_write_runs)
-    {"BLP_GROUP_GATHER": "1"},                          # rows gathered by the grouping write, not carried by the scatter
+    {"BLP_NO_WEDGE": "1", "BLP_HEAVY_WORK": "7"},       # short-row batches on the segment scorer (k_score SHORT)
     {"BLP_ITEM_NB": "1"},                               # one interleaved bucket (or the fewest that keep <= 1024 keys)
     {"BLP_ITEM_NB": "4", "BLP_GROUP_NBLK": "3"},        # few buckets, few scatter workgroups
-    {"BLP_SCATTER_KEYS": "1"},                          # the scatter's key array for the item counts (default: the records' x)
     {"BLP_LPT": "0"},                                   # run-grouped sources queued in id order (default: largest work first)
     {"BLP_LPT": "3"},                                   # ... and item-grouped ones
     {"BLP_LPT": "3", "BLP_SPLIT": "3", "BLP_HASH_WORK": "600"},  # ... with the hash-set partition of the queue
-    {"BLP_HOST_PLAN": "1"},                             # blp_batch_create's planning on the host mirror
-    {"BLP_HOST_PLAN": "1", "BLP_SPLIT": "3", "BLP_SPLIT_BIG": "1", "BLP_HASH_WORK": "600"},
 ])
 def test_kernel_paths_vs_oracle(gpu, knobs, monkeypatch):
     for k, v in knobs.items():
@@ -305,15 +297,13 @@ def test_business_fix_adamic_matches_oracle(gpu):
     assert_same_scores(got, exp, "adamic_adar")
 
 
-@pytest.mark.parametrize("variant", [None, "2", "2+gate"])
+@pytest.mark.parametrize("variant", [None, "2"])
 def test_coscheduled_passes_match_single_passes(gpu, variant, monkeypatch):
     # blp_batches_score: the user and business passes of one step run concurrently on their
     # own streams (the large-universe scorer held to a share of the CUs); results must equal
     # each pass scored alone, repeated steps included
     if variant:
         monkeypatch.setenv("BLP_VARIANT", variant[0])  # the large-universe block scorer on this graph
-    if variant and variant.endswith("gate"):
-        monkeypatch.setenv("BLP_PAIR_GATE", "1")  # the business grouping waits for the user grouping
     rng = np.random.default_rng(21)
     a, b = bipartite_edges(rng, 20000, 1500, 200000)
     G = blp.DeviceGraph(a, b)
@@ -503,11 +493,12 @@ def test_node2_planning_with_empty_row_runs(gpu):
     {"BLP_SPLIT": "3", "BLP_SPLIT_BIG": "1", "BLP_HASH_WORK": "600"},
     {"BLP_FORCE_GLOBAL": "1"},
 ])
-def test_device_plan_equals_host_plan(gpu, knobs, monkeypatch):
+def test_device_plan_scores_vs_oracle(gpu, knobs, monkeypatch):
     """blp_batch_create's planning pass on the device (k_plan_pairs / k_plan_sources: bounds, the
-    universe, runs, the sources, build work, heavy and hash-set routing) gives the host loops'
-    plan (BLP_HOST_PLAN=1) on both sides, for source-grouped and shuffled pair lists, and the
-    same scores (similarity.py:20-106)."""
+    universe, runs, the sources, build work, heavy and hash-set routing; the host planning loops
+    were removed in round 6) on both sides, for source-grouped and shuffled pair lists: the plan
+    is the same for a list and its shuffle where the runs do not matter, and every score equals
+    the C oracle's (similarity.py:20-106)."""
     for k, v in knobs.items():
         monkeypatch.setenv(k, v)
     rng = np.random.default_rng(21)
@@ -517,20 +508,17 @@ def test_device_plan_equals_host_plan(gpu, knobs, monkeypatch):
     x = np.repeat(np.sort(rng.choice(nu, 120, replace=False)), 40).astype(np.int32)
     y = rng.integers(nu, G.n, len(x)).astype(np.int32)
     perm = rng.permutation(len(x))
+    ids, da, db = dense_edges(a, b)
+    og = coracle.OracleGraph(len(ids), da, db)
     for xs, ys in ((x, y), (y, x), (x[perm], y[perm])):
         dev = G.batch(xs, ys)
-        monkeypatch.setenv("BLP_HOST_PLAN", "1")
-        host = G.batch(xs, ys)
-        monkeypatch.delenv("BLP_HOST_PLAN")
-        assert dev.plan() == host.plan(), (dev.plan(), host.plan())
-        assert dev.kernel(7) == host.kernel(7)
         dev.score(7)
-        host.score(7)
-        rd, rh = dev.fetch(7), host.fetch(7)
-        for k in ("cn", "jaccard", "adamic"):
-            np.testing.assert_array_equal(rd[k], rh[k])
+        rd = dev.fetch(7)
+        cn, jac, aa, _ = og.score_pairs(np.searchsorted(ids, G.node_ids[xs]), np.searchsorted(ids, G.node_ids[ys]), 7)
+        np.testing.assert_array_equal(rd["cn"], cn)
+        np.testing.assert_array_equal(rd["jaccard"], jac)
+        np.testing.assert_array_equal(rd["adamic"], aa)
         dev.close()
-        host.close()
     _check_against_oracle(a, b, y[perm], x[perm])
 
 
