@@ -101,7 +101,8 @@ def pmc_fields(kernel, pattern, sec=None):
                 fetch, write = 1024.0 * r["fetch_kb_raw"], 1024.0 * r["write_kb"]
                 out = {"traffic": 2 * fetch + write, "traffic_raw": fetch + write,
                        "traffic_source": "%s (kernel avg %.3f ms there)" % (os.path.relpath(f, ROOT),
-                                                                             r["avg_us"] / 1e3)}
+                                                                             r["avg_us"] / 1e3),
+                       "profile_kernel_ms": r["avg_us"] / 1e3}
                 if sec:
                     out["frac_dram"] = out["traffic"] / sec / 1e9 / HBM_PEAK_GBS
                     out["frac_dram_raw"] = out["traffic_raw"] / sec / 1e9 / HBM_PEAK_GBS
@@ -1197,21 +1198,42 @@ def main():
                         "hits": int(res[name]["cn"].astype(np.int64).sum()), "sources": int(len(np.unique(xs_)))}
                  for name, xs_, ys_ in [("user", ex_x, ex_y), ("business", ex_y, ex_x)] if name in res},
     }
-    # roofline of the dominant kernel: the user-side scorer (falls back to the first pass)
+    # roofline of the dominant kernel: the user-side scorer (falls back to the first pass); and
+    # (both sides) a second entry for the business pass -- its scorer and its per-step grouping,
+    # the chain that runs beside the user scorer on the remaining CUs
+    def roofline_of(name, bt, mask):
+        xs, ys = (ex_x, ex_y) if name == "user" else (ex_y, ex_x)
+        byts = alg_bytes(G, xs, ys, mask, res[name]["cn"])
+        sec = ktimes[name]["score_ms"] / 1e3
+        kname = bt.kernel(mask)
+        r = {"bound": "hbm", "achieved": byts / sec / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+             # basis: the kernel's in-step average (HIP events around every timed launch, on the
+             # batch's own stream); frac_profile below uses the committed profile's average instead
+             "frac": byts / sec / 1e9 / HBM_PEAK_GBS, "frac_basis": "in-step HIP-event average (%.4f ms)" % (1e3 * sec),
+             # the counters' HBM-side bytes over the same kernel time: what DRAM actually moved
+             **pmc_fields(kname, "r*_v*_bench.json", sec),
+             "kernel": "%s (%s side)" % (kname, name), "alg_bytes_per_launch": byts,
+             # what the counters name as the bound ("What bounds the user scorer"),
+             # from the newest committed counter summary of this kernel
+             "limiter": pmc_limiter(kname, "r*_v*_bench_pmc.txt")}
+        if r.get("profile_kernel_ms"):
+            r["frac_profile"] = byts / (r["profile_kernel_ms"] / 1e3) / 1e9 / HBM_PEAK_GBS
+        return r
+
     name0, bt0, mask0 = sorted(passes, key=lambda p: p[0] != "user")[0]
-    cn0 = res[name0]["cn"]
-    xs, ys = (ex_x, ex_y) if name0 == "user" else (ex_y, ex_x)
-    byts = alg_bytes(G, xs, ys, mask0, cn0)
-    sec = ktimes[name0]["score_ms"] / 1e3
-    kname = bt0.kernel(mask0)
-    out["roofline"] = {"bound": "hbm", "achieved": byts / sec / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                       "frac": byts / sec / 1e9 / HBM_PEAK_GBS,
-                       # the counters' HBM-side bytes over the same kernel time: what DRAM actually moved
-                       **pmc_fields(kname, "r*_v*_bench.json", sec),
-                       "kernel": "%s (%s side)" % (kname, name0), "alg_bytes_per_launch": byts,
-                       # what the counters name as the bound ("What bounds the user scorer"),
-                       # from the newest committed counter summary of this kernel
-                       "limiter": pmc_limiter(kname, "r*_v*_bench_pmc.txt")}
+    out["roofline"] = roofline_of(name0, bt0, mask0)
+    for name, bt, mask in passes:
+        if name == "business" and name0 == "user":
+            rb = roofline_of(name, bt, mask)
+            # the business grouping per step (bucket sort into item order): read (x, y), gather
+            # rp[y] and rp[y + 1], write the grouped metadata (caller index 4 B, row start 8 B,
+            # row length 4 B) -- 40 B per pair
+            gb = 40 * len(ex_x)
+            gsec = ktimes[name]["group_ms"] / 1e3
+            rb["grouping"] = {"alg_bytes_per_step": gb, "ms": 1e3 * gsec, "achieved": gb / gsec / 1e9,
+                              "frac": gb / gsec / 1e9 / HBM_PEAK_GBS}
+            rb["chain_ms"] = 1e3 * (gsec + ktimes[name]["score_ms"] / 1e3)
+            out["roofline_business"] = rb
     if dist.rank == 0 and args.sides == "both" and not (args.no_parity and args.no_cpu_baseline):
         import coracle
 

@@ -406,9 +406,9 @@ unsigned grid_for(int64_t n, int n_cu) {
 // per device (hipHostMalloc), never registered, unregistered or freed while the library is loaded.
 // Reader threads pread chunk i into slot i % SLOTS and queue its copy; before a slot is refilled
 // its previous copy's event is waited on. The reads and the DMA overlap.
-constexpr int UP_THREADS = 8;                 // reader threads
-constexpr int UP_SLOTS = 2 * UP_THREADS;      // each reader double-buffers its own slots
-constexpr size_t UP_SLOT = size_t(2) << 20;   // bytes per slot: 32 MiB pinned per device
+constexpr int UP_THREADS = 16;                // reader threads at most (BLP_PARSE_READERS: fewer)
+constexpr int UP_SLOTS = 2 * UP_THREADS;      // each reader double-buffers its own two slots
+constexpr size_t UP_SLOT = size_t(2) << 20;   // bytes per slot: 64 MiB pinned per device
 struct Staging {
   std::mutex mu;  // one upload at a time uses the ring
   uint8_t* host = nullptr;
@@ -444,16 +444,25 @@ Staging* staging_of(int device) {
 int staged_upload(Staging* sg, int fd, int64_t S, uint8_t* d_txt, hipStream_t st, size_t chunk, bool* read_ok) {
   std::lock_guard<std::mutex> lk(sg->mu);
   const int64_t nch = (S + (int64_t)chunk - 1) / (int64_t)chunk;
-  const int nt = (int)std::min<int64_t>(UP_THREADS, nch);
+  int readers = UP_THREADS;
+  if (const char* e = getenv("BLP_PARSE_READERS")) readers = std::max(1, std::min(UP_THREADS, atoi(e)));
+  const int nt = (int)std::min<int64_t>(readers, nch);
   std::mutex q_mu;  // a copy and the event recorded behind it are queued together
   std::atomic<int> bad_read{0};
   std::atomic<int> hip_err{(int)hipSuccess};
   std::atomic<int> err_line{0};
+  // BLP_GRAPH_PROF: where the readers' time goes (summed over threads, microseconds)
+  const bool prof = getenv("BLP_GRAPH_PROF") != nullptr;
+  std::atomic<long long> us_wait{0}, us_read{0}, us_queue{0};
+  auto now_us = []() {
+    return std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  };
   auto reader = [&](int t) {
     for (int64_t i = t; i < nch; i += nt) {
       if (bad_read.load(std::memory_order_relaxed) || hip_err.load(std::memory_order_relaxed) != hipSuccess) return;
-      const int s = (int)(i % UP_SLOTS);  // UP_SLOTS is a multiple of nt's bound: slot s is this reader's
+      const int s = (int)(i % (2 * nt));  // i = t (mod nt): slots t and t + nt are this reader's
       uint8_t* buf = sg->host + (size_t)s * UP_SLOT;
+      long long t0 = prof ? now_us() : 0;
       if (sg->pending[s]) {  // the slot's previous copy must have left it
         const hipError_t e = hipEventSynchronize(sg->ev[s]);
         if (e != hipSuccess) {
@@ -462,6 +471,11 @@ int staged_upload(Staging* sg, int fd, int64_t S, uint8_t* d_txt, hipStream_t st
           return;
         }
         sg->pending[s] = false;
+      }
+      if (prof) {
+        const long long t1 = now_us();
+        us_wait += t1 - t0;
+        t0 = t1;
       }
       const int64_t at0 = i * (int64_t)chunk, len = std::min<int64_t>((int64_t)chunk, S - at0);
       int64_t got = 0;
@@ -473,6 +487,11 @@ int staged_upload(Staging* sg, int fd, int64_t S, uint8_t* d_txt, hipStream_t st
         }
         got += r;
       }
+      if (prof) {
+        const long long t1 = now_us();
+        us_read += t1 - t0;
+        t0 = t1;
+      }
       std::lock_guard<std::mutex> q(q_mu);
       hipError_t e = hipMemcpyAsync(d_txt + at0, buf, (size_t)len, hipMemcpyHostToDevice, st);
       if (e == hipSuccess) e = hipEventRecord(sg->ev[s], st);
@@ -482,6 +501,7 @@ int staged_upload(Staging* sg, int fd, int64_t S, uint8_t* d_txt, hipStream_t st
         return;
       }
       sg->pending[s] = true;
+      if (prof) us_queue += now_us() - t0;
     }
   };
   std::vector<std::thread> th;
@@ -490,7 +510,12 @@ int staged_upload(Staging* sg, int fd, int64_t S, uint8_t* d_txt, hipStream_t st
   for (auto& h : th) h.join();
   // the ring is released only once nothing queued reads it (and a fault in the copies surfaces
   // here, attributed to the upload)
+  const long long ts = prof ? now_us() : 0;
   const hipError_t se = hipStreamSynchronize(st);
+  if (prof)
+    fprintf(stderr, "device_parse staged upload: %d readers, %lld chunks of %zu KiB; per reader avg: read %.3f ms, slot wait %.3f ms, "
+            "copy queue %.3f ms; final sync %.3f ms\n", nt, (long long)nch, chunk >> 10, us_read.load() / 1e3 / nt,
+            us_wait.load() / 1e3 / nt, us_queue.load() / 1e3 / nt, (now_us() - ts) / 1e3);
   for (bool& p : sg->pending) p = false;
   if (hip_err.load() != hipSuccess)
     return hip_fail((hipError_t)hip_err.load(), "graph.txt upload (copy queue)", __FILE__, err_line.load());
@@ -911,7 +936,7 @@ namespace blp {
 int preload_ingest() {
   hipFuncAttributes fa;
   if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&k_nl_count)) != hipSuccess) return -1;
-  int dev = 0;  // and the current device's graph.txt staging ring (32 MiB pinned, a few ms once)
+  int dev = 0;  // and the current device's graph.txt staging ring (64 MiB pinned, a few ms once)
   return hipGetDevice(&dev) == hipSuccess && staging_of(dev) ? 0 : -1;
 }
 }  // namespace blp

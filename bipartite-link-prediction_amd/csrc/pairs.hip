@@ -33,6 +33,9 @@
 #ifndef BLP_RC
 #define BLP_RC 1  // row-chunk loops in the large-universe k_score (0: merge-path loops)
 #endif
+#ifndef BLP_SHORT_PF
+#define BLP_SHORT_PF 0  // k_score_short stages the next source's record in LDS (experiment flag)
+#endif
 #ifndef BLP_SHORT_MINB
 #define BLP_SHORT_MINB 7  // short-row scorer: >= 7 workgroups of 256 per CU (<= 72 VGPRs)
 #endif
@@ -2334,6 +2337,10 @@ __global__ __launch_bounds__(256, BLP_SHORT_MINB) void k_score_short(ScoreArgs a
   __shared__ long long s_wtab[SAA ? 256 : 1];
   __shared__ int s_src[2];
   __shared__ unsigned s_h2[2];
+#if BLP_SHORT_PF
+  __shared__ int s_nc[2];             // the claim after the current one (dequeued two ahead)
+  __shared__ SrcRec s_rec[2];         // the next source's record, staged during this one's P3
+#endif
   (void)NW;
   if (SAA && a.wtab)
     for (int i = threadIdx.x; i < 256; i += BLOCK) s_wtab[i] = a.wtab[i];
@@ -2350,19 +2357,54 @@ __global__ __launch_bounds__(256, BLP_SHORT_MINB) void k_score_short(ScoreArgs a
     for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
     if (lane == 0 && c) atomicAdd(dst, c);
   };
+  // -DBLP_PROF phase clocks: 0 dequeue, 1 header + first pair's metadata issued, 2 P1, 3 P2,
+  // 4 distance 1, 5 P3 (scan + outputs + closing barrier)
+  PROF_INIT
+#if BLP_SHORT_PF
+  // Header prefetch (round 6): the record of the source after this one is loaded by 16 lanes
+  // during P1 and staged in LDS before the closing barrier, so a source's header is an LDS read
+  // instead of a dependent global round trip (25 % of the scorer's clocks, r06_check2 probe).
+  // The claim after the current one must be known then: claims are dequeued two ahead.
+  int nxt = threadIdx.x == 0 ? atomicAdd(&a.misc->queue, a.dq) : 0;
+  int nxt2 = threadIdx.x == 0 && nxt < n_active ? atomicAdd(&a.misc->queue, a.dq) : n_active;
+  bool staged = false;  // s_rec[k & 1] holds source k's record (uniform)
+#else
   int nxt = threadIdx.x == 0 ? atomicAdd(&a.misc->queue, a.dq) : 0;  // dequeue one ahead
+#endif
   int k = 0;  // sources scored by this workgroup: s_h2 slot k & 1
   for (int it = 0;; ++it) {
     if (threadIdx.x == 0) {
       s_src[it & 1] = nxt;
+#if BLP_SHORT_PF
+      s_nc[it & 1] = nxt2;
+      nxt = nxt2;
+      if (nxt2 < n_active) nxt2 = atomicAdd(&a.misc->queue, a.dq);
+#else
       if (nxt < n_active) nxt = atomicAdd(&a.misc->queue, a.dq);
+#endif
     }
     __syncthreads();
     const int s_first = s_src[it & 1];
+#if BLP_SHORT_PF
+    const int next_claim = s_nc[it & 1];
+#endif
+    PROF(0)
     if (s_first >= n_active) break;
     const int s_last = min(n_active, s_first + a.dq);
     for (int s = s_first; s < s_last; ++s, ++k) {
+#if BLP_SHORT_PF
+      if (!staged) {  // the workgroup's first source (or after the end of the list): fetched here
+        if ((int)threadIdx.x < 16)
+          reinterpret_cast<int*>(&s_rec[k & 1])[threadIdx.x] = reinterpret_cast<const int*>(a.rec + s)[threadIdx.x];
+        __syncthreads();
+      }
+      const SrcRec& r = s_rec[k & 1];
+      const int sn = s + 1 < s_last ? s + 1 : (next_claim < n_active ? next_claim : -1);
+      int rv = 0;  // lane t < 16: dword t of the next source's record
+      if (sn >= 0 && (int)threadIdx.x < 16) rv = reinterpret_cast<const int*>(a.rec + sn)[threadIdx.x];
+#else
       const SrcRec& r = a.rec[__builtin_amdgcn_readfirstlane(s)];
+#endif
       auto u32 = [](int32_t v) { return (int32_t)__builtin_amdgcn_readfirstlane(v); };
       auto u64 = [](int64_t v) {
         return (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(v >> 32)) << 32) |
@@ -2380,6 +2422,7 @@ __global__ __launch_bounds__(256, BLP_SHORT_MINB) void k_score_short(ScoreArgs a
         pair_row(a, pbeg + threadIdx.x, pf_start, pf_len);
         pf_out = a.g_out[pbeg + threadIdx.x];
       }
+      PROF(1)
       // P1: the pre-built set, counted while copied, or a zeroed bitmap
       unsigned cnt = 0;
       if (hslot >= 0) {
@@ -2395,6 +2438,7 @@ __global__ __launch_bounds__(256, BLP_SHORT_MINB) void k_score_short(ScoreArgs a
       if (threadIdx.x == 0) s_h2[slot ^ 1] = 0;  // the next source's counter (its last reader is past a barrier)
       add_count(cnt, &s_h2[slot]);
       __syncthreads();
+      PROF(2)
       // P2: N(N(x)) from x's wedge row, counting newly set bits
       if (hslot < 0) {
         cnt = 0;
@@ -2416,6 +2460,7 @@ __global__ __launch_bounds__(256, BLP_SHORT_MINB) void k_score_short(ScoreArgs a
         add_count(cnt, &s_h2[slot]);
         __syncthreads();
       }
+      PROF(3)
       // distance 1 (general graphs: N(x) meets the universe): drop it, counting the cleared bits
       if (nx_hi >= c0 && nx_lo < c0 + width) {
         cnt = 0;
@@ -2430,6 +2475,7 @@ __global__ __launch_bounds__(256, BLP_SHORT_MINB) void k_score_short(ScoreArgs a
         if (lane == 0 && cnt) atomicSub(&s_h2[slot], cnt);
         __syncthreads();
       }
+      PROF(4)
       // P3: |H2(x)| = the count minus x itself (distance 0); each thread scores its own pairs
       const int64_t xr = (int64_t)x - c0;
       const unsigned xbit = (xr >= 0 && xr < width) ? (bm[xr >> 5] >> (xr & 31)) & 1u : 0u;
@@ -2477,9 +2523,15 @@ __global__ __launch_bounds__(256, BLP_SHORT_MINB) void k_score_short(ScoreArgs a
           }
         }
       }
+#if BLP_SHORT_PF
+      if (sn >= 0 && (int)threadIdx.x < 16) reinterpret_cast<int*>(&s_rec[(k + 1) & 1])[threadIdx.x] = rv;
+      staged = sn >= 0;
+#endif
       __syncthreads();  // the bitmap and this source's counter are free for the next source
+      PROF(5)
     }
   }
+  PROF_FLUSH
 }
 
 // ------------------------------------------------------------------ HBM-bitmap scorer

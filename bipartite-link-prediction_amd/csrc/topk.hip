@@ -1130,6 +1130,9 @@ __global__ __launch_bounds__(TK_NT) void k_tk_dense_fill(TkArgs a) {
     }
 }
 
+// The arguments stay a by-value struct: through a pointer (round 6) the kernel spilled fewer
+// registers (SGPR spills 315 -> 52, VGPR spills 126 -> 65, scratch 396 -> 248 bytes per lane) and
+// was slower: 15.47 / 15.48 against 15.33 / 15.30 ms alternating on one box (r06_ab1).
 __global__ __launch_bounds__(TK_NT) void k_topk(TkArgs a) {
   __shared__ TkShared s;
   const int tid = threadIdx.x;
