@@ -71,6 +71,21 @@ def alg_bytes(G, x, y, mask, cn=None):
     return int(per_src + per_pair)
 
 
+def wset_alg_bytes(G, x, y, mask):
+    """Algorithmic bytes of the wedge-set scorer (k_score_wset) over pairs
+    (x business, y user), in caller order with no grouping:
+    per pair:  8 (pair ids) + 16 (rp[y], rp[y + 1]) + 4 d_y (N(y), coded ids)
+               + 4 d_y (the word of x in W(c) for each c in N(y)) + 4 (|H2(x)|)
+               + 4 (cn) + 8 (jaccard, if J) + 8 (adamic, if AA)"""
+    d = G.hop1_size.astype(np.int64)
+    per_pair = len(x) * (8 + 16 + 4 + 4) + 8 * int(d[y].sum())
+    if mask & blp.JACCARD:
+        per_pair += 8 * len(x)
+    if mask & blp.ADAMIC:
+        per_pair += 8 * len(x)
+    return int(per_pair)
+
+
 def pmc_fields(kernel, pattern, sec=None):
     """HBM-side bytes per launch of `kernel` from the newest committed PMC summary matching
     `pattern` under profiles/ (written by profiles/summarize.py from separate rocprofv3 --pmc
@@ -1203,9 +1218,10 @@ def main():
     # the chain that runs beside the user scorer on the remaining CUs
     def roofline_of(name, bt, mask):
         xs, ys = (ex_x, ex_y) if name == "user" else (ex_y, ex_x)
-        byts = alg_bytes(G, xs, ys, mask, res[name]["cn"])
-        sec = ktimes[name]["score_ms"] / 1e3
         kname = bt.kernel(mask)
+        byts = (wset_alg_bytes(G, xs, ys, mask) if kname.startswith("k_score_wset")
+                else alg_bytes(G, xs, ys, mask, res[name]["cn"]))
+        sec = ktimes[name]["score_ms"] / 1e3
         r = {"bound": "hbm", "achieved": byts / sec / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
              # basis: the kernel's in-step average (HIP events around every timed launch, on the
              # batch's own stream); frac_profile below uses the committed profile's average instead
@@ -1230,8 +1246,9 @@ def main():
             # row length 4 B) -- 40 B per pair
             gb = 40 * len(ex_x)
             gsec = ktimes[name]["group_ms"] / 1e3
-            rb["grouping"] = {"alg_bytes_per_step": gb, "ms": 1e3 * gsec, "achieved": gb / gsec / 1e9,
-                              "frac": gb / gsec / 1e9 / HBM_PEAK_GBS}
+            rb["grouping"] = ({"alg_bytes_per_step": gb, "ms": 1e3 * gsec, "achieved": gb / gsec / 1e9,
+                               "frac": gb / gsec / 1e9 / HBM_PEAK_GBS} if gsec > 0 else
+                              {"ms": 0.0, "note": "none: the wedge-set scorer reads the pairs in caller order"})
             rb["chain_ms"] = 1e3 * (gsec + ktimes[name]["score_ms"] / 1e3)
             out["roofline_business"] = rb
     if dist.rank == 0 and args.sides == "both" and not (args.no_parity and args.no_cpu_baseline):

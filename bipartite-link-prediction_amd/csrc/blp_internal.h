@@ -141,6 +141,15 @@ struct WedgeBitmaps {
   uint32_t* d_pool = nullptr;
   std::vector<int32_t> h_slot;
 };
+// The dense wedge-set index over [lo, hi) (round 6, hop3.hip wedge_sets): for EVERY node c of the
+// range, W(c) = N(N(c)) ∩ [lo, hi) as a bitmap of `words` u32 at d_pool + (c - lo) * words, and
+// d_h2[c - lo] = |W(c) \ {c}| (in a bipartite graph: |H2(c)|, the exact distance-2 set). Built from
+// the wedge rows; needs every node of the range with neighbours to hold one.
+struct WedgeSets {
+  int64_t lo = 0, hi = 0, words = 0;
+  uint32_t* d_pool = nullptr;
+  int32_t* d_h2 = nullptr;
+};
 }
 
 struct blp_graph {
@@ -185,6 +194,7 @@ struct blp_graph {
   // an id range [lo, hi), built on first use per range (the hop-3 mark range; the business
   // batch's universe) and kept with the graph (at most 4 ranges)
   std::vector<blp::WedgeBitmaps> wbm;
+  blp::WedgeSets* wset = nullptr;  // the dense wedge-set index (one range; built on first use, under wbm_mu)
   int wedge_users = 0;  // live batches whose plan reads the wedge index or its bitmaps (under wbm_mu)
   std::mutex wbm_mu;  // held across wedge_bitmaps' lookup-or-build (batches are created concurrently)
   // host mirrors used for launch planning (bitmap universe bounds) and the host-built indexes:
@@ -235,6 +245,7 @@ const int32_t* host_col_idx(blp_graph* g);
 void free_node2(blp_graph* g);
 // per translation unit: load its GPU code object now (hipFuncGetAttributes on one of its kernels)
 int preload_ingest();
+int preload_staging(int device);  // the graph.txt staging ring of `device` (ingest.hip), allocated once
 int preload_csr();
 int preload_graph();
 int preload_hot();
@@ -249,6 +260,10 @@ int repr_launch(const double* d_v, int64_t n, bool zero_int, char* d_out, int n_
 // the graph's wedge-row bitmaps over [lo, hi) (built and cached on first use); null with *rc == 0
 // when there is no wedge index or no cache slot left
 const WedgeBitmaps* wedge_bitmaps(blp_graph* g, int64_t lo, int64_t hi, int* rc);
+// the graph's dense wedge-set index over [lo, hi) (built and cached on first use; one range per
+// graph); null with *rc == 0 when it cannot be built (no wedge rows, a node of the range with
+// neighbours but no wedge row, over the HBM budget BLP_WSET_MB / 25 % of free HBM, or another range cached)
+const WedgeSets* wedge_sets(blp_graph* g, int64_t lo, int64_t hi, int* rc);
 void free_wedge_index(blp_graph* g);
 void free_hot_index(blp_graph* g);
 int timer_begin(blp_graph* g, int k, hipEvent_t* start);

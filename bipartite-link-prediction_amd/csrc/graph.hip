@@ -585,6 +585,9 @@ int blp_device_count(int* n) {
 int blp_stream_prewarm(int device, int n) {
   BLP_CHECK(n >= 0 && n <= 16, BLP_E_ARG, "blp_stream_prewarm: 0 <= n <= 16");
   BLP_HIP(hipSetDevice(device));
+  // first the pinned staging ring of the graph.txt upload: similarity.main's parse, on the other
+  // thread, reaches it within milliseconds
+  if (preload_staging(device)) return BLP_E_HIP_BASE;
   // Top the pool up to n streams (BLP_PREWARM_ALWAYS=1: always create n, the round-4 behaviour),
   // run one empty kernel on each new one, and hold stream_take until they are in the pool: the
   // caller's first GPU work then neither creates a stream nor overlaps this thread's creation (an

@@ -415,6 +415,57 @@ __global__ __launch_bounds__(HW_BLOCK) void k_wbm_fill(const int64_t* __restrict
   for (int i = threadIdx.x; i < words; i += HW_BLOCK) dst[i] = bm[i];
 }
 
+// The dense wedge-set index (blp_internal.h WedgeSets): one workgroup per node c of [lo, lo + n):
+// W(c) = the set of ids of c's wedge row inside [lo, hi), OR-ed in LDS (a word is read before its
+// bit is OR-ed: a wedge row repeats the popular ids of its member rows), then written out whole,
+// with |W(c) \ {c}| counted on the way.
+__global__ __launch_bounds__(HW_BLOCK) void k_wset_fill(const int64_t* __restrict__ wp, const uint4* __restrict__ wedge,
+                                                        int64_t lo, int64_t span, int words, uint32_t* __restrict__ pool,
+                                                        int32_t* __restrict__ h2) {
+  uint32_t* bm = hw_dyn;
+  __shared__ unsigned red[HW_BLOCK / 64];
+  const int64_t c = lo + blockIdx.x;
+  for (int i = threadIdx.x; i < words; i += HW_BLOCK) bm[i] = 0;
+  __syncthreads();
+  const uint32_t c0u = (uint32_t)lo, wu = (uint32_t)span;
+  const int64_t s = wp[c], e = wp[c + 1];
+  for (int64_t q = s + threadIdx.x; q < e; q += 4 * HW_BLOCK) {
+    uint4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = wedge[q + HW_BLOCK * u < e ? q + HW_BLOCK * u : q];  // a repeat ORs nothing new
+    uint32_t rr[16], wd[16];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      rr[4 * u] = v[u].x - c0u;
+      rr[4 * u + 1] = v[u].y - c0u;
+      rr[4 * u + 2] = v[u].z - c0u;
+      rr[4 * u + 3] = v[u].w - c0u;
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) wd[k] = bm[(rr[k] < wu ? rr[k] : 0u) >> 5];
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      if (rr[k] < wu && !((wd[k] >> (rr[k] & 31)) & 1u)) atomicOr(&bm[rr[k] >> 5], 1u << (rr[k] & 31));
+  }
+  __syncthreads();
+  uint32_t* dst = pool + (int64_t)blockIdx.x * words;
+  unsigned cnt = 0;
+  for (int i = threadIdx.x; i < words; i += HW_BLOCK) {
+    const uint32_t w = bm[i];
+    dst[i] = w;
+    cnt += __popc(w);
+  }
+  for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned t = 0;
+    for (int w = 0; w < HW_BLOCK / 64; ++w) t += red[w];
+    const uint32_t own = (bm[blockIdx.x >> 5] >> (blockIdx.x & 31)) & 1u;  // c itself (distance 0)
+    h2[blockIdx.x] = (int32_t)(t - own);
+  }
+}
+
 }  // namespace
 
 using namespace blp;
@@ -483,6 +534,55 @@ const WedgeBitmaps* wedge_bitmaps(blp_graph* g, int64_t lo, int64_t hi, int* rc)
   g->wbm.push_back(std::move(w));
   return &g->wbm.back();
 }
+const WedgeSets* wedge_sets(blp_graph* g, int64_t lo, int64_t hi, int* rc) {
+  *rc = BLP_OK;
+  if (!g->d_wp || hi <= lo || getenv("BLP_NO_WSET")) return nullptr;
+  std::lock_guard<std::mutex> lock(g->wbm_mu);
+  if (g->wset) return g->wset->lo == lo && g->wset->hi == hi ? g->wset : nullptr;
+  const int64_t span = hi - lo, words = (span + 31) / 32;
+  if (span >= (int64_t(1) << 31) || words > 16 * 1024) return nullptr;  // one LDS bitmap per node (<= 64 KiB)
+  // every node of the range with neighbours needs its wedge row (the set is built from it)
+  for (int64_t c = lo; c < hi; ++c)
+    if (g->hrp[c + 1] > g->hrp[c] && g->h_wp[c + 1] == g->h_wp[c]) return nullptr;
+  const double bytes = 4.0 * (double)words * (double)span + 4.0 * (double)span;
+  size_t free_b = 0, total_b = 0;
+  if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  free_b += dev_cache_bytes(g->device);
+  const double budget = std::min((double)((getenv("BLP_WSET_MB") ? atoll(getenv("BLP_WSET_MB")) : 4096) << 20),
+                                 0.25 * (double)free_b);
+  if (bytes > budget) return nullptr;
+  auto* w = new WedgeSets();
+  w->lo = lo;
+  w->hi = hi;
+  w->words = words;
+  auto hip = [&](hipError_t e, const char* what) {
+    if (e != hipSuccess) *rc = hip_fail(e, what, __FILE__, __LINE__);
+    return e == hipSuccess;
+  };
+  bool ok = hip(dev_malloc(&w->d_pool, 4 * (size_t)words * (size_t)span), "hipMalloc (wedge sets)") &&
+            hip(dev_malloc(&w->d_h2, 4 * (size_t)span), "hipMalloc (wedge-set sizes)");
+  if (ok) {
+    hipLaunchKernelGGL(k_wset_fill, dim3((unsigned)span), dim3(HW_BLOCK), 4 * (size_t)words, g->stream,
+                       (const int64_t*)g->d_wp, (const uint4*)g->d_wedge, lo, span, (int)words, w->d_pool, w->d_h2);
+    ok = hip(hipGetLastError(), "k_wset_fill launch") && hip(hipStreamSynchronize(g->stream), "hipStreamSynchronize");
+  }
+  if (!ok) {
+    if (w->d_pool) (void)hipFree(w->d_pool);
+    if (w->d_h2) (void)hipFree(w->d_h2);
+    delete w;
+    if (*rc == BLP_E_HIP_BASE - (int)hipErrorOutOfMemory) {  // no room: the batch takes the grouped path
+      (void)hipGetLastError();
+      *rc = BLP_OK;
+    }
+    return nullptr;
+  }
+  g->wset = w;
+  return w;
+}
+
 }  // namespace blp
 
 extern "C" int blp_hop3_sample(blp_graph* g, const int32_t* src, int64_t n_src, const int32_t* pos_off,

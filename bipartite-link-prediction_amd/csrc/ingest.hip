@@ -408,7 +408,8 @@ unsigned grid_for(int64_t n, int n_cu) {
 // its previous copy's event is waited on. The reads and the DMA overlap.
 constexpr int UP_THREADS = 16;                // reader threads at most (BLP_PARSE_READERS: fewer)
 constexpr int UP_SLOTS = 2 * UP_THREADS;      // each reader double-buffers its own two slots
-constexpr size_t UP_SLOT = size_t(2) << 20;   // bytes per slot: 64 MiB pinned per device
+constexpr size_t UP_SLOT = size_t(512) << 10; // bytes per slot: 16 MiB pinned per device (hipHostMalloc
+                                              // 3.9 ms; 64 MiB took 15-19 ms, r06_ab2_pinned)
 struct Staging {
   std::mutex mu;  // one upload at a time uses the ring
   uint8_t* host = nullptr;
@@ -571,8 +572,10 @@ int device_load(const char* path, int device, blp_edges** out) {
     int n_cu = 256, cu_attr = 0;
     if (hipDeviceGetAttribute(&cu_attr, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cu_attr > 0) n_cu = cu_attr;
     if (!(st = stream_take(device))) return BLP_E_HIP_BASE;
+    stage("setup");
     Staging* sg = staging_of(device);
     if (!sg) return BLP_E_HIP_BASE;
+    stage("ring");
     const bool tail_nl = last_byte == '\n';
     const int64_t T = S + (tail_nl ? 0 : 1);  // a missing final newline is supplied
     const int64_t nb = (T + NL_CHUNK - 1) / NL_CHUNK;
@@ -936,7 +939,8 @@ namespace blp {
 int preload_ingest() {
   hipFuncAttributes fa;
   if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&k_nl_count)) != hipSuccess) return -1;
-  int dev = 0;  // and the current device's graph.txt staging ring (64 MiB pinned, a few ms once)
+  int dev = 0;  // and the current device's graph.txt staging ring (16 MiB pinned, a few ms once)
   return hipGetDevice(&dev) == hipSuccess && staging_of(dev) ? 0 : -1;
 }
+int preload_staging(int device) { return staging_of(device) ? 0 : -1; }
 }  // namespace blp

@@ -33,9 +33,6 @@
 #ifndef BLP_RC
 #define BLP_RC 1  // row-chunk loops in the large-universe k_score (0: merge-path loops)
 #endif
-#ifndef BLP_SHORT_PF
-#define BLP_SHORT_PF 0  // k_score_short stages the next source's record in LDS (experiment flag)
-#endif
 #ifndef BLP_SHORT_MINB
 #define BLP_SHORT_MINB 7  // short-row scorer: >= 7 workgroups of 256 per CU (<= 72 VGPRs)
 #endif
@@ -2337,10 +2334,6 @@ __global__ __launch_bounds__(256, BLP_SHORT_MINB) void k_score_short(ScoreArgs a
   __shared__ long long s_wtab[SAA ? 256 : 1];
   __shared__ int s_src[2];
   __shared__ unsigned s_h2[2];
-#if BLP_SHORT_PF
-  __shared__ int s_nc[2];             // the claim after the current one (dequeued two ahead)
-  __shared__ SrcRec s_rec[2];         // the next source's record, staged during this one's P3
-#endif
   (void)NW;
   if (SAA && a.wtab)
     for (int i = threadIdx.x; i < 256; i += BLOCK) s_wtab[i] = a.wtab[i];
@@ -2360,51 +2353,23 @@ __global__ __launch_bounds__(256, BLP_SHORT_MINB) void k_score_short(ScoreArgs a
   // -DBLP_PROF phase clocks: 0 dequeue, 1 header + first pair's metadata issued, 2 P1, 3 P2,
   // 4 distance 1, 5 P3 (scan + outputs + closing barrier)
   PROF_INIT
-#if BLP_SHORT_PF
-  // Header prefetch (round 6): the record of the source after this one is loaded by 16 lanes
-  // during P1 and staged in LDS before the closing barrier, so a source's header is an LDS read
-  // instead of a dependent global round trip (25 % of the scorer's clocks, r06_check2 probe).
-  // The claim after the current one must be known then: claims are dequeued two ahead.
-  int nxt = threadIdx.x == 0 ? atomicAdd(&a.misc->queue, a.dq) : 0;
-  int nxt2 = threadIdx.x == 0 && nxt < n_active ? atomicAdd(&a.misc->queue, a.dq) : n_active;
-  bool staged = false;  // s_rec[k & 1] holds source k's record (uniform)
-#else
+  // (Staging the next source's record in LDS during this one's P3, with claims dequeued two ahead,
+  // cut the scorer 1.60 -> 1.42 ms in-step but slowed the co-scheduled user pass: step 2.135 -> 2.26
+  // ms at every CU share tried, r06_ab1-3.)
   int nxt = threadIdx.x == 0 ? atomicAdd(&a.misc->queue, a.dq) : 0;  // dequeue one ahead
-#endif
   int k = 0;  // sources scored by this workgroup: s_h2 slot k & 1
   for (int it = 0;; ++it) {
     if (threadIdx.x == 0) {
       s_src[it & 1] = nxt;
-#if BLP_SHORT_PF
-      s_nc[it & 1] = nxt2;
-      nxt = nxt2;
-      if (nxt2 < n_active) nxt2 = atomicAdd(&a.misc->queue, a.dq);
-#else
       if (nxt < n_active) nxt = atomicAdd(&a.misc->queue, a.dq);
-#endif
     }
     __syncthreads();
     const int s_first = s_src[it & 1];
-#if BLP_SHORT_PF
-    const int next_claim = s_nc[it & 1];
-#endif
     PROF(0)
     if (s_first >= n_active) break;
     const int s_last = min(n_active, s_first + a.dq);
     for (int s = s_first; s < s_last; ++s, ++k) {
-#if BLP_SHORT_PF
-      if (!staged) {  // the workgroup's first source (or after the end of the list): fetched here
-        if ((int)threadIdx.x < 16)
-          reinterpret_cast<int*>(&s_rec[k & 1])[threadIdx.x] = reinterpret_cast<const int*>(a.rec + s)[threadIdx.x];
-        __syncthreads();
-      }
-      const SrcRec& r = s_rec[k & 1];
-      const int sn = s + 1 < s_last ? s + 1 : (next_claim < n_active ? next_claim : -1);
-      int rv = 0;  // lane t < 16: dword t of the next source's record
-      if (sn >= 0 && (int)threadIdx.x < 16) rv = reinterpret_cast<const int*>(a.rec + sn)[threadIdx.x];
-#else
       const SrcRec& r = a.rec[__builtin_amdgcn_readfirstlane(s)];
-#endif
       auto u32 = [](int32_t v) { return (int32_t)__builtin_amdgcn_readfirstlane(v); };
       auto u64 = [](int64_t v) {
         return (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(v >> 32)) << 32) |
@@ -2523,15 +2488,89 @@ __global__ __launch_bounds__(256, BLP_SHORT_MINB) void k_score_short(ScoreArgs a
           }
         }
       }
-#if BLP_SHORT_PF
-      if (sn >= 0 && (int)threadIdx.x < 16) reinterpret_cast<int*>(&s_rec[(k + 1) & 1])[threadIdx.x] = rv;
-      staged = sn >= 0;
-#endif
       __syncthreads();  // the bitmap and this source's counter are free for the next source
       PROF(5)
     }
   }
   PROF_FLUSH
+}
+
+// ------------------------------------------------------------------ wedge-set scorer (round 6)
+// The business side of a bipartite graph without grouping or per-source builds. For a pair (x, y)
+// -- x a business, y a user -- the reference's CN is |H2(x) ∩ N(y)| with H2(x) = N(N(x)) \ {x}
+// (similarity.py:63-106). Membership is symmetric: c ∈ N(N(x)) ⟺ x ∈ N(N(c)). So instead of
+// building H2(x) in LDS per source (after sorting the pairs by x), each pair tests x's bit in the
+// wedge set W(c) of each c ∈ N(y) -- bitmaps the graph keeps in HBM (WedgeSets, hop3.hip; 1.25 GB at
+// config 2). One thread per pair, in caller order: a user's pairs are consecutive, so the row N(y)
+// and its ~10 sets are shared by a whole run of lanes and stay in L2. |H2(x)| comes from the index
+// too. Counts and exact Adamic-Adar words are the short-row scorer's, bit for bit; the outputs are
+// written in caller order, coalesced. The grid's blocks are mapped XCD-major: the blocks one XCD
+// runs at a time take consecutive pairs, so a run's sets are fetched into one L2, not eight.
+struct WsetArgs {
+  const int32_t* x;
+  const int32_t* y;
+  const uint32_t* pool;  // W(c) at pool + (c - lo) * words
+  const int32_t* h2;     // |W(c) \ {c}|
+  int64_t lo, span, words;
+};
+
+template <bool SAA>
+__global__ __launch_bounds__(256) void k_score_wset(ScoreArgs a, WsetArgs w) {
+  __shared__ long long s_wtab[SAA ? 256 : 1];
+  if (SAA && a.wtab)
+    for (int i = threadIdx.x; i < 256; i += 256) s_wtab[i] = a.wtab[i];
+  if (SAA) __syncthreads();
+  const bool want_j = (a.mask & BLP_JACCARD) != 0;
+  const bool want_a = SAA && (a.mask & BLP_ADAMIC) != 0;
+  const uint32_t span = (uint32_t)w.span, lou = (uint32_t)w.lo;
+  const int nb = (int)gridDim.x, bid = (int)blockIdx.x;
+  const int lb = (nb & 7) == 0 ? (bid & 7) * (nb >> 3) + (bid >> 3) : bid;  // XCD-major (blocks go to XCDs round robin)
+  for (int64_t i = (int64_t)lb * 256 + threadIdx.x; i < a.np; i += (int64_t)nb * 256) {
+    const int x = w.x[i], y = w.y[i];
+    if (!PS_OK(a.misc, x >= 0 && x < a.n_nodes && y >= 0 && y < a.n_nodes, 2, (int64_t)x, a.n_nodes)) continue;
+    const uint32_t xr = (uint32_t)x - lou;  // < span (planned: every source lies in the sets' range)
+    if (!PS_OK(a.misc, xr < span, 12, (int64_t)xr, w.span)) continue;
+    const int64_t st = a.rp[y];
+    const int len = (int)(a.rp[y + 1] - st);
+    const uint32_t* col = w.pool + (xr >> 5);  // x's word in every set
+    const uint32_t xb = xr & 31;
+    unsigned c = 0;
+    unsigned long long acc = 0;
+    uint32_t acch = 0;
+    for (int h = 0; h < len; h += SHORT_PART) {
+      int e[SHORT_PART];
+      row_part(a.cw, st, len, h, e);
+      uint32_t wd[SHORT_PART];
+#pragma unroll
+      for (int j = 0; j < SHORT_PART; ++j) {
+        const uint32_t id = (uint32_t)e[j] & a.idmask;
+        const uint32_t r = id - lou;
+        wd[j] = (h + j < len && r < span && id != (uint32_t)x) ? col[(int64_t)r * w.words] : 0u;
+      }
+#pragma unroll
+      for (int j = 0; j < SHORT_PART; ++j) {
+        const bool hit = (wd[j] >> xb) & 1u;
+        c += hit ? 1u : 0u;
+        if (SAA && want_a && hit) {
+          const uint32_t code = ((uint32_t)e[j] >> a.idbits) & 255u;
+          const unsigned long long wt = (unsigned long long)(code ? s_wtab[code] : a.aaw[e[j] & a.idmask]);
+          acc += wt;
+          acch += (uint32_t)(wt >> 32);
+        }
+      }
+    }
+    a.cn[i] = c;
+    if (SAA && want_a) a.aa[i] = blp::aa_value(acc, acch);
+    if (want_j) {
+      const long long uni = (long long)w.h2[xr] + len - (long long)c;
+      if (uni <= 0) {
+        a.jac[i] = __builtin_nan("");
+        atomicOr(&a.misc->zero_div, 1);
+      } else {
+        a.jac[i] = (double)c / (double)uni;  // correctly rounded, as Python's float division
+      }
+    }
+  }
 }
 
 // ------------------------------------------------------------------ HBM-bitmap scorer
@@ -3410,6 +3449,11 @@ struct blp_batch {
   int32_t* d_lpt = nullptr;      // [n_sources] the active list in that order, written by k_run_cnt
   int64_t n_hash = 0;          // such sources
   bool use_short = false;   // the short-row scorer takes this batch (decided once, at create)
+  // the graph's dense wedge-set index (k_score_wset; or null): a bipartite business-side batch
+  // scored pair by pair in caller order -- no grouping, no per-source bitmap build
+  const uint32_t* wset_pool = nullptr;
+  const int32_t* wset_h2 = nullptr;
+  int64_t wset_lo = 0, wset_span = 0, wset_words = 0;
   bool wedge_user = false;  // its plan reads the graph's wedge index (counted in g->wedge_users)
   int64_t work_elems = 0;  // planned build + scan elements (co-scheduling estimate)
   Knobs kn;               // environment switches, read once at create
@@ -3658,6 +3702,7 @@ static int batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_
   if (n_sources == 0) xlo = xhi = 0;
   bool runs = in_runs && !kn.no_runs;  // x non-decreasing: grouped by run heads (BLP_NO_RUNS: bucket sort)
   if (lo > hi) lo = hi = 0;
+  const int64_t lo_raw = lo;  // the universe's first id (the wedge-set range starts there, unaligned)
   lo &= ~int64_t(127);  // 128-bit aligned so dense rows map onto whole 16-byte LDS vectors
   b->runs = runs;
   b->lo = lo;
@@ -3933,6 +3978,27 @@ static int batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_
   if (b->chunks > 1 && dev_malloc(&b->d_aa_part, 16 * np) != hipSuccess)
     return bail(fail(BLP_E_HIP_BASE - (int)hipErrorOutOfMemory, "blp_batch_create: hipMalloc failed"));
   b->use_short = short_kernel(b);  // fixed here: d_rec's allocation and the launch must agree
+  // ---- the dense wedge-set path (k_score_wset). In a bipartite graph c ∈ H2(x) ⟺ x ∈ N(N(c)), c ≠ x,
+  // so CN(x, y) = #{c ∈ N(y), c ≠ x : bit x of W(c)} with W(c) = N(N(c)) from the graph's wedge-set
+  // index, and |H2(x)| = |W(x) \ {x}| from the same index. Taken by short-row batches with wedge
+  // rows whose rows read (the y and N(x)) lie outside the sets' range (N(x) is then never at
+  // distance 2) -- the business side of a review graph (BLP_NO_WSET=1: the grouped path)
+  if (b->use_short && n_pairs > 0 && g->d_wp && !kn.no_wedge && !b->global && !b->split && b->chunks == 1 && span > 0) {
+    const int64_t wlo = std::min<int64_t>(lo_raw, xlo), whi = std::max<int64_t>(hi, xhi);
+    if (rows_lo >= whi || rows_hi <= wlo) {
+      int rcw = BLP_OK;
+      const WedgeSets* ws = wedge_sets(g, wlo, whi, &rcw);
+      if (rcw) return bail(rcw);
+      if (ws) {
+        b->wset_pool = ws->d_pool;
+        b->wset_h2 = ws->d_h2;
+        b->wset_lo = ws->lo;
+        b->wset_span = ws->hi - ws->lo;
+        b->wset_words = ws->words;
+      }
+    }
+  }
+  stage("wset");
   // source records: the short-row scorer, and the large scorer (its header in one round trip)
   const bool want_rec = b->use_short || (b->variant == V_LARGE && !b->split && !b->global);
   if (want_rec &&
@@ -3956,7 +4022,7 @@ static int batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_
   // the plan reads the wedge index (wedge rows, wedge slices of heavy sources, wedge-row bitmaps):
   // the create's registration stays, so an out-of-memory retry releases the index only when no
   // live batch reads it; a plan that does not read it drops the registration
-  const bool reads_wedge = b->wedge_user && !kn.no_wedge && (b->use_short || b->split || wedge_items || b->wbm_slot);
+  const bool reads_wedge = b->wedge_user && !kn.no_wedge && (b->use_short || b->split || wedge_items || b->wbm_slot || b->wset_pool);
   if (b->wedge_user && !reads_wedge) {
     std::lock_guard<std::mutex> lk(g->wbm_mu);
     --g->wedge_users;
@@ -4060,6 +4126,8 @@ int blp_batch_kernel(const blp_batch* b, uint32_t mask, char* name, int cap) {
     snprintf(buf, sizeof buf, "k_score_global<%d, %d, 8>", G_BLOCK, G_SEG);
   else if (b->split)
     snprintf(buf, sizeof buf, "k_score_split<%d, %d, %d, 8>", S_BLOCK, b->split_big ? S_CAP_BIG : S_CAP, S_SEG);
+  else if (b->wset_pool)
+    snprintf(buf, sizeof buf, "k_score_wset<%s>", aa ? "true" : "false");
   else if (b->use_short && b->g->d_wp && !b->kn.no_wedge)
     snprintf(buf, sizeof buf, "k_score_short<%s>", aa ? "true" : "false");
   else if (b->use_short)
@@ -4097,6 +4165,69 @@ int blp_prof_read(unsigned long long* out) {  // experiment builds only: per-pha
 
 
 
+// A batch on the wedge-set path (k_score_wset): no grouping; one launch over the pairs
+static int score_wset(blp_graph* g, blp_batch* b, uint32_t mask) {
+  int rc;
+  const int64_t np = b->n_pairs;
+  BLP_HIP(hipMemsetAsync(b->d_misc, 0, offsetof(Misc, dbg), b->stream));
+  hipEvent_t t1, bt1;
+  if ((rc = timer_begin(g->timers[K_SCORE], b->stream, &t1))) return rc;
+  if ((rc = timer_begin(b->t_score, b->stream, &bt1))) return rc;
+  if (np) {
+    ScoreArgs a{};
+    a.rp = g->d_rp;
+    a.ci = g->d_ci;
+    a.aaw = g->d_aaw_fx;
+    const bool coded = g->d_ci_w && !b->kn.no_wcodes;
+    a.cw = coded ? g->d_ci_w : g->d_ci;
+    a.idbits = coded ? g->id_bits : 31;
+    a.idmask = (uint32_t)((1ull << a.idbits) - 1);
+    a.wtab = g->d_wtab;
+    a.misc = b->d_misc;
+    a.cn = b->d_cn;
+    a.jac = b->d_jac;
+    a.aa = b->d_aa;
+    a.mask = mask | BLP_CN;
+    a.np = np;
+    a.n_nodes = g->n;
+    a.nnz = g->nnz;
+    WsetArgs w{b->d_x, b->d_y, b->wset_pool, b->wset_h2, b->wset_lo, b->wset_span, b->wset_words};
+#ifdef BLP_DEBUG
+    if (b->kn.debug_null == "wset") w.pool = nullptr;  // test knob: the pre-launch check refuses it
+#endif
+    const char* missing = nullptr;
+    auto need = [&](const void* p, const char* what) {
+      if (!p && !missing) missing = what;
+    };
+    need(a.rp, "row offsets");
+    need(a.cw, "col_idx");
+    need(a.misc, "batch counters");
+    need(a.cn, "cn output");
+    need(a.jac, "jaccard output");
+    need(a.aa, "adamic output");
+    need(w.x, "pair x");
+    need(w.y, "pair y");
+    need(w.pool, "wedge sets");
+    need(w.h2, "wedge-set sizes");
+    if ((mask & BLP_ADAMIC) && !a.aaw) missing = missing ? missing : "aa weights";
+    if (missing) {
+      char msg[160];
+      snprintf(msg, sizeof msg, "blp_batch_score: the launch path reads a null device pointer (%s)", missing);
+      return fail(BLP_E_STATE, msg);
+    }
+    const int cus = b->cus > 0 ? b->cus : g->n_cu;
+    const int64_t want = (np + 255) / 256;
+    const int grid = (int)std::max<int64_t>(8, std::min<int64_t>(want, (int64_t)cus * 8) / 8 * 8);
+    if (mask & BLP_ADAMIC)
+      hipLaunchKernelGGL(k_score_wset<true>, dim3(grid), dim3(256), 0, b->stream, a, w);
+    else
+      hipLaunchKernelGGL(k_score_wset<false>, dim3(grid), dim3(256), 0, b->stream, a, w);
+    BLP_HIP(hipGetLastError());
+  }
+  if ((rc = timer_end(b->t_score, b->stream, bt1))) return rc;
+  return timer_end(g->timers[K_SCORE], b->stream, t1);
+}
+
 int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   BLP_CHECK(g && b && b->g == g, BLP_E_ARG, "blp_batch_score: graph/batch mismatch");
   BLP_CHECK((mask & ~7u) == 0, BLP_E_ARG, "blp_batch_score: unknown method bits");
@@ -4123,6 +4254,7 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   int32_t* bact = tiles + std::max(tiles_h, tiles_b) + 1;
   int32_t* abase = bact + b->nb;
   int4* tmp = reinterpret_cast<int4*>((reinterpret_cast<uintptr_t>(abase + b->nb) + 15) & ~uintptr_t(15));
+  if (b->wset_pool) return score_wset(g, b, mask);
   hipEvent_t t0, bt0;
   if ((rc = timer_begin(g->timers[K_GROUP], b->stream, &t0))) return rc;
   if ((rc = timer_begin(b->t_group, b->stream, &bt0))) return rc;
@@ -4418,13 +4550,22 @@ int blp_batches_score(blp_graph* g, int n, blp_batch* const* bs, const uint32_t*
   BLP_CHECK(g && n >= 0 && (n == 0 || (bs && masks)), BLP_E_ARG, "blp_batches_score: bad arguments");
   auto is_large = [](const blp_batch* b) { return b->variant == V_LARGE && !b->split && !b->global; };
   double t_large = 0.0, t_other = 0.0;
+  int n_wset = 0;
   for (int i = 0; i < n; ++i) {
     BLP_CHECK(bs[i] && bs[i]->g == g, BLP_E_ARG, "blp_batches_score: graph/batch mismatch");
     if (is_large(bs[i]))
       t_large += (double)bs[i]->work_elems / 1.2e9;
+    else if (bs[i]->wset_pool)
+      ++n_wset;
     else
       t_other += (double)bs[i]->work_elems / 1.8e8 + 3.9e-8 * (double)bs[i]->n_pairs;
   }
+  // wedge-set batches (k_score_wset: no grouping, one light launch) are enqueued beside the large
+  // pass, which then holds no CU share: the light launch runs while the large pass groups its
+  // pairs, and the large scorer takes the whole chip after it (config 2: 1.715-1.717 ms per step;
+  // after the large pass on its stream's completion, BLP_WSET_SERIAL=1: 1.761-1.764 ms; with the
+  // large pass held to 240 / 224 / 208 / 192 CUs: 1.80 / 1.85 / 1.96 / 2.05-2.07 ms, r06_check3)
+  static const bool wset_serial = getenv("BLP_WSET_SERIAL") && atoi(getenv("BLP_WSET_SERIAL")) > 0;
   int share = g->n_cu;
   if (t_large > 0.0 && t_other > 0.0) {
     const double f = t_large / (t_large + 0.38 * t_other);
@@ -4434,13 +4575,26 @@ int blp_batches_score(blp_graph* g, int n, blp_batch* const* bs, const uint32_t*
   // chunk-parallel batches (config 5's two passes) each take the whole chip: holding each
   // persistent grid to a CU share was slower at every share tried (1951 ms per config-5 step in
   // proportion to planned work, 864 / 903 ms at 176 / 128 user CUs, against 743 ms)
+  if (n_wset && !wset_serial && n > 0 && bs[0]->kn.cosched_cus > 0 && t_other == 0.0) t_other = 1.0;  // share applies
   int rc = BLP_OK;
-  for (int i = 0; i < n && !rc; ++i) {
-    blp_batch* b = bs[i];
-    b->cus = is_large(b) && t_other > 0.0 ? share : 0;
-    rc = blp_batch_score(g, b, masks[i]);
-    b->cus = 0;
+  hipEvent_t large_done = nullptr;
+  for (int pass = 0; pass < 2 && !rc; ++pass) {  // pass 0: every batch but the serial wedge-set ones
+    for (int i = 0; i < n && !rc; ++i) {
+      blp_batch* b = bs[i];
+      const bool later = wset_serial && b->wset_pool && t_large > 0.0;
+      if (later != (pass == 1)) continue;
+      if (later && large_done) BLP_HIP(hipStreamWaitEvent(b->stream, large_done, 0));
+      b->cus = is_large(b) && t_other > 0.0 ? share : 0;
+      rc = blp_batch_score(g, b, masks[i]);
+      b->cus = 0;
+      if (!rc && is_large(b) && wset_serial && n_wset && !large_done) {
+        hipError_t e = hipEventCreateWithFlags(&large_done, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventRecord(large_done, b->stream);
+        if (e != hipSuccess) rc = hip_fail(e, "blp_batches_score: large-pass event", __FILE__, __LINE__);
+      }
+    }
   }
+  if (large_done) (void)hipEventDestroy(large_done);
   return rc;
 }
 

@@ -214,6 +214,12 @@ void free_wedge_index(blp_graph* g) {
     if (w.d_pool) (void)hipFree(w.d_pool);
   }
   g->wbm.clear();
+  if (g->wset) {  // built from the wedge rows: goes with them
+    if (g->wset->d_pool) (void)hipFree(g->wset->d_pool);
+    if (g->wset->d_h2) (void)hipFree(g->wset->d_h2);
+    delete g->wset;
+    g->wset = nullptr;
+  }
 }
 
 }  // namespace blp

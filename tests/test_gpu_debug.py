@@ -67,6 +67,7 @@ def _run(mode, extra):
     ("large", {"BLP_VARIANT": "2"}),
     ("global", {"BLP_FORCE_GLOBAL": "1"}),
     ("no short kernel", {"BLP_NO_SHORT_KERNEL": "1"}),
+    ("grouped business", {"BLP_NO_WSET": "1"}),
 ])
 def test_debug_build_no_violations(gpu, mode, extra):
     r = _run(mode, extra)
@@ -85,7 +86,8 @@ def test_debug_build_reports_overfilled_hash_table(gpu):
     ("g_yb", {}),
     ("cn", {}),
     ("lq", {"BLP_SPLIT": "3"}),
-    ("wedge", {}),
+    ("wedge", {"BLP_NO_WSET": "1"}),  # the grouped short-row scorer's wedge rows
+    ("wset", {}),  # the wedge-set scorer's sets (k_score_wset, the business side by default)
 ])
 def test_null_launch_pointer_is_refused(gpu, field, extra):
     """A launch path's device pointer nulled (BLP_DEBUG_NULL, debug build only) is refused on the

@@ -4,9 +4,10 @@ passes of similarity.main enqueued as one co-scheduled step (blp_batches_score) 
 bench's timed step runs them, checked bit-exact against the C oracle (the reference algorithm,
 similarity.py:20-106, :108-126). The user pass must take the instance the bench times and
 rooflines: the large block scorer's packed-count variant (k_score<1024, 31744, 896, 8, false,
-true, true>, PKO: one LDS bitmap over the 1M-user universe, counts in the packed word) with its
-co-scheduled CU share; the business pass the three-barrier short-row scorer without Adamic-Adar -- the
-kernels and geometry of the headline number. Marked `gpu`."""
+true, true>, PKO: one LDS bitmap over the 1M-user universe, counts in the packed word); the
+business pass the wedge-set scorer without Adamic-Adar (k_score_wset<false>, round 6: pair by pair
+in caller order against the graph's dense wedge-set index, after the user pass) -- the kernels and
+geometry of the headline number. Marked `gpu`."""
 import os
 
 import numpy as np
@@ -34,7 +35,7 @@ def test_config2_slice_both_sides_coscheduled(gpu, create):
     plan = ub.plan()
     assert plan["block"] == 1024 and plan["chunks"] == 1 and plan["hi"] - plan["lo"] > 31744 * 16, plan
     assert ub.kernel(7) == "k_score<1024, 31744, 896, 8, false, true, true>", ub.kernel(7)  # bench.py's roofline kernel
-    assert bb.kernel(3) == "k_score_short<false>", bb.kernel(3)
+    assert bb.kernel(3) == "k_score_wset<false>", bb.kernel(3)  # the business pass on the graph's wedge sets
     G.score_batches([(ub, 7), (bb, 3)])  # the bench's step: both passes concurrent, user pass on its CU share
     got_u, got_b = ub.fetch(7), bb.fetch(3)
     ids, oa, ob = dense_edges(a, b)

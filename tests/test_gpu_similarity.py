@@ -153,6 +153,9 @@ def test_general_graph_exact_distance(gpu):
     {"BLP_SPLIT": "2", "BLP_SPLIT_BIG": "1", "BLP_HASH_WORK": "100000"},  # every source on the hash-set scorer (knob clamped to HT - 1)
     {"BLP_SPLIT": "4", "BLP_HASH_WORK": "400"},          # ... beside the 64 KiB chunk scorer
     {"BLP_NO_WEDGE": "1", "BLP_HEAVY_WORK": "7"},       # short-row batches on the segment scorer (k_score SHORT)
+    {"BLP_NO_WSET": "1"},                               # business side on the grouped short-row scorer (k_score_short)
+    {"BLP_NO_WSET": "1", "BLP_HEAVY_WORK": "7"},        # ... with wedge slices of heavy sources
+    {"BLP_WSET_MB": "0"},                               # wedge-set index over budget: the grouped path
     {"BLP_ITEM_NB": "1"},                               # one interleaved bucket (or the fewest that keep <= 1024 keys)
     {"BLP_ITEM_NB": "4", "BLP_GROUP_NBLK": "3"},        # few buckets, few scatter workgroups
     {"BLP_LPT": "0"},                                   # run-grouped sources queued in id order (default: largest work first)
@@ -622,3 +625,41 @@ def test_prewarm_concurrent_with_batches(gpu):
     for t in th:
         t.join(timeout=120)
     assert not any(t.is_alive() for t in th) and not errs, errs
+
+
+@pytest.mark.parametrize("mask", [3, 7])
+def test_wedge_set_path_equals_grouped_path(gpu, mask, monkeypatch):
+    """The business side on the graph's dense wedge-set index (k_score_wset, round 6: CN(x, y) =
+    #{c in N(y), c != x : x in N(N(c))}, pair by pair in caller order, no grouping) gives the
+    grouped short-row scorer's values bit for bit, and the C oracle's (similarity.py:63-106):
+    pairs grouped by user and shuffled, repeated pairs, and pairs whose user reviewed the business
+    (c == x in N(y) must not count). mask 7 is the fix_adamic business pass (exact AA words)."""
+    rng = np.random.default_rng(5)
+    a, b = bipartite_edges(rng, 9000, 700, 70000)
+    G = blp.DeviceGraph(a, b)
+    nu = G.n - len(np.unique(b))
+    users = np.repeat(rng.choice(nu, 150, replace=False), 40).astype(np.int32)
+    bus = rng.integers(nu, G.n, len(users)).astype(np.int32)
+    rp, ci = G.row_ptr, G.col_idx
+    own = np.array([ci[rp[u]] for u in users[:200:10]], np.int32)  # businesses the user reviewed
+    users = np.concatenate([users, users[:200:10], users[:50]])
+    bus = np.concatenate([bus, own, bus[:50]])
+    for order in ("grouped", "shuffled"):
+        if order == "shuffled":
+            p = rng.permutation(len(users))
+            users, bus = users[p], bus[p]
+        got = G.batch(bus, users)
+        assert got.kernel(mask) == "k_score_wset<%s>" % ("true" if mask & 4 else "false"), got.kernel(mask)
+        got.score(mask)
+        rw = got.fetch(mask)
+        monkeypatch.setenv("BLP_NO_WSET", "1")
+        ref = G.batch(bus, users)
+        monkeypatch.delenv("BLP_NO_WSET")
+        assert ref.kernel(mask).startswith("k_score_short"), ref.kernel(mask)
+        ref.score(mask)
+        rs = ref.fetch(mask)
+        for k in ("cn", "jaccard") + (("adamic",) if mask & 4 else ()):
+            np.testing.assert_array_equal(rw[k], rs[k], err_msg=k)
+        got.close()
+        ref.close()
+    _check_against_oracle(a, b, bus, users, mask)
