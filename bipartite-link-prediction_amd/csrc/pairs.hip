@@ -822,7 +822,7 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_run_write(const int32_t* __restr
   for (int q = 0; q < PT; ++q) {
     const int64_t i = t0 + q * SCAN_BLOCK + threadIdx.x;
     if (i < np) {
-      g_out[i] = (int32_t)i;
+      if (g_out) g_out[i] = (int32_t)i;
       g_yb[i] = st[q];
       g_yl[i] = (int32_t)(en[q] - st[q]);
       if (g_y) g_y[i] = yv[q];
@@ -1854,7 +1854,7 @@ struct ScoreArgs {
   const int32_t* off;      // per node: first grouped position of its pairs
   const int32_t* cnt;      // per node: number of pairs with that source
   const int32_t* active;   // active sources
-  const int32_t* g_out;    // grouped position -> caller index
+  const int32_t* g_out;    // grouped position -> caller index (null: the identity, run-grouped lists)
   const int64_t* g_yb;     // grouped position -> start of N(y) in ci
   const int32_t* g_yl;     // grouped position -> |N(y)|
   const int32_t* hot_idx;     // per node: dense-row number or -1 (null: no dense rows)
@@ -1883,6 +1883,12 @@ struct ScoreArgs {
   int64_t n_hot, hot_vecs;      // dense rows, their pool's vectors (BLP_DEBUG bounds)
   int lq_wgs;                   // workgroups d_lq was sized for (BLP_DEBUG bound)
 };
+
+// the caller index of grouped pair gp: g_out, or gp itself when the batch's grouped order is its
+// caller order (a list grouped by source: run-head grouping writes no g_out)
+__device__ __attribute__((always_inline)) inline int gout(const ScoreArgs& a, int64_t gp) {
+  return a.g_out ? a.g_out[gp] : (int)gp;
+}
 
 // N(y)'s row [st, st + len) of grouped pair gp, from the grouped metadata g_yb / g_yl.
 __device__ __attribute__((always_inline)) inline void pair_row(const ScoreArgs& a, int gp, int64_t& st, int& len) {
@@ -2036,7 +2042,7 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
       if (PF && nchunks == 1 && (int)threadIdx.x < min(SEG, pcnt)) {
         const int gp = pbeg + threadIdx.x;
         pair_row(a, gp, pf_start, pf_len);
-        pf_out = a.g_out[gp];
+        pf_out = gout(a, gp);
       }
       PROF(1)
 
@@ -2205,7 +2211,7 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
             int64_t st;
             pair_row(a, gp, st, len);
             s_start[threadIdx.x] = st;
-            pout = a.g_out[gp];  // used after the scan: its latency hides behind it
+            pout = gout(a, gp);  // used after the scan: its latency hides behind it
             if (!PKO) s_cn[threadIdx.x] = 0;
             if (SAA) {
               s_aa[2 * threadIdx.x] = 0;
@@ -2229,7 +2235,7 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
             const int gp = pbeg + sb + SEG + threadIdx.x;
             pf_start = a.g_yb[gp];
             pf_len = a.g_yl[gp];
-            pf_out = a.g_out[gp];
+            pf_out = gout(a, gp);
           }
           PROF(6)
           if (SHORT || (a.short_rows & 2)) {
@@ -2385,7 +2391,7 @@ __global__ __launch_bounds__(256, BLP_SHORT_MINB) void k_score_short(ScoreArgs a
       const bool pairs_ok = PS_OK(a.misc, pbeg >= 0 && (int64_t)pbeg + pcnt <= a.np, 3, (int64_t)pbeg + pcnt, a.np);
       if (pairs_ok && (int)threadIdx.x < pcnt) {
         pair_row(a, pbeg + threadIdx.x, pf_start, pf_len);
-        pf_out = a.g_out[pbeg + threadIdx.x];
+        pf_out = gout(a, pbeg + threadIdx.x);
       }
       PROF(1)
       // P1: the pre-built set, counted while copied, or a zeroed bitmap
@@ -2450,7 +2456,7 @@ __global__ __launch_bounds__(256, BLP_SHORT_MINB) void k_score_short(ScoreArgs a
         int len = pf_len, pout = pf_out;
         if (p != (int)threadIdx.x) {
           pair_row(a, pbeg + p, st, len);
-          pout = a.g_out[pbeg + p];
+          pout = gout(a, pbeg + p);
         }
         if (!PS_OK(a.misc, pout >= 0 && pout < a.np, 4, pout, a.np)) continue;
         if (!PS_OK(a.misc, st >= 0 && st + len <= a.nnz + blp::CI_PAD, 10, st + len, a.nnz)) continue;
@@ -2515,6 +2521,8 @@ struct WsetArgs {
 };
 
 template <bool SAA>
+// (Two pairs per thread, their chains in flight together: 96 VGPRs, 5 waves per SIMD, and the
+// step 1.735-1.741 against 1.716-1.722 ms, r06_check4.)
 __global__ __launch_bounds__(256) void k_score_wset(ScoreArgs a, WsetArgs w) {
   __shared__ long long s_wtab[SAA ? 256 : 1];
   if (SAA && a.wtab)
@@ -2655,7 +2663,7 @@ __global__ __launch_bounds__(BLOCK) void k_score_global(ScoreArgs a, uint32_t* g
           mp_scan<BLOCK, K, false>(a.cw, a.idmask, a.idbits, a.aaw, a.wtab, s_start, s_off, ns, c0, width, bm, s_cn, s_aa, threadIdx.x);
         __syncthreads();
         for (int t = threadIdx.x; t < ns; t += BLOCK) {
-          const int p = a.g_out[pbeg + sb + t];
+          const int p = gout(a, pbeg + sb + t);
           const unsigned c = s_cn[t];
           a.cn[p] = c;
           if (want_a) a.aa[p] = blp::aa_value(s_aa[2 * t], s_aa[2 * t + 1]);
@@ -3056,7 +3064,7 @@ __global__ __launch_bounds__(256) void k_split_combine(ScoreArgs a, int C, const
       const int64_t gp = pbeg + t;
       const unsigned long long lo = want_a ? paa[2 * gp] : 0ull, hi = want_a ? paa[2 * gp + 1] : 0ull;
       const unsigned cn = pk24 ? (unsigned)(hi & ((1u << SPLIT_CN_BITS) - 1)) : pcn[gp];
-      const int p = a.g_out[gp];
+      const int p = gout(a, gp);
       if (!PS_OK(a.misc, p >= 0 && p < a.np, 4, p, a.np)) continue;
       a.cn[p] = cn;
       if (want_a) a.aa[p] = pk24 ? blp::aa_value(lo, hi >> SPLIT_CN_BITS, 52) : blp::aa_value(lo, hi);
@@ -3171,7 +3179,7 @@ __global__ __launch_bounds__(BLOCK) void k_score_hash(ScoreArgs a) {
     if ((int)threadIdx.x < pcnt) {
       st0 = a.g_yb[pbeg + threadIdx.x];
       len0 = a.g_yl[pbeg + threadIdx.x];
-      p0 = a.g_out[pbeg + threadIdx.x];
+      p0 = gout(a, pbeg + threadIdx.x);
     }
     for (int i = threadIdx.x; i < HT / 4; i += BLOCK) reinterpret_cast<uint4*>(tab)[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
     __syncthreads();
@@ -3247,7 +3255,7 @@ __global__ __launch_bounds__(BLOCK) void k_score_hash(ScoreArgs a) {
       const int64_t st = first ? st0 : a.g_yb[gp];
       int len = first ? len0 : a.g_yl[gp];
       if (!PS_OK(a.misc, st >= 0 && len >= 0 && st + len <= a.nnz, 10, st + len, a.nnz)) len = 0;
-      const int p = first ? p0 : a.g_out[gp];
+      const int p = first ? p0 : gout(a, gp);
       if (!PS_OK(a.misc, p >= 0 && p < a.np, 4, p, a.np)) continue;
       unsigned c = 0;
       unsigned long long acc = 0, acch = 0;
@@ -3538,7 +3546,7 @@ static int launch_pointers(const blp_graph* g, const blp_batch* b, ScoreArgs& a,
   need(a.off, "source offsets");
   need(a.cnt, "source counts");
   need(a.active, "active sources");
-  need(a.g_out, "grouped caller index");
+  if (!b->runs) need(a.g_out, "grouped caller index");
   need(a.g_yb, "grouped row starts");
   need(a.g_yl, "grouped row lengths");
   need(a.misc, "batch counters");
@@ -4265,7 +4273,7 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
     hipLaunchKernelGGL(k_run_count, dim3((unsigned)tiles), dim3(SCAN_BLOCK), 0, b->stream, b->d_x, np, rtile);
     hipLaunchKernelGGL(k_scan_mid, dim3(1), dim3(SCAN_BLOCK), 0, b->stream, rtile, tiles, &b->d_misc->n_active);
     hipLaunchKernelGGL(k_run_write, dim3((unsigned)tiles), dim3(SCAN_BLOCK), 0, b->stream, b->d_x, b->d_y, np, g->d_rp,
-                       rtile, b->active.as<int32_t>(), b->off.as<int32_t>(), b->d_gout, b->d_gyb, b->d_gyl,
+                       rtile, b->active.as<int32_t>(), b->off.as<int32_t>(), (int32_t*)nullptr, b->d_gyb, b->d_gyl,
                        b->d_gy);
     hipLaunchKernelGGL(k_run_cnt, dim3(1024), dim3(256), 0, b->stream, b->active.as<int32_t>(), &b->d_misc->n_active,
                        np, b->off.as<int32_t>(), b->cnt.as<int32_t>(), b->d_rank, (int32_t)b->xlo, b->d_lpt);
@@ -4411,7 +4419,7 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   a.off = b->off.as<int32_t>();
   a.cnt = b->cnt.as<int32_t>();
   a.active = b->d_lpt ? b->d_lpt : b->active.as<int32_t>();  // BLP_LPT: the largest-first queue
-  a.g_out = b->d_gout;
+  a.g_out = b->runs ? nullptr : b->d_gout;  // run-grouped: grouped order is caller order
   a.g_yb = b->d_gyb;
   a.g_yl = b->d_gyl;
   a.hot_idx = b->use_hot ? g->d_hot_idx : nullptr;
