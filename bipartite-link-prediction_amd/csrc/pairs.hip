@@ -2522,7 +2522,10 @@ struct WsetArgs {
 
 template <bool SAA>
 // (Two pairs per thread, their chains in flight together: 96 VGPRs, 5 waves per SIMD, and the
-// step 1.735-1.741 against 1.716-1.722 ms, r06_check4.)
+// step 1.735-1.741 against 1.716-1.722 ms, r06_check4. Blocks on contiguous pair ranges, each
+// thread keeping its user's row in registers across its consecutive pairs: the kernel 0.242 ->
+// 0.266 ms, step 1.72 -> 1.73 ms, r06_ab5 -- ~3x more users in flight per XCD, so their sets
+// crowd the L2; the grid-stride window keeps one XCD on ~90 consecutive users.)
 __global__ __launch_bounds__(256) void k_score_wset(ScoreArgs a, WsetArgs w) {
   __shared__ long long s_wtab[SAA ? 256 : 1];
   if (SAA && a.wtab)
