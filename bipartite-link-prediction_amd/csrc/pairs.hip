@@ -4575,7 +4575,9 @@ int blp_batches_score(blp_graph* g, int n, blp_batch* const* bs, const uint32_t*
   // pass, which then holds no CU share: the light launch runs while the large pass groups its
   // pairs, and the large scorer takes the whole chip after it (config 2: 1.715-1.717 ms per step;
   // after the large pass on its stream's completion, BLP_WSET_SERIAL=1: 1.761-1.764 ms; with the
-  // large pass held to 240 / 224 / 208 / 192 CUs: 1.80 / 1.85 / 1.96 / 2.05-2.07 ms, r06_check3)
+  // large pass held to 240 / 224 / 208 / 192 CUs: 1.80 / 1.85 / 1.96 / 2.05-2.07 ms, r06_check3;
+  // gated on the large pass's grouping so its scorer is dispatched first: 1.76-1.77 ms, the light
+  // launch's blocks then interleave with the scorer's workgroups, 1.43 -> 1.61 ms, r06_ab6)
   static const bool wset_serial = getenv("BLP_WSET_SERIAL") && atoi(getenv("BLP_WSET_SERIAL")) > 0;
   int share = g->n_cu;
   if (t_large > 0.0 && t_other > 0.0) {
