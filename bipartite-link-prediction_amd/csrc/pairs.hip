@@ -4228,6 +4228,9 @@ static int score_wset(blp_graph* g, blp_batch* b, uint32_t mask) {
     }
     const int cus = b->cus > 0 ? b->cus : g->n_cu;
     const int64_t want = (np + 255) / 256;
+    // 8 blocks per CU, all resident (fewer keep fewer users' sets in an XCD's L2 at once, and lose
+    // more in parallelism: 6 / 4 / 3 / 2 per CU gave 1.72-1.74 / 1.74-1.76 / 1.75-1.76 / 1.74-1.75 ms
+    // against 1.713-1.716, r06_ab7)
     const int grid = (int)std::max<int64_t>(8, std::min<int64_t>(want, (int64_t)cus * 8) / 8 * 8);
     if (mask & BLP_ADAMIC)
       hipLaunchKernelGGL(k_score_wset<true>, dim3(grid), dim3(256), 0, b->stream, a, w);
