@@ -663,3 +663,30 @@ def test_wedge_set_path_equals_grouped_path(gpu, mask, monkeypatch):
         got.close()
         ref.close()
     _check_against_oracle(a, b, bus, users, mask)
+
+
+@pytest.mark.parametrize("extra", ["user-user", "business-business"])
+def test_wedge_set_path_refuses_non_bipartite(gpu, extra):
+    """The wedge-set path rests on N(x) lying outside the sets' range (distance 1 never in the
+    universe) -- a bipartite graph. A review graph with a few user-user or business-business
+    edges puts distance-2 users, or a business's business neighbours, in play; the batch must
+    take the grouped path, and its scores must equal the C oracle's (similarity.py:63-106)."""
+    rng = np.random.default_rng(8)
+    a, b = bipartite_edges(rng, 5000, 400, 30000)
+    users, bus = np.unique(a), np.unique(b)
+    k = 40
+    if extra == "user-user":
+        ea, eb = rng.choice(users, k), rng.choice(users, k)
+    else:
+        ea, eb = rng.choice(bus, k), rng.choice(bus, k)
+    a2, b2 = np.concatenate([a, ea]), np.concatenate([b, eb])
+    G = blp.DeviceGraph(a2, b2)
+    dense = {int(v): i for i, v in enumerate(G.node_ids)}  # original id -> dense id
+    u_src = np.array([dense[int(v)] for v in rng.choice(users, 80, replace=False)], np.int32)
+    x = np.repeat(u_src, 25).astype(np.int32)
+    y = np.array([dense[int(v)] for v in rng.choice(bus, len(x))], np.int32)
+    bt = G.batch(y, x)
+    assert not bt.kernel(3).startswith("k_score_wset"), bt.kernel(3)
+    bt.close()
+    _check_against_oracle(a2, b2, y, x, 3)
+    _check_against_oracle(a2, b2, y, x, 7)
