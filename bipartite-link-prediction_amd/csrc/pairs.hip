@@ -2976,27 +2976,50 @@ __global__ __launch_bounds__(BLOCK, CAP_WORDS > 16384 ? 4 : 8) void k_score_spli
           }
         }
         if (len > 0 && len <= short_max) {
-          int sv[SHORT_PART];
+          int sv[SHORT_PART] = {};  // ids past len stay 0 (masked by len below)
           row_part(a.cw, st, len, 0, sv);
-          uint32_t cnt = 0;
-          unsigned long long lo = 0, hi40 = 0;
+          // branch-free phases (as rc_scan): every bitmap word (and code weight) of the part is read
+          // before the first is used -- one LDS round trip per slice, not one per id -- and the
+          // weights come from the LDS code table; code-0 hits then gather aaw (rare)
+          uint32_t rr[SHORT_PART], wd[SHORT_PART];
 #pragma unroll
           for (int k = 0; k < SHORT_PART; ++k) {
-            if (k < len) {
-              const uint32_t r = in_chunk(sv[k], keep, c0u);
-              const uint32_t word = bm[(r < wu ? r : 0u) >> 5];
-              if (r < wu && ((word >> (r & 31)) & 1u)) {
-                ++cnt;
-                if (want_a) {
-                  const uint32_t code = ((uint32_t)sv[k] >> a.idbits) & 255u;
-                  const unsigned long long w = (unsigned long long)(code ? wtab[code] : a.aaw[sv[k] & a.idmask]);
+            const uint32_t r = in_chunk(sv[k], keep, c0u);
+            rr[k] = (k < len && r < wu) ? r : 0u;
+          }
+#pragma unroll
+          for (int k = 0; k < SHORT_PART; ++k) wd[k] = bm[rr[k] >> 5];
+          uint32_t hm = 0;
+#pragma unroll
+          for (int k = 0; k < SHORT_PART; ++k) {
+            const uint32_t r = in_chunk(sv[k], keep, c0u);
+            hm |= ((k < len && r < wu) ? (wd[k] >> (rr[k] & 31)) & 1u : 0u) << k;
+          }
+          unsigned long long lo = 0, hi40 = 0;
+          if (want_a && hm) {
+            long long wt[SHORT_PART];
+#pragma unroll
+            for (int k = 0; k < SHORT_PART; ++k) wt[k] = wtab[((uint32_t)sv[k] >> a.idbits) & 255u];
+            uint32_t esc = 0;
+#pragma unroll
+            for (int k = 0; k < SHORT_PART; ++k) {
+              const bool h = (hm >> k) & 1u;
+              const unsigned long long w = h ? (unsigned long long)wt[k] : 0ull;
+              lo += w;
+              hi40 += w >> PK_HS;
+              esc |= (h && ((((uint32_t)sv[k] >> a.idbits) & 255u) == 0u)) ? 1u << k : 0u;
+            }
+            if (esc) {
+#pragma unroll
+              for (int k = 0; k < SHORT_PART; ++k)
+                if ((esc >> k) & 1u) {
+                  const unsigned long long w = (unsigned long long)a.aaw[sv[k] & a.idmask];
                   lo += w;
                   hi40 += w >> PK_HS;
                 }
-              }
             }
           }
-          emit(pbeg + q, lo, (hi40 << PK_CN_BITS) | cnt);
+          emit(pbeg + q, lo, (hi40 << PK_CN_BITS) | (uint32_t)__popc(hm));
         } else if (len > short_max) {
           const int slot = atomicAdd(&s_nl, 1);  // < SPLIT_LQ: a round holds NW * SPLIT_ROUND * 64 pairs
           if (PS_OK(a.misc, slot < SPLIT_LQ, 5, slot, SPLIT_LQ))
