@@ -1043,6 +1043,34 @@ __device__ __attribute__((always_inline)) inline void mp_fetch(const int32_t* __
 // idmask | sign bit, so -1 maps to >= 2^31 - c0 > width (c0 <= idmask, width < 2^31).
 __device__ inline uint32_t in_chunk(int v, uint32_t keep, uint32_t c0u) { return ((uint32_t)v & keep) - c0u; }
 
+// Exact AA terms of the hit ids e[j] (bit j of hm): the code weights from the LDS code table
+// (wtab[0] = 0), then the code-0 hits' per-node weights from the global table in a loop of their
+// own. (A per-id `code ? wtab[code] : aaw[id]` compiles to one flat load of a selected LDS-or-
+// global address, which waits on both memory counters at every hit.)
+template <int N>
+__device__ __attribute__((always_inline)) inline void aa_terms(const int* e, uint32_t hm, int idbits, uint32_t idmask,
+                                                               const long long* wtab, const long long* __restrict__ aaw,
+                                                               unsigned long long& acc, uint32_t& acch) {
+  uint32_t esc = 0;
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    const uint32_t code = ((uint32_t)e[j] >> idbits) & 255u;
+    const unsigned long long w = ((hm >> j) & 1u) ? (unsigned long long)wtab[code] : 0ull;
+    acc += w;
+    acch += (uint32_t)(w >> 32);
+    esc |= (((hm >> j) & 1u) && code == 0u) ? 1u << j : 0u;
+  }
+  if (esc) {
+#pragma unroll
+    for (int j = 0; j < N; ++j)
+      if ((esc >> j) & 1u) {
+        const unsigned long long w = (unsigned long long)aaw[e[j] & idmask];
+        acc += w;
+        acch += (uint32_t)(w >> 32);
+      }
+  }
+}
+
 // Exact Adamic-Adar accumulation (blp_internal.h): a term W adds to the wrapping low word and
 // its high half to the exact high word. LDS accumulators are interleaved: s_aa[2 t] = lo,
 // s_aa[2 t + 1] = hi for segment t.
@@ -1337,8 +1365,9 @@ __device__ __attribute__((always_inline)) inline void pp_scan(const int32_t* __r
     if (r < wu && ((bm[r >> 5] >> (r & 31)) & 1u)) {
       atomicAdd(&s_cn[seg], 1u);
       if (AA) {
-        const uint32_t code = ((uint32_t)v >> idbits) & 255u;
-        const unsigned long long w = (unsigned long long)(code ? wtab[code] : aaw[v & idmask]);
+        unsigned long long w = 0;
+        uint32_t wh = 0;
+        aa_terms<1>(&v, 1u, idbits, idmask, wtab, aaw, w, wh);
         aa_push(s_aa, seg, w, w >> 32);
       }
     }
@@ -2558,16 +2587,15 @@ __global__ __launch_bounds__(256) void k_score_wset(ScoreArgs a, WsetArgs w) {
         const uint32_t r = id - lou;
         wd[j] = (h + j < len && r < span && id != (uint32_t)x) ? col[(int64_t)r * w.words] : 0u;
       }
+      if constexpr (SAA) {
+        uint32_t hm = 0;
 #pragma unroll
-      for (int j = 0; j < SHORT_PART; ++j) {
-        const bool hit = (wd[j] >> xb) & 1u;
-        c += hit ? 1u : 0u;
-        if (SAA && want_a && hit) {
-          const uint32_t code = ((uint32_t)e[j] >> a.idbits) & 255u;
-          const unsigned long long wt = (unsigned long long)(code ? s_wtab[code] : a.aaw[e[j] & a.idmask]);
-          acc += wt;
-          acch += (uint32_t)(wt >> 32);
-        }
+        for (int j = 0; j < SHORT_PART; ++j) hm |= ((wd[j] >> xb) & 1u) << j;
+        c += (unsigned)__popc(hm);
+        if (want_a && hm) aa_terms<SHORT_PART>(e, hm, a.idbits, a.idmask, s_wtab, a.aaw, acc, acch);
+      } else {
+#pragma unroll
+        for (int j = 0; j < SHORT_PART; ++j) c += (wd[j] >> xb) & 1u;
       }
     }
     a.cn[i] = c;
