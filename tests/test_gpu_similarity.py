@@ -139,6 +139,8 @@ def test_general_graph_exact_distance(gpu):
     {"BLP_WCODES": "3"},                                # coded and gathered weights mixed
     {"BLP_NO_WCODES": "1"},                             # scorers on the plain id stream
     {"BLP_WCODES": "3", "BLP_SPLIT": "3"},
+    {"BLP_WCODES": "3", "BLP_SPLIT": "3", "BLP_SPLIT_BIG": "1", "BLP_NO_HASH": "1"},  # short slices: code-0 hits gather aaw
+    {"BLP_NO_WCODES": "1", "BLP_SPLIT": "3", "BLP_SPLIT_BIG": "1", "BLP_NO_HASH": "1"},  # ... every hit gathers (plain ids)
     {"BLP_WCODES": "3", "BLP_FORCE_GLOBAL": "1"},
     {"BLP_WCODES": "3", "BLP_HEAVY_WORK": "50", "BLP_HOT_MIN": "8"},
     {"BLP_NO_WEDGE": "1"},                              # short-row build from CSR, not wedge rows
