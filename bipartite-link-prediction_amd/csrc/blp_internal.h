@@ -126,6 +126,10 @@ struct KernelTimer {
   std::vector<hipEvent_t> free_events;
   double total_ms = 0.0;
   int64_t launches = 0;
+  // a batch's timer also counts into its graph's timer of the same kind (under mirror_mu), so
+  // the graph totals need no timing events of their own on the batch's stream
+  KernelTimer* mirror = nullptr;
+  std::mutex* mirror_mu = nullptr;
 };
 
 }  // namespace blp
@@ -206,6 +210,10 @@ struct blp_graph {
   const int32_t* hci = nullptr;  // null until first needed when the graph was created without it (host_col_idx)
   std::mutex mirror_mu;          // held while host_col_idx fetches the column mirror
   blp::KernelTimer timers[blp::K_COUNT];
+  // the live batches' score / group timers (their pending events are collected into timers[]
+  // when the graph's totals are read) and the lock of both
+  std::vector<blp::KernelTimer*> live_timers;
+  std::mutex timer_mu;
 };
 
 namespace blp {

@@ -298,23 +298,39 @@ int timer_end(KernelTimer& t, hipStream_t s, hipEvent_t start) {
   t.pending_start.push_back(start);
   t.pending_stop.push_back(stop);
   t.launches++;
+  if (t.mirror) {
+    std::lock_guard<std::mutex> lk(*t.mirror_mu);
+    t.mirror->launches++;
+  }
   // keep the pending list bounded: fold finished pairs in as we go
   if (t.pending_stop.size() > 4096) return timer_collect(t);
   return BLP_OK;
 }
 
 int timer_collect(KernelTimer& t) {
-  for (size_t i = 0; i < t.pending_stop.size(); ++i) {
-    BLP_HIP(hipEventSynchronize(t.pending_stop[i]));
+  double added = 0.0;
+  int rc = BLP_OK;
+  size_t i = 0;
+  for (; i < t.pending_stop.size(); ++i) {
+    hipError_t e = hipEventSynchronize(t.pending_stop[i]);
     float ms = 0.f;
-    BLP_HIP(hipEventElapsedTime(&ms, t.pending_start[i], t.pending_stop[i]));
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, t.pending_start[i], t.pending_stop[i]);
+    if (e != hipSuccess) {
+      rc = hip_fail(e, "timer_collect", __FILE__, __LINE__);
+      break;
+    }
     t.total_ms += ms;
+    added += ms;
     t.free_events.push_back(t.pending_start[i]);
     t.free_events.push_back(t.pending_stop[i]);
   }
-  t.pending_start.clear();
-  t.pending_stop.clear();
-  return BLP_OK;
+  t.pending_start.erase(t.pending_start.begin(), t.pending_start.begin() + i);
+  t.pending_stop.erase(t.pending_stop.begin(), t.pending_stop.begin() + i);
+  if (t.mirror && added != 0.0) {
+    std::lock_guard<std::mutex> lk(*t.mirror_mu);
+    t.mirror->total_ms += added;
+  }
+  return rc;
 }
 
 void timer_release(KernelTimer& t) {
@@ -331,6 +347,15 @@ int timer_begin(blp_graph* g, int k, hipEvent_t* start) { return timer_begin(g->
 int timer_end(blp_graph* g, int k, hipEvent_t start) { return timer_end(g->timers[k], g->stream, start); }
 
 int timers_collect(blp_graph* g) {
+  std::vector<KernelTimer*> live;
+  {
+    std::lock_guard<std::mutex> lk(g->timer_mu);
+    live = g->live_timers;
+  }
+  for (KernelTimer* t : live) {  // (the batches' own calls are not concurrent with this one)
+    int rc = timer_collect(*t);
+    if (rc) return rc;
+  }
   for (int k = 0; k < K_COUNT; ++k) {
     int rc = timer_collect(g->timers[k]);
     if (rc) return rc;

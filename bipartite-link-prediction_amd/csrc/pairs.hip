@@ -3665,6 +3665,15 @@ static int batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_
   const Knobs kn = read_knobs();
   blp_batch* b = new blp_batch();
   b->g = g;
+  // the batch's timers count into the graph's score / group totals (blp_stats_get)
+  b->t_score.mirror = &g->timers[K_SCORE];
+  b->t_group.mirror = &g->timers[K_GROUP];
+  b->t_score.mirror_mu = b->t_group.mirror_mu = &g->timer_mu;
+  {
+    std::lock_guard<std::mutex> lk(g->timer_mu);
+    g->live_timers.push_back(&b->t_score);
+    g->live_timers.push_back(&b->t_group);
+  }
   b->n_pairs = n_pairs;
   b->kn = kn;
   auto bail = [&](int rc) {
@@ -4154,6 +4163,13 @@ int blp_batch_destroy(blp_batch* b) {
   if (b->g) (void)hipSetDevice(b->g->device);
   if (b->g && b->g->stream) (void)hipStreamSynchronize(b->g->stream);
   if (b->stream) (void)hipStreamSynchronize(b->stream);
+  if (b->g) {  // the batch's times join the graph's totals before its events go
+    (void)timer_collect(b->t_score);
+    (void)timer_collect(b->t_group);
+    std::lock_guard<std::mutex> lk(b->g->timer_mu);
+    auto& lt = b->g->live_timers;
+    lt.erase(std::remove_if(lt.begin(), lt.end(), [&](KernelTimer* t) { return t == &b->t_score || t == &b->t_group; }), lt.end());
+  }
   timer_release(b->t_score);
   timer_release(b->t_group);
   b->cnt.release();
@@ -4235,8 +4251,7 @@ static int score_wset(blp_graph* g, blp_batch* b, uint32_t mask) {
   int rc;
   const int64_t np = b->n_pairs;
   BLP_HIP(hipMemsetAsync(b->d_misc, 0, offsetof(Misc, dbg), b->stream));
-  hipEvent_t t1, bt1;
-  if ((rc = timer_begin(g->timers[K_SCORE], b->stream, &t1))) return rc;
+  hipEvent_t bt1;
   if ((rc = timer_begin(b->t_score, b->stream, &bt1))) return rc;
   if (np) {
     ScoreArgs a{};
@@ -4293,7 +4308,7 @@ static int score_wset(blp_graph* g, blp_batch* b, uint32_t mask) {
     BLP_HIP(hipGetLastError());
   }
   if ((rc = timer_end(b->t_score, b->stream, bt1))) return rc;
-  return timer_end(g->timers[K_SCORE], b->stream, t1);
+  return BLP_OK;
 }
 
 int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
@@ -4323,8 +4338,7 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   int32_t* abase = bact + b->nb;
   int4* tmp = reinterpret_cast<int4*>((reinterpret_cast<uintptr_t>(abase + b->nb) + 15) & ~uintptr_t(15));
   if (b->wset_pool) return score_wset(g, b, mask);
-  hipEvent_t t0, bt0;
-  if ((rc = timer_begin(g->timers[K_GROUP], b->stream, &t0))) return rc;
+  hipEvent_t bt0;
   if ((rc = timer_begin(b->t_group, b->stream, &bt0))) return rc;
   BLP_HIP(hipMemsetAsync(b->d_misc, 0, offsetof(Misc, dbg), b->stream));  // the debug record persists to fetch
   if (np && b->runs) {
@@ -4445,10 +4459,8 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   }
   BLP_HIP(hipGetLastError());
   if ((rc = timer_end(b->t_group, b->stream, bt0))) return rc;
-  if ((rc = timer_end(g->timers[K_GROUP], b->stream, t0))) return rc;
 
-  hipEvent_t t1, bt1;
-  if ((rc = timer_begin(g->timers[K_SCORE], b->stream, &t1))) return rc;
+  hipEvent_t bt1;
   if ((rc = timer_begin(b->t_score, b->stream, &bt1))) return rc;
   if (b->n_heavy) {
     BLP_HIP(hipMemsetAsync(b->d_heavy_bm, 0, 4 * b->hb_words * b->n_heavy, b->stream));
@@ -4597,7 +4609,7 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
     if (rc) return rc;
   }
   if ((rc = timer_end(b->t_score, b->stream, bt1))) return rc;
-  return timer_end(g->timers[K_SCORE], b->stream, t1);
+  return BLP_OK;
 }
 
 // Several passes of one step enqueued together (similarity.main: the user and the business

@@ -274,6 +274,53 @@ def test_batch_repeat_is_deterministic(gpu):
     assert launches == 4 and ms > 0
 
 
+def test_graph_score_totals_follow_the_batch_timers(gpu):
+    # the graph's score / group totals are the batches' own timers (no timing events of their
+    # own): launches and milliseconds add up, a destroyed batch's times stay in the totals, and
+    # batches scored from two host threads at once are each counted
+    import threading
+
+    rng = np.random.default_rng(5)
+    a, b = bipartite_edges(rng, 20000, 1000, 100000)
+    G = blp.DeviceGraph(a, b)
+    nu = G.n - len(np.unique(b))
+    x = np.repeat(rng.choice(nu, 100, replace=False), 50).astype(np.int32)
+    y = rng.integers(nu, G.n, len(x)).astype(np.int32)
+    G.stats_reset()
+    bx, by = G.batch(x, y), G.batch(y, x)
+    for _ in range(2):
+        bx.score(7)
+    by.score(3)
+    bx.fetch(7)
+    by.fetch(3)
+    ms, launches = G.stats(blp._lib.K_SCORE)
+    mx, nx = bx.stats(0)
+    my, ny = by.stats(0)
+    assert (launches, nx, ny) == (3, 2, 1)
+    assert ms == pytest.approx(mx + my, rel=1e-6) and ms > 0
+    gms, gl = G.stats(blp._lib.K_GROUP)
+    assert gl == bx.stats(1)[1] + by.stats(1)[1]
+    by.close()
+    assert G.stats(blp._lib.K_SCORE) == (pytest.approx(ms, rel=1e-6), 3)
+    bz = G.batch(y, x)
+
+    def run(bt, m):
+        for _ in range(5):
+            bt.score(m)
+
+    th = [threading.Thread(target=run, args=(bx, 7)), threading.Thread(target=run, args=(bz, 3))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    bx.fetch(7)
+    bz.fetch(3)
+    assert G.stats(blp._lib.K_SCORE)[1] == 13
+    bx.close()
+    bz.close()
+    assert G.stats(blp._lib.K_SCORE)[1] == 13
+
+
 def test_empty_and_zero_division(gpu):
     G = blp.DeviceGraph(np.array([0, 2]), np.array([1, 3]))
     r = G.score_pairs(np.zeros(0, np.int32), np.zeros(0, np.int32))
