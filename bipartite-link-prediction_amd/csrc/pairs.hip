@@ -778,6 +778,20 @@ __global__ void k_plan_sources(const int32_t* __restrict__ srcs, int64_t ns, con
   }
 }
 
+// ------------------------------------------------------------------ source records
+// Everything the short-row scorer needs about an active source before its first global read of
+// row data, gathered once per step after grouping: one 64-byte record per active source (read
+// with scalar loads) instead of the dependent chain active[s] -> off / cnt / rp / wp / heavy ->
+// ci[rp] (three round trips per source on the latency-bound business side).
+struct SrcRec {
+  int32_t x, pbeg, pcnt, hslot;
+  int64_t xb, xe;  // N(x) = ci[xb, xe)
+  int64_t wb, we;  // wedge row of x, in 16-byte vectors (wb == we: none)
+  int32_t nx_lo, nx_hi;  // first and last id of N(x) (nx_hi < nx_lo: empty)
+  int32_t pad[2];
+};
+static_assert(sizeof(SrcRec) == 64, "one 64-byte record per source");
+
 // ---- grouping of a pair list that arrives already grouped by source (x non-decreasing, as
 // similarity.users walks examples.json: every user's businesses together, similarity.py:
 // 30-32): the runs of equal x ARE the groups, so instead of the bucket sort one pass finds
@@ -785,8 +799,13 @@ __global__ void k_plan_sources(const int32_t* __restrict__ srcs, int64_t ns, con
 __device__ inline bool run_head(const int32_t* __restrict__ x, int64_t i) { return i == 0 || x[i] != x[i - 1]; }
 
 __global__ __launch_bounds__(SCAN_BLOCK) void k_run_count(const int32_t* __restrict__ x, int64_t np,
-                                                          int32_t* __restrict__ tile_cnt) {
+                                                          int32_t* __restrict__ tile_cnt, int32_t* __restrict__ zero,
+                                                          int zero_words) {
   __shared__ int red[SCAN_BLOCK / 64];
+  // block 0 zeroes the batch's counters (Misc up to dbg), which no kernel reads before the next
+  // one in stream order: one launch and one dependency fewer than a memset in front
+  if (blockIdx.x == 0)
+    for (int i = threadIdx.x; i < zero_words; i += SCAN_BLOCK) zero[i] = 0;
   const int64_t base = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)threadIdx.x * SCAN_ITEMS;
   int v = 0;
 #pragma unroll
@@ -852,13 +871,31 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_run_write(const int32_t* __restr
 // lpt in that order for the scorer's queue.
 __global__ void k_run_cnt(const int32_t* __restrict__ active, const int32_t* __restrict__ n_active, int64_t np,
                           const int32_t* __restrict__ off, int32_t* __restrict__ cnt,
-                          const int32_t* __restrict__ rank = nullptr, int32_t xlo = 0, int32_t* __restrict__ lpt = nullptr) {
+                          const int32_t* __restrict__ rank = nullptr, int32_t xlo = 0, int32_t* __restrict__ lpt = nullptr,
+                          SrcRec* __restrict__ rec = nullptr, const int64_t* __restrict__ rp = nullptr,
+                          const int32_t* __restrict__ ci = nullptr, const int32_t* __restrict__ heavy_slot = nullptr) {
   const int na = *n_active;
   for (int a = blockIdx.x * blockDim.x + threadIdx.x; a < na; a += gridDim.x * blockDim.x) {
     const int xa = active[a];
+    const int pb = off[xa];
     const int nxt = a + 1 < na ? off[active[a + 1]] : (int)np;
-    cnt[xa] = nxt - off[xa];
-    if (rank) lpt[rank[xa - xlo]] = xa;
+    cnt[xa] = nxt - pb;
+    const int s = rank ? rank[xa - xlo] : a;  // the source's place in the scorer's queue
+    if (rank) lpt[s] = xa;
+    if (rec) {  // the large scorer's source record (as k_source_records, without a wedge row)
+      SrcRec r;
+      r.x = xa;
+      r.pbeg = pb;
+      r.pcnt = nxt - pb;
+      r.hslot = heavy_slot ? heavy_slot[xa] : -1;
+      r.xb = rp[xa];
+      r.xe = rp[xa + 1];
+      r.wb = r.we = 0;
+      r.nx_lo = r.xe > r.xb ? ci[r.xb] : 0;
+      r.nx_hi = r.xe > r.xb ? ci[r.xe - 1] : -1;
+      r.pad[0] = r.pad[1] = 0;
+      rec[s] = r;
+    }
   }
 }
 
@@ -1833,19 +1870,6 @@ __global__ __launch_bounds__(BLOCK) void k_heavy(HeavyArgs h) {
   }
 }
 
-// ------------------------------------------------------------------ source records
-// Everything the short-row scorer needs about an active source before its first global read of
-// row data, gathered once per step after grouping: one 64-byte record per active source (read
-// with scalar loads) instead of the dependent chain active[s] -> off / cnt / rp / wp / heavy ->
-// ci[rp] (three round trips per source on the latency-bound business side).
-struct SrcRec {
-  int32_t x, pbeg, pcnt, hslot;
-  int64_t xb, xe;  // N(x) = ci[xb, xe)
-  int64_t wb, we;  // wedge row of x, in 16-byte vectors (wb == we: none)
-  int32_t nx_lo, nx_hi;  // first and last id of N(x) (nx_hi < nx_lo: empty)
-  int32_t pad[2];
-};
-static_assert(sizeof(SrcRec) == 64, "one 64-byte record per source");
 
 __global__ void k_source_records(const int32_t* __restrict__ active, const Misc* __restrict__ misc,
                                  const int32_t* __restrict__ off, const int32_t* __restrict__ cnt,
@@ -4340,17 +4364,25 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   if (b->wset_pool) return score_wset(g, b, mask);
   hipEvent_t bt0;
   if ((rc = timer_begin(b->t_group, b->stream, &bt0))) return rc;
-  BLP_HIP(hipMemsetAsync(b->d_misc, 0, offsetof(Misc, dbg), b->stream));  // the debug record persists to fetch
-  if (np && b->runs) {
+  // run-grouped batches: k_run_count zeroes the counters (one launch fewer); the large scorer's
+  // source records come from k_run_cnt (one more)
+  const bool run_group = np && b->runs;
+  const bool rec_in_cnt = run_group && b->d_rec && b->variant == V_LARGE && !b->split && !b->global && !b->use_short;
+  if (!run_group) BLP_HIP(hipMemsetAsync(b->d_misc, 0, offsetof(Misc, dbg), b->stream));  // the debug record persists to fetch
+  if (run_group) {
     const int64_t tiles = (np + SCAN_TILE - 1) / SCAN_TILE;
     int32_t* rtile = reinterpret_cast<int32_t*>(tmp);  // the bucket sort's pair buffer is free here
-    hipLaunchKernelGGL(k_run_count, dim3((unsigned)tiles), dim3(SCAN_BLOCK), 0, b->stream, b->d_x, np, rtile);
+    static_assert(offsetof(Misc, dbg) % 4 == 0, "counters zeroed as words");
+    hipLaunchKernelGGL(k_run_count, dim3((unsigned)tiles), dim3(SCAN_BLOCK), 0, b->stream, b->d_x, np, rtile,
+                       reinterpret_cast<int32_t*>(b->d_misc), (int)(offsetof(Misc, dbg) / 4));
     hipLaunchKernelGGL(k_scan_mid, dim3(1), dim3(SCAN_BLOCK), 0, b->stream, rtile, tiles, &b->d_misc->n_active);
     hipLaunchKernelGGL(k_run_write, dim3((unsigned)tiles), dim3(SCAN_BLOCK), 0, b->stream, b->d_x, b->d_y, np, g->d_rp,
                        rtile, b->active.as<int32_t>(), b->off.as<int32_t>(), (int32_t*)nullptr, b->d_gyb, b->d_gyl,
                        b->d_gy);
     hipLaunchKernelGGL(k_run_cnt, dim3(1024), dim3(256), 0, b->stream, b->active.as<int32_t>(), &b->d_misc->n_active,
-                       np, b->off.as<int32_t>(), b->cnt.as<int32_t>(), b->d_rank, (int32_t)b->xlo, b->d_lpt);
+                       np, b->off.as<int32_t>(), b->cnt.as<int32_t>(), b->d_rank, (int32_t)b->xlo, b->d_lpt,
+                       rec_in_cnt ? b->d_rec : nullptr, g->d_rp, g->d_ci,
+                       (const int32_t*)(b->wbm_slot ? b->wbm_slot : b->d_heavy_slot));
   } else if (np) {
     // items mode: interleaved buckets (v & (nb - 1)); bucket mode: contiguous (v >> shift)
     const int hshift = b->items ? 0 : b->shift, bmask = b->items ? b->nb - 1 : -1;
@@ -4590,10 +4622,12 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
     int per_cu = 1;
     if ((rc = variant_occupancy(b->variant, &per_cu))) return rc;
     if (b->d_rec && b->variant == V_LARGE) {  // the large scorer's source headers (after grouping)
-      hipLaunchKernelGGL(k_source_records, dim3((unsigned)std::min<int64_t>((b->n_sources + 255) / 256, 2048)),
-                         dim3(256), 0, b->stream, a.active, b->d_misc, a.off, a.cnt, g->d_rp, g->d_ci, a.heavy_slot,
-                         nullptr, b->d_rec);
-      BLP_HIP(hipGetLastError());
+      if (!rec_in_cnt) {  // (run-grouped batches: written by k_run_cnt)
+        hipLaunchKernelGGL(k_source_records, dim3((unsigned)std::min<int64_t>((b->n_sources + 255) / 256, 2048)),
+                           dim3(256), 0, b->stream, a.active, b->d_misc, a.off, a.cnt, g->d_rp, g->d_ci, a.heavy_slot,
+                           nullptr, b->d_rec);
+        BLP_HIP(hipGetLastError());
+      }
       a.rec = b->d_rec;
     }
     if (b->variant == V_SMALL)
