@@ -825,26 +825,28 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_run_write(const int32_t* __restr
   const int64_t t0 = (int64_t)blockIdx.x * SCAN_TILE;
   // per-pair metadata, coalesced; the tile's y loads, then its row_ptr gathers, all in flight
   constexpr int PT = SCAN_TILE / SCAN_BLOCK;
-  int yv[PT];
+  if (g_yb) {  // (null: the scorer reads y and rp itself, pair_row)
+    int yv[PT];
 #pragma unroll
-  for (int q = 0; q < PT; ++q) {
-    const int64_t i = t0 + q * SCAN_BLOCK + threadIdx.x;
-    yv[q] = i < np ? y[i] : 0;
-  }
-  int64_t st[PT], en[PT];
+    for (int q = 0; q < PT; ++q) {
+      const int64_t i = t0 + q * SCAN_BLOCK + threadIdx.x;
+      yv[q] = i < np ? y[i] : 0;
+    }
+    int64_t st[PT], en[PT];
 #pragma unroll
-  for (int q = 0; q < PT; ++q) {
-    st[q] = rp[yv[q]];
-    en[q] = rp[yv[q] + 1];
-  }
+    for (int q = 0; q < PT; ++q) {
+      st[q] = rp[yv[q]];
+      en[q] = rp[yv[q] + 1];
+    }
 #pragma unroll
-  for (int q = 0; q < PT; ++q) {
-    const int64_t i = t0 + q * SCAN_BLOCK + threadIdx.x;
-    if (i < np) {
-      if (g_out) g_out[i] = (int32_t)i;
-      g_yb[i] = st[q];
-      g_yl[i] = (int32_t)(en[q] - st[q]);
-      if (g_y) g_y[i] = yv[q];
+    for (int q = 0; q < PT; ++q) {
+      const int64_t i = t0 + q * SCAN_BLOCK + threadIdx.x;
+      if (i < np) {
+        if (g_out) g_out[i] = (int32_t)i;
+        g_yb[i] = st[q];
+        g_yl[i] = (int32_t)(en[q] - st[q]);
+        if (g_y) g_y[i] = yv[q];
+      }
     }
   }
   const int64_t base = t0 + (int64_t)threadIdx.x * SCAN_ITEMS;
@@ -1910,6 +1912,7 @@ struct ScoreArgs {
   const int32_t* g_out;    // grouped position -> caller index (null: the identity, run-grouped lists)
   const int64_t* g_yb;     // grouped position -> start of N(y) in ci
   const int32_t* g_yl;     // grouped position -> |N(y)|
+  const int32_t* py;       // or (run-grouped large-scorer batches) the caller-order y: N(y) from rp
   const int32_t* hot_idx;     // per node: dense-row number or -1 (null: no dense rows)
   const blp::HotRow* hot_tab;
   const uint4* hot_pool;
@@ -1945,8 +1948,14 @@ __device__ __attribute__((always_inline)) inline int gout(const ScoreArgs& a, in
 
 // N(y)'s row [st, st + len) of grouped pair gp, from the grouped metadata g_yb / g_yl.
 __device__ __attribute__((always_inline)) inline void pair_row(const ScoreArgs& a, int gp, int64_t& st, int& len) {
-  st = a.g_yb[gp];
-  len = a.g_yl[gp];
+  if (a.py) {  // one dependent load more (y, then rp[y]), behind the H2 build like the rest of the header
+    const int yv = a.py[gp];
+    st = a.rp[yv];
+    len = (int)(a.rp[yv + 1] - st);
+  } else {
+    st = a.g_yb[gp];
+    len = a.g_yl[gp];
+  }
 }
 
 template <int BLOCK, bool TAIL = true>  // TAIL: see block_exscan
@@ -2286,8 +2295,7 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
           have_pf = PF && !SHORT && BLP_PFN && nchunks == 1 && sb + SEG < pcnt;
           if (have_pf && (int)threadIdx.x < min(SEG, pcnt - sb - SEG)) {
             const int gp = pbeg + sb + SEG + threadIdx.x;
-            pf_start = a.g_yb[gp];
-            pf_len = a.g_yl[gp];
+            pair_row(a, gp, pf_start, pf_len);
             pf_out = gout(a, gp);
           }
           PROF(6)
@@ -3420,6 +3428,7 @@ struct Knobs {
   int64_t hash_work = -1;        // BLP_HASH_WORK: hash-set routing bound (build ids)
   bool no_wcodes = false;        // BLP_NO_WCODES: plain ids (per-hit weight gathers)
   bool split_nopk = false;       // BLP_SPLIT_NOPK: unpacked split partials
+  bool no_ydirect = false;       // BLP_NO_YDIRECT: run-grouped block scorer reads gathered row starts (test knob)
   int split_short = -1;          // BLP_SPLIT_SHORT: register-scanned slice bound (0: off)
   int cosched_cus = -1;          // BLP_COSCHED_CUS: tuning override of the co-scheduled CU share
   bool no_pko = false;           // BLP_NO_PKO: the large scorer's general variant instead of PKO
@@ -3461,6 +3470,7 @@ Knobs read_knobs() {
   k.hash_work = num("BLP_HASH_WORK", -1);
   k.no_wcodes = on("BLP_NO_WCODES");
   k.split_nopk = on("BLP_SPLIT_NOPK");
+  k.no_ydirect = on("BLP_NO_YDIRECT");
   k.split_short = (int)num("BLP_SPLIT_SHORT", -1);
   k.cosched_cus = (int)num("BLP_COSCHED_CUS", -1);
   k.no_pko = on("BLP_NO_PKO");
@@ -3628,8 +3638,10 @@ static int launch_pointers(const blp_graph* g, const blp_batch* b, ScoreArgs& a,
   need(a.cnt, "source counts");
   need(a.active, "active sources");
   if (!b->runs) need(a.g_out, "grouped caller index");
-  need(a.g_yb, "grouped row starts");
-  need(a.g_yl, "grouped row lengths");
+  if (!a.py) {
+    need(a.g_yb, "grouped row starts");
+    need(a.g_yl, "grouped row lengths");
+  }
   need(a.misc, "batch counters");
   need(a.cn, "cn output");
   need(a.jac, "jaccard output");
@@ -4368,6 +4380,9 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   // source records come from k_run_cnt (one more)
   const bool run_group = np && b->runs;
   const bool rec_in_cnt = run_group && b->d_rec && b->variant == V_LARGE && !b->split && !b->global && !b->use_short;
+  // ... and the block scorer of a run-grouped batch finds N(y) from the caller's y itself (grouped
+  // order is caller order): no per-pair row starts and lengths are gathered and written per step
+  const bool y_direct = run_group && !b->split && !b->global && !b->use_short && !b->kn.no_ydirect;
   if (!run_group) BLP_HIP(hipMemsetAsync(b->d_misc, 0, offsetof(Misc, dbg), b->stream));  // the debug record persists to fetch
   if (run_group) {
     const int64_t tiles = (np + SCAN_TILE - 1) / SCAN_TILE;
@@ -4377,8 +4392,8 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
                        reinterpret_cast<int32_t*>(b->d_misc), (int)(offsetof(Misc, dbg) / 4));
     hipLaunchKernelGGL(k_scan_mid, dim3(1), dim3(SCAN_BLOCK), 0, b->stream, rtile, tiles, &b->d_misc->n_active);
     hipLaunchKernelGGL(k_run_write, dim3((unsigned)tiles), dim3(SCAN_BLOCK), 0, b->stream, b->d_x, b->d_y, np, g->d_rp,
-                       rtile, b->active.as<int32_t>(), b->off.as<int32_t>(), (int32_t*)nullptr, b->d_gyb, b->d_gyl,
-                       b->d_gy);
+                       rtile, b->active.as<int32_t>(), b->off.as<int32_t>(), (int32_t*)nullptr,
+                       y_direct ? nullptr : b->d_gyb, y_direct ? nullptr : b->d_gyl, y_direct ? nullptr : b->d_gy);
     hipLaunchKernelGGL(k_run_cnt, dim3(1024), dim3(256), 0, b->stream, b->active.as<int32_t>(), &b->d_misc->n_active,
                        np, b->off.as<int32_t>(), b->cnt.as<int32_t>(), b->d_rank, (int32_t)b->xlo, b->d_lpt,
                        rec_in_cnt ? b->d_rec : nullptr, g->d_rp, g->d_ci,
@@ -4526,6 +4541,7 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   a.g_out = b->runs ? nullptr : b->d_gout;  // run-grouped: grouped order is caller order
   a.g_yb = b->d_gyb;
   a.g_yl = b->d_gyl;
+  a.py = y_direct ? b->d_y : nullptr;
   a.hot_idx = b->use_hot ? g->d_hot_idx : nullptr;
   a.hot_tab = (const HotRow*)g->d_hot_tab;
   a.hot_pool = (const uint4*)g->d_hot_pool;
