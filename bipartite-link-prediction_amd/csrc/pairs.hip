@@ -901,6 +901,51 @@ __global__ void k_run_cnt(const int32_t* __restrict__ active, const int32_t* __r
   }
 }
 
+// Run-grouped batches queued largest first (BLP_LPT) whose scorer reads source records: the
+// whole grouping in two launches instead of four. Every source is one run (x non-decreasing), so
+// the run heads need no prefix order: a head writes off[x] and its queue slot lpt[rank[x]], a run
+// tail writes its end into cnt[x]; block 0 zeroes the counters and sets n_active (the number of
+// sources). k_run_records then turns the ends into counts and writes the records.
+__global__ __launch_bounds__(256) void k_run_heads(const int32_t* __restrict__ x, int64_t np, int32_t xlo,
+                                                   const int32_t* __restrict__ rank, int32_t* __restrict__ off,
+                                                   int32_t* __restrict__ end, int32_t* __restrict__ lpt,
+                                                   int32_t* __restrict__ misc_words, int zero_words, int32_t n_sources) {
+  static_assert(offsetof(Misc, n_active) == 0, "n_active is the counters' first word");
+  if (blockIdx.x == 0)
+    for (int i = threadIdx.x; i < zero_words; i += blockDim.x) misc_words[i] = i == 0 ? n_sources : 0;
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < np; p += (int64_t)gridDim.x * blockDim.x) {
+    const int xi = x[p];
+    if (p == 0 || x[p - 1] != xi) {
+      off[xi] = (int32_t)p;
+      lpt[rank[xi - xlo]] = xi;
+    }
+    if (p == np - 1 || x[p + 1] != xi) end[xi] = (int32_t)(p + 1);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_run_records(const int32_t* __restrict__ lpt, int32_t n_sources,
+                                                     const int32_t* __restrict__ off, int32_t* __restrict__ cnt,
+                                                     const int64_t* __restrict__ rp, const int32_t* __restrict__ ci,
+                                                     const int32_t* __restrict__ heavy_slot, SrcRec* __restrict__ rec) {
+  for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < n_sources; s += gridDim.x * blockDim.x) {
+    const int xa = lpt[s];
+    const int pb = off[xa], n = cnt[xa] - pb;  // cnt held the run's end
+    cnt[xa] = n;
+    SrcRec r;
+    r.x = xa;
+    r.pbeg = pb;
+    r.pcnt = n;
+    r.hslot = heavy_slot ? heavy_slot[xa] : -1;
+    r.xb = rp[xa];
+    r.xe = rp[xa + 1];
+    r.wb = r.we = 0;
+    r.nx_lo = r.xe > r.xb ? ci[r.xb] : 0;
+    r.nx_hi = r.xe > r.xb ? ci[r.xe - 1] : -1;
+    r.pad[0] = r.pad[1] = 0;
+    rec[s] = r;
+  }
+}
+
 // BLP_LPT planning: each source's scan work, sum of |N(y)| over its pairs (wave-aggregated when
 // the wave's pairs share their source, as run-grouped lists do), into est[x - xlo]
 __global__ void k_src_scan_work(const int32_t* __restrict__ x, const int32_t* __restrict__ y, int64_t np,
@@ -3429,6 +3474,7 @@ struct Knobs {
   bool no_wcodes = false;        // BLP_NO_WCODES: plain ids (per-hit weight gathers)
   bool split_nopk = false;       // BLP_SPLIT_NOPK: unpacked split partials
   bool no_ydirect = false;       // BLP_NO_YDIRECT: run-grouped block scorer reads gathered row starts (test knob)
+  bool no_run_fast = false;      // BLP_NO_RUN_FAST: run grouping in four launches (scan order; test knob)
   int split_short = -1;          // BLP_SPLIT_SHORT: register-scanned slice bound (0: off)
   int cosched_cus = -1;          // BLP_COSCHED_CUS: tuning override of the co-scheduled CU share
   bool no_pko = false;           // BLP_NO_PKO: the large scorer's general variant instead of PKO
@@ -3471,6 +3517,7 @@ Knobs read_knobs() {
   k.no_wcodes = on("BLP_NO_WCODES");
   k.split_nopk = on("BLP_SPLIT_NOPK");
   k.no_ydirect = on("BLP_NO_YDIRECT");
+  k.no_run_fast = on("BLP_NO_RUN_FAST");
   k.split_short = (int)num("BLP_SPLIT_SHORT", -1);
   k.cosched_cus = (int)num("BLP_COSCHED_CUS", -1);
   k.no_pko = on("BLP_NO_PKO");
@@ -4383,8 +4430,18 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   // ... and the block scorer of a run-grouped batch finds N(y) from the caller's y itself (grouped
   // order is caller order): no per-pair row starts and lengths are gathered and written per step
   const bool y_direct = run_group && !b->split && !b->global && !b->use_short && !b->kn.no_ydirect;
+  const bool run_fast = rec_in_cnt && b->d_rank && b->d_lpt && !b->kn.no_run_fast;  // two launches (k_run_heads)
   if (!run_group) BLP_HIP(hipMemsetAsync(b->d_misc, 0, offsetof(Misc, dbg), b->stream));  // the debug record persists to fetch
-  if (run_group) {
+  if (run_fast) {
+    const unsigned gh = (unsigned)std::max<int64_t>(1, std::min<int64_t>((int64_t)g->n_cu * 8, (np + 255) / 256));
+    hipLaunchKernelGGL(k_run_heads, dim3(gh), dim3(256), 0, b->stream, b->d_x, np, (int32_t)b->xlo, b->d_rank,
+                       b->off.as<int32_t>(), b->cnt.as<int32_t>(), b->d_lpt, reinterpret_cast<int32_t*>(b->d_misc),
+                       (int)(offsetof(Misc, dbg) / 4), (int32_t)b->n_sources);
+    const unsigned gr = (unsigned)std::max<int64_t>(1, std::min<int64_t>((int64_t)g->n_cu * 4, (b->n_sources + 255) / 256));
+    hipLaunchKernelGGL(k_run_records, dim3(gr), dim3(256), 0, b->stream, b->d_lpt, (int32_t)b->n_sources,
+                       b->off.as<int32_t>(), b->cnt.as<int32_t>(), g->d_rp, g->d_ci,
+                       (const int32_t*)(b->wbm_slot ? b->wbm_slot : b->d_heavy_slot), b->d_rec);
+  } else if (run_group) {
     const int64_t tiles = (np + SCAN_TILE - 1) / SCAN_TILE;
     int32_t* rtile = reinterpret_cast<int32_t*>(tmp);  // the bucket sort's pair buffer is free here
     static_assert(offsetof(Misc, dbg) % 4 == 0, "counters zeroed as words");

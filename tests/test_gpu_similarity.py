@@ -162,6 +162,7 @@ def test_general_graph_exact_distance(gpu):
     {"BLP_ITEM_NB": "4", "BLP_GROUP_NBLK": "3"},        # few buckets, few scatter workgroups
     {"BLP_LPT": "0"},                                   # run-grouped sources queued in id order (default: largest work first)
     {"BLP_NO_YDIRECT": "1"},                            # run-grouped block scorer on gathered row starts / lengths
+    {"BLP_NO_RUN_FAST": "1"},                           # run grouping by tile counts, scan and writes (four launches)
     {"BLP_LPT": "3"},                                   # ... and item-grouped ones
     {"BLP_LPT": "3", "BLP_SPLIT": "3", "BLP_HASH_WORK": "600"},  # ... with the hash-set partition of the queue
 ])
