@@ -2144,13 +2144,23 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
       // short-row scorer (BLP_PF): the first pair segment's metadata is loaded now, so its
       // latency overlaps the H2 build instead of following it
       int64_t pf_start = 0;
-      int pf_len = 0, pf_out = 0;
+      int pf_len = 0, pf_out = 0, pf_y = 0;
       constexpr bool PF = SHORT ? BLP_PF : (RC && BLP_PFL);
-      if (PF && nchunks == 1 && (int)threadIdx.x < min(SEG, pcnt)) {
+      const bool pf_mine = PF && nchunks == 1 && (int)threadIdx.x < min(SEG, pcnt);
+      if (pf_mine) {
         const int gp = pbeg + threadIdx.x;
-        pair_row(a, gp, pf_start, pf_len);
+        if (a.py)  // two hops (y, then rp[y]): the second is issued once the bitmap's first phase is out
+          pf_y = a.py[gp];
+        else
+          pair_row(a, gp, pf_start, pf_len);
         pf_out = gout(a, gp);
       }
+      auto pf_rows = [&]() {
+        if (a.py && pf_mine) {
+          pf_start = a.rp[pf_y];
+          pf_len = (int)(a.rp[pf_y + 1] - pf_start);
+        }
+      };
       PROF(1)
 
       for (int ch = 0; ch < nchunks; ++ch) {
@@ -2163,6 +2173,7 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
           // 1'. pre-built by k_heavy (single-chunk universes only)
           const uint4* src4 = reinterpret_cast<const uint4*>(a.heavy_bm + (int64_t)hslot * a.hb_words);
           for (int i = threadIdx.x; i < nw4; i += BLOCK) bm4[i] = src4[i];
+          if (ch == 0) pf_rows();
           __syncthreads();
         } else {
           // 1. the dense rows of N(x) initialise the bitmap (their OR, 16-byte vectors), then
@@ -2230,6 +2241,7 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
           }
           __syncthreads();
           if (!SHORT && threadIdx.x == 0) s_nhot = 0;  // s_hot / s_nhot are read: ready for the next detection
+          if (ch == 0) pf_rows();  // in flight during the sparse build
           PROF(2)
           if (SHORT && a.wp) {
             // N(N(x)) from x's wedge row: one contiguous range, two 16-byte vectors per thread
@@ -2302,6 +2314,11 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
         for (int sb = 0; sb < pcnt; sb += SEG) {
           const int ns = min(SEG, pcnt - sb);
           int len = 0, pout = 0;
+          // the next segment's metadata (BLP_PFN), issued during this segment's offsets and scan;
+          // with a.py its first hop (y) goes out now, before the offsets' barriers
+          const bool nxt = PF && !SHORT && BLP_PFN && nchunks == 1 && sb + SEG < pcnt;
+          const bool nxt_mine = nxt && (int)threadIdx.x < min(SEG, pcnt - sb - SEG);
+          if (a.py && nxt_mine) pf_y = a.py[pbeg + sb + SEG + threadIdx.x];
           if (have_pf) {
             if ((int)threadIdx.x < ns) {
               s_start[threadIdx.x] = pf_start;
@@ -2336,11 +2353,16 @@ __global__ __launch_bounds__(BLOCK, SHORT ? BLP_SHORT_MINB : 1) void k_score(Sco
             if (threadIdx.x == 0) s_off[ns] = tot;
             __syncthreads();
           }
-          // the next segment's metadata, in flight during this segment's scan (BLP_PFN)
-          have_pf = PF && !SHORT && BLP_PFN && nchunks == 1 && sb + SEG < pcnt;
-          if (have_pf && (int)threadIdx.x < min(SEG, pcnt - sb - SEG)) {
+          // the next segment's row bounds, in flight during this segment's scan
+          have_pf = nxt;
+          if (nxt_mine) {
             const int gp = pbeg + sb + SEG + threadIdx.x;
-            pair_row(a, gp, pf_start, pf_len);
+            if (a.py) {
+              pf_start = a.rp[pf_y];
+              pf_len = (int)(a.rp[pf_y + 1] - pf_start);
+            } else {
+              pair_row(a, gp, pf_start, pf_len);
+            }
             pf_out = gout(a, gp);
           }
           PROF(6)
