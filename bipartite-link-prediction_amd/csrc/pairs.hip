@@ -4452,7 +4452,9 @@ int blp_batch_score(blp_graph* g, blp_batch* b, uint32_t mask) {
   // ... and the block scorer of a run-grouped batch finds N(y) from the caller's y itself (grouped
   // order is caller order): no per-pair row starts and lengths are gathered and written per step
   const bool y_direct = run_group && !b->split && !b->global && !b->use_short && !b->kn.no_ydirect;
-  const bool run_fast = rec_in_cnt && b->d_rank && b->d_lpt && !b->kn.no_run_fast;  // two launches (k_run_heads)
+  // two launches (k_run_heads, k_run_records); no per-pair row metadata is written, so the
+  // scorer must find N(y) itself (y_direct)
+  const bool run_fast = rec_in_cnt && y_direct && b->d_rank && b->d_lpt && !b->kn.no_run_fast;
   if (!run_group) BLP_HIP(hipMemsetAsync(b->d_misc, 0, offsetof(Misc, dbg), b->stream));  // the debug record persists to fetch
   if (run_fast) {
     const unsigned gh = (unsigned)std::max<int64_t>(1, std::min<int64_t>((int64_t)g->n_cu * 8, (np + 255) / 256));

@@ -163,6 +163,8 @@ def test_general_graph_exact_distance(gpu):
     {"BLP_LPT": "0"},                                   # run-grouped sources queued in id order (default: largest work first)
     {"BLP_NO_YDIRECT": "1"},                            # run-grouped block scorer on gathered row starts / lengths
     {"BLP_NO_RUN_FAST": "1"},                           # run grouping by tile counts, scan and writes (four launches)
+    {"BLP_VARIANT": "2", "BLP_NO_YDIRECT": "1"},        # ... the large scorer on gathered rows (so no two-launch grouping)
+    {"BLP_VARIANT": "2", "BLP_NO_RUN_FAST": "1"},       # ... the large scorer after the four-launch grouping
     {"BLP_LPT": "3"},                                   # ... and item-grouped ones
     {"BLP_LPT": "3", "BLP_SPLIT": "3", "BLP_HASH_WORK": "600"},  # ... with the hash-set partition of the queue
 ])
