@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 6, final check 5 at HEAD: the whole GPU suite, smoke(), the default bench line (full
+# Round 6, final check 6 at HEAD (end of round, every config): the whole GPU suite, smoke(), the default bench line (full
 # parity + CPU baseline), similarity.main at configs 2 (twice) and 1, and the driver's N > 1
 # launch path rehearsed with two ranks on the box's one GPU (BLP_DEVICE=0; RCCL refuses two
 # ranks on one device, so the exchange reports that error and the headline line stands).
