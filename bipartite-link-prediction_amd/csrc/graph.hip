@@ -274,40 +274,21 @@ void host_free(void* p, size_t bytes) {
   munmap(p, (bytes + HUGE_PAGE - 1) / HUGE_PAGE * HUGE_PAGE);
 }
 
-int timer_begin(KernelTimer& t, hipStream_t s, hipEvent_t* start) {
-  if (t.free_events.empty()) {
-    hipEvent_t e;
-    BLP_HIP(hipEventCreate(&e));
-    t.free_events.push_back(e);
+// A batch's timers (mirror_mu set: the graph's lock) are also read by the graph's stats calls,
+// which may come from another host thread: their lists are touched under that lock. The graph's
+// own timers (mirror_mu null) belong to the graph's calls.
+namespace {
+struct TimerLock {
+  std::mutex* m;
+  explicit TimerLock(const KernelTimer& t) : m(t.mirror_mu) {
+    if (m) m->lock();
   }
-  *start = t.free_events.back();
-  t.free_events.pop_back();
-  BLP_HIP(hipEventRecord(*start, s));
-  return BLP_OK;
-}
+  ~TimerLock() {
+    if (m) m->unlock();
+  }
+};
 
-int timer_end(KernelTimer& t, hipStream_t s, hipEvent_t start) {
-  hipEvent_t stop;
-  if (t.free_events.empty()) {
-    BLP_HIP(hipEventCreate(&stop));
-  } else {
-    stop = t.free_events.back();
-    t.free_events.pop_back();
-  }
-  BLP_HIP(hipEventRecord(stop, s));
-  t.pending_start.push_back(start);
-  t.pending_stop.push_back(stop);
-  t.launches++;
-  if (t.mirror) {
-    std::lock_guard<std::mutex> lk(*t.mirror_mu);
-    t.mirror->launches++;
-  }
-  // keep the pending list bounded: fold finished pairs in as we go
-  if (t.pending_stop.size() > 4096) return timer_collect(t);
-  return BLP_OK;
-}
-
-int timer_collect(KernelTimer& t) {
+int timer_collect_locked(KernelTimer& t) {
   double added = 0.0;
   int rc = BLP_OK;
   size_t i = 0;
@@ -326,11 +307,46 @@ int timer_collect(KernelTimer& t) {
   }
   t.pending_start.erase(t.pending_start.begin(), t.pending_start.begin() + i);
   t.pending_stop.erase(t.pending_stop.begin(), t.pending_stop.begin() + i);
-  if (t.mirror && added != 0.0) {
-    std::lock_guard<std::mutex> lk(*t.mirror_mu);
-    t.mirror->total_ms += added;
-  }
+  if (t.mirror) t.mirror->total_ms += added;  // (the mirror is guarded by the same lock)
   return rc;
+}
+}  // namespace
+
+int timer_begin(KernelTimer& t, hipStream_t s, hipEvent_t* start) {
+  TimerLock lk(t);
+  if (t.free_events.empty()) {
+    hipEvent_t e;
+    BLP_HIP(hipEventCreate(&e));
+    t.free_events.push_back(e);
+  }
+  *start = t.free_events.back();
+  t.free_events.pop_back();
+  BLP_HIP(hipEventRecord(*start, s));
+  return BLP_OK;
+}
+
+int timer_end(KernelTimer& t, hipStream_t s, hipEvent_t start) {
+  TimerLock lk(t);
+  hipEvent_t stop;
+  if (t.free_events.empty()) {
+    BLP_HIP(hipEventCreate(&stop));
+  } else {
+    stop = t.free_events.back();
+    t.free_events.pop_back();
+  }
+  BLP_HIP(hipEventRecord(stop, s));
+  t.pending_start.push_back(start);
+  t.pending_stop.push_back(stop);
+  t.launches++;
+  if (t.mirror) t.mirror->launches++;
+  // keep the pending list bounded: fold finished pairs in as we go
+  if (t.pending_stop.size() > 4096) return timer_collect_locked(t);
+  return BLP_OK;
+}
+
+int timer_collect(KernelTimer& t) {
+  TimerLock lk(t);
+  return timer_collect_locked(t);
 }
 
 void timer_release(KernelTimer& t) {
@@ -823,6 +839,7 @@ int blp_stats_reset(blp_graph* g) {
   BLP_CHECK(g, BLP_E_ARG, "blp_stats_reset: null graph");
   int rc = timers_collect(g);
   if (rc) return rc;
+  std::lock_guard<std::mutex> lk(g->timer_mu);  // the batches' timers add into the score / group totals
   for (auto& t : g->timers) {
     t.total_ms = 0.0;
     t.launches = 0;
@@ -834,6 +851,7 @@ int blp_stats_get(blp_graph* g, int kernel, double* total_ms, int64_t* launches)
   BLP_CHECK(g && kernel >= 0 && kernel < K_COUNT, BLP_E_ARG, "blp_stats_get: bad arguments");
   int rc = timers_collect(g);
   if (rc) return rc;
+  std::lock_guard<std::mutex> lk(g->timer_mu);
   if (total_ms) *total_ms = g->timers[kernel].total_ms;
   if (launches) *launches = g->timers[kernel].launches;
   return BLP_OK;

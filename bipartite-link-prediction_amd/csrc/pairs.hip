@@ -4817,6 +4817,7 @@ int blp_batch_stats(blp_batch* b, int which, double* total_ms, int64_t* launches
   int rc = set_device(b->g);
   if (rc) return rc;
   if ((rc = timer_collect(t))) return rc;
+  std::lock_guard<std::mutex> lk(b->g->timer_mu);
   if (total_ms) *total_ms = t.total_ms;
   if (launches) *launches = t.launches;
   return BLP_OK;
@@ -4828,6 +4829,7 @@ int blp_batch_stats_reset(blp_batch* b) {
   if (rc) return rc;
   for (KernelTimer* t : {&b->t_score, &b->t_group}) {
     if ((rc = timer_collect(*t))) return rc;
+    std::lock_guard<std::mutex> lk(b->g->timer_mu);  // (a graph stats call may collect this timer)
     t->total_ms = 0;
     t->launches = 0;
   }

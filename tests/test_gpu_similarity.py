@@ -312,11 +312,19 @@ def test_graph_score_totals_follow_the_batch_timers(gpu):
         for _ in range(5):
             bt.score(m)
 
-    th = [threading.Thread(target=run, args=(bx, 7)), threading.Thread(target=run, args=(bz, 3))]
+    reads = []
+
+    def watch():  # the graph's totals read while both batches score (the timers' lock)
+        for _ in range(20):
+            reads.append(G.stats(blp._lib.K_SCORE)[1])
+
+    th = [threading.Thread(target=run, args=(bx, 7)), threading.Thread(target=run, args=(bz, 3)),
+          threading.Thread(target=watch)]
     for t in th:
         t.start()
     for t in th:
         t.join()
+    assert reads == sorted(reads) and all(3 <= r <= 13 for r in reads)
     bx.fetch(7)
     bz.fetch(3)
     assert G.stats(blp._lib.K_SCORE)[1] == 13
