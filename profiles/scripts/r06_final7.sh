@@ -19,3 +19,6 @@ for c in c2 c2 yelp; do
 done
 BLP_DEVICE=0 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29555 bench.py --gpus 2 --steps 5 --warmup 1 > gpurun_out/r06fin7_r2.json 2> gpurun_out/r06fin7_r2.err || { tail -30 gpurun_out/r06fin7_r2.err; exit 1; }
 python -c "import json;d=json.loads(open('gpurun_out/r06fin7_r2.json').read().strip().splitlines()[-1]);print('r2', d['n_gpus'], round(d['ms_per_step'],4), d['value'], (d.get('parity') or {}).get('ok'), (d.get('exchange') or {}).get('error'))"
+# batch-creation stages at config 1 (score_create is 28 ms there against 7.5 ms at config 2)
+BLP_CREATE_PROF=1 timeout -k 10 300 python bench.py --mode e2e --config yelp > gpurun_out/r06fin7_e2e_yelp_prof.json 2> gpurun_out/r06fin7_e2e_yelp_prof.err || { tail -20 gpurun_out/r06fin7_e2e_yelp_prof.err; exit 1; }
+grep -i "create\|stage\|plan" gpurun_out/r06fin7_e2e_yelp_prof.err | head -40 || true
