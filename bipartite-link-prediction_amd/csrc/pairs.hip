@@ -3797,14 +3797,6 @@ static int batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_
   if (rc) return bail(rc);
   b->hi_prio = hi_prio;
   if (!(b->stream = stream_take(g->device, hi_prio))) return bail(BLP_E_HIP_BASE);  // pooled (blp_stream_prewarm)
-  {  // the graph's own uploads complete before this stream reads them (an event, not a host wait)
-    hipEvent_t ev;
-    BLP_HIP_OR(hipEventCreateWithFlags(&ev, hipEventDisableTiming), bail);
-    hipError_t e = hipEventRecord(ev, g->stream);
-    if (e == hipSuccess) e = hipStreamWaitEvent(b->stream, ev, 0);
-    (void)hipEventDestroy(ev);
-    BLP_HIP_OR(e, bail);
-  }
   // ---- the pairs go to HBM first: the device planning pass reads them there
   const size_t np = (size_t)std::max<int64_t>(n_pairs, 1);
   if (dev_malloc(&b->d_x, 4 * np) != hipSuccess || dev_malloc(&b->d_y, 4 * np) != hipSuccess ||
@@ -3825,6 +3817,16 @@ static int batch_create(blp_graph* g, const int32_t* x, const int32_t* y, int64_
       return bail(rc);
   }
   BLP_HIP_OR(hipMemsetAsync(b->d_misc, 0, sizeof(Misc), b->stream), bail);  // dbg[] is zeroed here, not per score
+  {  // the graph's own device work completes before this stream reads the graph (an event, not a
+     // host wait), queued after the pair upload: the upload's host syncs then do not wait for the
+     // graph build's last kernels
+    hipEvent_t ev;
+    BLP_HIP_OR(hipEventCreateWithFlags(&ev, hipEventDisableTiming), bail);
+    hipError_t e = hipEventRecord(ev, g->stream);
+    if (e == hipSuccess) e = hipStreamWaitEvent(b->stream, ev, 0);
+    (void)hipEventDestroy(ev);
+    BLP_HIP_OR(e, bail);
+  }
   stage("upload");
   // ---- plan: node universe touched by H2(x) and N(y); per-source build work
   int64_t lo = INT64_MAX, hi = INT64_MIN, scan_work = 0, max_scan_row = 0, max_build_row = 0;
